@@ -1,0 +1,216 @@
+/*
+ * wsmc.h — C ABI of the MI355X-native SMC inner loop for WeightedSampling.jl.
+ *
+ * This library replaces the per-particle hot path that sits behind the reference's
+ * store / state / operator interface. Each entry point names the reference interface it
+ * stands in for (paths relative to the reference repository root):
+ *
+ *   store      AbstractParticleStore            src/stores.jl:1-35, ColumnStore :70-128
+ *   state      SMCState weights / flags         src/types.jl:48-65
+ *   operators  apply!(Assign|Sample|Observe|Weight|Resample|Move, state)
+ *                                               src/transformers.jl:28, 172, 228, 283, 474, 588
+ *   numerics   exp_norm / ess_perc / logsumexp / stratified_resample / icdf
+ *                                               src/resampling.jl:13-77
+ *   proposals  RW / autoRW                      src/move_kernels.jl:189-253
+ *   kernels    default_kernels Normal / MvNormal / Uniform, the example HalfNormal
+ *                                               src/default_kernels.jl:83-102,
+ *                                               examples/damped_oscillator.jl:24-28
+ *   score fold score_logpdf! / score!          src/types.jl:198-206, src/transformers.jl:193-302
+ *
+ * Conventions
+ *   - All functions return WSMC_OK (0) or a nonzero wsmc_status; wsmc_last_error()
+ *     returns a thread-local message for the last failure.
+ *   - A context owns every device buffer of one particle shard on one GPU. Host pointers
+ *     are borrowed for the duration of a call. Downloads synchronise; everything else is
+ *     enqueued on the context's stream.
+ *   - Columns are particle-major SoA f64: a column of dimension d is d contiguous arrays
+ *     of N doubles (component-major), so component k of particle i is data[k*N + i].
+ *   - Particle, slot and column indices are 0-based (the reference is 1-based).
+ *   - One context per host thread (the reference is single-threaded, src/types.jl:24-26).
+ *   - No host pointers to device memory escape except through wsmc_col_device_ptr.
+ */
+#ifndef WSMC_H
+#define WSMC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    WSMC_OK = 0,
+    WSMC_EARG = 1,     /* invalid argument (reference: ArgumentError, src/move_kernels.jl:26) */
+    WSMC_EHIP = 2,     /* HIP runtime failure */
+    WSMC_ENOTPD = 3,   /* proposal covariance not positive definite (reference: PosDefException) */
+    WSMC_ERCCL = 4,    /* RCCL failure */
+    WSMC_ESTATE = 5,   /* operation invalid in the current state */
+    WSMC_ENOMEM = 6
+} wsmc_status;
+
+typedef struct wsmc_ctx wsmc_ctx;
+
+/* ---- argument forms -------------------------------------------------------
+ * The reference passes opaque Julia closures (argfn). The device path accepts the
+ * argument shapes @model's `vectorize` produces for the supported kernels: constants
+ * (Ref), columns, and affine combinations of up to two column components.
+ *   value(i) = c0 + coef[0]*col[0][comp[0]][i] + coef[1]*col[1][comp[1]][i]
+ * Unused slots have col = -1.                                                  */
+typedef struct {
+    double  c0;
+    int32_t col[2];
+    int32_t comp[2];
+    double  coef[2];
+} wsmc_operand;
+
+typedef enum {
+    WSMC_FAM_NORMAL = 0,        /* Normal(mu, sigma), sigma a std               */
+    WSMC_FAM_HALFNORMAL = 1,    /* Truncated(Normal(0, sigma), 0, Inf)          */
+    WSMC_FAM_UNIFORM = 2,       /* Uniform(a, b) = param[0], param[1]           */
+    WSMC_FAM_MVNORMAL_ISO = 3   /* MvNormal(mu, var*I), dim <= 4                */
+} wsmc_family;
+
+typedef enum {
+    WSMC_MEAN_AFFINE = 0,       /* mean component k = mu[k]                      */
+    WSMC_MEAN_OSCILLATOR = 1    /* mean = mu[0]*exp(-mu[2]*t)*cos(mu[1]*t+mu[3]), t = param[0]
+                                   (examples/damped_oscillator.jl:11)            */
+} wsmc_mean_fn;
+
+typedef struct {
+    int32_t family;
+    int32_t mean_fn;
+    int32_t dim;                /* 1 for scalar families */
+    int32_t reserved;
+    wsmc_operand mu[4];
+    wsmc_operand scale;         /* sigma (NORMAL, HALFNORMAL) or variance (MVNORMAL_ISO) */
+    double param[2];
+} wsmc_dist;
+
+typedef enum { WSMC_TERM_SAMPLE = 0, WSMC_TERM_OBSERVE = 1, WSMC_TERM_WEIGHT = 2 } wsmc_term_kind;
+
+/* One entry of the score tape: the statement's log-density contribution as
+ * score!(Sample|Observe|Weight) recomputes it (src/transformers.jl:193-199, 243-249, 297-302). */
+typedef struct {
+    wsmc_dist    dist;
+    wsmc_operand x[4];          /* the scored value (Sample: the drawn column) */
+    int32_t      kind;
+    int32_t      depth;         /* execution depth of the statement (src/types.jl:162-177) */
+} wsmc_term;
+
+typedef enum { WSMC_RESAMPLE_STRATIFIED = 0, WSMC_RESAMPLE_SYSTEMATIC = 1 } wsmc_scheme;
+typedef enum { WSMC_PROPOSAL_RW = 0, WSMC_PROPOSAL_AUTORW = 1 } wsmc_proposal;
+
+typedef struct {
+    int32_t resampled;          /* SMCState.resampled */
+    int32_t weights_changed;    /* SMCState.weights_changed */
+    int32_t depth;              /* SMCState.depth */
+    int32_t n_terms;            /* score tape length */
+    double  last_ess_perc;      /* last ESS/N computed by a Resample */
+    uint64_t op_counter;        /* stochastic-statement counter (RNG stream position) */
+    int64_t n_resamples;
+} wsmc_state;
+
+/* ---- context --------------------------------------------------------------- */
+const char* wsmc_last_error(void);
+int wsmc_version(int32_t* major, int32_t* minor);
+int wsmc_device_count(int32_t* n);
+/* SMCState(n_particles; rng) — src/types.jl:62-78. The seed keys the Philox streams. */
+int wsmc_create(wsmc_ctx** out, int64_t n_particles, int32_t device, uint64_t seed);
+int wsmc_destroy(wsmc_ctx* ctx);
+int wsmc_sync(wsmc_ctx* ctx);
+int wsmc_nparticles(wsmc_ctx* ctx, int64_t* n);
+int wsmc_get_state(wsmc_ctx* ctx, wsmc_state* out);
+/* Test hooks used by the reference's own tests (test/move_test.jl:36-37 set state.depth). */
+int wsmc_set_depth(wsmc_ctx* ctx, int32_t depth);
+int wsmc_set_op_counter(wsmc_ctx* ctx, uint64_t op);
+
+/* ---- multi-GPU shard (one process per GPU) ----------------------------------
+ * A context may own the shard [global_offset, global_offset + N) of a global
+ * population of global_n particles; RNG streams are keyed by the global index.
+ * RCCL is initialised from a unique id distributed by the caller (rank 0 creates it). */
+int wsmc_comm_unique_id(uint8_t out_id[128]);
+int wsmc_comm_init(wsmc_ctx* ctx, const uint8_t id[128], int32_t world, int32_t rank,
+                   int64_t global_offset, int64_t global_n);
+
+/* ---- store: AbstractParticleStore (src/stores.jl:1-35) ----------------------- */
+/* broadcast_setcol! column creation (src/stores.jl:85-96); existing name => same id */
+int wsmc_col_create(wsmc_ctx* ctx, const char* name, int32_t dim, int32_t* col_id);
+/* hascol / lookup; *col_id = -1 when absent */
+int wsmc_col_find(wsmc_ctx* ctx, const char* name, int32_t* col_id);
+/* colnames (insertion order) */
+int wsmc_col_count(wsmc_ctx* ctx, int32_t* n);
+int wsmc_col_info(wsmc_ctx* ctx, int32_t col_id, char* name_buf, int32_t buf_len, int32_t* dim);
+/* getcol (host copy, synchronising) */
+int wsmc_col_download(wsmc_ctx* ctx, int32_t col_id, double* host);
+/* broadcast_setcol!(store, name, identity, (v,)) with a host vector */
+int wsmc_col_upload(wsmc_ctx* ctx, int32_t col_id, const double* host);
+/* device pointer of the live buffer (valid until the next resample/gather) */
+int wsmc_col_device_ptr(wsmc_ctx* ctx, int32_t col_id, double** dptr);
+/* resample!(store, indices) with caller-supplied 0-based indices (src/stores.jl:105-128) */
+int wsmc_store_resample(wsmc_ctx* ctx, const int32_t* host_indices);
+
+/* ---- weights: SMCState.weights (src/types.jl:48-60) ------------------------- */
+int wsmc_weights_upload(wsmc_ctx* ctx, const double* host);
+int wsmc_weights_download(wsmc_ctx* ctx, double* host);
+/* logsumexp(weights) - log(N)  (src/utils.jl:21) */
+int wsmc_log_evidence(wsmc_ctx* ctx, double* out);
+
+/* ---- operators (apply!) ------------------------------------------------------ */
+/* Assign: out[k] .= expr[k] for k < dim(out)            src/transformers.jl:28-32 */
+int wsmc_assign(wsmc_ctx* ctx, int32_t out_col, const wsmc_operand* expr);
+/* Sample: out ~ dist (weighter === nothing)            src/transformers.jl:172-182 */
+int wsmc_sample(wsmc_ctx* ctx, int32_t out_col, const wsmc_dist* dist);
+/* Sample with importance_kernel(proposal, target)      src/default_kernels.jl:69-73 */
+int wsmc_sample_importance(wsmc_ctx* ctx, int32_t out_col, const wsmc_dist* proposal,
+                           const wsmc_dist* target);
+/* Observe: weights .+= logpdf(dist, x)                  src/transformers.jl:228-235 */
+int wsmc_observe(wsmc_ctx* ctx, const wsmc_dist* dist, const wsmc_operand* x);
+/* Weight (_ ~ f(args)): weights .+= logpdf(dist, x)     src/transformers.jl:283-289 */
+int wsmc_weight(wsmc_ctx* ctx, const wsmc_dist* dist, const wsmc_operand* x);
+/* Resample (gated on weights_changed, strict ESS test, log-mean reset)
+ *                                                       src/transformers.jl:474-498 */
+int wsmc_resample(wsmc_ctx* ctx, double ess_perc_min, int32_t scheme,
+                  int32_t* resampled_out, double* ess_perc_out);
+/* Move with RW / autoRW (src/transformers.jl:588-623, src/move_kernels.jl:189-253).
+ *   targets: d <= 4 scalar columns; lo/hi: per-target bounds (NULL = unbounded);
+ *   step: RW step size (std) or autoRW min_step; target_depth: state.depth at the move
+ *   (pass -1 to use the context's current depth); diversity: NaN = ungated.
+ *   *accepted_out (may be NULL) receives the number of accepted proposals.          */
+int wsmc_move(wsmc_ctx* ctx, int32_t proposal, const int32_t* targets, int32_t d, double step,
+              const double* lo, const double* hi, int32_t target_depth, double diversity,
+              int64_t* accepted_out);
+/* score_logpdf!(scores, state, targets, target_depth) (src/types.jl:198-206) -> host */
+int wsmc_score(wsmc_ctx* ctx, int32_t target_depth, double* host_scores);
+/* marginal_diversity(store, targets)  (src/transformers.jl:560-565) */
+int wsmc_marginal_diversity(wsmc_ctx* ctx, const int32_t* targets, int32_t d, double* out);
+/* the last resample's ancestors (0-based; debug/parity; synchronising) */
+int wsmc_last_ancestors(wsmc_ctx* ctx, int32_t* host);
+
+/* ---- fused runners (whole model loops; one HIP graph per run) ------------------
+ * 2D SSM bootstrap filter (examples/2D_ssm.jl:7-17) on a fresh context:
+ *   x{1} .= x0; v .= v0; for t: x{t+1} .= x{t} + v; dv ~ MvNormal(0, q_var I);
+ *   v .= v + dv; o_t => MvNormal(x{t+1}, r_var I)   (+ the auto-inserted Resamples)
+ * Columns created: x_1 .. x_{T+1} (dim 2, when keep_history), x (dim 2, otherwise), v, dv.
+ * Produces the same columns, weights and RNG stream positions as issuing the same
+ * statements one by one through the operators above.                                   */
+int wsmc_ssm2d_run(wsmc_ctx* ctx, const double* obs /* T x 2, row-major */, int32_t T,
+                   const double* x0, const double* v0, double q_var, double r_var,
+                   double ess_perc_min, int32_t scheme, int32_t keep_history,
+                   double* log_evidence_out);
+/* per-kernel timing of the last fused run (HIP events on the ctx stream), ms */
+typedef struct {
+    double total_ms;            /* whole run, first kernel to last                       */
+    double propagate_ms;        /* sum over steps of the propagate/observe kernel         */
+    double reduce_ms;           /* sum over steps of the weight-statistics kernel         */
+    double resample_ms;         /* sum over steps of the scan/ancestor kernel             */
+    double finalize_ms;         /* trace-back + final gather                              */
+    int32_t steps;
+    int32_t n_resamples;
+} wsmc_run_timing;
+int wsmc_run_set_timing(wsmc_ctx* ctx, int32_t enabled);
+int wsmc_run_get_timing(wsmc_ctx* ctx, wsmc_run_timing* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WSMC_H */

@@ -1,0 +1,494 @@
+/*
+ * wsmc_math.h — deterministic scalar math shared by the gfx950 kernels and the
+ * CPU oracle (oracle/wsmc_oracle.c).
+ *
+ * Why this exists: the reference (WeightedSampling.jl) draws from Julia's global
+ * Xoshiro/ziggurat RNG and calls libm / Distributions.jl (src/default_kernels.jl:12-23,
+ * src/resampling.jl:40, src/move_kernels.jl:150,201,209). Neither can be reproduced
+ * bit-for-bit on a GPU. The build therefore fixes ONE restatement of every random draw
+ * and every transcendental, and compiles the same source for the host (gcc, for the
+ * oracle) and for the device (hipcc, for the kernels). With FP contraction disabled
+ * (-ffp-contract=off on both sides; explicit fma() only where written) and IEEE
+ * correctly-rounded +,-,*,/,sqrt on both sides, every per-particle value is
+ * bit-identical between the CPU oracle and the HIP path.
+ *
+ * Contents
+ *   - Philox4x32-10 counter-based RNG (Salmon et al. 2011; Random123 constants)
+ *   - uniforms / Box–Muller normals keyed by (seed, op, particle, draw)
+ *   - exp / log / log1p / sin / cos restated from the fdlibm algorithms (Sun, 1993)
+ *   - Normal / HalfNormal / Uniform / isotropic-MvNormal log-densities
+ *     (Distributions.jl semantics used by src/default_kernels.jl:83-102 and
+ *      examples/damped_oscillator.jl:24-28)
+ *   - the integer (fixed-point) weight map used for order-independent CDFs and ESS
+ *   - the stratified / systematic target map and its inverse rank() used by resampling
+ *     (restates src/resampling.jl:13-43 on an integer CDF)
+ *   - the bound transforms of autoRW/RW (src/move_kernels.jl:37-85)
+ *
+ * Valid C99 (gcc) and HIP C++ (hipcc). No libm calls.
+ */
+#ifndef WSMC_MATH_H
+#define WSMC_MATH_H
+
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define WSMC_HD __host__ __device__ inline __attribute__((always_inline))
+#else
+#define WSMC_HD static inline __attribute__((always_inline))
+#endif
+
+typedef unsigned __int128 wsmc_u128;
+
+/* ------------------------------------------------------------------------- */
+/* bit casts                                                                  */
+/* ------------------------------------------------------------------------- */
+WSMC_HD uint64_t wsmc_d2bits(double x) { union { double d; uint64_t u; } v; v.d = x; return v.u; }
+WSMC_HD double wsmc_bits2d(uint64_t u) { union { double d; uint64_t u; } v; v.u = u; return v.d; }
+
+#define WSMC_INF (wsmc_bits2d(0x7ff0000000000000ULL))
+#define WSMC_NAN (wsmc_bits2d(0x7ff8000000000000ULL))
+#define WSMC_LOG2PI 1.8378770664093453     /* log(2*pi) rounded to double */
+#define WSMC_LOG2   0.69314718055994530942 /* log(2) */
+#define WSMC_PI     3.14159265358979311600
+#define WSMC_TWO_PI 6.28318530717958623200
+
+WSMC_HD int wsmc_isnan(double x) { return x != x; }
+WSMC_HD int wsmc_isfinite(double x) { return (wsmc_d2bits(x) & 0x7ff0000000000000ULL) != 0x7ff0000000000000ULL; }
+WSMC_HD double wsmc_fabs(double x) { return wsmc_bits2d(wsmc_d2bits(x) & 0x7fffffffffffffffULL); }
+
+/* 2^k for -1022 <= k <= 1023 */
+WSMC_HD double wsmc_pow2i(int k) { return wsmc_bits2d((uint64_t)(k + 1023) << 52); }
+
+/* exact u32 pieces -> one correctly rounded add: identical on gcc and hipcc */
+WSMC_HD double wsmc_u64_to_d(uint64_t v) {
+    return (double)(uint32_t)(v >> 32) * 4294967296.0 + (double)(uint32_t)v;
+}
+WSMC_HD double wsmc_u128_to_d(wsmc_u128 v) {
+    return wsmc_u64_to_d((uint64_t)(v >> 64)) * 18446744073709551616.0 + wsmc_u64_to_d((uint64_t)v);
+}
+
+/* truncating f64 -> u64 for 0 <= x < 2^64 by bit manipulation (no cvt differences) */
+WSMC_HD uint64_t wsmc_d_to_u64_trunc(double x) {
+    uint64_t b = wsmc_d2bits(x);
+    if (b >> 63) return 0;                       /* negative or -0 */
+    int e = (int)((b >> 52) & 0x7ff);
+    if (e < 1023) return 0;                      /* x < 1 (incl. subnormal, 0) */
+    uint64_t m = (b & 0x000fffffffffffffULL) | 0x0010000000000000ULL;
+    int sh = e - 1075;                           /* x = m * 2^sh */
+    if (sh >= 0) return sh >= 12 ? 0xffffffffffffffffULL : (m << sh);
+    return m >> (-sh);
+}
+
+/* floor(w * 2^96) as u128 for 0 <= w <= 1 (evidence fixed point) */
+WSMC_HD wsmc_u128 wsmc_fix96(double w) {
+    uint64_t b = wsmc_d2bits(w);
+    if (b >> 63) return 0;
+    int e = (int)((b >> 52) & 0x7ff);
+    if (e == 0 || e == 0x7ff) return 0;          /* 0, subnormal (< 2^-96 anyway), inf/nan */
+    wsmc_u128 m = (wsmc_u128)((b & 0x000fffffffffffffULL) | 0x0010000000000000ULL);
+    int sh = e - 1075 + 96;                      /* w*2^96 = m * 2^sh */
+    if (sh >= 0) return sh > 75 ? (wsmc_u128)0 : (m << sh);
+    if (sh <= -64) return 0;
+    return m >> (-sh);
+}
+
+/* order-preserving u64 encoding of f64 (for atomicMax); NaN canonicalised to +NaN (max) */
+WSMC_HD uint64_t wsmc_ord_enc(double x) {
+    uint64_t b = wsmc_isnan(x) ? 0x7ff8000000000000ULL : wsmc_d2bits(x);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ULL);
+}
+WSMC_HD double wsmc_ord_dec(uint64_t e) {
+    return wsmc_bits2d((e >> 63) ? (e & 0x7fffffffffffffffULL) : ~e);
+}
+#define WSMC_ORD_NEG_INF 0x000fffffffffffffULL   /* wsmc_ord_enc(-inf) */
+
+/* ------------------------------------------------------------------------- */
+/* Philox4x32-10                                                              */
+/* ------------------------------------------------------------------------- */
+typedef struct { uint32_t v[4]; } wsmc_u32x4;
+
+WSMC_HD uint32_t wsmc_mulhi32(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
+
+WSMC_HD wsmc_u32x4 wsmc_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+    for (int r = 0; r < 10; ++r) {
+        uint32_t hi0 = wsmc_mulhi32(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        uint32_t hi1 = wsmc_mulhi32(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    wsmc_u32x4 o; o.v[0] = c0; o.v[1] = c1; o.v[2] = c2; o.v[3] = c3;
+    return o;
+}
+
+/*
+ * Stream layout (the build's replacement for Julia's global RNG, src/types.jl:24-26):
+ *   key     = seed (64 bit)
+ *   counter = { particle index lo32, (block << 8) | lane-tag, op lo32, op hi32 }
+ * `op` is the context's monotonically increasing stochastic-statement counter, so a
+ * fused multi-step runner and the same statements issued one by one draw identical
+ * numbers. `block` selects the 128-bit block (2 uniforms / 2 normals) within an op.
+ */
+WSMC_HD wsmc_u32x4 wsmc_rng_block(uint64_t seed, uint64_t op, uint64_t idx, uint32_t block) {
+    return wsmc_philox((uint32_t)idx, (uint32_t)(idx >> 32) ^ (block << 16),
+                       (uint32_t)op, (uint32_t)(op >> 32),
+                       (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+/* 53-bit uniform in [0,1) from two words */
+WSMC_HD double wsmc_u01(uint32_t hi, uint32_t lo) {
+    uint64_t x = (((uint64_t)hi << 32) | lo) >> 11;
+    return (double)(int64_t)x * 1.1102230246251565404e-16; /* 2^-53; x < 2^53 exactly representable */
+}
+/* 53-bit uniform in (0,1] */
+WSMC_HD double wsmc_u01_open0(uint32_t hi, uint32_t lo) {
+    uint64_t x = ((((uint64_t)hi << 32) | lo) >> 11) + 1;
+    return (double)(int64_t)x * 1.1102230246251565404e-16;
+}
+
+/* ------------------------------------------------------------------------- */
+/* exp / log / log1p  (fdlibm e_exp.c / e_log.c algorithms, restated)         */
+/* ------------------------------------------------------------------------- */
+WSMC_HD double wsmc_scalbn_small(double y, int k) {
+    /* y in [0.5, 2), returns y * 2^k with a single rounding for normal results */
+    if (k > 1023) return y * wsmc_pow2i(1023) * wsmc_pow2i(k - 1023);
+    if (k < -1021) return (y * wsmc_pow2i(k + 1000)) * wsmc_pow2i(-1000);
+    return y * wsmc_pow2i(k);
+}
+
+WSMC_HD double wsmc_exp(double x) {
+    const double ln2hi = 6.93147180369123816490e-01, ln2lo = 1.90821492927058770002e-10,
+                 invln2 = 1.44269504088896338700e+00,
+                 P1 = 1.66666666666666019037e-01, P2 = -2.77777777770155933842e-03,
+                 P3 = 6.61375632143793436117e-05, P4 = -1.65339022054652515390e-06,
+                 P5 = 4.13813679705723846039e-08;
+    if (wsmc_isnan(x)) return x;
+    if (x > 709.782712893383973096) return WSMC_INF;
+    if (x < -745.13321910194110842) return 0.0;
+    double ax = wsmc_fabs(x);
+    if (ax < 3.725290298461914e-09) return 1.0 + x;  /* |x| < 2^-28 */
+    int k; double hi, lo;
+    if (ax < 0.34657359027997264) {                     /* |x| < 0.5 ln2 */
+        k = 0; hi = x; lo = 0.0;
+    } else {
+        k = (int)(x * invln2 + (x < 0.0 ? -0.5 : 0.5));
+        hi = x - (double)k * ln2hi;
+        lo = (double)k * ln2lo;
+    }
+    double r = hi - lo;
+    double z = r * r;
+    double c = r - z * (P1 + z * (P2 + z * (P3 + z * (P4 + z * P5))));
+    double y = 1.0 - ((lo - (r * c) / (2.0 - c)) - hi);
+    if (k == 0) return y;
+    return wsmc_scalbn_small(y, k);
+}
+
+WSMC_HD double wsmc_log(double x) {
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+                 Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
+                 Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
+                 Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+                 Lg7 = 1.479819860511658591e-01;
+    if (wsmc_isnan(x)) return x;
+    if (x < 0.0) return WSMC_NAN;
+    if (x == 0.0) return -WSMC_INF;
+    if (x == WSMC_INF) return x;
+    uint64_t b = wsmc_d2bits(x);
+    int k = 0;
+    if ((b >> 52) == 0) { x *= 18014398509481984.0; b = wsmc_d2bits(x); k = -54; } /* subnormal: *2^54 */
+    uint32_t hx = (uint32_t)(b >> 32);
+    k += (int)(hx >> 20) - 1023;
+    hx &= 0x000fffffu;
+    uint32_t i = (hx + 0x95f64u) & 0x100000u;
+    b = ((uint64_t)(hx | (i ^ 0x3ff00000u)) << 32) | (b & 0xffffffffULL);
+    x = wsmc_bits2d(b);                   /* x in [sqrt(2)/2, sqrt(2)) */
+    k += (int)(i >> 20);
+    double f = x - 1.0;
+    double s = f / (2.0 + f);
+    double dk = (double)k;
+    double z = s * s, w = z * z;
+    double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+    double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+    double R = t2 + t1;
+    double hfsq = 0.5 * f * f;
+    return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+}
+
+/* log1p via the Goldberg correction (accurate to a few ulp; used for log1pexp) */
+WSMC_HD double wsmc_log1p(double x) {
+    double u = 1.0 + x;
+    if (u == 1.0) return x;
+    if (u == WSMC_INF) return u;
+    return wsmc_log(u) * (x / (u - 1.0));
+}
+
+WSMC_HD double wsmc_sqrt(double x) { return __builtin_sqrt(x); }
+
+/* ------------------------------------------------------------------------- */
+/* sin / cos (fdlibm k_sin.c / k_cos.c kernels + Cody–Waite reduction)        */
+/* ------------------------------------------------------------------------- */
+WSMC_HD double wsmc_ksin(double x) {   /* |x| <= pi/4 */
+    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    double z = x * x;
+    double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+    return x + (x * z) * (S1 + z * r);
+}
+WSMC_HD double wsmc_kcos(double x) {   /* |x| <= pi/4 */
+    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    double z = x * x;
+    double r = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+    double hz = 0.5 * z;
+    double w = 1.0 - hz;
+    return w + (((1.0 - w) - hz) + z * r);
+}
+
+/* cos(2*pi*u), sin(2*pi*u) for u in [0,1), exact octant reduction */
+WSMC_HD void wsmc_sincos2pi(double u, double* s, double* c) {
+    const double PIO4 = 7.85398163397448278999e-01;
+    double y = u * 8.0;
+    int o = (int)y;
+    double f = y - (double)o;
+    if (o & 1) f = 1.0 - f;
+    double t = f * PIO4;
+    double st = wsmc_ksin(t), ct = wsmc_kcos(t);
+    double cs, sn;
+    switch (o & 7) {
+        case 0: cs = ct;  sn = st;  break;
+        case 1: cs = st;  sn = ct;  break;
+        case 2: cs = -st; sn = ct;  break;
+        case 3: cs = -ct; sn = st;  break;
+        case 4: cs = -ct; sn = -st; break;
+        case 5: cs = -st; sn = -ct; break;
+        case 6: cs = st;  sn = -ct; break;
+        default: cs = ct; sn = -st; break;
+    }
+    *s = sn; *c = cs;
+}
+
+/* cos(x) for |x| < 2^19*pi/2 (Cody–Waite three-part pi/2); NaN/inf -> NaN */
+WSMC_HD double wsmc_cos(double x) {
+    const double invpio2 = 6.36619772367581382433e-01,
+                 p1 = 1.57079632673412561417e+00,   /* first 33 bits of pi/2 */
+                 p2 = 6.07710050630396597660e-11,   /* next 33 bits */
+                 p3 = 2.02226624879595063154e-21;   /* pi/2 - p1 - p2 */
+    if (!wsmc_isfinite(x)) return WSMC_NAN;
+    double ax = wsmc_fabs(x);
+    if (ax <= 7.85398163397448278999e-01) return wsmc_kcos(x);
+    double fn = (double)(int64_t)(ax * invpio2 + 0.5);
+    double r = ((ax - fn * p1) - fn * p2) - fn * p3;
+    int n = (int)((int64_t)fn & 3);
+    switch (n) {
+        case 0: return wsmc_kcos(r);
+        case 1: return -wsmc_ksin(r);
+        case 2: return -wsmc_kcos(r);
+        default: return wsmc_ksin(r);
+    }
+}
+
+/* ------------------------------------------------------------------------- */
+/* draws                                                                      */
+/* ------------------------------------------------------------------------- */
+/* Box–Muller pair from one Philox block: z0 = r cos(2πu2), z1 = r sin(2πu2) */
+WSMC_HD void wsmc_normal_pair(wsmc_u32x4 w, double* z0, double* z1) {
+    double u1 = wsmc_u01_open0(w.v[0], w.v[1]);
+    double u2 = wsmc_u01(w.v[2], w.v[3]);
+    double r = wsmc_sqrt(-2.0 * wsmc_log(u1));
+    double s, c;
+    wsmc_sincos2pi(u2, &s, &c);
+    *z0 = r * c; *z1 = r * s;
+}
+/* k-th standard normal of (op, idx) */
+WSMC_HD double wsmc_normal_k(uint64_t seed, uint64_t op, uint64_t idx, uint32_t k) {
+    double z0, z1;
+    wsmc_normal_pair(wsmc_rng_block(seed, op, idx, k >> 1), &z0, &z1);
+    return (k & 1) ? z1 : z0;
+}
+/* k-th uniform in [0,1) of (op, idx) */
+WSMC_HD double wsmc_uniform_k(uint64_t seed, uint64_t op, uint64_t idx, uint32_t k) {
+    wsmc_u32x4 w = wsmc_rng_block(seed, op, idx, (k >> 1) | 0x80u);
+    return (k & 1) ? wsmc_u01(w.v[2], w.v[3]) : wsmc_u01(w.v[0], w.v[1]);
+}
+/* 32-bit stratum offset word for resampling slot n (systematic: n = 0) */
+WSMC_HD uint32_t wsmc_strat_word(uint64_t seed, uint64_t op, uint64_t n) {
+    return wsmc_rng_block(seed, op, n, 0x40u).v[0];
+}
+
+/* ------------------------------------------------------------------------- */
+/* log-densities (Distributions.jl semantics)                                 */
+/* ------------------------------------------------------------------------- */
+/* Normal(mu, sigma): -(z^2 + log(2pi))/2 - log(sigma),  z = (x - mu)/sigma     */
+WSMC_HD double wsmc_normal_logpdf(double mu, double sigma, double x) {
+    double z = (x - mu) / sigma;
+    return -(z * z + WSMC_LOG2PI) * 0.5 - wsmc_log(sigma);
+}
+/* Truncated(Normal(0, sigma), 0, Inf) — examples/damped_oscillator.jl:24-28 */
+WSMC_HD double wsmc_halfnormal_logpdf(double sigma, double x) {
+    if (!(x >= 0.0)) return -WSMC_INF;
+    return wsmc_normal_logpdf(0.0, sigma, x) + WSMC_LOG2;
+}
+/* Uniform(a, b) on the closed support [a, b] */
+WSMC_HD double wsmc_uniform_logpdf(double a, double b, double x) {
+    if (!(x >= a && x <= b)) return -WSMC_INF;
+    return -wsmc_log(b - a);
+}
+/* the damped-oscillator mean, examples/damped_oscillator.jl:11 */
+WSMC_HD double wsmc_oscillator(double t, double A, double om, double ga, double ph) {
+    return A * wsmc_exp(-ga * t) * wsmc_cos(om * t + ph);
+}
+
+/* ------------------------------------------------------------------------- */
+/* bound transforms of RW/autoRW (src/move_kernels.jl:37-85)                  */
+/* ------------------------------------------------------------------------- */
+WSMC_HD double wsmc_to_unc(double x, double lo, double hi) {
+    int flo = wsmc_isfinite(lo), fhi = wsmc_isfinite(hi);
+    if (flo && fhi) return wsmc_log(x - lo) - wsmc_log(hi - x);
+    if (flo) return wsmc_log(x - lo);
+    if (fhi) return wsmc_log(hi - x);
+    return x;
+}
+WSMC_HD double wsmc_from_unc(double z, double lo, double hi) {
+    int flo = wsmc_isfinite(lo), fhi = wsmc_isfinite(hi);
+    if (flo && fhi) return lo + (hi - lo) / (1.0 + wsmc_exp(-z));
+    if (flo) return lo + wsmc_exp(z);
+    if (fhi) return hi - wsmc_exp(z);
+    return z;
+}
+WSMC_HD double wsmc_log1pexp(double z) {
+    return z > 0.0 ? z + wsmc_log1p(wsmc_exp(-z)) : wsmc_log1p(wsmc_exp(z));
+}
+WSMC_HD double wsmc_log_abs_jac(double z, double lo, double hi) {
+    int flo = wsmc_isfinite(lo), fhi = wsmc_isfinite(hi);
+    if (flo && fhi) return wsmc_log(hi - lo) - wsmc_log1pexp(z) - wsmc_log1pexp(-z);
+    if (flo || fhi) return z;
+    return 0.0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* integer weights, ESS, and the stratified/systematic target map            */
+/* ------------------------------------------------------------------------- */
+/*
+ * exp_norm/ess_perc/icdf (src/resampling.jl:13-77) on an integer CDF:
+ *   q_i = floor(exp(lw_i - M) * 2^K),  K = 63 - ceil(log2 N)   =>  Q = sum q_i <= 2^63
+ * Integer sums are associative, so the CDF, Q, sum q^2 (ESS) and the ancestors are
+ * identical for any reduction order, grid shape or shard count.
+ */
+WSMC_HD int wsmc_qbits(uint64_t n) {
+    int c = 0;
+    while (((uint64_t)1 << c) < n) ++c;   /* ceil(log2 n) */
+    return 63 - c;
+}
+WSMC_HD uint64_t wsmc_qweight(double lw, double M, int K) {
+    double e = wsmc_exp(lw - M);
+    if (!(e > 0.0)) return 0;            /* -inf weights, NaN */
+    return wsmc_d_to_u64_trunc(e * wsmc_pow2i(K));
+}
+
+/*
+ * Targets: slot n (0-based) has A_n = n*2^32 + R_n (stratified: R_n = strat word of n;
+ * systematic: R_n = R_0), and x_n = floor(A_n * Q / (N * 2^32)) in [0, Q).  This is
+ * us[n] = (n-1)/N + rand()/N of src/resampling.jl:40 with the uniform on a 2^-32 grid,
+ * scaled to the integer CDF. ancestor(n) = smallest m with C_m > x_n, where C_m is the
+ * inclusive prefix of q — the `while s < us[n]` merge of src/resampling.jl:18-24.
+ */
+WSMC_HD uint64_t wsmc_target(uint64_t n, uint32_t R, uint64_t Q, uint64_t N) {
+    wsmc_u128 A = ((wsmc_u128)n << 32) | R;
+    wsmc_u128 num = A * (wsmc_u128)Q;
+    wsmc_u128 den = (wsmc_u128)N << 32;
+    return (uint64_t)(num / den);
+}
+
+/* #{ n : x_n < c }  (monotone in c); scheme 0 = stratified, 1 = systematic */
+WSMC_HD uint64_t wsmc_rank(uint64_t c, uint64_t Q, uint64_t N, int scheme,
+                           uint64_t seed, uint64_t op, uint64_t slot_base) {
+    if (c == 0) return 0;
+    if (c >= Q) return N;
+    wsmc_u128 cN = (wsmc_u128)c * (wsmc_u128)N;
+    /* n* = floor(c*N/Q): float estimate then exact integer correction */
+    double est = wsmc_u64_to_d(c) * wsmc_u64_to_d(N) / wsmc_u64_to_d(Q);
+    uint64_t ns = wsmc_d_to_u64_trunc(est);
+    if (ns > N) ns = N;
+    while ((wsmc_u128)ns * Q > cN) --ns;
+    while ((wsmc_u128)(ns + 1) * Q <= cN) ++ns;
+    if (ns >= N) return N;
+    uint32_t R = wsmc_strat_word(seed, op, scheme == 1 ? slot_base : slot_base + ns);
+    wsmc_u128 lhs = (((wsmc_u128)ns << 32) | R) * (wsmc_u128)Q;
+    wsmc_u128 rhs = cN << 32;
+    return ns + (lhs < rhs ? 1u : 0u);
+}
+
+/* 4x4-max Cholesky of a symmetric matrix (row-major a[d*d]) -> lower L; 0 if not PD */
+WSMC_HD int wsmc_cholesky(const double* a, double* L, int d) {
+    for (int i = 0; i < d * d; ++i) L[i] = 0.0;
+    for (int j = 0; j < d; ++j) {
+        double s = a[j * d + j];
+        for (int k = 0; k < j; ++k) s -= L[j * d + k] * L[j * d + k];
+        if (!(s > 0.0)) return 0;
+        double ljj = wsmc_sqrt(s);
+        L[j * d + j] = ljj;
+        for (int i = j + 1; i < d; ++i) {
+            double t = a[i * d + j];
+            for (int k = 0; k < j; ++k) t -= L[i * d + k] * L[j * d + k];
+            L[i * d + j] = t / ljj;
+        }
+    }
+    return 1;
+}
+
+/*
+ * Per-shard weight statistics and the global Resample decision
+ * (src/transformers.jl:479-489). G = 1 is the single-GPU case; G > 1 combines shard
+ * records in rank order (island resampling). Shared by oracle and kernels.
+ */
+typedef struct {
+    double M;          /* shard max log-weight (NaN if any NaN) */
+    uint64_t Q;        /* sum q_i */
+    wsmc_u128 Q2;      /* sum q_i^2 */
+    wsmc_u128 W;       /* sum floor(exp(lw_i - M) * 2^96) */
+    uint64_t n;        /* shard size */
+} wsmc_shard_stats;
+
+/* ess_perc = (sum w)^2 / (N sum w^2) with w = exp_norm(weights) (src/resampling.jl:51-54) */
+WSMC_HD double wsmc_global_ess(const wsmc_shard_stats* st, int G) {
+    double M = -WSMC_INF;
+    uint64_t N = 0;
+    int nan = 0;
+    for (int g = 0; g < G; ++g) {
+        if (wsmc_isnan(st[g].M)) nan = 1;
+        else if (st[g].M > M) M = st[g].M;
+        N += st[g].n;
+    }
+    if (nan) M = WSMC_NAN;
+    double sq = 0.0, sq2 = 0.0;
+    for (int g = 0; g < G; ++g) {
+        double f = wsmc_exp(st[g].M - M);
+        double sc = wsmc_pow2i(-wsmc_qbits(st[g].n));
+        double qd = wsmc_u64_to_d(st[g].Q), q2d = wsmc_u128_to_d(st[g].Q2);
+        sq = sq + (qd * sc) * f;
+        sq2 = sq2 + ((q2d * sc) * sc) * (f * f);
+    }
+    return (sq * sq) / (wsmc_u64_to_d(N) * sq2);
+}
+/* logsumexp(shard weights) - log(n): the value every weight is reset to (src/transformers.jl:486-489) */
+WSMC_HD double wsmc_shard_mean(const wsmc_shard_stats* s) {
+    double S = wsmc_u128_to_d(s->W) * wsmc_pow2i(-96);
+    return (s->M + wsmc_log(S)) - wsmc_log(wsmc_u64_to_d(s->n));
+}
+/* logsumexp(all weights) - log(N)  (src/utils.jl:21) */
+WSMC_HD double wsmc_global_log_evidence(const wsmc_shard_stats* st, int G) {
+    double M = -WSMC_INF;
+    uint64_t N = 0;
+    for (int g = 0; g < G; ++g) {
+        if (st[g].M > M || wsmc_isnan(st[g].M)) M = st[g].M;
+        N += st[g].n;
+    }
+    double S = 0.0;
+    for (int g = 0; g < G; ++g)
+        S = S + (wsmc_u128_to_d(st[g].W) * wsmc_pow2i(-96)) * wsmc_exp(st[g].M - M);
+    return (M + wsmc_log(S)) - wsmc_log(wsmc_u64_to_d(N));
+}
+
+#endif /* WSMC_MATH_H */

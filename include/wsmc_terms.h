@@ -1,0 +1,136 @@
+/*
+ * wsmc_terms.h — per-particle evaluation of operator arguments, draws, log-densities
+ * and the score fold. Shared verbatim by the HIP kernels and the CPU oracle so that
+ * every per-particle value is computed by the same sequence of IEEE operations.
+ *
+ *   operand     argfn shapes of @model `vectorize` (src/rewrites.jl:146-219)
+ *   sample      WeightedKernel.sampler = rand(D(args...))   (src/default_kernels.jl:18)
+ *   logpdf      WeightedKernel.logpdf  = logpdf(D(args...), x) (src/default_kernels.jl:20)
+ *   fold        score_logpdf!: scores start at 0.0 and every counted statement executed
+ *               before target_depth adds its term in program order
+ *               (src/types.jl:198-206, Sequence early stop src/transformers.jl:343-349)
+ */
+#ifndef WSMC_TERMS_H
+#define WSMC_TERMS_H
+
+#include "wsmc.h"
+#include "wsmc_math.h"
+
+/* MH proposal values substituted for target columns during the s_new fold */
+typedef struct {
+    int32_t n;
+    int32_t col[4];
+    double  val[4];
+} wsmc_override;
+
+WSMC_HD double wsmc_colval(double* const* cols, int64_t N, int32_t col, int32_t comp, int64_t i,
+                           const wsmc_override* ov) {
+    if (ov) {
+        for (int k = 0; k < ov->n; ++k)
+            if (ov->col[k] == col && comp == 0) return ov->val[k];
+    }
+    return cols[col][(int64_t)comp * N + i];
+}
+
+WSMC_HD double wsmc_operand_eval(const wsmc_operand* o, double* const* cols, int64_t N, int64_t i,
+                                 const wsmc_override* ov) {
+    double v = o->c0;
+    if (o->col[0] >= 0) v = v + o->coef[0] * wsmc_colval(cols, N, o->col[0], o->comp[0], i, ov);
+    if (o->col[1] >= 0) v = v + o->coef[1] * wsmc_colval(cols, N, o->col[1], o->comp[1], i, ov);
+    return v;
+}
+
+WSMC_HD double wsmc_dist_mean(const wsmc_dist* d, int k, double* const* cols, int64_t N, int64_t i,
+                              const wsmc_override* ov) {
+    if (d->mean_fn == WSMC_MEAN_OSCILLATOR) {
+        double A = wsmc_operand_eval(&d->mu[0], cols, N, i, ov);
+        double om = wsmc_operand_eval(&d->mu[1], cols, N, i, ov);
+        double ga = wsmc_operand_eval(&d->mu[2], cols, N, i, ov);
+        double ph = wsmc_operand_eval(&d->mu[3], cols, N, i, ov);
+        return wsmc_oscillator(d->param[0], A, om, ga, ph);
+    }
+    return wsmc_operand_eval(&d->mu[k], cols, N, i, ov);
+}
+
+/* logpdf(D(args...), x) for the supported families */
+WSMC_HD double wsmc_dist_logpdf(const wsmc_dist* d, const double* x, double* const* cols, int64_t N,
+                                int64_t i, const wsmc_override* ov) {
+    switch (d->family) {
+        case WSMC_FAM_NORMAL: {
+            double mu = wsmc_dist_mean(d, 0, cols, N, i, ov);
+            double sg = wsmc_operand_eval(&d->scale, cols, N, i, ov);
+            return wsmc_normal_logpdf(mu, sg, x[0]);
+        }
+        case WSMC_FAM_HALFNORMAL: {
+            double sg = wsmc_operand_eval(&d->scale, cols, N, i, ov);
+            return wsmc_halfnormal_logpdf(sg, x[0]);
+        }
+        case WSMC_FAM_UNIFORM:
+            return wsmc_uniform_logpdf(d->param[0], d->param[1], x[0]);
+        default: { /* WSMC_FAM_MVNORMAL_ISO: -(d log2pi + d log var + |x-mu|^2/var)/2 */
+            double var = wsmc_operand_eval(&d->scale, cols, N, i, ov);
+            double s = 0.0;
+            for (int k = 0; k < d->dim && k < 4; ++k) {
+                double dx = x[k] - wsmc_dist_mean(d, k, cols, N, i, ov);
+                s = s + dx * dx;
+            }
+            double dd = (double)d->dim;
+            return -((dd * WSMC_LOG2PI + dd * wsmc_log(var)) + s / var) * 0.5;
+        }
+    }
+}
+
+/* rand(D(args...)) for particle i (global RNG index idx) */
+WSMC_HD void wsmc_dist_sample(const wsmc_dist* d, double* x, uint64_t seed, uint64_t op, uint64_t idx,
+                              double* const* cols, int64_t N, int64_t i) {
+    switch (d->family) {
+        case WSMC_FAM_NORMAL: {
+            double mu = wsmc_dist_mean(d, 0, cols, N, i, 0);
+            double sg = wsmc_operand_eval(&d->scale, cols, N, i, 0);
+            x[0] = mu + sg * wsmc_normal_k(seed, op, idx, 0);
+            break;
+        }
+        case WSMC_FAM_HALFNORMAL: {
+            double sg = wsmc_operand_eval(&d->scale, cols, N, i, 0);
+            x[0] = sg * wsmc_fabs(wsmc_normal_k(seed, op, idx, 0));
+            break;
+        }
+        case WSMC_FAM_UNIFORM: {
+            double a = d->param[0], b = d->param[1];
+            x[0] = a + (b - a) * wsmc_uniform_k(seed, op, idx, 0);
+            break;
+        }
+        default: {
+            double var = wsmc_operand_eval(&d->scale, cols, N, i, 0);
+            double sd = wsmc_sqrt(var);
+            for (int k = 0; k < d->dim && k < 4; k += 2) {
+                double z0, z1;
+                wsmc_normal_pair(wsmc_rng_block(seed, op, idx, (uint32_t)(k >> 1)), &z0, &z1);
+                x[k] = wsmc_dist_mean(d, k, cols, N, i, 0) + sd * z0;
+                if (k + 1 < d->dim) x[k + 1] = wsmc_dist_mean(d, k + 1, cols, N, i, 0) + sd * z1;
+            }
+            break;
+        }
+    }
+}
+
+WSMC_HD double wsmc_term_logpdf(const wsmc_term* t, double* const* cols, int64_t N, int64_t i,
+                                const wsmc_override* ov) {
+    double x[4] = {0.0, 0.0, 0.0, 0.0};
+    int dim = t->dist.dim < 1 ? 1 : (t->dist.dim > 4 ? 4 : t->dist.dim);
+    for (int k = 0; k < dim; ++k) x[k] = wsmc_operand_eval(&t->x[k], cols, N, i, ov);
+    return wsmc_dist_logpdf(&t->dist, x, cols, N, i, ov);
+}
+
+/* score_logpdf! for one particle: 0.0 then += each term with depth < target_depth */
+WSMC_HD double wsmc_fold(const wsmc_term* terms, int32_t n, int32_t target_depth, double* const* cols,
+                         int64_t N, int64_t i, const wsmc_override* ov) {
+    double s = 0.0;
+    for (int32_t j = 0; j < n; ++j) {
+        if (terms[j].depth >= target_depth) break;
+        s = s + wsmc_term_logpdf(&terms[j], cols, N, i, ov);
+    }
+    return s;
+}
+
+#endif /* WSMC_TERMS_H */

@@ -1,0 +1,284 @@
+"""ctypes wrapper of the CPU oracle (oracle/wsmc_oracle.c).
+
+TEST INFRASTRUCTURE ONLY — imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, as the checker or the timed CPU baseline. The product never imports
+this module.
+
+``Oracle`` implements the same low-level context protocol as the product's
+``wsmc.Context`` (col_create / col_upload / col_download / assign / sample / observe /
+weight / resample / move / ...), so a model written against that protocol can be run on
+both and compared bit for bit.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import pathlib
+import subprocess
+
+import numpy as np
+
+_DIR = pathlib.Path(__file__).resolve().parent
+LIB_PATH = _DIR / "liboracle.so"
+
+_P = C.c_void_p
+_D = C.POINTER(C.c_double)
+_I32P = C.POINTER(C.c_int32)
+_SIG = {
+    "or_create": (_P, [C.c_int64, C.c_uint64]),
+    "or_destroy": (None, [_P]),
+    "or_set_shards": (C.c_int, [_P, C.c_int32]),
+    "or_nparticles": (C.c_int64, [_P]),
+    "or_get_op": (C.c_uint64, [_P]),
+    "or_set_op": (None, [_P, C.c_uint64]),
+    "or_get_depth": (C.c_int32, [_P]),
+    "or_set_depth": (None, [_P, C.c_int32]),
+    "or_resampled": (C.c_int32, [_P]),
+    "or_weights_changed": (C.c_int32, [_P]),
+    "or_last_ess": (C.c_double, [_P]),
+    "or_n_resamples": (C.c_int64, [_P]),
+    "or_nterms": (C.c_int32, [_P]),
+    "or_weights": (_D, [_P]),
+    "or_last_anc": (_I32P, [_P]),
+    "or_col_find": (C.c_int32, [_P, C.c_char_p]),
+    "or_col_create": (C.c_int32, [_P, C.c_char_p, C.c_int32]),
+    "or_col_dim": (C.c_int32, [_P, C.c_int32]),
+    "or_col_count": (C.c_int32, [_P]),
+    "or_col_name": (C.c_char_p, [_P, C.c_int32]),
+    "or_col_data": (_D, [_P, C.c_int32]),
+    "or_store_resample": (None, [_P, _I32P]),
+    "or_assign": (C.c_int, [_P, C.c_int32, _P]),
+    "or_sample": (C.c_int, [_P, C.c_int32, _P]),
+    "or_sample_importance": (C.c_int, [_P, C.c_int32, _P, _P]),
+    "or_observe": (C.c_int, [_P, _P, _P]),
+    "or_weight": (C.c_int, [_P, _P, _P]),
+    "or_resample": (C.c_int, [_P, C.c_double, C.c_int32, _I32P, _D]),
+    "or_log_evidence": (C.c_double, [_P]),
+    "or_canon_sum": (C.c_double, [_D, C.c_int64]),
+    "or_marginal_diversity": (C.c_double, [_P, _I32P, C.c_int32]),
+    "or_autorw_chol": (C.c_int, [_P, _I32P, C.c_int32, C.c_double, _D, _D, _D, _D]),
+    "or_move": (C.c_int, [_P, C.c_int32, _I32P, C.c_int32, C.c_double, _D, _D, C.c_int32,
+                          C.c_double, C.POINTER(C.c_int64)]),
+    "or_score": (None, [_P, C.c_int32, _D]),
+    "or_philox": (None, [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    "or_exp": (C.c_double, [C.c_double]),
+    "or_log": (C.c_double, [C.c_double]),
+    "or_log1p": (C.c_double, [C.c_double]),
+    "or_cos": (C.c_double, [C.c_double]),
+    "or_sincos2pi": (None, [C.c_double, _D, _D]),
+    "or_normal_k": (C.c_double, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32]),
+    "or_uniform_k": (C.c_double, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32]),
+    "or_rank": (C.c_uint64, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, C.c_uint64, C.c_uint64,
+                             C.c_uint64]),
+    "or_target": (C.c_uint64, [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64]),
+    "or_strat_word": (C.c_uint32, [C.c_uint64, C.c_uint64, C.c_uint64]),
+    "or_qweight": (C.c_uint64, [C.c_double, C.c_double, C.c_int]),
+    "or_qbits": (C.c_int, [C.c_uint64]),
+    "or_sizeof_term": (C.c_int32, []),
+    "or_sizeof_dist": (C.c_int32, []),
+}
+
+_lib = None
+
+
+def build() -> pathlib.Path:
+    subprocess.run(["make", "-s", "-C", str(_DIR)], check=True)
+    return LIB_PATH
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            build()
+        L = C.CDLL(str(LIB_PATH))
+        for name, (res, args) in _SIG.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _addr(obj) -> int:
+    return C.addressof(obj)
+
+
+def _dptr(a: np.ndarray):
+    return a.ctypes.data_as(_D)
+
+
+class Oracle:
+    """Sequential CPU restatement behind the same protocol as wsmc.Context."""
+
+    is_oracle = True
+
+    def __init__(self, n_particles: int, seed: int = 42, shards: int = 1):
+        self._L = lib()
+        self._h = self._L.or_create(int(n_particles), int(seed) & (2**64 - 1))
+        if not self._h:
+            raise ValueError("or_create failed")
+        self.n = int(n_particles)
+        self.seed = int(seed)
+        if shards != 1 and self._L.or_set_shards(self._h, int(shards)) != 0:
+            raise ValueError("bad shard count")
+        self.shards = shards
+
+    def close(self):
+        if self._h:
+            self._L.or_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- store ----
+    def col_find(self, name: str) -> int:
+        return int(self._L.or_col_find(self._h, name.encode()))
+
+    def col_create(self, name: str, dim: int = 1) -> int:
+        c = int(self._L.or_col_create(self._h, name.encode(), int(dim)))
+        if c < 0:
+            raise ValueError(f"cannot create column {name!r} (dim {dim})")
+        return c
+
+    def col_dim(self, col: int) -> int:
+        return int(self._L.or_col_dim(self._h, col))
+
+    def col_names(self):
+        return [self._L.or_col_name(self._h, c).decode() for c in range(self._L.or_col_count(self._h))]
+
+    def col_download(self, col: int) -> np.ndarray:
+        d = self.col_dim(col)
+        p = self._L.or_col_data(self._h, col)
+        a = np.ctypeslib.as_array(p, shape=(d * self.n,)).copy()
+        return a.reshape(d, self.n) if d > 1 else a
+
+    def col_upload(self, col: int, values) -> None:
+        d = self.col_dim(col)
+        v = np.ascontiguousarray(np.asarray(values, dtype=np.float64).reshape(d * self.n))
+        p = self._L.or_col_data(self._h, col)
+        np.ctypeslib.as_array(p, shape=(d * self.n,))[:] = v
+
+    def store_resample(self, indices) -> None:
+        idx = np.ascontiguousarray(np.asarray(indices, dtype=np.int32))
+        self._L.or_store_resample(self._h, idx.ctypes.data_as(_I32P))
+
+    # ---- weights / state ----
+    def weights_download(self) -> np.ndarray:
+        return np.ctypeslib.as_array(self._L.or_weights(self._h), shape=(self.n,)).copy()
+
+    def weights_upload(self, w) -> None:
+        np.ctypeslib.as_array(self._L.or_weights(self._h), shape=(self.n,))[:] = np.asarray(w, float)
+
+    def log_evidence(self) -> float:
+        return float(self._L.or_log_evidence(self._h))
+
+    def get_state(self) -> dict:
+        L, h = self._L, self._h
+        return dict(resampled=int(L.or_resampled(h)), weights_changed=int(L.or_weights_changed(h)),
+                    depth=int(L.or_get_depth(h)), n_terms=int(L.or_nterms(h)),
+                    last_ess_perc=float(L.or_last_ess(h)), op_counter=int(L.or_get_op(h)),
+                    n_resamples=int(L.or_n_resamples(h)))
+
+    def set_depth(self, d: int) -> None:
+        self._L.or_set_depth(self._h, int(d))
+
+    def set_op_counter(self, op: int) -> None:
+        self._L.or_set_op(self._h, int(op))
+
+    def last_ancestors(self) -> np.ndarray:
+        return np.ctypeslib.as_array(self._L.or_last_anc(self._h), shape=(self.n,)).copy()
+
+    # ---- operators ----
+    def _chk(self, r):
+        if r != 0:
+            raise RuntimeError(f"oracle op failed ({r})")
+
+    def assign(self, out: int, exprs) -> None:
+        arr = _operand_array(exprs)
+        self._chk(self._L.or_assign(self._h, out, _addr(arr)))
+        self.depth_bump = None
+
+    def sample(self, out: int, dist) -> None:
+        self._chk(self._L.or_sample(self._h, out, _addr(dist)))
+
+    def sample_importance(self, out: int, proposal, target) -> None:
+        self._chk(self._L.or_sample_importance(self._h, out, _addr(proposal), _addr(target)))
+
+    def observe(self, dist, x) -> None:
+        arr = _operand_array(x)
+        self._chk(self._L.or_observe(self._h, _addr(dist), _addr(arr)))
+
+    def weight(self, dist, x) -> None:
+        arr = _operand_array(x)
+        self._chk(self._L.or_weight(self._h, _addr(dist), _addr(arr)))
+
+    def resample(self, ess_perc_min: float, scheme: int = 0):
+        r = C.c_int32()
+        e = C.c_double()
+        self._chk(self._L.or_resample(self._h, float(ess_perc_min), int(scheme), C.byref(r), C.byref(e)))
+        return bool(r.value), float(e.value)
+
+    def move(self, proposal: int, targets, step: float, lo=None, hi=None, target_depth: int = -1,
+             diversity: float = float("nan")) -> int:
+        t = np.ascontiguousarray(np.asarray(targets, dtype=np.int32))
+        d = len(t)
+        lo_a = None if lo is None else np.ascontiguousarray(np.asarray(lo, float).reshape(d))
+        hi_a = None if hi is None else np.ascontiguousarray(np.asarray(hi, float).reshape(d))
+        acc = C.c_int64()
+        r = self._L.or_move(self._h, int(proposal), t.ctypes.data_as(_I32P), d, float(step),
+                            None if lo_a is None else _dptr(lo_a), None if hi_a is None else _dptr(hi_a),
+                            int(target_depth), float(diversity), C.byref(acc))
+        if r == 3:
+            raise np.linalg.LinAlgError("proposal covariance not positive definite")
+        self._chk(r)
+        return int(acc.value)
+
+    def score(self, target_depth: int) -> np.ndarray:
+        out = np.empty(self.n)
+        self._L.or_score(self._h, int(target_depth), _dptr(out))
+        return out
+
+    def marginal_diversity(self, targets) -> float:
+        t = np.ascontiguousarray(np.asarray(targets, dtype=np.int32))
+        return float(self._L.or_marginal_diversity(self._h, t.ctypes.data_as(_I32P), len(t)))
+
+    def autorw_cov(self, targets, min_step=1e-3, lo=None, hi=None):
+        t = np.ascontiguousarray(np.asarray(targets, dtype=np.int32))
+        d = len(t)
+        L = np.zeros(d * d)
+        cov = np.zeros(d * d)
+        lo_a = None if lo is None else np.ascontiguousarray(np.asarray(lo, float).reshape(d))
+        hi_a = None if hi is None else np.ascontiguousarray(np.asarray(hi, float).reshape(d))
+        ok = self._L.or_autorw_chol(self._h, t.ctypes.data_as(_I32P), d, float(min_step),
+                                    None if lo_a is None else _dptr(lo_a),
+                                    None if hi_a is None else _dptr(hi_a), _dptr(L), _dptr(cov))
+        return bool(ok), cov.reshape(d, d), L.reshape(d, d)
+
+
+def _operand_array(exprs):
+    from_list = list(exprs) if isinstance(exprs, (list, tuple)) else [exprs]
+    typ = type(from_list[0])
+    arr = (typ * 4)()
+    for k in range(4):
+        src = from_list[k] if k < len(from_list) else from_list[0]
+        C.memmove(C.addressof(arr) + k * C.sizeof(typ), C.addressof(src), C.sizeof(typ))
+    return arr
+
+
+# ---- raw primitives ------------------------------------------------------------------
+def philox(ctr, key):
+    c = (C.c_uint32 * 4)(*ctr)
+    k = (C.c_uint32 * 2)(*key)
+    o = (C.c_uint32 * 4)()
+    lib().or_philox(c, k, o)
+    return list(o)
+
+
+def canon_sum(vals) -> float:
+    v = np.ascontiguousarray(np.asarray(vals, dtype=np.float64))
+    return float(lib().or_canon_sum(_dptr(v), len(v)))

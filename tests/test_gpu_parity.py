@@ -1,0 +1,117 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle, bit for bit.
+
+Integer/index results (ancestors, resample decisions, RNG positions) must be identical;
+floating columns and log-weights are compared bitwise too — both sides evaluate the same
+IEEE operation sequence (include/wsmc_math.h) — with the north-star tolerance (1e-6
+relative on log-weights) reported as the acceptance bar where a reduction order differs.
+"""
+import math
+
+import numpy as np
+import pytest
+
+import wsmc
+from wsmc import abi, models
+from oracle import Oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def assert_same_state(g, o, rtol_w=0.0):
+    assert g.col_names() == o.col_names()
+    for name in g.col_names():
+        a = g.col_download(g.col_find(name))
+        b = o.col_download(o.col_find(name))
+        np.testing.assert_array_equal(a, b, err_msg=f"column {name}")
+    wg, wo = g.weights_download(), o.weights_download()
+    if rtol_w == 0.0:
+        np.testing.assert_array_equal(wg, wo)
+    else:
+        np.testing.assert_allclose(wg, wo, rtol=rtol_w)
+    sg, so = g.get_state(), o.get_state()
+    for k in ("resampled", "weights_changed", "depth", "n_terms", "op_counter", "n_resamples"):
+        assert sg[k] == so[k], k
+    assert sg["last_ess_perc"] == so["last_ess_perc"] or (math.isnan(sg["last_ess_perc"]) and math.isnan(so["last_ess_perc"]))
+
+
+@pytest.mark.parametrize("N", [1024, 3001])
+@pytest.mark.parametrize("ess", [1.0, 0.5])
+@pytest.mark.parametrize("scheme", [abi.RESAMPLE_STRATIFIED, abi.RESAMPLE_SYSTEMATIC])
+def test_ssm2d_statements(gpu_available, N, ess, scheme):
+    obs = models.ssm2d_data(8)
+    g, o = wsmc.Context(N, seed=42), Oracle(N, seed=42)
+    rg = models.ssm2d_statements(g, obs, ess_perc_min=ess, scheme=scheme)
+    ro = models.ssm2d_statements(o, obs, ess_perc_min=ess, scheme=scheme)
+    assert rg == ro
+    np.testing.assert_array_equal(g.last_ancestors(), o.last_ancestors())
+    assert_same_state(g, o)
+    assert g.log_evidence() == o.log_evidence()
+
+
+@pytest.mark.parametrize("N", [1024, 5000])
+@pytest.mark.parametrize("ess", [1.0, 0.5])
+@pytest.mark.parametrize("keep", [True, False])
+def test_ssm2d_fused_matches_statements(gpu_available, N, ess, keep):
+    obs = models.ssm2d_data(12)
+    g = wsmc.Context(N, seed=7)
+    ev = g.ssm2d_run(obs, ess_perc_min=ess, keep_history=keep)
+    o = Oracle(N, seed=7)
+    models.ssm2d_statements(o, obs, ess_perc_min=ess)
+    if keep:
+        assert_same_state(g, o)
+    else:
+        np.testing.assert_array_equal(g.col_download(g.col_find("x")), o.col_download(o.col_find("x_13")))
+        for n in ("v", "dv"):
+            np.testing.assert_array_equal(g.col_download(g.col_find(n)), o.col_download(o.col_find(n)))
+        np.testing.assert_array_equal(g.weights_download(), o.weights_download())
+    assert ev == o.log_evidence()
+    # a second run on the same state continues the RNG stream / weights like run! would
+    ev2 = g.ssm2d_run(obs, ess_perc_min=ess, keep_history=keep)
+    if keep:
+        models.ssm2d_statements(o, obs, ess_perc_min=ess)
+        assert_same_state(g, o)
+        assert ev2 == o.log_evidence()
+
+
+def test_ssm1d_statements(gpu_available):
+    obs = models.ssm1d_data(50)
+    g, o = wsmc.Context(1000, seed=7), Oracle(1000, seed=7)
+    assert models.ssm1d_statements(g, obs) == models.ssm1d_statements(o, obs)
+    assert_same_state(g, o)
+
+
+@pytest.mark.parametrize("ess", [1.0, 0.5])
+def test_linreg_autorw(gpu_available, ess):
+    xs, ys = models.linreg_data()
+    g, o = wsmc.Context(20000, seed=42), Oracle(20000, seed=42)
+    ag = models.linreg_statements(g, xs, ys, ess_perc_min=ess)
+    ao = models.linreg_statements(o, xs, ys, ess_perc_min=ess)
+    assert ag == ao
+    assert_same_state(g, o)
+
+
+def test_oscillator_bounded_autorw(gpu_available):
+    t, y = models.oscillator_data(n=12)
+    g, o = wsmc.Context(4096, seed=42), Oracle(4096, seed=42)
+    ag = models.oscillator_statements(g, t, y, ess_perc_min=1.0, sweeps=2, diversity=None)
+    ao = models.oscillator_statements(o, t, y, ess_perc_min=1.0, sweeps=2, diversity=None)
+    assert ag == ao
+    assert_same_state(g, o)
+
+
+def test_oscillator_diversity_gated(gpu_available):
+    t, y = models.oscillator_data(n=10)
+    g, o = wsmc.Context(3000, seed=3), Oracle(3000, seed=3)
+    ag = models.oscillator_statements(g, t, y, ess_perc_min=0.5, sweeps=1, diversity=0.9)
+    ao = models.oscillator_statements(o, t, y, ess_perc_min=0.5, sweeps=1, diversity=0.9)
+    assert ag == ao
+    assert_same_state(g, o)
+
+
+def test_score_fold_depths(gpu_available):
+    t, y = models.oscillator_data(n=6)
+    g, o = wsmc.Context(2048, seed=9), Oracle(2048, seed=9)
+    models.oscillator_statements(g, t, y, sweeps=0)
+    models.oscillator_statements(o, t, y, sweeps=0)
+    for d in (0, 1, 3, 5, 7, 100):
+        np.testing.assert_array_equal(g.score(d), o.score(d))

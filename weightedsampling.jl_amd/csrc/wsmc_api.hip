@@ -1,0 +1,959 @@
+// wsmc_api.hip — C ABI implementation: context, store, operators, fused runner, RCCL.
+//
+// Reference interfaces replaced (see include/wsmc.h for the per-function mapping):
+//   AbstractParticleStore / ColumnStore   src/stores.jl:1-128
+//   SMCState                              src/types.jl:48-78
+//   apply!(...)                           src/transformers.jl:28-623
+#include <hipcub/hipcub.hpp>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "wsmc_internal.h"
+
+using namespace wsmc;
+
+namespace wsmc {
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+}  // namespace wsmc
+
+#define CHECK_CTX(ctx)                                                   \
+    do {                                                                 \
+        if (!(ctx)) return fail(WSMC_EARG, "null context");              \
+        WSMC_HIP(hipSetDevice((ctx)->device));                           \
+    } while (0)
+
+static constexpr int kMaxWorld = 8;
+
+// ---- helpers -------------------------------------------------------------------------
+static int upload_colptr(wsmc_ctx* c) {
+    if (!c->colptr_dirty) return WSMC_OK;
+    WSMC_HIP(hipStreamSynchronize(c->stream));   // the pinned table may still be in flight
+    double** host = reinterpret_cast<double**>(c->pinned);
+    // pinned staging holds 512 pointers; larger tables go through a synchronous copy
+    if (c->cols.size() <= 256) {
+        for (size_t k = 0; k < c->cols.size(); ++k) host[k] = c->cols[k].front;
+        WSMC_HIP(hipMemcpyAsync(c->d_colptr, host, sizeof(double*) * c->cols.size(), hipMemcpyHostToDevice,
+                                c->stream));
+    } else {
+        std::vector<double*> tab(c->cols.size());
+        for (size_t k = 0; k < c->cols.size(); ++k) tab[k] = c->cols[k].front;
+        WSMC_HIP(hipMemcpyAsync(c->d_colptr, tab.data(), sizeof(double*) * tab.size(), hipMemcpyHostToDevice,
+                                c->stream));
+        WSMC_HIP(hipStreamSynchronize(c->stream));
+    }
+    c->colptr_dirty = false;
+    return WSMC_OK;
+}
+
+static int upload_tape(wsmc_ctx* c) {
+    const int64_t n = (int64_t)c->tape.size();
+    if (c->d_tape_n == n) return WSMC_OK;
+    if (n > c->d_tape_cap) {
+        int64_t cap = c->d_tape_cap ? c->d_tape_cap : 64;
+        while (cap < n) cap *= 2;
+        WSMC_HIP(hipStreamSynchronize(c->stream));
+        if (c->d_tape) WSMC_HIP(hipFree(c->d_tape));
+        WSMC_HIP(hipMalloc(&c->d_tape, sizeof(wsmc_term) * cap));
+        c->d_tape_cap = cap;
+        c->d_tape_n = 0;
+    }
+    WSMC_HIP(hipMemcpyAsync(c->d_tape + c->d_tape_n, c->tape.data() + c->d_tape_n,
+                            sizeof(wsmc_term) * (n - c->d_tape_n), hipMemcpyHostToDevice, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    c->d_tape_n = n;
+    return WSMC_OK;
+}
+
+static bool valid_col(const wsmc_ctx* c, int32_t col) { return col >= 0 && col < (int32_t)c->cols.size(); }
+
+static int check_operand(const wsmc_ctx* c, const wsmc_operand& o) {
+    for (int k = 0; k < 2; ++k) {
+        if (o.col[k] < 0) continue;
+        if (!valid_col(c, o.col[k])) return fail(WSMC_EARG, "operand references an unknown column");
+        if (o.comp[k] < 0 || o.comp[k] >= c->cols[o.col[k]].dim)
+            return fail(WSMC_EARG, "operand component out of range for column " + c->cols[o.col[k]].name);
+    }
+    return WSMC_OK;
+}
+
+static int check_dist(const wsmc_ctx* c, const wsmc_dist& d) {
+    if (d.family < WSMC_FAM_NORMAL || d.family > WSMC_FAM_MVNORMAL_ISO) return fail(WSMC_EARG, "unknown family");
+    if (d.dim < 1 || d.dim > 4) return fail(WSMC_EARG, "dist dim must be 1..4");
+    if (d.family != WSMC_FAM_MVNORMAL_ISO && d.dim != 1) return fail(WSMC_EARG, "scalar family with dim != 1");
+    if (d.mean_fn == WSMC_MEAN_OSCILLATOR && (d.family != WSMC_FAM_NORMAL))
+        return fail(WSMC_EARG, "oscillator mean only for Normal");
+    int r;
+    for (int k = 0; k < 4; ++k)
+        if ((r = check_operand(c, d.mu[k])) != WSMC_OK) return r;
+    return check_operand(c, d.scale);
+}
+
+static wsmc_operand col_operand(int32_t col, int32_t comp) {
+    wsmc_operand r;
+    std::memset(&r, 0, sizeof(r));
+    r.col[0] = col;
+    r.comp[0] = comp;
+    r.coef[0] = 1.0;
+    r.col[1] = -1;
+    return r;
+}
+
+static int gather_all_columns(wsmc_ctx* c) {
+    for (auto& col : c->cols) {
+        for (int k = 0; k < col.dim; ++k) {
+            WSMC_HIP(launch_gather(c->stream, col.back + (int64_t)k * c->N, col.front + (int64_t)k * c->N, c->anc,
+                                   c->N));
+        }
+        std::swap(col.front, col.back);
+    }
+    c->colptr_dirty = true;
+    return WSMC_OK;
+}
+
+static wsmc_shard_stats host_rec_stats(const ShardRec& r) {
+    wsmc_shard_stats st;
+    unsigned long long m = 0, Q = 0, l[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int s = 0; s < kSlots; ++s) {
+        m = std::max(m, r.v[s][0]);
+        Q += r.v[s][1];
+        for (int k = 0; k < 8; ++k) l[k] += r.v[s][2 + k];
+    }
+    st.M = wsmc_ord_dec(m);
+    st.Q = Q;
+    st.Q2 = (wsmc_u128)l[0] + ((wsmc_u128)l[1] << 32) + ((wsmc_u128)l[2] << 64) + ((wsmc_u128)l[3] << 96);
+    st.W = (wsmc_u128)l[4] + ((wsmc_u128)l[5] << 32) + ((wsmc_u128)l[6] << 64) + ((wsmc_u128)l[7] << 96);
+    st.n = r.v[0][10];
+    return st;
+}
+
+// ---- context -------------------------------------------------------------------------
+extern "C" {
+
+const char* wsmc_last_error(void) { return g_err.c_str(); }
+
+int wsmc_version(int32_t* major, int32_t* minor) {
+    if (major) *major = 0;
+    if (minor) *minor = 1;
+    return WSMC_OK;
+}
+
+int wsmc_device_count(int32_t* n) {
+    int k = 0;
+    WSMC_HIP(hipGetDeviceCount(&k));
+    *n = k;
+    return WSMC_OK;
+}
+
+int wsmc_create(wsmc_ctx** out, int64_t n_particles, int32_t device, uint64_t seed) {
+    if (!out) return fail(WSMC_EARG, "null out");
+    if (n_particles < 1 || n_particles >= (int64_t(1) << 31))
+        return fail(WSMC_EARG, "n_particles must be in [1, 2^31)");
+    WSMC_HIP(hipSetDevice(device));
+    wsmc_ctx* c = new wsmc_ctx();
+    c->device = device;
+    c->N = n_particles;
+    c->gN = n_particles;
+    c->seed = seed;
+    c->ntiles = (n_particles + kTile - 1) / kTile;
+    hipError_t e = hipSuccess;
+#define ALLOC(ptr, bytes)                                          \
+    if (e == hipSuccess) e = hipMalloc((void**)&(ptr), (bytes));
+    e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    ALLOC(c->w, sizeof(double) * c->N);
+    ALLOC(c->anc, sizeof(int32_t) * c->N);
+    ALLOC(c->tmp, sizeof(double) * 4 * c->N);
+    ALLOC(c->tileQ, sizeof(unsigned long long) * c->ntiles);
+    ALLOC(c->tilepart, sizeof(double) * 16 * c->ntiles);
+    ALLOC(c->rec, sizeof(ShardRec) * kMaxWorld);
+    ALLOC(c->dec, sizeof(Decision));
+    ALLOC(c->mom, sizeof(double) * 64);
+    ALLOC(c->dflag, sizeof(int32_t) * 4);
+    ALLOC(c->ucount, sizeof(unsigned long long) * 4);
+    ALLOC(c->d_colptr, sizeof(double*) * kMaxCols);
+    ALLOC(c->run_params, sizeof(uint64_t) * 8);
+#undef ALLOC
+    if (e == hipSuccess) e = hipHostMalloc(&c->pinned, 4096, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMemsetAsync(c->w, 0, sizeof(double) * c->N, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->anc, 0, sizeof(int32_t) * c->N, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) {
+        std::string m = std::string("wsmc_create: ") + hipGetErrorString(e);
+        wsmc_destroy(c);
+        return fail(WSMC_EHIP, m);
+    }
+    c->last_ess = std::nan("");
+    *out = c;
+    return WSMC_OK;
+}
+
+int wsmc_destroy(wsmc_ctx* c) {
+    if (!c) return WSMC_OK;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto& g : c->graphs) {
+        if (g.exec) (void)hipGraphExecDestroy(g.exec);
+        if (g.graph) (void)hipGraphDestroy(g.graph);
+        if (g.owned) (void)hipFree(g.owned);
+    }
+    for (auto ev : c->events) (void)hipEventDestroy(ev);
+    for (auto& col : c->cols) {
+        (void)hipFree(col.front);
+        (void)hipFree(col.back);
+    }
+    void* bufs[] = {c->w, c->anc, c->tmp, c->tileQ, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount,
+                    c->d_colptr, c->run_params, c->d_tape, c->run_rec, c->run_dec, c->anc_log, c->obs,
+                    c->vscratch, c->xscratch};
+    for (void* p : bufs)
+        if (p) (void)hipFree(p);
+    if (c->pinned) (void)hipHostFree(c->pinned);
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return WSMC_OK;
+}
+
+int wsmc_sync(wsmc_ctx* c) {
+    CHECK_CTX(c);
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    return WSMC_OK;
+}
+
+int wsmc_nparticles(wsmc_ctx* c, int64_t* n) {
+    if (!c || !n) return fail(WSMC_EARG, "null argument");
+    *n = c->N;
+    return WSMC_OK;
+}
+
+int wsmc_get_state(wsmc_ctx* c, wsmc_state* s) {
+    if (!c || !s) return fail(WSMC_EARG, "null argument");
+    s->resampled = c->resampled;
+    s->weights_changed = c->weights_changed;
+    s->depth = c->depth;
+    s->n_terms = (int32_t)c->tape.size();
+    s->last_ess_perc = c->last_ess;
+    s->op_counter = c->op;
+    s->n_resamples = c->n_resamples;
+    return WSMC_OK;
+}
+
+int wsmc_set_depth(wsmc_ctx* c, int32_t depth) {
+    if (!c) return fail(WSMC_EARG, "null context");
+    c->depth = depth;
+    return WSMC_OK;
+}
+
+int wsmc_set_op_counter(wsmc_ctx* c, uint64_t op) {
+    if (!c) return fail(WSMC_EARG, "null context");
+    c->op = op;
+    return WSMC_OK;
+}
+
+// ---- RCCL ----------------------------------------------------------------------------
+int wsmc_comm_unique_id(uint8_t out_id[128]) {
+    ncclUniqueId id;
+    WSMC_RCCL(ncclGetUniqueId(&id));
+    std::memcpy(out_id, id.internal, 128);
+    return WSMC_OK;
+}
+
+int wsmc_comm_init(wsmc_ctx* c, const uint8_t id[128], int32_t world, int32_t rank, int64_t goff, int64_t gN) {
+    CHECK_CTX(c);
+    if (world < 1 || world > kMaxWorld || rank < 0 || rank >= world) return fail(WSMC_EARG, "bad world/rank");
+    if (goff < 0 || goff + c->N > gN) return fail(WSMC_EARG, "shard outside the global population");
+    c->world = world;
+    c->rank = rank;
+    c->goff = goff;
+    c->gN = gN;
+    if (world > 1) {
+        ncclUniqueId uid;
+        std::memcpy(uid.internal, id, 128);
+        WSMC_RCCL(ncclCommInitRank(&c->comm, world, uid, rank));
+    }
+    return WSMC_OK;
+}
+
+// ---- store ---------------------------------------------------------------------------
+int wsmc_col_create(wsmc_ctx* c, const char* name, int32_t dim, int32_t* col_id) {
+    CHECK_CTX(c);
+    if (!name || !col_id) return fail(WSMC_EARG, "null argument");
+    for (size_t k = 0; k < c->cols.size(); ++k)
+        if (c->cols[k].name == name) {
+            if (c->cols[k].dim != dim) return fail(WSMC_EARG, std::string("column ") + name + " exists with another dim");
+            *col_id = (int32_t)k;
+            return WSMC_OK;
+        }
+    if (dim < 1 || dim > 4) return fail(WSMC_EARG, "column dim must be 1..4");
+    if ((int)c->cols.size() >= kMaxCols) return fail(WSMC_ENOMEM, "too many columns");
+    Column col;
+    col.name = name;
+    col.dim = dim;
+    WSMC_HIP(hipMalloc(&col.front, sizeof(double) * dim * c->N));
+    WSMC_HIP(hipMalloc(&col.back, sizeof(double) * dim * c->N));
+    WSMC_HIP(hipMemsetAsync(col.front, 0, sizeof(double) * dim * c->N, c->stream));
+    c->cols.push_back(col);
+    c->colptr_dirty = true;
+    *col_id = (int32_t)(c->cols.size() - 1);
+    return WSMC_OK;
+}
+
+int wsmc_col_find(wsmc_ctx* c, const char* name, int32_t* col_id) {
+    if (!c || !name || !col_id) return fail(WSMC_EARG, "null argument");
+    *col_id = -1;
+    for (size_t k = 0; k < c->cols.size(); ++k)
+        if (c->cols[k].name == name) *col_id = (int32_t)k;
+    return WSMC_OK;
+}
+
+int wsmc_col_count(wsmc_ctx* c, int32_t* n) {
+    if (!c || !n) return fail(WSMC_EARG, "null argument");
+    *n = (int32_t)c->cols.size();
+    return WSMC_OK;
+}
+
+int wsmc_col_info(wsmc_ctx* c, int32_t col, char* buf, int32_t len, int32_t* dim) {
+    if (!c || !valid_col(c, col)) return fail(WSMC_EARG, "bad column");
+    if (buf && len > 0) {
+        std::strncpy(buf, c->cols[col].name.c_str(), len - 1);
+        buf[len - 1] = 0;
+    }
+    if (dim) *dim = c->cols[col].dim;
+    return WSMC_OK;
+}
+
+int wsmc_col_download(wsmc_ctx* c, int32_t col, double* host) {
+    CHECK_CTX(c);
+    if (!valid_col(c, col) || !host) return fail(WSMC_EARG, "bad column or null buffer");
+    WSMC_HIP(hipMemcpyAsync(host, c->cols[col].front, sizeof(double) * c->cols[col].dim * c->N,
+                            hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    return WSMC_OK;
+}
+
+int wsmc_col_upload(wsmc_ctx* c, int32_t col, const double* host) {
+    CHECK_CTX(c);
+    if (!valid_col(c, col) || !host) return fail(WSMC_EARG, "bad column or null buffer");
+    WSMC_HIP(hipMemcpyAsync(c->cols[col].front, host, sizeof(double) * c->cols[col].dim * c->N,
+                            hipMemcpyHostToDevice, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    return WSMC_OK;
+}
+
+int wsmc_col_device_ptr(wsmc_ctx* c, int32_t col, double** dptr) {
+    if (!c || !valid_col(c, col) || !dptr) return fail(WSMC_EARG, "bad column");
+    *dptr = c->cols[col].front;
+    return WSMC_OK;
+}
+
+int wsmc_store_resample(wsmc_ctx* c, const int32_t* idx) {
+    CHECK_CTX(c);
+    if (!idx) return fail(WSMC_EARG, "null indices");
+    for (int64_t i = 0; i < c->N; ++i)
+        if (idx[i] < 0 || idx[i] >= c->N) return fail(WSMC_EARG, "index out of range");
+    WSMC_HIP(hipMemcpyAsync(c->anc, idx, sizeof(int32_t) * c->N, hipMemcpyHostToDevice, c->stream));
+    int r = gather_all_columns(c);
+    if (r) return r;
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    return WSMC_OK;
+}
+
+// ---- weights -------------------------------------------------------------------------
+int wsmc_weights_upload(wsmc_ctx* c, const double* host) {
+    CHECK_CTX(c);
+    if (!host) return fail(WSMC_EARG, "null buffer");
+    WSMC_HIP(hipMemcpyAsync(c->w, host, sizeof(double) * c->N, hipMemcpyHostToDevice, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    return WSMC_OK;
+}
+
+int wsmc_weights_download(wsmc_ctx* c, double* host) {
+    CHECK_CTX(c);
+    if (!host) return fail(WSMC_EARG, "null buffer");
+    WSMC_HIP(hipMemcpyAsync(host, c->w, sizeof(double) * c->N, hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    return WSMC_OK;
+}
+
+static int exchange_recs(wsmc_ctx* c, ShardRec* recs) {
+    if (c->world > 1) {
+        const size_t cnt = sizeof(ShardRec) / sizeof(unsigned long long);
+        WSMC_RCCL(ncclAllGather(recs + c->rank, recs, cnt, ncclUint64, c->comm, c->stream));
+    }
+    return WSMC_OK;
+}
+
+int wsmc_log_evidence(wsmc_ctx* c, double* out) {
+    CHECK_CTX(c);
+    if (!out) return fail(WSMC_EARG, "null out");
+    WSMC_HIP(hipMemsetAsync(c->rec, 0, sizeof(ShardRec) * c->world, c->stream));
+    WSMC_HIP(launch_log_evidence_stats(c->stream, c->w, c->N, c->rec + c->rank, c->tileQ));
+    int r = exchange_recs(c, c->rec);
+    if (r) return r;
+    std::vector<ShardRec> h(c->world);
+    WSMC_HIP(hipMemcpyAsync(h.data(), c->rec, sizeof(ShardRec) * c->world, hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    wsmc_shard_stats st[kMaxWorld];
+    for (int g = 0; g < c->world; ++g) st[g] = host_rec_stats(h[g]);
+    *out = wsmc_global_log_evidence(st, c->world);
+    return WSMC_OK;
+}
+
+// ---- operators -----------------------------------------------------------------------
+int wsmc_assign(wsmc_ctx* c, int32_t out, const wsmc_operand* expr) {
+    CHECK_CTX(c);
+    if (!valid_col(c, out) || !expr) return fail(WSMC_EARG, "bad output column");
+    const int dim = c->cols[out].dim;
+    for (int k = 0; k < dim; ++k) {
+        int r = check_operand(c, expr[k]);
+        if (r) return r;
+    }
+    int r = upload_colptr(c);
+    if (r) return r;
+    WSMC_HIP(launch_assign(c->stream, c->cols[out].front, dim, expr, c->d_colptr, c->N));
+    c->depth += 1;
+    return WSMC_OK;
+}
+
+static void push_sample_term(wsmc_ctx* c, int32_t out, const wsmc_dist& d) {
+    wsmc_term t;
+    std::memset(&t, 0, sizeof(t));
+    t.dist = d;
+    for (int k = 0; k < 4; ++k) t.x[k] = col_operand(k < d.dim ? out : -1, k);
+    t.kind = WSMC_TERM_SAMPLE;
+    t.depth = c->depth;
+    c->tape.push_back(t);
+}
+
+int wsmc_sample(wsmc_ctx* c, int32_t out, const wsmc_dist* d) {
+    CHECK_CTX(c);
+    if (!valid_col(c, out) || !d) return fail(WSMC_EARG, "bad output column");
+    int r = check_dist(c, *d);
+    if (r) return r;
+    if (d->dim != c->cols[out].dim) return fail(WSMC_EARG, "dist dim != column dim");
+    if ((r = upload_colptr(c))) return r;
+    const uint64_t op = c->op++;
+    WSMC_HIP(launch_sample(c->stream, c->cols[out].front, d->dim, *d, c->seed, op, c->goff, c->d_colptr, c->N));
+    push_sample_term(c, out, *d);
+    c->depth += 1;
+    return WSMC_OK;
+}
+
+int wsmc_sample_importance(wsmc_ctx* c, int32_t out, const wsmc_dist* prop, const wsmc_dist* targ) {
+    CHECK_CTX(c);
+    if (!valid_col(c, out) || !prop || !targ) return fail(WSMC_EARG, "bad arguments");
+    int r = check_dist(c, *prop);
+    if (!r) r = check_dist(c, *targ);
+    if (r) return r;
+    if (prop->dim != c->cols[out].dim || targ->dim != c->cols[out].dim) return fail(WSMC_EARG, "dim mismatch");
+    if ((r = upload_colptr(c))) return r;
+    const uint64_t op = c->op++;
+    WSMC_HIP(launch_sample_importance(c->stream, c->cols[out].front, prop->dim, *prop, *targ, c->w, c->seed, op,
+                                      c->goff, c->d_colptr, c->N));
+    c->weights_changed = 1;
+    push_sample_term(c, out, *targ);
+    c->depth += 1;
+    return WSMC_OK;
+}
+
+static int weigh(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x, int kind) {
+    CHECK_CTX(c);
+    if (!d || !x) return fail(WSMC_EARG, "null argument");
+    int r = check_dist(c, *d);
+    if (r) return r;
+    wsmc_term t;
+    std::memset(&t, 0, sizeof(t));
+    t.dist = *d;
+    for (int k = 0; k < 4; ++k) {
+        t.x[k] = x[k < d->dim ? k : 0];
+        if ((r = check_operand(c, t.x[k]))) return r;
+    }
+    t.kind = kind;
+    t.depth = c->depth;
+    if ((r = upload_colptr(c))) return r;
+    WSMC_HIP(launch_weigh(c->stream, t, c->w, c->d_colptr, c->N));
+    c->tape.push_back(t);
+    c->weights_changed = 1;
+    c->depth += 1;
+    return WSMC_OK;
+}
+
+int wsmc_observe(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x) { return weigh(c, d, x, WSMC_TERM_OBSERVE); }
+int wsmc_weight(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x) { return weigh(c, d, x, WSMC_TERM_WEIGHT); }
+
+int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resampled_out, double* ess_out) {
+    CHECK_CTX(c);
+    if (scheme != WSMC_RESAMPLE_STRATIFIED && scheme != WSMC_RESAMPLE_SYSTEMATIC)
+        return fail(WSMC_EARG, "unknown resampling scheme");
+    const uint64_t op = c->op++;
+    if (!c->weights_changed) {
+        if (resampled_out) *resampled_out = c->resampled;
+        if (ess_out) *ess_out = c->last_ess;
+        return WSMC_OK;
+    }
+    WSMC_HIP(hipMemsetAsync(c->rec, 0, sizeof(ShardRec) * c->world, c->stream));
+    WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, c->rec + c->rank));
+    WSMC_HIP(launch_rs_sums(c->stream, c->w, c->N, c->rec + c->rank, c->tileQ));
+    int r = exchange_recs(c, c->rec);
+    if (r) return r;
+    WSMC_HIP(launch_rs_scan(c->stream, c->w, c->N, c->rec, c->world, c->rank, ess_min, scheme, c->seed, op, nullptr,
+                            c->goff, c->tileQ, c->anc, c->dec));
+    Decision* hd = reinterpret_cast<Decision*>(c->pinned);
+    WSMC_HIP(hipMemcpyAsync(hd, c->dec, sizeof(Decision), hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    const Decision d = *hd;
+    c->last_ess = d.ess;
+    if (d.resampled) {
+        if ((r = gather_all_columns(c))) return r;
+        WSMC_HIP(launch_fill_weights(c->stream, c->w, c->dec, c->N));
+        c->resampled = 1;
+        c->n_resamples += 1;
+    } else {
+        c->resampled = 0;
+    }
+    c->weights_changed = 0;
+    if (resampled_out) *resampled_out = c->resampled;
+    if (ess_out) *ess_out = d.ess;
+    return WSMC_OK;
+}
+
+int wsmc_last_ancestors(wsmc_ctx* c, int32_t* host) {
+    CHECK_CTX(c);
+    if (!host) return fail(WSMC_EARG, "null buffer");
+    WSMC_HIP(hipMemcpyAsync(host, c->anc, sizeof(int32_t) * c->N, hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    return WSMC_OK;
+}
+
+int wsmc_score(wsmc_ctx* c, int32_t depth, double* host) {
+    CHECK_CTX(c);
+    if (!host) return fail(WSMC_EARG, "null buffer");
+    int r = upload_colptr(c);
+    if (!r) r = upload_tape(c);
+    if (r) return r;
+    WSMC_HIP(launch_score(c->stream, c->d_tape, (int32_t)c->tape.size(), depth, c->d_colptr, c->N, c->tmp));
+    WSMC_HIP(hipMemcpyAsync(host, c->tmp, sizeof(double) * c->N, hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    return WSMC_OK;
+}
+
+int wsmc_marginal_diversity(wsmc_ctx* c, const int32_t* targets, int32_t d, double* out) {
+    CHECK_CTX(c);
+    if (!targets || d < 1 || !out) return fail(WSMC_EARG, "bad targets");
+    for (int k = 0; k < d; ++k)
+        if (!valid_col(c, targets[k]) || c->cols[targets[k]].dim != 1)
+            return fail(WSMC_EARG, "diversity targets must be scalar columns");
+    unsigned long long* kin = reinterpret_cast<unsigned long long*>(c->tmp);
+    unsigned long long* kout = kin + c->N;
+    size_t tbytes = 0;
+    WSMC_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tbytes, kin, kout, (int)c->N, 0, 64, c->stream));
+    void* tstore = nullptr;
+    WSMC_HIP(hipMalloc(&tstore, tbytes + 16));
+    double best = INFINITY;
+    for (int k = 0; k < d; ++k) {
+        hipError_t e = launch_diversity_keys(c->stream, c->cols[targets[k]].front, kin, c->N);
+        if (e == hipSuccess)
+            e = hipcub::DeviceRadixSort::SortKeys(tstore, tbytes, kin, kout, (int)c->N, 0, 64, c->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(c->ucount, 0, sizeof(unsigned long long), c->stream);
+        if (e == hipSuccess) e = launch_count_unique(c->stream, kout, c->N, c->ucount);
+        unsigned long long u = 0;
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(&u, c->ucount, sizeof(u), hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) {
+            (void)hipFree(tstore);
+            return fail(WSMC_EHIP, std::string("marginal_diversity: ") + hipGetErrorString(e));
+        }
+        const double frac = wsmc_u64_to_d(u) / wsmc_u64_to_d((uint64_t)c->N);
+        if (frac < best) best = frac;
+    }
+    (void)hipFree(tstore);
+    *out = best;
+    return WSMC_OK;
+}
+
+int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, double step, const double* lo,
+              const double* hi, int32_t target_depth, double diversity, int64_t* accepted_out) {
+    CHECK_CTX(c);
+    const uint64_t op_prop = c->op++, op_acc = c->op++;
+    if (accepted_out) *accepted_out = 0;
+    if (!targets || d < 1 || d > 4) return fail(WSMC_EARG, "move needs 1..4 targets");
+    if (proposal != WSMC_PROPOSAL_RW && proposal != WSMC_PROPOSAL_AUTORW) return fail(WSMC_EARG, "unknown proposal");
+    for (int k = 0; k < d; ++k)
+        if (!valid_col(c, targets[k]) || c->cols[targets[k]].dim != 1)
+            return fail(WSMC_EARG, "move targets must be existing scalar columns");
+    if (c->world > 1) return fail(WSMC_ESTATE, "generic moves on sharded contexts are not supported yet");
+    if (!std::isnan(diversity)) {
+        double div = 0;
+        int r = wsmc_marginal_diversity(c, targets, d, &div);
+        if (r) return r;
+        if (div >= diversity) return WSMC_OK;
+    }
+    if (target_depth < 0) target_depth = c->depth;
+    double l[4], h[4];
+    bool bounded = false;
+    for (int k = 0; k < d; ++k) {
+        l[k] = lo ? lo[k] : -INFINITY;
+        h[k] = hi ? hi[k] : INFINITY;
+        if (std::isfinite(l[k]) || std::isfinite(h[k])) bounded = true;
+    }
+    if (!lo && !hi) bounded = false;
+    int r = upload_colptr(c);
+    if (!r) r = upload_tape(c);
+    if (r) return r;
+    WSMC_HIP(hipMemsetAsync(c->dflag, 0, sizeof(int32_t) * 4, c->stream));
+    WSMC_HIP(hipMemsetAsync(c->ucount, 0, sizeof(unsigned long long) * 4, c->stream));
+    if (proposal == WSMC_PROPOSAL_AUTORW) {
+        WSMC_HIP(hipMemsetAsync(c->rec, 0, sizeof(ShardRec), c->stream));
+        WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, c->rec));
+        const double* lp = bounded ? l : nullptr;
+        const double* hp = bounded ? h : nullptr;
+        WSMC_HIP(launch_moments(c->stream, c->w, c->rec, c->d_colptr, targets, d, lp, hp, 1, c->mom, c->N,
+                                c->tilepart));
+        WSMC_HIP(launch_moments_final(c->stream, c->tilepart, c->ntiles, d, 1, step, c->mom, c->dflag));
+        WSMC_HIP(launch_moments(c->stream, c->w, c->rec, c->d_colptr, targets, d, lp, hp, 2, c->mom, c->N,
+                                c->tilepart));
+        WSMC_HIP(launch_moments_final(c->stream, c->tilepart, c->ntiles, d, 2, step, c->mom, c->dflag));
+    } else {
+        WSMC_HIP(hipStreamSynchronize(c->stream));
+        double* L = reinterpret_cast<double*>(c->pinned);
+        for (int k = 0; k < 16; ++k) L[k] = 0.0;
+        for (int k = 0; k < d; ++k) L[k * d + k] = step;
+        WSMC_HIP(hipMemcpyAsync(c->mom + 32, L, sizeof(double) * 16, hipMemcpyHostToDevice, c->stream));
+    }
+    WSMC_HIP(launch_move(c->stream, c->d_tape, (int32_t)c->tape.size(), target_depth, c->d_colptr, targets, d,
+                         bounded ? l : nullptr, bounded ? h : nullptr, bounded ? 1 : 0, c->mom + 32, c->seed,
+                         op_prop, op_acc, c->goff, c->N, c->ucount));
+    struct {
+        int32_t flag[4];
+        unsigned long long acc[4];
+    }* hb = reinterpret_cast<decltype(hb)>(c->pinned);
+    WSMC_HIP(hipMemcpyAsync(hb->flag, c->dflag, sizeof(int32_t) * 4, hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipMemcpyAsync(hb->acc, c->ucount, sizeof(unsigned long long) * 4, hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    if (hb->flag[0]) return fail(WSMC_ENOTPD, "autoRW proposal covariance is not positive definite");
+    if (accepted_out) *accepted_out = (int64_t)hb->acc[0];
+    return WSMC_OK;
+}
+
+// ---- fused 2D SSM runner --------------------------------------------------------------
+static int ensure_run_buffers(wsmc_ctx* c, int32_t T) {
+    if (c->T_alloc >= T && c->run_rec) return WSMC_OK;
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    void* old[] = {c->run_rec, c->run_dec, c->anc_log, c->obs};
+    for (void* p : old)
+        if (p) WSMC_HIP(hipFree(p));
+    WSMC_HIP(hipMalloc(&c->run_rec, sizeof(ShardRec) * (T + 1) * kMaxWorld));
+    WSMC_HIP(hipMalloc(&c->run_dec, sizeof(Decision) * (T + 1)));
+    WSMC_HIP(hipMalloc(&c->anc_log, sizeof(int32_t) * (size_t)T * c->N));
+    WSMC_HIP(hipMalloc(&c->obs, sizeof(double) * 2 * (T + 1)));
+    if (!c->vscratch) WSMC_HIP(hipMalloc(&c->vscratch, sizeof(double) * 2 * c->N));
+    if (!c->xscratch) WSMC_HIP(hipMalloc(&c->xscratch, sizeof(double) * 2 * c->N));
+    c->T_alloc = T;
+    for (auto& g : c->graphs) {  // graphs bake old pointers
+        if (g.exec) (void)hipGraphExecDestroy(g.exec);
+        if (g.graph) (void)hipGraphDestroy(g.graph);
+        if (g.owned) (void)hipFree(g.owned);
+    }
+    c->graphs.clear();
+    return WSMC_OK;
+}
+
+struct RunPlan {
+    int32_t T = 0, keep = 0, scheme = 0;
+    double ess_min = 0, q_var = 0, r_var = 0;
+    double x0[2] = {0, 0}, v0[2] = {0, 0};
+    int32_t colx = -1, colv = -1, coldv = -1;
+    std::vector<int32_t> xcols;  // x_1 .. x_{T+1}
+    double** d_hist_work = nullptr;
+    double** d_hist_out = nullptr;
+};
+
+static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEvent_t>* ev) {
+    const int T = p.T;
+    const int64_t N = c->N;
+    const double r_var = p.r_var;
+    const double cpre = 2.0 * WSMC_LOG2PI + 2.0 * wsmc_log(r_var);
+    int evk = 0;
+    auto mark = [&]() -> hipError_t {
+        if (!ev) return hipSuccess;
+        return hipEventRecord((*ev)[evk++], c->stream);
+    };
+    WSMC_HIP(hipMemsetAsync(c->run_rec, 0, sizeof(ShardRec) * (T + 1) * c->world, c->stream));
+    WSMC_HIP(hipMemsetAsync(c->run_dec, 0, sizeof(Decision) * (T + 1), c->stream));
+    double* vbuf[2] = {c->cols[p.colv].back, c->vscratch};
+    double* xbuf[2] = {p.keep ? nullptr : c->cols[p.colx].back, c->xscratch};
+    for (int t = 1; t <= T; ++t) {
+        Ssm2dArgs a;
+        a.t = t;
+        a.keep_history = p.keep;
+        a.N = N;
+        a.goff = c->goff;
+        a.seed = c->seed;
+        a.op_dev = c->run_params;
+        a.obs = c->obs;
+        a.x0[0] = p.x0[0]; a.x0[1] = p.x0[1];
+        a.v0[0] = p.v0[0]; a.v0[1] = p.v0[1];
+        a.q_sd = wsmc_sqrt(p.q_var);
+        a.r_var = r_var;
+        a.c0 = cpre;
+        if (p.keep) {
+            a.x_prev = t > 1 ? c->cols[p.xcols[t]].back : nullptr;   // x_t (written at step t-1)
+            a.x_next = c->cols[p.xcols[t + 1]].back;                  // x_{t+1}
+        } else {
+            a.x_prev = t > 1 ? xbuf[t & 1] : nullptr;
+            a.x_next = xbuf[(t + 1) & 1];
+        }
+        a.v_prev = t > 1 ? vbuf[t & 1] : nullptr;
+        a.v_next = vbuf[(t + 1) & 1];
+        a.dv = c->cols[p.coldv].back;
+        a.w = c->w;
+        a.anc_prev = t > 1 ? c->anc_log + (size_t)(t - 2) * N : nullptr;
+        a.dec_prev = t > 1 ? c->run_dec + (t - 1) : nullptr;
+        ShardRec* recs = c->run_rec + (size_t)t * c->world;
+        a.rec = recs + c->rank;
+        WSMC_HIP(mark());
+        WSMC_HIP(launch_ssm2d_propagate(c->stream, a));
+        WSMC_HIP(mark());
+        WSMC_HIP(launch_rs_sums(c->stream, c->w, N, recs + c->rank, c->tileQ));
+        WSMC_HIP(mark());
+        int r = exchange_recs(c, recs);
+        if (r) return r;
+        WSMC_HIP(launch_rs_scan(c->stream, c->w, N, recs, c->world, c->rank, p.ess_min, p.scheme, c->seed,
+                                3ull * (uint64_t)(t - 1) + 2ull, c->run_params, c->goff, c->tileQ,
+                                c->anc_log + (size_t)(t - 1) * N, c->run_dec + t));
+        WSMC_HIP(mark());
+    }
+    Ssm2dFinal f;
+    f.T = T;
+    f.keep_history = p.keep;
+    f.N = N;
+    f.x0[0] = p.x0[0]; f.x0[1] = p.x0[1];
+    f.hist_work = p.d_hist_work;
+    f.hist_out = p.d_hist_out;
+    f.x_work = p.keep ? nullptr : xbuf[(T + 1) & 1];
+    f.x_out = p.keep ? nullptr : c->cols[p.colx].front;
+    f.v_work = vbuf[(T + 1) & 1];
+    f.v_out = c->cols[p.colv].front;
+    f.dv_work = c->cols[p.coldv].back;
+    f.dv_out = c->cols[p.coldv].front;
+    f.w = c->w;
+    f.anc_log = c->anc_log;
+    f.dec = c->run_dec;
+    WSMC_HIP(mark());
+    WSMC_HIP(launch_ssm2d_finalize(c->stream, f));
+    WSMC_HIP(mark());
+    return WSMC_OK;
+}
+
+int wsmc_run_set_timing(wsmc_ctx* c, int32_t enabled) {
+    if (!c) return fail(WSMC_EARG, "null context");
+    c->timing = enabled != 0;
+    return WSMC_OK;
+}
+
+int wsmc_run_get_timing(wsmc_ctx* c, wsmc_run_timing* out) {
+    if (!c || !out) return fail(WSMC_EARG, "null argument");
+    *out = c->last_timing;
+    return WSMC_OK;
+}
+
+int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, const double* v0, double q_var,
+                   double r_var, double ess_min, int32_t scheme, int32_t keep_history, double* log_evidence_out) {
+    CHECK_CTX(c);
+    if (!obs || T < 1 || !x0 || !v0) return fail(WSMC_EARG, "bad arguments");
+    if (scheme != WSMC_RESAMPLE_STRATIFIED && scheme != WSMC_RESAMPLE_SYSTEMATIC)
+        return fail(WSMC_EARG, "unknown resampling scheme");
+    if (!(q_var > 0) || !(r_var > 0)) return fail(WSMC_EARG, "variances must be positive");
+    RunPlan p;
+    p.T = T;
+    p.keep = keep_history ? 1 : 0;
+    p.scheme = scheme;
+    p.ess_min = ess_min;
+    p.q_var = q_var;
+    p.r_var = r_var;
+    p.x0[0] = x0[0]; p.x0[1] = x0[1];
+    p.v0[0] = v0[0]; p.v0[1] = v0[1];
+    int r;
+    // columns, in the order @model's statements create them (examples/2D_ssm.jl:8-16)
+    if (p.keep) {
+        p.xcols.assign(T + 2, -1);
+        int32_t id;
+        if ((r = wsmc_col_create(c, "x_1", 2, &id))) return r;
+        p.xcols[1] = id;
+        if ((r = wsmc_col_create(c, "v", 2, &p.colv))) return r;
+        for (int t = 1; t <= T; ++t) {
+            const std::string nm = "x_" + std::to_string(t + 1);
+            if ((r = wsmc_col_create(c, nm.c_str(), 2, &id))) return r;
+            p.xcols[t + 1] = id;
+            if (t == 1 && (r = wsmc_col_create(c, "dv", 2, &p.coldv))) return r;
+        }
+    } else {
+        if ((r = wsmc_col_create(c, "x", 2, &p.colx))) return r;
+        if ((r = wsmc_col_create(c, "v", 2, &p.colv))) return r;
+        if ((r = wsmc_col_create(c, "dv", 2, &p.coldv))) return r;
+    }
+    if ((r = ensure_run_buffers(c, T))) return r;
+    // per-run values: obs, op base
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    const uint64_t op_base = c->op;
+    std::vector<double> hobs(obs, obs + 2 * (size_t)T);
+    WSMC_HIP(hipMemcpyAsync(c->obs, hobs.data(), sizeof(double) * 2 * T, hipMemcpyHostToDevice, c->stream));
+    uint64_t* hp = reinterpret_cast<uint64_t*>(c->pinned);
+    hp[0] = op_base;
+    WSMC_HIP(hipMemcpyAsync(c->run_params, hp, sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+
+    char keybuf[512];
+    std::snprintf(keybuf, sizeof(keybuf), "ssm2d T=%d keep=%d sch=%d ess=%.17g q=%.17g r=%.17g x0=%.17g,%.17g v0=%.17g,%.17g w=%d tm=%d",
+                  T, p.keep, scheme, ess_min, q_var, r_var, x0[0], x0[1], v0[0], v0[1], c->world, (int)c->timing);
+    // the graph bakes column buffers: key on their addresses too
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](const void* q) { h = (h ^ (uint64_t)(uintptr_t)q) * 1099511628211ull; };
+    for (auto& col : c->cols) { mix(col.front); mix(col.back); }
+    mix(c->w); mix(c->anc_log); mix(c->run_rec); mix(c->obs);
+    const std::string key = std::string(keybuf) + " ptr=" + std::to_string(h);
+    auto build_tables = [&](double*** work, double*** outp) -> int {
+        *work = *outp = nullptr;
+        if (!p.keep) return WSMC_OK;
+        std::vector<double*> hw(T + 2, nullptr), ho(T + 2, nullptr);
+        for (int t = 1; t <= T + 1; ++t) {
+            hw[t] = c->cols[p.xcols[t]].back;
+            ho[t] = c->cols[p.xcols[t]].front;
+        }
+        double** tabs = nullptr;
+        WSMC_HIP(hipMalloc(&tabs, sizeof(double*) * 2 * (T + 2)));
+        WSMC_HIP(hipMemcpyAsync(tabs, hw.data(), sizeof(double*) * (T + 2), hipMemcpyHostToDevice, c->stream));
+        WSMC_HIP(hipMemcpyAsync(tabs + (T + 2), ho.data(), sizeof(double*) * (T + 2), hipMemcpyHostToDevice,
+                                c->stream));
+        WSMC_HIP(hipStreamSynchronize(c->stream));
+        *work = tabs;
+        *outp = tabs + (T + 2);
+        return WSMC_OK;
+    };
+    const bool use_graph = c->world == 1;
+    const int nev = 4 * T + 2;
+    std::vector<hipEvent_t> evs;
+    if (c->timing) {
+        while ((int)c->events.size() < nev) {
+            hipEvent_t e;
+            WSMC_HIP(hipEventCreate(&e));
+            c->events.push_back(e);
+        }
+        evs.assign(c->events.begin(), c->events.begin() + nev);
+    }
+    void* temp_tables = nullptr;
+    if (use_graph) {
+        RunGraph* g = nullptr;
+        for (auto& gg : c->graphs)
+            if (gg.key == key) g = &gg;
+        if (!g) {
+            RunGraph ng;
+            ng.key = key;
+            if ((r = build_tables(&p.d_hist_work, &p.d_hist_out))) return r;
+            ng.owned = p.d_hist_work;
+            WSMC_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+            r = enqueue_ssm2d(c, p, c->timing ? &evs : nullptr);
+            hipGraph_t graph = nullptr;
+            hipError_t ee = hipStreamEndCapture(c->stream, &graph);
+            if (r) {
+                if (graph) (void)hipGraphDestroy(graph);
+                if (ng.owned) (void)hipFree(ng.owned);
+                return r;
+            }
+            WSMC_HIP(ee);
+            ng.graph = graph;
+            WSMC_HIP(hipGraphInstantiate(&ng.exec, graph, nullptr, nullptr, 0));
+            c->graphs.push_back(ng);
+            g = &c->graphs.back();
+        }
+        WSMC_HIP(hipGraphLaunch(g->exec, c->stream));
+    } else {
+        if ((r = build_tables(&p.d_hist_work, &p.d_hist_out))) return r;
+        temp_tables = p.d_hist_work;
+        r = enqueue_ssm2d(c, p, c->timing ? &evs : nullptr);
+        if (r) {
+            if (temp_tables) (void)hipFree(temp_tables);
+            return r;
+        }
+    }
+    std::vector<Decision> hdec(T + 1);
+    WSMC_HIP(hipMemcpyAsync(hdec.data(), c->run_dec, sizeof(Decision) * (T + 1), hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    if (temp_tables) (void)hipFree(temp_tables);
+
+    // bookkeeping identical to issuing the statements one by one
+    int32_t nres = 0;
+    c->depth += 2;  // x{1} .= x0, v .= v0
+    for (int t = 1; t <= T; ++t) {
+        wsmc_dist dv;
+        std::memset(&dv, 0, sizeof(dv));
+        dv.family = WSMC_FAM_MVNORMAL_ISO;
+        dv.mean_fn = WSMC_MEAN_AFFINE;
+        dv.dim = 2;
+        for (int k = 0; k < 4; ++k) {
+            dv.mu[k].col[0] = dv.mu[k].col[1] = -1;
+        }
+        dv.scale.c0 = q_var;
+        dv.scale.col[0] = dv.scale.col[1] = -1;
+        c->depth += 1;  // x{t+1} .= x{t} + v
+        push_sample_term(c, p.coldv, dv);
+        c->depth += 1;  // dv ~ ...
+        c->depth += 1;  // v .= v + dv
+        wsmc_term ob;
+        std::memset(&ob, 0, sizeof(ob));
+        ob.dist.family = WSMC_FAM_MVNORMAL_ISO;
+        ob.dist.mean_fn = WSMC_MEAN_AFFINE;
+        ob.dist.dim = 2;
+        const int32_t xc = p.keep ? p.xcols[t + 1] : p.colx;
+        for (int k = 0; k < 4; ++k) ob.dist.mu[k] = col_operand(k < 2 ? xc : -1, k);
+        ob.dist.scale.c0 = r_var;
+        ob.dist.scale.col[0] = ob.dist.scale.col[1] = -1;
+        for (int k = 0; k < 4; ++k) {
+            std::memset(&ob.x[k], 0, sizeof(wsmc_operand));
+            ob.x[k].c0 = k < 2 ? obs[2 * (t - 1) + k] : 0.0;
+            ob.x[k].col[0] = ob.x[k].col[1] = -1;
+        }
+        ob.kind = WSMC_TERM_OBSERVE;
+        ob.depth = c->depth;
+        c->tape.push_back(ob);
+        c->depth += 1;  // o => ...
+        if (hdec[t].resampled) ++nres;
+    }
+    c->op = op_base + 3ull * (uint64_t)T;
+    c->resampled = hdec[T].resampled;
+    c->weights_changed = 0;
+    c->last_ess = hdec[T].ess;
+    c->n_resamples += nres;
+    c->colptr_dirty = true;
+    if (c->timing) {
+        wsmc_run_timing tm{};
+        float ms = 0.f;
+        int k = 0;
+        for (int t = 1; t <= T; ++t) {
+            WSMC_HIP(hipEventElapsedTime(&ms, evs[k], evs[k + 1]));
+            tm.propagate_ms += ms;
+            WSMC_HIP(hipEventElapsedTime(&ms, evs[k + 1], evs[k + 2]));
+            tm.reduce_ms += ms;
+            WSMC_HIP(hipEventElapsedTime(&ms, evs[k + 2], evs[k + 3]));
+            tm.resample_ms += ms;
+            k += 4;
+        }
+        WSMC_HIP(hipEventElapsedTime(&ms, evs[k], evs[k + 1]));
+        tm.finalize_ms = ms;
+        WSMC_HIP(hipEventElapsedTime(&ms, evs[0], evs[k + 1]));
+        tm.total_ms = ms;
+        tm.steps = T;
+        tm.n_resamples = nres;
+        c->last_timing = tm;
+    }
+    if (log_evidence_out) return wsmc_log_evidence(c, log_evidence_out);
+    return WSMC_OK;
+}
+
+}  // extern "C"

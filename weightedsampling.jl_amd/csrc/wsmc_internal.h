@@ -1,0 +1,213 @@
+// wsmc_internal.h — runtime structures of libwsmc (not part of the ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "wsmc.h"
+#include "wsmc_math.h"
+#include "wsmc_terms.h"
+
+namespace wsmc {
+
+constexpr int kBlock = 256;            // threads per workgroup (4 waves of 64)
+constexpr int kItems = 8;              // particles per thread in the tile kernels
+constexpr int kTile = kBlock * kItems; // 2048 particles per tile (canonical reduction tile)
+constexpr int kSlots = 8;              // per-XCD accumulator copies (blockIdx % 8)
+constexpr int kChunk = 4096;           // ancestor slots filled per LDS pass
+constexpr int kMaxCols = 4096;
+constexpr int kMaxShards = 8;     // one node: up to 8 GPUs
+
+// One shard's weight-statistics record. kSlots copies of each accumulator so the
+// per-block atomics spread over 8 addresses (one per XCD round-robin group).
+// v[s][0] = ordered max, v[s][1] = sum q, v[s][2..5] = sum q^2 limbs (32 bit),
+// v[s][6..9] = sum fix96 limbs, v[s][10] = shard size (slot 0 only).
+struct ShardRec {
+    unsigned long long v[kSlots][16];
+};
+
+// Resample outcome for one invocation (one step of a fused run).
+struct Decision {
+    int32_t resampled;
+    int32_t pad;
+    double mean;        // this shard's post-resample log-weight
+    double ess;         // global ESS/N
+    double M;           // this shard's max log-weight
+};
+
+struct Column {
+    std::string name;
+    int32_t dim = 1;
+    double* front = nullptr;   // live data (what getcol returns)
+    double* back = nullptr;    // ping-pong / scratch buffer
+};
+
+// cached HIP graph of one fused-run configuration
+struct RunGraph {
+    std::string key;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    void* owned = nullptr;     // device tables baked into the graph
+};
+
+}  // namespace wsmc
+
+struct wsmc_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int64_t N = 0;
+    uint64_t seed = 0;
+
+    // shard / RCCL
+    int world = 1, rank = 0;
+    int64_t goff = 0, gN = 0;
+    ncclComm_t comm = nullptr;
+
+    // store
+    std::vector<wsmc::Column> cols;
+    double** d_colptr = nullptr;     // device table of front pointers
+    bool colptr_dirty = true;
+
+    // SMCState
+    double* w = nullptr;
+    int32_t resampled = 0, weights_changed = 0, depth = 0;
+    double last_ess = 0.0;
+    uint64_t op = 0;
+    int64_t n_resamples = 0;
+
+    // score tape
+    std::vector<wsmc_term> tape;
+    wsmc_term* d_tape = nullptr;
+    int64_t d_tape_cap = 0, d_tape_n = 0;
+
+    // scratch
+    int32_t* anc = nullptr;                 // last ancestors [N]
+    double* tmp = nullptr;                  // [4N]
+    unsigned long long* tileQ = nullptr;    // [ntiles] per-tile sum q (scan offsets)
+    double* tilepart = nullptr;             // [16 * ntiles] canonical-sum tile partials
+    wsmc::ShardRec* rec = nullptr;          // [world] records of one generic resample
+    wsmc::Decision* dec = nullptr;          // [1] decision of one generic resample
+    double* mom = nullptr;                  // [64] moment / covariance / Cholesky results
+    int32_t* dflag = nullptr;               // [4] device error flags
+    unsigned long long* ucount = nullptr;   // [4] device counters
+    void* pinned = nullptr;                 // 4 KB pinned staging
+    int64_t ntiles = 0;
+
+    // fused runner state
+    int32_t T_alloc = 0;
+    wsmc::ShardRec* run_rec = nullptr;      // [(T+1) * world]
+    wsmc::Decision* run_dec = nullptr;      // [T+1]
+    int32_t* anc_log = nullptr;             // [T][N]
+    double* obs = nullptr;                  // [T*2]
+    double* vscratch = nullptr;             // [2N] second ping-pong buffer for v / x
+    double* xscratch = nullptr;             // [2N]
+    uint64_t* run_params = nullptr;         // [8] device copy of per-run values (op base)
+    std::vector<wsmc::RunGraph> graphs;
+    bool timing = false;
+    std::vector<hipEvent_t> events;
+    wsmc_run_timing last_timing{};
+};
+
+namespace wsmc {
+
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+
+#define WSMC_HIP(expr)                                                                   \
+    do {                                                                                 \
+        hipError_t _e = (expr);                                                          \
+        if (_e != hipSuccess)                                                            \
+            return ::wsmc::fail(WSMC_EHIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+#define WSMC_RCCL(expr)                                                                  \
+    do {                                                                                 \
+        ncclResult_t _r = (expr);                                                        \
+        if (_r != ncclSuccess)                                                           \
+            return ::wsmc::fail(WSMC_ERCCL, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
+    } while (0)
+
+// ---- kernel launchers (wsmc_kernels.hip) -------------------------------------------
+hipError_t launch_assign(hipStream_t s, double* out, int dim, const wsmc_operand* expr,
+                         double* const* cols, int64_t N);
+hipError_t launch_sample(hipStream_t s, double* out, int dim, const wsmc_dist& d, uint64_t seed,
+                         uint64_t op, int64_t goff, double* const* cols, int64_t N);
+hipError_t launch_sample_importance(hipStream_t s, double* out, int dim, const wsmc_dist& prop,
+                                    const wsmc_dist& targ, double* w, uint64_t seed, uint64_t op,
+                                    int64_t goff, double* const* cols, int64_t N);
+hipError_t launch_weigh(hipStream_t s, const wsmc_term& t, double* w, double* const* cols, int64_t N);
+hipError_t launch_rs_max(hipStream_t s, const double* w, int64_t N, ShardRec* rec);
+hipError_t launch_rs_sums(hipStream_t s, const double* w, int64_t N, ShardRec* rec,
+                          unsigned long long* tileQ);
+hipError_t launch_rs_scan(hipStream_t s, const double* w, int64_t N, const ShardRec* recs, int world,
+                          int rank, double ess_min, int scheme, uint64_t seed, uint64_t op,
+                          const uint64_t* op_dev, int64_t slot_base, const unsigned long long* tileQ,
+                          int32_t* anc, Decision* dec);
+hipError_t launch_gather(hipStream_t s, double* dst, const double* src, const int32_t* anc, int64_t N);
+hipError_t launch_fill_weights(hipStream_t s, double* w, const Decision* dec, int64_t N);
+hipError_t launch_log_evidence_stats(hipStream_t s, const double* w, int64_t N, ShardRec* rec,
+                                     unsigned long long* tileQ);
+hipError_t launch_score(hipStream_t s, const wsmc_term* tape, int32_t n, int32_t depth,
+                        double* const* cols, int64_t N, double* out);
+hipError_t launch_moments(hipStream_t s, const double* w, const ShardRec* rec, double* const* cols,
+                          const int32_t* tcols, int d, const double* lo, const double* hi,
+                          int pass, const double* mom, int64_t N, double* tilepart);
+hipError_t launch_moments_final(hipStream_t s, const double* tilepart, int64_t ntiles, int d,
+                                int pass, double min_step, double* mom, int32_t* flag);
+hipError_t launch_move(hipStream_t s, const wsmc_term* tape, int32_t nterms, int32_t depth,
+                       double* const* cols, const int32_t* tcols, int d, const double* lo,
+                       const double* hi, int bounded, const double* L, uint64_t seed,
+                       uint64_t op_prop, uint64_t op_acc, int64_t goff, int64_t N,
+                       unsigned long long* accepted);
+hipError_t launch_diversity_keys(hipStream_t s, const double* x, unsigned long long* keys, int64_t N);
+hipError_t launch_count_unique(hipStream_t s, const unsigned long long* keys, int64_t N,
+                               unsigned long long* count);
+
+// fused 2D SSM
+struct Ssm2dArgs {
+    int32_t t;                 // 1-based step
+    int32_t keep_history;
+    int64_t N;
+    int64_t goff;
+    uint64_t seed;
+    const uint64_t* op_dev;    // op base of the run (device)
+    const double* obs;         // [T][2]
+    double x0[2], v0[2];
+    double q_sd;               // sqrt(q_var)
+    double r_var;
+    double c0;                 // -(2 log 2pi + 2 log r_var)/2 (host-computed, shared math)
+    const double* x_prev;      // [2][N] x_t (pre-resample numbering of step t-1), unused at t = 1
+    double* x_next;            // [2][N]
+    const double* v_prev;      // [2][N]
+    double* v_next;            // [2][N]
+    double* dv;                // [2][N]
+    double* w;                 // [N]
+    const int32_t* anc_prev;   // [N] ancestors of step t-1
+    const Decision* dec_prev;  // decision of step t-1 (nullptr at t = 1)
+    ShardRec* rec;             // this step's record (this rank)
+};
+hipError_t launch_ssm2d_propagate(hipStream_t s, const Ssm2dArgs& a);
+struct Ssm2dFinal {
+    int32_t T;
+    int32_t keep_history;
+    int64_t N;
+    double x0[2];
+    double* const* hist_work;  // device table [T+2]: working buffers x_t (pre-resample), t=2..T+1
+    double* const* hist_out;   // device table [T+2]: final (front) buffers of x_t, t=1..T+1
+    const double* x_work;      // no-history: x_{T+1} working buffer
+    double* x_out;
+    const double* v_work;
+    double* v_out;
+    const double* dv_work;
+    double* dv_out;
+    double* w;
+    const int32_t* anc_log;    // [T][N]
+    const Decision* dec;       // [T+1], index t
+};
+hipError_t launch_ssm2d_finalize(hipStream_t s, const Ssm2dFinal& f);
+
+}  // namespace wsmc

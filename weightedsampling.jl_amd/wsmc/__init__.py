@@ -1,0 +1,18 @@
+"""wsmc — MI355X-native SMC inner loop for WeightedSampling.jl.
+
+The hot path (per-particle log-density accumulation, exp_norm + ESS, stratified /
+systematic resampling with ancestor indices, autoRW Metropolis–Hastings moves) runs as
+hand-written gfx950 HIP kernels in ``libwsmc.so`` behind the C ABI of include/wsmc.h.
+This package is the host-side mirror of the reference's operator interface; it has no
+CPU compute path.
+"""
+from . import abi
+from .abi import (PROPOSAL_AUTORW, PROPOSAL_RW, RESAMPLE_STRATIFIED, RESAMPLE_SYSTEMATIC, WSMCError,
+                  load_library)
+from .context import Context, device_count
+from .dsl import Col, Expr, HalfNormal, Kernel, MvNormal, Normal, Oscillator, Uniform
+from . import models
+
+__all__ = ["abi", "Context", "device_count", "Col", "Expr", "Kernel", "Normal", "MvNormal", "HalfNormal",
+           "Uniform", "Oscillator", "models", "load_library", "WSMCError", "RESAMPLE_STRATIFIED",
+           "RESAMPLE_SYSTEMATIC", "PROPOSAL_RW", "PROPOSAL_AUTORW"]

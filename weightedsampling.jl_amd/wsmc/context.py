@@ -1,0 +1,230 @@
+"""Low-level context: one particle shard on one GPU, driven through the C ABI.
+
+Each method is a thin, typed wrapper of one include/wsmc.h entry point. The same method
+set ("the context protocol") is what the high-level operators in ``transformers.py``
+call, so they are agnostic of how a context is implemented; tests drive the CPU oracle
+through the identical protocol to compare results bit for bit.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import numpy as np
+
+from . import abi
+from .abi import Dist, Operand, RunTiming, State, check, load_library
+
+_D = C.POINTER(C.c_double)
+_I32P = C.POINTER(C.c_int32)
+
+
+def _dptr(a: np.ndarray):
+    return a.ctypes.data_as(_D)
+
+
+def _operands4(exprs) -> C.Array:
+    ops = list(exprs) if isinstance(exprs, (list, tuple)) else [exprs]
+    arr = (Operand * 4)()
+    for k in range(4):
+        arr[k] = ops[k] if k < len(ops) else ops[0]
+    return arr
+
+
+class Context:
+    """A shard of ``n_particles`` particles on HIP device ``device`` (SMCState's storage)."""
+
+    is_oracle = False
+
+    def __init__(self, n_particles: int, seed: int = 42, device: int = 0):
+        self._L = load_library()
+        h = C.c_void_p()
+        check(self._L.wsmc_create(C.byref(h), int(n_particles), int(device), int(seed) & (2**64 - 1)))
+        self._h = h
+        self.n = int(n_particles)
+        self.seed = int(seed)
+        self.device = int(device)
+        self.world = 1
+        self.rank = 0
+
+    # ---- lifetime ----
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.wsmc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def sync(self) -> None:
+        check(self._L.wsmc_sync(self._h))
+
+    # ---- multi-GPU ----
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = (C.c_uint8 * 128)()
+        check(load_library().wsmc_comm_unique_id(buf))
+        return bytes(buf)
+
+    def comm_init(self, uid: bytes, world: int, rank: int, global_offset: int, global_n: int) -> None:
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        check(self._L.wsmc_comm_init(self._h, buf, int(world), int(rank), int(global_offset), int(global_n)))
+        self.world, self.rank = int(world), int(rank)
+
+    # ---- store (AbstractParticleStore) ----
+    def col_find(self, name: str) -> int:
+        c = C.c_int32()
+        check(self._L.wsmc_col_find(self._h, name.encode(), C.byref(c)))
+        return int(c.value)
+
+    def col_create(self, name: str, dim: int = 1) -> int:
+        c = C.c_int32()
+        check(self._L.wsmc_col_create(self._h, name.encode(), int(dim), C.byref(c)))
+        return int(c.value)
+
+    def col_dim(self, col: int) -> int:
+        d = C.c_int32()
+        check(self._L.wsmc_col_info(self._h, int(col), None, 0, C.byref(d)))
+        return int(d.value)
+
+    def col_names(self) -> list[str]:
+        n = C.c_int32()
+        check(self._L.wsmc_col_count(self._h, C.byref(n)))
+        out = []
+        buf = C.create_string_buffer(256)
+        for k in range(n.value):
+            check(self._L.wsmc_col_info(self._h, k, buf, 256, None))
+            out.append(buf.value.decode())
+        return out
+
+    def col_download(self, col: int) -> np.ndarray:
+        d = self.col_dim(col)
+        a = np.empty(d * self.n)
+        check(self._L.wsmc_col_download(self._h, int(col), _dptr(a)))
+        return a.reshape(d, self.n) if d > 1 else a
+
+    def col_upload(self, col: int, values) -> None:
+        d = self.col_dim(col)
+        v = np.ascontiguousarray(np.asarray(values, dtype=np.float64).reshape(d * self.n))
+        check(self._L.wsmc_col_upload(self._h, int(col), _dptr(v)))
+
+    def store_resample(self, indices) -> None:
+        idx = np.ascontiguousarray(np.asarray(indices, dtype=np.int32))
+        check(self._L.wsmc_store_resample(self._h, idx.ctypes.data_as(_I32P)))
+
+    # ---- weights / state ----
+    def weights_download(self) -> np.ndarray:
+        a = np.empty(self.n)
+        check(self._L.wsmc_weights_download(self._h, _dptr(a)))
+        return a
+
+    def weights_upload(self, w) -> None:
+        a = np.ascontiguousarray(np.asarray(w, dtype=np.float64).reshape(self.n))
+        check(self._L.wsmc_weights_upload(self._h, _dptr(a)))
+
+    def log_evidence(self) -> float:
+        v = C.c_double()
+        check(self._L.wsmc_log_evidence(self._h, C.byref(v)))
+        return float(v.value)
+
+    def get_state(self) -> dict:
+        s = State()
+        check(self._L.wsmc_get_state(self._h, C.byref(s)))
+        return dict(resampled=int(s.resampled), weights_changed=int(s.weights_changed), depth=int(s.depth),
+                    n_terms=int(s.n_terms), last_ess_perc=float(s.last_ess_perc),
+                    op_counter=int(s.op_counter), n_resamples=int(s.n_resamples))
+
+    def set_depth(self, d: int) -> None:
+        check(self._L.wsmc_set_depth(self._h, int(d)))
+
+    def set_op_counter(self, op: int) -> None:
+        check(self._L.wsmc_set_op_counter(self._h, int(op)))
+
+    def last_ancestors(self) -> np.ndarray:
+        a = np.empty(self.n, dtype=np.int32)
+        check(self._L.wsmc_last_ancestors(self._h, a.ctypes.data_as(_I32P)))
+        return a
+
+    # ---- operators ----
+    def assign(self, out: int, exprs) -> None:
+        check(self._L.wsmc_assign(self._h, int(out), _operands4(exprs)))
+
+    def sample(self, out: int, dist: Dist) -> None:
+        check(self._L.wsmc_sample(self._h, int(out), C.byref(dist)))
+
+    def sample_importance(self, out: int, proposal: Dist, target: Dist) -> None:
+        check(self._L.wsmc_sample_importance(self._h, int(out), C.byref(proposal), C.byref(target)))
+
+    def observe(self, dist: Dist, x) -> None:
+        check(self._L.wsmc_observe(self._h, C.byref(dist), _operands4(x)))
+
+    def weight(self, dist: Dist, x) -> None:
+        check(self._L.wsmc_weight(self._h, C.byref(dist), _operands4(x)))
+
+    def resample(self, ess_perc_min: float, scheme: int = abi.RESAMPLE_STRATIFIED):
+        r = C.c_int32()
+        e = C.c_double()
+        check(self._L.wsmc_resample(self._h, float(ess_perc_min), int(scheme), C.byref(r), C.byref(e)))
+        return bool(r.value), float(e.value)
+
+    def move(self, proposal: int, targets, step: float, lo=None, hi=None, target_depth: int = -1,
+             diversity: float = math.nan) -> int:
+        t = np.ascontiguousarray(np.asarray(targets, dtype=np.int32))
+        d = len(t)
+        lo_a = None if lo is None else np.ascontiguousarray(np.asarray(lo, float).reshape(d))
+        hi_a = None if hi is None else np.ascontiguousarray(np.asarray(hi, float).reshape(d))
+        acc = C.c_int64()
+        rc = self._L.wsmc_move(self._h, int(proposal), t.ctypes.data_as(_I32P), d, float(step),
+                               None if lo_a is None else _dptr(lo_a), None if hi_a is None else _dptr(hi_a),
+                               int(target_depth), float(diversity), C.byref(acc))
+        if rc == abi.WSMC_ENOTPD:
+            raise np.linalg.LinAlgError(self._L.wsmc_last_error().decode())
+        check(rc)
+        return int(acc.value)
+
+    def score(self, target_depth: int) -> np.ndarray:
+        out = np.empty(self.n)
+        check(self._L.wsmc_score(self._h, int(target_depth), _dptr(out)))
+        return out
+
+    def marginal_diversity(self, targets) -> float:
+        t = np.ascontiguousarray(np.asarray(targets, dtype=np.int32))
+        v = C.c_double()
+        check(self._L.wsmc_marginal_diversity(self._h, t.ctypes.data_as(_I32P), len(t), C.byref(v)))
+        return float(v.value)
+
+    # ---- fused runners ----
+    def ssm2d_run(self, obs, x0=(0.0, 0.0), v0=(1.0, 0.0), q_var=0.1, r_var=0.5, ess_perc_min=0.5,
+                  scheme: int = abi.RESAMPLE_STRATIFIED, keep_history: bool = True,
+                  want_evidence: bool = True):
+        o = np.ascontiguousarray(np.asarray(obs, dtype=np.float64).reshape(-1, 2))
+        x0a = np.asarray(x0, dtype=np.float64)
+        v0a = np.asarray(v0, dtype=np.float64)
+        ev = C.c_double()
+        check(self._L.wsmc_ssm2d_run(self._h, _dptr(o), len(o), _dptr(x0a), _dptr(v0a), float(q_var),
+                                     float(r_var), float(ess_perc_min), int(scheme), int(bool(keep_history)),
+                                     C.byref(ev) if want_evidence else None))
+        return float(ev.value) if want_evidence else None
+
+    def set_timing(self, enabled: bool) -> None:
+        check(self._L.wsmc_run_set_timing(self._h, int(bool(enabled))))
+
+    def timing(self) -> dict:
+        t = RunTiming()
+        check(self._L.wsmc_run_get_timing(self._h, C.byref(t)))
+        return {f: getattr(t, f) for f, _ in RunTiming._fields_}
+
+
+def device_count() -> int:
+    n = C.c_int32()
+    check(load_library().wsmc_device_count(C.byref(n)))
+    return int(n.value)
