@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""North-star benchmark: 2D SSM bootstrap filter (examples/2D_ssm.jl), particle-steps/s.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One bench "step" = one full run! of the T-step filter over one synthetic observation
+sequence (T = 100, the BASELINE.json configs[1] workload), including the final
+history trace-back that materialises x_1..x_{T+1} exactly as the reference's store holds
+them. N = 1,000,000 particles per GPU (weak scaling: each rank owns a 1M shard, ranks
+exchange one 1-KB statistics record per step over RCCL; island resampling).
+
+Rank 0 prints ONE JSON line (metric/value/.../roofline/cpu_baseline). Everything else
+goes to stderr.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import pathlib
+import sys
+import time
+
+REPO = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "weightedsampling.jl_amd"))
+
+import numpy as np  # noqa: E402
+
+METRIC = json.loads((REPO / "BASELINE.json").read_text())["metric"] if (REPO / "BASELINE.json").exists() else \
+    "particle-steps/sec (N_particles × T_steps / wall-s), 2D SSM bootstrap filter"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+PROP_BYTES_STEADY = 92         # propagate kernel, per particle, step t >= 2 after a resample
+PROP_BYTES_FIRST = 64          # step 1: x0/v0 are constants, weights read once
+STEP_BYTES = 104               # whole step algorithmic bytes
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--particles", type=int, default=1_000_000, help="particles per GPU")
+    ap.add_argument("--T", type=int, default=100)
+    ap.add_argument("--ess", type=float, default=1.0)
+    ap.add_argument("--scheme", choices=["stratified", "systematic"], default="stratified")
+    ap.add_argument("--no-history", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-particles", type=int, default=500_000)
+    ap.add_argument("--cpu-T", type=int, default=100)
+    ap.add_argument("--seed", type=int, default=42)
+    return ap.parse_args()
+
+
+def cpu_baseline(obs, n, T, ess, scheme):
+    """The oracle (C restatement of the reference path, eager ColumnStore gathers) on the host."""
+    sys.path.insert(0, str(REPO / "oracle"))
+    from oracle import Oracle  # test infrastructure: only the cpu_baseline leg loads it
+    import wsmc
+    o = Oracle(n, seed=42)
+    t0 = time.perf_counter()
+    wsmc.models.ssm2d_statements(o, obs[:T], ess_perc_min=ess, scheme=scheme)
+    dt = time.perf_counter() - t0
+    o.close()
+    return n * T / dt, dt
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # rendezvous, barriers and the max-over-ranks only
+        dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
+    import wsmc
+    from wsmc import abi
+
+    scheme = abi.RESAMPLE_STRATIFIED if args.scheme == "stratified" else abi.RESAMPLE_SYSTEMATIC
+    N = args.particles
+    T = args.T
+    obs = wsmc.models.ssm2d_data(max(T, args.cpu_T), seed=args.seed)
+    ctx = wsmc.Context(N, seed=args.seed + 1000003 * rank, device=local)
+    if world > 1:
+        import torch
+        uid = [wsmc.Context.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        ctx.comm_init(uid[0], world, rank, rank * N, world * N)
+
+    def barrier():
+        ctx.sync()
+        if dist is not None:
+            dist.barrier()
+
+    def one_run():
+        return ctx.ssm2d_run(obs[:T], ess_perc_min=args.ess, scheme=scheme, keep_history=not args.no_history,
+                             want_evidence=False)
+
+    for _ in range(args.warmup):
+        one_run()
+    # timed region: K full filter runs, no instrumentation
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_run()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    st = ctx.get_state()
+    ev = ctx.log_evidence()
+
+    # per-kernel durations: HIP events recorded on the context stream around every launch of
+    # the same graph (a separate instrumented pass of `steps` runs)
+    ctx.set_timing(True)
+    prop_ms = red_ms = rs_ms = fin_ms = tot_ms = 0.0
+    nres = 0
+    inst_runs = max(1, min(args.steps, 5))
+    one_run()  # capture the instrumented graph
+    for _ in range(inst_runs):
+        one_run()
+        tm = ctx.timing()
+        prop_ms += tm["propagate_ms"]; red_ms += tm["reduce_ms"]; rs_ms += tm["resample_ms"]
+        fin_ms += tm["finalize_ms"]; tot_ms += tm["total_ms"]; nres += tm["n_resamples"]
+    ctx.set_timing(False)
+    prop_ms /= inst_runs; red_ms /= inst_runs; rs_ms /= inst_runs; fin_ms /= inst_runs; tot_ms /= inst_runs
+    nres //= inst_runs
+
+    units = world * N * T * args.steps
+    value = units / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    # propagate-kernel algorithmic bytes per run (forced resampling: every step after t=1 reads
+    # through ancestors; t = 1 starts from the constant x0/v0)
+    forced = nres == T - 1
+    prop_bytes = N * (PROP_BYTES_FIRST + (T - 1) * PROP_BYTES_STEADY)
+    prop_gbs = prop_bytes / (prop_ms * 1e-3) / 1e9 if prop_ms > 0 else None
+    traffic = None
+    tf = REPO / "profiles" / "pmc_propagate_bytes.json"
+    if tf.exists():
+        try:
+            traffic = json.loads(tf.read_text()).get("bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cps, cdt = cpu_baseline(obs, args.cpu_particles, args.cpu_T, args.ess, scheme)
+        cpu = {"value": cps, "unit": "particle-steps/s", "cores": 1, "kind": "port",
+               "sample": f"oracle/ C restatement (eager ColumnStore gathers, 1 thread), 2D SSM "
+                         f"N={args.cpu_particles} T={args.cpu_T} ess_perc_min={args.ess}: {cdt:.2f} s"}
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "particle-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: examples/2D_ssm.jl observation recurrence (numpy Philox seed 42)",
+            "config": {"workload": "2D SSM bootstrap filter (examples/2D_ssm.jl), BASELINE configs[1]",
+                       "n_particles_per_gpu": N, "global_particles": world * N, "T": T,
+                       "ess_perc_min": args.ess, "scheme": args.scheme, "keep_history": not args.no_history,
+                       "parallelism": f"island-shard x{world}" if world > 1 else "single GPU"},
+            "roofline": {"bound": "hbm", "kernel": "k_ssm2d_prop (propagate+observe+max)",
+                         "achieved": prop_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": (prop_gbs / HBM_PEAK_GBS) if prop_gbs else None, "traffic": traffic,
+                         "algorithmic_bytes_per_run": prop_bytes, "avg_launch_us": prop_ms * 1e3 / T,
+                         "whole_step_GBs": value / world * STEP_BYTES / 1e9},
+            "cpu_baseline": cpu,
+            "breakdown_ms_per_run": {"propagate": prop_ms, "weight_stats": red_ms, "scan_ancestors": rs_ms,
+                                     "finalize_traceback": fin_ms, "instrumented_total": tot_ms,
+                                     "resamples_per_run": nres, "forced_every_step": forced},
+            "log_evidence_last": ev,
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

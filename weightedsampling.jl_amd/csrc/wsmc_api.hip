@@ -836,7 +836,7 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         *outp = tabs + (T + 2);
         return WSMC_OK;
     };
-    const bool use_graph = c->world == 1;
+    const bool use_graph = c->world == 1 && !c->timing;   // HIP cannot time events captured in graphs
     const int nev = 4 * T + 2;
     std::vector<hipEvent_t> evs;
     if (c->timing) {
@@ -876,6 +876,9 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
     } else {
         if ((r = build_tables(&p.d_hist_work, &p.d_hist_out))) return r;
         temp_tables = p.d_hist_work;
+        // instrumented runs: a bounded delay kernel keeps the GPU busy while the host queues
+        // the whole run, so no host-submission gap lands inside an event pair
+        if (c->timing) WSMC_HIP(launch_delay(c->stream, 20000));
         r = enqueue_ssm2d(c, p, c->timing ? &evs : nullptr);
         if (r) {
             if (temp_tables) (void)hipFree(temp_tables);

@@ -209,5 +209,6 @@ struct Ssm2dFinal {
     const Decision* dec;       // [T+1], index t
 };
 hipError_t launch_ssm2d_finalize(hipStream_t s, const Ssm2dFinal& f);
+hipError_t launch_delay(hipStream_t s, int microseconds);
 
 }  // namespace wsmc

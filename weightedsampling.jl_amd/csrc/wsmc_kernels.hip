@@ -726,6 +726,19 @@ hipError_t launch_ssm2d_propagate(hipStream_t s, const Ssm2dArgs& a) {
     hipLaunchKernelGGL(k_ssm2d_prop, grid_for(a.N), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
+// bounded spin on the 100 MHz constant clock (always exits): queue-filling delay for
+// instrumented runs
+__global__ void k_delay(int microseconds) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long ticks = (unsigned long long)microseconds * 100ull;
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+hipError_t launch_delay(hipStream_t s, int microseconds) {
+    if (microseconds > 100000) microseconds = 100000;
+    hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, s, microseconds);
+    return hipGetLastError();
+}
+
 hipError_t launch_ssm2d_finalize(hipStream_t s, const Ssm2dFinal& f) {
     hipLaunchKernelGGL(k_ssm2d_final, grid_for(f.N), dim3(kBlock), 0, s, f);
     return hipGetLastError();
