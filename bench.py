@@ -76,28 +76,27 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # rendezvous, barriers and the max-over-ranks only
-        dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
     import wsmc
     from wsmc import abi
+    from wsmc.hostcomm import from_env
+    # host rendezvous / barriers / max-over-ranks over TCP; the rank process never imports
+    # torch (its bundled HIP runtime would clash with libwsmc's ROCm one). The data path
+    # between ranks is RCCL inside libwsmc.
+    comm = from_env() if world > 1 else None
 
     scheme = abi.RESAMPLE_STRATIFIED if args.scheme == "stratified" else abi.RESAMPLE_SYSTEMATIC
     N = args.particles
     T = args.T
     obs = wsmc.models.ssm2d_data(max(T, args.cpu_T), seed=args.seed)
     ctx = wsmc.Context(N, seed=args.seed + 1000003 * rank, device=local)
-    if world > 1:
-        import torch
-        uid = [wsmc.Context.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        ctx.comm_init(uid[0], world, rank, rank * N, world * N)
+    if comm is not None:
+        uid = comm.broadcast(wsmc.Context.comm_unique_id() if rank == 0 else None)
+        ctx.comm_init(uid, world, rank, rank * N, world * N)
 
     def barrier():
         ctx.sync()
-        if dist is not None:
-            dist.barrier()
+        if comm is not None:
+            comm.barrier()
 
     def one_run():
         return ctx.ssm2d_run(obs[:T], ess_perc_min=args.ess, scheme=scheme, keep_history=not args.no_history,
@@ -112,11 +111,8 @@ def main():
         one_run()
     barrier()
     elapsed = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    if comm is not None:
+        elapsed = comm.max(elapsed)
     st = ctx.get_state()
     ev = ctx.log_evidence()
 
@@ -189,9 +185,9 @@ def main():
         }
         print(json.dumps(line), flush=True)
     ctx.close()
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+    if comm is not None:
+        comm.barrier()
+        comm.close()
 
 
 if __name__ == "__main__":

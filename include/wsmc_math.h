@@ -312,9 +312,17 @@ WSMC_HD double wsmc_uniform_k(uint64_t seed, uint64_t op, uint64_t idx, uint32_t
     wsmc_u32x4 w = wsmc_rng_block(seed, op, idx, (k >> 1) | 0x80u);
     return (k & 1) ? wsmc_u01(w.v[2], w.v[3]) : wsmc_u01(w.v[0], w.v[1]);
 }
-/* 32-bit stratum offset word for resampling slot n (systematic: n = 0) */
+/* 32-bit stratum offset word for resampling slot n (systematic: one word for all slots).
+ * A murmur3 fmix64 finalizer over (seed, op, n): a bijective 64-bit mixer, ~20 integer
+ * ops, cheap enough to evaluate inside the per-particle rank() of the ancestor scan. */
 WSMC_HD uint32_t wsmc_strat_word(uint64_t seed, uint64_t op, uint64_t n) {
-    return wsmc_rng_block(seed, op, n, 0x40u).v[0];
+    uint64_t z = seed ^ (op * 0x9E3779B97F4A7C15ULL) ^ (n * 0xD1B54A32D192ED03ULL) ^ 0x5851F42D4C957F2DULL;
+    z ^= z >> 33;
+    z *= 0xFF51AFD7ED558CCDULL;
+    z ^= z >> 33;
+    z *= 0xC4CEB9FE1A85EC53ULL;
+    z ^= z >> 33;
+    return (uint32_t)(z >> 32);
 }
 
 /* ------------------------------------------------------------------------- */
@@ -377,9 +385,8 @@ WSMC_HD double wsmc_log_abs_jac(double z, double lo, double hi) {
  * identical for any reduction order, grid shape or shard count.
  */
 WSMC_HD int wsmc_qbits(uint64_t n) {
-    int c = 0;
-    while (((uint64_t)1 << c) < n) ++c;   /* ceil(log2 n) */
-    return 63 - c;
+    /* 63 - ceil(log2 n) */
+    return n <= 1 ? 63 : 63 - (64 - __builtin_clzll(n - 1));
 }
 WSMC_HD uint64_t wsmc_qweight(double lw, double M, int K) {
     double e = wsmc_exp(lw - M);
@@ -401,23 +408,28 @@ WSMC_HD uint64_t wsmc_target(uint64_t n, uint32_t R, uint64_t Q, uint64_t N) {
     return (uint64_t)(num / den);
 }
 
-/* #{ n : x_n < c }  (monotone in c); scheme 0 = stratified, 1 = systematic */
-WSMC_HD uint64_t wsmc_rank(uint64_t c, uint64_t Q, uint64_t N, int scheme,
-                           uint64_t seed, uint64_t op, uint64_t slot_base) {
+/* #{ n : x_n < c }  (monotone in c); scheme 0 = stratified, 1 = systematic.
+ * ratio = N/Q as a double (any estimate works: the result is corrected exactly). */
+WSMC_HD uint64_t wsmc_rank_r(uint64_t c, uint64_t Q, uint64_t N, double ratio, int scheme,
+                             uint64_t seed, uint64_t op, uint64_t slot_base) {
     if (c == 0) return 0;
     if (c >= Q) return N;
-    wsmc_u128 cN = (wsmc_u128)c * (wsmc_u128)N;
-    /* n* = floor(c*N/Q): float estimate then exact integer correction */
-    double est = wsmc_u64_to_d(c) * wsmc_u64_to_d(N) / wsmc_u64_to_d(Q);
-    uint64_t ns = wsmc_d_to_u64_trunc(est);
+    const wsmc_u128 cN = (wsmc_u128)c * (wsmc_u128)N;
+    /* n* = floor(c*N/Q) and rem = c*N - n*·Q in [0, Q): float estimate, exact correction */
+    uint64_t ns = wsmc_d_to_u64_trunc(wsmc_u64_to_d(c) * ratio);
     if (ns > N) ns = N;
-    while ((wsmc_u128)ns * Q > cN) --ns;
-    while ((wsmc_u128)(ns + 1) * Q <= cN) ++ns;
+    wsmc_u128 p = (wsmc_u128)ns * (wsmc_u128)Q;
+    while (p > cN) { --ns; p -= Q; }
+    while (cN - p >= Q) { ++ns; p += Q; }
     if (ns >= N) return N;
-    uint32_t R = wsmc_strat_word(seed, op, scheme == 1 ? slot_base : slot_base + ns);
-    wsmc_u128 lhs = (((wsmc_u128)ns << 32) | R) * (wsmc_u128)Q;
-    wsmc_u128 rhs = cN << 32;
-    return ns + (lhs < rhs ? 1u : 0u);
+    const uint64_t rem = (uint64_t)(cN - p);
+    const uint32_t R = wsmc_strat_word(seed, op, scheme == 1 ? slot_base : slot_base + ns);
+    /* x_{n*} < c  <=>  (n*·2^32 + R)·Q < c·N·2^32  <=>  R·Q < rem·2^32 */
+    return ns + (((wsmc_u128)R * (wsmc_u128)Q) < ((wsmc_u128)rem << 32) ? 1u : 0u);
+}
+WSMC_HD uint64_t wsmc_rank(uint64_t c, uint64_t Q, uint64_t N, int scheme,
+                           uint64_t seed, uint64_t op, uint64_t slot_base) {
+    return wsmc_rank_r(c, Q, N, wsmc_u64_to_d(N) / wsmc_u64_to_d(Q), scheme, seed, op, slot_base);
 }
 
 /* 4x4-max Cholesky of a symmetric matrix (row-major a[d*d]) -> lower L; 0 if not PD */

@@ -28,6 +28,11 @@ _SIG = {
     "or_create": (_P, [C.c_int64, C.c_uint64]),
     "or_destroy": (None, [_P]),
     "or_set_shards": (C.c_int, [_P, C.c_int32]),
+    "or_set_global_offset": (None, [_P, C.c_int64]),
+    "or_shard_record": (None, [_P, C.POINTER(C.c_uint64)]),
+    "or_resample_records": (C.c_int, [_P, C.c_double, C.c_int32, C.POINTER(C.c_uint64), C.c_int32, C.c_int32,
+                                      _I32P, _D]),
+    "or_log_evidence_records": (C.c_double, [C.POINTER(C.c_uint64), C.c_int32]),
     "or_nparticles": (C.c_int64, [_P]),
     "or_get_op": (C.c_uint64, [_P]),
     "or_set_op": (None, [_P, C.c_uint64]),
@@ -113,7 +118,7 @@ class Oracle:
 
     is_oracle = True
 
-    def __init__(self, n_particles: int, seed: int = 42, shards: int = 1):
+    def __init__(self, n_particles: int, seed: int = 42, shards: int = 1, global_offset: int = 0):
         self._L = lib()
         self._h = self._L.or_create(int(n_particles), int(seed) & (2**64 - 1))
         if not self._h:
@@ -123,6 +128,23 @@ class Oracle:
         if shards != 1 and self._L.or_set_shards(self._h, int(shards)) != 0:
             raise ValueError("bad shard count")
         self.shards = shards
+        if global_offset:
+            self._L.or_set_global_offset(self._h, int(global_offset))
+
+    # ---- one shard of a multi-process run (record exchange) ----
+    def shard_record(self) -> np.ndarray:
+        out = np.zeros(8, dtype=np.uint64)
+        self._L.or_shard_record(self._h, out.ctypes.data_as(C.POINTER(C.c_uint64)))
+        return out
+
+    def resample_records(self, ess_perc_min: float, scheme: int, records: np.ndarray, rank: int):
+        r = np.ascontiguousarray(np.asarray(records, dtype=np.uint64).reshape(-1))
+        rs = C.c_int32()
+        e = C.c_double()
+        self._chk(self._L.or_resample_records(self._h, float(ess_perc_min), int(scheme),
+                                              r.ctypes.data_as(C.POINTER(C.c_uint64)), len(r) // 8, int(rank),
+                                              C.byref(rs), C.byref(e)))
+        return bool(rs.value), float(e.value)
 
     def close(self):
         if self._h:
@@ -277,6 +299,11 @@ def philox(ctr, key):
     o = (C.c_uint32 * 4)()
     lib().or_philox(c, k, o)
     return list(o)
+
+
+def log_evidence_records(records) -> float:
+    r = np.ascontiguousarray(np.asarray(records, dtype=np.uint64).reshape(-1))
+    return float(lib().or_log_evidence_records(r.ctypes.data_as(C.POINTER(C.c_uint64)), len(r) // 8))
 
 
 def canon_sum(vals) -> float:

@@ -62,6 +62,7 @@ typedef struct oracle {
     int32_t nterms, cap_terms;
     int32_t nshards;
     int64_t shard_off[OR_MAX_SHARDS + 1];
+    int64_t goff;              /* global index of particle 0 (one shard of a multi-process run) */
     int32_t* last_anc;
     double* scratch;
     double* tmp;               /* 4*N staging for statements that read their own output */
@@ -99,6 +100,7 @@ int or_set_shards(oracle* o, int32_t G) {
 }
 
 int64_t or_nparticles(oracle* o) { return o->N; }
+void or_set_global_offset(oracle* o, int64_t goff) { o->goff = goff; }
 uint64_t or_get_op(oracle* o) { return o->op; }
 void or_set_op(oracle* o, uint64_t op) { o->op = op; }
 int32_t or_get_depth(oracle* o) { return o->depth; }
@@ -184,7 +186,7 @@ static void sample_into(oracle* o, int32_t out, const wsmc_dist* d, uint64_t op,
     int dim = o->cols[out].dim;
     for (int64_t i = 0; i < N; ++i) {
         double x[4];
-        wsmc_dist_sample(d, x, o->seed, op, (uint64_t)i, o->colptr, N, i);
+        wsmc_dist_sample(d, x, o->seed, op, (uint64_t)(o->goff + i), o->colptr, N, i);
         for (int k = 0; k < dim; ++k) tmp[(int64_t)k * N + i] = x[k];
     }
 }
@@ -302,7 +304,6 @@ int or_resample(oracle* o, double ess_min, int32_t scheme, int32_t* resampled_ou
         if (ess_out) *ess_out = o->last_ess;
         return 0;
     }
-    int64_t N = o->N;
     int G = o->nshards;
     or_stats st[OR_MAX_SHARDS];
     for (int g = 0; g < G; ++g) {
@@ -315,7 +316,7 @@ int or_resample(oracle* o, double ess_min, int32_t scheme, int32_t* resampled_ou
         for (int g = 0; g < G; ++g) {
             int64_t a = o->shard_off[g], b = o->shard_off[g + 1], n = b - a;
             int K = wsmc_qbits((uint64_t)n);
-            shard_ancestors(o->w + a, n, K, st[g].M, st[g].Q, scheme, o->seed, op, (uint64_t)a,
+            shard_ancestors(o->w + a, n, K, st[g].M, st[g].Q, scheme, o->seed, op, (uint64_t)(o->goff + a),
                             o->last_anc + a);
             for (int64_t s = 0; s < n; ++s) o->last_anc[a + s] += (int32_t)a;
         }
@@ -335,6 +336,61 @@ int or_resample(oracle* o, double ess_min, int32_t scheme, int32_t* resampled_ou
     if (resampled_out) *resampled_out = o->resampled;
     if (ess_out) *ess_out = ess;
     return 0;
+}
+
+/* ---- one shard of a multi-process run: record exchange ------------------------------
+ * record layout (8 x u64): M bits, Q, Q2 lo, Q2 hi, W lo, W hi, n, 0 — the payload the GPU
+ * ranks exchange with ncclAllGather each step (weightedsampling.jl_amd/csrc, ShardRec). */
+void or_shard_record(oracle* o, uint64_t* out) {
+    or_stats s = shard_stats(o->w, o->N, wsmc_qbits((uint64_t)o->N));
+    out[0] = wsmc_d2bits(s.M); out[1] = s.Q;
+    out[2] = (uint64_t)s.Q2; out[3] = (uint64_t)(s.Q2 >> 64);
+    out[4] = (uint64_t)s.W; out[5] = (uint64_t)(s.W >> 64);
+    out[6] = s.n; out[7] = 0;
+}
+static or_stats record_stats(const uint64_t* r) {
+    or_stats s;
+    s.M = wsmc_bits2d(r[0]); s.Q = r[1];
+    s.Q2 = ((wsmc_u128)r[3] << 64) | r[2];
+    s.W = ((wsmc_u128)r[5] << 64) | r[4];
+    s.n = r[6];
+    return s;
+}
+/* Resample of this shard given every shard's record (rank order): global ESS decision,
+ * island resampling, shard log-mean reset. Same semantics as or_resample with shards. */
+int or_resample_records(oracle* o, double ess_min, int32_t scheme, const uint64_t* recs, int32_t G,
+                        int32_t rank, int32_t* resampled_out, double* ess_out) {
+    uint64_t op = o->op++;
+    if (!o->weights_changed) {
+        if (resampled_out) *resampled_out = o->resampled;
+        if (ess_out) *ess_out = o->last_ess;
+        return 0;
+    }
+    or_stats st[OR_MAX_SHARDS];
+    for (int g = 0; g < G; ++g) st[g] = record_stats(recs + 8 * g);
+    double ess = wsmc_global_ess(st, G);
+    o->last_ess = ess;
+    if (ess < ess_min) {
+        int K = wsmc_qbits((uint64_t)o->N);
+        shard_ancestors(o->w, o->N, K, st[rank].M, st[rank].Q, scheme, o->seed, op, (uint64_t)o->goff,
+                        o->last_anc);
+        double mean = wsmc_shard_mean(&st[rank]);
+        for (int64_t i = 0; i < o->N; ++i) o->w[i] = mean;
+        or_store_resample(o, o->last_anc);
+        o->resampled = 1;
+        o->n_resamples += 1;
+    } else {
+        o->resampled = 0;
+    }
+    o->weights_changed = 0;
+    if (resampled_out) *resampled_out = o->resampled;
+    if (ess_out) *ess_out = ess;
+    return 0;
+}
+double or_log_evidence_records(const uint64_t* recs, int32_t G) {
+    or_stats st[OR_MAX_SHARDS];
+    for (int g = 0; g < G; ++g) st[g] = record_stats(recs + 8 * g);
+    return wsmc_global_log_evidence(st, G);
 }
 
 /* logsumexp(weights) - log(N) via the same fixed point (src/utils.jl:21) */
@@ -484,7 +540,7 @@ int or_move(oracle* o, int32_t proposal, const int32_t* targets, int32_t d, doub
         double xi[4], dz[4];
         wsmc_override ov;
         ov.n = d;
-        for (int k = 0; k < d; ++k) xi[k] = wsmc_normal_k(o->seed, op_prop, (uint64_t)i, (uint32_t)k);
+        for (int k = 0; k < d; ++k) xi[k] = wsmc_normal_k(o->seed, op_prop, (uint64_t)(o->goff + i), (uint32_t)k);
         for (int k = 0; k < d; ++k) {
             double s = 0.0;
             for (int j = 0; j <= k; ++j) s = s + L[k * d + j] * xi[j];
@@ -503,7 +559,7 @@ int or_move(oracle* o, int32_t proposal, const int32_t* targets, int32_t d, doub
         }
         double s_old = wsmc_fold(o->tape, o->nterms, target_depth, o->colptr, N, i, 0);
         double s_new = wsmc_fold(o->tape, o->nterms, target_depth, o->colptr, N, i, &ov);
-        double u = wsmc_uniform_k(o->seed, op_acc, (uint64_t)i, 0);
+        double u = wsmc_uniform_k(o->seed, op_acc, (uint64_t)(o->goff + i), 0);
         ok[i] = wsmc_log(u) < (lpr + s_new) - s_old;   /* src/transformers.jl:615 */
     }
     for (int64_t i = 0; i < N; ++i) {

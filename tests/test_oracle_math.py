@@ -1,0 +1,191 @@
+"""CPU tests of the shared math (include/wsmc_math.h) and of the oracle's resampling
+restatement: known-answer vectors, accuracy against libm/numpy, the integer CDF target
+map and its inverse, canonical reduction order, and the reference's edge cases."""
+import math
+
+import numpy as np
+import pytest
+
+import oracle as O
+from oracle import Oracle
+import wsmc
+from wsmc import abi
+
+L = O.lib()
+
+
+def test_philox_random123_kat():
+    # Random123 kat_vectors, philox4x32_10
+    assert O.philox([0, 0, 0, 0], [0, 0]) == [0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8]
+    assert O.philox([0xffffffff] * 4, [0xffffffff] * 2) == [0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd]
+    assert O.philox([0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344], [0xa4093822, 0x299f31d0]) == \
+        [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1]
+
+
+def _ulps(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return np.abs(a - b) / np.spacing(np.maximum(np.abs(b), np.finfo(float).tiny))
+
+
+def test_exp_log_accuracy():
+    g = np.random.default_rng(0)
+    xs = np.concatenate([g.uniform(-745, 709, 20000), g.uniform(-1, 1, 20000), g.uniform(-1e-9, 1e-9, 100),
+                         [0.0, -0.0, 1e-300, -1e-300]])
+    e = np.array([L.or_exp(x) for x in xs])
+    ref = np.exp(xs)
+    ok = ref > 1e-300
+    assert np.max(_ulps(e[ok], ref[ok])) <= 1.0
+    assert L.or_exp(0.0) == 1.0 and L.or_exp(-800.0) == 0.0 and math.isinf(L.or_exp(710.0))
+    ys = np.concatenate([np.exp(g.uniform(-700, 700, 20000)), g.uniform(0.5, 2, 20000), [5e-324, 1e-310, 1.0]])
+    l = np.array([L.or_log(y) for y in ys])
+    assert np.max(_ulps(l, np.log(ys))[np.log(ys) != 0]) <= 1.0
+    assert L.or_log(1.0) == 0.0 and L.or_log(0.0) == -math.inf and math.isnan(L.or_log(-1.0))
+
+
+def test_trig_and_log1p():
+    g = np.random.default_rng(1)
+    zs = g.uniform(-500, 500, 20000)
+    assert np.max(np.abs(np.array([L.or_cos(z) for z in zs]) - np.cos(zs))) < 4e-16 * 500
+    import ctypes
+    s, c = ctypes.c_double(), ctypes.c_double()
+    for u in g.uniform(0, 1, 5000):
+        L.or_sincos2pi(u, ctypes.byref(s), ctypes.byref(c))
+        assert abs(s.value - math.sin(2 * math.pi * u)) < 1e-15
+        assert abs(c.value - math.cos(2 * math.pi * u)) < 1e-15
+    xx = np.exp(g.uniform(-40, 5, 5000))
+    assert np.max(np.abs(np.array([L.or_log1p(x) for x in xx]) - np.log1p(xx)) / np.log1p(xx)) < 1e-15
+
+
+def test_draw_moments():
+    z = np.array([L.or_normal_k(42, 7, i, k) for i in range(100000) for k in range(2)])
+    assert abs(z.mean()) < 0.01 and abs(z.var() - 1) < 0.01
+    u = np.array([L.or_uniform_k(42, 7, i, k) for i in range(50000) for k in range(2)])
+    assert u.min() >= 0.0 and u.max() < 1.0 and abs(u.mean() - 0.5) < 0.005
+
+
+def test_qbits():
+    for n, k in [(1, 63), (2, 62), (3, 61), (1024, 53), (1025, 52), (1 << 20, 43), (1_000_000, 43)]:
+        assert L.or_qbits(n) == k
+
+
+@pytest.mark.parametrize("scheme", [0, 1])
+def test_rank_inverts_targets(scheme):
+    """rank(c) = #{n : x_n < c} for the stratified / systematic integer targets."""
+    g = np.random.default_rng(scheme)
+    for trial in range(60):
+        N = int(g.integers(1, 40))
+        Q = int(g.integers(1, 2**62))
+        seed, op = int(g.integers(0, 2**63)), int(g.integers(0, 2**40))
+        base = int(g.integers(0, 1000))
+        R0 = L.or_strat_word(seed, op, base)
+        xs = [L.or_target(n, R0 if scheme else L.or_strat_word(seed, op, base + n), Q, N) for n in range(N)]
+        assert all(0 <= x < Q for x in xs) and xs == sorted(xs)
+        cs = sorted(set([0, 1, Q - 1, Q] + [int(x) for x in xs] + [int(x) + 1 for x in xs] +
+                        [int(v) for v in g.integers(0, Q, 20)]))
+        for c in cs:
+            assert L.or_rank(c, Q, N, scheme, seed, op, base) == sum(1 for x in xs if x < c)
+
+
+def test_canonical_sum_order():
+    g = np.random.default_rng(5)
+    for n in (1, 7, 2048, 2049, 100_000):
+        v = g.standard_normal(n)
+        assert abs(O.canon_sum(v) - math.fsum(v)) < 1e-9 * max(1, n)
+    # associativity matters: the canonical order is reproducible, not sequential
+    v = np.array([1e16, 1.0, -1e16] + [0.0] * 5000)
+    assert O.canon_sum(v) == O.canon_sum(v.copy())
+
+
+def _weights_state(lw, seed=1):
+    o = Oracle(len(lw), seed=seed)
+    c = o.col_create("x", 1)
+    o.col_upload(c, np.arange(len(lw), dtype=float))
+    o.weights_upload(lw)
+    return o, c
+
+
+def _force_changed(o):
+    # Observe a constant factor (logpdf of N(0,1) at 0): sets weights_changed like `=>`
+    d = wsmc.Normal(0.0, 1.0).dist(lambda n: o.col_find(n))
+    o.observe(d, [abi.Operand.const(0.0)])
+
+
+def test_resample_all_equal_weights_not_resampled():
+    o, _ = _weights_state(np.zeros(1000))
+    _force_changed(o)
+    rs, ess = o.resample(1.0)
+    assert not rs and ess == 1.0            # ESS% == 1 exactly; strict `<` (src/transformers.jl:484)
+
+
+def test_resample_dominant_particle():
+    lw = np.full(5000, -1000.0)
+    lw[1234] = 0.0
+    o, c = _weights_state(lw)
+    _force_changed(o)
+    rs, ess = o.resample(0.5)
+    assert rs and ess < 1e-3
+    assert np.all(o.col_download(c) == 1234.0)
+    w = o.weights_download()
+    assert np.all(w == w[0])
+
+
+def test_resample_neg_inf_and_nan():
+    lw = np.zeros(4096)
+    lw[::2] = -np.inf
+    o, c = _weights_state(lw)
+    _force_changed(o)
+    rs, ess = o.resample(1.0)
+    assert rs and abs(ess - 0.5) < 1e-12
+    assert np.all(o.col_download(c) % 2 == 1)   # zero-weight particles never chosen
+    lw = np.zeros(100)
+    lw[3] = np.nan
+    o, _ = _weights_state(lw)
+    _force_changed(o)
+    rs, ess = o.resample(1.0)
+    assert not rs and math.isnan(ess)          # exp_norm of NaN weights: no resample
+
+
+def test_resample_single_particle_and_gating():
+    o, _ = _weights_state(np.array([-3.0]))
+    rs, _ = o.resample(1.0)                    # weights_changed false -> no-op
+    assert not rs and o.get_state()["op_counter"] == 1
+    _force_changed(o)
+    rs, ess = o.resample(1.0)
+    assert not rs and ess == 1.0
+
+
+def test_stratified_offspring_bounds():
+    """Stratified resampling gives each particle floor/ceil(N w_i) ± 1 offspring."""
+    g = np.random.default_rng(3)
+    N = 10000
+    lw = g.standard_normal(N) * 2
+    o, c = _weights_state(lw)
+    _force_changed(o)
+    rs, _ = o.resample(1.0)
+    assert rs
+    cnt = np.bincount(o.last_ancestors(), minlength=N)
+    w = np.exp(lw - lw.max())
+    w /= w.sum()
+    assert np.all(np.abs(cnt - N * w) <= 2.0)
+    anc = o.last_ancestors()
+    assert np.all(np.diff(anc) >= 0)            # icdf output is sorted
+
+
+def test_island_resampling_preserves_evidence():
+    g = np.random.default_rng(9)
+    lw = g.standard_normal(8192) * 3
+    for shards in (1, 2, 4):
+        o = Oracle(len(lw), seed=2, shards=shards)
+        c = o.col_create("x", 1)
+        o.col_upload(c, np.arange(len(lw), dtype=float))
+        o.weights_upload(lw)
+        ev0 = o.log_evidence()
+        _force_changed(o)
+        ev1 = o.log_evidence()
+        rs, _ = o.resample(1.0)
+        assert rs
+        assert abs(o.log_evidence() - ev1) < 1e-12 * abs(ev1) + 1e-12
+        anc = o.last_ancestors()
+        n = len(lw) // shards
+        for s in range(shards):                # island: ancestors stay inside the shard
+            assert np.all((anc[s * n:(s + 1) * n] >= s * n) & (anc[s * n:(s + 1) * n] < (s + 1) * n))

@@ -163,6 +163,7 @@ int wsmc_create(wsmc_ctx** out, int64_t n_particles, int32_t device, uint64_t se
     c->gN = n_particles;
     c->seed = seed;
     c->ntiles = (n_particles + kTile - 1) / kTile;
+    c->nrstiles = (n_particles + kRsTile - 1) / kRsTile;
     hipError_t e = hipSuccess;
 #define ALLOC(ptr, bytes)                                          \
     if (e == hipSuccess) e = hipMalloc((void**)&(ptr), (bytes));
@@ -170,7 +171,8 @@ int wsmc_create(wsmc_ctx** out, int64_t n_particles, int32_t device, uint64_t se
     ALLOC(c->w, sizeof(double) * c->N);
     ALLOC(c->anc, sizeof(int32_t) * c->N);
     ALLOC(c->tmp, sizeof(double) * 4 * c->N);
-    ALLOC(c->tileQ, sizeof(unsigned long long) * c->ntiles);
+    ALLOC(c->tileQ, sizeof(unsigned long long) * c->nrstiles);
+    ALLOC(c->qbuf, sizeof(unsigned long long) * c->N);
     ALLOC(c->tilepart, sizeof(double) * 16 * c->ntiles);
     ALLOC(c->rec, sizeof(ShardRec) * kMaxWorld);
     ALLOC(c->dec, sizeof(Decision));
@@ -208,7 +210,7 @@ int wsmc_destroy(wsmc_ctx* c) {
         (void)hipFree(col.front);
         (void)hipFree(col.back);
     }
-    void* bufs[] = {c->w, c->anc, c->tmp, c->tileQ, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount,
+    void* bufs[] = {c->w, c->anc, c->tmp, c->tileQ, c->qbuf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount,
                     c->d_colptr, c->run_params, c->d_tape, c->run_rec, c->run_dec, c->anc_log, c->obs,
                     c->vscratch, c->xscratch};
     for (void* p : bufs)
@@ -393,7 +395,7 @@ int wsmc_log_evidence(wsmc_ctx* c, double* out) {
     CHECK_CTX(c);
     if (!out) return fail(WSMC_EARG, "null out");
     WSMC_HIP(hipMemsetAsync(c->rec, 0, sizeof(ShardRec) * c->world, c->stream));
-    WSMC_HIP(launch_log_evidence_stats(c->stream, c->w, c->N, c->rec + c->rank, c->tileQ));
+    WSMC_HIP(launch_log_evidence_stats(c->stream, c->w, c->N, c->rec + c->rank, c->tileQ, c->qbuf));
     int r = exchange_recs(c, c->rec);
     if (r) return r;
     std::vector<ShardRec> h(c->world);
@@ -499,11 +501,11 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
     }
     WSMC_HIP(hipMemsetAsync(c->rec, 0, sizeof(ShardRec) * c->world, c->stream));
     WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, c->rec + c->rank));
-    WSMC_HIP(launch_rs_sums(c->stream, c->w, c->N, c->rec + c->rank, c->tileQ));
+    WSMC_HIP(launch_rs_sums(c->stream, c->w, c->N, c->rec + c->rank, c->tileQ, c->qbuf));
     int r = exchange_recs(c, c->rec);
     if (r) return r;
     WSMC_HIP(launch_rs_scan(c->stream, c->w, c->N, c->rec, c->world, c->rank, ess_min, scheme, c->seed, op, nullptr,
-                            c->goff, c->tileQ, c->anc, c->dec));
+                            c->goff, c->tileQ, c->qbuf, c->anc, c->dec));
     Decision* hd = reinterpret_cast<Decision*>(c->pinned);
     WSMC_HIP(hipMemcpyAsync(hd, c->dec, sizeof(Decision), hipMemcpyDeviceToHost, c->stream));
     WSMC_HIP(hipStreamSynchronize(c->stream));
@@ -721,12 +723,12 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
         WSMC_HIP(mark());
         WSMC_HIP(launch_ssm2d_propagate(c->stream, a));
         WSMC_HIP(mark());
-        WSMC_HIP(launch_rs_sums(c->stream, c->w, N, recs + c->rank, c->tileQ));
+        WSMC_HIP(launch_rs_sums(c->stream, c->w, N, recs + c->rank, c->tileQ, c->qbuf));
         WSMC_HIP(mark());
         int r = exchange_recs(c, recs);
         if (r) return r;
         WSMC_HIP(launch_rs_scan(c->stream, c->w, N, recs, c->world, c->rank, p.ess_min, p.scheme, c->seed,
-                                3ull * (uint64_t)(t - 1) + 2ull, c->run_params, c->goff, c->tileQ,
+                                3ull * (uint64_t)(t - 1) + 2ull, c->run_params, c->goff, c->tileQ, c->qbuf,
                                 c->anc_log + (size_t)(t - 1) * N, c->run_dec + t));
         WSMC_HIP(mark());
     }

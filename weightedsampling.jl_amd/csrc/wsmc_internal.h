@@ -17,13 +17,16 @@ namespace wsmc {
 constexpr int kBlock = 256;            // threads per workgroup (4 waves of 64)
 constexpr int kItems = 8;              // particles per thread in the tile kernels
 constexpr int kTile = kBlock * kItems; // 2048 particles per tile (canonical reduction tile)
-constexpr int kSlots = 8;              // per-XCD accumulator copies (blockIdx % 8)
-constexpr int kChunk = 4096;           // ancestor slots filled per LDS pass
+constexpr int kSlots = 64;             // accumulator copies, one 128-B line each (blockIdx % 64)
+constexpr int kRsItems = 4;            // particles per thread in the resample kernels
+constexpr int kRsTile = kBlock * kRsItems;  // 1024-particle resample tiles
+constexpr int kRsChunk = 2048;         // ancestor slots filled per LDS pass
 constexpr int kMaxCols = 4096;
 constexpr int kMaxShards = 8;     // one node: up to 8 GPUs
 
-// One shard's weight-statistics record. kSlots copies of each accumulator so the
-// per-block atomics spread over 8 addresses (one per XCD round-robin group).
+// One shard's weight-statistics record. kSlots copies of each accumulator, one 128-B line
+// per copy, so the per-block atomics spread over 64 lines (memory-side atomics to one line
+// serialise at ~100/us).
 // v[s][0] = ordered max, v[s][1] = sum q, v[s][2..5] = sum q^2 limbs (32 bit),
 // v[s][6..9] = sum fix96 limbs, v[s][10] = shard size (slot 0 only).
 struct ShardRec {
@@ -87,7 +90,8 @@ struct wsmc_ctx {
     // scratch
     int32_t* anc = nullptr;                 // last ancestors [N]
     double* tmp = nullptr;                  // [4N]
-    unsigned long long* tileQ = nullptr;    // [ntiles] per-tile sum q (scan offsets)
+    unsigned long long* tileQ = nullptr;    // [nrstiles] per-tile sum q (scan offsets)
+    unsigned long long* qbuf = nullptr;     // [N] integer weights q_i of the last weight-statistics pass
     double* tilepart = nullptr;             // [16 * ntiles] canonical-sum tile partials
     wsmc::ShardRec* rec = nullptr;          // [world] records of one generic resample
     wsmc::Decision* dec = nullptr;          // [1] decision of one generic resample
@@ -95,7 +99,8 @@ struct wsmc_ctx {
     int32_t* dflag = nullptr;               // [4] device error flags
     unsigned long long* ucount = nullptr;   // [4] device counters
     void* pinned = nullptr;                 // 4 KB pinned staging
-    int64_t ntiles = 0;
+    int64_t ntiles = 0;      // canonical-sum tiles (2048)
+    int64_t nrstiles = 0;    // resample tiles (1024)
 
     // fused runner state
     int32_t T_alloc = 0;
@@ -142,15 +147,15 @@ hipError_t launch_sample_importance(hipStream_t s, double* out, int dim, const w
 hipError_t launch_weigh(hipStream_t s, const wsmc_term& t, double* w, double* const* cols, int64_t N);
 hipError_t launch_rs_max(hipStream_t s, const double* w, int64_t N, ShardRec* rec);
 hipError_t launch_rs_sums(hipStream_t s, const double* w, int64_t N, ShardRec* rec,
-                          unsigned long long* tileQ);
+                          unsigned long long* tileQ, unsigned long long* qbuf);
 hipError_t launch_rs_scan(hipStream_t s, const double* w, int64_t N, const ShardRec* recs, int world,
                           int rank, double ess_min, int scheme, uint64_t seed, uint64_t op,
                           const uint64_t* op_dev, int64_t slot_base, const unsigned long long* tileQ,
-                          int32_t* anc, Decision* dec);
+                          const unsigned long long* qbuf, int32_t* anc, Decision* dec);
 hipError_t launch_gather(hipStream_t s, double* dst, const double* src, const int32_t* anc, int64_t N);
 hipError_t launch_fill_weights(hipStream_t s, double* w, const Decision* dec, int64_t N);
 hipError_t launch_log_evidence_stats(hipStream_t s, const double* w, int64_t N, ShardRec* rec,
-                                     unsigned long long* tileQ);
+                                     unsigned long long* tileQ, unsigned long long* qbuf);
 hipError_t launch_score(hipStream_t s, const wsmc_term* tape, int32_t n, int32_t depth,
                         double* const* cols, int64_t N, double* out);
 hipError_t launch_moments(hipStream_t s, const double* w, const ShardRec* rec, double* const* cols,

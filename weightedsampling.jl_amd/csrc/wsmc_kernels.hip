@@ -170,57 +170,72 @@ __global__ __launch_bounds__(kBlock) void k_rs_max(const double* __restrict__ w,
     if (threadIdx.x == 0) atomic_max_filtered(&rec->v[blockIdx.x % kSlots][0], m);
 }
 
-__device__ __forceinline__ double rec_max(const ShardRec* r) {
-    u64 m = 0;
-#pragma unroll
-    for (int s = 0; s < kSlots; ++s) m = max(m, r->v[s][0]);
-    return wsmc_ord_dec(m);
+// slot reductions by one wave: lane l owns slot l (kSlots == 64)
+static_assert(kSlots == 64, "one lane per accumulator slot");
+__device__ __forceinline__ u64 wave_rec_max_enc(const ShardRec* r) {
+    return wave_max_u64(r->v[threadIdx.x & 63][0]);
 }
-
-__device__ __forceinline__ wsmc_shard_stats rec_stats(const ShardRec* r) {
-    wsmc_shard_stats st;
-    u64 m = 0, Q = 0, l[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int s = 0; s < kSlots; ++s) {
-        m = max(m, r->v[s][0]);
-        Q += r->v[s][1];
-        for (int k = 0; k < 8; ++k) l[k] += r->v[s][2 + k];
+// block-uniform max of the record (all threads); uses one wave + LDS
+__device__ __forceinline__ double block_rec_max(const ShardRec* r, u64* lds1) {
+    if (threadIdx.x < 64) {
+        const u64 m = wave_rec_max_enc(r);
+        if (threadIdx.x == 0) lds1[0] = m;
     }
-    st.M = wsmc_ord_dec(m);
-    st.Q = Q;
-    st.Q2 = (wsmc_u128)l[0] + ((wsmc_u128)l[1] << 32) + ((wsmc_u128)l[2] << 64) + ((wsmc_u128)l[3] << 96);
-    st.W = (wsmc_u128)l[4] + ((wsmc_u128)l[5] << 32) + ((wsmc_u128)l[6] << 64) + ((wsmc_u128)l[7] << 96);
+    __syncthreads();
+    const double M = wsmc_ord_dec(lds1[0]);
+    __syncthreads();
+    return M;
+}
+// full shard statistics, computed by one wave (every lane returns the same value)
+__device__ __forceinline__ wsmc_shard_stats wave_rec_stats(const ShardRec* r) {
+    const int l = threadIdx.x & 63;
+    wsmc_shard_stats st;
+    st.M = wsmc_ord_dec(wave_max_u64(r->v[l][0]));
+    st.Q = wave_sum_u64(r->v[l][1]);
+    u64 lim[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) lim[k] = wave_sum_u64(r->v[l][2 + k]);
+    st.Q2 = (wsmc_u128)lim[0] + ((wsmc_u128)lim[1] << 32) + ((wsmc_u128)lim[2] << 64) + ((wsmc_u128)lim[3] << 96);
+    st.W = (wsmc_u128)lim[4] + ((wsmc_u128)lim[5] << 32) + ((wsmc_u128)lim[6] << 64) + ((wsmc_u128)lim[7] << 96);
     st.n = r->v[0][10];
     return st;
 }
 
-// one tile per block, striped items (coalesced): sum q, sum q^2 (4 x 32-bit limbs),
-// sum fix96(e) (4 limbs). Per-tile sum q -> tileQ (scan offsets).
+// one resample tile (1024 particles) per block, striped items (coalesced): sum q,
+// sum q^2 (4 x 32-bit limbs), sum fix96(e) (4 limbs) into the shard record (atomics spread
+// over kSlots copies); the tile's sum q -> tileQ (scan offsets).
 __global__ __launch_bounds__(kBlock) void k_rs_sums(const double* __restrict__ w, int64_t N, ShardRec* rec,
-                                                    u64* __restrict__ tileQ) {
+                                                    u64* __restrict__ tileQ, u64* __restrict__ qbuf) {
     __shared__ u64 lds[4][9];
-    const double M = rec_max(rec);
+    __shared__ u64 s_m[1];
+    const int64_t base = (int64_t)blockIdx.x * kRsTile;
+    double lw[kRsItems];
+#pragma unroll
+    for (int j = 0; j < kRsItems; ++j) {
+        const int64_t i = base + (int64_t)j * kBlock + threadIdx.x;
+        lw[j] = i < N ? w[i] : -WSMC_INF;
+    }
+    const double M = block_rec_max(rec, s_m);
     const int K = wsmc_qbits((uint64_t)N);
     const double scale = wsmc_pow2i(K);
-    const int64_t base = (int64_t)blockIdx.x * kTile;
     u64 acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int j = 0; j < kItems; ++j) {
+    for (int j = 0; j < kRsItems; ++j) {
+        const double e = wsmc_exp(lw[j] - M);
+        const u64 q = (e > 0.0) ? (u64)wsmc_d_to_u64_trunc(e * scale) : 0ull;
         const int64_t i = base + (int64_t)j * kBlock + threadIdx.x;
-        if (i < N) {
-            const double e = wsmc_exp(w[i] - M);
-            const u64 q = (e > 0.0) ? (u64)wsmc_d_to_u64_trunc(e * scale) : 0ull;
-            const wsmc_u128 q2 = (wsmc_u128)q * q;
-            const wsmc_u128 f = wsmc_fix96(e);
-            acc[0] += q;
-            acc[1] += (uint32_t)q2;
-            acc[2] += (uint32_t)(q2 >> 32);
-            acc[3] += (uint32_t)(q2 >> 64);
-            acc[4] += (uint32_t)(q2 >> 96);
-            acc[5] += (uint32_t)f;
-            acc[6] += (uint32_t)(f >> 32);
-            acc[7] += (uint32_t)(f >> 64);
-            acc[8] += (uint32_t)(f >> 96);
-        }
+        if (i < N) qbuf[i] = q;
+        const wsmc_u128 q2 = (wsmc_u128)q * q;
+        const wsmc_u128 f = wsmc_fix96(e);
+        acc[0] += q;
+        acc[1] += (uint32_t)q2;
+        acc[2] += (uint32_t)(q2 >> 32);
+        acc[3] += (uint32_t)(q2 >> 64);
+        acc[4] += (uint32_t)(q2 >> 96);
+        acc[5] += (uint32_t)f;
+        acc[6] += (uint32_t)(f >> 32);
+        acc[7] += (uint32_t)(f >> 64);
+        acc[8] += (uint32_t)(f >> 96);
     }
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
@@ -237,6 +252,35 @@ __global__ __launch_bounds__(kBlock) void k_rs_sums(const double* __restrict__ w
     if (blockIdx.x == 0 && threadIdx.x == 0) rec->v[0][10] = (u64)N;
 }
 
+// Global Resample decision from the shard records (rank order), the same arithmetic as
+// wsmc_global_ess / wsmc_shard_mean. Called by all 64 lanes of one wave.
+__device__ void decide(const ShardRec* recs, int world, int rank, double ess_min, double* ess_out,
+                       int* rs_out, wsmc_shard_stats* mine) {
+    double M = -WSMC_INF;
+    uint64_t N = 0;
+    int nan = 0;
+    for (int g = 0; g < world; ++g) {
+        const double Mg = wsmc_ord_dec(wave_rec_max_enc(&recs[g]));
+        if (wsmc_isnan(Mg)) nan = 1;
+        else if (Mg > M) M = Mg;
+        N += recs[g].v[0][10];
+    }
+    if (nan) M = WSMC_NAN;
+    double sq = 0.0, sq2 = 0.0;
+    for (int g = 0; g < world; ++g) {
+        const wsmc_shard_stats st = wave_rec_stats(&recs[g]);
+        const double f = wsmc_exp(st.M - M);
+        const double sc = wsmc_pow2i(-wsmc_qbits(st.n));
+        const double qd = wsmc_u64_to_d(st.Q), q2d = wsmc_u128_to_d(st.Q2);
+        sq = sq + (qd * sc) * f;
+        sq2 = sq2 + ((q2d * sc) * sc) * (f * f);
+        if (g == rank) *mine = st;
+    }
+    const double ess = (sq * sq) / (wsmc_u64_to_d(N) * sq2);
+    *ess_out = ess;
+    *rs_out = ess < ess_min;
+}
+
 // Decision + inclusive integer CDF + ancestor fill for one tile.
 // ancestor(slot) = smallest m with C_m > x_slot (src/resampling.jl:13-26); particle m owns
 // slots [rank(C_{m-1}), rank(C_m)) and the block fills its contiguous slot range through
@@ -246,26 +290,37 @@ __global__ __launch_bounds__(kBlock) void k_rs_scan(const double* __restrict__ w
                                                     double ess_min, int scheme, uint64_t seed,
                                                     uint64_t op, const uint64_t* op_dev,
                                                     int64_t slot_base, const u64* __restrict__ tileQ,
+                                                    const u64* __restrict__ qbuf,
                                                     int32_t* __restrict__ anc, Decision* dec) {
     __shared__ u64 s_u4[4];
     __shared__ int s_i4[4];
     __shared__ u64 s_hi[kBlock];
-    __shared__ int marks[kChunk];
-    __shared__ double s_dec[4];     // M, resample flag, Q, K
-    __shared__ u64 s_Q;
+    __shared__ int marks[kRsChunk];
+    __shared__ u64 s_Q, s_L;
+    __shared__ int s_rs;
     const int th = threadIdx.x;
-    const uint64_t opx = op_eff(op, op_dev);
+    const int64_t base = (int64_t)blockIdx.x * kRsTile;
 
-    if (th == 0) {
-        wsmc_shard_stats st[kMaxShards];
-        for (int g = 0; g < world && g < kMaxShards; ++g) st[g] = rec_stats(&recs[g]);
-        const double ess = wsmc_global_ess(st, world);
-        const int rs = ess < ess_min;
-        const wsmc_shard_stats& me = st[rank];
-        s_dec[0] = me.M;
-        s_dec[1] = rs ? 1.0 : 0.0;
-        s_Q = me.Q;
-        if (blockIdx.x == 0) {
+    // issue this tile's loads and the offset loads before the decision
+    u64 q[kRsItems];
+#pragma unroll
+    for (int j = 0; j < kRsItems; ++j) {
+        const int64_t i = base + (int64_t)th * kRsItems + j;
+        q[j] = i < N ? qbuf[i] : 0ull;
+    }
+    u64 part = 0;
+    for (int64_t b = th; b < (int64_t)blockIdx.x; b += kBlock) part += tileQ[b];
+
+    if (th < 64) {
+        double ess;
+        int rs;
+        wsmc_shard_stats me;
+        decide(recs, world, rank, ess_min, &ess, &rs, &me);
+        if (th == 0) {
+            s_Q = me.Q;
+            s_rs = rs;
+        }
+        if (blockIdx.x == 0 && th == 0) {
             dec->resampled = rs;
             dec->ess = ess;
             dec->M = me.M;
@@ -273,64 +328,47 @@ __global__ __launch_bounds__(kBlock) void k_rs_scan(const double* __restrict__ w
         }
     }
     __syncthreads();
-    if (s_dec[1] == 0.0) return;
-    const double M = s_dec[0];
+    if (!s_rs) return;
+    const uint64_t opx = op_eff(op, op_dev);
     const u64 Q = s_Q;
-    const int K = wsmc_qbits((uint64_t)N);
-    const double scale = wsmc_pow2i(K);
-    const int64_t base = (int64_t)blockIdx.x * kTile;
-
-    // tile offset = sum of the previous tiles' q totals
-    u64 part = 0;
-    for (int64_t b = th; b < (int64_t)blockIdx.x; b += kBlock) part += tileQ[b];
+    const double ratio = wsmc_u64_to_d((uint64_t)N) / wsmc_u64_to_d(Q);
     const u64 off = block_sum_u64(part, s_u4);
 
-    // blocked items: thread th owns particles base + th*8 .. +7
-    u64 q[kItems];
+    // blocked items: thread th owns particles base + th*4 .. +3
     u64 tsum = 0;
 #pragma unroll
-    for (int j = 0; j < kItems; ++j) {
-        const int64_t i = base + (int64_t)th * kItems + j;
-        u64 qq = 0;
-        if (i < N) {
-            const double e = wsmc_exp(w[i] - M);
-            qq = (e > 0.0) ? (u64)wsmc_d_to_u64_trunc(e * scale) : 0ull;
-        }
-        q[j] = qq;
-        tsum += qq;
-    }
+    for (int j = 0; j < kRsItems; ++j) tsum += q[j];
     u64 tot;
     const u64 pre = block_excl_scan_u64(tsum, s_u4, &tot);
     // hi_j = rank(C_j); lo_0 = rank(C_{-1})
-    u64 hi[kItems];
+    u64 hi[kRsItems];
     u64 C = off + pre;
-    const u64 lo0 = wsmc_rank(C, Q, (uint64_t)N, scheme, seed, opx, (uint64_t)slot_base);
+    const u64 lo0 = wsmc_rank_r(C, Q, (uint64_t)N, ratio, scheme, seed, opx, (uint64_t)slot_base);
     u64 prev = lo0;
 #pragma unroll
-    for (int j = 0; j < kItems; ++j) {
+    for (int j = 0; j < kRsItems; ++j) {
         C += q[j];
-        hi[j] = q[j] ? wsmc_rank(C, Q, (uint64_t)N, scheme, seed, opx, (uint64_t)slot_base) : prev;
+        hi[j] = q[j] ? wsmc_rank_r(C, Q, (uint64_t)N, ratio, scheme, seed, opx, (uint64_t)slot_base) : prev;
         prev = hi[j];
     }
-    __shared__ u64 s_L;
-    s_hi[th] = hi[kItems - 1];
+    s_hi[th] = hi[kRsItems - 1];
     if (th == 0) s_L = lo0;
     __syncthreads();
     const u64 Ls = s_L, H = s_hi[kBlock - 1];
 
     int carry = -1;
-    for (u64 cb = Ls; cb < H; cb += kChunk) {
+    constexpr int PT = kRsChunk / kBlock;   // slots per thread per chunk
+    for (u64 cb = Ls; cb < H; cb += kRsChunk) {
 #pragma unroll
-        for (int k = 0; k < kChunk / kBlock; ++k) marks[k * kBlock + th] = -1;
+        for (int k = 0; k < PT; ++k) marks[k * kBlock + th] = -1;
         __syncthreads();
         u64 lo = lo0;
 #pragma unroll
-        for (int j = 0; j < kItems; ++j) {
-            if (lo < hi[j] && lo >= cb && lo < cb + kChunk) marks[lo - cb] = th * kItems + j;
+        for (int j = 0; j < kRsItems; ++j) {
+            if (lo < hi[j] && lo >= cb && lo < cb + kRsChunk) marks[lo - cb] = th * kRsItems + j;
             lo = hi[j];
         }
         __syncthreads();
-        constexpr int PT = kChunk / kBlock;   // 16 slots per thread
         int run[PT];
         int m = -1;
 #pragma unroll
@@ -390,7 +428,8 @@ __global__ __launch_bounds__(kBlock) void k_moments(const double* __restrict__ w
                                                     const double* mom, int64_t N, int64_t ntiles,
                                                     double* tilepart) {
     __shared__ double lds4[4];
-    const double M = rec_max(rec);
+    __shared__ u64 s_m[1];
+    const double M = block_rec_max(rec, s_m);
     const int64_t base = (int64_t)blockIdx.x * kTile;
     double acc[10];
     const int nv = pass == 1 ? 1 + d : d * (d + 1) / 2;
@@ -617,6 +656,7 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_final(Ssm2dFinal f) {
 // ------------------------------------------------------------------------------------
 static inline dim3 grid_for(int64_t N) { return dim3((unsigned)((N + kBlock - 1) / kBlock)); }
 static inline dim3 tiles_for(int64_t N) { return dim3((unsigned)((N + kTile - 1) / kTile)); }
+static inline dim3 rs_tiles_for(int64_t N) { return dim3((unsigned)((N + kRsTile - 1) / kRsTile)); }
 
 hipError_t launch_assign(hipStream_t s, double* out, int dim, const wsmc_operand* expr,
                          double* const* cols, int64_t N) {
@@ -648,15 +688,15 @@ hipError_t launch_rs_max(hipStream_t s, const double* w, int64_t N, ShardRec* re
     hipLaunchKernelGGL(k_rs_max, dim3((unsigned)nb), dim3(kBlock), 0, s, w, N, rec);
     return hipGetLastError();
 }
-hipError_t launch_rs_sums(hipStream_t s, const double* w, int64_t N, ShardRec* rec, u64* tileQ) {
-    hipLaunchKernelGGL(k_rs_sums, tiles_for(N), dim3(kBlock), 0, s, w, N, rec, tileQ);
+hipError_t launch_rs_sums(hipStream_t s, const double* w, int64_t N, ShardRec* rec, u64* tileQ, u64* qbuf) {
+    hipLaunchKernelGGL(k_rs_sums, rs_tiles_for(N), dim3(kBlock), 0, s, w, N, rec, tileQ, qbuf);
     return hipGetLastError();
 }
 hipError_t launch_rs_scan(hipStream_t s, const double* w, int64_t N, const ShardRec* recs, int world, int rank,
                           double ess_min, int scheme, uint64_t seed, uint64_t op, const uint64_t* op_dev,
-                          int64_t slot_base, const u64* tileQ, int32_t* anc, Decision* dec) {
-    hipLaunchKernelGGL(k_rs_scan, tiles_for(N), dim3(kBlock), 0, s, w, N, recs, world, rank, ess_min, scheme,
-                       seed, op, op_dev, slot_base, tileQ, anc, dec);
+                          int64_t slot_base, const u64* tileQ, const u64* qbuf, int32_t* anc, Decision* dec) {
+    hipLaunchKernelGGL(k_rs_scan, rs_tiles_for(N), dim3(kBlock), 0, s, w, N, recs, world, rank, ess_min, scheme,
+                       seed, op, op_dev, slot_base, tileQ, qbuf, anc, dec);
     return hipGetLastError();
 }
 hipError_t launch_gather(hipStream_t s, double* dst, const double* src, const int32_t* anc, int64_t N) {
@@ -667,10 +707,11 @@ hipError_t launch_fill_weights(hipStream_t s, double* w, const Decision* dec, in
     hipLaunchKernelGGL(k_fill_weights, grid_for(N), dim3(kBlock), 0, s, w, dec, N);
     return hipGetLastError();
 }
-hipError_t launch_log_evidence_stats(hipStream_t s, const double* w, int64_t N, ShardRec* rec, u64* tileQ) {
+hipError_t launch_log_evidence_stats(hipStream_t s, const double* w, int64_t N, ShardRec* rec, u64* tileQ,
+                                     u64* qbuf) {
     hipError_t e = launch_rs_max(s, w, N, rec);
     if (e != hipSuccess) return e;
-    return launch_rs_sums(s, w, N, rec, tileQ);
+    return launch_rs_sums(s, w, N, rec, tileQ, qbuf);
 }
 hipError_t launch_score(hipStream_t s, const wsmc_term* tape, int32_t n, int32_t depth, double* const* cols,
                         int64_t N, double* out) {
