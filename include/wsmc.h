@@ -210,6 +210,12 @@ typedef struct {
 int wsmc_run_set_timing(wsmc_ctx* ctx, int32_t enabled);
 int wsmc_run_get_timing(wsmc_ctx* ctx, wsmc_run_timing* out);
 
+/* ---- diagnostics ---------------------------------------------------------------
+ * Average time (us) of `iters` back-to-back launches of one resample kernel on the
+ * context's current weights: kernel 0 = weight statistics, 1 = reduce, 2 = ancestor scan;
+ * mode 0 = production variant, > 0 = ablations (see csrc/wsmc_kernels.hip).        */
+int wsmc_debug_kernel_bench(wsmc_ctx* ctx, int32_t kernel, int32_t mode, int32_t iters, double* avg_us);
+
 #ifdef __cplusplus
 }
 #endif

@@ -115,3 +115,62 @@ def test_score_fold_depths(gpu_available):
     models.oscillator_statements(o, t, y, sweeps=0)
     for d in (0, 1, 3, 5, 7, 100):
         np.testing.assert_array_equal(g.score(d), o.score(d))
+
+
+def _skewed_weights(kind, N, rng):
+    if kind == "dominant":        # one particle takes (almost) every slot: N / 2048 fill tasks on one tile
+        w = np.full(N, -800.0)
+        w[(N * 2) // 3] = 0.0
+    elif kind == "two_tiles":     # two dominant particles in different tiles
+        w = np.full(N, -50.0)
+        w[min(1, N - 1)] = 0.0
+        w[N - 1] = math.log(3.0)
+    elif kind == "many_heavy":    # > 256 heavy tiles (the reduce kernel's queue overflows)
+        w = np.full(N, -800.0)
+        w[np.arange(0, N, 10 * 1024)[:300]] = 0.0
+    elif kind == "heavy_tail":
+        w = 6.0 * rng.standard_normal(N)
+    elif kind == "zeros":         # most particles have zero weight (-inf log-weight)
+        w = np.full(N, -np.inf)
+        w[rng.choice(N, size=max(1, N // 50), replace=False)] = rng.standard_normal(max(1, N // 50))
+    else:                         # flat: every particle one slot
+        w = np.zeros(N)
+    return w
+
+
+@pytest.mark.parametrize("N", [1, 5, 1023, 1025, 70001])
+@pytest.mark.parametrize("kind", ["dominant", "two_tiles", "heavy_tail", "zeros", "flat"])
+@pytest.mark.parametrize("scheme", [abi.RESAMPLE_STRATIFIED, abi.RESAMPLE_SYSTEMATIC])
+def test_resample_skewed_weights(gpu_available, N, kind, scheme):
+    """Ancestor fill under weight skew (balanced fill tasks, src/resampling.jl:13-26)."""
+    w = _skewed_weights(kind, N, np.random.default_rng(N))
+    g, o = wsmc.Context(N, seed=5), Oracle(N, seed=5)
+    from wsmc.dsl import Normal
+    for c in (g, o):
+        c.col_create("x")
+        c.assign(c.col_find("x"), abi.Operand.const(1.0))
+        c.weights_upload(w)
+        # a constant Weight marks the weights changed (uploading them does not; src/transformers.jl:232)
+        c.weight(Normal(0.0, 1.0).dist(c.col_find), [abi.Operand.const(0.0)])
+    assert g.log_evidence() == o.log_evidence()
+    rg, ro = g.resample(2.0, scheme), o.resample(2.0, scheme)
+    assert rg == ro and rg[0]
+    a = g.last_ancestors()
+    np.testing.assert_array_equal(a, o.last_ancestors())
+    assert np.all(np.diff(a) >= 0) and a.min() >= 0 and a.max() < N
+    assert_same_state(g, o)
+
+
+@pytest.mark.parametrize("kind", ["dominant", "many_heavy", "heavy_tail"])
+def test_resample_skewed_large(gpu_available, kind):
+    """> 1024 tiles (several per reduce thread) and > 256 heavy tiles."""
+    N = 3_100_003
+    w = _skewed_weights(kind, N, np.random.default_rng(7))
+    g, o = wsmc.Context(N, seed=8), Oracle(N, seed=8)
+    from wsmc.dsl import Normal
+    for c in (g, o):
+        c.weights_upload(w)
+        c.weight(Normal(0.0, 1.0).dist(c.col_find), [abi.Operand.const(0.0)])
+    assert g.resample(2.0) == o.resample(2.0)
+    np.testing.assert_array_equal(g.last_ancestors(), o.last_ancestors())
+    np.testing.assert_array_equal(g.weights_download(), o.weights_download())

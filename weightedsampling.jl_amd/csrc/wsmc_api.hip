@@ -118,19 +118,13 @@ static int gather_all_columns(wsmc_ctx* c) {
     return WSMC_OK;
 }
 
-static wsmc_shard_stats host_rec_stats(const ShardRec& r) {
+static wsmc_shard_stats host_record_stats(const ShardRecord& r) {
     wsmc_shard_stats st;
-    unsigned long long m = 0, Q = 0, l[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int s = 0; s < kSlots; ++s) {
-        m = std::max(m, r.v[s][0]);
-        Q += r.v[s][1];
-        for (int k = 0; k < 8; ++k) l[k] += r.v[s][2 + k];
-    }
-    st.M = wsmc_ord_dec(m);
-    st.Q = Q;
-    st.Q2 = (wsmc_u128)l[0] + ((wsmc_u128)l[1] << 32) + ((wsmc_u128)l[2] << 64) + ((wsmc_u128)l[3] << 96);
-    st.W = (wsmc_u128)l[4] + ((wsmc_u128)l[5] << 32) + ((wsmc_u128)l[6] << 64) + ((wsmc_u128)l[7] << 96);
-    st.n = r.v[0][10];
+    st.M = wsmc_ord_dec(r.menc);
+    st.Q = r.Q;
+    st.Q2 = ((wsmc_u128)r.q2hi << 64) | r.q2lo;
+    st.W = ((wsmc_u128)r.whi << 64) | r.wlo;
+    st.n = r.n;
     return st;
 }
 
@@ -171,10 +165,15 @@ int wsmc_create(wsmc_ctx** out, int64_t n_particles, int32_t device, uint64_t se
     ALLOC(c->w, sizeof(double) * c->N);
     ALLOC(c->anc, sizeof(int32_t) * c->N);
     ALLOC(c->tmp, sizeof(double) * 4 * c->N);
-    ALLOC(c->tileQ, sizeof(unsigned long long) * c->nrstiles);
+    ALLOC(c->tilep, sizeof(unsigned long long) * kPart * c->nrstiles);
+    ALLOC(c->tileOff, sizeof(unsigned long long) * c->nrstiles);
+    ALLOC(c->tileL, sizeof(unsigned long long) * (c->nrstiles + 1));
+    ALLOC(c->taskOff, sizeof(int32_t) * c->nrstiles);
+    ALLOC(c->taskTile, sizeof(int32_t) * (c->nrstiles + n_particles / kRsChunk + 1));
+    ALLOC(c->mslots, sizeof(MaxSlots));
     ALLOC(c->qbuf, sizeof(unsigned long long) * c->N);
     ALLOC(c->tilepart, sizeof(double) * 16 * c->ntiles);
-    ALLOC(c->rec, sizeof(ShardRec) * kMaxWorld);
+    ALLOC(c->rec, sizeof(ShardRecord) * kMaxWorld);
     ALLOC(c->dec, sizeof(Decision));
     ALLOC(c->mom, sizeof(double) * 64);
     ALLOC(c->dflag, sizeof(int32_t) * 4);
@@ -210,8 +209,8 @@ int wsmc_destroy(wsmc_ctx* c) {
         (void)hipFree(col.front);
         (void)hipFree(col.back);
     }
-    void* bufs[] = {c->w, c->anc, c->tmp, c->tileQ, c->qbuf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount,
-                    c->d_colptr, c->run_params, c->d_tape, c->run_rec, c->run_dec, c->anc_log, c->obs,
+    void* bufs[] = {c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->tileL, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount,
+                    c->d_colptr, c->run_params, c->d_tape, c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs,
                     c->vscratch, c->xscratch};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
@@ -383,9 +382,41 @@ int wsmc_weights_download(wsmc_ctx* c, double* host) {
     return WSMC_OK;
 }
 
-static int exchange_recs(wsmc_ctx* c, ShardRec* recs) {
+static int exchange_recs(wsmc_ctx* c, ShardRecord* recs);
+// max (unless the caller's kernel already filled the slots), sums, reduce, [exchange + decide]
+static FillPlan fill_plan(wsmc_ctx* c, int scheme, uint64_t op, const uint64_t* op_dev) {
+    FillPlan p;
+    p.tileL = c->tileL;
+    p.taskOff = c->taskOff;
+    p.taskTile = c->taskTile;
+    p.scheme = scheme;
+    p.seed = c->seed;
+    p.op = op;
+    p.op_dev = op_dev;
+    p.slot_base = c->goff;
+    return p;
+}
+
+static int enqueue_resample_stats(wsmc_ctx* c, const double* w, MaxSlots* ms, ShardRecord* recs, double ess_min,
+                                  Decision* dec, bool run_max, const FillPlan& plan, hipEvent_t* ev = nullptr) {
+    if (run_max) {
+        WSMC_HIP(hipMemsetAsync(ms, 0, sizeof(MaxSlots), c->stream));
+        WSMC_HIP(launch_rs_max(c->stream, w, c->N, ms));
+    }
+    WSMC_HIP(launch_rs_sums(c->stream, w, c->N, ms, c->tilep, c->qbuf, ev ? ev[0] : nullptr, ev ? ev[1] : nullptr));
+    WSMC_HIP(launch_rs_reduce(c->stream, ms, c->tilep, c->N, c->tileOff, recs + c->rank, c->world == 1, ess_min, dec,
+                              &plan, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr));
     if (c->world > 1) {
-        const size_t cnt = sizeof(ShardRec) / sizeof(unsigned long long);
+        int r = exchange_recs(c, recs);
+        if (r) return r;
+        WSMC_HIP(launch_rs_decide(c->stream, recs, c->world, c->rank, ess_min, dec));
+    }
+    return WSMC_OK;
+}
+
+static int exchange_recs(wsmc_ctx* c, ShardRecord* recs) {
+    if (c->world > 1) {
+        const size_t cnt = sizeof(ShardRecord) / sizeof(unsigned long long);
         WSMC_RCCL(ncclAllGather(recs + c->rank, recs, cnt, ncclUint64, c->comm, c->stream));
     }
     return WSMC_OK;
@@ -394,15 +425,16 @@ static int exchange_recs(wsmc_ctx* c, ShardRec* recs) {
 int wsmc_log_evidence(wsmc_ctx* c, double* out) {
     CHECK_CTX(c);
     if (!out) return fail(WSMC_EARG, "null out");
-    WSMC_HIP(hipMemsetAsync(c->rec, 0, sizeof(ShardRec) * c->world, c->stream));
-    WSMC_HIP(launch_log_evidence_stats(c->stream, c->w, c->N, c->rec + c->rank, c->tileQ, c->qbuf));
+    WSMC_HIP(hipMemsetAsync(c->mslots, 0, sizeof(MaxSlots), c->stream));
+    WSMC_HIP(launch_log_evidence_stats(c->stream, c->w, c->N, c->mslots, c->tilep, c->qbuf, c->tileOff,
+                                       c->rec + c->rank));
     int r = exchange_recs(c, c->rec);
     if (r) return r;
-    std::vector<ShardRec> h(c->world);
-    WSMC_HIP(hipMemcpyAsync(h.data(), c->rec, sizeof(ShardRec) * c->world, hipMemcpyDeviceToHost, c->stream));
+    std::vector<ShardRecord> h(c->world);
+    WSMC_HIP(hipMemcpyAsync(h.data(), c->rec, sizeof(ShardRecord) * c->world, hipMemcpyDeviceToHost, c->stream));
     WSMC_HIP(hipStreamSynchronize(c->stream));
     wsmc_shard_stats st[kMaxWorld];
-    for (int g = 0; g < c->world; ++g) st[g] = host_rec_stats(h[g]);
+    for (int g = 0; g < c->world; ++g) st[g] = host_record_stats(h[g]);
     *out = wsmc_global_log_evidence(st, c->world);
     return WSMC_OK;
 }
@@ -499,13 +531,10 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
         if (ess_out) *ess_out = c->last_ess;
         return WSMC_OK;
     }
-    WSMC_HIP(hipMemsetAsync(c->rec, 0, sizeof(ShardRec) * c->world, c->stream));
-    WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, c->rec + c->rank));
-    WSMC_HIP(launch_rs_sums(c->stream, c->w, c->N, c->rec + c->rank, c->tileQ, c->qbuf));
-    int r = exchange_recs(c, c->rec);
+    const FillPlan plan = fill_plan(c, scheme, op, nullptr);
+    int r = enqueue_resample_stats(c, c->w, c->mslots, c->rec, ess_min, c->dec, true, plan);
     if (r) return r;
-    WSMC_HIP(launch_rs_scan(c->stream, c->w, c->N, c->rec, c->world, c->rank, ess_min, scheme, c->seed, op, nullptr,
-                            c->goff, c->tileQ, c->qbuf, c->anc, c->dec));
+    WSMC_HIP(launch_rs_scan(c->stream, c->N, c->rec + c->rank, c->dec, plan, c->tileOff, c->qbuf, c->anc));
     Decision* hd = reinterpret_cast<Decision*>(c->pinned);
     WSMC_HIP(hipMemcpyAsync(hd, c->dec, sizeof(Decision), hipMemcpyDeviceToHost, c->stream));
     WSMC_HIP(hipStreamSynchronize(c->stream));
@@ -612,14 +641,14 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
     WSMC_HIP(hipMemsetAsync(c->dflag, 0, sizeof(int32_t) * 4, c->stream));
     WSMC_HIP(hipMemsetAsync(c->ucount, 0, sizeof(unsigned long long) * 4, c->stream));
     if (proposal == WSMC_PROPOSAL_AUTORW) {
-        WSMC_HIP(hipMemsetAsync(c->rec, 0, sizeof(ShardRec), c->stream));
-        WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, c->rec));
+        WSMC_HIP(hipMemsetAsync(c->mslots, 0, sizeof(MaxSlots), c->stream));
+        WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, c->mslots));
         const double* lp = bounded ? l : nullptr;
         const double* hp = bounded ? h : nullptr;
-        WSMC_HIP(launch_moments(c->stream, c->w, c->rec, c->d_colptr, targets, d, lp, hp, 1, c->mom, c->N,
+        WSMC_HIP(launch_moments(c->stream, c->w, c->mslots, c->d_colptr, targets, d, lp, hp, 1, c->mom, c->N,
                                 c->tilepart));
         WSMC_HIP(launch_moments_final(c->stream, c->tilepart, c->ntiles, d, 1, step, c->mom, c->dflag));
-        WSMC_HIP(launch_moments(c->stream, c->w, c->rec, c->d_colptr, targets, d, lp, hp, 2, c->mom, c->N,
+        WSMC_HIP(launch_moments(c->stream, c->w, c->mslots, c->d_colptr, targets, d, lp, hp, 2, c->mom, c->N,
                                 c->tilepart));
         WSMC_HIP(launch_moments_final(c->stream, c->tilepart, c->ntiles, d, 2, step, c->mom, c->dflag));
     } else {
@@ -648,10 +677,11 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
 static int ensure_run_buffers(wsmc_ctx* c, int32_t T) {
     if (c->T_alloc >= T && c->run_rec) return WSMC_OK;
     WSMC_HIP(hipStreamSynchronize(c->stream));
-    void* old[] = {c->run_rec, c->run_dec, c->anc_log, c->obs};
+    void* old[] = {c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs};
     for (void* p : old)
         if (p) WSMC_HIP(hipFree(p));
-    WSMC_HIP(hipMalloc(&c->run_rec, sizeof(ShardRec) * (T + 1) * kMaxWorld));
+    WSMC_HIP(hipMalloc(&c->run_max, sizeof(MaxSlots) * (T + 1)));
+    WSMC_HIP(hipMalloc(&c->run_rec, sizeof(ShardRecord) * (T + 1) * kMaxWorld));
     WSMC_HIP(hipMalloc(&c->run_dec, sizeof(Decision) * (T + 1)));
     WSMC_HIP(hipMalloc(&c->anc_log, sizeof(int32_t) * (size_t)T * c->N));
     WSMC_HIP(hipMalloc(&c->obs, sizeof(double) * 2 * (T + 1)));
@@ -677,17 +707,15 @@ struct RunPlan {
     double** d_hist_out = nullptr;
 };
 
+// events (timing mode): per step 8 = {prop, sums, reduce, scan} x {start, stop} bound to the
+// dispatches themselves (hipExtLaunchKernelGGL), then 2 for the finalize kernel
 static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEvent_t>* ev) {
     const int T = p.T;
     const int64_t N = c->N;
     const double r_var = p.r_var;
     const double cpre = 2.0 * WSMC_LOG2PI + 2.0 * wsmc_log(r_var);
-    int evk = 0;
-    auto mark = [&]() -> hipError_t {
-        if (!ev) return hipSuccess;
-        return hipEventRecord((*ev)[evk++], c->stream);
-    };
-    WSMC_HIP(hipMemsetAsync(c->run_rec, 0, sizeof(ShardRec) * (T + 1) * c->world, c->stream));
+    auto E = [&](int k) -> hipEvent_t { return ev ? (*ev)[k] : nullptr; };
+    WSMC_HIP(hipMemsetAsync(c->run_max, 0, sizeof(MaxSlots) * (T + 1), c->stream));
     WSMC_HIP(hipMemsetAsync(c->run_dec, 0, sizeof(Decision) * (T + 1), c->stream));
     double* vbuf[2] = {c->cols[p.colv].back, c->vscratch};
     double* xbuf[2] = {p.keep ? nullptr : c->cols[p.colx].back, c->xscratch};
@@ -718,19 +746,18 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
         a.w = c->w;
         a.anc_prev = t > 1 ? c->anc_log + (size_t)(t - 2) * N : nullptr;
         a.dec_prev = t > 1 ? c->run_dec + (t - 1) : nullptr;
-        ShardRec* recs = c->run_rec + (size_t)t * c->world;
-        a.rec = recs + c->rank;
-        WSMC_HIP(mark());
-        WSMC_HIP(launch_ssm2d_propagate(c->stream, a));
-        WSMC_HIP(mark());
-        WSMC_HIP(launch_rs_sums(c->stream, c->w, N, recs + c->rank, c->tileQ, c->qbuf));
-        WSMC_HIP(mark());
-        int r = exchange_recs(c, recs);
+        MaxSlots* ms = c->run_max + t;
+        ShardRecord* recs = c->run_rec + (size_t)t * c->world;
+        a.ms = ms;
+        const int k0 = 8 * (t - 1);
+        WSMC_HIP(launch_ssm2d_propagate(c->stream, a, E(k0), E(k0 + 1)));
+        hipEvent_t evs[4] = {E(k0 + 2), E(k0 + 3), E(k0 + 4), E(k0 + 5)};
+        const FillPlan plan = fill_plan(c, p.scheme, 3ull * (uint64_t)(t - 1) + 2ull, c->run_params);
+        int r = enqueue_resample_stats(c, c->w, ms, recs, p.ess_min, c->run_dec + t, false, plan,
+                                       ev ? evs : nullptr);
         if (r) return r;
-        WSMC_HIP(launch_rs_scan(c->stream, c->w, N, recs, c->world, c->rank, p.ess_min, p.scheme, c->seed,
-                                3ull * (uint64_t)(t - 1) + 2ull, c->run_params, c->goff, c->tileQ, c->qbuf,
-                                c->anc_log + (size_t)(t - 1) * N, c->run_dec + t));
-        WSMC_HIP(mark());
+        WSMC_HIP(launch_rs_scan(c->stream, N, recs + c->rank, c->run_dec + t, plan, c->tileOff, c->qbuf,
+                                c->anc_log + (size_t)(t - 1) * N, E(k0 + 6), E(k0 + 7)));
     }
     Ssm2dFinal f;
     f.T = T;
@@ -748,9 +775,7 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
     f.w = c->w;
     f.anc_log = c->anc_log;
     f.dec = c->run_dec;
-    WSMC_HIP(mark());
-    WSMC_HIP(launch_ssm2d_finalize(c->stream, f));
-    WSMC_HIP(mark());
+    WSMC_HIP(launch_ssm2d_finalize(c->stream, f, E(8 * T), E(8 * T + 1)));
     return WSMC_OK;
 }
 
@@ -818,7 +843,7 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
     uint64_t h = 1469598103934665603ull;
     auto mix = [&](const void* q) { h = (h ^ (uint64_t)(uintptr_t)q) * 1099511628211ull; };
     for (auto& col : c->cols) { mix(col.front); mix(col.back); }
-    mix(c->w); mix(c->anc_log); mix(c->run_rec); mix(c->obs);
+    mix(c->w); mix(c->anc_log); mix(c->run_rec); mix(c->run_max); mix(c->obs);
     const std::string key = std::string(keybuf) + " ptr=" + std::to_string(h);
     auto build_tables = [&](double*** work, double*** outp) -> int {
         *work = *outp = nullptr;
@@ -839,7 +864,7 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         return WSMC_OK;
     };
     const bool use_graph = c->world == 1 && !c->timing;   // HIP cannot time events captured in graphs
-    const int nev = 4 * T + 2;
+    const int nev = 8 * T + 2;
     std::vector<hipEvent_t> evs;
     if (c->timing) {
         while ((int)c->events.size() < nev) {
@@ -939,25 +964,42 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
     if (c->timing) {
         wsmc_run_timing tm{};
         float ms = 0.f;
-        int k = 0;
         for (int t = 1; t <= T; ++t) {
+            const int k = 8 * (t - 1);
             WSMC_HIP(hipEventElapsedTime(&ms, evs[k], evs[k + 1]));
             tm.propagate_ms += ms;
-            WSMC_HIP(hipEventElapsedTime(&ms, evs[k + 1], evs[k + 2]));
-            tm.reduce_ms += ms;
             WSMC_HIP(hipEventElapsedTime(&ms, evs[k + 2], evs[k + 3]));
+            tm.reduce_ms += ms;
+            WSMC_HIP(hipEventElapsedTime(&ms, evs[k + 4], evs[k + 5]));
+            tm.reduce_ms += ms;
+            WSMC_HIP(hipEventElapsedTime(&ms, evs[k + 6], evs[k + 7]));
             tm.resample_ms += ms;
-            k += 4;
         }
-        WSMC_HIP(hipEventElapsedTime(&ms, evs[k], evs[k + 1]));
+        WSMC_HIP(hipEventElapsedTime(&ms, evs[8 * T], evs[8 * T + 1]));
         tm.finalize_ms = ms;
-        WSMC_HIP(hipEventElapsedTime(&ms, evs[0], evs[k + 1]));
+        WSMC_HIP(hipEventElapsedTime(&ms, evs[0], evs[8 * T + 1]));
         tm.total_ms = ms;
         tm.steps = T;
         tm.n_resamples = nres;
         c->last_timing = tm;
     }
     if (log_evidence_out) return wsmc_log_evidence(c, log_evidence_out);
+    return WSMC_OK;
+}
+
+int wsmc_debug_kernel_bench(wsmc_ctx* c, int32_t kernel, int32_t mode, int32_t iters, double* avg_us) {
+    CHECK_CTX(c);
+    if (!avg_us || iters < 1) return fail(WSMC_EARG, "bad arguments");
+    // populate max slots / partials / offsets / record from the current weights; force a resample
+    WSMC_HIP(hipMemsetAsync(c->mslots, 0, sizeof(MaxSlots), c->stream));
+    WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, c->mslots));
+    WSMC_HIP(launch_rs_sums(c->stream, c->w, c->N, c->mslots, c->tilep, c->qbuf));
+    const FillPlan plan = fill_plan(c, WSMC_RESAMPLE_STRATIFIED, c->op, nullptr);
+    WSMC_HIP(launch_rs_reduce(c->stream, c->mslots, c->tilep, c->N, c->tileOff, c->rec, 1, 2.0, c->dec, &plan));
+    float ms = 0.f;
+    WSMC_HIP(debug_kernel_bench(c->stream, kernel, mode, iters, c->w, c->N, c->mslots, c->tilep, c->qbuf,
+                                c->tileOff, c->rec, c->dec, plan, c->anc, &ms));
+    *avg_us = 1e3 * ms / iters;
     return WSMC_OK;
 }
 

@@ -17,26 +17,37 @@ namespace wsmc {
 constexpr int kBlock = 256;            // threads per workgroup (4 waves of 64)
 constexpr int kItems = 8;              // particles per thread in the tile kernels
 constexpr int kTile = kBlock * kItems; // 2048 particles per tile (canonical reduction tile)
-constexpr int kSlots = 64;             // accumulator copies, one 128-B line each (blockIdx % 64)
-constexpr int kRsItems = 4;            // particles per thread in the resample kernels
-constexpr int kRsTile = kBlock * kRsItems;  // 1024-particle resample tiles
-constexpr int kRsChunk = 2048;         // ancestor slots filled per LDS pass
+constexpr int kSlots = 64;             // max-accumulator slots (blockIdx % 64)
+constexpr int kRsBlock = 1024;         // threads of the weight-statistics / reduce workgroups
+constexpr int kRsTile = 1024;          // particles per resample tile
+constexpr int kScanBlock = 256;        // threads of the ancestor-fill workgroup (4 particles each)
+constexpr int kRsChunk = 2048;         // ancestor slots per fill task
 constexpr int kMaxCols = 4096;
 constexpr int kMaxShards = 8;     // one node: up to 8 GPUs
 
-// One shard's weight-statistics record. kSlots copies of each accumulator, one 128-B line
-// per copy, so the per-block atomics spread over 64 lines (memory-side atomics to one line
-// serialise at ~100/us).
-// v[s][0] = ordered max, v[s][1] = sum q, v[s][2..5] = sum q^2 limbs (32 bit),
-// v[s][6..9] = sum fix96 limbs, v[s][10] = shard size (slot 0 only).
-struct ShardRec {
+// Max accumulator of one Resample: 64 ordered-encoded slots, one per block group
+// (blockIdx % 64), filled with read-filtered atomicMax. One 128-B line per slot: memory-side
+// atomics and filtered loads to one line serialise, so the slots must not share lines.
+struct MaxSlots {
     unsigned long long v[kSlots][16];
 };
+
+// One shard's weight statistics: what the ranks exchange (64 B per step).
+struct ShardRecord {
+    unsigned long long menc;   // ordered encoding of the shard max log-weight
+    unsigned long long Q;      // sum q_i
+    unsigned long long q2lo, q2hi;  // sum q_i^2 (u128)
+    unsigned long long wlo, whi;    // sum floor(exp(lw - M) 2^96) (u128)
+    unsigned long long n;      // shard size
+    unsigned long long pad;
+};
+
+constexpr int kPart = 9;   // per-tile partials: sum q, 4 limbs of sum q^2, 4 limbs of sum fix96
 
 // Resample outcome for one invocation (one step of a fused run).
 struct Decision {
     int32_t resampled;
-    int32_t pad;
+    int32_t ntasks;     // ancestor-fill tasks of this shard (<= ntiles + N / kRsChunk + 1)
     double mean;        // this shard's post-resample log-weight
     double ess;         // global ESS/N
     double M;           // this shard's max log-weight
@@ -90,10 +101,15 @@ struct wsmc_ctx {
     // scratch
     int32_t* anc = nullptr;                 // last ancestors [N]
     double* tmp = nullptr;                  // [4N]
-    unsigned long long* tileQ = nullptr;    // [nrstiles] per-tile sum q (scan offsets)
+    unsigned long long* tilep = nullptr;    // [nrstiles * kPart] per-tile integer partials
+    unsigned long long* tileOff = nullptr;  // [nrstiles] exclusive prefix of the tiles' sum q
+    unsigned long long* tileL = nullptr;    // [nrstiles + 1] first ancestor slot owned by each tile
+    int32_t* taskOff = nullptr;             // [nrstiles] first fill task of each tile
+    int32_t* taskTile = nullptr;            // [nrstiles + N / kRsChunk + 1] tile of each fill task
     unsigned long long* qbuf = nullptr;     // [N] integer weights q_i of the last weight-statistics pass
     double* tilepart = nullptr;             // [16 * ntiles] canonical-sum tile partials
-    wsmc::ShardRec* rec = nullptr;          // [world] records of one generic resample
+    wsmc::MaxSlots* mslots = nullptr;       // [1] max slots of one generic resample / evidence
+    wsmc::ShardRecord* rec = nullptr;       // [world] shard records of one generic resample
     wsmc::Decision* dec = nullptr;          // [1] decision of one generic resample
     double* mom = nullptr;                  // [64] moment / covariance / Cholesky results
     int32_t* dflag = nullptr;               // [4] device error flags
@@ -104,7 +120,8 @@ struct wsmc_ctx {
 
     // fused runner state
     int32_t T_alloc = 0;
-    wsmc::ShardRec* run_rec = nullptr;      // [(T+1) * world]
+    wsmc::MaxSlots* run_max = nullptr;      // [T+1]
+    wsmc::ShardRecord* run_rec = nullptr;   // [(T+1) * world]
     wsmc::Decision* run_dec = nullptr;      // [T+1]
     int32_t* anc_log = nullptr;             // [T][N]
     double* obs = nullptr;                  // [T*2]
@@ -145,20 +162,36 @@ hipError_t launch_sample_importance(hipStream_t s, double* out, int dim, const w
                                     const wsmc_dist& targ, double* w, uint64_t seed, uint64_t op,
                                     int64_t goff, double* const* cols, int64_t N);
 hipError_t launch_weigh(hipStream_t s, const wsmc_term& t, double* w, double* const* cols, int64_t N);
-hipError_t launch_rs_max(hipStream_t s, const double* w, int64_t N, ShardRec* rec);
-hipError_t launch_rs_sums(hipStream_t s, const double* w, int64_t N, ShardRec* rec,
-                          unsigned long long* tileQ, unsigned long long* qbuf);
-hipError_t launch_rs_scan(hipStream_t s, const double* w, int64_t N, const ShardRec* recs, int world,
-                          int rank, double ess_min, int scheme, uint64_t seed, uint64_t op,
-                          const uint64_t* op_dev, int64_t slot_base, const unsigned long long* tileQ,
-                          const unsigned long long* qbuf, int32_t* anc, Decision* dec);
+hipError_t launch_rs_max(hipStream_t s, const double* w, int64_t N, MaxSlots* ms);
+hipError_t launch_rs_sums(hipStream_t s, const double* w, int64_t N, const MaxSlots* ms,
+                          unsigned long long* tilep, unsigned long long* qbuf,
+                          hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+struct FillPlan {          // ancestor-fill task planning (in the reduce kernel)
+    unsigned long long* tileL;
+    int32_t* taskOff;
+    int32_t* taskTile;
+    int scheme;
+    uint64_t seed, op;
+    const uint64_t* op_dev;
+    int64_t slot_base;
+};
+hipError_t launch_rs_reduce(hipStream_t s, const MaxSlots* ms, const unsigned long long* tilep, int64_t N,
+                            unsigned long long* tileOff, ShardRecord* rec, int decide_local, double ess_min,
+                            Decision* dec, const FillPlan* plan, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+hipError_t launch_rs_decide(hipStream_t s, const ShardRecord* recs, int world, int rank, double ess_min,
+                            Decision* dec);
+hipError_t launch_rs_scan(hipStream_t s, int64_t N, const ShardRecord* rec, const Decision* dec,
+                          const FillPlan& plan, const unsigned long long* tileOff,
+                          const unsigned long long* qbuf, int32_t* anc, hipEvent_t e0 = nullptr,
+                          hipEvent_t e1 = nullptr);
 hipError_t launch_gather(hipStream_t s, double* dst, const double* src, const int32_t* anc, int64_t N);
 hipError_t launch_fill_weights(hipStream_t s, double* w, const Decision* dec, int64_t N);
-hipError_t launch_log_evidence_stats(hipStream_t s, const double* w, int64_t N, ShardRec* rec,
-                                     unsigned long long* tileQ, unsigned long long* qbuf);
+hipError_t launch_log_evidence_stats(hipStream_t s, const double* w, int64_t N, MaxSlots* ms,
+                                     unsigned long long* tilep, unsigned long long* qbuf,
+                                     unsigned long long* tileOff, ShardRecord* rec);
 hipError_t launch_score(hipStream_t s, const wsmc_term* tape, int32_t n, int32_t depth,
                         double* const* cols, int64_t N, double* out);
-hipError_t launch_moments(hipStream_t s, const double* w, const ShardRec* rec, double* const* cols,
+hipError_t launch_moments(hipStream_t s, const double* w, const MaxSlots* ms, double* const* cols,
                           const int32_t* tcols, int d, const double* lo, const double* hi,
                           int pass, const double* mom, int64_t N, double* tilepart);
 hipError_t launch_moments_final(hipStream_t s, const double* tilepart, int64_t ntiles, int d,
@@ -193,9 +226,10 @@ struct Ssm2dArgs {
     double* w;                 // [N]
     const int32_t* anc_prev;   // [N] ancestors of step t-1
     const Decision* dec_prev;  // decision of step t-1 (nullptr at t = 1)
-    ShardRec* rec;             // this step's record (this rank)
+    MaxSlots* ms;              // this step's max slots
 };
-hipError_t launch_ssm2d_propagate(hipStream_t s, const Ssm2dArgs& a);
+hipError_t launch_ssm2d_propagate(hipStream_t s, const Ssm2dArgs& a, hipEvent_t e0 = nullptr,
+                                  hipEvent_t e1 = nullptr);
 struct Ssm2dFinal {
     int32_t T;
     int32_t keep_history;
@@ -213,7 +247,12 @@ struct Ssm2dFinal {
     const int32_t* anc_log;    // [T][N]
     const Decision* dec;       // [T+1], index t
 };
-hipError_t launch_ssm2d_finalize(hipStream_t s, const Ssm2dFinal& f);
+hipError_t launch_ssm2d_finalize(hipStream_t s, const Ssm2dFinal& f, hipEvent_t e0 = nullptr,
+                                 hipEvent_t e1 = nullptr);
 hipError_t launch_delay(hipStream_t s, int microseconds);
+hipError_t debug_kernel_bench(hipStream_t s, int kernel, int mode, int iters, const double* w, int64_t N,
+                              MaxSlots* ms, unsigned long long* tilep, unsigned long long* qbuf,
+                              unsigned long long* tileOff, ShardRecord* rec, Decision* dec, const FillPlan& plan,
+                              int32_t* anc, float* ms_out);
 
 }  // namespace wsmc

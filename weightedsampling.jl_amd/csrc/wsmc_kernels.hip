@@ -9,6 +9,8 @@
 // Layout: particle-major SoA f64 (component k of particle i at data[k*N + i]); one thread
 // per particle for streaming kernels (coalesced 8-B lanes), 256-thread workgroups of
 // 4 wave64s; tile kernels own 2048 particles (8 per thread).
+#include <hip/hip_ext.h>
+
 #include "wsmc_internal.h"
 
 namespace wsmc {
@@ -58,8 +60,9 @@ __device__ __forceinline__ u64 block_max_u64(u64 v, u64* lds4) {
     __syncthreads();
     return a > b ? a : b;
 }
-// exclusive prefix sum over the block (thread order), also returns the block total
-__device__ __forceinline__ u64 block_excl_scan_u64(u64 v, u64* lds4, u64* total) {
+// exclusive prefix sum over a block of NW waves (thread order), also returns the total
+template <int NW = 4>
+__device__ __forceinline__ u64 block_excl_scan_u64(u64 v, u64* ldsw, u64* total) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     u64 x = v;
 #pragma unroll
@@ -67,16 +70,22 @@ __device__ __forceinline__ u64 block_excl_scan_u64(u64 v, u64* lds4, u64* total)
         u64 y = __shfl_up(x, off, 64);
         if (lane >= off) x += y;
     }
-    if (lane == 63) lds4[w] = x;
+    if (lane == 63) ldsw[w] = x;
     __syncthreads();
-    u64 pre = 0;
-    for (int k = 0; k < w; ++k) pre += lds4[k];
-    *total = lds4[0] + lds4[1] + lds4[2] + lds4[3];
+    u64 pre = 0, t = 0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        const u64 s = ldsw[k];
+        pre += k < w ? s : 0ull;
+        t += s;
+    }
+    *total = t;
     __syncthreads();
     return pre + x - v;
 }
-// exclusive prefix max over the block (int, -1 = empty)
-__device__ __forceinline__ int block_excl_max_i32(int v, int* lds4, int* total) {
+// exclusive prefix max over a block of NW waves (int, -1 = empty)
+template <int NW = 4>
+__device__ __forceinline__ int block_excl_max_i32(int v, int* ldsw, int* total) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     int x = v;
 #pragma unroll
@@ -86,12 +95,15 @@ __device__ __forceinline__ int block_excl_max_i32(int v, int* lds4, int* total) 
     }
     int ex = __shfl_up(x, 1, 64);
     if (lane == 0) ex = -1;
-    if (lane == 63) lds4[w] = x;
+    if (lane == 63) ldsw[w] = x;
     __syncthreads();
-    int pre = -1;
-    for (int k = 0; k < w; ++k) pre = lds4[k] > pre ? lds4[k] : pre;
-    int t = lds4[0];
-    for (int k = 1; k < 4; ++k) t = lds4[k] > t ? lds4[k] : t;
+    int pre = -1, t = -1;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        const int s = ldsw[k];
+        if (k < w) pre = s > pre ? s : pre;
+        t = s > t ? s : t;
+    }
     *total = t;
     __syncthreads();
     return ex > pre ? ex : pre;
@@ -159,237 +171,303 @@ __global__ __launch_bounds__(kBlock) void k_weigh(wsmc_term t, double* w, double
 }
 
 // ------------------------------------------------------------------------------------
-// Resample: max, integer sums, scan + ancestor fill (src/transformers.jl:474-498)
+// Resample (src/transformers.jl:474-498) as four passes per invocation:
+//   max      block max of the log-weights -> 64 slots (read-filtered atomicMax)
+//   sums     per 1024-particle tile: q_i = floor(exp(lw_i - M) 2^K) (stored), and the exact
+//            integer partials sum q, sum q^2, sum floor(exp(lw_i - M) 2^96) (plain stores)
+//   reduce   one block: shard totals (ShardRecord), exclusive tile offsets, and — on one
+//            GPU — the ESS decision and post-resample log-mean
+//   scan     per tile: inclusive integer CDF from the offsets and the stratified /
+//            systematic ancestor fill (the icdf merge, src/resampling.jl:13-26)
+// Every decision-relevant quantity is an integer, so results do not depend on the order
+// of any reduction, the grid shape or the shard count.
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_rs_max(const double* __restrict__ w, int64_t N, ShardRec* rec) {
+__global__ __launch_bounds__(kBlock) void k_rs_max(const double* __restrict__ w, int64_t N, MaxSlots* ms) {
     __shared__ u64 lds[4];
     u64 m = 0;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < N; i += (int64_t)gridDim.x * kBlock)
         m = max(m, (u64)wsmc_ord_enc(w[i]));
     m = block_max_u64(m, lds);
-    if (threadIdx.x == 0) atomic_max_filtered(&rec->v[blockIdx.x % kSlots][0], m);
+    if (threadIdx.x == 0) atomic_max_filtered(&ms->v[blockIdx.x % kSlots][0], m);
 }
 
-// slot reductions by one wave: lane l owns slot l (kSlots == 64)
-static_assert(kSlots == 64, "one lane per accumulator slot");
-__device__ __forceinline__ u64 wave_rec_max_enc(const ShardRec* r) {
-    return wave_max_u64(r->v[threadIdx.x & 63][0]);
+static_assert(kSlots == 64, "one lane per max slot");
+// max over the 64 slots by one wave (every lane of the calling wave gets it); no barrier
+__device__ __forceinline__ double wave_slots_max(const MaxSlots* ms) {
+    return wsmc_ord_dec(wave_max_u64(ms->v[threadIdx.x & 63][0]));
 }
-// block-uniform max of the record (all threads); uses one wave + LDS
-__device__ __forceinline__ double block_rec_max(const ShardRec* r, u64* lds1) {
-    if (threadIdx.x < 64) {
-        const u64 m = wave_rec_max_enc(r);
-        if (threadIdx.x == 0) lds1[0] = m;
+// exact integer block sums of kPart values through LDS (transpose, two levels)
+template <int NT>
+__device__ __forceinline__ void block_sum_parts(const u64 (&acc)[kPart], u64 (*red)[NT], u64 (*red2)[16],
+                                                u64* out /* kPart, valid in threads < kPart */) {
+    const int th = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < kPart; ++k) red[k][th] = acc[k];
+    __syncthreads();
+    if (th < kPart * 16) {
+        const int k = th >> 4, seg = th & 15;
+        u64 t = 0;
+#pragma unroll 8
+        for (int j = 0; j < NT / 16; ++j) t += red[k][j * 16 + seg];
+        red2[k][seg] = t;
     }
     __syncthreads();
-    const double M = wsmc_ord_dec(lds1[0]);
-    __syncthreads();
-    return M;
-}
-// full shard statistics, computed by one wave (every lane returns the same value)
-__device__ __forceinline__ wsmc_shard_stats wave_rec_stats(const ShardRec* r) {
-    const int l = threadIdx.x & 63;
-    wsmc_shard_stats st;
-    st.M = wsmc_ord_dec(wave_max_u64(r->v[l][0]));
-    st.Q = wave_sum_u64(r->v[l][1]);
-    u64 lim[8];
+    if (th < kPart) {
+        u64 t = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) lim[k] = wave_sum_u64(r->v[l][2 + k]);
-    st.Q2 = (wsmc_u128)lim[0] + ((wsmc_u128)lim[1] << 32) + ((wsmc_u128)lim[2] << 64) + ((wsmc_u128)lim[3] << 96);
-    st.W = (wsmc_u128)lim[4] + ((wsmc_u128)lim[5] << 32) + ((wsmc_u128)lim[6] << 64) + ((wsmc_u128)lim[7] << 96);
-    st.n = r->v[0][10];
+        for (int j = 0; j < 16; ++j) t += red2[th][j];
+        out[th] = t;
+    }
+}
+
+// MODE (diagnostics only; production = 0): 1 = no exp, 2 = no q^2/fix96 partials,
+// 3 = no block reduction, 4 = load/store only
+template <int MODE>
+__global__ __launch_bounds__(kRsBlock) void k_rs_sums_t(const double* __restrict__ w, int64_t N,
+                                                        const MaxSlots* __restrict__ ms, u64* __restrict__ tilep,
+                                                        u64* __restrict__ qbuf) {
+    __shared__ u64 red[kPart][kRsBlock];
+    __shared__ u64 red2[kPart][16];
+    __shared__ u64 outp[kPart];
+    const int th = threadIdx.x;
+    const int64_t i = (int64_t)blockIdx.x * kRsTile + th;
+    const double lw = i < N ? w[i] : -WSMC_INF;
+    const double M = MODE == 4 ? 0.0 : wave_slots_max(ms);
+    const int K = wsmc_qbits((uint64_t)N);
+    const double e = (MODE == 1 || MODE == 4) ? lw - M : wsmc_exp(lw - M);
+    const u64 q = MODE == 4 ? (u64)wsmc_d2bits(e) : ((e > 0.0) ? (u64)wsmc_d_to_u64_trunc(e * wsmc_pow2i(K)) : 0ull);
+    if (i < N) qbuf[i] = q;
+    if (MODE == 4) return;
+    const wsmc_u128 q2 = MODE == 2 ? (wsmc_u128)q : (wsmc_u128)q * q;
+    const wsmc_u128 f = MODE == 2 ? (wsmc_u128)q : wsmc_fix96(e);
+    const u64 acc[kPart] = {q, (uint32_t)q2, (uint32_t)(q2 >> 32), (uint32_t)(q2 >> 64), (uint32_t)(q2 >> 96),
+                            (uint32_t)f, (uint32_t)(f >> 32), (uint32_t)(f >> 64), (uint32_t)(f >> 96)};
+    if (MODE == 3) {
+        u64 x = 0;
+        for (int k = 0; k < kPart; ++k) x ^= acc[k];
+        if (x == 0x123456789ull) tilep[0] = x;
+        return;
+    }
+    block_sum_parts<kRsBlock>(acc, red, red2, outp);
+    if (th < kPart) tilep[(int64_t)blockIdx.x * kPart + th] = outp[th];
+}
+
+__device__ __forceinline__ wsmc_shard_stats record_stats(const ShardRecord& r) {
+    wsmc_shard_stats st;
+    st.M = wsmc_ord_dec(r.menc);
+    st.Q = r.Q;
+    st.Q2 = ((wsmc_u128)r.q2hi << 64) | r.q2lo;
+    st.W = ((wsmc_u128)r.whi << 64) | r.wlo;
+    st.n = r.n;
     return st;
 }
 
-// one resample tile (1024 particles) per block, striped items (coalesced): sum q,
-// sum q^2 (4 x 32-bit limbs), sum fix96(e) (4 limbs) into the shard record (atomics spread
-// over kSlots copies); the tile's sum q -> tileQ (scan offsets).
-__global__ __launch_bounds__(kBlock) void k_rs_sums(const double* __restrict__ w, int64_t N, ShardRec* rec,
-                                                    u64* __restrict__ tileQ, u64* __restrict__ qbuf) {
-    __shared__ u64 lds[4][9];
-    __shared__ u64 s_m[1];
-    const int64_t base = (int64_t)blockIdx.x * kRsTile;
-    double lw[kRsItems];
-#pragma unroll
-    for (int j = 0; j < kRsItems; ++j) {
-        const int64_t i = base + (int64_t)j * kBlock + threadIdx.x;
-        lw[j] = i < N ? w[i] : -WSMC_INF;
-    }
-    const double M = block_rec_max(rec, s_m);
-    const int K = wsmc_qbits((uint64_t)N);
-    const double scale = wsmc_pow2i(K);
-    u64 acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-    for (int j = 0; j < kRsItems; ++j) {
-        const double e = wsmc_exp(lw[j] - M);
-        const u64 q = (e > 0.0) ? (u64)wsmc_d_to_u64_trunc(e * scale) : 0ull;
-        const int64_t i = base + (int64_t)j * kBlock + threadIdx.x;
-        if (i < N) qbuf[i] = q;
-        const wsmc_u128 q2 = (wsmc_u128)q * q;
-        const wsmc_u128 f = wsmc_fix96(e);
-        acc[0] += q;
-        acc[1] += (uint32_t)q2;
-        acc[2] += (uint32_t)(q2 >> 32);
-        acc[3] += (uint32_t)(q2 >> 64);
-        acc[4] += (uint32_t)(q2 >> 96);
-        acc[5] += (uint32_t)f;
-        acc[6] += (uint32_t)(f >> 32);
-        acc[7] += (uint32_t)(f >> 64);
-        acc[8] += (uint32_t)(f >> 96);
-    }
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        u64 v = wave_sum_u64(acc[k]);
-        if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6][k] = v;
-    }
-    __syncthreads();
-    if (threadIdx.x < 9) {
-        const int k = threadIdx.x;
-        const u64 v = (lds[0][k] + lds[1][k]) + (lds[2][k] + lds[3][k]);
-        if (k == 0) tileQ[blockIdx.x] = v;
-        if (v) atomicAdd(&rec->v[blockIdx.x % kSlots][1 + k], v);
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) rec->v[0][10] = (u64)N;
-}
-
-// Global Resample decision from the shard records (rank order), the same arithmetic as
-// wsmc_global_ess / wsmc_shard_mean. Called by all 64 lanes of one wave.
-__device__ void decide(const ShardRec* recs, int world, int rank, double ess_min, double* ess_out,
-                       int* rs_out, wsmc_shard_stats* mine) {
+// Global decision from the shard records (rank order): the same arithmetic as
+// wsmc_global_ess / wsmc_shard_mean, streamed over the records (no local arrays).
+__device__ void decide_records(const ShardRecord* recs, int world, int rank, double ess_min, Decision* dec) {
     double M = -WSMC_INF;
     uint64_t N = 0;
     int nan = 0;
     for (int g = 0; g < world; ++g) {
-        const double Mg = wsmc_ord_dec(wave_rec_max_enc(&recs[g]));
+        const double Mg = wsmc_ord_dec(recs[g].menc);
         if (wsmc_isnan(Mg)) nan = 1;
         else if (Mg > M) M = Mg;
-        N += recs[g].v[0][10];
+        N += recs[g].n;
     }
     if (nan) M = WSMC_NAN;
     double sq = 0.0, sq2 = 0.0;
     for (int g = 0; g < world; ++g) {
-        const wsmc_shard_stats st = wave_rec_stats(&recs[g]);
+        const wsmc_shard_stats st = record_stats(recs[g]);
         const double f = wsmc_exp(st.M - M);
         const double sc = wsmc_pow2i(-wsmc_qbits(st.n));
         const double qd = wsmc_u64_to_d(st.Q), q2d = wsmc_u128_to_d(st.Q2);
         sq = sq + (qd * sc) * f;
         sq2 = sq2 + ((q2d * sc) * sc) * (f * f);
-        if (g == rank) *mine = st;
     }
     const double ess = (sq * sq) / (wsmc_u64_to_d(N) * sq2);
-    *ess_out = ess;
-    *rs_out = ess < ess_min;
+    const int rs = ess < ess_min;
+    const wsmc_shard_stats me = record_stats(recs[rank]);
+    dec->resampled = rs;
+    dec->ess = ess;
+    dec->M = me.M;
+    dec->mean = rs ? wsmc_shard_mean(&me) : 0.0;
 }
 
-// Decision + inclusive integer CDF + ancestor fill for one tile.
-// ancestor(slot) = smallest m with C_m > x_slot (src/resampling.jl:13-26); particle m owns
-// slots [rank(C_{m-1}), rank(C_m)) and the block fills its contiguous slot range through
-// an LDS mark array + max-scan (load-balanced within the block).
-__global__ __launch_bounds__(kBlock) void k_rs_scan(const double* __restrict__ w, int64_t N,
-                                                    const ShardRec* recs, int world, int rank,
-                                                    double ess_min, int scheme, uint64_t seed,
-                                                    uint64_t op, const uint64_t* op_dev,
-                                                    int64_t slot_base, const u64* __restrict__ tileQ,
-                                                    const u64* __restrict__ qbuf,
-                                                    int32_t* __restrict__ anc, Decision* dec) {
-    __shared__ u64 s_u4[4];
-    __shared__ int s_i4[4];
-    __shared__ u64 s_hi[kBlock];
-    __shared__ int marks[kRsChunk];
-    __shared__ u64 s_Q, s_L;
-    __shared__ int s_rs;
+// one block: shard totals, tile offsets, the ancestor-fill task plan and (one GPU) the decision
+__global__ __launch_bounds__(kRsBlock) void k_rs_reduce(const MaxSlots* __restrict__ ms,
+                                                        const u64* __restrict__ tilep, int64_t ntiles, int64_t N,
+                                                        u64* __restrict__ tileOff, ShardRecord* rec,
+                                                        int decide_local, double ess_min, Decision* dec,
+                                                        FillPlan plan) {
+    __shared__ u64 red[kPart][kRsBlock];
+    __shared__ u64 red2[kPart][16];
+    __shared__ u64 tot[kPart];
+    __shared__ u64 s_w[kRsBlock / 64];
+    constexpr int kHeavyTasks = 4, kHeavyQueue = 256;
+    __shared__ int s_heavy[kHeavyQueue][3];
+    __shared__ int s_nheavy;
     const int th = threadIdx.x;
-    const int64_t base = (int64_t)blockIdx.x * kRsTile;
-
-    // issue this tile's loads and the offset loads before the decision
-    u64 q[kRsItems];
+    // thread th owns the contiguous tiles [b0, b1): loads each tile's partials once
+    const int64_t per = (ntiles + kRsBlock - 1) / kRsBlock;
+    const int64_t b0 = (int64_t)th * per, b1 = b0 + per < ntiles ? b0 + per : ntiles;
+    u64 acc[kPart] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int64_t b = b0; b < b1; ++b)
 #pragma unroll
-    for (int j = 0; j < kRsItems; ++j) {
-        const int64_t i = base + (int64_t)th * kRsItems + j;
-        q[j] = i < N ? qbuf[i] : 0ull;
+        for (int k = 0; k < kPart; ++k) acc[k] += tilep[b * kPart + k];
+    block_sum_parts<kRsBlock>(acc, red, red2, tot);
+    u64 total;
+    u64 pre = block_excl_scan_u64<kRsBlock / 64>(acc[0], s_w, &total);
+    // tile offsets and the first slot each tile owns: L_b = rank(tileOff_b) (Q = this shard's
+    // total); each thread also ranks its successor's first offset, so the per-tile slot
+    // counts need no cross-thread exchange
+    const bool planned = plan.tileL != nullptr;   // uniform: log-evidence reuses this kernel unplanned
+    const u64 Q = total;
+    const uint64_t opx = planned ? op_eff(plan.op, plan.op_dev) : 0ull;
+    const double ratio = Q ? wsmc_u64_to_d((uint64_t)N) / wsmc_u64_to_d(Q) : 0.0;
+    auto rank_of = [&](u64 c) -> u64 {
+        return Q ? wsmc_rank_r(c, Q, (uint64_t)N, ratio, plan.scheme, plan.seed, opx, (uint64_t)plan.slot_base)
+                 : 0ull;
+    };
+    int nt = 0;
+    u64 Lb = (planned && b0 < b1) ? rank_of(pre) : 0ull;
+    for (int64_t b = b0; b < b1; ++b) {
+        tileOff[b] = pre;
+        pre += tilep[b * kPart];
+        if (planned) {
+            const u64 Ln = b + 1 == ntiles ? (u64)N : rank_of(pre);
+            plan.tileL[b] = Lb;
+            nt += (int)((Ln - Lb + kRsChunk - 1) / kRsChunk);
+            Lb = Ln;
+        }
     }
-    u64 part = 0;
-    for (int64_t b = th; b < (int64_t)blockIdx.x; b += kBlock) part += tileQ[b];
-
+    u64 tt = 0;
+    if (planned) {
+        if (th == 0) plan.tileL[ntiles] = (u64)N;
+        // fill tasks: ceil(slots / kRsChunk) per tile; exclusive scan -> taskOff; task -> tile map
+        int tpre = (int)block_excl_scan_u64<kRsBlock / 64>((u64)nt, s_w, &tt);
+        const u64 Lend = Lb;   // first slot of tile b1 (ranked above)
+        // a tile with many tasks (a dominant particle) is queued and its map entries are
+        // written by the whole block, so one thread never loops over N / kRsChunk entries
+        if (th == 0) s_nheavy = 0;
+        __syncthreads();
+        for (int64_t b = b0; b < b1; ++b) {
+            const u64 lo = plan.tileL[b];                    // written by this thread
+            const u64 hi = b + 1 < b1 ? plan.tileL[b + 1] : Lend;
+            const int k = (int)((hi - lo + kRsChunk - 1) / kRsChunk);
+            plan.taskOff[b] = tpre;
+            int q = -1;
+            if (k > kHeavyTasks) {
+                q = atomicAdd(&s_nheavy, 1);
+                if (q < kHeavyQueue) { s_heavy[q][0] = (int)b; s_heavy[q][1] = tpre; s_heavy[q][2] = k; }
+            }
+            if (q < 0 || q >= kHeavyQueue)
+                for (int j = 0; j < k; ++j) plan.taskTile[tpre + j] = (int32_t)b;
+            tpre += k;
+        }
+        __syncthreads();
+        const int nh = s_nheavy < kHeavyQueue ? s_nheavy : kHeavyQueue;
+        for (int e = 0; e < nh; ++e)
+            for (int j = th; j < s_heavy[e][2]; j += kRsBlock) plan.taskTile[s_heavy[e][1] + j] = s_heavy[e][0];
+    }
     if (th < 64) {
-        double ess;
-        int rs;
-        wsmc_shard_stats me;
-        decide(recs, world, rank, ess_min, &ess, &rs, &me);
+        const u64 menc = wave_max_u64(ms->v[th][0]);
         if (th == 0) {
-            s_Q = me.Q;
-            s_rs = rs;
-        }
-        if (blockIdx.x == 0 && th == 0) {
-            dec->resampled = rs;
-            dec->ess = ess;
-            dec->M = me.M;
-            dec->mean = rs ? wsmc_shard_mean(&me) : 0.0;
-        }
-    }
-    __syncthreads();
-    if (!s_rs) return;
-    const uint64_t opx = op_eff(op, op_dev);
-    const u64 Q = s_Q;
-    const double ratio = wsmc_u64_to_d((uint64_t)N) / wsmc_u64_to_d(Q);
-    const u64 off = block_sum_u64(part, s_u4);
-
-    // blocked items: thread th owns particles base + th*4 .. +3
-    u64 tsum = 0;
-#pragma unroll
-    for (int j = 0; j < kRsItems; ++j) tsum += q[j];
-    u64 tot;
-    const u64 pre = block_excl_scan_u64(tsum, s_u4, &tot);
-    // hi_j = rank(C_j); lo_0 = rank(C_{-1})
-    u64 hi[kRsItems];
-    u64 C = off + pre;
-    const u64 lo0 = wsmc_rank_r(C, Q, (uint64_t)N, ratio, scheme, seed, opx, (uint64_t)slot_base);
-    u64 prev = lo0;
-#pragma unroll
-    for (int j = 0; j < kRsItems; ++j) {
-        C += q[j];
-        hi[j] = q[j] ? wsmc_rank_r(C, Q, (uint64_t)N, ratio, scheme, seed, opx, (uint64_t)slot_base) : prev;
-        prev = hi[j];
-    }
-    s_hi[th] = hi[kRsItems - 1];
-    if (th == 0) s_L = lo0;
-    __syncthreads();
-    const u64 Ls = s_L, H = s_hi[kBlock - 1];
-
-    int carry = -1;
-    constexpr int PT = kRsChunk / kBlock;   // slots per thread per chunk
-    for (u64 cb = Ls; cb < H; cb += kRsChunk) {
-#pragma unroll
-        for (int k = 0; k < PT; ++k) marks[k * kBlock + th] = -1;
-        __syncthreads();
-        u64 lo = lo0;
-#pragma unroll
-        for (int j = 0; j < kRsItems; ++j) {
-            if (lo < hi[j] && lo >= cb && lo < cb + kRsChunk) marks[lo - cb] = th * kRsItems + j;
-            lo = hi[j];
-        }
-        __syncthreads();
-        int run[PT];
-        int m = -1;
-#pragma unroll
-        for (int k = 0; k < PT; ++k) {
-            const int v = marks[th * PT + k];
-            m = v > m ? v : m;
-            run[k] = m;
-        }
-        int ctot;
-        const int ex = block_excl_max_i32(m, s_i4, &ctot);
-        const int lead = ex > carry ? ex : carry;
-#pragma unroll
-        for (int k = 0; k < PT; ++k) {
-            const u64 slot = cb + (u64)(th * PT + k);
-            if (slot < H) {
-                const int a = run[k] > lead ? run[k] : lead;
-                anc[slot] = (int32_t)(base + a);
+            ShardRecord r;
+            r.menc = menc;
+            r.Q = tot[0];
+            const wsmc_u128 Q2 = (wsmc_u128)tot[1] + ((wsmc_u128)tot[2] << 32) + ((wsmc_u128)tot[3] << 64) +
+                                 ((wsmc_u128)tot[4] << 96);
+            const wsmc_u128 W = (wsmc_u128)tot[5] + ((wsmc_u128)tot[6] << 32) + ((wsmc_u128)tot[7] << 64) +
+                                ((wsmc_u128)tot[8] << 96);
+            r.q2lo = (u64)Q2; r.q2hi = (u64)(Q2 >> 64);
+            r.wlo = (u64)W; r.whi = (u64)(W >> 64);
+            r.n = (u64)N;
+            r.pad = 0;
+            *rec = r;
+            if (dec) {
+                dec->ntasks = (int32_t)tt;
+                if (decide_local) decide_records(&r, 1, 0, ess_min, dec);
             }
         }
-        carry = ctot > carry ? ctot : carry;
-        __syncthreads();
+    }
+}
+
+// multi-GPU: decision from the all-gathered records
+__global__ void k_rs_decide(const ShardRecord* recs, int world, int rank, double ess_min, Decision* dec) {
+    if (threadIdx.x == 0) decide_records(recs, world, rank, ess_min, dec);
+}
+
+// Ancestor fill, one block per task (<= kRsChunk consecutive slots of one tile).
+// ancestor(slot) = smallest m with C_m > x_slot (the icdf merge, src/resampling.jl:13-26):
+// with hi_m = rank(C_m) (monotone), the ancestor of slot n of tile b is the first particle
+// m of the tile with hi_m > n, found by binary search in LDS. Work per block is bounded
+// whatever the weight skew (a dominant particle only adds tasks).
+// MODE (diagnostics only; production = 0): 1 = no rank (cheap estimate), 2 = no fill,
+// 3 = scan only
+template <int MODE>
+__global__ __launch_bounds__(kScanBlock) void k_rs_scan_t(int64_t N, const ShardRecord* __restrict__ rec,
+                                                          const Decision* __restrict__ dec, FillPlan plan,
+                                                          const u64* __restrict__ tileOff,
+                                                          const u64* __restrict__ qbuf, int32_t* __restrict__ anc) {
+    constexpr int IT = kRsTile / kScanBlock;   // 4 particles per thread, blocked
+    __shared__ u64 s_uw[kScanBlock / 64];
+    __shared__ uint32_t hiL[kRsTile];
+    if (!dec->resampled) return;
+    const int t = blockIdx.x;
+    if (t >= dec->ntasks) return;
+    const int th = threadIdx.x;
+    const int b = plan.taskTile[t];
+    const int j = t - plan.taskOff[b];
+    const u64 L = plan.tileL[b], H = plan.tileL[b + 1];
+    const u64 cs = L + (u64)j * kRsChunk;
+    const u64 ce = cs + kRsChunk < H ? cs + kRsChunk : H;
+    const int64_t base = (int64_t)b * kRsTile;
+    u64 q[IT];
+    u64 tsum = 0;
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        const int64_t i = base + (int64_t)th * IT + k;
+        q[k] = i < N ? qbuf[i] : 0ull;
+        tsum += q[k];
+    }
+    const u64 off = tileOff[b];
+    const u64 Q = rec->Q;
+    const uint64_t opx = op_eff(plan.op, plan.op_dev);
+    const double ratio = wsmc_u64_to_d((uint64_t)N) / wsmc_u64_to_d(Q);
+    u64 tot;
+    const u64 pre = block_excl_scan_u64<kScanBlock / 64>(tsum, s_uw, &tot);
+    if (MODE == 3) {
+        if (pre == 0x123456789ull) anc[0] = 1;
+        return;
+    }
+    u64 C = off + pre;
+    u64 prev = L;   // rank(C) of the previous particle (a particle with q = 0 owns no slots)
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        C += q[k];
+        u64 h = prev;
+        if (q[k] || k == 0) h = MODE == 1 ? (u64)(wsmc_u64_to_d(C) * ratio)
+                                : wsmc_rank_r(C, Q, (uint64_t)N, ratio, plan.scheme, plan.seed, opx,
+                                              (uint64_t)plan.slot_base);
+        if (MODE == 1 && h > H) h = H;
+        if (MODE == 1 && h < L) h = L;
+        hiL[th * IT + k] = (uint32_t)(h - L);
+        prev = h;
+    }
+    if (MODE == 2) {
+        if (hiL[th * IT] == 0xffffffffu) anc[0] = 1;
+        return;
+    }
+    __syncthreads();
+    // hiL is non-decreasing (a zero-q particle repeats its predecessor's rank), so the
+    // first m with hiL[m] > r is found by a branch-free binary search
+    for (u64 n = cs + th; n < ce; n += kScanBlock) {
+        const uint32_t r = (uint32_t)(n - L);
+        int m = 0;
+#pragma unroll
+        for (int step = kRsTile / 2; step > 0; step >>= 1)
+            if (hiL[m + step - 1] <= r) m += step;
+        anc[n] = (int32_t)(base + m);
     }
 }
 
@@ -423,13 +501,12 @@ struct MomArgs {
 
 // pass 1: values {e, e*z_k};  pass 2: values {(e*(z_a-mean_a))*(z_b-mean_b), a <= b}
 // written as canonical tile partials tilepart[v * ntiles + tile]
-__global__ __launch_bounds__(kBlock) void k_moments(const double* __restrict__ w, const ShardRec* rec,
+__global__ __launch_bounds__(kBlock) void k_moments(const double* __restrict__ w, const MaxSlots* ms,
                                                     double* const* cols, MomArgs ma, int d, int pass,
                                                     const double* mom, int64_t N, int64_t ntiles,
                                                     double* tilepart) {
     __shared__ double lds4[4];
-    __shared__ u64 s_m[1];
-    const double M = block_rec_max(rec, s_m);
+    const double M = wave_slots_max(ms);
     const int64_t base = (int64_t)blockIdx.x * kTile;
     double acc[10];
     const int nv = pass == 1 ? 1 + d : d * (d + 1) / 2;
@@ -616,7 +693,7 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_prop(Ssm2dArgs a) {
         menc = wsmc_ord_enc(wn);
     }
     menc = block_max_u64(menc, lds4);
-    if (threadIdx.x == 0) atomic_max_filtered(&a.rec->v[blockIdx.x % kSlots][0], menc);
+    if (threadIdx.x == 0) atomic_max_filtered(&a.ms->v[blockIdx.x % kSlots][0], menc);
 }
 
 // trace the ancestor log back once and materialise the final columns — the result
@@ -657,6 +734,7 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_final(Ssm2dFinal f) {
 static inline dim3 grid_for(int64_t N) { return dim3((unsigned)((N + kBlock - 1) / kBlock)); }
 static inline dim3 tiles_for(int64_t N) { return dim3((unsigned)((N + kTile - 1) / kTile)); }
 static inline dim3 rs_tiles_for(int64_t N) { return dim3((unsigned)((N + kRsTile - 1) / kRsTile)); }
+static_assert(kRsChunk % kRsBlock == 0, "chunk is a multiple of the block");
 
 hipError_t launch_assign(hipStream_t s, double* out, int dim, const wsmc_operand* expr,
                          double* const* cols, int64_t N) {
@@ -681,24 +759,90 @@ hipError_t launch_weigh(hipStream_t s, const wsmc_term& t, double* w, double* co
     hipLaunchKernelGGL(k_weigh, grid_for(N), dim3(kBlock), 0, s, t, w, cols, N);
     return hipGetLastError();
 }
-hipError_t launch_rs_max(hipStream_t s, const double* w, int64_t N, ShardRec* rec) {
+template <typename K, typename... Args>
+static hipError_t launch_timed(K kernel, dim3 grid, dim3 block, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
+                               Args... args) {
+    if (e0 || e1)
+        hipExtLaunchKernelGGL(kernel, grid, block, 0, s, e0, e1, 0, args...);
+    else
+        hipLaunchKernelGGL(kernel, grid, block, 0, s, args...);
+    return hipGetLastError();
+}
+
+hipError_t launch_rs_max(hipStream_t s, const double* w, int64_t N, MaxSlots* ms) {
     int64_t nb = (N + kBlock * 4 - 1) / (kBlock * 4);
     if (nb > 2048) nb = 2048;
     if (nb < 1) nb = 1;
-    hipLaunchKernelGGL(k_rs_max, dim3((unsigned)nb), dim3(kBlock), 0, s, w, N, rec);
+    hipLaunchKernelGGL(k_rs_max, dim3((unsigned)nb), dim3(kBlock), 0, s, w, N, ms);
     return hipGetLastError();
 }
-hipError_t launch_rs_sums(hipStream_t s, const double* w, int64_t N, ShardRec* rec, u64* tileQ, u64* qbuf) {
-    hipLaunchKernelGGL(k_rs_sums, rs_tiles_for(N), dim3(kBlock), 0, s, w, N, rec, tileQ, qbuf);
+hipError_t launch_rs_sums(hipStream_t s, const double* w, int64_t N, const MaxSlots* ms, u64* tilep, u64* qbuf,
+                          hipEvent_t e0, hipEvent_t e1) {
+    return launch_timed(k_rs_sums_t<0>, rs_tiles_for(N), dim3(kRsBlock), s, e0, e1, w, N, ms, tilep, qbuf);
+}
+hipError_t launch_rs_reduce(hipStream_t s, const MaxSlots* ms, const u64* tilep, int64_t N, u64* tileOff,
+                            ShardRecord* rec, int decide_local, double ess_min, Decision* dec,
+                            const FillPlan* plan, hipEvent_t e0, hipEvent_t e1) {
+    const int64_t nt = (N + kRsTile - 1) / kRsTile;
+    FillPlan p{};
+    if (plan) p = *plan;
+    return launch_timed(k_rs_reduce, dim3(1), dim3(kRsBlock), s, e0, e1, ms, tilep, nt, N, tileOff, rec,
+                        decide_local, ess_min, dec, p);
+}
+hipError_t launch_rs_decide(hipStream_t s, const ShardRecord* recs, int world, int rank, double ess_min,
+                            Decision* dec) {
+    hipLaunchKernelGGL(k_rs_decide, dim3(1), dim3(64), 0, s, recs, world, rank, ess_min, dec);
     return hipGetLastError();
 }
-hipError_t launch_rs_scan(hipStream_t s, const double* w, int64_t N, const ShardRec* recs, int world, int rank,
-                          double ess_min, int scheme, uint64_t seed, uint64_t op, const uint64_t* op_dev,
-                          int64_t slot_base, const u64* tileQ, const u64* qbuf, int32_t* anc, Decision* dec) {
-    hipLaunchKernelGGL(k_rs_scan, rs_tiles_for(N), dim3(kBlock), 0, s, w, N, recs, world, rank, ess_min, scheme,
-                       seed, op, op_dev, slot_base, tileQ, qbuf, anc, dec);
-    return hipGetLastError();
+static inline dim3 fill_tasks_for(int64_t N) {
+    return dim3((unsigned)((N + kRsTile - 1) / kRsTile + N / kRsChunk + 1));
 }
+hipError_t launch_rs_scan(hipStream_t s, int64_t N, const ShardRecord* rec, const Decision* dec,
+                          const FillPlan& plan, const u64* tileOff, const u64* qbuf, int32_t* anc, hipEvent_t e0,
+                          hipEvent_t e1) {
+    return launch_timed(k_rs_scan_t<0>, fill_tasks_for(N), dim3(kScanBlock), s, e0, e1, N, rec, dec, plan, tileOff,
+                        qbuf, anc);
+}
+
+// diagnostics: time `iters` launches of a kernel variant on the context's current buffers
+hipError_t debug_kernel_bench(hipStream_t s, int kernel, int mode, int iters, const double* w, int64_t N,
+                              MaxSlots* ms, u64* tilep, u64* qbuf, u64* tileOff, ShardRecord* rec, Decision* dec,
+                              const FillPlan& plan, int32_t* anc, float* ms_out) {
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    const dim3 g = rs_tiles_for(N), blk(kRsBlock), gs = fill_tasks_for(N), bs(kScanBlock);
+    hipEventRecord(a, s);
+    for (int it = 0; it < iters; ++it) {
+        if (kernel == 0) {
+            switch (mode) {
+                case 0: hipLaunchKernelGGL(k_rs_sums_t<0>, g, blk, 0, s, w, N, ms, tilep, qbuf); break;
+                case 1: hipLaunchKernelGGL(k_rs_sums_t<1>, g, blk, 0, s, w, N, ms, tilep, qbuf); break;
+                case 2: hipLaunchKernelGGL(k_rs_sums_t<2>, g, blk, 0, s, w, N, ms, tilep, qbuf); break;
+                case 3: hipLaunchKernelGGL(k_rs_sums_t<3>, g, blk, 0, s, w, N, ms, tilep, qbuf); break;
+                default: hipLaunchKernelGGL(k_rs_sums_t<4>, g, blk, 0, s, w, N, ms, tilep, qbuf); break;
+            }
+        } else if (kernel == 1) {
+            launch_rs_reduce(s, ms, tilep, N, tileOff, rec, 1, 2.0, dec, &plan);
+        } else {
+            switch (mode) {
+                case 0: hipLaunchKernelGGL(k_rs_scan_t<0>, gs, bs, 0, s, N, rec, dec, plan, tileOff, qbuf, anc); break;
+                case 1: hipLaunchKernelGGL(k_rs_scan_t<1>, gs, bs, 0, s, N, rec, dec, plan, tileOff, qbuf, anc); break;
+                case 2: hipLaunchKernelGGL(k_rs_scan_t<2>, gs, bs, 0, s, N, rec, dec, plan, tileOff, qbuf, anc); break;
+                default: hipLaunchKernelGGL(k_rs_scan_t<3>, gs, bs, 0, s, N, rec, dec, plan, tileOff, qbuf, anc); break;
+            }
+        }
+    }
+    hipEventRecord(b, s);
+    hipError_t e = hipEventSynchronize(b);
+    float t = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&t, a, b);
+    *ms_out = t;
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+    return e != hipSuccess ? e : hipGetLastError();
+}
+
 hipError_t launch_gather(hipStream_t s, double* dst, const double* src, const int32_t* anc, int64_t N) {
     hipLaunchKernelGGL(k_gather, grid_for(N), dim3(kBlock), 0, s, dst, src, anc, N);
     return hipGetLastError();
@@ -707,18 +851,19 @@ hipError_t launch_fill_weights(hipStream_t s, double* w, const Decision* dec, in
     hipLaunchKernelGGL(k_fill_weights, grid_for(N), dim3(kBlock), 0, s, w, dec, N);
     return hipGetLastError();
 }
-hipError_t launch_log_evidence_stats(hipStream_t s, const double* w, int64_t N, ShardRec* rec, u64* tileQ,
-                                     u64* qbuf) {
-    hipError_t e = launch_rs_max(s, w, N, rec);
-    if (e != hipSuccess) return e;
-    return launch_rs_sums(s, w, N, rec, tileQ, qbuf);
+hipError_t launch_log_evidence_stats(hipStream_t s, const double* w, int64_t N, MaxSlots* ms, u64* tilep,
+                                     u64* qbuf, u64* tileOff, ShardRecord* rec) {
+    hipError_t e = launch_rs_max(s, w, N, ms);
+    if (e == hipSuccess) e = launch_rs_sums(s, w, N, ms, tilep, qbuf);
+    if (e == hipSuccess) e = launch_rs_reduce(s, ms, tilep, N, tileOff, rec, 0, 0.0, nullptr, nullptr);
+    return e;
 }
 hipError_t launch_score(hipStream_t s, const wsmc_term* tape, int32_t n, int32_t depth, double* const* cols,
                         int64_t N, double* out) {
     hipLaunchKernelGGL(k_score, grid_for(N), dim3(kBlock), 0, s, tape, n, depth, cols, N, out);
     return hipGetLastError();
 }
-hipError_t launch_moments(hipStream_t s, const double* w, const ShardRec* rec, double* const* cols,
+hipError_t launch_moments(hipStream_t s, const double* w, const MaxSlots* rec, double* const* cols,
                           const int32_t* tcols, int d, const double* lo, const double* hi, int pass,
                           const double* mom, int64_t N, double* tilepart) {
     MomArgs ma;
@@ -763,9 +908,8 @@ hipError_t launch_count_unique(hipStream_t s, const u64* keys, int64_t N, u64* c
     hipLaunchKernelGGL(k_count_unique, dim3((unsigned)nb), dim3(kBlock), 0, s, keys, N, count);
     return hipGetLastError();
 }
-hipError_t launch_ssm2d_propagate(hipStream_t s, const Ssm2dArgs& a) {
-    hipLaunchKernelGGL(k_ssm2d_prop, grid_for(a.N), dim3(kBlock), 0, s, a);
-    return hipGetLastError();
+hipError_t launch_ssm2d_propagate(hipStream_t s, const Ssm2dArgs& a, hipEvent_t e0, hipEvent_t e1) {
+    return launch_timed(k_ssm2d_prop, grid_for(a.N), dim3(kBlock), s, e0, e1, a);
 }
 // bounded spin on the 100 MHz constant clock (always exits): queue-filling delay for
 // instrumented runs
@@ -780,9 +924,8 @@ hipError_t launch_delay(hipStream_t s, int microseconds) {
     return hipGetLastError();
 }
 
-hipError_t launch_ssm2d_finalize(hipStream_t s, const Ssm2dFinal& f) {
-    hipLaunchKernelGGL(k_ssm2d_final, grid_for(f.N), dim3(kBlock), 0, s, f);
-    return hipGetLastError();
+hipError_t launch_ssm2d_finalize(hipStream_t s, const Ssm2dFinal& f, hipEvent_t e0, hipEvent_t e1) {
+    return launch_timed(k_ssm2d_final, grid_for(f.N), dim3(kBlock), s, e0, e1, f);
 }
 
 }  // namespace wsmc

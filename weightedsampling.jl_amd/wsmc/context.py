@@ -218,6 +218,11 @@ class Context:
     def set_timing(self, enabled: bool) -> None:
         check(self._L.wsmc_run_set_timing(self._h, int(bool(enabled))))
 
+    def debug_kernel_bench(self, kernel: int, mode: int = 0, iters: int = 50) -> float:
+        v = C.c_double()
+        check(self._L.wsmc_debug_kernel_bench(self._h, int(kernel), int(mode), int(iters), C.byref(v)))
+        return float(v.value)
+
     def timing(self) -> dict:
         t = RunTiming()
         check(self._L.wsmc_run_get_timing(self._h, C.byref(t)))
