@@ -1,0 +1,371 @@
+"""
+    WeightedSamplingHIP
+
+MI355X backend for WeightedSampling.jl: a `HipColumnStore <: AbstractParticleStore`
+(src/stores.jl:1-35) plus `apply!` specialisations for `SMCState{<:HipColumnStore}` that
+route the per-particle hot path (Sample / Observe / Weight / Assign / Resample / Move) to
+`libwsmc.so` through `ccall` (include/wsmc.h). The reference package is not edited: Julia's
+dispatch picks these methods because they are more specific in the store type
+(src/types.jl:48).
+
+UNTESTED: the build image has no Julia toolchain. Every `ccall` below mirrors a binding of
+the Python ctypes layer (`weightedsampling.jl_amd/wsmc/abi.py`), which the test-suite runs
+against the same library on MI355X. See INTEGRATION.md.
+
+Device arguments are recognised structurally. `getcol` on a `HipColumnStore` returns a
+`DeviceColumn` proxy. Broadcasting `+ - *` over proxies and `Ref` constants (the shapes
+`vectorize` emits, src/rewrites.jl:146-219) builds a lazy affine `DeviceExpr`, which
+becomes a `wsmc_operand`. Any other expression is materialised on the host (download →
+compute → temporary device column), which is correct but slow.
+"""
+module WeightedSamplingHIP
+
+using WeightedSampling
+using LinearAlgebra: PosDefException, I
+using Distributions: Normal, MvNormal, Uniform, Truncated
+const WS = WeightedSampling
+import WeightedSampling: nparticles, hascol, getcol, colnames, broadcast_setcol!, resample!, apply!,
+    log_evidence
+
+export HipColumnStore, ssm2d_run!, sync_weights!
+
+const libwsmc = get(ENV, "WSMC_LIB", joinpath(@__DIR__, "..", "wsmc", "libwsmc.so"))
+
+# ---------------------------------------------------------------------------------------
+# C structs (include/wsmc.h) — field order and sizes must match (tests/test_abi.py checks
+# the C side against the Python mirror; Julia isbits structs follow the same C layout)
+# ---------------------------------------------------------------------------------------
+struct WsmcOperand
+    c0::Float64
+    col::NTuple{2,Int32}
+    comp::NTuple{2,Int32}
+    coef::NTuple{2,Float64}
+end
+const_operand(v) = WsmcOperand(Float64(v), (Int32(-1), Int32(-1)), (Int32(0), Int32(0)), (0.0, 0.0))
+
+struct WsmcDist
+    family::Int32
+    mean_fn::Int32
+    dim::Int32
+    reserved::Int32
+    mu::NTuple{4,WsmcOperand}
+    scale::WsmcOperand
+    param::NTuple{2,Float64}
+end
+
+struct WsmcState
+    resampled::Int32
+    weights_changed::Int32
+    depth::Int32
+    n_terms::Int32
+    last_ess_perc::Float64
+    op_counter::UInt64
+    n_resamples::Int64
+end
+
+const WSMC_ENOTPD = 3
+const FAM_NORMAL, FAM_HALFNORMAL, FAM_UNIFORM, FAM_MVNORMAL_ISO = Int32(0), Int32(1), Int32(2), Int32(3)
+const MEAN_AFFINE = Int32(0)
+const RESAMPLE_STRATIFIED = Int32(0)
+const PROPOSAL_RW, PROPOSAL_AUTORW = Int32(0), Int32(1)
+
+function check(rc::Integer)
+    rc == 0 && return nothing
+    msg = unsafe_string(ccall((:wsmc_last_error, libwsmc), Cstring, ()))
+    rc == WSMC_ENOTPD && throw(PosDefException(1))        # reference: cholesky in MvNormal(λΣ)
+    error("libwsmc error $rc: $msg")
+end
+
+# ---------------------------------------------------------------------------------------
+# the store (AbstractParticleStore, src/stores.jl:1-35)
+# ---------------------------------------------------------------------------------------
+mutable struct HipColumnStore <: WS.AbstractParticleStore
+    ctx::Ptr{Cvoid}
+    n::Int
+    names::Vector{Symbol}
+    ids::Dict{Symbol,Int32}
+    dims::Dict{Symbol,Int}
+    tmp::Int                       # counter for host-materialised temporaries
+end
+
+function HipColumnStore(n::Integer; seed::Integer=42, device::Integer=0)
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:wsmc_create, libwsmc), Cint, (Ptr{Ptr{Cvoid}}, Int64, Int32, UInt64),
+                h, n, device, seed % UInt64))
+    s = HipColumnStore(h[], Int(n), Symbol[], Dict{Symbol,Int32}(), Dict{Symbol,Int}(), 0)
+    finalizer(s) do s
+        s.ctx == C_NULL || ccall((:wsmc_destroy, libwsmc), Cint, (Ptr{Cvoid},), s.ctx)
+        s.ctx = C_NULL
+    end
+    return s
+end
+
+nparticles(s::HipColumnStore) = s.n
+hascol(s::HipColumnStore, name::Symbol) = haskey(s.ids, name)
+colnames(s::HipColumnStore) = s.names
+
+function column!(s::HipColumnStore, name::Symbol, dim::Integer)
+    haskey(s.ids, name) && return s.ids[name]
+    id = Ref{Int32}(0)
+    check(ccall((:wsmc_col_create, libwsmc), Cint, (Ptr{Cvoid}, Cstring, Int32, Ptr{Int32}),
+                s.ctx, String(name), dim, id))
+    s.ids[name] = id[]
+    s.dims[name] = dim
+    push!(s.names, name)
+    return id[]
+end
+
+"""Host copy of a column: `Vector{Float64}` (dim 1) or `Vector{Vector{Float64}}`."""
+function download(s::HipColumnStore, name::Symbol)
+    d = s.dims[name]
+    buf = Vector{Float64}(undef, d * s.n)
+    check(ccall((:wsmc_col_download, libwsmc), Cint, (Ptr{Cvoid}, Int32, Ptr{Float64}), s.ctx, s.ids[name], buf))
+    d == 1 && return buf
+    m = reshape(buf, s.n, d)                     # device layout is SoA [dim][N]
+    return [m[i, :] for i in 1:s.n]
+end
+
+function upload!(s::HipColumnStore, name::Symbol, v::AbstractVector)
+    d = eltype(v) <: AbstractVector ? length(first(v)) : 1
+    id = column!(s, name, d)
+    buf = d == 1 ? Vector{Float64}(v) : vec(permutedims(reduce(hcat, v)))   # -> [dim][N]
+    check(ccall((:wsmc_col_upload, libwsmc), Cint, (Ptr{Cvoid}, Int32, Ptr{Float64}), s.ctx, id, buf))
+end
+
+"""The generic write path (src/stores.jl:85-96): evaluated on the host, then uploaded."""
+function broadcast_setcol!(s::HipColumnStore, name::Symbol, f, args::Tuple)
+    upload!(s, name, f.(map(materialize_host, args)...))
+    return nothing
+end
+
+"""resample!(store, indices) with 1-based Julia indices (src/stores.jl:105-117)."""
+function resample!(s::HipColumnStore, indices::AbstractVector{<:Integer})
+    idx = Int32.(indices .- 1)
+    check(ccall((:wsmc_store_resample, libwsmc), Cint, (Ptr{Cvoid}, Ptr{Int32}), s.ctx, idx))
+    return nothing
+end
+
+# device proxies --------------------------------------------------------------------------
+"""Component `comp` (0-based) of device column `id` — or the whole column when `comp < 0`."""
+struct DeviceColumn <: AbstractVector{Float64}
+    store::HipColumnStore
+    name::Symbol
+    comp::Int32
+end
+Base.size(c::DeviceColumn) = (c.store.n,)
+Base.getindex(c::DeviceColumn, i::Int) = materialize_host(c)[i]   # generic host code: slow but correct
+
+"""Lazy affine form c0 + Σ coef·col[comp] (≤ 2 terms: the wsmc_operand shape)."""
+struct DeviceExpr
+    store::HipColumnStore
+    c0::Float64
+    terms::Vector{Tuple{Symbol,Int32,Float64}}
+end
+
+getcol(s::HipColumnStore, name::Symbol) = DeviceColumn(s, name, s.dims[name] == 1 ? Int32(0) : Int32(-1))
+
+struct DeviceStyle <: Broadcast.BroadcastStyle end
+Base.BroadcastStyle(::Type{DeviceColumn}) = DeviceStyle()
+Base.BroadcastStyle(::DeviceStyle, ::Broadcast.BroadcastStyle) = DeviceStyle()
+
+lift(x::DeviceColumn) = DeviceExpr(x.store, 0.0, [(x.name, x.comp, 1.0)])
+lift(x::DeviceExpr) = x
+lift(x::Base.RefValue{<:Real}) = x[]
+lift(x::Real) = x
+lift(bc::Broadcast.Broadcasted) = affine(bc.f, map(lift, bc.args)...)
+
+affine(::typeof(+), a::DeviceExpr, b::Real) = DeviceExpr(a.store, a.c0 + b, a.terms)
+affine(::typeof(+), a::Real, b::DeviceExpr) = affine(+, b, a)
+affine(::typeof(+), a::DeviceExpr, b::DeviceExpr) = DeviceExpr(a.store, a.c0 + b.c0, vcat(a.terms, b.terms))
+affine(::typeof(-), a::DeviceExpr, b::Real) = DeviceExpr(a.store, a.c0 - b, a.terms)
+affine(::typeof(-), a::Real, b::DeviceExpr) = affine(+, affine(*, -1.0, b), a)
+affine(::typeof(-), a::DeviceExpr, b::DeviceExpr) = affine(+, a, affine(*, -1.0, b))
+affine(::typeof(*), a::Real, b::DeviceExpr) = DeviceExpr(b.store, a * b.c0, [(n, c, a * k) for (n, c, k) in b.terms])
+affine(::typeof(*), a::DeviceExpr, b::Real) = affine(*, b, a)
+affine(::typeof(getindex), a::DeviceExpr, k::Integer) =                    # x[k] of a vector column
+    DeviceExpr(a.store, a.c0, [(n, Int32(k - 1), coef) for (n, _, coef) in a.terms])
+affine(f, args...) = nothing                                               # not affine: host path
+
+function Broadcast.materialize(bc::Broadcast.Broadcasted{DeviceStyle})
+    e = lift(bc)
+    e isa DeviceExpr && length(e.terms) <= 2 && return e
+    return Broadcast.materialize(Broadcast.broadcasted(bc.f, map(materialize_host, bc.args)...))
+end
+
+materialize_host(x) = x
+materialize_host(c::DeviceColumn) =
+    c.comp < 0 ? download(c.store, c.name) : getindex.(download(c.store, c.name), c.comp + 1)
+materialize_host(e::DeviceExpr) = e.c0 .+ sum(k .* materialize_host(DeviceColumn(e.store, n, c)) for (n, c, k) in e.terms)
+
+"""A `wsmc_operand` for one scalar argument; host vectors become temporary device columns."""
+function operand(s::HipColumnStore, x)
+    x isa Base.RefValue && return const_operand(x[])
+    x isa Real && return const_operand(x)
+    x isa DeviceColumn && (x = lift(x))
+    if x isa DeviceExpr
+        cols = [(s.ids[n], c < 0 ? Int32(0) : c, k) for (n, c, k) in x.terms]
+        pad = (Int32(-1), Int32(0), 0.0)
+        a = length(cols) >= 1 ? cols[1] : pad
+        b = length(cols) >= 2 ? cols[2] : pad
+        return WsmcOperand(x.c0, (a[1], b[1]), (a[2], b[2]), (a[3], b[3]))
+    end
+    s.tmp += 1                                    # host-materialised argument
+    name = Symbol("__wsmc_tmp", s.tmp)
+    upload!(s, name, collect(Float64, x))
+    return WsmcOperand(0.0, (s.ids[name], Int32(-1)), (Int32(0), Int32(0)), (1.0, 0.0))
+end
+
+"""Operands of a (possibly vector) argument, component by component."""
+function operands(s::HipColumnStore, x, dim::Integer)
+    if x isa Base.RefValue && x[] isa AbstractVector
+        v = x[]
+        return ntuple(k -> const_operand(k <= dim ? v[k] : 0.0), 4)
+    elseif x isa DeviceColumn && x.comp < 0
+        return ntuple(k -> operand(s, DeviceColumn(s, x.name, Int32(min(k, dim) - 1))), 4)
+    end
+    o = operand(s, x)
+    return (o, o, o, o)
+end
+
+# kernels recognised by identity (src/default_kernels.jl:83-102) --------------------------
+function device_dist(s::HipColumnStore, kernel, args)
+    K = WS.default_kernels
+    if kernel === K.Normal
+        mu, sigma = args
+        o = operand(s, mu)
+        return WsmcDist(FAM_NORMAL, MEAN_AFFINE, 1, 0, (o, o, o, o), operand(s, sigma), (0.0, 0.0))
+    elseif kernel === K.Uniform
+        a, b = map(x -> x isa Base.RefValue ? x[] : x, args)
+        z = const_operand(0.0)
+        return WsmcDist(FAM_UNIFORM, MEAN_AFFINE, 1, 0, (z, z, z, z), const_operand(1.0), (Float64(a), Float64(b)))
+    elseif kernel === K.MvNormal
+        mu, Sigma = args
+        S = Sigma isa Base.RefValue ? Sigma[] : Sigma
+        d = size(S, 1)
+        var = S[1, 1]
+        S == var * I(d) || return nothing                 # isotropic covariance only
+        return WsmcDist(FAM_MVNORMAL_ISO, MEAN_AFFINE, d, 0, operands(s, mu, d), const_operand(var), (0.0, 0.0))
+    end
+    return nothing
+end
+
+# ---------------------------------------------------------------------------------------
+# operators on SMCState{<:HipColumnStore}
+# ---------------------------------------------------------------------------------------
+const HipState = SMCState{<:HipColumnStore}
+
+function mirror_flags!(state::HipState)
+    st = Ref{WsmcState}()
+    check(ccall((:wsmc_get_state, libwsmc), Cint, (Ptr{Cvoid}, Ptr{WsmcState}), state.store.ctx, st))
+    state.resampled = st[].resampled != 0
+    state.weights_changed = st[].weights_changed != 0
+    return st[]
+end
+
+function apply!(t::WS.Assign, state::HipState)
+    s = state.store
+    v = t.argfn(state)
+    d = v isa DeviceColumn && v.comp < 0 ? s.dims[v.name] : 1
+    id = column!(s, t.lhs, d)
+    ops = operands(s, v, d)
+    check(ccall((:wsmc_assign, libwsmc), Cint, (Ptr{Cvoid}, Int32, Ptr{WsmcOperand}), s.ctx, id, Ref(ops)))
+    WS.advance!(state)
+end
+
+function apply!(t::WS.Sample, state::HipState)
+    s = state.store
+    args = t.argfn(state)
+    dist = t.kernel.weighter === nothing ? device_dist(s, t.kernel, args) : nothing
+    if dist === nothing                           # host path: reference apply!, weights round-trip
+        invoke(apply!, Tuple{WS.Sample,SMCState}, t, sync_weights!(state))
+        check(ccall((:wsmc_weights_upload, libwsmc), Cint, (Ptr{Cvoid}, Ptr{Float64}), s.ctx, state.weights))
+        return nothing
+    end
+    id = column!(s, t.lhs, dist.dim)
+    check(ccall((:wsmc_sample, libwsmc), Cint, (Ptr{Cvoid}, Int32, Ref{WsmcDist}), s.ctx, id, dist))
+    WS.advance!(state)
+end
+
+for (T, fn) in ((WS.Observe, :wsmc_observe), (WS.Weight, :wsmc_weight))
+    @eval function apply!(t::$T, state::HipState)
+        s = state.store
+        args = t.argfn(state)
+        dist = device_dist(s, t.kernel, args)
+        dist === nothing && error("WeightedSamplingHIP: kernel not supported on the device path")
+        x = $(T === WS.Observe ? :(t.lhsfn(state)) : :(Ref(0.0)))
+        check(ccall(($(QuoteNode(fn)), libwsmc), Cint, (Ptr{Cvoid}, Ref{WsmcDist}, Ptr{WsmcOperand}),
+                    s.ctx, dist, Ref(operands(s, x, dist.dim))))
+        state.weights_changed = true
+        WS.advance!(state)
+    end
+end
+
+function apply!(::WS.Resample, state::HipState)
+    r = Ref{Int32}(0)
+    e = Ref{Float64}(0.0)
+    check(ccall((:wsmc_resample, libwsmc), Cint, (Ptr{Cvoid}, Float64, Int32, Ptr{Int32}, Ptr{Float64}),
+                state.store.ctx, state.ess_perc_min, RESAMPLE_STRATIFIED, r, e))
+    mirror_flags!(state)
+    return nothing
+end
+
+"""`Move` with the built-in `RW` / `autoRW` proposals (recognised by identity)."""
+function apply!(t::WS.Move, state::HipState)
+    s = state.store
+    args = t.argfn(state)
+    kind = t.proposal === WS.autoRW ? PROPOSAL_AUTORW :
+           t.proposal === WS.RW ? PROPOSAL_RW :
+           error("WeightedSamplingHIP: only RW / autoRW proposals run on the device")
+    step = isempty(args) ? 1e-3 : Float64(WS._scalar_arg(args[1]))
+    bounds = length(args) >= 2 ? args[2] : nothing
+    d = length(t.targets)
+    ids = Int32[s.ids[c] for c in t.targets]
+    lo = hi = C_NULL
+    if bounds !== nothing
+        b = WS._normalize_bounds(bounds, d)
+        lo = Float64[x[1] for x in b]
+        hi = Float64[x[2] for x in b]
+    end
+    div = t.diversity_threshold === nothing ? NaN : Float64(t.diversity_threshold)
+    acc = Ref{Int64}(0)
+    check(ccall((:wsmc_move, libwsmc), Cint,
+                (Ptr{Cvoid}, Int32, Ptr{Int32}, Int32, Float64, Ptr{Float64}, Ptr{Float64}, Int32, Float64, Ptr{Int64}),
+                s.ctx, kind, ids, d, step, lo, hi, state.depth, div, acc))
+    return nothing
+end
+
+# weights live on the device; the host vector is a mirror refreshed on demand ------------
+function sync_weights!(state::HipState)
+    resize!(state.weights, state.store.n)
+    check(ccall((:wsmc_weights_download, libwsmc), Cint, (Ptr{Cvoid}, Ptr{Float64}),
+                state.store.ctx, state.weights))
+    return state
+end
+
+function log_evidence(state::HipState)
+    v = Ref{Float64}(0.0)
+    check(ccall((:wsmc_log_evidence, libwsmc), Cint, (Ptr{Cvoid}, Ptr{Float64}), state.store.ctx, v))
+    return v[]
+end
+
+"""
+    ssm2d_run!(state, obs; q_var=0.1, r_var=0.5, keep_history=true) -> log_evidence
+
+The fused fast path: one HIP-graph launch for the whole `run!` of examples/2D_ssm.jl:7-17
+on a fresh state (columns x_1..x_{T+1}, v, dv as the reference's store would hold them).
+"""
+function ssm2d_run!(state::HipState, obs::AbstractMatrix; x0=(0.0, 0.0), v0=(1.0, 0.0), q_var=0.1,
+                    r_var=0.5, keep_history=true)
+    T = size(obs, 1)
+    o = Vector{Float64}(vec(permutedims(Float64.(obs))))          # row-major T x 2
+    ev = Ref{Float64}(0.0)
+    check(ccall((:wsmc_ssm2d_run, libwsmc), Cint,
+                (Ptr{Cvoid}, Ptr{Float64}, Int32, Ptr{Float64}, Ptr{Float64}, Float64, Float64, Float64, Int32,
+                 Int32, Ptr{Float64}),
+                state.store.ctx, o, T, collect(Float64, x0), collect(Float64, v0), q_var, r_var,
+                state.ess_perc_min, RESAMPLE_STRATIFIED, keep_history, ev))
+    mirror_flags!(state)
+    return ev[]
+end
+
+end # module
