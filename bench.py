@@ -32,8 +32,9 @@ import numpy as np  # noqa: E402
 METRIC = json.loads((REPO / "BASELINE.json").read_text())["metric"] if (REPO / "BASELINE.json").exists() else \
     "particle-steps/sec (N_particles × T_steps / wall-s), 2D SSM bootstrap filter"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-PROP_BYTES_STEADY = 92         # propagate kernel, per particle, step t >= 2 after a resample
-PROP_BYTES_FIRST = 64          # step 1: x0/v0 are constants, weights read once
+PROP_BYTES_STEADY = 76         # propagate kernel, per particle, 2 <= t < T after a resample
+PROP_BYTES_FIRST = 48          # step 1: x0/v0 are constants (write x, v, w)
+PROP_BYTES_LAST_DV = 16        # dv is stored at the last step only
 STEP_BYTES = 104               # whole step algorithmic bytes
 
 
@@ -138,7 +139,7 @@ def main():
     # propagate-kernel algorithmic bytes per run (forced resampling: every step after t=1 reads
     # through ancestors; t = 1 starts from the constant x0/v0)
     forced = nres == T - 1
-    prop_bytes = N * (PROP_BYTES_FIRST + (T - 1) * PROP_BYTES_STEADY)
+    prop_bytes = N * (PROP_BYTES_FIRST + (T - 1) * PROP_BYTES_STEADY + PROP_BYTES_LAST_DV)
     prop_gbs = prop_bytes / (prop_ms * 1e-3) / 1e9 if prop_ms > 0 else None
     traffic = None
     tf = REPO / "profiles" / "pmc_propagate_bytes.json"

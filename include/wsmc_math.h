@@ -79,18 +79,8 @@ WSMC_HD uint64_t wsmc_d_to_u64_trunc(double x) {
     return m >> (-sh);
 }
 
-/* floor(w * 2^96) as u128 for 0 <= w <= 1 (evidence fixed point) */
-WSMC_HD wsmc_u128 wsmc_fix96(double w) {
-    uint64_t b = wsmc_d2bits(w);
-    if (b >> 63) return 0;
-    int e = (int)((b >> 52) & 0x7ff);
-    if (e == 0 || e == 0x7ff) return 0;          /* 0, subnormal (< 2^-96 anyway), inf/nan */
-    wsmc_u128 m = (wsmc_u128)((b & 0x000fffffffffffffULL) | 0x0010000000000000ULL);
-    int sh = e - 1075 + 96;                      /* w*2^96 = m * 2^sh */
-    if (sh >= 0) return sh > 75 ? (wsmc_u128)0 : (m << sh);
-    if (sh <= -64) return 0;
-    return m >> (-sh);
-}
+/* floor for doubles: IEEE-exact on both compilers (v_floor_f64 / roundsd) */
+WSMC_HD double wsmc_floor(double x) { return __builtin_floor(x); }
 
 /* order-preserving u64 encoding of f64 (for atomicMax); NaN canonicalised to +NaN (max) */
 WSMC_HD uint64_t wsmc_ord_enc(double x) {
@@ -181,6 +171,34 @@ WSMC_HD double wsmc_exp(double x) {
     double y = 1.0 - ((lo - (r * c) / (2.0 - c)) - hi);
     if (k == 0) return y;
     return wsmc_scalbn_small(y, k);
+}
+
+/*
+ * exp(x) for the Resample statistics, x = lw - M <= 0 (include/wsmc_math.h wsmc_qparts):
+ * Cody-Waite reduction by ln2 and a degree-13 Taylor polynomial in Horner form with
+ * explicit fma (IEEE-exact on v_fma_f64 and x86 FMA3), no division or branches on the
+ * value path. Returns 0 for x < -80 (exp(-80) < 2^-115, below every fixed point the
+ * statistics keep) and NaN for NaN. |error| ~ 2 ulp on [-80, 0].
+ */
+WSMC_HD double wsmc_expw(double x) {
+    if (!(x >= -80.0)) return wsmc_isnan(x) ? x : 0.0;
+    const double kd = wsmc_floor(x * 1.44269504088896338700e+00 + 0.5);
+    const double r = (x - kd * 6.93147180369123816490e-01) - kd * 1.90821492927058770002e-10;
+    double p = 1.6059043836821613e-10;                 /* 1/13! */
+    p = __builtin_fma(p, r, 2.08767569878681e-09);
+    p = __builtin_fma(p, r, 2.505210838544172e-08);
+    p = __builtin_fma(p, r, 2.755731922398589e-07);
+    p = __builtin_fma(p, r, 2.7557319223985893e-06);
+    p = __builtin_fma(p, r, 2.48015873015873e-05);
+    p = __builtin_fma(p, r, 0.0001984126984126984);
+    p = __builtin_fma(p, r, 0.001388888888888889);
+    p = __builtin_fma(p, r, 0.008333333333333333);
+    p = __builtin_fma(p, r, 0.041666666666666664);
+    p = __builtin_fma(p, r, 0.16666666666666666);
+    p = __builtin_fma(p, r, 0.5);
+    p = __builtin_fma(p, r, 1.0);
+    p = __builtin_fma(p, r, 1.0);
+    return p * wsmc_pow2i((int)kd);
 }
 
 WSMC_HD double wsmc_log(double x) {
@@ -380,8 +398,9 @@ WSMC_HD double wsmc_log_abs_jac(double z, double lo, double hi) {
 /* ------------------------------------------------------------------------- */
 /*
  * exp_norm/ess_perc/icdf (src/resampling.jl:13-77) on an integer CDF:
- *   q_i = floor(exp(lw_i - M) * 2^K),  K = 63 - ceil(log2 N)   =>  Q = sum q_i <= 2^63
- * Integer sums are associative, so the CDF, Q, sum q^2 (ESS) and the ancestors are
+ *   q_i = floor(expw(lw_i - M) * 2^K),  K = 63 - ceil(log2 N)   =>  Q = sum q_i <= 2^63
+ * (expw: the division-free exp above)
+ * Integer sums are associative, so the CDF, Q, the ESS sums and the ancestors are
  * identical for any reduction order, grid shape or shard count.
  */
 WSMC_HD int wsmc_qbits(uint64_t n) {
@@ -389,9 +408,32 @@ WSMC_HD int wsmc_qbits(uint64_t n) {
     return n <= 1 ? 63 : 63 - (64 - __builtin_clzll(n - 1));
 }
 WSMC_HD uint64_t wsmc_qweight(double lw, double M, int K) {
-    double e = wsmc_exp(lw - M);
+    double e = wsmc_expw(lw - M);
     if (!(e > 0.0)) return 0;            /* -inf weights, NaN */
     return wsmc_d_to_u64_trunc(e * wsmc_pow2i(K));
+}
+
+/*
+ * The three exact per-particle integers behind the Resample statistics (e = exp(lw - M)):
+ *   q   = floor(e * 2^K)                 CDF weight (above)
+ *   q21 = floor(e * 2^21)                ESS weight:  ESS% = (sum q21)^2 / (N sum q21^2)
+ *   wf  = floor(frac(e * 2^K) * 2^42)    so that  sum floor(e * 2^(K+42)) = Q * 2^42 + sum wf,
+ *                                        the fixed point of logsumexp (evidence, log-mean)
+ * Each is an exact integer in f64 (q21^2 < 2^43, wf < 2^42), so a device can sum them in
+ * f64 over 1024-particle tiles without rounding (< 2^53) and every reduction order,
+ * grid and shard layout gives the same bits.
+ */
+typedef struct { uint64_t q, q21, wf; } wsmc_qparts;
+WSMC_HD wsmc_qparts wsmc_qparts_of(double lw, double M, int K) {
+    wsmc_qparts p = {0, 0, 0};
+    double e = wsmc_expw(lw - M);
+    if (!(e > 0.0)) return p;
+    double s = e * wsmc_pow2i(K);
+    double qd = wsmc_floor(s);
+    p.q = wsmc_d_to_u64_trunc(qd);
+    p.wf = wsmc_d_to_u64_trunc(wsmc_floor((s - qd) * 4398046511104.0));   /* 2^42 */
+    p.q21 = wsmc_d_to_u64_trunc(wsmc_floor(e * 2097152.0));              /* 2^21 */
+    return p;
 }
 
 /*
@@ -410,22 +452,28 @@ WSMC_HD uint64_t wsmc_target(uint64_t n, uint32_t R, uint64_t Q, uint64_t N) {
 
 /* #{ n : x_n < c }  (monotone in c); scheme 0 = stratified, 1 = systematic.
  * ratio = N/Q as a double (any estimate works: the result is corrected exactly). */
+/* x * y exactly, for y < 2^32 (two 32x32->64 products; cheap on the device) */
+WSMC_HD wsmc_u128 wsmc_mul64x32(uint64_t x, uint32_t y) {
+    return ((wsmc_u128)((x >> 32) * (uint64_t)y) << 32) + (wsmc_u128)((x & 0xffffffffULL) * (uint64_t)y);
+}
 WSMC_HD uint64_t wsmc_rank_r(uint64_t c, uint64_t Q, uint64_t N, double ratio, int scheme,
                              uint64_t seed, uint64_t op, uint64_t slot_base) {
     if (c == 0) return 0;
     if (c >= Q) return N;
-    const wsmc_u128 cN = (wsmc_u128)c * (wsmc_u128)N;
-    /* n* = floor(c*N/Q) and rem = c*N - n*·Q in [0, Q): float estimate, exact correction */
+    /* N < 2^32 (a shard): every product below is 64 x 32 bits */
+    const wsmc_u128 cN = wsmc_mul64x32(c, (uint32_t)N);
+    /* n* = floor(c*N/Q) and rem = c*N - n*·Q in [0, Q): float estimate, exact correction
+       (the estimate only seeds the correction, so its rounding never shows in the result) */
     uint64_t ns = wsmc_d_to_u64_trunc(wsmc_u64_to_d(c) * ratio);
     if (ns > N) ns = N;
-    wsmc_u128 p = (wsmc_u128)ns * (wsmc_u128)Q;
+    wsmc_u128 p = wsmc_mul64x32(Q, (uint32_t)ns);
     while (p > cN) { --ns; p -= Q; }
     while (cN - p >= Q) { ++ns; p += Q; }
     if (ns >= N) return N;
     const uint64_t rem = (uint64_t)(cN - p);
     const uint32_t R = wsmc_strat_word(seed, op, scheme == 1 ? slot_base : slot_base + ns);
     /* x_{n*} < c  <=>  (n*·2^32 + R)·Q < c·N·2^32  <=>  R·Q < rem·2^32 */
-    return ns + (((wsmc_u128)R * (wsmc_u128)Q) < ((wsmc_u128)rem << 32) ? 1u : 0u);
+    return ns + (wsmc_mul64x32(Q, R) < ((wsmc_u128)rem << 32) ? 1u : 0u);
 }
 WSMC_HD uint64_t wsmc_rank(uint64_t c, uint64_t Q, uint64_t N, int scheme,
                            uint64_t seed, uint64_t op, uint64_t slot_base) {
@@ -458,12 +506,14 @@ WSMC_HD int wsmc_cholesky(const double* a, double* L, int d) {
 typedef struct {
     double M;          /* shard max log-weight (NaN if any NaN) */
     uint64_t Q;        /* sum q_i */
-    wsmc_u128 Q2;      /* sum q_i^2 */
-    wsmc_u128 W;       /* sum floor(exp(lw_i - M) * 2^96) */
+    uint64_t S1;       /* sum q21_i */
+    wsmc_u128 S2;      /* sum q21_i^2 */
+    wsmc_u128 Wf;      /* sum wf_i  (sum floor(e_i 2^(K+42)) = Q 2^42 + Wf) */
     uint64_t n;        /* shard size */
 } wsmc_shard_stats;
 
-/* ess_perc = (sum w)^2 / (N sum w^2) with w = exp_norm(weights) (src/resampling.jl:51-54) */
+/* ess_perc = (sum w)^2 / (N sum w^2) with w = exp_norm(weights) (src/resampling.jl:51-54),
+ * on the 21-bit quantised weights q21 of every shard, rescaled by exp(M_g - M) */
 WSMC_HD double wsmc_global_ess(const wsmc_shard_stats* st, int G) {
     double M = -WSMC_INF;
     uint64_t N = 0;
@@ -477,17 +527,20 @@ WSMC_HD double wsmc_global_ess(const wsmc_shard_stats* st, int G) {
     double sq = 0.0, sq2 = 0.0;
     for (int g = 0; g < G; ++g) {
         double f = wsmc_exp(st[g].M - M);
-        double sc = wsmc_pow2i(-wsmc_qbits(st[g].n));
-        double qd = wsmc_u64_to_d(st[g].Q), q2d = wsmc_u128_to_d(st[g].Q2);
-        sq = sq + (qd * sc) * f;
-        sq2 = sq2 + ((q2d * sc) * sc) * (f * f);
+        sq = sq + (wsmc_u64_to_d(st[g].S1) * 4.76837158203125e-07) * f;            /* 2^-21 */
+        sq2 = sq2 + (wsmc_u128_to_d(st[g].S2) * 2.2737367544323206e-13) * (f * f); /* 2^-42 */
     }
     return (sq * sq) / (wsmc_u64_to_d(N) * sq2);
 }
+/* sum exp(lw_i - M) of one shard, from its fixed point sum floor(e 2^(K+42)) */
+WSMC_HD double wsmc_shard_expsum(const wsmc_shard_stats* s) {
+    int K = wsmc_qbits(s->n);
+    wsmc_u128 W = ((wsmc_u128)s->Q << 42) + s->Wf;
+    return wsmc_u128_to_d(W) * wsmc_pow2i(-(K + 42));
+}
 /* logsumexp(shard weights) - log(n): the value every weight is reset to (src/transformers.jl:486-489) */
 WSMC_HD double wsmc_shard_mean(const wsmc_shard_stats* s) {
-    double S = wsmc_u128_to_d(s->W) * wsmc_pow2i(-96);
-    return (s->M + wsmc_log(S)) - wsmc_log(wsmc_u64_to_d(s->n));
+    return (s->M + wsmc_log(wsmc_shard_expsum(s))) - wsmc_log(wsmc_u64_to_d(s->n));
 }
 /* logsumexp(all weights) - log(N)  (src/utils.jl:21) */
 WSMC_HD double wsmc_global_log_evidence(const wsmc_shard_stats* st, int G) {
@@ -498,8 +551,7 @@ WSMC_HD double wsmc_global_log_evidence(const wsmc_shard_stats* st, int G) {
         N += st[g].n;
     }
     double S = 0.0;
-    for (int g = 0; g < G; ++g)
-        S = S + (wsmc_u128_to_d(st[g].W) * wsmc_pow2i(-96)) * wsmc_exp(st[g].M - M);
+    for (int g = 0; g < G; ++g) S = S + wsmc_shard_expsum(&st[g]) * wsmc_exp(st[g].M - M);
     return (M + wsmc_log(S)) - wsmc_log(wsmc_u64_to_d(N));
 }
 

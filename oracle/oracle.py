@@ -67,6 +67,7 @@ _SIG = {
     "or_score": (None, [_P, C.c_int32, _D]),
     "or_philox": (None, [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "or_exp": (C.c_double, [C.c_double]),
+    "or_expw": (C.c_double, [C.c_double]),
     "or_log": (C.c_double, [C.c_double]),
     "or_log1p": (C.c_double, [C.c_double]),
     "or_cos": (C.c_double, [C.c_double]),

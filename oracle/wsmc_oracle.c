@@ -269,13 +269,13 @@ static or_stats shard_stats(const double* lw, int64_t n, int K) {
         else if (lw[i] > M) M = lw[i];
     }
     s.M = nan ? WSMC_NAN : M;                    /* maximum() propagates NaN */
-    s.Q = 0; s.Q2 = 0; s.W = 0; s.n = (uint64_t)n;
+    s.Q = 0; s.S1 = 0; s.S2 = 0; s.Wf = 0; s.n = (uint64_t)n;
     for (int64_t i = 0; i < n; ++i) {
-        uint64_t q = wsmc_qweight(lw[i], s.M, K);
-        s.Q += q;
-        s.Q2 += (wsmc_u128)q * q;
-        double e = wsmc_exp(lw[i] - s.M);
-        s.W += wsmc_fix96(e);
+        wsmc_qparts p = wsmc_qparts_of(lw[i], s.M, K);
+        s.Q += p.q;
+        s.S1 += p.q21;
+        s.S2 += (wsmc_u128)p.q21 * p.q21;
+        s.Wf += p.wf;
     }
     return s;
 }
@@ -339,21 +339,23 @@ int or_resample(oracle* o, double ess_min, int32_t scheme, int32_t* resampled_ou
 }
 
 /* ---- one shard of a multi-process run: record exchange ------------------------------
- * record layout (8 x u64): M bits, Q, Q2 lo, Q2 hi, W lo, W hi, n, 0 — the payload the GPU
+ * record layout (8 x u64): M bits, Q, S1, S2 lo, S2 hi, Wf lo, Wf hi, n — the payload the GPU
  * ranks exchange with ncclAllGather each step (weightedsampling.jl_amd/csrc, ShardRec). */
 void or_shard_record(oracle* o, uint64_t* out) {
     or_stats s = shard_stats(o->w, o->N, wsmc_qbits((uint64_t)o->N));
     out[0] = wsmc_d2bits(s.M); out[1] = s.Q;
-    out[2] = (uint64_t)s.Q2; out[3] = (uint64_t)(s.Q2 >> 64);
-    out[4] = (uint64_t)s.W; out[5] = (uint64_t)(s.W >> 64);
-    out[6] = s.n; out[7] = 0;
+    out[2] = s.S1;
+    out[3] = (uint64_t)s.S2; out[4] = (uint64_t)(s.S2 >> 64);
+    out[5] = (uint64_t)s.Wf; out[6] = (uint64_t)(s.Wf >> 64);
+    out[7] = s.n;
 }
 static or_stats record_stats(const uint64_t* r) {
     or_stats s;
     s.M = wsmc_bits2d(r[0]); s.Q = r[1];
-    s.Q2 = ((wsmc_u128)r[3] << 64) | r[2];
-    s.W = ((wsmc_u128)r[5] << 64) | r[4];
-    s.n = r[6];
+    s.S1 = r[2];
+    s.S2 = ((wsmc_u128)r[4] << 64) | r[3];
+    s.Wf = ((wsmc_u128)r[6] << 64) | r[5];
+    s.n = r[7];
     return s;
 }
 /* Resample of this shard given every shard's record (rank order): global ESS decision,
@@ -584,6 +586,7 @@ void or_philox(const uint32_t* ctr, const uint32_t* key, uint32_t* out) {
     for (int k = 0; k < 4; ++k) out[k] = r.v[k];
 }
 double or_exp(double x) { return wsmc_exp(x); }
+double or_expw(double x) { return wsmc_expw(x); }
 double or_log(double x) { return wsmc_log(x); }
 double or_log1p(double x) { return wsmc_log1p(x); }
 double or_cos(double x) { return wsmc_cos(x); }

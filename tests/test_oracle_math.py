@@ -42,6 +42,17 @@ def test_exp_log_accuracy():
     assert L.or_log(1.0) == 0.0 and L.or_log(0.0) == -math.inf and math.isnan(L.or_log(-1.0))
 
 
+def test_expw_accuracy():
+    """The Resample-statistics exp (division-free, fma Horner): <= 2 ulp on [-80, 0]."""
+    g = np.random.default_rng(3)
+    xs = np.concatenate([g.uniform(-80, 0, 40000), g.uniform(-1, 0, 20000), -np.logspace(-300, 1.9, 2000),
+                         [0.0, -0.0, -80.0, -1e-300]])
+    e = np.array([L.or_expw(x) for x in xs])
+    assert np.max(_ulps(e, np.exp(xs))) <= 2.0
+    assert L.or_expw(0.0) == 1.0 and L.or_expw(-80.0000001) == 0.0 and L.or_expw(-math.inf) == 0.0
+    assert math.isnan(L.or_expw(math.nan))
+
+
 def test_trig_and_log1p():
     g = np.random.default_rng(1)
     zs = g.uniform(-500, 500, 20000)

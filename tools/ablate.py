@@ -9,7 +9,7 @@ c = wsmc.Context(N, seed=1)
 obs = wsmc.models.ssm2d_data(20)
 for ess in (1.0, 0.0):
     c.ssm2d_run(obs, ess_perc_min=ess, keep_history=False)
-    for k, modes in ((0, range(5)), (1, [0]), (2, range(4))):
+    for k, modes in ((0, (0, 1, 4)), (1, [0]), (2, range(4))):
         for m in modes:
             c.debug_kernel_bench(k, m, 5)
             print(f"ess {ess} kernel {k} mode {m}: {c.debug_kernel_bench(k, m, 100):.2f} us", flush=True)

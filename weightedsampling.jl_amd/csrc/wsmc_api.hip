@@ -122,8 +122,9 @@ static wsmc_shard_stats host_record_stats(const ShardRecord& r) {
     wsmc_shard_stats st;
     st.M = wsmc_ord_dec(r.menc);
     st.Q = r.Q;
-    st.Q2 = ((wsmc_u128)r.q2hi << 64) | r.q2lo;
-    st.W = ((wsmc_u128)r.whi << 64) | r.wlo;
+    st.S1 = r.s1;
+    st.S2 = ((wsmc_u128)r.s2hi << 64) | r.s2lo;
+    st.Wf = ((wsmc_u128)r.wfhi << 64) | r.wflo;
     st.n = r.n;
     return st;
 }
@@ -742,7 +743,9 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
         }
         a.v_prev = t > 1 ? vbuf[t & 1] : nullptr;
         a.v_next = vbuf[(t + 1) & 1];
-        a.dv = c->cols[p.coldv].back;
+        // the reference's dv column holds the latest draw only: earlier steps' draws are
+        // overwritten before anything reads them, so only step T stores it
+        a.dv = t == T ? c->cols[p.coldv].back : nullptr;
         a.w = c->w;
         a.anc_prev = t > 1 ? c->anc_log + (size_t)(t - 2) * N : nullptr;
         a.dec_prev = t > 1 ? c->run_dec + (t - 1) : nullptr;

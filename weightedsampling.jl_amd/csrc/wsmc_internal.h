@@ -18,7 +18,8 @@ constexpr int kBlock = 256;            // threads per workgroup (4 waves of 64)
 constexpr int kItems = 8;              // particles per thread in the tile kernels
 constexpr int kTile = kBlock * kItems; // 2048 particles per tile (canonical reduction tile)
 constexpr int kSlots = 64;             // max-accumulator slots (blockIdx % 64)
-constexpr int kRsBlock = 1024;         // threads of the weight-statistics / reduce workgroups
+constexpr int kRsBlock = 1024;         // threads of the reduce workgroup
+constexpr int kSumBlock = 256;         // threads of the weight-statistics workgroup (4 particles each)
 constexpr int kRsTile = 1024;          // particles per resample tile
 constexpr int kScanBlock = 256;        // threads of the ancestor-fill workgroup (4 particles each)
 constexpr int kRsChunk = 2048;         // ancestor slots per fill task
@@ -36,13 +37,14 @@ struct MaxSlots {
 struct ShardRecord {
     unsigned long long menc;   // ordered encoding of the shard max log-weight
     unsigned long long Q;      // sum q_i
-    unsigned long long q2lo, q2hi;  // sum q_i^2 (u128)
-    unsigned long long wlo, whi;    // sum floor(exp(lw - M) 2^96) (u128)
+    unsigned long long s1;     // sum q21_i (ESS weights, include/wsmc_math.h wsmc_qparts)
+    unsigned long long s2lo, s2hi;  // sum q21_i^2 (u128)
+    unsigned long long wflo, wfhi;  // sum wf_i (u128): sum floor(e 2^(K+42)) = Q 2^42 + Wf
     unsigned long long n;      // shard size
-    unsigned long long pad;
 };
 
-constexpr int kPart = 9;   // per-tile partials: sum q, 4 limbs of sum q^2, 4 limbs of sum fix96
+constexpr int kPart = 4;      // per-tile partials: sum q, sum q21, sum q21^2, sum wf (all exact)
+constexpr int kRedPart = 6;   // reduce-kernel parts: Q, S1, S2 lo32/hi, Wf lo32/hi
 
 // Resample outcome for one invocation (one step of a fused run).
 struct Decision {
@@ -222,7 +224,7 @@ struct Ssm2dArgs {
     double* x_next;            // [2][N]
     const double* v_prev;      // [2][N]
     double* v_next;            // [2][N]
-    double* dv;                // [2][N]
+    double* dv;                // [2][N]; written at the last step only (the column keeps the latest draw)
     double* w;                 // [N]
     const int32_t* anc_prev;   // [N] ancestors of step t-1
     const Decision* dec_prev;  // decision of step t-1 (nullptr at t = 1)

@@ -11,6 +11,7 @@
 // 4 wave64s; tile kernels own 2048 particles (8 per thread).
 #include <hip/hip_ext.h>
 
+#include <cstdlib>
 #include "wsmc_internal.h"
 
 namespace wsmc {
@@ -196,15 +197,15 @@ static_assert(kSlots == 64, "one lane per max slot");
 __device__ __forceinline__ double wave_slots_max(const MaxSlots* ms) {
     return wsmc_ord_dec(wave_max_u64(ms->v[threadIdx.x & 63][0]));
 }
-// exact integer block sums of kPart values through LDS (transpose, two levels)
-template <int NT>
-__device__ __forceinline__ void block_sum_parts(const u64 (&acc)[kPart], u64 (*red)[NT], u64 (*red2)[16],
-                                                u64* out /* kPart, valid in threads < kPart */) {
+// exact integer block sums of P values through LDS (transpose, two levels)
+template <int NT, int P>
+__device__ __forceinline__ void block_sum_parts(const u64 (&acc)[P], u64 (*red)[NT], u64 (*red2)[16],
+                                                u64* out /* P, valid in threads < P */) {
     const int th = threadIdx.x;
 #pragma unroll
-    for (int k = 0; k < kPart; ++k) red[k][th] = acc[k];
+    for (int k = 0; k < P; ++k) red[k][th] = acc[k];
     __syncthreads();
-    if (th < kPart * 16) {
+    if (th < P * 16) {
         const int k = th >> 4, seg = th & 15;
         u64 t = 0;
 #pragma unroll 8
@@ -212,7 +213,7 @@ __device__ __forceinline__ void block_sum_parts(const u64 (&acc)[kPart], u64 (*r
         red2[k][seg] = t;
     }
     __syncthreads();
-    if (th < kPart) {
+    if (th < P) {
         u64 t = 0;
 #pragma unroll
         for (int j = 0; j < 16; ++j) t += red2[th][j];
@@ -220,44 +221,92 @@ __device__ __forceinline__ void block_sum_parts(const u64 (&acc)[kPart], u64 (*r
     }
 }
 
-// MODE (diagnostics only; production = 0): 1 = no exp, 2 = no q^2/fix96 partials,
-// 3 = no block reduction, 4 = load/store only
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) v = v + __shfl_xor(v, off, 64);
+    return v;
+}
+
+// Weight statistics of one 1024-particle tile (256 threads x 4 particles, coalesced):
+// q (stored for the fill), and the tile sums of q, q21, q21^2, wf (include/wsmc_math.h
+// wsmc_qparts). q21, q21^2 and wf are exact integers in f64 and their tile sums stay
+// below 2^53, so f64 accumulation is exact and order-free — no 128-bit arithmetic per
+// particle. MODE (diagnostics only; production = 0): 1 = no exp, 4 = load/store only.
 template <int MODE>
-__global__ __launch_bounds__(kRsBlock) void k_rs_sums_t(const double* __restrict__ w, int64_t N,
-                                                        const MaxSlots* __restrict__ ms, u64* __restrict__ tilep,
-                                                        u64* __restrict__ qbuf) {
-    __shared__ u64 red[kPart][kRsBlock];
-    __shared__ u64 red2[kPart][16];
-    __shared__ u64 outp[kPart];
+__global__ __launch_bounds__(kSumBlock) void k_rs_sums_t(const double* __restrict__ w, int64_t N,
+                                                         const MaxSlots* __restrict__ ms, u64* __restrict__ tilep,
+                                                         u64* __restrict__ qbuf) {
+    constexpr int IT = kRsTile / kSumBlock;
+    __shared__ double s_f[3][kSumBlock / 64];
+    __shared__ u64 s_q[kSumBlock / 64];
     const int th = threadIdx.x;
-    const int64_t i = (int64_t)blockIdx.x * kRsTile + th;
-    const double lw = i < N ? w[i] : -WSMC_INF;
-    const double M = MODE == 4 ? 0.0 : wave_slots_max(ms);
-    const int K = wsmc_qbits((uint64_t)N);
-    const double e = (MODE == 1 || MODE == 4) ? lw - M : wsmc_exp(lw - M);
-    const u64 q = MODE == 4 ? (u64)wsmc_d2bits(e) : ((e > 0.0) ? (u64)wsmc_d_to_u64_trunc(e * wsmc_pow2i(K)) : 0ull);
-    if (i < N) qbuf[i] = q;
-    if (MODE == 4) return;
-    const wsmc_u128 q2 = MODE == 2 ? (wsmc_u128)q : (wsmc_u128)q * q;
-    const wsmc_u128 f = MODE == 2 ? (wsmc_u128)q : wsmc_fix96(e);
-    const u64 acc[kPart] = {q, (uint32_t)q2, (uint32_t)(q2 >> 32), (uint32_t)(q2 >> 64), (uint32_t)(q2 >> 96),
-                            (uint32_t)f, (uint32_t)(f >> 32), (uint32_t)(f >> 64), (uint32_t)(f >> 96)};
-    if (MODE == 3) {
-        u64 x = 0;
-        for (int k = 0; k < kPart; ++k) x ^= acc[k];
-        if (x == 0x123456789ull) tilep[0] = x;
-        return;
+    const int64_t base = (int64_t)blockIdx.x * kRsTile;
+    double lw[IT];
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        const int64_t i = base + (int64_t)k * kSumBlock + th;
+        lw[k] = i < N ? w[i] : -WSMC_INF;
     }
-    block_sum_parts<kRsBlock>(acc, red, red2, outp);
-    if (th < kPart) tilep[(int64_t)blockIdx.x * kPart + th] = outp[th];
+    const double M = MODE == 4 ? 0.0 : wave_slots_max(ms);
+    const double sK = wsmc_pow2i(wsmc_qbits((uint64_t)N));
+    u64 Q = 0;
+    double S1 = 0.0, S2 = 0.0, WF = 0.0;
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        const int64_t i = base + (int64_t)k * kSumBlock + th;
+        if (MODE == 4) {
+            if (i < N) qbuf[i] = (u64)wsmc_d2bits(lw[k]);
+            continue;
+        }
+        const double e = MODE == 1 ? (lw[k] > M - 1.0 ? 1.0 : 0.5) : wsmc_expw(lw[k] - M);
+        u64 q = 0;
+        double q21 = 0.0, wf = 0.0;
+        if (e > 0.0) {
+            const double sc = e * sK;
+            const double qd = wsmc_floor(sc);
+            q = (u64)qd;                                        // exact integer <= 2^63
+            wf = wsmc_floor((sc - qd) * 4398046511104.0);      // 2^42
+            q21 = wsmc_floor(e * 2097152.0);                   // 2^21
+        }
+        if (i < N) qbuf[i] = q;
+        Q += q;
+        S1 = S1 + q21;
+        S2 = S2 + q21 * q21;
+        WF = WF + wf;
+    }
+    if (MODE == 4) return;
+    Q = wave_sum_u64(Q);
+    S1 = wave_sum_f64(S1);
+    S2 = wave_sum_f64(S2);
+    WF = wave_sum_f64(WF);
+    const int wv = th >> 6;
+    if ((th & 63) == 0) {
+        s_q[wv] = Q;
+        s_f[0][wv] = S1; s_f[1][wv] = S2; s_f[2][wv] = WF;
+    }
+    __syncthreads();
+    if (th < kPart) {
+        u64 t = 0;
+        if (th == 0) {
+#pragma unroll
+            for (int v = 0; v < kSumBlock / 64; ++v) t += s_q[v];
+        } else {
+            double f = 0.0;
+#pragma unroll
+            for (int v = 0; v < kSumBlock / 64; ++v) f = f + s_f[th - 1][v];
+            t = (u64)f;                                         // exact: < 2^53
+        }
+        tilep[(int64_t)blockIdx.x * kPart + th] = t;
+    }
 }
 
 __device__ __forceinline__ wsmc_shard_stats record_stats(const ShardRecord& r) {
     wsmc_shard_stats st;
     st.M = wsmc_ord_dec(r.menc);
     st.Q = r.Q;
-    st.Q2 = ((wsmc_u128)r.q2hi << 64) | r.q2lo;
-    st.W = ((wsmc_u128)r.whi << 64) | r.wlo;
+    st.S1 = r.s1;
+    st.S2 = ((wsmc_u128)r.s2hi << 64) | r.s2lo;
+    st.Wf = ((wsmc_u128)r.wfhi << 64) | r.wflo;
     st.n = r.n;
     return st;
 }
@@ -277,12 +326,11 @@ __device__ void decide_records(const ShardRecord* recs, int world, int rank, dou
     if (nan) M = WSMC_NAN;
     double sq = 0.0, sq2 = 0.0;
     for (int g = 0; g < world; ++g) {
+        // the arithmetic of wsmc_global_ess, streamed over the records
         const wsmc_shard_stats st = record_stats(recs[g]);
         const double f = wsmc_exp(st.M - M);
-        const double sc = wsmc_pow2i(-wsmc_qbits(st.n));
-        const double qd = wsmc_u64_to_d(st.Q), q2d = wsmc_u128_to_d(st.Q2);
-        sq = sq + (qd * sc) * f;
-        sq2 = sq2 + ((q2d * sc) * sc) * (f * f);
+        sq = sq + (wsmc_u64_to_d(st.S1) * 4.76837158203125e-07) * f;
+        sq2 = sq2 + (wsmc_u128_to_d(st.S2) * 2.2737367544323206e-13) * (f * f);
     }
     const double ess = (sq * sq) / (wsmc_u64_to_d(N) * sq2);
     const int rs = ess < ess_min;
@@ -299,27 +347,33 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_reduce(const MaxSlots* __restri
                                                         u64* __restrict__ tileOff, ShardRecord* rec,
                                                         int decide_local, double ess_min, Decision* dec,
                                                         FillPlan plan) {
-    __shared__ u64 red[kPart][kRsBlock];
-    __shared__ u64 red2[kPart][16];
-    __shared__ u64 tot[kPart];
+    __shared__ u64 red[kRedPart][kRsBlock];
+    __shared__ u64 red2[kRedPart][16];
+    __shared__ u64 tot[kRedPart];
     __shared__ u64 s_w[kRsBlock / 64];
     constexpr int kHeavyTasks = 4, kHeavyQueue = 256;
     __shared__ int s_heavy[kHeavyQueue][3];
     __shared__ int s_nheavy;
+    __shared__ u64 s_L[kRsBlock + 1];
     const int th = threadIdx.x;
+    // the max slots are read first so their latency overlaps the partials' loads
+    const u64 mslot = th < kSlots ? ms->v[th][0] : 0ull;
     // thread th owns the contiguous tiles [b0, b1): loads each tile's partials once
     const int64_t per = (ntiles + kRsBlock - 1) / kRsBlock;
-    const int64_t b0 = (int64_t)th * per, b1 = b0 + per < ntiles ? b0 + per : ntiles;
-    u64 acc[kPart] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const int64_t b0 = (int64_t)th * per < ntiles ? (int64_t)th * per : ntiles;
+    const int64_t b1 = b0 + per < ntiles ? b0 + per : ntiles;
+    u64 t4[kPart] = {0, 0, 0, 0};
     for (int64_t b = b0; b < b1; ++b)
 #pragma unroll
-        for (int k = 0; k < kPart; ++k) acc[k] += tilep[b * kPart + k];
-    block_sum_parts<kRsBlock>(acc, red, red2, tot);
+        for (int k = 0; k < kPart; ++k) t4[k] += tilep[b * kPart + k];
+    // Q and S1 totals fit u64; S2 and Wf are summed as 32-bit limbs into u128
+    const u64 acc[kRedPart] = {t4[0], t4[1], t4[2] & 0xffffffffull, t4[2] >> 32, t4[3] & 0xffffffffull,
+                               t4[3] >> 32};
+    block_sum_parts<kRsBlock, kRedPart>(acc, red, red2, tot);
     u64 total;
     u64 pre = block_excl_scan_u64<kRsBlock / 64>(acc[0], s_w, &total);
     // tile offsets and the first slot each tile owns: L_b = rank(tileOff_b) (Q = this shard's
-    // total); each thread also ranks its successor's first offset, so the per-tile slot
-    // counts need no cross-thread exchange
+    // total); a thread's successor tile start comes from its neighbour through LDS
     const bool planned = plan.tileL != nullptr;   // uniform: log-evidence reuses this kernel unplanned
     const u64 Q = total;
     const uint64_t opx = planned ? op_eff(plan.op, plan.op_dev) : 0ull;
@@ -328,32 +382,47 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_reduce(const MaxSlots* __restri
         return Q ? wsmc_rank_r(c, Q, (uint64_t)N, ratio, plan.scheme, plan.seed, opx, (uint64_t)plan.slot_base)
                  : 0ull;
     };
+    u64 Lfirst = (u64)N;
+    {
+        u64 c = pre;
+        for (int64_t b = b0; b < b1; ++b) {
+            tileOff[b] = c;
+            if (planned) {
+                const u64 Lb = rank_of(c);
+                plan.tileL[b] = Lb;
+                if (b == b0) Lfirst = Lb;
+            }
+            c += tilep[b * kPart];
+        }
+    }
     int nt = 0;
-    u64 Lb = (planned && b0 < b1) ? rank_of(pre) : 0ull;
-    for (int64_t b = b0; b < b1; ++b) {
-        tileOff[b] = pre;
-        pre += tilep[b * kPart];
-        if (planned) {
-            const u64 Ln = b + 1 == ntiles ? (u64)N : rank_of(pre);
-            plan.tileL[b] = Lb;
-            nt += (int)((Ln - Lb + kRsChunk - 1) / kRsChunk);
-            Lb = Ln;
+    if (planned) {
+        s_L[th] = Lfirst;
+        if (th == 0) s_L[kRsBlock] = (u64)N;
+        __syncthreads();
+        const u64 Lend = s_L[th + 1];   // first slot of tile b1 (N past the last tile)
+        for (int64_t b = b0; b < b1; ++b) {
+            const u64 hi = b + 1 < b1 ? plan.tileL[b + 1] : Lend;   // own tiles: written above
+            const int k = (int)((hi - plan.tileL[b] + kRsChunk - 1) / kRsChunk);
+            nt += k > 1 ? k - 1 : 0;   // the first chunk of every tile is block b of the fill grid
         }
     }
     u64 tt = 0;
     if (planned) {
         if (th == 0) plan.tileL[ntiles] = (u64)N;
-        // fill tasks: ceil(slots / kRsChunk) per tile; exclusive scan -> taskOff; task -> tile map
+        // overflow fill tasks: the chunks after a tile's first; exclusive scan -> taskOff;
+        // overflow task -> tile map
         int tpre = (int)block_excl_scan_u64<kRsBlock / 64>((u64)nt, s_w, &tt);
-        const u64 Lend = Lb;   // first slot of tile b1 (ranked above)
+        const u64 Lend = s_L[th + 1];
         // a tile with many tasks (a dominant particle) is queued and its map entries are
         // written by the whole block, so one thread never loops over N / kRsChunk entries
         if (th == 0) s_nheavy = 0;
         __syncthreads();
         for (int64_t b = b0; b < b1; ++b) {
-            const u64 lo = plan.tileL[b];                    // written by this thread
+            const u64 lo = plan.tileL[b];
             const u64 hi = b + 1 < b1 ? plan.tileL[b + 1] : Lend;
-            const int k = (int)((hi - lo + kRsChunk - 1) / kRsChunk);
+            const int kc = (int)((hi - lo + kRsChunk - 1) / kRsChunk);
+            const int k = kc > 1 ? kc - 1 : 0;
             plan.taskOff[b] = tpre;
             int q = -1;
             if (k > kHeavyTasks) {
@@ -370,19 +439,17 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_reduce(const MaxSlots* __restri
             for (int j = th; j < s_heavy[e][2]; j += kRsBlock) plan.taskTile[s_heavy[e][1] + j] = s_heavy[e][0];
     }
     if (th < 64) {
-        const u64 menc = wave_max_u64(ms->v[th][0]);
+        const u64 menc = wave_max_u64(mslot);
         if (th == 0) {
             ShardRecord r;
             r.menc = menc;
             r.Q = tot[0];
-            const wsmc_u128 Q2 = (wsmc_u128)tot[1] + ((wsmc_u128)tot[2] << 32) + ((wsmc_u128)tot[3] << 64) +
-                                 ((wsmc_u128)tot[4] << 96);
-            const wsmc_u128 W = (wsmc_u128)tot[5] + ((wsmc_u128)tot[6] << 32) + ((wsmc_u128)tot[7] << 64) +
-                                ((wsmc_u128)tot[8] << 96);
-            r.q2lo = (u64)Q2; r.q2hi = (u64)(Q2 >> 64);
-            r.wlo = (u64)W; r.whi = (u64)(W >> 64);
+            r.s1 = tot[1];
+            const wsmc_u128 S2 = (wsmc_u128)tot[2] + ((wsmc_u128)tot[3] << 32);
+            const wsmc_u128 Wf = (wsmc_u128)tot[4] + ((wsmc_u128)tot[5] << 32);
+            r.s2lo = (u64)S2; r.s2hi = (u64)(S2 >> 64);
+            r.wflo = (u64)Wf; r.wfhi = (u64)(Wf >> 64);
             r.n = (u64)N;
-            r.pad = 0;
             *rec = r;
             if (dec) {
                 dec->ntasks = (int32_t)tt;
@@ -397,30 +464,30 @@ __global__ void k_rs_decide(const ShardRecord* recs, int world, int rank, double
     if (threadIdx.x == 0) decide_records(recs, world, rank, ess_min, dec);
 }
 
-// Ancestor fill, one block per task (<= kRsChunk consecutive slots of one tile).
-// ancestor(slot) = smallest m with C_m > x_slot (the icdf merge, src/resampling.jl:13-26):
-// with hi_m = rank(C_m) (monotone), the ancestor of slot n of tile b is the first particle
-// m of the tile with hi_m > n, found by binary search in LDS. Work per block is bounded
-// whatever the weight skew (a dominant particle only adds tasks).
-// MODE (diagnostics only; production = 0): 1 = no rank (cheap estimate), 2 = no fill,
-// 3 = scan only
+constexpr int kOverflowBlocks = 256;   // fill blocks serving overflow chunks (grid-stride)
+
+constexpr int kScatterMax = 8;          // slots a thread writes for one particle before the block helps
+
+struct FillLds {
+    u64 uw[kScanBlock / 64];
+    u64 last[kScanBlock / 64];
+    int nheavy;
+    int heavy[kRsChunk / kScatterMax + 1][3];   // particle (tile-local), first slot, end slot (chunk-local)
+};
+
+// fill chunk j of tile b (block-uniform arguments; ends with a barrier so LDS can be reused).
+// Particle m owns the slots [hi_{m-1}, hi_m) with hi_m = rank(C_m); each thread ranks its 4
+// (blocked) particles and scatters their slots within the chunk. A particle owning more
+// than kScatterMax slots of the chunk is queued and filled by the whole block, so a lane
+// never loops long whatever the weights.
 template <int MODE>
-__global__ __launch_bounds__(kScanBlock) void k_rs_scan_t(int64_t N, const ShardRecord* __restrict__ rec,
-                                                          const Decision* __restrict__ dec, FillPlan plan,
-                                                          const u64* __restrict__ tileOff,
-                                                          const u64* __restrict__ qbuf, int32_t* __restrict__ anc) {
+__device__ __forceinline__ void fill_chunk(int64_t N, int b, int j, u64 Q, const FillPlan& plan, uint64_t opx,
+                                           const u64* __restrict__ tileOff, const u64* __restrict__ qbuf,
+                                           int32_t* __restrict__ anc, FillLds& sh) {
     constexpr int IT = kRsTile / kScanBlock;   // 4 particles per thread, blocked
-    __shared__ u64 s_uw[kScanBlock / 64];
-    __shared__ uint32_t hiL[kRsTile];
-    if (!dec->resampled) return;
-    const int t = blockIdx.x;
-    if (t >= dec->ntasks) return;
-    const int th = threadIdx.x;
-    const int b = plan.taskTile[t];
-    const int j = t - plan.taskOff[b];
+    const int th = threadIdx.x, lane = th & 63, wv = th >> 6;
     const u64 L = plan.tileL[b], H = plan.tileL[b + 1];
-    const u64 cs = L + (u64)j * kRsChunk;
-    const u64 ce = cs + kRsChunk < H ? cs + kRsChunk : H;
+    const u64 off = tileOff[b];
     const int64_t base = (int64_t)b * kRsTile;
     u64 q[IT];
     u64 tsum = 0;
@@ -430,44 +497,96 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_scan_t(int64_t N, const Shard
         q[k] = i < N ? qbuf[i] : 0ull;
         tsum += q[k];
     }
-    const u64 off = tileOff[b];
-    const u64 Q = rec->Q;
-    const uint64_t opx = op_eff(plan.op, plan.op_dev);
+    const u64 cs = L + (u64)j * kRsChunk;
+    const u64 ce = cs + kRsChunk < H ? cs + kRsChunk : H;
+    if (cs >= ce) return;                          // uniform
     const double ratio = wsmc_u64_to_d((uint64_t)N) / wsmc_u64_to_d(Q);
+    if (th == 0) sh.nheavy = 0;
     u64 tot;
-    const u64 pre = block_excl_scan_u64<kScanBlock / 64>(tsum, s_uw, &tot);
+    const u64 pre = block_excl_scan_u64<kScanBlock / 64>(tsum, sh.uw, &tot);
     if (MODE == 3) {
         if (pre == 0x123456789ull) anc[0] = 1;
         return;
     }
     u64 C = off + pre;
-    u64 prev = L;   // rank(C) of the previous particle (a particle with q = 0 owns no slots)
+    u64 hi[IT];
+    u64 prev = L;
 #pragma unroll
     for (int k = 0; k < IT; ++k) {
         C += q[k];
-        u64 h = prev;
+        u64 h = prev;                              // a particle with q = 0 owns no slots
         if (q[k] || k == 0) h = MODE == 1 ? (u64)(wsmc_u64_to_d(C) * ratio)
                                 : wsmc_rank_r(C, Q, (uint64_t)N, ratio, plan.scheme, plan.seed, opx,
                                               (uint64_t)plan.slot_base);
         if (MODE == 1 && h > H) h = H;
         if (MODE == 1 && h < L) h = L;
-        hiL[th * IT + k] = (uint32_t)(h - L);
+        hi[k] = h;
         prev = h;
     }
+    // first slot of the thread's first particle = hi of the previous thread's last particle
+    u64 lo = __shfl_up(hi[IT - 1], 1, 64);
+    if (lane == 63) sh.last[wv] = hi[IT - 1];
+    __syncthreads();
+    if (lane == 0) lo = wv > 0 ? sh.last[wv - 1] : L;
     if (MODE == 2) {
-        if (hiL[th * IT] == 0xffffffffu) anc[0] = 1;
+        if (lo == 0x123456789ull) anc[0] = 1;
         return;
     }
-    __syncthreads();
-    // hiL is non-decreasing (a zero-q particle repeats its predecessor's rank), so the
-    // first m with hiL[m] > r is found by a branch-free binary search
-    for (u64 n = cs + th; n < ce; n += kScanBlock) {
-        const uint32_t r = (uint32_t)(n - L);
-        int m = 0;
 #pragma unroll
-        for (int step = kRsTile / 2; step > 0; step >>= 1)
-            if (hiL[m + step - 1] <= r) m += step;
-        anc[n] = (int32_t)(base + m);
+    for (int k = 0; k < IT; ++k) {
+        const u64 a = lo > cs ? lo : cs;
+        const u64 e = hi[k] < ce ? hi[k] : ce;
+        const int32_t m = (int32_t)(base + th * IT + k);
+        if (a < e) {
+            if (e - a > (u64)kScatterMax) {
+                const int x = atomicAdd(&sh.nheavy, 1);
+                sh.heavy[x][0] = m;
+                sh.heavy[x][1] = (int)(a - cs);
+                sh.heavy[x][2] = (int)(e - cs);
+            } else {
+                for (u64 n = a; n < e; ++n) anc[n] = m;
+            }
+        }
+        lo = hi[k];
+    }
+    __syncthreads();
+    const int nh = sh.nheavy;
+    for (int x = 0; x < nh; ++x) {
+        const int m = sh.heavy[x][0];
+        for (int n = sh.heavy[x][1] + th; n < sh.heavy[x][2]; n += kScanBlock) anc[cs + n] = m;
+    }
+    __syncthreads();
+}
+
+// Ancestor fill (the icdf merge, src/resampling.jl:13-26): ancestor(slot n) = smallest m
+// with C_m > x_n, i.e. particle m owns the slots [rank(C_{m-1}), rank(C_m)) with
+// rank(c) = #{n : x_n < c}. Block b < ntiles fills the first chunk
+// (<= kRsChunk slots) of tile b: no lookup, every load independent. kOverflowBlocks more
+// blocks take, grid-stride, the later chunks of tiles owning more than kRsChunk slots
+// (a dominant particle adds chunks, never a long loop in one block).
+// MODE (diagnostics only; production = 0): 1 = no rank (cheap estimate), 2 = no fill,
+// 3 = scan only
+template <int MODE>
+__global__ __launch_bounds__(kScanBlock) void k_rs_scan_t(int64_t N, const ShardRecord* __restrict__ rec,
+                                                          const Decision* __restrict__ dec, FillPlan plan,
+                                                          const u64* __restrict__ tileOff,
+                                                          const u64* __restrict__ qbuf, int32_t* __restrict__ anc) {
+    __shared__ FillLds sh;
+    const int t = blockIdx.x;
+    const int ntiles = (int)((N + kRsTile - 1) / kRsTile);
+    const int rs = dec->resampled;
+    const u64 Q = rec->Q;
+    const uint64_t opx = op_eff(plan.op, plan.op_dev);
+    if (t < ntiles) {
+        if (!rs) return;
+        fill_chunk<MODE>(N, t, 0, Q, plan, opx, tileOff, qbuf, anc, sh);
+        return;
+    }
+    if (!rs) return;
+    const int ntasks = dec->ntasks;
+    for (int o = t - ntiles; o < ntasks; o += kOverflowBlocks) {
+        const int b = plan.taskTile[o];
+        fill_chunk<MODE>(N, b, 1 + o - plan.taskOff[b], Q, plan, opx, tileOff, qbuf, anc, sh);
     }
 }
 
@@ -652,13 +771,23 @@ __device__ __forceinline__ double aff2(double a, double b) {
     return v;
 }
 
+// One step of the fused 2D SSM (examples/2D_ssm.jl:11-16) for PPT particles per thread
+// (strided by the block size, so every load and store stays coalesced): gather x_t, v
+// through the previous step's ancestors, draw dv, x_{t+1} = x_t + v, v += dv, observe,
+// and fold the block's max log-weight into one of 64 line-strided slots.
+template <int PPT>
 __global__ __launch_bounds__(kBlock) void k_ssm2d_prop(Ssm2dArgs a) {
     __shared__ u64 lds4[4];
     const int64_t N = a.N;
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const bool rs = a.t > 1 && a.dec_prev->resampled;
+    const double mean = rs ? a.dec_prev->mean : 0.0;
+    const uint64_t op_dv = a.op_dev[0] + 3ull * (uint64_t)(a.t - 1);
+    const double o0 = a.obs[2 * (a.t - 1)], o1 = a.obs[2 * (a.t - 1) + 1];
     u64 menc = 0;
-    if (i < N) {
-        const bool rs = a.t > 1 && a.dec_prev->resampled;
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+        const int64_t i = ((int64_t)blockIdx.x * PPT + k) * kBlock + threadIdx.x;
+        if (i >= N) continue;
         const int64_t src = rs ? (int64_t)a.anc_prev[i] : i;
         double x0, x1, v0, v1;
         if (a.t == 1) {
@@ -670,27 +799,26 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_prop(Ssm2dArgs a) {
         // x{t+1} .= x{t} + v
         const double xn0 = aff2(x0, v0), xn1 = aff2(x1, v1);
         // dv ~ MvNormal([0,0], q*I)
-        const uint64_t op_dv = a.op_dev[0] + 3ull * (uint64_t)(a.t - 1);
         double z0, z1;
         wsmc_normal_pair(wsmc_rng_block(a.seed, op_dv, (uint64_t)(a.goff + i), 0u), &z0, &z1);
         const double dv0 = 0.0 + a.q_sd * z0, dv1 = 0.0 + a.q_sd * z1;
         // v .= v + dv
         const double vn0 = aff2(v0, dv0), vn1 = aff2(v1, dv1);
         // o => MvNormal(x{t+1}, r*I)
-        const double o0 = a.obs[2 * (a.t - 1)], o1 = a.obs[2 * (a.t - 1) + 1];
         const double m0 = 0.0 + 1.0 * xn0, m1 = 0.0 + 1.0 * xn1;
         double s = 0.0;
         const double d0 = o0 - m0, d1 = o1 - m1;
         s = s + d0 * d0;
         s = s + d1 * d1;
         const double lp = -(a.c0 + s / a.r_var) * 0.5;
-        const double wb = rs ? a.dec_prev->mean : a.w[i];
+        const double wb = rs ? mean : a.w[i];
         const double wn = wb + lp;
         a.x_next[i] = xn0; a.x_next[N + i] = xn1;
         a.v_next[i] = vn0; a.v_next[N + i] = vn1;
-        a.dv[i] = dv0; a.dv[N + i] = dv1;
+        if (a.dv) { a.dv[i] = dv0; a.dv[N + i] = dv1; }
         a.w[i] = wn;
-        menc = wsmc_ord_enc(wn);
+        const u64 e = wsmc_ord_enc(wn);
+        menc = e > menc ? e : menc;
     }
     menc = block_max_u64(menc, lds4);
     if (threadIdx.x == 0) atomic_max_filtered(&a.ms->v[blockIdx.x % kSlots][0], menc);
@@ -734,7 +862,6 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_final(Ssm2dFinal f) {
 static inline dim3 grid_for(int64_t N) { return dim3((unsigned)((N + kBlock - 1) / kBlock)); }
 static inline dim3 tiles_for(int64_t N) { return dim3((unsigned)((N + kTile - 1) / kTile)); }
 static inline dim3 rs_tiles_for(int64_t N) { return dim3((unsigned)((N + kRsTile - 1) / kRsTile)); }
-static_assert(kRsChunk % kRsBlock == 0, "chunk is a multiple of the block");
 
 hipError_t launch_assign(hipStream_t s, double* out, int dim, const wsmc_operand* expr,
                          double* const* cols, int64_t N) {
@@ -778,7 +905,7 @@ hipError_t launch_rs_max(hipStream_t s, const double* w, int64_t N, MaxSlots* ms
 }
 hipError_t launch_rs_sums(hipStream_t s, const double* w, int64_t N, const MaxSlots* ms, u64* tilep, u64* qbuf,
                           hipEvent_t e0, hipEvent_t e1) {
-    return launch_timed(k_rs_sums_t<0>, rs_tiles_for(N), dim3(kRsBlock), s, e0, e1, w, N, ms, tilep, qbuf);
+    return launch_timed(k_rs_sums_t<0>, rs_tiles_for(N), dim3(kSumBlock), s, e0, e1, w, N, ms, tilep, qbuf);
 }
 hipError_t launch_rs_reduce(hipStream_t s, const MaxSlots* ms, const u64* tilep, int64_t N, u64* tileOff,
                             ShardRecord* rec, int decide_local, double ess_min, Decision* dec,
@@ -794,8 +921,9 @@ hipError_t launch_rs_decide(hipStream_t s, const ShardRecord* recs, int world, i
     hipLaunchKernelGGL(k_rs_decide, dim3(1), dim3(64), 0, s, recs, world, rank, ess_min, dec);
     return hipGetLastError();
 }
+// one block per tile (its first chunk) + grid-stride overflow blocks
 static inline dim3 fill_tasks_for(int64_t N) {
-    return dim3((unsigned)((N + kRsTile - 1) / kRsTile + N / kRsChunk + 1));
+    return dim3((unsigned)((N + kRsTile - 1) / kRsTile + kOverflowBlocks));
 }
 hipError_t launch_rs_scan(hipStream_t s, int64_t N, const ShardRecord* rec, const Decision* dec,
                           const FillPlan& plan, const u64* tileOff, const u64* qbuf, int32_t* anc, hipEvent_t e0,
@@ -811,15 +939,13 @@ hipError_t debug_kernel_bench(hipStream_t s, int kernel, int mode, int iters, co
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    const dim3 g = rs_tiles_for(N), blk(kRsBlock), gs = fill_tasks_for(N), bs(kScanBlock);
+    const dim3 g = rs_tiles_for(N), blk(kSumBlock), gs = fill_tasks_for(N), bs(kScanBlock);
     hipEventRecord(a, s);
     for (int it = 0; it < iters; ++it) {
         if (kernel == 0) {
             switch (mode) {
                 case 0: hipLaunchKernelGGL(k_rs_sums_t<0>, g, blk, 0, s, w, N, ms, tilep, qbuf); break;
                 case 1: hipLaunchKernelGGL(k_rs_sums_t<1>, g, blk, 0, s, w, N, ms, tilep, qbuf); break;
-                case 2: hipLaunchKernelGGL(k_rs_sums_t<2>, g, blk, 0, s, w, N, ms, tilep, qbuf); break;
-                case 3: hipLaunchKernelGGL(k_rs_sums_t<3>, g, blk, 0, s, w, N, ms, tilep, qbuf); break;
                 default: hipLaunchKernelGGL(k_rs_sums_t<4>, g, blk, 0, s, w, N, ms, tilep, qbuf); break;
             }
         } else if (kernel == 1) {
@@ -908,8 +1034,25 @@ hipError_t launch_count_unique(hipStream_t s, const u64* keys, int64_t N, u64* c
     hipLaunchKernelGGL(k_count_unique, dim3((unsigned)nb), dim3(kBlock), 0, s, keys, N, count);
     return hipGetLastError();
 }
+static int prop_ppt() {
+    static int v = [] {
+        const char* e = getenv("WSMC_PROP_PPT");   // diagnostics: particles per thread
+        const int x = e ? atoi(e) : 1;
+        return x == 2 || x == 4 ? x : 1;
+    }();
+    return v;
+}
 hipError_t launch_ssm2d_propagate(hipStream_t s, const Ssm2dArgs& a, hipEvent_t e0, hipEvent_t e1) {
-    return launch_timed(k_ssm2d_prop, grid_for(a.N), dim3(kBlock), s, e0, e1, a);
+    switch (prop_ppt()) {
+        case 2:
+            return launch_timed(k_ssm2d_prop<2>, dim3((unsigned)((a.N + 2 * kBlock - 1) / (2 * kBlock))),
+                                dim3(kBlock), s, e0, e1, a);
+        case 4:
+            return launch_timed(k_ssm2d_prop<4>, dim3((unsigned)((a.N + 4 * kBlock - 1) / (4 * kBlock))),
+                                dim3(kBlock), s, e0, e1, a);
+        default:
+            return launch_timed(k_ssm2d_prop<1>, grid_for(a.N), dim3(kBlock), s, e0, e1, a);
+    }
 }
 // bounded spin on the 100 MHz constant clock (always exits): queue-filling delay for
 // instrumented runs
