@@ -48,7 +48,7 @@ def test_ssm2d_statements(gpu_available, N, ess, scheme):
     assert g.log_evidence() == o.log_evidence()
 
 
-@pytest.mark.parametrize("N", [1024, 5000])
+@pytest.mark.parametrize("N", [1024, 5001])
 @pytest.mark.parametrize("ess", [1.0, 0.5])
 @pytest.mark.parametrize("keep", [True, False])
 def test_ssm2d_fused_matches_statements(gpu_available, N, ess, keep):
@@ -64,6 +64,7 @@ def test_ssm2d_fused_matches_statements(gpu_available, N, ess, keep):
         for n in ("v", "dv"):
             np.testing.assert_array_equal(g.col_download(g.col_find(n)), o.col_download(o.col_find(n)))
         np.testing.assert_array_equal(g.weights_download(), o.weights_download())
+    np.testing.assert_array_equal(g.last_ancestors(), o.last_ancestors())
     assert ev == o.log_evidence()
     # a second run on the same state continues the RNG stream / weights like run! would
     ev2 = g.ssm2d_run(obs, ess_perc_min=ess, keep_history=keep)

@@ -168,7 +168,6 @@ int wsmc_create(wsmc_ctx** out, int64_t n_particles, int32_t device, uint64_t se
     ALLOC(c->tmp, sizeof(double) * 4 * c->N);
     ALLOC(c->tilep, sizeof(unsigned long long) * kPart * c->nrstiles);
     ALLOC(c->tileOff, sizeof(unsigned long long) * c->nrstiles);
-    ALLOC(c->tileL, sizeof(unsigned long long) * (c->nrstiles + 1));
     ALLOC(c->taskOff, sizeof(int32_t) * c->nrstiles);
     ALLOC(c->taskTile, sizeof(int32_t) * (c->nrstiles + n_particles / kRsChunk + 1));
     ALLOC(c->mslots, sizeof(MaxSlots));
@@ -210,7 +209,7 @@ int wsmc_destroy(wsmc_ctx* c) {
         (void)hipFree(col.front);
         (void)hipFree(col.back);
     }
-    void* bufs[] = {c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->tileL, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount,
+    void* bufs[] = {c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount,
                     c->d_colptr, c->run_params, c->d_tape, c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs,
                     c->vscratch, c->xscratch};
     for (void* p : bufs)
@@ -387,7 +386,7 @@ static int exchange_recs(wsmc_ctx* c, ShardRecord* recs);
 // max (unless the caller's kernel already filled the slots), sums, reduce, [exchange + decide]
 static FillPlan fill_plan(wsmc_ctx* c, int scheme, uint64_t op, const uint64_t* op_dev) {
     FillPlan p;
-    p.tileL = c->tileL;
+    p.tilep = c->tilep;
     p.taskOff = c->taskOff;
     p.taskTile = c->taskTile;
     p.scheme = scheme;
@@ -675,6 +674,9 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
 }
 
 // ---- fused 2D SSM runner --------------------------------------------------------------
+// ancestor-log rows are padded to 16 B so every row start is aligned for paired loads
+static inline int64_t anc_stride(int64_t N) { return (N + 3) & ~(int64_t)3; }
+
 static int ensure_run_buffers(wsmc_ctx* c, int32_t T) {
     if (c->T_alloc >= T && c->run_rec) return WSMC_OK;
     WSMC_HIP(hipStreamSynchronize(c->stream));
@@ -684,7 +686,7 @@ static int ensure_run_buffers(wsmc_ctx* c, int32_t T) {
     WSMC_HIP(hipMalloc(&c->run_max, sizeof(MaxSlots) * (T + 1)));
     WSMC_HIP(hipMalloc(&c->run_rec, sizeof(ShardRecord) * (T + 1) * kMaxWorld));
     WSMC_HIP(hipMalloc(&c->run_dec, sizeof(Decision) * (T + 1)));
-    WSMC_HIP(hipMalloc(&c->anc_log, sizeof(int32_t) * (size_t)T * c->N));
+    WSMC_HIP(hipMalloc(&c->anc_log, sizeof(int32_t) * (size_t)T * anc_stride(c->N)));
     WSMC_HIP(hipMalloc(&c->obs, sizeof(double) * 2 * (T + 1)));
     if (!c->vscratch) WSMC_HIP(hipMalloc(&c->vscratch, sizeof(double) * 2 * c->N));
     if (!c->xscratch) WSMC_HIP(hipMalloc(&c->xscratch, sizeof(double) * 2 * c->N));
@@ -747,7 +749,7 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
         // overwritten before anything reads them, so only step T stores it
         a.dv = t == T ? c->cols[p.coldv].back : nullptr;
         a.w = c->w;
-        a.anc_prev = t > 1 ? c->anc_log + (size_t)(t - 2) * N : nullptr;
+        a.anc_prev = t > 1 ? c->anc_log + (size_t)(t - 2) * anc_stride(N) : nullptr;
         a.dec_prev = t > 1 ? c->run_dec + (t - 1) : nullptr;
         MaxSlots* ms = c->run_max + t;
         ShardRecord* recs = c->run_rec + (size_t)t * c->world;
@@ -760,7 +762,7 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
                                        ev ? evs : nullptr);
         if (r) return r;
         WSMC_HIP(launch_rs_scan(c->stream, N, recs + c->rank, c->run_dec + t, plan, c->tileOff, c->qbuf,
-                                c->anc_log + (size_t)(t - 1) * N, E(k0 + 6), E(k0 + 7)));
+                                c->anc_log + (size_t)(t - 1) * anc_stride(N), E(k0 + 6), E(k0 + 7)));
     }
     Ssm2dFinal f;
     f.T = T;
@@ -777,6 +779,7 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
     f.dv_out = c->cols[p.coldv].front;
     f.w = c->w;
     f.anc_log = c->anc_log;
+    f.anc_stride = anc_stride(N);
     f.dec = c->run_dec;
     WSMC_HIP(launch_ssm2d_finalize(c->stream, f, E(8 * T), E(8 * T + 1)));
     return WSMC_OK;
@@ -919,6 +922,13 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
     WSMC_HIP(hipMemcpyAsync(hdec.data(), c->run_dec, sizeof(Decision) * (T + 1), hipMemcpyDeviceToHost, c->stream));
     WSMC_HIP(hipStreamSynchronize(c->stream));
     if (temp_tables) (void)hipFree(temp_tables);
+    // wsmc_last_ancestors reports the run's last resample, as after the statement sequence
+    for (int t = T; t >= 1; --t)
+        if (hdec[t].resampled) {
+            WSMC_HIP(hipMemcpyAsync(c->anc, c->anc_log + (size_t)(t - 1) * anc_stride(c->N), sizeof(int32_t) * c->N,
+                                    hipMemcpyDeviceToDevice, c->stream));
+            break;
+        }
 
     // bookkeeping identical to issuing the statements one by one
     int32_t nres = 0;

@@ -105,9 +105,8 @@ struct wsmc_ctx {
     double* tmp = nullptr;                  // [4N]
     unsigned long long* tilep = nullptr;    // [nrstiles * kPart] per-tile integer partials
     unsigned long long* tileOff = nullptr;  // [nrstiles] exclusive prefix of the tiles' sum q
-    unsigned long long* tileL = nullptr;    // [nrstiles + 1] first ancestor slot owned by each tile
-    int32_t* taskOff = nullptr;             // [nrstiles] first fill task of each tile
-    int32_t* taskTile = nullptr;            // [nrstiles + N / kRsChunk + 1] tile of each fill task
+    int32_t* taskOff = nullptr;             // [nrstiles] first overflow fill task of each tile
+    int32_t* taskTile = nullptr;            // [N / kRsChunk + nrstiles + 1] tile of each overflow task
     unsigned long long* qbuf = nullptr;     // [N] integer weights q_i of the last weight-statistics pass
     double* tilepart = nullptr;             // [16 * ntiles] canonical-sum tile partials
     wsmc::MaxSlots* mslots = nullptr;       // [1] max slots of one generic resample / evidence
@@ -169,7 +168,7 @@ hipError_t launch_rs_sums(hipStream_t s, const double* w, int64_t N, const MaxSl
                           unsigned long long* tilep, unsigned long long* qbuf,
                           hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 struct FillPlan {          // ancestor-fill task planning (in the reduce kernel)
-    unsigned long long* tileL;
+    const unsigned long long* tilep;   // per-tile partials (sum q first)
     int32_t* taskOff;
     int32_t* taskTile;
     int scheme;
@@ -220,13 +219,14 @@ struct Ssm2dArgs {
     double q_sd;               // sqrt(q_var)
     double r_var;
     double c0;                 // -(2 log 2pi + 2 log r_var)/2 (host-computed, shared math)
-    const double* x_prev;      // [2][N] x_t (pre-resample numbering of step t-1), unused at t = 1
-    double* x_next;            // [2][N]
-    const double* v_prev;      // [2][N]
-    double* v_next;            // [2][N]
-    double* dv;                // [2][N]; written at the last step only (the column keeps the latest draw)
+    // working buffers are particle-major pairs [N][2] (the output columns are SoA [2][N])
+    const double* x_prev;      // x_t (pre-resample numbering of step t-1), unused at t = 1
+    double* x_next;
+    const double* v_prev;
+    double* v_next;
+    double* dv;                // written at the last step only (the column keeps the latest draw)
     double* w;                 // [N]
-    const int32_t* anc_prev;   // [N] ancestors of step t-1
+    const int32_t* anc_prev;   // [N] ancestors of step t-1 (8-B aligned row)
     const Decision* dec_prev;  // decision of step t-1 (nullptr at t = 1)
     MaxSlots* ms;              // this step's max slots
 };
@@ -246,7 +246,8 @@ struct Ssm2dFinal {
     const double* dv_work;
     double* dv_out;
     double* w;
-    const int32_t* anc_log;    // [T][N]
+    const int32_t* anc_log;    // [T][anc_stride]
+    int64_t anc_stride;        // row stride of the ancestor log (N rounded up to 4)
     const Decision* dec;       // [T+1], index t
 };
 hipError_t launch_ssm2d_finalize(hipStream_t s, const Ssm2dFinal& f, hipEvent_t e0 = nullptr,

@@ -16,6 +16,8 @@
 
 namespace wsmc {
 
+typedef double d2 __attribute__((ext_vector_type(2)));
+
 typedef unsigned long long u64;
 
 // ------------------------------------------------------------------------------------
@@ -342,7 +344,18 @@ __device__ void decide_records(const ShardRecord* recs, int world, int rank, dou
 }
 
 // one block: shard totals, tile offsets, the ancestor-fill task plan and (one GPU) the decision
-__global__ __launch_bounds__(kRsBlock) void k_rs_reduce(const MaxSlots* __restrict__ ms,
+// overflow chunks (past the first) a tile with integer weight sum qb may need
+__device__ __forceinline__ int ovf_chunks(u64 qb, double ratio) {
+    if (qb == 0) return 0;
+    const double bound = wsmc_u64_to_d(qb) * ratio + 3.0;   // >= cnt_b + 1 (estimate error << 1)
+    const int k = (int)(bound * (1.0 / kRsChunk));          // floor(bound / chunk)
+    return k;                                               // ceil(bound / chunk) - 1 <= k
+}
+
+// MODE (diagnostics only; production = 0): 1 = no fill plan, 2 = no decision,
+// 3 = partial sums + record only
+template <int MODE>
+__global__ __launch_bounds__(kRsBlock) void k_rs_reduce_t(const MaxSlots* __restrict__ ms,
                                                         const u64* __restrict__ tilep, int64_t ntiles, int64_t N,
                                                         u64* __restrict__ tileOff, ShardRecord* rec,
                                                         int decide_local, double ess_min, Decision* dec,
@@ -354,7 +367,6 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_reduce(const MaxSlots* __restri
     constexpr int kHeavyTasks = 4, kHeavyQueue = 256;
     __shared__ int s_heavy[kHeavyQueue][3];
     __shared__ int s_nheavy;
-    __shared__ u64 s_L[kRsBlock + 1];
     const int th = threadIdx.x;
     // the max slots are read first so their latency overlaps the partials' loads
     const u64 mslot = th < kSlots ? ms->v[th][0] : 0ull;
@@ -372,57 +384,32 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_reduce(const MaxSlots* __restri
     block_sum_parts<kRsBlock, kRedPart>(acc, red, red2, tot);
     u64 total;
     u64 pre = block_excl_scan_u64<kRsBlock / 64>(acc[0], s_w, &total);
-    // tile offsets and the first slot each tile owns: L_b = rank(tileOff_b) (Q = this shard's
-    // total); a thread's successor tile start comes from its neighbour through LDS
-    const bool planned = plan.tileL != nullptr;   // uniform: log-evidence reuses this kernel unplanned
-    const u64 Q = total;
-    const uint64_t opx = planned ? op_eff(plan.op, plan.op_dev) : 0ull;
-    const double ratio = Q ? wsmc_u64_to_d((uint64_t)N) / wsmc_u64_to_d(Q) : 0.0;
-    auto rank_of = [&](u64 c) -> u64 {
-        return Q ? wsmc_rank_r(c, Q, (uint64_t)N, ratio, plan.scheme, plan.seed, opx, (uint64_t)plan.slot_base)
-                 : 0ull;
-    };
-    u64 Lfirst = (u64)N;
+    // tile offsets; overflow fill tasks sized from the tile sums alone: a tile owns
+    // cnt_b <= Q_b N / Q + 2 slots (stratified and systematic targets are one per 1/N
+    // stratum), so ceil((Q_b N / Q + 3) / kRsChunk) - 1 chunks past the first always
+    // suffice (a chunk found empty exits). Fill blocks rank their own tile's boundaries.
+    const bool planned = MODE != 1 && MODE != 3 && plan.taskOff != nullptr;   // log-evidence: unplanned
+    const double ratio = total ? wsmc_u64_to_d((uint64_t)N) / wsmc_u64_to_d(total) : 0.0;
+    int nt = 0;
     {
         u64 c = pre;
         for (int64_t b = b0; b < b1; ++b) {
             tileOff[b] = c;
-            if (planned) {
-                const u64 Lb = rank_of(c);
-                plan.tileL[b] = Lb;
-                if (b == b0) Lfirst = Lb;
-            }
-            c += tilep[b * kPart];
-        }
-    }
-    int nt = 0;
-    if (planned) {
-        s_L[th] = Lfirst;
-        if (th == 0) s_L[kRsBlock] = (u64)N;
-        __syncthreads();
-        const u64 Lend = s_L[th + 1];   // first slot of tile b1 (N past the last tile)
-        for (int64_t b = b0; b < b1; ++b) {
-            const u64 hi = b + 1 < b1 ? plan.tileL[b + 1] : Lend;   // own tiles: written above
-            const int k = (int)((hi - plan.tileL[b] + kRsChunk - 1) / kRsChunk);
-            nt += k > 1 ? k - 1 : 0;   // the first chunk of every tile is block b of the fill grid
+            const u64 qb = b1 - b0 == 1 ? t4[0] : tilep[b * kPart];
+            c += qb;
+            if (planned) nt += ovf_chunks(qb, ratio);
         }
     }
     u64 tt = 0;
     if (planned) {
-        if (th == 0) plan.tileL[ntiles] = (u64)N;
-        // overflow fill tasks: the chunks after a tile's first; exclusive scan -> taskOff;
-        // overflow task -> tile map
+        // overflow task -> tile map; exclusive scan of the per-tile counts -> taskOff
         int tpre = (int)block_excl_scan_u64<kRsBlock / 64>((u64)nt, s_w, &tt);
-        const u64 Lend = s_L[th + 1];
         // a tile with many tasks (a dominant particle) is queued and its map entries are
         // written by the whole block, so one thread never loops over N / kRsChunk entries
         if (th == 0) s_nheavy = 0;
         __syncthreads();
         for (int64_t b = b0; b < b1; ++b) {
-            const u64 lo = plan.tileL[b];
-            const u64 hi = b + 1 < b1 ? plan.tileL[b + 1] : Lend;
-            const int kc = (int)((hi - lo + kRsChunk - 1) / kRsChunk);
-            const int k = kc > 1 ? kc - 1 : 0;
+            const int k = ovf_chunks(b1 - b0 == 1 ? t4[0] : tilep[b * kPart], ratio);
             plan.taskOff[b] = tpre;
             int q = -1;
             if (k > kHeavyTasks) {
@@ -453,7 +440,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_reduce(const MaxSlots* __restri
             *rec = r;
             if (dec) {
                 dec->ntasks = (int32_t)tt;
-                if (decide_local) decide_records(&r, 1, 0, ess_min, dec);
+                if (decide_local && MODE != 2 && MODE != 3) decide_records(&r, 1, 0, ess_min, dec);
             }
         }
     }
@@ -469,6 +456,7 @@ constexpr int kOverflowBlocks = 256;   // fill blocks serving overflow chunks (g
 constexpr int kScatterMax = 8;          // slots a thread writes for one particle before the block helps
 
 struct FillLds {
+    u64 LH[2];
     u64 uw[kScanBlock / 64];
     u64 last[kScanBlock / 64];
     int nheavy;
@@ -486,7 +474,6 @@ __device__ __forceinline__ void fill_chunk(int64_t N, int b, int j, u64 Q, const
                                            int32_t* __restrict__ anc, FillLds& sh) {
     constexpr int IT = kRsTile / kScanBlock;   // 4 particles per thread, blocked
     const int th = threadIdx.x, lane = th & 63, wv = th >> 6;
-    const u64 L = plan.tileL[b], H = plan.tileL[b + 1];
     const u64 off = tileOff[b];
     const int64_t base = (int64_t)b * kRsTile;
     u64 q[IT];
@@ -497,13 +484,23 @@ __device__ __forceinline__ void fill_chunk(int64_t N, int b, int j, u64 Q, const
         q[k] = i < N ? qbuf[i] : 0ull;
         tsum += q[k];
     }
-    const u64 cs = L + (u64)j * kRsChunk;
-    const u64 ce = cs + kRsChunk < H ? cs + kRsChunk : H;
-    if (cs >= ce) return;                          // uniform
     const double ratio = wsmc_u64_to_d((uint64_t)N) / wsmc_u64_to_d(Q);
+    // the tile's slot range [L, H) = [rank(off), rank(off + Q_b)), ranked by two threads
+    // while the others scan; the scan's barrier publishes them
+    if (th < 2) {
+        const u64 c = th == 0 ? off : off + plan.tilep[(int64_t)b * kPart];
+        sh.LH[th] = wsmc_rank_r(c, Q, (uint64_t)N, ratio, plan.scheme, plan.seed, opx, (uint64_t)plan.slot_base);
+    }
     if (th == 0) sh.nheavy = 0;
     u64 tot;
     const u64 pre = block_excl_scan_u64<kScanBlock / 64>(tsum, sh.uw, &tot);
+    const u64 L = sh.LH[0], H = sh.LH[1];
+    const u64 cs = L + (u64)j * kRsChunk;
+    const u64 ce = cs + kRsChunk < H ? cs + kRsChunk : H;
+    if (cs >= ce) {                                // uniform; keep LDS reuse ordered
+        __syncthreads();
+        return;
+    }
     if (MODE == 3) {
         if (pre == 0x123456789ull) anc[0] = 1;
         return;
@@ -550,10 +547,11 @@ __device__ __forceinline__ void fill_chunk(int64_t N, int b, int j, u64 Q, const
         lo = hi[k];
     }
     __syncthreads();
+    // queued particles: one per wave at a time, the wave's lanes striding over its slots
     const int nh = sh.nheavy;
-    for (int x = 0; x < nh; ++x) {
+    for (int x = wv; x < nh; x += kScanBlock / 64) {
         const int m = sh.heavy[x][0];
-        for (int n = sh.heavy[x][1] + th; n < sh.heavy[x][2]; n += kScanBlock) anc[cs + n] = m;
+        for (int n = sh.heavy[x][1] + lane; n < sh.heavy[x][2]; n += 64) anc[cs + n] = m;
     }
     __syncthreads();
 }
@@ -771,11 +769,16 @@ __device__ __forceinline__ double aff2(double a, double b) {
     return v;
 }
 
-// One step of the fused 2D SSM (examples/2D_ssm.jl:11-16) for PPT particles per thread
-// (strided by the block size, so every load and store stays coalesced): gather x_t, v
-// through the previous step's ancestors, draw dv, x_{t+1} = x_t + v, v += dv, observe,
-// and fold the block's max log-weight into one of 64 line-strided slots.
-template <int PPT>
+// One step of the fused 2D SSM (examples/2D_ssm.jl:11-16) for two adjacent particles per
+// thread. The run's working state is particle-major pairs ([N][2]: x_t, v, dv), so each
+// gather through an ancestor is one 16-B load and every store (x, v, w pairs) is 16 B per
+// lane. Gathers x_t, v through the previous step's ancestors, draws dv, x_{t+1} = x_t + v,
+// v += dv, observes, and folds the block's max log-weight into one of 64 line-strided slots.
+// MODE (diagnostics only, results wrong; production = 0): 1 = no draw (dv = 0),
+// 2 = no ancestor gather (src = i), 3 = both. Measured (1M): 16.8 / 15.0 / 16.9 / 15.0 us —
+// the kernel is bound by its 36 B read + 40 B write per particle. Write-through (sc1) or
+// nontemporal 16-B stores were slower (22-25 us).
+template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_ssm2d_prop(Ssm2dArgs a) {
     __shared__ u64 lds4[4];
     const int64_t N = a.N;
@@ -783,42 +786,78 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_prop(Ssm2dArgs a) {
     const double mean = rs ? a.dec_prev->mean : 0.0;
     const uint64_t op_dv = a.op_dev[0] + 3ull * (uint64_t)(a.t - 1);
     const double o0 = a.obs[2 * (a.t - 1)], o1 = a.obs[2 * (a.t - 1) + 1];
+    const int64_t i0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 2;
     u64 menc = 0;
-#pragma unroll
-    for (int k = 0; k < PPT; ++k) {
-        const int64_t i = ((int64_t)blockIdx.x * PPT + k) * kBlock + threadIdx.x;
-        if (i >= N) continue;
-        const int64_t src = rs ? (int64_t)a.anc_prev[i] : i;
-        double x0, x1, v0, v1;
-        if (a.t == 1) {
-            x0 = a.x0[0]; x1 = a.x0[1]; v0 = a.v0[0]; v1 = a.v0[1];
-        } else {
-            x0 = a.x_prev[src]; x1 = a.x_prev[N + src];
-            v0 = a.v_prev[src]; v1 = a.v_prev[N + src];
+    if (i0 < N) {
+        const bool two = i0 + 1 < N;
+        int64_t src[2] = {i0, i0 + 1};
+        if (rs && (MODE & 2) == 0) {
+            if (two) {
+                const int2 s2 = *reinterpret_cast<const int2*>(a.anc_prev + i0);
+                src[0] = s2.x; src[1] = s2.y;
+            } else {
+                src[0] = a.anc_prev[i0];
+            }
         }
-        // x{t+1} .= x{t} + v
-        const double xn0 = aff2(x0, v0), xn1 = aff2(x1, v1);
-        // dv ~ MvNormal([0,0], q*I)
-        double z0, z1;
-        wsmc_normal_pair(wsmc_rng_block(a.seed, op_dv, (uint64_t)(a.goff + i), 0u), &z0, &z1);
-        const double dv0 = 0.0 + a.q_sd * z0, dv1 = 0.0 + a.q_sd * z1;
-        // v .= v + dv
-        const double vn0 = aff2(v0, dv0), vn1 = aff2(v1, dv1);
-        // o => MvNormal(x{t+1}, r*I)
-        const double m0 = 0.0 + 1.0 * xn0, m1 = 0.0 + 1.0 * xn1;
-        double s = 0.0;
-        const double d0 = o0 - m0, d1 = o1 - m1;
-        s = s + d0 * d0;
-        s = s + d1 * d1;
-        const double lp = -(a.c0 + s / a.r_var) * 0.5;
-        const double wb = rs ? mean : a.w[i];
-        const double wn = wb + lp;
-        a.x_next[i] = xn0; a.x_next[N + i] = xn1;
-        a.v_next[i] = vn0; a.v_next[N + i] = vn1;
-        if (a.dv) { a.dv[i] = dv0; a.dv[N + i] = dv1; }
-        a.w[i] = wn;
-        const u64 e = wsmc_ord_enc(wn);
-        menc = e > menc ? e : menc;
+        double wb[2] = {mean, mean};
+        if (!rs) {
+            if (two) {
+                const d2 w2 = *reinterpret_cast<const d2*>(a.w + i0);
+                wb[0] = w2.x; wb[1] = w2.y;
+            } else {
+                wb[0] = a.w[i0];
+            }
+        }
+        d2 xp[2], vp[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            if (a.t == 1) {
+                xp[k] = d2{a.x0[0], a.x0[1]};
+                vp[k] = d2{a.v0[0], a.v0[1]};
+            } else if (k == 0 || two) {
+                xp[k] = *reinterpret_cast<const d2*>(a.x_prev + 2 * src[k]);
+                vp[k] = *reinterpret_cast<const d2*>(a.v_prev + 2 * src[k]);
+            }
+        }
+        d2 xn[2], vn[2], dvv[2];
+        double wn[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            // x{t+1} .= x{t} + v
+            const double xn0 = aff2(xp[k].x, vp[k].x), xn1 = aff2(xp[k].y, vp[k].y);
+            // dv ~ MvNormal([0,0], q*I)
+            double z0 = 0.0, z1 = 0.0;
+            if ((MODE & 1) == 0)
+                wsmc_normal_pair(wsmc_rng_block(a.seed, op_dv, (uint64_t)(a.goff + i0 + k), 0u), &z0, &z1);
+            const double dv0 = 0.0 + a.q_sd * z0, dv1 = 0.0 + a.q_sd * z1;
+            // v .= v + dv
+            const double vn0 = aff2(vp[k].x, dv0), vn1 = aff2(vp[k].y, dv1);
+            // o => MvNormal(x{t+1}, r*I)
+            const double m0 = 0.0 + 1.0 * xn0, m1 = 0.0 + 1.0 * xn1;
+            double s = 0.0;
+            const double d0 = o0 - m0, d1 = o1 - m1;
+            s = s + d0 * d0;
+            s = s + d1 * d1;
+            const double lp = -(a.c0 + s / a.r_var) * 0.5;
+            wn[k] = wb[k] + lp;
+            xn[k] = d2{xn0, xn1};
+            vn[k] = d2{vn0, vn1};
+            dvv[k] = d2{dv0, dv1};
+        }
+        *reinterpret_cast<d2*>(a.x_next + 2 * i0) = xn[0];
+        *reinterpret_cast<d2*>(a.v_next + 2 * i0) = vn[0];
+        if (a.dv) *reinterpret_cast<d2*>(a.dv + 2 * i0) = dvv[0];
+        menc = wsmc_ord_enc(wn[0]);
+        if (two) {
+            *reinterpret_cast<d2*>(a.x_next + 2 * i0 + 2) = xn[1];
+            *reinterpret_cast<d2*>(a.v_next + 2 * i0 + 2) = vn[1];
+            if (a.dv) *reinterpret_cast<d2*>(a.dv + 2 * i0 + 2) = dvv[1];
+            *reinterpret_cast<d2*>(a.w + i0) = d2{wn[0], wn[1]};
+            const u64 e1 = wsmc_ord_enc(wn[1]);
+            menc = e1 > menc ? e1 : menc;
+        } else {
+            a.w[i0] = wn[0];
+        }
     }
     menc = block_max_u64(menc, lds4);
     if (threadIdx.x == 0) atomic_max_filtered(&a.ms->v[blockIdx.x % kSlots][0], menc);
@@ -831,26 +870,31 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_final(Ssm2dFinal f) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= N) return;
     const int T = f.T;
+    const int64_t S = f.anc_stride;
     int64_t a = i;
-    if (f.dec[T].resampled) a = f.anc_log[(int64_t)(T - 1) * N + i];
-    f.v_out[i] = f.v_work[a]; f.v_out[N + i] = f.v_work[N + a];
-    f.dv_out[i] = f.dv_work[a]; f.dv_out[N + i] = f.dv_work[N + a];
+    if (f.dec[T].resampled) a = f.anc_log[(int64_t)(T - 1) * S + i];
+    // working buffers are particle-major pairs; output columns are SoA [2][N]
+    const d2 v = *reinterpret_cast<const d2*>(f.v_work + 2 * a);
+    f.v_out[i] = v.x; f.v_out[N + i] = v.y;
+    const d2 dv = *reinterpret_cast<const d2*>(f.dv_work + 2 * a);
+    f.dv_out[i] = dv.x; f.dv_out[N + i] = dv.y;
     if (f.dec[T].resampled) f.w[i] = f.dec[T].mean;
     if (!f.keep_history) {
-        f.x_out[i] = f.x_work[a]; f.x_out[N + i] = f.x_work[N + a];
+        const d2 x = *reinterpret_cast<const d2*>(f.x_work + 2 * a);
+        f.x_out[i] = x.x; f.x_out[N + i] = x.y;
         return;
     }
     // x_{T+1} was written at step T
     {
-        const double* src = f.hist_work[T + 1];
+        const d2 x = *reinterpret_cast<const d2*>(f.hist_work[T + 1] + 2 * a);
         double* dst = f.hist_out[T + 1];
-        dst[i] = src[a]; dst[N + i] = src[N + a];
+        dst[i] = x.x; dst[N + i] = x.y;
     }
     for (int s = T - 1; s >= 1; --s) {
-        if (f.dec[s].resampled) a = f.anc_log[(int64_t)(s - 1) * N + a];
-        const double* src = f.hist_work[s + 1];
+        if (f.dec[s].resampled) a = f.anc_log[(int64_t)(s - 1) * S + a];
+        const d2 x = *reinterpret_cast<const d2*>(f.hist_work[s + 1] + 2 * a);
         double* dst = f.hist_out[s + 1];
-        dst[i] = src[a]; dst[N + i] = src[N + a];
+        dst[i] = x.x; dst[N + i] = x.y;
     }
     double* d1 = f.hist_out[1];
     d1[i] = f.x0[0]; d1[N + i] = f.x0[1];
@@ -913,7 +957,7 @@ hipError_t launch_rs_reduce(hipStream_t s, const MaxSlots* ms, const u64* tilep,
     const int64_t nt = (N + kRsTile - 1) / kRsTile;
     FillPlan p{};
     if (plan) p = *plan;
-    return launch_timed(k_rs_reduce, dim3(1), dim3(kRsBlock), s, e0, e1, ms, tilep, nt, N, tileOff, rec,
+    return launch_timed(k_rs_reduce_t<0>, dim3(1), dim3(kRsBlock), s, e0, e1, ms, tilep, nt, N, tileOff, rec,
                         decide_local, ess_min, dec, p);
 }
 hipError_t launch_rs_decide(hipStream_t s, const ShardRecord* recs, int world, int rank, double ess_min,
@@ -949,7 +993,13 @@ hipError_t debug_kernel_bench(hipStream_t s, int kernel, int mode, int iters, co
                 default: hipLaunchKernelGGL(k_rs_sums_t<4>, g, blk, 0, s, w, N, ms, tilep, qbuf); break;
             }
         } else if (kernel == 1) {
-            launch_rs_reduce(s, ms, tilep, N, tileOff, rec, 1, 2.0, dec, &plan);
+            const int64_t nt = (N + kRsTile - 1) / kRsTile;
+            switch (mode) {
+                case 0: hipLaunchKernelGGL(k_rs_reduce_t<0>, dim3(1), dim3(kRsBlock), 0, s, ms, tilep, nt, N, tileOff, rec, 1, 2.0, dec, plan); break;
+                case 1: hipLaunchKernelGGL(k_rs_reduce_t<1>, dim3(1), dim3(kRsBlock), 0, s, ms, tilep, nt, N, tileOff, rec, 1, 2.0, dec, plan); break;
+                case 2: hipLaunchKernelGGL(k_rs_reduce_t<2>, dim3(1), dim3(kRsBlock), 0, s, ms, tilep, nt, N, tileOff, rec, 1, 2.0, dec, plan); break;
+                default: hipLaunchKernelGGL(k_rs_reduce_t<3>, dim3(1), dim3(kRsBlock), 0, s, ms, tilep, nt, N, tileOff, rec, 1, 2.0, dec, plan); break;
+            }
         } else {
             switch (mode) {
                 case 0: hipLaunchKernelGGL(k_rs_scan_t<0>, gs, bs, 0, s, N, rec, dec, plan, tileOff, qbuf, anc); break;
@@ -1034,24 +1084,20 @@ hipError_t launch_count_unique(hipStream_t s, const u64* keys, int64_t N, u64* c
     hipLaunchKernelGGL(k_count_unique, dim3((unsigned)nb), dim3(kBlock), 0, s, keys, N, count);
     return hipGetLastError();
 }
-static int prop_ppt() {
+static int prop_mode() {
     static int v = [] {
-        const char* e = getenv("WSMC_PROP_PPT");   // diagnostics: particles per thread
-        const int x = e ? atoi(e) : 1;
-        return x == 2 || x == 4 ? x : 1;
+        const char* e = getenv("WSMC_DIAG_PROP_MODE");   // diagnostics only: ablated propagate
+        return e ? atoi(e) & 3 : 0;
     }();
     return v;
 }
 hipError_t launch_ssm2d_propagate(hipStream_t s, const Ssm2dArgs& a, hipEvent_t e0, hipEvent_t e1) {
-    switch (prop_ppt()) {
-        case 2:
-            return launch_timed(k_ssm2d_prop<2>, dim3((unsigned)((a.N + 2 * kBlock - 1) / (2 * kBlock))),
-                                dim3(kBlock), s, e0, e1, a);
-        case 4:
-            return launch_timed(k_ssm2d_prop<4>, dim3((unsigned)((a.N + 4 * kBlock - 1) / (4 * kBlock))),
-                                dim3(kBlock), s, e0, e1, a);
-        default:
-            return launch_timed(k_ssm2d_prop<1>, grid_for(a.N), dim3(kBlock), s, e0, e1, a);
+    const dim3 g((unsigned)((a.N + 2 * kBlock - 1) / (2 * kBlock)));
+    switch (prop_mode()) {
+        case 1: return launch_timed(k_ssm2d_prop<1>, g, dim3(kBlock), s, e0, e1, a);
+        case 2: return launch_timed(k_ssm2d_prop<2>, g, dim3(kBlock), s, e0, e1, a);
+        case 3: return launch_timed(k_ssm2d_prop<3>, g, dim3(kBlock), s, e0, e1, a);
+        default: return launch_timed(k_ssm2d_prop<0>, g, dim3(kBlock), s, e0, e1, a);
     }
 }
 // bounded spin on the 100 MHz constant clock (always exits): queue-filling delay for
