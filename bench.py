@@ -89,7 +89,8 @@ def main():
     N = args.particles
     T = args.T
     obs = wsmc.models.ssm2d_data(max(T, args.cpu_T), seed=args.seed)
-    ctx = wsmc.Context(N, seed=args.seed + 1000003 * rank, device=local)
+    # one seed for every rank: the Philox streams are keyed by the global particle index
+    ctx = wsmc.Context(N, seed=args.seed, device=local)
     if comm is not None:
         uid = comm.broadcast(wsmc.Context.comm_unique_id() if rank == 0 else None)
         ctx.comm_init(uid, world, rank, rank * N, world * N)

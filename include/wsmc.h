@@ -131,6 +131,14 @@ int wsmc_set_op_counter(wsmc_ctx* ctx, uint64_t op);
 int wsmc_comm_unique_id(uint8_t out_id[128]);
 int wsmc_comm_init(wsmc_ctx* ctx, const uint8_t id[128], int32_t world, int32_t rank,
                    int64_t global_offset, int64_t global_n);
+/* The same sharding with a host-side exchange instead of RCCL: `exchange` receives this
+ * shard's record (`words` u64) and must return every rank's record in rank order in `all`
+ * (world * words), returning 0 on success. For hosts that carry their own transport (an
+ * MPI binding, a test harness putting several shards on one device); the device path is
+ * otherwise identical. */
+typedef int (*wsmc_exchange_fn)(void* user, const uint64_t* mine, int32_t words, uint64_t* all);
+int wsmc_comm_init_host(wsmc_ctx* ctx, wsmc_exchange_fn exchange, void* user, int32_t world, int32_t rank,
+                        int64_t global_offset, int64_t global_n);
 
 /* ---- store: AbstractParticleStore (src/stores.jl:1-35) ----------------------- */
 /* broadcast_setcol! column creation (src/stores.jl:85-96); existing name => same id */

@@ -1,0 +1,92 @@
+"""World-2 device path on one GPU: two processes, each a shard (HIP context) of one
+population, exchanging their shard records through the host (wsmc_comm_init_host) instead
+of RCCL — RCCL refuses two ranks on one device, and the box has one. Everything else on
+the device is the multi-GPU path: per-shard records, rank-order global decision, island
+resampling, shard log-mean reset, record-combined evidence. Results must equal the
+single-process sharded oracle bit for bit."""
+import os
+import pathlib
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+REPO = pathlib.Path(__file__).resolve().parents[1]
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, N, T, ess, scheme, outdir):
+    sys.path[:0] = [str(REPO / "weightedsampling.jl_amd")]
+    import wsmc
+    from wsmc.hostcomm import HostComm
+    comm = HostComm(rank, world, "127.0.0.1", port, tag="ms", timeout=120)
+    n = N // world
+    obs2 = wsmc.models.ssm2d_data(T)
+    out = {}
+    # statement-by-statement (generic operators)
+    c = wsmc.Context(n, seed=21, device=0)
+    c.comm_init_host(comm.allgather, world, rank, rank * n, N)
+    flags = wsmc.models.ssm2d_statements(c, obs2, ess_perc_min=ess, scheme=scheme)
+    out["flags"] = np.array(flags)
+    out["w"] = c.weights_download()
+    out["ev"] = np.array([c.log_evidence()])
+    for name in c.col_names():
+        out["s_" + name] = c.col_download(c.col_find(name))
+    c.close()
+    # fused run
+    f = wsmc.Context(n, seed=21, device=0)
+    f.comm_init_host(comm.allgather, world, rank, rank * n, N)
+    out["fev"] = np.array([f.ssm2d_run(obs2, ess_perc_min=ess, scheme=scheme, keep_history=True)])
+    out["fw"] = f.weights_download()
+    for name in f.col_names():
+        out["f_" + name] = f.col_download(f.col_find(name))
+    f.close()
+    comm.barrier()
+    comm.close()
+    np.savez(os.path.join(outdir, f"rank{rank}.npz"), **out)
+
+
+@pytest.mark.parametrize("ess,scheme", [(1.0, 0), (0.5, 1)])
+def test_two_shards_one_gpu_match_sharded_oracle(gpu_available, tmp_path, ess, scheme):
+    import multiprocessing as mp
+    sys.path.insert(0, str(REPO / "oracle"))
+    from oracle import Oracle
+    import wsmc
+    N, T, world = 4096, 10, 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=_worker, args=(r, world, port, N, T, ess, scheme, str(tmp_path))) for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(300)
+    codes = [p.exitcode for p in ps]
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+    assert codes == [0] * world, codes
+    ref = Oracle(N, seed=21, shards=world)
+    flags = wsmc.models.ssm2d_statements(ref, wsmc.models.ssm2d_data(T), ess_perc_min=ess, scheme=scheme)
+    n = N // world
+    for r in range(world):
+        p = np.load(tmp_path / f"rank{r}.npz")
+        sl = slice(r * n, (r + 1) * n)
+        assert list(p["flags"]) == flags
+        np.testing.assert_array_equal(p["w"], ref.weights_download()[sl])
+        np.testing.assert_array_equal(p["fw"], ref.weights_download()[sl])
+        for name in ref.col_names():
+            full = ref.col_download(ref.col_find(name))
+            np.testing.assert_array_equal(p["s_" + name], full[..., sl], err_msg=name)
+            np.testing.assert_array_equal(p["f_" + name], full[..., sl], err_msg=name)
+        assert p["ev"][0] == ref.log_evidence()
+        assert p["fev"][0] == ref.log_evidence()
+

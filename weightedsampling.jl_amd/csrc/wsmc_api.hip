@@ -281,6 +281,21 @@ int wsmc_comm_init(wsmc_ctx* c, const uint8_t id[128], int32_t world, int32_t ra
     return WSMC_OK;
 }
 
+int wsmc_comm_init_host(wsmc_ctx* c, wsmc_exchange_fn exchange, void* user, int32_t world, int32_t rank,
+                        int64_t goff, int64_t gN) {
+    CHECK_CTX(c);
+    if (!exchange) return fail(WSMC_EARG, "null exchange");
+    if (world < 1 || world > kMaxWorld || rank < 0 || rank >= world) return fail(WSMC_EARG, "bad world/rank");
+    if (goff < 0 || goff + c->N > gN) return fail(WSMC_EARG, "shard outside the global population");
+    c->world = world;
+    c->rank = rank;
+    c->goff = goff;
+    c->gN = gN;
+    c->host_exchange = exchange;
+    c->host_user = user;
+    return WSMC_OK;
+}
+
 // ---- store ---------------------------------------------------------------------------
 int wsmc_col_create(wsmc_ctx* c, const char* name, int32_t dim, int32_t* col_id) {
     CHECK_CTX(c);
@@ -415,10 +430,21 @@ static int enqueue_resample_stats(wsmc_ctx* c, const double* w, MaxSlots* ms, Sh
 }
 
 static int exchange_recs(wsmc_ctx* c, ShardRecord* recs) {
-    if (c->world > 1) {
-        const size_t cnt = sizeof(ShardRecord) / sizeof(unsigned long long);
-        WSMC_RCCL(ncclAllGather(recs + c->rank, recs, cnt, ncclUint64, c->comm, c->stream));
+    if (c->world <= 1) return WSMC_OK;
+    const int words = (int)(sizeof(ShardRecord) / sizeof(unsigned long long));
+    if (c->host_exchange) {
+        std::vector<ShardRecord> h(c->world);
+        WSMC_HIP(hipMemcpyAsync(&h[c->rank], recs + c->rank, sizeof(ShardRecord), hipMemcpyDeviceToHost, c->stream));
+        WSMC_HIP(hipStreamSynchronize(c->stream));
+        const ShardRecord mine = h[c->rank];
+        if (c->host_exchange(c->host_user, reinterpret_cast<const uint64_t*>(&mine), words,
+                             reinterpret_cast<uint64_t*>(h.data())) != 0)
+            return fail(WSMC_ERCCL, "host record exchange failed");
+        WSMC_HIP(hipMemcpyAsync(recs, h.data(), sizeof(ShardRecord) * c->world, hipMemcpyHostToDevice, c->stream));
+        WSMC_HIP(hipStreamSynchronize(c->stream));
+        return WSMC_OK;
     }
+    WSMC_RCCL(ncclAllGather(recs + c->rank, recs, words, ncclUint64, c->comm, c->stream));
     return WSMC_OK;
 }
 

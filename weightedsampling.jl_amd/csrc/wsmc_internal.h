@@ -82,6 +82,8 @@ struct wsmc_ctx {
     int world = 1, rank = 0;
     int64_t goff = 0, gN = 0;
     ncclComm_t comm = nullptr;
+    wsmc_exchange_fn host_exchange = nullptr;   // host-side record exchange (instead of RCCL)
+    void* host_user = nullptr;
 
     // store
     std::vector<wsmc::Column> cols;

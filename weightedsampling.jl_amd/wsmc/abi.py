@@ -82,6 +82,8 @@ SIGNATURES = {
     "wsmc_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
     "wsmc_comm_init": (C.c_int, [_P, C.POINTER(C.c_uint8), C.c_int32, C.c_int32, C.c_int64,
                                  C.c_int64]),
+    "wsmc_comm_init_host": (C.c_int, [_P, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int64,
+                                      C.c_int64]),
     "wsmc_col_create": (C.c_int, [_P, C.c_char_p, C.c_int32, _I32P]),
     "wsmc_col_find": (C.c_int, [_P, C.c_char_p, _I32P]),
     "wsmc_col_count": (C.c_int, [_P, _I32P]),
@@ -110,6 +112,10 @@ SIGNATURES = {
     "wsmc_run_get_timing": (C.c_int, [_P, C.POINTER(RunTiming)]),
     "wsmc_debug_kernel_bench": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_int32, _D]),
 }
+
+
+# int exchange(void* user, const uint64_t* mine, int32_t words, uint64_t* all)
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.c_int32, C.POINTER(C.c_uint64))
 
 
 class WSMCError(RuntimeError):

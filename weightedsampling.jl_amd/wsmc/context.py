@@ -80,6 +80,23 @@ class Context:
         check(self._L.wsmc_comm_init(self._h, buf, int(world), int(rank), int(global_offset), int(global_n)))
         self.world, self.rank = int(world), int(rank)
 
+    def comm_init_host(self, allgather, world: int, rank: int, global_offset: int, global_n: int) -> None:
+        """Shard this context with a host-side record exchange: ``allgather(list_of_u64)`` must
+        return every rank's list in rank order (e.g. wsmc.hostcomm.HostComm.allgather)."""
+        def _exchange(_user, mine, words, out):
+            try:
+                recs = allgather([int(mine[k]) for k in range(words)])
+                for r, rec in enumerate(recs):
+                    for k in range(words):
+                        out[r * words + k] = int(rec[k])
+                return 0
+            except Exception:
+                return 1
+        self._exchange_cb = abi.EXCHANGE_FN(_exchange)   # keep alive as long as the context
+        check(self._L.wsmc_comm_init_host(self._h, C.cast(self._exchange_cb, C.c_void_p), None, int(world),
+                                          int(rank), int(global_offset), int(global_n)))
+        self.world, self.rank = int(world), int(rank)
+
     # ---- store (AbstractParticleStore) ----
     def col_find(self, name: str) -> int:
         c = C.c_int32()
