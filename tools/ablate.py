@@ -14,7 +14,7 @@ for name, ess in (("spread", 1.0), ("skewed", 0.0)):
     c.ssm2d_run(obs, ess_perc_min=ess, keep_history=False)
     if name == "spread":
         c.weight(Normal(0.0, 0.3).dist(c.col_find), [abi.Operand.column(c.col_find("v"), 0)])
-    for k, modes in ((0, (0, 1, 4)), (1, range(4)), (2, range(4))):
+    for k, modes in ((0, (0, 1, 4)), (1, range(4)), (2, range(4)), (3, (0, 1))):
         for m in modes:
             c.debug_kernel_bench(k, m, 5)
             print(f"{name} kernel {k} mode {m}: {c.debug_kernel_bench(k, m, 100):.2f} us", flush=True)

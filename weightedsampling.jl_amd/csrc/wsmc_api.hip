@@ -210,7 +210,7 @@ int wsmc_destroy(wsmc_ctx* c) {
         (void)hipFree(col.back);
     }
     void* bufs[] = {c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount,
-                    c->d_colptr, c->run_params, c->d_tape, c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs,
+                    c->d_colptr, c->run_params, c->d_tape, c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp,
                     c->vscratch, c->xscratch};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
@@ -702,11 +702,19 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
 // ---- fused 2D SSM runner --------------------------------------------------------------
 // ancestor-log rows are padded to 16 B so every row start is aligned for paired loads
 static inline int64_t anc_stride(int64_t N) { return (N + 3) & ~(int64_t)3; }
+// per-step group sums of the fused single-GPU resample
+static inline int64_t run_grp_words(int64_t N) {
+    const int64_t nt = (N + kRsTile - 1) / kRsTile, G = group_tiles(N);
+    return ((nt + G - 1) / G) * kGroupLine;
+}
+static inline size_t run_grp_bytes(int64_t N, int32_t T) {
+    return sizeof(unsigned long long) * (size_t)run_grp_words(N) * (size_t)(T + 1);
+}
 
 static int ensure_run_buffers(wsmc_ctx* c, int32_t T) {
     if (c->T_alloc >= T && c->run_rec) return WSMC_OK;
     WSMC_HIP(hipStreamSynchronize(c->stream));
-    void* old[] = {c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs};
+    void* old[] = {c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp};
     for (void* p : old)
         if (p) WSMC_HIP(hipFree(p));
     WSMC_HIP(hipMalloc(&c->run_max, sizeof(MaxSlots) * (T + 1)));
@@ -714,6 +722,7 @@ static int ensure_run_buffers(wsmc_ctx* c, int32_t T) {
     WSMC_HIP(hipMalloc(&c->run_dec, sizeof(Decision) * (T + 1)));
     WSMC_HIP(hipMalloc(&c->anc_log, sizeof(int32_t) * (size_t)T * anc_stride(c->N)));
     WSMC_HIP(hipMalloc(&c->obs, sizeof(double) * 2 * (T + 1)));
+    WSMC_HIP(hipMalloc(&c->run_grp, run_grp_bytes(c->N, T)));
     if (!c->vscratch) WSMC_HIP(hipMalloc(&c->vscratch, sizeof(double) * 2 * c->N));
     if (!c->xscratch) WSMC_HIP(hipMalloc(&c->xscratch, sizeof(double) * 2 * c->N));
     c->T_alloc = T;
@@ -746,6 +755,9 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
     auto E = [&](int k) -> hipEvent_t { return ev ? (*ev)[k] : nullptr; };
     WSMC_HIP(hipMemsetAsync(c->run_max, 0, sizeof(MaxSlots) * (T + 1), c->stream));
     WSMC_HIP(hipMemsetAsync(c->run_dec, 0, sizeof(Decision) * (T + 1), c->stream));
+    const bool fused_fill = c->world == 1;   // no reduce kernel: group sums + one fill launch
+    if (fused_fill) WSMC_HIP(hipMemsetAsync(c->run_grp, 0, run_grp_bytes(N, T), c->stream));
+    const int G = group_tiles(N);
     double* vbuf[2] = {c->cols[p.colv].back, c->vscratch};
     double* xbuf[2] = {p.keep ? nullptr : c->cols[p.colx].back, c->xscratch};
     for (int t = 1; t <= T; ++t) {
@@ -784,11 +796,19 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
         WSMC_HIP(launch_ssm2d_propagate(c->stream, a, E(k0), E(k0 + 1)));
         hipEvent_t evs[4] = {E(k0 + 2), E(k0 + 3), E(k0 + 4), E(k0 + 5)};
         const FillPlan plan = fill_plan(c, p.scheme, 3ull * (uint64_t)(t - 1) + 2ull, c->run_params);
+        int32_t* anc_row = c->anc_log + (size_t)(t - 1) * anc_stride(N);
+        if (fused_fill) {
+            unsigned long long* grp = c->run_grp + (size_t)t * run_grp_words(N);
+            WSMC_HIP(launch_rs_sums(c->stream, c->w, N, ms, c->tilep, c->qbuf, E(k0 + 2), E(k0 + 3), grp, G));
+            WSMC_HIP(launch_rs_fill_fused(c->stream, N, plan, grp, G, ms, p.ess_min, recs, c->run_dec + t, c->qbuf,
+                                          anc_row, E(k0 + 6), E(k0 + 7)));
+            continue;
+        }
         int r = enqueue_resample_stats(c, c->w, ms, recs, p.ess_min, c->run_dec + t, false, plan,
                                        ev ? evs : nullptr);
         if (r) return r;
-        WSMC_HIP(launch_rs_scan(c->stream, N, recs + c->rank, c->run_dec + t, plan, c->tileOff, c->qbuf,
-                                c->anc_log + (size_t)(t - 1) * anc_stride(N), E(k0 + 6), E(k0 + 7)));
+        WSMC_HIP(launch_rs_scan(c->stream, N, recs + c->rank, c->run_dec + t, plan, c->tileOff, c->qbuf, anc_row,
+                                E(k0 + 6), E(k0 + 7)));
     }
     Ssm2dFinal f;
     f.T = T;
@@ -1009,8 +1029,10 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
             tm.propagate_ms += ms;
             WSMC_HIP(hipEventElapsedTime(&ms, evs[k + 2], evs[k + 3]));
             tm.reduce_ms += ms;
-            WSMC_HIP(hipEventElapsedTime(&ms, evs[k + 4], evs[k + 5]));
-            tm.reduce_ms += ms;
+            if (c->world > 1) {   // the reduce kernel runs only on the sharded path
+                WSMC_HIP(hipEventElapsedTime(&ms, evs[k + 4], evs[k + 5]));
+                tm.reduce_ms += ms;
+            }
             WSMC_HIP(hipEventElapsedTime(&ms, evs[k + 6], evs[k + 7]));
             tm.resample_ms += ms;
         }
@@ -1035,9 +1057,14 @@ int wsmc_debug_kernel_bench(wsmc_ctx* c, int32_t kernel, int32_t mode, int32_t i
     WSMC_HIP(launch_rs_sums(c->stream, c->w, c->N, c->mslots, c->tilep, c->qbuf));
     const FillPlan plan = fill_plan(c, WSMC_RESAMPLE_STRATIFIED, c->op, nullptr);
     WSMC_HIP(launch_rs_reduce(c->stream, c->mslots, c->tilep, c->N, c->tileOff, c->rec, 1, 2.0, c->dec, &plan));
+    double* stream4 = nullptr;
+    if (kernel == 3) WSMC_HIP(hipMalloc(&stream4, sizeof(double) * 8 * (size_t)c->N));
+    if (stream4) WSMC_HIP(hipMemsetAsync(stream4, 0, sizeof(double) * 8 * (size_t)c->N, c->stream));
     float ms = 0.f;
-    WSMC_HIP(debug_kernel_bench(c->stream, kernel, mode, iters, c->w, c->N, c->mslots, c->tilep, c->qbuf,
-                                c->tileOff, c->rec, c->dec, plan, c->anc, &ms));
+    const hipError_t e = debug_kernel_bench(c->stream, kernel, mode, iters, c->w, c->N, c->mslots, c->tilep, c->qbuf,
+                                            c->tileOff, c->rec, c->dec, plan, c->anc, stream4, &ms);
+    if (stream4) (void)hipFree(stream4);
+    WSMC_HIP(e);
     *avg_us = 1e3 * ms / iters;
     return WSMC_OK;
 }

@@ -83,6 +83,7 @@ struct wsmc_ctx {
     int64_t goff = 0, gN = 0;
     ncclComm_t comm = nullptr;
     wsmc_exchange_fn host_exchange = nullptr;   // host-side record exchange (instead of RCCL)
+    unsigned long long* run_grp = nullptr;      // [T+1][ngroups][kGroupLine] fused-run group sums
     void* host_user = nullptr;
 
     // store
@@ -168,7 +169,8 @@ hipError_t launch_weigh(hipStream_t s, const wsmc_term& t, double* w, double* co
 hipError_t launch_rs_max(hipStream_t s, const double* w, int64_t N, MaxSlots* ms);
 hipError_t launch_rs_sums(hipStream_t s, const double* w, int64_t N, const MaxSlots* ms,
                           unsigned long long* tilep, unsigned long long* qbuf,
-                          hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+                          hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr,
+                          unsigned long long* grp = nullptr, int G = 1);
 struct FillPlan {          // ancestor-fill task planning (in the reduce kernel)
     const unsigned long long* tilep;   // per-tile partials (sum q first)
     int32_t* taskOff;
@@ -187,6 +189,18 @@ hipError_t launch_rs_scan(hipStream_t s, int64_t N, const ShardRecord* rec, cons
                           const FillPlan& plan, const unsigned long long* tileOff,
                           const unsigned long long* qbuf, int32_t* anc, hipEvent_t e0 = nullptr,
                           hipEvent_t e1 = nullptr);
+// fused single-GPU run: group sums (kGroupLine u64 per group) replace the reduce kernel
+constexpr int kGroupLine = 8;
+inline int group_tiles(int64_t N) {   // tiles per group: ~sqrt(ntiles), >= 16
+    const int64_t nt = (N + kRsTile - 1) / kRsTile;
+    int G = 16;
+    while ((int64_t)G * G < nt) ++G;
+    return G;
+}
+hipError_t launch_rs_fill_fused(hipStream_t s, int64_t N, const FillPlan& plan, const unsigned long long* grp,
+                                int G, const MaxSlots* ms, double ess_min, ShardRecord* rec, Decision* dec,
+                                const unsigned long long* qbuf, int32_t* anc, hipEvent_t e0 = nullptr,
+                                hipEvent_t e1 = nullptr);
 hipError_t launch_gather(hipStream_t s, double* dst, const double* src, const int32_t* anc, int64_t N);
 hipError_t launch_fill_weights(hipStream_t s, double* w, const Decision* dec, int64_t N);
 hipError_t launch_log_evidence_stats(hipStream_t s, const double* w, int64_t N, MaxSlots* ms,
@@ -258,6 +272,6 @@ hipError_t launch_delay(hipStream_t s, int microseconds);
 hipError_t debug_kernel_bench(hipStream_t s, int kernel, int mode, int iters, const double* w, int64_t N,
                               MaxSlots* ms, unsigned long long* tilep, unsigned long long* qbuf,
                               unsigned long long* tileOff, ShardRecord* rec, Decision* dec, const FillPlan& plan,
-                              int32_t* anc, float* ms_out);
+                              int32_t* anc, double* stream4, float* ms_out);
 
 }  // namespace wsmc

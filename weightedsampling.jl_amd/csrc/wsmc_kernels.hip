@@ -237,7 +237,7 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
 template <int MODE>
 __global__ __launch_bounds__(kSumBlock) void k_rs_sums_t(const double* __restrict__ w, int64_t N,
                                                          const MaxSlots* __restrict__ ms, u64* __restrict__ tilep,
-                                                         u64* __restrict__ qbuf) {
+                                                         u64* __restrict__ qbuf, u64* __restrict__ grp, int G) {
     constexpr int IT = kRsTile / kSumBlock;
     __shared__ double s_f[3][kSumBlock / 64];
     __shared__ u64 s_q[kSumBlock / 64];
@@ -299,6 +299,8 @@ __global__ __launch_bounds__(kSumBlock) void k_rs_sums_t(const double* __restric
             t = (u64)f;                                         // exact: < 2^53
         }
         tilep[(int64_t)blockIdx.x * kPart + th] = t;
+        // group sums of q (fused single-GPU path; integer atomics, so order-free)
+        if (grp && th == 0) atomicAdd(grp + (int64_t)(blockIdx.x / G) * kGroupLine, t);
     }
 }
 
@@ -468,22 +470,25 @@ struct FillLds {
 // (blocked) particles and scatters their slots within the chunk. A particle owning more
 // than kScatterMax slots of the chunk is queued and filled by the whole block, so a lane
 // never loops long whatever the weights.
-template <int MODE>
-__device__ __forceinline__ void fill_chunk(int64_t N, int b, int j, u64 Q, const FillPlan& plan, uint64_t opx,
-                                           const u64* __restrict__ tileOff, const u64* __restrict__ qbuf,
-                                           int32_t* __restrict__ anc, FillLds& sh) {
-    constexpr int IT = kRsTile / kScanBlock;   // 4 particles per thread, blocked
-    const int th = threadIdx.x, lane = th & 63, wv = th >> 6;
-    const u64 off = tileOff[b];
-    const int64_t base = (int64_t)b * kRsTile;
-    u64 q[IT];
-    u64 tsum = 0;
+template <int IT>
+__device__ __forceinline__ void load_tile_q(int64_t N, int b, const u64* __restrict__ qbuf, u64 (&q)[IT]) {
 #pragma unroll
     for (int k = 0; k < IT; ++k) {
-        const int64_t i = base + (int64_t)th * IT + k;
+        const int64_t i = (int64_t)b * kRsTile + (int64_t)threadIdx.x * IT + k;
         q[k] = i < N ? qbuf[i] : 0ull;
-        tsum += q[k];
     }
+}
+
+template <int MODE>
+__device__ __forceinline__ void fill_chunk_q(int64_t N, int b, int j, u64 Q, u64 off, const FillPlan& plan,
+                                             uint64_t opx, const u64 (&q)[kRsTile / kScanBlock],
+                                             int32_t* __restrict__ anc, FillLds& sh) {
+    constexpr int IT = kRsTile / kScanBlock;   // 4 particles per thread, blocked
+    const int th = threadIdx.x, lane = th & 63, wv = th >> 6;
+    const int64_t base = (int64_t)b * kRsTile;
+    u64 tsum = 0;
+#pragma unroll
+    for (int k = 0; k < IT; ++k) tsum += q[k];
     const double ratio = wsmc_u64_to_d((uint64_t)N) / wsmc_u64_to_d(Q);
     // the tile's slot range [L, H) = [rank(off), rank(off + Q_b)), ranked by two threads
     // while the others scan; the scan's barrier publishes them
@@ -556,6 +561,15 @@ __device__ __forceinline__ void fill_chunk(int64_t N, int b, int j, u64 Q, const
     __syncthreads();
 }
 
+template <int MODE>
+__device__ __forceinline__ void fill_chunk(int64_t N, int b, int j, u64 Q, u64 off, const FillPlan& plan,
+                                           uint64_t opx, const u64* __restrict__ qbuf, int32_t* __restrict__ anc,
+                                           FillLds& sh) {
+    u64 q[kRsTile / kScanBlock];
+    load_tile_q(N, b, qbuf, q);
+    fill_chunk_q<MODE>(N, b, j, Q, off, plan, opx, q, anc, sh);
+}
+
 // Ancestor fill (the icdf merge, src/resampling.jl:13-26): ancestor(slot n) = smallest m
 // with C_m > x_n, i.e. particle m owns the slots [rank(C_{m-1}), rank(C_m)) with
 // rank(c) = #{n : x_n < c}. Block b < ntiles fills the first chunk
@@ -577,14 +591,143 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_scan_t(int64_t N, const Shard
     const uint64_t opx = op_eff(plan.op, plan.op_dev);
     if (t < ntiles) {
         if (!rs) return;
-        fill_chunk<MODE>(N, t, 0, Q, plan, opx, tileOff, qbuf, anc, sh);
+        fill_chunk<MODE>(N, t, 0, Q, tileOff[t], plan, opx, qbuf, anc, sh);
         return;
     }
     if (!rs) return;
     const int ntasks = dec->ntasks;
     for (int o = t - ntiles; o < ntasks; o += kOverflowBlocks) {
         const int b = plan.taskTile[o];
-        fill_chunk<MODE>(N, b, 1 + o - plan.taskOff[b], Q, plan, opx, tileOff, qbuf, anc, sh);
+        fill_chunk<MODE>(N, b, 1 + o - plan.taskOff[b], Q, tileOff[b], plan, opx, qbuf, anc, sh);
+    }
+}
+
+// ---- fused single-GPU resample: no reduce kernel ----------------------------------
+// block sum of two u64 values (all threads get the totals)
+__device__ __forceinline__ void block_sum2_u64(u64& a, u64& b, u64 (*lds)[2]) {
+    a = wave_sum_u64(a);
+    b = wave_sum_u64(b);
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { lds[wv][0] = a; lds[wv][1] = b; }
+    __syncthreads();
+    a = 0; b = 0;
+#pragma unroll
+    for (int v = 0; v < kScanBlock / 64; ++v) { a += lds[v][0]; b += lds[v][1]; }
+    __syncthreads();
+}
+
+// The decision and the ancestor fill of one Resample in one launch (single GPU, fused run).
+// The weight-statistics kernel left per-tile partials and per-group sums (G tiles a group):
+//  * block ntiles + kOverflowBlocks builds the shard record from the tile partials, the
+//    group sums and the max slots and takes the decision (strict ESS test, log-mean) —
+//    concurrently with the fill;
+//  * block b < ntiles fills the first chunk of tile b, its CDF offset being the groups
+//    before it plus the tiles before it in its group (O(sqrt(ntiles)) loads, no reduce pass);
+//  * kOverflowBlocks blocks plan the overflow chunks from the tile sums and fill them.
+// The fill does not wait for the decision: when the step does not resample, the row it
+// writes is never read (the next step and the trace-back check the decision).
+__global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPlan plan, const u64* __restrict__ grp,
+                                                              int G, const MaxSlots* __restrict__ ms, double ess_min,
+                                                              ShardRecord* rec, Decision* dec,
+                                                              const u64* __restrict__ qbuf, int32_t* __restrict__ anc) {
+    __shared__ FillLds sh;
+    __shared__ u64 s_red[kScanBlock / 64][2];
+    __shared__ u64 s_parts[kScanBlock / 64][kRedPart];
+    __shared__ u64 s_task[3];
+    const int t = blockIdx.x, th = threadIdx.x;
+    const int ntiles = (int)((N + kRsTile - 1) / kRsTile);
+    const int ngroups = (ntiles + G - 1) / G;
+    if (t == ntiles + kOverflowBlocks) {
+        // ---- the record and the decision ----
+        u64 acc[kRedPart] = {0, 0, 0, 0, 0, 0};
+        for (int g = th; g < ngroups; g += kScanBlock) acc[0] += grp[(int64_t)g * kGroupLine];
+        for (int b = th; b < ntiles; b += kScanBlock) {
+            const u64 s1 = plan.tilep[(int64_t)b * kPart + 1], s2 = plan.tilep[(int64_t)b * kPart + 2],
+                      wf = plan.tilep[(int64_t)b * kPart + 3];
+            acc[1] += s1;
+            acc[2] += s2 & 0xffffffffull; acc[3] += s2 >> 32;
+            acc[4] += wf & 0xffffffffull; acc[5] += wf >> 32;
+        }
+        const u64 menc = th < kSlots ? wave_max_u64(ms->v[th & (kSlots - 1)][0]) : 0ull;
+#pragma unroll
+        for (int k = 0; k < kRedPart; ++k) acc[k] = wave_sum_u64(acc[k]);
+        if ((th & 63) == 0)
+#pragma unroll
+            for (int k = 0; k < kRedPart; ++k) s_parts[th >> 6][k] = acc[k];
+        __syncthreads();
+        if (th == 0) {
+            u64 tot[kRedPart] = {0, 0, 0, 0, 0, 0};
+            for (int v = 0; v < kScanBlock / 64; ++v)
+                for (int k = 0; k < kRedPart; ++k) tot[k] += s_parts[v][k];
+            ShardRecord r;
+            r.menc = menc;
+            r.Q = tot[0];
+            r.s1 = tot[1];
+            const wsmc_u128 S2 = (wsmc_u128)tot[2] + ((wsmc_u128)tot[3] << 32);
+            const wsmc_u128 Wf = (wsmc_u128)tot[4] + ((wsmc_u128)tot[5] << 32);
+            r.s2lo = (u64)S2; r.s2hi = (u64)(S2 >> 64);
+            r.wflo = (u64)Wf; r.wfhi = (u64)(Wf >> 64);
+            r.n = (u64)N;
+            *rec = r;
+            decide_records(&r, 1, 0, ess_min, dec);
+        }
+        return;
+    }
+    const uint64_t opx = op_eff(plan.op, plan.op_dev);
+    if (t < ntiles) {
+        // ---- first chunk of tile t (its q loads in flight while the offset is summed) ----
+        u64 q[kRsTile / kScanBlock];
+        load_tile_q(N, t, qbuf, q);
+        const int g = t / G;
+        u64 pre = 0, tot = 0;
+        for (int k = th; k < ngroups; k += kScanBlock) {
+            const u64 v = grp[(int64_t)k * 8];
+            tot += v;
+            pre += k < g ? v : 0ull;
+        }
+        for (int b = g * G + th; b < t; b += kScanBlock) pre += plan.tilep[(int64_t)b * kPart];
+        block_sum2_u64(pre, tot, s_red);
+        fill_chunk_q<0>(N, t, 0, tot, pre, plan, opx, q, anc, sh);
+        return;
+    }
+    // ---- overflow chunks: plan from the tile sums (contiguous tiles per thread) ----
+    u64 Q = 0, dummy = 0;
+    for (int k = th; k < ngroups; k += kScanBlock) Q += grp[(int64_t)k * 8];
+    block_sum2_u64(Q, dummy, s_red);
+    const double ratio = Q ? wsmc_u64_to_d((uint64_t)N) / wsmc_u64_to_d(Q) : 0.0;
+    const int per = (ntiles + kScanBlock - 1) / kScanBlock;
+    const int b0 = th * per < ntiles ? th * per : ntiles;
+    const int b1 = b0 + per < ntiles ? b0 + per : ntiles;
+    u64 qs = 0, ns = 0;
+    for (int b = b0; b < b1; ++b) {
+        const u64 qb = plan.tilep[(int64_t)b * kPart];
+        qs += qb;
+        ns += (u64)ovf_chunks(qb, ratio);
+    }
+    u64 qtot, ntasks;
+    const u64 qpre = block_excl_scan_u64<kScanBlock / 64>(qs, sh.uw, &qtot);
+    const u64 npre = block_excl_scan_u64<kScanBlock / 64>(ns, sh.uw, &ntasks);
+    for (u64 o = (u64)(t - ntiles); o < ntasks; o += kOverflowBlocks) {
+        if (o >= npre && o < npre + ns) {          // exactly one thread owns task o
+            u64 c = qpre, n0 = npre;
+            for (int b = b0; b < b1; ++b) {
+                const u64 qb = plan.tilep[(int64_t)b * kPart];
+                const u64 k = (u64)ovf_chunks(qb, ratio);
+                if (o < n0 + k) {
+                    s_task[0] = (u64)b;
+                    s_task[1] = 1 + (o - n0);
+                    s_task[2] = c;
+                    break;
+                }
+                n0 += k;
+                c += qb;
+            }
+        }
+        __syncthreads();
+        const int b = (int)s_task[0];
+        const int j = (int)s_task[1];
+        const u64 off = s_task[2];
+        fill_chunk<0>(N, b, j, Q, off, plan, opx, qbuf, anc, sh);   // ends with a barrier
     }
 }
 
@@ -948,8 +1091,15 @@ hipError_t launch_rs_max(hipStream_t s, const double* w, int64_t N, MaxSlots* ms
     return hipGetLastError();
 }
 hipError_t launch_rs_sums(hipStream_t s, const double* w, int64_t N, const MaxSlots* ms, u64* tilep, u64* qbuf,
-                          hipEvent_t e0, hipEvent_t e1) {
-    return launch_timed(k_rs_sums_t<0>, rs_tiles_for(N), dim3(kSumBlock), s, e0, e1, w, N, ms, tilep, qbuf);
+                          hipEvent_t e0, hipEvent_t e1, u64* grp, int G) {
+    return launch_timed(k_rs_sums_t<0>, rs_tiles_for(N), dim3(kSumBlock), s, e0, e1, w, N, ms, tilep, qbuf, grp, G);
+}
+hipError_t launch_rs_fill_fused(hipStream_t s, int64_t N, const FillPlan& plan, const u64* grp, int G,
+                                const MaxSlots* ms, double ess_min, ShardRecord* rec, Decision* dec, const u64* qbuf,
+                                int32_t* anc, hipEvent_t e0, hipEvent_t e1) {
+    const dim3 g((unsigned)((N + kRsTile - 1) / kRsTile + kOverflowBlocks + 1));
+    return launch_timed(k_rs_fill_fused, g, dim3(kScanBlock), s, e0, e1, N, plan, grp, G, ms, ess_min, rec, dec, qbuf,
+                        anc);
 }
 hipError_t launch_rs_reduce(hipStream_t s, const MaxSlots* ms, const u64* tilep, int64_t N, u64* tileOff,
                             ShardRecord* rec, int decide_local, double ess_min, Decision* dec,
@@ -976,10 +1126,32 @@ hipError_t launch_rs_scan(hipStream_t s, int64_t N, const ShardRecord* rec, cons
                         qbuf, anc);
 }
 
+// diagnostics: the propagate kernel's memory pattern with no arithmetic — per particle a
+// 4-B index + 2 x 16-B reads, 2 x 16-B + 8-B writes (76 B), 2 particles per thread.
+// MODE 0: identity index; 1: index gather through anc (the step's ancestors)
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_stream_like_prop(const int32_t* __restrict__ anc,
+                                                            const double* __restrict__ xs,
+                                                            const double* __restrict__ vs, double* __restrict__ xd,
+                                                            double* __restrict__ vd, double* __restrict__ wd,
+                                                            int64_t N) {
+    const int64_t i0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 2;
+    if (i0 + 1 >= N) return;
+    const int2 s2 = *reinterpret_cast<const int2*>(anc + i0);
+    const int64_t a0 = MODE ? s2.x : i0, a1 = MODE ? s2.y : i0 + 1;
+    const d2 x0 = *reinterpret_cast<const d2*>(xs + 2 * a0), x1 = *reinterpret_cast<const d2*>(xs + 2 * a1);
+    const d2 v0 = *reinterpret_cast<const d2*>(vs + 2 * a0), v1 = *reinterpret_cast<const d2*>(vs + 2 * a1);
+    *reinterpret_cast<d2*>(xd + 2 * i0) = x0 + v0;
+    *reinterpret_cast<d2*>(xd + 2 * i0 + 2) = x1 + v1;
+    *reinterpret_cast<d2*>(vd + 2 * i0) = v0;
+    *reinterpret_cast<d2*>(vd + 2 * i0 + 2) = v1;
+    *reinterpret_cast<d2*>(wd + i0) = d2{x0.x + (double)s2.x, x1.x};
+}
+
 // diagnostics: time `iters` launches of a kernel variant on the context's current buffers
 hipError_t debug_kernel_bench(hipStream_t s, int kernel, int mode, int iters, const double* w, int64_t N,
                               MaxSlots* ms, u64* tilep, u64* qbuf, u64* tileOff, ShardRecord* rec, Decision* dec,
-                              const FillPlan& plan, int32_t* anc, float* ms_out) {
+                              const FillPlan& plan, int32_t* anc, double* stream4, float* ms_out) {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
@@ -988,10 +1160,20 @@ hipError_t debug_kernel_bench(hipStream_t s, int kernel, int mode, int iters, co
     for (int it = 0; it < iters; ++it) {
         if (kernel == 0) {
             switch (mode) {
-                case 0: hipLaunchKernelGGL(k_rs_sums_t<0>, g, blk, 0, s, w, N, ms, tilep, qbuf); break;
-                case 1: hipLaunchKernelGGL(k_rs_sums_t<1>, g, blk, 0, s, w, N, ms, tilep, qbuf); break;
-                default: hipLaunchKernelGGL(k_rs_sums_t<4>, g, blk, 0, s, w, N, ms, tilep, qbuf); break;
+                case 0: hipLaunchKernelGGL(k_rs_sums_t<0>, g, blk, 0, s, w, N, ms, tilep, qbuf, nullptr, 1); break;
+                case 1: hipLaunchKernelGGL(k_rs_sums_t<1>, g, blk, 0, s, w, N, ms, tilep, qbuf, nullptr, 1); break;
+                default: hipLaunchKernelGGL(k_rs_sums_t<4>, g, blk, 0, s, w, N, ms, tilep, qbuf, nullptr, 1); break;
             }
+        } else if (kernel == 3) {
+            // scratch: stream4 = 4 x [2N] doubles (x src, v src, x dst, v dst), wd = w
+            const dim3 gp((unsigned)((N + 2 * kBlock - 1) / (2 * kBlock)));
+            double* b4 = stream4;
+            if (mode == 0)
+                hipLaunchKernelGGL(k_stream_like_prop<0>, gp, dim3(kBlock), 0, s, anc, b4, b4 + 2 * N, b4 + 4 * N,
+                                   b4 + 6 * N, const_cast<double*>(w), N);
+            else
+                hipLaunchKernelGGL(k_stream_like_prop<1>, gp, dim3(kBlock), 0, s, anc, b4, b4 + 2 * N, b4 + 4 * N,
+                                   b4 + 6 * N, const_cast<double*>(w), N);
         } else if (kernel == 1) {
             const int64_t nt = (N + kRsTile - 1) / kRsTile;
             switch (mode) {
