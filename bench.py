@@ -56,6 +56,10 @@ def parse():
     ap.add_argument("--cpu-particles", type=int, default=500_000)
     ap.add_argument("--cpu-T", type=int, default=100)
     ap.add_argument("--seed", type=int, default=42)
+    # test hooks for the multi-rank code path on a one-GPU box (RCCL refuses two ranks on
+    # one device): exchange shard records through the host rendezvous, all ranks on GPU 0
+    ap.add_argument("--exchange", choices=["rccl", "host"], default="rccl")
+    ap.add_argument("--same-device", action="store_true")
     return ap.parse_args()
 
 
@@ -90,10 +94,13 @@ def main():
     T = args.T
     obs = wsmc.models.ssm2d_data(max(T, args.cpu_T), seed=args.seed)
     # one seed for every rank: the Philox streams are keyed by the global particle index
-    ctx = wsmc.Context(N, seed=args.seed, device=local)
+    ctx = wsmc.Context(N, seed=args.seed, device=0 if args.same_device else local)
     if comm is not None:
-        uid = comm.broadcast(wsmc.Context.comm_unique_id() if rank == 0 else None)
-        ctx.comm_init(uid, world, rank, rank * N, world * N)
+        if args.exchange == "host":
+            ctx.comm_init_host(comm.allgather, world, rank, rank * N, world * N)
+        else:
+            uid = comm.broadcast(wsmc.Context.comm_unique_id() if rank == 0 else None)
+            ctx.comm_init(uid, world, rank, rank * N, world * N)
 
     def barrier():
         ctx.sync()
@@ -139,7 +146,8 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     # propagate-kernel algorithmic bytes per run (forced resampling: every step after t=1 reads
     # through ancestors; t = 1 starts from the constant x0/v0)
-    forced = nres == T - 1
+    # every step resampled (step 1 of a fresh single-GPU state has equal weights, ESS = 1)
+    forced = nres >= T - 1
     prop_bytes = N * (PROP_BYTES_FIRST + (T - 1) * PROP_BYTES_STEADY + PROP_BYTES_LAST_DV)
     prop_gbs = prop_bytes / (prop_ms * 1e-3) / 1e9 if prop_ms > 0 else None
     traffic = None
@@ -173,7 +181,8 @@ def main():
             "config": {"workload": "2D SSM bootstrap filter (examples/2D_ssm.jl), BASELINE configs[1]",
                        "n_particles_per_gpu": N, "global_particles": world * N, "T": T,
                        "ess_perc_min": args.ess, "scheme": args.scheme, "keep_history": not args.no_history,
-                       "parallelism": f"island-shard x{world}" if world > 1 else "single GPU"},
+                       "parallelism": (f"island-shard x{world}" + (" (host exchange, test mode)" if args.exchange == "host" else ""))
+                           if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "kernel": "k_ssm2d_prop (propagate+observe+max)",
                          "achieved": prop_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (prop_gbs / HBM_PEAK_GBS) if prop_gbs else None, "traffic": traffic,

@@ -55,13 +55,13 @@ def _worker(rank, world, port, N, T, ess, scheme, outdir):
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), **out)
 
 
-@pytest.mark.parametrize("ess,scheme", [(1.0, 0), (0.5, 1)])
-def test_two_shards_one_gpu_match_sharded_oracle(gpu_available, tmp_path, ess, scheme):
+@pytest.mark.parametrize("N,ess,scheme", [(4096, 1.0, 0), (4096, 0.5, 1), (140002, 1.0, 0), (140002, 0.5, 0)])
+def test_two_shards_one_gpu_match_sharded_oracle(gpu_available, tmp_path, N, ess, scheme):
     import multiprocessing as mp
     sys.path.insert(0, str(REPO / "oracle"))
     from oracle import Oracle
     import wsmc
-    N, T, world = 4096, 10, 2
+    T, world = 10, 2
     port = _free_port()
     ctx = mp.get_context("spawn")
     ps = [ctx.Process(target=_worker, args=(r, world, port, N, T, ess, scheme, str(tmp_path))) for r in range(world)]

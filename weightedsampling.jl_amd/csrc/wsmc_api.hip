@@ -30,7 +30,6 @@ int fail(int code, const std::string& msg) {
         WSMC_HIP(hipSetDevice((ctx)->device));                           \
     } while (0)
 
-static constexpr int kMaxWorld = 8;
 
 // ---- helpers -------------------------------------------------------------------------
 static int upload_colptr(wsmc_ctx* c) {
@@ -216,6 +215,9 @@ int wsmc_destroy(wsmc_ctx* c) {
         if (p) (void)hipFree(p);
     if (c->pinned) (void)hipHostFree(c->pinned);
     if (c->comm) (void)ncclCommDestroy(c->comm);
+    if (c->ev_sums) (void)hipEventDestroy(c->ev_sums);
+    if (c->ev_dec) (void)hipEventDestroy(c->ev_dec);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return WSMC_OK;
@@ -426,6 +428,27 @@ static int enqueue_resample_stats(wsmc_ctx* c, const double* w, MaxSlots* ms, Sh
         if (r) return r;
         WSMC_HIP(launch_rs_decide(c->stream, recs, c->world, c->rank, ess_min, dec));
     }
+    return WSMC_OK;
+}
+
+// all-gather `words` u64 per rank in place (rank r's block at buf + r * words) on stream s
+static int exchange_words(wsmc_ctx* c, unsigned long long* buf, int64_t words, hipStream_t s) {
+    if (c->world <= 1) return WSMC_OK;
+    if (c->host_exchange) {
+        std::vector<unsigned long long> h((size_t)words * c->world);
+        WSMC_HIP(hipMemcpyAsync(h.data() + (size_t)c->rank * words, buf + (size_t)c->rank * words,
+                                sizeof(unsigned long long) * words, hipMemcpyDeviceToHost, s));
+        WSMC_HIP(hipStreamSynchronize(s));
+        const std::vector<unsigned long long> mine(h.begin() + (size_t)c->rank * words,
+                                                   h.begin() + (size_t)(c->rank + 1) * words);
+        if (c->host_exchange(c->host_user, reinterpret_cast<const uint64_t*>(mine.data()), (int32_t)words,
+                             reinterpret_cast<uint64_t*>(h.data())) != 0)
+            return fail(WSMC_ERCCL, "host exchange failed");
+        WSMC_HIP(hipMemcpyAsync(buf, h.data(), sizeof(unsigned long long) * h.size(), hipMemcpyHostToDevice, s));
+        WSMC_HIP(hipStreamSynchronize(s));
+        return WSMC_OK;
+    }
+    WSMC_RCCL(ncclAllGather(buf + (size_t)c->rank * words, buf, (size_t)words, ncclUint64, c->comm, s));
     return WSMC_OK;
 }
 
@@ -710,11 +733,19 @@ static inline int64_t run_grp_words(int64_t N) {
 static inline size_t run_grp_bytes(int64_t N, int32_t T) {
     return sizeof(unsigned long long) * (size_t)run_grp_words(N) * (size_t)(T + 1);
 }
+// sharded fused run: one exchange payload per rank and step = an 8-word header (max
+// log-weight, size) + the shard's group sums
+static inline int64_t run_pay_words(int64_t N) { return kGroupLine + run_grp_words(N); }
 
 static int ensure_run_buffers(wsmc_ctx* c, int32_t T) {
+    if (c->world > 1 && !c->stream2) {
+        WSMC_HIP(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+        WSMC_HIP(hipEventCreateWithFlags(&c->ev_sums, hipEventDisableTiming));
+        WSMC_HIP(hipEventCreateWithFlags(&c->ev_dec, hipEventDisableTiming));
+    }
     if (c->T_alloc >= T && c->run_rec) return WSMC_OK;
     WSMC_HIP(hipStreamSynchronize(c->stream));
-    void* old[] = {c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp};
+    void* old[] = {c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp, c->run_pay};
     for (void* p : old)
         if (p) WSMC_HIP(hipFree(p));
     WSMC_HIP(hipMalloc(&c->run_max, sizeof(MaxSlots) * (T + 1)));
@@ -723,6 +754,7 @@ static int ensure_run_buffers(wsmc_ctx* c, int32_t T) {
     WSMC_HIP(hipMalloc(&c->anc_log, sizeof(int32_t) * (size_t)T * anc_stride(c->N)));
     WSMC_HIP(hipMalloc(&c->obs, sizeof(double) * 2 * (T + 1)));
     WSMC_HIP(hipMalloc(&c->run_grp, run_grp_bytes(c->N, T)));
+    WSMC_HIP(hipMalloc(&c->run_pay, sizeof(unsigned long long) * (size_t)run_pay_words(c->N) * kMaxWorld * (T + 1)));
     if (!c->vscratch) WSMC_HIP(hipMalloc(&c->vscratch, sizeof(double) * 2 * c->N));
     if (!c->xscratch) WSMC_HIP(hipMalloc(&c->xscratch, sizeof(double) * 2 * c->N));
     c->T_alloc = T;
@@ -755,9 +787,16 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
     auto E = [&](int k) -> hipEvent_t { return ev ? (*ev)[k] : nullptr; };
     WSMC_HIP(hipMemsetAsync(c->run_max, 0, sizeof(MaxSlots) * (T + 1), c->stream));
     WSMC_HIP(hipMemsetAsync(c->run_dec, 0, sizeof(Decision) * (T + 1), c->stream));
-    const bool fused_fill = c->world == 1;   // no reduce kernel: group sums + one fill launch
-    if (fused_fill) WSMC_HIP(hipMemsetAsync(c->run_grp, 0, run_grp_bytes(N, T), c->stream));
+    // one GPU: group sums + one fill launch whose extra block decides. Sharded: the group
+    // sums are the exchange payload; all-gather + decision run on stream2, overlapped with
+    // the local fill (island resampling fills from the shard's own Q); the next step's
+    // propagate waits for the decision.
+    const bool sharded = c->world > 1;
     const int G = group_tiles(N);
+    const int64_t PW = run_pay_words(N);
+    const int ngroups = (int)(run_grp_words(N) / kGroupLine);
+    if (!sharded) WSMC_HIP(hipMemsetAsync(c->run_grp, 0, run_grp_bytes(N, T), c->stream));
+    else WSMC_HIP(hipMemsetAsync(c->run_pay, 0, sizeof(unsigned long long) * PW * c->world * (T + 1), c->stream));
     double* vbuf[2] = {c->cols[p.colv].back, c->vscratch};
     double* xbuf[2] = {p.keep ? nullptr : c->cols[p.colx].back, c->xscratch};
     for (int t = 1; t <= T; ++t) {
@@ -793,23 +832,32 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
         ShardRecord* recs = c->run_rec + (size_t)t * c->world;
         a.ms = ms;
         const int k0 = 8 * (t - 1);
+        if (sharded && t > 1) WSMC_HIP(hipStreamWaitEvent(c->stream, c->ev_dec, 0));
         WSMC_HIP(launch_ssm2d_propagate(c->stream, a, E(k0), E(k0 + 1)));
-        hipEvent_t evs[4] = {E(k0 + 2), E(k0 + 3), E(k0 + 4), E(k0 + 5)};
         const FillPlan plan = fill_plan(c, p.scheme, 3ull * (uint64_t)(t - 1) + 2ull, c->run_params);
         int32_t* anc_row = c->anc_log + (size_t)(t - 1) * anc_stride(N);
-        if (fused_fill) {
+        if (!sharded) {
             unsigned long long* grp = c->run_grp + (size_t)t * run_grp_words(N);
             WSMC_HIP(launch_rs_sums(c->stream, c->w, N, ms, c->tilep, c->qbuf, E(k0 + 2), E(k0 + 3), grp, G));
             WSMC_HIP(launch_rs_fill_fused(c->stream, N, plan, grp, G, ms, p.ess_min, recs, c->run_dec + t, c->qbuf,
                                           anc_row, E(k0 + 6), E(k0 + 7)));
             continue;
         }
-        int r = enqueue_resample_stats(c, c->w, ms, recs, p.ess_min, c->run_dec + t, false, plan,
-                                       ev ? evs : nullptr);
+        unsigned long long* pay = c->run_pay + (size_t)t * c->world * PW;
+        unsigned long long* mine = pay + (size_t)c->rank * PW;
+        WSMC_HIP(launch_rs_sums(c->stream, c->w, N, ms, c->tilep, c->qbuf, E(k0 + 2), E(k0 + 3), mine + kGroupLine,
+                                G, mine));
+        WSMC_HIP(hipEventRecord(c->ev_sums, c->stream));
+        WSMC_HIP(hipStreamWaitEvent(c->stream2, c->ev_sums, 0));
+        int r = exchange_words(c, pay, PW, c->stream2);
         if (r) return r;
-        WSMC_HIP(launch_rs_scan(c->stream, N, recs + c->rank, c->run_dec + t, plan, c->tileOff, c->qbuf, anc_row,
-                                E(k0 + 6), E(k0 + 7)));
+        WSMC_HIP(launch_rs_decide_groups(c->stream2, pay, PW, ngroups, c->world, c->rank, p.ess_min, recs,
+                                         c->run_dec + t));
+        WSMC_HIP(hipEventRecord(c->ev_dec, c->stream2));
+        WSMC_HIP(launch_rs_fill_fused(c->stream, N, plan, mine + kGroupLine, G, ms, p.ess_min, recs, nullptr, c->qbuf,
+                                      anc_row, E(k0 + 6), E(k0 + 7)));
     }
+    if (sharded) WSMC_HIP(hipStreamWaitEvent(c->stream, c->ev_dec, 0));
     Ssm2dFinal f;
     f.T = T;
     f.keep_history = p.keep;
@@ -1029,10 +1077,6 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
             tm.propagate_ms += ms;
             WSMC_HIP(hipEventElapsedTime(&ms, evs[k + 2], evs[k + 3]));
             tm.reduce_ms += ms;
-            if (c->world > 1) {   // the reduce kernel runs only on the sharded path
-                WSMC_HIP(hipEventElapsedTime(&ms, evs[k + 4], evs[k + 5]));
-                tm.reduce_ms += ms;
-            }
             WSMC_HIP(hipEventElapsedTime(&ms, evs[k + 6], evs[k + 7]));
             tm.resample_ms += ms;
         }

@@ -84,6 +84,10 @@ struct wsmc_ctx {
     ncclComm_t comm = nullptr;
     wsmc_exchange_fn host_exchange = nullptr;   // host-side record exchange (instead of RCCL)
     unsigned long long* run_grp = nullptr;      // [T+1][ngroups][kGroupLine] fused-run group sums
+    unsigned long long* run_pay = nullptr;      // sharded fused run: [T+1][world][PW] exchange payloads
+    int64_t run_pay_world = 0;
+    hipStream_t stream2 = nullptr;              // sharded fused run: exchange + decision stream
+    hipEvent_t ev_sums = nullptr, ev_dec = nullptr;
     void* host_user = nullptr;
 
     // store
@@ -170,7 +174,9 @@ hipError_t launch_rs_max(hipStream_t s, const double* w, int64_t N, MaxSlots* ms
 hipError_t launch_rs_sums(hipStream_t s, const double* w, int64_t N, const MaxSlots* ms,
                           unsigned long long* tilep, unsigned long long* qbuf,
                           hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr,
-                          unsigned long long* grp = nullptr, int G = 1);
+                          unsigned long long* grp = nullptr, int G = 1, unsigned long long* hdr = nullptr);
+hipError_t launch_rs_decide_groups(hipStream_t s, const unsigned long long* pay, int64_t PW, int ngroups, int world,
+                                   int rank, double ess_min, ShardRecord* recs, Decision* dec);
 struct FillPlan {          // ancestor-fill task planning (in the reduce kernel)
     const unsigned long long* tilep;   // per-tile partials (sum q first)
     int32_t* taskOff;
@@ -191,6 +197,7 @@ hipError_t launch_rs_scan(hipStream_t s, int64_t N, const ShardRecord* rec, cons
                           hipEvent_t e1 = nullptr);
 // fused single-GPU run: group sums (kGroupLine u64 per group) replace the reduce kernel
 constexpr int kGroupLine = 8;
+constexpr int kMaxWorld = kMaxShards;   // ranks of one node
 inline int group_tiles(int64_t N) {   // tiles per group: ~sqrt(ntiles), >= 16
     const int64_t nt = (N + kRsTile - 1) / kRsTile;
     int G = 16;
