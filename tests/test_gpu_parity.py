@@ -175,3 +175,44 @@ def test_resample_skewed_large(gpu_available, kind):
     assert g.resample(2.0) == o.resample(2.0)
     np.testing.assert_array_equal(g.last_ancestors(), o.last_ancestors())
     np.testing.assert_array_equal(g.weights_download(), o.weights_download())
+
+
+@pytest.mark.parametrize("kind", ["all_neg_inf", "one_nan", "one_pos_inf"])
+def test_resample_degenerate_weights(gpu_available, kind):
+    """exp_norm of all -Inf / any NaN weights is NaN, so ESS is NaN and the strict test
+    never resamples (src/resampling.jl:72-77, src/transformers.jl:484); +Inf dominates."""
+    N = 3000
+    w = np.random.default_rng(3).standard_normal(N)
+    if kind == "all_neg_inf":
+        w[:] = -np.inf
+    elif kind == "one_nan":
+        w[17] = np.nan
+    else:
+        w[17] = np.inf
+    from wsmc.dsl import Normal
+    g, o = wsmc.Context(N, seed=5), Oracle(N, seed=5)
+    for c in (g, o):
+        c.col_create("x")
+        c.assign(c.col_find("x"), abi.Operand.const(1.0))
+        c.weights_upload(w)
+        c.weight(Normal(0.0, 1.0).dist(c.col_find), [abi.Operand.const(0.0)])
+    lg, lo = g.log_evidence(), o.log_evidence()
+    assert lg == lo or (math.isnan(lg) and math.isnan(lo))
+    rg, ro = g.resample(1.0), o.resample(1.0)
+    assert rg[0] == ro[0]
+    assert rg[1] == ro[1] or (math.isnan(rg[1]) and math.isnan(ro[1]))
+    np.testing.assert_array_equal(g.weights_download(), o.weights_download())
+
+
+def test_ssm2d_fused_nan_observation(gpu_available):
+    """A NaN observation makes every weight NaN mid-run: no resample from then on, in the
+    fused run exactly as in the statements and the oracle."""
+    obs = models.ssm2d_data(8).copy()
+    obs[4, 1] = np.nan
+    g = wsmc.Context(2048, seed=3)
+    evg = g.ssm2d_run(obs, ess_perc_min=1.0, keep_history=True)
+    o = Oracle(2048, seed=3)
+    flags = models.ssm2d_statements(o, obs, ess_perc_min=1.0)
+    assert flags[5:] == [False] * 3
+    assert_same_state(g, o)
+    assert math.isnan(evg) and math.isnan(o.log_evidence())
