@@ -497,7 +497,7 @@ __device__ __forceinline__ void load_tile_q(int64_t N, int b, const u64* __restr
 }
 
 template <int MODE>
-__device__ __forceinline__ void fill_chunk_q(int64_t N, int b, int j, u64 Q, u64 off, const FillPlan& plan,
+__device__ __forceinline__ void fill_chunk_q(int64_t N, int b, int j, u64 Q, u64 off, u64 qb, const FillPlan& plan,
                                              uint64_t opx, const u64 (&q)[kRsTile / kScanBlock],
                                              int32_t* __restrict__ anc, FillLds& sh) {
     constexpr int IT = kRsTile / kScanBlock;   // 4 particles per thread, blocked
@@ -510,7 +510,7 @@ __device__ __forceinline__ void fill_chunk_q(int64_t N, int b, int j, u64 Q, u64
     // the tile's slot range [L, H) = [rank(off), rank(off + Q_b)), ranked by two threads
     // while the others scan; the scan's barrier publishes them
     if (th < 2) {
-        const u64 c = th == 0 ? off : off + plan.tilep[(int64_t)b * kPart];
+        const u64 c = th == 0 ? off : off + qb;
         sh.LH[th] = wsmc_rank_r(c, Q, (uint64_t)N, ratio, plan.scheme, plan.seed, opx, (uint64_t)plan.slot_base);
     }
     if (th == 0) sh.nheavy = 0;
@@ -584,7 +584,8 @@ __device__ __forceinline__ void fill_chunk(int64_t N, int b, int j, u64 Q, u64 o
                                            FillLds& sh) {
     u64 q[kRsTile / kScanBlock];
     load_tile_q(N, b, qbuf, q);
-    fill_chunk_q<MODE>(N, b, j, Q, off, plan, opx, q, anc, sh);
+    const u64 qb = plan.tilep[(int64_t)b * kPart];
+    fill_chunk_q<MODE>(N, b, j, Q, off, qb, plan, opx, q, anc, sh);
 }
 
 // Ancestor fill (the icdf merge, src/resampling.jl:13-26): ancestor(slot n) = smallest m
@@ -696,6 +697,7 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
         // ---- first chunk of tile t (its q loads in flight while the offset is summed) ----
         u64 q[kRsTile / kScanBlock];
         load_tile_q(N, t, qbuf, q);
+        const u64 qb = plan.tilep[(int64_t)t * kPart];   // every load of the block is issued here
         const int g = t / G;
         u64 pre = 0, tot = 0;
         for (int k = th; k < ngroups; k += kScanBlock) {
@@ -705,7 +707,7 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
         }
         for (int b = g * G + th; b < t; b += kScanBlock) pre += plan.tilep[(int64_t)b * kPart];
         block_sum2_u64(pre, tot, s_red);
-        fill_chunk_q<0>(N, t, 0, tot, pre, plan, opx, q, anc, sh);
+        fill_chunk_q<0>(N, t, 0, tot, pre, qb, plan, opx, q, anc, sh);
         return;
     }
     // ---- overflow chunks: plan from the tile sums (contiguous tiles per thread) ----
