@@ -163,6 +163,18 @@ int wsmc_weights_download(wsmc_ctx* ctx, double* host);
 /* logsumexp(weights) - log(N)  (src/utils.jl:21) */
 int wsmc_log_evidence(wsmc_ctx* ctx, double* out);
 
+/* ---- analysis reductions (src/utils.jl), no N-sized download -------------------------
+ * Weighted moments under w = exp_norm(weights) of up to 4 expressions (operand form):
+ * mean[k] = sum w_i v_k(i) / sum w_i           expectation / @E (src/utils.jl:11, 23-58)
+ * cov[a*d+b] = sum w_i (v_a - mean_a)(v_b - mean_b) / sum w_i
+ *                                             describe's std(..., corrected=false) (:233-240)
+ * in the canonical reduction order of the autoRW moments; cov may be NULL. */
+int wsmc_weighted_moments(wsmc_ctx* ctx, const wsmc_operand* exprs, int32_t d, double* mean, double* cov);
+/* unweighted minimum / maximum of a column component (describe, src/utils.jl:238-239) */
+int wsmc_col_minmax(wsmc_ctx* ctx, int32_t col_id, int32_t comp, double* min_out, double* max_out);
+/* ess_perc(exp_norm(weights)) (src/resampling.jl:51-54) without resampling or any state change */
+int wsmc_ess(wsmc_ctx* ctx, double* ess_perc);
+
 /* ---- operators (apply!) ------------------------------------------------------ */
 /* Assign: out[k] .= expr[k] for k < dim(out)            src/transformers.jl:28-32 */
 int wsmc_assign(wsmc_ctx* ctx, int32_t out_col, const wsmc_operand* expr);

@@ -66,6 +66,9 @@ _SIG = {
                           C.c_double, C.POINTER(C.c_int64)]),
     "or_score": (None, [_P, C.c_int32, _D]),
     "or_philox": (None, [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    "or_weighted_moments": (C.c_int, [_P, C.c_void_p, C.c_int32, _D, _D]),
+    "or_col_minmax": (C.c_int, [_P, C.c_int32, C.c_int32, _D, _D]),
+    "or_ess": (C.c_double, [_P]),
     "or_exp": (C.c_double, [C.c_double]),
     "or_expw": (C.c_double, [C.c_double]),
     "or_log": (C.c_double, [C.c_double]),
@@ -199,6 +202,25 @@ class Oracle:
 
     def log_evidence(self) -> float:
         return float(self._L.or_log_evidence(self._h))
+
+    # ---- analysis reductions ----
+    def weighted_moments(self, exprs, want_cov: bool = True):
+        ex = list(exprs) if isinstance(exprs, (list, tuple)) else [exprs]
+        d = len(ex)
+        arr = _operand_array(ex)
+        mean = np.zeros(d)
+        cov = np.zeros(d * d)
+        self._chk(self._L.or_weighted_moments(self._h, _addr(arr), d, _dptr(mean),
+                                              _dptr(cov) if want_cov else None))
+        return mean, (cov.reshape(d, d) if want_cov else None)
+
+    def col_minmax(self, col: int, comp: int = 0):
+        mn, mx = C.c_double(), C.c_double()
+        self._chk(self._L.or_col_minmax(self._h, int(col), int(comp), C.byref(mn), C.byref(mx)))
+        return float(mn.value), float(mx.value)
+
+    def ess(self) -> float:
+        return float(self._L.or_ess(self._h))
 
     def get_state(self) -> dict:
         L, h = self._L, self._h

@@ -395,6 +395,62 @@ double or_log_evidence_records(const uint64_t* recs, int32_t G) {
     return wsmc_global_log_evidence(st, G);
 }
 
+/* ---- analysis reductions (src/utils.jl) ------------------------------------------------
+ * Weighted moments under exp_norm(weights) of d <= 4 operand expressions, in the canonical
+ * reduction order the device uses (or_canon_sum): expectation / @E (src/utils.jl:11, 23-58)
+ * and describe's mean and std(corrected=false) (:233-240). */
+double or_canon_sum(const double* vals, int64_t n);
+int or_weighted_moments(oracle* o, const wsmc_operand* ex, int32_t d, double* mean, double* cov) {
+    int64_t N = o->N;
+    if (d < 1 || d > 4) return WSMC_EARG;
+    double M = -WSMC_INF;
+    for (int64_t i = 0; i < N; ++i) if (o->w[i] > M || wsmc_isnan(o->w[i])) M = o->w[i];
+    double* e = (double*)malloc(sizeof(double) * (size_t)N);
+    double* z = (double*)malloc(sizeof(double) * (size_t)(N * d));
+    double* v = o->scratch;
+    for (int64_t i = 0; i < N; ++i) e[i] = wsmc_exp(o->w[i] - M);
+    for (int k = 0; k < d; ++k)
+        for (int64_t i = 0; i < N; ++i) z[(int64_t)k * N + i] = wsmc_operand_eval(&ex[k], o->colptr, N, i, 0);
+    double S0 = or_canon_sum(e, N);
+    for (int k = 0; k < d; ++k) {
+        for (int64_t i = 0; i < N; ++i) v[i] = e[i] * z[(int64_t)k * N + i];
+        mean[k] = or_canon_sum(v, N) / S0;
+    }
+    if (cov)
+        for (int a = 0; a < d; ++a)
+            for (int b = a; b < d; ++b) {
+                for (int64_t i = 0; i < N; ++i)
+                    v[i] = (e[i] * (z[(int64_t)a * N + i] - mean[a])) * (z[(int64_t)b * N + i] - mean[b]);
+                double c = or_canon_sum(v, N) / S0;
+                cov[a * d + b] = c; cov[b * d + a] = c;
+            }
+    free(e); free(z);
+    return 0;
+}
+/* minimum / maximum of a column component; NaN propagates (Base.minimum / maximum) */
+int or_col_minmax(oracle* o, int32_t col, int32_t comp, double* mn, double* mx) {
+    if (col < 0 || col >= o->ncols || comp < 0 || comp >= o->cols[col].dim) return WSMC_EARG;
+    const double* x = o->cols[col].front + (int64_t)comp * o->N;
+    uint64_t a = 0, b = 0;
+    for (int64_t i = 0; i < o->N; ++i) {
+        uint64_t ea = wsmc_ord_enc(x[i]), eb = wsmc_ord_enc(-x[i]);
+        if (ea > a) a = ea;
+        if (eb > b) b = eb;
+    }
+    *mx = wsmc_ord_dec(a);
+    *mn = -wsmc_ord_dec(b);
+    return 0;
+}
+/* ess_perc of the current weights, no state change (src/resampling.jl:51-54) */
+double or_ess(oracle* o) {
+    or_stats st[OR_MAX_SHARDS];
+    for (int g = 0; g < o->nshards; ++g) {
+        int64_t a = o->shard_off[g], b = o->shard_off[g + 1];
+        st[g] = shard_stats(o->w + a, b - a, wsmc_qbits((uint64_t)(b - a)));
+    }
+    return wsmc_global_ess(st, o->nshards);
+}
+
 /* logsumexp(weights) - log(N) via the same fixed point (src/utils.jl:21) */
 double or_log_evidence(oracle* o) {
     or_stats st[OR_MAX_SHARDS];

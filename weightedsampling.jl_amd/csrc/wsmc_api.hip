@@ -471,6 +471,73 @@ static int exchange_recs(wsmc_ctx* c, ShardRecord* recs) {
     return WSMC_OK;
 }
 
+// ---- analysis reductions (src/utils.jl) ----------------------------------------------
+int wsmc_weighted_moments(wsmc_ctx* c, const wsmc_operand* exprs, int32_t d, double* mean, double* cov) {
+    CHECK_CTX(c);
+    if (!exprs || !mean || d < 1 || d > 4) return fail(WSMC_EARG, "need 1..4 expressions and a mean buffer");
+    if (c->world > 1) return fail(WSMC_ESTATE, "analysis reductions on sharded contexts are not supported yet");
+    for (int k = 0; k < d; ++k) {
+        int r = check_operand(c, exprs[k]);
+        if (r) return r;
+    }
+    int r = upload_colptr(c);
+    if (r) return r;
+    wsmc_operand ex[4];
+    for (int k = 0; k < 4; ++k) ex[k] = exprs[k < d ? k : 0];
+    WSMC_HIP(hipMemsetAsync(c->mslots, 0, sizeof(MaxSlots), c->stream));
+    WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, c->mslots));
+    WSMC_HIP(launch_moments_expr(c->stream, c->w, c->mslots, c->d_colptr, ex, d, 1, c->mom, c->N, c->tilepart));
+    WSMC_HIP(launch_moments_final(c->stream, c->tilepart, c->ntiles, d, 1, 0.0, c->mom, c->dflag, 1));
+    if (cov) {
+        WSMC_HIP(launch_moments_expr(c->stream, c->w, c->mslots, c->d_colptr, ex, d, 2, c->mom, c->N, c->tilepart));
+        WSMC_HIP(launch_moments_final(c->stream, c->tilepart, c->ntiles, d, 2, 0.0, c->mom, c->dflag, 1));
+    }
+    double h[32];
+    WSMC_HIP(hipMemcpyAsync(h, c->mom, sizeof(double) * 32, hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    for (int k = 0; k < d; ++k) mean[k] = h[k];
+    if (cov)
+        for (int k = 0; k < d * d; ++k) cov[k] = h[16 + k];
+    return WSMC_OK;
+}
+
+int wsmc_col_minmax(wsmc_ctx* c, int32_t col, int32_t comp, double* mn, double* mx) {
+    CHECK_CTX(c);
+    if (col < 0 || col >= (int32_t)c->cols.size()) return fail(WSMC_EARG, "bad column");
+    if (comp < 0 || comp >= c->cols[col].dim) return fail(WSMC_EARG, "bad component");
+    if (!mn || !mx) return fail(WSMC_EARG, "null output");
+    WSMC_HIP(hipMemsetAsync(c->mslots, 0, sizeof(MaxSlots), c->stream));
+    WSMC_HIP(launch_minmax(c->stream, c->cols[col].front + (int64_t)comp * c->N, c->N, c->mslots));
+    MaxSlots h;
+    WSMC_HIP(hipMemcpyAsync(&h, c->mslots, sizeof(MaxSlots), hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    unsigned long long a = 0, b = 0;
+    for (int k = 0; k < kSlots; ++k) {
+        a = h.v[k][0] > a ? h.v[k][0] : a;
+        b = h.v[k][1] > b ? h.v[k][1] : b;
+    }
+    *mx = wsmc_ord_dec(a);
+    *mn = -wsmc_ord_dec(b);
+    return WSMC_OK;
+}
+
+int wsmc_ess(wsmc_ctx* c, double* ess_perc) {
+    CHECK_CTX(c);
+    if (!ess_perc) return fail(WSMC_EARG, "null output");
+    WSMC_HIP(hipMemsetAsync(c->mslots, 0, sizeof(MaxSlots), c->stream));
+    WSMC_HIP(launch_log_evidence_stats(c->stream, c->w, c->N, c->mslots, c->tilep, c->qbuf, c->tileOff,
+                                       c->rec + c->rank));
+    int r = exchange_recs(c, c->rec);
+    if (r) return r;
+    std::vector<ShardRecord> h(c->world);
+    WSMC_HIP(hipMemcpyAsync(h.data(), c->rec, sizeof(ShardRecord) * c->world, hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    wsmc_shard_stats st[kMaxWorld];
+    for (int g = 0; g < c->world; ++g) st[g] = host_record_stats(h[g]);
+    *ess_perc = wsmc_global_ess(st, c->world);
+    return WSMC_OK;
+}
+
 int wsmc_log_evidence(wsmc_ctx* c, double* out) {
     CHECK_CTX(c);
     if (!out) return fail(WSMC_EARG, "null out");

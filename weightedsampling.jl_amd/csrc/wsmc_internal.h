@@ -219,7 +219,11 @@ hipError_t launch_moments(hipStream_t s, const double* w, const MaxSlots* ms, do
                           const int32_t* tcols, int d, const double* lo, const double* hi,
                           int pass, const double* mom, int64_t N, double* tilepart);
 hipError_t launch_moments_final(hipStream_t s, const double* tilepart, int64_t ntiles, int d,
-                                int pass, double min_step, double* mom, int32_t* flag);
+                                int pass, double min_step, double* mom, int32_t* flag, int raw = 0);
+hipError_t launch_moments_expr(hipStream_t s, const double* w, const MaxSlots* ms, double* const* cols,
+                               const wsmc_operand* ex, int d, int pass, const double* mom, int64_t N,
+                               double* tilepart);
+hipError_t launch_minmax(hipStream_t s, const double* x, int64_t N, MaxSlots* ms);
 hipError_t launch_move(hipStream_t s, const wsmc_term* tape, int32_t nterms, int32_t depth,
                        double* const* cols, const int32_t* tcols, int d, const double* lo,
                        const double* hi, int bounded, const double* L, uint64_t seed,

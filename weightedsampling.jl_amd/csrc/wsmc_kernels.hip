@@ -777,6 +777,8 @@ __global__ __launch_bounds__(kBlock) void k_score(const wsmc_term* tape, int32_t
 struct MomArgs {
     int32_t tcol[4];
     double lo[4], hi[4];
+    int32_t use_ex;          // analysis moments: values are operand expressions (identity transform)
+    wsmc_operand ex[4];
 };
 
 // pass 1: values {e, e*z_k};  pass 2: values {(e*(z_a-mean_a))*(z_b-mean_b), a <= b}
@@ -803,7 +805,9 @@ __global__ __launch_bounds__(kBlock) void k_moments(const double* __restrict__ w
         if (i < N) {
             const double e = wsmc_exp(w[i] - M);
             double z[4];
-            for (int k = 0; k < d; ++k) z[k] = wsmc_to_unc(cols[ma.tcol[k]][i], ma.lo[k], ma.hi[k]);
+            for (int k = 0; k < d; ++k)
+                z[k] = ma.use_ex ? wsmc_operand_eval(&ma.ex[k], cols, N, i, nullptr)
+                                 : wsmc_to_unc(cols[ma.tcol[k]][i], ma.lo[k], ma.hi[k]);
             if (pass == 1) {
                 vals[0] = e;
                 for (int k = 0; k < d; ++k) vals[1 + k] = e * z[k];
@@ -826,7 +830,7 @@ __global__ __launch_bounds__(kBlock) void k_moments(const double* __restrict__ w
 // pass 2 -> mom[16..16+d*d) = lambda*Sigma (zeros -> min_step), mom[32..32+d*d) = chol
 __global__ __launch_bounds__(kBlock) void k_moments_final(const double* tilepart, int64_t ntiles, int d,
                                                           int pass, double min_step, double* mom,
-                                                          int32_t* flag) {
+                                                          int32_t* flag, int raw) {
     __shared__ double lds4[4];
     __shared__ double tot[10];
     const int nv = pass == 1 ? 1 + d : d * (d + 1) / 2;
@@ -853,6 +857,10 @@ __global__ __launch_bounds__(kBlock) void k_moments_final(const double* tilepart
             S[a * d + b] = c;
             S[b * d + a] = c;
         }
+    if (raw) {   // analysis moments: the weighted covariance itself
+        for (int k = 0; k < d * d; ++k) mom[16 + k] = S[k];
+        return;
+    }
     const double lam = 2.38 / wsmc_sqrt((double)d);
     for (int k = 0; k < d * d; ++k) {
         if (S[k] == 0.0) S[k] = min_step;
@@ -1297,15 +1305,52 @@ hipError_t launch_moments(hipStream_t s, const double* w, const MaxSlots* rec, d
         ma.lo[k] = (k < d && lo) ? lo[k] : -WSMC_INF;
         ma.hi[k] = (k < d && hi) ? hi[k] : WSMC_INF;
     }
+    ma.use_ex = 0;
     const int64_t nt = (N + kTile - 1) / kTile;
     hipLaunchKernelGGL(k_moments, tiles_for(N), dim3(kBlock), 0, s, w, rec, cols, ma, d, pass, mom, N, nt,
                        tilepart);
     return hipGetLastError();
 }
+hipError_t launch_moments_expr(hipStream_t s, const double* w, const MaxSlots* ms, double* const* cols,
+                               const wsmc_operand* ex, int d, int pass, const double* mom, int64_t N,
+                               double* tilepart) {
+    MomArgs ma;
+    for (int k = 0; k < 4; ++k) {
+        ma.tcol[k] = 0;
+        ma.lo[k] = -WSMC_INF;
+        ma.hi[k] = WSMC_INF;
+        ma.ex[k] = ex[k < d ? k : 0];
+    }
+    ma.use_ex = 1;
+    const int64_t nt = (N + kTile - 1) / kTile;
+    hipLaunchKernelGGL(k_moments, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, d, pass, mom, N, nt, tilepart);
+    return hipGetLastError();
+}
+// unweighted min / max of one column component (describe): ordered-encoding maxima of x and
+// of -x into the line-strided slots (NaN propagates, as Base.minimum / maximum)
+__global__ __launch_bounds__(kBlock) void k_minmax(const double* __restrict__ x, int64_t N, MaxSlots* ms) {
+    __shared__ u64 lds4[4];
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    u64 a = 0, b = 0;
+    if (i < N) {
+        a = wsmc_ord_enc(x[i]);
+        b = wsmc_ord_enc(-x[i]);
+    }
+    a = block_max_u64(a, lds4);
+    b = block_max_u64(b, lds4);
+    if (threadIdx.x == 0) {
+        atomic_max_filtered(&ms->v[blockIdx.x % kSlots][0], a);
+        atomic_max_filtered(&ms->v[blockIdx.x % kSlots][1], b);
+    }
+}
+hipError_t launch_minmax(hipStream_t s, const double* x, int64_t N, MaxSlots* ms) {
+    hipLaunchKernelGGL(k_minmax, grid_for(N), dim3(kBlock), 0, s, x, N, ms);
+    return hipGetLastError();
+}
 hipError_t launch_moments_final(hipStream_t s, const double* tilepart, int64_t ntiles, int d, int pass,
-                                double min_step, double* mom, int32_t* flag) {
+                                double min_step, double* mom, int32_t* flag, int raw) {
     hipLaunchKernelGGL(k_moments_final, dim3(1), dim3(kBlock), 0, s, tilepart, ntiles, d, pass, min_step, mom,
-                       flag);
+                       flag, raw);
     return hipGetLastError();
 }
 hipError_t launch_move(hipStream_t s, const wsmc_term* tape, int32_t nterms, int32_t depth, double* const* cols,

@@ -95,6 +95,9 @@ SIGNATURES = {
     "wsmc_weights_upload": (C.c_int, [_P, _D]),
     "wsmc_weights_download": (C.c_int, [_P, _D]),
     "wsmc_log_evidence": (C.c_int, [_P, _D]),
+    "wsmc_weighted_moments": (C.c_int, [_P, C.POINTER(Operand), C.c_int32, _D, _D]),
+    "wsmc_col_minmax": (C.c_int, [_P, C.c_int32, C.c_int32, _D, _D]),
+    "wsmc_ess": (C.c_int, [_P, _D]),
     "wsmc_assign": (C.c_int, [_P, C.c_int32, C.POINTER(Operand)]),
     "wsmc_sample": (C.c_int, [_P, C.c_int32, C.POINTER(Dist)]),
     "wsmc_sample_importance": (C.c_int, [_P, C.c_int32, C.POINTER(Dist), C.POINTER(Dist)]),

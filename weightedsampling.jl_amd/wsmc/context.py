@@ -153,6 +153,30 @@ class Context:
         check(self._L.wsmc_log_evidence(self._h, C.byref(v)))
         return float(v.value)
 
+    # ---- analysis reductions (src/utils.jl) ----
+    def weighted_moments(self, exprs, want_cov: bool = True):
+        """Means (and uncorrected covariance) of up to 4 operand expressions under
+        exp_norm(weights): expectation / @E and describe's mean / std."""
+        ex = list(exprs) if isinstance(exprs, (list, tuple)) else [exprs]
+        d = len(ex)
+        arr = (Operand * 4)()
+        for k in range(4):
+            arr[k] = ex[k] if k < d else ex[0]
+        mean = np.zeros(d)
+        cov = np.zeros(d * d)
+        check(self._L.wsmc_weighted_moments(self._h, arr, d, _dptr(mean), _dptr(cov) if want_cov else None))
+        return mean, (cov.reshape(d, d) if want_cov else None)
+
+    def col_minmax(self, col: int, comp: int = 0):
+        mn, mx = C.c_double(), C.c_double()
+        check(self._L.wsmc_col_minmax(self._h, int(col), int(comp), C.byref(mn), C.byref(mx)))
+        return float(mn.value), float(mx.value)
+
+    def ess(self) -> float:
+        v = C.c_double()
+        check(self._L.wsmc_ess(self._h, C.byref(v)))
+        return float(v.value)
+
     def get_state(self) -> dict:
         s = State()
         check(self._L.wsmc_get_state(self._h, C.byref(s)))

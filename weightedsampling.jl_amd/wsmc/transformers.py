@@ -325,6 +325,50 @@ def marginal_diversity(store: HipColumnStore, targets) -> float:
     return store.ctx.marginal_diversity([store.resolve(t) for t in targets])
 
 
+# ---------------------------------------------------------------------------------------
+# analysis (src/utils.jl), reduced on the device
+# ---------------------------------------------------------------------------------------
+def expectation(state: SMCState, expr) -> float:
+    """Weighted expectation under exp_norm(weights) (src/utils.jl:11; @E, :23-58) of an affine
+    expression of particle variables, e.g. ``expectation(state, Col("x"))`` or
+    ``Col("alpha") + 2.0 * Col("beta")``. Non-affine functions are evaluated on the host from
+    ``state[name]``."""
+    mean, _ = state.ctx.weighted_moments([Expr.lift(expr).operand(state.store.resolve)], want_cov=False)
+    return float(mean[0])
+
+
+def describe(state: SMCState, cols=None) -> list[dict]:
+    """describe(state; cols) (src/utils.jl:157-289): per numeric column its weighted mean,
+    weighted std (StatsBase, corrected=false), min, max and ESS = N * ess_perc; vector
+    columns component-wise. The weighted median and the sparkline histogram need a sort or
+    a histogram pass and are not computed on the device (median/hist are None)."""
+    store = state.store
+    names = store.colnames() if cols is None else list(cols)
+    for n in names:
+        if not store.hascol(n):
+            raise ValueError(f"Column {n} not found in store")
+    ess = state.nparticles() * state.ctx.ess()
+    rows = []
+    for n in names:
+        c = store.resolve(n)
+        d = state.ctx.col_dim(c)
+        means, stds, mins, maxs = [], [], [], []
+        for k0 in range(0, d, 4):
+            ks = list(range(k0, min(d, k0 + 4)))
+            mean, cov = state.ctx.weighted_moments([Operand.column(c, k) for k in ks])
+            means += list(mean)
+            stds += [math.sqrt(cov[j, j]) for j in range(len(ks))]
+        for k in range(d):
+            mn, mx = state.ctx.col_minmax(c, k)
+            mins.append(mn)
+            maxs.append(mx)
+        one = d == 1
+        rows.append(dict(variable=n, mean=means[0] if one else means, median=None,
+                         std=stds[0] if one else stds, min=mins[0] if one else mins,
+                         max=maxs[0] if one else maxs, hist=None, ess=ess))
+    return rows
+
+
 def resampled(state: SMCState) -> bool:
     """The `if resampled` predicate of @model bodies (src/rewrites.jl:360-368)."""
     return state.resampled
