@@ -52,18 +52,39 @@ WSMC_HD double wsmc_dist_mean(const wsmc_dist* d, int k, double* const* cols, in
     return wsmc_operand_eval(&d->mu[k], cols, N, i, ov);
 }
 
+/* log of a scale parameter, remembered across the terms of one fold: a particle's terms
+ * often share one sigma / variance value (e.g. a sigma column), and the log of the same
+ * bits is the same bits, so reusing it changes nothing but the work. */
+typedef struct {
+    uint64_t arg;
+    double val;
+    int valid;
+} wsmc_logmemo;
+WSMC_HD double wsmc_log_memo(wsmc_logmemo* m, double x) {
+    if (!m) return wsmc_log(x);
+    uint64_t b = wsmc_d2bits(x);
+    if (m->valid && m->arg == b) return m->val;
+    m->arg = b;
+    m->val = wsmc_log(x);
+    m->valid = 1;
+    return m->val;
+}
+
 /* logpdf(D(args...), x) for the supported families */
-WSMC_HD double wsmc_dist_logpdf(const wsmc_dist* d, const double* x, double* const* cols, int64_t N,
-                                int64_t i, const wsmc_override* ov) {
+WSMC_HD double wsmc_dist_logpdf_m(const wsmc_dist* d, const double* x, double* const* cols, int64_t N,
+                                  int64_t i, const wsmc_override* ov, wsmc_logmemo* lm) {
     switch (d->family) {
-        case WSMC_FAM_NORMAL: {
+        case WSMC_FAM_NORMAL: {   /* wsmc_normal_logpdf with a remembered log(sigma) */
             double mu = wsmc_dist_mean(d, 0, cols, N, i, ov);
             double sg = wsmc_operand_eval(&d->scale, cols, N, i, ov);
-            return wsmc_normal_logpdf(mu, sg, x[0]);
+            double z = (x[0] - mu) / sg;
+            return -(z * z + WSMC_LOG2PI) * 0.5 - wsmc_log_memo(lm, sg);
         }
-        case WSMC_FAM_HALFNORMAL: {
+        case WSMC_FAM_HALFNORMAL: {   /* wsmc_halfnormal_logpdf likewise */
             double sg = wsmc_operand_eval(&d->scale, cols, N, i, ov);
-            return wsmc_halfnormal_logpdf(sg, x[0]);
+            if (!(x[0] >= 0.0)) return -WSMC_INF;
+            double z = (x[0] - 0.0) / sg;
+            return (-(z * z + WSMC_LOG2PI) * 0.5 - wsmc_log_memo(lm, sg)) + WSMC_LOG2;
         }
         case WSMC_FAM_UNIFORM:
             return wsmc_uniform_logpdf(d->param[0], d->param[1], x[0]);
@@ -75,9 +96,13 @@ WSMC_HD double wsmc_dist_logpdf(const wsmc_dist* d, const double* x, double* con
                 s = s + dx * dx;
             }
             double dd = (double)d->dim;
-            return -((dd * WSMC_LOG2PI + dd * wsmc_log(var)) + s / var) * 0.5;
+            return -((dd * WSMC_LOG2PI + dd * wsmc_log_memo(lm, var)) + s / var) * 0.5;
         }
     }
+}
+WSMC_HD double wsmc_dist_logpdf(const wsmc_dist* d, const double* x, double* const* cols, int64_t N,
+                                int64_t i, const wsmc_override* ov) {
+    return wsmc_dist_logpdf_m(d, x, cols, N, i, ov, 0);
 }
 
 /* rand(D(args...)) for particle i (global RNG index idx) */
@@ -114,21 +139,39 @@ WSMC_HD void wsmc_dist_sample(const wsmc_dist* d, double* x, uint64_t seed, uint
     }
 }
 
-WSMC_HD double wsmc_term_logpdf(const wsmc_term* t, double* const* cols, int64_t N, int64_t i,
-                                const wsmc_override* ov) {
+WSMC_HD double wsmc_term_logpdf_m(const wsmc_term* t, double* const* cols, int64_t N, int64_t i,
+                                  const wsmc_override* ov, wsmc_logmemo* lm) {
     double x[4] = {0.0, 0.0, 0.0, 0.0};
     int dim = t->dist.dim < 1 ? 1 : (t->dist.dim > 4 ? 4 : t->dist.dim);
     for (int k = 0; k < dim; ++k) x[k] = wsmc_operand_eval(&t->x[k], cols, N, i, ov);
-    return wsmc_dist_logpdf(&t->dist, x, cols, N, i, ov);
+    return wsmc_dist_logpdf_m(&t->dist, x, cols, N, i, ov, lm);
+}
+WSMC_HD double wsmc_term_logpdf(const wsmc_term* t, double* const* cols, int64_t N, int64_t i,
+                                const wsmc_override* ov) {
+    return wsmc_term_logpdf_m(t, cols, N, i, ov, 0);
 }
 
 /* score_logpdf! for one particle: 0.0 then += each term with depth < target_depth */
 WSMC_HD double wsmc_fold(const wsmc_term* terms, int32_t n, int32_t target_depth, double* const* cols,
                          int64_t N, int64_t i, const wsmc_override* ov) {
     double s = 0.0;
+    wsmc_logmemo lm = {0, 0.0, 0};
     for (int32_t j = 0; j < n; ++j) {
         if (terms[j].depth >= target_depth) break;
-        s = s + wsmc_term_logpdf(&terms[j], cols, N, i, ov);
+        s = s + wsmc_term_logpdf_m(&terms[j], cols, N, i, ov, &lm);
+    }
+    return s;
+}
+
+/* the same left fold continued from s0 over terms [j0, n) — bit-identical to wsmc_fold when
+ * s0 is the fold over [0, j0) of the same values (the carried score of a Move) */
+WSMC_HD double wsmc_fold_from(double s0, const wsmc_term* terms, int32_t j0, int32_t n, int32_t target_depth,
+                              double* const* cols, int64_t N, int64_t i, const wsmc_override* ov) {
+    double s = s0;
+    wsmc_logmemo lm = {0, 0.0, 0};
+    for (int32_t j = j0; j < n; ++j) {
+        if (terms[j].depth >= target_depth) break;
+        s = s + wsmc_term_logpdf_m(&terms[j], cols, N, i, ov, &lm);
     }
     return s;
 }

@@ -216,3 +216,60 @@ def test_ssm2d_fused_nan_observation(gpu_available):
     assert flags[5:] == [False] * 3
     assert_same_state(g, o)
     assert math.isnan(evg) and math.isnan(o.log_evidence())
+
+
+def _move_program(c, variant):
+    """Moves interleaved with every operation that can stale a carried score."""
+    from wsmc.dsl import Normal
+    R = models.resolver(c)
+    a = c.col_create("a")
+    b = c.col_create("b")
+    c.sample(a, Normal(0.0, 2.0).dist(R))
+    c.sample(b, Normal(1.0, 1.0).dist(R))
+    c.observe(Normal(wsmc.Col("a") + wsmc.Col("b"), 0.7).dist(R), models._const([1.5]))
+    accs = [c.move(abi.PROPOSAL_AUTORW, [a], 1e-3)]
+    if variant == "assign":       # rewrite a column the tape reads
+        c.assign(b, abi.Operand.column(b, coef=0.5, c0=0.1))
+    elif variant == "upload":
+        c.col_upload(a, np.linspace(-1, 1, c.n))
+    elif variant == "resample_indices":
+        c.store_resample(np.arange(c.n)[::-1].copy())
+    elif variant == "resample":
+        c.observe(Normal(wsmc.Col("a"), 1.0).dist(R), models._const([0.3]))
+        c.resample(1.0)
+    elif variant == "resample_col":   # re-sample b (earlier terms read the new values)
+        c.sample(b, Normal(0.0, 1.0).dist(R))
+    elif variant == "shallower":
+        c.set_depth(2)
+    c.observe(Normal(wsmc.Col("b"), 1.3).dist(R), models._const([0.9]))
+    accs.append(c.move(abi.PROPOSAL_RW, [b], 0.4))
+    accs.append(c.move(abi.PROPOSAL_AUTORW, [a, b], 1e-3))
+    return accs
+
+
+@pytest.mark.parametrize("variant", ["none", "assign", "upload", "resample_indices", "resample", "resample_col",
+                                     "shallower"])
+def test_move_carried_scores(gpu_available, variant):
+    """The device carries each particle's Move score (a left fold, continued over new terms)
+    and must invalidate it exactly when the reference would see different term values."""
+    g, o = wsmc.Context(4099, seed=12), Oracle(4099, seed=12)
+    assert _move_program(g, variant) == _move_program(o, variant)
+    assert_same_state(g, o)
+
+
+def test_move_not_pd_leaves_state(gpu_available):
+    """autoRW with a singular covariance raises PosDefException before touching anything
+    (src/move_kernels.jl:150, TODO.md:4)."""
+    from wsmc.dsl import Normal
+    res = []
+    for c in (wsmc.Context(2048, seed=4), Oracle(2048, seed=4)):
+        R = models.resolver(c)
+        a, b = c.col_create("a"), c.col_create("b")
+        c.sample(a, Normal(0.0, 1.0).dist(R))
+        c.assign(b, abi.Operand.column(a, coef=2.0))      # b = 2a: rank-1 covariance
+        c.observe(Normal(wsmc.Col("a"), 1.0).dist(R), models._const([0.2]))
+        with pytest.raises(np.linalg.LinAlgError):
+            c.move(abi.PROPOSAL_AUTORW, [a, b], 1e-3)
+        c.move(abi.PROPOSAL_RW, [a], 0.3)
+        res.append(c)
+    assert_same_state(*res)

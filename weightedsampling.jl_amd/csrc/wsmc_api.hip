@@ -105,6 +105,21 @@ static wsmc_operand col_operand(int32_t col, int32_t comp) {
     return r;
 }
 
+// does any tape term read column `col` (its value, its distribution's arguments)?
+static bool tape_reads(const wsmc_ctx* c, int32_t col) {
+    auto uses = [&](const wsmc_operand& o) { return o.col[0] == col || o.col[1] == col; };
+    for (const wsmc_term& t : c->tape) {
+        for (int k = 0; k < 4; ++k)
+            if (uses(t.x[k]) || uses(t.dist.mu[k])) return true;
+        if (uses(t.dist.scale)) return true;
+    }
+    return false;
+}
+// a write to a column the tape reads changes past terms' values: the carried scores are stale
+static void scores_touch(wsmc_ctx* c, int32_t col) {
+    if (c->scache_terms >= 0 && tape_reads(c, col)) c->scache_terms = -1;
+}
+
 static int gather_all_columns(wsmc_ctx* c) {
     for (auto& col : c->cols) {
         for (int k = 0; k < col.dim; ++k) {
@@ -112,6 +127,10 @@ static int gather_all_columns(wsmc_ctx* c) {
                                    c->N));
         }
         std::swap(col.front, col.back);
+    }
+    if (c->scache && c->scache_terms >= 0) {   // carried Move scores follow their particles
+        WSMC_HIP(launch_gather(c->stream, c->scache_back, c->scache, c->anc, c->N));
+        std::swap(c->scache, c->scache_back);
     }
     c->colptr_dirty = true;
     return WSMC_OK;
@@ -208,7 +227,7 @@ int wsmc_destroy(wsmc_ctx* c) {
         (void)hipFree(col.front);
         (void)hipFree(col.back);
     }
-    void* bufs[] = {c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount,
+    void* bufs[] = {c->scache, c->scache_back, c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount,
                     c->d_colptr, c->run_params, c->d_tape, c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp,
                     c->vscratch, c->xscratch};
     for (void* p : bufs)
@@ -250,6 +269,7 @@ int wsmc_get_state(wsmc_ctx* c, wsmc_state* s) {
 int wsmc_set_depth(wsmc_ctx* c, int32_t depth) {
     if (!c) return fail(WSMC_EARG, "null context");
     c->depth = depth;
+    c->scache_terms = -1;
     return WSMC_OK;
 }
 
@@ -358,6 +378,7 @@ int wsmc_col_download(wsmc_ctx* c, int32_t col, double* host) {
 int wsmc_col_upload(wsmc_ctx* c, int32_t col, const double* host) {
     CHECK_CTX(c);
     if (!valid_col(c, col) || !host) return fail(WSMC_EARG, "bad column or null buffer");
+    scores_touch(c, col);
     WSMC_HIP(hipMemcpyAsync(c->cols[col].front, host, sizeof(double) * c->cols[col].dim * c->N,
                             hipMemcpyHostToDevice, c->stream));
     WSMC_HIP(hipStreamSynchronize(c->stream));
@@ -566,6 +587,7 @@ int wsmc_assign(wsmc_ctx* c, int32_t out, const wsmc_operand* expr) {
     }
     int r = upload_colptr(c);
     if (r) return r;
+    scores_touch(c, out);
     WSMC_HIP(launch_assign(c->stream, c->cols[out].front, dim, expr, c->d_colptr, c->N));
     c->depth += 1;
     return WSMC_OK;
@@ -589,6 +611,7 @@ int wsmc_sample(wsmc_ctx* c, int32_t out, const wsmc_dist* d) {
     if (d->dim != c->cols[out].dim) return fail(WSMC_EARG, "dist dim != column dim");
     if ((r = upload_colptr(c))) return r;
     const uint64_t op = c->op++;
+    scores_touch(c, out);
     WSMC_HIP(launch_sample(c->stream, c->cols[out].front, d->dim, *d, c->seed, op, c->goff, c->d_colptr, c->N));
     push_sample_term(c, out, *d);
     c->depth += 1;
@@ -604,6 +627,7 @@ int wsmc_sample_importance(wsmc_ctx* c, int32_t out, const wsmc_dist* prop, cons
     if (prop->dim != c->cols[out].dim || targ->dim != c->cols[out].dim) return fail(WSMC_EARG, "dim mismatch");
     if ((r = upload_colptr(c))) return r;
     const uint64_t op = c->op++;
+    scores_touch(c, out);
     WSMC_HIP(launch_sample_importance(c->stream, c->cols[out].front, prop->dim, *prop, *targ, c->w, c->seed, op,
                                       c->goff, c->d_colptr, c->N));
     c->weights_changed = 1;
@@ -774,9 +798,19 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         for (int k = 0; k < d; ++k) L[k * d + k] = step;
         WSMC_HIP(hipMemcpyAsync(c->mom + 32, L, sizeof(double) * 16, hipMemcpyHostToDevice, c->stream));
     }
+    // carried scores: the fold prefix of this move is the terms before the first one at or
+    // beyond target_depth; continue the cache if it covers a prefix of it
+    int32_t kD = 0;
+    while (kD < (int32_t)c->tape.size() && c->tape[kD].depth < target_depth) ++kD;
+    if (!c->scache) {
+        WSMC_HIP(hipMalloc(&c->scache, sizeof(double) * c->N));
+        WSMC_HIP(hipMalloc(&c->scache_back, sizeof(double) * c->N));
+    }
+    const int32_t cache_from = (c->scache_terms >= 0 && c->scache_terms <= kD) ? c->scache_terms : -1;
     WSMC_HIP(launch_move(c->stream, c->d_tape, (int32_t)c->tape.size(), target_depth, c->d_colptr, targets, d,
                          bounded ? l : nullptr, bounded ? h : nullptr, bounded ? 1 : 0, c->mom + 32, c->seed,
-                         op_prop, op_acc, c->goff, c->N, c->ucount));
+                         op_prop, op_acc, c->goff, c->N, c->ucount,
+                         proposal == WSMC_PROPOSAL_AUTORW ? c->dflag : nullptr, c->scache, cache_from));
     struct {
         int32_t flag[4];
         unsigned long long acc[4];
@@ -785,6 +819,7 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
     WSMC_HIP(hipMemcpyAsync(hb->acc, c->ucount, sizeof(unsigned long long) * 4, hipMemcpyDeviceToHost, c->stream));
     WSMC_HIP(hipStreamSynchronize(c->stream));
     if (hb->flag[0]) return fail(WSMC_ENOTPD, "autoRW proposal covariance is not positive definite");
+    c->scache_terms = kD;
     if (accepted_out) *accepted_out = (int64_t)hb->acc[0];
     return WSMC_OK;
 }
@@ -961,6 +996,7 @@ int wsmc_run_get_timing(wsmc_ctx* c, wsmc_run_timing* out) {
 int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, const double* v0, double q_var,
                    double r_var, double ess_min, int32_t scheme, int32_t keep_history, double* log_evidence_out) {
     CHECK_CTX(c);
+    c->scache_terms = -1;   // the run rewrites columns the tape reads
     if (!obs || T < 1 || !x0 || !v0) return fail(WSMC_EARG, "bad arguments");
     if (scheme != WSMC_RESAMPLE_STRATIFIED && scheme != WSMC_RESAMPLE_SYSTEMATIC)
         return fail(WSMC_EARG, "unknown resampling scheme");

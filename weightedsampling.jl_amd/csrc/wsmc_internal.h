@@ -84,6 +84,11 @@ struct wsmc_ctx {
     ncclComm_t comm = nullptr;
     wsmc_exchange_fn host_exchange = nullptr;   // host-side record exchange (instead of RCCL)
     unsigned long long* run_grp = nullptr;      // [T+1][ngroups][kGroupLine] fused-run group sums
+    // Move score cache: each particle's fold over the first scache_terms tape terms (its
+    // score after its last move); -1 = invalid (a column the tape reads was rewritten)
+    double* scache = nullptr;
+    double* scache_back = nullptr;
+    int32_t scache_terms = -1;
     unsigned long long* run_pay = nullptr;      // sharded fused run: [T+1][world][PW] exchange payloads
     int64_t run_pay_world = 0;
     hipStream_t stream2 = nullptr;              // sharded fused run: exchange + decision stream
@@ -228,7 +233,7 @@ hipError_t launch_move(hipStream_t s, const wsmc_term* tape, int32_t nterms, int
                        double* const* cols, const int32_t* tcols, int d, const double* lo,
                        const double* hi, int bounded, const double* L, uint64_t seed,
                        uint64_t op_prop, uint64_t op_acc, int64_t goff, int64_t N,
-                       unsigned long long* accepted);
+                       unsigned long long* accepted, const int32_t* flag, double* scache, int32_t cache_from);
 hipError_t launch_diversity_keys(hipStream_t s, const double* x, unsigned long long* keys, int64_t N);
 hipError_t launch_count_unique(hipStream_t s, const unsigned long long* keys, int64_t N,
                                unsigned long long* count);

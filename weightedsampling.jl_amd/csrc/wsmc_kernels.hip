@@ -872,11 +872,18 @@ __global__ __launch_bounds__(kBlock) void k_moments_final(const double* tilepart
     if (!ok) flag[0] = 1;
 }
 
+// Move (src/transformers.jl:588-623). scache carries each particle's score from its last
+// move (the fold is a left-to-right sum, so continuing it over the terms appended since
+// [cache_from, nterms) gives the same bits as refolding); cache_from < 0 = refold.
+// A non-PD autoRW covariance (flag set by the moments pass) skips the move untouched,
+// as the reference throws before modifying anything.
 __global__ __launch_bounds__(kBlock) void k_move(const wsmc_term* tape, int32_t nterms, int32_t depth,
                                                  double* const* cols, MomArgs ma, int d, int bounded,
                                                  const double* Lm, uint64_t seed, uint64_t op_prop,
-                                                 uint64_t op_acc, int64_t goff, int64_t N, u64* accepted) {
+                                                 uint64_t op_acc, int64_t goff, int64_t N, u64* accepted,
+                                                 const int32_t* flag, double* scache, int32_t cache_from) {
     __shared__ u64 lds4[4];
+    if (flag && flag[0]) return;
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     u64 acc = 0;
     if (i < N) {
@@ -900,13 +907,16 @@ __global__ __launch_bounds__(kBlock) void k_move(const wsmc_term* tape, int32_t 
             ov.col[k] = ma.tcol[k];
             ov.val[k] = xn;
         }
-        const double s_old = wsmc_fold(tape, nterms, depth, cols, N, i, nullptr);
+        const double s_old = cache_from >= 0
+                                 ? wsmc_fold_from(scache[i], tape, cache_from, nterms, depth, cols, N, i, nullptr)
+                                 : wsmc_fold(tape, nterms, depth, cols, N, i, nullptr);
         const double s_new = wsmc_fold(tape, nterms, depth, cols, N, i, &ov);
         const double u = wsmc_uniform_k(seed, op_acc, (uint64_t)(goff + i), 0);
-        if (wsmc_log(u) < (lpr + s_new) - s_old) {
+        if (wsmc_log(u) < (lpr + s_new) - s_old) {   // strict; NaN rejects (src/transformers.jl:615)
             for (int k = 0; k < d; ++k) cols[ma.tcol[k]][i] = ov.val[k];
             acc = 1;
         }
+        scache[i] = acc ? s_new : s_old;
     }
     acc = block_sum_u64(acc, lds4);
     if (threadIdx.x == 0 && acc) atomicAdd(accepted, acc);
@@ -1356,7 +1366,8 @@ hipError_t launch_moments_final(hipStream_t s, const double* tilepart, int64_t n
 hipError_t launch_move(hipStream_t s, const wsmc_term* tape, int32_t nterms, int32_t depth, double* const* cols,
                        const int32_t* tcols, int d, const double* lo, const double* hi, int bounded,
                        const double* L, uint64_t seed, uint64_t op_prop, uint64_t op_acc, int64_t goff,
-                       int64_t N, u64* accepted) {
+                       int64_t N, u64* accepted, const int32_t* flag, double* scache,
+                       int32_t cache_from) {
     MomArgs ma;
     for (int k = 0; k < 4; ++k) {
         ma.tcol[k] = k < d ? tcols[k] : 0;
@@ -1364,7 +1375,7 @@ hipError_t launch_move(hipStream_t s, const wsmc_term* tape, int32_t nterms, int
         ma.hi[k] = (k < d && hi) ? hi[k] : WSMC_INF;
     }
     hipLaunchKernelGGL(k_move, grid_for(N), dim3(kBlock), 0, s, tape, nterms, depth, cols, ma, d, bounded, L,
-                       seed, op_prop, op_acc, goff, N, accepted);
+                       seed, op_prop, op_acc, goff, N, accepted, flag, scache, cache_from);
     return hipGetLastError();
 }
 hipError_t launch_diversity_keys(hipStream_t s, const double* x, u64* keys, int64_t N) {
