@@ -531,6 +531,7 @@ double or_marginal_diversity(oracle* o, const int32_t* targets, int32_t d) {
 /* autoRW covariance: exp_norm(weights)-weighted, uncorrected (StatsBase cov with
  * ProbabilityWeights, corrected=false), zero entries -> min_step, times 2.38/sqrt(d);
  * returns the lower Cholesky factor in L (row-major d x d), 0 if not PD. */
+double or_canon_sum(const double* vals, int64_t n);
 int or_autorw_chol(oracle* o, const int32_t* targets, int32_t d, double min_step, const double* lo,
                    const double* hi, double* L, double* cov_out) {
     int64_t N = o->N;
@@ -545,18 +546,38 @@ int or_autorw_chol(oracle* o, const int32_t* targets, int32_t d, double min_step
         double l = lo ? lo[k] : -WSMC_INF, h = hi ? hi[k] : WSMC_INF;
         for (int64_t i = 0; i < N; ++i) z[(int64_t)k * N + i] = wsmc_to_unc(x[i], l, h);
     }
-    double S0 = or_canon_sum(e, N);
+    /* canonical sums per shard, combined in rank order (one shard: the plain canonical sum);
+       the device ranks exchange exactly these per-shard totals */
+    int G = o->nshards;
+    double S0 = 0.0;
+    for (int g = 0; g < G; ++g) {
+        int64_t a = o->shard_off[g], b = o->shard_off[g + 1];
+        double t = or_canon_sum(e + a, b - a);
+        S0 = g == 0 ? t : S0 + t;
+    }
     double mean[4];
     for (int k = 0; k < d; ++k) {
         for (int64_t i = 0; i < N; ++i) v[i] = e[i] * z[(int64_t)k * N + i];
-        mean[k] = or_canon_sum(v, N) / S0;
+        double t1 = 0.0;
+        for (int g = 0; g < G; ++g) {
+            int64_t a = o->shard_off[g], b = o->shard_off[g + 1];
+            double t = or_canon_sum(v + a, b - a);
+            t1 = g == 0 ? t : t1 + t;
+        }
+        mean[k] = t1 / S0;
     }
     double S[16];
     for (int a = 0; a < d; ++a)
         for (int b = a; b < d; ++b) {
             for (int64_t i = 0; i < N; ++i)
                 v[i] = (e[i] * (z[(int64_t)a * N + i] - mean[a])) * (z[(int64_t)b * N + i] - mean[b]);
-            double c = or_canon_sum(v, N) / S0;
+            double t2 = 0.0;
+            for (int g = 0; g < G; ++g) {
+                int64_t lo_ = o->shard_off[g], hi_ = o->shard_off[g + 1];
+                double t = or_canon_sum(v + lo_, hi_ - lo_);
+                t2 = g == 0 ? t : t2 + t;
+            }
+            double c = t2 / S0;
             S[a * d + b] = c; S[b * d + a] = c;
         }
     double lam = 2.38 / wsmc_sqrt((double)d);

@@ -90,3 +90,74 @@ def test_two_shards_one_gpu_match_sharded_oracle(gpu_available, tmp_path, N, ess
         assert p["ev"][0] == ref.log_evidence()
         assert p["fev"][0] == ref.log_evidence()
 
+
+
+def _move_worker(rank, world, port, N, which, outdir):
+    sys.path[:0] = [str(REPO / "weightedsampling.jl_amd")]
+    import wsmc
+    from wsmc.hostcomm import HostComm
+    comm = HostComm(rank, world, "127.0.0.1", port, tag="mv", timeout=120)
+    n = N // world
+    c = wsmc.Context(n, seed=33, device=0)
+    c.comm_init_host(comm.allgather, world, rank, rank * n, N)
+    if which == "c3":
+        xs, ys = wsmc.models.linreg_data()
+        acc = wsmc.models.linreg_statements(c, xs[:6], ys[:6], ess_perc_min=1.0)
+    else:
+        t, y = wsmc.models.oscillator_data(n=5)
+        acc = wsmc.models.oscillator_statements(c, t, y, ess_perc_min=1.0, scheme=wsmc.RESAMPLE_SYSTEMATIC,
+                                                sweeps=2, diversity=None)
+    out = {"acc": np.array(acc), "w": c.weights_download(), "ev": np.array([c.log_evidence()])}
+    for name in c.col_names():
+        out["c_" + name] = c.col_download(c.col_find(name))
+    # the diversity gate needs a global unique count: refused on shards, not silently local
+    try:
+        c.move(wsmc.PROPOSAL_AUTORW, [c.col_find(c.col_names()[0])], 1e-3, diversity=0.9)
+        out["gate"] = np.array([0])
+    except wsmc.WSMCError:
+        out["gate"] = np.array([1])
+    c.close()
+    comm.barrier()
+    comm.close()
+    np.savez(os.path.join(outdir, f"mv{rank}.npz"), **out)
+
+
+@pytest.mark.parametrize("which", ["c3", "c5"])
+def test_two_shards_moves_match_sharded_oracle(gpu_available, tmp_path, which):
+    """Sharded autoRW: global max, per-rank canonical moment totals combined in rank order."""
+    import multiprocessing as mp
+    sys.path.insert(0, str(REPO / "oracle"))
+    from oracle import Oracle
+    import wsmc
+    N, world = 6002, 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=_move_worker, args=(r, world, port, N, which, str(tmp_path))) for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(300)
+    codes = [p.exitcode for p in ps]
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+    assert codes == [0] * world, codes
+    ref = Oracle(N, seed=33, shards=world)
+    if which == "c3":
+        xs, ys = wsmc.models.linreg_data()
+        acc = wsmc.models.linreg_statements(ref, xs[:6], ys[:6], ess_perc_min=1.0)
+    else:
+        t, y = wsmc.models.oscillator_data(n=5)
+        acc = wsmc.models.oscillator_statements(ref, t, y, ess_perc_min=1.0, scheme=wsmc.RESAMPLE_SYSTEMATIC,
+                                                sweeps=2, diversity=None)
+    n = N // world
+    parts = [np.load(tmp_path / f"mv{r}.npz") for r in range(world)]
+    # accepted counts are per shard; their sum is the single-process count
+    np.testing.assert_array_equal(sum(p["acc"] for p in parts), np.array(acc))
+    for r, p in enumerate(parts):
+        sl = slice(r * n, (r + 1) * n)
+        np.testing.assert_array_equal(p["w"], ref.weights_download()[sl])
+        for name in ref.col_names():
+            np.testing.assert_array_equal(p["c_" + name], ref.col_download(ref.col_find(name))[..., sl], err_msg=name)
+        assert p["ev"][0] == ref.log_evidence()
+        assert p["gate"][0] == 1

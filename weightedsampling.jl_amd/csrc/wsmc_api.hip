@@ -184,6 +184,7 @@ int wsmc_create(wsmc_ctx** out, int64_t n_particles, int32_t device, uint64_t se
     ALLOC(c->w, sizeof(double) * c->N);
     ALLOC(c->anc, sizeof(int32_t) * c->N);
     ALLOC(c->tmp, sizeof(double) * 4 * c->N);
+    ALLOC(c->xchg, sizeof(unsigned long long) * 16 * kMaxWorld);
     ALLOC(c->tilep, sizeof(unsigned long long) * kPart * c->nrstiles);
     ALLOC(c->tileOff, sizeof(unsigned long long) * c->nrstiles);
     ALLOC(c->taskOff, sizeof(int32_t) * c->nrstiles);
@@ -227,7 +228,7 @@ int wsmc_destroy(wsmc_ctx* c) {
         (void)hipFree(col.front);
         (void)hipFree(col.back);
     }
-    void* bufs[] = {c->scache, c->scache_back, c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount,
+    void* bufs[] = {c->xchg, c->scache, c->scache_back, c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount,
                     c->d_colptr, c->run_params, c->d_tape, c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp,
                     c->vscratch, c->xscratch};
     for (void* p : bufs)
@@ -749,6 +750,93 @@ int wsmc_marginal_diversity(wsmc_ctx* c, const int32_t* targets, int32_t d, doub
     return WSMC_OK;
 }
 
+// autoRW proposal factor on a sharded context: global max log-weight, then
+// each rank's canonical moment totals all-gathered and combined in rank order (the
+// oracle's sharded restatement), then the same min_step / 2.38/sqrt(d) / Cholesky as the
+// single-GPU kernel, on the host. Leaves L in mom + 32; WSMC_ENOTPD before any change.
+static int sharded_autorw(wsmc_ctx* c, const int32_t* targets, int d, const double* lo, const double* hi,
+                          double min_step) {
+    const int W = c->world;
+    // global max: local slots -> one encoded max per rank -> all-gather -> max
+    WSMC_HIP(hipMemsetAsync(c->mslots, 0, sizeof(MaxSlots), c->stream));
+    WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, c->mslots));
+    MaxSlots hs;
+    WSMC_HIP(hipMemcpyAsync(&hs, c->mslots, sizeof(MaxSlots), hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    unsigned long long menc = 0;
+    for (int k = 0; k < kSlots; ++k) menc = hs.v[k][0] > menc ? hs.v[k][0] : menc;
+    std::vector<unsigned long long> ex(W);
+    auto all_gather_host = [&](const unsigned long long* mine, int words, unsigned long long* all) -> int {
+        unsigned long long* dbuf = c->xchg;   // 16 words per rank
+        WSMC_HIP(hipMemcpyAsync(dbuf + (size_t)c->rank * words, mine, sizeof(unsigned long long) * words,
+                                hipMemcpyHostToDevice, c->stream));
+        int r = exchange_words(c, dbuf, words, c->stream);
+        if (r) return r;
+        WSMC_HIP(hipMemcpyAsync(all, dbuf, sizeof(unsigned long long) * words * W, hipMemcpyDeviceToHost, c->stream));
+        WSMC_HIP(hipStreamSynchronize(c->stream));
+        return WSMC_OK;
+    };
+    int r = all_gather_host(&menc, 1, ex.data());
+    if (r) return r;
+    for (int g = 0; g < W; ++g) menc = ex[g] > menc ? ex[g] : menc;
+    std::memset(&hs, 0, sizeof(hs));
+    hs.v[0][0] = menc;
+    WSMC_HIP(hipMemcpyAsync(c->mslots, &hs, sizeof(MaxSlots), hipMemcpyHostToDevice, c->stream));
+    // pass 1: totals {sum e, sum e z_k} per rank -> rank-order sums -> means
+    const int n1 = 1 + d, n2 = d * (d + 1) / 2;
+    std::vector<unsigned long long> all(10 * W);
+    double mom[64];
+    WSMC_HIP(launch_moments(c->stream, c->w, c->mslots, c->d_colptr, targets, d, lo, hi, 1, c->mom, c->N,
+                            c->tilepart));
+    WSMC_HIP(launch_moments_final(c->stream, c->tilepart, c->ntiles, d, 1, min_step, c->mom, c->dflag, 2));
+    WSMC_HIP(hipMemcpyAsync(mom, c->mom, sizeof(mom), hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    if ((r = all_gather_host(reinterpret_cast<const unsigned long long*>(mom + 48), n1, all.data()))) return r;
+    std::vector<double> t1(n1);
+    for (int v = 0; v < n1; ++v) {
+        double acc = 0.0;
+        for (int g = 0; g < W; ++g) {
+            double x;
+            std::memcpy(&x, &all[(size_t)g * n1 + v], 8);
+            acc = g == 0 ? x : acc + x;
+        }
+        t1[v] = acc;
+    }
+    const double S0 = t1[0];
+    for (int k = 0; k < d; ++k) mom[k] = t1[1 + k] / S0;
+    mom[8] = S0;
+    WSMC_HIP(hipMemcpyAsync(c->mom, mom, sizeof(double) * 16, hipMemcpyHostToDevice, c->stream));
+    // pass 2: centred products per rank -> rank-order sums -> covariance -> factor
+    WSMC_HIP(launch_moments(c->stream, c->w, c->mslots, c->d_colptr, targets, d, lo, hi, 2, c->mom, c->N,
+                            c->tilepart));
+    WSMC_HIP(launch_moments_final(c->stream, c->tilepart, c->ntiles, d, 2, min_step, c->mom, c->dflag, 2));
+    WSMC_HIP(hipMemcpyAsync(mom + 48, c->mom + 48, sizeof(double) * 16, hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    if ((r = all_gather_host(reinterpret_cast<const unsigned long long*>(mom + 48), n2, all.data()))) return r;
+    double S[16], L[16];
+    int v = 0;
+    for (int a = 0; a < d; ++a)
+        for (int b = a; b < d; ++b, ++v) {
+            double acc = 0.0;
+            for (int g = 0; g < W; ++g) {
+                double x;
+                std::memcpy(&x, &all[(size_t)g * n2 + v], 8);
+                acc = g == 0 ? x : acc + x;
+            }
+            const double cv = acc / S0;
+            S[a * d + b] = cv;
+            S[b * d + a] = cv;
+        }
+    const double lam = 2.38 / wsmc_sqrt((double)d);
+    for (int k = 0; k < d * d; ++k) {
+        if (S[k] == 0.0) S[k] = min_step;
+        S[k] = lam * S[k];
+    }
+    if (!wsmc_cholesky(S, L, d)) return fail(WSMC_ENOTPD, "autoRW proposal covariance is not positive definite");
+    WSMC_HIP(hipMemcpyAsync(c->mom + 32, L, sizeof(double) * 16, hipMemcpyHostToDevice, c->stream));
+    return WSMC_OK;
+}
+
 int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, double step, const double* lo,
               const double* hi, int32_t target_depth, double diversity, int64_t* accepted_out) {
     CHECK_CTX(c);
@@ -759,7 +847,9 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
     for (int k = 0; k < d; ++k)
         if (!valid_col(c, targets[k]) || c->cols[targets[k]].dim != 1)
             return fail(WSMC_EARG, "move targets must be existing scalar columns");
-    if (c->world > 1) return fail(WSMC_ESTATE, "generic moves on sharded contexts are not supported yet");
+    if (c->world > 1 && !std::isnan(diversity))
+        return fail(WSMC_ESTATE, "diversity-gated moves on sharded contexts are not supported (needs a global "
+                                 "unique count)");
     if (!std::isnan(diversity)) {
         double div = 0;
         int r = wsmc_marginal_diversity(c, targets, d, &div);
@@ -780,7 +870,10 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
     if (r) return r;
     WSMC_HIP(hipMemsetAsync(c->dflag, 0, sizeof(int32_t) * 4, c->stream));
     WSMC_HIP(hipMemsetAsync(c->ucount, 0, sizeof(unsigned long long) * 4, c->stream));
-    if (proposal == WSMC_PROPOSAL_AUTORW) {
+    if (proposal == WSMC_PROPOSAL_AUTORW && c->world > 1) {
+        int rr = sharded_autorw(c, targets, d, bounded ? l : nullptr, bounded ? h : nullptr, step);
+        if (rr) return rr;
+    } else if (proposal == WSMC_PROPOSAL_AUTORW) {
         WSMC_HIP(hipMemsetAsync(c->mslots, 0, sizeof(MaxSlots), c->stream));
         WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, c->mslots));
         const double* lp = bounded ? l : nullptr;
@@ -810,7 +903,8 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
     WSMC_HIP(launch_move(c->stream, c->d_tape, (int32_t)c->tape.size(), target_depth, c->d_colptr, targets, d,
                          bounded ? l : nullptr, bounded ? h : nullptr, bounded ? 1 : 0, c->mom + 32, c->seed,
                          op_prop, op_acc, c->goff, c->N, c->ucount,
-                         proposal == WSMC_PROPOSAL_AUTORW ? c->dflag : nullptr, c->scache, cache_from));
+                         (proposal == WSMC_PROPOSAL_AUTORW && c->world == 1) ? c->dflag : nullptr, c->scache,
+                         cache_from));
     struct {
         int32_t flag[4];
         unsigned long long acc[4];

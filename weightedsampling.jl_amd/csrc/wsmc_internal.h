@@ -86,6 +86,7 @@ struct wsmc_ctx {
     unsigned long long* run_grp = nullptr;      // [T+1][ngroups][kGroupLine] fused-run group sums
     // Move score cache: each particle's fold over the first scache_terms tape terms (its
     // score after its last move); -1 = invalid (a column the tape reads was rewritten)
+    unsigned long long* xchg = nullptr;   // sharded moves: small all-gather buffer (16 words per rank)
     double* scache = nullptr;
     double* scache_back = nullptr;
     int32_t scache_terms = -1;

@@ -842,6 +842,8 @@ __global__ __launch_bounds__(kBlock) void k_moments_final(const double* tilepart
     }
     __syncthreads();
     if (threadIdx.x != 0) return;
+    for (int v = 0; v < nv; ++v) mom[48 + v] = tot[v];   // raw shard totals (sharded moves combine them)
+    if (raw == 2) return;                                // sharded: the host combines and factorises
     if (pass == 1) {
         const double S0 = tot[0];
         for (int k = 0; k < d; ++k) mom[k] = tot[1 + k] / S0;
