@@ -65,6 +65,10 @@ _SIG = {
     "or_move": (C.c_int, [_P, C.c_int32, _I32P, C.c_int32, C.c_double, _D, _D, C.c_int32,
                           C.c_double, C.POINTER(C.c_int64)]),
     "or_score": (None, [_P, C.c_int32, _D]),
+    "or_moment_totals": (C.c_int, [_P, _I32P, C.c_int32, _D, _D, C.c_int32, C.c_double, _D, _D]),
+    "or_factor": (C.c_int, [_D, C.c_int32, C.c_double, _D]),
+    "or_move_factor": (C.c_int, [_P, _I32P, C.c_int32, _D, _D, _D, C.c_int32, C.POINTER(C.c_int64)]),
+    "or_skip_move": (None, [_P]),
     "or_philox": (None, [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "or_weighted_moments": (C.c_int, [_P, C.c_void_p, C.c_int32, _D, _D]),
     "or_col_minmax": (C.c_int, [_P, C.c_int32, C.c_int32, _D, _D]),
@@ -282,6 +286,48 @@ class Oracle:
             raise np.linalg.LinAlgError("proposal covariance not positive definite")
         self._chk(r)
         return int(acc.value)
+
+    # ---- one shard's part of the sharded autoRW protocol ----
+    def moment_totals(self, targets, pass_: int, M: float, mean=None, lo=None, hi=None) -> np.ndarray:
+        """pass 1: [sum e, sum e z_k]; pass 2: centred products (a <= b); e = exp(w - M)."""
+        t = np.ascontiguousarray(np.asarray(targets, dtype=np.int32))
+        d = len(t)
+        lo_a, hi_a = self._bounds(lo, d), self._bounds(hi, d)
+        m = np.ascontiguousarray(np.zeros(d) if mean is None else np.asarray(mean, float).reshape(d))
+        out = np.zeros(1 + d if pass_ == 1 else d * (d + 1) // 2)
+        self._chk(self._L.or_moment_totals(self._h, t.ctypes.data_as(_I32P), d,
+                                           None if lo_a is None else _dptr(lo_a),
+                                           None if hi_a is None else _dptr(hi_a), int(pass_), float(M),
+                                           _dptr(m), _dptr(out)))
+        return out
+
+    @staticmethod
+    def factor(S, min_step: float):
+        """min_step fill, x 2.38/sqrt(d), lower Cholesky; None if not positive definite."""
+        S = np.ascontiguousarray(np.asarray(S, float))
+        d = S.shape[0]
+        L = np.zeros(d * d)
+        ok = lib().or_factor(_dptr(S.reshape(-1).copy()), d, float(min_step), _dptr(L))
+        return L.reshape(d, d) if ok else None
+
+    def move_factor(self, targets, L, lo=None, hi=None, target_depth: int = -1) -> int:
+        t = np.ascontiguousarray(np.asarray(targets, dtype=np.int32))
+        d = len(t)
+        lo_a, hi_a = self._bounds(lo, d), self._bounds(hi, d)
+        Lf = np.ascontiguousarray(np.asarray(L, float).reshape(-1))
+        acc = C.c_int64()
+        self._chk(self._L.or_move_factor(self._h, t.ctypes.data_as(_I32P), d,
+                                         None if lo_a is None else _dptr(lo_a),
+                                         None if hi_a is None else _dptr(hi_a), _dptr(Lf), int(target_depth),
+                                         C.byref(acc)))
+        return int(acc.value)
+
+    def skip_move(self) -> None:
+        self._L.or_skip_move(self._h)
+
+    @staticmethod
+    def _bounds(b, d):
+        return None if b is None else np.ascontiguousarray(np.asarray(b, float).reshape(d))
 
     def score(self, target_depth: int) -> np.ndarray:
         out = np.empty(self.n)

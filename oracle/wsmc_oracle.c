@@ -395,6 +395,73 @@ double or_log_evidence_records(const uint64_t* recs, int32_t G) {
     return wsmc_global_log_evidence(st, G);
 }
 
+double or_canon_sum(const double* v, int64_t n);
+static int move_apply(oracle* o, const int32_t* targets, int32_t d, int bounded, const double* l, const double* h,
+                      const double* L, int32_t target_depth, uint64_t op_prop, uint64_t op_acc,
+                      int64_t* accepted_out);
+/* ---- one shard's part of a sharded autoRW move (the device ranks' protocol) ----
+ * pass 1: out = {sum e, sum e z_k}; pass 2: out = centred products (a <= b), canonical sums
+ * over this oracle's particles with e = exp(w - M) for the given global M */
+int or_moment_totals(oracle* o, const int32_t* targets, int32_t d, const double* lo, const double* hi,
+                     int32_t pass, double M, const double* mean, double* out) {
+    int64_t N = o->N;
+    if (d < 1 || d > 4) return WSMC_EARG;
+    double* e = (double*)malloc(sizeof(double) * (size_t)N);
+    double* z = (double*)malloc(sizeof(double) * (size_t)(N * d));
+    double* v = o->scratch;
+    for (int64_t i = 0; i < N; ++i) e[i] = wsmc_exp(o->w[i] - M);
+    for (int k = 0; k < d; ++k) {
+        const double* x = o->cols[targets[k]].front;
+        double l = lo ? lo[k] : -WSMC_INF, h = hi ? hi[k] : WSMC_INF;
+        for (int64_t i = 0; i < N; ++i) z[(int64_t)k * N + i] = wsmc_to_unc(x[i], l, h);
+    }
+    int nv = 0;
+    if (pass == 1) {
+        out[nv++] = or_canon_sum(e, N);
+        for (int k = 0; k < d; ++k) {
+            for (int64_t i = 0; i < N; ++i) v[i] = e[i] * z[(int64_t)k * N + i];
+            out[nv++] = or_canon_sum(v, N);
+        }
+    } else {
+        for (int a = 0; a < d; ++a)
+            for (int b = a; b < d; ++b) {
+                for (int64_t i = 0; i < N; ++i)
+                    v[i] = (e[i] * (z[(int64_t)a * N + i] - mean[a])) * (z[(int64_t)b * N + i] - mean[b]);
+                out[nv++] = or_canon_sum(v, N);
+            }
+    }
+    free(e); free(z);
+    return 0;
+}
+/* covariance S (d x d, already divided by S0) -> zeros to min_step, x 2.38/sqrt(d), Cholesky */
+int or_factor(const double* S_in, int32_t d, double min_step, double* L) {
+    double S[16];
+    double lam = 2.38 / wsmc_sqrt((double)d);
+    for (int k = 0; k < d * d; ++k) {
+        S[k] = S_in[k];
+        if (S[k] == 0.0) S[k] = min_step;
+        S[k] = lam * S[k];
+    }
+    return wsmc_cholesky(S, L, d);
+}
+/* a Move with a given factor L (consumes the Move's two op counters like or_move) */
+int or_move_factor(oracle* o, const int32_t* targets, int32_t d, const double* lo, const double* hi,
+                   const double* L, int32_t target_depth, int64_t* accepted_out) {
+    uint64_t op_prop = o->op++, op_acc = o->op++;
+    if (accepted_out) *accepted_out = 0;
+    if (target_depth < 0) target_depth = o->depth;
+    int bounded = 0;
+    double l[4], h[4];
+    for (int k = 0; k < d; ++k) {
+        l[k] = lo ? lo[k] : -WSMC_INF; h[k] = hi ? hi[k] : WSMC_INF;
+        if (wsmc_isfinite(l[k]) || wsmc_isfinite(h[k])) bounded = 1;
+    }
+    if (!lo && !hi) bounded = 0;
+    return move_apply(o, targets, d, bounded, l, h, L, target_depth, op_prop, op_acc, accepted_out);
+}
+/* consume a Move's two op counters without moving (a shard whose factor failed) */
+void or_skip_move(oracle* o) { o->op += 2; }
+
 /* ---- analysis reductions (src/utils.jl) ------------------------------------------------
  * Weighted moments under exp_norm(weights) of d <= 4 operand expressions, in the canonical
  * reduction order the device uses (or_canon_sum): expectation / @E (src/utils.jl:11, 23-58)
@@ -590,6 +657,9 @@ int or_autorw_chol(oracle* o, const int32_t* targets, int32_t d, double min_step
     return wsmc_cholesky(S, L, d);
 }
 
+static int move_apply(oracle* o, const int32_t* targets, int32_t d, int bounded, const double* l, const double* h,
+                      const double* L, int32_t target_depth, uint64_t op_prop, uint64_t op_acc,
+                      int64_t* accepted_out);
 int or_move(oracle* o, int32_t proposal, const int32_t* targets, int32_t d, double step, const double* lo,
             const double* hi, int32_t target_depth, double diversity, int64_t* accepted_out) {
     uint64_t op_prop = o->op++, op_acc = o->op++;
@@ -597,7 +667,6 @@ int or_move(oracle* o, int32_t proposal, const int32_t* targets, int32_t d, doub
     if (d < 1 || d > 4) return WSMC_EARG;
     if (!wsmc_isnan(diversity) && or_marginal_diversity(o, targets, d) >= diversity) return 0;
     if (target_depth < 0) target_depth = o->depth;
-    int64_t N = o->N;
     int bounded = 0;
     double l[4], h[4];
     for (int k = 0; k < d; ++k) {
@@ -612,6 +681,14 @@ int or_move(oracle* o, int32_t proposal, const int32_t* targets, int32_t d, doub
         for (int k = 0; k < d * d; ++k) L[k] = 0.0;
         for (int k = 0; k < d; ++k) L[k * d + k] = step;
     }
+    return move_apply(o, targets, d, bounded, l, h, L, target_depth, op_prop, op_acc, accepted_out);
+}
+
+/* the proposal + accept/reject of a Move given its factor L (src/transformers.jl:604-621) */
+static int move_apply(oracle* o, const int32_t* targets, int32_t d, int bounded, const double* l, const double* h,
+                      const double* L, int32_t target_depth, uint64_t op_prop, uint64_t op_acc,
+                      int64_t* accepted_out) {
+    int64_t N = o->N;
     int64_t acc = 0;
     double* newv = (double*)malloc(sizeof(double) * (size_t)(N * d));
     unsigned char* ok = (unsigned char*)malloc((size_t)N);

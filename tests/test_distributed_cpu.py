@@ -5,7 +5,10 @@
    Resample with all_gather, and applies the global decision locally — exactly what the
    GPU ranks do with ncclAllGather inside libwsmc. The result must equal the
    single-process run with the same shard layout, bit for bit.
-2. The torch-free TCP rendezvous bench.py ranks use (wsmc.hostcomm).
+2. The sharded autoRW protocol: global max, per-rank canonical moment totals exchanged
+   and combined in rank order, the factor on every rank, the move applied locally — the
+   sequence libwsmc's sharded Move runs over RCCL.
+3. The torch-free TCP rendezvous bench.py ranks use (wsmc.hostcomm).
 """
 import os
 import pathlib
@@ -56,6 +59,47 @@ class ShardCtx:
         recs = self.exchange(self.o.shard_record())
         return self.o.resample_records(ess_perc_min, scheme, np.stack(recs), self.rank)
 
+    def _allgather_f64(self, vals):
+        words = np.ascontiguousarray(np.asarray(vals, float)).view(np.uint64)
+        return [r.view(np.float64) for r in self.exchange(words)]
+
+    def move(self, proposal, targets, step, lo=None, hi=None, target_depth=-1, diversity=float("nan")):
+        import math
+        from wsmc import abi
+        if not math.isnan(diversity):
+            raise RuntimeError("the diversity gate needs a global unique count: refused on shards")
+        if proposal != abi.PROPOSAL_AUTORW:
+            return self.o.move(proposal, targets, step, lo, hi, target_depth)
+        d = len(targets)
+        bounded = any(math.isfinite(b) for bb in (lo or [], hi or []) for b in bb)
+        lo, hi = (lo, hi) if bounded else (None, None)
+        # global max (NaN if any rank holds a NaN weight, as the device's ordered max)
+        w = self.o.weights_download()
+        m = np.array([np.nan if np.isnan(w).any() else (w.max() if len(w) else -np.inf)])
+        ms = np.concatenate(self._allgather_f64(m))
+        M = np.nan if np.isnan(ms).any() else float(ms.max())
+
+        def rank_order_sum(parts):
+            acc = parts[0].copy()
+            for x in parts[1:]:
+                acc = acc + x
+            return acc
+        t1 = rank_order_sum(self._allgather_f64(self.o.moment_totals(targets, 1, M, lo=lo, hi=hi)))
+        S0 = t1[0]
+        mean = t1[1:] / S0
+        t2 = rank_order_sum(self._allgather_f64(self.o.moment_totals(targets, 2, M, mean, lo=lo, hi=hi)))
+        S = np.zeros((d, d))
+        v = 0
+        for a in range(d):
+            for b in range(a, d):
+                S[a, b] = S[b, a] = t2[v] / S0
+                v += 1
+        L = self.o.factor(S, step)
+        if L is None:
+            self.o.skip_move()
+            raise np.linalg.LinAlgError("proposal covariance not positive definite")
+        return self.o.move_factor(targets, L, lo, hi, target_depth)
+
 
 def _gloo_worker(rank, world, port, N, T, ess, scheme, outdir):
     sys.path[:0] = [str(REPO / "weightedsampling.jl_amd"), str(REPO / "oracle")]
@@ -102,6 +146,67 @@ def test_island_protocol_gloo_world2(tmp_path, ess, scheme):
             full = ref.col_download(ref.col_find(name))
             np.testing.assert_array_equal(p[name.replace("_", "U")], full[..., r * n:(r + 1) * n])
         assert p["ev"][0] == ref.log_evidence()
+
+
+def _move_worker(rank, world, port, N, which, outdir):
+    sys.path[:0] = [str(REPO / "weightedsampling.jl_amd"), str(REPO / "oracle")]
+    import torch
+    import torch.distributed as dist
+    from oracle import Oracle
+    import wsmc
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def exchange(rec):
+        t = torch.from_numpy(np.ascontiguousarray(rec).view(np.int64).copy())
+        out = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(out, t)
+        return [o.numpy().view(np.uint64) for o in out]
+
+    n = N // world
+    o = Oracle(n, seed=33, global_offset=rank * n)
+    ctx = ShardCtx(o, exchange, rank)
+    acc = _move_program(ctx, which)
+    gate = 0
+    try:
+        ctx.move(wsmc.PROPOSAL_AUTORW, [o.col_find(o.col_names()[0])], 1e-3, diversity=0.9)
+    except RuntimeError:
+        gate = 1
+    cols = {"c_" + name: o.col_download(o.col_find(name)) for name in o.col_names()}
+    np.savez(os.path.join(outdir, f"mv{rank}.npz"), acc=np.array(acc), w=o.weights_download(),
+             gate=np.array([gate]), **cols)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _move_program(ctx, which):
+    import wsmc
+    if which == "c3":
+        xs, ys = wsmc.models.linreg_data()
+        return wsmc.models.linreg_statements(ctx, xs[:6], ys[:6], ess_perc_min=1.0)
+    t, y = wsmc.models.oscillator_data(n=4)
+    return wsmc.models.oscillator_statements(ctx, t, y, ess_perc_min=1.0, scheme=wsmc.RESAMPLE_SYSTEMATIC,
+                                             sweeps=2, diversity=None)
+
+
+@pytest.mark.parametrize("which", ["c3", "c5"])
+def test_sharded_autorw_protocol_gloo_world2(tmp_path, which):
+    """C3 (1-d autoRW) and C5 (bounded 4-d + 1-d autoRW) on two gloo ranks == the sharded oracle."""
+    from oracle import Oracle
+    N, world = 3002, 2
+    _spawn(_move_worker, world, (world, _free_port(), N, which, str(tmp_path)))
+    ref = Oracle(N, seed=33, shards=world)
+    acc = _move_program(ref, which)
+    n = N // world
+    parts = [np.load(tmp_path / f"mv{r}.npz") for r in range(world)]
+    np.testing.assert_array_equal(sum(p["acc"] for p in parts), np.array(acc))
+    for r, p in enumerate(parts):
+        sl = slice(r * n, (r + 1) * n)
+        np.testing.assert_array_equal(p["w"], ref.weights_download()[sl])
+        for name in ref.col_names():
+            np.testing.assert_array_equal(p["c_" + name], ref.col_download(ref.col_find(name))[..., sl],
+                                          err_msg=name)
+        assert p["gate"][0] == 1
 
 
 def _hostcomm_worker(rank, world, port, outdir):
