@@ -27,7 +27,7 @@ const WS = WeightedSampling
 import WeightedSampling: nparticles, hascol, getcol, colnames, broadcast_setcol!, resample!, apply!,
     log_evidence
 
-export HipColumnStore, ssm2d_run!, sync_weights!
+export HipColumnStore, ssm2d_run!, sync_weights!, expectation, describe_device
 
 const libwsmc = get(ENV, "WSMC_LIB", joinpath(@__DIR__, "..", "wsmc", "libwsmc.so"))
 
@@ -346,6 +346,56 @@ function log_evidence(state::HipState)
     v = Ref{Float64}(0.0)
     check(ccall((:wsmc_log_evidence, libwsmc), Cint, (Ptr{Cvoid}, Ptr{Float64}), state.store.ctx, v))
     return v[]
+end
+
+# analysis reductions (src/utils.jl) on the device: no N-sized download ---------------------
+"""
+    expectation(state, x) -> Float64
+
+`expectation(f, state)` / `@E` (src/utils.jl:11, :23-58) for an affine expression of particle
+variables, e.g. `expectation(state, getcol(state.store, :α) .+ 2.0 .* getcol(state.store, :β))`.
+Non-affine expressions go through `operand`'s host path (a temporary device column).
+"""
+function expectation(state::HipState, x)
+    op = operand(state.store, x isa Broadcast.Broadcasted ? Broadcast.materialize(x) : x)
+    m = Ref{Float64}(0.0)
+    check(ccall((:wsmc_weighted_moments, libwsmc), Cint,
+                (Ptr{Cvoid}, Ref{WsmcOperand}, Int32, Ptr{Float64}, Ptr{Float64}),
+                state.store.ctx, op, 1, m, C_NULL))
+    return m[]
+end
+
+"""
+    describe_device(state; cols=colnames(state.store)) -> Vector{NamedTuple}
+
+The numeric part of `describe(state)` (src/utils.jl:157-289): weighted mean and std
+(`corrected=false`), min, max and ESS per column, component-wise for vector columns. The
+weighted median and the sparkline need a sort / histogram pass: `describe(sync!(state))`
+on the host gives those.
+"""
+function describe_device(state::HipState; cols=collect(keys(state.store.ids)))
+    s = state.store
+    essp = Ref{Float64}(0.0)
+    check(ccall((:wsmc_ess, libwsmc), Cint, (Ptr{Cvoid}, Ptr{Float64}), s.ctx, essp))
+    rows = NamedTuple[]
+    for name in cols
+        haskey(s.ids, name) || throw(ArgumentError("Column $name not found in store"))
+        id, d = s.ids[name], s.dims[name]
+        μ, σ, lo, hi = Float64[], Float64[], Float64[], Float64[]
+        for k in 0:d-1
+            op = WsmcOperand(0.0, (id, Int32(-1)), (Int32(k), Int32(0)), (1.0, 0.0))
+            m, v = Ref{Float64}(0.0), Ref{Float64}(0.0)
+            check(ccall((:wsmc_weighted_moments, libwsmc), Cint,
+                        (Ptr{Cvoid}, Ref{WsmcOperand}, Int32, Ptr{Float64}, Ptr{Float64}), s.ctx, op, 1, m, v))
+            a, b = Ref{Float64}(0.0), Ref{Float64}(0.0)
+            check(ccall((:wsmc_col_minmax, libwsmc), Cint, (Ptr{Cvoid}, Int32, Int32, Ptr{Float64}, Ptr{Float64}),
+                        s.ctx, id, Int32(k), a, b))
+            push!(μ, m[]); push!(σ, sqrt(v[])); push!(lo, a[]); push!(hi, b[])
+        end
+        pick(x) = d == 1 ? x[1] : x
+        push!(rows, (variable=name, mean=pick(μ), std=pick(σ), min=pick(lo), max=pick(hi), ess=s.n * essp[]))
+    end
+    return rows
 end
 
 """
