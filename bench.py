@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--particles", type=int, default=1_000_000, help="particles per GPU")
     ap.add_argument("--T", type=int, default=100)
     ap.add_argument("--ess", type=float, default=1.0)
-    ap.add_argument("--scheme", choices=["stratified", "systematic"], default="stratified")
+    ap.add_argument("--scheme", choices=["stratified", "systematic", "multinomial"], default="stratified")
     ap.add_argument("--no-history", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-particles", type=int, default=500_000)
@@ -89,7 +89,8 @@ def main():
     # between ranks is RCCL inside libwsmc.
     comm = from_env() if world > 1 else None
 
-    scheme = abi.RESAMPLE_STRATIFIED if args.scheme == "stratified" else abi.RESAMPLE_SYSTEMATIC
+    scheme = {"stratified": abi.RESAMPLE_STRATIFIED, "systematic": abi.RESAMPLE_SYSTEMATIC,
+              "multinomial": abi.RESAMPLE_MULTINOMIAL}[args.scheme]
     N = args.particles
     T = args.T
     obs = wsmc.models.ssm2d_data(max(T, args.cpu_T), seed=args.seed)

@@ -97,7 +97,11 @@ typedef struct {
     int32_t      depth;         /* execution depth of the statement (src/types.jl:162-177) */
 } wsmc_term;
 
-typedef enum { WSMC_RESAMPLE_STRATIFIED = 0, WSMC_RESAMPLE_SYSTEMATIC = 1 } wsmc_scheme;
+typedef enum {
+    WSMC_RESAMPLE_STRATIFIED = 0,   /* the reference's stratified_resample (src/resampling.jl:35-43) */
+    WSMC_RESAMPLE_SYSTEMATIC = 1,   /* one uniform for all strata (north-star addition) */
+    WSMC_RESAMPLE_MULTINOMIAL = 2   /* independent draws (north-star addition) */
+} wsmc_scheme;
 typedef enum { WSMC_PROPOSAL_RW = 0, WSMC_PROPOSAL_AUTORW = 1 } wsmc_proposal;
 
 typedef struct {

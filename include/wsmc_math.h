@@ -480,6 +480,26 @@ WSMC_HD uint64_t wsmc_rank(uint64_t c, uint64_t Q, uint64_t N, int scheme,
     return wsmc_rank_r(c, Q, N, wsmc_u64_to_d(N) / wsmc_u64_to_d(Q), scheme, seed, op, slot_base);
 }
 
+/*
+ * Multinomial resampling (north-star addition; the reference has stratified only):
+ * slot n draws U_n, a 64-bit word of (seed, op, n), and x_n = floor(U_n * Q / 2^64) in [0, Q);
+ * ancestor(n) = smallest m with C_m > x_n (the same icdf rule as above), so particle m is
+ * drawn with probability q_m / Q. The draws are independent across slots and unsorted:
+ * the device materialises C and searches it.
+ */
+WSMC_HD uint64_t wsmc_multi_word(uint64_t seed, uint64_t op, uint64_t n) {
+    uint64_t z = seed ^ (op * 0x9E3779B97F4A7C15ULL) ^ (n * 0xD1B54A32D192ED03ULL) ^ 0x2545F4914F6CDD1DULL;
+    z ^= z >> 33;
+    z *= 0xFF51AFD7ED558CCDULL;
+    z ^= z >> 33;
+    z *= 0xC4CEB9FE1A85EC53ULL;
+    z ^= z >> 33;
+    return z;
+}
+WSMC_HD uint64_t wsmc_multi_target(uint64_t U, uint64_t Q) {
+    return (uint64_t)(((wsmc_u128)U * (wsmc_u128)Q) >> 64);
+}
+
 /* 4x4-max Cholesky of a symmetric matrix (row-major a[d*d]) -> lower L; 0 if not PD */
 WSMC_HD int wsmc_cholesky(const double* a, double* L, int d) {
     for (int i = 0; i < d * d; ++i) L[i] = 0.0;

@@ -283,6 +283,23 @@ static or_stats shard_stats(const double* lw, int64_t n, int K) {
 /* the icdf merge (src/resampling.jl:13-26) on the integer CDF, one shard */
 static void shard_ancestors(const double* lw, int64_t n, int K, double M, uint64_t Q, int scheme,
                             uint64_t seed, uint64_t op, uint64_t slot_base, int32_t* anc) {
+    if (scheme == WSMC_RESAMPLE_MULTINOMIAL) {
+        /* independent draws: ancestor = smallest m with C_m > x (binary search of the prefix) */
+        uint64_t* C = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)(n > 0 ? n : 1));
+        uint64_t acc = 0;
+        for (int64_t i = 0; i < n; ++i) { acc += wsmc_qweight(lw[i], M, K); C[i] = acc; }
+        for (int64_t s = 0; s < n; ++s) {
+            uint64_t x = wsmc_multi_target(wsmc_multi_word(seed, op, slot_base + (uint64_t)s), Q);
+            int64_t lo = 0, hi = n - 1;
+            while (lo < hi) {
+                int64_t mid = lo + (hi - lo) / 2;
+                if (C[mid] > x) hi = mid; else lo = mid + 1;
+            }
+            anc[s] = (int32_t)lo;
+        }
+        free(C);
+        return;
+    }
     uint64_t C = wsmc_qweight(lw[0], M, K);       /* s = weights[1] */
     int64_t m = 0;
     uint32_t R0 = wsmc_strat_word(seed, op, slot_base);

@@ -129,7 +129,7 @@ def _gloo_worker(rank, world, port, N, T, ess, scheme, outdir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ess,scheme", [(1.0, 0), (0.5, 1)])
+@pytest.mark.parametrize("ess,scheme", [(1.0, 0), (0.5, 1), (1.0, 2)])
 def test_island_protocol_gloo_world2(tmp_path, ess, scheme):
     from oracle import Oracle
     import wsmc

@@ -55,7 +55,8 @@ def _worker(rank, world, port, N, T, ess, scheme, outdir):
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), **out)
 
 
-@pytest.mark.parametrize("N,ess,scheme", [(4096, 1.0, 0), (4096, 0.5, 1), (140002, 1.0, 0), (140002, 0.5, 0)])
+@pytest.mark.parametrize("N,ess,scheme", [(4096, 1.0, 0), (4096, 0.5, 1), (4096, 1.0, 2), (140002, 1.0, 0),
+                                          (140002, 0.5, 0)])
 def test_two_shards_one_gpu_match_sharded_oracle(gpu_available, tmp_path, N, ess, scheme):
     import multiprocessing as mp
     sys.path.insert(0, str(REPO / "oracle"))

@@ -36,7 +36,7 @@ def assert_same_state(g, o, rtol_w=0.0):
 
 @pytest.mark.parametrize("N", [1024, 3001])
 @pytest.mark.parametrize("ess", [1.0, 0.5])
-@pytest.mark.parametrize("scheme", [abi.RESAMPLE_STRATIFIED, abi.RESAMPLE_SYSTEMATIC])
+@pytest.mark.parametrize("scheme", [abi.RESAMPLE_STRATIFIED, abi.RESAMPLE_SYSTEMATIC, abi.RESAMPLE_MULTINOMIAL])
 def test_ssm2d_statements(gpu_available, N, ess, scheme):
     obs = models.ssm2d_data(8)
     g, o = wsmc.Context(N, seed=42), Oracle(N, seed=42)
@@ -72,6 +72,19 @@ def test_ssm2d_fused_matches_statements(gpu_available, N, ess, keep):
         models.ssm2d_statements(o, obs, ess_perc_min=ess)
         assert_same_state(g, o)
         assert ev2 == o.log_evidence()
+
+
+@pytest.mark.parametrize("ess", [1.0, 0.5])
+def test_ssm2d_fused_multinomial(gpu_available, ess):
+    """The fused run with multinomial draws (CDF + search kernels inside the graph)."""
+    N, obs = 5001, models.ssm2d_data(12)
+    g = wsmc.Context(N, seed=9)
+    ev = g.ssm2d_run(obs, ess_perc_min=ess, scheme=abi.RESAMPLE_MULTINOMIAL, keep_history=True)
+    o = Oracle(N, seed=9)
+    models.ssm2d_statements(o, obs, ess_perc_min=ess, scheme=abi.RESAMPLE_MULTINOMIAL)
+    assert_same_state(g, o)
+    np.testing.assert_array_equal(g.last_ancestors(), o.last_ancestors())
+    assert ev == o.log_evidence()
 
 
 def test_ssm1d_statements(gpu_available):
@@ -141,7 +154,7 @@ def _skewed_weights(kind, N, rng):
 
 @pytest.mark.parametrize("N", [1, 5, 1023, 1025, 70001])
 @pytest.mark.parametrize("kind", ["dominant", "two_tiles", "heavy_tail", "zeros", "flat"])
-@pytest.mark.parametrize("scheme", [abi.RESAMPLE_STRATIFIED, abi.RESAMPLE_SYSTEMATIC])
+@pytest.mark.parametrize("scheme", [abi.RESAMPLE_STRATIFIED, abi.RESAMPLE_SYSTEMATIC, abi.RESAMPLE_MULTINOMIAL])
 def test_resample_skewed_weights(gpu_available, N, kind, scheme):
     """Ancestor fill under weight skew (balanced fill tasks, src/resampling.jl:13-26)."""
     w = _skewed_weights(kind, N, np.random.default_rng(N))
@@ -158,13 +171,17 @@ def test_resample_skewed_weights(gpu_available, N, kind, scheme):
     assert rg == ro and rg[0]
     a = g.last_ancestors()
     np.testing.assert_array_equal(a, o.last_ancestors())
-    assert np.all(np.diff(a) >= 0) and a.min() >= 0 and a.max() < N
+    assert a.min() >= 0 and a.max() < N
+    if scheme != abi.RESAMPLE_MULTINOMIAL:     # strata give monotone ancestors; draws do not
+        assert np.all(np.diff(a) >= 0)
     assert_same_state(g, o)
 
 
 @pytest.mark.parametrize("kind", ["dominant", "many_heavy", "heavy_tail"])
-def test_resample_skewed_large(gpu_available, kind):
-    """> 1024 tiles (several per reduce thread) and > 256 heavy tiles."""
+@pytest.mark.parametrize("scheme", [abi.RESAMPLE_STRATIFIED, abi.RESAMPLE_MULTINOMIAL])
+def test_resample_skewed_large(gpu_available, kind, scheme):
+    """> 1024 tiles (several per reduce thread), > 256 heavy tiles; multinomial: > 2048
+    tiles, so the coarse search table strides."""
     N = 3_100_003
     w = _skewed_weights(kind, N, np.random.default_rng(7))
     g, o = wsmc.Context(N, seed=8), Oracle(N, seed=8)
@@ -172,7 +189,7 @@ def test_resample_skewed_large(gpu_available, kind):
     for c in (g, o):
         c.weights_upload(w)
         c.weight(Normal(0.0, 1.0).dist(c.col_find), [abi.Operand.const(0.0)])
-    assert g.resample(2.0) == o.resample(2.0)
+    assert g.resample(2.0, scheme) == o.resample(2.0, scheme)
     np.testing.assert_array_equal(g.last_ancestors(), o.last_ancestors())
     np.testing.assert_array_equal(g.weights_download(), o.weights_download())
 

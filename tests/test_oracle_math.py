@@ -200,3 +200,61 @@ def test_island_resampling_preserves_evidence():
         n = len(lw) // shards
         for s in range(shards):                # island: ancestors stay inside the shard
             assert np.all((anc[s * n:(s + 1) * n] >= s * n) & (anc[s * n:(s + 1) * n] < (s + 1) * n))
+
+
+def _fmix_multi(seed, op, n):
+    """wsmc_multi_word restated with Python integers (include/wsmc_math.h)."""
+    m = (1 << 64) - 1
+    z = seed ^ ((op * 0x9E3779B97F4A7C15) & m) ^ ((n * 0xD1B54A32D192ED03) & m) ^ 0x2545F4914F6CDD1D
+    z ^= z >> 33
+    z = (z * 0xFF51AFD7ED558CCD) & m
+    z ^= z >> 33
+    z = (z * 0xC4CEB9FE1A85EC53) & m
+    z ^= z >> 33
+    return z
+
+
+@pytest.mark.parametrize("N", [1, 7, 1000, 4099])
+def test_multinomial_matches_python_restatement(N):
+    """ancestor(n) = smallest m with C_m > floor(U_n Q / 2^64): an independent restatement
+    (Python integers, bisect) of the oracle's multinomial draws."""
+    import bisect
+    lw = np.random.default_rng(N).standard_normal(N) * 2
+    lw[::5] = -np.inf
+    if N == 1:
+        lw[0] = 0.0
+    o, _ = _weights_state(lw, seed=77)
+    _force_changed(o)
+    w = o.weights_download()
+    op = o.get_state()["op_counter"]
+    rs, _ = o.resample(2.0, abi.RESAMPLE_MULTINOMIAL)
+    assert rs
+    K, M = L.or_qbits(N), float(np.max(w))
+    C, acc = [], 0
+    for x in w:
+        acc += L.or_qweight(float(x), M, K)
+        C.append(acc)
+    Q = C[-1]
+    want = [bisect.bisect_right(C, (_fmix_multi(77, op, n) * Q) >> 64) for n in range(N)]
+    np.testing.assert_array_equal(o.last_ancestors(), want)
+
+
+def test_multinomial_offspring_distribution():
+    """Offspring counts are Multinomial(N, w): mean N w_i, chi-square near its d.o.f."""
+    N = 20000
+    lw = np.random.default_rng(5).standard_normal(N)
+    w = np.exp(lw - lw.max())
+    w /= w.sum()
+    tot = np.zeros(N)
+    reps = 8
+    for r in range(reps):
+        o, _ = _weights_state(lw, seed=100 + r)
+        _force_changed(o)
+        assert o.resample(2.0, abi.RESAMPLE_MULTINOMIAL)[0]
+        cnt = np.bincount(o.last_ancestors(), minlength=N)
+        tot += cnt
+        assert cnt.sum() == N
+    e = reps * N * w
+    chi2 = float(np.sum((tot - e) ** 2 / e))
+    # sum of N cells with expectation ~ N - 1, sd ~ sqrt(2N)
+    assert abs(chi2 - (N - 1)) < 6 * math.sqrt(2 * N)

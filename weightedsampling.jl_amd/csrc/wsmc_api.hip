@@ -228,7 +228,7 @@ int wsmc_destroy(wsmc_ctx* c) {
         (void)hipFree(col.front);
         (void)hipFree(col.back);
     }
-    void* bufs[] = {c->xchg, c->scache, c->scache_back, c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount,
+    void* bufs[] = {c->xchg, c->scache, c->scache_back, c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->cdf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount,
                     c->d_colptr, c->run_params, c->d_tape, c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp,
                     c->vscratch, c->xscratch};
     for (void* p : bufs)
@@ -434,6 +434,14 @@ static FillPlan fill_plan(wsmc_ctx* c, int scheme, uint64_t op, const uint64_t* 
     p.op_dev = op_dev;
     p.slot_base = c->goff;
     return p;
+}
+
+static bool valid_scheme(int32_t s) {
+    return s == WSMC_RESAMPLE_STRATIFIED || s == WSMC_RESAMPLE_SYSTEMATIC || s == WSMC_RESAMPLE_MULTINOMIAL;
+}
+static int ensure_cdf(wsmc_ctx* c) {
+    if (!c->cdf) WSMC_HIP(hipMalloc(&c->cdf, sizeof(unsigned long long) * (size_t)c->N));
+    return WSMC_OK;
 }
 
 static int enqueue_resample_stats(wsmc_ctx* c, const double* w, MaxSlots* ms, ShardRecord* recs, double ess_min,
@@ -664,8 +672,8 @@ int wsmc_weight(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x) { return
 
 int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resampled_out, double* ess_out) {
     CHECK_CTX(c);
-    if (scheme != WSMC_RESAMPLE_STRATIFIED && scheme != WSMC_RESAMPLE_SYSTEMATIC)
-        return fail(WSMC_EARG, "unknown resampling scheme");
+    if (!valid_scheme(scheme)) return fail(WSMC_EARG, "unknown resampling scheme");
+    if (scheme == WSMC_RESAMPLE_MULTINOMIAL && ensure_cdf(c)) return WSMC_EHIP;
     const uint64_t op = c->op++;
     if (!c->weights_changed) {
         if (resampled_out) *resampled_out = c->resampled;
@@ -675,7 +683,11 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
     const FillPlan plan = fill_plan(c, scheme, op, nullptr);
     int r = enqueue_resample_stats(c, c->w, c->mslots, c->rec, ess_min, c->dec, true, plan);
     if (r) return r;
-    WSMC_HIP(launch_rs_scan(c->stream, c->N, c->rec + c->rank, c->dec, plan, c->tileOff, c->qbuf, c->anc));
+    if (scheme == WSMC_RESAMPLE_MULTINOMIAL)
+        WSMC_HIP(launch_rs_multinomial(c->stream, c->N, c->rec + c->rank, c->dec, plan, c->tileOff, c->qbuf, c->cdf,
+                                       c->anc));
+    else
+        WSMC_HIP(launch_rs_scan(c->stream, c->N, c->rec + c->rank, c->dec, plan, c->tileOff, c->qbuf, c->anc));
     Decision* hd = reinterpret_cast<Decision*>(c->pinned);
     WSMC_HIP(hipMemcpyAsync(hd, c->dec, sizeof(Decision), hipMemcpyDeviceToHost, c->stream));
     WSMC_HIP(hipStreamSynchronize(c->stream));
@@ -1028,10 +1040,24 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
         ShardRecord* recs = c->run_rec + (size_t)t * c->world;
         a.ms = ms;
         const int k0 = 8 * (t - 1);
-        if (sharded && t > 1) WSMC_HIP(hipStreamWaitEvent(c->stream, c->ev_dec, 0));
+        if (sharded && t > 1 && p.scheme != WSMC_RESAMPLE_MULTINOMIAL) WSMC_HIP(hipStreamWaitEvent(c->stream, c->ev_dec, 0));
         WSMC_HIP(launch_ssm2d_propagate(c->stream, a, E(k0), E(k0 + 1)));
         const FillPlan plan = fill_plan(c, p.scheme, 3ull * (uint64_t)(t - 1) + 2ull, c->run_params);
         int32_t* anc_row = c->anc_log + (size_t)(t - 1) * anc_stride(N);
+        if (p.scheme == WSMC_RESAMPLE_MULTINOMIAL) {
+            // unsorted draws: sums, reduce (tile offsets, record), [exchange + decide], CDF + search
+            WSMC_HIP(launch_rs_sums(c->stream, c->w, N, ms, c->tilep, c->qbuf, E(k0 + 2), E(k0 + 3)));
+            WSMC_HIP(launch_rs_reduce(c->stream, ms, c->tilep, N, c->tileOff, recs + c->rank, !sharded, p.ess_min,
+                                      c->run_dec + t, &plan, E(k0 + 6), nullptr));
+            if (sharded) {
+                int r = exchange_recs(c, recs);
+                if (r) return r;
+                WSMC_HIP(launch_rs_decide(c->stream, recs, c->world, c->rank, p.ess_min, c->run_dec + t));
+            }
+            WSMC_HIP(launch_rs_multinomial(c->stream, N, recs + c->rank, c->run_dec + t, plan, c->tileOff, c->qbuf,
+                                           c->cdf, anc_row, nullptr, E(k0 + 7)));
+            continue;
+        }
         if (!sharded) {
             unsigned long long* grp = c->run_grp + (size_t)t * run_grp_words(N);
             WSMC_HIP(launch_rs_sums(c->stream, c->w, N, ms, c->tilep, c->qbuf, E(k0 + 2), E(k0 + 3), grp, G));
@@ -1092,8 +1118,8 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
     CHECK_CTX(c);
     c->scache_terms = -1;   // the run rewrites columns the tape reads
     if (!obs || T < 1 || !x0 || !v0) return fail(WSMC_EARG, "bad arguments");
-    if (scheme != WSMC_RESAMPLE_STRATIFIED && scheme != WSMC_RESAMPLE_SYSTEMATIC)
-        return fail(WSMC_EARG, "unknown resampling scheme");
+    if (!valid_scheme(scheme)) return fail(WSMC_EARG, "unknown resampling scheme");
+    if (scheme == WSMC_RESAMPLE_MULTINOMIAL && ensure_cdf(c)) return WSMC_EHIP;
     if (!(q_var > 0) || !(r_var > 0)) return fail(WSMC_EARG, "variances must be positive");
     RunPlan p;
     p.T = T;

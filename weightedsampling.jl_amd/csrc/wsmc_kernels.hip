@@ -620,6 +620,75 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_scan_t(int64_t N, const Shard
     }
 }
 
+// ---- multinomial resampling (include/wsmc_math.h wsmc_multi_word) ------------------
+// The draws are unsorted, so the CDF is materialised: C_i = tileOff[b] + inclusive prefix
+// of q within the tile (one block per 1024-particle tile, 4 blocked particles per thread).
+__global__ __launch_bounds__(kScanBlock) void k_rs_cdf(int64_t N, const Decision* __restrict__ dec,
+                                                       const u64* __restrict__ tileOff,
+                                                       const u64* __restrict__ qbuf, u64* __restrict__ cdf) {
+    constexpr int IT = kRsTile / kScanBlock;
+    __shared__ u64 s_w[kScanBlock / 64];
+    if (!dec->resampled) return;
+    const int b = blockIdx.x;
+    u64 q[IT];
+    load_tile_q(N, b, qbuf, q);
+    u64 ts = 0;
+#pragma unroll
+    for (int k = 0; k < IT; ++k) ts += q[k];
+    u64 tot;
+    u64 c = tileOff[b] + block_excl_scan_u64<kScanBlock / 64>(ts, s_w, &tot);
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        c += q[k];
+        const int64_t i = (int64_t)b * kRsTile + (int64_t)threadIdx.x * IT + k;
+        if (i < N) cdf[i] = c;
+    }
+}
+
+// ancestor(n) = smallest m with C_m > x_n, x_n = floor(U_n Q / 2^64): the tile by a binary
+// search of a coarse tile-offset table in LDS, then of tileOff, then of the tile's C
+// (10 levels, one 8-KB region). 4 slots per thread, strided so the anc stores coalesce.
+constexpr int kMultiCoarse = 2048;
+__global__ __launch_bounds__(kScanBlock) void k_rs_multi(int64_t N, const ShardRecord* __restrict__ rec,
+                                                         const Decision* __restrict__ dec, FillPlan plan,
+                                                         const u64* __restrict__ tileOff,
+                                                         const u64* __restrict__ cdf, int32_t* __restrict__ anc) {
+    __shared__ u64 coarse[kMultiCoarse];
+    if (!dec->resampled) return;
+    const int64_t ntiles = (N + kRsTile - 1) / kRsTile;
+    const int64_t stride = (ntiles + kMultiCoarse - 1) / kMultiCoarse;
+    const int ncoarse = (int)((ntiles + stride - 1) / stride);
+    for (int k = threadIdx.x; k < ncoarse; k += kScanBlock) coarse[k] = tileOff[(int64_t)k * stride];
+    __syncthreads();
+    const u64 Q = rec->Q;
+    const uint64_t opx = op_eff(plan.op, plan.op_dev);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t n = (int64_t)blockIdx.x * (4 * kScanBlock) + (int64_t)k * kScanBlock + threadIdx.x;
+        if (n >= N) break;
+        const u64 x = wsmc_multi_target(wsmc_multi_word(plan.seed, opx, (uint64_t)(plan.slot_base + n)), Q);
+        // largest coarse entry <= x (coarse[0] = 0 <= x)
+        int lo = 0, hi = ncoarse;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (coarse[mid] <= x) lo = mid; else hi = mid;
+        }
+        // largest tile b in the coarse cell with tileOff[b] <= x: it holds the answer
+        int64_t blo = (int64_t)lo * stride, bhi = blo + stride < ntiles ? blo + stride : ntiles;
+        while (bhi - blo > 1) {
+            const int64_t mid = (blo + bhi) >> 1;
+            if (tileOff[mid] <= x) blo = mid; else bhi = mid;
+        }
+        // smallest m in the tile with C_m > x
+        int64_t mlo = blo * kRsTile, mhi = (mlo + kRsTile < N ? mlo + kRsTile : N) - 1;
+        while (mlo < mhi) {
+            const int64_t mid = (mlo + mhi) >> 1;
+            if (cdf[mid] > x) mhi = mid; else mlo = mid + 1;
+        }
+        anc[n] = (int32_t)mlo;
+    }
+}
+
 // ---- fused single-GPU resample: no reduce kernel ----------------------------------
 // block sum of two u64 values (all threads get the totals)
 __device__ __forceinline__ void block_sum2_u64(u64& a, u64& b, u64 (*lds)[2]) {
@@ -1211,6 +1280,17 @@ hipError_t launch_rs_scan(hipStream_t s, int64_t N, const ShardRecord* rec, cons
                           hipEvent_t e1) {
     return launch_timed(k_rs_scan_t<0>, fill_tasks_for(N), dim3(kScanBlock), s, e0, e1, N, rec, dec, plan, tileOff,
                         qbuf, anc);
+}
+
+hipError_t launch_rs_multinomial(hipStream_t s, int64_t N, const ShardRecord* rec, const Decision* dec,
+                                 const FillPlan& plan, const u64* tileOff, const u64* qbuf, u64* cdf, int32_t* anc,
+                                 hipEvent_t e0, hipEvent_t e1) {
+    const unsigned nt = (unsigned)((N + kRsTile - 1) / kRsTile);
+    // e0 opens on the CDF kernel, e1 closes on the search (either may be null)
+    hipError_t e = launch_timed(k_rs_cdf, dim3(nt), dim3(kScanBlock), s, e0, nullptr, N, dec, tileOff, qbuf, cdf);
+    if (e != hipSuccess) return e;
+    const unsigned nb = (unsigned)((N + 4 * kScanBlock - 1) / (4 * kScanBlock));
+    return launch_timed(k_rs_multi, dim3(nb), dim3(kScanBlock), s, nullptr, e1, N, rec, dec, plan, tileOff, cdf, anc);
 }
 
 // diagnostics: the propagate kernel's memory pattern with no arithmetic — per particle a

@@ -7,7 +7,7 @@ This package is the host-side mirror of the reference's operator interface; it h
 CPU compute path.
 """
 from . import abi
-from .abi import (PROPOSAL_AUTORW, PROPOSAL_RW, RESAMPLE_STRATIFIED, RESAMPLE_SYSTEMATIC, WSMCError,
+from .abi import (PROPOSAL_AUTORW, PROPOSAL_RW, RESAMPLE_MULTINOMIAL, RESAMPLE_STRATIFIED, RESAMPLE_SYSTEMATIC, WSMCError,
                   load_library)
 from .context import Context, device_count
 from .dsl import Col, Expr, HalfNormal, Kernel, MvNormal, Normal, Oscillator, Uniform
@@ -18,7 +18,7 @@ from .transformers import (Assign, Cond, FusedSSM2D, HipColumnStore, ImportanceK
 
 __all__ = ["abi", "Context", "device_count", "Col", "Expr", "Kernel", "Normal", "MvNormal", "HalfNormal",
            "Uniform", "Oscillator", "models", "load_library", "WSMCError", "RESAMPLE_STRATIFIED",
-           "RESAMPLE_SYSTEMATIC", "PROPOSAL_RW", "PROPOSAL_AUTORW", "Assign", "Cond", "FusedSSM2D",
+           "RESAMPLE_SYSTEMATIC", "RESAMPLE_MULTINOMIAL", "PROPOSAL_RW", "PROPOSAL_AUTORW", "Assign", "Cond", "FusedSSM2D",
            "HipColumnStore", "ImportanceKernel", "Loop", "Move", "Observe", "Resample", "RW", "Sample", "Sequence",
            "SMCState", "Weight", "apply", "autoRW", "describe", "expectation", "importance_kernel", "marginal_diversity", "resampled", "run",
            "score_logpdf"]

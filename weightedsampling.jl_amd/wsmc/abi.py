@@ -17,7 +17,7 @@ WSMC_OK, WSMC_EARG, WSMC_EHIP, WSMC_ENOTPD, WSMC_ERCCL, WSMC_ESTATE, WSMC_ENOMEM
 FAM_NORMAL, FAM_HALFNORMAL, FAM_UNIFORM, FAM_MVNORMAL_ISO = range(4)
 MEAN_AFFINE, MEAN_OSCILLATOR = range(2)
 TERM_SAMPLE, TERM_OBSERVE, TERM_WEIGHT = range(3)
-RESAMPLE_STRATIFIED, RESAMPLE_SYSTEMATIC = range(2)
+RESAMPLE_STRATIFIED, RESAMPLE_SYSTEMATIC, RESAMPLE_MULTINOMIAL = range(3)
 PROPOSAL_RW, PROPOSAL_AUTORW = range(2)
 
 

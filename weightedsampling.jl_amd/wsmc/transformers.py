@@ -217,7 +217,8 @@ class Weight(ParticleTransformer):
 
 @dataclass
 class Resample(ParticleTransformer):
-    """Resample() (src/transformers.jl:474-498); scheme: stratified (reference) or systematic."""
+    """Resample() (src/transformers.jl:474-498); scheme: stratified (reference), systematic or
+    multinomial."""
     scheme: int | None = None
 
     def apply(self, state):
