@@ -481,11 +481,15 @@ WSMC_HD uint64_t wsmc_rank(uint64_t c, uint64_t Q, uint64_t N, int scheme,
 }
 
 /*
- * Multinomial resampling (north-star addition; the reference has stratified only):
- * slot n draws U_n, a 64-bit word of (seed, op, n), and x_n = floor(U_n * Q / 2^64) in [0, Q);
- * ancestor(n) = smallest m with C_m > x_n (the same icdf rule as above), so particle m is
- * drawn with probability q_m / Q. The draws are independent across slots and unsorted:
- * the device materialises C and searches it.
+ * Multinomial resampling (north-star addition; the reference has stratified only), drawn
+ * as sorted uniforms from normalised exponential spacings (the order statistics of N iid
+ * uniforms: U_(n) = P_n / P_N, P_n = E_0 + ... + E_n, N + 1 exponentials). The offspring
+ * counts are Multinomial(N, q/Q); the ancestors come out sorted, so the column gather and
+ * the history trace-back stay coalesced.
+ * Exact in integers: E_k = floor(-log(u_k) * 2^24) + 1 >= 1 (u_k in (0, 1], a 53-bit word of
+ * (seed, op, slot k); the terminal E_N has its own stream), so every P_n < 2^62 for
+ * N < 2^31 and P_n < P_N for n < N. Slot n's ancestor is the smallest m with
+ * C_m > floor(Q P_n / P_N), i.e. Q * P_n < C_m * P_N (u128 products, no division).
  */
 WSMC_HD uint64_t wsmc_multi_word(uint64_t seed, uint64_t op, uint64_t n) {
     uint64_t z = seed ^ (op * 0x9E3779B97F4A7C15ULL) ^ (n * 0xD1B54A32D192ED03ULL) ^ 0x2545F4914F6CDD1DULL;
@@ -496,8 +500,18 @@ WSMC_HD uint64_t wsmc_multi_word(uint64_t seed, uint64_t op, uint64_t n) {
     z ^= z >> 33;
     return z;
 }
-WSMC_HD uint64_t wsmc_multi_target(uint64_t U, uint64_t Q) {
-    return (uint64_t)(((wsmc_u128)U * (wsmc_u128)Q) >> 64);
+WSMC_HD uint64_t wsmc_multi_expo(uint64_t word) {
+    const double u = wsmc_u64_to_d((word >> 11) + 1) * 1.1102230246251565e-16;   /* (0, 1], 2^-53 grid */
+    return wsmc_d_to_u64_trunc(wsmc_floor(-wsmc_log(u) * 16777216.0)) + 1;       /* 2^24 fixed point */
+}
+/* E_k of slot k (k < n) and the terminal E_n of a shard of n slots starting at slot_base */
+WSMC_HD uint64_t wsmc_multi_e(uint64_t seed, uint64_t op, uint64_t slot_base, uint64_t k, uint64_t n) {
+    return k < n ? wsmc_multi_expo(wsmc_multi_word(seed, op, slot_base + k))
+                 : wsmc_multi_expo(wsmc_multi_word(seed, ~op, slot_base));
+}
+/* C_m > floor(Q P / PN)  <=>  Q P < C_m PN */
+WSMC_HD int wsmc_multi_above(uint64_t Cm, uint64_t Q, uint64_t P, uint64_t PN) {
+    return (wsmc_u128)Q * (wsmc_u128)P < (wsmc_u128)Cm * (wsmc_u128)PN;
 }
 
 /* 4x4-max Cholesky of a symmetric matrix (row-major a[d*d]) -> lower L; 0 if not PD */

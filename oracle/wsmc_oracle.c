@@ -284,20 +284,19 @@ static or_stats shard_stats(const double* lw, int64_t n, int K) {
 static void shard_ancestors(const double* lw, int64_t n, int K, double M, uint64_t Q, int scheme,
                             uint64_t seed, uint64_t op, uint64_t slot_base, int32_t* anc) {
     if (scheme == WSMC_RESAMPLE_MULTINOMIAL) {
-        /* independent draws: ancestor = smallest m with C_m > x (binary search of the prefix) */
-        uint64_t* C = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)(n > 0 ? n : 1));
-        uint64_t acc = 0;
-        for (int64_t i = 0; i < n; ++i) { acc += wsmc_qweight(lw[i], M, K); C[i] = acc; }
+        /* sorted draws from exponential spacings, then the same merge as the strata */
+        uint64_t PN = 0;
+        for (int64_t k = 0; k <= n; ++k) PN += wsmc_multi_e(seed, op, slot_base, (uint64_t)k, (uint64_t)n);
+        uint64_t P = 0, C = wsmc_qweight(lw[0], M, K);
+        int64_t m = 0;
         for (int64_t s = 0; s < n; ++s) {
-            uint64_t x = wsmc_multi_target(wsmc_multi_word(seed, op, slot_base + (uint64_t)s), Q);
-            int64_t lo = 0, hi = n - 1;
-            while (lo < hi) {
-                int64_t mid = lo + (hi - lo) / 2;
-                if (C[mid] > x) hi = mid; else lo = mid + 1;
+            P += wsmc_multi_e(seed, op, slot_base, (uint64_t)s, (uint64_t)n);
+            while (!wsmc_multi_above(C, Q, P, PN)) {   /* while C_m <= x_s */
+                m += 1;
+                C += wsmc_qweight(lw[m], M, K);
             }
-            anc[s] = (int32_t)lo;
+            anc[s] = (int32_t)m;
         }
-        free(C);
         return;
     }
     uint64_t C = wsmc_qweight(lw[0], M, K);       /* s = weights[1] */

@@ -171,9 +171,7 @@ def test_resample_skewed_weights(gpu_available, N, kind, scheme):
     assert rg == ro and rg[0]
     a = g.last_ancestors()
     np.testing.assert_array_equal(a, o.last_ancestors())
-    assert a.min() >= 0 and a.max() < N
-    if scheme != abi.RESAMPLE_MULTINOMIAL:     # strata give monotone ancestors; draws do not
-        assert np.all(np.diff(a) >= 0)
+    assert np.all(np.diff(a) >= 0) and a.min() >= 0 and a.max() < N   # sorted for every scheme
     assert_same_state(g, o)
 
 

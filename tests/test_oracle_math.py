@@ -214,16 +214,22 @@ def _fmix_multi(seed, op, n):
     return z
 
 
+def _expo(word):
+    u = float((word >> 11) + 1) * 2.0 ** -53              # exact: <= 2^53
+    return int(math.floor(-L.or_log(u) * 16777216.0)) + 1
+
+
 @pytest.mark.parametrize("N", [1, 7, 1000, 4099])
 def test_multinomial_matches_python_restatement(N):
-    """ancestor(n) = smallest m with C_m > floor(U_n Q / 2^64): an independent restatement
-    (Python integers, bisect) of the oracle's multinomial draws."""
+    """Sorted multinomial draws from exponential spacings (include/wsmc_math.h), restated
+    with Python integers and bisect: ancestor(n) = smallest m with C_m > floor(Q P_n / P_N)."""
     import bisect
     lw = np.random.default_rng(N).standard_normal(N) * 2
     lw[::5] = -np.inf
     if N == 1:
         lw[0] = 0.0
-    o, _ = _weights_state(lw, seed=77)
+    seed = 77
+    o, _ = _weights_state(lw, seed=seed)
     _force_changed(o)
     w = o.weights_download()
     op = o.get_state()["op_counter"]
@@ -235,8 +241,15 @@ def test_multinomial_matches_python_restatement(N):
         acc += L.or_qweight(float(x), M, K)
         C.append(acc)
     Q = C[-1]
-    want = [bisect.bisect_right(C, (_fmix_multi(77, op, n) * Q) >> 64) for n in range(N)]
-    np.testing.assert_array_equal(o.last_ancestors(), want)
+    E = [_expo(_fmix_multi(seed, op, k)) for k in range(N)] + [_expo(_fmix_multi(seed, op ^ ((1 << 64) - 1), 0))]
+    PN = sum(E)
+    P, want = 0, []
+    for n in range(N):
+        P += E[n]
+        want.append(bisect.bisect_right(C, (Q * P) // PN))
+    anc = o.last_ancestors()
+    np.testing.assert_array_equal(anc, want)
+    assert np.all(np.diff(anc) >= 0)                     # sorted draws: monotone ancestors
 
 
 def test_multinomial_offspring_distribution():

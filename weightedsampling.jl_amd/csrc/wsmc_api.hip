@@ -440,7 +440,9 @@ static bool valid_scheme(int32_t s) {
     return s == WSMC_RESAMPLE_STRATIFIED || s == WSMC_RESAMPLE_SYSTEMATIC || s == WSMC_RESAMPLE_MULTINOMIAL;
 }
 static int ensure_cdf(wsmc_ctx* c) {
-    if (!c->cdf) WSMC_HIP(hipMalloc(&c->cdf, sizeof(unsigned long long) * (size_t)c->N));
+    // [N] CDF + the exponential-spacing tile sums (one per 1024 slots of N + 1, + the total)
+    const size_t words = (size_t)c->N + (size_t)((c->N + 1 + kRsTile - 1) / kRsTile) + 1;
+    if (!c->cdf) WSMC_HIP(hipMalloc(&c->cdf, sizeof(unsigned long long) * words));
     return WSMC_OK;
 }
 

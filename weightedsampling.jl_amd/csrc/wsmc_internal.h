@@ -121,7 +121,7 @@ struct wsmc_ctx {
     int32_t* taskOff = nullptr;             // [nrstiles] first overflow fill task of each tile
     int32_t* taskTile = nullptr;            // [N / kRsChunk + nrstiles + 1] tile of each overflow task
     unsigned long long* qbuf = nullptr;     // [N] integer weights q_i of the last weight-statistics pass
-    unsigned long long* cdf = nullptr;      // [N] inclusive CDF of q (multinomial resampling; lazy)
+    unsigned long long* cdf = nullptr;      // [N] inclusive CDF of q + spacing tile sums (multinomial; lazy)
     double* tilepart = nullptr;             // [16 * ntiles] canonical-sum tile partials
     wsmc::MaxSlots* mslots = nullptr;       // [1] max slots of one generic resample / evidence
     wsmc::ShardRecord* rec = nullptr;       // [world] shard records of one generic resample
@@ -202,7 +202,7 @@ hipError_t launch_rs_scan(hipStream_t s, int64_t N, const ShardRecord* rec, cons
                           const FillPlan& plan, const unsigned long long* tileOff,
                           const unsigned long long* qbuf, int32_t* anc, hipEvent_t e0 = nullptr,
                           hipEvent_t e1 = nullptr);
-// multinomial: materialise the CDF (one block per tile), then one search per slot
+// multinomial: materialise the CDF, sorted draws from exponential spacings, one bounded search per slot
 hipError_t launch_rs_multinomial(hipStream_t s, int64_t N, const ShardRecord* rec, const Decision* dec,
                                  const FillPlan& plan, const unsigned long long* tileOff,
                                  const unsigned long long* qbuf, unsigned long long* cdf, int32_t* anc,

@@ -645,47 +645,118 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_cdf(int64_t N, const Decision
     }
 }
 
-// ancestor(n) = smallest m with C_m > x_n, x_n = floor(U_n Q / 2^64): the tile by a binary
-// search of a coarse tile-offset table in LDS, then of tileOff, then of the tile's C
-// (10 levels, one 8-KB region). 4 slots per thread, strided so the anc stores coalesce.
-constexpr int kMultiCoarse = 2048;
-__global__ __launch_bounds__(kScanBlock) void k_rs_multi(int64_t N, const ShardRecord* __restrict__ rec,
-                                                         const Decision* __restrict__ dec, FillPlan plan,
-                                                         const u64* __restrict__ tileOff,
-                                                         const u64* __restrict__ cdf, int32_t* __restrict__ anc) {
-    __shared__ u64 coarse[kMultiCoarse];
+// Sorted multinomial draws (include/wsmc_math.h wsmc_multi_e): P_n = E_0 + ... + E_n over
+// the shard's N + 1 exponentials. Pass 1: per-1024-slot tile sums of E.
+__global__ __launch_bounds__(kScanBlock) void k_multi_esum(int64_t N, const Decision* __restrict__ dec,
+                                                           FillPlan plan, u64* __restrict__ esum) {
+    constexpr int IT = kRsTile / kScanBlock;
+    __shared__ u64 s_w[kScanBlock / 64];
     if (!dec->resampled) return;
-    const int64_t ntiles = (N + kRsTile - 1) / kRsTile;
-    const int64_t stride = (ntiles + kMultiCoarse - 1) / kMultiCoarse;
-    const int ncoarse = (int)((ntiles + stride - 1) / stride);
-    for (int k = threadIdx.x; k < ncoarse; k += kScanBlock) coarse[k] = tileOff[(int64_t)k * stride];
-    __syncthreads();
-    const u64 Q = rec->Q;
     const uint64_t opx = op_eff(plan.op, plan.op_dev);
+    u64 t = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int64_t n = (int64_t)blockIdx.x * (4 * kScanBlock) + (int64_t)k * kScanBlock + threadIdx.x;
-        if (n >= N) break;
-        const u64 x = wsmc_multi_target(wsmc_multi_word(plan.seed, opx, (uint64_t)(plan.slot_base + n)), Q);
-        // largest coarse entry <= x (coarse[0] = 0 <= x)
-        int lo = 0, hi = ncoarse;
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (coarse[mid] <= x) lo = mid; else hi = mid;
-        }
-        // largest tile b in the coarse cell with tileOff[b] <= x: it holds the answer
-        int64_t blo = (int64_t)lo * stride, bhi = blo + stride < ntiles ? blo + stride : ntiles;
-        while (bhi - blo > 1) {
-            const int64_t mid = (blo + bhi) >> 1;
-            if (tileOff[mid] <= x) blo = mid; else bhi = mid;
-        }
-        // smallest m in the tile with C_m > x
-        int64_t mlo = blo * kRsTile, mhi = (mlo + kRsTile < N ? mlo + kRsTile : N) - 1;
-        while (mlo < mhi) {
-            const int64_t mid = (mlo + mhi) >> 1;
-            if (cdf[mid] > x) mhi = mid; else mlo = mid + 1;
-        }
-        anc[n] = (int32_t)mlo;
+    for (int k = 0; k < IT; ++k) {
+        const int64_t i = (int64_t)blockIdx.x * kRsTile + (int64_t)k * kScanBlock + threadIdx.x;
+        if (i <= N) t += wsmc_multi_e(plan.seed, opx, (uint64_t)plan.slot_base, (uint64_t)i, (uint64_t)N);
+    }
+    t = wave_sum_u64(t);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        u64 a = 0;
+#pragma unroll
+        for (int v = 0; v < kScanBlock / 64; ++v) a += s_w[v];
+        esum[blockIdx.x] = a;
+    }
+}
+// pass 2 (one block): exclusive offsets of the tile sums in place; esum[nb] = P_N
+__global__ __launch_bounds__(kScanBlock) void k_multi_escan(int64_t nb, const Decision* __restrict__ dec,
+                                                            u64* __restrict__ esum) {
+    __shared__ u64 s_w[kScanBlock / 64];
+    if (!dec->resampled) return;
+    const int64_t per = (nb + kScanBlock - 1) / kScanBlock;
+    const int64_t b0 = (int64_t)threadIdx.x * per < nb ? (int64_t)threadIdx.x * per : nb;
+    const int64_t b1 = b0 + per < nb ? b0 + per : nb;
+    u64 t = 0;
+    for (int64_t b = b0; b < b1; ++b) t += esum[b];
+    u64 tot;
+    u64 c = block_excl_scan_u64<kScanBlock / 64>(t, s_w, &tot);
+    for (int64_t b = b0; b < b1; ++b) {
+        const u64 v = esum[b];
+        esum[b] = c;
+        c += v;
+    }
+    if (threadIdx.x == 0) esum[nb] = tot;
+}
+// smallest m in [lo, hi] with C_m > floor(Q P / PN) (the answer is known to lie there)
+__device__ __forceinline__ int64_t multi_search(const u64* __restrict__ cdf, int64_t lo, int64_t hi, u64 Q, u64 P,
+                                                u64 PN) {
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (wsmc_multi_above(cdf[mid], Q, P, PN)) hi = mid; else lo = mid + 1;
+    }
+    return lo;
+}
+// the ancestor of one slot from scratch: the tile (tileOff), then within it
+__device__ int64_t multi_locate(int64_t N, const u64* __restrict__ tileOff, const u64* __restrict__ cdf, u64 Q,
+                                u64 P, u64 PN) {
+    const int64_t nt = (N + kRsTile - 1) / kRsTile;
+    int64_t lo = 0, hi = nt;                       // largest b with tileOff[b] <= x (tileOff[0] = 0)
+    while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (!wsmc_multi_above(tileOff[mid], Q, P, PN)) lo = mid; else hi = mid;
+    }
+    const int64_t m0 = lo * kRsTile, m1 = (m0 + kRsTile < N ? m0 + kRsTile : N) - 1;
+    return multi_search(cdf, m0, m1, Q, P, PN);
+}
+// pass 3: slots of one tile (4 consecutive per thread): recompute E, block scan -> P_n; the
+// first and last slot are located from scratch, every other slot searches between them
+__global__ __launch_bounds__(kScanBlock) void k_multi_fill(int64_t N, const ShardRecord* __restrict__ rec,
+                                                           const Decision* __restrict__ dec, FillPlan plan,
+                                                           const u64* __restrict__ tileOff,
+                                                           const u64* __restrict__ cdf, const u64* __restrict__ esum,
+                                                           int32_t* __restrict__ anc) {
+    constexpr int IT = kRsTile / kScanBlock;
+    __shared__ u64 s_w[kScanBlock / 64];
+    __shared__ int64_t s_m[2];
+    if (!dec->resampled) return;
+    const int th = threadIdx.x;
+    const int64_t base = (int64_t)blockIdx.x * kRsTile;
+    const int64_t last = (base + kRsTile < N ? base + kRsTile : N) - 1;
+    const uint64_t opx = op_eff(plan.op, plan.op_dev);
+    const int64_t nb = (N + 1 + kRsTile - 1) / kRsTile;
+    const u64 PN = esum[nb], Q = rec->Q;
+    u64 e[IT], t = 0;
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        const int64_t i = base + (int64_t)th * IT + k;
+        e[k] = i <= last ? wsmc_multi_e(plan.seed, opx, (uint64_t)plan.slot_base, (uint64_t)i, (uint64_t)N) : 0ull;
+        t += e[k];
+    }
+    u64 tot;
+    u64 P = esum[blockIdx.x] + block_excl_scan_u64<kScanBlock / 64>(t, s_w, &tot);
+    u64 Pk[IT];
+#pragma unroll
+    for (int k = 0; k < IT; ++k) { P += e[k]; Pk[k] = P; }
+    // the block's first slot (thread 0, k = 0) and last slot bound every search
+    if (th == 0) s_m[0] = multi_locate(N, tileOff, cdf, Q, Pk[0], PN);
+    const int64_t lt = last - base;                 // tile-local index of the last slot
+    if (th == lt / IT) {
+        u64 Pl = Pk[0];
+#pragma unroll
+        for (int k = 0; k < IT; ++k)
+            if (k == lt % IT) Pl = Pk[k];
+        s_m[1] = multi_locate(N, tileOff, cdf, Q, Pl, PN);
+    }
+    __syncthreads();
+    const int64_t mlo = s_m[0], mhi = s_m[1];
+    int64_t lo = mlo;
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        const int64_t i = base + (int64_t)th * IT + k;
+        if (i > last) break;
+        lo = multi_search(cdf, lo, mhi, Q, Pk[k], PN);   // sorted: start at the previous answer
+        anc[i] = (int32_t)lo;
     }
 }
 
@@ -1286,11 +1357,16 @@ hipError_t launch_rs_multinomial(hipStream_t s, int64_t N, const ShardRecord* re
                                  const FillPlan& plan, const u64* tileOff, const u64* qbuf, u64* cdf, int32_t* anc,
                                  hipEvent_t e0, hipEvent_t e1) {
     const unsigned nt = (unsigned)((N + kRsTile - 1) / kRsTile);
-    // e0 opens on the CDF kernel, e1 closes on the search (either may be null)
+    const int64_t nb = (N + 1 + kRsTile - 1) / kRsTile;
+    u64* esum = cdf + N;                            // nb + 1 words past the CDF
+    // e0 opens on the CDF kernel, e1 closes on the fill (either may be null)
     hipError_t e = launch_timed(k_rs_cdf, dim3(nt), dim3(kScanBlock), s, e0, nullptr, N, dec, tileOff, qbuf, cdf);
     if (e != hipSuccess) return e;
-    const unsigned nb = (unsigned)((N + 4 * kScanBlock - 1) / (4 * kScanBlock));
-    return launch_timed(k_rs_multi, dim3(nb), dim3(kScanBlock), s, nullptr, e1, N, rec, dec, plan, tileOff, cdf, anc);
+    hipLaunchKernelGGL(k_multi_esum, dim3((unsigned)nb), dim3(kScanBlock), 0, s, N, dec, plan, esum);
+    hipLaunchKernelGGL(k_multi_escan, dim3(1), dim3(kScanBlock), 0, s, nb, dec, esum);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    return launch_timed(k_multi_fill, dim3(nt), dim3(kScanBlock), s, nullptr, e1, N, rec, dec, plan, tileOff, cdf,
+                        esum, anc);
 }
 
 // diagnostics: the propagate kernel's memory pattern with no arithmetic — per particle a
