@@ -440,11 +440,14 @@ static bool valid_scheme(int32_t s) {
     return s == WSMC_RESAMPLE_STRATIFIED || s == WSMC_RESAMPLE_SYSTEMATIC || s == WSMC_RESAMPLE_MULTINOMIAL;
 }
 static int ensure_cdf(wsmc_ctx* c) {
-    // [N] CDF + the exponential-spacing tile sums (one per 1024 slots of N + 1, + the total)
-    const size_t words = (size_t)c->N + (size_t)((c->N + 1 + kRsTile - 1) / kRsTile) + 1;
+    // [N] tile-local CDF + the exponential-spacing tile sums (one per tile, + the total)
+    const size_t words = (size_t)c->N + (size_t)((c->N + kRsTile - 1) / kRsTile) + 1;
     if (!c->cdf) WSMC_HIP(hipMalloc(&c->cdf, sizeof(unsigned long long) * words));
     return WSMC_OK;
 }
+
+// multinomial: c->cdf holds the tile-local CDF [N], then the spacing tile sums / offsets
+static unsigned long long* multi_esum(wsmc_ctx* c) { return c->cdf + c->N; }
 
 static int enqueue_resample_stats(wsmc_ctx* c, const double* w, MaxSlots* ms, ShardRecord* recs, double ess_min,
                                   Decision* dec, bool run_max, const FillPlan& plan, hipEvent_t* ev = nullptr) {
@@ -452,9 +455,14 @@ static int enqueue_resample_stats(wsmc_ctx* c, const double* w, MaxSlots* ms, Sh
         WSMC_HIP(hipMemsetAsync(ms, 0, sizeof(MaxSlots), c->stream));
         WSMC_HIP(launch_rs_max(c->stream, w, c->N, ms));
     }
-    WSMC_HIP(launch_rs_sums(c->stream, w, c->N, ms, c->tilep, c->qbuf, ev ? ev[0] : nullptr, ev ? ev[1] : nullptr));
+    const bool multi = plan.scheme == WSMC_RESAMPLE_MULTINOMIAL;
+    if (multi)
+        WSMC_HIP(launch_rs_sums_multi(c->stream, w, c->N, ms, plan, c->tilep, c->cdf, multi_esum(c),
+                                      ev ? ev[0] : nullptr, ev ? ev[1] : nullptr));
+    else
+        WSMC_HIP(launch_rs_sums(c->stream, w, c->N, ms, c->tilep, c->qbuf, ev ? ev[0] : nullptr, ev ? ev[1] : nullptr));
     WSMC_HIP(launch_rs_reduce(c->stream, ms, c->tilep, c->N, c->tileOff, recs + c->rank, c->world == 1, ess_min, dec,
-                              &plan, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr));
+                              &plan, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr, multi ? multi_esum(c) : nullptr));
     if (c->world > 1) {
         int r = exchange_recs(c, recs);
         if (r) return r;
@@ -686,8 +694,8 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
     int r = enqueue_resample_stats(c, c->w, c->mslots, c->rec, ess_min, c->dec, true, plan);
     if (r) return r;
     if (scheme == WSMC_RESAMPLE_MULTINOMIAL)
-        WSMC_HIP(launch_rs_multinomial(c->stream, c->N, c->rec + c->rank, c->dec, plan, c->tileOff, c->qbuf, c->cdf,
-                                       c->anc));
+        WSMC_HIP(launch_rs_multinomial(c->stream, c->N, c->rec + c->rank, c->dec, plan, c->tileOff, c->cdf,
+                                       multi_esum(c), c->anc));
     else
         WSMC_HIP(launch_rs_scan(c->stream, c->N, c->rec + c->rank, c->dec, plan, c->tileOff, c->qbuf, c->anc));
     Decision* hd = reinterpret_cast<Decision*>(c->pinned);
@@ -1048,16 +1056,17 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
         int32_t* anc_row = c->anc_log + (size_t)(t - 1) * anc_stride(N);
         if (p.scheme == WSMC_RESAMPLE_MULTINOMIAL) {
             // unsorted draws: sums, reduce (tile offsets, record), [exchange + decide], CDF + search
-            WSMC_HIP(launch_rs_sums(c->stream, c->w, N, ms, c->tilep, c->qbuf, E(k0 + 2), E(k0 + 3)));
+            WSMC_HIP(launch_rs_sums_multi(c->stream, c->w, N, ms, plan, c->tilep, c->cdf, multi_esum(c), E(k0 + 2),
+                                          E(k0 + 3)));
             WSMC_HIP(launch_rs_reduce(c->stream, ms, c->tilep, N, c->tileOff, recs + c->rank, !sharded, p.ess_min,
-                                      c->run_dec + t, &plan, E(k0 + 6), nullptr));
+                                      c->run_dec + t, &plan, E(k0 + 6), nullptr, multi_esum(c)));
             if (sharded) {
                 int r = exchange_recs(c, recs);
                 if (r) return r;
                 WSMC_HIP(launch_rs_decide(c->stream, recs, c->world, c->rank, p.ess_min, c->run_dec + t));
             }
-            WSMC_HIP(launch_rs_multinomial(c->stream, N, recs + c->rank, c->run_dec + t, plan, c->tileOff, c->qbuf,
-                                           c->cdf, anc_row, nullptr, E(k0 + 7)));
+            WSMC_HIP(launch_rs_multinomial(c->stream, N, recs + c->rank, c->run_dec + t, plan, c->tileOff, c->cdf,
+                                           multi_esum(c), anc_row, nullptr, E(k0 + 7)));
             continue;
         }
         if (!sharded) {

@@ -121,7 +121,7 @@ struct wsmc_ctx {
     int32_t* taskOff = nullptr;             // [nrstiles] first overflow fill task of each tile
     int32_t* taskTile = nullptr;            // [N / kRsChunk + nrstiles + 1] tile of each overflow task
     unsigned long long* qbuf = nullptr;     // [N] integer weights q_i of the last weight-statistics pass
-    unsigned long long* cdf = nullptr;      // [N] inclusive CDF of q + spacing tile sums (multinomial; lazy)
+    unsigned long long* cdf = nullptr;      // [N] tile-local CDF of q + spacing tile sums (multinomial; lazy)
     double* tilepart = nullptr;             // [16 * ntiles] canonical-sum tile partials
     wsmc::MaxSlots* mslots = nullptr;       // [1] max slots of one generic resample / evidence
     wsmc::ShardRecord* rec = nullptr;       // [world] shard records of one generic resample
@@ -195,17 +195,22 @@ struct FillPlan {          // ancestor-fill task planning (in the reduce kernel)
 };
 hipError_t launch_rs_reduce(hipStream_t s, const MaxSlots* ms, const unsigned long long* tilep, int64_t N,
                             unsigned long long* tileOff, ShardRecord* rec, int decide_local, double ess_min,
-                            Decision* dec, const FillPlan* plan, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+                            Decision* dec, const FillPlan* plan, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr,
+                            unsigned long long* esum = nullptr);
 hipError_t launch_rs_decide(hipStream_t s, const ShardRecord* recs, int world, int rank, double ess_min,
                             Decision* dec);
 hipError_t launch_rs_scan(hipStream_t s, int64_t N, const ShardRecord* rec, const Decision* dec,
                           const FillPlan& plan, const unsigned long long* tileOff,
                           const unsigned long long* qbuf, int32_t* anc, hipEvent_t e0 = nullptr,
                           hipEvent_t e1 = nullptr);
-// multinomial: materialise the CDF, sorted draws from exponential spacings, one bounded search per slot
+// multinomial: weight statistics + tile-local CDF + spacing tile sums, then the fill
+// (the reduce kernel turns the spacing sums into offsets when given esum)
+hipError_t launch_rs_sums_multi(hipStream_t s, const double* w, int64_t N, const MaxSlots* ms, const FillPlan& plan,
+                                unsigned long long* tilep, unsigned long long* lcdf, unsigned long long* esum,
+                                hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t launch_rs_multinomial(hipStream_t s, int64_t N, const ShardRecord* rec, const Decision* dec,
                                  const FillPlan& plan, const unsigned long long* tileOff,
-                                 const unsigned long long* qbuf, unsigned long long* cdf, int32_t* anc,
+                                 const unsigned long long* lcdf, const unsigned long long* esum, int32_t* anc,
                                  hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 // fused single-GPU run: group sums (kGroupLine u64 per group) replace the reduce kernel
 constexpr int kGroupLine = 8;

@@ -378,7 +378,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_reduce_t(const MaxSlots* __rest
                                                         const u64* __restrict__ tilep, int64_t ntiles, int64_t N,
                                                         u64* __restrict__ tileOff, ShardRecord* rec,
                                                         int decide_local, double ess_min, Decision* dec,
-                                                        FillPlan plan) {
+                                                        FillPlan plan, u64* __restrict__ esum) {
     __shared__ u64 red[kRedPart][kRsBlock];
     __shared__ u64 red2[kRedPart][16];
     __shared__ u64 tot[kRedPart];
@@ -418,6 +418,20 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_reduce_t(const MaxSlots* __rest
             c += qb;
             if (planned) nt += ovf_chunks(qb, ratio);
         }
+    }
+    // multinomial: exclusive offsets of the exponential-spacing tile sums, in place, and
+    // their total in esum[ntiles]
+    if (esum) {
+        u64 es = 0;
+        for (int64_t b = b0; b < b1; ++b) es += esum[b];
+        u64 etot;
+        u64 ec = block_excl_scan_u64<kRsBlock / 64>(es, s_w, &etot);
+        for (int64_t b = b0; b < b1; ++b) {
+            const u64 v = esum[b];
+            esum[b] = ec;
+            ec += v;
+        }
+        if (th == 0) esum[ntiles] = etot;
     }
     u64 tt = 0;
     if (planned) {
@@ -620,112 +634,129 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_scan_t(int64_t N, const Shard
     }
 }
 
-// ---- multinomial resampling (include/wsmc_math.h wsmc_multi_word) ------------------
-// The draws are unsorted, so the CDF is materialised: C_i = tileOff[b] + inclusive prefix
-// of q within the tile (one block per 1024-particle tile, 4 blocked particles per thread).
-__global__ __launch_bounds__(kScanBlock) void k_rs_cdf(int64_t N, const Decision* __restrict__ dec,
-                                                       const u64* __restrict__ tileOff,
-                                                       const u64* __restrict__ qbuf, u64* __restrict__ cdf) {
-    constexpr int IT = kRsTile / kScanBlock;
-    __shared__ u64 s_w[kScanBlock / 64];
-    if (!dec->resampled) return;
-    const int b = blockIdx.x;
-    u64 q[IT];
-    load_tile_q(N, b, qbuf, q);
-    u64 ts = 0;
+// ---- multinomial resampling (include/wsmc_math.h wsmc_multi_e) ----------------------
+// Weight statistics for a multinomial Resample: the tile partials of k_rs_sums_t (the same
+// exact integers), plus per particle the tile-local inclusive prefix of q (C_m =
+// tileOff[tile] + lcdf[m]) and per tile the sum of the slots' exponential spacings E.
+// 4 blocked particles per thread so one block scan gives the prefix.
+__global__ __launch_bounds__(kSumBlock) void k_rs_sums_multi(const double* __restrict__ w, int64_t N,
+                                                             const MaxSlots* __restrict__ ms, FillPlan plan,
+                                                             u64* __restrict__ tilep, u64* __restrict__ lcdf,
+                                                             u64* __restrict__ esum) {
+    constexpr int IT = kRsTile / kSumBlock;
+    __shared__ double s_f[3][kSumBlock / 64];
+    __shared__ u64 s_q[2][kSumBlock / 64];
+    __shared__ u64 s_w[kSumBlock / 64];
+    const int th = threadIdx.x;
+    const int64_t base = (int64_t)blockIdx.x * kRsTile + (int64_t)th * IT;
+    double lw[IT];
 #pragma unroll
-    for (int k = 0; k < IT; ++k) ts += q[k];
-    u64 tot;
-    u64 c = tileOff[b] + block_excl_scan_u64<kScanBlock / 64>(ts, s_w, &tot);
+    for (int k = 0; k < IT; ++k) lw[k] = base + k < N ? w[base + k] : -WSMC_INF;
+    const double M = wave_slots_max(ms);
+    const double sK = wsmc_pow2i(wsmc_qbits((uint64_t)N));
+    const uint64_t opx = op_eff(plan.op, plan.op_dev);
+    u64 q[IT], Q = 0, E = 0;
+    double S1 = 0.0, S2 = 0.0, WF = 0.0;
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        const double e = wsmc_expw(lw[k] - M);
+        q[k] = 0;
+        double q21 = 0.0, wf = 0.0;
+        if (e > 0.0) {
+            const double sc = e * sK;
+            const double qd = wsmc_floor(sc);
+            q[k] = (u64)qd;
+            wf = wsmc_floor((sc - qd) * 4398046511104.0);      // 2^42
+            q21 = wsmc_floor(e * 2097152.0);                   // 2^21
+        }
+        Q += q[k];
+        S1 = S1 + q21;
+        S2 = S2 + q21 * q21;
+        WF = WF + wf;
+        if (base + k < N)
+            E += wsmc_multi_e(plan.seed, opx, (uint64_t)plan.slot_base, (uint64_t)(base + k), (uint64_t)N);
+    }
+    u64 qtot;
+    u64 c = block_excl_scan_u64<kSumBlock / 64>(Q, s_w, &qtot);
 #pragma unroll
     for (int k = 0; k < IT; ++k) {
         c += q[k];
-        const int64_t i = (int64_t)b * kRsTile + (int64_t)threadIdx.x * IT + k;
-        if (i < N) cdf[i] = c;
+        if (base + k < N) lcdf[base + k] = c;
+    }
+    E = wave_sum_u64(E);
+    S1 = wave_sum_f64(S1);
+    S2 = wave_sum_f64(S2);
+    WF = wave_sum_f64(WF);
+    const int wv = th >> 6;
+    if ((th & 63) == 0) {
+        s_q[0][wv] = E;
+        s_f[0][wv] = S1; s_f[1][wv] = S2; s_f[2][wv] = WF;
+    }
+    __syncthreads();
+    if (th < kPart + 1) {
+        u64 t = 0;
+        if (th == 0) {
+            t = qtot;
+        } else if (th == kPart) {
+#pragma unroll
+            for (int v = 0; v < kSumBlock / 64; ++v) t += s_q[0][v];
+            esum[blockIdx.x] = t;
+            return;
+        } else {
+            double f = 0.0;
+#pragma unroll
+            for (int v = 0; v < kSumBlock / 64; ++v) f = f + s_f[th - 1][v];
+            t = (u64)f;                                         // exact: < 2^53
+        }
+        tilep[(int64_t)blockIdx.x * kPart + th] = t;
     }
 }
 
-// Sorted multinomial draws (include/wsmc_math.h wsmc_multi_e): P_n = E_0 + ... + E_n over
-// the shard's N + 1 exponentials. Pass 1: per-1024-slot tile sums of E.
-__global__ __launch_bounds__(kScanBlock) void k_multi_esum(int64_t N, const Decision* __restrict__ dec,
-                                                           FillPlan plan, u64* __restrict__ esum) {
-    constexpr int IT = kRsTile / kScanBlock;
-    __shared__ u64 s_w[kScanBlock / 64];
-    if (!dec->resampled) return;
-    const uint64_t opx = op_eff(plan.op, plan.op_dev);
-    u64 t = 0;
-#pragma unroll
-    for (int k = 0; k < IT; ++k) {
-        const int64_t i = (int64_t)blockIdx.x * kRsTile + (int64_t)k * kScanBlock + threadIdx.x;
-        if (i <= N) t += wsmc_multi_e(plan.seed, opx, (uint64_t)plan.slot_base, (uint64_t)i, (uint64_t)N);
-    }
-    t = wave_sum_u64(t);
-    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = t;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        u64 a = 0;
-#pragma unroll
-        for (int v = 0; v < kScanBlock / 64; ++v) a += s_w[v];
-        esum[blockIdx.x] = a;
-    }
+__device__ __forceinline__ u64 multi_cval(const u64* __restrict__ tileOff, const u64* __restrict__ lcdf, int64_t m) {
+    return tileOff[m / kRsTile] + lcdf[m];
 }
-// pass 2 (one block): exclusive offsets of the tile sums in place; esum[nb] = P_N
-__global__ __launch_bounds__(kScanBlock) void k_multi_escan(int64_t nb, const Decision* __restrict__ dec,
-                                                            u64* __restrict__ esum) {
-    __shared__ u64 s_w[kScanBlock / 64];
-    if (!dec->resampled) return;
-    const int64_t per = (nb + kScanBlock - 1) / kScanBlock;
-    const int64_t b0 = (int64_t)threadIdx.x * per < nb ? (int64_t)threadIdx.x * per : nb;
-    const int64_t b1 = b0 + per < nb ? b0 + per : nb;
-    u64 t = 0;
-    for (int64_t b = b0; b < b1; ++b) t += esum[b];
-    u64 tot;
-    u64 c = block_excl_scan_u64<kScanBlock / 64>(t, s_w, &tot);
-    for (int64_t b = b0; b < b1; ++b) {
-        const u64 v = esum[b];
-        esum[b] = c;
-        c += v;
-    }
-    if (threadIdx.x == 0) esum[nb] = tot;
-}
-// smallest m in [lo, hi] with C_m > floor(Q P / PN) (the answer is known to lie there)
-__device__ __forceinline__ int64_t multi_search(const u64* __restrict__ cdf, int64_t lo, int64_t hi, u64 Q, u64 P,
-                                                u64 PN) {
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (wsmc_multi_above(cdf[mid], Q, P, PN)) hi = mid; else lo = mid + 1;
-    }
-    return lo;
-}
-// the ancestor of one slot from scratch: the tile (tileOff), then within it
-__device__ int64_t multi_locate(int64_t N, const u64* __restrict__ tileOff, const u64* __restrict__ cdf, u64 Q,
+// the ancestor of one slot from scratch: the tile (largest b with tileOff[b] <= x), then
+// the smallest m in it with C_m > x
+__device__ int64_t multi_locate(int64_t N, const u64* __restrict__ tileOff, const u64* __restrict__ lcdf, u64 Q,
                                 u64 P, u64 PN) {
     const int64_t nt = (N + kRsTile - 1) / kRsTile;
-    int64_t lo = 0, hi = nt;                       // largest b with tileOff[b] <= x (tileOff[0] = 0)
+    int64_t lo = 0, hi = nt;
     while (hi - lo > 1) {
         const int64_t mid = (lo + hi) >> 1;
         if (!wsmc_multi_above(tileOff[mid], Q, P, PN)) lo = mid; else hi = mid;
     }
-    const int64_t m0 = lo * kRsTile, m1 = (m0 + kRsTile < N ? m0 + kRsTile : N) - 1;
-    return multi_search(cdf, m0, m1, Q, P, PN);
+    const u64 off = tileOff[lo];
+    int64_t m0 = lo * kRsTile, m1 = (m0 + kRsTile < N ? m0 + kRsTile : N) - 1;
+    while (m0 < m1) {
+        const int64_t mid = (m0 + m1) >> 1;
+        if (wsmc_multi_above(off + lcdf[mid], Q, P, PN)) m1 = mid; else m0 = mid + 1;
+    }
+    return m0;
 }
-// pass 3: slots of one tile (4 consecutive per thread): recompute E, block scan -> P_n; the
-// first and last slot are located from scratch, every other slot searches between them
+
+// Slots of one tile (4 consecutive per thread): E recomputed, block scan + the tile's
+// offset (reduce kernel) -> P_n; P_N = total + the terminal E_N. The first and last slot
+// are located from scratch; the CDF between their ancestors is staged in LDS when it
+// spans <= kMultiStage particles (the usual case), and every slot searches from the
+// previous slot's answer.
+constexpr int kMultiStage = 4096;
 __global__ __launch_bounds__(kScanBlock) void k_multi_fill(int64_t N, const ShardRecord* __restrict__ rec,
                                                            const Decision* __restrict__ dec, FillPlan plan,
                                                            const u64* __restrict__ tileOff,
-                                                           const u64* __restrict__ cdf, const u64* __restrict__ esum,
+                                                           const u64* __restrict__ lcdf, const u64* __restrict__ esum,
                                                            int32_t* __restrict__ anc) {
     constexpr int IT = kRsTile / kScanBlock;
     __shared__ u64 s_w[kScanBlock / 64];
     __shared__ int64_t s_m[2];
+    __shared__ u64 sC[kMultiStage];
     if (!dec->resampled) return;
     const int th = threadIdx.x;
     const int64_t base = (int64_t)blockIdx.x * kRsTile;
     const int64_t last = (base + kRsTile < N ? base + kRsTile : N) - 1;
+    const int64_t nt = (N + kRsTile - 1) / kRsTile;
     const uint64_t opx = op_eff(plan.op, plan.op_dev);
-    const int64_t nb = (N + 1 + kRsTile - 1) / kRsTile;
-    const u64 PN = esum[nb], Q = rec->Q;
+    const u64 Q = rec->Q;
+    const u64 PN = esum[nt] + wsmc_multi_e(plan.seed, opx, (uint64_t)plan.slot_base, (uint64_t)N, (uint64_t)N);
     u64 e[IT], t = 0;
 #pragma unroll
     for (int k = 0; k < IT; ++k) {
@@ -738,25 +769,49 @@ __global__ __launch_bounds__(kScanBlock) void k_multi_fill(int64_t N, const Shar
     u64 Pk[IT];
 #pragma unroll
     for (int k = 0; k < IT; ++k) { P += e[k]; Pk[k] = P; }
-    // the block's first slot (thread 0, k = 0) and last slot bound every search
-    if (th == 0) s_m[0] = multi_locate(N, tileOff, cdf, Q, Pk[0], PN);
-    const int64_t lt = last - base;                 // tile-local index of the last slot
+    const int64_t lt = last - base;
+    if (th == 0) s_m[0] = multi_locate(N, tileOff, lcdf, Q, Pk[0], PN);
     if (th == lt / IT) {
         u64 Pl = Pk[0];
 #pragma unroll
         for (int k = 0; k < IT; ++k)
             if (k == lt % IT) Pl = Pk[k];
-        s_m[1] = multi_locate(N, tileOff, cdf, Q, Pl, PN);
+        s_m[1] = multi_locate(N, tileOff, lcdf, Q, Pl, PN);
     }
     __syncthreads();
     const int64_t mlo = s_m[0], mhi = s_m[1];
+    const int64_t span = mhi - mlo + 1;
+    if (span <= kMultiStage) {
+        for (int64_t j = th; j < span; j += kScanBlock) sC[j] = multi_cval(tileOff, lcdf, mlo + j);
+        __syncthreads();
+        int lo = 0;
+        const int hi = (int)(span - 1);
+#pragma unroll
+        for (int k = 0; k < IT; ++k) {
+            const int64_t i = base + (int64_t)th * IT + k;
+            if (i > last) break;
+            int a = lo, b = hi;
+            while (a < b) {
+                const int mid = (a + b) >> 1;
+                if (wsmc_multi_above(sC[mid], Q, Pk[k], PN)) b = mid; else a = mid + 1;
+            }
+            lo = a;
+            anc[i] = (int32_t)(mlo + a);
+        }
+        return;
+    }
     int64_t lo = mlo;
 #pragma unroll
     for (int k = 0; k < IT; ++k) {
         const int64_t i = base + (int64_t)th * IT + k;
         if (i > last) break;
-        lo = multi_search(cdf, lo, mhi, Q, Pk[k], PN);   // sorted: start at the previous answer
-        anc[i] = (int32_t)lo;
+        int64_t a = lo, b = mhi;
+        while (a < b) {
+            const int64_t mid = (a + b) >> 1;
+            if (wsmc_multi_above(multi_cval(tileOff, lcdf, mid), Q, Pk[k], PN)) b = mid; else a = mid + 1;
+        }
+        lo = a;
+        anc[i] = (int32_t)a;
     }
 }
 
@@ -1330,12 +1385,12 @@ hipError_t launch_rs_fill_fused(hipStream_t s, int64_t N, const FillPlan& plan, 
 }
 hipError_t launch_rs_reduce(hipStream_t s, const MaxSlots* ms, const u64* tilep, int64_t N, u64* tileOff,
                             ShardRecord* rec, int decide_local, double ess_min, Decision* dec,
-                            const FillPlan* plan, hipEvent_t e0, hipEvent_t e1) {
+                            const FillPlan* plan, hipEvent_t e0, hipEvent_t e1, u64* esum) {
     const int64_t nt = (N + kRsTile - 1) / kRsTile;
     FillPlan p{};
     if (plan) p = *plan;
     return launch_timed(k_rs_reduce_t<0>, dim3(1), dim3(kRsBlock), s, e0, e1, ms, tilep, nt, N, tileOff, rec,
-                        decide_local, ess_min, dec, p);
+                        decide_local, ess_min, dec, p, esum);
 }
 hipError_t launch_rs_decide(hipStream_t s, const ShardRecord* recs, int world, int rank, double ess_min,
                             Decision* dec) {
@@ -1353,20 +1408,17 @@ hipError_t launch_rs_scan(hipStream_t s, int64_t N, const ShardRecord* rec, cons
                         qbuf, anc);
 }
 
+hipError_t launch_rs_sums_multi(hipStream_t s, const double* w, int64_t N, const MaxSlots* ms, const FillPlan& plan,
+                                u64* tilep, u64* lcdf, u64* esum, hipEvent_t e0, hipEvent_t e1) {
+    return launch_timed(k_rs_sums_multi, rs_tiles_for(N), dim3(kSumBlock), s, e0, e1, w, N, ms, plan, tilep, lcdf,
+                        esum);
+}
 hipError_t launch_rs_multinomial(hipStream_t s, int64_t N, const ShardRecord* rec, const Decision* dec,
-                                 const FillPlan& plan, const u64* tileOff, const u64* qbuf, u64* cdf, int32_t* anc,
-                                 hipEvent_t e0, hipEvent_t e1) {
+                                 const FillPlan& plan, const u64* tileOff, const u64* lcdf, const u64* esum,
+                                 int32_t* anc, hipEvent_t e0, hipEvent_t e1) {
     const unsigned nt = (unsigned)((N + kRsTile - 1) / kRsTile);
-    const int64_t nb = (N + 1 + kRsTile - 1) / kRsTile;
-    u64* esum = cdf + N;                            // nb + 1 words past the CDF
-    // e0 opens on the CDF kernel, e1 closes on the fill (either may be null)
-    hipError_t e = launch_timed(k_rs_cdf, dim3(nt), dim3(kScanBlock), s, e0, nullptr, N, dec, tileOff, qbuf, cdf);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_multi_esum, dim3((unsigned)nb), dim3(kScanBlock), 0, s, N, dec, plan, esum);
-    hipLaunchKernelGGL(k_multi_escan, dim3(1), dim3(kScanBlock), 0, s, nb, dec, esum);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    return launch_timed(k_multi_fill, dim3(nt), dim3(kScanBlock), s, nullptr, e1, N, rec, dec, plan, tileOff, cdf,
-                        esum, anc);
+    return launch_timed(k_multi_fill, dim3(nt), dim3(kScanBlock), s, e0, e1, N, rec, dec, plan, tileOff, lcdf, esum,
+                        anc);
 }
 
 // diagnostics: the propagate kernel's memory pattern with no arithmetic — per particle a
@@ -1420,10 +1472,10 @@ hipError_t debug_kernel_bench(hipStream_t s, int kernel, int mode, int iters, co
         } else if (kernel == 1) {
             const int64_t nt = (N + kRsTile - 1) / kRsTile;
             switch (mode) {
-                case 0: hipLaunchKernelGGL(k_rs_reduce_t<0>, dim3(1), dim3(kRsBlock), 0, s, ms, tilep, nt, N, tileOff, rec, 1, 2.0, dec, plan); break;
-                case 1: hipLaunchKernelGGL(k_rs_reduce_t<1>, dim3(1), dim3(kRsBlock), 0, s, ms, tilep, nt, N, tileOff, rec, 1, 2.0, dec, plan); break;
-                case 2: hipLaunchKernelGGL(k_rs_reduce_t<2>, dim3(1), dim3(kRsBlock), 0, s, ms, tilep, nt, N, tileOff, rec, 1, 2.0, dec, plan); break;
-                default: hipLaunchKernelGGL(k_rs_reduce_t<3>, dim3(1), dim3(kRsBlock), 0, s, ms, tilep, nt, N, tileOff, rec, 1, 2.0, dec, plan); break;
+                case 0: hipLaunchKernelGGL(k_rs_reduce_t<0>, dim3(1), dim3(kRsBlock), 0, s, ms, tilep, nt, N, tileOff, rec, 1, 2.0, dec, plan, nullptr); break;
+                case 1: hipLaunchKernelGGL(k_rs_reduce_t<1>, dim3(1), dim3(kRsBlock), 0, s, ms, tilep, nt, N, tileOff, rec, 1, 2.0, dec, plan, nullptr); break;
+                case 2: hipLaunchKernelGGL(k_rs_reduce_t<2>, dim3(1), dim3(kRsBlock), 0, s, ms, tilep, nt, N, tileOff, rec, 1, 2.0, dec, plan, nullptr); break;
+                default: hipLaunchKernelGGL(k_rs_reduce_t<3>, dim3(1), dim3(kRsBlock), 0, s, ms, tilep, nt, N, tileOff, rec, 1, 2.0, dec, plan, nullptr); break;
             }
         } else {
             switch (mode) {
