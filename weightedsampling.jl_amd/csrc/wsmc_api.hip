@@ -448,6 +448,8 @@ static int ensure_cdf(wsmc_ctx* c) {
 
 // multinomial: c->cdf holds the tile-local CDF [N], then the spacing tile sums / offsets
 static unsigned long long* multi_esum(wsmc_ctx* c) { return c->cdf + c->N; }
+// and the slots' spacings E (u32) in the q buffer, which the multinomial path does not use
+static uint32_t* multi_ebuf(wsmc_ctx* c) { return reinterpret_cast<uint32_t*>(c->qbuf); }
 
 static int enqueue_resample_stats(wsmc_ctx* c, const double* w, MaxSlots* ms, ShardRecord* recs, double ess_min,
                                   Decision* dec, bool run_max, const FillPlan& plan, hipEvent_t* ev = nullptr) {
@@ -457,7 +459,7 @@ static int enqueue_resample_stats(wsmc_ctx* c, const double* w, MaxSlots* ms, Sh
     }
     const bool multi = plan.scheme == WSMC_RESAMPLE_MULTINOMIAL;
     if (multi)
-        WSMC_HIP(launch_rs_sums_multi(c->stream, w, c->N, ms, plan, c->tilep, c->cdf, multi_esum(c),
+        WSMC_HIP(launch_rs_sums_multi(c->stream, w, c->N, ms, plan, c->tilep, c->cdf, multi_esum(c), multi_ebuf(c),
                                       ev ? ev[0] : nullptr, ev ? ev[1] : nullptr));
     else
         WSMC_HIP(launch_rs_sums(c->stream, w, c->N, ms, c->tilep, c->qbuf, ev ? ev[0] : nullptr, ev ? ev[1] : nullptr));
@@ -695,7 +697,7 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
     if (r) return r;
     if (scheme == WSMC_RESAMPLE_MULTINOMIAL)
         WSMC_HIP(launch_rs_multinomial(c->stream, c->N, c->rec + c->rank, c->dec, plan, c->tileOff, c->cdf,
-                                       multi_esum(c), c->anc));
+                                       multi_esum(c), multi_ebuf(c), c->anc));
     else
         WSMC_HIP(launch_rs_scan(c->stream, c->N, c->rec + c->rank, c->dec, plan, c->tileOff, c->qbuf, c->anc));
     Decision* hd = reinterpret_cast<Decision*>(c->pinned);
@@ -1056,7 +1058,7 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
         int32_t* anc_row = c->anc_log + (size_t)(t - 1) * anc_stride(N);
         if (p.scheme == WSMC_RESAMPLE_MULTINOMIAL) {
             // unsorted draws: sums, reduce (tile offsets, record), [exchange + decide], CDF + search
-            WSMC_HIP(launch_rs_sums_multi(c->stream, c->w, N, ms, plan, c->tilep, c->cdf, multi_esum(c), E(k0 + 2),
+            WSMC_HIP(launch_rs_sums_multi(c->stream, c->w, N, ms, plan, c->tilep, c->cdf, multi_esum(c), multi_ebuf(c), E(k0 + 2),
                                           E(k0 + 3)));
             WSMC_HIP(launch_rs_reduce(c->stream, ms, c->tilep, N, c->tileOff, recs + c->rank, !sharded, p.ess_min,
                                       c->run_dec + t, &plan, E(k0 + 6), nullptr, multi_esum(c)));
@@ -1066,7 +1068,7 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
                 WSMC_HIP(launch_rs_decide(c->stream, recs, c->world, c->rank, p.ess_min, c->run_dec + t));
             }
             WSMC_HIP(launch_rs_multinomial(c->stream, N, recs + c->rank, c->run_dec + t, plan, c->tileOff, c->cdf,
-                                           multi_esum(c), anc_row, nullptr, E(k0 + 7)));
+                                           multi_esum(c), multi_ebuf(c), anc_row, nullptr, E(k0 + 7)));
             continue;
         }
         if (!sharded) {

@@ -207,11 +207,12 @@ hipError_t launch_rs_scan(hipStream_t s, int64_t N, const ShardRecord* rec, cons
 // (the reduce kernel turns the spacing sums into offsets when given esum)
 hipError_t launch_rs_sums_multi(hipStream_t s, const double* w, int64_t N, const MaxSlots* ms, const FillPlan& plan,
                                 unsigned long long* tilep, unsigned long long* lcdf, unsigned long long* esum,
-                                hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+                                uint32_t* ebuf, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t launch_rs_multinomial(hipStream_t s, int64_t N, const ShardRecord* rec, const Decision* dec,
                                  const FillPlan& plan, const unsigned long long* tileOff,
-                                 const unsigned long long* lcdf, const unsigned long long* esum, int32_t* anc,
-                                 hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+                                 const unsigned long long* lcdf, const unsigned long long* esum,
+                                 const uint32_t* ebuf, int32_t* anc, hipEvent_t e0 = nullptr,
+                                 hipEvent_t e1 = nullptr);
 // fused single-GPU run: group sums (kGroupLine u64 per group) replace the reduce kernel
 constexpr int kGroupLine = 8;
 constexpr int kMaxWorld = kMaxShards;   // ranks of one node
