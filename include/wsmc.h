@@ -143,6 +143,19 @@ int wsmc_comm_init(wsmc_ctx* ctx, const uint8_t id[128], int32_t world, int32_t 
 typedef int (*wsmc_exchange_fn)(void* user, const uint64_t* mine, int32_t words, uint64_t* all);
 int wsmc_comm_init_host(wsmc_ctx* ctx, wsmc_exchange_fn exchange, void* user, int32_t world, int32_t rank,
                         int64_t global_offset, int64_t global_n);
+/* How a sharded Resample draws:
+ *  WSMC_SHARD_ISLAND (default): one record all-gather per step; each shard resamples
+ *    within itself and resets to its own log-mean (evidence-preserving). Not the
+ *    single-GPU ancestors.
+ *  WSMC_SHARD_EXACT: the reference's stratified/systematic Resample over the whole
+ *    population — identical bits to one context holding every particle (ancestors as
+ *    global indices, columns, weights, evidence): the global max is exchanged first,
+ *    the records are summed as integers, each shard fills its contiguous window of
+ *    global slots and the particles move to their owners (grouped send/recv).
+ * Exact mode covers the statement operators; wsmc_ssm2d_run and multinomial draws on
+ * shards stay island (WSMC_ESTATE / WSMC_EARG otherwise). */
+typedef enum { WSMC_SHARD_ISLAND = 0, WSMC_SHARD_EXACT = 1 } wsmc_shard_mode;
+int wsmc_comm_set_shard_mode(wsmc_ctx* ctx, int32_t mode);
 
 /* ---- store: AbstractParticleStore (src/stores.jl:1-35) ----------------------- */
 /* broadcast_setcol! column creation (src/stores.jl:85-96); existing name => same id */

@@ -162,3 +162,77 @@ def test_two_shards_moves_match_sharded_oracle(gpu_available, tmp_path, which):
             np.testing.assert_array_equal(p["c_" + name], ref.col_download(ref.col_find(name))[..., sl], err_msg=name)
         assert p["ev"][0] == ref.log_evidence()
         assert p["gate"][0] == 1
+
+
+# ---- exact sharding: the shards together give the single-context bits ---------------------
+def _exact_worker(rank, world, port, sizes, T, ess, scheme, outdir):
+    sys.path[:0] = [str(REPO / "weightedsampling.jl_amd")]
+    import wsmc
+    from wsmc import abi
+    from wsmc.hostcomm import HostComm
+    comm = HostComm(rank, world, "127.0.0.1", port, tag="ex", timeout=120)
+    n, goff, N = sizes[rank], sum(sizes[:rank]), sum(sizes)
+    c = wsmc.Context(n, seed=21, device=0)
+    c.comm_init_host(comm.allgather, world, rank, goff, N)
+    c.comm_set_shard_mode(abi.SHARD_EXACT)
+    flags = wsmc.models.ssm2d_statements(c, wsmc.models.ssm2d_data(T), ess_perc_min=ess, scheme=scheme)
+    out = {"flags": np.array(flags), "w": c.weights_download(), "anc": c.last_ancestors(),
+           "ev": np.array([c.log_evidence()]), "ess": np.array([c.ess()])}
+    for name in c.col_names():
+        out["s_" + name] = c.col_download(c.col_find(name))
+    # what exact shards refuse rather than silently doing island work
+    refused = []
+    try:
+        c.ssm2d_run(wsmc.models.ssm2d_data(2), ess_perc_min=ess)
+    except wsmc.WSMCError:
+        refused.append("fused")
+    try:
+        c.resample(2.0, abi.RESAMPLE_MULTINOMIAL)
+    except wsmc.WSMCError:
+        refused.append("multinomial")
+    out["refused"] = np.array(refused)
+    c.close()
+    comm.barrier()
+    comm.close()
+    np.savez(os.path.join(outdir, f"ex{rank}.npz"), **out)
+
+
+@pytest.mark.parametrize("sizes,ess,scheme", [((2048, 2048), 1.0, 0), ((2048, 2048), 0.5, 1),
+                                              ((3000, 1096), 1.0, 0), ((70001, 70001), 1.0, 0),
+                                              ((70001, 70001), 0.5, 1)])
+def test_exact_shards_match_single_context_oracle(gpu_available, tmp_path, sizes, ess, scheme):
+    """WSMC_SHARD_EXACT: two shards (one ragged layout) == the unsharded oracle: flags,
+    weights, every column, global ancestor indices, log-evidence and ESS, bit for bit."""
+    import multiprocessing as mp
+    sys.path.insert(0, str(REPO / "oracle"))
+    from oracle import Oracle
+    import wsmc
+    T, world = 8, len(sizes)
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=_exact_worker, args=(r, world, port, sizes, T, ess, scheme, str(tmp_path)))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(300)
+    codes = [p.exitcode for p in ps]
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+    assert codes == [0] * world, codes
+    N = sum(sizes)
+    ref = Oracle(N, seed=21)
+    flags = wsmc.models.ssm2d_statements(ref, wsmc.models.ssm2d_data(T), ess_perc_min=ess, scheme=scheme)
+    for r in range(world):
+        p = np.load(tmp_path / f"ex{r}.npz")
+        sl = slice(sum(sizes[:r]), sum(sizes[:r + 1]))
+        assert list(p["flags"]) == flags
+        np.testing.assert_array_equal(p["w"], ref.weights_download()[sl])
+        np.testing.assert_array_equal(p["anc"], ref.last_ancestors()[sl])
+        for name in ref.col_names():
+            np.testing.assert_array_equal(p["s_" + name], ref.col_download(ref.col_find(name))[..., sl],
+                                          err_msg=name)
+        assert p["ev"][0] == ref.log_evidence()
+        assert p["ess"][0] == ref.ess()
+        assert list(p["refused"]) == ["fused", "multinomial"]

@@ -230,7 +230,7 @@ int wsmc_destroy(wsmc_ctx* c) {
     }
     void* bufs[] = {c->xchg, c->scache, c->scache_back, c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->cdf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount,
                     c->d_colptr, c->run_params, c->d_tape, c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp,
-                    c->vscratch, c->xscratch};
+                    c->vscratch, c->xscratch, c->run_pay, c->xp, c->comb, c->anc_out, c->xbuf, c->d_comp};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     if (c->pinned) (void)hipHostFree(c->pinned);
@@ -316,6 +316,13 @@ int wsmc_comm_init_host(wsmc_ctx* c, wsmc_exchange_fn exchange, void* user, int3
     c->gN = gN;
     c->host_exchange = exchange;
     c->host_user = user;
+    return WSMC_OK;
+}
+
+int wsmc_comm_set_shard_mode(wsmc_ctx* c, int32_t mode) {
+    CHECK_CTX(c);
+    if (mode != WSMC_SHARD_ISLAND && mode != WSMC_SHARD_EXACT) return fail(WSMC_EARG, "unknown shard mode");
+    c->shard_mode = mode;
     return WSMC_OK;
 }
 
@@ -513,6 +520,195 @@ static int exchange_recs(wsmc_ctx* c, ShardRecord* recs) {
     return WSMC_OK;
 }
 
+// ---- exact sharding ---------------------------------------------------
+static bool exact_mode(const wsmc_ctx* c) { return c->world > 1 && c->shard_mode == WSMC_SHARD_EXACT; }
+
+static int ensure_exact(wsmc_ctx* c) {
+    if (!c->xp) WSMC_HIP(hipMalloc(&c->xp, sizeof(ExactPlan)));
+    if (!c->comb) WSMC_HIP(hipMalloc(&c->comb, sizeof(ShardRecord)));
+    if (!c->anc_out) WSMC_HIP(hipMalloc(&c->anc_out, sizeof(int32_t) * (size_t)c->gN));
+    if (!c->task_global) {
+        // a shard may own up to all gN slots: sum_b floor((Q_b gN / Q + 3) / kRsChunk)
+        // <= gN / kRsChunk + ntiles overflow tasks
+        WSMC_HIP(hipStreamSynchronize(c->stream));
+        WSMC_HIP(hipFree(c->taskTile));
+        WSMC_HIP(hipMalloc(&c->taskTile, sizeof(int32_t) * (size_t)(c->nrstiles + c->gN / kRsChunk + 1)));
+        c->task_global = true;
+    }
+    return WSMC_OK;
+}
+
+// the global max (the ranks' local maxima all-gathered), the shard's q relative to it with
+// K from the global N, its record, and every rank's record: their integer sums are exactly
+// the statistics one context holding all particles computes
+static int exact_records(wsmc_ctx* c) {
+    WSMC_HIP(hipMemsetAsync(c->mslots, 0, sizeof(MaxSlots), c->stream));
+    WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, c->mslots));
+    WSMC_HIP(launch_max_publish(c->stream, c->mslots, c->xchg + c->rank));
+    int r = exchange_words(c, c->xchg, 1, c->stream);
+    if (r) return r;
+    WSMC_HIP(launch_max_adopt(c->stream, c->xchg, c->world, c->mslots));
+    WSMC_HIP(launch_rs_sums(c->stream, c->w, c->N, c->mslots, c->tilep, c->qbuf, nullptr, nullptr, nullptr, 1, nullptr,
+                            c->gN));
+    WSMC_HIP(launch_rs_reduce(c->stream, c->mslots, c->tilep, c->N, c->tileOff, c->rec + c->rank, 0, 0.0, nullptr,
+                              nullptr));
+    return exchange_recs(c, c->rec);
+}
+static int exact_global_stats(wsmc_ctx* c, wsmc_shard_stats* st) {
+    int r = exact_records(c);
+    if (r) return r;
+    std::vector<ShardRecord> h(c->world);
+    WSMC_HIP(hipMemcpyAsync(h.data(), c->rec, sizeof(ShardRecord) * c->world, hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    *st = host_record_stats(h[0]);
+    st->Q = 0; st->S1 = 0; st->S2 = 0; st->Wf = 0; st->n = 0;
+    for (int g = 0; g < c->world; ++g) {
+        const wsmc_shard_stats x = host_record_stats(h[g]);
+        st->Q += x.Q; st->S1 += x.S1; st->S2 += x.S2; st->Wf += x.Wf; st->n += x.n;
+    }
+    return WSMC_OK;
+}
+
+static inline unsigned long long overlap(unsigned long long a0, unsigned long long a1, unsigned long long b0,
+                                         unsigned long long b1) {
+    const unsigned long long lo = a0 > b0 ? a0 : b0, hi = a1 < b1 ? a1 : b1;
+    return hi > lo ? hi - lo : 0ull;
+}
+
+// the window's slots move to their owners: local ones in place, the rest packed per peer,
+// exchanged (grouped RCCL send/recv, or the host exchange), unpacked
+static int exact_move_particles(wsmc_ctx* c, const ExactPlan& x) {
+    const int W = c->world, me = c->rank;
+    std::vector<const double*> src;
+    std::vector<double*> dst;
+    for (auto& col : c->cols)
+        for (int k = 0; k < col.dim; ++k) {
+            src.push_back(col.front + (int64_t)k * c->N);
+            dst.push_back(col.back + (int64_t)k * c->N);
+        }
+    const bool cache = c->scache && c->scache_terms >= 0;   // carried Move scores follow their particles
+    if (cache) {
+        src.push_back(c->scache);
+        dst.push_back(c->scache_back);
+    }
+    const int nc = (int)src.size();
+    const size_t need = 2 * (size_t)(nc > 0 ? nc : 1);
+    if (c->d_comp_cap < need) {
+        if (c->d_comp) WSMC_HIP(hipFree(c->d_comp));
+        WSMC_HIP(hipMalloc(&c->d_comp, sizeof(double*) * need));
+        c->d_comp_cap = need;
+    }
+    std::vector<double*> tab(need, nullptr);
+    for (int k = 0; k < nc; ++k) {
+        tab[k] = const_cast<double*>(src[k]);
+        tab[nc + k] = dst[k];
+    }
+    WSMC_HIP(hipMemcpyAsync(c->d_comp, tab.data(), sizeof(double*) * need, hipMemcpyHostToDevice, c->stream));
+    // routing tables (every rank derives every rank's blocks from the same plan)
+    const unsigned long long D = (unsigned long long)nc + 1;
+    auto sendlen = [&](int g, int r) { return overlap(x.seg[g], x.seg[g + 1], x.gofs[r], x.gofs[r + 1]); };
+    ExactRoute rt{};
+    rt.world = W; rt.rank = me; rt.ncomp = nc;
+    rt.a = x.a; rt.b = x.b;
+    for (int g = 0; g <= W; ++g) rt.gofs[g] = x.gofs[g];
+    unsigned long long S = 0, R = 0;
+    std::vector<unsigned long long> Sg(W, 0);
+    for (int g = 0; g < W; ++g)
+        for (int r = 0; r < W; ++r)
+            if (r != g) Sg[g] += sendlen(g, r) * D;
+    for (int r = 0; r < W; ++r) {
+        rt.sendoff[r] = S;
+        if (r != me) S += sendlen(me, r) * D;
+    }
+    rt.recvpre[0] = 0;
+    for (int g = 0; g < W; ++g) {
+        const unsigned long long n = g == me ? 0ull : sendlen(g, me);
+        rt.recvoff[g] = R;
+        rt.recvlen[g] = n;
+        rt.recvdst[g] = (x.seg[g] > x.gofs[me] ? x.seg[g] : x.gofs[me]) - x.gofs[me];
+        rt.recvpre[g + 1] = rt.recvpre[g] + n;
+        R += n * D;
+    }
+    const size_t words = (size_t)(S + R) + 1;
+    if (c->xbuf_cap < words) {
+        if (c->xbuf) WSMC_HIP(hipFree(c->xbuf));
+        WSMC_HIP(hipMalloc(&c->xbuf, sizeof(unsigned long long) * words));
+        c->xbuf_cap = words;
+    }
+    unsigned long long* sendbuf = c->xbuf;
+    unsigned long long* recvbuf = c->xbuf + S;
+    WSMC_HIP(launch_exact_pack(c->stream, rt, c->anc_out, c->d_comp, c->d_comp + nc, c->anc, sendbuf));
+    if (c->host_exchange) {
+        // test transport: every rank all-gathers its whole send area (padded to the largest)
+        unsigned long long maxS = 0;
+        for (int g = 0; g < W; ++g) maxS = Sg[g] > maxS ? Sg[g] : maxS;
+        if (maxS > 0) {
+            if (maxS > 0x7fffffffull) return fail(WSMC_EARG, "host exchange block too large");
+            std::vector<unsigned long long> mine(maxS, 0ull), all((size_t)maxS * W);
+            if (S) WSMC_HIP(hipMemcpyAsync(mine.data(), sendbuf, sizeof(unsigned long long) * S, hipMemcpyDeviceToHost,
+                                           c->stream));
+            WSMC_HIP(hipStreamSynchronize(c->stream));
+            if (c->host_exchange(c->host_user, reinterpret_cast<const uint64_t*>(mine.data()), (int32_t)maxS,
+                                 reinterpret_cast<uint64_t*>(all.data())) != 0)
+                return fail(WSMC_ERCCL, "host particle exchange failed");
+            std::vector<unsigned long long> rv((size_t)R + 1);
+            for (int g = 0; g < W; ++g) {
+                if (g == me || !rt.recvlen[g]) continue;
+                unsigned long long off = 0;
+                for (int r = 0; r < me; ++r)
+                    if (r != g) off += sendlen(g, r) * D;
+                std::memcpy(rv.data() + rt.recvoff[g], all.data() + (size_t)g * maxS + off,
+                            sizeof(unsigned long long) * rt.recvlen[g] * D);
+            }
+            if (R) WSMC_HIP(hipMemcpyAsync(recvbuf, rv.data(), sizeof(unsigned long long) * R, hipMemcpyHostToDevice,
+                                           c->stream));
+            WSMC_HIP(hipStreamSynchronize(c->stream));
+        }
+    } else {
+        WSMC_RCCL(ncclGroupStart());
+        for (int r = 0; r < W; ++r) {
+            if (r == me) continue;
+            const unsigned long long ns = sendlen(me, r) * D, nr = rt.recvlen[r] * D;
+            if (ns) WSMC_RCCL(ncclSend(sendbuf + rt.sendoff[r], (size_t)ns, ncclUint64, r, c->comm, c->stream));
+            if (nr) WSMC_RCCL(ncclRecv(recvbuf + rt.recvoff[r], (size_t)nr, ncclUint64, r, c->comm, c->stream));
+        }
+        WSMC_RCCL(ncclGroupEnd());
+    }
+    WSMC_HIP(launch_exact_unpack(c->stream, rt, recvbuf, c->d_comp + nc, c->anc));
+    for (auto& col : c->cols) std::swap(col.front, col.back);
+    if (cache) std::swap(c->scache, c->scache_back);
+    c->colptr_dirty = true;
+    return WSMC_OK;
+}
+
+// Resample over the whole population: the single-GPU decision,
+// ancestors, columns, weights and evidence, bit for bit
+static int exact_resample(wsmc_ctx* c, double ess_min, int32_t scheme, uint64_t op, Decision* out) {
+    int r = ensure_exact(c);
+    if (r) return r;
+    if ((r = exact_records(c))) return r;
+    FillPlan plan = fill_plan(c, scheme, op, nullptr);
+    plan.slot_base = 0;                       // slots are global: their keys too
+    WSMC_HIP(launch_rs_decide_exact(c->stream, c->rec, c->world, c->rank, ess_min, plan, c->comb, c->dec, c->xp));
+    plan.xp = c->xp;
+    // fill tasks planned with the global strata (N / Q of the whole population)
+    WSMC_HIP(launch_rs_reduce(c->stream, c->mslots, c->tilep, c->N, c->tileOff, c->rec + c->rank, 0, ess_min, c->dec,
+                              &plan));
+    WSMC_HIP(launch_rs_scan(c->stream, c->N, c->comb, c->dec, plan, c->tileOff, c->qbuf, c->anc_out));
+    struct Host { Decision d; ExactPlan x; };
+    Host* h = reinterpret_cast<Host*>(c->pinned);
+    static_assert(sizeof(Host) <= 4096, "pinned staging");
+    WSMC_HIP(hipMemcpyAsync(&h->d, c->dec, sizeof(Decision), hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipMemcpyAsync(&h->x, c->xp, sizeof(ExactPlan), hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    *out = h->d;
+    if (!out->resampled) return WSMC_OK;
+    const ExactPlan x = h->x;
+    if ((r = exact_move_particles(c, x))) return r;
+    WSMC_HIP(launch_fill_weights(c->stream, c->w, c->dec, c->N));
+    return WSMC_OK;
+}
+
 // ---- analysis reductions (src/utils.jl) ----------------------------------------------
 int wsmc_weighted_moments(wsmc_ctx* c, const wsmc_operand* exprs, int32_t d, double* mean, double* cov) {
     CHECK_CTX(c);
@@ -566,6 +762,13 @@ int wsmc_col_minmax(wsmc_ctx* c, int32_t col, int32_t comp, double* mn, double* 
 int wsmc_ess(wsmc_ctx* c, double* ess_perc) {
     CHECK_CTX(c);
     if (!ess_perc) return fail(WSMC_EARG, "null output");
+    if (exact_mode(c)) {
+        wsmc_shard_stats st;
+        int r = exact_global_stats(c, &st);
+        if (r) return r;
+        *ess_perc = wsmc_global_ess(&st, 1);
+        return WSMC_OK;
+    }
     WSMC_HIP(hipMemsetAsync(c->mslots, 0, sizeof(MaxSlots), c->stream));
     WSMC_HIP(launch_log_evidence_stats(c->stream, c->w, c->N, c->mslots, c->tilep, c->qbuf, c->tileOff,
                                        c->rec + c->rank));
@@ -583,6 +786,13 @@ int wsmc_ess(wsmc_ctx* c, double* ess_perc) {
 int wsmc_log_evidence(wsmc_ctx* c, double* out) {
     CHECK_CTX(c);
     if (!out) return fail(WSMC_EARG, "null out");
+    if (exact_mode(c)) {
+        wsmc_shard_stats st;
+        int r = exact_global_stats(c, &st);
+        if (r) return r;
+        *out = wsmc_global_log_evidence(&st, 1);
+        return WSMC_OK;
+    }
     WSMC_HIP(hipMemsetAsync(c->mslots, 0, sizeof(MaxSlots), c->stream));
     WSMC_HIP(launch_log_evidence_stats(c->stream, c->w, c->N, c->mslots, c->tilep, c->qbuf, c->tileOff,
                                        c->rec + c->rank));
@@ -685,11 +895,25 @@ int wsmc_weight(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x) { return
 int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resampled_out, double* ess_out) {
     CHECK_CTX(c);
     if (!valid_scheme(scheme)) return fail(WSMC_EARG, "unknown resampling scheme");
+    if (scheme == WSMC_RESAMPLE_MULTINOMIAL && exact_mode(c))
+        return fail(WSMC_EARG, "multinomial draws on exact shards are not supported (island mode is)");
     if (scheme == WSMC_RESAMPLE_MULTINOMIAL && ensure_cdf(c)) return WSMC_EHIP;
     const uint64_t op = c->op++;
     if (!c->weights_changed) {
         if (resampled_out) *resampled_out = c->resampled;
         if (ess_out) *ess_out = c->last_ess;
+        return WSMC_OK;
+    }
+    if (exact_mode(c)) {
+        Decision d;
+        int r = exact_resample(c, ess_min, scheme, op, &d);
+        if (r) return r;
+        c->last_ess = d.ess;
+        c->resampled = d.resampled;
+        if (d.resampled) c->n_resamples += 1;
+        c->weights_changed = 0;
+        if (resampled_out) *resampled_out = c->resampled;
+        if (ess_out) *ess_out = d.ess;
         return WSMC_OK;
     }
     const FillPlan plan = fill_plan(c, scheme, op, nullptr);
@@ -1132,6 +1356,8 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
     c->scache_terms = -1;   // the run rewrites columns the tape reads
     if (!obs || T < 1 || !x0 || !v0) return fail(WSMC_EARG, "bad arguments");
     if (!valid_scheme(scheme)) return fail(WSMC_EARG, "unknown resampling scheme");
+    if (exact_mode(c))
+        return fail(WSMC_ESTATE, "the fused run on exact shards is not built (island mode, or the statements)");
     if (scheme == WSMC_RESAMPLE_MULTINOMIAL && ensure_cdf(c)) return WSMC_EHIP;
     if (!(q_var > 0) || !(r_var > 0)) return fail(WSMC_EARG, "variances must be positive");
     RunPlan p;

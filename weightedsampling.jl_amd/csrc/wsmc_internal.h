@@ -55,6 +55,18 @@ struct Decision {
     double M;           // this shard's max log-weight
 };
 
+// Exact cross-shard resampling: the global CDF and the slot windows,
+// built on the device from the all-gathered records (k_rs_decide_exact). Shard g's
+// particles own the contiguous global slots [seg[g], seg[g+1]) (ancestors are monotone).
+struct ExactPlan {
+    unsigned long long Q;       // global sum q (q relative to the global max, K from the global N)
+    unsigned long long N;       // global particle count
+    unsigned long long cbase;   // this shard's CDF offset: sum of the lower ranks' Q
+    unsigned long long a, b;    // this shard's slot window [a, b)
+    unsigned long long seg[kMaxShards + 1];    // slot windows of every rank
+    unsigned long long gofs[kMaxShards + 1];   // particle offsets of every rank
+};
+
 struct Column {
     std::string name;
     int32_t dim = 1;
@@ -122,6 +134,16 @@ struct wsmc_ctx {
     int32_t* taskTile = nullptr;            // [N / kRsChunk + nrstiles + 1] tile of each overflow task
     unsigned long long* qbuf = nullptr;     // [N] integer weights q_i of the last weight-statistics pass
     unsigned long long* cdf = nullptr;      // [N] tile-local CDF of q + spacing tile sums (multinomial; lazy)
+    // exact sharding (wsmc_comm_set_shard_mode)
+    int32_t shard_mode = 0;                 // WSMC_SHARD_ISLAND / WSMC_SHARD_EXACT
+    wsmc::ExactPlan* xp = nullptr;          // [1] device plan
+    wsmc::ShardRecord* comb = nullptr;      // [1] combined (global) record
+    int32_t* anc_out = nullptr;             // [gN] the window's ancestors (local particle ids)
+    bool task_global = false;               // taskTile sized for a window of up to gN slots
+    unsigned long long* xbuf = nullptr;     // send + receive buffers (words)
+    size_t xbuf_cap = 0;
+    double** d_comp = nullptr;              // [2 * cap] component pointer tables (src, dst)
+    size_t d_comp_cap = 0;
     double* tilepart = nullptr;             // [16 * ntiles] canonical-sum tile partials
     wsmc::MaxSlots* mslots = nullptr;       // [1] max slots of one generic resample / evidence
     wsmc::ShardRecord* rec = nullptr;       // [world] shard records of one generic resample
@@ -181,7 +203,8 @@ hipError_t launch_rs_max(hipStream_t s, const double* w, int64_t N, MaxSlots* ms
 hipError_t launch_rs_sums(hipStream_t s, const double* w, int64_t N, const MaxSlots* ms,
                           unsigned long long* tilep, unsigned long long* qbuf,
                           hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr,
-                          unsigned long long* grp = nullptr, int G = 1, unsigned long long* hdr = nullptr);
+                          unsigned long long* grp = nullptr, int G = 1, unsigned long long* hdr = nullptr,
+                          int64_t Nk = 0 /* N of K = 63 - ceil(log2 N): the global N when exact */);
 hipError_t launch_rs_decide_groups(hipStream_t s, const unsigned long long* pay, int64_t PW, int ngroups, int world,
                                    int rank, double ess_min, ShardRecord* recs, Decision* dec);
 struct FillPlan {          // ancestor-fill task planning (in the reduce kernel)
@@ -192,6 +215,7 @@ struct FillPlan {          // ancestor-fill task planning (in the reduce kernel)
     uint64_t seed, op;
     const uint64_t* op_dev;
     int64_t slot_base;
+    const ExactPlan* xp = nullptr;     // exact sharding: global Q / N / offsets, window-relative slots
 };
 hipError_t launch_rs_reduce(hipStream_t s, const MaxSlots* ms, const unsigned long long* tilep, int64_t N,
                             unsigned long long* tileOff, ShardRecord* rec, int decide_local, double ess_min,
@@ -199,6 +223,29 @@ hipError_t launch_rs_reduce(hipStream_t s, const MaxSlots* ms, const unsigned lo
                             unsigned long long* esum = nullptr);
 hipError_t launch_rs_decide(hipStream_t s, const ShardRecord* recs, int world, int rank, double ess_min,
                             Decision* dec);
+// exact sharding: global max from the all-gathered per-rank maxima (words[world]) into ms
+hipError_t launch_max_adopt(hipStream_t s, const unsigned long long* words, int world, MaxSlots* ms);
+hipError_t launch_max_publish(hipStream_t s, const MaxSlots* ms, unsigned long long* word);
+// exact sharding: records summed as integers (the single-GPU decision bits), slot windows
+hipError_t launch_rs_decide_exact(hipStream_t s, const ShardRecord* recs, int world, int rank, double ess_min,
+                                  const FillPlan& plan, ShardRecord* comb, Decision* dec, ExactPlan* xp);
+// exact sharding: slot -> owner routing of the filled window (local slots written in place,
+// the rest packed per peer as [component][slot] u64 blocks), and the receive side
+struct ExactRoute {
+    int32_t world, rank, ncomp;                 // ncomp double components (+1 ancestor id word)
+    unsigned long long a, b;                    // this rank's window
+    unsigned long long gofs[kMaxShards + 1];
+    unsigned long long sendoff[kMaxShards];     // words, per peer
+    unsigned long long recvoff[kMaxShards];     // words, per source
+    unsigned long long recvlen[kMaxShards];     // slots, per source
+    unsigned long long recvdst[kMaxShards];     // first local slot, per source
+    unsigned long long recvpre[kMaxShards + 1]; // prefix of recvlen (slots)
+};
+hipError_t launch_exact_pack(hipStream_t s, const ExactRoute& rt, const int32_t* anc_out,
+                             const double* const* src, double* const* dst, int32_t* anc_local,
+                             unsigned long long* sendbuf);
+hipError_t launch_exact_unpack(hipStream_t s, const ExactRoute& rt, const unsigned long long* recvbuf,
+                               double* const* dst, int32_t* anc_local);
 hipError_t launch_rs_scan(hipStream_t s, int64_t N, const ShardRecord* rec, const Decision* dec,
                           const FillPlan& plan, const unsigned long long* tileOff,
                           const unsigned long long* qbuf, int32_t* anc, hipEvent_t e0 = nullptr,

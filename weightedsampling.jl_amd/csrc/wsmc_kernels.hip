@@ -238,7 +238,7 @@ template <int MODE>
 __global__ __launch_bounds__(kSumBlock) void k_rs_sums_t(const double* __restrict__ w, int64_t N,
                                                          const MaxSlots* __restrict__ ms, u64* __restrict__ tilep,
                                                          u64* __restrict__ qbuf, u64* __restrict__ grp, int G,
-                                                         u64* __restrict__ hdr) {
+                                                         u64* __restrict__ hdr, int64_t Nk) {
     constexpr int IT = kRsTile / kSumBlock;
     __shared__ double s_f[3][kSumBlock / 64];
     __shared__ u64 s_q[kSumBlock / 64];
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(kSumBlock) void k_rs_sums_t(const double* __restric
         lw[k] = i < N ? w[i] : -WSMC_INF;
     }
     const double M = MODE == 4 ? 0.0 : wave_slots_max(ms);
-    const double sK = wsmc_pow2i(wsmc_qbits((uint64_t)N));
+    const double sK = wsmc_pow2i(wsmc_qbits((uint64_t)Nk));   // Nk: the global N when exact-sharded
     u64 Q = 0;
     double S1 = 0.0, S2 = 0.0, WF = 0.0;
 #pragma unroll
@@ -408,7 +408,9 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_reduce_t(const MaxSlots* __rest
     // stratum), so ceil((Q_b N / Q + 3) / kRsChunk) - 1 chunks past the first always
     // suffice (a chunk found empty exits). Fill blocks rank their own tile's boundaries.
     const bool planned = MODE != 1 && MODE != 3 && plan.taskOff != nullptr;   // log-evidence: unplanned
-    const double ratio = total ? wsmc_u64_to_d((uint64_t)N) / wsmc_u64_to_d(total) : 0.0;
+    // targets are one per 1/N stratum of the CDF being filled: the global one when exact
+    const double ratio = plan.xp ? wsmc_u64_to_d(plan.xp->N) / wsmc_u64_to_d(plan.xp->Q)
+                                 : total ? wsmc_u64_to_d((uint64_t)N) / wsmc_u64_to_d(total) : 0.0;
     int nt = 0;
     {
         u64 c = pre;
@@ -484,6 +486,97 @@ __global__ void k_rs_decide(const ShardRecord* recs, int world, int rank, double
     if (threadIdx.x == 0) decide_records(recs, world, rank, ess_min, dec);
 }
 
+// ---- exact sharding ----------------------------------------------------
+__global__ void k_max_publish(const MaxSlots* ms, u64* word) {
+    const u64 m = wave_max_u64(ms->v[threadIdx.x & 63][0]);
+    if (threadIdx.x == 0) *word = m;
+}
+// the global max (ordered encodings: NaN dominates, as the device max does) into slot 0
+__global__ void k_max_adopt(const u64* words, int world, MaxSlots* ms) {
+    const int th = threadIdx.x;
+    u64 m = 0;
+    for (int g = 0; g < world; ++g) m = words[g] > m ? words[g] : m;
+    ms->v[th & 63][0] = th == 0 ? m : 0ull;
+}
+// Sum the records as integers (every shard's q is relative to the global max with K from
+// the global N, so the sums are exactly the single-GPU ones) and decide once, as one GPU
+// does; then the global CDF offsets and every rank's window of global slots.
+__global__ void k_rs_decide_exact(const ShardRecord* recs, int world, int rank, double ess_min, FillPlan plan,
+                                  ShardRecord* comb, Decision* dec, ExactPlan* xp) {
+    if (threadIdx.x != 0) return;
+    ShardRecord r = recs[0];
+    wsmc_u128 S2 = 0, Wf = 0;
+    u64 Q = 0, S1 = 0, n = 0;
+    u64 cb[kMaxShards + 1];
+    for (int g = 0; g < world; ++g) {
+        cb[g] = Q;
+        xp->gofs[g] = n;
+        Q += recs[g].Q;
+        S1 += recs[g].s1;
+        S2 += ((wsmc_u128)recs[g].s2hi << 64) | recs[g].s2lo;
+        Wf += ((wsmc_u128)recs[g].wfhi << 64) | recs[g].wflo;
+        n += recs[g].n;
+        r.menc = recs[g].menc > r.menc ? recs[g].menc : r.menc;
+    }
+    cb[world] = Q;
+    xp->gofs[world] = n;
+    r.Q = Q;
+    r.s1 = S1;
+    r.s2lo = (u64)S2; r.s2hi = (u64)(S2 >> 64);
+    r.wflo = (u64)Wf; r.wfhi = (u64)(Wf >> 64);
+    r.n = n;
+    *comb = r;
+    decide_records(&r, 1, 0, ess_min, dec);
+    const uint64_t opx = op_eff(plan.op, plan.op_dev);
+    xp->Q = Q;
+    xp->N = n;
+    for (int g = 0; g <= world; ++g)
+        xp->seg[g] = Q ? wsmc_rank(cb[g], Q, n, plan.scheme, plan.seed, opx, 0) : 0;
+    xp->cbase = cb[rank];
+    xp->a = xp->seg[rank];
+    xp->b = xp->seg[rank + 1];
+}
+// slot j of the window: its owner keeps its components (written straight into the back
+// buffers if that is this rank, packed into the peer's send block otherwise)
+__global__ __launch_bounds__(kBlock) void k_exact_pack(ExactRoute rt, const int32_t* __restrict__ anc_out,
+                                                       const double* const* __restrict__ src,
+                                                       double* const* __restrict__ dst, int32_t* __restrict__ anc_local,
+                                                       u64* __restrict__ sendbuf) {
+    const u64 cnt = rt.b - rt.a;
+    const u64 j = (u64)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= cnt) return;
+    const u64 sl = rt.a + j;
+    int r = 0;
+    while (r + 1 < rt.world && sl >= rt.gofs[r + 1]) ++r;
+    const int32_t m = anc_out[j];
+    const u64 gid = rt.gofs[rt.rank] + (u64)m;      // the ancestor's global index
+    if (r == rt.rank) {
+        const u64 li = sl - rt.gofs[rt.rank];
+        for (int c = 0; c < rt.ncomp; ++c) dst[c][li] = src[c][m];
+        anc_local[li] = (int32_t)gid;
+        return;
+    }
+    const u64 lo = rt.a > rt.gofs[r] ? rt.a : rt.gofs[r];
+    const u64 hi = rt.b < rt.gofs[r + 1] ? rt.b : rt.gofs[r + 1];
+    const u64 len = hi - lo, idx = sl - lo;
+    u64* blk = sendbuf + rt.sendoff[r];
+    for (int c = 0; c < rt.ncomp; ++c) blk[(u64)c * len + idx] = (u64)wsmc_d2bits(src[c][m]);
+    blk[(u64)rt.ncomp * len + idx] = gid;
+}
+__global__ __launch_bounds__(kBlock) void k_exact_unpack(ExactRoute rt, const u64* __restrict__ recvbuf,
+                                                         double* const* __restrict__ dst,
+                                                         int32_t* __restrict__ anc_local) {
+    const u64 j = (u64)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= rt.recvpre[rt.world]) return;
+    int g = 0;
+    while (j >= rt.recvpre[g + 1]) ++g;
+    const u64 idx = j - rt.recvpre[g], len = rt.recvlen[g];
+    const u64* blk = recvbuf + rt.recvoff[g];
+    const u64 li = rt.recvdst[g] + idx;
+    for (int c = 0; c < rt.ncomp; ++c) dst[c][li] = wsmc_bits2d(blk[(u64)c * len + idx]);
+    anc_local[li] = (int32_t)blk[(u64)rt.ncomp * len + idx];
+}
+
 constexpr int kOverflowBlocks = 256;   // fill blocks serving overflow chunks (grid-stride)
 
 constexpr int kScatterMax = 8;          // slots a thread writes for one particle before the block helps
@@ -520,12 +613,15 @@ __device__ __forceinline__ void fill_chunk_q(int64_t N, int b, int j, u64 Q, u64
     u64 tsum = 0;
 #pragma unroll
     for (int k = 0; k < IT; ++k) tsum += q[k];
-    const double ratio = wsmc_u64_to_d((uint64_t)N) / wsmc_u64_to_d(Q);
+    // exact sharding: targets over the global population, slots written window-relative
+    const uint64_t Nr = plan.xp ? plan.xp->N : (uint64_t)N;
+    const u64 s0 = plan.xp ? plan.xp->a : 0ull;
+    const double ratio = wsmc_u64_to_d(Nr) / wsmc_u64_to_d(Q);
     // the tile's slot range [L, H) = [rank(off), rank(off + Q_b)), ranked by two threads
     // while the others scan; the scan's barrier publishes them
     if (th < 2) {
         const u64 c = th == 0 ? off : off + qb;
-        sh.LH[th] = wsmc_rank_r(c, Q, (uint64_t)N, ratio, plan.scheme, plan.seed, opx, (uint64_t)plan.slot_base);
+        sh.LH[th] = wsmc_rank_r(c, Q, Nr, ratio, plan.scheme, plan.seed, opx, (uint64_t)plan.slot_base);
     }
     if (th == 0) sh.nheavy = 0;
     u64 tot;
@@ -549,7 +645,7 @@ __device__ __forceinline__ void fill_chunk_q(int64_t N, int b, int j, u64 Q, u64
         C += q[k];
         u64 h = prev;                              // a particle with q = 0 owns no slots
         if (q[k] || k == 0) h = MODE == 1 ? (u64)(wsmc_u64_to_d(C) * ratio)
-                                : wsmc_rank_r(C, Q, (uint64_t)N, ratio, plan.scheme, plan.seed, opx,
+                                : wsmc_rank_r(C, Q, Nr, ratio, plan.scheme, plan.seed, opx,
                                               (uint64_t)plan.slot_base);
         if (MODE == 1 && h > H) h = H;
         if (MODE == 1 && h < L) h = L;
@@ -577,7 +673,7 @@ __device__ __forceinline__ void fill_chunk_q(int64_t N, int b, int j, u64 Q, u64
                 sh.heavy[x][1] = (int)(a - cs);
                 sh.heavy[x][2] = (int)(e - cs);
             } else {
-                for (u64 n = a; n < e; ++n) anc[n] = m;
+                for (u64 n = a; n < e; ++n) anc[n - s0] = m;
             }
         }
         lo = hi[k];
@@ -587,7 +683,7 @@ __device__ __forceinline__ void fill_chunk_q(int64_t N, int b, int j, u64 Q, u64
     const int nh = sh.nheavy;
     for (int x = wv; x < nh; x += kScanBlock / 64) {
         const int m = sh.heavy[x][0];
-        for (int n = sh.heavy[x][1] + lane; n < sh.heavy[x][2]; n += 64) anc[cs + n] = m;
+        for (int n = sh.heavy[x][1] + lane; n < sh.heavy[x][2]; n += 64) anc[cs - s0 + n] = m;
     }
     __syncthreads();
 }
@@ -619,18 +715,19 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_scan_t(int64_t N, const Shard
     const int t = blockIdx.x;
     const int ntiles = (int)((N + kRsTile - 1) / kRsTile);
     const int rs = dec->resampled;
-    const u64 Q = rec->Q;
+    if (!rs) return;
+    // exact sharding: the global CDF (this shard's tiles offset by the lower ranks' Q)
+    const u64 Q = plan.xp ? plan.xp->Q : rec->Q;
+    const u64 cb = plan.xp ? plan.xp->cbase : 0ull;
     const uint64_t opx = op_eff(plan.op, plan.op_dev);
     if (t < ntiles) {
-        if (!rs) return;
-        fill_chunk<MODE>(N, t, 0, Q, tileOff[t], plan, opx, qbuf, anc, sh);
+        fill_chunk<MODE>(N, t, 0, Q, cb + tileOff[t], plan, opx, qbuf, anc, sh);
         return;
     }
-    if (!rs) return;
     const int ntasks = dec->ntasks;
     for (int o = t - ntiles; o < ntasks; o += kOverflowBlocks) {
         const int b = plan.taskTile[o];
-        fill_chunk<MODE>(N, b, 1 + o - plan.taskOff[b], Q, tileOff[b], plan, opx, qbuf, anc, sh);
+        fill_chunk<MODE>(N, b, 1 + o - plan.taskOff[b], Q, cb + tileOff[b], plan, opx, qbuf, anc, sh);
     }
 }
 
@@ -1389,9 +1486,9 @@ hipError_t launch_rs_max(hipStream_t s, const double* w, int64_t N, MaxSlots* ms
     return hipGetLastError();
 }
 hipError_t launch_rs_sums(hipStream_t s, const double* w, int64_t N, const MaxSlots* ms, u64* tilep, u64* qbuf,
-                          hipEvent_t e0, hipEvent_t e1, u64* grp, int G, u64* hdr) {
+                          hipEvent_t e0, hipEvent_t e1, u64* grp, int G, u64* hdr, int64_t Nk) {
     return launch_timed(k_rs_sums_t<0>, rs_tiles_for(N), dim3(kSumBlock), s, e0, e1, w, N, ms, tilep, qbuf, grp, G,
-                        hdr);
+                        hdr, Nk > 0 ? Nk : N);
 }
 // Global decision of a sharded fused step from the all-gathered payloads (rank order):
 // each rank's record from its group sums, then the rank-order combine (decide_records).
@@ -1460,6 +1557,35 @@ hipError_t launch_rs_decide(hipStream_t s, const ShardRecord* recs, int world, i
     hipLaunchKernelGGL(k_rs_decide, dim3(1), dim3(64), 0, s, recs, world, rank, ess_min, dec);
     return hipGetLastError();
 }
+hipError_t launch_max_publish(hipStream_t s, const MaxSlots* ms, u64* word) {
+    hipLaunchKernelGGL(k_max_publish, dim3(1), dim3(64), 0, s, ms, word);
+    return hipGetLastError();
+}
+hipError_t launch_max_adopt(hipStream_t s, const u64* words, int world, MaxSlots* ms) {
+    hipLaunchKernelGGL(k_max_adopt, dim3(1), dim3(64), 0, s, words, world, ms);
+    return hipGetLastError();
+}
+hipError_t launch_rs_decide_exact(hipStream_t s, const ShardRecord* recs, int world, int rank, double ess_min,
+                                  const FillPlan& plan, ShardRecord* comb, Decision* dec, ExactPlan* xp) {
+    hipLaunchKernelGGL(k_rs_decide_exact, dim3(1), dim3(64), 0, s, recs, world, rank, ess_min, plan, comb, dec, xp);
+    return hipGetLastError();
+}
+hipError_t launch_exact_pack(hipStream_t s, const ExactRoute& rt, const int32_t* anc_out, const double* const* src,
+                             double* const* dst, int32_t* anc_local, u64* sendbuf) {
+    const u64 cnt = rt.b - rt.a;
+    if (!cnt) return hipSuccess;
+    hipLaunchKernelGGL(k_exact_pack, dim3((unsigned)((cnt + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rt, anc_out,
+                       src, dst, anc_local, sendbuf);
+    return hipGetLastError();
+}
+hipError_t launch_exact_unpack(hipStream_t s, const ExactRoute& rt, const u64* recvbuf, double* const* dst,
+                               int32_t* anc_local) {
+    const u64 cnt = rt.recvpre[rt.world];
+    if (!cnt) return hipSuccess;
+    hipLaunchKernelGGL(k_exact_unpack, dim3((unsigned)((cnt + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rt,
+                       recvbuf, dst, anc_local);
+    return hipGetLastError();
+}
 // one block per tile (its first chunk) + grid-stride overflow blocks
 static inline dim3 fill_tasks_for(int64_t N) {
     return dim3((unsigned)((N + kRsTile - 1) / kRsTile + kOverflowBlocks));
@@ -1518,9 +1644,9 @@ hipError_t debug_kernel_bench(hipStream_t s, int kernel, int mode, int iters, co
     for (int it = 0; it < iters; ++it) {
         if (kernel == 0) {
             switch (mode) {
-                case 0: hipLaunchKernelGGL(k_rs_sums_t<0>, g, blk, 0, s, w, N, ms, tilep, qbuf, nullptr, 1, nullptr); break;
-                case 1: hipLaunchKernelGGL(k_rs_sums_t<1>, g, blk, 0, s, w, N, ms, tilep, qbuf, nullptr, 1, nullptr); break;
-                default: hipLaunchKernelGGL(k_rs_sums_t<4>, g, blk, 0, s, w, N, ms, tilep, qbuf, nullptr, 1, nullptr); break;
+                case 0: hipLaunchKernelGGL(k_rs_sums_t<0>, g, blk, 0, s, w, N, ms, tilep, qbuf, nullptr, 1, nullptr, N); break;
+                case 1: hipLaunchKernelGGL(k_rs_sums_t<1>, g, blk, 0, s, w, N, ms, tilep, qbuf, nullptr, 1, nullptr, N); break;
+                default: hipLaunchKernelGGL(k_rs_sums_t<4>, g, blk, 0, s, w, N, ms, tilep, qbuf, nullptr, 1, nullptr, N); break;
             }
         } else if (kernel == 3) {
             // scratch: stream4 = 4 x [2N] doubles (x src, v src, x dst, v dst), wd = w

@@ -18,6 +18,7 @@ FAM_NORMAL, FAM_HALFNORMAL, FAM_UNIFORM, FAM_MVNORMAL_ISO = range(4)
 MEAN_AFFINE, MEAN_OSCILLATOR = range(2)
 TERM_SAMPLE, TERM_OBSERVE, TERM_WEIGHT = range(3)
 RESAMPLE_STRATIFIED, RESAMPLE_SYSTEMATIC, RESAMPLE_MULTINOMIAL = range(3)
+SHARD_ISLAND, SHARD_EXACT = range(2)
 PROPOSAL_RW, PROPOSAL_AUTORW = range(2)
 
 
@@ -82,6 +83,7 @@ SIGNATURES = {
     "wsmc_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
     "wsmc_comm_init": (C.c_int, [_P, C.POINTER(C.c_uint8), C.c_int32, C.c_int32, C.c_int64,
                                  C.c_int64]),
+    "wsmc_comm_set_shard_mode": (C.c_int, [_P, C.c_int32]),
     "wsmc_comm_init_host": (C.c_int, [_P, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int64,
                                       C.c_int64]),
     "wsmc_col_create": (C.c_int, [_P, C.c_char_p, C.c_int32, _I32P]),

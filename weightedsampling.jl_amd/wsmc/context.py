@@ -85,10 +85,12 @@ class Context:
         return every rank's list in rank order (e.g. wsmc.hostcomm.HostComm.allgather)."""
         def _exchange(_user, mine, words, out):
             try:
-                recs = allgather([int(mine[k]) for k in range(words)])
+                nb = 8 * int(words)
+                recs = allgather(C.string_at(mine, nb))        # raw u64 words of this rank
                 for r, rec in enumerate(recs):
-                    for k in range(words):
-                        out[r * words + k] = int(rec[k])
+                    if len(rec) != nb:
+                        return 1
+                    C.memmove(C.addressof(out.contents) + r * nb, rec, nb)
                 return 0
             except Exception:
                 return 1
@@ -96,6 +98,11 @@ class Context:
         check(self._L.wsmc_comm_init_host(self._h, C.cast(self._exchange_cb, C.c_void_p), None, int(world),
                                           int(rank), int(global_offset), int(global_n)))
         self.world, self.rank = int(world), int(rank)
+
+    def comm_set_shard_mode(self, mode: int) -> None:
+        """abi.SHARD_ISLAND (default) or abi.SHARD_EXACT: sharded Resample over the whole
+        population, bit-identical to one context holding every particle (include/wsmc.h)."""
+        check(self._L.wsmc_comm_set_shard_mode(self._h, int(mode)))
 
     # ---- store (AbstractParticleStore) ----
     def col_find(self, name: str) -> int:
