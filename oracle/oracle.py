@@ -28,6 +28,7 @@ _SIG = {
     "or_create": (_P, [C.c_int64, C.c_uint64]),
     "or_destroy": (None, [_P]),
     "or_set_shards": (C.c_int, [_P, C.c_int32]),
+    "or_set_shard_exact": (None, [_P, C.c_int32]),
     "or_set_global_offset": (None, [_P, C.c_int64]),
     "or_shard_record": (None, [_P, C.POINTER(C.c_uint64)]),
     "or_resample_records": (C.c_int, [_P, C.c_double, C.c_int32, C.POINTER(C.c_uint64), C.c_int32, C.c_int32,
@@ -126,7 +127,8 @@ class Oracle:
 
     is_oracle = True
 
-    def __init__(self, n_particles: int, seed: int = 42, shards: int = 1, global_offset: int = 0):
+    def __init__(self, n_particles: int, seed: int = 42, shards: int = 1, global_offset: int = 0,
+                 exact: bool = False):
         self._L = lib()
         self._h = self._L.or_create(int(n_particles), int(seed) & (2**64 - 1))
         if not self._h:
@@ -136,6 +138,8 @@ class Oracle:
         if shards != 1 and self._L.or_set_shards(self._h, int(shards)) != 0:
             raise ValueError("bad shard count")
         self.shards = shards
+        if exact:   # exact sharding: population-wide Resample, per-shard autoRW moment order
+            self._L.or_set_shard_exact(self._h, 1)
         if global_offset:
             self._L.or_set_global_offset(self._h, int(global_offset))
 

@@ -61,6 +61,7 @@ typedef struct oracle {
     wsmc_term* tape;
     int32_t nterms, cap_terms;
     int32_t nshards;
+    int32_t exact;     /* exact sharding: Resample/ESS/evidence over the whole population */
     int64_t shard_off[OR_MAX_SHARDS + 1];
     int64_t goff;              /* global index of particle 0 (one shard of a multi-process run) */
     int32_t* last_anc;
@@ -90,6 +91,16 @@ void or_destroy(oracle* o) {
     for (int c = 0; c < o->ncols; ++c) { free(o->cols[c].front); free(o->cols[c].back); }
     free(o->w); free(o->last_anc); free(o->scratch); free(o->tmp); free(o->tape);
     free(o);
+}
+
+/* WSMC_SHARD_EXACT: the device shards resample the whole population (the single-context
+ * bits) while the autoRW moments stay per-shard canonical sums in rank order */
+void or_set_shard_exact(oracle* o, int32_t exact) { o->exact = exact != 0; }
+/* the partition Resample / ESS / evidence use: the shards, or one part when exact */
+static int rs_parts(const oracle* o, int64_t* off) {
+    if (o->exact) { off[0] = 0; off[1] = o->N; return 1; }
+    for (int g = 0; g <= o->nshards; ++g) off[g] = o->shard_off[g];
+    return o->nshards;
 }
 
 int or_set_shards(oracle* o, int32_t G) {
@@ -320,24 +331,25 @@ int or_resample(oracle* o, double ess_min, int32_t scheme, int32_t* resampled_ou
         if (ess_out) *ess_out = o->last_ess;
         return 0;
     }
-    int G = o->nshards;
+    int64_t off[OR_MAX_SHARDS + 1];
+    int G = rs_parts(o, off);
     or_stats st[OR_MAX_SHARDS];
     for (int g = 0; g < G; ++g) {
-        int64_t a = o->shard_off[g], b = o->shard_off[g + 1];
+        int64_t a = off[g], b = off[g + 1];
         st[g] = shard_stats(o->w + a, b - a, wsmc_qbits((uint64_t)(b - a)));
     }
     double ess = wsmc_global_ess(st, G);
     o->last_ess = ess;
     if (ess < ess_min) {                          /* strict, src/transformers.jl:484 */
         for (int g = 0; g < G; ++g) {
-            int64_t a = o->shard_off[g], b = o->shard_off[g + 1], n = b - a;
+            int64_t a = off[g], b = off[g + 1], n = b - a;
             int K = wsmc_qbits((uint64_t)n);
             shard_ancestors(o->w + a, n, K, st[g].M, st[g].Q, scheme, o->seed, op, (uint64_t)(o->goff + a),
                             o->last_anc + a);
             for (int64_t s = 0; s < n; ++s) o->last_anc[a + s] += (int32_t)a;
         }
         for (int g = 0; g < G; ++g) {
-            int64_t a = o->shard_off[g], b = o->shard_off[g + 1];
+            int64_t a = off[g], b = off[g + 1];
             /* logsumexp(logW) - log(N): m + log(sum exp(x - m)) - log(n) */
             double mean = wsmc_shard_mean(&st[g]);
             for (int64_t i = a; i < b; ++i) o->w[i] = mean;      /* fill!(weights, mean) */
@@ -527,21 +539,25 @@ int or_col_minmax(oracle* o, int32_t col, int32_t comp, double* mn, double* mx) 
 /* ess_perc of the current weights, no state change (src/resampling.jl:51-54) */
 double or_ess(oracle* o) {
     or_stats st[OR_MAX_SHARDS];
-    for (int g = 0; g < o->nshards; ++g) {
-        int64_t a = o->shard_off[g], b = o->shard_off[g + 1];
+    int64_t off[OR_MAX_SHARDS + 1];
+    int G = rs_parts(o, off);
+    for (int g = 0; g < G; ++g) {
+        int64_t a = off[g], b = off[g + 1];
         st[g] = shard_stats(o->w + a, b - a, wsmc_qbits((uint64_t)(b - a)));
     }
-    return wsmc_global_ess(st, o->nshards);
+    return wsmc_global_ess(st, G);
 }
 
 /* logsumexp(weights) - log(N) via the same fixed point (src/utils.jl:21) */
 double or_log_evidence(oracle* o) {
     or_stats st[OR_MAX_SHARDS];
-    for (int g = 0; g < o->nshards; ++g) {
-        int64_t a = o->shard_off[g], b = o->shard_off[g + 1];
+    int64_t off[OR_MAX_SHARDS + 1];
+    int G = rs_parts(o, off);
+    for (int g = 0; g < G; ++g) {
+        int64_t a = off[g], b = off[g + 1];
         st[g] = shard_stats(o->w + a, b - a, wsmc_qbits((uint64_t)(b - a)));
     }
-    return wsmc_global_log_evidence(st, o->nshards);
+    return wsmc_global_log_evidence(st, G);
 }
 
 /* ---- canonical reduction order (shared with the HIP moment kernels) -------- */

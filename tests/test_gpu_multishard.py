@@ -93,14 +93,17 @@ def test_two_shards_one_gpu_match_sharded_oracle(gpu_available, tmp_path, N, ess
 
 
 
-def _move_worker(rank, world, port, N, which, outdir):
+def _move_worker(rank, world, port, N, which, outdir, exact=False):
     sys.path[:0] = [str(REPO / "weightedsampling.jl_amd")]
     import wsmc
+    from wsmc import abi
     from wsmc.hostcomm import HostComm
     comm = HostComm(rank, world, "127.0.0.1", port, tag="mv", timeout=120)
     n = N // world
     c = wsmc.Context(n, seed=33, device=0)
     c.comm_init_host(comm.allgather, world, rank, rank * n, N)
+    if exact:
+        c.comm_set_shard_mode(abi.SHARD_EXACT)
     if which == "c3":
         xs, ys = wsmc.models.linreg_data()
         acc = wsmc.models.linreg_statements(c, xs[:6], ys[:6], ess_perc_min=1.0)
@@ -123,9 +126,11 @@ def _move_worker(rank, world, port, N, which, outdir):
     np.savez(os.path.join(outdir, f"mv{rank}.npz"), **out)
 
 
+@pytest.mark.parametrize("exact", [False, True])
 @pytest.mark.parametrize("which", ["c3", "c5"])
-def test_two_shards_moves_match_sharded_oracle(gpu_available, tmp_path, which):
-    """Sharded autoRW: global max, per-rank canonical moment totals combined in rank order."""
+def test_two_shards_moves_match_sharded_oracle(gpu_available, tmp_path, which, exact):
+    """Sharded autoRW: global max, per-rank canonical moment totals combined in rank order;
+    with exact sharding the Resamples are population-wide (the oracle's exact flag)."""
     import multiprocessing as mp
     sys.path.insert(0, str(REPO / "oracle"))
     from oracle import Oracle
@@ -133,7 +138,8 @@ def test_two_shards_moves_match_sharded_oracle(gpu_available, tmp_path, which):
     N, world = 6002, 2
     port = _free_port()
     ctx = mp.get_context("spawn")
-    ps = [ctx.Process(target=_move_worker, args=(r, world, port, N, which, str(tmp_path))) for r in range(world)]
+    ps = [ctx.Process(target=_move_worker, args=(r, world, port, N, which, str(tmp_path), exact))
+          for r in range(world)]
     for p in ps:
         p.start()
     for p in ps:
@@ -143,7 +149,7 @@ def test_two_shards_moves_match_sharded_oracle(gpu_available, tmp_path, which):
         if p.is_alive():
             p.kill()
     assert codes == [0] * world, codes
-    ref = Oracle(N, seed=33, shards=world)
+    ref = Oracle(N, seed=33, shards=world, exact=exact)
     if which == "c3":
         xs, ys = wsmc.models.linreg_data()
         acc = wsmc.models.linreg_statements(ref, xs[:6], ys[:6], ess_perc_min=1.0)

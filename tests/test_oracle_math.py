@@ -271,3 +271,18 @@ def test_multinomial_offspring_distribution():
     chi2 = float(np.sum((tot - e) ** 2 / e))
     # sum of N cells with expectation ~ N - 1, sd ~ sqrt(2N)
     assert abs(chi2 - (N - 1)) < 6 * math.sqrt(2 * N)
+
+
+def test_exact_shard_flag_is_the_single_population():
+    """The oracle's exact-sharding flag resamples the whole population: without moves it
+    is the unsharded run; island shards differ (their own Q and log-mean)."""
+    obs = wsmc.models.ssm2d_data(6)
+    runs = {}
+    for key, kw in (("one", {}), ("exact", {"shards": 2, "exact": True}), ("island", {"shards": 2})):
+        o = Oracle(3000, seed=4, **kw)
+        wsmc.models.ssm2d_statements(o, obs, ess_perc_min=1.0)
+        runs[key] = (o.weights_download(), o.last_ancestors(), o.log_evidence())
+    np.testing.assert_array_equal(runs["exact"][0], runs["one"][0])
+    np.testing.assert_array_equal(runs["exact"][1], runs["one"][1])
+    assert runs["exact"][2] == runs["one"][2]
+    assert not np.array_equal(runs["island"][1], runs["one"][1])
