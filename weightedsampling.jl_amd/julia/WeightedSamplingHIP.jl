@@ -27,7 +27,7 @@ const WS = WeightedSampling
 import WeightedSampling: nparticles, hascol, getcol, colnames, broadcast_setcol!, resample!, apply!,
     log_evidence
 
-export HipColumnStore, ssm2d_run!, sync_weights!, expectation, describe_device
+export HipColumnStore, ssm2d_run!, sync_weights!, expectation, describe_device, shard!, comm_unique_id
 
 const libwsmc = get(ENV, "WSMC_LIB", joinpath(@__DIR__, "..", "wsmc", "libwsmc.so"))
 
@@ -346,6 +346,25 @@ function log_evidence(state::HipState)
     v = Ref{Float64}(0.0)
     check(ccall((:wsmc_log_evidence, libwsmc), Cint, (Ptr{Cvoid}, Ptr{Float64}), state.store.ctx, v))
     return v[]
+end
+
+# multi-GPU: one process per GPU, each store a shard of one population (SURVEY §8(e)) ----
+"""RCCL unique id, created on rank 0 and broadcast by the caller (e.g. `MPI.bcast`)."""
+comm_unique_id() = (b = zeros(UInt8, 128); check(ccall((:wsmc_comm_unique_id, libwsmc), Cint, (Ptr{UInt8},), b)); b)
+
+"""
+    shard!(store, uid, world, rank, global_offset, global_n; exact=false)
+
+Join the RCCL communicator as shard `rank` of `global_n` particles. `exact=true` makes
+every Resample population-wide (`WSMC_SHARD_EXACT`: the single-GPU bits, particles move
+between ranks); the default is island resampling (one record all-gather per step).
+"""
+function shard!(s::HipColumnStore, uid::Vector{UInt8}, world::Integer, rank::Integer, goff::Integer,
+                gN::Integer; exact::Bool=false)
+    check(ccall((:wsmc_comm_init, libwsmc), Cint, (Ptr{Cvoid}, Ptr{UInt8}, Int32, Int32, Int64, Int64),
+                s.ctx, uid, world, rank, goff, gN))
+    exact && check(ccall((:wsmc_comm_set_shard_mode, libwsmc), Cint, (Ptr{Cvoid}, Int32), s.ctx, 1))
+    return s
 end
 
 # analysis reductions (src/utils.jl) on the device: no N-sized download ---------------------
