@@ -29,6 +29,12 @@ _SIG = {
     "or_destroy": (None, [_P]),
     "or_set_shards": (C.c_int, [_P, C.c_int32]),
     "or_set_shard_exact": (None, [_P, C.c_int32]),
+    "or_exact_record": (None, [_P, C.c_double, C.c_int64, C.POINTER(C.c_uint64)]),
+    "or_combine_records": (None, [C.POINTER(C.c_uint64), C.c_int32, C.POINTER(C.c_uint64)]),
+    "or_record_summary": (None, [C.POINTER(C.c_uint64), _D, _D, _D]),
+    "or_exact_window": (C.c_int, [_P, C.c_double, C.c_int64, C.c_uint64, C.c_uint64, C.c_int32, C.c_uint64,
+                                  _I32P, C.POINTER(C.c_uint64)]),
+    "or_set_resample_flags": (None, [_P, C.c_int32, C.c_int32, C.c_double]),
     "or_set_global_offset": (None, [_P, C.c_int64]),
     "or_shard_record": (None, [_P, C.POINTER(C.c_uint64)]),
     "or_resample_records": (C.c_int, [_P, C.c_double, C.c_int32, C.POINTER(C.c_uint64), C.c_int32, C.c_int32,
@@ -157,6 +163,39 @@ class Oracle:
                                               r.ctypes.data_as(C.POINTER(C.c_uint64)), len(r) // 8, int(rank),
                                               C.byref(rs), C.byref(e)))
         return bool(rs.value), float(e.value)
+
+    # ---- one shard of an exact-sharded run (the device ranks' protocol) ----
+    def exact_record(self, M: float, global_n: int) -> np.ndarray:
+        out = np.zeros(8, dtype=np.uint64)
+        self._L.or_exact_record(self._h, float(M), int(global_n), out.ctypes.data_as(C.POINTER(C.c_uint64)))
+        return out
+
+    @staticmethod
+    def combine_records(records) -> np.ndarray:
+        r = np.ascontiguousarray(np.asarray(records, dtype=np.uint64).reshape(-1))
+        out = np.zeros(8, dtype=np.uint64)
+        lib().or_combine_records(r.ctypes.data_as(C.POINTER(C.c_uint64)), len(r) // 8,
+                                 out.ctypes.data_as(C.POINTER(C.c_uint64)))
+        return out
+
+    @staticmethod
+    def record_summary(rec):
+        """(ESS%, post-resample log-mean, log-evidence) of one record."""
+        r = np.ascontiguousarray(np.asarray(rec, dtype=np.uint64))
+        e, m, v = C.c_double(), C.c_double(), C.c_double()
+        lib().or_record_summary(r.ctypes.data_as(C.POINTER(C.c_uint64)), C.byref(e), C.byref(m), C.byref(v))
+        return e.value, m.value, v.value
+
+    def exact_window(self, M: float, global_n: int, Q: int, cbase: int, scheme: int, op: int):
+        anc = np.zeros(int(global_n), dtype=np.int32)
+        ab = np.zeros(2, dtype=np.uint64)
+        self._L.or_exact_window(self._h, float(M), int(global_n), int(Q), int(cbase), int(scheme), int(op),
+                                anc.ctypes.data_as(_I32P), ab.ctypes.data_as(C.POINTER(C.c_uint64)))
+        a, b = int(ab[0]), int(ab[1])
+        return a, b, anc[:b - a].copy()
+
+    def set_resample_flags(self, resampled: bool, weights_changed: bool, last_ess: float) -> None:
+        self._L.or_set_resample_flags(self._h, int(resampled), int(weights_changed), float(last_ess))
 
     def close(self):
         if self._h:

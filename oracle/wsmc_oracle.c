@@ -366,6 +366,71 @@ int or_resample(oracle* o, double ess_min, int32_t scheme, int32_t* resampled_ou
     return 0;
 }
 
+/* ---- one shard of an exact-sharded run: the device ranks' protocol ----
+ * record of this shard's weights relative to a given (global) max, K from the global N */
+void or_exact_record(oracle* o, double M, int64_t gN, uint64_t* out) {
+    const int K = wsmc_qbits((uint64_t)gN);
+    uint64_t Q = 0, S1 = 0;
+    wsmc_u128 S2 = 0, Wf = 0;
+    for (int64_t i = 0; i < o->N; ++i) {
+        wsmc_qparts p = wsmc_qparts_of(o->w[i], M, K);
+        Q += p.q; S1 += p.q21; S2 += (wsmc_u128)p.q21 * p.q21; Wf += p.wf;
+    }
+    out[0] = wsmc_d2bits(M); out[1] = Q; out[2] = S1;
+    out[3] = (uint64_t)S2; out[4] = (uint64_t)(S2 >> 64);
+    out[5] = (uint64_t)Wf; out[6] = (uint64_t)(Wf >> 64);
+    out[7] = (uint64_t)o->N;
+}
+/* the records summed as integers: the single-population statistics */
+void or_combine_records(const uint64_t* recs, int32_t G, uint64_t* out) {
+    uint64_t Q = 0, S1 = 0, n = 0;
+    wsmc_u128 S2 = 0, Wf = 0;
+    for (int g = 0; g < G; ++g) {
+        const uint64_t* r = recs + 8 * g;
+        Q += r[1]; S1 += r[2];
+        S2 += ((wsmc_u128)r[4] << 64) | r[3];
+        Wf += ((wsmc_u128)r[6] << 64) | r[5];
+        n += r[7];
+    }
+    out[0] = recs[0]; out[1] = Q; out[2] = S1;
+    out[3] = (uint64_t)S2; out[4] = (uint64_t)(S2 >> 64);
+    out[5] = (uint64_t)Wf; out[6] = (uint64_t)(Wf >> 64);
+    out[7] = n;
+}
+/* ESS%, post-resample log-mean and log-evidence of one (combined) record */
+void or_record_summary(const uint64_t* rec, double* ess, double* mean, double* evidence) {
+    or_stats st;
+    st.M = wsmc_bits2d(rec[0]); st.Q = rec[1]; st.S1 = rec[2];
+    st.S2 = ((wsmc_u128)rec[4] << 64) | rec[3];
+    st.Wf = ((wsmc_u128)rec[6] << 64) | rec[5];
+    st.n = rec[7];
+    *ess = wsmc_global_ess(&st, 1);
+    *mean = wsmc_shard_mean(&st);
+    *evidence = wsmc_global_log_evidence(&st, 1);
+}
+/* this shard's window of global slots [a, b) and its ancestors (local ids): particle m owns
+ * [rank(C_{m-1}), rank(C_m)) of the global CDF (cbase + the local prefix) */
+int or_exact_window(oracle* o, double M, int64_t gN, uint64_t Q, uint64_t cbase, int32_t scheme, uint64_t op,
+                    int32_t* anc_out, uint64_t* ab) {
+    const int K = wsmc_qbits((uint64_t)gN);
+    uint64_t C = cbase;
+    const uint64_t a = wsmc_rank(C, Q, (uint64_t)gN, scheme, o->seed, op, 0);
+    uint64_t lo = a;
+    for (int64_t m = 0; m < o->N; ++m) {
+        C += wsmc_qweight(o->w[m], M, K);
+        const uint64_t hi = wsmc_rank(C, Q, (uint64_t)gN, scheme, o->seed, op, 0);
+        for (uint64_t sl = lo; sl < hi; ++sl) anc_out[sl - a] = (int32_t)m;
+        lo = hi;
+    }
+    ab[0] = a; ab[1] = lo;
+    return 0;
+}
+/* test hook: the flags a Resample leaves (an exchange driven from outside the oracle) */
+void or_set_resample_flags(oracle* o, int32_t resampled, int32_t weights_changed, double last_ess) {
+    o->resampled = resampled; o->weights_changed = weights_changed; o->last_ess = last_ess;
+    if (resampled) o->n_resamples += 1;
+}
+
 /* ---- one shard of a multi-process run: record exchange ------------------------------
  * record layout (8 x u64): M bits, Q, S1, S2 lo, S2 hi, Wf lo, Wf hi, n — the payload the GPU
  * ranks exchange with ncclAllGather each step (weightedsampling.jl_amd/csrc, ShardRec). */

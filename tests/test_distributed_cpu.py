@@ -8,7 +8,10 @@
 2. The sharded autoRW protocol: global max, per-rank canonical moment totals exchanged
    and combined in rank order, the factor on every rank, the move applied locally — the
    sequence libwsmc's sharded Move runs over RCCL.
-3. The torch-free TCP rendezvous bench.py ranks use (wsmc.hostcomm).
+3. Exact sharding: global max, integer record sums, the shard's window of global slots,
+   the particles moved to their owners — the device ranks' WSMC_SHARD_EXACT protocol.
+   Two gloo ranks must reproduce the unsharded oracle bit for bit.
+4. The torch-free TCP rendezvous bench.py ranks use (wsmc.hostcomm).
 """
 import os
 import pathlib
@@ -207,6 +210,119 @@ def test_sharded_autorw_protocol_gloo_world2(tmp_path, which):
             np.testing.assert_array_equal(p["c_" + name], ref.col_download(ref.col_find(name))[..., sl],
                                           err_msg=name)
         assert p["gate"][0] == 1
+
+
+class ExactShardCtx(ShardCtx):
+    """Context-protocol adapter: an oracle shard whose Resample / log_evidence follow the
+    exact-sharding protocol (include/wsmc.h WSMC_SHARD_EXACT)."""
+
+    def __init__(self, oracle, exchange, gather_obj, rank, world, goff, gN):
+        super().__init__(oracle, exchange, rank)
+        self.gather_obj, self.world, self.goff, self.gN = gather_obj, world, goff, gN
+        self.last_anc = np.zeros(oracle.n, dtype=np.int32)
+
+    def _records(self):
+        from oracle import Oracle
+        w = self.o.weights_download()
+        m = np.nan if np.isnan(w).any() else float(w.max())
+        ms = np.concatenate(self._allgather_f64(np.array([m])))
+        M = np.nan if np.isnan(ms).any() else float(ms.max())
+        recs = self.exchange(self.o.exact_record(M, self.gN))
+        return M, recs, Oracle.combine_records(np.stack(recs))
+
+    def log_evidence(self):
+        from oracle import Oracle
+        return Oracle.record_summary(self._records()[2])[2]
+
+    def last_ancestors(self):
+        return self.last_anc
+
+    def resample(self, ess_perc_min, scheme=0):
+        from oracle import Oracle
+        st = self.o.get_state()
+        op = st["op_counter"]
+        self.o.set_op_counter(op + 1)                       # a Resample consumes one op, even a no-op
+        if not st["weights_changed"]:
+            return bool(st["resampled"]), st["last_ess_perc"]
+        M, recs, comb = self._records()
+        ess, mean, _ = Oracle.record_summary(comb)
+        if not ess < ess_perc_min:
+            self.o.set_resample_flags(False, False, ess)
+            return False, ess
+        Q = int(comb[1])
+        cbase = sum(int(r[1]) for r in recs[:self.rank])
+        a, b, anc = self.o.exact_window(M, self.gN, Q, cbase, scheme, op)
+        names = self.o.col_names()
+        data = {nm: self.o.col_download(self.o.col_find(nm))[..., anc] for nm in names}
+        parts = self.gather_obj((a, b, data, self.goff + anc))
+        lo, hi = self.goff, self.goff + self.o.n
+        new = {nm: np.empty_like(self.o.col_download(self.o.col_find(nm))) for nm in names}
+        gid = np.empty(self.o.n, dtype=np.int64)
+        for pa, pb, pdata, pgid in parts:
+            s0, s1 = max(pa, lo), min(pb, hi)
+            if s1 <= s0:
+                continue
+            gid[s0 - lo:s1 - lo] = pgid[s0 - pa:s1 - pa]
+            for nm in names:
+                new[nm][..., s0 - lo:s1 - lo] = pdata[nm][..., s0 - pa:s1 - pa]
+        for nm in names:
+            self.o.col_upload(self.o.col_find(nm), new[nm])
+        self.o.weights_upload(np.full(self.o.n, mean))
+        self.o.set_resample_flags(True, False, ess)
+        self.last_anc = gid.astype(np.int32)
+        return True, ess
+
+
+def _exact_worker(rank, world, port, sizes, T, ess, scheme, outdir):
+    sys.path[:0] = [str(REPO / "weightedsampling.jl_amd"), str(REPO / "oracle")]
+    import torch
+    import torch.distributed as dist
+    from oracle import Oracle
+    import wsmc
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def exchange(rec):
+        t = torch.from_numpy(np.ascontiguousarray(rec).view(np.int64).copy())
+        out = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(out, t)
+        return [o.numpy().view(np.uint64) for o in out]
+
+    def gather_obj(obj):
+        out = [None] * world
+        dist.all_gather_object(out, obj)
+        return out
+
+    n, goff, N = sizes[rank], sum(sizes[:rank]), sum(sizes)
+    o = Oracle(n, seed=13, global_offset=goff)
+    ctx = ExactShardCtx(o, exchange, gather_obj, rank, world, goff, N)
+    flags = wsmc.models.ssm2d_statements(ctx, wsmc.models.ssm2d_data(T), ess_perc_min=ess, scheme=scheme)
+    ev = ctx.log_evidence()
+    cols = {name: o.col_download(o.col_find(name)) for name in o.col_names()}
+    np.savez(os.path.join(outdir, f"ex{rank}.npz"), w=o.weights_download(), flags=np.array(flags),
+             anc=ctx.last_ancestors(), ev=np.array([ev]), **{k.replace("_", "U"): v for k, v in cols.items()})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("sizes,ess,scheme", [((2048, 2048), 1.0, 0), ((3000, 1096), 0.5, 1)])
+def test_exact_protocol_gloo_world2(tmp_path, sizes, ess, scheme):
+    from oracle import Oracle
+    import wsmc
+    T, world = 8, len(sizes)
+    _spawn(_exact_worker, world, (world, _free_port(), sizes, T, ess, scheme, str(tmp_path)))
+    ref = Oracle(sum(sizes), seed=13)
+    flags = wsmc.models.ssm2d_statements(ref, wsmc.models.ssm2d_data(T), ess_perc_min=ess, scheme=scheme)
+    for r in range(world):
+        p = np.load(tmp_path / f"ex{r}.npz")
+        sl = slice(sum(sizes[:r]), sum(sizes[:r + 1]))
+        assert list(p["flags"]) == flags
+        np.testing.assert_array_equal(p["w"], ref.weights_download()[sl])
+        np.testing.assert_array_equal(p["anc"], ref.last_ancestors()[sl])
+        for name in ref.col_names():
+            np.testing.assert_array_equal(p[name.replace("_", "U")], ref.col_download(ref.col_find(name))[..., sl],
+                                          err_msg=name)
+        assert p["ev"][0] == ref.log_evidence()
 
 
 def _hostcomm_worker(rank, world, port, outdir):
