@@ -191,6 +191,14 @@ int wsmc_weighted_moments(wsmc_ctx* ctx, const wsmc_operand* exprs, int32_t d, d
 int wsmc_col_minmax(wsmc_ctx* ctx, int32_t col_id, int32_t comp, double* min_out, double* max_out);
 /* ess_perc(exp_norm(weights)) (src/resampling.jl:51-54) without resampling or any state change */
 int wsmc_ess(wsmc_ctx* ctx, double* ess_perc);
+/* sample(state, n; replace) (src/utils.jl:92-118): n particle indices (0-based) drawn by
+ * the normalised weights — with replacement independent draws in draw order, without
+ * replacement the n largest Efraimidis–Spirakis keys (include/wsmc_math.h wsmc_es_key).
+ * Consumes one op counter (the reference draws from the global RNG). WSMC_EARG for n <= 0
+ * or (!replace && n > N), as the reference's ArgumentError; single-shard contexts only. */
+int wsmc_sample_particles(wsmc_ctx* ctx, int64_t n, int32_t replace, int64_t* idx_out);
+/* rows idx[0..n) of a column, [dim][n] (getcol(store, c)[indices], src/utils.jl:117) */
+int wsmc_col_gather_rows(wsmc_ctx* ctx, int32_t col_id, const int64_t* idx, int64_t n, double* out);
 
 /* ---- operators (apply!) ------------------------------------------------------ */
 /* Assign: out[k] .= expr[k] for k < dim(out)            src/transformers.jl:28-32 */

@@ -509,9 +509,26 @@ WSMC_HD uint64_t wsmc_multi_e(uint64_t seed, uint64_t op, uint64_t slot_base, ui
     return k < n ? wsmc_multi_expo(wsmc_multi_word(seed, op, slot_base + k))
                  : wsmc_multi_expo(wsmc_multi_word(seed, ~op, slot_base));
 }
+/* floor(U Q / 2^64) in [0, Q): one independent draw on the integer CDF */
+WSMC_HD uint64_t wsmc_multi_target(uint64_t U, uint64_t Q) {
+    return (uint64_t)(((wsmc_u128)U * (wsmc_u128)Q) >> 64);
+}
 /* C_m > floor(Q P / PN)  <=>  Q P < C_m PN */
 WSMC_HD int wsmc_multi_above(uint64_t Cm, uint64_t Q, uint64_t P, uint64_t PN) {
     return (wsmc_u128)Q * (wsmc_u128)P < (wsmc_u128)Cm * (wsmc_u128)PN;
+}
+
+/*
+ * sample(state, n; replace) (src/utils.jl:92-118) on the integer weights q:
+ *  replace = true:  draw j is the smallest m with C_m > floor(U_j Q / 2^64), U_j a 64-bit
+ *                   word of (seed, op, j) — independent draws, in draw order;
+ *  replace = false: Efraimidis–Spirakis keys log(u_i) / q_i (u_i in (0, 1], a 53-bit word of
+ *                   (seed, op, i); -inf for q_i = 0), the n largest, ties to the lower index.
+ */
+WSMC_HD double wsmc_es_key(uint64_t seed, uint64_t op, uint64_t i, uint64_t q) {
+    if (q == 0) return -WSMC_INF;
+    const double u = wsmc_u64_to_d((wsmc_multi_word(seed, op, i) >> 11) + 1) * 1.1102230246251565e-16;
+    return wsmc_log(u) / wsmc_u64_to_d(q);
 }
 
 /* 4x4-max Cholesky of a symmetric matrix (row-major a[d*d]) -> lower L; 0 if not PD */

@@ -80,6 +80,8 @@ _SIG = {
     "or_weighted_moments": (C.c_int, [_P, C.c_void_p, C.c_int32, _D, _D]),
     "or_col_minmax": (C.c_int, [_P, C.c_int32, C.c_int32, _D, _D]),
     "or_ess": (C.c_double, [_P]),
+    "or_sample_particles": (C.c_int, [_P, C.c_int64, C.c_int32, C.POINTER(C.c_int64)]),
+    "or_es_key": (C.c_double, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64]),
     "or_exp": (C.c_double, [C.c_double]),
     "or_expw": (C.c_double, [C.c_double]),
     "or_log": (C.c_double, [C.c_double]),
@@ -268,6 +270,17 @@ class Oracle:
 
     def ess(self) -> float:
         return float(self._L.or_ess(self._h))
+
+    def sample_particles(self, n: int, replace: bool = True) -> np.ndarray:
+        out = np.zeros(max(int(n), 0), dtype=np.int64)
+        r = self._L.or_sample_particles(self._h, int(n), int(bool(replace)), out.ctypes.data_as(C.POINTER(C.c_int64)))
+        if r == 1:
+            raise ValueError("bad sample size")
+        self._chk(r)
+        return out
+
+    def col_gather_rows(self, col: int, idx) -> np.ndarray:
+        return self.col_download(col)[..., np.asarray(idx, dtype=np.int64)]
 
     def get_state(self) -> dict:
         L, h = self._L, self._h

@@ -366,6 +366,53 @@ int or_resample(oracle* o, double ess_min, int32_t scheme, int32_t* resampled_ou
     return 0;
 }
 
+/* ---- sample(state, n; replace) (src/utils.jl:92-118) ---------------------------------- */
+static uint64_t* g_sort_keys;   /* qsort context (single-threaded test infrastructure) */
+static int cmp_es(const void* a, const void* b) {
+    const int64_t i = *(const int64_t*)a, j = *(const int64_t*)b;
+    if (g_sort_keys[i] != g_sort_keys[j]) return g_sort_keys[i] > g_sort_keys[j] ? -1 : 1;   /* key desc */
+    return i < j ? -1 : (i > j);                                                           /* index asc */
+}
+double or_es_key(uint64_t seed, uint64_t op, uint64_t i, uint64_t q) { return wsmc_es_key(seed, op, i, q); }
+int or_sample_particles(oracle* o, int64_t n, int32_t replace, int64_t* out) {
+    const int64_t N = o->N;
+    if (n <= 0 || (!replace && n > N)) return WSMC_EARG;
+    const uint64_t op = o->op++;
+    or_stats st = shard_stats(o->w, N, wsmc_qbits((uint64_t)N));
+    if (st.Q == 0) return WSMC_ESTATE;                  /* exp_norm of these weights is NaN */
+    const int K = wsmc_qbits((uint64_t)N);
+    uint64_t* q = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)N);
+    for (int64_t i = 0; i < N; ++i) q[i] = wsmc_qweight(o->w[i], st.M, K);
+    if (replace) {
+        uint64_t* C = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)N);
+        uint64_t acc = 0;
+        for (int64_t i = 0; i < N; ++i) { acc += q[i]; C[i] = acc; }
+        for (int64_t j = 0; j < n; ++j) {
+            const uint64_t x = wsmc_multi_target(wsmc_multi_word(o->seed, op, (uint64_t)j), st.Q);
+            int64_t lo = 0, hi = N - 1;
+            while (lo < hi) {
+                const int64_t mid = lo + (hi - lo) / 2;
+                if (C[mid] > x) hi = mid; else lo = mid + 1;
+            }
+            out[j] = lo;
+        }
+        free(C);
+    } else {
+        uint64_t* keys = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)N);
+        int64_t* idx = (int64_t*)malloc(sizeof(int64_t) * (size_t)N);
+        for (int64_t i = 0; i < N; ++i) {
+            keys[i] = wsmc_ord_enc(wsmc_es_key(o->seed, op, (uint64_t)i, q[i]));
+            idx[i] = i;
+        }
+        g_sort_keys = keys;
+        qsort(idx, (size_t)N, sizeof(int64_t), cmp_es);
+        for (int64_t j = 0; j < n; ++j) out[j] = idx[j];
+        free(keys); free(idx);
+    }
+    free(q);
+    return 0;
+}
+
 /* ---- one shard of an exact-sharded run: the device ranks' protocol ----
  * record of this shard's weights relative to a given (global) max, K from the global N */
 void or_exact_record(oracle* o, double M, int64_t gN, uint64_t* out) {

@@ -783,6 +783,81 @@ int wsmc_ess(wsmc_ctx* c, double* ess_perc) {
     return WSMC_OK;
 }
 
+int wsmc_sample_particles(wsmc_ctx* c, int64_t n, int32_t replace, int64_t* idx_out) {
+    CHECK_CTX(c);
+    if (!idx_out) return fail(WSMC_EARG, "null output");
+    if (n <= 0) return fail(WSMC_EARG, "Number of samples must be positive");
+    if (!replace && n > c->N) return fail(WSMC_EARG, "Cannot sample more particles than N without replacement");
+    if (c->world > 1) return fail(WSMC_ESTATE, "sample() on sharded contexts is not supported");
+    const uint64_t op = c->op++;
+    // the integer weights relative to the max (and, with replacement, their CDF)
+    WSMC_HIP(hipMemsetAsync(c->mslots, 0, sizeof(MaxSlots), c->stream));
+    WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, c->mslots));
+    if (replace) {
+        if (ensure_cdf(c)) return WSMC_EHIP;
+        const FillPlan plan = fill_plan(c, WSMC_RESAMPLE_MULTINOMIAL, op, nullptr);
+        WSMC_HIP(launch_rs_sums_multi(c->stream, c->w, c->N, c->mslots, plan, c->tilep, c->cdf, multi_esum(c),
+                                      multi_ebuf(c)));
+    } else {
+        WSMC_HIP(launch_rs_sums(c->stream, c->w, c->N, c->mslots, c->tilep, c->qbuf));
+    }
+    WSMC_HIP(launch_rs_reduce(c->stream, c->mslots, c->tilep, c->N, c->tileOff, c->rec, 0, 0.0, nullptr, nullptr));
+    ShardRecord* hr = reinterpret_cast<ShardRecord*>(c->pinned);
+    WSMC_HIP(hipMemcpyAsync(hr, c->rec, sizeof(ShardRecord), hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    if (hr->Q == 0) return fail(WSMC_ESTATE, "the weights do not normalise (all -Inf or NaN)");
+    if (replace) {
+        int64_t* d = nullptr;
+        WSMC_HIP(hipMalloc(&d, sizeof(int64_t) * (size_t)n));
+        hipError_t e = launch_sample_draws(c->stream, n, c->N, c->rec, c->tileOff, c->cdf, c->seed, op, d);
+        if (e == hipSuccess) e = hipMemcpyAsync(idx_out, d, sizeof(int64_t) * n, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        (void)hipFree(d);
+        if (e != hipSuccess) return fail(WSMC_EHIP, std::string("sample: ") + hipGetErrorString(e));
+        return WSMC_OK;
+    }
+    // keys, then a stable descending radix sort of (key, index): the first n are the sample
+    unsigned long long* kin = reinterpret_cast<unsigned long long*>(c->tmp);
+    unsigned long long* kout = kin + c->N;
+    unsigned long long* vin = kout + c->N;
+    unsigned long long* vout = vin + c->N;
+    WSMC_HIP(launch_es_keys(c->stream, c->w, c->N, c->mslots, c->seed, op, kin, vin));
+    size_t tbytes = 0;
+    WSMC_HIP(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tbytes, kin, kout, vin, vout, (int)c->N, 0, 64,
+                                                          c->stream));
+    void* tstore = nullptr;
+    WSMC_HIP(hipMalloc(&tstore, tbytes + 16));
+    hipError_t e = hipcub::DeviceRadixSort::SortPairsDescending(tstore, tbytes, kin, kout, vin, vout, (int)c->N, 0, 64,
+                                                                c->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(idx_out, vout, sizeof(int64_t) * n, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(tstore);
+    if (e != hipSuccess) return fail(WSMC_EHIP, std::string("sample: ") + hipGetErrorString(e));
+    return WSMC_OK;
+}
+
+int wsmc_col_gather_rows(wsmc_ctx* c, int32_t col, const int64_t* idx, int64_t n, double* out) {
+    CHECK_CTX(c);
+    if (!valid_col(c, col) || !idx || !out || n < 0) return fail(WSMC_EARG, "bad arguments");
+    if (n == 0) return WSMC_OK;
+    for (int64_t j = 0; j < n; ++j)
+        if (idx[j] < 0 || idx[j] >= c->N) return fail(WSMC_EARG, "row index out of range");
+    const int dim = c->cols[col].dim;
+    int64_t* d = nullptr;
+    double* o = nullptr;
+    WSMC_HIP(hipMalloc(&d, sizeof(int64_t) * (size_t)n));
+    hipError_t e = hipMalloc(&o, sizeof(double) * (size_t)n * dim);
+    if (e == hipSuccess) e = hipMemcpyAsync(d, idx, sizeof(int64_t) * n, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = launch_gather_rows(c->stream, c->cols[col].front, c->N, dim, d, n, o);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, o, sizeof(double) * n * dim, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(d);
+    if (o) (void)hipFree(o);
+    if (e != hipSuccess) return fail(WSMC_EHIP, std::string("gather rows: ") + hipGetErrorString(e));
+    return WSMC_OK;
+}
+
 int wsmc_log_evidence(wsmc_ctx* c, double* out) {
     CHECK_CTX(c);
     if (!out) return fail(WSMC_EARG, "null out");

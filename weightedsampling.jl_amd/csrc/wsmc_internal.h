@@ -223,6 +223,14 @@ hipError_t launch_rs_reduce(hipStream_t s, const MaxSlots* ms, const unsigned lo
                             unsigned long long* esum = nullptr);
 hipError_t launch_rs_decide(hipStream_t s, const ShardRecord* recs, int world, int rank, double ess_min,
                             Decision* dec);
+// sample(state, n; replace): draws on the integer CDF / Efraimidis-Spirakis keys / row gather
+hipError_t launch_sample_draws(hipStream_t s, int64_t n, int64_t N, const ShardRecord* rec,
+                               const unsigned long long* tileOff, const unsigned long long* lcdf, uint64_t seed,
+                               uint64_t op, int64_t* out);
+hipError_t launch_es_keys(hipStream_t s, const double* w, int64_t N, const MaxSlots* ms, uint64_t seed, uint64_t op,
+                          unsigned long long* keys, unsigned long long* idx);
+hipError_t launch_gather_rows(hipStream_t s, const double* src, int64_t N, int dim, const int64_t* idx, int64_t n,
+                              double* out);
 // exact sharding: global max from the all-gathered per-rank maxima (words[world]) into ms
 hipError_t launch_max_adopt(hipStream_t s, const unsigned long long* words, int world, MaxSlots* ms);
 hipError_t launch_max_publish(hipStream_t s, const MaxSlots* ms, unsigned long long* word);

@@ -935,6 +935,50 @@ __global__ __launch_bounds__(kScanBlock) void k_multi_fill(int64_t N, const Shar
     }
 }
 
+// ---- sample(state, n; replace) (src/utils.jl:92-118; include/wsmc_math.h) -------------
+// with replacement: one independent draw per thread, located in the integer CDF
+__global__ __launch_bounds__(kBlock) void k_sample_draws(int64_t n, int64_t N, const ShardRecord* __restrict__ rec,
+                                                         const u64* __restrict__ tileOff,
+                                                         const u64* __restrict__ lcdf, uint64_t seed, uint64_t op,
+                                                         int64_t* __restrict__ out) {
+    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= n) return;
+    const u64 x = wsmc_multi_target(wsmc_multi_word(seed, op, (uint64_t)j), rec->Q);
+    const int64_t nt = (N + kRsTile - 1) / kRsTile;
+    int64_t lo = 0, hi = nt;                         // largest tile b with tileOff[b] <= x
+    while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (tileOff[mid] <= x) lo = mid; else hi = mid;
+    }
+    const u64 off = tileOff[lo];
+    int64_t m0 = lo * kRsTile, m1 = (m0 + kRsTile < N ? m0 + kRsTile : N) - 1;
+    while (m0 < m1) {                                // smallest m in the tile with C_m > x
+        const int64_t mid = (m0 + m1) >> 1;
+        if (off + lcdf[mid] > x) m1 = mid; else m0 = mid + 1;
+    }
+    out[j] = m0;
+}
+// without replacement: Efraimidis–Spirakis keys (ordered encoding) and indices to sort
+__global__ __launch_bounds__(kBlock) void k_es_keys(const double* __restrict__ w, int64_t N,
+                                                    const MaxSlots* __restrict__ ms, uint64_t seed, uint64_t op,
+                                                    u64* __restrict__ keys, u64* __restrict__ idx) {
+    const double M = wave_slots_max(ms);
+    const int K = wsmc_qbits((uint64_t)N);
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= N) return;
+    keys[i] = wsmc_ord_enc(wsmc_es_key(seed, op, (uint64_t)i, wsmc_qweight(w[i], M, K)));
+    idx[i] = (u64)i;
+}
+// rows of a column: out[k][j] = col[k][idx[j]]
+__global__ __launch_bounds__(kBlock) void k_gather_rows(const double* __restrict__ src, int64_t N, int dim,
+                                                        const int64_t* __restrict__ idx, int64_t n,
+                                                        double* __restrict__ out) {
+    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= n) return;
+    const int64_t i = idx[j];
+    for (int k = 0; k < dim; ++k) out[(int64_t)k * n + j] = src[(int64_t)k * N + i];
+}
+
 // ---- fused single-GPU resample: no reduce kernel ----------------------------------
 // block sum of two u64 values (all threads get the totals)
 __device__ __forceinline__ void block_sum2_u64(u64& a, u64& b, u64 (*lds)[2]) {
@@ -1584,6 +1628,23 @@ hipError_t launch_exact_unpack(hipStream_t s, const ExactRoute& rt, const u64* r
     if (!cnt) return hipSuccess;
     hipLaunchKernelGGL(k_exact_unpack, dim3((unsigned)((cnt + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rt,
                        recvbuf, dst, anc_local);
+    return hipGetLastError();
+}
+hipError_t launch_sample_draws(hipStream_t s, int64_t n, int64_t N, const ShardRecord* rec, const u64* tileOff,
+                               const u64* lcdf, uint64_t seed, uint64_t op, int64_t* out) {
+    hipLaunchKernelGGL(k_sample_draws, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n, N, rec,
+                       tileOff, lcdf, seed, op, out);
+    return hipGetLastError();
+}
+hipError_t launch_es_keys(hipStream_t s, const double* w, int64_t N, const MaxSlots* ms, uint64_t seed, uint64_t op,
+                          u64* keys, u64* idx) {
+    hipLaunchKernelGGL(k_es_keys, grid_for(N), dim3(kBlock), 0, s, w, N, ms, seed, op, keys, idx);
+    return hipGetLastError();
+}
+hipError_t launch_gather_rows(hipStream_t s, const double* src, int64_t N, int dim, const int64_t* idx, int64_t n,
+                              double* out) {
+    hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, src, N, dim,
+                       idx, n, out);
     return hipGetLastError();
 }
 // one block per tile (its first chunk) + grid-stride overflow blocks

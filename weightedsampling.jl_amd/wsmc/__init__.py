@@ -13,12 +13,12 @@ from .context import Context, device_count
 from .dsl import Col, Expr, HalfNormal, Kernel, MvNormal, Normal, Oscillator, Uniform
 from . import models
 from .transformers import (Assign, Cond, FusedSSM2D, HipColumnStore, ImportanceKernel, Loop, Move, Observe,
-                           Resample, RW, Sample, Sequence, SMCState, Weight, apply, autoRW, describe,
-                           expectation, importance_kernel, marginal_diversity, resampled, run, score_logpdf)
+                           Resample, RW, Sample, Sequence, SMCState, Weight, apply, autoRW, dataframe, describe,
+                           expectation, importance_kernel, marginal_diversity, resampled, run, sample, score_logpdf)
 
 __all__ = ["abi", "Context", "device_count", "Col", "Expr", "Kernel", "Normal", "MvNormal", "HalfNormal",
            "Uniform", "Oscillator", "models", "load_library", "WSMCError", "RESAMPLE_STRATIFIED",
            "RESAMPLE_SYSTEMATIC", "RESAMPLE_MULTINOMIAL", "PROPOSAL_RW", "PROPOSAL_AUTORW", "Assign", "Cond", "FusedSSM2D",
            "HipColumnStore", "ImportanceKernel", "Loop", "Move", "Observe", "Resample", "RW", "Sample", "Sequence",
            "SMCState", "Weight", "apply", "autoRW", "describe", "expectation", "importance_kernel", "marginal_diversity", "resampled", "run",
-           "score_logpdf"]
+           "score_logpdf", "sample", "dataframe"]

@@ -184,6 +184,22 @@ class Context:
         check(self._L.wsmc_ess(self._h, C.byref(v)))
         return float(v.value)
 
+    def sample_particles(self, n: int, replace: bool = True) -> np.ndarray:
+        """sample(state, n; replace) indices (0-based), src/utils.jl:92-118."""
+        out = np.zeros(max(int(n), 0), dtype=np.int64)
+        check(self._L.wsmc_sample_particles(self._h, int(n), int(bool(replace)),
+                                            out.ctypes.data_as(C.POINTER(C.c_int64))))
+        return out
+
+    def col_gather_rows(self, col: int, idx) -> np.ndarray:
+        """getcol(store, c)[idx] on the device: [n] (scalar column) or [dim][n]."""
+        ix = np.ascontiguousarray(np.asarray(idx, dtype=np.int64))
+        dim = self.col_dim(col)
+        out = np.zeros((dim, len(ix)))
+        check(self._L.wsmc_col_gather_rows(self._h, int(col), ix.ctypes.data_as(C.POINTER(C.c_int64)), len(ix),
+                                           _dptr(out)))
+        return out[0] if dim == 1 else out
+
     def get_state(self) -> dict:
         s = State()
         check(self._L.wsmc_get_state(self._h, C.byref(s)))

@@ -338,6 +338,29 @@ def expectation(state: SMCState, expr) -> float:
     return float(mean[0])
 
 
+def sample(state: SMCState, n: int, replace: bool = True) -> dict:
+    """StatsBase.sample(state, n; replace) (src/utils.jl:92-118): n particles drawn by the
+    normalised weights, one entry per column (``values[indices]``; vector columns [n, dim]).
+    The indices are drawn and the rows gathered on the device."""
+    idx = state.ctx.sample_particles(n, replace)
+    out = {}
+    for name in state.store.colnames():
+        v = state.ctx.col_gather_rows(state.store.resolve(name), idx)
+        out[name] = v if v.ndim == 1 else v.T
+    return out
+
+
+def dataframe(state: SMCState) -> dict:
+    """DataFrame(state) (src/utils.jl:69-88): every column plus ``log_weight`` (the raw
+    log-weights), unnormalised; a host copy of the whole population."""
+    out = {}
+    for name in state.store.colnames():
+        v = state.ctx.col_download(state.store.resolve(name))
+        out[name] = v if v.ndim == 1 else v.T
+    out["log_weight"] = state.ctx.weights_download()
+    return out
+
+
 def describe(state: SMCState, cols=None) -> list[dict]:
     """describe(state; cols) (src/utils.jl:157-289): per numeric column its weighted mean,
     weighted std (StatsBase, corrected=false), min, max and ESS = N * ess_perc; vector
