@@ -191,6 +191,11 @@ int wsmc_weighted_moments(wsmc_ctx* ctx, const wsmc_operand* exprs, int32_t d, d
 int wsmc_col_minmax(wsmc_ctx* ctx, int32_t col_id, int32_t comp, double* min_out, double* max_out);
 /* ess_perc(exp_norm(weights)) (src/resampling.jl:51-54) without resampling or any state change */
 int wsmc_ess(wsmc_ctx* ctx, double* ess_perc);
+/* describe()'s weighted median (StatsBase.quantile(v, Weights(w), 0.5)) and 8-bin sparkline
+ * histogram levels (1..8, src/utils.jl:134-141) of one column component, on the integer
+ * weights (include/wsmc_math.h); single-shard contexts only */
+int wsmc_weighted_median(wsmc_ctx* ctx, int32_t col_id, int32_t comp, double* out);
+int wsmc_histogram(wsmc_ctx* ctx, int32_t col_id, int32_t comp, int32_t levels[8]);
 /* sample(state, n; replace) (src/utils.jl:92-118): n particle indices (0-based) drawn by
  * the normalised weights — with replacement independent draws in draw order, without
  * replacement the n largest Efraimidis–Spirakis keys (include/wsmc_math.h wsmc_es_key).

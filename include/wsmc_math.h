@@ -531,6 +531,54 @@ WSMC_HD double wsmc_es_key(uint64_t seed, uint64_t op, uint64_t i, uint64_t q) {
     return wsmc_log(u) / wsmc_u64_to_d(q);
 }
 
+/*
+ * describe()'s weighted median and sparkline histogram (src/utils.jl:94-141, :233-240), on
+ * the integer weights q (exact sums, any order):
+ *  median = StatsBase.quantile(v, Weights(w), 0.5): zero weights dropped, pairs sorted by
+ *    (value, weight), h = (W - w1)/2 + w1 with w1 the first pair's weight; the first k with
+ *    S_k > h (in integers: 2 S_k > Q + q1); vkold + (h - S_{k-1}) / w_k * (vk - vkold);
+ *    no such k -> the largest value.
+ *  histogram: 8 bins on edges range(lo, hi, length = 9) (Julia's twice-precision range:
+ *    lo + k (hi - lo) / 8 rounded once, restated in double-double), bin =
+ *    clamp(searchsortedlast(edges, v), 1, 8); levels clamp(ceil(8 c_b / max c), 1, 8).
+ */
+WSMC_HD double wsmc_linspace_edge(double lo, double hi, int k, int n) {
+    if (k == 0) return lo;
+    if (k == n) return hi;
+    /* hi - lo = d + e exactly (TwoSum) */
+    const double d = hi - lo;
+    const double bb = d - hi;
+    const double e = (hi - (d - bb)) + (-lo - bb);
+    /* k (d + e) / n: k d exactly as p + pe (fma), then / n (n a power of two: exact) */
+    const double p = (double)k * d;
+    const double pe = __builtin_fma((double)k, d, -p);
+    const double inv = 1.0 / (double)n;
+    const double s_hi = p * inv, s_lo = (pe + (double)k * e) * inv;
+    /* lo + s_hi + s_lo, rounded once (TwoSum of lo + s_hi, then the tails) */
+    const double t = lo + s_hi;
+    const double tb = t - lo;
+    const double te = (lo - (t - tb)) + (s_hi - tb);
+    return t + (te + s_lo);
+}
+WSMC_HD int wsmc_hist_bin(double v, const double* edges, int nbins) {
+    int c = 0;                                   /* searchsortedlast: #edges <= v */
+    for (int k = 0; k <= nbins; ++k) c += edges[k] <= v;
+    return c < 1 ? 0 : (c > nbins ? nbins - 1 : c - 1);   /* 0-based, clamped */
+}
+WSMC_HD int wsmc_spark_level(uint64_t c, uint64_t maxc) {
+    if (maxc == 0) return 1;
+    const wsmc_u128 num = (wsmc_u128)c * 8u + (maxc - 1);
+    int l = (int)(num / maxc);
+    return l < 1 ? 1 : (l > 8 ? 8 : l);
+}
+/* the median's last step: vkold + (h - Skold) / (Sk - Skold) * (vk - vkold), with
+ * h - Skold = (Q + q1 - 2 Skold) / 2 */
+WSMC_HD double wsmc_median_interp(double vkold, double vk, uint64_t Q, uint64_t q1, uint64_t Skold, uint64_t wk) {
+    const wsmc_u128 num = (wsmc_u128)Q + q1 - 2 * (wsmc_u128)Skold;
+    const double f = wsmc_u128_to_d(num) / (2.0 * wsmc_u64_to_d(wk));
+    return vkold + f * (vk - vkold);
+}
+
 /* 4x4-max Cholesky of a symmetric matrix (row-major a[d*d]) -> lower L; 0 if not PD */
 WSMC_HD int wsmc_cholesky(const double* a, double* L, int d) {
     for (int i = 0; i < d * d; ++i) L[i] = 0.0;

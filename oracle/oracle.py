@@ -82,6 +82,8 @@ _SIG = {
     "or_ess": (C.c_double, [_P]),
     "or_sample_particles": (C.c_int, [_P, C.c_int64, C.c_int32, C.POINTER(C.c_int64)]),
     "or_es_key": (C.c_double, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64]),
+    "or_weighted_median": (C.c_int, [_P, C.c_int32, C.c_int32, _D]),
+    "or_histogram": (C.c_int, [_P, C.c_int32, C.c_int32, _I32P]),
     "or_exp": (C.c_double, [C.c_double]),
     "or_expw": (C.c_double, [C.c_double]),
     "or_log": (C.c_double, [C.c_double]),
@@ -281,6 +283,16 @@ class Oracle:
 
     def col_gather_rows(self, col: int, idx) -> np.ndarray:
         return self.col_download(col)[..., np.asarray(idx, dtype=np.int64)]
+
+    def weighted_median(self, col: int, comp: int = 0) -> float:
+        v = C.c_double()
+        self._chk(self._L.or_weighted_median(self._h, int(col), int(comp), C.byref(v)))
+        return float(v.value)
+
+    def histogram(self, col: int, comp: int = 0) -> np.ndarray:
+        lv = np.zeros(8, dtype=np.int32)
+        self._chk(self._L.or_histogram(self._h, int(col), int(comp), lv.ctypes.data_as(_I32P)))
+        return lv
 
     def get_state(self) -> dict:
         L, h = self._L, self._h

@@ -413,6 +413,80 @@ int or_sample_particles(oracle* o, int64_t n, int32_t replace, int64_t* out) {
     return 0;
 }
 
+/* ---- describe(): weighted median and sparkline histogram (src/utils.jl:94-141, :233-240) */
+typedef struct { uint64_t v; uint64_t q; } or_vq;
+static int cmp_vq(const void* a, const void* b) {
+    const or_vq *x = (const or_vq*)a, *y = (const or_vq*)b;
+    if (x->v != y->v) return x->v < y->v ? -1 : 1;     /* value (ordered encoding) asc */
+    return x->q < y->q ? -1 : (x->q > y->q);           /* then weight asc */
+}
+static uint64_t* or_qvec(oracle* o) {
+    or_stats st = shard_stats(o->w, o->N, wsmc_qbits((uint64_t)o->N));
+    const int K = wsmc_qbits((uint64_t)o->N);
+    uint64_t* q = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)o->N);
+    for (int64_t i = 0; i < o->N; ++i) q[i] = wsmc_qweight(o->w[i], st.M, K);
+    return q;
+}
+int or_weighted_median(oracle* o, int32_t col, int32_t comp, double* out) {
+    if (col < 0 || col >= o->ncols || comp < 0 || comp >= o->cols[col].dim) return WSMC_EARG;
+    const int64_t N = o->N;
+    const double* x = o->cols[col].front + (int64_t)comp * N;
+    for (int64_t i = 0; i < N; ++i)
+        if (wsmc_isnan(x[i])) { *out = x[i]; return 0; }     /* a NaN value: NaN */
+    uint64_t* q = or_qvec(o);
+    or_vq* a = (or_vq*)malloc(sizeof(or_vq) * (size_t)(N > 0 ? N : 1));
+    int64_t n = 0;
+    uint64_t Q = 0;
+    for (int64_t i = 0; i < N; ++i)
+        if (q[i]) { a[n].v = wsmc_ord_enc(x[i]); a[n].q = q[i]; Q += q[i]; ++n; }   /* zero weights dropped */
+    free(q);
+    if (n == 0) { free(a); return WSMC_ESTATE; }       /* weights cannot sum to zero */
+    qsort(a, (size_t)n, sizeof(or_vq), cmp_vq);
+    const uint64_t q1 = a[0].q;
+    const wsmc_u128 H2 = (wsmc_u128)Q + q1;             /* 2 h */
+    uint64_t Sk = 0, Skold = 0;
+    double vk = 0.0, vkold = 0.0;
+    int64_t k = 0;
+    *out = wsmc_ord_dec(a[n - 1].v);                    /* the largest value */
+    while (2 * (wsmc_u128)Sk <= H2) {
+        if (k == n) { free(a); return 0; }
+        Skold = Sk; vkold = vk;
+        vk = wsmc_ord_dec(a[k].v);
+        Sk += a[k].q;
+        ++k;
+    }
+    *out = wsmc_median_interp(vkold, vk, Q, q1, Skold, a[k - 1].q);
+    free(a);
+    return 0;
+}
+int or_histogram(oracle* o, int32_t col, int32_t comp, int32_t* levels) {
+    if (col < 0 || col >= o->ncols || comp < 0 || comp >= o->cols[col].dim) return WSMC_EARG;
+    const int64_t N = o->N;
+    const double* x = o->cols[col].front + (int64_t)comp * N;
+    double lo = WSMC_INF, hi = -WSMC_INF;
+    int nan = 0;
+    for (int64_t i = 0; i < N; ++i) {
+        if (wsmc_isnan(x[i])) nan = 1;
+        if (x[i] < lo) lo = x[i];
+        if (x[i] > hi) hi = x[i];
+    }
+    if (nan) lo = hi = WSMC_NAN;                        /* extrema propagate NaN: every value in bin 1 */
+    if (lo == hi) { for (int b = 0; b < 8; ++b) levels[b] = 8; return 0; }
+    double edges[9];
+    for (int k = 0; k <= 8; ++k) edges[k] = wsmc_linspace_edge(lo, hi, k, 8);
+    uint64_t* q = or_qvec(o);
+    uint64_t Qs = 0;
+    for (int64_t i = 0; i < N; ++i) Qs += q[i];
+    if (Qs == 0) { free(q); return WSMC_ESTATE; }       /* the weights do not normalise */
+    uint64_t cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int64_t i = 0; i < N; ++i) cnt[wsmc_hist_bin(x[i], edges, 8)] += q[i];
+    free(q);
+    uint64_t mx = 0;
+    for (int b = 0; b < 8; ++b) mx = cnt[b] > mx ? cnt[b] : mx;
+    for (int b = 0; b < 8; ++b) levels[b] = wsmc_spark_level(cnt[b], mx);
+    return 0;
+}
+
 /* ---- one shard of an exact-sharded run: the device ranks' protocol ----
  * record of this shard's weights relative to a given (global) max, K from the global N */
 void or_exact_record(oracle* o, double M, int64_t gN, uint64_t* out) {

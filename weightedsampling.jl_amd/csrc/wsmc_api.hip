@@ -759,6 +759,88 @@ int wsmc_col_minmax(wsmc_ctx* c, int32_t col, int32_t comp, double* mn, double* 
     return WSMC_OK;
 }
 
+// integer weights q of the current log-weights into qbuf; their total (0: not normalisable)
+static int local_q(wsmc_ctx* c, unsigned long long* Q) {
+    WSMC_HIP(hipMemsetAsync(c->mslots, 0, sizeof(MaxSlots), c->stream));
+    WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, c->mslots));
+    WSMC_HIP(launch_rs_sums(c->stream, c->w, c->N, c->mslots, c->tilep, c->qbuf));
+    WSMC_HIP(launch_rs_reduce(c->stream, c->mslots, c->tilep, c->N, c->tileOff, c->rec, 0, 0.0, nullptr, nullptr));
+    ShardRecord* hr = reinterpret_cast<ShardRecord*>(c->pinned);
+    WSMC_HIP(hipMemcpyAsync(hr, c->rec, sizeof(ShardRecord), hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    *Q = hr->Q;
+    return WSMC_OK;
+}
+
+int wsmc_weighted_median(wsmc_ctx* c, int32_t col, int32_t comp, double* out) {
+    CHECK_CTX(c);
+    if (!out) return fail(WSMC_EARG, "null output");
+    if (c->world > 1) return fail(WSMC_ESTATE, "analysis reductions on sharded contexts are not supported yet");
+    double mn, mx;
+    int r = wsmc_col_minmax(c, col, comp, &mn, &mx);
+    if (r) return r;
+    if (wsmc_isnan(mx)) { *out = mx; return WSMC_OK; }          // a NaN value: NaN (StatsBase)
+    unsigned long long Q = 0;
+    if ((r = local_q(c, &Q))) return r;
+    if (Q == 0) return fail(WSMC_ESTATE, "weight vector cannot sum to zero");
+    const int64_t N = c->N;
+    unsigned long long* kin = reinterpret_cast<unsigned long long*>(c->tmp);
+    unsigned long long* kout = kin + N;
+    unsigned long long* vin = kout + N;
+    unsigned long long* vout = vin + N;
+    WSMC_HIP(launch_median_keys(c->stream, c->cols[col].front + (int64_t)comp * N, c->qbuf, N, kin, vin));
+    // (value, weight) order: stable radix sorts by weight, then by value
+    size_t tb1 = 0, tb2 = 0;
+    WSMC_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb1, kin, kout, vin, vout, (int)N, 0, 64, c->stream));
+    WSMC_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tb2, vin, kout, (int)N, c->stream));
+    const size_t tb = (tb1 > tb2 ? tb1 : tb2) + 16;
+    void* ts = nullptr;
+    double* dout = nullptr;
+    WSMC_HIP(hipMalloc(&ts, tb));
+    hipError_t e = hipMalloc(&dout, sizeof(double));
+    size_t t = tb;
+    if (e == hipSuccess) e = hipcub::DeviceRadixSort::SortPairs(ts, t, kin, kout, vin, vout, (int)N, 0, 64, c->stream);
+    t = tb;
+    if (e == hipSuccess) e = hipcub::DeviceRadixSort::SortPairs(ts, t, vout, kin, kout, vin, (int)N, 0, 64, c->stream);
+    t = tb;
+    if (e == hipSuccess) e = hipcub::DeviceScan::InclusiveSum(ts, t, vin, kout, (int)N, c->stream);
+    if (e == hipSuccess) e = launch_median_pick(c->stream, kin, vin, kout, N, dout);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, dout, sizeof(double), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(ts);
+    if (dout) (void)hipFree(dout);
+    if (e != hipSuccess) return fail(WSMC_EHIP, std::string("weighted median: ") + hipGetErrorString(e));
+    return WSMC_OK;
+}
+
+int wsmc_histogram(wsmc_ctx* c, int32_t col, int32_t comp, int32_t levels[8]) {
+    CHECK_CTX(c);
+    if (!levels) return fail(WSMC_EARG, "null output");
+    if (c->world > 1) return fail(WSMC_ESTATE, "analysis reductions on sharded contexts are not supported yet");
+    double lo, hi;
+    int r = wsmc_col_minmax(c, col, comp, &lo, &hi);
+    if (r) return r;
+    if (lo == hi) {                                                // _sparkline(fill(sum(w), 8))
+        for (int b = 0; b < 8; ++b) levels[b] = 8;
+        return WSMC_OK;
+    }
+    unsigned long long Q = 0;
+    if ((r = local_q(c, &Q))) return r;
+    if (Q == 0) return fail(WSMC_ESTATE, "the weights do not normalise (all -Inf or NaN)");
+    double edges[9];
+    for (int k = 0; k <= 8; ++k) edges[k] = wsmc_linspace_edge(lo, hi, k, 8);
+    unsigned long long* cnt = c->xchg;
+    WSMC_HIP(hipMemsetAsync(cnt, 0, sizeof(unsigned long long) * 8, c->stream));
+    WSMC_HIP(launch_hist(c->stream, c->cols[col].front + (int64_t)comp * c->N, c->qbuf, c->N, edges, cnt));
+    unsigned long long h[8];
+    WSMC_HIP(hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    unsigned long long mxc = 0;
+    for (int b = 0; b < 8; ++b) mxc = h[b] > mxc ? h[b] : mxc;
+    for (int b = 0; b < 8; ++b) levels[b] = wsmc_spark_level(h[b], mxc);
+    return WSMC_OK;
+}
+
 int wsmc_ess(wsmc_ctx* c, double* ess_perc) {
     CHECK_CTX(c);
     if (!ess_perc) return fail(WSMC_EARG, "null output");

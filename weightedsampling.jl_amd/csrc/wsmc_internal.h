@@ -223,6 +223,13 @@ hipError_t launch_rs_reduce(hipStream_t s, const MaxSlots* ms, const unsigned lo
                             unsigned long long* esum = nullptr);
 hipError_t launch_rs_decide(hipStream_t s, const ShardRecord* recs, int world, int rank, double ess_min,
                             Decision* dec);
+// describe(): median sort keys, the StatsBase walk on the sorted prefix, histogram counts
+hipError_t launch_median_keys(hipStream_t s, const double* x, const unsigned long long* q, int64_t N,
+                              unsigned long long* kq, unsigned long long* kv);
+hipError_t launch_median_pick(hipStream_t s, const unsigned long long* v, const unsigned long long* q,
+                              const unsigned long long* S, int64_t N, double* out);
+hipError_t launch_hist(hipStream_t s, const double* x, const unsigned long long* q, int64_t N, const double* edges,
+                       unsigned long long* cnt);
 // sample(state, n; replace): draws on the integer CDF / Efraimidis-Spirakis keys / row gather
 hipError_t launch_sample_draws(hipStream_t s, int64_t n, int64_t N, const ShardRecord* rec,
                                const unsigned long long* tileOff, const unsigned long long* lcdf, uint64_t seed,

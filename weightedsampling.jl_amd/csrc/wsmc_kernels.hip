@@ -979,6 +979,58 @@ __global__ __launch_bounds__(kBlock) void k_gather_rows(const double* __restrict
     for (int k = 0; k < dim; ++k) out[(int64_t)k * n + j] = src[(int64_t)k * N + i];
 }
 
+// ---- describe(): weighted median / histogram (include/wsmc_math.h) --------------------
+__global__ __launch_bounds__(kBlock) void k_median_keys(const double* __restrict__ x, const u64* __restrict__ q,
+                                                        int64_t N, u64* __restrict__ kq, u64* __restrict__ kv) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= N) return;
+    kq[i] = q[i];
+    kv[i] = wsmc_ord_enc(x[i]);
+}
+// first index in [0, N) with S[i] >= t (S non-decreasing); N if none
+__device__ int64_t lower_bound_u64(const u64* S, int64_t N, u64 t) {
+    int64_t lo = 0, hi = N;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (S[mid] >= t) hi = mid; else lo = mid + 1;
+    }
+    return lo;
+}
+// sorted (value, q) pairs + inclusive prefix S of q: StatsBase's walk by binary search
+__global__ void k_median_pick(const u64* __restrict__ v, const u64* __restrict__ q, const u64* __restrict__ S,
+                              int64_t N, double* out) {
+    if (threadIdx.x != 0) return;
+    const u64 Q = S[N - 1];
+    const int64_t i1 = lower_bound_u64(S, N, 1);                 // the first nonzero weight
+    const u64 q1 = q[i1];
+    const wsmc_u128 H2 = (wsmc_u128)Q + q1;                       // 2 h
+    int64_t lo = 0, hi = N;                                       // first k with 2 S_k > 2 h
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (2 * (wsmc_u128)S[mid] > H2) hi = mid; else lo = mid + 1;
+    }
+    if (lo == N) {                                                // h beyond the total: the largest value
+        *out = wsmc_ord_dec(v[lower_bound_u64(S, N, Q)]);
+        return;
+    }
+    const u64 wk = q[lo], Skold = S[lo] - wk;
+    const double vkold = Skold ? wsmc_ord_dec(v[lower_bound_u64(S, N, Skold)]) : 0.0;
+    *out = wsmc_median_interp(vkold, wsmc_ord_dec(v[lo]), Q, q1, Skold, wk);
+}
+struct HistEdges { double e[9]; };
+__global__ __launch_bounds__(kBlock) void k_hist(const double* __restrict__ x, const u64* __restrict__ q, int64_t N,
+                                                 HistEdges ed, u64* __restrict__ cnt) {
+    __shared__ u64 s_c[8];
+    if (threadIdx.x < 8) s_c[threadIdx.x] = 0;
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < N; i += (int64_t)gridDim.x * kBlock) {
+        const u64 w = q[i];
+        if (w) atomicAdd(&s_c[wsmc_hist_bin(x[i], ed.e, 8)], w);   // integers: order-free
+    }
+    __syncthreads();
+    if (threadIdx.x < 8 && s_c[threadIdx.x]) atomicAdd(&cnt[threadIdx.x], s_c[threadIdx.x]);
+}
+
 // ---- fused single-GPU resample: no reduce kernel ----------------------------------
 // block sum of two u64 values (all threads get the totals)
 __device__ __forceinline__ void block_sum2_u64(u64& a, u64& b, u64 (*lds)[2]) {
@@ -1645,6 +1697,22 @@ hipError_t launch_gather_rows(hipStream_t s, const double* src, int64_t N, int d
                               double* out) {
     hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, src, N, dim,
                        idx, n, out);
+    return hipGetLastError();
+}
+hipError_t launch_median_keys(hipStream_t s, const double* x, const u64* q, int64_t N, u64* kq, u64* kv) {
+    hipLaunchKernelGGL(k_median_keys, grid_for(N), dim3(kBlock), 0, s, x, q, N, kq, kv);
+    return hipGetLastError();
+}
+hipError_t launch_median_pick(hipStream_t s, const u64* v, const u64* q, const u64* S, int64_t N, double* out) {
+    hipLaunchKernelGGL(k_median_pick, dim3(1), dim3(64), 0, s, v, q, S, N, out);
+    return hipGetLastError();
+}
+hipError_t launch_hist(hipStream_t s, const double* x, const u64* q, int64_t N, const double* edges, u64* cnt) {
+    HistEdges ed;
+    for (int k = 0; k < 9; ++k) ed.e[k] = edges[k];
+    int64_t nb = (N + kBlock - 1) / kBlock;
+    if (nb > 2048) nb = 2048;
+    hipLaunchKernelGGL(k_hist, dim3((unsigned)nb), dim3(kBlock), 0, s, x, q, N, ed, cnt);
     return hipGetLastError();
 }
 // one block per tile (its first chunk) + grid-stride overflow blocks

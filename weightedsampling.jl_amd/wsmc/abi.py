@@ -100,6 +100,8 @@ SIGNATURES = {
     "wsmc_weighted_moments": (C.c_int, [_P, C.POINTER(Operand), C.c_int32, _D, _D]),
     "wsmc_col_minmax": (C.c_int, [_P, C.c_int32, C.c_int32, _D, _D]),
     "wsmc_ess": (C.c_int, [_P, _D]),
+    "wsmc_weighted_median": (C.c_int, [_P, C.c_int32, C.c_int32, _D]),
+    "wsmc_histogram": (C.c_int, [_P, C.c_int32, C.c_int32, C.POINTER(C.c_int32)]),
     "wsmc_sample_particles": (C.c_int, [_P, C.c_int64, C.c_int32, C.POINTER(C.c_int64)]),
     "wsmc_col_gather_rows": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_int64), C.c_int64, _D]),
     "wsmc_assign": (C.c_int, [_P, C.c_int32, C.POINTER(Operand)]),

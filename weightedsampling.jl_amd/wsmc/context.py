@@ -184,6 +184,18 @@ class Context:
         check(self._L.wsmc_ess(self._h, C.byref(v)))
         return float(v.value)
 
+    def weighted_median(self, col: int, comp: int = 0) -> float:
+        """StatsBase.quantile(v, Weights(w), 0.5) of a column component (describe's median)."""
+        v = C.c_double()
+        check(self._L.wsmc_weighted_median(self._h, int(col), int(comp), C.byref(v)))
+        return float(v.value)
+
+    def histogram(self, col: int, comp: int = 0) -> np.ndarray:
+        """describe's 8-bin weighted sparkline as levels 1..8 (src/utils.jl:120-141)."""
+        lv = np.zeros(8, dtype=np.int32)
+        check(self._L.wsmc_histogram(self._h, int(col), int(comp), lv.ctypes.data_as(C.POINTER(C.c_int32))))
+        return lv
+
     def sample_particles(self, n: int, replace: bool = True) -> np.ndarray:
         """sample(state, n; replace) indices (0-based), src/utils.jl:92-118."""
         out = np.zeros(max(int(n), 0), dtype=np.int64)

@@ -361,11 +361,15 @@ def dataframe(state: SMCState) -> dict:
     return out
 
 
+SPARK_CHARS = "▁▂▃▄▅▆▇█"
+
+
 def describe(state: SMCState, cols=None) -> list[dict]:
     """describe(state; cols) (src/utils.jl:157-289): per numeric column its weighted mean,
-    weighted std (StatsBase, corrected=false), min, max and ESS = N * ess_perc; vector
-    columns component-wise. The weighted median and the sparkline histogram need a sort or
-    a histogram pass and are not computed on the device (median/hist are None)."""
+    weighted median (StatsBase quantile 0.5), weighted std (StatsBase, corrected=false), min,
+    max, the 8-bin weighted sparkline (scalar columns; "" for vector columns) and
+    ESS = N * ess_perc; vector columns component-wise. Everything is reduced on the device
+    (the median and histogram on the integer weights, include/wsmc_math.h)."""
     store = state.store
     names = store.colnames() if cols is None else list(cols)
     for n in names:
@@ -376,7 +380,7 @@ def describe(state: SMCState, cols=None) -> list[dict]:
     for n in names:
         c = store.resolve(n)
         d = state.ctx.col_dim(c)
-        means, stds, mins, maxs = [], [], [], []
+        means, stds, mins, maxs, meds = [], [], [], [], []
         for k0 in range(0, d, 4):
             ks = list(range(k0, min(d, k0 + 4)))
             mean, cov = state.ctx.weighted_moments([Operand.column(c, k) for k in ks])
@@ -386,10 +390,12 @@ def describe(state: SMCState, cols=None) -> list[dict]:
             mn, mx = state.ctx.col_minmax(c, k)
             mins.append(mn)
             maxs.append(mx)
+            meds.append(state.ctx.weighted_median(c, k))
         one = d == 1
-        rows.append(dict(variable=n, mean=means[0] if one else means, median=None,
+        hist = "".join(SPARK_CHARS[v - 1] for v in state.ctx.histogram(c, 0)) if one else ""
+        rows.append(dict(variable=n, mean=means[0] if one else means, median=meds[0] if one else meds,
                          std=stds[0] if one else stds, min=mins[0] if one else mins,
-                         max=maxs[0] if one else maxs, hist=None, ess=ess))
+                         max=maxs[0] if one else maxs, hist=hist, ess=ess))
     return rows
 
 
