@@ -27,7 +27,8 @@ const WS = WeightedSampling
 import WeightedSampling: nparticles, hascol, getcol, colnames, broadcast_setcol!, resample!, apply!,
     log_evidence
 
-export HipColumnStore, ssm2d_run!, sync_weights!, expectation, describe_device, shard!, comm_unique_id
+export HipColumnStore, ssm2d_run!, sync_weights!, expectation, describe_device, sample_device, shard!,
+       comm_unique_id
 
 const libwsmc = get(ENV, "WSMC_LIB", joinpath(@__DIR__, "..", "wsmc", "libwsmc.so"))
 
@@ -348,6 +349,29 @@ function log_evidence(state::HipState)
     return v[]
 end
 
+const SPARK = ['▁', '▂', '▃', '▄', '▅', '▆', '▇', '█']
+
+"""
+    sample_device(state, n; replace=true) -> Dict{Symbol,Any}
+
+`sample(state, n; replace)` (src/utils.jl:92-118): indices drawn and rows gathered on the
+device; one entry per column (vector columns as a dim x n matrix).
+"""
+function sample_device(state::HipState, n::Integer; replace::Bool=true)
+    s = state.store
+    idx = zeros(Int64, n)
+    check(ccall((:wsmc_sample_particles, libwsmc), Cint, (Ptr{Cvoid}, Int64, Int32, Ptr{Int64}),
+                s.ctx, n, Int32(replace), idx))
+    out = Dict{Symbol,Any}()
+    for (name, id) in s.ids
+        buf = Vector{Float64}(undef, s.dims[name] * n)
+        check(ccall((:wsmc_col_gather_rows, libwsmc), Cint, (Ptr{Cvoid}, Int32, Ptr{Int64}, Int64, Ptr{Float64}),
+                    s.ctx, id, idx, n, buf))
+        out[name] = s.dims[name] == 1 ? buf : permutedims(reshape(buf, n, s.dims[name]))
+    end
+    return out
+end
+
 # multi-GPU: one process per GPU, each store a shard of one population (SURVEY §8(e)) ----
 """RCCL unique id, created on rank 0 and broadcast by the caller (e.g. `MPI.bcast`)."""
 comm_unique_id() = (b = zeros(UInt8, 128); check(ccall((:wsmc_comm_unique_id, libwsmc), Cint, (Ptr{UInt8},), b)); b)
@@ -400,7 +424,7 @@ function describe_device(state::HipState; cols=collect(keys(state.store.ids)))
     for name in cols
         haskey(s.ids, name) || throw(ArgumentError("Column $name not found in store"))
         id, d = s.ids[name], s.dims[name]
-        μ, σ, lo, hi = Float64[], Float64[], Float64[], Float64[]
+        μ, σ, lo, hi, med = Float64[], Float64[], Float64[], Float64[], Float64[]
         for k in 0:d-1
             op = WsmcOperand(0.0, (id, Int32(-1)), (Int32(k), Int32(0)), (1.0, 0.0))
             m, v = Ref{Float64}(0.0), Ref{Float64}(0.0)
@@ -409,10 +433,20 @@ function describe_device(state::HipState; cols=collect(keys(state.store.ids)))
             a, b = Ref{Float64}(0.0), Ref{Float64}(0.0)
             check(ccall((:wsmc_col_minmax, libwsmc), Cint, (Ptr{Cvoid}, Int32, Int32, Ptr{Float64}, Ptr{Float64}),
                         s.ctx, id, Int32(k), a, b))
-            push!(μ, m[]); push!(σ, sqrt(v[])); push!(lo, a[]); push!(hi, b[])
+            md = Ref{Float64}(0.0)
+            check(ccall((:wsmc_weighted_median, libwsmc), Cint, (Ptr{Cvoid}, Int32, Int32, Ptr{Float64}),
+                        s.ctx, id, Int32(k), md))
+            push!(μ, m[]); push!(σ, sqrt(v[])); push!(lo, a[]); push!(hi, b[]); push!(med, md[])
+        end
+        hist = ""
+        if d == 1
+            lv = zeros(Int32, 8)
+            check(ccall((:wsmc_histogram, libwsmc), Cint, (Ptr{Cvoid}, Int32, Int32, Ptr{Int32}), s.ctx, id, 0, lv))
+            hist = join(SPARK[l] for l in lv)
         end
         pick(x) = d == 1 ? x[1] : x
-        push!(rows, (variable=name, mean=pick(μ), std=pick(σ), min=pick(lo), max=pick(hi), ess=s.n * essp[]))
+        push!(rows, (variable=name, mean=pick(μ), median=pick(med), std=pick(σ), min=pick(lo), max=pick(hi),
+                     hist=hist, ess=s.n * essp[]))
     end
     return rows
 end
