@@ -230,7 +230,7 @@ int wsmc_destroy(wsmc_ctx* c) {
     }
     void* bufs[] = {c->xchg, c->scache, c->scache_back, c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->cdf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount,
                     c->d_colptr, c->run_params, c->d_tape, c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp,
-                    c->vscratch, c->xscratch, c->run_pay, c->xp, c->comb, c->anc_out, c->xbuf, c->d_comp};
+                    c->vscratch, c->xscratch, c->run_pay, c->xp, c->comb, c->anc_out, c->xbuf, c->d_comp, c->d_ctape};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     if (c->pinned) (void)hipHostFree(c->pinned);
@@ -1305,11 +1305,54 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         WSMC_HIP(hipMalloc(&c->scache_back, sizeof(double) * c->N));
     }
     const int32_t cache_from = (c->scache_terms >= 0 && c->scache_terms <= kD) ? c->scache_terms : -1;
-    WSMC_HIP(launch_move(c->stream, c->d_tape, (int32_t)c->tape.size(), target_depth, c->d_colptr, targets, d,
-                         bounded ? l : nullptr, bounded ? h : nullptr, bounded ? 1 : 0, c->mom + 32, c->seed,
-                         op_prop, op_acc, c->goff, c->N, c->ucount,
-                         (proposal == WSMC_PROPOSAL_AUTORW && c->world == 1) ? c->dflag : nullptr, c->scache,
-                         cache_from));
+    // compile the fold's tape prefix: every (column, component) it reads becomes a slot
+    // (targets first); > kFoldSlots distinct reads keep the generic interpreter
+    std::vector<std::pair<int32_t, int32_t>> slots;
+    auto slot_of = [&](int32_t col, int32_t comp) -> int32_t {
+        for (size_t s = 0; s < slots.size(); ++s)
+            if (slots[s].first == col && slots[s].second == comp) return (int32_t)s;
+        slots.emplace_back(col, comp);
+        return (int32_t)slots.size() - 1;
+    };
+    for (int k = 0; k < d; ++k) slot_of(targets[k], 0);
+    std::vector<wsmc_term> ct(c->tape.begin(), c->tape.begin() + kD);
+    auto remap = [&](wsmc_operand& o) {
+        for (int k = 0; k < 2; ++k)
+            if (o.col[k] >= 0) {
+                o.col[k] = slot_of(o.col[k], o.comp[k]);
+                o.comp[k] = 0;
+            }
+    };
+    for (auto& t : ct) {
+        for (int k = 0; k < 4; ++k) { remap(t.x[k]); remap(t.dist.mu[k]); }
+        remap(t.dist.scale);
+    }
+    const int32_t* mflag = (proposal == WSMC_PROPOSAL_AUTORW && c->world == 1) ? c->dflag : nullptr;
+    if ((int)slots.size() <= kFoldSlots) {
+        if ((int64_t)ct.size() > c->d_ctape_cap) {
+            int64_t cap = c->d_ctape_cap ? c->d_ctape_cap : 64;
+            while (cap < (int64_t)ct.size()) cap *= 2;
+            WSMC_HIP(hipStreamSynchronize(c->stream));
+            if (c->d_ctape) WSMC_HIP(hipFree(c->d_ctape));
+            WSMC_HIP(hipMalloc(&c->d_ctape, sizeof(wsmc_term) * cap));
+            c->d_ctape_cap = cap;
+        }
+        if (!ct.empty())
+            WSMC_HIP(hipMemcpyAsync(c->d_ctape, ct.data(), sizeof(wsmc_term) * ct.size(), hipMemcpyHostToDevice,
+                                    c->stream));
+        FoldSlots fs{};
+        fs.n = (int32_t)slots.size();
+        for (size_t s = 0; s < slots.size(); ++s)
+            fs.p[s] = c->cols[slots[s].first].front + (int64_t)slots[s].second * c->N;
+        for (int k = 0; k < d; ++k) fs.t[k] = c->cols[targets[k]].front;
+        WSMC_HIP(launch_move_c(c->stream, c->d_ctape, kD, target_depth, fs, targets, d, bounded ? l : nullptr,
+                               bounded ? h : nullptr, bounded ? 1 : 0, c->mom + 32, c->seed, op_prop, op_acc, c->goff,
+                               c->N, c->ucount, mflag, c->scache, cache_from));
+    } else {
+        WSMC_HIP(launch_move(c->stream, c->d_tape, (int32_t)c->tape.size(), target_depth, c->d_colptr, targets, d,
+                             bounded ? l : nullptr, bounded ? h : nullptr, bounded ? 1 : 0, c->mom + 32, c->seed,
+                             op_prop, op_acc, c->goff, c->N, c->ucount, mflag, c->scache, cache_from));
+    }
     struct {
         int32_t flag[4];
         unsigned long long acc[4];

@@ -19,9 +19,15 @@ constexpr int kItems = 8;              // particles per thread in the tile kerne
 constexpr int kTile = kBlock * kItems; // 2048 particles per tile (canonical reduction tile)
 constexpr int kSlots = 64;             // max-accumulator slots (blockIdx % 64)
 constexpr int kRsBlock = 1024;         // threads of the reduce workgroup
-constexpr int kSumBlock = 256;         // threads of the weight-statistics workgroup (4 particles each)
+#ifndef WSMC_SUM_BLOCK
+#define WSMC_SUM_BLOCK 256                // build-time override for block-size experiments (tools/)
+#endif
+#ifndef WSMC_SCAN_BLOCK
+#define WSMC_SCAN_BLOCK 256
+#endif
+constexpr int kSumBlock = WSMC_SUM_BLOCK;   // threads of the weight-statistics workgroup (1024 / kSumBlock particles each)
 constexpr int kRsTile = 1024;          // particles per resample tile
-constexpr int kScanBlock = 256;        // threads of the ancestor-fill workgroup (4 particles each)
+constexpr int kScanBlock = WSMC_SCAN_BLOCK;   // threads of the ancestor-fill workgroup (1024 / kScanBlock particles each)
 constexpr int kRsChunk = 2048;         // ancestor slots per fill task
 constexpr int kMaxCols = 4096;
 constexpr int kMaxShards = 8;     // one node: up to 8 GPUs
@@ -143,6 +149,8 @@ struct wsmc_ctx {
     unsigned long long* xbuf = nullptr;     // send + receive buffers (words)
     size_t xbuf_cap = 0;
     double** d_comp = nullptr;              // [2 * cap] component pointer tables (src, dst)
+    wsmc_term* d_ctape = nullptr;           // compiled Move tape (slot operands)
+    int64_t d_ctape_cap = 0;
     size_t d_comp_cap = 0;
     double* tilepart = nullptr;             // [16 * ntiles] canonical-sum tile partials
     wsmc::MaxSlots* mslots = nullptr;       // [1] max slots of one generic resample / evidence
@@ -230,6 +238,17 @@ hipError_t launch_median_pick(hipStream_t s, const unsigned long long* v, const 
                               const unsigned long long* S, int64_t N, double* out);
 hipError_t launch_hist(hipStream_t s, const double* x, const unsigned long long* q, int64_t N, const double* edges,
                        unsigned long long* cnt);
+// Move over a compiled tape (operands renumbered to slots; the targets are slots 0..d-1)
+constexpr int kFoldSlots = 16;
+struct FoldSlots {
+    const double* p[kFoldSlots];   // slot s = column component values [N]
+    double* t[4];                  // the target columns (written on accept)
+    int32_t n;
+};
+hipError_t launch_move_c(hipStream_t s, const wsmc_term* ctape, int32_t nterms, int32_t depth, const FoldSlots& fs,
+                         const int32_t* tcols, int d, const double* lo, const double* hi, int bounded,
+                         const double* L, uint64_t seed, uint64_t op_prop, uint64_t op_acc, int64_t goff, int64_t N,
+                         unsigned long long* accepted, const int32_t* flag, double* scache, int32_t cache_from);
 // sample(state, n; replace): draws on the integer CDF / Efraimidis-Spirakis keys / row gather
 hipError_t launch_sample_draws(hipStream_t s, int64_t n, int64_t N, const ShardRecord* rec,
                                const unsigned long long* tileOff, const unsigned long long* lcdf, uint64_t seed,

@@ -1335,6 +1335,64 @@ __global__ __launch_bounds__(kBlock) void k_move(const wsmc_term* tape, int32_t 
     if (threadIdx.x == 0 && acc) atomicAdd(accepted, acc);
 }
 
+// The same Move over a compiled tape: the host renumbers every (column, component) the
+// fold reads into slots (the targets first), each thread loads its slot values once — all
+// loads independent, in flight together — into LDS, and the shared fold (include/
+// wsmc_terms.h, unchanged arithmetic) reads them through LDS slot pointers. The generic
+// fold's per-term chain term -> column pointer -> global value becomes LDS reads.
+__global__ __launch_bounds__(kBlock) void k_move_c(const wsmc_term* ctape, int32_t nterms, int32_t depth,
+                                                   FoldSlots fs, MomArgs ma, int d, int bounded, const double* Lm,
+                                                   uint64_t seed, uint64_t op_prop, uint64_t op_acc, int64_t goff,
+                                                   int64_t N, u64* accepted, const int32_t* flag, double* scache,
+                                                   int32_t cache_from) {
+    extern __shared__ double sv[];                  // [fs.n][kBlock] (dynamic: occupancy follows the slots)
+    __shared__ double* sp[kFoldSlots];
+    __shared__ u64 lds4[4];
+    if (flag && flag[0]) return;
+    const int th = threadIdx.x;
+    const int64_t i = (int64_t)blockIdx.x * kBlock + th;
+    if (th < fs.n) sp[th] = sv + th * kBlock;
+    for (int s = 0; s < fs.n; ++s) sv[s * kBlock + th] = i < N ? fs.p[s][i] : 0.0;
+    double s_cache = (i < N && cache_from >= 0) ? scache[i] : 0.0;
+    __syncthreads();
+    u64 acc = 0;
+    if (i < N) {
+        double xi[4], dz[4];
+        for (int k = 0; k < d; ++k) xi[k] = wsmc_normal_k(seed, op_prop, (uint64_t)(goff + i), (uint32_t)k);
+        for (int k = 0; k < d; ++k) {
+            double s = 0.0;
+            for (int j = 0; j <= k; ++j) s = s + Lm[k * d + j] * xi[j];
+            dz[k] = s;
+        }
+        wsmc_override ov;
+        ov.n = d;
+        double lpr = 0.0;
+        for (int k = 0; k < d; ++k) {
+            const double x = sv[k * kBlock + th];        // targets are slots 0..d-1
+            const double zo = bounded ? wsmc_to_unc(x, ma.lo[k], ma.hi[k]) : x;
+            const double zn = zo + dz[k];
+            const double xn = bounded ? wsmc_from_unc(zn, ma.lo[k], ma.hi[k]) : zn;
+            if (bounded)
+                lpr = lpr + (wsmc_log_abs_jac(zn, ma.lo[k], ma.hi[k]) - wsmc_log_abs_jac(zo, ma.lo[k], ma.hi[k]));
+            ov.col[k] = k;
+            ov.val[k] = xn;
+        }
+        double* const* cols = sp;
+        const double s_old = cache_from >= 0 ? wsmc_fold_from(s_cache, ctape, cache_from, nterms, depth, cols, 0, th,
+                                                              nullptr)
+                                             : wsmc_fold(ctape, nterms, depth, cols, 0, th, nullptr);
+        const double s_new = wsmc_fold(ctape, nterms, depth, cols, 0, th, &ov);
+        const double u = wsmc_uniform_k(seed, op_acc, (uint64_t)(goff + i), 0);
+        if (wsmc_log(u) < (lpr + s_new) - s_old) {   // strict; NaN rejects (src/transformers.jl:615)
+            for (int k = 0; k < d; ++k) fs.t[k][i] = ov.val[k];
+            acc = 1;
+        }
+        scache[i] = acc ? s_new : s_old;
+    }
+    acc = block_sum_u64(acc, lds4);
+    if (threadIdx.x == 0 && acc) atomicAdd(accepted, acc);
+}
+
 // marginal_diversity keys: isequal semantics (all NaN equal, -0.0 != 0.0)
 __global__ __launch_bounds__(kBlock) void k_div_keys(const double* x, u64* keys, int64_t N) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -1904,6 +1962,21 @@ hipError_t launch_move(hipStream_t s, const wsmc_term* tape, int32_t nterms, int
     }
     hipLaunchKernelGGL(k_move, grid_for(N), dim3(kBlock), 0, s, tape, nterms, depth, cols, ma, d, bounded, L,
                        seed, op_prop, op_acc, goff, N, accepted, flag, scache, cache_from);
+    return hipGetLastError();
+}
+hipError_t launch_move_c(hipStream_t s, const wsmc_term* ctape, int32_t nterms, int32_t depth, const FoldSlots& fs,
+                         const int32_t* tcols, int d, const double* lo, const double* hi, int bounded,
+                         const double* L, uint64_t seed, uint64_t op_prop, uint64_t op_acc, int64_t goff, int64_t N,
+                         u64* accepted, const int32_t* flag, double* scache, int32_t cache_from) {
+    MomArgs ma;
+    for (int k = 0; k < 4; ++k) {
+        ma.tcol[k] = k < d ? tcols[k] : 0;
+        ma.lo[k] = (k < d && lo) ? lo[k] : -WSMC_INF;
+        ma.hi[k] = (k < d && hi) ? hi[k] : WSMC_INF;
+    }
+    const size_t lds = sizeof(double) * kBlock * (size_t)fs.n;
+    hipLaunchKernelGGL(k_move_c, grid_for(N), dim3(kBlock), lds, s, ctape, nterms, depth, fs, ma, d, bounded, L, seed,
+                       op_prop, op_acc, goff, N, accepted, flag, scache, cache_from);
     return hipGetLastError();
 }
 hipError_t launch_diversity_keys(hipStream_t s, const double* x, u64* keys, int64_t N) {

@@ -141,7 +141,8 @@ def load_library(path: os.PathLike | None = None) -> C.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = pathlib.Path(path) if path is not None else LIB_PATH
+    # WSMC_LIB: an alternative build of the same library (block-size experiments, tools/)
+    p = pathlib.Path(path) if path is not None else pathlib.Path(os.environ.get("WSMC_LIB", LIB_PATH))
     if not p.exists():
         raise ImportError(
             f"{p} not found: the HIP library is required (build it with "
