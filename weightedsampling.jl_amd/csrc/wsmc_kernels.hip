@@ -1340,51 +1340,73 @@ __global__ __launch_bounds__(kBlock) void k_move(const wsmc_term* tape, int32_t 
 // loads independent, in flight together — into LDS, and the shared fold (include/
 // wsmc_terms.h, unchanged arithmetic) reads them through LDS slot pointers. The generic
 // fold's per-term chain term -> column pointer -> global value becomes LDS reads.
+// the Move kernels' fold (inlined: an out-of-line copy measured slower, C3 4.47 vs 4.16 ms,
+// C5 1.15 vs 0.76 s per run; WSMC_FOLD_NOINLINE builds it out of line for comparison)
+#ifdef WSMC_FOLD_NOINLINE
+__device__ __noinline__
+#else
+__device__ __forceinline__
+#endif
+double move_fold(double s0, const wsmc_term* tape, int32_t j0, int32_t n, int32_t depth, double* const* cols, int th) {
+    return wsmc_fold_from(s0, tape, j0, n, depth, cols, 0, th, nullptr);
+}
+
 __global__ __launch_bounds__(kBlock) void k_move_c(const wsmc_term* ctape, int32_t nterms, int32_t depth,
                                                    FoldSlots fs, MomArgs ma, int d, int bounded, const double* Lm,
                                                    uint64_t seed, uint64_t op_prop, uint64_t op_acc, int64_t goff,
                                                    int64_t N, u64* accepted, const int32_t* flag, double* scache,
                                                    int32_t cache_from) {
-    extern __shared__ double sv[];                  // [fs.n][kBlock] (dynamic: occupancy follows the slots)
-    __shared__ double* sp[kFoldSlots];
+    // [fs.n][kBlock] current slot values, then [4][kBlock] proposed target values (dynamic LDS)
+    extern __shared__ double sv[];
+    __shared__ double* sp[kFoldSlots];      // current values
+    __shared__ double* spn[kFoldSlots];     // the s_new fold: targets -> proposals (no override lookups)
     __shared__ u64 lds4[4];
     if (flag && flag[0]) return;
     const int th = threadIdx.x;
     const int64_t i = (int64_t)blockIdx.x * kBlock + th;
-    if (th < fs.n) sp[th] = sv + th * kBlock;
+    double* prop = sv + fs.n * kBlock;
+    if (th < fs.n) {
+        sp[th] = sv + th * kBlock;
+        spn[th] = th < d ? prop + th * kBlock : sv + th * kBlock;
+    }
     for (int s = 0; s < fs.n; ++s) sv[s * kBlock + th] = i < N ? fs.p[s][i] : 0.0;
-    double s_cache = (i < N && cache_from >= 0) ? scache[i] : 0.0;
+    const double s_cache = (i < N && cache_from >= 0) ? scache[i] : 0.0;
     __syncthreads();
     u64 acc = 0;
     if (i < N) {
-        double xi[4], dz[4];
-        for (int k = 0; k < d; ++k) xi[k] = wsmc_normal_k(seed, op_prop, (uint64_t)(goff + i), (uint32_t)k);
-        for (int k = 0; k < d; ++k) {
-            double s = 0.0;
-            for (int j = 0; j <= k; ++j) s = s + Lm[k * d + j] * xi[j];
-            dz[k] = s;
+        double xi[4] = {0.0, 0.0, 0.0, 0.0}, dz[4] = {0.0, 0.0, 0.0, 0.0}, xn[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (k < d) xi[k] = wsmc_normal_k(seed, op_prop, (uint64_t)(goff + i), (uint32_t)k);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (k >= d) break;
+            double sum = 0.0;
+#pragma unroll
+            for (int j = 0; j <= k; ++j) sum = sum + Lm[k * d + j] * xi[j];
+            dz[k] = sum;
         }
-        wsmc_override ov;
-        ov.n = d;
         double lpr = 0.0;
-        for (int k = 0; k < d; ++k) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (k >= d) break;
             const double x = sv[k * kBlock + th];        // targets are slots 0..d-1
             const double zo = bounded ? wsmc_to_unc(x, ma.lo[k], ma.hi[k]) : x;
             const double zn = zo + dz[k];
-            const double xn = bounded ? wsmc_from_unc(zn, ma.lo[k], ma.hi[k]) : zn;
+            xn[k] = bounded ? wsmc_from_unc(zn, ma.lo[k], ma.hi[k]) : zn;
             if (bounded)
                 lpr = lpr + (wsmc_log_abs_jac(zn, ma.lo[k], ma.hi[k]) - wsmc_log_abs_jac(zo, ma.lo[k], ma.hi[k]));
-            ov.col[k] = k;
-            ov.val[k] = xn;
+            prop[k * kBlock + th] = xn[k];
         }
-        double* const* cols = sp;
-        const double s_old = cache_from >= 0 ? wsmc_fold_from(s_cache, ctape, cache_from, nterms, depth, cols, 0, th,
-                                                              nullptr)
-                                             : wsmc_fold(ctape, nterms, depth, cols, 0, th, nullptr);
-        const double s_new = wsmc_fold(ctape, nterms, depth, cols, 0, th, &ov);
+        // fold_from(0.0, .., 0, ..) is wsmc_fold: the same left fold from 0.0
+        const double s_old = cache_from >= 0 ? move_fold(s_cache, ctape, cache_from, nterms, depth, sp, th)
+                                             : move_fold(0.0, ctape, 0, nterms, depth, sp, th);
+        const double s_new = move_fold(0.0, ctape, 0, nterms, depth, spn, th);
         const double u = wsmc_uniform_k(seed, op_acc, (uint64_t)(goff + i), 0);
         if (wsmc_log(u) < (lpr + s_new) - s_old) {   // strict; NaN rejects (src/transformers.jl:615)
-            for (int k = 0; k < d; ++k) fs.t[k][i] = ov.val[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < d) fs.t[k][i] = xn[k];
             acc = 1;
         }
         scache[i] = acc ? s_new : s_old;
@@ -1974,7 +1996,7 @@ hipError_t launch_move_c(hipStream_t s, const wsmc_term* ctape, int32_t nterms, 
         ma.lo[k] = (k < d && lo) ? lo[k] : -WSMC_INF;
         ma.hi[k] = (k < d && hi) ? hi[k] : WSMC_INF;
     }
-    const size_t lds = sizeof(double) * kBlock * (size_t)fs.n;
+    const size_t lds = sizeof(double) * kBlock * (size_t)(fs.n + 4);
     hipLaunchKernelGGL(k_move_c, grid_for(N), dim3(kBlock), lds, s, ctape, nterms, depth, fs, ma, d, bounded, L, seed,
                        op_prop, op_acc, goff, N, accepted, flag, scache, cache_from);
     return hipGetLastError();
