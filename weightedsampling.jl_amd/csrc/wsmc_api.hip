@@ -1342,6 +1342,7 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
                                     c->stream));
         FoldSlots fs{};
         fs.n = (int32_t)slots.size();
+        for (const auto& t : ct) fs.heavy |= t.dist.mean_fn == WSMC_MEAN_OSCILLATOR ? 1 : 0;
         for (size_t s = 0; s < slots.size(); ++s)
             fs.p[s] = c->cols[slots[s].first].front + (int64_t)slots[s].second * c->N;
         for (int k = 0; k < d; ++k) fs.t[k] = c->cols[targets[k]].front;

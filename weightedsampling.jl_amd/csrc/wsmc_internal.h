@@ -244,6 +244,7 @@ struct FoldSlots {
     const double* p[kFoldSlots];   // slot s = column component values [N]
     double* t[4];                  // the target columns (written on accept)
     int32_t n;
+    int32_t heavy;                 // transcendental-heavy terms (oscillator means): one particle per thread
 };
 hipError_t launch_move_c(hipStream_t s, const wsmc_term* ctape, int32_t nterms, int32_t depth, const FoldSlots& fs,
                          const int32_t* tcols, int d, const double* lo, const double* hi, int bounded,

@@ -1340,76 +1340,104 @@ __global__ __launch_bounds__(kBlock) void k_move(const wsmc_term* tape, int32_t 
 // loads independent, in flight together — into LDS, and the shared fold (include/
 // wsmc_terms.h, unchanged arithmetic) reads them through LDS slot pointers. The generic
 // fold's per-term chain term -> column pointer -> global value becomes LDS reads.
-// the Move kernels' fold (inlined: an out-of-line copy measured slower, C3 4.47 vs 4.16 ms,
-// C5 1.15 vs 0.76 s per run; WSMC_FOLD_NOINLINE builds it out of line for comparison)
-#ifdef WSMC_FOLD_NOINLINE
-__device__ __noinline__
-#else
-__device__ __forceinline__
-#endif
-double move_fold(double s0, const wsmc_term* tape, int32_t j0, int32_t n, int32_t depth, double* const* cols, int th) {
-    return wsmc_fold_from(s0, tape, j0, n, depth, cols, 0, th, nullptr);
+// K particles per thread: the tape is walked once per thread for K particles, so the
+// interpreter's serial chain of scalar term loads and branches (what the one-particle
+// kernel waits on: VALU active 10%) is shared; each particle keeps its own accumulator and
+// log memo, so every fold is the same left fold as wsmc_fold / wsmc_fold_from.
+template <int K>
+__device__ __forceinline__ void fold_k(double (&s)[K], const wsmc_term* tape, int32_t j0, int32_t n, int32_t depth,
+                                       double* const* cols, const int (&ix)[K], const bool (&ok)[K]) {
+    wsmc_logmemo lm[K];
+#pragma unroll
+    for (int p = 0; p < K; ++p) lm[p] = wsmc_logmemo{0, 0.0, 0};
+    for (int32_t j = j0; j < n; ++j) {
+        if (tape[j].depth >= depth) break;
+#pragma unroll
+        for (int p = 0; p < K; ++p)
+            if (ok[p]) s[p] = s[p] + wsmc_term_logpdf_m(&tape[j], cols, 0, ix[p], nullptr, &lm[p]);
+    }
 }
 
+// The same Move over a compiled tape (slots; targets are slots 0..d-1), K particles per
+// thread: slot values staged once in LDS ([slot][K * kBlock]), proposals in their own LDS
+// rows so the s_new fold reads them through its own pointer table (no override lookups).
+template <int K>
 __global__ __launch_bounds__(kBlock) void k_move_c(const wsmc_term* ctape, int32_t nterms, int32_t depth,
                                                    FoldSlots fs, MomArgs ma, int d, int bounded, const double* Lm,
                                                    uint64_t seed, uint64_t op_prop, uint64_t op_acc, int64_t goff,
                                                    int64_t N, u64* accepted, const int32_t* flag, double* scache,
                                                    int32_t cache_from) {
-    // [fs.n][kBlock] current slot values, then [4][kBlock] proposed target values (dynamic LDS)
-    extern __shared__ double sv[];
-    __shared__ double* sp[kFoldSlots];      // current values
-    __shared__ double* spn[kFoldSlots];     // the s_new fold: targets -> proposals (no override lookups)
+    constexpr int W = K * kBlock;            // LDS row length
+    extern __shared__ double sv[];           // [fs.n][W] current values, then [4][W] proposals
+    __shared__ double* sp[kFoldSlots];
+    __shared__ double* spn[kFoldSlots];
     __shared__ u64 lds4[4];
     if (flag && flag[0]) return;
     const int th = threadIdx.x;
-    const int64_t i = (int64_t)blockIdx.x * kBlock + th;
-    double* prop = sv + fs.n * kBlock;
+    const int64_t base = (int64_t)blockIdx.x * W;
+    double* prop = sv + fs.n * W;
     if (th < fs.n) {
-        sp[th] = sv + th * kBlock;
-        spn[th] = th < d ? prop + th * kBlock : sv + th * kBlock;
+        sp[th] = sv + th * W;
+        spn[th] = th < d ? prop + th * W : sv + th * W;
     }
-    for (int s = 0; s < fs.n; ++s) sv[s * kBlock + th] = i < N ? fs.p[s][i] : 0.0;
-    const double s_cache = (i < N && cache_from >= 0) ? scache[i] : 0.0;
+    int ix[K];
+    bool ok[K];
+    int64_t gi[K];
+#pragma unroll
+    for (int p = 0; p < K; ++p) {
+        ix[p] = p * kBlock + th;
+        gi[p] = base + ix[p];
+        ok[p] = gi[p] < N;
+    }
+    for (int sl = 0; sl < fs.n; ++sl)
+#pragma unroll
+        for (int p = 0; p < K; ++p) sv[sl * W + ix[p]] = ok[p] ? fs.p[sl][gi[p]] : 0.0;
+    double so[K], sn[K], lpr[K];
+#pragma unroll
+    for (int p = 0; p < K; ++p) {
+        so[p] = (ok[p] && cache_from >= 0) ? scache[gi[p]] : 0.0;
+        sn[p] = 0.0;
+        lpr[p] = 0.0;
+    }
     __syncthreads();
-    u64 acc = 0;
-    if (i < N) {
-        double xi[4] = {0.0, 0.0, 0.0, 0.0}, dz[4] = {0.0, 0.0, 0.0, 0.0}, xn[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int p = 0; p < K; ++p) {
+        if (!ok[p]) continue;
+        double xi[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            if (k < d) xi[k] = wsmc_normal_k(seed, op_prop, (uint64_t)(goff + i), (uint32_t)k);
+            if (k < d) xi[k] = wsmc_normal_k(seed, op_prop, (uint64_t)(goff + gi[p]), (uint32_t)k);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             if (k >= d) break;
-            double sum = 0.0;
+            double dz = 0.0;
 #pragma unroll
-            for (int j = 0; j <= k; ++j) sum = sum + Lm[k * d + j] * xi[j];
-            dz[k] = sum;
-        }
-        double lpr = 0.0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (k >= d) break;
-            const double x = sv[k * kBlock + th];        // targets are slots 0..d-1
+            for (int j = 0; j <= k; ++j) dz = dz + Lm[k * d + j] * xi[j];
+            const double x = sv[k * W + ix[p]];
             const double zo = bounded ? wsmc_to_unc(x, ma.lo[k], ma.hi[k]) : x;
-            const double zn = zo + dz[k];
-            xn[k] = bounded ? wsmc_from_unc(zn, ma.lo[k], ma.hi[k]) : zn;
+            const double zn = zo + dz;
+            const double xn = bounded ? wsmc_from_unc(zn, ma.lo[k], ma.hi[k]) : zn;
             if (bounded)
-                lpr = lpr + (wsmc_log_abs_jac(zn, ma.lo[k], ma.hi[k]) - wsmc_log_abs_jac(zo, ma.lo[k], ma.hi[k]));
-            prop[k * kBlock + th] = xn[k];
+                lpr[p] = lpr[p] + (wsmc_log_abs_jac(zn, ma.lo[k], ma.hi[k]) - wsmc_log_abs_jac(zo, ma.lo[k], ma.hi[k]));
+            prop[k * W + ix[p]] = xn;
         }
-        // fold_from(0.0, .., 0, ..) is wsmc_fold: the same left fold from 0.0
-        const double s_old = cache_from >= 0 ? move_fold(s_cache, ctape, cache_from, nterms, depth, sp, th)
-                                             : move_fold(0.0, ctape, 0, nterms, depth, sp, th);
-        const double s_new = move_fold(0.0, ctape, 0, nterms, depth, spn, th);
-        const double u = wsmc_uniform_k(seed, op_acc, (uint64_t)(goff + i), 0);
-        if (wsmc_log(u) < (lpr + s_new) - s_old) {   // strict; NaN rejects (src/transformers.jl:615)
+    }
+    // s_old: the carried score continued over the new terms, or the full fold
+    fold_k<K>(so, ctape, cache_from >= 0 ? cache_from : 0, nterms, depth, sp, ix, ok);
+    fold_k<K>(sn, ctape, 0, nterms, depth, spn, ix, ok);
+    u64 acc = 0;
+#pragma unroll
+    for (int p = 0; p < K; ++p) {
+        if (!ok[p]) continue;
+        const double u = wsmc_uniform_k(seed, op_acc, (uint64_t)(goff + gi[p]), 0);
+        const bool a = wsmc_log(u) < (lpr[p] + sn[p]) - so[p];   // strict; NaN rejects (src/transformers.jl:615)
+        if (a) {
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if (k < d) fs.t[k][i] = xn[k];
-            acc = 1;
+                if (k < d) fs.t[k][gi[p]] = prop[k * W + ix[p]];
+            acc += 1;
         }
-        scache[i] = acc ? s_new : s_old;
+        scache[gi[p]] = a ? sn[p] : so[p];
     }
     acc = block_sum_u64(acc, lds4);
     if (threadIdx.x == 0 && acc) atomicAdd(accepted, acc);
@@ -1996,9 +2024,19 @@ hipError_t launch_move_c(hipStream_t s, const wsmc_term* ctape, int32_t nterms, 
         ma.lo[k] = (k < d && lo) ? lo[k] : -WSMC_INF;
         ma.hi[k] = (k < d && hi) ? hi[k] : WSMC_INF;
     }
-    const size_t lds = sizeof(double) * kBlock * (size_t)(fs.n + 4);
-    hipLaunchKernelGGL(k_move_c, grid_for(N), dim3(kBlock), lds, s, ctape, nterms, depth, fs, ma, d, bounded, L, seed,
-                       op_prop, op_acc, goff, N, accepted, flag, scache, cache_from);
+    // particles per thread: 2 when the terms are cheap (the scalar term chain dominates:
+    // C3 3.7 vs 4.3 ms per run), 1 when they are transcendental-heavy (occupancy wins: C5
+    // 0.76 vs 0.88 s); 4 was slower for both
+    const size_t row = sizeof(double) * kBlock * (size_t)(fs.n + 4);
+    if (fs.heavy) {
+        const dim3 g((unsigned)((N + kBlock - 1) / kBlock));
+        hipLaunchKernelGGL(k_move_c<1>, g, dim3(kBlock), row, s, ctape, nterms, depth, fs, ma, d, bounded, L, seed,
+                           op_prop, op_acc, goff, N, accepted, flag, scache, cache_from);
+    } else {
+        const dim3 g((unsigned)((N + 2 * kBlock - 1) / (2 * kBlock)));
+        hipLaunchKernelGGL(k_move_c<2>, g, dim3(kBlock), 2 * row, s, ctape, nterms, depth, fs, ma, d, bounded, L,
+                           seed, op_prop, op_acc, goff, N, accepted, flag, scache, cache_from);
+    }
     return hipGetLastError();
 }
 hipError_t launch_diversity_keys(hipStream_t s, const double* x, u64* keys, int64_t N) {
