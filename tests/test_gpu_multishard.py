@@ -189,15 +189,28 @@ def _exact_worker(rank, world, port, sizes, T, ess, scheme, outdir):
     # what exact shards refuse rather than silently doing island work
     refused = []
     try:
-        c.ssm2d_run(wsmc.models.ssm2d_data(2), ess_perc_min=ess)
-    except wsmc.WSMCError:
-        refused.append("fused")
-    try:
         c.resample(2.0, abi.RESAMPLE_MULTINOMIAL)
     except wsmc.WSMCError:
         refused.append("multinomial")
+    try:
+        c.ssm2d_run(wsmc.models.ssm2d_data(2), ess_perc_min=ess, scheme=abi.RESAMPLE_MULTINOMIAL)
+    except wsmc.WSMCError:
+        refused.append("fused multinomial")
     out["refused"] = np.array(refused)
     c.close()
+    # the fused run on exact shards: the same bits (history traced back across ranks)
+    for keep in (True, False):
+        f = wsmc.Context(n, seed=21, device=0)
+        f.comm_init_host(comm.allgather, world, rank, goff, N)
+        f.comm_set_shard_mode(abi.SHARD_EXACT)
+        tag = "fk" if keep else "fn"
+        out[tag + "ev"] = np.array([f.ssm2d_run(wsmc.models.ssm2d_data(T), ess_perc_min=ess, scheme=scheme,
+                                                keep_history=keep)])
+        out[tag + "w"] = f.weights_download()
+        out[tag + "anc"] = f.last_ancestors()
+        for name in f.col_names():
+            out[tag + "_" + name] = f.col_download(f.col_find(name))
+        f.close()
     comm.barrier()
     comm.close()
     np.savez(os.path.join(outdir, f"ex{rank}.npz"), **out)
@@ -241,4 +254,15 @@ def test_exact_shards_match_single_context_oracle(gpu_available, tmp_path, sizes
                                           err_msg=name)
         assert p["ev"][0] == ref.log_evidence()
         assert p["ess"][0] == ref.ess()
-        assert list(p["refused"]) == ["fused", "multinomial"]
+        assert list(p["refused"]) == ["multinomial", "fused multinomial"]
+        for tag in ("fk", "fn"):
+            assert p[tag + "ev"][0] == ref.log_evidence(), tag
+            np.testing.assert_array_equal(p[tag + "w"], ref.weights_download()[sl])
+            np.testing.assert_array_equal(p[tag + "anc"], ref.last_ancestors()[sl])
+            for name in ("v", "dv"):
+                np.testing.assert_array_equal(p[tag + "_" + name], ref.col_download(ref.col_find(name))[..., sl],
+                                              err_msg=tag + name)
+        for name in ref.col_names():                       # the traced-back history
+            np.testing.assert_array_equal(p["fk_" + name], ref.col_download(ref.col_find(name))[..., sl],
+                                          err_msg=name)
+        np.testing.assert_array_equal(p["fn_x"], ref.col_download(ref.col_find(f"x_{T + 1}"))[..., sl])

@@ -576,24 +576,15 @@ static inline unsigned long long overlap(unsigned long long a0, unsigned long lo
 }
 
 // the window's slots move to their owners: local ones in place, the rest packed per peer,
-// exchanged (grouped RCCL send/recv, or the host exchange), unpacked
-static int exact_move_particles(wsmc_ctx* c, const ExactPlan& x) {
+// exchanged (grouped RCCL send/recv, or the host exchange), unpacked. src/dst: component
+// arrays (element stride `stride`); anc_local receives the global ancestor ids.
+static int exact_route(wsmc_ctx* c, const ExactPlan& x, const std::vector<const double*>& src,
+                       const std::vector<double*>& dst, int stride, int32_t* anc_local) {
     const int W = c->world, me = c->rank;
-    std::vector<const double*> src;
-    std::vector<double*> dst;
-    for (auto& col : c->cols)
-        for (int k = 0; k < col.dim; ++k) {
-            src.push_back(col.front + (int64_t)k * c->N);
-            dst.push_back(col.back + (int64_t)k * c->N);
-        }
-    const bool cache = c->scache && c->scache_terms >= 0;   // carried Move scores follow their particles
-    if (cache) {
-        src.push_back(c->scache);
-        dst.push_back(c->scache_back);
-    }
     const int nc = (int)src.size();
     const size_t need = 2 * (size_t)(nc > 0 ? nc : 1);
     if (c->d_comp_cap < need) {
+        WSMC_HIP(hipStreamSynchronize(c->stream));
         if (c->d_comp) WSMC_HIP(hipFree(c->d_comp));
         WSMC_HIP(hipMalloc(&c->d_comp, sizeof(double*) * need));
         c->d_comp_cap = need;
@@ -604,11 +595,12 @@ static int exact_move_particles(wsmc_ctx* c, const ExactPlan& x) {
         tab[nc + k] = dst[k];
     }
     WSMC_HIP(hipMemcpyAsync(c->d_comp, tab.data(), sizeof(double*) * need, hipMemcpyHostToDevice, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));   // `tab` is pageable and local
     // routing tables (every rank derives every rank's blocks from the same plan)
     const unsigned long long D = (unsigned long long)nc + 1;
     auto sendlen = [&](int g, int r) { return overlap(x.seg[g], x.seg[g + 1], x.gofs[r], x.gofs[r + 1]); };
     ExactRoute rt{};
-    rt.world = W; rt.rank = me; rt.ncomp = nc;
+    rt.world = W; rt.rank = me; rt.ncomp = nc; rt.stride = stride;
     rt.a = x.a; rt.b = x.b;
     for (int g = 0; g <= W; ++g) rt.gofs[g] = x.gofs[g];
     unsigned long long S = 0, R = 0;
@@ -631,13 +623,14 @@ static int exact_move_particles(wsmc_ctx* c, const ExactPlan& x) {
     }
     const size_t words = (size_t)(S + R) + 1;
     if (c->xbuf_cap < words) {
+        WSMC_HIP(hipStreamSynchronize(c->stream));
         if (c->xbuf) WSMC_HIP(hipFree(c->xbuf));
         WSMC_HIP(hipMalloc(&c->xbuf, sizeof(unsigned long long) * words));
         c->xbuf_cap = words;
     }
     unsigned long long* sendbuf = c->xbuf;
     unsigned long long* recvbuf = c->xbuf + S;
-    WSMC_HIP(launch_exact_pack(c->stream, rt, c->anc_out, c->d_comp, c->d_comp + nc, c->anc, sendbuf));
+    WSMC_HIP(launch_exact_pack(c->stream, rt, c->anc_out, c->d_comp, c->d_comp + nc, anc_local, sendbuf));
     if (c->host_exchange) {
         // test transport: every rank all-gathers its whole send area (padded to the largest)
         unsigned long long maxS = 0;
@@ -674,38 +667,165 @@ static int exact_move_particles(wsmc_ctx* c, const ExactPlan& x) {
         }
         WSMC_RCCL(ncclGroupEnd());
     }
-    WSMC_HIP(launch_exact_unpack(c->stream, rt, recvbuf, c->d_comp + nc, c->anc));
+    WSMC_HIP(launch_exact_unpack(c->stream, rt, recvbuf, c->d_comp + nc, anc_local));
+    return WSMC_OK;
+}
+
+// every column (and the carried Move scores) follows the window's ancestors
+static int exact_move_particles(wsmc_ctx* c, const ExactPlan& x) {
+    std::vector<const double*> src;
+    std::vector<double*> dst;
+    for (auto& col : c->cols)
+        for (int k = 0; k < col.dim; ++k) {
+            src.push_back(col.front + (int64_t)k * c->N);
+            dst.push_back(col.back + (int64_t)k * c->N);
+        }
+    const bool cache = c->scache && c->scache_terms >= 0;   // carried Move scores follow their particles
+    if (cache) {
+        src.push_back(c->scache);
+        dst.push_back(c->scache_back);
+    }
+    int r = exact_route(c, x, src, dst, 1, c->anc);
+    if (r) return r;
     for (auto& col : c->cols) std::swap(col.front, col.back);
     if (cache) std::swap(c->scache, c->scache_back);
     c->colptr_dirty = true;
     return WSMC_OK;
 }
 
-// Resample over the whole population (SURVEY §8(e) item 4): the single-GPU decision,
-// ancestors, columns, weights and evidence, bit for bit
-static int exact_resample(wsmc_ctx* c, double ess_min, int32_t scheme, uint64_t op, Decision* out) {
+// decide (the single-context bits) and fill this shard's window of global slots (anc_out)
+static int exact_decide_fill(wsmc_ctx* c, double ess_min, int32_t scheme, uint64_t op, Decision* dec_dev,
+                             Decision* hd, ExactPlan* hx) {
     int r = ensure_exact(c);
     if (r) return r;
     if ((r = exact_records(c))) return r;
     FillPlan plan = fill_plan(c, scheme, op, nullptr);
     plan.slot_base = 0;                       // slots are global: their keys too
-    WSMC_HIP(launch_rs_decide_exact(c->stream, c->rec, c->world, c->rank, ess_min, plan, c->comb, c->dec, c->xp));
+    WSMC_HIP(launch_rs_decide_exact(c->stream, c->rec, c->world, c->rank, ess_min, plan, c->comb, dec_dev, c->xp));
     plan.xp = c->xp;
     // fill tasks planned with the global strata (N / Q of the whole population)
-    WSMC_HIP(launch_rs_reduce(c->stream, c->mslots, c->tilep, c->N, c->tileOff, c->rec + c->rank, 0, ess_min, c->dec,
+    WSMC_HIP(launch_rs_reduce(c->stream, c->mslots, c->tilep, c->N, c->tileOff, c->rec + c->rank, 0, ess_min, dec_dev,
                               &plan));
-    WSMC_HIP(launch_rs_scan(c->stream, c->N, c->comb, c->dec, plan, c->tileOff, c->qbuf, c->anc_out));
+    WSMC_HIP(launch_rs_scan(c->stream, c->N, c->comb, dec_dev, plan, c->tileOff, c->qbuf, c->anc_out));
     struct Host { Decision d; ExactPlan x; };
     Host* h = reinterpret_cast<Host*>(c->pinned);
     static_assert(sizeof(Host) <= 4096, "pinned staging");
-    WSMC_HIP(hipMemcpyAsync(&h->d, c->dec, sizeof(Decision), hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipMemcpyAsync(&h->d, dec_dev, sizeof(Decision), hipMemcpyDeviceToHost, c->stream));
     WSMC_HIP(hipMemcpyAsync(&h->x, c->xp, sizeof(ExactPlan), hipMemcpyDeviceToHost, c->stream));
     WSMC_HIP(hipStreamSynchronize(c->stream));
-    *out = h->d;
-    if (!out->resampled) return WSMC_OK;
-    const ExactPlan x = h->x;
+    *hd = h->d;
+    *hx = h->x;
+    return WSMC_OK;
+}
+
+// Resample over the whole population (SURVEY §8(e) item 4): the single-GPU decision,
+// ancestors, columns, weights and evidence, bit for bit
+static int exact_resample(wsmc_ctx* c, double ess_min, int32_t scheme, uint64_t op, Decision* out) {
+    ExactPlan x;
+    int r = exact_decide_fill(c, ess_min, scheme, op, c->dec, out, &x);
+    if (r || !out->resampled) return r;
     if ((r = exact_move_particles(c, x))) return r;
     WSMC_HIP(launch_fill_weights(c->stream, c->w, c->dec, c->N));
+    return WSMC_OK;
+}
+
+// One level of the distributed trace-back: every rank's lineage ids a[0..n) are sorted
+// (stratified / systematic ancestors are monotone, so are their compositions), so a rank
+// needs one contiguous range [a[0], a[n-1]] of global indices. Owners send their part of
+// (x pair of hist, ancestor of arow) for it; xout gets hist[a] (SoA), anext arow[a] (or a).
+static int trace_level(wsmc_ctx* c, const ExactPlan& x, const double* hist, const int32_t* arow, const int32_t* a,
+                       int32_t* anext, double* xout) {
+    const int W = c->world, me = c->rank;
+    const int64_t n = c->N;
+    int32_t* h2 = reinterpret_cast<int32_t*>(c->pinned);
+    WSMC_HIP(hipMemcpyAsync(h2, a, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipMemcpyAsync(h2 + 1, a + n - 1, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    std::vector<unsigned long long> rng(2 * (size_t)W);
+    {
+        unsigned long long* mine = reinterpret_cast<unsigned long long*>(c->pinned) + 64;   // pinned staging
+        mine[0] = (unsigned long long)(uint32_t)h2[0];
+        mine[1] = (unsigned long long)(uint32_t)h2[1] + 1;                                  // [lo, hi)
+        WSMC_HIP(hipMemcpyAsync(c->xchg + 2 * me, mine, sizeof(unsigned long long) * 2, hipMemcpyHostToDevice,
+                                c->stream));
+        int r = exchange_words(c, c->xchg, 2, c->stream);
+        if (r) return r;
+        WSMC_HIP(hipMemcpyAsync(rng.data(), c->xchg, sizeof(unsigned long long) * 2 * W, hipMemcpyDeviceToHost,
+                                c->stream));
+        WSMC_HIP(hipStreamSynchronize(c->stream));
+    }
+    auto part = [&](int owner, int req) {   // [start, end) global of owner's rows requester needs
+        const unsigned long long lo = rng[2 * req] > x.gofs[owner] ? rng[2 * req] : x.gofs[owner];
+        const unsigned long long hi = rng[2 * req + 1] < x.gofs[owner + 1] ? rng[2 * req + 1] : x.gofs[owner + 1];
+        return std::make_pair(lo, hi > lo ? hi : lo);
+    };
+    const unsigned long long lome = rng[2 * me], R = (rng[2 * me + 1] - lome) * 3;
+    unsigned long long S = 0;
+    std::vector<unsigned long long> soff(W, 0), Sg(W, 0);
+    for (int g = 0; g < W; ++g)
+        for (int r = 0; r < W; ++r)
+            if (r != g) { auto pr = part(g, r); Sg[g] += (pr.second - pr.first) * 3; }
+    for (int r = 0; r < W; ++r) {
+        soff[r] = S;
+        if (r != me) { auto pr = part(me, r); S += (pr.second - pr.first) * 3; }
+    }
+    const size_t words = (size_t)(S + R) + 1;
+    if (c->xbuf_cap < words) {
+        WSMC_HIP(hipStreamSynchronize(c->stream));
+        if (c->xbuf) WSMC_HIP(hipFree(c->xbuf));
+        WSMC_HIP(hipMalloc(&c->xbuf, sizeof(unsigned long long) * words));
+        c->xbuf_cap = words;
+    }
+    unsigned long long* sendbuf = c->xbuf;
+    unsigned long long* recvbuf = c->xbuf + S;
+    const unsigned long long g0 = x.gofs[me];
+    for (int r = 0; r < W; ++r) {
+        auto pr = part(me, r);
+        if (pr.second <= pr.first) continue;
+        unsigned long long* dst = r == me ? recvbuf + (pr.first - lome) * 3 : sendbuf + soff[r];
+        WSMC_HIP(launch_trace_pack(c->stream, hist, arow, (int64_t)(pr.first - g0), (int64_t)(pr.second - pr.first),
+                                   dst));
+    }
+    if (c->host_exchange) {
+        unsigned long long maxS = 0;
+        for (int g = 0; g < W; ++g) maxS = Sg[g] > maxS ? Sg[g] : maxS;
+        if (maxS > 0) {
+            if (maxS > 0x7fffffffull) return fail(WSMC_EARG, "host exchange block too large");
+            std::vector<unsigned long long> mine(maxS, 0ull), all((size_t)maxS * W);
+            if (S) WSMC_HIP(hipMemcpyAsync(mine.data(), sendbuf, sizeof(unsigned long long) * S, hipMemcpyDeviceToHost,
+                                           c->stream));
+            WSMC_HIP(hipStreamSynchronize(c->stream));
+            if (c->host_exchange(c->host_user, reinterpret_cast<const uint64_t*>(mine.data()), (int32_t)maxS,
+                                 reinterpret_cast<uint64_t*>(all.data())) != 0)
+                return fail(WSMC_ERCCL, "host trace-back exchange failed");
+            for (int g = 0; g < W; ++g) {
+                if (g == me) continue;
+                auto pr = part(g, me);
+                if (pr.second <= pr.first) continue;
+                unsigned long long off = 0;
+                for (int r = 0; r < me; ++r)
+                    if (r != g) { auto q = part(g, r); off += (q.second - q.first) * 3; }
+                WSMC_HIP(hipMemcpyAsync(recvbuf + (pr.first - lome) * 3, all.data() + (size_t)g * maxS + off,
+                                        sizeof(unsigned long long) * (pr.second - pr.first) * 3, hipMemcpyHostToDevice,
+                                        c->stream));
+            }
+            WSMC_HIP(hipStreamSynchronize(c->stream));
+        }
+    } else {
+        WSMC_RCCL(ncclGroupStart());
+        for (int r = 0; r < W; ++r) {
+            if (r == me) continue;
+            auto ps = part(me, r), pr = part(r, me);
+            if (ps.second > ps.first)
+                WSMC_RCCL(ncclSend(sendbuf + soff[r], (size_t)(ps.second - ps.first) * 3, ncclUint64, r, c->comm,
+                                   c->stream));
+            if (pr.second > pr.first)
+                WSMC_RCCL(ncclRecv(recvbuf + (pr.first - lome) * 3, (size_t)(pr.second - pr.first) * 3, ncclUint64,
+                                   r, c->comm, c->stream));
+        }
+        WSMC_RCCL(ncclGroupEnd());
+    }
+    WSMC_HIP(launch_trace_lookup(c->stream, recvbuf, (int64_t)lome, a, n, xout, anext, arow ? 1 : 0));
     return WSMC_OK;
 }
 
@@ -1539,6 +1659,109 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
     return WSMC_OK;
 }
 
+// The fused 2D SSM run on exact shards (SURVEY §8(e) item 4, C4 with the single-GPU bits),
+// eager and host-driven. Each step:
+//   propagate from the state already gathered in slot order (identity read);
+//   exact statistics, decision and the window fill (exact_decide_fill);
+//   on a resample the state (x, v; dv at the last step) moves to the owners of its slots,
+//   with the global ancestor ids into the ancestor log.
+// The history x_1..x_{T+1} is traced back across ranks: one range exchange per step
+// (trace_level).
+static int ssm2d_run_exact(wsmc_ctx* c, const RunPlan& p, uint64_t op_base) {
+    const int T = p.T;
+    const int64_t N = c->N;
+    int r = ensure_exact(c);
+    if (r) return r;
+    for (int k = 0; k < 9; ++k)
+        if (!c->xrun[k]) WSMC_HIP(hipMalloc(&c->xrun[k], sizeof(double) * 2 * (size_t)N));
+    for (int k = 0; k < 2; ++k)
+        if (!c->lineage[k]) WSMC_HIP(hipMalloc(&c->lineage[k], sizeof(int32_t) * (size_t)N));
+    double* Gx[2] = {c->xrun[0], c->xrun[1]};
+    double* Gv[2] = {c->xrun[2], c->xrun[3]};
+    double* Gdv = c->xrun[4];
+    double* Xt[2] = {c->xrun[5], c->xrun[6]};
+    double* Vt[2] = {c->xrun[7], c->xrun[8]};
+    WSMC_HIP(hipMemsetAsync(c->run_max, 0, sizeof(MaxSlots) * (T + 1), c->stream));
+    WSMC_HIP(hipMemsetAsync(c->run_dec, 0, sizeof(Decision) * (T + 1), c->stream));
+    const double cpre = 2.0 * WSMC_LOG2PI + 2.0 * wsmc_log(p.r_var);
+    const double* cur_x = nullptr;
+    const double* cur_v = nullptr;
+    double* dvw = c->cols[p.coldv].back;   // pairs: the last step's draws
+    const double* cur_dv = dvw;
+    std::vector<int> rs(T + 1, 0);
+    ExactPlan hx{};
+    for (int t = 1; t <= T; ++t) {
+        Ssm2dArgs a;
+        a.t = t;
+        a.keep_history = p.keep;
+        a.N = N;
+        a.goff = c->goff;
+        a.seed = c->seed;
+        a.op_dev = c->run_params;
+        a.obs = c->obs;
+        a.x0[0] = p.x0[0]; a.x0[1] = p.x0[1];
+        a.v0[0] = p.v0[0]; a.v0[1] = p.v0[1];
+        a.q_sd = wsmc_sqrt(p.q_var);
+        a.r_var = p.r_var;
+        a.c0 = cpre;
+        a.x_prev = cur_x;
+        a.v_prev = cur_v;
+        a.x_next = p.keep ? c->cols[p.xcols[t + 1]].back : Xt[t & 1];
+        a.v_next = Vt[t & 1];
+        a.dv = t == T ? dvw : nullptr;
+        a.w = c->w;
+        a.anc_prev = nullptr;
+        a.identity = 1;
+        a.dec_prev = t > 1 ? c->run_dec + (t - 1) : nullptr;
+        a.ms = c->run_max + t;
+        WSMC_HIP(launch_ssm2d_propagate(c->stream, a));
+        Decision hd;
+        if ((r = exact_decide_fill(c, p.ess_min, p.scheme, op_base + 3ull * (uint64_t)(t - 1) + 2ull, c->run_dec + t,
+                                   &hd, &hx)))
+            return r;
+        rs[t] = hd.resampled;
+        if (!hd.resampled) {
+            cur_x = a.x_next;
+            cur_v = a.v_next;
+            continue;
+        }
+        std::vector<const double*> src = {a.x_next, a.x_next + 1, a.v_next, a.v_next + 1};
+        std::vector<double*> dst = {Gx[t & 1], Gx[t & 1] + 1, Gv[t & 1], Gv[t & 1] + 1};
+        if (t == T) {
+            src.push_back(dvw); src.push_back(dvw + 1);
+            dst.push_back(Gdv); dst.push_back(Gdv + 1);
+            cur_dv = Gdv;
+        }
+        if ((r = exact_route(c, hx, src, dst, 2, c->anc_log + (size_t)(t - 1) * anc_stride(N)))) return r;
+        cur_x = Gx[t & 1];
+        cur_v = Gv[t & 1];
+    }
+    if (rs[T]) WSMC_HIP(launch_fill_weights(c->stream, c->w, c->run_dec + T, N));
+    WSMC_HIP(launch_pairs_to_soa(c->stream, cur_v, c->cols[p.colv].front, N));
+    WSMC_HIP(launch_pairs_to_soa(c->stream, cur_dv, c->cols[p.coldv].front, N));
+    if (!p.keep) {
+        WSMC_HIP(launch_pairs_to_soa(c->stream, cur_x, c->cols[p.colx].front, N));
+        return WSMC_OK;
+    }
+    WSMC_HIP(launch_fill_const2(c->stream, c->cols[p.xcols[1]].front, p.x0[0], p.x0[1], N));
+    // lineage at step T: the last ancestors (global ids), then one range exchange per step:
+    // level t gives x_{t+1} = hist[t+1][a_t] and a_{t-1} = ancestors of step t-1 at a_t
+    int32_t* A = c->lineage[0];
+    int32_t* B = c->lineage[1];
+    if (rs[T])
+        WSMC_HIP(hipMemcpyAsync(A, c->anc_log + (size_t)(T - 1) * anc_stride(N), sizeof(int32_t) * N,
+                                hipMemcpyDeviceToDevice, c->stream));
+    else
+        WSMC_HIP(launch_iota(c->stream, A, N, c->goff));
+    for (int t = T; t >= 1; --t) {
+        const int32_t* arow = (t >= 2 && rs[t - 1]) ? c->anc_log + (size_t)(t - 2) * anc_stride(N) : nullptr;
+        if ((r = trace_level(c, hx, c->cols[p.xcols[t + 1]].back, arow, A, B, c->cols[p.xcols[t + 1]].front)))
+            return r;
+        std::swap(A, B);
+    }
+    return WSMC_OK;
+}
+
 int wsmc_run_set_timing(wsmc_ctx* c, int32_t enabled) {
     if (!c) return fail(WSMC_EARG, "null context");
     c->timing = enabled != 0;
@@ -1557,8 +1780,8 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
     c->scache_terms = -1;   // the run rewrites columns the tape reads
     if (!obs || T < 1 || !x0 || !v0) return fail(WSMC_EARG, "bad arguments");
     if (!valid_scheme(scheme)) return fail(WSMC_EARG, "unknown resampling scheme");
-    if (exact_mode(c))
-        return fail(WSMC_ESTATE, "the fused run on exact shards is not built (island mode, or the statements)");
+    if (exact_mode(c) && scheme == WSMC_RESAMPLE_MULTINOMIAL)
+        return fail(WSMC_EARG, "multinomial draws on exact shards are not supported (island mode is)");
     if (scheme == WSMC_RESAMPLE_MULTINOMIAL && ensure_cdf(c)) return WSMC_EHIP;
     if (!(q_var > 0) || !(r_var > 0)) return fail(WSMC_EARG, "variances must be positive");
     RunPlan p;
@@ -1627,6 +1850,7 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         return WSMC_OK;
     };
     const bool use_graph = c->world == 1 && !c->timing;   // HIP cannot time events captured in graphs
+    if (exact_mode(c) && c->timing) return fail(WSMC_ESTATE, "run timing is not available on exact shards");
     const int nev = 8 * T + 2;
     std::vector<hipEvent_t> evs;
     if (c->timing) {
@@ -1638,7 +1862,9 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         evs.assign(c->events.begin(), c->events.begin() + nev);
     }
     void* temp_tables = nullptr;
-    if (use_graph) {
+    if (exact_mode(c)) {
+        if ((r = ssm2d_run_exact(c, p, op_base))) return r;
+    } else if (use_graph) {
         RunGraph* g = nullptr;
         for (auto& gg : c->graphs)
             if (gg.key == key) g = &gg;

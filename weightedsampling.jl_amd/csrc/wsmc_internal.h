@@ -149,6 +149,8 @@ struct wsmc_ctx {
     unsigned long long* xbuf = nullptr;     // send + receive buffers (words)
     size_t xbuf_cap = 0;
     double** d_comp = nullptr;              // [2 * cap] component pointer tables (src, dst)
+    double* xrun[9] = {};                    // exact-sharded fused run: gathered / scratch pair buffers
+    int32_t* lineage[2] = {};                // [N] global lineage ids (distributed trace-back)
     wsmc_term* d_ctape = nullptr;           // compiled Move tape (slot operands)
     int64_t d_ctape_cap = 0;
     size_t d_comp_cap = 0;
@@ -250,6 +252,15 @@ hipError_t launch_move_c(hipStream_t s, const wsmc_term* ctape, int32_t nterms, 
                          const int32_t* tcols, int d, const double* lo, const double* hi, int bounded,
                          const double* L, uint64_t seed, uint64_t op_prop, uint64_t op_acc, int64_t goff, int64_t N,
                          unsigned long long* accepted, const int32_t* flag, double* scache, int32_t cache_from);
+// exact-sharded fused run: contiguous slices of (x pair, ancestor) by global index for the
+// distributed trace-back, the lineage lookup, pairs -> SoA
+hipError_t launch_trace_pack(hipStream_t s, const double* xpairs, const int32_t* arow, int64_t start, int64_t count,
+                             unsigned long long* out);
+hipError_t launch_trace_lookup(hipStream_t s, const unsigned long long* recv, int64_t lo, const int32_t* a, int64_t n,
+                               double* xout, int32_t* anext, int use_a);
+hipError_t launch_pairs_to_soa(hipStream_t s, const double* pairs, double* soa, int64_t n);
+hipError_t launch_fill_const2(hipStream_t s, double* soa, double v0, double v1, int64_t n);
+hipError_t launch_iota(hipStream_t s, int32_t* a, int64_t n, int64_t base);
 // sample(state, n; replace): draws on the integer CDF / Efraimidis-Spirakis keys / row gather
 hipError_t launch_sample_draws(hipStream_t s, int64_t n, int64_t N, const ShardRecord* rec,
                                const unsigned long long* tileOff, const unsigned long long* lcdf, uint64_t seed,
@@ -268,6 +279,7 @@ hipError_t launch_rs_decide_exact(hipStream_t s, const ShardRecord* recs, int wo
 // the rest packed per peer as [component][slot] u64 blocks), and the receive side
 struct ExactRoute {
     int32_t world, rank, ncomp;                 // ncomp double components (+1 ancestor id word)
+    int32_t stride = 1;                         // element stride of every component (2: pair layout)
     unsigned long long a, b;                    // this rank's window
     unsigned long long gofs[kMaxShards + 1];
     unsigned long long sendoff[kMaxShards];     // words, per peer
@@ -356,6 +368,7 @@ struct Ssm2dArgs {
     const int32_t* anc_prev;   // [N] ancestors of step t-1 (8-B aligned row)
     const Decision* dec_prev;  // decision of step t-1 (nullptr at t = 1)
     MaxSlots* ms;              // this step's max slots
+    int32_t identity = 0;      // exact shards: the previous state is already in slot order (no gather)
 };
 hipError_t launch_ssm2d_propagate(hipStream_t s, const Ssm2dArgs& a, hipEvent_t e0 = nullptr,
                                   hipEvent_t e1 = nullptr);

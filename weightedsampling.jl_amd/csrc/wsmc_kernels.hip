@@ -552,7 +552,7 @@ __global__ __launch_bounds__(kBlock) void k_exact_pack(ExactRoute rt, const int3
     const u64 gid = rt.gofs[rt.rank] + (u64)m;      // the ancestor's global index
     if (r == rt.rank) {
         const u64 li = sl - rt.gofs[rt.rank];
-        for (int c = 0; c < rt.ncomp; ++c) dst[c][li] = src[c][m];
+        for (int c = 0; c < rt.ncomp; ++c) dst[c][li * rt.stride] = src[c][(u64)m * rt.stride];
         anc_local[li] = (int32_t)gid;
         return;
     }
@@ -560,7 +560,7 @@ __global__ __launch_bounds__(kBlock) void k_exact_pack(ExactRoute rt, const int3
     const u64 hi = rt.b < rt.gofs[r + 1] ? rt.b : rt.gofs[r + 1];
     const u64 len = hi - lo, idx = sl - lo;
     u64* blk = sendbuf + rt.sendoff[r];
-    for (int c = 0; c < rt.ncomp; ++c) blk[(u64)c * len + idx] = (u64)wsmc_d2bits(src[c][m]);
+    for (int c = 0; c < rt.ncomp; ++c) blk[(u64)c * len + idx] = (u64)wsmc_d2bits(src[c][(u64)m * rt.stride]);
     blk[(u64)rt.ncomp * len + idx] = gid;
 }
 __global__ __launch_bounds__(kBlock) void k_exact_unpack(ExactRoute rt, const u64* __restrict__ recvbuf,
@@ -573,7 +573,7 @@ __global__ __launch_bounds__(kBlock) void k_exact_unpack(ExactRoute rt, const u6
     const u64 idx = j - rt.recvpre[g], len = rt.recvlen[g];
     const u64* blk = recvbuf + rt.recvoff[g];
     const u64 li = rt.recvdst[g] + idx;
-    for (int c = 0; c < rt.ncomp; ++c) dst[c][li] = wsmc_bits2d(blk[(u64)c * len + idx]);
+    for (int c = 0; c < rt.ncomp; ++c) dst[c][li * rt.stride] = wsmc_bits2d(blk[(u64)c * len + idx]);
     anc_local[li] = (int32_t)blk[(u64)rt.ncomp * len + idx];
 }
 
@@ -1505,7 +1505,7 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_prop(Ssm2dArgs a) {
         src[j][0] = i0; src[j][1] = i0 + 1;
         // the ancestors are loaded speculatively (the previous step's row always exists at
         // t > 1), in parallel with the decision flag, not after it
-        if (ok[j] && a.t > 1 && (MODE & 2) == 0) {
+        if (ok[j] && a.t > 1 && (MODE & 2) == 0 && !a.identity) {
             int2 s2;
             if (two[j]) {
                 s2 = *reinterpret_cast<const int2*>(a.anc_prev + i0);
@@ -1603,6 +1603,48 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_prop(Ssm2dArgs a) {
     }
     menc = block_max_u64(menc, lds4);
     if (threadIdx.x == 0) atomic_max_filtered(&a.ms->v[blockIdx.x % kSlots][0], menc);
+}
+
+// ---- exact-sharded fused run: distributed trace-back -------------------
+// words per global index: x pair (2 doubles) + the ancestor id of the step before
+__global__ __launch_bounds__(kBlock) void k_trace_pack(const double* __restrict__ xpairs,
+                                                       const int32_t* __restrict__ arow, int64_t start, int64_t count,
+                                                       u64* __restrict__ out) {
+    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= count) return;
+    const d2 x = *reinterpret_cast<const d2*>(xpairs + 2 * (start + j));
+    out[3 * j] = (u64)wsmc_d2bits(x.x);
+    out[3 * j + 1] = (u64)wsmc_d2bits(x.y);
+    out[3 * j + 2] = arow ? (u64)(uint32_t)arow[start + j] : 0ull;
+}
+__global__ __launch_bounds__(kBlock) void k_trace_lookup(const u64* __restrict__ recv, int64_t lo,
+                                                         const int32_t* __restrict__ a, int64_t n,
+                                                         double* __restrict__ xout, int32_t* __restrict__ anext,
+                                                         int use_a) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const int64_t o = (int64_t)a[i] - lo;
+    xout[i] = wsmc_bits2d(recv[3 * o]);
+    xout[n + i] = wsmc_bits2d(recv[3 * o + 1]);
+    anext[i] = use_a ? (int32_t)(uint32_t)recv[3 * o + 2] : a[i];
+}
+__global__ __launch_bounds__(kBlock) void k_pairs_to_soa(const double* __restrict__ pairs, double* __restrict__ soa,
+                                                         int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const d2 v = *reinterpret_cast<const d2*>(pairs + 2 * i);
+    soa[i] = v.x;
+    soa[n + i] = v.y;
+}
+__global__ __launch_bounds__(kBlock) void k_fill_const2(double* __restrict__ soa, double v0, double v1, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    soa[i] = v0;
+    soa[n + i] = v1;
+}
+__global__ __launch_bounds__(kBlock) void k_iota(int32_t* __restrict__ a, int64_t n, int64_t base) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) a[i] = (int32_t)(base + i);
 }
 
 // trace the ancestor log back once and materialise the final columns — the result
@@ -2037,6 +2079,30 @@ hipError_t launch_move_c(hipStream_t s, const wsmc_term* ctape, int32_t nterms, 
         hipLaunchKernelGGL(k_move_c<2>, g, dim3(kBlock), 2 * row, s, ctape, nterms, depth, fs, ma, d, bounded, L,
                            seed, op_prop, op_acc, goff, N, accepted, flag, scache, cache_from);
     }
+    return hipGetLastError();
+}
+hipError_t launch_trace_pack(hipStream_t s, const double* xpairs, const int32_t* arow, int64_t start, int64_t count,
+                             u64* out) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_trace_pack, dim3((unsigned)((count + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, xpairs, arow,
+                       start, count, out);
+    return hipGetLastError();
+}
+hipError_t launch_trace_lookup(hipStream_t s, const u64* recv, int64_t lo, const int32_t* a, int64_t n, double* xout,
+                               int32_t* anext, int use_a) {
+    hipLaunchKernelGGL(k_trace_lookup, grid_for(n), dim3(kBlock), 0, s, recv, lo, a, n, xout, anext, use_a);
+    return hipGetLastError();
+}
+hipError_t launch_pairs_to_soa(hipStream_t s, const double* pairs, double* soa, int64_t n) {
+    hipLaunchKernelGGL(k_pairs_to_soa, grid_for(n), dim3(kBlock), 0, s, pairs, soa, n);
+    return hipGetLastError();
+}
+hipError_t launch_fill_const2(hipStream_t s, double* soa, double v0, double v1, int64_t n) {
+    hipLaunchKernelGGL(k_fill_const2, grid_for(n), dim3(kBlock), 0, s, soa, v0, v1, n);
+    return hipGetLastError();
+}
+hipError_t launch_iota(hipStream_t s, int32_t* a, int64_t n, int64_t base) {
+    hipLaunchKernelGGL(k_iota, grid_for(n), dim3(kBlock), 0, s, a, n, base);
     return hipGetLastError();
 }
 hipError_t launch_diversity_keys(hipStream_t s, const double* x, u64* keys, int64_t N) {
