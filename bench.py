@@ -8,8 +8,10 @@
 One bench "step" = one full run! of the T-step filter over one synthetic observation
 sequence (T = 100, the BASELINE.json configs[1] workload), including the final
 history trace-back that materialises x_1..x_{T+1} exactly as the reference's store holds
-them. N = 1,000,000 particles per GPU (weak scaling: each rank owns a 1M shard, ranks
-exchange one 1-KB statistics record per step over RCCL; island resampling).
+them. N = 1,000,000 particles per GPU (weak scaling: each rank owns a 1M shard). Island
+resampling by default — ranks exchange one statistics payload per step over RCCL;
+`--shard-mode exact` resamples the whole population with the single-GPU bits (particles
+move between ranks).
 
 Rank 0 prints ONE JSON line (metric/value/.../roofline/cpu_baseline). Everything else
 goes to stderr.
@@ -60,6 +62,9 @@ def parse():
     # one device): exchange shard records through the host rendezvous, all ranks on GPU 0
     ap.add_argument("--exchange", choices=["rccl", "host"], default="rccl")
     ap.add_argument("--same-device", action="store_true")
+    # island (default): one record all-gather per step, shard-local resampling;
+    # exact: population-wide resampling, the single-GPU bits (particles move between ranks)
+    ap.add_argument("--shard-mode", choices=["island", "exact"], default="island")
     return ap.parse_args()
 
 
@@ -102,6 +107,9 @@ def main():
         else:
             uid = comm.broadcast(wsmc.Context.comm_unique_id() if rank == 0 else None)
             ctx.comm_init(uid, world, rank, rank * N, world * N)
+        if args.shard_mode == "exact":
+            ctx.comm_set_shard_mode(abi.SHARD_EXACT)
+    exact = comm is not None and args.shard_mode == "exact"
 
     def barrier():
         ctx.sync()
@@ -127,20 +135,22 @@ def main():
     ev = ctx.log_evidence()
 
     # per-kernel durations: HIP events recorded on the context stream around every launch of
-    # the same graph (a separate instrumented pass of `steps` runs)
-    ctx.set_timing(True)
+    # the same graph (a separate instrumented pass of `steps` runs); not available on exact
+    # shards (their eager, host-driven run is not instrumented)
     prop_ms = red_ms = rs_ms = fin_ms = tot_ms = 0.0
     nres = 0
-    inst_runs = max(1, min(args.steps, 5))
-    one_run()  # capture the instrumented graph
-    for _ in range(inst_runs):
-        one_run()
-        tm = ctx.timing()
-        prop_ms += tm["propagate_ms"]; red_ms += tm["reduce_ms"]; rs_ms += tm["resample_ms"]
-        fin_ms += tm["finalize_ms"]; tot_ms += tm["total_ms"]; nres += tm["n_resamples"]
-    ctx.set_timing(False)
-    prop_ms /= inst_runs; red_ms /= inst_runs; rs_ms /= inst_runs; fin_ms /= inst_runs; tot_ms /= inst_runs
-    nres //= inst_runs
+    if not exact:
+        ctx.set_timing(True)
+        inst_runs = max(1, min(args.steps, 5))
+        one_run()  # capture the instrumented graph
+        for _ in range(inst_runs):
+            one_run()
+            tm = ctx.timing()
+            prop_ms += tm["propagate_ms"]; red_ms += tm["reduce_ms"]; rs_ms += tm["resample_ms"]
+            fin_ms += tm["finalize_ms"]; tot_ms += tm["total_ms"]; nres += tm["n_resamples"]
+        ctx.set_timing(False)
+        prop_ms /= inst_runs; red_ms /= inst_runs; rs_ms /= inst_runs; fin_ms /= inst_runs; tot_ms /= inst_runs
+        nres //= inst_runs
 
     units = world * N * T * args.steps
     value = units / elapsed
@@ -182,17 +192,19 @@ def main():
             "config": {"workload": "2D SSM bootstrap filter (examples/2D_ssm.jl), BASELINE configs[1]",
                        "n_particles_per_gpu": N, "global_particles": world * N, "T": T,
                        "ess_perc_min": args.ess, "scheme": args.scheme, "keep_history": not args.no_history,
-                       "parallelism": (f"island-shard x{world}" + (" (host exchange, test mode)" if args.exchange == "host" else ""))
+                       "parallelism": (f"{args.shard_mode}-shard x{world}"
+                                       + (" (host exchange, test mode)" if args.exchange == "host" else ""))
                            if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "kernel": "k_ssm2d_prop (propagate+observe+max)",
                          "achieved": prop_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (prop_gbs / HBM_PEAK_GBS) if prop_gbs else None, "traffic": traffic,
-                         "algorithmic_bytes_per_run": prop_bytes, "avg_launch_us": prop_ms * 1e3 / T,
+                         "algorithmic_bytes_per_run": prop_bytes, "avg_launch_us": prop_ms * 1e3 / T if prop_ms > 0 else None,
                          "whole_step_GBs": value / world * STEP_BYTES / 1e9},
             "cpu_baseline": cpu,
-            "breakdown_ms_per_run": {"propagate": prop_ms, "weight_stats": red_ms, "scan_ancestors": rs_ms,
-                                     "finalize_traceback": fin_ms, "instrumented_total": tot_ms,
-                                     "resamples_per_run": nres, "forced_every_step": forced},
+            "breakdown_ms_per_run": None if exact else {
+                "propagate": prop_ms, "weight_stats": red_ms, "scan_ancestors": rs_ms,
+                "finalize_traceback": fin_ms, "instrumented_total": tot_ms,
+                "resamples_per_run": nres, "forced_every_step": forced},
             "log_evidence_last": ev,
         }
         print(json.dumps(line), flush=True)

@@ -152,8 +152,8 @@ int wsmc_comm_init_host(wsmc_ctx* ctx, wsmc_exchange_fn exchange, void* user, in
  *    global indices, columns, weights, evidence): the global max is exchanged first,
  *    the records are summed as integers, each shard fills its contiguous window of
  *    global slots and the particles move to their owners (grouped send/recv).
- * Exact mode covers the statement operators; wsmc_ssm2d_run and multinomial draws on
- * shards stay island (WSMC_ESTATE / WSMC_EARG otherwise). */
+ * Exact mode covers the statement operators and wsmc_ssm2d_run (history traced back
+ * across ranks); multinomial draws on exact shards return WSMC_EARG. */
 typedef enum { WSMC_SHARD_ISLAND = 0, WSMC_SHARD_EXACT = 1 } wsmc_shard_mode;
 int wsmc_comm_set_shard_mode(wsmc_ctx* ctx, int32_t mode);
 
