@@ -233,6 +233,10 @@ int wsmc_destroy(wsmc_ctx* c) {
                     c->vscratch, c->xscratch, c->run_pay, c->xp, c->comb, c->anc_out, c->xbuf, c->d_comp, c->d_ctape};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
+    for (double* p : c->xrun)
+        if (p) (void)hipFree(p);
+    for (int32_t* p : c->lineage)
+        if (p) (void)hipFree(p);
     if (c->pinned) (void)hipHostFree(c->pinned);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     if (c->ev_sums) (void)hipEventDestroy(c->ev_sums);
