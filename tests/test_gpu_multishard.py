@@ -266,3 +266,80 @@ def test_exact_shards_match_single_context_oracle(gpu_available, tmp_path, sizes
             np.testing.assert_array_equal(p["fk_" + name], ref.col_download(ref.col_find(name))[..., sl],
                                           err_msg=name)
         np.testing.assert_array_equal(p["fn_x"], ref.col_download(ref.col_find(f"x_{T + 1}"))[..., sl])
+
+
+def _exact_skew_worker(rank, world, port, sizes, kind, outdir):
+    sys.path[:0] = [str(REPO / "weightedsampling.jl_amd")]
+    import wsmc
+    from wsmc import abi
+    from wsmc.dsl import Normal
+    from wsmc.hostcomm import HostComm
+    comm = HostComm(rank, world, "127.0.0.1", port, tag="xs", timeout=120)
+    n, goff, N = sizes[rank], sum(sizes[:rank]), sum(sizes)
+    c = wsmc.Context(n, seed=8, device=0)
+    c.comm_init_host(comm.allgather, world, rank, goff, N)
+    c.comm_set_shard_mode(abi.SHARD_EXACT)
+    w = _skew(kind, N)[goff:goff + n]
+    cx = c.col_create("x")
+    c.col_upload(cx, np.arange(goff, goff + n, dtype=float))
+    c.weights_upload(w)
+    c.weight(Normal(0.0, 1.0).dist(c.col_find), [abi.Operand.const(0.0)])
+    rs, ess = c.resample(2.0, abi.RESAMPLE_STRATIFIED)
+    out = {"rs": np.array([rs, ess]), "w": c.weights_download(), "anc": c.last_ancestors(),
+           "x": c.col_download(cx), "ev": np.array([c.log_evidence()])}
+    c.close()
+    comm.barrier()
+    comm.close()
+    np.savez(os.path.join(outdir, f"xs{rank}.npz"), **out)
+
+
+def _skew(kind, N):
+    w = np.full(N, -np.inf)
+    if kind == "last_shard":          # every slot's ancestor lives on the last rank
+        w[N - 50:] = np.linspace(-1.0, 0.0, 50)
+    elif kind == "one_particle":      # one dominant particle on rank 0
+        w[:] = -200.0
+        w[7] = 0.0
+    else:                             # alternating mass: many short windows
+        w[::3] = 0.0
+    return w
+
+
+@pytest.mark.parametrize("kind", ["last_shard", "one_particle", "alternating"])
+def test_exact_shards_skewed_windows(gpu_available, tmp_path, kind):
+    """Exact sharding with all weight on one shard (full migration, empty windows) or one
+    particle: the unsharded oracle's ancestors, columns, weights and evidence."""
+    import multiprocessing as mp
+    sys.path.insert(0, str(REPO / "oracle"))
+    from oracle import Oracle
+    from wsmc import abi
+    from wsmc.dsl import Normal
+    sizes = (3000, 1096, 2001)
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=_exact_skew_worker, args=(r, len(sizes), port, sizes, kind, str(tmp_path)))
+          for r in range(len(sizes))]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(300)
+    codes = [p.exitcode for p in ps]
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+    assert codes == [0] * len(sizes), codes
+    N = sum(sizes)
+    o = Oracle(N, seed=8)
+    cx = o.col_create("x")
+    o.col_upload(cx, np.arange(N, dtype=float))
+    o.weights_upload(_skew(kind, N))
+    o.weight(Normal(0.0, 1.0).dist(o.col_find), [abi.Operand.const(0.0)])
+    rs, ess = o.resample(2.0, abi.RESAMPLE_STRATIFIED)
+    for r in range(len(sizes)):
+        p = np.load(tmp_path / f"xs{r}.npz")
+        sl = slice(sum(sizes[:r]), sum(sizes[:r + 1]))
+        assert bool(p["rs"][0]) == rs and p["rs"][1] == ess
+        np.testing.assert_array_equal(p["anc"], o.last_ancestors()[sl])
+        np.testing.assert_array_equal(p["x"], o.col_download(cx)[sl])
+        np.testing.assert_array_equal(p["w"], o.weights_download()[sl])
+        assert p["ev"][0] == o.log_evidence()
