@@ -165,7 +165,9 @@ def main():
     tf = REPO / "profiles" / "pmc_propagate_bytes.json"
     if tf.exists():
         try:
-            traffic = json.loads(tf.read_text()).get("bytes_per_launch")
+            tj = json.loads(tf.read_text())
+            # measured for one configuration: reported only for that N
+            traffic = tj.get("bytes_per_launch") if tj.get("n_particles", N) == N else None
         except Exception:
             traffic = None
 
