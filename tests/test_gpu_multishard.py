@@ -218,7 +218,7 @@ def _exact_worker(rank, world, port, sizes, T, ess, scheme, outdir):
 
 @pytest.mark.parametrize("sizes,ess,scheme", [((2048, 2048), 1.0, 0), ((2048, 2048), 0.5, 1),
                                               ((3000, 1096), 1.0, 0), ((70001, 70001), 1.0, 0),
-                                              ((70001, 70001), 0.5, 1)])
+                                              ((70001, 70001), 0.5, 1), ((1, 1), 1.0, 0), ((1, 2, 1), 1.0, 1)])
 def test_exact_shards_match_single_context_oracle(gpu_available, tmp_path, sizes, ess, scheme):
     """WSMC_SHARD_EXACT: two shards (one ragged layout) == the unsharded oracle: flags,
     weights, every column, global ancestor indices, log-evidence and ESS, bit for bit."""

@@ -288,3 +288,17 @@ def test_move_not_pd_leaves_state(gpu_available):
         c.move(abi.PROPOSAL_RW, [a], 0.3)
         res.append(c)
     assert_same_state(*res)
+
+
+@pytest.mark.parametrize("N", [1, 2, 3, 1023, 1025])
+@pytest.mark.parametrize("scheme", [abi.RESAMPLE_STRATIFIED, abi.RESAMPLE_MULTINOMIAL])
+def test_ssm2d_fused_tiny_populations(gpu_available, N, scheme):
+    """The fused run at the smallest sizes (odd tails of the pair layout, one tile)."""
+    obs = models.ssm2d_data(6)
+    g = wsmc.Context(N, seed=3)
+    ev = g.ssm2d_run(obs, ess_perc_min=1.0, scheme=scheme, keep_history=True)
+    o = Oracle(N, seed=3)
+    models.ssm2d_statements(o, obs, ess_perc_min=1.0, scheme=scheme)
+    assert_same_state(g, o)
+    np.testing.assert_array_equal(g.last_ancestors(), o.last_ancestors())
+    assert ev == o.log_evidence()
