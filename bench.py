@@ -172,7 +172,7 @@ def main():
             traffic = None
 
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:   # the baseline is an N=1 figure
         cps, cdt = cpu_baseline(obs, args.cpu_particles, args.cpu_T, args.ess, scheme)
         cpu = {"value": cps, "unit": "particle-steps/s", "cores": 1, "kind": "port",
                "sample": f"oracle/ C restatement (eager ColumnStore gathers, 1 thread), 2D SSM "
