@@ -3,8 +3,8 @@
 set -e
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --output-format csv -d gpurun_out/sqm -o run -- python tools/bench_moves.py c3 > gpurun_out/sqm.log 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_FLAT SQ_INSTS_LDS --output-format csv -d gpurun_out/sqm2 -o run -- python tools/bench_moves.py c3 > gpurun_out/sqm2.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --output-format csv -d gpurun_out/sqm -o run -- python tools/bench_moves.py ${WHICH:-c3} > gpurun_out/sqm.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_FLAT SQ_INSTS_LDS --output-format csv -d gpurun_out/sqm2 -o run -- python tools/bench_moves.py ${WHICH:-c3} > gpurun_out/sqm2.log 2>&1
 python tools/summarize_pmc.py gpurun_out/sqm_summary.json gpurun_out/sqm > /dev/null
 python tools/summarize_pmc.py gpurun_out/sqm2_summary.json gpurun_out/sqm2 > /dev/null
 python - <<'PY'
