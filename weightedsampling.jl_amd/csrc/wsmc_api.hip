@@ -1853,7 +1853,11 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         *outp = tabs + (T + 2);
         return WSMC_OK;
     };
-    const bool use_graph = c->world == 1 && !c->timing;   // HIP cannot time events captured in graphs
+    static const bool no_graph = [] {   // diagnostics only: the same run enqueued eagerly
+        const char* e = getenv("WSMC_DIAG_NO_GRAPH");
+        return e && atoi(e) != 0;
+    }();
+    const bool use_graph = c->world == 1 && !c->timing && !no_graph;   // HIP cannot time events captured in graphs
     if (exact_mode(c) && c->timing) return fail(WSMC_ESTATE, "run timing is not available on exact shards");
     const int nev = 8 * T + 2;
     std::vector<hipEvent_t> evs;
