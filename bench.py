@@ -55,8 +55,10 @@ def parse():
     ap.add_argument("--scheme", choices=["stratified", "systematic", "multinomial"], default="stratified")
     ap.add_argument("--no-history", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-particles", type=int, default=500_000)
+    ap.add_argument("--cpu-particles", type=int, default=1_000_000, help="all-cores port sample")
     ap.add_argument("--cpu-T", type=int, default=100)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: OMP_NUM_THREADS or the affinity mask")
+    ap.add_argument("--cpu-1t-particles", type=int, default=500_000, help="single-thread statement-oracle sample")
     ap.add_argument("--seed", type=int, default=42)
     # test hooks for the multi-rank code path on a one-GPU box (RCCL refuses two ranks on
     # one device): exchange shard records through the host rendezvous, all ranks on GPU 0
@@ -68,12 +70,46 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(obs, n, T, ess, scheme):
-    """The oracle (C restatement of the reference path, eager ColumnStore gathers) on the host."""
+def cpu_threads(requested: int) -> int:
+    if requested > 0:
+        return requested
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return max(1, min(int(env), aff) if env.isdigit() and int(env) > 0 else aff)
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown CPU"
+
+
+def cpu_baseline_mt(obs, n, T, ess, scheme, threads, seed):
+    """All host cores (SURVEY.md §8(d) ii): the multi-threaded C port of the same fused run
+    (oracle/wsmc_port_mt.c, OpenMP over particles, gather-on-read + one trace-back), which the
+    tests hold bit-identical to the statement oracle. Returns (particle-steps/s, seconds)."""
+    sys.path.insert(0, str(REPO / "oracle"))
+    import oracle  # test infrastructure: only the cpu_baseline leg loads it
+    oracle.ssm2d_run_mt(min(n, 4096), obs[:2], seed=seed, ess_perc_min=ess, scheme=scheme, threads=threads,
+                        outputs=False)   # warm-up (thread pool, page faults of a small run)
+    t0 = time.perf_counter()
+    oracle.ssm2d_run_mt(n, obs[:T], seed=seed, ess_perc_min=ess, scheme=scheme, threads=threads, outputs=False)
+    dt = time.perf_counter() - t0
+    return n * T / dt, dt
+
+
+def cpu_baseline_1t(obs, n, T, ess, scheme, seed):
+    """One thread (SURVEY.md §8(d) i, the reference's own -t 1 methodology): the statement
+    oracle, i.e. the reference's algorithm with its eager ColumnStore gathers of every column
+    at each resample (src/stores.jl:105-128)."""
     sys.path.insert(0, str(REPO / "oracle"))
     from oracle import Oracle  # test infrastructure: only the cpu_baseline leg loads it
     import wsmc
-    o = Oracle(n, seed=42)
+    o = Oracle(n, seed=seed)
     t0 = time.perf_counter()
     wsmc.models.ssm2d_statements(o, obs[:T], ess_perc_min=ess, scheme=scheme)
     dt = time.perf_counter() - t0
@@ -173,10 +209,21 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:   # the baseline is an N=1 figure
-        cps, cdt = cpu_baseline(obs, args.cpu_particles, args.cpu_T, args.ess, scheme)
-        cpu = {"value": cps, "unit": "particle-steps/s", "cores": 1, "kind": "port",
-               "sample": f"oracle/ C restatement (eager ColumnStore gathers, 1 thread), 2D SSM "
-                         f"N={args.cpu_particles} T={args.cpu_T} ess_perc_min={args.ess}: {cdt:.2f} s"}
+        if scheme == abi.RESAMPLE_MULTINOMIAL:   # the MT port covers the strata (the reference's scheme)
+            cpu = None
+        else:
+            nth = cpu_threads(args.cpu_threads)
+            cps, cdt = cpu_baseline_mt(obs, args.cpu_particles, args.cpu_T, args.ess, scheme, nth, args.seed)
+            c1, c1dt = cpu_baseline_1t(obs, args.cpu_1t_particles, args.cpu_T, args.ess, scheme, args.seed)
+            cpu = {"value": cps, "unit": "particle-steps/s", "cores": nth, "kind": "port",
+                   "sample": f"oracle/wsmc_port_mt.c (OpenMP over particles, {nth} threads on {cpu_model()}): "
+                             f"the full 2D SSM run, N={args.cpu_particles} T={args.cpu_T} "
+                             f"ess_perc_min={args.ess}, history traced back: {cdt:.2f} s",
+                   "single_thread": {"value": c1, "unit": "particle-steps/s", "cores": 1, "kind": "port",
+                                     "sample": f"oracle/wsmc_oracle.c statements (the reference's eager "
+                                               f"ColumnStore gathers), N={args.cpu_1t_particles} "
+                                               f"T={args.cpu_T}: {c1dt:.2f} s"},
+                   "gpu_over_cpu": value / cps}
     if rank == 0:
         line = {
             "metric": METRIC,

@@ -98,6 +98,9 @@ _SIG = {
     "or_strat_word": (C.c_uint32, [C.c_uint64, C.c_uint64, C.c_uint64]),
     "or_qweight": (C.c_uint64, [C.c_double, C.c_double, C.c_int]),
     "or_qbits": (C.c_int, [C.c_uint64]),
+    "or_ssm2d_run_mt": (C.c_int, [C.c_int64, C.c_uint64, C.c_uint64, _D, _D, C.c_int32, _D, _D, C.c_double,
+                                  C.c_double, C.c_double, C.c_int32, C.c_int32, C.c_int32, _D, _D, _D, _D,
+                                  _I32P, _D]),
     "or_sizeof_term": (C.c_int32, []),
     "or_sizeof_dist": (C.c_int32, []),
 }
@@ -441,6 +444,42 @@ def philox(ctr, key):
 def log_evidence_records(records) -> float:
     r = np.ascontiguousarray(np.asarray(records, dtype=np.uint64).reshape(-1))
     return float(lib().or_log_evidence_records(r.ctypes.data_as(C.POINTER(C.c_uint64)), len(r) // 8))
+
+
+def ssm2d_run_mt(n, obs, seed=42, x0=(0.0, 0.0), v0=(1.0, 0.0), q_var=0.1, r_var=0.5, ess_perc_min=0.5,
+                 scheme=0, keep_history=True, threads=1, op_base=0, weights=None, outputs=True):
+    """The fused 2D SSM run (examples/2D_ssm.jl) on the CPU with OpenMP over particles
+    (oracle/wsmc_port_mt.c): the all-cores CPU baseline, bit-identical to the statements.
+    Returns a dict (columns SoA [2][N] like col_download, weights, flags, log_evidence);
+    with outputs=False nothing is copied out (the run, trace-back included, still happens)."""
+    obs = np.ascontiguousarray(np.asarray(obs, dtype=np.float64).reshape(-1, 2))
+    T = obs.shape[0]
+    x0a = np.asarray(x0, dtype=np.float64)
+    v0a = np.asarray(v0, dtype=np.float64)
+    w0 = None if weights is None else np.ascontiguousarray(np.asarray(weights, dtype=np.float64))
+    ncol = (T + 1) if keep_history else 1
+    xs = np.empty((ncol, 2, n)) if outputs else None
+    v = np.empty((2, n)) if outputs else None
+    dv = np.empty((2, n)) if outputs else None
+    w = np.empty(n) if outputs else None
+    flags = np.zeros(T, dtype=np.int32)
+    ev = C.c_double(0.0)
+    nul = C.cast(None, _D)
+    r = lib().or_ssm2d_run_mt(n, seed, op_base, _dptr(w0) if w0 is not None else nul, _dptr(obs), T,
+                              _dptr(x0a), _dptr(v0a), q_var, r_var, ess_perc_min, scheme, int(bool(keep_history)),
+                              threads, _dptr(xs) if outputs else nul, _dptr(v) if outputs else nul,
+                              _dptr(dv) if outputs else nul, _dptr(w) if outputs else nul,
+                              flags.ctypes.data_as(_I32P), C.byref(ev))
+    if r:
+        raise ValueError("or_ssm2d_run_mt: bad arguments or out of memory")
+    out = {"flags": flags.astype(bool), "log_evidence": ev.value}
+    if outputs:
+        if keep_history:
+            out.update({f"x_{t + 1}": xs[t] for t in range(T + 1)})
+        else:
+            out["x"] = xs[0]
+        out.update({"v": v, "dv": dv, "weights": w})
+    return out
 
 
 def canon_sum(vals) -> float:
