@@ -230,7 +230,7 @@ int wsmc_destroy(wsmc_ctx* c) {
     }
     void* bufs[] = {c->xchg, c->scache, c->scache_back, c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->cdf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount,
                     c->d_colptr, c->run_params, c->d_tape, c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp,
-                    c->vscratch, c->xscratch, c->run_pay, c->xp, c->comb, c->anc_out, c->xbuf, c->d_comp, c->d_ctape};
+                    c->vscratch, c->xscratch, c->run_pay, c->xp, c->comb, c->anc_out, c->xbuf, c->d_comp, c->d_ctape, c->d_prog};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (double* p : c->xrun)
@@ -1366,6 +1366,61 @@ static int sharded_autorw(wsmc_ctx* c, const int32_t* targets, int d, const doub
     return WSMC_OK;
 }
 
+// ---- the fold as a segment program (FoldProgram, csrc/wsmc_internal.h) ----------------
+static bool same_bits(double a, double b) { return std::memcmp(&a, &b, sizeof(double)) == 0; }
+static bool same_operand(const wsmc_operand& a, const wsmc_operand& b, bool c0, bool coef0, bool coef1) {
+    return (c0 || same_bits(a.c0, b.c0)) && (coef0 || same_bits(a.coef[0], b.coef[0])) &&
+           (coef1 || same_bits(a.coef[1], b.coef[1])) && a.col[0] == b.col[0] && a.col[1] == b.col[1] &&
+           a.comp[0] == b.comp[0] && a.comp[1] == b.comp[1];
+}
+static bool const_operand(const wsmc_operand& o) { return o.col[0] < 0 && o.col[1] < 0; }
+// the run kind a term can open: a scalar Normal whose scored value is a constant
+static int run_kind(const wsmc_term& t) {
+    if (t.dist.family != WSMC_FAM_NORMAL || t.dist.dim != 1 || !const_operand(t.x[0])) return kSegTerm;
+    return t.dist.mean_fn == WSMC_MEAN_OSCILLATOR ? kSegNormalOsc : kSegNormalAff;
+}
+// b continues a's run: everything equal except the run's per-term constants
+static bool same_run(const wsmc_term& a, const wsmc_term& b, int kind) {
+    if (run_kind(b) != kind || a.dist.mean_fn != b.dist.mean_fn) return false;
+    const bool osc = kind == kSegNormalOsc;
+    for (int k = 0; k < 4; ++k)
+        if (!same_operand(a.dist.mu[k], b.dist.mu[k], !osc && k == 0, !osc && k == 0, !osc && k == 0)) return false;
+    if (!same_operand(a.dist.scale, b.dist.scale, false, false, false)) return false;
+    if (!(osc || same_bits(a.dist.param[0], b.dist.param[0])) || !same_bits(a.dist.param[1], b.dist.param[1]))
+        return false;
+    return same_operand(a.x[0], b.x[0], true, false, false);   // x[0].c0 = the observation
+}
+// segments of terms [j0, j1) appended to segs (constants to cst); returns their count
+static int32_t compile_fold(const std::vector<wsmc_term>& ct, int32_t j0, int32_t j1, std::vector<FoldSeg>& segs,
+                            std::vector<double>& cst) {
+    const size_t s0 = segs.size();
+    for (int32_t j = j0; j < j1;) {
+        const int kind = run_kind(ct[j]);
+        int32_t e = j + 1;
+        if (kind != kSegTerm)
+            while (e < j1 && same_run(ct[j], ct[e], kind)) ++e;
+        if (kind == kSegTerm || e - j < 2) {
+            segs.push_back(FoldSeg{kSegTerm, 1, j, 0});
+            ++j;
+            continue;
+        }
+        segs.push_back(FoldSeg{kind, e - j, j, (int32_t)cst.size()});
+        for (int32_t k = j; k < e; ++k) {
+            const wsmc_term& t = ct[k];
+            if (kind == kSegNormalOsc) {
+                cst.push_back(t.dist.param[0]);
+            } else {
+                cst.push_back(t.dist.mu[0].c0);
+                cst.push_back(t.dist.mu[0].coef[0]);
+                cst.push_back(t.dist.mu[0].coef[1]);
+            }
+            cst.push_back(t.x[0].c0);
+        }
+        j = e;
+    }
+    return (int32_t)(segs.size() - s0);
+}
+
 int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, double step, const double* lo,
               const double* hi, int32_t target_depth, double diversity, int64_t* accepted_out) {
     CHECK_CTX(c);
@@ -1464,6 +1519,33 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         if (!ct.empty())
             WSMC_HIP(hipMemcpyAsync(c->d_ctape, ct.data(), sizeof(wsmc_term) * ct.size(), hipMemcpyHostToDevice,
                                     c->stream));
+        // the fold program: s_new over [0, kD), s_old over [cache_from or 0, kD)
+        std::vector<FoldSeg> segs;
+        std::vector<double> cst;
+        const int32_t nseg_new = compile_fold(ct, 0, kD, segs, cst);
+        const int32_t seg_old0 = (int32_t)segs.size();
+        const int32_t nseg_old = compile_fold(ct, cache_from >= 0 ? cache_from : 0, kD, segs, cst);
+        const size_t seg_bytes = sizeof(FoldSeg) * segs.size();
+        const size_t prog_bytes = seg_bytes + sizeof(double) * cst.size();
+        if ((int64_t)prog_bytes > c->d_prog_cap) {
+            int64_t cap = c->d_prog_cap ? c->d_prog_cap : 4096;
+            while (cap < (int64_t)prog_bytes) cap *= 2;
+            WSMC_HIP(hipStreamSynchronize(c->stream));
+            if (c->d_prog) WSMC_HIP(hipFree(c->d_prog));
+            WSMC_HIP(hipMalloc(&c->d_prog, cap));
+            c->d_prog_cap = cap;
+        }
+        std::vector<char> hprog(prog_bytes);
+        if (seg_bytes) std::memcpy(hprog.data(), segs.data(), seg_bytes);
+        if (!cst.empty()) std::memcpy(hprog.data() + seg_bytes, cst.data(), sizeof(double) * cst.size());
+        if (prog_bytes)
+            WSMC_HIP(hipMemcpyAsync(c->d_prog, hprog.data(), prog_bytes, hipMemcpyHostToDevice, c->stream));
+        FoldProgram prog;
+        prog.seg_new = reinterpret_cast<const FoldSeg*>(c->d_prog);
+        prog.seg_old = reinterpret_cast<const FoldSeg*>(c->d_prog) + seg_old0;
+        prog.nseg_new = nseg_new;
+        prog.nseg_old = nseg_old;
+        prog.cst = reinterpret_cast<const double*>(reinterpret_cast<const char*>(c->d_prog) + seg_bytes);
         FoldSlots fs{};
         fs.n = (int32_t)slots.size();
         for (const auto& t : ct) fs.heavy |= t.dist.mean_fn == WSMC_MEAN_OSCILLATOR ? 1 : 0;
@@ -1472,7 +1554,7 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         for (int k = 0; k < d; ++k) fs.t[k] = c->cols[targets[k]].front;
         WSMC_HIP(launch_move_c(c->stream, c->d_ctape, kD, target_depth, fs, targets, d, bounded ? l : nullptr,
                                bounded ? h : nullptr, bounded ? 1 : 0, c->mom + 32, c->seed, op_prop, op_acc, c->goff,
-                               c->N, c->ucount, mflag, c->scache, cache_from));
+                               c->N, c->ucount, mflag, c->scache, cache_from, prog));
     } else {
         WSMC_HIP(launch_move(c->stream, c->d_tape, (int32_t)c->tape.size(), target_depth, c->d_colptr, targets, d,
                              bounded ? l : nullptr, bounded ? h : nullptr, bounded ? 1 : 0, c->mom + 32, c->seed,

@@ -153,6 +153,8 @@ struct wsmc_ctx {
     int32_t* lineage[2] = {};                // [N] global lineage ids (distributed trace-back)
     wsmc_term* d_ctape = nullptr;           // compiled Move tape (slot operands)
     int64_t d_ctape_cap = 0;
+    void* d_prog = nullptr;                 // compiled fold program: segments, then constants
+    int64_t d_prog_cap = 0;                 // bytes
     size_t d_comp_cap = 0;
     double* tilepart = nullptr;             // [16 * ntiles] canonical-sum tile partials
     wsmc::MaxSlots* mslots = nullptr;       // [1] max slots of one generic resample / evidence
@@ -248,10 +250,29 @@ struct FoldSlots {
     int32_t n;
     int32_t heavy;                 // transcendental-heavy terms (oscillator means): one particle per thread
 };
+// The fold as a program of segments over the compiled tape: a run of consecutive Normal
+// terms that differ only in their constants (the observations of a model's loop, e.g.
+// examples/damped_oscillator.jl:36 or examples/linear_regression.jl:21) is one segment whose
+// per-particle invariants (the mean's column reads, sigma and its log) are evaluated once;
+// its terms' constants are packed in `cst`. Every other term is a one-term segment.
+enum { kSegTerm = 0, kSegNormalOsc = 1, kSegNormalAff = 2 };
+struct FoldSeg {
+    int32_t kind;
+    int32_t count;   // terms in the segment
+    int32_t tmpl;    // index of its first term in the compiled tape
+    int32_t coff;    // offset of its constants: Osc (t, y) per term; Aff (c0, coef0, coef1, y) per term
+};
+struct FoldProgram {
+    const FoldSeg* seg_new;    // the s_new fold, terms [0, n)
+    const FoldSeg* seg_old;    // the s_old fold, terms [cache_from or 0, n)
+    int32_t nseg_new, nseg_old;
+    const double* cst;
+};
 hipError_t launch_move_c(hipStream_t s, const wsmc_term* ctape, int32_t nterms, int32_t depth, const FoldSlots& fs,
                          const int32_t* tcols, int d, const double* lo, const double* hi, int bounded,
                          const double* L, uint64_t seed, uint64_t op_prop, uint64_t op_acc, int64_t goff, int64_t N,
-                         unsigned long long* accepted, const int32_t* flag, double* scache, int32_t cache_from);
+                         unsigned long long* accepted, const int32_t* flag, double* scache, int32_t cache_from,
+                         const FoldProgram& prog);
 // exact-sharded fused run: contiguous slices of (x pair, ancestor) by global index for the
 // distributed trace-back, the lineage lookup, pairs -> SoA
 hipError_t launch_trace_pack(hipStream_t s, const double* xpairs, const int32_t* arow, int64_t start, int64_t count,

@@ -1340,21 +1340,81 @@ __global__ __launch_bounds__(kBlock) void k_move(const wsmc_term* tape, int32_t 
 // loads independent, in flight together — into LDS, and the shared fold (include/
 // wsmc_terms.h, unchanged arithmetic) reads them through LDS slot pointers. The generic
 // fold's per-term chain term -> column pointer -> global value becomes LDS reads.
-// K particles per thread: the tape is walked once per thread for K particles, so the
+// K particles per thread: the program is walked once per thread for K particles, so the
 // interpreter's serial chain of scalar term loads and branches (what the one-particle
 // kernel waits on: VALU active 10%) is shared; each particle keeps its own accumulator and
 // log memo, so every fold is the same left fold as wsmc_fold / wsmc_fold_from.
+//
+// The fold runs a segment program (FoldProgram): one-term segments go through the shared
+// term evaluator; a run segment evaluates its per-particle invariants once and then only the
+// per-term arithmetic, its constants read as wave-uniform scalars. Every term's arithmetic is
+// wsmc_term_logpdf_m's (the same operations in the same order, the same log memo), so the
+// fold is bit-identical to the term-by-term one.
 template <int K>
-__device__ __forceinline__ void fold_k(double (&s)[K], const wsmc_term* tape, int32_t j0, int32_t n, int32_t depth,
-                                       double* const* cols, const int (&ix)[K], const bool (&ok)[K]) {
+__device__ __forceinline__ void fold_seg(double (&s)[K], const wsmc_term* tape, const FoldSeg* segs, int32_t nseg,
+                                         const double* __restrict__ cst, double* const* cols, const int (&ix)[K],
+                                         const bool (&ok)[K]) {
     wsmc_logmemo lm[K];
 #pragma unroll
     for (int p = 0; p < K; ++p) lm[p] = wsmc_logmemo{0, 0.0, 0};
-    for (int32_t j = j0; j < n; ++j) {
-        if (tape[j].depth >= depth) break;
+    for (int32_t g = 0; g < nseg; ++g) {
+        const FoldSeg sg = segs[g];
+        const wsmc_term* tp = &tape[sg.tmpl];
+        if (sg.kind == kSegNormalOsc) {
+            // Normal(A exp(-gamma t) cos(omega t + phi), sigma) observed at y, over (t, y) pairs
+            double A[K], om[K], ga[K], ph[K], sd[K], lsd[K];
+#pragma unroll
+            for (int p = 0; p < K; ++p) {
+                A[p] = wsmc_operand_eval(&tp->dist.mu[0], cols, 0, ix[p], nullptr);
+                om[p] = wsmc_operand_eval(&tp->dist.mu[1], cols, 0, ix[p], nullptr);
+                ga[p] = wsmc_operand_eval(&tp->dist.mu[2], cols, 0, ix[p], nullptr);
+                ph[p] = wsmc_operand_eval(&tp->dist.mu[3], cols, 0, ix[p], nullptr);
+                sd[p] = wsmc_operand_eval(&tp->dist.scale, cols, 0, ix[p], nullptr);
+                lsd[p] = wsmc_log_memo(&lm[p], sd[p]);
+            }
+            const double* c = cst + sg.coff;
+            for (int32_t k = 0; k < sg.count; ++k) {
+                const double t = c[2 * k], y = c[2 * k + 1];
+#pragma unroll
+                for (int p = 0; p < K; ++p) {
+                    if (!ok[p]) continue;
+                    const double mu = wsmc_oscillator(t, A[p], om[p], ga[p], ph[p]);
+                    const double z = (y - mu) / sd[p];
+                    s[p] = s[p] + (-(z * z + WSMC_LOG2PI) * 0.5 - lsd[p]);
+                }
+            }
+            continue;
+        }
+        if (sg.kind == kSegNormalAff) {
+            // Normal(c0 + coef0 col0 + coef1 col1, sigma) observed at y, over (c0, coef0, coef1, y)
+            const wsmc_operand& m = tp->dist.mu[0];
+            const bool h0 = m.col[0] >= 0, h1 = m.col[1] >= 0;
+            double v0[K], v1[K], sd[K], lsd[K];
+#pragma unroll
+            for (int p = 0; p < K; ++p) {
+                v0[p] = h0 ? cols[m.col[0]][ix[p]] : 0.0;
+                v1[p] = h1 ? cols[m.col[1]][ix[p]] : 0.0;
+                sd[p] = wsmc_operand_eval(&tp->dist.scale, cols, 0, ix[p], nullptr);
+                lsd[p] = wsmc_log_memo(&lm[p], sd[p]);
+            }
+            const double* c = cst + sg.coff;
+            for (int32_t k = 0; k < sg.count; ++k) {
+                const double c0 = c[4 * k], a0 = c[4 * k + 1], a1 = c[4 * k + 2], y = c[4 * k + 3];
+#pragma unroll
+                for (int p = 0; p < K; ++p) {
+                    if (!ok[p]) continue;
+                    double mu = c0;
+                    if (h0) mu = mu + a0 * v0[p];
+                    if (h1) mu = mu + a1 * v1[p];
+                    const double z = (y - mu) / sd[p];
+                    s[p] = s[p] + (-(z * z + WSMC_LOG2PI) * 0.5 - lsd[p]);
+                }
+            }
+            continue;
+        }
 #pragma unroll
         for (int p = 0; p < K; ++p)
-            if (ok[p]) s[p] = s[p] + wsmc_term_logpdf_m(&tape[j], cols, 0, ix[p], nullptr, &lm[p]);
+            if (ok[p]) s[p] = s[p] + wsmc_term_logpdf_m(tp, cols, 0, ix[p], nullptr, &lm[p]);
     }
 }
 
@@ -1366,7 +1426,7 @@ __global__ __launch_bounds__(kBlock) void k_move_c(const wsmc_term* ctape, int32
                                                    FoldSlots fs, MomArgs ma, int d, int bounded, const double* Lm,
                                                    uint64_t seed, uint64_t op_prop, uint64_t op_acc, int64_t goff,
                                                    int64_t N, u64* accepted, const int32_t* flag, double* scache,
-                                                   int32_t cache_from) {
+                                                   int32_t cache_from, FoldProgram prog) {
     constexpr int W = K * kBlock;            // LDS row length
     extern __shared__ double sv[];           // [fs.n][W] current values, then [4][W] proposals
     __shared__ double* sp[kFoldSlots];
@@ -1423,8 +1483,8 @@ __global__ __launch_bounds__(kBlock) void k_move_c(const wsmc_term* ctape, int32
         }
     }
     // s_old: the carried score continued over the new terms, or the full fold
-    fold_k<K>(so, ctape, cache_from >= 0 ? cache_from : 0, nterms, depth, sp, ix, ok);
-    fold_k<K>(sn, ctape, 0, nterms, depth, spn, ix, ok);
+    fold_seg<K>(so, ctape, prog.seg_old, prog.nseg_old, prog.cst, sp, ix, ok);
+    fold_seg<K>(sn, ctape, prog.seg_new, prog.nseg_new, prog.cst, spn, ix, ok);
     u64 acc = 0;
 #pragma unroll
     for (int p = 0; p < K; ++p) {
@@ -2059,7 +2119,8 @@ hipError_t launch_move(hipStream_t s, const wsmc_term* tape, int32_t nterms, int
 hipError_t launch_move_c(hipStream_t s, const wsmc_term* ctape, int32_t nterms, int32_t depth, const FoldSlots& fs,
                          const int32_t* tcols, int d, const double* lo, const double* hi, int bounded,
                          const double* L, uint64_t seed, uint64_t op_prop, uint64_t op_acc, int64_t goff, int64_t N,
-                         u64* accepted, const int32_t* flag, double* scache, int32_t cache_from) {
+                         u64* accepted, const int32_t* flag, double* scache, int32_t cache_from,
+                         const FoldProgram& prog) {
     MomArgs ma;
     for (int k = 0; k < 4; ++k) {
         ma.tcol[k] = k < d ? tcols[k] : 0;
@@ -2073,11 +2134,11 @@ hipError_t launch_move_c(hipStream_t s, const wsmc_term* ctape, int32_t nterms, 
     if (fs.heavy) {
         const dim3 g((unsigned)((N + kBlock - 1) / kBlock));
         hipLaunchKernelGGL(k_move_c<1>, g, dim3(kBlock), row, s, ctape, nterms, depth, fs, ma, d, bounded, L, seed,
-                           op_prop, op_acc, goff, N, accepted, flag, scache, cache_from);
+                           op_prop, op_acc, goff, N, accepted, flag, scache, cache_from, prog);
     } else {
         const dim3 g((unsigned)((N + 2 * kBlock - 1) / (2 * kBlock)));
         hipLaunchKernelGGL(k_move_c<2>, g, dim3(kBlock), 2 * row, s, ctape, nterms, depth, fs, ma, d, bounded, L,
-                           seed, op_prop, op_acc, goff, N, accepted, flag, scache, cache_from);
+                           seed, op_prop, op_acc, goff, N, accepted, flag, scache, cache_from, prog);
     }
     return hipGetLastError();
 }
