@@ -2131,7 +2131,11 @@ hipError_t launch_move_c(hipStream_t s, const wsmc_term* ctape, int32_t nterms, 
     // C3 3.7 vs 4.3 ms per run), 1 when they are transcendental-heavy (occupancy wins: C5
     // 0.76 vs 0.88 s); 4 was slower for both
     const size_t row = sizeof(double) * kBlock * (size_t)(fs.n + 4);
-    if (fs.heavy) {
+    static const int kdiag = [] {   // diagnostics only: force 1 or 2 particles per thread
+        const char* e = getenv("WSMC_DIAG_MOVE_K");
+        return e ? atoi(e) : 0;
+    }();
+    if (kdiag == 1 || (kdiag != 2 && fs.heavy)) {
         const dim3 g((unsigned)((N + kBlock - 1) / kBlock));
         hipLaunchKernelGGL(k_move_c<1>, g, dim3(kBlock), row, s, ctape, nterms, depth, fs, ma, d, bounded, L, seed,
                            op_prop, op_acc, goff, N, accepted, flag, scache, cache_from, prog);
