@@ -294,17 +294,18 @@ WSMC_HD double wsmc_cos(double x) {
                  p2 = 6.07710050630396597660e-11,   /* next 33 bits */
                  p3 = 2.02226624879595063154e-21;   /* pi/2 - p1 - p2 */
     if (!wsmc_isfinite(x)) return WSMC_NAN;
-    double ax = wsmc_fabs(x);
-    if (ax <= 7.85398163397448278999e-01) return wsmc_kcos(x);
-    double fn = (double)(int64_t)(ax * invpio2 + 0.5);
-    double r = ((ax - fn * p1) - fn * p2) - fn * p3;
-    int n = (int)((int64_t)fn & 3);
-    switch (n) {
-        case 0: return wsmc_kcos(r);
-        case 1: return -wsmc_ksin(r);
-        case 2: return -wsmc_kcos(r);
-        default: return wsmc_ksin(r);
-    }
+    /* branch-free on the value path (a wave's lanes sit in different quadrants): both
+       kernel polynomials, then selects; |x| <= pi/4 is quadrant 0 with r = x. The values
+       are those of the branchy form (kcos(x) for small |x|, else the quadrant's kernel). */
+    const double ax = wsmc_fabs(x);
+    const int small = ax <= 7.85398163397448278999e-01;
+    const double fn = (double)(int64_t)(ax * invpio2 + 0.5);
+    const double rr = ((ax - fn * p1) - fn * p2) - fn * p3;
+    const double r = small ? x : rr;
+    const int n = small ? 0 : (int)((int64_t)fn & 3);
+    const double kc = wsmc_kcos(r), ks = wsmc_ksin(r);
+    const double v = (n & 1) ? ks : kc;
+    return ((n + 1) & 2) ? -v : v;   /* n = 1, 2 negate */
 }
 
 /* ------------------------------------------------------------------------- */
