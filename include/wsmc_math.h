@@ -273,18 +273,12 @@ WSMC_HD void wsmc_sincos2pi(double u, double* s, double* c) {
     if (o & 1) f = 1.0 - f;
     double t = f * PIO4;
     double st = wsmc_ksin(t), ct = wsmc_kcos(t);
-    double cs, sn;
-    switch (o & 7) {
-        case 0: cs = ct;  sn = st;  break;
-        case 1: cs = st;  sn = ct;  break;
-        case 2: cs = -st; sn = ct;  break;
-        case 3: cs = -ct; sn = st;  break;
-        case 4: cs = -ct; sn = -st; break;
-        case 5: cs = -st; sn = -ct; break;
-        case 6: cs = st;  sn = -ct; break;
-        default: cs = ct; sn = -st; break;
-    }
-    *s = sn; *c = cs;
+    /* octant o: (cos, sin) = (ct, st), (st, ct), (-st, ct), (-ct, st), (-ct, -st), (-st, -ct),
+       (st, -ct), (ct, -st) for o = 0..7 — as selects, no divergent switch */
+    const int swap = ((o + 1) & 2) != 0;            /* o = 1, 2, 5, 6 */
+    const double a = swap ? st : ct, b = swap ? ct : st;
+    *c = ((o + 2) & 4) ? -a : a;                    /* o = 2..5 */
+    *s = (o & 4) ? -b : b;                          /* o = 4..7 */
 }
 
 /* cos(x) for |x| < 2^19*pi/2 (Cody–Waite three-part pi/2); NaN/inf -> NaN */
