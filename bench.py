@@ -88,26 +88,62 @@ def cpu_model() -> str:
     return "unknown CPU"
 
 
-def cpu_baseline_mt(obs, n, T, ess, scheme, threads, seed):
-    """All host cores (SURVEY.md §8(d) ii): the multi-threaded C port of the same fused run
-    (oracle/wsmc_port_mt.c, OpenMP over particles, gather-on-read + one trace-back), which the
-    tests hold bit-identical to the statement oracle. Returns (particle-steps/s, seconds)."""
+def _oracle():
     sys.path.insert(0, str(REPO / "oracle"))
     import oracle  # test infrastructure: only the cpu_baseline leg loads it
-    oracle.ssm2d_run_mt(min(n, 4096), obs[:2], seed=seed, ess_perc_min=ess, scheme=scheme, threads=threads,
-                        outputs=False)   # warm-up (thread pool, page faults of a small run)
+    return oracle
+
+
+def cpu_baseline_mt(obs, n, T, ess, scheme, threads, seed):
+    """The bit-exact all-cores port of the same fused run (oracle/wsmc_port_mt.c, OpenMP over
+    particles, gather-on-read + one trace-back), which the tests hold bit-identical to the
+    statement oracle and so to the device. Returns (particle-steps/s, seconds)."""
+    oracle = _oracle()
+    oracle.keep_heap()
+    oracle.ssm2d_run_mt(n, obs[:T], seed=seed, ess_perc_min=ess, scheme=scheme, threads=threads,
+                        outputs=False)   # warm-up: thread pool, first touch of the run's buffers
     t0 = time.perf_counter()
     oracle.ssm2d_run_mt(n, obs[:T], seed=seed, ess_perc_min=ess, scheme=scheme, threads=threads, outputs=False)
     dt = time.perf_counter() - t0
     return n * T / dt, dt
 
 
+def cpu_baseline_fast(obs, n, T, ess, threads, seed):
+    """The reference's algorithm at the reference's speed (oracle/wsmc_port_fast.c:
+    xoshiro256++ + ziggurat normals, libm, the f64 icdf merge; statistically, not bitwise,
+    equal — tests/test_port_fast.py), the same fused organisation (gather-on-read, one
+    trace-back). The fastest CPU implementation here, hence the baseline `value` (SURVEY.md
+    §8(d) ii with threads = all host cores, i with threads = 1)."""
+    oracle = _oracle()
+    oracle.keep_heap()
+    oracle.fast_ssm2d_run(n, obs[:T], ess_perc_min=ess, seed=seed, threads=threads)   # warm-up (first touch)
+    t0 = time.perf_counter()
+    oracle.fast_ssm2d_run(n, obs[:T], ess_perc_min=ess, seed=seed, threads=threads)
+    dt = time.perf_counter() - t0
+    return n * T / dt, dt
+
+
+def cpu_fairness_lgssm(n=100_000, T=200, seed=42):
+    """SURVEY.md §8(d) CPU-baseline sanity check: the same fast port on the reference's own
+    benchmark model (benchmarks/ssm/WeightedSampling/lgssm1d.jl, forced resampling), 1
+    thread, N = 1e5, against the reference's published 5.30e7 particle-steps/s
+    (benchmarks/ssm/results/grid_results.csv:46)."""
+    oracle = _oracle()
+    import wsmc
+    data = wsmc.models.lgssm1d_data(T, seed=seed)
+    oracle.keep_heap()
+    oracle.fast_lgssm1d_run(n, data[:10], ess_perc_min=1.0, seed=seed, threads=1)   # warm-up (first touch)
+    t0 = time.perf_counter()
+    oracle.fast_lgssm1d_run(n, data, ess_perc_min=1.0, seed=seed, threads=1)
+    dt = time.perf_counter() - t0
+    return n * T / dt, dt
+
+
 def cpu_baseline_1t(obs, n, T, ess, scheme, seed):
-    """One thread (SURVEY.md §8(d) i, the reference's own -t 1 methodology): the statement
-    oracle, i.e. the reference's algorithm with its eager ColumnStore gathers of every column
-    at each resample (src/stores.jl:105-128)."""
-    sys.path.insert(0, str(REPO / "oracle"))
-    from oracle import Oracle  # test infrastructure: only the cpu_baseline leg loads it
+    """One thread, bit-exact: the statement oracle, i.e. the reference's algorithm with its
+    eager ColumnStore gathers of every column at each resample (src/stores.jl:105-128)."""
+    from oracle import Oracle  # noqa: F401  (path set by _oracle)
+    _oracle()
     import wsmc
     o = Oracle(n, seed=seed)
     t0 = time.perf_counter()
@@ -213,17 +249,33 @@ def main():
             cpu = None
         else:
             nth = cpu_threads(args.cpu_threads)
-            cps, cdt = cpu_baseline_mt(obs, args.cpu_particles, args.cpu_T, args.ess, scheme, nth, args.seed)
-            c1, c1dt = cpu_baseline_1t(obs, args.cpu_1t_particles, args.cpu_T, args.ess, scheme, args.seed)
-            cpu = {"value": cps, "unit": "particle-steps/s", "cores": nth, "kind": "port",
-                   "sample": f"oracle/wsmc_port_mt.c (OpenMP over particles, {nth} threads on {cpu_model()}): "
-                             f"the full 2D SSM run, N={args.cpu_particles} T={args.cpu_T} "
-                             f"ess_perc_min={args.ess}, history traced back: {cdt:.2f} s",
-                   "single_thread": {"value": c1, "unit": "particle-steps/s", "cores": 1, "kind": "port",
-                                     "sample": f"oracle/wsmc_oracle.c statements (the reference's eager "
-                                               f"ColumnStore gathers), N={args.cpu_1t_particles} "
-                                               f"T={args.cpu_T}: {c1dt:.2f} s"},
-                   "gpu_over_cpu": value / cps}
+            n, T = args.cpu_particles, args.cpu_T
+            fps, fdt = cpu_baseline_fast(obs, n, T, args.ess, nth, args.seed)
+            f1, f1dt = cpu_baseline_fast(obs, args.cpu_1t_particles, T, args.ess, 1, args.seed)
+            cps, cdt = cpu_baseline_mt(obs, n, T, args.ess, scheme, nth, args.seed)
+            c1, c1dt = cpu_baseline_1t(obs, args.cpu_1t_particles, T, args.ess, scheme, args.seed)
+            lg, lgdt = cpu_fairness_lgssm()
+            cpu = {"value": fps, "unit": "particle-steps/s", "cores": nth, "kind": "port",
+                   "sample": f"oracle/wsmc_port_fast.c (the reference's algorithm with xoshiro256++/ziggurat/"
+                             f"libm, OpenMP over particles, {nth} threads on {cpu_model()}): the full 2D SSM "
+                             f"run, N={n} T={T} ess_perc_min={args.ess}, history traced back: {fdt:.2f} s",
+                   "single_thread": {"value": f1, "unit": "particle-steps/s", "cores": 1, "kind": "port",
+                                     "sample": f"oracle/wsmc_port_fast.c, 1 thread, N={args.cpu_1t_particles} "
+                                               f"T={T}: {f1dt:.2f} s"},
+                   "exact_port": {"value": cps, "unit": "particle-steps/s", "cores": nth, "kind": "port",
+                                  "sample": f"oracle/wsmc_port_mt.c (bit-identical to the device), {nth} threads, "
+                                            f"N={n} T={T}: {cdt:.2f} s"},
+                   "exact_single_thread": {"value": c1, "unit": "particle-steps/s", "cores": 1, "kind": "port",
+                                           "sample": f"oracle/wsmc_oracle.c statements (the reference's eager "
+                                                     f"ColumnStore gathers), N={args.cpu_1t_particles} T={T}: "
+                                                     f"{c1dt:.2f} s"},
+                   "fairness_lgssm1d_1t": {"value": lg, "unit": "particle-steps/s", "cores": 1,
+                                           "reference_published": 5.30e7,
+                                           "ratio": lg / 5.30e7,
+                                           "sample": "oracle/wsmc_port_fast.c on benchmarks/ssm/WeightedSampling/"
+                                                     f"lgssm1d.jl, N=100000 T=200 forced, 1 thread: {lgdt:.2f} s"},
+                   "gpu_over_cpu": value / fps,
+                   "gpu_over_exact_port": value / cps}
     if rank == 0:
         line = {
             "metric": METRIC,

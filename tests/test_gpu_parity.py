@@ -95,6 +95,18 @@ def test_ssm1d_statements(gpu_available):
 
 
 @pytest.mark.parametrize("ess", [1.0, 0.5])
+def test_lgssm1d_statements(gpu_available, ess):
+    """The reference's own benchmark model (benchmarks/ssm/WeightedSampling/lgssm1d.jl): the
+    sampled column is rebound (read and written by the same Sample)."""
+    data = models.lgssm1d_data(30)
+    g, o = wsmc.Context(3001, seed=42), Oracle(3001, seed=42)
+    assert models.lgssm1d_statements(g, data, ess_perc_min=ess) == models.lgssm1d_statements(o, data, ess_perc_min=ess)
+    np.testing.assert_array_equal(g.last_ancestors(), o.last_ancestors())
+    assert_same_state(g, o)
+    assert g.log_evidence() == o.log_evidence()
+
+
+@pytest.mark.parametrize("ess", [1.0, 0.5])
 def test_linreg_autorw(gpu_available, ess):
     xs, ys = models.linreg_data()
     g, o = wsmc.Context(20000, seed=42), Oracle(20000, seed=42)

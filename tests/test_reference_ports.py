@@ -283,3 +283,21 @@ def test_ssm1d_kalman(backend):
     ctx = make_state(backend, N, seed=7).ctx
     wsmc.models.ssm1d_statements(ctx, obs)
     assert abs(ctx.log_evidence() - ev_exact / 2) < 1.0
+
+
+# benchmarks/ssm/WeightedSampling/lgssm1d.jl (the reference's own CPU benchmark model) ----
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_lgssm1d_kalman(backend):
+    """x ~ Normal(0.9x, 1), y => Normal(x, 0.5), forced resampling (benchmarks/ssm/README.md:13-16),
+    against the exact filter of benchmarks/ssm/simulate.jl:41-59."""
+    T, N = 100, 50_000
+    data = wsmc.models.lgssm1d_data(T)
+    exact_mean, exact_ev = kalman_filter_evidence(data, 0.9, 1.0, 0.5)
+    ctx = make_state(backend, N, seed=42).ctx
+    flags = wsmc.models.lgssm1d_statements(ctx, data, ess_perc_min=1.0)
+    assert all(flags)
+    assert ctx.col_names() == ["x"]                # x is rebound: one column, no history
+    w = exp_norm(ctx.weights_download())
+    x = ctx.col_download(ctx.col_find("x"))
+    assert abs(np.sum(w * x) - exact_mean) < 0.05
+    assert abs(ctx.log_evidence() - exact_ev) < 1.0

@@ -7,6 +7,7 @@ context protocol (``wsmc.Context`` on the GPU). Column creation order, depth,
 score-tape and RNG stream positions therefore match the fused runners.
 
     ssm1d_statements       examples/1D_ssm.jl:7-16
+    lgssm1d_statements     benchmarks/ssm/WeightedSampling/lgssm1d.jl:18-24 (the reference's own CPU benchmark)
     ssm2d_statements       examples/2D_ssm.jl:7-17
     linreg_statements      examples/linear_regression.jl:17-27
     oscillator_statements  examples/damped_oscillator.jl:30-43
@@ -83,6 +84,26 @@ def ssm1d_statements(ctx, obs, q_sd=0.1, r_sd=1.0, ess_perc_min=0.5, scheme=abi.
     return resampled
 
 
+def lgssm1d_statements(ctx, data, a=0.9, q=1.0, r=0.5, x0_std=1.0, ess_perc_min=1.0,
+                       scheme=abi.RESAMPLE_STRATIFIED):
+    """The reference's own CPU benchmark model, benchmarks/ssm/WeightedSampling/lgssm1d.jl:18-24:
+    x ~ Normal(0, x0_std); for y in data: x ~ Normal(a x, q); y => Normal(x, r); end.
+    `x` is rebound, so the store keeps one column (no history), and every `~`/`=>` is
+    followed by its auto-inserted Resample (a no-op after a Sample)."""
+    R = resolver(ctx)
+    cx = ctx.col_create("x", 1)
+    ctx.sample(cx, Normal(0.0, x0_std).dist(R))
+    ctx.resample(ess_perc_min, scheme)
+    resampled = []
+    for y in np.asarray(data, dtype=float):
+        ctx.sample(cx, Normal(Col("x") * a, q).dist(R))                     # x ~ Normal(a*x, q)
+        ctx.resample(ess_perc_min, scheme)
+        ctx.observe(Normal(Col("x"), r).dist(R), _const([y]))               # y => Normal(x, r)
+        rs, _ = ctx.resample(ess_perc_min, scheme)
+        resampled.append(rs)
+    return resampled
+
+
 def linreg_statements(ctx, xs, ys, prior_sd=10.0, obs_sd=1.0, ess_perc_min=0.5,
                       scheme=abi.RESAMPLE_STRATIFIED, min_step=1e-3):
     """examples/linear_regression.jl:17-27: α, β ~ N(0,10); y => N(α + β x, 1);
@@ -152,6 +173,17 @@ def ssm1d_data(T: int, seed: int = 7):
     for t in range(T):
         obs[t] = x + 1.0 * rng.standard_normal()
         x, v = x + v, v + 0.1 * rng.standard_normal()
+    return obs
+
+
+def lgssm1d_data(T: int, a=0.9, q=1.0, r=0.5, x0_std=1.0, seed: int = 42):
+    """benchmarks/ssm/simulate.jl:21-31 (simulate_lgssm1d) on numpy's Philox stream."""
+    rng = np.random.Generator(np.random.Philox(seed))
+    x = x0_std * rng.standard_normal()
+    obs = np.empty(T)
+    for t in range(T):
+        x = a * x + q * rng.standard_normal()
+        obs[t] = x + r * rng.standard_normal()
     return obs
 
 
