@@ -255,27 +255,32 @@ def main():
             cps, cdt = cpu_baseline_mt(obs, n, T, args.ess, scheme, nth, args.seed)
             c1, c1dt = cpu_baseline_1t(obs, args.cpu_1t_particles, T, args.ess, scheme, args.seed)
             lg, lgdt = cpu_fairness_lgssm()
-            cpu = {"value": fps, "unit": "particle-steps/s", "cores": nth, "kind": "port",
-                   "sample": f"oracle/wsmc_port_fast.c (the reference's algorithm with xoshiro256++/ziggurat/"
-                             f"libm, OpenMP over particles, {nth} threads on {cpu_model()}): the full 2D SSM "
-                             f"run, N={n} T={T} ess_perc_min={args.ess}, history traced back: {fdt:.2f} s",
-                   "single_thread": {"value": f1, "unit": "particle-steps/s", "cores": 1, "kind": "port",
-                                     "sample": f"oracle/wsmc_port_fast.c, 1 thread, N={args.cpu_1t_particles} "
-                                               f"T={T}: {f1dt:.2f} s"},
-                   "exact_port": {"value": cps, "unit": "particle-steps/s", "cores": nth, "kind": "port",
-                                  "sample": f"oracle/wsmc_port_mt.c (bit-identical to the device), {nth} threads, "
-                                            f"N={n} T={T}: {cdt:.2f} s"},
-                   "exact_single_thread": {"value": c1, "unit": "particle-steps/s", "cores": 1, "kind": "port",
-                                           "sample": f"oracle/wsmc_oracle.c statements (the reference's eager "
-                                                     f"ColumnStore gathers), N={args.cpu_1t_particles} T={T}: "
-                                                     f"{c1dt:.2f} s"},
-                   "fairness_lgssm1d_1t": {"value": lg, "unit": "particle-steps/s", "cores": 1,
-                                           "reference_published": 5.30e7,
-                                           "ratio": lg / 5.30e7,
-                                           "sample": "oracle/wsmc_port_fast.c on benchmarks/ssm/WeightedSampling/"
-                                                     f"lgssm1d.jl, N=100000 T=200 forced, 1 thread: {lgdt:.2f} s"},
-                   "gpu_over_cpu": value / fps,
-                   "gpu_over_exact_port": value / cps}
+            fast = {"value": fps, "unit": "particle-steps/s", "cores": nth, "kind": "port",
+                    "sample": f"oracle/wsmc_port_fast.c (the reference's algorithm with xoshiro256++/ziggurat/"
+                              f"libm, OpenMP over particles, {nth} threads on {cpu_model()}): the full 2D SSM "
+                              f"run, N={n} T={T} ess_perc_min={args.ess}, history traced back: {fdt:.2f} s"}
+            exact = {"value": cps, "unit": "particle-steps/s", "cores": nth, "kind": "port",
+                     "sample": f"oracle/wsmc_port_mt.c (bit-identical to the device; OpenMP over particles, "
+                               f"{nth} threads on {cpu_model()}): the full 2D SSM run, N={n} T={T} "
+                               f"ess_perc_min={args.ess}, history traced back: {cdt:.2f} s"}
+            # the baseline is the faster of the two all-cores ports; the other is reported beside it
+            best, other, other_key = (fast, exact, "exact_port") if fps >= cps else (exact, fast, "fast_port")
+            cpu = dict(best)
+            cpu.update({
+                other_key: other,
+                "single_thread": {"value": f1, "unit": "particle-steps/s", "cores": 1, "kind": "port",
+                                  "sample": f"oracle/wsmc_port_fast.c, 1 thread, N={args.cpu_1t_particles} "
+                                            f"T={T}: {f1dt:.2f} s"},
+                "exact_single_thread": {"value": c1, "unit": "particle-steps/s", "cores": 1, "kind": "port",
+                                        "sample": f"oracle/wsmc_oracle.c statements (the reference's eager "
+                                                  f"ColumnStore gathers), N={args.cpu_1t_particles} T={T}: "
+                                                  f"{c1dt:.2f} s"},
+                "fairness_lgssm1d_1t": {"value": lg, "unit": "particle-steps/s", "cores": 1,
+                                        "reference_published": 5.30e7, "ratio": lg / 5.30e7,
+                                        "sample": "oracle/wsmc_port_fast.c on benchmarks/ssm/WeightedSampling/"
+                                                  f"lgssm1d.jl, N=100000 T=200 forced, 1 thread: {lgdt:.2f} s"},
+                "gpu_over_cpu": value / best["value"],
+                "gpu_over_single_thread": value / f1})
     if rank == 0:
         line = {
             "metric": METRIC,
