@@ -8,7 +8,9 @@
 One bench "step" = one full run! of the T-step filter over one synthetic observation
 sequence (T = 100, the BASELINE.json configs[1] workload), including the final
 history trace-back that materialises x_1..x_{T+1} exactly as the reference's store holds
-them. N = 1,000,000 particles per GPU (weak scaling: each rank owns a 1M shard). Island
+them. N = 1,000,000 particles per GPU (weak scaling: each rank owns a 1M shard;
+`--global-particles G` splits one population of G over the ranks instead, for C4's strong
+scaling, e.g. G = 8,000,000 on 1/2/4/8 GPUs). Island
 resampling by default — ranks exchange one statistics payload per step over RCCL;
 `--shard-mode exact` resamples the whole population with the single-GPU bits (particles
 move between ranks).
@@ -49,7 +51,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--particles", type=int, default=1_000_000, help="particles per GPU")
+    ap.add_argument("--particles", type=int, default=1_000_000, help="particles per GPU (weak scaling)")
+    ap.add_argument("--global-particles", type=int, default=0,
+                    help="total particles split over the ranks (strong scaling, C4's 8M on 1/2/4/8 GPUs)")
     ap.add_argument("--T", type=int, default=100)
     ap.add_argument("--ess", type=float, default=1.0)
     ap.add_argument("--scheme", choices=["stratified", "systematic", "multinomial"], default="stratified")
@@ -168,17 +172,24 @@ def main():
 
     scheme = {"stratified": abi.RESAMPLE_STRATIFIED, "systematic": abi.RESAMPLE_SYSTEMATIC,
               "multinomial": abi.RESAMPLE_MULTINOMIAL}[args.scheme]
-    N = args.particles
+    if args.global_particles > 0:   # strong scaling: ragged contiguous shards of one population
+        G = args.global_particles
+        N = G // world + (1 if rank < G % world else 0)
+        goff = rank * (G // world) + min(rank, G % world)
+        gN = G
+    else:                           # weak scaling: N per rank
+        N = args.particles
+        goff, gN = rank * N, world * N
     T = args.T
     obs = wsmc.models.ssm2d_data(max(T, args.cpu_T), seed=args.seed)
     # one seed for every rank: the Philox streams are keyed by the global particle index
     ctx = wsmc.Context(N, seed=args.seed, device=0 if args.same_device else local)
     if comm is not None:
         if args.exchange == "host":
-            ctx.comm_init_host(comm.allgather, world, rank, rank * N, world * N)
+            ctx.comm_init_host(comm.allgather, world, rank, goff, gN)
         else:
             uid = comm.broadcast(wsmc.Context.comm_unique_id() if rank == 0 else None)
-            ctx.comm_init(uid, world, rank, rank * N, world * N)
+            ctx.comm_init(uid, world, rank, goff, gN)
         if args.shard_mode == "exact":
             ctx.comm_set_shard_mode(abi.SHARD_EXACT)
     exact = comm is not None and args.shard_mode == "exact"
@@ -224,7 +235,7 @@ def main():
         prop_ms /= inst_runs; red_ms /= inst_runs; rs_ms /= inst_runs; fin_ms /= inst_runs; tot_ms /= inst_runs
         nres //= inst_runs
 
-    units = world * N * T * args.steps
+    units = gN * T * args.steps
     value = units / elapsed
     ms_per_step = elapsed / args.steps * 1e3
     # propagate-kernel algorithmic bytes per run (forced resampling: every step after t=1 reads
@@ -291,12 +302,12 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.global_particles > 0 else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: examples/2D_ssm.jl observation recurrence (numpy Philox seed 42)",
             "config": {"workload": "2D SSM bootstrap filter (examples/2D_ssm.jl), BASELINE configs[1]",
-                       "n_particles_per_gpu": N, "global_particles": world * N, "T": T,
+                       "n_particles_per_gpu": N, "global_particles": gN, "T": T,
                        "ess_perc_min": args.ess, "scheme": args.scheme, "keep_history": not args.no_history,
                        "parallelism": (f"{args.shard_mode}-shard x{world}"
                                        + (" (host exchange, test mode)" if args.exchange == "host" else ""))
