@@ -36,27 +36,40 @@ def c3(N=1_000_000, reps=3):
             "log_evidence": ev}
 
 
-def c5(N=4_000_000, T=60, sweeps=5, reps=1):
+def c5(N=4_000_000, T=60, sweeps=5, reps=1, scheme="systematic", ess=1.0, diversity=None):
     t_obs, y_obs = models.oscillator_data(n=T)
-    best = math.inf
+    sch = {"systematic": wsmc.RESAMPLE_SYSTEMATIC, "stratified": wsmc.RESAMPLE_STRATIFIED}[scheme]
+    best, moved = math.inf, 0
     for _ in range(reps + 1):
         ctx = wsmc.Context(N, seed=42)
         ctx.sync()
         t0 = time.perf_counter()
-        acc = models.oscillator_statements(ctx, t_obs, y_obs, ess_perc_min=1.0, scheme=wsmc.RESAMPLE_SYSTEMATIC,
-                                           sweeps=sweeps, diversity=None)
+        acc = models.oscillator_statements(ctx, t_obs, y_obs, ess_perc_min=ess, scheme=sch, sweeps=sweeps,
+                                           diversity=diversity)
         ctx.sync()
         dt = time.perf_counter() - t0
         ctx.close()
         best = min(best, dt)
-    # score terms per particle: every move folds twice over the 5 priors + t observations
-    terms = sum(2 * 2 * sweeps * (5 + t) for t in range(1, T + 1))
-    return {"config": f"C5 damped oscillator, systematic, {sweeps} ungated sweeps (N={N}, T={T}, ess 1.0)",
-            "N": N, "T": T, "seconds_per_run": best, "particle_steps_per_s": N * T / best,
-            "score_terms_per_particle": terms, "score_terms_per_s": N * terms / best}
+        moved = sum(x for a in acc for x in a)   # accepted proposals (a skipped gated move: 0)
+    gate = "ungated" if diversity is None else f"diversity={diversity}"
+    out = {"config": f"C5 damped oscillator, {scheme}, {sweeps} {gate} sweep(s) (N={N}, T={T}, ess {ess})",
+           "N": N, "T": T, "seconds_per_run": best, "particle_steps_per_s": N * T / best,
+           "accepted": moved, "moves_offered": 2 * sweeps * T}
+    if diversity is None and ess >= 1.0:
+        # score terms per particle: every move folds twice over the 5 priors + t observations
+        terms = sum(2 * 2 * sweeps * (5 + t) for t in range(1, T + 1))
+        out.update({"score_terms_per_particle": terms, "score_terms_per_s": N * terms / best})
+    return out
+
+
+LEGS = {
+    "c3": c3,
+    "c5": c5,                                                             # canonical (systematic)
+    "c5_stratified": lambda: c5(scheme="stratified"),                     # the reference's scheme
+    "c5_example": lambda: c5(sweeps=1, scheme="stratified", ess=0.5, diversity=0.9),   # as written
+}
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["c3", "c5"]
-    for w in which:
-        print(json.dumps(c3() if w == "c3" else c5()), flush=True)
+    for w in sys.argv[1:] or ["c3", "c5"]:
+        print(json.dumps(LEGS[w]()), flush=True)
