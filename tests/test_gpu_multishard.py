@@ -343,3 +343,80 @@ def test_exact_shards_skewed_windows(gpu_available, tmp_path, kind):
         np.testing.assert_array_equal(p["x"], o.col_download(cx)[sl])
         np.testing.assert_array_equal(p["w"], o.weights_download()[sl])
         assert p["ev"][0] == o.log_evidence()
+
+
+def _rccl1_worker(mode, outdir):
+    """One process, a one-rank RCCL communicator: every exchange of the sharded paths goes
+    through ncclAllGather / ncclSend / ncclRecv for real (with one rank), and one shard is
+    the whole population, so the results must equal the unsharded oracle."""
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")     # the rendezvous of a lone rank
+    sys.path[:0] = [str(REPO / "weightedsampling.jl_amd")]
+    import wsmc
+    from wsmc import abi
+    N, T = 5001, 12
+    obs2 = wsmc.models.ssm2d_data(T)
+    out = {}
+
+    def ctx(seed):
+        c = wsmc.Context(N, seed=seed, device=0)
+        c.comm_init(wsmc.Context.comm_unique_id(), 1, 0, 0, N)   # a fresh rendezvous per communicator
+        if mode == "exact":
+            c.comm_set_shard_mode(abi.SHARD_EXACT)
+        return c
+    c = ctx(21)                                           # statements
+    out["flags"] = np.array(wsmc.models.ssm2d_statements(c, obs2, ess_perc_min=0.5))
+    out["w"] = c.weights_download()
+    out["ev"] = np.array([c.log_evidence()])
+    for name in c.col_names():
+        out["s_" + name] = c.col_download(c.col_find(name))
+    c.close()
+    f = ctx(22)                                           # the fused run
+    out["fev"] = np.array([f.ssm2d_run(obs2, ess_perc_min=1.0, keep_history=True)])
+    out["fw"] = f.weights_download()
+    for name in f.col_names():
+        out["f_" + name] = f.col_download(f.col_find(name))
+    f.close()
+    m = ctx(23)                                           # autoRW moves (moment exchange)
+    xs, ys = wsmc.models.linreg_data()
+    out["acc"] = np.array(wsmc.models.linreg_statements(m, xs[:6], ys[:6], ess_perc_min=1.0))
+    out["mw"] = m.weights_download()
+    for name in m.col_names():
+        out["m_" + name] = m.col_download(m.col_find(name))
+    m.close()
+    np.savez(os.path.join(outdir, f"rccl1_{mode}.npz"), **out)
+
+
+@pytest.mark.parametrize("mode", ["island", "exact"])
+def test_one_rank_rccl_matches_unsharded_oracle(gpu_available, tmp_path, mode):
+    """The RCCL calls of the multi-GPU path on the box's one GPU (a one-rank communicator)."""
+    import multiprocessing as mp
+    sys.path.insert(0, str(REPO / "oracle"))
+    from oracle import Oracle
+    import wsmc
+    p = mp.get_context("spawn").Process(target=_rccl1_worker, args=(mode, str(tmp_path)))
+    p.start()
+    p.join(100)
+    if p.is_alive():
+        p.kill()
+    assert p.exitcode == 0, p.exitcode
+    r = np.load(tmp_path / f"rccl1_{mode}.npz")
+    N, T = 5001, 12
+    obs2 = wsmc.models.ssm2d_data(T)
+    o = Oracle(N, seed=21)
+    assert list(r["flags"]) == wsmc.models.ssm2d_statements(o, obs2, ess_perc_min=0.5)
+    np.testing.assert_array_equal(r["w"], o.weights_download())
+    for name in o.col_names():
+        np.testing.assert_array_equal(r["s_" + name], o.col_download(o.col_find(name)), err_msg=name)
+    assert r["ev"][0] == o.log_evidence()
+    o = Oracle(N, seed=22)
+    wsmc.models.ssm2d_statements(o, obs2, ess_perc_min=1.0)
+    np.testing.assert_array_equal(r["fw"], o.weights_download())
+    for name in o.col_names():
+        np.testing.assert_array_equal(r["f_" + name], o.col_download(o.col_find(name)), err_msg=name)
+    assert r["fev"][0] == o.log_evidence()
+    o = Oracle(N, seed=23)
+    xs, ys = wsmc.models.linreg_data()
+    assert [tuple(a) for a in r["acc"]] == wsmc.models.linreg_statements(o, xs[:6], ys[:6], ess_perc_min=1.0)
+    np.testing.assert_array_equal(r["mw"], o.weights_download())
+    for name in o.col_names():
+        np.testing.assert_array_equal(r["m_" + name], o.col_download(o.col_find(name)), err_msg=name)

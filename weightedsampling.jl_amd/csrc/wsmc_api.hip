@@ -300,7 +300,7 @@ int wsmc_comm_init(wsmc_ctx* c, const uint8_t id[128], int32_t world, int32_t ra
     c->rank = rank;
     c->goff = goff;
     c->gN = gN;
-    if (world > 1) {
+    {   // world 1 too: a one-rank communicator runs the exchange paths on one GPU
         ncclUniqueId uid;
         std::memcpy(uid.internal, id, 128);
         WSMC_RCCL(ncclCommInitRank(&c->comm, world, uid, rank));
@@ -433,6 +433,11 @@ int wsmc_weights_download(wsmc_ctx* c, double* host) {
 }
 
 static int exchange_recs(wsmc_ctx* c, ShardRecord* recs);
+// The exchange (sharded) code paths run when the population is split over ranks, and also
+// for a one-rank communicator (world 1 with an RCCL comm or a host exchange): one shard is
+// the whole population, so the results equal the unsharded path's, which lets one GPU
+// exercise the RCCL calls themselves (tests/test_gpu_multishard.py).
+static inline bool is_sharded(const wsmc_ctx* c) { return c->world > 1 || c->comm || c->host_exchange; }
 // max (unless the caller's kernel already filled the slots), sums, reduce, [exchange + decide]
 static FillPlan fill_plan(wsmc_ctx* c, int scheme, uint64_t op, const uint64_t* op_dev) {
     FillPlan p;
@@ -474,9 +479,9 @@ static int enqueue_resample_stats(wsmc_ctx* c, const double* w, MaxSlots* ms, Sh
                                       ev ? ev[0] : nullptr, ev ? ev[1] : nullptr));
     else
         WSMC_HIP(launch_rs_sums(c->stream, w, c->N, ms, c->tilep, c->qbuf, ev ? ev[0] : nullptr, ev ? ev[1] : nullptr));
-    WSMC_HIP(launch_rs_reduce(c->stream, ms, c->tilep, c->N, c->tileOff, recs + c->rank, c->world == 1, ess_min, dec,
+    WSMC_HIP(launch_rs_reduce(c->stream, ms, c->tilep, c->N, c->tileOff, recs + c->rank, !is_sharded(c), ess_min, dec,
                               &plan, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr, multi ? multi_esum(c) : nullptr));
-    if (c->world > 1) {
+    if (is_sharded(c)) {
         int r = exchange_recs(c, recs);
         if (r) return r;
         WSMC_HIP(launch_rs_decide(c->stream, recs, c->world, c->rank, ess_min, dec));
@@ -486,7 +491,7 @@ static int enqueue_resample_stats(wsmc_ctx* c, const double* w, MaxSlots* ms, Sh
 
 // all-gather `words` u64 per rank in place (rank r's block at buf + r * words) on stream s
 static int exchange_words(wsmc_ctx* c, unsigned long long* buf, int64_t words, hipStream_t s) {
-    if (c->world <= 1) return WSMC_OK;
+    if (!is_sharded(c)) return WSMC_OK;
     if (c->host_exchange) {
         std::vector<unsigned long long> h((size_t)words * c->world);
         WSMC_HIP(hipMemcpyAsync(h.data() + (size_t)c->rank * words, buf + (size_t)c->rank * words,
@@ -506,7 +511,7 @@ static int exchange_words(wsmc_ctx* c, unsigned long long* buf, int64_t words, h
 }
 
 static int exchange_recs(wsmc_ctx* c, ShardRecord* recs) {
-    if (c->world <= 1) return WSMC_OK;
+    if (!is_sharded(c)) return WSMC_OK;
     const int words = (int)(sizeof(ShardRecord) / sizeof(unsigned long long));
     if (c->host_exchange) {
         std::vector<ShardRecord> h(c->world);
@@ -525,7 +530,7 @@ static int exchange_recs(wsmc_ctx* c, ShardRecord* recs) {
 }
 
 // ---- exact sharding ---------------------------------------------------
-static bool exact_mode(const wsmc_ctx* c) { return c->world > 1 && c->shard_mode == WSMC_SHARD_EXACT; }
+static bool exact_mode(const wsmc_ctx* c) { return is_sharded(c) && c->shard_mode == WSMC_SHARD_EXACT; }
 
 static int ensure_exact(wsmc_ctx* c) {
     if (!c->xp) WSMC_HIP(hipMalloc(&c->xp, sizeof(ExactPlan)));
@@ -1454,7 +1459,7 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
     if (r) return r;
     WSMC_HIP(hipMemsetAsync(c->dflag, 0, sizeof(int32_t) * 4, c->stream));
     WSMC_HIP(hipMemsetAsync(c->ucount, 0, sizeof(unsigned long long) * 4, c->stream));
-    if (proposal == WSMC_PROPOSAL_AUTORW && c->world > 1) {
+    if (proposal == WSMC_PROPOSAL_AUTORW && is_sharded(c)) {
         int rr = sharded_autorw(c, targets, d, bounded ? l : nullptr, bounded ? h : nullptr, step);
         if (rr) return rr;
     } else if (proposal == WSMC_PROPOSAL_AUTORW) {
@@ -1506,7 +1511,7 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         for (int k = 0; k < 4; ++k) { remap(t.x[k]); remap(t.dist.mu[k]); }
         remap(t.dist.scale);
     }
-    const int32_t* mflag = (proposal == WSMC_PROPOSAL_AUTORW && c->world == 1) ? c->dflag : nullptr;
+    const int32_t* mflag = (proposal == WSMC_PROPOSAL_AUTORW && !is_sharded(c)) ? c->dflag : nullptr;
     if ((int)slots.size() <= kFoldSlots) {
         if ((int64_t)ct.size() > c->d_ctape_cap) {
             int64_t cap = c->d_ctape_cap ? c->d_ctape_cap : 64;
@@ -1589,7 +1594,7 @@ static inline size_t run_grp_bytes(int64_t N, int32_t T) {
 static inline int64_t run_pay_words(int64_t N) { return kGroupLine + run_grp_words(N); }
 
 static int ensure_run_buffers(wsmc_ctx* c, int32_t T) {
-    if (c->world > 1 && !c->stream2) {
+    if (is_sharded(c) && !c->stream2) {
         WSMC_HIP(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
         WSMC_HIP(hipEventCreateWithFlags(&c->ev_sums, hipEventDisableTiming));
         WSMC_HIP(hipEventCreateWithFlags(&c->ev_dec, hipEventDisableTiming));
@@ -1642,7 +1647,7 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
     // sums are the exchange payload; all-gather + decision run on stream2, overlapped with
     // the local fill (island resampling fills from the shard's own Q); the next step's
     // propagate waits for the decision.
-    const bool sharded = c->world > 1;
+    const bool sharded = is_sharded(c);
     const int G = group_tiles(N);
     const int64_t PW = run_pay_words(N);
     const int ngroups = (int)(run_grp_words(N) / kGroupLine);
@@ -1939,7 +1944,7 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         const char* e = getenv("WSMC_DIAG_NO_GRAPH");
         return e && atoi(e) != 0;
     }();
-    const bool use_graph = c->world == 1 && !c->timing && !no_graph;   // HIP cannot time events captured in graphs
+    const bool use_graph = !is_sharded(c) && !c->timing && !no_graph;   // HIP cannot time events captured in graphs
     if (exact_mode(c) && c->timing) return fail(WSMC_ESTATE, "run timing is not available on exact shards");
     const int nev = 8 * T + 2;
     std::vector<hipEvent_t> evs;
