@@ -71,6 +71,9 @@ def parse():
     # island (default): one record all-gather per step, shard-local resampling;
     # exact: population-wide resampling, the single-GPU bits (particles move between ranks)
     ap.add_argument("--shard-mode", choices=["island", "exact"], default="island")
+    # diagnostics: one rank with a one-rank RCCL communicator, so the run takes the sharded
+    # (eager, RCCL all-gather per step) path on one GPU — the multi-GPU step cost minus xGMI
+    ap.add_argument("--rccl-one-rank", action="store_true")
     return ap.parse_args()
 
 
@@ -159,6 +162,12 @@ def cpu_baseline_1t(obs, n, T, ess, scheme, seed):
 
 def main():
     args = parse()
+    # stdout carries the one JSON line only: native libraries write to fd 1 too (RCCL prints
+    # its version banner at communicator creation), so fd 1 points at stderr for the run and
+    # the JSON line goes to a private duplicate of the original stdout
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -192,7 +201,11 @@ def main():
             ctx.comm_init(uid, world, rank, goff, gN)
         if args.shard_mode == "exact":
             ctx.comm_set_shard_mode(abi.SHARD_EXACT)
-    exact = comm is not None and args.shard_mode == "exact"
+    if comm is None and args.rccl_one_rank:
+        ctx.comm_init(wsmc.Context.comm_unique_id(), 1, 0, 0, N)
+        if args.shard_mode == "exact":
+            ctx.comm_set_shard_mode(abi.SHARD_EXACT)
+    exact = (comm is not None or args.rccl_one_rank) and args.shard_mode == "exact"
 
     def barrier():
         ctx.sync()
@@ -311,7 +324,8 @@ def main():
                        "ess_perc_min": args.ess, "scheme": args.scheme, "keep_history": not args.no_history,
                        "parallelism": (f"{args.shard_mode}-shard x{world}"
                                        + (" (host exchange, test mode)" if args.exchange == "host" else ""))
-                           if world > 1 else "single GPU"},
+                           if world > 1 else ("single GPU, one-rank RCCL communicator (diagnostic)"
+                                              if args.rccl_one_rank else "single GPU")},
             "roofline": {"bound": "hbm", "kernel": "k_ssm2d_prop (propagate+observe+max)",
                          "achieved": prop_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (prop_gbs / HBM_PEAK_GBS) if prop_gbs else None, "traffic": traffic,
@@ -324,7 +338,7 @@ def main():
                 "resamples_per_run": nres, "forced_every_step": forced},
             "log_evidence_last": ev,
         }
-        print(json.dumps(line), flush=True)
+        os.write(json_fd, (json.dumps(line) + "\n").encode())
     ctx.close()
     if comm is not None:
         comm.barrier()
