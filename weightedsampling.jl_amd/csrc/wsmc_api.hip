@@ -230,7 +230,7 @@ int wsmc_destroy(wsmc_ctx* c) {
     }
     void* bufs[] = {c->xchg, c->scache, c->scache_back, c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->cdf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount,
                     c->d_colptr, c->run_params, c->d_tape, c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp,
-                    c->vscratch, c->xscratch, c->run_pay, c->xp, c->comb, c->anc_out, c->xbuf, c->d_comp, c->d_ctape, c->d_prog};
+                    c->vscratch, c->xscratch, c->xp, c->comb, c->anc_out, c->xbuf, c->d_comp, c->d_ctape, c->d_prog};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (double* p : c->xrun)
@@ -239,9 +239,6 @@ int wsmc_destroy(wsmc_ctx* c) {
         if (p) (void)hipFree(p);
     if (c->pinned) (void)hipHostFree(c->pinned);
     if (c->comm) (void)ncclCommDestroy(c->comm);
-    if (c->ev_sums) (void)hipEventDestroy(c->ev_sums);
-    if (c->ev_dec) (void)hipEventDestroy(c->ev_dec);
-    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return WSMC_OK;
@@ -557,7 +554,7 @@ static int exact_records(wsmc_ctx* c) {
     int r = exchange_words(c, c->xchg, 1, c->stream);
     if (r) return r;
     WSMC_HIP(launch_max_adopt(c->stream, c->xchg, c->world, c->mslots));
-    WSMC_HIP(launch_rs_sums(c->stream, c->w, c->N, c->mslots, c->tilep, c->qbuf, nullptr, nullptr, nullptr, 1, nullptr,
+    WSMC_HIP(launch_rs_sums(c->stream, c->w, c->N, c->mslots, c->tilep, c->qbuf, nullptr, nullptr, nullptr, 1,
                             c->gN));
     WSMC_HIP(launch_rs_reduce(c->stream, c->mslots, c->tilep, c->N, c->tileOff, c->rec + c->rank, 0, 0.0, nullptr,
                               nullptr));
@@ -1589,19 +1586,11 @@ static inline int64_t run_grp_words(int64_t N) {
 static inline size_t run_grp_bytes(int64_t N, int32_t T) {
     return sizeof(unsigned long long) * (size_t)run_grp_words(N) * (size_t)(T + 1);
 }
-// sharded fused run: one exchange payload per rank and step = an 8-word header (max
-// log-weight, size) + the shard's group sums
-static inline int64_t run_pay_words(int64_t N) { return kGroupLine + run_grp_words(N); }
 
 static int ensure_run_buffers(wsmc_ctx* c, int32_t T) {
-    if (is_sharded(c) && !c->stream2) {
-        WSMC_HIP(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
-        WSMC_HIP(hipEventCreateWithFlags(&c->ev_sums, hipEventDisableTiming));
-        WSMC_HIP(hipEventCreateWithFlags(&c->ev_dec, hipEventDisableTiming));
-    }
     if (c->T_alloc >= T && c->run_rec) return WSMC_OK;
     WSMC_HIP(hipStreamSynchronize(c->stream));
-    void* old[] = {c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp, c->run_pay};
+    void* old[] = {c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp};
     for (void* p : old)
         if (p) WSMC_HIP(hipFree(p));
     WSMC_HIP(hipMalloc(&c->run_max, sizeof(MaxSlots) * (T + 1)));
@@ -1610,7 +1599,6 @@ static int ensure_run_buffers(wsmc_ctx* c, int32_t T) {
     WSMC_HIP(hipMalloc(&c->anc_log, sizeof(int32_t) * (size_t)T * anc_stride(c->N)));
     WSMC_HIP(hipMalloc(&c->obs, sizeof(double) * 2 * (T + 1)));
     WSMC_HIP(hipMalloc(&c->run_grp, run_grp_bytes(c->N, T)));
-    WSMC_HIP(hipMalloc(&c->run_pay, sizeof(unsigned long long) * (size_t)run_pay_words(c->N) * kMaxWorld * (T + 1)));
     if (!c->vscratch) WSMC_HIP(hipMalloc(&c->vscratch, sizeof(double) * 2 * c->N));
     if (!c->xscratch) WSMC_HIP(hipMalloc(&c->xscratch, sizeof(double) * 2 * c->N));
     c->T_alloc = T;
@@ -1643,16 +1631,9 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
     auto E = [&](int k) -> hipEvent_t { return ev ? (*ev)[k] : nullptr; };
     WSMC_HIP(hipMemsetAsync(c->run_max, 0, sizeof(MaxSlots) * (T + 1), c->stream));
     WSMC_HIP(hipMemsetAsync(c->run_dec, 0, sizeof(Decision) * (T + 1), c->stream));
-    // one GPU: group sums + one fill launch whose extra block decides. Sharded: the group
-    // sums are the exchange payload; all-gather + decision run on stream2, overlapped with
-    // the local fill (island resampling fills from the shard's own Q); the next step's
-    // propagate waits for the decision.
     const bool sharded = is_sharded(c);
     const int G = group_tiles(N);
-    const int64_t PW = run_pay_words(N);
-    const int ngroups = (int)(run_grp_words(N) / kGroupLine);
-    if (!sharded) WSMC_HIP(hipMemsetAsync(c->run_grp, 0, run_grp_bytes(N, T), c->stream));
-    else WSMC_HIP(hipMemsetAsync(c->run_pay, 0, sizeof(unsigned long long) * PW * c->world * (T + 1), c->stream));
+    WSMC_HIP(hipMemsetAsync(c->run_grp, 0, run_grp_bytes(N, T), c->stream));
     double* vbuf[2] = {c->cols[p.colv].back, c->vscratch};
     double* xbuf[2] = {p.keep ? nullptr : c->cols[p.colx].back, c->xscratch};
     for (int t = 1; t <= T; ++t) {
@@ -1688,7 +1669,6 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
         ShardRecord* recs = c->run_rec + (size_t)t * c->world;
         a.ms = ms;
         const int k0 = 8 * (t - 1);
-        if (sharded && t > 1 && p.scheme != WSMC_RESAMPLE_MULTINOMIAL) WSMC_HIP(hipStreamWaitEvent(c->stream, c->ev_dec, 0));
         WSMC_HIP(launch_ssm2d_propagate(c->stream, a, E(k0), E(k0 + 1)));
         const FillPlan plan = fill_plan(c, p.scheme, 3ull * (uint64_t)(t - 1) + 2ull, c->run_params);
         int32_t* anc_row = c->anc_log + (size_t)(t - 1) * anc_stride(N);
@@ -1707,28 +1687,20 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
                                            multi_esum(c), multi_ebuf(c), anc_row, nullptr, E(k0 + 7)));
             continue;
         }
-        if (!sharded) {
-            unsigned long long* grp = c->run_grp + (size_t)t * run_grp_words(N);
-            WSMC_HIP(launch_rs_sums(c->stream, c->w, N, ms, c->tilep, c->qbuf, E(k0 + 2), E(k0 + 3), grp, G));
-            WSMC_HIP(launch_rs_fill_fused(c->stream, N, plan, grp, G, ms, p.ess_min, recs, c->run_dec + t, c->qbuf,
-                                          anc_row, E(k0 + 6), E(k0 + 7)));
-            continue;
+        // group sums of q + one fill launch whose extra block builds the shard record (and,
+        // on one GPU, decides). Sharded: the records are all-gathered on the same stream and
+        // every rank decides in rank order (k_rs_decide); island resampling fills from the
+        // shard's own Q, so the fill never waits for the collective.
+        unsigned long long* grp = c->run_grp + (size_t)t * run_grp_words(N);
+        WSMC_HIP(launch_rs_sums(c->stream, c->w, N, ms, c->tilep, c->qbuf, E(k0 + 2), E(k0 + 3), grp, G));
+        WSMC_HIP(launch_rs_fill_fused(c->stream, N, plan, grp, G, ms, p.ess_min, recs + c->rank,
+                                      sharded ? nullptr : c->run_dec + t, c->qbuf, anc_row, E(k0 + 6), E(k0 + 7)));
+        if (sharded) {
+            int r = exchange_recs(c, recs);
+            if (r) return r;
+            WSMC_HIP(launch_rs_decide(c->stream, recs, c->world, c->rank, p.ess_min, c->run_dec + t));
         }
-        unsigned long long* pay = c->run_pay + (size_t)t * c->world * PW;
-        unsigned long long* mine = pay + (size_t)c->rank * PW;
-        WSMC_HIP(launch_rs_sums(c->stream, c->w, N, ms, c->tilep, c->qbuf, E(k0 + 2), E(k0 + 3), mine + kGroupLine,
-                                G, mine));
-        WSMC_HIP(hipEventRecord(c->ev_sums, c->stream));
-        WSMC_HIP(hipStreamWaitEvent(c->stream2, c->ev_sums, 0));
-        int r = exchange_words(c, pay, PW, c->stream2);
-        if (r) return r;
-        WSMC_HIP(launch_rs_decide_groups(c->stream2, pay, PW, ngroups, c->world, c->rank, p.ess_min, recs,
-                                         c->run_dec + t));
-        WSMC_HIP(hipEventRecord(c->ev_dec, c->stream2));
-        WSMC_HIP(launch_rs_fill_fused(c->stream, N, plan, mine + kGroupLine, G, ms, p.ess_min, recs, nullptr, c->qbuf,
-                                      anc_row, E(k0 + 6), E(k0 + 7)));
     }
-    if (sharded) WSMC_HIP(hipStreamWaitEvent(c->stream, c->ev_dec, 0));
     Ssm2dFinal f;
     f.T = T;
     f.keep_history = p.keep;
@@ -1921,6 +1893,7 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
     auto mix = [&](const void* q) { h = (h ^ (uint64_t)(uintptr_t)q) * 1099511628211ull; };
     for (auto& col : c->cols) { mix(col.front); mix(col.back); }
     mix(c->w); mix(c->anc_log); mix(c->run_rec); mix(c->run_max); mix(c->obs);
+    mix(c->comm);   // a captured collective bakes its communicator
     const std::string key = std::string(keybuf) + " ptr=" + std::to_string(h);
     auto build_tables = [&](double*** work, double*** outp) -> int {
         *work = *outp = nullptr;
@@ -1944,7 +1917,9 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         const char* e = getenv("WSMC_DIAG_NO_GRAPH");
         return e && atoi(e) != 0;
     }();
-    const bool use_graph = !is_sharded(c) && !c->timing && !no_graph;   // HIP cannot time events captured in graphs
+    // HIP cannot time events captured in graphs; a host exchange (test mode) synchronises
+    // inside the run, and exact shards are host-driven. RCCL collectives are captured.
+    const bool use_graph = !c->timing && !no_graph && !exact_mode(c) && !c->host_exchange;
     if (exact_mode(c) && c->timing) return fail(WSMC_ESTATE, "run timing is not available on exact shards");
     const int nev = 8 * T + 2;
     std::vector<hipEvent_t> evs;

@@ -108,10 +108,6 @@ struct wsmc_ctx {
     double* scache = nullptr;
     double* scache_back = nullptr;
     int32_t scache_terms = -1;
-    unsigned long long* run_pay = nullptr;      // sharded fused run: [T+1][world][PW] exchange payloads
-    int64_t run_pay_world = 0;
-    hipStream_t stream2 = nullptr;              // sharded fused run: exchange + decision stream
-    hipEvent_t ev_sums = nullptr, ev_dec = nullptr;
     void* host_user = nullptr;
 
     // store
@@ -215,10 +211,8 @@ hipError_t launch_rs_max(hipStream_t s, const double* w, int64_t N, MaxSlots* ms
 hipError_t launch_rs_sums(hipStream_t s, const double* w, int64_t N, const MaxSlots* ms,
                           unsigned long long* tilep, unsigned long long* qbuf,
                           hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr,
-                          unsigned long long* grp = nullptr, int G = 1, unsigned long long* hdr = nullptr,
+                          unsigned long long* grp = nullptr, int G = 1,
                           int64_t Nk = 0 /* N of K = 63 - ceil(log2 N): the global N when exact */);
-hipError_t launch_rs_decide_groups(hipStream_t s, const unsigned long long* pay, int64_t PW, int ngroups, int world,
-                                   int rank, double ess_min, ShardRecord* recs, Decision* dec);
 struct FillPlan {          // ancestor-fill task planning (in the reduce kernel)
     const unsigned long long* tilep;   // per-tile partials (sum q first)
     int32_t* taskOff;
@@ -328,7 +322,7 @@ hipError_t launch_rs_multinomial(hipStream_t s, int64_t N, const ShardRecord* re
                                  const unsigned long long* lcdf, const unsigned long long* esum,
                                  const uint32_t* ebuf, int32_t* anc, hipEvent_t e0 = nullptr,
                                  hipEvent_t e1 = nullptr);
-// fused single-GPU run: group sums (kGroupLine u64 per group) replace the reduce kernel
+// fused run: group sums of q (kGroupLine u64 per group, one line each) replace the reduce kernel
 constexpr int kGroupLine = 8;
 constexpr int kMaxWorld = kMaxShards;   // ranks of one node
 inline int group_tiles(int64_t N) {   // tiles per group: ~sqrt(ntiles), >= 16

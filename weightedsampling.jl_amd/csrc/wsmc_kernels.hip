@@ -238,7 +238,7 @@ template <int MODE>
 __global__ __launch_bounds__(kSumBlock) void k_rs_sums_t(const double* __restrict__ w, int64_t N,
                                                          const MaxSlots* __restrict__ ms, u64* __restrict__ tilep,
                                                          u64* __restrict__ qbuf, u64* __restrict__ grp, int G,
-                                                         u64* __restrict__ hdr, int64_t Nk) {
+                                                         int64_t Nk) {
     constexpr int IT = kRsTile / kSumBlock;
     __shared__ double s_f[3][kSumBlock / 64];
     __shared__ u64 s_q[kSumBlock / 64];
@@ -300,24 +300,9 @@ __global__ __launch_bounds__(kSumBlock) void k_rs_sums_t(const double* __restric
             t = (u64)f;                                         // exact: < 2^53
         }
         tilep[(int64_t)blockIdx.x * kPart + th] = t;
-        // group sums (fused runs; integer atomics, so order-free). One GPU needs only the
-        // sums of q; a shard (hdr != null) publishes all four (S2, Wf as 32-bit limbs) as
-        // its exchange payload, headed by its max log-weight and size
-        if (grp) {
-            u64* gp = grp + (int64_t)(blockIdx.x / G) * kGroupLine;
-            if (!hdr) {
-                if (th == 0) atomicAdd(gp, t);
-            } else if (th < 2) {
-                atomicAdd(gp + th, t);
-            } else {
-                atomicAdd(gp + 2 * th - 2, t & 0xffffffffull);
-                atomicAdd(gp + 2 * th - 1, t >> 32);
-            }
-        }
-        if (hdr && blockIdx.x == 0 && th == 0) {
-            hdr[0] = wsmc_ord_enc(M);
-            hdr[1] = (u64)N;
-        }
+        // group sums of q (fused runs; integer atomics, so order-free): the fill's CDF
+        // offsets and the shard record's Q
+        if (grp && th == 0) atomicAdd(grp + (int64_t)(blockIdx.x / G) * kGroupLine, t);
     }
 }
 
@@ -1067,8 +1052,8 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
     const int ntiles = (int)((N + kRsTile - 1) / kRsTile);
     const int ngroups = (ntiles + G - 1) / G;
     if (t == ntiles + kOverflowBlocks) {
-        if (!dec) return;   // sharded runs decide from the exchanged payloads (k_rs_decide_groups)
-        // ---- the record and the decision ----
+        // ---- the shard record and (one GPU, dec != null) the decision; a sharded run
+        // all-gathers the records and decides afterwards (k_rs_decide) ----
         u64 acc[kRedPart] = {0, 0, 0, 0, 0, 0};
         for (int g = th; g < ngroups; g += kScanBlock) acc[0] += grp[(int64_t)g * kGroupLine];
         for (int b = th; b < ntiles; b += kScanBlock) {
@@ -1099,7 +1084,7 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
             r.wflo = (u64)Wf; r.wfhi = (u64)(Wf >> 64);
             r.n = (u64)N;
             *rec = r;
-            decide_records(&r, 1, 0, ess_min, dec);
+            if (dec) decide_records(&r, 1, 0, ess_min, dec);
         }
         return;
     }
@@ -1792,55 +1777,9 @@ hipError_t launch_rs_max(hipStream_t s, const double* w, int64_t N, MaxSlots* ms
     return hipGetLastError();
 }
 hipError_t launch_rs_sums(hipStream_t s, const double* w, int64_t N, const MaxSlots* ms, u64* tilep, u64* qbuf,
-                          hipEvent_t e0, hipEvent_t e1, u64* grp, int G, u64* hdr, int64_t Nk) {
+                          hipEvent_t e0, hipEvent_t e1, u64* grp, int G, int64_t Nk) {
     return launch_timed(k_rs_sums_t<0>, rs_tiles_for(N), dim3(kSumBlock), s, e0, e1, w, N, ms, tilep, qbuf, grp, G,
-                        hdr, Nk > 0 ? Nk : N);
-}
-// Global decision of a sharded fused step from the all-gathered payloads (rank order):
-// each rank's record from its group sums, then the rank-order combine (decide_records).
-__global__ __launch_bounds__(kScanBlock) void k_rs_decide_groups(const u64* __restrict__ pay, int64_t PW, int ngroups,
-                                                                 int world, int rank, double ess_min,
-                                                                 ShardRecord* recs, Decision* dec) {
-    __shared__ u64 s_parts[kScanBlock / 64][kRedPart];
-    __shared__ ShardRecord s_rec[kMaxWorld];
-    const int th = threadIdx.x;
-    for (int r = 0; r < world; ++r) {
-        const u64* pr = pay + (int64_t)r * PW;
-        u64 acc[kRedPart] = {0, 0, 0, 0, 0, 0};
-        for (int g = th; g < ngroups; g += kScanBlock)
-#pragma unroll
-            for (int k = 0; k < kRedPart; ++k) acc[k] += pr[kGroupLine + (int64_t)g * kGroupLine + k];
-#pragma unroll
-        for (int k = 0; k < kRedPart; ++k) acc[k] = wave_sum_u64(acc[k]);
-        if ((th & 63) == 0)
-#pragma unroll
-            for (int k = 0; k < kRedPart; ++k) s_parts[th >> 6][k] = acc[k];
-        __syncthreads();
-        if (th == 0) {
-            u64 tot[kRedPart] = {0, 0, 0, 0, 0, 0};
-            for (int v = 0; v < kScanBlock / 64; ++v)
-                for (int k = 0; k < kRedPart; ++k) tot[k] += s_parts[v][k];
-            ShardRecord rc;
-            rc.menc = pr[0];
-            rc.Q = tot[0];
-            rc.s1 = tot[1];
-            const wsmc_u128 S2 = (wsmc_u128)tot[2] + ((wsmc_u128)tot[3] << 32);
-            const wsmc_u128 Wf = (wsmc_u128)tot[4] + ((wsmc_u128)tot[5] << 32);
-            rc.s2lo = (u64)S2; rc.s2hi = (u64)(S2 >> 64);
-            rc.wflo = (u64)Wf; rc.wfhi = (u64)(Wf >> 64);
-            rc.n = pr[1];
-            s_rec[r] = rc;
-            recs[r] = rc;
-        }
-        __syncthreads();
-    }
-    if (th == 0) decide_records(s_rec, world, rank, ess_min, dec);
-}
-hipError_t launch_rs_decide_groups(hipStream_t s, const u64* pay, int64_t PW, int ngroups, int world, int rank,
-                                   double ess_min, ShardRecord* recs, Decision* dec) {
-    hipLaunchKernelGGL(k_rs_decide_groups, dim3(1), dim3(kScanBlock), 0, s, pay, PW, ngroups, world, rank, ess_min,
-                       recs, dec);
-    return hipGetLastError();
+                        Nk > 0 ? Nk : N);
 }
 hipError_t launch_rs_fill_fused(hipStream_t s, int64_t N, const FillPlan& plan, const u64* grp, int G,
                                 const MaxSlots* ms, double ess_min, ShardRecord* rec, Decision* dec, const u64* qbuf,
@@ -1983,9 +1922,9 @@ hipError_t debug_kernel_bench(hipStream_t s, int kernel, int mode, int iters, co
     for (int it = 0; it < iters; ++it) {
         if (kernel == 0) {
             switch (mode) {
-                case 0: hipLaunchKernelGGL(k_rs_sums_t<0>, g, blk, 0, s, w, N, ms, tilep, qbuf, nullptr, 1, nullptr, N); break;
-                case 1: hipLaunchKernelGGL(k_rs_sums_t<1>, g, blk, 0, s, w, N, ms, tilep, qbuf, nullptr, 1, nullptr, N); break;
-                default: hipLaunchKernelGGL(k_rs_sums_t<4>, g, blk, 0, s, w, N, ms, tilep, qbuf, nullptr, 1, nullptr, N); break;
+                case 0: hipLaunchKernelGGL(k_rs_sums_t<0>, g, blk, 0, s, w, N, ms, tilep, qbuf, nullptr, 1, N); break;
+                case 1: hipLaunchKernelGGL(k_rs_sums_t<1>, g, blk, 0, s, w, N, ms, tilep, qbuf, nullptr, 1, N); break;
+                default: hipLaunchKernelGGL(k_rs_sums_t<4>, g, blk, 0, s, w, N, ms, tilep, qbuf, nullptr, 1, N); break;
             }
         } else if (kernel == 3) {
             // scratch: stream4 = 4 x [2N] doubles (x src, v src, x dst, v dst), wd = w
