@@ -93,6 +93,19 @@ def test_two_shards_one_gpu_match_sharded_oracle(gpu_available, tmp_path, N, ess
 
 
 
+def _move_program(ctx, which):
+    import wsmc
+    if which == "c3":
+        xs, ys = wsmc.models.linreg_data()
+        return wsmc.models.linreg_statements(ctx, xs[:6], ys[:6], ess_perc_min=1.0)
+    if which == "c5g":   # the example's gated moves (ess 0.5): the population-wide unique count;
+        t, y = wsmc.models.oscillator_data(n=8)          # at 0.7 the gate both skips and runs
+        return wsmc.models.oscillator_statements(ctx, t, y, ess_perc_min=0.5, sweeps=2, diversity=0.7)
+    t, y = wsmc.models.oscillator_data(n=5)
+    return wsmc.models.oscillator_statements(ctx, t, y, ess_perc_min=1.0, scheme=wsmc.RESAMPLE_SYSTEMATIC,
+                                             sweeps=2, diversity=None)
+
+
 def _move_worker(rank, world, port, N, which, outdir, exact=False):
     sys.path[:0] = [str(REPO / "weightedsampling.jl_amd")]
     import wsmc
@@ -104,22 +117,10 @@ def _move_worker(rank, world, port, N, which, outdir, exact=False):
     c.comm_init_host(comm.allgather, world, rank, rank * n, N)
     if exact:
         c.comm_set_shard_mode(abi.SHARD_EXACT)
-    if which == "c3":
-        xs, ys = wsmc.models.linreg_data()
-        acc = wsmc.models.linreg_statements(c, xs[:6], ys[:6], ess_perc_min=1.0)
-    else:
-        t, y = wsmc.models.oscillator_data(n=5)
-        acc = wsmc.models.oscillator_statements(c, t, y, ess_perc_min=1.0, scheme=wsmc.RESAMPLE_SYSTEMATIC,
-                                                sweeps=2, diversity=None)
+    acc = _move_program(c, which)
     out = {"acc": np.array(acc), "w": c.weights_download(), "ev": np.array([c.log_evidence()])}
     for name in c.col_names():
         out["c_" + name] = c.col_download(c.col_find(name))
-    # the diversity gate needs a global unique count: refused on shards, not silently local
-    try:
-        c.move(wsmc.PROPOSAL_AUTORW, [c.col_find(c.col_names()[0])], 1e-3, diversity=0.9)
-        out["gate"] = np.array([0])
-    except wsmc.WSMCError:
-        out["gate"] = np.array([1])
     c.close()
     comm.barrier()
     comm.close()
@@ -127,7 +128,7 @@ def _move_worker(rank, world, port, N, which, outdir, exact=False):
 
 
 @pytest.mark.parametrize("exact", [False, True])
-@pytest.mark.parametrize("which", ["c3", "c5"])
+@pytest.mark.parametrize("which", ["c3", "c5", "c5g"])
 def test_two_shards_moves_match_sharded_oracle(gpu_available, tmp_path, which, exact):
     """Sharded autoRW: global max, per-rank canonical moment totals combined in rank order;
     with exact sharding the Resamples are population-wide (the oracle's exact flag)."""
@@ -150,13 +151,7 @@ def test_two_shards_moves_match_sharded_oracle(gpu_available, tmp_path, which, e
             p.kill()
     assert codes == [0] * world, codes
     ref = Oracle(N, seed=33, shards=world, exact=exact)
-    if which == "c3":
-        xs, ys = wsmc.models.linreg_data()
-        acc = wsmc.models.linreg_statements(ref, xs[:6], ys[:6], ess_perc_min=1.0)
-    else:
-        t, y = wsmc.models.oscillator_data(n=5)
-        acc = wsmc.models.oscillator_statements(ref, t, y, ess_perc_min=1.0, scheme=wsmc.RESAMPLE_SYSTEMATIC,
-                                                sweeps=2, diversity=None)
+    acc = _move_program(ref, which)
     n = N // world
     parts = [np.load(tmp_path / f"mv{r}.npz") for r in range(world)]
     # accepted counts are per shard; their sum is the single-process count
@@ -167,7 +162,6 @@ def test_two_shards_moves_match_sharded_oracle(gpu_available, tmp_path, which, e
         for name in ref.col_names():
             np.testing.assert_array_equal(p["c_" + name], ref.col_download(ref.col_find(name))[..., sl], err_msg=name)
         assert p["ev"][0] == ref.log_evidence()
-        assert p["gate"][0] == 1
 
 
 # ---- exact sharding: the shards together give the single-context bits ---------------------
@@ -383,6 +377,11 @@ def _rccl1_worker(mode, outdir):
     for name in m.col_names():
         out["m_" + name] = m.col_download(m.col_find(name))
     m.close()
+    g = ctx(24)                                           # diversity-gated moves (global_unique)
+    out["gacc"] = np.array(_move_program(g, "c5g"))
+    for name in g.col_names():
+        out["g_" + name] = g.col_download(g.col_find(name))
+    g.close()
     np.savez(os.path.join(outdir, f"rccl1_{mode}.npz"), **out)
 
 
@@ -420,3 +419,7 @@ def test_one_rank_rccl_matches_unsharded_oracle(gpu_available, tmp_path, mode):
     np.testing.assert_array_equal(r["mw"], o.weights_download())
     for name in o.col_names():
         np.testing.assert_array_equal(r["m_" + name], o.col_download(o.col_find(name)), err_msg=name)
+    o = Oracle(N, seed=24)
+    assert [tuple(a) for a in r["gacc"]] == _move_program(o, "c5g")
+    for name in o.col_names():
+        np.testing.assert_array_equal(r["g_" + name], o.col_download(o.col_find(name)), err_msg=name)

@@ -1246,6 +1246,77 @@ int wsmc_score(wsmc_ctx* c, int32_t depth, double* host) {
     return WSMC_OK;
 }
 
+// The population-wide unique count of a shard's sorted keys: each rank
+// compacts its unique keys, the ranks all-gather them (padded to the largest count, after
+// an all-gather of the counts), and every rank sorts the union and counts it. Every rank
+// gets the same count; it equals the unsharded count. `sorted` is N keys; scratch is
+// allocated per call (the gate runs once per move).
+static int global_unique(wsmc_ctx* c, const unsigned long long* sorted, unsigned long long* u_out) {
+    using u64 = unsigned long long;
+    const int W = c->world, me = c->rank;
+    const int64_t N = c->N;
+    std::vector<void*> owned;
+    auto dalloc = [&](size_t bytes) -> void* {
+        void* p = nullptr;
+        if (hipMalloc(&p, bytes ? bytes : 16) != hipSuccess) return nullptr;
+        owned.push_back(p);
+        return p;
+    };
+    auto done = [&](int rc) {
+        for (void* p : owned) (void)hipFree(p);
+        return rc;
+    };
+#define GU_HIP(x)                                                                                  \
+    do {                                                                                           \
+        const hipError_t e_ = (x);                                                                 \
+        if (e_ != hipSuccess) return done(fail(WSMC_EHIP, std::string("global_unique: ") + hipGetErrorString(e_))); \
+    } while (0)
+    u64* uq = static_cast<u64*>(dalloc(sizeof(u64) * N));
+    u64* cnt = static_cast<u64*>(dalloc(sizeof(u64) * W));
+    u64* nsel = static_cast<u64*>(dalloc(sizeof(u64)));
+    if (!uq || !cnt || !nsel) return done(fail(WSMC_EHIP, "global_unique: out of device memory"));
+    size_t tb = 0;
+    if (hipcub::DeviceSelect::Unique(nullptr, tb, sorted, uq, nsel, (int)N, c->stream) != hipSuccess)
+        return done(fail(WSMC_EHIP, "global_unique: select"));
+    void* tmp = dalloc(tb);
+    if (!tmp) return done(fail(WSMC_EHIP, "global_unique: out of device memory"));
+    GU_HIP(hipcub::DeviceSelect::Unique(tmp, tb, sorted, uq, nsel, (int)N, c->stream));
+    GU_HIP(hipMemcpyAsync(cnt + me, nsel, sizeof(u64), hipMemcpyDeviceToDevice, c->stream));
+    int r = exchange_words(c, cnt, 1, c->stream);
+    if (r) return done(r);
+    std::vector<u64> hc(W);
+    GU_HIP(hipMemcpyAsync(hc.data(), cnt, sizeof(u64) * W, hipMemcpyDeviceToHost, c->stream));
+    GU_HIP(hipStreamSynchronize(c->stream));
+    u64 M = 1, tot = 0;
+    for (int g = 0; g < W; ++g) {
+        M = hc[g] > M ? hc[g] : M;
+        tot += hc[g];
+    }
+    u64* gbuf = static_cast<u64*>(dalloc(sizeof(u64) * M * W));
+    u64* all = static_cast<u64*>(dalloc(sizeof(u64) * tot));
+    u64* alls = static_cast<u64*>(dalloc(sizeof(u64) * tot));
+    if (!gbuf || !all || !alls) return done(fail(WSMC_EHIP, "global_unique: out of device memory"));
+    if (hc[me]) GU_HIP(hipMemcpyAsync(gbuf + M * me, uq, sizeof(u64) * hc[me], hipMemcpyDeviceToDevice, c->stream));
+    if ((r = exchange_words(c, gbuf, (int64_t)M, c->stream))) return done(r);
+    u64 off = 0;
+    for (int g = 0; g < W; ++g) {   // the valid prefix of every rank's block
+        if (hc[g]) GU_HIP(hipMemcpyAsync(all + off, gbuf + M * g, sizeof(u64) * hc[g], hipMemcpyDeviceToDevice,
+                                           c->stream));
+        off += hc[g];
+    }
+    size_t sb = 0;
+    GU_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, sb, all, alls, (int)tot, 0, 64, c->stream));
+    void* stmp = dalloc(sb);
+    if (!stmp) return done(fail(WSMC_EHIP, "global_unique: out of device memory"));
+    GU_HIP(hipcub::DeviceRadixSort::SortKeys(stmp, sb, all, alls, (int)tot, 0, 64, c->stream));
+    GU_HIP(hipMemsetAsync(nsel, 0, sizeof(u64), c->stream));
+    GU_HIP(launch_count_unique(c->stream, alls, (int64_t)tot, nsel));
+    GU_HIP(hipMemcpyAsync(u_out, nsel, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    GU_HIP(hipStreamSynchronize(c->stream));
+    return done(WSMC_OK);
+#undef GU_HIP
+}
+
 int wsmc_marginal_diversity(wsmc_ctx* c, const int32_t* targets, int32_t d, double* out) {
     CHECK_CTX(c);
     if (!targets || d < 1 || !out) return fail(WSMC_EARG, "bad targets");
@@ -1258,22 +1329,37 @@ int wsmc_marginal_diversity(wsmc_ctx* c, const int32_t* targets, int32_t d, doub
     WSMC_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tbytes, kin, kout, (int)c->N, 0, 64, c->stream));
     void* tstore = nullptr;
     WSMC_HIP(hipMalloc(&tstore, tbytes + 16));
+    // one shard: length(unique(col)) / N; sharded: the population-wide count over the global N
+    const bool global = is_sharded(c);
+    const uint64_t Nd = global ? (uint64_t)c->gN : (uint64_t)c->N;
     double best = INFINITY;
     for (int k = 0; k < d; ++k) {
         hipError_t e = launch_diversity_keys(c->stream, c->cols[targets[k]].front, kin, c->N);
         if (e == hipSuccess)
             e = hipcub::DeviceRadixSort::SortKeys(tstore, tbytes, kin, kout, (int)c->N, 0, 64, c->stream);
-        if (e == hipSuccess) e = hipMemsetAsync(c->ucount, 0, sizeof(unsigned long long), c->stream);
-        if (e == hipSuccess) e = launch_count_unique(c->stream, kout, c->N, c->ucount);
         unsigned long long u = 0;
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(&u, c->ucount, sizeof(u), hipMemcpyDeviceToHost, c->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-        if (e != hipSuccess) {
-            (void)hipFree(tstore);
-            return fail(WSMC_EHIP, std::string("marginal_diversity: ") + hipGetErrorString(e));
+        if (global) {
+            if (e != hipSuccess) {
+                (void)hipFree(tstore);
+                return fail(WSMC_EHIP, std::string("marginal_diversity: ") + hipGetErrorString(e));
+            }
+            const int r = global_unique(c, kout, &u);
+            if (r) {
+                (void)hipFree(tstore);
+                return r;
+            }
+        } else {
+            if (e == hipSuccess) e = hipMemsetAsync(c->ucount, 0, sizeof(unsigned long long), c->stream);
+            if (e == hipSuccess) e = launch_count_unique(c->stream, kout, c->N, c->ucount);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(&u, c->ucount, sizeof(u), hipMemcpyDeviceToHost, c->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+            if (e != hipSuccess) {
+                (void)hipFree(tstore);
+                return fail(WSMC_EHIP, std::string("marginal_diversity: ") + hipGetErrorString(e));
+            }
         }
-        const double frac = wsmc_u64_to_d(u) / wsmc_u64_to_d((uint64_t)c->N);
+        const double frac = wsmc_u64_to_d(u) / wsmc_u64_to_d(Nd);
         if (frac < best) best = frac;
     }
     (void)hipFree(tstore);
@@ -1433,9 +1519,6 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
     for (int k = 0; k < d; ++k)
         if (!valid_col(c, targets[k]) || c->cols[targets[k]].dim != 1)
             return fail(WSMC_EARG, "move targets must be existing scalar columns");
-    if (c->world > 1 && !std::isnan(diversity))
-        return fail(WSMC_ESTATE, "diversity-gated moves on sharded contexts are not supported (needs a global "
-                                 "unique count)");
     if (!std::isnan(diversity)) {
         double div = 0;
         int r = wsmc_marginal_diversity(c, targets, d, &div);
