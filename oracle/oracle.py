@@ -342,11 +342,11 @@ class Oracle:
         arr = _operand_array(x)
         self._chk(self._L.or_weight(self._h, _addr(dist), _addr(arr)))
 
-    def resample(self, ess_perc_min: float, scheme: int = 0):
+    def resample(self, ess_perc_min: float, scheme: int = 0, wait: bool = True):
         r = C.c_int32()
         e = C.c_double()
         self._chk(self._L.or_resample(self._h, float(ess_perc_min), int(scheme), C.byref(r), C.byref(e)))
-        return bool(r.value), float(e.value)
+        return (bool(r.value), float(e.value)) if wait else None
 
     def move(self, proposal: int, targets, step: float, lo=None, hi=None, target_depth: int = -1,
              diversity: float = float("nan")) -> int:

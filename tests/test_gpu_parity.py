@@ -107,6 +107,27 @@ def test_lgssm1d_statements(gpu_available, ess):
 
 
 @pytest.mark.parametrize("ess", [1.0, 0.5])
+@pytest.mark.parametrize("scheme", [abi.RESAMPLE_STRATIFIED, abi.RESAMPLE_MULTINOMIAL])
+def test_async_resample_matches_oracle(gpu_available, ess, scheme):
+    """Resample with no flag requested: the decision stays on the device (gated gather and
+    weight reset, identity copies when it does not resample); get_state() folds the pending
+    decisions in. The state must equal the synchronous oracle's."""
+    data = models.lgssm1d_data(40)
+    g, o = wsmc.Context(5001, seed=8), Oracle(5001, seed=8)
+    assert models.lgssm1d_statements(g, data, ess_perc_min=ess, scheme=scheme, wait=False) is None
+    flags = models.lgssm1d_statements(o, data, ess_perc_min=ess, scheme=scheme)
+    assert (ess < 1.0) == (not all(flags))          # ess 0.5 skips some steps: the identity path runs
+    assert_same_state(g, o)
+    np.testing.assert_array_equal(g.last_ancestors(), o.last_ancestors())
+    assert g.log_evidence() == o.log_evidence()
+    # a waited Resample after pending ones reports the same flag as the oracle's
+    for ctx in (g, o):
+        ctx.observe(wsmc.dsl.Normal(wsmc.dsl.Col("x"), 0.5).dist(models.resolver(ctx)), models._const([0.3]))
+    assert g.resample(ess, scheme) == o.resample(ess, scheme)
+    assert_same_state(g, o)
+
+
+@pytest.mark.parametrize("ess", [1.0, 0.5])
 def test_linreg_autorw(gpu_available, ess):
     xs, ys = models.linreg_data()
     g, o = wsmc.Context(20000, seed=42), Oracle(20000, seed=42)

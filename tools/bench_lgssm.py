@@ -35,21 +35,22 @@ def threads() -> int:
     return len(os.sched_getaffinity(0))
 
 
-def gpu(N=1_000_000, T=1000, reps=2):
+def gpu(N=1_000_000, T=1000, reps=2, wait=False):
     data = models.lgssm1d_data(T)
     best, ev = float("inf"), None
     for _ in range(reps + 1):           # the first run is the warm-up
         ctx = wsmc.Context(N, seed=42)
         ctx.sync()
         t0 = time.perf_counter()
-        flags = models.lgssm1d_statements(ctx, data, ess_perc_min=1.0)
+        models.lgssm1d_statements(ctx, data, ess_perc_min=1.0, wait=wait)   # no `if resampled`: no flags needed
         ctx.sync()
         dt = time.perf_counter() - t0
         ev = ctx.log_evidence()
+        nres = ctx.get_state()["n_resamples"]
         ctx.close()
         best = min(best, dt)
-    return {"leg": "gpu statements", "N": N, "T": T, "seconds_per_run": best, "particle_steps_per_s": N * T / best,
-            "resamples": int(sum(flags)), "log_evidence": ev, "reference_published_s": PUBLISHED_RUN_S,
+    return {"leg": "gpu statements" + (", flags to the host" if wait else ", decisions on the device"),
+            "N": N, "T": T, "seconds_per_run": best, "particle_steps_per_s": N * T / best, "resamples": nres, "log_evidence": ev, "reference_published_s": PUBLISHED_RUN_S,
             "speedup_vs_published": PUBLISHED_RUN_S / best}
 
 
@@ -68,10 +69,12 @@ def cpu(N, T, nth, reps=1):
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["gpu", "cpu_1t", "cpu_all"]
+    which = sys.argv[1:] or ["gpu", "gpu_wait", "cpu_1t", "cpu_all"]
     for w in which:
         if w == "gpu":
             r = gpu()
+        elif w == "gpu_wait":
+            r = gpu(wait=True)
         elif w == "cpu_1t":
             r = cpu(100_000, 1000, 1)
         else:

@@ -120,16 +120,19 @@ static void scores_touch(wsmc_ctx* c, int32_t col) {
     if (c->scache_terms >= 0 && tape_reads(c, col)) c->scache_terms = -1;
 }
 
-static int gather_all_columns(wsmc_ctx* c) {
+// dec != null: an asynchronous Resample, the gather is gated on the device-side decision
+static int gather_all_columns(wsmc_ctx* c, const Decision* dec = nullptr) {
+    auto gather = [&](double* dst, const double* src) {
+        return dec ? launch_gather_dec(c->stream, dst, src, c->anc, dec, c->N)
+                   : launch_gather(c->stream, dst, src, c->anc, c->N);
+    };
     for (auto& col : c->cols) {
-        for (int k = 0; k < col.dim; ++k) {
-            WSMC_HIP(launch_gather(c->stream, col.back + (int64_t)k * c->N, col.front + (int64_t)k * c->N, c->anc,
-                                   c->N));
-        }
+        for (int k = 0; k < col.dim; ++k)
+            WSMC_HIP(gather(col.back + (int64_t)k * c->N, col.front + (int64_t)k * c->N));
         std::swap(col.front, col.back);
     }
     if (c->scache && c->scache_terms >= 0) {   // carried Move scores follow their particles
-        WSMC_HIP(launch_gather(c->stream, c->scache_back, c->scache, c->anc, c->N));
+        WSMC_HIP(gather(c->scache_back, c->scache));
         std::swap(c->scache, c->scache_back);
     }
     c->colptr_dirty = true;
@@ -201,6 +204,7 @@ int wsmc_create(wsmc_ctx** out, int64_t n_particles, int32_t device, uint64_t se
     ALLOC(c->run_params, sizeof(uint64_t) * 8);
 #undef ALLOC
     if (e == hipSuccess) e = hipHostMalloc(&c->pinned, 4096, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&c->dec_ring, sizeof(Decision) * kDecRing, hipHostMallocDefault);
     if (e == hipSuccess) e = hipMemsetAsync(c->w, 0, sizeof(double) * c->N, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->anc, 0, sizeof(int32_t) * c->N, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -238,9 +242,25 @@ int wsmc_destroy(wsmc_ctx* c) {
     for (int32_t* p : c->lineage)
         if (p) (void)hipFree(p);
     if (c->pinned) (void)hipHostFree(c->pinned);
+    if (c->dec_ring) (void)hipHostFree(c->dec_ring);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
+    return WSMC_OK;
+}
+
+// fold the decisions of asynchronous Resamples (pinned ring, in issue order) into the host
+// mirror of state.resampled / n_resamples / last_ess
+static int resolve_decisions(wsmc_ctx* c) {
+    if (!c->dec_pending) return WSMC_OK;
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < c->dec_pending; ++i) {
+        const Decision& d = c->dec_ring[i];
+        c->last_ess = d.ess;
+        c->resampled = d.resampled;
+        if (d.resampled) c->n_resamples += 1;
+    }
+    c->dec_pending = 0;
     return WSMC_OK;
 }
 
@@ -258,6 +278,7 @@ int wsmc_nparticles(wsmc_ctx* c, int64_t* n) {
 
 int wsmc_get_state(wsmc_ctx* c, wsmc_state* s) {
     if (!c || !s) return fail(WSMC_EARG, "null argument");
+    if (int r = resolve_decisions(c)) return r;
     s->resampled = c->resampled;
     s->weights_changed = c->weights_changed;
     s->depth = c->depth;
@@ -1182,6 +1203,11 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
         return fail(WSMC_EARG, "multinomial draws on exact shards are not supported (island mode is)");
     if (scheme == WSMC_RESAMPLE_MULTINOMIAL && ensure_cdf(c)) return WSMC_EHIP;
     const uint64_t op = c->op++;
+    // no flag requested: the decision stays on the device (gated gather / weight reset), no
+    // host round trip; it is folded into the host state at the next read
+    const bool async = !resampled_out && !ess_out && !exact_mode(c);
+    if (!async)
+        if (int r = resolve_decisions(c)) return r;
     if (!c->weights_changed) {
         if (resampled_out) *resampled_out = c->resampled;
         if (ess_out) *ess_out = c->last_ess;
@@ -1207,6 +1233,17 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
                                        multi_esum(c), multi_ebuf(c), c->anc));
     else
         WSMC_HIP(launch_rs_scan(c->stream, c->N, c->rec + c->rank, c->dec, plan, c->tileOff, c->qbuf, c->anc));
+    if (async) {
+        if (c->dec_pending == kDecRing)
+            if ((r = resolve_decisions(c))) return r;
+        WSMC_HIP(hipMemcpyAsync(&c->dec_ring[c->dec_pending], c->dec, sizeof(Decision), hipMemcpyDeviceToHost,
+                                c->stream));
+        c->dec_pending += 1;
+        if ((r = gather_all_columns(c, c->dec))) return r;
+        WSMC_HIP(launch_fill_weights(c->stream, c->w, c->dec, c->N));
+        c->weights_changed = 0;
+        return WSMC_OK;
+    }
     Decision* hd = reinterpret_cast<Decision*>(c->pinned);
     WSMC_HIP(hipMemcpyAsync(hd, c->dec, sizeof(Decision), hipMemcpyDeviceToHost, c->stream));
     WSMC_HIP(hipStreamSynchronize(c->stream));
@@ -1923,6 +1960,7 @@ int wsmc_run_get_timing(wsmc_ctx* c, wsmc_run_timing* out) {
 int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, const double* v0, double q_var,
                    double r_var, double ess_min, int32_t scheme, int32_t keep_history, double* log_evidence_out) {
     CHECK_CTX(c);
+    if (int r = resolve_decisions(c)) return r;
     c->scache_terms = -1;   // the run rewrites columns the tape reads
     if (!obs || T < 1 || !x0 || !v0) return fail(WSMC_EARG, "bad arguments");
     if (!valid_scheme(scheme)) return fail(WSMC_EARG, "unknown resampling scheme");

@@ -53,6 +53,7 @@ constexpr int kPart = 4;      // per-tile partials: sum q, sum q21, sum q21^2, s
 constexpr int kRedPart = 6;   // reduce-kernel parts: Q, S1, S2 lo32/hi, Wf lo32/hi
 
 // Resample outcome for one invocation (one step of a fused run).
+constexpr int kDecRing = 1024;   // asynchronous Resample decisions held before a forced resolve
 struct Decision {
     int32_t resampled;
     int32_t ntasks;     // ancestor-fill tasks of this shard (<= ntiles + N / kRsChunk + 1)
@@ -93,6 +94,10 @@ struct RunGraph {
 struct wsmc_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // asynchronous Resamples (no flag requested): their decisions are copied into a pinned
+    // ring and folded into resampled / n_resamples / last_ess at the next host read
+    wsmc::Decision* dec_ring = nullptr;
+    int dec_pending = 0;
     int64_t N = 0;
     uint64_t seed = 0;
 
@@ -336,6 +341,8 @@ hipError_t launch_rs_fill_fused(hipStream_t s, int64_t N, const FillPlan& plan, 
                                 const unsigned long long* qbuf, int32_t* anc, hipEvent_t e0 = nullptr,
                                 hipEvent_t e1 = nullptr);
 hipError_t launch_gather(hipStream_t s, double* dst, const double* src, const int32_t* anc, int64_t N);
+hipError_t launch_gather_dec(hipStream_t s, double* dst, const double* src, const int32_t* anc, const Decision* dec,
+                             int64_t N);
 hipError_t launch_fill_weights(hipStream_t s, double* w, const Decision* dec, int64_t N);
 hipError_t launch_log_evidence_stats(hipStream_t s, const double* w, int64_t N, MaxSlots* ms,
                                      unsigned long long* tilep, unsigned long long* qbuf,

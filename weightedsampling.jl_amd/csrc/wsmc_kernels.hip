@@ -1963,6 +1963,21 @@ hipError_t debug_kernel_bench(hipStream_t s, int kernel, int mode, int iters, co
     return e != hipSuccess ? e : hipGetLastError();
 }
 
+// the ColumnStore gather of an asynchronous Resample (the host has not seen the decision):
+// through the ancestors if it resampled, else an identity copy, so the host's front/back
+// swap is right either way
+__global__ __launch_bounds__(kBlock) void k_gather_dec(double* __restrict__ dst, const double* __restrict__ src,
+                                                       const int32_t* __restrict__ anc, const Decision* dec,
+                                                       int64_t N) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= N) return;
+    dst[i] = src[dec->resampled ? (int64_t)anc[i] : i];
+}
+hipError_t launch_gather_dec(hipStream_t s, double* dst, const double* src, const int32_t* anc, const Decision* dec,
+                             int64_t N) {
+    hipLaunchKernelGGL(k_gather_dec, grid_for(N), dim3(kBlock), 0, s, dst, src, anc, dec, N);
+    return hipGetLastError();
+}
 hipError_t launch_gather(hipStream_t s, double* dst, const double* src, const int32_t* anc, int64_t N) {
     hipLaunchKernelGGL(k_gather, grid_for(N), dim3(kBlock), 0, s, dst, src, anc, N);
     return hipGetLastError();

@@ -246,7 +246,13 @@ class Context:
     def weight(self, dist: Dist, x) -> None:
         check(self._L.wsmc_weight(self._h, C.byref(dist), _operands4(x)))
 
-    def resample(self, ess_perc_min: float, scheme: int = abi.RESAMPLE_STRATIFIED):
+    def resample(self, ess_perc_min: float, scheme: int = abi.RESAMPLE_STRATIFIED, wait: bool = True):
+        """Resample.apply!; returns (resampled, ESS%). wait=False leaves the decision on the
+        device (no host round trip; the gather and weight reset are gated there) and returns
+        None; get_state() folds it in later."""
+        if not wait:
+            check(self._L.wsmc_resample(self._h, float(ess_perc_min), int(scheme), None, None))
+            return None
         r = C.c_int32()
         e = C.c_double()
         check(self._L.wsmc_resample(self._h, float(ess_perc_min), int(scheme), C.byref(r), C.byref(e)))

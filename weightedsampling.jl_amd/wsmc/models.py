@@ -85,23 +85,26 @@ def ssm1d_statements(ctx, obs, q_sd=0.1, r_sd=1.0, ess_perc_min=0.5, scheme=abi.
 
 
 def lgssm1d_statements(ctx, data, a=0.9, q=1.0, r=0.5, x0_std=1.0, ess_perc_min=1.0,
-                       scheme=abi.RESAMPLE_STRATIFIED):
+                       scheme=abi.RESAMPLE_STRATIFIED, wait=True):
     """The reference's own CPU benchmark model, benchmarks/ssm/WeightedSampling/lgssm1d.jl:18-24:
     x ~ Normal(0, x0_std); for y in data: x ~ Normal(a x, q); y => Normal(x, r); end.
     `x` is rebound, so the store keeps one column (no history), and every `~`/`=>` is
-    followed by its auto-inserted Resample (a no-op after a Sample)."""
+    followed by its auto-inserted Resample (a no-op after a Sample). The model has no `if
+    resampled`, so with wait=False no Resample returns its flag to the host (the decisions
+    stay on the device) and the function returns None."""
     R = resolver(ctx)
     cx = ctx.col_create("x", 1)
     ctx.sample(cx, Normal(0.0, x0_std).dist(R))
-    ctx.resample(ess_perc_min, scheme)
+    ctx.resample(ess_perc_min, scheme, wait=wait)
     resampled = []
     for y in np.asarray(data, dtype=float):
         ctx.sample(cx, Normal(Col("x") * a, q).dist(R))                     # x ~ Normal(a*x, q)
-        ctx.resample(ess_perc_min, scheme)
+        ctx.resample(ess_perc_min, scheme, wait=wait)
         ctx.observe(Normal(Col("x"), r).dist(R), _const([y]))               # y => Normal(x, r)
-        rs, _ = ctx.resample(ess_perc_min, scheme)
-        resampled.append(rs)
-    return resampled
+        rs = ctx.resample(ess_perc_min, scheme, wait=wait)
+        if wait:
+            resampled.append(rs[0])
+    return resampled if wait else None
 
 
 def linreg_statements(ctx, xs, ys, prior_sd=10.0, obs_sd=1.0, ess_perc_min=0.5,
