@@ -218,7 +218,10 @@ int wsmc_observe(wsmc_ctx* ctx, const wsmc_dist* dist, const wsmc_operand* x);
 /* Weight (_ ~ f(args)): weights .+= logpdf(dist, x)     src/transformers.jl:283-289 */
 int wsmc_weight(wsmc_ctx* ctx, const wsmc_dist* dist, const wsmc_operand* x);
 /* Resample (gated on weights_changed, strict ESS test, log-mean reset)
- *                                                       src/transformers.jl:474-498 */
+ *                                                       src/transformers.jl:474-498
+ *   resampled_out / ess_perc_out both NULL: asynchronous — the decision stays on the device
+ *   (gated gather and weight reset, no host wait) and is folded into wsmc_get_state's
+ *   resampled / n_resamples / last_ess_perc at the next read (exact shards always wait). */
 int wsmc_resample(wsmc_ctx* ctx, double ess_perc_min, int32_t scheme,
                   int32_t* resampled_out, double* ess_perc_out);
 /* Move with RW / autoRW (src/transformers.jl:588-623, src/move_kernels.jl:189-253).
