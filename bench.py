@@ -95,6 +95,9 @@ def cpu_model() -> str:
     return "unknown CPU"
 
 
+CPU_REPS = 5   # timed all-cores CPU runs after the warm-up; the median is reported
+
+
 def _oracle():
     sys.path.insert(0, str(REPO / "oracle"))
     import oracle  # test infrastructure: only the cpu_baseline leg loads it
@@ -109,9 +112,13 @@ def cpu_baseline_mt(obs, n, T, ess, scheme, threads, seed):
     oracle.keep_heap()
     oracle.ssm2d_run_mt(n, obs[:T], seed=seed, ess_perc_min=ess, scheme=scheme, threads=threads,
                         outputs=False)   # warm-up: thread pool, first touch of the run's buffers
-    t0 = time.perf_counter()
-    oracle.ssm2d_run_mt(n, obs[:T], seed=seed, ess_perc_min=ess, scheme=scheme, threads=threads, outputs=False)
-    dt = time.perf_counter() - t0
+    ts = []
+    for _ in range(CPU_REPS):
+        t0 = time.perf_counter()
+        oracle.ssm2d_run_mt(n, obs[:T], seed=seed, ess_perc_min=ess, scheme=scheme, threads=threads,
+                            outputs=False)
+        ts.append(time.perf_counter() - t0)
+    dt = sorted(ts)[len(ts) // 2]   # median
     return n * T / dt, dt
 
 
@@ -124,9 +131,12 @@ def cpu_baseline_fast(obs, n, T, ess, threads, seed):
     oracle = _oracle()
     oracle.keep_heap()
     oracle.fast_ssm2d_run(n, obs[:T], ess_perc_min=ess, seed=seed, threads=threads)   # warm-up (first touch)
-    t0 = time.perf_counter()
-    oracle.fast_ssm2d_run(n, obs[:T], ess_perc_min=ess, seed=seed, threads=threads)
-    dt = time.perf_counter() - t0
+    ts = []
+    for _ in range(CPU_REPS if threads > 1 else 1):
+        t0 = time.perf_counter()
+        oracle.fast_ssm2d_run(n, obs[:T], ess_perc_min=ess, seed=seed, threads=threads)
+        ts.append(time.perf_counter() - t0)
+    dt = sorted(ts)[len(ts) // 2]   # median
     return n * T / dt, dt
 
 
@@ -279,16 +289,17 @@ def main():
             cps, cdt = cpu_baseline_mt(obs, n, T, args.ess, scheme, nth, args.seed)
             c1, c1dt = cpu_baseline_1t(obs, args.cpu_1t_particles, T, args.ess, scheme, args.seed)
             lg, lgdt = cpu_fairness_lgssm()
-            fast = {"value": fps, "unit": "particle-steps/s", "cores": nth, "kind": "port",
+            fast_leg = {"value": fps, "unit": "particle-steps/s", "cores": nth, "kind": "port",
                     "sample": f"oracle/wsmc_port_fast.c (the reference's algorithm with xoshiro256++/ziggurat/"
                               f"libm, OpenMP over particles, {nth} threads on {cpu_model()}): the full 2D SSM "
-                              f"run, N={n} T={T} ess_perc_min={args.ess}, history traced back: {fdt:.2f} s"}
-            exact = {"value": cps, "unit": "particle-steps/s", "cores": nth, "kind": "port",
+                              f"run, N={n} T={T} ess_perc_min={args.ess}, history traced back: {fdt:.2f} s (median of {CPU_REPS})"}
+            exact_leg = {"value": cps, "unit": "particle-steps/s", "cores": nth, "kind": "port",
                      "sample": f"oracle/wsmc_port_mt.c (bit-identical to the device; OpenMP over particles, "
                                f"{nth} threads on {cpu_model()}): the full 2D SSM run, N={n} T={T} "
-                               f"ess_perc_min={args.ess}, history traced back: {cdt:.2f} s"}
+                               f"ess_perc_min={args.ess}, history traced back: {cdt:.2f} s (median of {CPU_REPS})"}
             # the baseline is the faster of the two all-cores ports; the other is reported beside it
-            best, other, other_key = (fast, exact, "exact_port") if fps >= cps else (exact, fast, "fast_port")
+            best, other, other_key = ((fast_leg, exact_leg, "exact_port") if fps >= cps
+                                      else (exact_leg, fast_leg, "fast_port"))
             cpu = dict(best)
             cpu.update({
                 other_key: other,
