@@ -423,3 +423,68 @@ def test_one_rank_rccl_matches_unsharded_oracle(gpu_available, tmp_path, mode):
     assert [tuple(a) for a in r["gacc"]] == _move_program(o, "c5g")
     for name in o.col_names():
         np.testing.assert_array_equal(r["g_" + name], o.col_download(o.col_find(name)), err_msg=name)
+
+
+def _analysis_worker(rank, world, port, sizes, outdir):
+    sys.path[:0] = [str(REPO / "weightedsampling.jl_amd")]
+    import wsmc
+    from wsmc.abi import Operand
+    from wsmc.hostcomm import HostComm
+    comm = HostComm(rank, world, "127.0.0.1", port, tag="an", timeout=120)
+    n, goff, N = sizes[rank], sum(sizes[:rank]), sum(sizes)
+    c = wsmc.Context(n, seed=44, device=0)
+    c.comm_init_host(comm.allgather, world, rank, goff, N)
+    xs, ys = wsmc.models.linreg_data()
+    wsmc.models.linreg_statements(c, xs[:5], ys[:5], ess_perc_min=0.3)
+    a, b = c.col_find("α"), c.col_find("β")
+    mean, cov = c.weighted_moments([Operand.column(a), Operand.column(b, coef=2.0, c0=1.0)])
+    out = {"mean": np.asarray(mean), "cov": np.asarray(cov), "ess": np.array([c.ess()]),
+           "ev": np.array([c.log_evidence()])}
+    for k, col in (("a", a), ("b", b)):
+        out["mm" + k] = np.array(c.col_minmax(col))
+        out["h" + k] = c.histogram(col)
+    c.close()
+    comm.barrier()
+    comm.close()
+    np.savez(os.path.join(outdir, f"an{rank}.npz"), **out)
+
+
+@pytest.mark.parametrize("sizes", [(3000, 3000), (70001, 70001)])
+def test_two_shards_analysis_match_single_context(gpu_available, tmp_path, sizes):
+    """describe / @E on island shards: min/max, the sparkline histogram (integer weights
+    relative to the population's max: bit-identical bins) and ESS equal the sharded oracle's
+    population-wide values exactly; the weighted moments are rank-order combinations of
+    per-shard canonical sums, equal to the population's up to summation order."""
+    import multiprocessing as mp
+    sys.path.insert(0, str(REPO / "oracle"))
+    from oracle import Oracle
+    import wsmc
+    from wsmc.abi import Operand
+    world = len(sizes)
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=_analysis_worker, args=(r, world, port, sizes, str(tmp_path))) for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(300)
+    codes = [p.exitcode for p in ps]
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+    assert codes == [0] * world, codes
+    # island shards resample within themselves: the reference population is the sharded oracle's
+    o = Oracle(sum(sizes), seed=44, shards=world)
+    xs, ys = wsmc.models.linreg_data()
+    wsmc.models.linreg_statements(o, xs[:5], ys[:5], ess_perc_min=0.3)
+    a, b = o.col_find("α"), o.col_find("β")
+    mean, cov = o.weighted_moments([Operand.column(a), Operand.column(b, coef=2.0, c0=1.0)])
+    parts = [np.load(tmp_path / f"an{r}.npz") for r in range(world)]
+    for p in parts:
+        for k, col in (("a", a), ("b", b)):
+            np.testing.assert_array_equal(p["mm" + k], np.array(o.col_minmax(col)))
+            np.testing.assert_array_equal(p["h" + k], o.histogram(col))
+        assert p["ess"][0] == o.ess()
+        assert p["ev"][0] == o.log_evidence()
+        np.testing.assert_allclose(p["mean"], mean, rtol=1e-12)
+        np.testing.assert_allclose(p["cov"], cov, rtol=1e-10)

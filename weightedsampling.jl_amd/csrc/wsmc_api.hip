@@ -857,10 +857,41 @@ static int trace_level(wsmc_ctx* c, const ExactPlan& x, const double* hist, cons
 }
 
 // ---- analysis reductions (src/utils.jl) ----------------------------------------------
+// all-gather `words` (<= 16) host words per rank through the exchange buffer; all[W * words]
+static int allgather_host_words(wsmc_ctx* c, const unsigned long long* mine, int words, unsigned long long* all) {
+    unsigned long long* dbuf = c->xchg;   // 16 words per rank
+    WSMC_HIP(hipMemcpyAsync(dbuf + (size_t)c->rank * words, mine, sizeof(unsigned long long) * words,
+                            hipMemcpyHostToDevice, c->stream));
+    int r = exchange_words(c, dbuf, words, c->stream);
+    if (r) return r;
+    WSMC_HIP(hipMemcpyAsync(all, dbuf, sizeof(unsigned long long) * words * c->world, hipMemcpyDeviceToHost,
+                            c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    return WSMC_OK;
+}
+// the population's max log-weight into c->mslots (slot 0; the others zero), so that every
+// shard's exp(lw - M) and integer weights are relative to the same M
+static int adopt_global_max(wsmc_ctx* c) {
+    WSMC_HIP(hipMemsetAsync(c->mslots, 0, sizeof(MaxSlots), c->stream));
+    WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, c->mslots));
+    MaxSlots hs;
+    WSMC_HIP(hipMemcpyAsync(&hs, c->mslots, sizeof(MaxSlots), hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    unsigned long long menc = 0;
+    for (int k = 0; k < kSlots; ++k) menc = hs.v[k][0] > menc ? hs.v[k][0] : menc;
+    std::vector<unsigned long long> ex(c->world);
+    int r = allgather_host_words(c, &menc, 1, ex.data());
+    if (r) return r;
+    for (int g = 0; g < c->world; ++g) menc = ex[g] > menc ? ex[g] : menc;
+    std::memset(&hs, 0, sizeof(hs));
+    hs.v[0][0] = menc;
+    WSMC_HIP(hipMemcpyAsync(c->mslots, &hs, sizeof(MaxSlots), hipMemcpyHostToDevice, c->stream));
+    return WSMC_OK;
+}
+
 int wsmc_weighted_moments(wsmc_ctx* c, const wsmc_operand* exprs, int32_t d, double* mean, double* cov) {
     CHECK_CTX(c);
     if (!exprs || !mean || d < 1 || d > 4) return fail(WSMC_EARG, "need 1..4 expressions and a mean buffer");
-    if (c->world > 1) return fail(WSMC_ESTATE, "analysis reductions on sharded contexts are not supported yet");
     for (int k = 0; k < d; ++k) {
         int r = check_operand(c, exprs[k]);
         if (r) return r;
@@ -869,6 +900,54 @@ int wsmc_weighted_moments(wsmc_ctx* c, const wsmc_operand* exprs, int32_t d, dou
     if (r) return r;
     wsmc_operand ex[4];
     for (int k = 0; k < 4; ++k) ex[k] = exprs[k < d ? k : 0];
+    if (is_sharded(c)) {
+        // population-wide: the global max, then each shard's canonical totals combined in
+        // rank order (the sharded autoRW's moment protocol), means, then centred products
+        if ((r = adopt_global_max(c))) return r;
+        const int W = c->world, n1 = 1 + d, n2 = d * (d + 1) / 2;
+        std::vector<unsigned long long> all(16 * W);
+        double mom[64];
+        auto rank_sums = [&](int n, double* out) {
+            for (int v = 0; v < n; ++v) {
+                double acc = 0.0;
+                for (int g = 0; g < W; ++g) {
+                    double x;
+                    std::memcpy(&x, &all[(size_t)g * n + v], 8);
+                    acc = g == 0 ? x : acc + x;
+                }
+                out[v] = acc;
+            }
+        };
+        WSMC_HIP(launch_moments_expr(c->stream, c->w, c->mslots, c->d_colptr, ex, d, 1, c->mom, c->N, c->tilepart));
+        WSMC_HIP(launch_moments_final(c->stream, c->tilepart, c->ntiles, d, 1, 0.0, c->mom, c->dflag, 2));
+        WSMC_HIP(hipMemcpyAsync(mom, c->mom, sizeof(mom), hipMemcpyDeviceToHost, c->stream));
+        WSMC_HIP(hipStreamSynchronize(c->stream));
+        if ((r = allgather_host_words(c, reinterpret_cast<const unsigned long long*>(mom + 48), n1, all.data())))
+            return r;
+        double t1[5];
+        rank_sums(n1, t1);
+        const double S0 = t1[0];
+        for (int k = 0; k < d; ++k) mean[k] = mom[k] = t1[1 + k] / S0;
+        mom[8] = S0;
+        if (!cov) return WSMC_OK;
+        WSMC_HIP(hipMemcpyAsync(c->mom, mom, sizeof(double) * 16, hipMemcpyHostToDevice, c->stream));
+        WSMC_HIP(launch_moments_expr(c->stream, c->w, c->mslots, c->d_colptr, ex, d, 2, c->mom, c->N, c->tilepart));
+        WSMC_HIP(launch_moments_final(c->stream, c->tilepart, c->ntiles, d, 2, 0.0, c->mom, c->dflag, 2));
+        WSMC_HIP(hipMemcpyAsync(mom + 48, c->mom + 48, sizeof(double) * 16, hipMemcpyDeviceToHost, c->stream));
+        WSMC_HIP(hipStreamSynchronize(c->stream));
+        if ((r = allgather_host_words(c, reinterpret_cast<const unsigned long long*>(mom + 48), n2, all.data())))
+            return r;
+        double t2[10];
+        rank_sums(n2, t2);
+        int v = 0;
+        for (int a = 0; a < d; ++a)
+            for (int b = a; b < d; ++b) {
+                const double cv = t2[v++] / S0;
+                cov[a * d + b] = cv;
+                cov[b * d + a] = cv;
+            }
+        return WSMC_OK;
+    }
     WSMC_HIP(hipMemsetAsync(c->mslots, 0, sizeof(MaxSlots), c->stream));
     WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, c->mslots));
     WSMC_HIP(launch_moments_expr(c->stream, c->w, c->mslots, c->d_colptr, ex, d, 1, c->mom, c->N, c->tilepart));
@@ -900,6 +979,16 @@ int wsmc_col_minmax(wsmc_ctx* c, int32_t col, int32_t comp, double* mn, double* 
     for (int k = 0; k < kSlots; ++k) {
         a = h.v[k][0] > a ? h.v[k][0] : a;
         b = h.v[k][1] > b ? h.v[k][1] : b;
+    }
+    if (is_sharded(c)) {   // the population's extremes (order-free)
+        const unsigned long long mine[2] = {a, b};
+        std::vector<unsigned long long> all(2 * c->world);
+        const int r = allgather_host_words(c, mine, 2, all.data());
+        if (r) return r;
+        for (int g = 0; g < c->world; ++g) {
+            a = all[2 * g] > a ? all[2 * g] : a;
+            b = all[2 * g + 1] > b ? all[2 * g + 1] : b;
+        }
     }
     *mx = wsmc_ord_dec(a);
     *mn = -wsmc_ord_dec(b);
@@ -963,16 +1052,33 @@ int wsmc_weighted_median(wsmc_ctx* c, int32_t col, int32_t comp, double* out) {
 int wsmc_histogram(wsmc_ctx* c, int32_t col, int32_t comp, int32_t levels[8]) {
     CHECK_CTX(c);
     if (!levels) return fail(WSMC_EARG, "null output");
-    if (c->world > 1) return fail(WSMC_ESTATE, "analysis reductions on sharded contexts are not supported yet");
     double lo, hi;
-    int r = wsmc_col_minmax(c, col, comp, &lo, &hi);
+    int r = wsmc_col_minmax(c, col, comp, &lo, &hi);   // population-wide on shards
     if (r) return r;
     if (lo == hi) {                                                // _sparkline(fill(sum(w), 8))
         for (int b = 0; b < 8; ++b) levels[b] = 8;
         return WSMC_OK;
     }
     unsigned long long Q = 0;
-    if ((r = local_q(c, &Q))) return r;
+    const bool sh = is_sharded(c);
+    if (sh) {
+        // integer weights relative to the population's max with the global N's K: exactly
+        // the single-context q, so the summed bins are the unsharded bins
+        if ((r = adopt_global_max(c))) return r;
+        WSMC_HIP(launch_rs_sums(c->stream, c->w, c->N, c->mslots, c->tilep, c->qbuf, nullptr, nullptr, nullptr, 1,
+                                c->gN));
+        WSMC_HIP(launch_rs_reduce(c->stream, c->mslots, c->tilep, c->N, c->tileOff, c->rec, 0, 0.0, nullptr,
+                                  nullptr));
+        ShardRecord* hr = reinterpret_cast<ShardRecord*>(c->pinned);
+        WSMC_HIP(hipMemcpyAsync(hr, c->rec, sizeof(ShardRecord), hipMemcpyDeviceToHost, c->stream));
+        WSMC_HIP(hipStreamSynchronize(c->stream));
+        const unsigned long long mine = hr->Q;
+        std::vector<unsigned long long> all(c->world);
+        if ((r = allgather_host_words(c, &mine, 1, all.data()))) return r;
+        for (int g = 0; g < c->world; ++g) Q += all[g];
+    } else if ((r = local_q(c, &Q))) {
+        return r;
+    }
     if (Q == 0) return fail(WSMC_ESTATE, "the weights do not normalise (all -Inf or NaN)");
     double edges[9];
     for (int k = 0; k <= 8; ++k) edges[k] = wsmc_linspace_edge(lo, hi, k, 8);
@@ -982,6 +1088,14 @@ int wsmc_histogram(wsmc_ctx* c, int32_t col, int32_t comp, int32_t levels[8]) {
     unsigned long long h[8];
     WSMC_HIP(hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     WSMC_HIP(hipStreamSynchronize(c->stream));
+    if (sh) {   // integer bin sums: order-free
+        std::vector<unsigned long long> all(8 * c->world);
+        if ((r = allgather_host_words(c, h, 8, all.data()))) return r;
+        for (int b = 0; b < 8; ++b) {
+            h[b] = 0;
+            for (int g = 0; g < c->world; ++g) h[b] += all[(size_t)g * 8 + b];
+        }
+    }
     unsigned long long mxc = 0;
     for (int b = 0; b < 8; ++b) mxc = h[b] > mxc ? h[b] : mxc;
     for (int b = 0; b < 8; ++b) levels[b] = wsmc_spark_level(h[b], mxc);
