@@ -443,6 +443,7 @@ def _analysis_worker(rank, world, port, sizes, outdir):
     for k, col in (("a", a), ("b", b)):
         out["mm" + k] = np.array(c.col_minmax(col))
         out["h" + k] = c.histogram(col)
+        out["md" + k] = np.array([c.weighted_median(col)])
     c.close()
     comm.barrier()
     comm.close()
@@ -452,7 +453,8 @@ def _analysis_worker(rank, world, port, sizes, outdir):
 @pytest.mark.parametrize("sizes", [(3000, 3000), (70001, 70001)])
 def test_two_shards_analysis_match_single_context(gpu_available, tmp_path, sizes):
     """describe / @E on island shards: min/max, the sparkline histogram (integer weights
-    relative to the population's max: bit-identical bins) and ESS equal the sharded oracle's
+    relative to the population's max: bit-identical bins), the weighted median (over the
+    all-gathered (value, q) union) and ESS equal the sharded oracle's
     population-wide values exactly; the weighted moments are rank-order combinations of
     per-shard canonical sums, equal to the population's up to summation order."""
     import multiprocessing as mp
@@ -484,6 +486,7 @@ def test_two_shards_analysis_match_single_context(gpu_available, tmp_path, sizes
         for k, col in (("a", a), ("b", b)):
             np.testing.assert_array_equal(p["mm" + k], np.array(o.col_minmax(col)))
             np.testing.assert_array_equal(p["h" + k], o.histogram(col))
+            assert p["md" + k][0] == o.weighted_median(col)
         assert p["ess"][0] == o.ess()
         assert p["ev"][0] == o.log_evidence()
         np.testing.assert_allclose(p["mean"], mean, rtol=1e-12)

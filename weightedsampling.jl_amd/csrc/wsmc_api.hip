@@ -1008,45 +1008,91 @@ static int local_q(wsmc_ctx* c, unsigned long long* Q) {
     return WSMC_OK;
 }
 
-int wsmc_weighted_median(wsmc_ctx* c, int32_t col, int32_t comp, double* out) {
-    CHECK_CTX(c);
-    if (!out) return fail(WSMC_EARG, "null output");
-    if (c->world > 1) return fail(WSMC_ESTATE, "analysis reductions on sharded contexts are not supported yet");
-    double mn, mx;
-    int r = wsmc_col_minmax(c, col, comp, &mn, &mx);
-    if (r) return r;
-    if (wsmc_isnan(mx)) { *out = mx; return WSMC_OK; }          // a NaN value: NaN (StatsBase)
-    unsigned long long Q = 0;
-    if ((r = local_q(c, &Q))) return r;
-    if (Q == 0) return fail(WSMC_ESTATE, "weight vector cannot sum to zero");
-    const int64_t N = c->N;
-    unsigned long long* kin = reinterpret_cast<unsigned long long*>(c->tmp);
-    unsigned long long* kout = kin + N;
-    unsigned long long* vin = kout + N;
-    unsigned long long* vout = vin + N;
-    WSMC_HIP(launch_median_keys(c->stream, c->cols[col].front + (int64_t)comp * N, c->qbuf, N, kin, vin));
+// StatsBase's weighted median of n (value, integer weight) pairs; zero weights drop out, so
+// zero-weight padding is harmless
+static int median_of(wsmc_ctx* c, const double* x, const unsigned long long* q, int64_t n, double* out) {
+    using u64 = unsigned long long;
+    u64* buf = nullptr;
+    WSMC_HIP(hipMalloc(&buf, sizeof(u64) * 4 * (size_t)n));
+    u64 *kin = buf, *kout = buf + n, *vin = buf + 2 * n, *vout = buf + 3 * n;
+    hipError_t e = launch_median_keys(c->stream, x, q, n, kin, vin);
     // (value, weight) order: stable radix sorts by weight, then by value
     size_t tb1 = 0, tb2 = 0;
-    WSMC_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb1, kin, kout, vin, vout, (int)N, 0, 64, c->stream));
-    WSMC_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tb2, vin, kout, (int)N, c->stream));
+    if (e == hipSuccess)
+        e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb1, kin, kout, vin, vout, (int)n, 0, 64, c->stream);
+    if (e == hipSuccess) e = hipcub::DeviceScan::InclusiveSum(nullptr, tb2, vin, kout, (int)n, c->stream);
     const size_t tb = (tb1 > tb2 ? tb1 : tb2) + 16;
     void* ts = nullptr;
     double* dout = nullptr;
-    WSMC_HIP(hipMalloc(&ts, tb));
-    hipError_t e = hipMalloc(&dout, sizeof(double));
+    if (e == hipSuccess) e = hipMalloc(&ts, tb);
+    if (e == hipSuccess) e = hipMalloc(&dout, sizeof(double));
     size_t t = tb;
-    if (e == hipSuccess) e = hipcub::DeviceRadixSort::SortPairs(ts, t, kin, kout, vin, vout, (int)N, 0, 64, c->stream);
+    if (e == hipSuccess) e = hipcub::DeviceRadixSort::SortPairs(ts, t, kin, kout, vin, vout, (int)n, 0, 64, c->stream);
     t = tb;
-    if (e == hipSuccess) e = hipcub::DeviceRadixSort::SortPairs(ts, t, vout, kin, kout, vin, (int)N, 0, 64, c->stream);
+    if (e == hipSuccess) e = hipcub::DeviceRadixSort::SortPairs(ts, t, vout, kin, kout, vin, (int)n, 0, 64, c->stream);
     t = tb;
-    if (e == hipSuccess) e = hipcub::DeviceScan::InclusiveSum(ts, t, vin, kout, (int)N, c->stream);
-    if (e == hipSuccess) e = launch_median_pick(c->stream, kin, vin, kout, N, dout);
+    if (e == hipSuccess) e = hipcub::DeviceScan::InclusiveSum(ts, t, vin, kout, (int)n, c->stream);
+    if (e == hipSuccess) e = launch_median_pick(c->stream, kin, vin, kout, n, dout);
     if (e == hipSuccess) e = hipMemcpyAsync(out, dout, sizeof(double), hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    (void)hipFree(ts);
+    if (ts) (void)hipFree(ts);
     if (dout) (void)hipFree(dout);
+    (void)hipFree(buf);
     if (e != hipSuccess) return fail(WSMC_EHIP, std::string("weighted median: ") + hipGetErrorString(e));
     return WSMC_OK;
+}
+
+int wsmc_weighted_median(wsmc_ctx* c, int32_t col, int32_t comp, double* out) {
+    CHECK_CTX(c);
+    if (!out) return fail(WSMC_EARG, "null output");
+    double mn, mx;
+    int r = wsmc_col_minmax(c, col, comp, &mn, &mx);   // population-wide on shards
+    if (r) return r;
+    if (wsmc_isnan(mx)) { *out = mx; return WSMC_OK; }          // a NaN value: NaN (StatsBase)
+    const double* x = c->cols[col].front + (int64_t)comp * c->N;
+    if (!is_sharded(c)) {
+        unsigned long long Q = 0;
+        if ((r = local_q(c, &Q))) return r;
+        if (Q == 0) return fail(WSMC_ESTATE, "weight vector cannot sum to zero");
+        return median_of(c, x, c->qbuf, c->N, out);
+    }
+    // shards: integer weights relative to the population's max (the single-context q), then
+    // every rank's (value, q) all-gathered, zero-weight padded to the largest shard, and the
+    // median taken over the union on every rank
+    using u64 = unsigned long long;
+    if ((r = adopt_global_max(c))) return r;
+    WSMC_HIP(launch_rs_sums(c->stream, c->w, c->N, c->mslots, c->tilep, c->qbuf, nullptr, nullptr, nullptr, 1, c->gN));
+    WSMC_HIP(launch_rs_reduce(c->stream, c->mslots, c->tilep, c->N, c->tileOff, c->rec, 0, 0.0, nullptr, nullptr));
+    ShardRecord* hr = reinterpret_cast<ShardRecord*>(c->pinned);
+    WSMC_HIP(hipMemcpyAsync(hr, c->rec, sizeof(ShardRecord), hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    const u64 mine[2] = {(u64)c->N, hr->Q};
+    std::vector<u64> all(2 * c->world);
+    if ((r = allgather_host_words(c, mine, 2, all.data()))) return r;
+    u64 nmax = 1, Q = 0;
+    for (int g = 0; g < c->world; ++g) {
+        nmax = all[2 * g] > nmax ? all[2 * g] : nmax;
+        Q += all[2 * g + 1];
+    }
+    if (Q == 0) return fail(WSMC_ESTATE, "weight vector cannot sum to zero");
+    const int64_t U = (int64_t)nmax * c->world;
+    u64* g = nullptr;
+    WSMC_HIP(hipMalloc(&g, sizeof(u64) * 2 * (size_t)U));
+    u64 *gx = g, *gq = g + U;
+    hipError_t e = hipMemsetAsync(g, 0, sizeof(u64) * 2 * (size_t)U, c->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(gx + nmax * c->rank, x, sizeof(double) * c->N, hipMemcpyDeviceToDevice, c->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(gq + nmax * c->rank, c->qbuf, sizeof(u64) * c->N, hipMemcpyDeviceToDevice, c->stream);
+    if (e != hipSuccess) {
+        (void)hipFree(g);
+        return fail(WSMC_EHIP, std::string("weighted median: ") + hipGetErrorString(e));
+    }
+    r = exchange_words(c, gx, (int64_t)nmax, c->stream);
+    if (!r) r = exchange_words(c, gq, (int64_t)nmax, c->stream);
+    if (!r) r = median_of(c, reinterpret_cast<const double*>(gx), gq, U, out);
+    (void)hipFree(g);
+    return r;
 }
 
 int wsmc_histogram(wsmc_ctx* c, int32_t col, int32_t comp, int32_t levels[8]) {
