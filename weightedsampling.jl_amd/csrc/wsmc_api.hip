@@ -2200,7 +2200,7 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
     }();
     // HIP cannot time events captured in graphs; a host exchange (test mode) synchronises
     // inside the run, and exact shards are host-driven. RCCL collectives are captured.
-    const bool use_graph = !c->timing && !no_graph && !exact_mode(c) && !c->host_exchange;
+    const bool use_graph = !c->timing && !no_graph && !c->no_graph && !exact_mode(c) && !c->host_exchange;
     if (exact_mode(c) && c->timing) return fail(WSMC_ESTATE, "run timing is not available on exact shards");
     const int nev = 8 * T + 2;
     std::vector<hipEvent_t> evs;
@@ -2215,41 +2215,64 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
     void* temp_tables = nullptr;
     if (exact_mode(c)) {
         if ((r = ssm2d_run_exact(c, p, op_base))) return r;
-    } else if (use_graph) {
-        RunGraph* g = nullptr;
-        for (auto& gg : c->graphs)
-            if (gg.key == key) g = &gg;
-        if (!g) {
-            RunGraph ng;
-            ng.key = key;
+    } else {
+        bool graphed = false;
+        if (use_graph) {
+            RunGraph* g = nullptr;
+            for (auto& gg : c->graphs)
+                if (gg.key == key) g = &gg;
+            if (!g) {
+                RunGraph ng;
+                ng.key = key;
+                if ((r = build_tables(&p.d_hist_work, &p.d_hist_out))) return r;
+                ng.owned = p.d_hist_work;
+                WSMC_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+                r = enqueue_ssm2d(c, p, c->timing ? &evs : nullptr);
+                static const bool diag_fail = [] {   // diagnostics: exercise the eager fallback
+                    const char* e = getenv("WSMC_DIAG_CAPTURE_FAIL");
+                    return e && atoi(e) != 0;
+                }();
+                if (!r && diag_fail) r = fail(WSMC_EHIP, "diagnostic capture failure");
+                hipGraph_t graph = nullptr;
+                hipError_t ee = hipStreamEndCapture(c->stream, &graph);
+                hipGraphExec_t exec = nullptr;
+                if (!r && ee == hipSuccess) ee = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+                if (r || ee != hipSuccess) {
+                    if (graph) (void)hipGraphDestroy(graph);
+                    if (ng.owned) (void)hipFree(ng.owned);
+                    p.d_hist_work = p.d_hist_out = nullptr;
+                    if (!is_sharded(c)) {
+                        if (r) return r;
+                        WSMC_HIP(ee);
+                    }
+                    // a sharded run whose collectives would not capture runs eagerly from now on
+                    (void)hipGetLastError();
+                    std::fprintf(stderr, "wsmc: capturing the sharded run failed (%s); running it eagerly\n",
+                                 r ? wsmc_last_error() : hipGetErrorString(ee));
+                    c->no_graph = true;
+                } else {
+                    ng.graph = graph;
+                    ng.exec = exec;
+                    c->graphs.push_back(ng);
+                    g = &c->graphs.back();
+                }
+            }
+            if (g) {
+                WSMC_HIP(hipGraphLaunch(g->exec, c->stream));
+                graphed = true;
+            }
+        }
+        if (!graphed) {
             if ((r = build_tables(&p.d_hist_work, &p.d_hist_out))) return r;
-            ng.owned = p.d_hist_work;
-            WSMC_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+            temp_tables = p.d_hist_work;
+            // instrumented runs: a bounded delay kernel keeps the GPU busy while the host
+            // queues the whole run, so no host-submission gap lands inside an event pair
+            if (c->timing) WSMC_HIP(launch_delay(c->stream, 20000));
             r = enqueue_ssm2d(c, p, c->timing ? &evs : nullptr);
-            hipGraph_t graph = nullptr;
-            hipError_t ee = hipStreamEndCapture(c->stream, &graph);
             if (r) {
-                if (graph) (void)hipGraphDestroy(graph);
-                if (ng.owned) (void)hipFree(ng.owned);
+                if (temp_tables) (void)hipFree(temp_tables);
                 return r;
             }
-            WSMC_HIP(ee);
-            ng.graph = graph;
-            WSMC_HIP(hipGraphInstantiate(&ng.exec, graph, nullptr, nullptr, 0));
-            c->graphs.push_back(ng);
-            g = &c->graphs.back();
-        }
-        WSMC_HIP(hipGraphLaunch(g->exec, c->stream));
-    } else {
-        if ((r = build_tables(&p.d_hist_work, &p.d_hist_out))) return r;
-        temp_tables = p.d_hist_work;
-        // instrumented runs: a bounded delay kernel keeps the GPU busy while the host queues
-        // the whole run, so no host-submission gap lands inside an event pair
-        if (c->timing) WSMC_HIP(launch_delay(c->stream, 20000));
-        r = enqueue_ssm2d(c, p, c->timing ? &evs : nullptr);
-        if (r) {
-            if (temp_tables) (void)hipFree(temp_tables);
-            return r;
         }
     }
     std::vector<Decision> hdec(T + 1);

@@ -98,6 +98,7 @@ struct wsmc_ctx {
     // ring and folded into resampled / n_resamples / last_ess at the next host read
     wsmc::Decision* dec_ring = nullptr;
     int dec_pending = 0;
+    bool no_graph = false;   // a sharded run's capture failed once: run it eagerly
     int64_t N = 0;
     uint64_t seed = 0;
 
