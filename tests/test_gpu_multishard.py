@@ -444,6 +444,9 @@ def _analysis_worker(rank, world, port, sizes, outdir):
         out["mm" + k] = np.array(c.col_minmax(col))
         out["h" + k] = c.histogram(col)
         out["md" + k] = np.array([c.weighted_median(col)])
+    out["sr"] = c.sample_particles(257, replace=True)
+    out["sn"] = c.sample_particles(300, replace=False)
+    out["sall"] = c.sample_particles(N, replace=False)       # every particle, zero weights last
     c.close()
     comm.barrier()
     comm.close()
@@ -454,7 +457,8 @@ def _analysis_worker(rank, world, port, sizes, outdir):
 def test_two_shards_analysis_match_single_context(gpu_available, tmp_path, sizes):
     """describe / @E on island shards: min/max, the sparkline histogram (integer weights
     relative to the population's max: bit-identical bins), the weighted median (over the
-    all-gathered (value, q) union) and ESS equal the sharded oracle's
+    all-gathered (value, q) union), sample(state, n; replace) (global indices) and ESS equal
+    the sharded oracle's
     population-wide values exactly; the weighted moments are rank-order combinations of
     per-shard canonical sums, equal to the population's up to summation order."""
     import multiprocessing as mp
@@ -482,12 +486,20 @@ def test_two_shards_analysis_match_single_context(gpu_available, tmp_path, sizes
     a, b = o.col_find("α"), o.col_find("β")
     mean, cov = o.weighted_moments([Operand.column(a), Operand.column(b, coef=2.0, c0=1.0)])
     parts = [np.load(tmp_path / f"an{r}.npz") for r in range(world)]
+    # each sample() consumes one op counter: draw in the workers' order, once
+    sr = o.sample_particles(257, replace=True)
+    sn = o.sample_particles(300, replace=False)
+    sall = o.sample_particles(sum(sizes), replace=False)
+    assert sorted(sall) == list(range(sum(sizes)))
     for p in parts:
         for k, col in (("a", a), ("b", b)):
             np.testing.assert_array_equal(p["mm" + k], np.array(o.col_minmax(col)))
             np.testing.assert_array_equal(p["h" + k], o.histogram(col))
             assert p["md" + k][0] == o.weighted_median(col)
         assert p["ess"][0] == o.ess()
+        np.testing.assert_array_equal(p["sr"], sr)
+        np.testing.assert_array_equal(p["sn"], sn)
+        np.testing.assert_array_equal(p["sall"], sall)
         assert p["ev"][0] == o.log_evidence()
         np.testing.assert_allclose(p["mean"], mean, rtol=1e-12)
         np.testing.assert_allclose(p["cov"], cov, rtol=1e-10)

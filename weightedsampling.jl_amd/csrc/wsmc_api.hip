@@ -1172,12 +1172,120 @@ int wsmc_ess(wsmc_ctx* c, double* ess_perc) {
     return WSMC_OK;
 }
 
+// sample(state, n; replace) over a sharded population (global indices, the single-context
+// draws): integer weights relative to the population's max with the global N's K.
+//   replace: every rank locates the draws whose target falls in its CDF range (its base is
+//   the lower ranks' Q); the owners' answers are all-gathered.
+//   no replace: each rank's top-min(n, N) Efraimidis–Spirakis keys (keyed by global index)
+//   are all-gathered and the union re-sorted: by global index, then stably by key
+//   (descending), as one context's stable sort orders them.
+static int sample_particles_sharded(wsmc_ctx* c, int64_t n, int32_t replace, int64_t* idx_out) {
+    using u64 = unsigned long long;
+    const uint64_t op = c->op++;
+    const int W = c->world;
+    int r = adopt_global_max(c);
+    if (r) return r;
+    WSMC_HIP(launch_rs_sums(c->stream, c->w, c->N, c->mslots, c->tilep, c->qbuf, nullptr, nullptr, nullptr, 1, c->gN));
+    WSMC_HIP(launch_rs_reduce(c->stream, c->mslots, c->tilep, c->N, c->tileOff, c->rec, 0, 0.0, nullptr, nullptr));
+    ShardRecord* hr = reinterpret_cast<ShardRecord*>(c->pinned);
+    WSMC_HIP(hipMemcpyAsync(hr, c->rec, sizeof(ShardRecord), hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    const u64 mine = hr->Q, mine2[2] = {hr->Q, (u64)c->N};
+    std::vector<u64> qs(2 * W);
+    if ((r = allgather_host_words(c, mine2, 2, qs.data()))) return r;
+    u64 Q = 0, base = 0, nmax = 1;
+    for (int g = 0; g < W; ++g) {
+        if (g < c->rank) base += qs[2 * g];
+        Q += qs[2 * g];
+        nmax = qs[2 * g + 1] > nmax ? qs[2 * g + 1] : nmax;
+    }
+    if (Q == 0) return fail(WSMC_ESTATE, "the weights do not normalise (all -Inf or NaN)");
+    std::vector<void*> owned;
+    auto done = [&](int rc) {
+        for (void* p : owned) (void)hipFree(p);
+        return rc;
+    };
+    auto dalloc = [&](size_t bytes) -> void* {
+        void* p = nullptr;
+        if (hipMalloc(&p, bytes ? bytes : 16) != hipSuccess) return nullptr;
+        owned.push_back(p);
+        return p;
+    };
+#define SP_HIP(x)                                                                                  \
+    do {                                                                                           \
+        const hipError_t e_ = (x);                                                                 \
+        if (e_ != hipSuccess) return done(fail(WSMC_EHIP, std::string("sample: ") + hipGetErrorString(e_))); \
+    } while (0)
+    if (replace) {
+        u64* cdf = static_cast<u64*>(dalloc(sizeof(u64) * c->N));
+        int64_t* all = static_cast<int64_t*>(dalloc(sizeof(int64_t) * (size_t)n * W));
+        if (!cdf || !all) return done(fail(WSMC_EHIP, "sample: out of device memory"));
+        size_t tb = 0;
+        SP_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tb, c->qbuf, cdf, (int)c->N, c->stream));
+        void* ts = dalloc(tb);
+        if (!ts) return done(fail(WSMC_EHIP, "sample: out of device memory"));
+        SP_HIP(hipcub::DeviceScan::InclusiveSum(ts, tb, c->qbuf, cdf, (int)c->N, c->stream));
+        SP_HIP(launch_sample_draws_shard(c->stream, n, c->N, cdf, base, mine, Q, c->seed, op, c->goff,
+                                         all + (size_t)n * c->rank));
+        if ((r = exchange_words(c, reinterpret_cast<u64*>(all), n, c->stream))) return done(r);
+        std::vector<int64_t> h((size_t)n * W);
+        SP_HIP(hipMemcpyAsync(h.data(), all, sizeof(int64_t) * h.size(), hipMemcpyDeviceToHost, c->stream));
+        SP_HIP(hipStreamSynchronize(c->stream));
+        for (int64_t j = 0; j < n; ++j) {   // exactly one rank owns each draw
+            int64_t v = 0;
+            for (int g = 0; g < W; ++g) v = h[(size_t)g * n + j] ? h[(size_t)g * n + j] : v;
+            idx_out[j] = v - 1;
+        }
+        return done(WSMC_OK);
+    }
+    // a shard contributes at most its top m (the same m on every rank; shorter shards pad)
+    const int64_t m = n < (int64_t)nmax ? n : (int64_t)nmax, mloc = m < c->N ? m : c->N;
+    u64* kin = reinterpret_cast<u64*>(c->tmp);
+    u64* kout = kin + c->N;
+    u64* vin = kout + c->N;
+    u64* vout = vin + c->N;
+    SP_HIP(launch_es_keys_shard(c->stream, c->w, c->N, c->gN, c->goff, c->mslots, c->seed, op, kin, vin));
+    size_t tb = 0;
+    SP_HIP(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tb, kin, kout, vin, vout, (int)c->N, 0, 64,
+                                                        c->stream));
+    const int64_t U = m * W;
+    u64* gk = static_cast<u64*>(dalloc(sizeof(u64) * 2 * (size_t)U));   // keys, then indices
+    u64* t4 = static_cast<u64*>(dalloc(sizeof(u64) * 4 * (size_t)U));
+    size_t tb2 = 0, tb3 = 0;
+    if (!gk || !t4) return done(fail(WSMC_EHIP, "sample: out of device memory"));
+    SP_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, gk, t4, gk, t4, (int)U, 0, 64, c->stream));
+    SP_HIP(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tb3, gk, t4, gk, t4, (int)U, 0, 64, c->stream));
+    size_t tmax = tb > tb2 ? tb : tb2;
+    tmax = tmax > tb3 ? tmax : tb3;
+    void* ts = dalloc(tmax + 16);
+    if (!ts) return done(fail(WSMC_EHIP, "sample: out of device memory"));
+    size_t t = tmax;
+    SP_HIP(hipcub::DeviceRadixSort::SortPairsDescending(ts, t, kin, kout, vin, vout, (int)c->N, 0, 64, c->stream));
+    u64* gkeys = gk;
+    u64* gidx = gk + U;
+    SP_HIP(hipMemsetAsync(gk, 0, sizeof(u64) * 2 * (size_t)U, c->stream));   // padding never wins: key 0
+    SP_HIP(hipMemcpyAsync(gkeys + m * c->rank, kout, sizeof(u64) * mloc, hipMemcpyDeviceToDevice, c->stream));
+    SP_HIP(hipMemcpyAsync(gidx + m * c->rank, vout, sizeof(u64) * mloc, hipMemcpyDeviceToDevice, c->stream));
+    if ((r = exchange_words(c, gkeys, m, c->stream))) return done(r);
+    if ((r = exchange_words(c, gidx, m, c->stream))) return done(r);
+    // by global index, then stably by key, descending
+    u64 *i1 = t4, *k1 = t4 + U, *k2 = t4 + 2 * U, *i2 = t4 + 3 * U;
+    t = tmax;
+    SP_HIP(hipcub::DeviceRadixSort::SortPairs(ts, t, gidx, i1, gkeys, k1, (int)U, 0, 64, c->stream));
+    t = tmax;
+    SP_HIP(hipcub::DeviceRadixSort::SortPairsDescending(ts, t, k1, k2, i1, i2, (int)U, 0, 64, c->stream));
+    SP_HIP(hipMemcpyAsync(idx_out, i2, sizeof(int64_t) * n, hipMemcpyDeviceToHost, c->stream));
+    SP_HIP(hipStreamSynchronize(c->stream));
+#undef SP_HIP
+    return done(WSMC_OK);
+}
+
 int wsmc_sample_particles(wsmc_ctx* c, int64_t n, int32_t replace, int64_t* idx_out) {
     CHECK_CTX(c);
     if (!idx_out) return fail(WSMC_EARG, "null output");
     if (n <= 0) return fail(WSMC_EARG, "Number of samples must be positive");
-    if (!replace && n > c->N) return fail(WSMC_EARG, "Cannot sample more particles than N without replacement");
-    if (c->world > 1) return fail(WSMC_ESTATE, "sample() on sharded contexts is not supported");
+    if (!replace && n > c->gN) return fail(WSMC_EARG, "Cannot sample more particles than N without replacement");
+    if (is_sharded(c)) return sample_particles_sharded(c, n, replace, idx_out);
     const uint64_t op = c->op++;
     // the integer weights relative to the max (and, with replacement, their CDF)
     WSMC_HIP(hipMemsetAsync(c->mslots, 0, sizeof(MaxSlots), c->stream));

@@ -344,6 +344,12 @@ hipError_t launch_rs_fill_fused(hipStream_t s, int64_t N, const FillPlan& plan, 
 hipError_t launch_gather(hipStream_t s, double* dst, const double* src, const int32_t* anc, int64_t N);
 hipError_t launch_gather_dec(hipStream_t s, double* dst, const double* src, const int32_t* anc, const Decision* dec,
                              int64_t N);
+hipError_t launch_sample_draws_shard(hipStream_t s, int64_t n, int64_t N, const unsigned long long* cdf,
+                                     unsigned long long base, unsigned long long Qloc, unsigned long long Q,
+                                     uint64_t seed, uint64_t op, int64_t goff, int64_t* out);
+hipError_t launch_es_keys_shard(hipStream_t s, const double* w, int64_t N, int64_t gN, int64_t goff,
+                                const MaxSlots* ms, uint64_t seed, uint64_t op, unsigned long long* keys,
+                                unsigned long long* idx);
 hipError_t launch_fill_weights(hipStream_t s, double* w, const Decision* dec, int64_t N);
 hipError_t launch_log_evidence_stats(hipStream_t s, const double* w, int64_t N, MaxSlots* ms,
                                      unsigned long long* tilep, unsigned long long* qbuf,

@@ -954,6 +954,52 @@ __global__ __launch_bounds__(kBlock) void k_es_keys(const double* __restrict__ w
     keys[i] = wsmc_ord_enc(wsmc_es_key(seed, op, (uint64_t)i, wsmc_qweight(w[i], M, K)));
     idx[i] = (u64)i;
 }
+// sample(state, n; replace=true) on a shard: draw j's target x (the single-context formula
+// over the population's Q) lands in this shard iff base <= x < base + Qloc; then its
+// ancestor is the smallest local m with base + C_m > x. out[j] = global index + 1, or 0.
+__global__ __launch_bounds__(kBlock) void k_sample_draws_shard(int64_t n, int64_t N, const u64* __restrict__ cdf,
+                                                               u64 base, u64 Qloc, u64 Q, uint64_t seed,
+                                                               uint64_t op, int64_t goff, int64_t* __restrict__ out) {
+    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= n) return;
+    const u64 x = wsmc_multi_target(wsmc_multi_word(seed, op, (uint64_t)j), Q);
+    if (x < base || x - base >= Qloc) {
+        out[j] = 0;
+        return;
+    }
+    const u64 xl = x - base;
+    int64_t lo = 0, hi = N - 1;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (cdf[mid] > xl) hi = mid; else lo = mid + 1;
+    }
+    out[j] = goff + lo + 1;
+}
+hipError_t launch_sample_draws_shard(hipStream_t s, int64_t n, int64_t N, const u64* cdf, u64 base, u64 Qloc, u64 Q,
+                                     uint64_t seed, uint64_t op, int64_t goff, int64_t* out) {
+    hipLaunchKernelGGL(k_sample_draws_shard, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n, N,
+                       cdf, base, Qloc, Q, seed, op, goff, out);
+    return hipGetLastError();
+}
+// Efraimidis–Spirakis keys of a shard: the global index keys the draw, the integer weight is
+// relative to the population's max with the global N's K
+__global__ __launch_bounds__(kBlock) void k_es_keys_shard(const double* __restrict__ w, int64_t N, int64_t gN,
+                                                          int64_t goff, const MaxSlots* __restrict__ ms,
+                                                          uint64_t seed, uint64_t op, u64* __restrict__ keys,
+                                                          u64* __restrict__ idx) {
+    const double M = wave_slots_max(ms);
+    const int K = wsmc_qbits((uint64_t)gN);
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= N) return;
+    keys[i] = wsmc_ord_enc(wsmc_es_key(seed, op, (uint64_t)(goff + i), wsmc_qweight(w[i], M, K)));
+    idx[i] = (u64)(goff + i);
+}
+hipError_t launch_es_keys_shard(hipStream_t s, const double* w, int64_t N, int64_t gN, int64_t goff,
+                                const MaxSlots* ms, uint64_t seed, uint64_t op, u64* keys, u64* idx) {
+    hipLaunchKernelGGL(k_es_keys_shard, dim3((unsigned)((N + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, w, N, gN, goff,
+                       ms, seed, op, keys, idx);
+    return hipGetLastError();
+}
 // rows of a column: out[k][j] = col[k][idx[j]]
 __global__ __launch_bounds__(kBlock) void k_gather_rows(const double* __restrict__ src, int64_t N, int dim,
                                                         const int64_t* __restrict__ idx, int64_t n,
