@@ -1960,11 +1960,16 @@ __global__ __launch_bounds__(kBlock) void k_stream_like_prop(const int32_t* __re
 hipError_t debug_kernel_bench(hipStream_t s, int kernel, int mode, int iters, const double* w, int64_t N,
                               MaxSlots* ms, u64* tilep, u64* qbuf, u64* tileOff, ShardRecord* rec, Decision* dec,
                               const FillPlan& plan, int32_t* anc, double* stream4, float* ms_out) {
-    hipEvent_t a, b;
-    hipEventCreate(&a);
-    hipEventCreate(&b);
+    hipEvent_t a = nullptr, b = nullptr;
+    hipError_t e0 = hipEventCreate(&a);
+    if (e0 == hipSuccess) e0 = hipEventCreate(&b);
+    if (e0 == hipSuccess) e0 = hipEventRecord(a, s);
+    if (e0 != hipSuccess) {
+        if (a) (void)hipEventDestroy(a);
+        if (b) (void)hipEventDestroy(b);
+        return e0;
+    }
     const dim3 g = rs_tiles_for(N), blk(kSumBlock), gs = fill_tasks_for(N), bs(kScanBlock);
-    hipEventRecord(a, s);
     for (int it = 0; it < iters; ++it) {
         if (kernel == 0) {
             switch (mode) {
@@ -1999,13 +2004,13 @@ hipError_t debug_kernel_bench(hipStream_t s, int kernel, int mode, int iters, co
             }
         }
     }
-    hipEventRecord(b, s);
-    hipError_t e = hipEventSynchronize(b);
+    hipError_t e = hipEventRecord(b, s);
+    if (e == hipSuccess) e = hipEventSynchronize(b);
     float t = 0.f;
     if (e == hipSuccess) e = hipEventElapsedTime(&t, a, b);
     *ms_out = t;
-    hipEventDestroy(a);
-    hipEventDestroy(b);
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
     return e != hipSuccess ? e : hipGetLastError();
 }
 
