@@ -193,6 +193,8 @@ int wsmc_create(wsmc_ctx** out, int64_t n_particles, int32_t device, uint64_t se
     ALLOC(c->taskOff, sizeof(int32_t) * c->nrstiles);
     ALLOC(c->taskTile, sizeof(int32_t) * (c->nrstiles + n_particles / kRsChunk + 1));
     ALLOC(c->mslots, sizeof(MaxSlots));
+    ALLOC(c->wslots[0], sizeof(MaxSlots));
+    ALLOC(c->wslots[1], sizeof(MaxSlots));
     ALLOC(c->qbuf, sizeof(unsigned long long) * c->N);
     ALLOC(c->tilepart, sizeof(double) * 16 * c->ntiles);
     ALLOC(c->rec, sizeof(ShardRecord) * kMaxWorld);
@@ -206,6 +208,8 @@ int wsmc_create(wsmc_ctx** out, int64_t n_particles, int32_t device, uint64_t se
     if (e == hipSuccess) e = hipHostMalloc(&c->pinned, 4096, hipHostMallocDefault);
     if (e == hipSuccess) e = hipHostMalloc((void**)&c->dec_ring, sizeof(Decision) * kDecRing, hipHostMallocDefault);
     if (e == hipSuccess) e = hipMemsetAsync(c->w, 0, sizeof(double) * c->N, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->wslots[0], 0, sizeof(MaxSlots), c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->wslots[1], 0, sizeof(MaxSlots), c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->anc, 0, sizeof(int32_t) * c->N, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) {
@@ -232,7 +236,7 @@ int wsmc_destroy(wsmc_ctx* c) {
         (void)hipFree(col.front);
         (void)hipFree(col.back);
     }
-    void* bufs[] = {c->xchg, c->scache, c->scache_back, c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->cdf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount,
+    void* bufs[] = {c->xchg, c->scache, c->scache_back, c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->cdf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount, c->wslots[0], c->wslots[1],
                     c->d_colptr, c->run_params, c->d_tape, c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp,
                     c->vscratch, c->xscratch, c->xp, c->comb, c->anc_out, c->xbuf, c->d_comp, c->d_ctape, c->d_prog};
     for (void* p : bufs)
@@ -437,6 +441,7 @@ int wsmc_store_resample(wsmc_ctx* c, const int32_t* idx) {
 int wsmc_weights_upload(wsmc_ctx* c, const double* host) {
     CHECK_CTX(c);
     if (!host) return fail(WSMC_EARG, "null buffer");
+    c->wseq += 1;
     WSMC_HIP(hipMemcpyAsync(c->w, host, sizeof(double) * c->N, hipMemcpyHostToDevice, c->stream));
     WSMC_HIP(hipStreamSynchronize(c->stream));
     return WSMC_OK;
@@ -752,6 +757,7 @@ static int exact_resample(wsmc_ctx* c, double ess_min, int32_t scheme, uint64_t 
     int r = exact_decide_fill(c, ess_min, scheme, op, c->dec, out, &x);
     if (r || !out->resampled) return r;
     if ((r = exact_move_particles(c, x))) return r;
+    c->wseq += 1;
     WSMC_HIP(launch_fill_weights(c->stream, c->w, c->dec, c->N));
     return WSMC_OK;
 }
@@ -1431,6 +1437,7 @@ int wsmc_sample_importance(wsmc_ctx* c, int32_t out, const wsmc_dist* prop, cons
     if ((r = upload_colptr(c))) return r;
     const uint64_t op = c->op++;
     scores_touch(c, out);
+    c->wseq += 1;
     WSMC_HIP(launch_sample_importance(c->stream, c->cols[out].front, prop->dim, *prop, *targ, c->w, c->seed, op,
                                       c->goff, c->d_colptr, c->N));
     c->weights_changed = 1;
@@ -1454,7 +1461,12 @@ static int weigh(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x, int kin
     t.kind = kind;
     t.depth = c->depth;
     if ((r = upload_colptr(c))) return r;
-    WSMC_HIP(launch_weigh(c->stream, t, c->w, c->d_colptr, c->N));
+    const int wb = c->wnext;
+    WSMC_HIP(launch_weigh(c->stream, t, c->w, c->d_colptr, c->N, c->wslots[wb], c->wslots[wb ^ 1]));
+    c->wnext = wb ^ 1;
+    c->wmax_buf = wb;
+    c->wseq += 1;
+    c->wmax_seq = c->wseq;
     c->tape.push_back(t);
     c->weights_changed = 1;
     c->depth += 1;
@@ -1494,7 +1506,10 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
         return WSMC_OK;
     }
     const FillPlan plan = fill_plan(c, scheme, op, nullptr);
-    int r = enqueue_resample_stats(c, c->w, c->mslots, c->rec, ess_min, c->dec, true, plan);
+    // the last weight write was an Observe / Weight: its kernel left the max in wslots
+    const bool pre = c->wmax_buf >= 0 && c->wmax_seq == c->wseq;
+    MaxSlots* ms = pre ? c->wslots[c->wmax_buf] : c->mslots;
+    int r = enqueue_resample_stats(c, c->w, ms, c->rec, ess_min, c->dec, !pre, plan);
     if (r) return r;
     if (scheme == WSMC_RESAMPLE_MULTINOMIAL)
         WSMC_HIP(launch_rs_multinomial(c->stream, c->N, c->rec + c->rank, c->dec, plan, c->tileOff, c->cdf,
@@ -1508,6 +1523,7 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
                                 c->stream));
         c->dec_pending += 1;
         if ((r = gather_all_columns(c, c->dec))) return r;
+        c->wseq += 1;
         WSMC_HIP(launch_fill_weights(c->stream, c->w, c->dec, c->N));
         c->weights_changed = 0;
         return WSMC_OK;
@@ -1519,6 +1535,7 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
     c->last_ess = d.ess;
     if (d.resampled) {
         if ((r = gather_all_columns(c))) return r;
+        c->wseq += 1;
         WSMC_HIP(launch_fill_weights(c->stream, c->w, c->dec, c->N));
         c->resampled = 1;
         c->n_resamples += 1;
@@ -2230,6 +2247,7 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
     CHECK_CTX(c);
     if (int r = resolve_decisions(c)) return r;
     c->scache_terms = -1;   // the run rewrites columns the tape reads
+    c->wseq += 1;           // ... and the weights
     if (!obs || T < 1 || !x0 || !v0) return fail(WSMC_EARG, "bad arguments");
     if (!valid_scheme(scheme)) return fail(WSMC_EARG, "unknown resampling scheme");
     if (exact_mode(c) && scheme == WSMC_RESAMPLE_MULTINOMIAL)

@@ -99,6 +99,12 @@ struct wsmc_ctx {
     wsmc::Decision* dec_ring = nullptr;
     int dec_pending = 0;
     bool no_graph = false;   // a sharded run's capture failed once: run it eagerly
+    // the max of the weights as the last Observe / Weight left them (double-buffered slots:
+    // each such launch maxes into wslots[wnext] and zeroes the other); valid while
+    // wmax_seq == wseq, the count of weight writes
+    wsmc::MaxSlots* wslots[2] = {nullptr, nullptr};
+    int wnext = 0, wmax_buf = -1;
+    uint64_t wseq = 0, wmax_seq = ~0ull;
     int64_t N = 0;
     uint64_t seed = 0;
 
@@ -212,7 +218,8 @@ hipError_t launch_sample(hipStream_t s, double* out, int dim, const wsmc_dist& d
 hipError_t launch_sample_importance(hipStream_t s, double* out, int dim, const wsmc_dist& prop,
                                     const wsmc_dist& targ, double* w, uint64_t seed, uint64_t op,
                                     int64_t goff, double* const* cols, int64_t N);
-hipError_t launch_weigh(hipStream_t s, const wsmc_term& t, double* w, double* const* cols, int64_t N);
+hipError_t launch_weigh(hipStream_t s, const wsmc_term& t, double* w, double* const* cols, int64_t N, MaxSlots* ms,
+                        MaxSlots* ms_next);
 hipError_t launch_rs_max(hipStream_t s, const double* w, int64_t N, MaxSlots* ms);
 hipError_t launch_rs_sums(hipStream_t s, const double* w, int64_t N, const MaxSlots* ms,
                           unsigned long long* tilep, unsigned long long* qbuf,

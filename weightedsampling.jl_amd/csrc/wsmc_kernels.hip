@@ -167,10 +167,23 @@ __global__ __launch_bounds__(kBlock) void k_sample_importance(double* out, int d
     w[i] = w[i] + (lt - lp);
 }
 
-__global__ __launch_bounds__(kBlock) void k_weigh(wsmc_term t, double* w, double* const* cols, int64_t N) {
+// Observe / Weight: weights += logpdf, and the block max of the new weights into the 64
+// slots of `ms` (zero on entry), so the Resample that follows needs no max pass; block 0
+// zeroes `ms_next`, the slots the next launch will use (k_rs_max's encoding and slots)
+__global__ __launch_bounds__(kBlock) void k_weigh(wsmc_term t, double* w, double* const* cols, int64_t N,
+                                                  MaxSlots* ms, MaxSlots* ms_next) {
+    __shared__ u64 lds[4];
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= N) return;
-    w[i] = w[i] + wsmc_term_logpdf(&t, cols, N, i, nullptr);
+    u64 m = 0;
+    if (i < N) {
+        const double v = w[i] + wsmc_term_logpdf(&t, cols, N, i, nullptr);
+        w[i] = v;
+        m = wsmc_ord_enc(v);
+    }
+    m = block_max_u64(m, lds);
+    if (threadIdx.x == 0) atomic_max_filtered(&ms->v[blockIdx.x % kSlots][0], m);
+    if (blockIdx.x == 0)
+        for (int k = threadIdx.x; k < kSlots * 16; k += kBlock) ms_next->v[k >> 4][k & 15] = 0ull;
 }
 
 // ------------------------------------------------------------------------------------
@@ -1801,8 +1814,9 @@ hipError_t launch_sample_importance(hipStream_t s, double* out, int dim, const w
                        op, goff, cols, N);
     return hipGetLastError();
 }
-hipError_t launch_weigh(hipStream_t s, const wsmc_term& t, double* w, double* const* cols, int64_t N) {
-    hipLaunchKernelGGL(k_weigh, grid_for(N), dim3(kBlock), 0, s, t, w, cols, N);
+hipError_t launch_weigh(hipStream_t s, const wsmc_term& t, double* w, double* const* cols, int64_t N, MaxSlots* ms,
+                        MaxSlots* ms_next) {
+    hipLaunchKernelGGL(k_weigh, grid_for(N), dim3(kBlock), 0, s, t, w, cols, N, ms, ms_next);
     return hipGetLastError();
 }
 template <typename K, typename... Args>
