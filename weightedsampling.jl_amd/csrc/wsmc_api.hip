@@ -120,21 +120,39 @@ static void scores_touch(wsmc_ctx* c, int32_t col) {
     if (c->scache_terms >= 0 && tape_reads(c, col)) c->scache_terms = -1;
 }
 
-// dec != null: an asynchronous Resample, the gather is gated on the device-side decision
-static int gather_all_columns(wsmc_ctx* c, const Decision* dec = nullptr) {
-    auto gather = [&](double* dst, const double* src) {
-        return dec ? launch_gather_dec(c->stream, dst, src, c->anc, dec, c->N)
-                   : launch_gather(c->stream, dst, src, c->anc, c->N);
+// ColumnStore.resample! of every column (and the carried Move scores) through c->anc, in
+// k_resample_apply launches of up to kGatherSet components; the last one also resets the
+// weights to dec->mean when w_reset is given. dec != null gates everything on the
+// device-side decision (the asynchronous Resample: identity copies when it did not
+// resample, so the front/back swap holds); null = an explicit resample!(store, idx).
+static int gather_all_columns(wsmc_ctx* c, const Decision* dec = nullptr, double* w_reset = nullptr) {
+    GatherSet gs;
+    gs.n = 0;
+    auto flush = [&](bool last) -> hipError_t {
+        const hipError_t e = launch_resample_apply(c->stream, gs, c->anc, dec, last ? w_reset : nullptr, c->N);
+        gs.n = 0;
+        return e;
+    };
+    auto add = [&](double* dst, const double* src) -> hipError_t {
+        if (gs.n == kGatherSet) {
+            const hipError_t e = flush(false);
+            if (e != hipSuccess) return e;
+        }
+        gs.dst[gs.n] = dst;
+        gs.src[gs.n] = src;
+        gs.n += 1;
+        return hipSuccess;
     };
     for (auto& col : c->cols) {
         for (int k = 0; k < col.dim; ++k)
-            WSMC_HIP(gather(col.back + (int64_t)k * c->N, col.front + (int64_t)k * c->N));
+            WSMC_HIP(add(col.back + (int64_t)k * c->N, col.front + (int64_t)k * c->N));
         std::swap(col.front, col.back);
     }
     if (c->scache && c->scache_terms >= 0) {   // carried Move scores follow their particles
-        WSMC_HIP(gather(c->scache_back, c->scache));
+        WSMC_HIP(add(c->scache_back, c->scache));
         std::swap(c->scache, c->scache_back);
     }
+    WSMC_HIP(flush(true));
     c->colptr_dirty = true;
     return WSMC_OK;
 }
@@ -1522,9 +1540,8 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
         WSMC_HIP(hipMemcpyAsync(&c->dec_ring[c->dec_pending], c->dec, sizeof(Decision), hipMemcpyDeviceToHost,
                                 c->stream));
         c->dec_pending += 1;
-        if ((r = gather_all_columns(c, c->dec))) return r;
         c->wseq += 1;
-        WSMC_HIP(launch_fill_weights(c->stream, c->w, c->dec, c->N));
+        if ((r = gather_all_columns(c, c->dec, c->w))) return r;   // gated gathers + weight reset
         c->weights_changed = 0;
         return WSMC_OK;
     }
@@ -1534,9 +1551,8 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
     const Decision d = *hd;
     c->last_ess = d.ess;
     if (d.resampled) {
-        if ((r = gather_all_columns(c))) return r;
         c->wseq += 1;
-        WSMC_HIP(launch_fill_weights(c->stream, c->w, c->dec, c->N));
+        if ((r = gather_all_columns(c, c->dec, c->w))) return r;   // gathers + weight reset
         c->resampled = 1;
         c->n_resamples += 1;
     } else {

@@ -349,6 +349,15 @@ hipError_t launch_rs_fill_fused(hipStream_t s, int64_t N, const FillPlan& plan, 
                                 const unsigned long long* qbuf, int32_t* anc, hipEvent_t e0 = nullptr,
                                 hipEvent_t e1 = nullptr);
 hipError_t launch_gather(hipStream_t s, double* dst, const double* src, const int32_t* anc, int64_t N);
+// up to kGatherSet (dst, src) column-component pairs of one Resample, passed by value
+constexpr int kGatherSet = 48;
+struct GatherSet {
+    double* dst[kGatherSet];
+    const double* src[kGatherSet];
+    int n;
+};
+hipError_t launch_resample_apply(hipStream_t s, const GatherSet& gs, const int32_t* anc, const Decision* dec,
+                                 double* w, int64_t N);
 hipError_t launch_gather_dec(hipStream_t s, double* dst, const double* src, const int32_t* anc, const Decision* dec,
                              int64_t N);
 hipError_t launch_sample_draws_shard(hipStream_t s, int64_t n, int64_t N, const unsigned long long* cdf,

@@ -2028,6 +2028,29 @@ hipError_t debug_kernel_bench(hipStream_t s, int kernel, int mode, int iters, co
     return e != hipSuccess ? e : hipGetLastError();
 }
 
+// ColumnStore.resample! of every column component (and the carried Move scores) plus the
+// weight reset in one launch: blockIdx.y selects a (dst, src) pair, y == n the weights.
+// dec: gate on the device-side decision (identity copy when it did not resample) — the
+// asynchronous Resample; null: the host has seen a resample. w null: no weight reset.
+__global__ __launch_bounds__(kBlock) void k_resample_apply(GatherSet gs, const int32_t* __restrict__ anc,
+                                                           const Decision* dec, double* w, int64_t N) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= N) return;
+    const int k = blockIdx.y;
+    const bool rs = dec ? dec->resampled != 0 : true;
+    if (k == gs.n) {
+        if (rs && dec) w[i] = dec->mean;
+        return;
+    }
+    gs.dst[k][i] = gs.src[k][rs ? (int64_t)anc[i] : i];
+}
+hipError_t launch_resample_apply(hipStream_t s, const GatherSet& gs, const int32_t* anc, const Decision* dec,
+                                 double* w, int64_t N) {
+    const dim3 g((unsigned)((N + kBlock - 1) / kBlock), (unsigned)(gs.n + (w ? 1 : 0)));
+    if (g.y == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_resample_apply, g, dim3(kBlock), 0, s, gs, anc, dec, w, N);
+    return hipGetLastError();
+}
 // the ColumnStore gather of an asynchronous Resample (the host has not seen the decision):
 // through the ancestors if it resampled, else an identity copy, so the host's front/back
 // swap is right either way

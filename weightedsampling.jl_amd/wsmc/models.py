@@ -97,10 +97,12 @@ def lgssm1d_statements(ctx, data, a=0.9, q=1.0, r=0.5, x0_std=1.0, ess_perc_min=
     ctx.sample(cx, Normal(0.0, x0_std).dist(R))
     ctx.resample(ess_perc_min, scheme, wait=wait)
     resampled = []
+    transition = Normal(Col("x") * a, q).dist(R)       # the loop body's kernels (built once)
+    likelihood = Normal(Col("x"), r).dist(R)
     for y in np.asarray(data, dtype=float):
-        ctx.sample(cx, Normal(Col("x") * a, q).dist(R))                     # x ~ Normal(a*x, q)
+        ctx.sample(cx, transition)                                          # x ~ Normal(a*x, q)
         ctx.resample(ess_perc_min, scheme, wait=wait)
-        ctx.observe(Normal(Col("x"), r).dist(R), _const([y]))               # y => Normal(x, r)
+        ctx.observe(likelihood, _const([y]))                                # y => Normal(x, r)
         rs = ctx.resample(ess_perc_min, scheme, wait=wait)
         if wait:
             resampled.append(rs[0])
