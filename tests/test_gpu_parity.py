@@ -335,3 +335,23 @@ def test_ssm2d_fused_tiny_populations(gpu_available, N, scheme):
     assert_same_state(g, o)
     np.testing.assert_array_equal(g.last_ancestors(), o.last_ancestors())
     assert ev == o.log_evidence()
+
+
+def test_ssm2d_fused_full_size_matches_port(gpu_available):
+    """The bench workload itself (BASELINE configs[1]: 1M particles, T = 100, forced
+    resampling, history kept) against the bit-exact all-cores CPU port of the same run
+    (oracle/wsmc_port_mt.c, held bit-identical to the statement oracle by test_port_mt.py):
+    every traced-back column x_1..x_101, v, dv, the weights and the evidence."""
+    import os
+    import oracle as orc
+    N, T = 1_000_000, 100
+    obs = models.ssm2d_data(T)
+    g = wsmc.Context(N, seed=42)
+    ev = g.ssm2d_run(obs, ess_perc_min=1.0, keep_history=True)
+    r = orc.ssm2d_run_mt(N, obs, seed=42, ess_perc_min=1.0, threads=min(16, os.cpu_count() or 1))
+    assert ev == r["log_evidence"]
+    assert list(r["flags"]) == [False] + [True] * (T - 1)
+    np.testing.assert_array_equal(g.weights_download(), r["weights"])
+    for name in ["x_%d" % t for t in range(1, T + 2)] + ["v", "dv"]:
+        np.testing.assert_array_equal(g.col_download(g.col_find(name)), r[name], err_msg=name)
+    g.close()
