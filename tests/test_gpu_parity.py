@@ -355,3 +355,28 @@ def test_ssm2d_fused_full_size_matches_port(gpu_available):
     for name in ["x_%d" % t for t in range(1, T + 2)] + ["v", "dv"]:
         np.testing.assert_array_equal(g.col_download(g.col_find(name)), r[name], err_msg=name)
     g.close()
+
+
+def test_linreg_full_size_matches_oracle(gpu_available):
+    """C3 at its configured size (BASELINE configs[2]: 1M particles, forced resampling, an
+    autoRW pair after every resample) against the statement oracle, bit for bit: the
+    acceptance counts of all 20 moves, both columns, the weights and the evidence."""
+    xs, ys = models.linreg_data()
+    g, o = wsmc.Context(1_000_000, seed=42), Oracle(1_000_000, seed=42)
+    assert models.linreg_statements(g, xs, ys, ess_perc_min=1.0) == models.linreg_statements(o, xs, ys,
+                                                                                            ess_perc_min=1.0)
+    assert_same_state(g, o)
+    assert g.log_evidence() == o.log_evidence()
+
+
+def test_oscillator_long_tape_matches_oracle(gpu_available):
+    """C5's move program (configs[4]: systematic resampling, 5 ungated sweeps of the bounded
+    4-D and 1-D autoRW moves per step) over its first 20 observations at 100k particles:
+    score tapes of up to 25 terms through the compiled segment program, bit for bit."""
+    t, y = models.oscillator_data(n=60)
+    t, y = t[:20], y[:20]
+    g, o = wsmc.Context(100_000, seed=42), Oracle(100_000, seed=42)
+    kw = dict(ess_perc_min=1.0, scheme=abi.RESAMPLE_SYSTEMATIC, sweeps=5, diversity=None)
+    assert models.oscillator_statements(g, t, y, **kw) == models.oscillator_statements(o, t, y, **kw)
+    assert_same_state(g, o)
+    assert g.log_evidence() == o.log_evidence()
