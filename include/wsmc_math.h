@@ -409,25 +409,36 @@ WSMC_HD uint64_t wsmc_qweight(double lw, double M, int K) {
 }
 
 /*
- * The three exact per-particle integers behind the Resample statistics (e = exp(lw - M)):
+ * The exact per-particle integers behind the Resample statistics (e = exp(lw - M), e2 = e*e
+ * rounded once in f64):
  *   q   = floor(e * 2^K)                 CDF weight (above)
- *   q21 = floor(e * 2^21)                ESS weight:  ESS% = (sum q21)^2 / (N sum q21^2)
- *   wf  = floor(frac(e * 2^K) * 2^42)    so that  sum floor(e * 2^(K+42)) = Q * 2^42 + sum wf,
- *                                        the fixed point of logsumexp (evidence, log-mean)
- * Each is an exact integer in f64 (q21^2 < 2^43, wf < 2^42), so a device can sum them in
- * f64 over 1024-particle tiles without rounding (< 2^53) and every reduction order,
- * grid and shard layout gives the same bits.
+ *   wf  = floor(frac(e * 2^K) * 2^42)    so that  sum floor(e * 2^(K+42)) = Q * 2^42 + sum wf:
+ *                                        sum_i e_i to 2^-(K+42) per particle (logsumexp,
+ *                                        evidence, log-mean)
+ *   q2  = floor(e2 * 2^K)                the same two-part fixed point of e^2:
+ *   wf2 = floor(frac(e2 * 2^K) * 2^42)   sum floor(e2 * 2^(K+42)) = Q2 * 2^42 + sum wf2
+ * ESS% = (sum e)^2 / (N sum e^2) (src/resampling.jl:51-54 on w = e / sum e) is then taken
+ * from the two 85-bit sums: both are exact integers, so every reduction order, grid and shard
+ * layout gives the same bits, and each sum carries at most N 2^-(K+42) <= 2^-42 of
+ * truncation against a max term of 1 — the ESS matches the reference's f64 value to ~1e-15
+ * relative, heavy tails included. wf, wf2 < 2^42 and a 1024-particle tile sum stays below
+ * 2^53, so a device sums them in f64 exactly; q, q2 <= 2^K and their totals are u64
+ * (Q2 <= Q <= 2^63, since e2 <= e).
  */
-typedef struct { uint64_t q, q21, wf; } wsmc_qparts;
+typedef struct { uint64_t q, wf, q2, wf2; } wsmc_qparts;
 WSMC_HD wsmc_qparts wsmc_qparts_of(double lw, double M, int K) {
-    wsmc_qparts p = {0, 0, 0};
+    wsmc_qparts p = {0, 0, 0, 0};
     double e = wsmc_expw(lw - M);
     if (!(e > 0.0)) return p;
-    double s = e * wsmc_pow2i(K);
+    const double sK = wsmc_pow2i(K);
+    double s = e * sK;
     double qd = wsmc_floor(s);
     p.q = wsmc_d_to_u64_trunc(qd);
     p.wf = wsmc_d_to_u64_trunc(wsmc_floor((s - qd) * 4398046511104.0));   /* 2^42 */
-    p.q21 = wsmc_d_to_u64_trunc(wsmc_floor(e * 2097152.0));              /* 2^21 */
+    double s2 = (e * e) * sK;
+    double q2d = wsmc_floor(s2);
+    p.q2 = wsmc_d_to_u64_trunc(q2d);
+    p.wf2 = wsmc_d_to_u64_trunc(wsmc_floor((s2 - q2d) * 4398046511104.0));
     return p;
 }
 
@@ -600,14 +611,28 @@ WSMC_HD int wsmc_cholesky(const double* a, double* L, int d) {
 typedef struct {
     double M;          /* shard max log-weight (NaN if any NaN) */
     uint64_t Q;        /* sum q_i */
-    uint64_t S1;       /* sum q21_i */
-    wsmc_u128 S2;      /* sum q21_i^2 */
+    uint64_t Q2;       /* sum q2_i */
+    wsmc_u128 Wf2;     /* sum wf2_i (sum floor(e_i^2 2^(K+42)) = Q2 2^42 + Wf2) */
     wsmc_u128 Wf;      /* sum wf_i  (sum floor(e_i 2^(K+42)) = Q 2^42 + Wf) */
     uint64_t n;        /* shard size */
 } wsmc_shard_stats;
 
-/* ess_perc = (sum w)^2 / (N sum w^2) with w = exp_norm(weights) (src/resampling.jl:51-54),
- * on the 21-bit quantised weights q21 of every shard, rescaled by exp(M_g - M) */
+/* sum exp(lw_i - M) of one shard, from its fixed point sum floor(e 2^(K+42)) */
+WSMC_HD double wsmc_shard_expsum(const wsmc_shard_stats* s) {
+    int K = wsmc_qbits(s->n);
+    wsmc_u128 W = ((wsmc_u128)s->Q << 42) + s->Wf;
+    return wsmc_u128_to_d(W) * wsmc_pow2i(-(K + 42));
+}
+/* sum exp(lw_i - M)^2 of one shard, from its fixed point Q2 2^42 + Wf2 */
+WSMC_HD double wsmc_shard_expsum2(const wsmc_shard_stats* s) {
+    int K = wsmc_qbits(s->n);
+    wsmc_u128 W = ((wsmc_u128)s->Q2 << 42) + s->Wf2;
+    return wsmc_u128_to_d(W) * wsmc_pow2i(-(K + 42));
+}
+/* ess_perc = 1 / (N sum w^2), w = exp_norm(weights) (src/resampling.jl:51-54), i.e.
+ * (sum e)^2 / (N sum e^2), over every shard's fixed-point sums rescaled by exp(M_g - M)
+ * (rank order). One shard: f = 1 and the value is the exact-sum ratio; all-equal weights
+ * give exactly 1. */
 WSMC_HD double wsmc_global_ess(const wsmc_shard_stats* st, int G) {
     double M = -WSMC_INF;
     uint64_t N = 0;
@@ -618,19 +643,13 @@ WSMC_HD double wsmc_global_ess(const wsmc_shard_stats* st, int G) {
         N += st[g].n;
     }
     if (nan) M = WSMC_NAN;
-    double sq = 0.0, sq2 = 0.0;
+    double s1 = 0.0, s2 = 0.0;
     for (int g = 0; g < G; ++g) {
         double f = wsmc_exp(st[g].M - M);
-        sq = sq + (wsmc_u64_to_d(st[g].S1) * 4.76837158203125e-07) * f;            /* 2^-21 */
-        sq2 = sq2 + (wsmc_u128_to_d(st[g].S2) * 2.2737367544323206e-13) * (f * f); /* 2^-42 */
+        s1 = s1 + wsmc_shard_expsum(&st[g]) * f;
+        s2 = s2 + wsmc_shard_expsum2(&st[g]) * (f * f);
     }
-    return (sq * sq) / (wsmc_u64_to_d(N) * sq2);
-}
-/* sum exp(lw_i - M) of one shard, from its fixed point sum floor(e 2^(K+42)) */
-WSMC_HD double wsmc_shard_expsum(const wsmc_shard_stats* s) {
-    int K = wsmc_qbits(s->n);
-    wsmc_u128 W = ((wsmc_u128)s->Q << 42) + s->Wf;
-    return wsmc_u128_to_d(W) * wsmc_pow2i(-(K + 42));
+    return (s1 * s1) / (wsmc_u64_to_d(N) * s2);
 }
 /* logsumexp(shard weights) - log(n): the value every weight is reset to (src/transformers.jl:486-489) */
 WSMC_HD double wsmc_shard_mean(const wsmc_shard_stats* s) {

@@ -280,12 +280,12 @@ static or_stats shard_stats(const double* lw, int64_t n, int K) {
         else if (lw[i] > M) M = lw[i];
     }
     s.M = nan ? WSMC_NAN : M;                    /* maximum() propagates NaN */
-    s.Q = 0; s.S1 = 0; s.S2 = 0; s.Wf = 0; s.n = (uint64_t)n;
+    s.Q = 0; s.Q2 = 0; s.Wf2 = 0; s.Wf = 0; s.n = (uint64_t)n;
     for (int64_t i = 0; i < n; ++i) {
         wsmc_qparts p = wsmc_qparts_of(lw[i], s.M, K);
         s.Q += p.q;
-        s.S1 += p.q21;
-        s.S2 += (wsmc_u128)p.q21 * p.q21;
+        s.Q2 += p.q2;
+        s.Wf2 += p.wf2;
         s.Wf += p.wf;
     }
     return s;
@@ -491,38 +491,38 @@ int or_histogram(oracle* o, int32_t col, int32_t comp, int32_t* levels) {
  * record of this shard's weights relative to a given (global) max, K from the global N */
 void or_exact_record(oracle* o, double M, int64_t gN, uint64_t* out) {
     const int K = wsmc_qbits((uint64_t)gN);
-    uint64_t Q = 0, S1 = 0;
-    wsmc_u128 S2 = 0, Wf = 0;
+    uint64_t Q = 0, Q2 = 0;
+    wsmc_u128 Wf2 = 0, Wf = 0;
     for (int64_t i = 0; i < o->N; ++i) {
         wsmc_qparts p = wsmc_qparts_of(o->w[i], M, K);
-        Q += p.q; S1 += p.q21; S2 += (wsmc_u128)p.q21 * p.q21; Wf += p.wf;
+        Q += p.q; Q2 += p.q2; Wf2 += p.wf2; Wf += p.wf;
     }
-    out[0] = wsmc_d2bits(M); out[1] = Q; out[2] = S1;
-    out[3] = (uint64_t)S2; out[4] = (uint64_t)(S2 >> 64);
+    out[0] = wsmc_d2bits(M); out[1] = Q; out[2] = Q2;
+    out[3] = (uint64_t)Wf2; out[4] = (uint64_t)(Wf2 >> 64);
     out[5] = (uint64_t)Wf; out[6] = (uint64_t)(Wf >> 64);
     out[7] = (uint64_t)o->N;
 }
 /* the records summed as integers: the single-population statistics */
 void or_combine_records(const uint64_t* recs, int32_t G, uint64_t* out) {
-    uint64_t Q = 0, S1 = 0, n = 0;
-    wsmc_u128 S2 = 0, Wf = 0;
+    uint64_t Q = 0, Q2 = 0, n = 0;
+    wsmc_u128 Wf2 = 0, Wf = 0;
     for (int g = 0; g < G; ++g) {
         const uint64_t* r = recs + 8 * g;
-        Q += r[1]; S1 += r[2];
-        S2 += ((wsmc_u128)r[4] << 64) | r[3];
+        Q += r[1]; Q2 += r[2];
+        Wf2 += ((wsmc_u128)r[4] << 64) | r[3];
         Wf += ((wsmc_u128)r[6] << 64) | r[5];
         n += r[7];
     }
-    out[0] = recs[0]; out[1] = Q; out[2] = S1;
-    out[3] = (uint64_t)S2; out[4] = (uint64_t)(S2 >> 64);
+    out[0] = recs[0]; out[1] = Q; out[2] = Q2;
+    out[3] = (uint64_t)Wf2; out[4] = (uint64_t)(Wf2 >> 64);
     out[5] = (uint64_t)Wf; out[6] = (uint64_t)(Wf >> 64);
     out[7] = n;
 }
 /* ESS%, post-resample log-mean and log-evidence of one (combined) record */
 void or_record_summary(const uint64_t* rec, double* ess, double* mean, double* evidence) {
     or_stats st;
-    st.M = wsmc_bits2d(rec[0]); st.Q = rec[1]; st.S1 = rec[2];
-    st.S2 = ((wsmc_u128)rec[4] << 64) | rec[3];
+    st.M = wsmc_bits2d(rec[0]); st.Q = rec[1]; st.Q2 = rec[2];
+    st.Wf2 = ((wsmc_u128)rec[4] << 64) | rec[3];
     st.Wf = ((wsmc_u128)rec[6] << 64) | rec[5];
     st.n = rec[7];
     *ess = wsmc_global_ess(&st, 1);
@@ -553,21 +553,21 @@ void or_set_resample_flags(oracle* o, int32_t resampled, int32_t weights_changed
 }
 
 /* ---- one shard of a multi-process run: record exchange ------------------------------
- * record layout (8 x u64): M bits, Q, S1, S2 lo, S2 hi, Wf lo, Wf hi, n — the payload the GPU
+ * record layout (8 x u64): M bits, Q, Q2, Wf2 lo, Wf2 hi, Wf lo, Wf hi, n — the payload the GPU
  * ranks exchange with ncclAllGather each step (weightedsampling.jl_amd/csrc, ShardRec). */
 void or_shard_record(oracle* o, uint64_t* out) {
     or_stats s = shard_stats(o->w, o->N, wsmc_qbits((uint64_t)o->N));
     out[0] = wsmc_d2bits(s.M); out[1] = s.Q;
-    out[2] = s.S1;
-    out[3] = (uint64_t)s.S2; out[4] = (uint64_t)(s.S2 >> 64);
+    out[2] = s.Q2;
+    out[3] = (uint64_t)s.Wf2; out[4] = (uint64_t)(s.Wf2 >> 64);
     out[5] = (uint64_t)s.Wf; out[6] = (uint64_t)(s.Wf >> 64);
     out[7] = s.n;
 }
 static or_stats record_stats(const uint64_t* r) {
     or_stats s;
     s.M = wsmc_bits2d(r[0]); s.Q = r[1];
-    s.S1 = r[2];
-    s.S2 = ((wsmc_u128)r[4] << 64) | r[3];
+    s.Q2 = r[2];
+    s.Wf2 = ((wsmc_u128)r[4] << 64) | r[3];
     s.Wf = ((wsmc_u128)r[6] << 64) | r[5];
     s.n = r[7];
     return s;

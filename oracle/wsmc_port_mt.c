@@ -39,8 +39,8 @@ static inline double aff2(double a, double b) {
 typedef struct {
     double M;
     int nan;
-    uint64_t Q, S1;
-    wsmc_u128 S2, Wf;
+    uint64_t Q, Q2;
+    wsmc_u128 Wf2, Wf;
 } part_stats;
 
 /*
@@ -139,23 +139,23 @@ int or_ssm2d_run_mt(int64_t N, uint64_t seed, uint64_t op_base, const double* w0
 #pragma omp parallel num_threads(nthreads)
         {
             const int th = omp_get_thread_num();
-            uint64_t Q = 0, S1 = 0;
-            wsmc_u128 S2 = 0, Wf = 0;
+            uint64_t Q = 0, Q2 = 0;
+            wsmc_u128 Wf2 = 0, Wf = 0;
 #pragma omp for schedule(static)
             for (int64_t n = 0; n < N; ++n) {
                 const wsmc_qparts p = wsmc_qparts_of(w[n], M, K);
                 q[n] = p.q;
                 Q += p.q;
-                S1 += p.q21;
-                S2 += (wsmc_u128)p.q21 * p.q21;
+                Q2 += p.q2;
+                Wf2 += p.wf2;
                 Wf += p.wf;
             }
-            ps[th].Q = Q; ps[th].S1 = S1; ps[th].S2 = S2; ps[th].Wf = Wf;
+            ps[th].Q = Q; ps[th].Q2 = Q2; ps[th].Wf2 = Wf2; ps[th].Wf = Wf;
         }
         wsmc_shard_stats st;
-        st.M = M; st.Q = 0; st.S1 = 0; st.S2 = 0; st.Wf = 0; st.n = (uint64_t)N;
+        st.M = M; st.Q = 0; st.Q2 = 0; st.Wf2 = 0; st.Wf = 0; st.n = (uint64_t)N;
         for (int k = 0; k < nthreads; ++k) {
-            st.Q += ps[k].Q; st.S1 += ps[k].S1; st.S2 += ps[k].S2; st.Wf += ps[k].Wf;
+            st.Q += ps[k].Q; st.Q2 += ps[k].Q2; st.Wf2 += ps[k].Wf2; st.Wf += ps[k].Wf;
         }
         const double ess = wsmc_global_ess(&st, 1);
         rs[t] = ess < ess_min;                    /* strict, src/transformers.jl:484 */
@@ -220,10 +220,10 @@ int or_ssm2d_run_mt(int64_t N, uint64_t seed, uint64_t op_base, const double* w0
             else if (w[i] > M) M = w[i];
         }
         wsmc_shard_stats st;
-        st.M = nan ? WSMC_NAN : M; st.Q = 0; st.S1 = 0; st.S2 = 0; st.Wf = 0; st.n = (uint64_t)N;
+        st.M = nan ? WSMC_NAN : M; st.Q = 0; st.Q2 = 0; st.Wf2 = 0; st.Wf = 0; st.n = (uint64_t)N;
         for (int64_t i = 0; i < N; ++i) {
             const wsmc_qparts p = wsmc_qparts_of(w[i], st.M, K);
-            st.Q += p.q; st.S1 += p.q21; st.S2 += (wsmc_u128)p.q21 * p.q21; st.Wf += p.wf;
+            st.Q += p.q; st.Q2 += p.q2; st.Wf2 += p.wf2; st.Wf += p.wf;
         }
         *log_evidence = wsmc_global_log_evidence(&st, 1);
     }

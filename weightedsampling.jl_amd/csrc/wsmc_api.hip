@@ -161,8 +161,8 @@ static wsmc_shard_stats host_record_stats(const ShardRecord& r) {
     wsmc_shard_stats st;
     st.M = wsmc_ord_dec(r.menc);
     st.Q = r.Q;
-    st.S1 = r.s1;
-    st.S2 = ((wsmc_u128)r.s2hi << 64) | r.s2lo;
+    st.Q2 = r.q2;
+    st.Wf2 = ((wsmc_u128)r.wf2hi << 64) | r.wf2lo;
     st.Wf = ((wsmc_u128)r.wfhi << 64) | r.wflo;
     st.n = r.n;
     return st;
@@ -611,10 +611,10 @@ static int exact_global_stats(wsmc_ctx* c, wsmc_shard_stats* st) {
     WSMC_HIP(hipMemcpyAsync(h.data(), c->rec, sizeof(ShardRecord) * c->world, hipMemcpyDeviceToHost, c->stream));
     WSMC_HIP(hipStreamSynchronize(c->stream));
     *st = host_record_stats(h[0]);
-    st->Q = 0; st->S1 = 0; st->S2 = 0; st->Wf = 0; st->n = 0;
+    st->Q = 0; st->Q2 = 0; st->Wf2 = 0; st->Wf = 0; st->n = 0;
     for (int g = 0; g < c->world; ++g) {
         const wsmc_shard_stats x = host_record_stats(h[g]);
-        st->Q += x.Q; st->S1 += x.S1; st->S2 += x.S2; st->Wf += x.Wf; st->n += x.n;
+        st->Q += x.Q; st->Q2 += x.Q2; st->Wf2 += x.Wf2; st->Wf += x.Wf; st->n += x.n;
     }
     return WSMC_OK;
 }

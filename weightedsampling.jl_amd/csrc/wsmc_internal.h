@@ -43,14 +43,14 @@ struct MaxSlots {
 struct ShardRecord {
     unsigned long long menc;   // ordered encoding of the shard max log-weight
     unsigned long long Q;      // sum q_i
-    unsigned long long s1;     // sum q21_i (ESS weights, include/wsmc_math.h wsmc_qparts)
-    unsigned long long s2lo, s2hi;  // sum q21_i^2 (u128)
+    unsigned long long q2;     // sum q2_i (ESS: the fixed point of e^2, include/wsmc_math.h wsmc_qparts)
+    unsigned long long wf2lo, wf2hi;  // sum wf2_i (u128): sum floor(e^2 2^(K+42)) = Q2 2^42 + Wf2
     unsigned long long wflo, wfhi;  // sum wf_i (u128): sum floor(e 2^(K+42)) = Q 2^42 + Wf
     unsigned long long n;      // shard size
 };
 
-constexpr int kPart = 4;      // per-tile partials: sum q, sum q21, sum q21^2, sum wf (all exact)
-constexpr int kRedPart = 6;   // reduce-kernel parts: Q, S1, S2 lo32/hi, Wf lo32/hi
+constexpr int kPart = 4;      // per-tile partials: sum q, sum q2, sum wf2, sum wf (all exact)
+constexpr int kRedPart = 6;   // reduce-kernel parts: Q, Q2, Wf2 lo32/hi, Wf lo32/hi
 
 // Resample outcome for one invocation (one step of a fused run).
 constexpr int kDecRing = 1024;   // asynchronous Resample decisions held before a forced resolve

@@ -242,19 +242,74 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
     return v;
 }
 
+// The per-particle Resample statistics (include/wsmc_math.h wsmc_qparts): q and the tile
+// accumulators of q, q2 (u64) and wf2, wf (exact integers in f64: a tile's sums stay below
+// 2^53, so f64 accumulation is exact and order-free — no 128-bit arithmetic per particle).
+struct QAcc {
+    u64 Q = 0, Q2 = 0;
+    double WF2 = 0.0, WF = 0.0;
+};
+__device__ __forceinline__ u64 qacc_add(QAcc& a, double e, double sK) {
+    u64 q = 0, q2 = 0;
+    double wf = 0.0, wf2 = 0.0;
+    if (e > 0.0) {
+        const double sc = e * sK;
+        const double qd = wsmc_floor(sc);
+        q = (u64)qd;                                        // exact integer <= 2^63
+        wf = wsmc_floor((sc - qd) * 4398046511104.0);      // 2^42
+        const double sc2 = (e * e) * sK;
+        const double q2d = wsmc_floor(sc2);
+        q2 = (u64)q2d;
+        wf2 = wsmc_floor((sc2 - q2d) * 4398046511104.0);
+    }
+    a.Q += q;
+    a.Q2 += q2;
+    a.WF2 = a.WF2 + wf2;
+    a.WF = a.WF + wf;
+    return q;
+}
+// a block's QAcc -> the tile partials (sum q, sum q2, sum wf2, sum wf) in threads < kPart;
+// s_u [2][nw], s_f [2][nw] LDS; returns the tile's sum q in thread 0 (0 elsewhere)
+template <int NB>
+__device__ __forceinline__ u64 qacc_tile(QAcc a, u64 (*s_u)[NB / 64], double (*s_f)[NB / 64], u64* out) {
+    const int th = threadIdx.x;
+    a.Q = wave_sum_u64(a.Q);
+    a.Q2 = wave_sum_u64(a.Q2);
+    a.WF2 = wave_sum_f64(a.WF2);
+    a.WF = wave_sum_f64(a.WF);
+    const int wv = th >> 6;
+    if ((th & 63) == 0) {
+        s_u[0][wv] = a.Q; s_u[1][wv] = a.Q2;
+        s_f[0][wv] = a.WF2; s_f[1][wv] = a.WF;
+    }
+    __syncthreads();
+    u64 t = 0;
+    if (th < kPart) {
+        if (th < 2) {
+#pragma unroll
+            for (int v = 0; v < NB / 64; ++v) t += s_u[th][v];
+        } else {
+            double f = 0.0;
+#pragma unroll
+            for (int v = 0; v < NB / 64; ++v) f = f + s_f[th - 2][v];
+            t = (u64)f;                                         // exact: < 2^53
+        }
+        out[th] = t;
+    }
+    return th == 0 ? t : 0ull;
+}
+
 // Weight statistics of one 1024-particle tile (256 threads x 4 particles, coalesced):
-// q (stored for the fill), and the tile sums of q, q21, q21^2, wf (include/wsmc_math.h
-// wsmc_qparts). q21, q21^2 and wf are exact integers in f64 and their tile sums stay
-// below 2^53, so f64 accumulation is exact and order-free — no 128-bit arithmetic per
-// particle. MODE (diagnostics only; production = 0): 1 = no exp, 4 = load/store only.
+// q (stored for the fill) and the tile partials of qacc_tile.
+// MODE (diagnostics only; production = 0): 1 = no exp, 4 = load/store only.
 template <int MODE>
 __global__ __launch_bounds__(kSumBlock) void k_rs_sums_t(const double* __restrict__ w, int64_t N,
                                                          const MaxSlots* __restrict__ ms, u64* __restrict__ tilep,
                                                          u64* __restrict__ qbuf, u64* __restrict__ grp, int G,
                                                          int64_t Nk) {
     constexpr int IT = kRsTile / kSumBlock;
-    __shared__ double s_f[3][kSumBlock / 64];
-    __shared__ u64 s_q[kSumBlock / 64];
+    __shared__ double s_f[2][kSumBlock / 64];
+    __shared__ u64 s_u[2][kSumBlock / 64];
     const int th = threadIdx.x;
     const int64_t base = (int64_t)blockIdx.x * kRsTile;
     double lw[IT];
@@ -265,8 +320,7 @@ __global__ __launch_bounds__(kSumBlock) void k_rs_sums_t(const double* __restric
     }
     const double M = MODE == 4 ? 0.0 : wave_slots_max(ms);
     const double sK = wsmc_pow2i(wsmc_qbits((uint64_t)Nk));   // Nk: the global N when exact-sharded
-    u64 Q = 0;
-    double S1 = 0.0, S2 = 0.0, WF = 0.0;
+    QAcc acc;
 #pragma unroll
     for (int k = 0; k < IT; ++k) {
         const int64_t i = base + (int64_t)k * kSumBlock + th;
@@ -275,56 +329,22 @@ __global__ __launch_bounds__(kSumBlock) void k_rs_sums_t(const double* __restric
             continue;
         }
         const double e = MODE == 1 ? (lw[k] > M - 1.0 ? 1.0 : 0.5) : wsmc_expw(lw[k] - M);
-        u64 q = 0;
-        double q21 = 0.0, wf = 0.0;
-        if (e > 0.0) {
-            const double sc = e * sK;
-            const double qd = wsmc_floor(sc);
-            q = (u64)qd;                                        // exact integer <= 2^63
-            wf = wsmc_floor((sc - qd) * 4398046511104.0);      // 2^42
-            q21 = wsmc_floor(e * 2097152.0);                   // 2^21
-        }
+        const u64 q = qacc_add(acc, e, sK);
         if (i < N) qbuf[i] = q;
-        Q += q;
-        S1 = S1 + q21;
-        S2 = S2 + q21 * q21;
-        WF = WF + wf;
     }
     if (MODE == 4) return;
-    Q = wave_sum_u64(Q);
-    S1 = wave_sum_f64(S1);
-    S2 = wave_sum_f64(S2);
-    WF = wave_sum_f64(WF);
-    const int wv = th >> 6;
-    if ((th & 63) == 0) {
-        s_q[wv] = Q;
-        s_f[0][wv] = S1; s_f[1][wv] = S2; s_f[2][wv] = WF;
-    }
-    __syncthreads();
-    if (th < kPart) {
-        u64 t = 0;
-        if (th == 0) {
-#pragma unroll
-            for (int v = 0; v < kSumBlock / 64; ++v) t += s_q[v];
-        } else {
-            double f = 0.0;
-#pragma unroll
-            for (int v = 0; v < kSumBlock / 64; ++v) f = f + s_f[th - 1][v];
-            t = (u64)f;                                         // exact: < 2^53
-        }
-        tilep[(int64_t)blockIdx.x * kPart + th] = t;
-        // group sums of q (fused runs; integer atomics, so order-free): the fill's CDF
-        // offsets and the shard record's Q
-        if (grp && th == 0) atomicAdd(grp + (int64_t)(blockIdx.x / G) * kGroupLine, t);
-    }
+    const u64 t = qacc_tile<kSumBlock>(acc, s_u, s_f, tilep + (int64_t)blockIdx.x * kPart);
+    // group sums of q (fused runs; integer atomics, so order-free): the fill's CDF
+    // offsets and the shard record's Q
+    if (grp && th == 0) atomicAdd(grp + (int64_t)(blockIdx.x / G) * kGroupLine, t);
 }
 
 __device__ __forceinline__ wsmc_shard_stats record_stats(const ShardRecord& r) {
     wsmc_shard_stats st;
     st.M = wsmc_ord_dec(r.menc);
     st.Q = r.Q;
-    st.S1 = r.s1;
-    st.S2 = ((wsmc_u128)r.s2hi << 64) | r.s2lo;
+    st.Q2 = r.q2;
+    st.Wf2 = ((wsmc_u128)r.wf2hi << 64) | r.wf2lo;
     st.Wf = ((wsmc_u128)r.wfhi << 64) | r.wflo;
     st.n = r.n;
     return st;
@@ -343,15 +363,15 @@ __device__ void decide_records(const ShardRecord* recs, int world, int rank, dou
         N += recs[g].n;
     }
     if (nan) M = WSMC_NAN;
-    double sq = 0.0, sq2 = 0.0;
+    double s1 = 0.0, s2 = 0.0;
     for (int g = 0; g < world; ++g) {
         // the arithmetic of wsmc_global_ess, streamed over the records
         const wsmc_shard_stats st = record_stats(recs[g]);
         const double f = wsmc_exp(st.M - M);
-        sq = sq + (wsmc_u64_to_d(st.S1) * 4.76837158203125e-07) * f;
-        sq2 = sq2 + (wsmc_u128_to_d(st.S2) * 2.2737367544323206e-13) * (f * f);
+        s1 = s1 + wsmc_shard_expsum(&st) * f;
+        s2 = s2 + wsmc_shard_expsum2(&st) * (f * f);
     }
-    const double ess = (sq * sq) / (wsmc_u64_to_d(N) * sq2);
+    const double ess = (s1 * s1) / (wsmc_u64_to_d(N) * s2);
     const int rs = ess < ess_min;
     const wsmc_shard_stats me = record_stats(recs[rank]);
     dec->resampled = rs;
@@ -395,7 +415,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_reduce_t(const MaxSlots* __rest
     for (int64_t b = b0; b < b1; ++b)
 #pragma unroll
         for (int k = 0; k < kPart; ++k) t4[k] += tilep[b * kPart + k];
-    // Q and S1 totals fit u64; S2 and Wf are summed as 32-bit limbs into u128
+    // Q and Q2 totals fit u64; Wf2 and Wf are summed as 32-bit limbs into u128
     const u64 acc[kRedPart] = {t4[0], t4[1], t4[2] & 0xffffffffull, t4[2] >> 32, t4[3] & 0xffffffffull,
                                t4[3] >> 32};
     block_sum_parts<kRsBlock, kRedPart>(acc, red, red2, tot);
@@ -464,10 +484,10 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_reduce_t(const MaxSlots* __rest
             ShardRecord r;
             r.menc = menc;
             r.Q = tot[0];
-            r.s1 = tot[1];
-            const wsmc_u128 S2 = (wsmc_u128)tot[2] + ((wsmc_u128)tot[3] << 32);
+            r.q2 = tot[1];
+            const wsmc_u128 Wf2 = (wsmc_u128)tot[2] + ((wsmc_u128)tot[3] << 32);
             const wsmc_u128 Wf = (wsmc_u128)tot[4] + ((wsmc_u128)tot[5] << 32);
-            r.s2lo = (u64)S2; r.s2hi = (u64)(S2 >> 64);
+            r.wf2lo = (u64)Wf2; r.wf2hi = (u64)(Wf2 >> 64);
             r.wflo = (u64)Wf; r.wfhi = (u64)(Wf >> 64);
             r.n = (u64)N;
             *rec = r;
@@ -503,15 +523,15 @@ __global__ void k_rs_decide_exact(const ShardRecord* recs, int world, int rank, 
                                   ShardRecord* comb, Decision* dec, ExactPlan* xp) {
     if (threadIdx.x != 0) return;
     ShardRecord r = recs[0];
-    wsmc_u128 S2 = 0, Wf = 0;
-    u64 Q = 0, S1 = 0, n = 0;
+    wsmc_u128 Wf2 = 0, Wf = 0;
+    u64 Q = 0, Q2 = 0, n = 0;
     u64 cb[kMaxShards + 1];
     for (int g = 0; g < world; ++g) {
         cb[g] = Q;
         xp->gofs[g] = n;
         Q += recs[g].Q;
-        S1 += recs[g].s1;
-        S2 += ((wsmc_u128)recs[g].s2hi << 64) | recs[g].s2lo;
+        Q2 += recs[g].q2;
+        Wf2 += ((wsmc_u128)recs[g].wf2hi << 64) | recs[g].wf2lo;
         Wf += ((wsmc_u128)recs[g].wfhi << 64) | recs[g].wflo;
         n += recs[g].n;
         r.menc = recs[g].menc > r.menc ? recs[g].menc : r.menc;
@@ -519,8 +539,8 @@ __global__ void k_rs_decide_exact(const ShardRecord* recs, int world, int rank, 
     cb[world] = Q;
     xp->gofs[world] = n;
     r.Q = Q;
-    r.s1 = S1;
-    r.s2lo = (u64)S2; r.s2hi = (u64)(S2 >> 64);
+    r.q2 = Q2;
+    r.wf2lo = (u64)Wf2; r.wf2hi = (u64)(Wf2 >> 64);
     r.wflo = (u64)Wf; r.wfhi = (u64)(Wf >> 64);
     r.n = n;
     *comb = r;
@@ -739,8 +759,9 @@ __global__ __launch_bounds__(kSumBlock) void k_rs_sums_multi(const double* __res
                                                              u64* __restrict__ tilep, u64* __restrict__ lcdf,
                                                              u64* __restrict__ esum, uint32_t* __restrict__ ebuf) {
     constexpr int IT = kRsTile / kSumBlock;
-    __shared__ double s_f[3][kSumBlock / 64];
-    __shared__ u64 s_q[2][kSumBlock / 64];
+    __shared__ double s_f[2][kSumBlock / 64];
+    __shared__ u64 s_u[2][kSumBlock / 64];
+    __shared__ u64 s_e[kSumBlock / 64];
     __shared__ u64 s_w[kSumBlock / 64];
     const int th = threadIdx.x;
     const int64_t base = (int64_t)blockIdx.x * kRsTile + (int64_t)th * IT;
@@ -750,24 +771,11 @@ __global__ __launch_bounds__(kSumBlock) void k_rs_sums_multi(const double* __res
     const double M = wave_slots_max(ms);
     const double sK = wsmc_pow2i(wsmc_qbits((uint64_t)N));
     const uint64_t opx = op_eff(plan.op, plan.op_dev);
-    u64 q[IT], Q = 0, E = 0;
-    double S1 = 0.0, S2 = 0.0, WF = 0.0;
+    u64 q[IT], E = 0;
+    QAcc acc;
 #pragma unroll
     for (int k = 0; k < IT; ++k) {
-        const double e = wsmc_expw(lw[k] - M);
-        q[k] = 0;
-        double q21 = 0.0, wf = 0.0;
-        if (e > 0.0) {
-            const double sc = e * sK;
-            const double qd = wsmc_floor(sc);
-            q[k] = (u64)qd;
-            wf = wsmc_floor((sc - qd) * 4398046511104.0);      // 2^42
-            q21 = wsmc_floor(e * 2097152.0);                   // 2^21
-        }
-        Q += q[k];
-        S1 = S1 + q21;
-        S2 = S2 + q21 * q21;
-        WF = WF + wf;
+        q[k] = qacc_add(acc, wsmc_expw(lw[k] - M), sK);
         if (base + k < N) {
             const u64 ek = wsmc_multi_e(plan.seed, opx, (uint64_t)plan.slot_base, (uint64_t)(base + k), (uint64_t)N);
             E += ek;
@@ -775,38 +783,20 @@ __global__ __launch_bounds__(kSumBlock) void k_rs_sums_multi(const double* __res
         }
     }
     u64 qtot;
-    u64 c = block_excl_scan_u64<kSumBlock / 64>(Q, s_w, &qtot);
+    u64 c = block_excl_scan_u64<kSumBlock / 64>(acc.Q, s_w, &qtot);
 #pragma unroll
     for (int k = 0; k < IT; ++k) {
         c += q[k];
         if (base + k < N) lcdf[base + k] = c;
     }
     E = wave_sum_u64(E);
-    S1 = wave_sum_f64(S1);
-    S2 = wave_sum_f64(S2);
-    WF = wave_sum_f64(WF);
-    const int wv = th >> 6;
-    if ((th & 63) == 0) {
-        s_q[0][wv] = E;
-        s_f[0][wv] = S1; s_f[1][wv] = S2; s_f[2][wv] = WF;
-    }
-    __syncthreads();
-    if (th < kPart + 1) {
+    if ((th & 63) == 0) s_e[th >> 6] = E;
+    qacc_tile<kSumBlock>(acc, s_u, s_f, tilep + (int64_t)blockIdx.x * kPart);   // its barrier publishes s_e
+    if (th == kPart) {
         u64 t = 0;
-        if (th == 0) {
-            t = qtot;
-        } else if (th == kPart) {
 #pragma unroll
-            for (int v = 0; v < kSumBlock / 64; ++v) t += s_q[0][v];
-            esum[blockIdx.x] = t;
-            return;
-        } else {
-            double f = 0.0;
-#pragma unroll
-            for (int v = 0; v < kSumBlock / 64; ++v) f = f + s_f[th - 1][v];
-            t = (u64)f;                                         // exact: < 2^53
-        }
-        tilep[(int64_t)blockIdx.x * kPart + th] = t;
+        for (int v = 0; v < kSumBlock / 64; ++v) t += s_e[v];
+        esum[blockIdx.x] = t;
     }
 }
 
@@ -1116,10 +1106,10 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
         u64 acc[kRedPart] = {0, 0, 0, 0, 0, 0};
         for (int g = th; g < ngroups; g += kScanBlock) acc[0] += grp[(int64_t)g * kGroupLine];
         for (int b = th; b < ntiles; b += kScanBlock) {
-            const u64 s1 = plan.tilep[(int64_t)b * kPart + 1], s2 = plan.tilep[(int64_t)b * kPart + 2],
+            const u64 q2 = plan.tilep[(int64_t)b * kPart + 1], wf2 = plan.tilep[(int64_t)b * kPart + 2],
                       wf = plan.tilep[(int64_t)b * kPart + 3];
-            acc[1] += s1;
-            acc[2] += s2 & 0xffffffffull; acc[3] += s2 >> 32;
+            acc[1] += q2;
+            acc[2] += wf2 & 0xffffffffull; acc[3] += wf2 >> 32;
             acc[4] += wf & 0xffffffffull; acc[5] += wf >> 32;
         }
         const u64 menc = th < kSlots ? wave_max_u64(ms->v[th & (kSlots - 1)][0]) : 0ull;
@@ -1136,10 +1126,10 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
             ShardRecord r;
             r.menc = menc;
             r.Q = tot[0];
-            r.s1 = tot[1];
-            const wsmc_u128 S2 = (wsmc_u128)tot[2] + ((wsmc_u128)tot[3] << 32);
+            r.q2 = tot[1];
+            const wsmc_u128 Wf2 = (wsmc_u128)tot[2] + ((wsmc_u128)tot[3] << 32);
             const wsmc_u128 Wf = (wsmc_u128)tot[4] + ((wsmc_u128)tot[5] << 32);
-            r.s2lo = (u64)S2; r.s2hi = (u64)(S2 >> 64);
+            r.wf2lo = (u64)Wf2; r.wf2hi = (u64)(Wf2 >> 64);
             r.wflo = (u64)Wf; r.wfhi = (u64)(Wf >> 64);
             r.n = (u64)N;
             *rec = r;
