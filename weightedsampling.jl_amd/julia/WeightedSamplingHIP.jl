@@ -273,15 +273,60 @@ function apply!(t::WS.Assign, state::HipState)
     WS.advance!(state)
 end
 
+"""
+    importance_kernel(proposal, target)
+
+`WeightedSampling.importance_kernel` (src/default_kernels.jl:69-73), registered so that a
+`Sample` through it lowers to `wsmc_sample_importance` (draw from `proposal`, weights +=
+logpdf(target) − logpdf(proposal), tape term = logpdf(target)). Kernels built by the
+reference's own `importance_kernel` are recognised too, through the closures' captured
+`proposal` / `target` fields.
+"""
+const IMPORTANCE = IdDict{Any,Tuple{Any,Any}}()
+function importance_kernel(proposal, target)
+    k = WS.importance_kernel(proposal, target)
+    IMPORTANCE[k] = (proposal, target)
+    return k
+end
+function importance_parts(k)
+    haskey(IMPORTANCE, k) && return IMPORTANCE[k]
+    f = k.weighter
+    (hasfield(typeof(f), :proposal) && hasfield(typeof(f), :target)) || return nothing
+    return (getfield(f, :proposal), getfield(f, :target))
+end
+
+"""A Distributions.jl object with constant parameters as a `WsmcDist` (or `nothing`)."""
+function const_dist(d)
+    z = const_operand(0.0)
+    d isa Normal && return WsmcDist(FAM_NORMAL, MEAN_AFFINE, 1, 0, ntuple(_ -> const_operand(d.μ), 4),
+                                    const_operand(d.σ), (0.0, 0.0))
+    d isa Uniform && return WsmcDist(FAM_UNIFORM, MEAN_AFFINE, 1, 0, (z, z, z, z), const_operand(1.0), (d.a, d.b))
+    return nothing
+end
+
 function apply!(t::WS.Sample, state::HipState)
     s = state.store
     args = t.argfn(state)
-    dist = t.kernel.weighter === nothing ? device_dist(s, t.kernel, args) : nothing
-    if dist === nothing                           # host path: reference apply!, weights round-trip
-        invoke(apply!, Tuple{WS.Sample,SMCState}, t, sync_weights!(state))
-        check(ccall((:wsmc_weights_upload, libwsmc), Cint, (Ptr{Cvoid}, Ptr{Float64}), s.ctx, state.weights))
+    if t.kernel.weighter !== nothing
+        # A weighted Sample lowers only for importance kernels over device families. Any other
+        # weighter would need the host to weigh AND extend the device's score tape and depth,
+        # so it is refused rather than desynchronising weights_changed / depth from the
+        # device (src/transformers.jl:172-182).
+        parts = importance_parts(t.kernel)
+        pd, td = parts === nothing ? (nothing, nothing) : map(const_dist, parts)
+        (pd === nothing || td === nothing) &&
+            error("WeightedSamplingHIP: weighted Sample kernel not supported on the device path " *
+                  "(importance_kernel over constant Normal / Uniform is)")
+        id = column!(s, t.lhs, 1)
+        check(ccall((:wsmc_sample_importance, libwsmc), Cint, (Ptr{Cvoid}, Int32, Ref{WsmcDist}, Ref{WsmcDist}),
+                    s.ctx, id, pd, td))
+        state.weights_changed = true
+        WS.advance!(state)
         return nothing
     end
+    dist = device_dist(s, t.kernel, args)
+    dist === nothing && error("WeightedSamplingHIP: Sample kernel not supported on the device path " *
+                              "(Normal, Uniform, isotropic MvNormal and importance_kernel are)")
     id = column!(s, t.lhs, dist.dim)
     check(ccall((:wsmc_sample, libwsmc), Cint, (Ptr{Cvoid}, Int32, Ref{WsmcDist}), s.ctx, id, dist))
     WS.advance!(state)
