@@ -193,14 +193,18 @@ int wsmc_col_minmax(wsmc_ctx* ctx, int32_t col_id, int32_t comp, double* min_out
 int wsmc_ess(wsmc_ctx* ctx, double* ess_perc);
 /* describe()'s weighted median (StatsBase.quantile(v, Weights(w), 0.5)) and 8-bin sparkline
  * histogram levels (1..8, src/utils.jl:134-141) of one column component, on the integer
- * weights (include/wsmc_math.h); single-shard contexts only */
+ * weights (include/wsmc_math.h). On shards both are population-wide: the median takes the
+ * union of every rank's (value, q) pairs, the sparkline sums integer bins taken at the
+ * population's max log-weight — the bits of one context holding every particle. */
 int wsmc_weighted_median(wsmc_ctx* ctx, int32_t col_id, int32_t comp, double* out);
 int wsmc_histogram(wsmc_ctx* ctx, int32_t col_id, int32_t comp, int32_t levels[8]);
 /* sample(state, n; replace) (src/utils.jl:92-118): n particle indices (0-based) drawn by
  * the normalised weights — with replacement independent draws in draw order, without
  * replacement the n largest Efraimidis–Spirakis keys (include/wsmc_math.h wsmc_es_key).
  * Consumes one op counter (the reference draws from the global RNG). WSMC_EARG for n <= 0
- * or (!replace && n > N), as the reference's ArgumentError; single-shard contexts only. */
+ * or (!replace && n > N), as the reference's ArgumentError. On shards the indices are
+ * global and the draws are the single-context draws (each target located by the rank whose
+ * CDF range holds it; without replacement the union of the ranks' top-n keys). */
 int wsmc_sample_particles(wsmc_ctx* ctx, int64_t n, int32_t replace, int64_t* idx_out);
 /* rows idx[0..n) of a column, [dim][n] (getcol(store, c)[indices], src/utils.jl:117) */
 int wsmc_col_gather_rows(wsmc_ctx* ctx, int32_t col_id, const int64_t* idx, int64_t n, double* out);

@@ -393,14 +393,18 @@ WSMC_HD double wsmc_log_abs_jac(double z, double lo, double hi) {
 /* ------------------------------------------------------------------------- */
 /*
  * exp_norm/ess_perc/icdf (src/resampling.jl:13-77) on an integer CDF:
- *   q_i = floor(expw(lw_i - M) * 2^K),  K = 63 - ceil(log2 N)   =>  Q = sum q_i <= 2^63
+ *   q_i = floor(expw(lw_i - M) * 2^K),  K = min(63 - ceil(log2 N), 43)   =>  Q = sum q_i <= 2^63
  * (expw: the division-free exp above)
  * Integer sums are associative, so the CDF, Q, the ESS sums and the ancestors are
  * identical for any reduction order, grid shape or shard count.
  */
 WSMC_HD int wsmc_qbits(uint64_t n) {
-    /* 63 - ceil(log2 n) */
-    return n <= 1 ? 63 : 63 - (64 - __builtin_clzll(n - 1));
+    /* min(63 - ceil(log2 n), 43): Q = sum q_i <= n 2^K <= 2^63, and a 1024-particle tile's
+       sums of q, q2 (<= 2^(K+10) <= 2^53) and wf, wf2 (< 2^52) are exact in f64, so a device
+       accumulates all four per-particle integers in f64 and converts once per tile. The cap
+       binds below n = 2^20 (C2's 1M particles already have K = 43). */
+    const int k = n <= 1 ? 63 : 63 - (64 - __builtin_clzll(n - 1));
+    return k < 43 ? k : 43;
 }
 WSMC_HD uint64_t wsmc_qweight(double lw, double M, int K) {
     double e = wsmc_expw(lw - M);

@@ -75,7 +75,9 @@ def test_draw_moments():
 
 
 def test_qbits():
-    for n, k in [(1, 63), (2, 62), (3, 61), (1024, 53), (1025, 52), (1 << 20, 43), (1_000_000, 43)]:
+    # min(63 - ceil(log2 n), 43): the cap keeps a tile's f64 sums exact (include/wsmc_math.h)
+    for n, k in [(1, 43), (2, 43), (1024, 43), (1 << 20, 43), (1_000_000, 43), ((1 << 20) + 1, 42),
+                 (8_000_000, 40), (1 << 31, 32)]:
         assert L.or_qbits(n) == k
 
 

@@ -215,7 +215,7 @@ def check_against_reference(name, lw, out, ref, ess_min):
 
 
 def wsmc_qbits(n):
-    return 63 if n <= 1 else 63 - (n - 1).bit_length()
+    return min(43, 63 if n <= 1 else 63 - (n - 1).bit_length())
 
 
 def test_strat_word_restatement_matches_oracle():

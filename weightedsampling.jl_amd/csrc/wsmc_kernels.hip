@@ -22,19 +22,72 @@ typedef unsigned long long u64;
 
 // ------------------------------------------------------------------------------------
 // wave / block primitives (wave64)
+// Cross-lane moves are DPP (a VALU operand modifier) rather than ds_bpermute (an LDS
+// round trip per step): quad_perm 1,0,3,2 / 2,3,0,1, row_ror 4 / 8 reduce within each row
+// of 16 lanes, row_bcast 15 / 31 carry the rows up to lane 63. Lanes without a source read
+// the identity (update_dpp's `old`).
 // ------------------------------------------------------------------------------------
+enum : int {
+    kDppQuad1032 = 0xb1, kDppQuad2301 = 0x4e, kDppRowRor4 = 0x124, kDppRowRor8 = 0x128,
+    kDppRowShr1 = 0x111, kDppRowShr2 = 0x112, kDppRowShr3 = 0x113, kDppRowShr4 = 0x114,
+    kDppRowShr8 = 0x118, kDppBcast15 = 0x142, kDppBcast31 = 0x143, kDppWaveShr1 = 0x138
+};
+template <int CTRL, int ROW = 0xf, int BANK = 0xf>
+__device__ __forceinline__ u64 dpp_u64(u64 v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, ROW, BANK, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, ROW, BANK, false);
+    return ((u64)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {   // identity 0.0 (bits 0)
+    return __builtin_bit_cast(double, dpp_u64<CTRL>(__builtin_bit_cast(u64, v)));
+}
+__device__ __forceinline__ u64 lane63_u64(u64 v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63);
+    return ((u64)hi << 32) | lo;
+}
+// wave totals (every lane gets the result)
 __device__ __forceinline__ u64 wave_sum_u64(u64 v) {
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
-    return v;
+    v += dpp_u64<kDppQuad1032>(v);
+    v += dpp_u64<kDppQuad2301>(v);
+    v += dpp_u64<kDppRowRor4>(v);
+    v += dpp_u64<kDppRowRor8>(v);
+    v += dpp_u64<kDppBcast15>(v);
+    v += dpp_u64<kDppBcast31>(v);
+    return lane63_u64(v);
 }
 __device__ __forceinline__ u64 wave_max_u64(u64 v) {
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        u64 o = __shfl_xor(v, off, 64);
-        v = o > v ? o : v;
-    }
-    return v;
+    u64 o;
+    o = dpp_u64<kDppQuad1032>(v); v = o > v ? o : v;
+    o = dpp_u64<kDppQuad2301>(v); v = o > v ? o : v;
+    o = dpp_u64<kDppRowRor4>(v); v = o > v ? o : v;
+    o = dpp_u64<kDppRowRor8>(v); v = o > v ? o : v;
+    o = dpp_u64<kDppBcast15>(v); v = o > v ? o : v;
+    o = dpp_u64<kDppBcast31>(v); v = o > v ? o : v;
+    return lane63_u64(v);
+}
+// wave total of f64 values that are exact integers whose sum stays below 2^53 (any order
+// gives the same bits); NOT for canonical floating sums (block_sum_canon)
+__device__ __forceinline__ double wave_sum_f64_exact(double v) {
+    v = v + dpp_f64<kDppQuad1032>(v);
+    v = v + dpp_f64<kDppQuad2301>(v);
+    v = v + dpp_f64<kDppRowRor4>(v);
+    v = v + dpp_f64<kDppRowRor8>(v);
+    v = v + dpp_f64<kDppBcast15>(v);
+    v = v + dpp_f64<kDppBcast31>(v);
+    return __builtin_bit_cast(double, lane63_u64(__builtin_bit_cast(u64, v)));
+}
+// inclusive prefix sum over the wave (lane order)
+__device__ __forceinline__ u64 wave_incl_scan_u64(u64 v) {
+    u64 x = v + dpp_u64<kDppRowShr1>(v);
+    x += dpp_u64<kDppRowShr2>(v);
+    x += dpp_u64<kDppRowShr3>(v);
+    x += dpp_u64<kDppRowShr4, 0xf, 0xe>(x);
+    x += dpp_u64<kDppRowShr8, 0xf, 0xc>(x);
+    x += dpp_u64<kDppBcast15, 0xa, 0xf>(x);
+    x += dpp_u64<kDppBcast31, 0xc, 0xf>(x);
+    return x;
 }
 // canonical f64 block sum: xor butterfly 1..32 inside each wave, then (w0+w1)+(w2+w3)
 __device__ __forceinline__ double block_sum_canon(double v, double* lds4) {
@@ -67,12 +120,7 @@ __device__ __forceinline__ u64 block_max_u64(u64 v, u64* lds4) {
 template <int NW = 4>
 __device__ __forceinline__ u64 block_excl_scan_u64(u64 v, u64* ldsw, u64* total) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    u64 x = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        u64 y = __shfl_up(x, off, 64);
-        if (lane >= off) x += y;
-    }
+    const u64 x = wave_incl_scan_u64(v);
     if (lane == 63) ldsw[w] = x;
     __syncthreads();
     u64 pre = 0, t = 0;
@@ -236,64 +284,53 @@ __device__ __forceinline__ void block_sum_parts(const u64 (&acc)[P], u64 (*red)[
     }
 }
 
-__device__ __forceinline__ double wave_sum_f64(double v) {
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) v = v + __shfl_xor(v, off, 64);
-    return v;
-}
-
 // The per-particle Resample statistics (include/wsmc_math.h wsmc_qparts): q and the tile
-// accumulators of q, q2 (u64) and wf2, wf (exact integers in f64: a tile's sums stay below
-// 2^53, so f64 accumulation is exact and order-free — no 128-bit arithmetic per particle).
+// accumulators of q, q2, wf2, wf.
+// All four are exact integers held in f64: q, q2 <= 2^K <= 2^43 and wf, wf2 < 2^42, so a
+// 1024-particle tile's sums stay below 2^53 (wsmc_qbits) and f64 accumulation is exact and
+// order-free — no 64-bit integer arithmetic or conversion per particle.
 struct QAcc {
-    u64 Q = 0, Q2 = 0;
-    double WF2 = 0.0, WF = 0.0;
+    double Q = 0.0, Q2 = 0.0, WF2 = 0.0, WF = 0.0;
 };
+// an exact integer-valued double in [0, 2^52) -> u64 (the low mantissa bits of d + 2^52)
+__device__ __forceinline__ u64 d_small_to_u64(double d) {
+    return __builtin_bit_cast(u64, d + 4503599627370496.0) - 0x4330000000000000ull;
+}
 __device__ __forceinline__ u64 qacc_add(QAcc& a, double e, double sK) {
-    u64 q = 0, q2 = 0;
-    double wf = 0.0, wf2 = 0.0;
-    if (e > 0.0) {
-        const double sc = e * sK;
-        const double qd = wsmc_floor(sc);
-        q = (u64)qd;                                        // exact integer <= 2^63
-        wf = wsmc_floor((sc - qd) * 4398046511104.0);      // 2^42
-        const double sc2 = (e * e) * sK;
-        const double q2d = wsmc_floor(sc2);
-        q2 = (u64)q2d;
-        wf2 = wsmc_floor((sc2 - q2d) * 4398046511104.0);
-    }
-    a.Q += q;
-    a.Q2 += q2;
+    e = e > 0.0 ? e : 0.0;                                  // -inf weights, NaN: all parts 0
+    const double sc = e * sK;
+    const double qd = wsmc_floor(sc);
+    const double wf = wsmc_floor((sc - qd) * 4398046511104.0);      // 2^42
+    const double sc2 = (e * e) * sK;
+    const double q2d = wsmc_floor(sc2);
+    const double wf2 = wsmc_floor((sc2 - q2d) * 4398046511104.0);
+    a.Q = a.Q + qd;
+    a.Q2 = a.Q2 + q2d;
     a.WF2 = a.WF2 + wf2;
     a.WF = a.WF + wf;
-    return q;
+    return d_small_to_u64(qd);
 }
 // a block's QAcc -> the tile partials (sum q, sum q2, sum wf2, sum wf) in threads < kPart;
-// s_u [2][nw], s_f [2][nw] LDS; returns the tile's sum q in thread 0 (0 elsewhere)
+// s_f [4][nw] LDS; returns the tile's sum q in thread 0 (0 elsewhere)
 template <int NB>
-__device__ __forceinline__ u64 qacc_tile(QAcc a, u64 (*s_u)[NB / 64], double (*s_f)[NB / 64], u64* out) {
+__device__ __forceinline__ u64 qacc_tile(QAcc a, double (*s_f)[NB / 64], u64* out) {
     const int th = threadIdx.x;
-    a.Q = wave_sum_u64(a.Q);
-    a.Q2 = wave_sum_u64(a.Q2);
-    a.WF2 = wave_sum_f64(a.WF2);
-    a.WF = wave_sum_f64(a.WF);
+    a.Q = wave_sum_f64_exact(a.Q);
+    a.Q2 = wave_sum_f64_exact(a.Q2);
+    a.WF2 = wave_sum_f64_exact(a.WF2);
+    a.WF = wave_sum_f64_exact(a.WF);
     const int wv = th >> 6;
     if ((th & 63) == 0) {
-        s_u[0][wv] = a.Q; s_u[1][wv] = a.Q2;
-        s_f[0][wv] = a.WF2; s_f[1][wv] = a.WF;
+        s_f[0][wv] = a.Q; s_f[1][wv] = a.Q2;
+        s_f[2][wv] = a.WF2; s_f[3][wv] = a.WF;
     }
     __syncthreads();
     u64 t = 0;
     if (th < kPart) {
-        if (th < 2) {
+        double f = 0.0;
 #pragma unroll
-            for (int v = 0; v < NB / 64; ++v) t += s_u[th][v];
-        } else {
-            double f = 0.0;
-#pragma unroll
-            for (int v = 0; v < NB / 64; ++v) f = f + s_f[th - 2][v];
-            t = (u64)f;                                         // exact: < 2^53
-        }
+        for (int v = 0; v < NB / 64; ++v) f = f + s_f[th][v];
+        t = (u64)f;                                         // exact integer <= 2^53
         out[th] = t;
     }
     return th == 0 ? t : 0ull;
@@ -308,8 +345,7 @@ __global__ __launch_bounds__(kSumBlock) void k_rs_sums_t(const double* __restric
                                                          u64* __restrict__ qbuf, u64* __restrict__ grp, int G,
                                                          int64_t Nk) {
     constexpr int IT = kRsTile / kSumBlock;
-    __shared__ double s_f[2][kSumBlock / 64];
-    __shared__ u64 s_u[2][kSumBlock / 64];
+    __shared__ double s_f[kPart][kSumBlock / 64];
     const int th = threadIdx.x;
     const int64_t base = (int64_t)blockIdx.x * kRsTile;
     double lw[IT];
@@ -333,10 +369,16 @@ __global__ __launch_bounds__(kSumBlock) void k_rs_sums_t(const double* __restric
         if (i < N) qbuf[i] = q;
     }
     if (MODE == 4) return;
-    const u64 t = qacc_tile<kSumBlock>(acc, s_u, s_f, tilep + (int64_t)blockIdx.x * kPart);
+    const u64 t = qacc_tile<kSumBlock>(acc, s_f, tilep + (int64_t)blockIdx.x * kPart);
     // group sums of q (fused runs; integer atomics, so order-free): the fill's CDF
     // offsets and the shard record's Q
-    if (grp && th == 0) atomicAdd(grp + (int64_t)(blockIdx.x / G) * kGroupLine, t);
+    // word 1: the group's largest tile sum (the fill's overflow blocks exit early when no
+    // tile can own more than one chunk of slots)
+    if (grp && th == 0) {
+        u64* gl = grp + (int64_t)(blockIdx.x / G) * kGroupLine;
+        atomicAdd(gl, t);
+        atomicMax(gl + 1, t);
+    }
 }
 
 __device__ __forceinline__ wsmc_shard_stats record_stats(const ShardRecord& r) {
@@ -605,7 +647,26 @@ struct FillLds {
     u64 last[kScanBlock / 64];
     int nheavy;
     int heavy[kRsChunk / kScatterMax + 1][3];   // particle (tile-local), first slot, end slot (chunk-local)
+    int32_t out[kRsChunk];                      // the chunk's ancestors, staged for coalesced stores
 };
+
+// write the staged chunk sh.out[0, n) to dst[0, n): 16-B stores on the aligned body,
+// single stores on the ragged ends (dst is 4-B aligned; any slot offset)
+__device__ __forceinline__ void store_chunk(int32_t* __restrict__ dst, int n, const FillLds& sh) {
+    const int head = (int)((4 - (((uintptr_t)dst >> 2) & 3)) & 3);    // slots before a 16-B boundary
+    const int h = head < n ? head : n;
+    const int nv = (n - h) >> 2;                                        // whole 16-B vectors
+    for (int v = threadIdx.x; v < nv; v += kScanBlock) {
+        const int k = h + 4 * v;
+        int4 o;
+        o.x = sh.out[k]; o.y = sh.out[k + 1]; o.z = sh.out[k + 2]; o.w = sh.out[k + 3];
+        *reinterpret_cast<int4*>(dst + k) = o;
+    }
+    const int tail0 = h + 4 * nv;
+    const int th = threadIdx.x;
+    if (th < h) dst[th] = sh.out[th];
+    else if (th >= 4 && th - 4 < n - tail0) dst[tail0 + th - 4] = sh.out[tail0 + th - 4];
+}
 
 // fill chunk j of tile b (block-uniform arguments; ends with a barrier so LDS can be reused).
 // Particle m owns the slots [hi_{m-1}, hi_m) with hi_m = rank(C_m); each thread ranks its 4
@@ -671,7 +732,7 @@ __device__ __forceinline__ void fill_chunk_q(int64_t N, int b, int j, u64 Q, u64
         prev = h;
     }
     // first slot of the thread's first particle = hi of the previous thread's last particle
-    u64 lo = __shfl_up(hi[IT - 1], 1, 64);
+    u64 lo = dpp_u64<kDppWaveShr1>(hi[IT - 1]);   // lane l gets lane l-1's (lane 0: set below)
     if (lane == 63) sh.last[wv] = hi[IT - 1];
     __syncthreads();
     if (lane == 0) lo = wv > 0 ? sh.last[wv - 1] : L;
@@ -679,19 +740,22 @@ __device__ __forceinline__ void fill_chunk_q(int64_t N, int b, int j, u64 Q, u64
         if (lo == 0x123456789ull) anc[0] = 1;
         return;
     }
+    // the chunk's ancestors are scattered into LDS, then stored coalesced (a particle's
+    // slots written straight to HBM were one masked 4-B store per slot per lane)
 #pragma unroll
     for (int k = 0; k < IT; ++k) {
         const u64 a = lo > cs ? lo : cs;
         const u64 e = hi[k] < ce ? hi[k] : ce;
         const int32_t m = (int32_t)(base + th * IT + k);
         if (a < e) {
-            if (e - a > (u64)kScatterMax) {
+            const int a0 = (int)(a - cs), e0 = (int)(e - cs);
+            if (e0 - a0 > kScatterMax) {
                 const int x = atomicAdd(&sh.nheavy, 1);
                 sh.heavy[x][0] = m;
-                sh.heavy[x][1] = (int)(a - cs);
-                sh.heavy[x][2] = (int)(e - cs);
+                sh.heavy[x][1] = a0;
+                sh.heavy[x][2] = e0;
             } else {
-                for (u64 n = a; n < e; ++n) anc[n - s0] = m;
+                for (int n = a0; n < e0; ++n) sh.out[n] = m;
             }
         }
         lo = hi[k];
@@ -701,8 +765,10 @@ __device__ __forceinline__ void fill_chunk_q(int64_t N, int b, int j, u64 Q, u64
     const int nh = sh.nheavy;
     for (int x = wv; x < nh; x += kScanBlock / 64) {
         const int m = sh.heavy[x][0];
-        for (int n = sh.heavy[x][1] + lane; n < sh.heavy[x][2]; n += 64) anc[cs - s0 + n] = m;
+        for (int n = sh.heavy[x][1] + lane; n < sh.heavy[x][2]; n += 64) sh.out[n] = m;
     }
+    __syncthreads();
+    store_chunk(anc + (cs - s0), (int)(ce - cs), sh);
     __syncthreads();
 }
 
@@ -759,8 +825,7 @@ __global__ __launch_bounds__(kSumBlock) void k_rs_sums_multi(const double* __res
                                                              u64* __restrict__ tilep, u64* __restrict__ lcdf,
                                                              u64* __restrict__ esum, uint32_t* __restrict__ ebuf) {
     constexpr int IT = kRsTile / kSumBlock;
-    __shared__ double s_f[2][kSumBlock / 64];
-    __shared__ u64 s_u[2][kSumBlock / 64];
+    __shared__ double s_f[kPart][kSumBlock / 64];
     __shared__ u64 s_e[kSumBlock / 64];
     __shared__ u64 s_w[kSumBlock / 64];
     const int th = threadIdx.x;
@@ -783,7 +848,7 @@ __global__ __launch_bounds__(kSumBlock) void k_rs_sums_multi(const double* __res
         }
     }
     u64 qtot;
-    u64 c = block_excl_scan_u64<kSumBlock / 64>(acc.Q, s_w, &qtot);
+    u64 c = block_excl_scan_u64<kSumBlock / 64>(d_small_to_u64(acc.Q), s_w, &qtot);
 #pragma unroll
     for (int k = 0; k < IT; ++k) {
         c += q[k];
@@ -791,7 +856,7 @@ __global__ __launch_bounds__(kSumBlock) void k_rs_sums_multi(const double* __res
     }
     E = wave_sum_u64(E);
     if ((th & 63) == 0) s_e[th >> 6] = E;
-    qacc_tile<kSumBlock>(acc, s_u, s_f, tilep + (int64_t)blockIdx.x * kPart);   // its barrier publishes s_e
+    qacc_tile<kSumBlock>(acc, s_f, tilep + (int64_t)blockIdx.x * kPart);   // its barrier publishes s_e
     if (th == kPart) {
         u64 t = 0;
 #pragma unroll
@@ -1156,10 +1221,18 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
         return;
     }
     // ---- overflow chunks: plan from the tile sums (contiguous tiles per thread) ----
-    u64 Q = 0, dummy = 0;
-    for (int k = th; k < ngroups; k += kScanBlock) Q += grp[(int64_t)k * 8];
+    u64 Q = 0, qmax = 0;
+    for (int k = th; k < ngroups; k += kScanBlock) {
+        Q += grp[(int64_t)k * kGroupLine];
+        const u64 m = grp[(int64_t)k * kGroupLine + 1];
+        qmax = m > qmax ? m : qmax;
+    }
+    qmax = block_max_u64(qmax, sh.uw);
+    u64 dummy = 0;
     block_sum2_u64(Q, dummy, s_red);
     const double ratio = Q ? wsmc_u64_to_d((uint64_t)N) / wsmc_u64_to_d(Q) : 0.0;
+    if (ovf_chunks(qmax, ratio) == 0) return;   // no tile owns more than its first chunk
+
     const int per = (ntiles + kScanBlock - 1) / kScanBlock;
     const int b0 = th * per < ntiles ? th * per : ntiles;
     const int b1 = b0 + per < ntiles ? b0 + per : ntiles;
