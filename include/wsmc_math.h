@@ -326,16 +326,33 @@ WSMC_HD double wsmc_uniform_k(uint64_t seed, uint64_t op, uint64_t idx, uint32_t
     return (k & 1) ? wsmc_u01(w.v[2], w.v[3]) : wsmc_u01(w.v[0], w.v[1]);
 }
 /* 32-bit stratum offset word for resampling slot n (systematic: one word for all slots).
- * A murmur3 fmix64 finalizer over (seed, op, n): a bijective 64-bit mixer, ~20 integer
- * ops, cheap enough to evaluate inside the per-particle rank() of the ancestor scan. */
-WSMC_HD uint32_t wsmc_strat_word(uint64_t seed, uint64_t op, uint64_t n) {
-    uint64_t z = seed ^ (op * 0x9E3779B97F4A7C15ULL) ^ (n * 0xD1B54A32D192ED03ULL) ^ 0x5851F42D4C957F2DULL;
+ * A per-Resample key k = murmur3 fmix64(seed ^ op*phi ^ c) (uniform over a launch, so the
+ * device evaluates it once on the scalar unit), then a 32-bit integer hash of the slot:
+ * x = lo32(n) ^ lo32(k) ^ (hi32(n) * c' ^ hi32(k)), and Wellons' lowbias32 finalizer
+ * (xorshift-multiply x2, a bijection on 32 bits). About 8 vector ops with two 32-bit
+ * multiplies inside the per-particle rank() of the ancestor fill, where the 64-bit fmix of
+ * every slot cost four times that. */
+WSMC_HD uint64_t wsmc_strat_key(uint64_t seed, uint64_t op) {
+    uint64_t z = seed ^ (op * 0x9E3779B97F4A7C15ULL) ^ 0x5851F42D4C957F2DULL;
     z ^= z >> 33;
     z *= 0xFF51AFD7ED558CCDULL;
     z ^= z >> 33;
     z *= 0xC4CEB9FE1A85EC53ULL;
     z ^= z >> 33;
-    return (uint32_t)(z >> 32);
+    return z;
+}
+WSMC_HD uint32_t wsmc_strat_hash(uint64_t key, uint64_t n) {
+    uint32_t x = (uint32_t)n ^ (uint32_t)key;
+    x ^= (uint32_t)(n >> 32) * 0x85EBCA6Bu ^ (uint32_t)(key >> 32);
+    x ^= x >> 16;
+    x *= 0x7FEB352Du;
+    x ^= x >> 15;
+    x *= 0x846CA68Bu;
+    x ^= x >> 16;
+    return x;
+}
+WSMC_HD uint32_t wsmc_strat_word(uint64_t seed, uint64_t op, uint64_t n) {
+    return wsmc_strat_hash(wsmc_strat_key(seed, op), n);
 }
 
 /* ------------------------------------------------------------------------- */

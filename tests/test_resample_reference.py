@@ -6,7 +6,7 @@ ess_perc = 1/(N sum w^2), logsumexp, the stratified uniforms us[n] = (n-1)/N + r
 the sequential icdf merge). It uses nothing from include/wsmc_math.h: the build's integer
 CDF, fixed-point sums and rank arithmetic are never consulted. The only shared input is the
 uniform each slot draws (`rand()` of src/resampling.jl:40 is the build's 32-bit stratum word,
-restated below from its published definition, murmur3 fmix64 over (seed, op, slot)), so
+restated below from its definition, a keyed lowbias32 hash of the slot), so
 the two sides resample the same weights with the same uniforms.
 
 Checked on benign, heavy-tailed, dominant, near-threshold (ESS = 0.5 +- 1e-6), -Inf,
@@ -34,6 +34,7 @@ from backends import make_ctx
 from wsmc.dsl import Uniform
 from wsmc.models import resolver
 
+M32 = (1 << 32) - 1
 M64 = (1 << 64) - 1
 
 
@@ -73,30 +74,43 @@ def ref_icdf(w, us):
     return np.searchsorted(c, us, side="left"), c
 
 
-def strat_word(seed, op, n):
-    """The 32-bit uniform word of resampling slot n (the build's stream for rand() of
-    src/resampling.jl:40): murmur3's fmix64 over (seed, op, n)."""
-    z = (seed ^ ((op * 0x9E3779B97F4A7C15) & M64) ^ ((n * 0xD1B54A32D192ED03) & M64) ^ 0x5851F42D4C957F2D) & M64
+def strat_key(seed, op):
+    """The per-Resample key: murmur3's fmix64 over (seed, op)."""
+    z = (seed ^ ((op * 0x9E3779B97F4A7C15) & M64) ^ 0x5851F42D4C957F2D) & M64
     z ^= z >> 33
     z = (z * 0xFF51AFD7ED558CCD) & M64
     z ^= z >> 33
     z = (z * 0xC4CEB9FE1A85EC53) & M64
     z ^= z >> 33
-    return z >> 32
+    return z
+
+
+def strat_word(seed, op, n):
+    """The 32-bit uniform word of resampling slot n (the build's stream for rand() of
+    src/resampling.jl:40): the keyed lowbias32 hash of the slot."""
+    k = strat_key(seed, op)
+    x = (n ^ k) & M32
+    x ^= (((n >> 32) * 0x85EBCA6B) & M32) ^ (k >> 32)
+    x ^= x >> 16
+    x = (x * 0x7FEB352D) & M32
+    x ^= x >> 15
+    x = (x * 0x846CA68B) & M32
+    x ^= x >> 16
+    return x
 
 
 def strat_words(seed, op, n, start=0):
-    s = np.uint64(seed)
-    k = np.arange(start, start + n, dtype=np.uint64)
+    k = strat_key(seed, op)
+    idx = np.arange(start, start + n, dtype=np.uint64)
     with np.errstate(over="ignore"):
-        z = s ^ np.uint64((op * 0x9E3779B97F4A7C15) & M64) ^ (k * np.uint64(0xD1B54A32D192ED03)) \
-            ^ np.uint64(0x5851F42D4C957F2D)
-        z ^= z >> np.uint64(33)
-        z *= np.uint64(0xFF51AFD7ED558CCD)
-        z ^= z >> np.uint64(33)
-        z *= np.uint64(0xC4CEB9FE1A85EC53)
-        z ^= z >> np.uint64(33)
-    return (z >> np.uint64(32)).astype(np.float64)
+        x = ((idx ^ np.uint64(k)) & np.uint64(M32)).astype(np.uint32)
+        x ^= ((idx >> np.uint64(32)).astype(np.uint32) * np.uint32(0x85EBCA6B)) ^ np.uint32(k >> 32)
+        x ^= x >> np.uint32(16)
+        x *= np.uint32(0x7FEB352D)
+        x ^= x >> np.uint32(15)
+        x *= np.uint32(0x846CA68B)
+        x ^= x >> np.uint32(16)
+    return x.astype(np.float64)
 
 
 class RefResample:

@@ -1162,9 +1162,12 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
     __shared__ u64 s_red[kScanBlock / 64][2];
     __shared__ u64 s_parts[kScanBlock / 64][kRedPart];
     __shared__ u64 s_task[3];
-    const int t = blockIdx.x, th = threadIdx.x;
+    const int th = threadIdx.x;
     const int ntiles = (int)((N + kRsTile - 1) / kRsTile);
     const int ngroups = (ntiles + G - 1) / G;
+    // block 0 (dispatched first: its serial decision is the longest chain) is the record
+    // block; blocks 1..ntiles fill the tiles' first chunks, the rest serve overflow chunks
+    const int t = blockIdx.x == 0 ? ntiles + kOverflowBlocks : (int)blockIdx.x - 1;
     if (t == ntiles + kOverflowBlocks) {
         // ---- the shard record and (one GPU, dec != null) the decision; a sharded run
         // all-gathers the records and decides afterwards (k_rs_decide) ----
