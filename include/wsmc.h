@@ -173,6 +173,16 @@ int wsmc_col_upload(wsmc_ctx* ctx, int32_t col_id, const double* host);
 int wsmc_col_device_ptr(wsmc_ctx* ctx, int32_t col_id, double** dptr);
 /* resample!(store, indices) with caller-supplied 0-based indices (src/stores.jl:105-128) */
 int wsmc_store_resample(wsmc_ctx* ctx, const int32_t* host_indices);
+/* Lazy genealogy of the store (the default; ColumnStore.resample! gathers every column at
+ * every resample, src/stores.jl:105-128, which is O(T^2 N) over a run that keeps a history
+ * column per step). A Resample logs its int32 ancestors and gathers only the columns an
+ * operator touched since the previous Resample; the others are brought up to date, all in
+ * one trace over the log, when a later operator or getcol reads one. Values are bit-identical
+ * to the eager gathers (a gather is a copy). lazy = 0 restores the eager gathers (after
+ * bringing every column up to date); exact shards are always eager.
+ * wsmc_store_info: log entries held and columns currently behind the log. */
+int wsmc_store_set_lazy(wsmc_ctx* ctx, int32_t lazy);
+int wsmc_store_info(wsmc_ctx* ctx, int64_t* log_entries, int32_t* stale_columns);
 
 /* ---- weights: SMCState.weights (src/types.jl:48-60) ------------------------- */
 int wsmc_weights_upload(wsmc_ctx* ctx, const double* host);

@@ -59,9 +59,10 @@ class ShardCtx:
     def __getattr__(self, k):
         return getattr(self.o, k)
 
-    def resample(self, ess_perc_min, scheme=0):
+    def resample(self, ess_perc_min, scheme=0, wait=True):
         recs = self.exchange(self.o.shard_record())
-        return self.o.resample_records(ess_perc_min, scheme, np.stack(recs), self.rank)
+        r = self.o.resample_records(ess_perc_min, scheme, np.stack(recs), self.rank)
+        return r if wait else None
 
     def _global_unique(self, col):
         x = self.o.col_download(col)
@@ -249,7 +250,11 @@ class ExactShardCtx(ShardCtx):
     def last_ancestors(self):
         return self.last_anc
 
-    def resample(self, ess_perc_min, scheme=0):
+    def resample(self, ess_perc_min, scheme=0, wait=True):
+        r = self._resample(ess_perc_min, scheme)
+        return r if wait else None
+
+    def _resample(self, ess_perc_min, scheme=0):
         from oracle import Oracle
         st = self.o.get_state()
         op = st["op_counter"]

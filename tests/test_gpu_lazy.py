@@ -1,0 +1,97 @@
+"""Lazy genealogy of the generic store ("Lazy genealogy"): a Resample logs its
+ancestors and gathers only the columns touched since the previous Resample; history columns
+are brought up to date by one trace over the log when read. The reference gathers every
+column at every resample (src/stores.jl:105-128); the values must be identical — checked
+against the eager device store and the CPU oracle (whose store is the reference's eager
+ColumnStore), bit for bit."""
+import numpy as np
+import pytest
+
+import wsmc
+from wsmc import abi, models
+from oracle import Oracle
+from test_gpu_parity import assert_same_state
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("scheme", [abi.RESAMPLE_STRATIFIED, abi.RESAMPLE_MULTINOMIAL])
+@pytest.mark.parametrize("wait", [True, False])
+def test_lazy_history_matches_oracle(gpu_available, scheme, wait):
+    """C2's statements over T = 150 steps (> one trace launch's 96 log entries): the history
+    columns x_1..x_T stay behind the log until downloaded, then match the eager oracle."""
+    N, T = 3001, 150
+    obs = models.ssm2d_data(T)
+    g, o = wsmc.Context(N, seed=5), Oracle(N, seed=5)
+    models.ssm2d_statements(g, obs, ess_perc_min=1.0, scheme=scheme, wait=wait)
+    models.ssm2d_statements(o, obs, ess_perc_min=1.0, scheme=scheme)
+    info = g.store_info()
+    assert info["stale_columns"] >= T - 2          # x_1 .. x_{T-1}: left behind, never gathered
+    assert T - 2 <= info["log_entries"] <= T + 1   # one ancestor row per resampling step
+    np.testing.assert_array_equal(g.last_ancestors(), o.last_ancestors())
+    assert_same_state(g, o)                        # downloads every column: one trace
+    assert g.store_info()["stale_columns"] == 0
+    assert g.log_evidence() == o.log_evidence()
+
+
+def test_lazy_equals_eager_device_store(gpu_available):
+    """The same run on a lazy and an eager (WSMC eager gathers) device store, bit for bit, at
+    the example default ess 0.5 (some steps do not resample: gated identity entries)."""
+    N, T = 5001, 40
+    obs = models.ssm2d_data(T)
+    a, b = wsmc.Context(N, seed=11), wsmc.Context(N, seed=11)
+    b.store_set_lazy(False)
+    models.ssm2d_statements(a, obs, ess_perc_min=0.5, wait=False)
+    models.ssm2d_statements(b, obs, ess_perc_min=0.5, wait=False)
+    assert b.store_info() == {"log_entries": 0, "stale_columns": 0}
+    assert_same_state(a, b)
+
+
+def test_lazy_log_stays_short_without_history(gpu_available):
+    """The LGSSM rebinds one column: every column is current after each Resample, so the log
+    keeps at most the newest row (last_ancestors) however long the run."""
+    data = models.lgssm1d_data(60)
+    g, o = wsmc.Context(2049, seed=3), Oracle(2049, seed=3)
+    models.lgssm1d_statements(g, data, ess_perc_min=1.0, wait=False)
+    models.lgssm1d_statements(o, data, ess_perc_min=1.0)
+    assert g.store_info()["stale_columns"] == 0
+    g.get_state()                                   # folds the pending decisions in
+    assert g.store_info()["log_entries"] <= 1
+    assert_same_state(g, o)
+    np.testing.assert_array_equal(g.last_ancestors(), o.last_ancestors())
+
+
+def test_lazy_switch_to_eager_midrun(gpu_available):
+    """Turning the lazy store off mid-run brings every column up to date first."""
+    N = 2500
+    obs = models.ssm2d_data(30)
+    g, o = wsmc.Context(N, seed=9), Oracle(N, seed=9)
+    models.ssm2d_statements(g, obs[:15], ess_perc_min=1.0)
+    models.ssm2d_statements(o, obs[:15], ess_perc_min=1.0)
+    assert g.store_info()["stale_columns"] > 0
+    g.store_set_lazy(False)
+    info = g.store_info()
+    assert info["stale_columns"] == 0 and info["log_entries"] <= 1   # the newest row: last_ancestors
+    assert_same_state(g, o)
+
+
+def test_lazy_explicit_store_resample(gpu_available):
+    """resample!(store, idx) with caller indices is logged like a Resample: a column the
+    operators stopped touching picks it up when read."""
+    N = 1000
+    rng = np.random.default_rng(1)
+    g, o = wsmc.Context(N, seed=2), Oracle(N, seed=2)
+    for ctx in (g, o):
+        a = ctx.col_create("a", 1)
+        ctx.col_upload(a, np.arange(N, dtype=float))
+        b = ctx.col_create("b", 2)
+        ctx.col_upload(b, np.arange(2 * N, dtype=float) * 0.5)
+    idx1 = rng.integers(0, N, N).astype(np.int32)
+    idx2 = np.sort(rng.integers(0, N, N)).astype(np.int32)
+    for ctx in (g, o):
+        ctx.store_resample(idx1)                   # both touched: gathered at once
+        ctx.col_upload(ctx.col_find("b"), np.ones(2 * N))
+        ctx.store_resample(idx2)                   # a untouched since the last one: left behind
+    assert g.store_info()["stale_columns"] == 1
+    assert_same_state(g, o)
+    np.testing.assert_array_equal(g.last_ancestors(), idx2)   # the last resample!'s indices

@@ -6,6 +6,7 @@
 //   apply!(...)                           src/transformers.jl:28-623
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -120,16 +121,18 @@ static void scores_touch(wsmc_ctx* c, int32_t col) {
     if (c->scache_terms >= 0 && tape_reads(c, col)) c->scache_terms = -1;
 }
 
-// ColumnStore.resample! of every column (and the carried Move scores) through c->anc, in
-// k_resample_apply launches of up to kGatherSet components; the last one also resets the
-// weights to dec->mean when w_reset is given. dec != null gates everything on the
-// device-side decision (the asynchronous Resample: identity copies when it did not
-// resample, so the front/back swap holds); null = an explicit resample!(store, idx).
-static int gather_all_columns(wsmc_ctx* c, const Decision* dec = nullptr, double* w_reset = nullptr) {
+// ColumnStore.resample! (src/stores.jl:105-128) of the given columns (and the carried Move
+// scores) through `anc`, in k_resample_apply launches of up to kGatherSet components; the
+// last one also resets the weights to dec->mean when w_reset is given. dec != null gates
+// everything on the device-side decision (the asynchronous Resample: identity copies when it
+// did not resample, so the front/back swap holds); null = an explicit resample!(store, idx).
+// The gathered columns' values become those of epoch `to_epoch`.
+static int gather_columns(wsmc_ctx* c, const std::vector<int32_t>& which, const int32_t* anc, const Decision* dec,
+                          double* w_reset, int64_t to_epoch) {
     GatherSet gs;
     gs.n = 0;
     auto flush = [&](bool last) -> hipError_t {
-        const hipError_t e = launch_resample_apply(c->stream, gs, c->anc, dec, last ? w_reset : nullptr, c->N);
+        const hipError_t e = launch_resample_apply(c->stream, gs, anc, dec, last ? w_reset : nullptr, c->N);
         gs.n = 0;
         return e;
     };
@@ -143,10 +146,12 @@ static int gather_all_columns(wsmc_ctx* c, const Decision* dec = nullptr, double
         gs.n += 1;
         return hipSuccess;
     };
-    for (auto& col : c->cols) {
+    for (int32_t id : which) {
+        Column& col = c->cols[id];
         for (int k = 0; k < col.dim; ++k)
             WSMC_HIP(add(col.back + (int64_t)k * c->N, col.front + (int64_t)k * c->N));
         std::swap(col.front, col.back);
+        col.epoch = to_epoch;
     }
     if (c->scache && c->scache_terms >= 0) {   // carried Move scores follow their particles
         WSMC_HIP(add(c->scache_back, c->scache));
@@ -154,6 +159,135 @@ static int gather_all_columns(wsmc_ctx* c, const Decision* dec = nullptr, double
     }
     WSMC_HIP(flush(true));
     c->colptr_dirty = true;
+    return WSMC_OK;
+}
+
+// ---- lazy genealogy (AncRow, wsmc_internal.h) ---------------------------------------------
+static inline size_t row_anc_bytes(int64_t N) { return (sizeof(int32_t) * (size_t)N + 255) & ~(size_t)255; }
+static int acquire_row(wsmc_ctx* c, AncRow* out) {
+    if (!c->row_pool.empty()) {
+        *out = c->row_pool.back();
+        c->row_pool.pop_back();
+    } else {
+        void* p = nullptr;
+        WSMC_HIP(hipMalloc(&p, row_anc_bytes(c->N) + 256));
+        out->anc = reinterpret_cast<int32_t*>(p);
+        out->dec = reinterpret_cast<Decision*>(reinterpret_cast<char*>(p) + row_anc_bytes(c->N));
+    }
+    out->known = -1;
+    return WSMC_OK;
+}
+// entries no column, no pending decision and no last_ancestors query can reach return to the pool
+static void gc_log(wsmc_ctx* c) {
+    int64_t keep = c->epoch;
+    for (const auto& col : c->cols) keep = std::min(keep, col.epoch);
+    if (c->anc_last_epoch >= 0) keep = std::min(keep, c->anc_last_epoch);
+    for (int64_t e : c->dec_epochs) keep = std::min(keep, e);
+    while (c->log_base < keep && !c->alog.empty()) {
+        c->row_pool.push_back(c->alog.front());
+        c->alog.pop_front();
+        c->log_base += 1;
+    }
+}
+// Bring every stale column to the current epoch: one walk over the log per particle, from
+// the newest entry back to the oldest a stale column needs (kTraceLev entries per launch,
+// the composed index carried between launches), each column read where its epoch is reached.
+static int materialize_all(wsmc_ctx* c) {
+    std::vector<std::pair<int64_t, int32_t>> stale;   // (levels to apply, column)
+    for (int32_t id = 0; id < (int32_t)c->cols.size(); ++id)
+        if (c->cols[id].epoch < c->epoch) stale.emplace_back(c->epoch - c->cols[id].epoch, id);
+    if (stale.empty()) return WSMC_OK;
+    std::sort(stale.begin(), stale.end());
+    const int64_t maxlev = stale.back().first;
+    if (c->epoch - maxlev < c->log_base) return fail(WSMC_ESTATE, "lazy genealogy: log entry already released");
+    int32_t* scratch[2] = {reinterpret_cast<int32_t*>(c->tmp), reinterpret_cast<int32_t*>(c->tmp) + c->N};
+    const int32_t* a_in = nullptr;
+    size_t next = 0;
+    for (int64_t base = 0, pass = 0; base < maxlev; base += kTraceLev, ++pass) {
+        const int nl = (int)std::min<int64_t>(kTraceLev, maxlev - base);
+        TraceArgs t{};
+        t.nlev = nl;
+        for (int j = 0; j < nl; ++j) {
+            const AncRow& r = c->alog[(size_t)(c->epoch - 1 - (base + j) - c->log_base)];
+            t.rows[j] = r.anc;
+            t.decs[j] = r.dec;
+        }
+        int32_t* a_out = base + nl < maxlev ? scratch[pass & 1] : nullptr;
+        t.a_in = a_in;
+        // this level range's columns, kTraceCols components a launch (each launch repeats the walk)
+        std::vector<TraceComp> comps;
+        for (; next < stale.size() && stale[next].first <= base + nl; ++next) {
+            Column& col = c->cols[stale[next].second];
+            for (int k = 0; k < col.dim; ++k)
+                comps.push_back({col.back + (int64_t)k * c->N, col.front + (int64_t)k * c->N,
+                                 (int32_t)(stale[next].first - base)});
+        }
+        size_t done = 0;
+        do {
+            const size_t n = std::min<size_t>(kTraceCols, comps.size() - done);
+            t.ncomp = (int32_t)n;
+            for (size_t k = 0; k < n; ++k) t.comp[k] = comps[done + k];
+            done += n;
+            t.a_out = done >= comps.size() ? a_out : nullptr;
+            WSMC_HIP(launch_lazy_trace(c->stream, t, c->N));
+        } while (done < comps.size());
+        a_in = a_out;
+    }
+    for (const auto& sc : stale) {
+        Column& col = c->cols[sc.second];
+        std::swap(col.front, col.back);
+        col.epoch = c->epoch;
+    }
+    c->colptr_dirty = true;
+    gc_log(c);
+    return WSMC_OK;
+}
+// an operator reads (or writes) these columns: mark them touched this epoch and bring any
+// stale one up to date first (all stale columns together: one walk of the log)
+static int need_cols(wsmc_ctx* c, const std::vector<int32_t>& ids) {
+    bool stale = false;
+    for (int32_t id : ids) {
+        if (id < 0 || id >= (int32_t)c->cols.size()) continue;
+        c->cols[id].touch = c->epoch;
+        stale |= c->cols[id].epoch < c->epoch;
+    }
+    return stale ? materialize_all(c) : WSMC_OK;
+}
+static void cols_of(const wsmc_operand& o, std::vector<int32_t>& v) {
+    for (int k = 0; k < 2; ++k)
+        if (o.col[k] >= 0) v.push_back(o.col[k]);
+}
+static void cols_of(const wsmc_dist& d, std::vector<int32_t>& v) {
+    for (int k = 0; k < 4; ++k) cols_of(d.mu[k], v);
+    cols_of(d.scale, v);
+}
+static void cols_of(const wsmc_term& t, std::vector<int32_t>& v) {
+    cols_of(t.dist, v);
+    for (int k = 0; k < 4; ++k) cols_of(t.x[k], v);
+}
+// a column an operator overwrites in full: its old values (of any epoch) are dead
+static void wrote_col(wsmc_ctx* c, int32_t id) {
+    c->cols[id].epoch = c->epoch;
+    c->cols[id].touch = c->epoch;
+}
+// the ColumnStore.resample! of one Resample / resample!(store, idx) with ancestors `row`:
+// lazy — log the row, gather the columns touched since the previous Resample (the live
+// state), leave the rest for a later trace; eager (exact shards, WSMC_EAGER_GATHER) — all
+static int store_resample_row(wsmc_ctx* c, const AncRow& row, const Decision* dec, double* w_reset) {
+    std::vector<int32_t> which;
+    for (int32_t id = 0; id < (int32_t)c->cols.size(); ++id) {
+        const Column& col = c->cols[id];
+        if (!c->lazy || (col.touch == c->epoch && col.epoch == c->epoch)) which.push_back(id);
+    }
+    if (!c->lazy) {   // every column is current: no log entry
+        int r = gather_columns(c, which, row.anc, dec, w_reset, c->epoch);
+        return r;
+    }
+    c->alog.push_back(row);
+    c->epoch += 1;
+    int r = gather_columns(c, which, row.anc, dec, w_reset, c->epoch);
+    if (r) return r;
+    gc_log(c);
     return WSMC_OK;
 }
 
@@ -217,6 +351,7 @@ int wsmc_create(wsmc_ctx** out, int64_t n_particles, int32_t device, uint64_t se
     ALLOC(c->tilepart, sizeof(double) * 16 * c->ntiles);
     ALLOC(c->rec, sizeof(ShardRecord) * kMaxWorld);
     ALLOC(c->dec, sizeof(Decision));
+    ALLOC(c->dec_always, sizeof(Decision));
     ALLOC(c->mom, sizeof(double) * 64);
     ALLOC(c->dflag, sizeof(int32_t) * 4);
     ALLOC(c->ucount, sizeof(unsigned long long) * 4);
@@ -229,7 +364,16 @@ int wsmc_create(wsmc_ctx** out, int64_t n_particles, int32_t device, uint64_t se
     if (e == hipSuccess) e = hipMemsetAsync(c->wslots[0], 0, sizeof(MaxSlots), c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->wslots[1], 0, sizeof(MaxSlots), c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->anc, 0, sizeof(int32_t) * c->N, c->stream);
+    if (e == hipSuccess) {
+        Decision always{};
+        always.resampled = 1;
+        e = hipMemcpy(c->dec_always, &always, sizeof(Decision), hipMemcpyHostToDevice);
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    {   // diagnostics / A-B: the reference's eager gather of every column at every resample
+        const char* eg = getenv("WSMC_EAGER_GATHER");
+        c->lazy = !(eg && atoi(eg) != 0);
+    }
     if (e != hipSuccess) {
         std::string m = std::string("wsmc_create: ") + hipGetErrorString(e);
         wsmc_destroy(c);
@@ -254,7 +398,9 @@ int wsmc_destroy(wsmc_ctx* c) {
         (void)hipFree(col.front);
         (void)hipFree(col.back);
     }
-    void* bufs[] = {c->xchg, c->scache, c->scache_back, c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->cdf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount, c->wslots[0], c->wslots[1],
+    for (auto& r : c->alog) (void)hipFree(r.anc);
+    for (auto& r : c->row_pool) (void)hipFree(r.anc);
+    void* bufs[] = {c->dec_always, c->xchg, c->scache, c->scache_back, c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->cdf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount, c->wslots[0], c->wslots[1],
                     c->d_colptr, c->run_params, c->d_tape, c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp,
                     c->vscratch, c->xscratch, c->xp, c->comb, c->anc_out, c->xbuf, c->d_comp, c->d_ctape, c->d_prog};
     for (void* p : bufs)
@@ -281,8 +427,21 @@ static int resolve_decisions(wsmc_ctx* c) {
         c->last_ess = d.ess;
         c->resampled = d.resampled;
         if (d.resampled) c->n_resamples += 1;
+        if (i < (int)c->dec_epochs.size()) {   // the lazy log entry of this Resample
+            const int64_t e = c->dec_epochs[i];
+            if (e >= c->log_base && e - c->log_base < (int64_t)c->alog.size()) {
+                AncRow& r = c->alog[(size_t)(e - c->log_base)];
+                r.known = d.resampled;
+                if (d.resampled) {
+                    c->anc_last = r.anc;
+                    c->anc_last_epoch = e;
+                }
+            }
+        }
     }
     c->dec_pending = 0;
+    c->dec_epochs.clear();
+    gc_log(c);
     return WSMC_OK;
 }
 
@@ -366,6 +525,14 @@ int wsmc_comm_init_host(wsmc_ctx* c, wsmc_exchange_fn exchange, void* user, int3
 int wsmc_comm_set_shard_mode(wsmc_ctx* c, int32_t mode) {
     CHECK_CTX(c);
     if (mode != WSMC_SHARD_ISLAND && mode != WSMC_SHARD_EXACT) return fail(WSMC_EARG, "unknown shard mode");
+    // exact shards move every column between ranks at each Resample: the store stays eager
+    if (mode == WSMC_SHARD_EXACT) {
+        if (int r = materialize_all(c)) return r;
+        c->lazy = false;
+    } else {
+        const char* eg = getenv("WSMC_EAGER_GATHER");
+        c->lazy = !(eg && atoi(eg) != 0);
+    }
     c->shard_mode = mode;
     return WSMC_OK;
 }
@@ -388,6 +555,7 @@ int wsmc_col_create(wsmc_ctx* c, const char* name, int32_t dim, int32_t* col_id)
     WSMC_HIP(hipMalloc(&col.front, sizeof(double) * dim * c->N));
     WSMC_HIP(hipMalloc(&col.back, sizeof(double) * dim * c->N));
     WSMC_HIP(hipMemsetAsync(col.front, 0, sizeof(double) * dim * c->N, c->stream));
+    col.epoch = c->epoch;   // zeros, current
     c->cols.push_back(col);
     c->colptr_dirty = true;
     *col_id = (int32_t)(c->cols.size() - 1);
@@ -421,6 +589,7 @@ int wsmc_col_info(wsmc_ctx* c, int32_t col, char* buf, int32_t len, int32_t* dim
 int wsmc_col_download(wsmc_ctx* c, int32_t col, double* host) {
     CHECK_CTX(c);
     if (!valid_col(c, col) || !host) return fail(WSMC_EARG, "bad column or null buffer");
+    if (int r = need_cols(c, {col})) return r;
     WSMC_HIP(hipMemcpyAsync(host, c->cols[col].front, sizeof(double) * c->cols[col].dim * c->N,
                             hipMemcpyDeviceToHost, c->stream));
     WSMC_HIP(hipStreamSynchronize(c->stream));
@@ -431,6 +600,7 @@ int wsmc_col_upload(wsmc_ctx* c, int32_t col, const double* host) {
     CHECK_CTX(c);
     if (!valid_col(c, col) || !host) return fail(WSMC_EARG, "bad column or null buffer");
     scores_touch(c, col);
+    wrote_col(c, col);
     WSMC_HIP(hipMemcpyAsync(c->cols[col].front, host, sizeof(double) * c->cols[col].dim * c->N,
                             hipMemcpyHostToDevice, c->stream));
     WSMC_HIP(hipStreamSynchronize(c->stream));
@@ -439,6 +609,8 @@ int wsmc_col_upload(wsmc_ctx* c, int32_t col, const double* host) {
 
 int wsmc_col_device_ptr(wsmc_ctx* c, int32_t col, double** dptr) {
     if (!c || !valid_col(c, col) || !dptr) return fail(WSMC_EARG, "bad column");
+    WSMC_HIP(hipSetDevice(c->device));
+    if (int r = need_cols(c, {col})) return r;
     *dptr = c->cols[col].front;
     return WSMC_OK;
 }
@@ -448,10 +620,44 @@ int wsmc_store_resample(wsmc_ctx* c, const int32_t* idx) {
     if (!idx) return fail(WSMC_EARG, "null indices");
     for (int64_t i = 0; i < c->N; ++i)
         if (idx[i] < 0 || idx[i] >= c->N) return fail(WSMC_EARG, "index out of range");
-    WSMC_HIP(hipMemcpyAsync(c->anc, idx, sizeof(int32_t) * c->N, hipMemcpyHostToDevice, c->stream));
-    int r = gather_all_columns(c);
-    if (r) return r;
+    // logged like a Resample that resampled (its decision: always)
+    AncRow row;
+    row.anc = c->anc;
+    int r;
+    if (c->lazy && (r = acquire_row(c, &row))) return r;
+    WSMC_HIP(hipMemcpyAsync(row.anc, idx, sizeof(int32_t) * c->N, hipMemcpyHostToDevice, c->stream));
+    if (c->lazy)
+        WSMC_HIP(hipMemcpyAsync(row.dec, c->dec_always, sizeof(Decision), hipMemcpyDeviceToDevice, c->stream));
+    row.known = 1;
+    if ((r = store_resample_row(c, row, nullptr, nullptr))) return r;
+    c->anc_last = row.anc;
+    c->anc_last_epoch = c->lazy ? c->epoch - 1 : -1;
     WSMC_HIP(hipStreamSynchronize(c->stream));
+    return WSMC_OK;
+}
+
+static bool exact_mode(const wsmc_ctx* c);
+int wsmc_store_set_lazy(wsmc_ctx* c, int32_t lazy) {
+    CHECK_CTX(c);
+    if (!lazy || exact_mode(c)) {
+        if (int r = resolve_decisions(c)) return r;
+        if (int r = materialize_all(c)) return r;
+        c->lazy = false;
+        gc_log(c);
+        return WSMC_OK;
+    }
+    c->lazy = true;
+    return WSMC_OK;
+}
+
+int wsmc_store_info(wsmc_ctx* c, int64_t* log_entries, int32_t* stale_columns) {
+    if (!c) return fail(WSMC_EARG, "null context");
+    if (log_entries) *log_entries = (int64_t)c->alog.size();
+    if (stale_columns) {
+        int32_t n = 0;
+        for (const auto& col : c->cols) n += col.epoch < c->epoch ? 1 : 0;
+        *stale_columns = n;
+    }
     return WSMC_OK;
 }
 
@@ -916,11 +1122,14 @@ static int adopt_global_max(wsmc_ctx* c) {
 int wsmc_weighted_moments(wsmc_ctx* c, const wsmc_operand* exprs, int32_t d, double* mean, double* cov) {
     CHECK_CTX(c);
     if (!exprs || !mean || d < 1 || d > 4) return fail(WSMC_EARG, "need 1..4 expressions and a mean buffer");
+    std::vector<int32_t> reads;
     for (int k = 0; k < d; ++k) {
         int r = check_operand(c, exprs[k]);
         if (r) return r;
+        cols_of(exprs[k], reads);
     }
-    int r = upload_colptr(c);
+    int r = need_cols(c, reads);
+    if (!r) r = upload_colptr(c);
     if (r) return r;
     wsmc_operand ex[4];
     for (int k = 0; k < 4; ++k) ex[k] = exprs[k < d ? k : 0];
@@ -994,6 +1203,7 @@ int wsmc_col_minmax(wsmc_ctx* c, int32_t col, int32_t comp, double* mn, double* 
     if (col < 0 || col >= (int32_t)c->cols.size()) return fail(WSMC_EARG, "bad column");
     if (comp < 0 || comp >= c->cols[col].dim) return fail(WSMC_EARG, "bad component");
     if (!mn || !mx) return fail(WSMC_EARG, "null output");
+    if (int r = need_cols(c, {col})) return r;
     WSMC_HIP(hipMemsetAsync(c->mslots, 0, sizeof(MaxSlots), c->stream));
     WSMC_HIP(launch_minmax(c->stream, c->cols[col].front + (int64_t)comp * c->N, c->N, c->mslots));
     MaxSlots h;
@@ -1364,6 +1574,7 @@ int wsmc_col_gather_rows(wsmc_ctx* c, int32_t col, const int64_t* idx, int64_t n
     if (n == 0) return WSMC_OK;
     for (int64_t j = 0; j < n; ++j)
         if (idx[j] < 0 || idx[j] >= c->N) return fail(WSMC_EARG, "row index out of range");
+    if (int r = need_cols(c, {col})) return r;
     const int dim = c->cols[col].dim;
     int64_t* d = nullptr;
     double* o = nullptr;
@@ -1412,9 +1623,13 @@ int wsmc_assign(wsmc_ctx* c, int32_t out, const wsmc_operand* expr) {
         int r = check_operand(c, expr[k]);
         if (r) return r;
     }
-    int r = upload_colptr(c);
+    std::vector<int32_t> reads;
+    for (int k = 0; k < dim; ++k) cols_of(expr[k], reads);
+    int r = need_cols(c, reads);
+    if (!r) r = upload_colptr(c);
     if (r) return r;
     scores_touch(c, out);
+    wrote_col(c, out);
     WSMC_HIP(launch_assign(c->stream, c->cols[out].front, dim, expr, c->d_colptr, c->N));
     c->depth += 1;
     return WSMC_OK;
@@ -1436,9 +1651,13 @@ int wsmc_sample(wsmc_ctx* c, int32_t out, const wsmc_dist* d) {
     int r = check_dist(c, *d);
     if (r) return r;
     if (d->dim != c->cols[out].dim) return fail(WSMC_EARG, "dist dim != column dim");
+    std::vector<int32_t> reads;
+    cols_of(*d, reads);
+    if ((r = need_cols(c, reads))) return r;
     if ((r = upload_colptr(c))) return r;
     const uint64_t op = c->op++;
     scores_touch(c, out);
+    wrote_col(c, out);
     WSMC_HIP(launch_sample(c->stream, c->cols[out].front, d->dim, *d, c->seed, op, c->goff, c->d_colptr, c->N));
     push_sample_term(c, out, *d);
     c->depth += 1;
@@ -1452,9 +1671,14 @@ int wsmc_sample_importance(wsmc_ctx* c, int32_t out, const wsmc_dist* prop, cons
     if (!r) r = check_dist(c, *targ);
     if (r) return r;
     if (prop->dim != c->cols[out].dim || targ->dim != c->cols[out].dim) return fail(WSMC_EARG, "dim mismatch");
+    std::vector<int32_t> reads;
+    cols_of(*prop, reads);
+    cols_of(*targ, reads);
+    if ((r = need_cols(c, reads))) return r;
     if ((r = upload_colptr(c))) return r;
     const uint64_t op = c->op++;
     scores_touch(c, out);
+    wrote_col(c, out);
     c->wseq += 1;
     WSMC_HIP(launch_sample_importance(c->stream, c->cols[out].front, prop->dim, *prop, *targ, c->w, c->seed, op,
                                       c->goff, c->d_colptr, c->N));
@@ -1478,6 +1702,9 @@ static int weigh(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x, int kin
     }
     t.kind = kind;
     t.depth = c->depth;
+    std::vector<int32_t> reads;
+    cols_of(t, reads);
+    if ((r = need_cols(c, reads))) return r;
     if ((r = upload_colptr(c))) return r;
     const int wb = c->wnext;
     WSMC_HIP(launch_weigh(c->stream, t, c->w, c->d_colptr, c->N, c->wslots[wb], c->wslots[wb ^ 1]));
@@ -1523,39 +1750,52 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
         if (ess_out) *ess_out = d.ess;
         return WSMC_OK;
     }
+    // the ancestors and the decision land in a log row (lazy genealogy) or in c->anc / c->dec
+    AncRow row;
+    row.anc = c->anc;
+    row.dec = c->dec;
+    int r;
+    if (c->lazy && (r = acquire_row(c, &row))) return r;
     const FillPlan plan = fill_plan(c, scheme, op, nullptr);
     // the last weight write was an Observe / Weight: its kernel left the max in wslots
     const bool pre = c->wmax_buf >= 0 && c->wmax_seq == c->wseq;
     MaxSlots* ms = pre ? c->wslots[c->wmax_buf] : c->mslots;
-    int r = enqueue_resample_stats(c, c->w, ms, c->rec, ess_min, c->dec, !pre, plan);
-    if (r) return r;
+    if ((r = enqueue_resample_stats(c, c->w, ms, c->rec, ess_min, row.dec, !pre, plan))) return r;
     if (scheme == WSMC_RESAMPLE_MULTINOMIAL)
-        WSMC_HIP(launch_rs_multinomial(c->stream, c->N, c->rec + c->rank, c->dec, plan, c->tileOff, c->cdf,
-                                       multi_esum(c), multi_ebuf(c), c->anc));
+        WSMC_HIP(launch_rs_multinomial(c->stream, c->N, c->rec + c->rank, row.dec, plan, c->tileOff, c->cdf,
+                                       multi_esum(c), multi_ebuf(c), row.anc));
     else
-        WSMC_HIP(launch_rs_scan(c->stream, c->N, c->rec + c->rank, c->dec, plan, c->tileOff, c->qbuf, c->anc));
+        WSMC_HIP(launch_rs_scan(c->stream, c->N, c->rec + c->rank, row.dec, plan, c->tileOff, c->qbuf, row.anc));
     if (async) {
         if (c->dec_pending == kDecRing)
             if ((r = resolve_decisions(c))) return r;
-        WSMC_HIP(hipMemcpyAsync(&c->dec_ring[c->dec_pending], c->dec, sizeof(Decision), hipMemcpyDeviceToHost,
+        WSMC_HIP(hipMemcpyAsync(&c->dec_ring[c->dec_pending], row.dec, sizeof(Decision), hipMemcpyDeviceToHost,
                                 c->stream));
         c->dec_pending += 1;
+        if (c->lazy) c->dec_epochs.push_back(c->epoch);   // the log entry this Resample becomes
         c->wseq += 1;
-        if ((r = gather_all_columns(c, c->dec, c->w))) return r;   // gated gathers + weight reset
+        if ((r = store_resample_row(c, row, row.dec, c->w))) return r;   // gated gathers + weight reset
         c->weights_changed = 0;
         return WSMC_OK;
     }
     Decision* hd = reinterpret_cast<Decision*>(c->pinned);
-    WSMC_HIP(hipMemcpyAsync(hd, c->dec, sizeof(Decision), hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipMemcpyAsync(hd, row.dec, sizeof(Decision), hipMemcpyDeviceToHost, c->stream));
     WSMC_HIP(hipStreamSynchronize(c->stream));
     const Decision d = *hd;
     c->last_ess = d.ess;
     if (d.resampled) {
         c->wseq += 1;
-        if ((r = gather_all_columns(c, c->dec, c->w))) return r;   // gathers + weight reset
+        row.known = 1;
+        if ((r = store_resample_row(c, row, row.dec, c->w))) return r;   // gathers + weight reset
+        if (c->lazy) {
+            c->anc_last = row.anc;
+            c->anc_last_epoch = c->epoch - 1;
+            gc_log(c);
+        }
         c->resampled = 1;
         c->n_resamples += 1;
     } else {
+        if (c->lazy) c->row_pool.push_back(row);   // nothing to log: no particle moved
         c->resampled = 0;
     }
     c->weights_changed = 0;
@@ -1567,7 +1807,9 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
 int wsmc_last_ancestors(wsmc_ctx* c, int32_t* host) {
     CHECK_CTX(c);
     if (!host) return fail(WSMC_EARG, "null buffer");
-    WSMC_HIP(hipMemcpyAsync(host, c->anc, sizeof(int32_t) * c->N, hipMemcpyDeviceToHost, c->stream));
+    if (int r = resolve_decisions(c)) return r;   // which pending Resample resampled last
+    const int32_t* src = c->anc_last ? c->anc_last : c->anc;
+    WSMC_HIP(hipMemcpyAsync(host, src, sizeof(int32_t) * c->N, hipMemcpyDeviceToHost, c->stream));
     WSMC_HIP(hipStreamSynchronize(c->stream));
     return WSMC_OK;
 }
@@ -1575,7 +1817,10 @@ int wsmc_last_ancestors(wsmc_ctx* c, int32_t* host) {
 int wsmc_score(wsmc_ctx* c, int32_t depth, double* host) {
     CHECK_CTX(c);
     if (!host) return fail(WSMC_EARG, "null buffer");
-    int r = upload_colptr(c);
+    std::vector<int32_t> reads;
+    for (const auto& t : c->tape) cols_of(t, reads);
+    int r = need_cols(c, reads);
+    if (!r) r = upload_colptr(c);
     if (!r) r = upload_tape(c);
     if (r) return r;
     WSMC_HIP(launch_score(c->stream, c->d_tape, (int32_t)c->tape.size(), depth, c->d_colptr, c->N, c->tmp));
@@ -1661,6 +1906,7 @@ int wsmc_marginal_diversity(wsmc_ctx* c, const int32_t* targets, int32_t d, doub
     for (int k = 0; k < d; ++k)
         if (!valid_col(c, targets[k]) || c->cols[targets[k]].dim != 1)
             return fail(WSMC_EARG, "diversity targets must be scalar columns");
+    if (int r = need_cols(c, std::vector<int32_t>(targets, targets + d))) return r;
     unsigned long long* kin = reinterpret_cast<unsigned long long*>(c->tmp);
     unsigned long long* kout = kin + c->N;
     size_t tbytes = 0;
@@ -1872,7 +2118,11 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         if (std::isfinite(l[k]) || std::isfinite(h[k])) bounded = true;
     }
     if (!lo && !hi) bounded = false;
-    int r = upload_colptr(c);
+    // the move reads its targets and every column of the score tape, and rewrites the targets
+    std::vector<int32_t> reads(targets, targets + d);
+    for (const auto& t : c->tape) cols_of(t, reads);
+    int r = need_cols(c, reads);
+    if (!r) r = upload_colptr(c);
     if (!r) r = upload_tape(c);
     if (r) return r;
     WSMC_HIP(hipMemsetAsync(c->dflag, 0, sizeof(int32_t) * 4, c->stream));
@@ -2426,8 +2676,19 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         if (hdec[t].resampled) {
             WSMC_HIP(hipMemcpyAsync(c->anc, c->anc_log + (size_t)(t - 1) * anc_stride(c->N), sizeof(int32_t) * c->N,
                                     hipMemcpyDeviceToDevice, c->stream));
+            c->anc_last = nullptr;
+            c->anc_last_epoch = -1;
             break;
         }
+    // the run wrote its columns in full (traced back): current
+    if (p.keep) {
+        for (int t = 1; t <= T + 1; ++t) wrote_col(c, p.xcols[t]);
+    } else {
+        wrote_col(c, p.colx);
+    }
+    wrote_col(c, p.colv);
+    wrote_col(c, p.coldv);
+    gc_log(c);
 
     // bookkeeping identical to issuing the statements one by one
     int32_t nres = 0;

@@ -5,6 +5,7 @@
 #include <rccl/rccl.h>
 
 #include <cstdint>
+#include <deque>
 #include <string>
 #include <vector>
 
@@ -77,8 +78,36 @@ struct ExactPlan {
 struct Column {
     std::string name;
     int32_t dim = 1;
-    double* front = nullptr;   // live data (what getcol returns)
+    double* front = nullptr;   // live data (what getcol returns) as of `epoch`
     double* back = nullptr;    // ping-pong / scratch buffer
+    int64_t epoch = 0;         // lazy genealogy: front holds the values before log entry `epoch`
+    int64_t touch = -1;        // the last epoch in which an operator read or wrote the column
+};
+
+// Lazy genealogy of the generic store (ColumnStore.resample!, src/stores.jl:105-128): a
+// Resample records its ancestor row and its device-side decision as one log entry; only the
+// columns an operator touched since the previous Resample are gathered at once. A column
+// left behind (history such as x{t}) is brought up to date by one trace over the log when
+// something reads it — bit-identical, since a gather is a copy.
+struct AncRow {
+    int32_t* anc = nullptr;        // [N] ancestors of the entry
+    Decision* dec = nullptr;       // the entry's decision (gates the trace: identity if it did not resample)
+    int32_t known = -1;            // host knowledge of dec->resampled: -1 pending (asynchronous Resample)
+};
+constexpr int kTraceLev = 96;      // log entries one trace launch walks
+constexpr int kTraceCols = 48;     // column components one trace launch writes
+struct TraceComp {
+    double* dst;
+    const double* src;
+    int32_t level;                 // entries to apply (1 = the newest only), ascending in the table
+};
+struct TraceArgs {
+    const int32_t* rows[kTraceLev];      // rows[0] = the newest entry
+    const Decision* decs[kTraceLev];
+    TraceComp comp[kTraceCols];
+    int32_t nlev, ncomp;
+    const int32_t* a_in;                 // composed indices before rows[0] (null = identity)
+    int32_t* a_out;                      // composed indices after the last row (null = not kept)
 };
 
 // cached HIP graph of one fused-run configuration
@@ -174,6 +203,16 @@ struct wsmc_ctx {
     void* pinned = nullptr;                 // 4 KB pinned staging
     int64_t ntiles = 0;      // canonical-sum tiles (2048)
     int64_t nrstiles = 0;    // resample tiles (1024)
+
+    // lazy genealogy (AncRow): entries for epochs [log_base, epoch)
+    bool lazy = true;
+    int64_t epoch = 0, log_base = 0;
+    std::deque<wsmc::AncRow> alog;
+    std::vector<wsmc::AncRow> row_pool;     // free rows (ancestors + decision)
+    std::vector<int64_t> dec_epochs;        // log entry of each pending asynchronous decision
+    int32_t* anc_last = nullptr;            // wsmc_last_ancestors: newest row known to have resampled
+    int64_t anc_last_epoch = -1;
+    wsmc::Decision* dec_always = nullptr;   // [1] resampled = 1 (explicit resample!(store, idx))
 
     // fused runner state
     int32_t T_alloc = 0;
@@ -349,6 +388,7 @@ hipError_t launch_rs_fill_fused(hipStream_t s, int64_t N, const FillPlan& plan, 
                                 const unsigned long long* qbuf, int32_t* anc, hipEvent_t e0 = nullptr,
                                 hipEvent_t e1 = nullptr);
 hipError_t launch_gather(hipStream_t s, double* dst, const double* src, const int32_t* anc, int64_t N);
+hipError_t launch_lazy_trace(hipStream_t s, const TraceArgs& a, int64_t N);
 // up to kGatherSet (dst, src) column-component pairs of one Resample, passed by value
 constexpr int kGatherSet = 48;
 struct GatherSet {

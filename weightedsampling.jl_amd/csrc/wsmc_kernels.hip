@@ -1272,6 +1272,23 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
     }
 }
 
+// Lazy genealogy: bring stale columns up to date through the Resample log (ColumnStore's
+// per-resample gathers, src/stores.jl:105-128, composed). Per particle i: a = i, then for
+// each entry from the newest back (a = anc[a] where that Resample resampled) the columns
+// whose values predate the entries applied so far read src[a]. Rows are monotone
+// (stratified / systematic / sorted multinomial), so the gathers stay nearly coalesced.
+__global__ __launch_bounds__(kBlock) void k_lazy_trace(TraceArgs t, int64_t N) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= N) return;
+    int64_t a = t.a_in ? t.a_in[i] : i;
+    int k = 0;
+    for (int lev = 0; lev < t.nlev; ++lev) {
+        if (t.decs[lev]->resampled) a = t.rows[lev][a];
+        for (; k < t.ncomp && t.comp[k].level == lev + 1; ++k) t.comp[k].dst[i] = t.comp[k].src[a];
+    }
+    if (t.a_out) t.a_out[i] = (int32_t)a;
+}
+
 __global__ __launch_bounds__(kBlock) void k_gather(double* __restrict__ dst, const double* __restrict__ src,
                                                    const int32_t* __restrict__ anc, int64_t N) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -1895,6 +1912,10 @@ static hipError_t launch_timed(K kernel, dim3 grid, dim3 block, hipStream_t s, h
     return hipGetLastError();
 }
 
+hipError_t launch_lazy_trace(hipStream_t s, const TraceArgs& a, int64_t N) {
+    hipLaunchKernelGGL(k_lazy_trace, grid_for(N), dim3(kBlock), 0, s, a, N);
+    return hipGetLastError();
+}
 hipError_t launch_rs_max(hipStream_t s, const double* w, int64_t N, MaxSlots* ms) {
     int64_t nb = (N + kBlock * 4 - 1) / (kBlock * 4);
     if (nb > 2048) nb = 2048;

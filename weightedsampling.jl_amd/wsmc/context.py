@@ -145,6 +145,16 @@ class Context:
         idx = np.ascontiguousarray(np.asarray(indices, dtype=np.int32))
         check(self._L.wsmc_store_resample(self._h, idx.ctypes.data_as(_I32P)))
 
+    def store_set_lazy(self, lazy: bool) -> None:
+        """Lazy genealogy (default) or the eager ColumnStore gather of every column."""
+        check(self._L.wsmc_store_set_lazy(self._h, 1 if lazy else 0))
+
+    def store_info(self) -> dict:
+        e = C.c_int64()
+        st = C.c_int32()
+        check(self._L.wsmc_store_info(self._h, C.byref(e), C.byref(st)))
+        return {"log_entries": e.value, "stale_columns": st.value}
+
     # ---- weights / state ----
     def weights_download(self) -> np.ndarray:
         a = np.empty(self.n)

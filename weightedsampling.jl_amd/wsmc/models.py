@@ -38,8 +38,10 @@ def _const(vals):
 
 # ---------------------------------------------------------------------------------------
 def ssm2d_statements(ctx, obs, x0=(0.0, 0.0), v0=(1.0, 0.0), q_var=0.1, r_var=0.5,
-                     ess_perc_min=0.5, scheme=abi.RESAMPLE_STRATIFIED):
-    """examples/2D_ssm.jl:7-17 (Σ's are covariances: 0.1·I₂ and 0.5·I₂)."""
+                     ess_perc_min=0.5, scheme=abi.RESAMPLE_STRATIFIED, wait=True):
+    """examples/2D_ssm.jl:7-17 (Σ's are covariances: 0.1·I₂ and 0.5·I₂), one C-ABI call per
+    statement. The model has no `if resampled`: with wait=False no Resample returns its flag
+    (the decisions stay on the device) and the function returns None."""
     R = resolver(ctx)
     obs = np.asarray(obs, dtype=float).reshape(-1, 2)
     cx1 = ctx.col_create("x_1", 2)
@@ -48,18 +50,23 @@ def ssm2d_statements(ctx, obs, x0=(0.0, 0.0), v0=(1.0, 0.0), q_var=0.1, r_var=0.
     ctx.assign(cv, _const(v0))                        # v .= [1.0, 0.0]
     I2 = np.eye(2)
     resampled = []
+    cdv, v_next = -1, None
+    dv_dist = MvNormal([0.0, 0.0], q_var * I2).dist(R)                      # the loop's kernels, built once
     for t, o in enumerate(obs, start=1):
         xt, xn = f"x_{t}", f"x_{t + 1}"
         cxn = ctx.col_create(xn, 2)
+        if t == 1:   # @model's column order: x_1, v, x_2, dv, x_3, ...
+            cdv = ctx.col_create("dv", 2)
+            v_next = value_operands(Col("v") + Col("dv"), 2, R)
         ctx.assign(cxn, value_operands(Col(xt) + Col("v"), 2, R))            # x{t+1} .= x{t} + v
-        cdv = ctx.col_create("dv", 2)
-        ctx.sample(cdv, MvNormal([0.0, 0.0], q_var * I2).dist(R))           # dv ~ MvNormal(0, 0.1 I)
-        ctx.resample(ess_perc_min, scheme)                                  # auto-inserted (no-op)
-        ctx.assign(cv, value_operands(Col("v") + Col("dv"), 2, R))          # v .= v + dv
+        ctx.sample(cdv, dv_dist)                                            # dv ~ MvNormal(0, 0.1 I)
+        ctx.resample(ess_perc_min, scheme, wait=wait)                       # auto-inserted (no-op)
+        ctx.assign(cv, v_next)                                              # v .= v + dv
         ctx.observe(MvNormal(Col(xn), r_var * I2).dist(R), _const(o))       # o => MvNormal(x{t+1}, 0.5 I)
-        rs, _ = ctx.resample(ess_perc_min, scheme)
-        resampled.append(rs)
-    return resampled
+        rs = ctx.resample(ess_perc_min, scheme, wait=wait)
+        if wait:
+            resampled.append(rs[0])
+    return resampled if wait else None
 
 
 def ssm1d_statements(ctx, obs, q_sd=0.1, r_sd=1.0, ess_perc_min=0.5, scheme=abi.RESAMPLE_STRATIFIED):
