@@ -74,6 +74,12 @@ def parse():
     # diagnostics: one rank with a one-rank RCCL communicator, so the run takes the sharded
     # (eager, RCCL all-gather per step) path on one GPU — the multi-GPU step cost minus xGMI
     ap.add_argument("--rccl-one-rank", action="store_true")
+    # the same workload through the generic statement operators (one C-ABI call per statement,
+    # the path a Julia run! on HipColumnStore takes) instead of the fused runner; with
+    # --eager-store the store gathers every column at every resample, as the reference's
+    # ColumnStore does (src/stores.jl:105-128)
+    ap.add_argument("--statements", action="store_true")
+    ap.add_argument("--eager-store", action="store_true")
     return ap.parse_args()
 
 
@@ -222,9 +228,20 @@ def main():
         if comm is not None:
             comm.barrier()
 
-    def one_run():
-        return ctx.ssm2d_run(obs[:T], ess_perc_min=args.ess, scheme=scheme, keep_history=not args.no_history,
-                             want_evidence=False)
+    if args.statements:
+        if args.eager_store:
+            ctx.store_set_lazy(False)
+
+        def one_run():
+            # run!(ssm(obs), state) statement by statement; no `if resampled` in the model, so
+            # no Resample returns its flag to the host. The history x_1..x_{T+1} is brought up
+            # to date at the end (one trace over the Resample log), as the fused run traces back.
+            wsmc.models.ssm2d_statements(ctx, obs[:T], ess_perc_min=args.ess, scheme=scheme, wait=False)
+            ctx.store_materialize()
+    else:
+        def one_run():
+            return ctx.ssm2d_run(obs[:T], ess_perc_min=args.ess, scheme=scheme,
+                                 keep_history=not args.no_history, want_evidence=False)
 
     for _ in range(args.warmup):
         one_run()
@@ -245,7 +262,7 @@ def main():
     # shards (their eager, host-driven run is not instrumented)
     prop_ms = red_ms = rs_ms = fin_ms = tot_ms = 0.0
     nres = 0
-    if not exact:
+    if not exact and not args.statements:
         ctx.set_timing(True)
         inst_runs = max(1, min(args.steps, 5))
         one_run()  # capture the instrumented graph
@@ -267,15 +284,17 @@ def main():
     forced = nres >= T - 1
     prop_bytes = N * (PROP_BYTES_FIRST + (T - 1) * PROP_BYTES_STEADY + PROP_BYTES_LAST_DV)
     prop_gbs = prop_bytes / (prop_ms * 1e-3) / 1e9 if prop_ms > 0 else None
-    traffic = None
-    tf = REPO / "profiles" / "pmc_propagate_bytes.json"
-    if tf.exists():
+    def pmc(name):   # PMC-measured bytes (profiles/), reported only for the N they were measured at
+        f = REPO / "profiles" / name
         try:
-            tj = json.loads(tf.read_text())
-            # measured for one configuration: reported only for that N
-            traffic = tj.get("bytes_per_launch") if tj.get("n_particles", N) == N else None
+            j = json.loads(f.read_text())
+            return j if j.get("n_particles", N) == N and j.get("T", T) == T else None
         except Exception:
-            traffic = None
+            return None
+    tj = pmc("pmc_propagate_bytes.json")
+    traffic = tj.get("bytes_per_launch") if tj else None
+    sj = pmc("pmc_step_bytes.json")
+    step_traffic = sj.get("bytes_per_particle_step") if sj and not args.statements else None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:   # the baseline is an N=1 figure
@@ -324,26 +343,40 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
+            "ms_per_step": ms_per_step,          # one bench step = one full T-step run
+            "ms_per_run": ms_per_step,
+            "us_per_filter_step": ms_per_step * 1e3 / T,
             "higher_is_better": True,
             "scaling": "strong" if args.global_particles > 0 else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: examples/2D_ssm.jl observation recurrence (numpy Philox seed 42)",
-            "config": {"workload": "2D SSM bootstrap filter (examples/2D_ssm.jl), BASELINE configs[1]",
+            "config": {"workload": "2D SSM bootstrap filter (examples/2D_ssm.jl), BASELINE configs[1]"
+                                   + (" through the generic statement operators (one C-ABI call per statement, "
+                                      + ("eager store: every column gathered at every resample)" if args.eager_store
+                                         else "lazy genealogy)") if args.statements else ""),
                        "n_particles_per_gpu": N, "global_particles": gN, "T": T,
                        "ess_perc_min": args.ess, "scheme": args.scheme, "keep_history": not args.no_history,
                        "parallelism": (f"{args.shard_mode}-shard x{world}"
                                        + (" (host exchange, test mode)" if args.exchange == "host" else ""))
                            if world > 1 else ("single GPU, one-rank RCCL communicator (diagnostic)"
                                               if args.rccl_one_rank else "single GPU")},
-            "roofline": {"bound": "hbm", "kernel": "k_ssm2d_prop (propagate+observe+max)",
-                         "achieved": prop_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": (prop_gbs / HBM_PEAK_GBS) if prop_gbs else None, "traffic": traffic,
-                         "algorithmic_bytes_per_run": prop_bytes, "avg_launch_us": prop_ms * 1e3 / T if prop_ms > 0 else None,
-                         "whole_step_GBs": value / world * STEP_BYTES / 1e9},
+            # the whole step against HBM — achieved = particle-steps/s per GPU x
+            # 104 algorithmic B (CDF materialisation and trace-back count as overhead); traffic =
+            # the PMC-measured HBM bytes per particle-step of every kernel of the run (trace-back
+            # included). The dominant kernel's own figure (HIP events on its dispatches) beside it.
+            "roofline": {"bound": "hbm", "achieved": value / world * STEP_BYTES / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": value / world * STEP_BYTES / 1e9 / HBM_PEAK_GBS,
+                         "traffic": step_traffic, "algorithmic_bytes_per_particle_step": STEP_BYTES,
+                         "definition": "whole step: particle-steps/s per GPU x 104 B / 8 TB/s (SURVEY.md 8d)",
+                         "dominant_kernel": None if args.statements else {
+                             "kernel": "k_ssm2d_prop (propagate+observe+max)", "achieved": prop_gbs,
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": (prop_gbs / HBM_PEAK_GBS) if prop_gbs else None, "traffic": traffic,
+                             "algorithmic_bytes_per_run": prop_bytes,
+                             "avg_launch_us": prop_ms * 1e3 / T if prop_ms > 0 else None}},
             "cpu_baseline": cpu,
-            "breakdown_ms_per_run": None if exact else {
+            "breakdown_ms_per_run": None if exact or args.statements else {
                 "propagate": prop_ms, "weight_stats": red_ms, "scan_ancestors": rs_ms,
                 "finalize_traceback": fin_ms, "instrumented_total": tot_ms,
                 "resamples_per_run": nres, "forced_every_step": forced},

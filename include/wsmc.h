@@ -182,6 +182,9 @@ int wsmc_store_resample(wsmc_ctx* ctx, const int32_t* host_indices);
  * bringing every column up to date); exact shards are always eager.
  * wsmc_store_info: log entries held and columns currently behind the log. */
 int wsmc_store_set_lazy(wsmc_ctx* ctx, int32_t lazy);
+/* bring every column up to date now (one trace over the log; what a DataFrame(state) export
+ * or a run's end needs), without a host copy */
+int wsmc_store_materialize(wsmc_ctx* ctx);
 int wsmc_store_info(wsmc_ctx* ctx, int64_t* log_entries, int32_t* stale_columns);
 
 /* ---- weights: SMCState.weights (src/types.jl:48-60) ------------------------- */

@@ -105,9 +105,11 @@ WSMC_HD double wsmc_dist_logpdf(const wsmc_dist* d, const double* x, double* con
     return wsmc_dist_logpdf_m(d, x, cols, N, i, ov, 0);
 }
 
-/* rand(D(args...)) for particle i (global RNG index idx) */
-WSMC_HD void wsmc_dist_sample(const wsmc_dist* d, double* x, uint64_t seed, uint64_t op, uint64_t idx,
-                              double* const* cols, int64_t N, int64_t i) {
+/* rand(D(args...)) for particle i (global RNG index idx). sd_pre: for an MvNormal whose
+ * variance operand is a constant, wsmc_sqrt of it evaluated once by the caller (the same
+ * function of the same bits, so the same result as evaluating it per particle); else null. */
+WSMC_HD void wsmc_dist_sample_m(const wsmc_dist* d, double* x, uint64_t seed, uint64_t op, uint64_t idx,
+                                double* const* cols, int64_t N, int64_t i, const double* sd_pre) {
     switch (d->family) {
         case WSMC_FAM_NORMAL: {
             double mu = wsmc_dist_mean(d, 0, cols, N, i, 0);
@@ -126,8 +128,7 @@ WSMC_HD void wsmc_dist_sample(const wsmc_dist* d, double* x, uint64_t seed, uint
             break;
         }
         default: {
-            double var = wsmc_operand_eval(&d->scale, cols, N, i, 0);
-            double sd = wsmc_sqrt(var);
+            double sd = sd_pre ? *sd_pre : wsmc_sqrt(wsmc_operand_eval(&d->scale, cols, N, i, 0));
             for (int k = 0; k < d->dim && k < 4; k += 2) {
                 double z0, z1;
                 wsmc_normal_pair(wsmc_rng_block(seed, op, idx, (uint32_t)(k >> 1)), &z0, &z1);
@@ -138,6 +139,13 @@ WSMC_HD void wsmc_dist_sample(const wsmc_dist* d, double* x, uint64_t seed, uint
         }
     }
 }
+
+WSMC_HD void wsmc_dist_sample(const wsmc_dist* d, double* x, uint64_t seed, uint64_t op, uint64_t idx,
+                              double* const* cols, int64_t N, int64_t i) {
+    wsmc_dist_sample_m(d, x, seed, op, idx, cols, N, i, 0);
+}
+/* the operand is a constant (reads no column) */
+WSMC_HD int wsmc_operand_is_const(const wsmc_operand* o) { return o->col[0] < 0 && o->col[1] < 0; }
 
 WSMC_HD double wsmc_term_logpdf_m(const wsmc_term* t, double* const* cols, int64_t N, int64_t i,
                                   const wsmc_override* ov, wsmc_logmemo* lm) {

@@ -48,13 +48,13 @@ def test_lazy_equals_eager_device_store(gpu_available):
 
 
 def test_lazy_log_stays_short_without_history(gpu_available):
-    """The LGSSM rebinds one column: every column is current after each Resample, so the log
-    keeps at most the newest row (last_ancestors) however long the run."""
+    """The LGSSM rebinds one column, read at every step: it is never more than one entry behind,
+    so the log keeps at most the newest row however long the run."""
     data = models.lgssm1d_data(60)
     g, o = wsmc.Context(2049, seed=3), Oracle(2049, seed=3)
     models.lgssm1d_statements(g, data, ess_perc_min=1.0, wait=False)
     models.lgssm1d_statements(o, data, ess_perc_min=1.0)
-    assert g.store_info()["stale_columns"] == 0
+    assert g.store_info()["stale_columns"] <= 1    # x, one entry behind the last Resample
     g.get_state()                                   # folds the pending decisions in
     assert g.store_info()["log_entries"] <= 1
     assert_same_state(g, o)
@@ -89,9 +89,9 @@ def test_lazy_explicit_store_resample(gpu_available):
     idx1 = rng.integers(0, N, N).astype(np.int32)
     idx2 = np.sort(rng.integers(0, N, N)).astype(np.int32)
     for ctx in (g, o):
-        ctx.store_resample(idx1)                   # both touched: gathered at once
-        ctx.col_upload(ctx.col_find("b"), np.ones(2 * N))
-        ctx.store_resample(idx2)                   # a untouched since the last one: left behind
-    assert g.store_info()["stale_columns"] == 1
+        ctx.store_resample(idx1)                   # both left behind (one log entry)
+        ctx.col_upload(ctx.col_find("b"), np.ones(2 * N))   # b rewritten: current again
+        ctx.store_resample(idx2)                   # a two entries behind, b one
+    assert g.store_info()["stale_columns"] == 2
     assert_same_state(g, o)
     np.testing.assert_array_equal(g.last_ancestors(), idx2)   # the last resample!'s indices

@@ -12,11 +12,14 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 echo smoke ok
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 cat $O/bench.json
+timeout -k 10 400 python bench.py --no-cpu-baseline --statements > $O/bench_statements.json 2> $O/bench_statements.err || { tail -20 $O/bench_statements.err; exit 1; }
+cat $O/bench_statements.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python bench.py --no-cpu-baseline > $O/stats.log 2>&1 || { tail -20 $O/stats.log; exit 1; }
 ARGS="--steps 2 --warmup 1 --no-cpu-baseline"
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- python bench.py $ARGS > $O/fetch.log 2>&1 || { tail -20 $O/fetch.log; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python bench.py $ARGS > $O/write.log 2>&1 || { tail -20 $O/write.log; exit 1; }
 python tools/summarize_pmc.py $O/pmc_summary.json $O/fetch $O/write > /dev/null
+python tools/pmc_step_bytes.py $O/pmc_summary.json 1000000 100 $O/pmc_step_bytes.json
 python - <<'PY'
 import csv, json
 for x in csv.DictReader(open('gpurun_out/round/stats/run_kernel_stats.csv')):

@@ -131,34 +131,35 @@ static int gather_columns(wsmc_ctx* c, const std::vector<int32_t>& which, const 
                           double* w_reset, int64_t to_epoch) {
     GatherSet gs;
     gs.n = 0;
+    gs.tab = c->d_colptr;   // the kernel moves each gathered column's table entry to its new front
     auto flush = [&](bool last) -> hipError_t {
         const hipError_t e = launch_resample_apply(c->stream, gs, anc, dec, last ? w_reset : nullptr, c->N);
         gs.n = 0;
         return e;
     };
-    auto add = [&](double* dst, const double* src) -> hipError_t {
+    auto add = [&](double* dst, const double* src, int32_t col) -> hipError_t {
         if (gs.n == kGatherSet) {
             const hipError_t e = flush(false);
             if (e != hipSuccess) return e;
         }
         gs.dst[gs.n] = dst;
         gs.src[gs.n] = src;
+        gs.col[gs.n] = col;
         gs.n += 1;
         return hipSuccess;
     };
     for (int32_t id : which) {
         Column& col = c->cols[id];
         for (int k = 0; k < col.dim; ++k)
-            WSMC_HIP(add(col.back + (int64_t)k * c->N, col.front + (int64_t)k * c->N));
+            WSMC_HIP(add(col.back + (int64_t)k * c->N, col.front + (int64_t)k * c->N, k == 0 ? id : -1));
         std::swap(col.front, col.back);
         col.epoch = to_epoch;
     }
     if (c->scache && c->scache_terms >= 0) {   // carried Move scores follow their particles
-        WSMC_HIP(add(c->scache_back, c->scache));
+        WSMC_HIP(add(c->scache_back, c->scache, -1));
         std::swap(c->scache, c->scache_back);
     }
     WSMC_HIP(flush(true));
-    c->colptr_dirty = true;
     return WSMC_OK;
 }
 
@@ -192,10 +193,14 @@ static void gc_log(wsmc_ctx* c) {
 // Bring every stale column to the current epoch: one walk over the log per particle, from
 // the newest entry back to the oldest a stale column needs (kTraceLev entries per launch,
 // the composed index carried between launches), each column read where its epoch is reached.
-static int materialize_all(wsmc_ctx* c) {
+static int materialize(wsmc_ctx* c, const std::vector<int32_t>* only) {
     std::vector<std::pair<int64_t, int32_t>> stale;   // (levels to apply, column)
+    std::vector<char> want(c->cols.size(), only ? 0 : 1);
+    if (only)
+        for (int32_t id : *only)
+            if (id >= 0 && id < (int32_t)c->cols.size()) want[id] = 1;
     for (int32_t id = 0; id < (int32_t)c->cols.size(); ++id)
-        if (c->cols[id].epoch < c->epoch) stale.emplace_back(c->epoch - c->cols[id].epoch, id);
+        if (want[id] && c->cols[id].epoch < c->epoch) stale.emplace_back(c->epoch - c->cols[id].epoch, id);
     if (stale.empty()) return WSMC_OK;
     std::sort(stale.begin(), stale.end());
     const int64_t maxlev = stale.back().first;
@@ -203,27 +208,41 @@ static int materialize_all(wsmc_ctx* c) {
     int32_t* scratch[2] = {reinterpret_cast<int32_t*>(c->tmp), reinterpret_cast<int32_t*>(c->tmp) + c->N};
     const int32_t* a_in = nullptr;
     size_t next = 0;
-    for (int64_t base = 0, pass = 0; base < maxlev; base += kTraceLev, ++pass) {
-        const int nl = (int)std::min<int64_t>(kTraceLev, maxlev - base);
+    // launches over consecutive level ranges, each walking its entries once and carrying the
+    // composed index to the next; a range ends at kTraceLev entries or where its columns'
+    // components would pass kTraceCols (a single level with more repeats its walk)
+    for (int64_t base = 0, pass = 0; base < maxlev; ++pass) {
+        int64_t hi = std::min<int64_t>(base + kTraceLev, maxlev);
+        size_t ncomp = 0, end = next;
+        while (end < stale.size() && stale[end].first <= hi) {
+            const int d = c->cols[stale[end].second].dim;
+            if (ncomp + d > (size_t)kTraceCols && ncomp > 0 && stale[end].first > stale[next].first) {
+                hi = stale[end].first - 1;   // close the range before this column's level
+                break;
+            }
+            ncomp += d;
+            ++end;
+        }
+        const int nl = (int)(hi - base);
         TraceArgs t{};
         t.nlev = nl;
+        t.tab = c->d_colptr;
         for (int j = 0; j < nl; ++j) {
             const AncRow& r = c->alog[(size_t)(c->epoch - 1 - (base + j) - c->log_base)];
             t.rows[j] = r.anc;
             t.decs[j] = r.dec;
         }
-        int32_t* a_out = base + nl < maxlev ? scratch[pass & 1] : nullptr;
+        int32_t* a_out = hi < maxlev ? scratch[pass & 1] : nullptr;
         t.a_in = a_in;
-        // this level range's columns, kTraceCols components a launch (each launch repeats the walk)
         std::vector<TraceComp> comps;
-        for (; next < stale.size() && stale[next].first <= base + nl; ++next) {
+        for (; next < stale.size() && stale[next].first <= hi; ++next) {
             Column& col = c->cols[stale[next].second];
             for (int k = 0; k < col.dim; ++k)
                 comps.push_back({col.back + (int64_t)k * c->N, col.front + (int64_t)k * c->N,
-                                 (int32_t)(stale[next].first - base)});
+                                 (int32_t)(stale[next].first - base), k == 0 ? stale[next].second : -1});
         }
         size_t done = 0;
-        do {
+        do {   // more than kTraceCols components in the range: repeat the walk per batch
             const size_t n = std::min<size_t>(kTraceCols, comps.size() - done);
             t.ncomp = (int32_t)n;
             for (size_t k = 0; k < n; ++k) t.comp[k] = comps[done + k];
@@ -232,18 +251,19 @@ static int materialize_all(wsmc_ctx* c) {
             WSMC_HIP(launch_lazy_trace(c->stream, t, c->N));
         } while (done < comps.size());
         a_in = a_out;
+        base = hi;
     }
     for (const auto& sc : stale) {
         Column& col = c->cols[sc.second];
         std::swap(col.front, col.back);
         col.epoch = c->epoch;
     }
-    c->colptr_dirty = true;
     gc_log(c);
     return WSMC_OK;
 }
-// an operator reads (or writes) these columns: mark them touched this epoch and bring any
-// stale one up to date first (all stale columns together: one walk of the log)
+static int materialize_all(wsmc_ctx* c) { return materialize(c, nullptr); }
+// an operator reads these columns: bring the stale ones among them up to date first (one
+// walk of the log for all of them); history the operator does not read stays behind
 static int need_cols(wsmc_ctx* c, const std::vector<int32_t>& ids) {
     bool stale = false;
     for (int32_t id : ids) {
@@ -251,7 +271,7 @@ static int need_cols(wsmc_ctx* c, const std::vector<int32_t>& ids) {
         c->cols[id].touch = c->epoch;
         stale |= c->cols[id].epoch < c->epoch;
     }
-    return stale ? materialize_all(c) : WSMC_OK;
+    return stale ? materialize(c, &ids) : WSMC_OK;
 }
 static void cols_of(const wsmc_operand& o, std::vector<int32_t>& v) {
     for (int k = 0; k < 2; ++k)
@@ -271,22 +291,19 @@ static void wrote_col(wsmc_ctx* c, int32_t id) {
     c->cols[id].touch = c->epoch;
 }
 // the ColumnStore.resample! of one Resample / resample!(store, idx) with ancestors `row`:
-// lazy — log the row, gather the columns touched since the previous Resample (the live
-// state), leave the rest for a later trace; eager (exact shards, WSMC_EAGER_GATHER) — all
+// lazy — log the row; every column is left behind until an operator reads it (the carried
+// Move scores and the weight reset are applied now); eager (exact shards, store_set_lazy(0)
+// or WSMC_EAGER_GATHER) — every column gathered, as ColumnStore does
 static int store_resample_row(wsmc_ctx* c, const AncRow& row, const Decision* dec, double* w_reset) {
     std::vector<int32_t> which;
-    for (int32_t id = 0; id < (int32_t)c->cols.size(); ++id) {
-        const Column& col = c->cols[id];
-        if (!c->lazy || (col.touch == c->epoch && col.epoch == c->epoch)) which.push_back(id);
-    }
     if (!c->lazy) {   // every column is current: no log entry
-        int r = gather_columns(c, which, row.anc, dec, w_reset, c->epoch);
-        return r;
+        for (int32_t id = 0; id < (int32_t)c->cols.size(); ++id) which.push_back(id);
+        return gather_columns(c, which, row.anc, dec, w_reset, c->epoch);
     }
     c->alog.push_back(row);
     c->epoch += 1;
-    int r = gather_columns(c, which, row.anc, dec, w_reset, c->epoch);
-    if (r) return r;
+    if (w_reset || (c->scache && c->scache_terms >= 0))
+        if (int r = gather_columns(c, which, row.anc, dec, w_reset, c->epoch)) return r;
     gc_log(c);
     return WSMC_OK;
 }
@@ -360,6 +377,8 @@ int wsmc_create(wsmc_ctx** out, int64_t n_particles, int32_t device, uint64_t se
 #undef ALLOC
     if (e == hipSuccess) e = hipHostMalloc(&c->pinned, 4096, hipHostMallocDefault);
     if (e == hipSuccess) e = hipHostMalloc((void**)&c->dec_ring, sizeof(Decision) * kDecRing, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->dec_ring_dev, c->dec_ring, 0);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&c->pinned_dev, c->pinned, 0);
     if (e == hipSuccess) e = hipMemsetAsync(c->w, 0, sizeof(double) * c->N, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->wslots[0], 0, sizeof(MaxSlots), c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->wslots[1], 0, sizeof(MaxSlots), c->stream);
@@ -648,6 +667,11 @@ int wsmc_store_set_lazy(wsmc_ctx* c, int32_t lazy) {
     }
     c->lazy = true;
     return WSMC_OK;
+}
+
+int wsmc_store_materialize(wsmc_ctx* c) {
+    CHECK_CTX(c);
+    return materialize_all(c);
 }
 
 int wsmc_store_info(wsmc_ctx* c, int64_t* log_entries, int32_t* stale_columns) {
@@ -1623,14 +1647,48 @@ int wsmc_assign(wsmc_ctx* c, int32_t out, const wsmc_operand* expr) {
         int r = check_operand(c, expr[k]);
         if (r) return r;
     }
-    std::vector<int32_t> reads;
-    for (int k = 0; k < dim; ++k) cols_of(expr[k], reads);
-    int r = need_cols(c, reads);
+    // operand columns one Resample behind are read through that Resample's ancestors inside
+    // the kernel (no materialising pass); any further behind are brought up to date first
+    std::vector<int32_t> deep;
+    for (int k = 0; k < dim; ++k)
+        for (int m = 0; m < 2; ++m) {
+            const int32_t id = expr[k].col[m];
+            if (id >= 0 && c->cols[id].epoch < c->epoch - 1) deep.push_back(id);
+        }
+    int r = deep.empty() ? WSMC_OK : materialize(c, &deep);
     if (!r) r = upload_colptr(c);
     if (r) return r;
+    Indirect ind;
+    bool out_read_behind = false;
+    for (int k = 0; k < dim; ++k)
+        for (int m = 0; m < 2; ++m) {
+            const int32_t id = expr[k].col[m];
+            if (id < 0) continue;
+            c->cols[id].touch = c->epoch;
+            if (c->cols[id].epoch < c->epoch) {
+                ind.mask |= 1u << (2 * k + m);
+                out_read_behind |= id == out;
+            }
+        }
+    if (ind.mask) {
+        const AncRow& nr = c->alog.back();   // entry epoch - 1 (kept alive by the stale column)
+        ind.row = nr.anc;
+        ind.dec = nr.dec;
+    }
+    std::vector<const double*> fronts(c->cols.size());
+    for (size_t k = 0; k < c->cols.size(); ++k) fronts[k] = c->cols[k].front;   // before any swap
+    ind.front = fronts.data();
+    double* dst = c->cols[out].front;
+    if (out_read_behind) {   // out read through the ancestors: write a fresh buffer (no read/write race)
+        dst = c->cols[out].back;
+        ind.tab_col = out;
+        ind.tab = c->d_colptr;
+        std::swap(c->cols[out].front, c->cols[out].back);
+    }
     scores_touch(c, out);
     wrote_col(c, out);
-    WSMC_HIP(launch_assign(c->stream, c->cols[out].front, dim, expr, c->d_colptr, c->N));
+    WSMC_HIP(launch_assign(c->stream, dst, dim, expr, c->d_colptr, c->N, ind));
+    gc_log(c);
     c->depth += 1;
     return WSMC_OK;
 }
@@ -1756,10 +1814,19 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
     row.dec = c->dec;
     int r;
     if (c->lazy && (r = acquire_row(c, &row))) return r;
-    const FillPlan plan = fill_plan(c, scheme, op, nullptr);
+    FillPlan plan = fill_plan(c, scheme, op, nullptr);
+    // stratified / systematic: the fill's tile blocks also reset the weights to the log-mean
+    const bool fill_resets = scheme != WSMC_RESAMPLE_MULTINOMIAL;
+    if (fill_resets) plan.w_reset = c->w;
     // the last weight write was an Observe / Weight: its kernel left the max in wslots
     const bool pre = c->wmax_buf >= 0 && c->wmax_seq == c->wseq;
     MaxSlots* ms = pre ? c->wslots[c->wmax_buf] : c->mslots;
+    // the fill kernel writes the decision straight into host-mapped memory (no copy op): the
+    // asynchronous ring's next slot, or the pinned staging the synchronous path reads
+    if (async && c->dec_pending == kDecRing)
+        if ((r = resolve_decisions(c))) return r;
+    Decision* hd = reinterpret_cast<Decision*>(c->pinned);
+    plan.host_dec = async ? c->dec_ring_dev + c->dec_pending : reinterpret_cast<Decision*>(c->pinned_dev);
     if ((r = enqueue_resample_stats(c, c->w, ms, c->rec, ess_min, row.dec, !pre, plan))) return r;
     if (scheme == WSMC_RESAMPLE_MULTINOMIAL)
         WSMC_HIP(launch_rs_multinomial(c->stream, c->N, c->rec + c->rank, row.dec, plan, c->tileOff, c->cdf,
@@ -1767,26 +1834,20 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
     else
         WSMC_HIP(launch_rs_scan(c->stream, c->N, c->rec + c->rank, row.dec, plan, c->tileOff, c->qbuf, row.anc));
     if (async) {
-        if (c->dec_pending == kDecRing)
-            if ((r = resolve_decisions(c))) return r;
-        WSMC_HIP(hipMemcpyAsync(&c->dec_ring[c->dec_pending], row.dec, sizeof(Decision), hipMemcpyDeviceToHost,
-                                c->stream));
         c->dec_pending += 1;
         if (c->lazy) c->dec_epochs.push_back(c->epoch);   // the log entry this Resample becomes
         c->wseq += 1;
-        if ((r = store_resample_row(c, row, row.dec, c->w))) return r;   // gated gathers + weight reset
+        if ((r = store_resample_row(c, row, row.dec, fill_resets ? nullptr : c->w))) return r;   // gated
         c->weights_changed = 0;
         return WSMC_OK;
     }
-    Decision* hd = reinterpret_cast<Decision*>(c->pinned);
-    WSMC_HIP(hipMemcpyAsync(hd, row.dec, sizeof(Decision), hipMemcpyDeviceToHost, c->stream));
     WSMC_HIP(hipStreamSynchronize(c->stream));
     const Decision d = *hd;
     c->last_ess = d.ess;
     if (d.resampled) {
         c->wseq += 1;
         row.known = 1;
-        if ((r = store_resample_row(c, row, row.dec, c->w))) return r;   // gathers + weight reset
+        if ((r = store_resample_row(c, row, row.dec, fill_resets ? nullptr : c->w))) return r;
         if (c->lazy) {
             c->anc_last = row.anc;
             c->anc_last_epoch = c->epoch - 1;

@@ -100,6 +100,8 @@ struct TraceComp {
     double* dst;
     const double* src;
     int32_t level;                 // entries to apply (1 = the newest only), ascending in the table
+    int32_t col;                   // column id when this is its component 0 (-1 otherwise): the
+                                   // device pointer table entry is set to dst (the new front)
 };
 struct TraceArgs {
     const int32_t* rows[kTraceLev];      // rows[0] = the newest entry
@@ -108,6 +110,7 @@ struct TraceArgs {
     int32_t nlev, ncomp;
     const int32_t* a_in;                 // composed indices before rows[0] (null = identity)
     int32_t* a_out;                      // composed indices after the last row (null = not kept)
+    double** tab;                        // the context's device column-pointer table
 };
 
 // cached HIP graph of one fused-run configuration
@@ -126,6 +129,8 @@ struct wsmc_ctx {
     // asynchronous Resamples (no flag requested): their decisions are copied into a pinned
     // ring and folded into resampled / n_resamples / last_ess at the next host read
     wsmc::Decision* dec_ring = nullptr;
+    wsmc::Decision* dec_ring_dev = nullptr;   // the ring as the device addresses it (host-mapped)
+    void* pinned_dev = nullptr;               // `pinned` as the device addresses it
     int dec_pending = 0;
     bool no_graph = false;   // a sharded run's capture failed once: run it eagerly
     // the max of the weights as the last Observe / Weight left them (double-buffered slots:
@@ -250,8 +255,17 @@ int fail(int code, const std::string& msg);
     } while (0)
 
 // ---- kernel launchers (wsmc_kernels.hip) -------------------------------------------
+// gather-on-read of operand columns one lazy-log entry behind (k_assign)
+struct Indirect {
+    const int32_t* row = nullptr;     // the newest log entry's ancestors
+    const Decision* dec = nullptr;    // its decision (identity when it did not resample)
+    uint32_t mask = 0;                // operand slots read through the row
+    int32_t tab_col = -1;             // column whose table entry becomes `out`
+    double** tab = nullptr;
+    const double* const* front = nullptr;   // host: every column's front buffer (resolves operands)
+};
 hipError_t launch_assign(hipStream_t s, double* out, int dim, const wsmc_operand* expr,
-                         double* const* cols, int64_t N);
+                         double* const* cols, int64_t N, const Indirect& ind);
 hipError_t launch_sample(hipStream_t s, double* out, int dim, const wsmc_dist& d, uint64_t seed,
                          uint64_t op, int64_t goff, double* const* cols, int64_t N);
 hipError_t launch_sample_importance(hipStream_t s, double* out, int dim, const wsmc_dist& prop,
@@ -274,6 +288,8 @@ struct FillPlan {          // ancestor-fill task planning (in the reduce kernel)
     const uint64_t* op_dev;
     int64_t slot_base;
     const ExactPlan* xp = nullptr;     // exact sharding: global Q / N / offsets, window-relative slots
+    double* w_reset = nullptr;         // generic Resample: the tile blocks reset the weights to dec->mean
+    Decision* host_dec = nullptr;      // generic Resample: the decision also written to host-mapped memory
 };
 hipError_t launch_rs_reduce(hipStream_t s, const MaxSlots* ms, const unsigned long long* tilep, int64_t N,
                             unsigned long long* tileOff, ShardRecord* rec, int decide_local, double ess_min,
@@ -394,6 +410,8 @@ constexpr int kGatherSet = 48;
 struct GatherSet {
     double* dst[kGatherSet];
     const double* src[kGatherSet];
+    int32_t col[kGatherSet];       // column id for its component 0 (-1 otherwise): table entry := dst
+    double** tab;                  // the device column-pointer table (null: not updated)
     int n;
 };
 hipError_t launch_resample_apply(hipStream_t s, const GatherSet& gs, const int32_t* anc, const Decision* dec,

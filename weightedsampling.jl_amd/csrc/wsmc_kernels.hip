@@ -172,16 +172,34 @@ __device__ __forceinline__ uint64_t op_eff(uint64_t op, const uint64_t* op_dev) 
 // ------------------------------------------------------------------------------------
 // elementwise operators: Assign / Sample / Observe / Weight
 // ------------------------------------------------------------------------------------
-struct AssignArgs { wsmc_operand e[4]; };
+// the expressions and their operand columns resolved by the host to component pointers
+// (p[k][m] = column col[m] of expression k at its component), so the kernel reads no table
+struct AssignArgs {
+    wsmc_operand e[4];
+    const double* p[4][2];
+};
 
+// Assign (src/transformers.jl:28-32). Gather-on-read (lazy genealogy): operand column slot
+// s = 2k + m (expression k, column m) with bit s of ind.mask reads its column one log entry
+// behind, through that entry's ancestors — ColumnStore's gather fused into the read. The
+// arithmetic is wsmc_operand_eval's, term for term. ind.tab_col >= 0: `out` is written to a
+// fresh buffer whose address goes into the device pointer table (the host swaps front/back).
 __global__ __launch_bounds__(kBlock) void k_assign(double* out, int dim, AssignArgs a,
-                                                   double* const* cols, int64_t N) {
+                                                   double* const* cols, int64_t N, Indirect ind) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= N) return;
+    if (i == 0 && ind.tab_col >= 0) ind.tab[ind.tab_col] = out;
+    const int64_t j = (ind.mask && (!ind.dec || ind.dec->resampled)) ? (int64_t)ind.row[i] : i;
     double x[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-        if (k < dim) x[k] = wsmc_operand_eval(&a.e[k], cols, N, i, nullptr);
+    for (int k = 0; k < 4; ++k) {
+        if (k >= dim) continue;
+        const wsmc_operand& o = a.e[k];
+        double v = o.c0;
+        if (o.col[0] >= 0) v = v + o.coef[0] * a.p[k][0][(ind.mask >> (2 * k)) & 1 ? j : i];
+        if (o.col[1] >= 0) v = v + o.coef[1] * a.p[k][1][(ind.mask >> (2 * k + 1)) & 1 ? j : i];
+        x[k] = v;
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k)
         if (k < dim) out[(int64_t)k * N + i] = x[k];
@@ -189,11 +207,13 @@ __global__ __launch_bounds__(kBlock) void k_assign(double* out, int dim, AssignA
 
 __global__ __launch_bounds__(kBlock) void k_sample(double* out, int dim, wsmc_dist d, uint64_t seed,
                                                    uint64_t op, int64_t goff, double* const* cols,
-                                                   int64_t N) {
+                                                   int64_t N, int has_sd, double sd) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= N) return;
     double x[4];
-    wsmc_dist_sample(&d, x, seed, op, (uint64_t)(goff + i), cols, N, i);
+    // has_sd: a constant MvNormal variance, its sqrt evaluated once by the host (the same
+    // restated function of the same bits each particle would evaluate)
+    wsmc_dist_sample_m(&d, x, seed, op, (uint64_t)(goff + i), cols, N, i, has_sd ? &sd : nullptr);
 #pragma unroll
     for (int k = 0; k < 4; ++k)
         if (k < dim) out[(int64_t)k * N + i] = x[k];
@@ -219,12 +239,15 @@ __global__ __launch_bounds__(kBlock) void k_sample_importance(double* out, int d
 // slots of `ms` (zero on entry), so the Resample that follows needs no max pass; block 0
 // zeroes `ms_next`, the slots the next launch will use (k_rs_max's encoding and slots)
 __global__ __launch_bounds__(kBlock) void k_weigh(wsmc_term t, double* w, double* const* cols, int64_t N,
-                                                  MaxSlots* ms, MaxSlots* ms_next) {
+                                                  MaxSlots* ms, MaxSlots* ms_next, wsmc_logmemo lm0) {
     __shared__ u64 lds[4];
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     u64 m = 0;
     if (i < N) {
-        const double v = w[i] + wsmc_term_logpdf(&t, cols, N, i, nullptr);
+        // lm0: a constant scale operand's log, evaluated once by the host and handed to the
+        // term through the fold's log memo (the same bits every particle would compute)
+        wsmc_logmemo lm = lm0;
+        const double v = w[i] + wsmc_term_logpdf_m(&t, cols, N, i, nullptr, &lm);
         w[i] = v;
         m = wsmc_ord_enc(v);
     }
@@ -798,6 +821,7 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_scan_t(int64_t N, const Shard
     __shared__ FillLds sh;
     const int t = blockIdx.x;
     const int ntiles = (int)((N + kRsTile - 1) / kRsTile);
+    if (t == 0 && threadIdx.x == 0 && plan.host_dec) *plan.host_dec = *dec;   // the host's copy
     const int rs = dec->resampled;
     if (!rs) return;
     // exact sharding: the global CDF (this shard's tiles offset by the lower ranks' Q)
@@ -806,6 +830,13 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_scan_t(int64_t N, const Shard
     const uint64_t opx = op_eff(plan.op, plan.op_dev);
     if (t < ntiles) {
         fill_chunk<MODE>(N, t, 0, Q, cb + tileOff[t], plan, opx, qbuf, anc, sh);
+        if (plan.w_reset) {   // the weights reset to the log-mean (the fill read q, not w)
+            const double mean = dec->mean;
+            for (int k = threadIdx.x; k < kRsTile; k += kScanBlock) {
+                const int64_t i = (int64_t)t * kRsTile + k;
+                if (i < N) plan.w_reset[i] = mean;
+            }
+        }
         return;
     }
     const int ntasks = dec->ntasks;
@@ -907,6 +938,7 @@ __global__ __launch_bounds__(kScanBlock) void k_multi_fill(int64_t N, const Shar
     __shared__ u64 s_w[kScanBlock / 64];
     __shared__ int64_t s_m[2];
     __shared__ u64 sC[kMultiStage];
+    if (blockIdx.x == 0 && threadIdx.x == 0 && plan.host_dec) *plan.host_dec = *dec;   // the host's copy
     if (!dec->resampled) return;
     const int th = threadIdx.x;
     const int64_t base = (int64_t)blockIdx.x * kRsTile;
@@ -1280,6 +1312,9 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
 __global__ __launch_bounds__(kBlock) void k_lazy_trace(TraceArgs t, int64_t N) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= N) return;
+    if (i == 0)   // the columns' new fronts into the device pointer table
+        for (int c = 0; c < t.ncomp; ++c)
+            if (t.comp[c].col >= 0) t.tab[t.comp[c].col] = t.comp[c].dst;
     int64_t a = t.a_in ? t.a_in[i] : i;
     int k = 0;
     for (int lev = 0; lev < t.nlev; ++lev) {
@@ -1879,15 +1914,21 @@ static inline dim3 tiles_for(int64_t N) { return dim3((unsigned)((N + kTile - 1)
 static inline dim3 rs_tiles_for(int64_t N) { return dim3((unsigned)((N + kRsTile - 1) / kRsTile)); }
 
 hipError_t launch_assign(hipStream_t s, double* out, int dim, const wsmc_operand* expr,
-                         double* const* cols, int64_t N) {
+                         double* const* cols, int64_t N, const Indirect& ind) {
     AssignArgs a;
-    for (int k = 0; k < 4; ++k) a.e[k] = expr[k < dim ? k : 0];
-    hipLaunchKernelGGL(k_assign, grid_for(N), dim3(kBlock), 0, s, out, dim, a, cols, N);
+    for (int k = 0; k < 4; ++k) {
+        a.e[k] = expr[k < dim ? k : 0];
+        for (int m = 0; m < 2; ++m)
+            a.p[k][m] = a.e[k].col[m] >= 0 ? ind.front[a.e[k].col[m]] + (int64_t)a.e[k].comp[m] * N : nullptr;
+    }
+    hipLaunchKernelGGL(k_assign, grid_for(N), dim3(kBlock), 0, s, out, dim, a, cols, N, ind);
     return hipGetLastError();
 }
 hipError_t launch_sample(hipStream_t s, double* out, int dim, const wsmc_dist& d, uint64_t seed, uint64_t op,
                          int64_t goff, double* const* cols, int64_t N) {
-    hipLaunchKernelGGL(k_sample, grid_for(N), dim3(kBlock), 0, s, out, dim, d, seed, op, goff, cols, N);
+    const int has_sd = d.family == WSMC_FAM_MVNORMAL_ISO && wsmc_operand_is_const(&d.scale);
+    const double sd = has_sd ? wsmc_sqrt(wsmc_operand_eval(&d.scale, nullptr, N, 0, nullptr)) : 0.0;
+    hipLaunchKernelGGL(k_sample, grid_for(N), dim3(kBlock), 0, s, out, dim, d, seed, op, goff, cols, N, has_sd, sd);
     return hipGetLastError();
 }
 hipError_t launch_sample_importance(hipStream_t s, double* out, int dim, const wsmc_dist& prop,
@@ -1899,7 +1940,14 @@ hipError_t launch_sample_importance(hipStream_t s, double* out, int dim, const w
 }
 hipError_t launch_weigh(hipStream_t s, const wsmc_term& t, double* w, double* const* cols, int64_t N, MaxSlots* ms,
                         MaxSlots* ms_next) {
-    hipLaunchKernelGGL(k_weigh, grid_for(N), dim3(kBlock), 0, s, t, w, cols, N, ms, ms_next);
+    wsmc_logmemo lm0 = {0, 0.0, 0};
+    if (t.dist.family != WSMC_FAM_UNIFORM && wsmc_operand_is_const(&t.dist.scale)) {
+        const double sc = wsmc_operand_eval(&t.dist.scale, nullptr, N, 0, nullptr);
+        lm0.arg = wsmc_d2bits(sc);
+        lm0.val = wsmc_log(sc);
+        lm0.valid = 1;
+    }
+    hipLaunchKernelGGL(k_weigh, grid_for(N), dim3(kBlock), 0, s, t, w, cols, N, ms, ms_next, lm0);
     return hipGetLastError();
 }
 template <typename K, typename... Args>
@@ -2125,6 +2173,7 @@ __global__ __launch_bounds__(kBlock) void k_resample_apply(GatherSet gs, const i
     if (i >= N) return;
     const int k = blockIdx.y;
     const bool rs = dec ? dec->resampled != 0 : true;
+    if (i == 0 && k < gs.n && gs.tab && gs.col[k] >= 0) gs.tab[gs.col[k]] = gs.dst[k];   // new front
     if (k == gs.n) {
         if (rs && dec) w[i] = dec->mean;
         return;

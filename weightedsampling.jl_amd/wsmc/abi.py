@@ -95,6 +95,7 @@ SIGNATURES = {
     "wsmc_col_device_ptr": (C.c_int, [_P, C.c_int32, C.POINTER(_D)]),
     "wsmc_store_resample": (C.c_int, [_P, _I32P]),
     "wsmc_store_set_lazy": (C.c_int, [_P, C.c_int32]),
+    "wsmc_store_materialize": (C.c_int, [_P]),
     "wsmc_store_info": (C.c_int, [_P, C.POINTER(C.c_int64), _I32P]),
     "wsmc_weights_upload": (C.c_int, [_P, _D]),
     "wsmc_weights_download": (C.c_int, [_P, _D]),

@@ -149,6 +149,10 @@ class Context:
         """Lazy genealogy (default) or the eager ColumnStore gather of every column."""
         check(self._L.wsmc_store_set_lazy(self._h, 1 if lazy else 0))
 
+    def store_materialize(self) -> None:
+        """Bring every column up to date (one trace over the Resample log)."""
+        check(self._L.wsmc_store_materialize(self._h))
+
     def store_info(self) -> dict:
         e = C.c_int64()
         st = C.c_int32()
