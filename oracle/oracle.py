@@ -98,7 +98,7 @@ _SIG = {
     "or_strat_word": (C.c_uint32, [C.c_uint64, C.c_uint64, C.c_uint64]),
     "or_qweight": (C.c_uint64, [C.c_double, C.c_double, C.c_int]),
     "or_qbits": (C.c_int, [C.c_uint64]),
-    "or_ssm2d_run_mt": (C.c_int, [C.c_int64, C.c_uint64, C.c_uint64, _D, _D, C.c_int32, _D, _D, C.c_double,
+    "or_ssm2d_run_mt": (C.c_int, [C.c_int64, C.c_uint64, C.c_uint64, C.c_uint64, _D, _D, C.c_int32, _D, _D, C.c_double,
                                   C.c_double, C.c_double, C.c_int32, C.c_int32, C.c_int32, _D, _D, _D, _D,
                                   _I32P, _D]),
     "fp_keep_heap": (C.c_int, []),
@@ -452,11 +452,12 @@ def log_evidence_records(records) -> float:
 
 
 def ssm2d_run_mt(n, obs, seed=42, x0=(0.0, 0.0), v0=(1.0, 0.0), q_var=0.1, r_var=0.5, ess_perc_min=0.5,
-                 scheme=0, keep_history=True, threads=1, op_base=0, weights=None, outputs=True):
+                 scheme=0, keep_history=True, threads=1, op_base=0, weights=None, outputs=True, goff=0):
     """The fused 2D SSM run (examples/2D_ssm.jl) on the CPU with OpenMP over particles
     (oracle/wsmc_port_mt.c): the all-cores CPU baseline, bit-identical to the statements.
     Returns a dict (columns SoA [2][N] like col_download, weights, flags, log_evidence);
-    with outputs=False nothing is copied out (the run, trace-back included, still happens)."""
+    with outputs=False nothing is copied out (the run, trace-back included, still happens).
+    goff: the particles' global offset (RNG index and stratum slot base): one island shard."""
     obs = np.ascontiguousarray(np.asarray(obs, dtype=np.float64).reshape(-1, 2))
     T = obs.shape[0]
     x0a = np.asarray(x0, dtype=np.float64)
@@ -470,7 +471,7 @@ def ssm2d_run_mt(n, obs, seed=42, x0=(0.0, 0.0), v0=(1.0, 0.0), q_var=0.1, r_var
     flags = np.zeros(T, dtype=np.int32)
     ev = C.c_double(0.0)
     nul = C.cast(None, _D)
-    r = lib().or_ssm2d_run_mt(n, seed, op_base, _dptr(w0) if w0 is not None else nul, _dptr(obs), T,
+    r = lib().or_ssm2d_run_mt(n, seed, op_base, goff, _dptr(w0) if w0 is not None else nul, _dptr(obs), T,
                               _dptr(x0a), _dptr(v0a), q_var, r_var, ess_perc_min, scheme, int(bool(keep_history)),
                               threads, _dptr(xs) if outputs else nul, _dptr(v) if outputs else nul,
                               _dptr(dv) if outputs else nul, _dptr(w) if outputs else nul,

@@ -910,6 +910,8 @@ static int move_apply(oracle* o, const int32_t* targets, int32_t d, int bounded,
     int64_t acc = 0;
     double* newv = (double*)malloc(sizeof(double) * (size_t)(N * d));
     unsigned char* ok = (unsigned char*)malloc((size_t)N);
+    /* particles are independent (counter-based draws, per-particle folds): OpenMP changes no bit */
+#pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < N; ++i) {
         double xi[4], dz[4];
         wsmc_override ov;
@@ -948,6 +950,7 @@ static int move_apply(oracle* o, const int32_t* targets, int32_t d, int bounded,
 
 /* score_logpdf (src/types.jl:198-206) */
 void or_score(oracle* o, int32_t target_depth, double* out) {
+#pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < o->N; ++i)
         out[i] = wsmc_fold(o->tape, o->nterms, target_depth, o->colptr, o->N, i, 0);
 }

@@ -49,7 +49,8 @@ typedef struct {
  *   v, dv   SoA [2][N];  w [N];  flags [T] (resampled per step)
  * returns 0, or -1 on a bad argument / allocation failure
  */
-int or_ssm2d_run_mt(int64_t N, uint64_t seed, uint64_t op_base, const double* w0, const double* obs, int32_t T,
+int or_ssm2d_run_mt(int64_t N, uint64_t seed, uint64_t op_base, uint64_t goff, const double* w0, const double* obs,
+                    int32_t T,
                     const double* x0, const double* v0, double q_var, double r_var, double ess_min, int32_t scheme,
                     int32_t keep_history, int32_t nthreads, double* xs, double* v_out, double* dv_out, double* w_out,
                     int32_t* flags, double* log_evidence) {
@@ -107,7 +108,7 @@ int or_ssm2d_run_mt(int64_t N, uint64_t seed, uint64_t op_base, const double* w0
                 const double xa = t > 1 ? xp[2 * s] : x0[0], xb = t > 1 ? xp[2 * s + 1] : x0[1];
                 const double va = t > 1 ? vp[2 * s] : v0[0], vbb = t > 1 ? vp[2 * s + 1] : v0[1];
                 double z0, z1;
-                wsmc_normal_pair(wsmc_rng_block(seed, op_dv, (uint64_t)n, 0u), &z0, &z1);
+                wsmc_normal_pair(wsmc_rng_block(seed, op_dv, goff + (uint64_t)n, 0u), &z0, &z1);
                 const double xn0 = aff2(xa, va), xn1 = aff2(xb, vbb);            /* x{t+1} .= x{t} + v */
                 const double dv0 = 0.0 + q_sd * z0, dv1 = 0.0 + q_sd * z1;       /* dv ~ MvNormal(0, q I) */
                 const double vn0 = aff2(va, dv0), vn1 = aff2(vbb, dv1);          /* v .= v + dv */
@@ -179,10 +180,10 @@ int or_ssm2d_run_mt(int64_t N, uint64_t seed, uint64_t op_base, const double* w0
             for (int k = 0; k < nthreads; ++k) coff[k + 1] += coff[k];
             /* particle m owns the slots [rank(C_{m-1}), rank(C_m)) */
             uint64_t C = coff[th];
-            uint64_t prev = wsmc_rank_r(C, Q, (uint64_t)N, ratio, scheme, seed, op_rs, 0);
+            uint64_t prev = wsmc_rank_r(C, Q, (uint64_t)N, ratio, scheme, seed, op_rs, goff);
             for (int64_t m = lo; m < hi; ++m) {
                 C += q[m];
-                const uint64_t h = q[m] ? wsmc_rank_r(C, Q, (uint64_t)N, ratio, scheme, seed, op_rs, 0) : prev;
+                const uint64_t h = q[m] ? wsmc_rank_r(C, Q, (uint64_t)N, ratio, scheme, seed, op_rs, goff) : prev;
                 for (uint64_t s = prev; s < h; ++s) a[s] = (int32_t)m;
                 prev = h;
             }

@@ -53,3 +53,23 @@ def test_port_mt_degenerate_weights():
     np.testing.assert_array_equal(r["weights"], o.weights_download())
     for name in o.col_names():
         np.testing.assert_array_equal(r[name], o.col_download(o.col_find(name)), err_msg=name)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_port_mt_goff_is_one_island_shard(world):
+    """With the global offset (RNG index and stratum slot base) the port runs one island shard
+    of a sharded population: under forced resampling (every step resamples, whatever the
+    global ESS; the first step's weights are all equal everywhere) shard r's columns and weights equal the sharded oracle's slice — the
+    reference the C4 shard tests hold the device against at 4M particles a shard."""
+    n, T = 1500, 12
+    obs = wsmc.models.ssm2d_data(T)
+    o = Oracle(n * world, seed=77, shards=world)
+    flags = wsmc.models.ssm2d_statements(o, obs, ess_perc_min=1.0)
+    assert all(flags[1:])                   # step 1: x_2 = x0 + v0 for all, equal weights, ESS = 1
+    for r in range(world):
+        p = oracle.ssm2d_run_mt(n, obs, seed=77, ess_perc_min=1.0, threads=4, goff=r * n)
+        assert list(p["flags"]) == [bool(f) for f in flags]
+        sl = slice(r * n, (r + 1) * n)
+        for name in o.col_names():
+            np.testing.assert_array_equal(p[name], o.col_download(o.col_find(name))[..., sl], err_msg=name)
+        np.testing.assert_array_equal(p["weights"], o.weights_download()[sl])
