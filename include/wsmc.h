@@ -121,6 +121,19 @@ int wsmc_device_count(int32_t* n);
 /* SMCState(n_particles; rng) — src/types.jl:62-78. The seed keys the Philox streams. */
 int wsmc_create(wsmc_ctx** out, int64_t n_particles, int32_t device, uint64_t seed);
 int wsmc_destroy(wsmc_ctx* ctx);
+/* SMCState over n_gpus devices in ONE handle ("multi-GPU inside one
+ * context"): the population [0, n_particles) is split into n_gpus contiguous shards (ragged),
+ * shard g on devices[g] (NULL: device g). transport WSMC_TRANSPORT_RCCL: one communicator per
+ * device from ncclCommInitAll (distinct devices); WSMC_TRANSPORT_HOST: records exchanged in
+ * host memory between the shards' threads (several shards may share a device). Every other
+ * entry point accepts the handle: a call runs on every shard concurrently (one host thread per
+ * shard, so each shard's collectives meet the others', as one process per GPU would) and host
+ * buffers of n_particles are split / joined by shard. Island sharding by default
+ * (wsmc_comm_set_shard_mode applies to every shard). Per-shard-only calls
+ * (wsmc_col_device_ptr, wsmc_store_resample, wsmc_debug_kernel_bench) need n_gpus = 1. */
+typedef enum { WSMC_TRANSPORT_RCCL = 0, WSMC_TRANSPORT_HOST = 1 } wsmc_transport;
+int wsmc_create_multi(wsmc_ctx** out, int64_t n_particles, int32_t n_gpus, const int32_t* devices,
+                      uint64_t seed, int32_t transport);
 int wsmc_sync(wsmc_ctx* ctx);
 int wsmc_nparticles(wsmc_ctx* ctx, int64_t* n);
 int wsmc_get_state(wsmc_ctx* ctx, wsmc_state* out);

@@ -503,3 +503,45 @@ def test_two_shards_analysis_match_single_context(gpu_available, tmp_path, sizes
         assert p["ev"][0] == o.log_evidence()
         np.testing.assert_allclose(p["mean"], mean, rtol=1e-12)
         np.testing.assert_allclose(p["cov"], cov, rtol=1e-10)
+
+
+# ---- one handle over several shards (wsmc_create_multi) -------------------------------------
+def _multi_program(ctx):
+    import wsmc
+    obs = wsmc.models.ssm2d_data(10)
+    flags = wsmc.models.ssm2d_statements(ctx, obs, ess_perc_min=1.0)
+    xs, ys = wsmc.models.linreg_data()
+    cx = ctx.col_create("alpha", 1)
+    ctx.sample(cx, wsmc.dsl.Normal(0.0, 10.0).dist(wsmc.models.resolver(ctx)))
+    acc = ctx.move(wsmc.PROPOSAL_AUTORW, [cx], 1e-3)
+    return flags, acc
+
+
+@pytest.mark.parametrize("shards,transport,mode", [(1, 0, "island"), (1, 0, "exact"), (2, 1, "island"),
+                                                   (2, 1, "exact"), (3, 1, "island")])
+def test_multi_handle_matches_oracle(gpu_available, shards, transport, mode):
+    """SMCState over several shards in one handle: one communicator from
+    ncclCommInitAll (one shard: the RCCL exchange paths on one GPU), or two / three shards on
+    the one device with the in-process exchange; every call fans out to the shards' threads.
+    Island shards equal the sharded oracle; exact shards one context, bit for bit."""
+    sys.path.insert(0, str(REPO / "oracle"))
+    from oracle import Oracle
+    import wsmc
+    from wsmc import abi
+    from test_gpu_parity import assert_same_state
+    N = 3001
+    g = wsmc.Context.multi(N, shards, seed=13, devices=[0] * shards, transport=transport)
+    if mode == "exact":
+        g.comm_set_shard_mode(abi.SHARD_EXACT)
+    o = Oracle(N, seed=13, shards=shards, exact=(mode == "exact")) if shards > 1 else Oracle(N, seed=13)
+    fg, ag = _multi_program(g)
+    fo, ao = _multi_program(o)
+    assert fg == fo
+    assert ag == ao
+    assert_same_state(g, o)
+    assert g.log_evidence() == o.log_evidence()
+    assert g.ess() == o.ess()
+    rows = np.array([0, N - 1, N // 2, 7, N // 3 + 1])
+    np.testing.assert_array_equal(g.col_gather_rows(g.col_find("v"), rows),
+                                  o.col_download(o.col_find("v"))[:, rows])
+    g.close()

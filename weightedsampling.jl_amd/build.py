@@ -23,7 +23,7 @@ CSRC = PKG / "csrc"
 INCLUDE = REPO / "include"
 OUT = PKG / "wsmc" / "libwsmc.so"
 OBJDIR = PKG / "build"
-SOURCES = ["wsmc_kernels.hip", "wsmc_api.hip"]
+SOURCES = ["wsmc_kernels.hip", "wsmc_api.hip", "wsmc_multi.hip"]
 ARCH = os.environ.get("WSMC_OFFLOAD_ARCH", "gfx950")
 
 

@@ -404,6 +404,7 @@ int wsmc_create(wsmc_ctx** out, int64_t n_particles, int32_t device, uint64_t se
 }
 
 int wsmc_destroy(wsmc_ctx* c) {
+    if (c && c->multi) return multi_destroy(c);
     if (!c) return WSMC_OK;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
@@ -465,6 +466,7 @@ static int resolve_decisions(wsmc_ctx* c) {
 }
 
 int wsmc_sync(wsmc_ctx* c) {
+    if (c && c->multi) return multi_sync(c);
     CHECK_CTX(c);
     WSMC_HIP(hipStreamSynchronize(c->stream));
     return WSMC_OK;
@@ -477,6 +479,7 @@ int wsmc_nparticles(wsmc_ctx* c, int64_t* n) {
 }
 
 int wsmc_get_state(wsmc_ctx* c, wsmc_state* s) {
+    if (c && c->multi) return s ? multi_get_state(c, s) : fail(WSMC_EARG, "null argument");
     if (!c || !s) return fail(WSMC_EARG, "null argument");
     if (int r = resolve_decisions(c)) return r;
     s->resampled = c->resampled;
@@ -490,6 +493,7 @@ int wsmc_get_state(wsmc_ctx* c, wsmc_state* s) {
 }
 
 int wsmc_set_depth(wsmc_ctx* c, int32_t depth) {
+    if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { return wsmc_set_depth(x, depth); });
     if (!c) return fail(WSMC_EARG, "null context");
     c->depth = depth;
     c->scache_terms = -1;
@@ -497,6 +501,7 @@ int wsmc_set_depth(wsmc_ctx* c, int32_t depth) {
 }
 
 int wsmc_set_op_counter(wsmc_ctx* c, uint64_t op) {
+    if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { return wsmc_set_op_counter(x, op); });
     if (!c) return fail(WSMC_EARG, "null context");
     c->op = op;
     return WSMC_OK;
@@ -511,6 +516,7 @@ int wsmc_comm_unique_id(uint8_t out_id[128]) {
 }
 
 int wsmc_comm_init(wsmc_ctx* c, const uint8_t id[128], int32_t world, int32_t rank, int64_t goff, int64_t gN) {
+    if (c && c->multi) return fail(WSMC_EARG, "a multi-device handle is sharded at creation");
     CHECK_CTX(c);
     if (world < 1 || world > kMaxWorld || rank < 0 || rank >= world) return fail(WSMC_EARG, "bad world/rank");
     if (goff < 0 || goff + c->N > gN) return fail(WSMC_EARG, "shard outside the global population");
@@ -528,6 +534,7 @@ int wsmc_comm_init(wsmc_ctx* c, const uint8_t id[128], int32_t world, int32_t ra
 
 int wsmc_comm_init_host(wsmc_ctx* c, wsmc_exchange_fn exchange, void* user, int32_t world, int32_t rank,
                         int64_t goff, int64_t gN) {
+    if (c && c->multi) return fail(WSMC_EARG, "a multi-device handle is sharded at creation");
     CHECK_CTX(c);
     if (!exchange) return fail(WSMC_EARG, "null exchange");
     if (world < 1 || world > kMaxWorld || rank < 0 || rank >= world) return fail(WSMC_EARG, "bad world/rank");
@@ -542,6 +549,7 @@ int wsmc_comm_init_host(wsmc_ctx* c, wsmc_exchange_fn exchange, void* user, int3
 }
 
 int wsmc_comm_set_shard_mode(wsmc_ctx* c, int32_t mode) {
+    if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { return wsmc_comm_set_shard_mode(x, mode); });
     CHECK_CTX(c);
     if (mode != WSMC_SHARD_ISLAND && mode != WSMC_SHARD_EXACT) return fail(WSMC_EARG, "unknown shard mode");
     // exact shards move every column between ranks at each Resample: the store stays eager
@@ -558,6 +566,7 @@ int wsmc_comm_set_shard_mode(wsmc_ctx* c, int32_t mode) {
 
 // ---- store ---------------------------------------------------------------------------
 int wsmc_col_create(wsmc_ctx* c, const char* name, int32_t dim, int32_t* col_id) {
+    if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { int32_t id = -1; int r = wsmc_col_create(x, name, dim, &id); if (x == multi_first(c) && col_id) *col_id = id; return r; });
     CHECK_CTX(c);
     if (!name || !col_id) return fail(WSMC_EARG, "null argument");
     for (size_t k = 0; k < c->cols.size(); ++k)
@@ -582,6 +591,7 @@ int wsmc_col_create(wsmc_ctx* c, const char* name, int32_t dim, int32_t* col_id)
 }
 
 int wsmc_col_find(wsmc_ctx* c, const char* name, int32_t* col_id) {
+    if (c && c->multi) return wsmc_col_find(multi_first(c), name, col_id);
     if (!c || !name || !col_id) return fail(WSMC_EARG, "null argument");
     *col_id = -1;
     for (size_t k = 0; k < c->cols.size(); ++k)
@@ -590,12 +600,14 @@ int wsmc_col_find(wsmc_ctx* c, const char* name, int32_t* col_id) {
 }
 
 int wsmc_col_count(wsmc_ctx* c, int32_t* n) {
+    if (c && c->multi) return wsmc_col_count(multi_first(c), n);
     if (!c || !n) return fail(WSMC_EARG, "null argument");
     *n = (int32_t)c->cols.size();
     return WSMC_OK;
 }
 
 int wsmc_col_info(wsmc_ctx* c, int32_t col, char* buf, int32_t len, int32_t* dim) {
+    if (c && c->multi) return wsmc_col_info(multi_first(c), col, buf, len, dim);
     if (!c || !valid_col(c, col)) return fail(WSMC_EARG, "bad column");
     if (buf && len > 0) {
         std::strncpy(buf, c->cols[col].name.c_str(), len - 1);
@@ -606,6 +618,7 @@ int wsmc_col_info(wsmc_ctx* c, int32_t col, char* buf, int32_t len, int32_t* dim
 }
 
 int wsmc_col_download(wsmc_ctx* c, int32_t col, double* host) {
+    if (c && c->multi) return host ? multi_col_download(c, col, host) : fail(WSMC_EARG, "null buffer");
     CHECK_CTX(c);
     if (!valid_col(c, col) || !host) return fail(WSMC_EARG, "bad column or null buffer");
     if (int r = need_cols(c, {col})) return r;
@@ -616,6 +629,7 @@ int wsmc_col_download(wsmc_ctx* c, int32_t col, double* host) {
 }
 
 int wsmc_col_upload(wsmc_ctx* c, int32_t col, const double* host) {
+    if (c && c->multi) return host ? multi_col_upload(c, col, host) : fail(WSMC_EARG, "null buffer");
     CHECK_CTX(c);
     if (!valid_col(c, col) || !host) return fail(WSMC_EARG, "bad column or null buffer");
     scores_touch(c, col);
@@ -627,6 +641,7 @@ int wsmc_col_upload(wsmc_ctx* c, int32_t col, const double* host) {
 }
 
 int wsmc_col_device_ptr(wsmc_ctx* c, int32_t col, double** dptr) {
+    if (c && c->multi) return multi_G(c) == 1 ? wsmc_col_device_ptr(multi_first(c), col, dptr) : fail(WSMC_EARG, "a column of a multi-device handle lives on several devices");
     if (!c || !valid_col(c, col) || !dptr) return fail(WSMC_EARG, "bad column");
     WSMC_HIP(hipSetDevice(c->device));
     if (int r = need_cols(c, {col})) return r;
@@ -635,6 +650,7 @@ int wsmc_col_device_ptr(wsmc_ctx* c, int32_t col, double** dptr) {
 }
 
 int wsmc_store_resample(wsmc_ctx* c, const int32_t* idx) {
+    if (c && c->multi) return multi_G(c) == 1 ? wsmc_store_resample(multi_first(c), idx) : fail(WSMC_EARG, "resample!(store, idx) with global indices needs one shard");
     CHECK_CTX(c);
     if (!idx) return fail(WSMC_EARG, "null indices");
     for (int64_t i = 0; i < c->N; ++i)
@@ -657,6 +673,7 @@ int wsmc_store_resample(wsmc_ctx* c, const int32_t* idx) {
 
 static bool exact_mode(const wsmc_ctx* c);
 int wsmc_store_set_lazy(wsmc_ctx* c, int32_t lazy) {
+    if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { return wsmc_store_set_lazy(x, lazy); });
     CHECK_CTX(c);
     if (!lazy || exact_mode(c)) {
         if (int r = resolve_decisions(c)) return r;
@@ -670,11 +687,13 @@ int wsmc_store_set_lazy(wsmc_ctx* c, int32_t lazy) {
 }
 
 int wsmc_store_materialize(wsmc_ctx* c) {
+    if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { return wsmc_store_materialize(x); });
     CHECK_CTX(c);
     return materialize_all(c);
 }
 
 int wsmc_store_info(wsmc_ctx* c, int64_t* log_entries, int32_t* stale_columns) {
+    if (c && c->multi) return wsmc_store_info(multi_first(c), log_entries, stale_columns);
     if (!c) return fail(WSMC_EARG, "null context");
     if (log_entries) *log_entries = (int64_t)c->alog.size();
     if (stale_columns) {
@@ -687,6 +706,7 @@ int wsmc_store_info(wsmc_ctx* c, int64_t* log_entries, int32_t* stale_columns) {
 
 // ---- weights -------------------------------------------------------------------------
 int wsmc_weights_upload(wsmc_ctx* c, const double* host) {
+    if (c && c->multi) return host ? multi_weights(c, host, nullptr) : fail(WSMC_EARG, "null buffer");
     CHECK_CTX(c);
     if (!host) return fail(WSMC_EARG, "null buffer");
     c->wseq += 1;
@@ -696,6 +716,7 @@ int wsmc_weights_upload(wsmc_ctx* c, const double* host) {
 }
 
 int wsmc_weights_download(wsmc_ctx* c, double* host) {
+    if (c && c->multi) return host ? multi_weights(c, nullptr, host) : fail(WSMC_EARG, "null buffer");
     CHECK_CTX(c);
     if (!host) return fail(WSMC_EARG, "null buffer");
     WSMC_HIP(hipMemcpyAsync(host, c->w, sizeof(double) * c->N, hipMemcpyDeviceToHost, c->stream));
@@ -1144,6 +1165,7 @@ static int adopt_global_max(wsmc_ctx* c) {
 }
 
 int wsmc_weighted_moments(wsmc_ctx* c, const wsmc_operand* exprs, int32_t d, double* mean, double* cov) {
+    if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { double m[4], v[16]; int r = wsmc_weighted_moments(x, exprs, d, mean ? m : nullptr, cov ? v : nullptr); if (!r && x == multi_first(c)) { if (mean) std::memcpy(mean, m, sizeof(double) * (d > 0 && d <= 4 ? d : 0)); if (cov) std::memcpy(cov, v, sizeof(double) * (d > 0 && d <= 4 ? d * d : 0)); } return r; });
     CHECK_CTX(c);
     if (!exprs || !mean || d < 1 || d > 4) return fail(WSMC_EARG, "need 1..4 expressions and a mean buffer");
     std::vector<int32_t> reads;
@@ -1223,6 +1245,7 @@ int wsmc_weighted_moments(wsmc_ctx* c, const wsmc_operand* exprs, int32_t d, dou
 }
 
 int wsmc_col_minmax(wsmc_ctx* c, int32_t col, int32_t comp, double* mn, double* mx) {
+    if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { double a, b; int r = wsmc_col_minmax(x, col, comp, mn ? &a : nullptr, mx ? &b : nullptr); if (!r && x == multi_first(c)) { *mn = a; *mx = b; } return r; });
     CHECK_CTX(c);
     if (col < 0 || col >= (int32_t)c->cols.size()) return fail(WSMC_EARG, "bad column");
     if (comp < 0 || comp >= c->cols[col].dim) return fail(WSMC_EARG, "bad component");
@@ -1301,6 +1324,7 @@ static int median_of(wsmc_ctx* c, const double* x, const unsigned long long* q, 
 }
 
 int wsmc_weighted_median(wsmc_ctx* c, int32_t col, int32_t comp, double* out) {
+    if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { double v; int r = wsmc_weighted_median(x, col, comp, out ? &v : nullptr); if (!r && x == multi_first(c)) *out = v; return r; });
     CHECK_CTX(c);
     if (!out) return fail(WSMC_EARG, "null output");
     double mn, mx;
@@ -1354,6 +1378,7 @@ int wsmc_weighted_median(wsmc_ctx* c, int32_t col, int32_t comp, double* out) {
 }
 
 int wsmc_histogram(wsmc_ctx* c, int32_t col, int32_t comp, int32_t levels[8]) {
+    if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { int32_t lv[8]; int r = wsmc_histogram(x, col, comp, levels ? lv : nullptr); if (!r && x == multi_first(c)) std::memcpy(levels, lv, sizeof(lv)); return r; });
     CHECK_CTX(c);
     if (!levels) return fail(WSMC_EARG, "null output");
     double lo, hi;
@@ -1407,6 +1432,7 @@ int wsmc_histogram(wsmc_ctx* c, int32_t col, int32_t comp, int32_t levels[8]) {
 }
 
 int wsmc_ess(wsmc_ctx* c, double* ess_perc) {
+    if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { double v; int r = wsmc_ess(x, &v); if (x == multi_first(c) && ess_perc) *ess_perc = v; return r; });
     CHECK_CTX(c);
     if (!ess_perc) return fail(WSMC_EARG, "null output");
     if (exact_mode(c)) {
@@ -1539,6 +1565,7 @@ static int sample_particles_sharded(wsmc_ctx* c, int64_t n, int32_t replace, int
 }
 
 int wsmc_sample_particles(wsmc_ctx* c, int64_t n, int32_t replace, int64_t* idx_out) {
+    if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { std::vector<int64_t> v(n > 0 ? (size_t)n : 1); int r = wsmc_sample_particles(x, n, replace, idx_out ? v.data() : nullptr); if (!r && x == multi_first(c)) std::memcpy(idx_out, v.data(), sizeof(int64_t) * (size_t)n); return r; });
     CHECK_CTX(c);
     if (!idx_out) return fail(WSMC_EARG, "null output");
     if (n <= 0) return fail(WSMC_EARG, "Number of samples must be positive");
@@ -1593,6 +1620,7 @@ int wsmc_sample_particles(wsmc_ctx* c, int64_t n, int32_t replace, int64_t* idx_
 }
 
 int wsmc_col_gather_rows(wsmc_ctx* c, int32_t col, const int64_t* idx, int64_t n, double* out) {
+    if (c && c->multi) return (idx && out && n >= 0) ? multi_gather_rows(c, col, idx, n, out) : fail(WSMC_EARG, "bad arguments");
     CHECK_CTX(c);
     if (!valid_col(c, col) || !idx || !out || n < 0) return fail(WSMC_EARG, "bad arguments");
     if (n == 0) return WSMC_OK;
@@ -1615,6 +1643,7 @@ int wsmc_col_gather_rows(wsmc_ctx* c, int32_t col, const int64_t* idx, int64_t n
 }
 
 int wsmc_log_evidence(wsmc_ctx* c, double* out) {
+    if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { double v; int r = wsmc_log_evidence(x, &v); if (x == multi_first(c) && out) *out = v; return r; });
     CHECK_CTX(c);
     if (!out) return fail(WSMC_EARG, "null out");
     if (exact_mode(c)) {
@@ -1640,6 +1669,7 @@ int wsmc_log_evidence(wsmc_ctx* c, double* out) {
 
 // ---- operators -----------------------------------------------------------------------
 int wsmc_assign(wsmc_ctx* c, int32_t out, const wsmc_operand* expr) {
+    if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { return wsmc_assign(x, out, expr); });
     CHECK_CTX(c);
     if (!valid_col(c, out) || !expr) return fail(WSMC_EARG, "bad output column");
     const int dim = c->cols[out].dim;
@@ -1704,6 +1734,7 @@ static void push_sample_term(wsmc_ctx* c, int32_t out, const wsmc_dist& d) {
 }
 
 int wsmc_sample(wsmc_ctx* c, int32_t out, const wsmc_dist* d) {
+    if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { return wsmc_sample(x, out, d); });
     CHECK_CTX(c);
     if (!valid_col(c, out) || !d) return fail(WSMC_EARG, "bad output column");
     int r = check_dist(c, *d);
@@ -1723,6 +1754,7 @@ int wsmc_sample(wsmc_ctx* c, int32_t out, const wsmc_dist* d) {
 }
 
 int wsmc_sample_importance(wsmc_ctx* c, int32_t out, const wsmc_dist* prop, const wsmc_dist* targ) {
+    if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { return wsmc_sample_importance(x, out, prop, targ); });
     CHECK_CTX(c);
     if (!valid_col(c, out) || !prop || !targ) return fail(WSMC_EARG, "bad arguments");
     int r = check_dist(c, *prop);
@@ -1747,6 +1779,7 @@ int wsmc_sample_importance(wsmc_ctx* c, int32_t out, const wsmc_dist* prop, cons
 }
 
 static int weigh(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x, int kind) {
+    if (c && c->multi) return multi_each(c, [&](wsmc_ctx* s) { return weigh(s, d, x, kind); });
     CHECK_CTX(c);
     if (!d || !x) return fail(WSMC_EARG, "null argument");
     int r = check_dist(c, *d);
@@ -1780,6 +1813,7 @@ int wsmc_observe(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x) { retur
 int wsmc_weight(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x) { return weigh(c, d, x, WSMC_TERM_WEIGHT); }
 
 int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resampled_out, double* ess_out) {
+    if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { int32_t rs = 0; double e = 0; const bool f = x == multi_first(c); int r = wsmc_resample(x, ess_min, scheme, resampled_out ? &rs : nullptr, ess_out ? &e : nullptr); if (!r && f) { if (resampled_out) *resampled_out = rs; if (ess_out) *ess_out = e; } return r; });
     CHECK_CTX(c);
     if (!valid_scheme(scheme)) return fail(WSMC_EARG, "unknown resampling scheme");
     if (scheme == WSMC_RESAMPLE_MULTINOMIAL && exact_mode(c))
@@ -1866,6 +1900,7 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
 }
 
 int wsmc_last_ancestors(wsmc_ctx* c, int32_t* host) {
+    if (c && c->multi) return host ? multi_last_ancestors(c, host) : fail(WSMC_EARG, "null buffer");
     CHECK_CTX(c);
     if (!host) return fail(WSMC_EARG, "null buffer");
     if (int r = resolve_decisions(c)) return r;   // which pending Resample resampled last
@@ -1876,6 +1911,7 @@ int wsmc_last_ancestors(wsmc_ctx* c, int32_t* host) {
 }
 
 int wsmc_score(wsmc_ctx* c, int32_t depth, double* host) {
+    if (c && c->multi) return host ? multi_score(c, depth, host) : fail(WSMC_EARG, "null buffer");
     CHECK_CTX(c);
     if (!host) return fail(WSMC_EARG, "null buffer");
     std::vector<int32_t> reads;
@@ -1962,6 +1998,7 @@ static int global_unique(wsmc_ctx* c, const unsigned long long* sorted, unsigned
 }
 
 int wsmc_marginal_diversity(wsmc_ctx* c, const int32_t* targets, int32_t d, double* out) {
+    if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { double v; int r = wsmc_marginal_diversity(x, targets, d, out ? &v : nullptr); if (!r && x == multi_first(c)) *out = v; return r; });
     CHECK_CTX(c);
     if (!targets || d < 1 || !out) return fail(WSMC_EARG, "bad targets");
     for (int k = 0; k < d; ++k)
@@ -2156,6 +2193,8 @@ static int32_t compile_fold(const std::vector<wsmc_term>& ct, int32_t j0, int32_
 
 int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, double step, const double* lo,
               const double* hi, int32_t target_depth, double diversity, int64_t* accepted_out) {
+    if (c && c->multi)
+        return multi_move(c, proposal, targets, d, step, lo, hi, target_depth, diversity, accepted_out);
     CHECK_CTX(c);
     const uint64_t op_prop = c->op++, op_acc = c->op++;
     if (accepted_out) *accepted_out = 0;
@@ -2558,12 +2597,14 @@ static int ssm2d_run_exact(wsmc_ctx* c, const RunPlan& p, uint64_t op_base) {
 }
 
 int wsmc_run_set_timing(wsmc_ctx* c, int32_t enabled) {
+    if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { return wsmc_run_set_timing(x, enabled); });
     if (!c) return fail(WSMC_EARG, "null context");
     c->timing = enabled != 0;
     return WSMC_OK;
 }
 
 int wsmc_run_get_timing(wsmc_ctx* c, wsmc_run_timing* out) {
+    if (c && c->multi) return wsmc_run_get_timing(multi_first(c), out);
     if (!c || !out) return fail(WSMC_EARG, "null argument");
     *out = c->last_timing;
     return WSMC_OK;
@@ -2571,6 +2612,14 @@ int wsmc_run_get_timing(wsmc_ctx* c, wsmc_run_timing* out) {
 
 int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, const double* v0, double q_var,
                    double r_var, double ess_min, int32_t scheme, int32_t keep_history, double* log_evidence_out) {
+    if (c && c->multi)
+        return multi_each(c, [&](wsmc_ctx* x) {
+            double ev = 0;
+            int r = wsmc_ssm2d_run(x, obs, T, x0, v0, q_var, r_var, ess_min, scheme, keep_history,
+                                   log_evidence_out ? &ev : nullptr);
+            if (!r && log_evidence_out && x == multi_first(c)) *log_evidence_out = ev;
+            return r;
+        });
     CHECK_CTX(c);
     if (int r = resolve_decisions(c)) return r;
     c->scache_terms = -1;   // the run rewrites columns the tape reads
@@ -2820,6 +2869,7 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
 }
 
 int wsmc_debug_kernel_bench(wsmc_ctx* c, int32_t kernel, int32_t mode, int32_t iters, double* avg_us) {
+    if (c && c->multi) return multi_G(c) == 1 ? wsmc_debug_kernel_bench(multi_first(c), kernel, mode, iters, avg_us) : fail(WSMC_EARG, "diagnostics need one shard");
     CHECK_CTX(c);
     if (!avg_us || iters < 1) return fail(WSMC_EARG, "bad arguments");
     // populate max slots / partials / offsets / record from the current weights; force a resample

@@ -6,6 +6,7 @@
 
 #include <cstdint>
 #include <deque>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -121,9 +122,11 @@ struct RunGraph {
     void* owned = nullptr;     // device tables baked into the graph
 };
 
+struct MultiState;   // wsmc_multi.hip
 }  // namespace wsmc
 
 struct wsmc_ctx {
+    wsmc::MultiState* multi = nullptr;   // a handle over several shards (wsmc_create_multi)
     int device = 0;
     hipStream_t stream = nullptr;
     // asynchronous Resamples (no flag requested): their decisions are copied into a pinned
@@ -496,6 +499,21 @@ struct Ssm2dFinal {
 hipError_t launch_ssm2d_finalize(hipStream_t s, const Ssm2dFinal& f, hipEvent_t e0 = nullptr,
                                  hipEvent_t e1 = nullptr);
 hipError_t launch_delay(hipStream_t s, int microseconds);
+// one handle over several devices (wsmc_multi.hip): the ABI entry points fan out
+int multi_destroy(wsmc_ctx* c);
+wsmc_ctx* multi_first(wsmc_ctx* c);
+int multi_G(wsmc_ctx* c);
+int multi_sync(wsmc_ctx* c);
+int multi_get_state(wsmc_ctx* c, wsmc_state* out);
+int multi_each(wsmc_ctx* c, const std::function<int(wsmc_ctx*)>& f);
+int multi_col_download(wsmc_ctx* c, int32_t col, double* host);
+int multi_col_upload(wsmc_ctx* c, int32_t col, const double* host);
+int multi_weights(wsmc_ctx* c, const double* up, double* down);
+int multi_score(wsmc_ctx* c, int32_t depth, double* host);
+int multi_last_ancestors(wsmc_ctx* c, int32_t* host);
+int multi_gather_rows(wsmc_ctx* c, int32_t col, const int64_t* idx, int64_t n, double* out);
+int multi_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, double step, const double* lo,
+               const double* hi, int32_t target_depth, double diversity, int64_t* accepted_out);
 hipError_t debug_kernel_bench(hipStream_t s, int kernel, int mode, int iters, const double* w, int64_t N,
                               MaxSlots* ms, unsigned long long* tilep, unsigned long long* qbuf,
                               unsigned long long* tileOff, ShardRecord* rec, Decision* dec, const FillPlan& plan,

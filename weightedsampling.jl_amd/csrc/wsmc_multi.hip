@@ -1,0 +1,352 @@
+// wsmc_multi.hip — one handle over several devices (`wsmc_create(…, n_gpus, …)`,
+// "multi-GPU inside one context"), so a single-threaded host — the reference's model,
+// src/types.jl:24-26 — can hold one SMCState spanning the node without an MPI launcher.
+//
+// The population [0, N) is split into G contiguous shards [N g / G, N (g+1) / G); shard g is an ordinary sharded context on its device, exactly what one
+// process per GPU would create (wsmc_comm_init / wsmc_comm_init_host), so every sharded code
+// path and its bit-exactness carry over unchanged. A call on the handle fans out to one host
+// thread per shard (persistent workers; shard 0 runs on the caller's thread): each shard
+// issues its own RCCL collectives from its own thread, as one process per GPU would, and
+// the collectives of the G shards meet. Host buffers of N particles are split by shard on the
+// way in and joined on the way out; population-wide results (evidence, ESS, moments, median,
+// histogram, diversity, sample, flags) are identical on every shard and taken from shard 0.
+#include <condition_variable>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "wsmc_internal.h"
+
+namespace wsmc {
+
+struct MultiState;
+
+namespace {
+
+struct Worker {
+    std::thread th;
+    std::mutex m;
+    std::condition_variable cv;
+    std::function<void()> job;
+    bool has = false, done = false, quit = false;
+};
+
+struct XArg {
+    MultiState* M;
+    int rank;
+};
+
+}  // namespace
+
+struct MultiState {
+    int G = 1;
+    int64_t N = 0;
+    std::vector<int64_t> off;          // shard g = [off[g], off[g+1])
+    std::vector<wsmc_ctx*> sub;
+    std::vector<std::unique_ptr<Worker>> workers;   // workers[g] for g >= 1
+    // in-process record exchange (transport 1)
+    std::mutex xm;
+    std::condition_variable xcv;
+    int arrived = 0, departed = 0;
+    uint64_t gen_in = 0, gen_out = 0;
+    std::vector<uint64_t> xbuf;
+    std::vector<XArg> xargs;
+};
+
+static void worker_loop(Worker* w) {
+    for (;;) {
+        std::function<void()> job;
+        {
+            std::unique_lock<std::mutex> lk(w->m);
+            w->cv.wait(lk, [&] { return w->has || w->quit; });
+            if (w->quit && !w->has) return;
+            job = std::move(w->job);
+            w->has = false;
+        }
+        job();
+        {
+            std::lock_guard<std::mutex> lk(w->m);
+            w->done = true;
+        }
+        w->cv.notify_all();
+    }
+}
+
+// fn(g, shard) on every shard concurrently; the first failing shard's code and message
+static int run_all(MultiState* M, const std::function<int(int, wsmc_ctx*)>& fn) {
+    std::vector<int> rc(M->G, 0);
+    std::vector<std::string> msg(M->G);
+    for (int g = 1; g < M->G; ++g) {
+        Worker* w = M->workers[g].get();
+        std::lock_guard<std::mutex> lk(w->m);
+        w->job = [&, g] {
+            rc[g] = fn(g, M->sub[g]);
+            if (rc[g]) msg[g] = wsmc_last_error();
+        };
+        w->has = true;
+        w->done = false;
+        w->cv.notify_all();
+    }
+    rc[0] = fn(0, M->sub[0]);
+    if (rc[0]) msg[0] = wsmc_last_error();
+    for (int g = 1; g < M->G; ++g) {
+        Worker* w = M->workers[g].get();
+        std::unique_lock<std::mutex> lk(w->m);
+        w->cv.wait(lk, [&] { return w->done; });
+    }
+    for (int g = 0; g < M->G; ++g)
+        if (rc[g]) return fail(rc[g], "shard " + std::to_string(g) + ": " + msg[g]);
+    return WSMC_OK;
+}
+
+// all-gather of one u64 record per shard through host memory (the shards are threads of this
+// process): a two-phase barrier so no shard overwrites the buffer before every shard copied it
+static int multi_exchange(void* user, const uint64_t* mine, int32_t words, uint64_t* all) {
+    XArg* a = static_cast<XArg*>(user);
+    MultiState* M = a->M;
+    std::unique_lock<std::mutex> lk(M->xm);
+    if (M->xbuf.size() < (size_t)M->G * (size_t)words) M->xbuf.resize((size_t)M->G * (size_t)words);
+    std::memcpy(M->xbuf.data() + (size_t)a->rank * words, mine, sizeof(uint64_t) * (size_t)words);
+    const uint64_t g_in = M->gen_in;
+    if (++M->arrived == M->G) {
+        M->arrived = 0;
+        M->gen_in += 1;
+        M->xcv.notify_all();
+    } else {
+        M->xcv.wait(lk, [&] { return M->gen_in != g_in; });
+    }
+    std::memcpy(all, M->xbuf.data(), sizeof(uint64_t) * (size_t)M->G * (size_t)words);
+    const uint64_t g_out = M->gen_out;
+    if (++M->departed == M->G) {
+        M->departed = 0;
+        M->gen_out += 1;
+        M->xcv.notify_all();
+    } else {
+        M->xcv.wait(lk, [&] { return M->gen_out != g_out; });
+    }
+    return 0;
+}
+
+static inline int64_t nloc(const MultiState* M, int g) { return M->off[g + 1] - M->off[g]; }
+
+// [dim][N] host <-> per-shard [dim][n_g]
+static void split_rows(const MultiState* M, int g, const double* host, int dim, std::vector<double>& out) {
+    const int64_t n = nloc(M, g);
+    out.resize((size_t)dim * n);
+    for (int k = 0; k < dim; ++k)
+        std::memcpy(out.data() + (size_t)k * n, host + (size_t)k * M->N + M->off[g], sizeof(double) * n);
+}
+static void join_rows(const MultiState* M, int g, const std::vector<double>& in, int dim, double* host) {
+    const int64_t n = nloc(M, g);
+    for (int k = 0; k < dim; ++k)
+        std::memcpy(host + (size_t)k * M->N + M->off[g], in.data() + (size_t)k * n, sizeof(double) * n);
+}
+
+int multi_destroy(wsmc_ctx* c) {
+    MultiState* M = c->multi;
+    for (int g = 1; g < M->G; ++g) {
+        Worker* w = M->workers[g].get();
+        {
+            std::lock_guard<std::mutex> lk(w->m);
+            w->quit = true;
+        }
+        w->cv.notify_all();
+        if (w->th.joinable()) w->th.join();
+    }
+    for (auto* s : M->sub)
+        if (s) wsmc_destroy(s);
+    delete M;
+    delete c;
+    return WSMC_OK;
+}
+
+}  // namespace wsmc
+
+using namespace wsmc;
+
+// ---- the per-function fan-out (called from the ABI entry points when ctx->multi) -------------
+namespace wsmc {
+
+wsmc_ctx* multi_first(wsmc_ctx* c) { return c->multi->sub[0]; }
+int multi_G(wsmc_ctx* c) { return c->multi->G; }
+int multi_sync(wsmc_ctx* c) { return run_all(c->multi, [](int, wsmc_ctx* s) { return wsmc_sync(s); }); }
+int multi_get_state(wsmc_ctx* c, wsmc_state* out) {
+    std::vector<wsmc_state> st(c->multi->G);
+    int r = run_all(c->multi, [&](int g, wsmc_ctx* s) { return wsmc_get_state(s, &st[g]); });
+    if (!r) *out = st[0];
+    return r;
+}
+int multi_each(wsmc_ctx* c, const std::function<int(wsmc_ctx*)>& f) {
+    return run_all(c->multi, [&](int, wsmc_ctx* s) { return f(s); });
+}
+int multi_col_download(wsmc_ctx* c, int32_t col, double* host) {
+    MultiState* M = c->multi;
+    int32_t dim = 0;
+    int r = wsmc_col_info(M->sub[0], col, nullptr, 0, &dim);
+    if (r) return r;
+    std::vector<std::vector<double>> buf(M->G);
+    r = run_all(M, [&](int g, wsmc_ctx* s) {
+        buf[g].resize((size_t)dim * nloc(M, g));
+        return wsmc_col_download(s, col, buf[g].data());
+    });
+    if (r) return r;
+    for (int g = 0; g < M->G; ++g) join_rows(M, g, buf[g], dim, host);
+    return WSMC_OK;
+}
+int multi_col_upload(wsmc_ctx* c, int32_t col, const double* host) {
+    MultiState* M = c->multi;
+    int32_t dim = 0;
+    int r = wsmc_col_info(M->sub[0], col, nullptr, 0, &dim);
+    if (r) return r;
+    std::vector<std::vector<double>> buf(M->G);
+    for (int g = 0; g < M->G; ++g) split_rows(M, g, host, dim, buf[g]);
+    return run_all(M, [&](int g, wsmc_ctx* s) { return wsmc_col_upload(s, col, buf[g].data()); });
+}
+int multi_weights(wsmc_ctx* c, const double* up, double* down) {
+    MultiState* M = c->multi;
+    std::vector<std::vector<double>> buf(M->G);
+    if (up)
+        for (int g = 0; g < M->G; ++g) split_rows(M, g, up, 1, buf[g]);
+    int r = run_all(M, [&](int g, wsmc_ctx* s) {
+        if (up) return wsmc_weights_upload(s, buf[g].data());
+        buf[g].resize(nloc(M, g));
+        return wsmc_weights_download(s, buf[g].data());
+    });
+    if (!r && down)
+        for (int g = 0; g < M->G; ++g) join_rows(M, g, buf[g], 1, down);
+    return r;
+}
+int multi_score(wsmc_ctx* c, int32_t depth, double* host) {
+    MultiState* M = c->multi;
+    std::vector<std::vector<double>> buf(M->G);
+    int r = run_all(M, [&](int g, wsmc_ctx* s) {
+        buf[g].resize(nloc(M, g));
+        return wsmc_score(s, depth, buf[g].data());
+    });
+    if (!r)
+        for (int g = 0; g < M->G; ++g) join_rows(M, g, buf[g], 1, host);
+    return r;
+}
+int multi_last_ancestors(wsmc_ctx* c, int32_t* host) {
+    MultiState* M = c->multi;
+    std::vector<std::vector<int32_t>> buf(M->G);
+    int r = run_all(M, [&](int g, wsmc_ctx* s) {
+        buf[g].resize(nloc(M, g));
+        return wsmc_last_ancestors(s, buf[g].data());
+    });
+    if (!r)
+        for (int g = 0; g < M->G; ++g)
+            std::memcpy(host + M->off[g], buf[g].data(), sizeof(int32_t) * nloc(M, g));
+    return r;
+}
+int multi_gather_rows(wsmc_ctx* c, int32_t col, const int64_t* idx, int64_t n, double* out) {
+    MultiState* M = c->multi;
+    int32_t dim = 0;
+    int r = wsmc_col_info(M->sub[0], col, nullptr, 0, &dim);
+    if (r) return r;
+    std::vector<std::vector<int64_t>> li(M->G), pos(M->G);
+    for (int64_t j = 0; j < n; ++j) {
+        if (idx[j] < 0 || idx[j] >= M->N) return fail(WSMC_EARG, "row index out of range");
+        int g = 0;
+        while (idx[j] >= M->off[g + 1]) ++g;
+        li[g].push_back(idx[j] - M->off[g]);
+        pos[g].push_back(j);
+    }
+    std::vector<std::vector<double>> buf(M->G);
+    r = run_all(M, [&](int g, wsmc_ctx* s) {   // local reads only: no collective
+        if (li[g].empty()) return (int)WSMC_OK;
+        buf[g].resize((size_t)dim * li[g].size());
+        return wsmc_col_gather_rows(s, col, li[g].data(), (int64_t)li[g].size(), buf[g].data());
+    });
+    if (r) return r;
+    for (int g = 0; g < M->G; ++g) {
+        const size_t m = li[g].size();
+        for (size_t q = 0; q < m; ++q)
+            for (int k = 0; k < dim; ++k) out[(size_t)k * n + pos[g][q]] = buf[g][(size_t)k * m + q];
+    }
+    return WSMC_OK;
+}
+int multi_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, double step, const double* lo,
+               const double* hi, int32_t target_depth, double diversity, int64_t* accepted_out) {
+    std::vector<int64_t> acc(c->multi->G, 0);
+    int r = run_all(c->multi, [&](int g, wsmc_ctx* s) {
+        return wsmc_move(s, proposal, targets, d, step, lo, hi, target_depth, diversity, &acc[g]);
+    });
+    if (!r && accepted_out) {
+        int64_t t = 0;
+        for (int64_t a : acc) t += a;
+        *accepted_out = t;
+    }
+    return r;
+}
+
+}  // namespace wsmc
+
+extern "C" int wsmc_create_multi(wsmc_ctx** out, int64_t n_particles, int32_t n_gpus, const int32_t* devices,
+                                 uint64_t seed, int32_t transport) {
+    if (!out) return fail(WSMC_EARG, "null out");
+    *out = nullptr;
+    if (n_gpus < 1 || n_gpus > kMaxWorld) return fail(WSMC_EARG, "n_gpus must be 1..8");
+    if (n_particles < n_gpus) return fail(WSMC_EARG, "fewer particles than shards");
+    if (transport != WSMC_TRANSPORT_RCCL && transport != WSMC_TRANSPORT_HOST) return fail(WSMC_EARG, "unknown transport");
+    const int G = n_gpus;
+    std::vector<int32_t> devs(G);
+    for (int g = 0; g < G; ++g) devs[g] = devices ? devices[g] : g;
+    if (transport == WSMC_TRANSPORT_RCCL)
+        for (int g = 0; g < G; ++g)
+            for (int h = 0; h < g; ++h)
+                if (devs[g] == devs[h]) return fail(WSMC_EARG, "RCCL shards need distinct devices (transport 1 shares one)");
+    MultiState* M = new MultiState();
+    M->G = G;
+    M->N = n_particles;
+    M->off.resize(G + 1);
+    for (int g = 0; g <= G; ++g) M->off[g] = n_particles * g / G;   // the oracle's shard layout
+    M->sub.assign(G, nullptr);
+    M->xargs.resize(G);
+    auto cleanup = [&](int code) {
+        for (auto* s : M->sub)
+            if (s) wsmc_destroy(s);
+        delete M;
+        return code;
+    };
+    for (int g = 0; g < G; ++g) {
+        int r = wsmc_create(&M->sub[g], M->off[g + 1] - M->off[g], devs[g], seed);
+        if (r) return cleanup(r);
+    }
+    if (transport == WSMC_TRANSPORT_RCCL) {
+        std::vector<ncclComm_t> comms(G);
+        const ncclResult_t nr = ncclCommInitAll(comms.data(), G, devs.data());
+        if (nr != ncclSuccess) return cleanup(fail(WSMC_ERCCL, std::string("ncclCommInitAll: ") + ncclGetErrorString(nr)));
+        for (int g = 0; g < G; ++g) {
+            wsmc_ctx* s = M->sub[g];
+            s->world = G;
+            s->rank = g;
+            s->goff = M->off[g];
+            s->gN = n_particles;
+            s->comm = comms[g];   // the shard's destroy releases it
+        }
+    } else {
+        for (int g = 0; g < G; ++g) {
+            M->xargs[g] = XArg{M, g};
+            int r = wsmc_comm_init_host(M->sub[g], multi_exchange, &M->xargs[g], G, g, M->off[g], n_particles);
+            if (r) return cleanup(r);
+        }
+    }
+    M->workers.resize(G);
+    for (int g = 1; g < G; ++g) {
+        M->workers[g] = std::make_unique<Worker>();
+        M->workers[g]->th = std::thread(worker_loop, M->workers[g].get());
+    }
+    wsmc_ctx* c = new wsmc_ctx();
+    c->multi = M;
+    c->device = devs[0];
+    c->N = n_particles;
+    c->gN = n_particles;
+    c->seed = seed;
+    c->world = G;
+    *out = c;
+    return WSMC_OK;
+}

@@ -19,6 +19,7 @@ MEAN_AFFINE, MEAN_OSCILLATOR = range(2)
 TERM_SAMPLE, TERM_OBSERVE, TERM_WEIGHT = range(3)
 RESAMPLE_STRATIFIED, RESAMPLE_SYSTEMATIC, RESAMPLE_MULTINOMIAL = range(3)
 SHARD_ISLAND, SHARD_EXACT = range(2)
+TRANSPORT_RCCL, TRANSPORT_HOST = range(2)
 PROPOSAL_RW, PROPOSAL_AUTORW = range(2)
 
 
@@ -75,6 +76,7 @@ SIGNATURES = {
     "wsmc_device_count": (C.c_int, [_I32P]),
     "wsmc_create": (C.c_int, [C.POINTER(_P), C.c_int64, C.c_int32, C.c_uint64]),
     "wsmc_destroy": (C.c_int, [_P]),
+    "wsmc_create_multi": (C.c_int, [C.POINTER(_P), C.c_int64, C.c_int32, _I32P, C.c_uint64, C.c_int32]),
     "wsmc_sync": (C.c_int, [_P]),
     "wsmc_nparticles": (C.c_int, [_P, C.POINTER(C.c_int64)]),
     "wsmc_get_state": (C.c_int, [_P, C.POINTER(State)]),

@@ -47,6 +47,28 @@ class Context:
         self.world = 1
         self.rank = 0
 
+    @classmethod
+    def multi(cls, n_particles: int, n_gpus: int, seed: int = 42, devices=None,
+              transport: int = abi.TRANSPORT_RCCL) -> "Context":
+        """One handle over n_gpus shards (wsmc_create_multi): every call fans out to the
+        shards; host arrays cover all n_particles."""
+        self = cls.__new__(cls)
+        self._L = load_library()
+        h = C.c_void_p()
+        devs = None
+        if devices is not None:
+            devs = (C.c_int32 * n_gpus)(*[int(d) for d in devices])
+        check(self._L.wsmc_create_multi(C.byref(h), int(n_particles), int(n_gpus),
+                                        C.cast(devs, _I32P) if devs is not None else None,
+                                        int(seed) & (2**64 - 1), int(transport)))
+        self._h = h
+        self.n = int(n_particles)
+        self.seed = int(seed)
+        self.device = int(devices[0]) if devices is not None else 0
+        self.world = 1
+        self.rank = 0
+        return self
+
     # ---- lifetime ----
     def close(self) -> None:
         if getattr(self, "_h", None):
