@@ -27,7 +27,7 @@ const WS = WeightedSampling
 import WeightedSampling: nparticles, hascol, getcol, colnames, broadcast_setcol!, resample!, apply!,
     log_evidence
 
-export HipColumnStore, ssm2d_run!, sync_weights!, expectation, describe_device, sample_device, shard!,
+export HipColumnStore, lazy!, materialize!, ssm2d_run!, sync_weights!, expectation, describe_device, sample_device, shard!,
        comm_unique_id
 
 const libwsmc = get(ENV, "WSMC_LIB", joinpath(@__DIR__, "..", "wsmc", "libwsmc.so"))
@@ -89,10 +89,34 @@ mutable struct HipColumnStore <: WS.AbstractParticleStore
     tmp::Int                       # counter for host-materialised temporaries
 end
 
-function HipColumnStore(n::Integer; seed::Integer=42, device::Integer=0)
+"""
+    HipColumnStore(n; seed=42, device=0)
+    HipColumnStore(n; gpus=8, devices=0:7, seed=42, transport=:rccl, shard_mode=:island)
+
+One store of `n` particles on one device, or — `gpus > 1` — one handle over `gpus` devices
+(`wsmc_create_multi`): contiguous shards, RCCL communicators from `ncclCommInitAll`, every
+operator fanned out to the shards by the library, host vectors of all `n` particles split and
+joined there. Julia stays single-threaded (src/types.jl:24-26) and needs no MPI launcher.
+`shard_mode = :exact` resamples the whole population with the one-device bits.
+"""
+function HipColumnStore(n::Integer; seed::Integer=42, device::Integer=0, gpus::Integer=1,
+                        devices=nothing, transport::Symbol=:rccl, shard_mode::Symbol=:island)
     h = Ref{Ptr{Cvoid}}(C_NULL)
-    check(ccall((:wsmc_create, libwsmc), Cint, (Ptr{Ptr{Cvoid}}, Int64, Int32, UInt64),
-                h, n, device, seed % UInt64))
+    if gpus == 1 && devices === nothing
+        check(ccall((:wsmc_create, libwsmc), Cint, (Ptr{Ptr{Cvoid}}, Int64, Int32, UInt64),
+                    h, n, device, seed % UInt64))
+    else
+        devs = Int32.(devices === nothing ? collect(0:gpus-1) : collect(devices))
+        length(devs) == gpus || throw(ArgumentError("devices must list one device per shard"))
+        tr = transport === :rccl ? Int32(0) : transport === :host ? Int32(1) :
+             throw(ArgumentError("transport must be :rccl or :host"))
+        check(ccall((:wsmc_create_multi, libwsmc), Cint,
+                    (Ptr{Ptr{Cvoid}}, Int64, Int32, Ptr{Int32}, UInt64, Int32),
+                    h, n, gpus, devs, seed % UInt64, tr))
+        if shard_mode === :exact
+            check(ccall((:wsmc_comm_set_shard_mode, libwsmc), Cint, (Ptr{Cvoid}, Int32), h[], 1))
+        end
+    end
     s = HipColumnStore(h[], Int(n), Symbol[], Dict{Symbol,Int32}(), Dict{Symbol,Int}(), 0)
     finalizer(s) do s
         s.ctx == C_NULL || ccall((:wsmc_destroy, libwsmc), Cint, (Ptr{Cvoid},), s.ctx)
@@ -115,6 +139,18 @@ function column!(s::HipColumnStore, name::Symbol, dim::Integer)
     push!(s.names, name)
     return id[]
 end
+
+"""
+    lazy!(s, on)      materialize!(s)
+
+The store's genealogy (DESIGN.md §3 "Lazy genealogy"): with `on` (the default) a Resample logs
+its ancestors and columns catch up when read; `lazy!(s, false)` restores ColumnStore's eager
+gather of every column at every resample (src/stores.jl:105-128). `materialize!` brings every
+column up to date now (a `getcol` does it for its column anyway).
+"""
+lazy!(s::HipColumnStore, on::Bool) =
+    check(ccall((:wsmc_store_set_lazy, libwsmc), Cint, (Ptr{Cvoid}, Int32), s.ctx, on ? 1 : 0))
+materialize!(s::HipColumnStore) = check(ccall((:wsmc_store_materialize, libwsmc), Cint, (Ptr{Cvoid},), s.ctx))
 
 """Host copy of a column: `Vector{Float64}` (dim 1) or `Vector{Vector{Float64}}`."""
 function download(s::HipColumnStore, name::Symbol)
