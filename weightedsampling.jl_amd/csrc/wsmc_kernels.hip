@@ -696,6 +696,35 @@ __device__ __forceinline__ void store_chunk(int32_t* __restrict__ dst, int n, co
 // (blocked) particles and scatters their slots within the chunk. A particle owning more
 // than kScatterMax slots of the chunk is queued and filled by the whole block, so a lane
 // never loops long whatever the weights.
+// rank(c) = #{n : x_n < c} (include/wsmc_math.h wsmc_rank_r), bit-identical, decided in f64
+// when f64 provably decides it. With y = c N / Q evaluated as fl(fl(c) * fl(N / Q)) (four
+// roundings: |y - cN/Q| <= 4 * 2^-53 * N <= 2^-17 for N <= 2^34, any global population of
+// one node), the exact rank is floor(cN/Q) + [R / 2^32 < frac(cN/Q)] (R the slot's stratum
+// word). If frac(y) is further than 2^-15 from 0 and 1, floor(y) is the exact floor; if
+// R / 2^32 is further than 2^-15 from frac(y), the comparison is the exact one. Otherwise
+// (about 2e-4 of the particles) the exact 64x32-bit path decides. The fast path is a conversion, a product, a floor, the 32-bit slot
+// hash and two compares, where the exact path is three 64x32 products and 128-bit compares.
+__device__ __forceinline__ u64 d_small_to_u64(double d);
+__device__ __forceinline__ u64 rank_fast(u64 c, u64 Q, u64 N, double ratio, int scheme, uint64_t seed,
+                                         uint64_t op, uint64_t slot_base, uint64_t key) {
+    if (c == 0) return 0;
+    if (c >= Q) return N;
+    constexpr double kMargin = 3.0517578125e-05;    // 2^-15
+    const double y = wsmc_u64_to_d(c) * ratio;
+    const double fl = wsmc_floor(y);
+    const double f = y - fl;                        // exact
+    if (f > kMargin && f < 1.0 - kMargin) {
+        const u64 ns = d_small_to_u64(fl);
+        if (ns < N) {
+            const uint32_t R = wsmc_strat_hash(key, scheme == 1 ? slot_base : slot_base + ns);
+            const double dd = f - (double)R * 2.3283064365386963e-10;   // f - R / 2^32
+            if (dd > kMargin) return ns + 1;
+            if (dd < -kMargin) return ns;
+        }
+    }
+    return wsmc_rank_r(c, Q, N, ratio, scheme, seed, op, slot_base);
+}
+
 template <int IT>
 __device__ __forceinline__ void load_tile_q(int64_t N, int b, const u64* __restrict__ qbuf, u64 (&q)[IT]) {
 #pragma unroll
@@ -721,9 +750,10 @@ __device__ __forceinline__ void fill_chunk_q(int64_t N, int b, int j, u64 Q, u64
     const double ratio = wsmc_u64_to_d(Nr) / wsmc_u64_to_d(Q);
     // the tile's slot range [L, H) = [rank(off), rank(off + Q_b)), ranked by two threads
     // while the others scan; the scan's barrier publishes them
+    const uint64_t key = wsmc_strat_key(plan.seed, opx);   // uniform: the slot hash's key
     if (th < 2) {
         const u64 c = th == 0 ? off : off + qb;
-        sh.LH[th] = wsmc_rank_r(c, Q, Nr, ratio, plan.scheme, plan.seed, opx, (uint64_t)plan.slot_base);
+        sh.LH[th] = rank_fast(c, Q, Nr, ratio, plan.scheme, plan.seed, opx, (uint64_t)plan.slot_base, key);
     }
     if (th == 0) sh.nheavy = 0;
     u64 tot;
@@ -747,8 +777,8 @@ __device__ __forceinline__ void fill_chunk_q(int64_t N, int b, int j, u64 Q, u64
         C += q[k];
         u64 h = prev;                              // a particle with q = 0 owns no slots
         if (q[k] || k == 0) h = MODE == 1 ? (u64)(wsmc_u64_to_d(C) * ratio)
-                                : wsmc_rank_r(C, Q, Nr, ratio, plan.scheme, plan.seed, opx,
-                                              (uint64_t)plan.slot_base);
+                                : rank_fast(C, Q, Nr, ratio, plan.scheme, plan.seed, opx,
+                                            (uint64_t)plan.slot_base, key);
         if (MODE == 1 && h > H) h = H;
         if (MODE == 1 && h < L) h = L;
         hi[k] = h;
