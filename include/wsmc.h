@@ -258,7 +258,11 @@ int wsmc_resample(wsmc_ctx* ctx, double ess_perc_min, int32_t scheme,
  *   targets: d <= 4 scalar columns; lo/hi: per-target bounds (NULL = unbounded);
  *   step: RW step size (std) or autoRW min_step; target_depth: state.depth at the move
  *   (pass -1 to use the context's current depth); diversity: NaN = ungated.
- *   *accepted_out (may be NULL) receives the number of accepted proposals.          */
+ *   *accepted_out (may be NULL) receives the number of accepted proposals. With
+ *   accepted_out NULL the Move is asynchronous (no host wait, as the reference's Move
+ *   returns nothing): a not-positive-definite autoRW covariance leaves the state untouched
+ *   and is reported as WSMC_ENOTPD by the next synchronizing call (wsmc_sync, get_state,
+ *   a download, a waited Resample or Move).                                          */
 int wsmc_move(wsmc_ctx* ctx, int32_t proposal, const int32_t* targets, int32_t d, double step,
               const double* lo, const double* hi, int32_t target_depth, double diversity,
               int64_t* accepted_out);

@@ -349,7 +349,7 @@ class Oracle:
         return (bool(r.value), float(e.value)) if wait else None
 
     def move(self, proposal: int, targets, step: float, lo=None, hi=None, target_depth: int = -1,
-             diversity: float = float("nan")) -> int:
+             diversity: float = float("nan"), wait: bool = True):
         t = np.ascontiguousarray(np.asarray(targets, dtype=np.int32))
         d = len(t)
         lo_a = None if lo is None else np.ascontiguousarray(np.asarray(lo, float).reshape(d))
@@ -361,7 +361,7 @@ class Oracle:
         if r == 3:
             raise np.linalg.LinAlgError("proposal covariance not positive definite")
         self._chk(r)
-        return int(acc.value)
+        return int(acc.value) if wait else None
 
     # ---- one shard's part of the sharded autoRW protocol ----
     def moment_totals(self, targets, pass_: int, M: float, mean=None, lo=None, hi=None) -> np.ndarray:

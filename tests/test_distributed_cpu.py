@@ -77,7 +77,11 @@ class ShardCtx:
         words = np.ascontiguousarray(np.asarray(vals, float)).view(np.uint64)
         return [r.view(np.float64) for r in self.exchange(words)]
 
-    def move(self, proposal, targets, step, lo=None, hi=None, target_depth=-1, diversity=float("nan")):
+    def move(self, proposal, targets, step, lo=None, hi=None, target_depth=-1, diversity=float("nan"), wait=True):
+        acc = self._move(proposal, targets, step, lo, hi, target_depth, diversity)
+        return acc if wait else None
+
+    def _move(self, proposal, targets, step, lo=None, hi=None, target_depth=-1, diversity=float("nan")):
         import math
         from wsmc import abi
         if not math.isnan(diversity):

@@ -380,3 +380,40 @@ def test_oscillator_long_tape_matches_oracle(gpu_available):
     assert models.oscillator_statements(g, t, y, **kw) == models.oscillator_statements(o, t, y, **kw)
     assert_same_state(g, o)
     assert g.log_evidence() == o.log_evidence()
+
+
+@pytest.mark.parametrize("ess", [1.0, 0.5])
+def test_async_moves_match_oracle(gpu_available, ess):
+    """Moves with no accepted count requested run without a host wait (the reference's Move
+    returns nothing); the state equals the oracle's."""
+    xs, ys = models.linreg_data()
+    g, o = wsmc.Context(20001, seed=6), Oracle(20001, seed=6)
+    models.linreg_statements(g, xs, ys, ess_perc_min=ess, wait_moves=False)
+    models.linreg_statements(o, xs, ys, ess_perc_min=ess)
+    assert_same_state(g, o)
+    t, y = models.oscillator_data(n=6)
+    g, o = wsmc.Context(9001, seed=6), Oracle(9001, seed=6)
+    models.oscillator_statements(g, t, y, ess_perc_min=1.0, sweeps=2, diversity=None, wait_moves=False)
+    models.oscillator_statements(o, t, y, ess_perc_min=1.0, sweeps=2, diversity=None)
+    assert_same_state(g, o)
+
+
+def test_async_move_not_pd_reported_at_next_sync(gpu_available):
+    """An asynchronous autoRW with a singular covariance leaves the state untouched and the
+    PosDefException surfaces at the next synchronizing call."""
+    from wsmc.dsl import Normal
+    c, o = wsmc.Context(2048, seed=4), Oracle(2048, seed=4)
+    for x in (c, o):
+        R = models.resolver(x)
+        a, b = x.col_create("a"), x.col_create("b")
+        x.sample(a, Normal(0.0, 1.0).dist(R))
+        x.assign(b, abi.Operand.column(a, coef=2.0))      # b = 2a: rank-1 covariance
+        x.observe(Normal(wsmc.Col("a"), 1.0).dist(R), models._const([0.2]))
+    assert c.move(abi.PROPOSAL_AUTORW, [a, b], 1e-3, wait=False) is None
+    with pytest.raises(wsmc.WSMCError):
+        c.get_state()
+    with pytest.raises(np.linalg.LinAlgError):
+        o.move(abi.PROPOSAL_AUTORW, [a, b], 1e-3)
+    c.move(abi.PROPOSAL_RW, [a], 0.3)
+    o.move(abi.PROPOSAL_RW, [a], 0.3)
+    assert_same_state(c, o)

@@ -17,21 +17,22 @@ import wsmc
 from wsmc import models
 
 
-def c3(N=1_000_000, reps=3):
+def c3(N=1_000_000, reps=3, wait_moves=True):
     xs, ys = models.linreg_data()
     best = math.inf
     for _ in range(reps + 1):
         ctx = wsmc.Context(N, seed=42)
         ctx.sync()
         t0 = time.perf_counter()
-        acc = models.linreg_statements(ctx, xs, ys, ess_perc_min=1.0)
+        acc = models.linreg_statements(ctx, xs, ys, ess_perc_min=1.0, wait_moves=wait_moves)
         ctx.sync()
         dt = time.perf_counter() - t0
         ev = ctx.log_evidence()
         ctx.close()
         best = min(best, dt)
     T = len(xs)
-    return {"config": "C3 linear regression + autoRW (N=1M, T=10, ess 1.0)", "N": N, "T": T,
+    return {"config": "C3 linear regression + autoRW (N=1M, T=10, ess 1.0)"
+                      + ("" if wait_moves else ", asynchronous moves (no accepted counts)"), "N": N, "T": T,
             "seconds_per_run": best, "particle_steps_per_s": N * T / best, "moves": 2 * len(acc),
             "log_evidence": ev}
 
@@ -67,6 +68,7 @@ LEGS = {
     "c5": c5,                                                             # canonical (systematic)
     "c5_stratified": lambda: c5(scheme="stratified"),                     # the reference's scheme
     "c5_example": lambda: c5(sweeps=1, scheme="stratified", ess=0.5, diversity=0.9),   # as written
+    "c3async": lambda: c3(wait_moves=False),
 }
 
 

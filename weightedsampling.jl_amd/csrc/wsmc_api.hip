@@ -465,10 +465,27 @@ static int resolve_decisions(wsmc_ctx* c) {
     return WSMC_OK;
 }
 
+// an asynchronous Move (no accepted count requested) leaves its not-positive-definite flag on
+// the device; the next synchronizing call reads it and reports the reference's PosDefException
+static int check_deferred(wsmc_ctx* c) {
+    if (!c->move_pending) return WSMC_OK;
+    int32_t* hf = reinterpret_cast<int32_t*>(c->pinned) + 1000;
+    WSMC_HIP(hipMemcpyAsync(hf, c->dflag, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    c->move_pending = false;
+    if (hf[0]) {
+        c->scache_terms = -1;
+        WSMC_HIP(hipMemsetAsync(c->dflag, 0, sizeof(int32_t) * 4, c->stream));
+        return fail(WSMC_ENOTPD, "autoRW proposal covariance is not positive definite (an asynchronous Move)");
+    }
+    return WSMC_OK;
+}
+
 int wsmc_sync(wsmc_ctx* c) {
     if (c && c->multi) return multi_sync(c);
     CHECK_CTX(c);
     WSMC_HIP(hipStreamSynchronize(c->stream));
+    if (int r = check_deferred(c)) return r;
     return WSMC_OK;
 }
 
@@ -482,6 +499,7 @@ int wsmc_get_state(wsmc_ctx* c, wsmc_state* s) {
     if (c && c->multi) return s ? multi_get_state(c, s) : fail(WSMC_EARG, "null argument");
     if (!c || !s) return fail(WSMC_EARG, "null argument");
     if (int r = resolve_decisions(c)) return r;
+    if (int r = check_deferred(c)) return r;
     s->resampled = c->resampled;
     s->weights_changed = c->weights_changed;
     s->depth = c->depth;
@@ -622,6 +640,7 @@ int wsmc_col_download(wsmc_ctx* c, int32_t col, double* host) {
     CHECK_CTX(c);
     if (!valid_col(c, col) || !host) return fail(WSMC_EARG, "bad column or null buffer");
     if (int r = need_cols(c, {col})) return r;
+    if (int r = check_deferred(c)) return r;
     WSMC_HIP(hipMemcpyAsync(host, c->cols[col].front, sizeof(double) * c->cols[col].dim * c->N,
                             hipMemcpyDeviceToHost, c->stream));
     WSMC_HIP(hipStreamSynchronize(c->stream));
@@ -719,6 +738,7 @@ int wsmc_weights_download(wsmc_ctx* c, double* host) {
     if (c && c->multi) return host ? multi_weights(c, nullptr, host) : fail(WSMC_EARG, "null buffer");
     CHECK_CTX(c);
     if (!host) return fail(WSMC_EARG, "null buffer");
+    if (int r = check_deferred(c)) return r;
     WSMC_HIP(hipMemcpyAsync(host, c->w, sizeof(double) * c->N, hipMemcpyDeviceToHost, c->stream));
     WSMC_HIP(hipStreamSynchronize(c->stream));
     return WSMC_OK;
@@ -1169,6 +1189,7 @@ int wsmc_weighted_moments(wsmc_ctx* c, const wsmc_operand* exprs, int32_t d, dou
     CHECK_CTX(c);
     if (!exprs || !mean || d < 1 || d > 4) return fail(WSMC_EARG, "need 1..4 expressions and a mean buffer");
     std::vector<int32_t> reads;
+    if (int r = check_deferred(c)) return r;   // the moment kernels share the flag word
     for (int k = 0; k < d; ++k) {
         int r = check_operand(c, exprs[k]);
         if (r) return r;
@@ -1823,8 +1844,10 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
     // no flag requested: the decision stays on the device (gated gather / weight reset), no
     // host round trip; it is folded into the host state at the next read
     const bool async = !resampled_out && !ess_out && !exact_mode(c);
-    if (!async)
+    if (!async) {
         if (int r = resolve_decisions(c)) return r;
+        if (int r = check_deferred(c)) return r;
+    }
     if (!c->weights_changed) {
         if (resampled_out) *resampled_out = c->resampled;
         if (ess_out) *ess_out = c->last_ess;
@@ -2225,8 +2248,12 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
     if (!r) r = upload_colptr(c);
     if (!r) r = upload_tape(c);
     if (r) return r;
-    WSMC_HIP(hipMemsetAsync(c->dflag, 0, sizeof(int32_t) * 4, c->stream));
-    WSMC_HIP(hipMemsetAsync(c->ucount, 0, sizeof(unsigned long long) * 4, c->stream));
+    // asynchronous (no count requested): no host wait; a pending failure flag stays set (the
+    // kernels skip on it) until the next synchronizing call reports it
+    const bool async = !accepted_out && !is_sharded(c);
+    if (!async && (r = check_deferred(c))) return r;
+    if (!c->move_pending) WSMC_HIP(hipMemsetAsync(c->dflag, 0, sizeof(int32_t) * 4, c->stream));
+    if (accepted_out) WSMC_HIP(hipMemsetAsync(c->ucount, 0, sizeof(unsigned long long) * 4, c->stream));
     if (proposal == WSMC_PROPOSAL_AUTORW && is_sharded(c)) {
         int rr = sharded_autorw(c, targets, d, bounded ? l : nullptr, bounded ? h : nullptr, step);
         if (rr) return rr;
@@ -2332,6 +2359,11 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         WSMC_HIP(launch_move(c->stream, c->d_tape, (int32_t)c->tape.size(), target_depth, c->d_colptr, targets, d,
                              bounded ? l : nullptr, bounded ? h : nullptr, bounded ? 1 : 0, c->mom + 32, c->seed,
                              op_prop, op_acc, c->goff, c->N, c->ucount, mflag, c->scache, cache_from));
+    }
+    if (async) {
+        c->scache_terms = kD;
+        c->move_pending = true;
+        return WSMC_OK;
     }
     struct {
         int32_t flag[4];

@@ -221,6 +221,7 @@ struct wsmc_ctx {
     int32_t* anc_last = nullptr;            // wsmc_last_ancestors: newest row known to have resampled
     int64_t anc_last_epoch = -1;
     wsmc::Decision* dec_always = nullptr;   // [1] resampled = 1 (explicit resample!(store, idx))
+    bool move_pending = false;              // an asynchronous Move's PD flag not yet read back
 
     // fused runner state
     int32_t T_alloc = 0;

@@ -295,7 +295,9 @@ class Context:
         return bool(r.value), float(e.value)
 
     def move(self, proposal: int, targets, step: float, lo=None, hi=None, target_depth: int = -1,
-             diversity: float = math.nan) -> int:
+             diversity: float = math.nan, wait: bool = True):
+        """Move.apply!; returns the accepted count. wait=False: asynchronous (returns None; a
+        PosDefException surfaces at the next synchronizing call)."""
         t = np.ascontiguousarray(np.asarray(targets, dtype=np.int32))
         d = len(t)
         lo_a = None if lo is None else np.ascontiguousarray(np.asarray(lo, float).reshape(d))
@@ -303,11 +305,11 @@ class Context:
         acc = C.c_int64()
         rc = self._L.wsmc_move(self._h, int(proposal), t.ctypes.data_as(_I32P), d, float(step),
                                None if lo_a is None else _dptr(lo_a), None if hi_a is None else _dptr(hi_a),
-                               int(target_depth), float(diversity), C.byref(acc))
+                               int(target_depth), float(diversity), C.byref(acc) if wait else None)
         if rc == abi.WSMC_ENOTPD:
             raise np.linalg.LinAlgError(self._L.wsmc_last_error().decode())
         check(rc)
-        return int(acc.value)
+        return int(acc.value) if wait else None
 
     def score(self, target_depth: int) -> np.ndarray:
         out = np.empty(self.n)

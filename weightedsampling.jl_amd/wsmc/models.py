@@ -117,7 +117,7 @@ def lgssm1d_statements(ctx, data, a=0.9, q=1.0, r=0.5, x0_std=1.0, ess_perc_min=
 
 
 def linreg_statements(ctx, xs, ys, prior_sd=10.0, obs_sd=1.0, ess_perc_min=0.5,
-                      scheme=abi.RESAMPLE_STRATIFIED, min_step=1e-3):
+                      scheme=abi.RESAMPLE_STRATIFIED, min_step=1e-3, wait_moves=True):
     """examples/linear_regression.jl:17-27: α, β ~ N(0,10); y => N(α + β x, 1);
     `if resampled; α << autoRW(); β << autoRW(); end`."""
     R = resolver(ctx)
@@ -131,15 +131,15 @@ def linreg_statements(ctx, xs, ys, prior_sd=10.0, obs_sd=1.0, ess_perc_min=0.5,
     for x, y in zip(xs, ys):
         ctx.observe(Normal(Col("α") + Col("β") * float(x), obs_sd).dist(R), _const([y]))
         rs, _ = ctx.resample(ess_perc_min, scheme)
-        if rs:
-            a1 = ctx.move(abi.PROPOSAL_AUTORW, [ca], min_step)
-            a2 = ctx.move(abi.PROPOSAL_AUTORW, [cb], min_step)
+        if rs:   # `if resampled` reads the flag; the moves need not return their counts
+            a1 = ctx.move(abi.PROPOSAL_AUTORW, [ca], min_step, wait=wait_moves)
+            a2 = ctx.move(abi.PROPOSAL_AUTORW, [cb], min_step, wait=wait_moves)
             accepted.append((a1, a2))
     return accepted
 
 
 def oscillator_statements(ctx, t_obs, y_obs, ess_perc_min=0.5, scheme=abi.RESAMPLE_STRATIFIED,
-                          sweeps=1, diversity=0.9, min_step=1e-3):
+                          sweeps=1, diversity=0.9, min_step=1e-3, wait_moves=True):
     """examples/damped_oscillator.jl:30-43 with `sweeps` repetitions of the two moves."""
     R = resolver(ctx)
     names = ["A", "ω", "γ", "ϕ", "σ"]
@@ -158,9 +158,9 @@ def oscillator_statements(ctx, t_obs, y_obs, ess_perc_min=0.5, scheme=abi.RESAMP
         ctx.resample(ess_perc_min, scheme)
         for _ in range(sweeps):
             a1 = ctx.move(abi.PROPOSAL_AUTORW, joint, min_step, lo=[0.0] * 4, hi=[math.inf] * 4,
-                          diversity=div)
+                          diversity=div, wait=wait_moves)
             a2 = ctx.move(abi.PROPOSAL_AUTORW, [cols["ϕ"]], min_step, lo=[-math.pi], hi=[math.pi],
-                          diversity=div)
+                          diversity=div, wait=wait_moves)
             accepted.append((a1, a2))
     return accepted
 
