@@ -357,6 +357,12 @@ def main():
                                          else "lazy genealogy)") if args.statements else ""),
                        "n_particles_per_gpu": N, "global_particles": gN, "T": T,
                        "ess_perc_min": args.ess, "scheme": args.scheme, "keep_history": not args.no_history,
+                       # island shards resample within themselves after the global decision: a
+                       # different (unbiased) estimator than the reference's single-population
+                       # Resample, which exact shards reproduce bit for bit
+                       "estimator": ("reference (single population)" if (world == 1 and not args.rccl_one_rank)
+                                     or args.shard_mode == "exact"
+                                     else "island resampling (per-shard strata, global decision)"),
                        "parallelism": (f"{args.shard_mode}-shard x{world}"
                                        + (" (host exchange, test mode)" if args.exchange == "host" else ""))
                            if world > 1 else ("single GPU, one-rank RCCL communicator (diagnostic)"
