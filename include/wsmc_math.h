@@ -201,6 +201,30 @@ WSMC_HD double wsmc_expw(double x) {
     return p * wsmc_pow2i((int)kd);
 }
 
+/* exp without a division (the damped-oscillator mean, evaluated O(t) times per particle per
+ * Move fold): for |x| <= 700 the Cody-Waite reduction and degree-13 Taylor polynomial of
+ * wsmc_expw (~2 ulp) scaled by 2^k in the normal range; wsmc_exp elsewhere (and NaN). */
+WSMC_HD double wsmc_exp_nd(double x) {
+    if (!(x >= -700.0 && x <= 700.0)) return wsmc_exp(x);
+    const double kd = wsmc_floor(x * 1.44269504088896338700e+00 + 0.5);
+    const double r = (x - kd * 6.93147180369123816490e-01) - kd * 1.90821492927058770002e-10;
+    double p = 1.6059043836821613e-10;                 /* 1/13! */
+    p = __builtin_fma(p, r, 2.08767569878681e-09);
+    p = __builtin_fma(p, r, 2.505210838544172e-08);
+    p = __builtin_fma(p, r, 2.755731922398589e-07);
+    p = __builtin_fma(p, r, 2.7557319223985893e-06);
+    p = __builtin_fma(p, r, 2.48015873015873e-05);
+    p = __builtin_fma(p, r, 0.0001984126984126984);
+    p = __builtin_fma(p, r, 0.001388888888888889);
+    p = __builtin_fma(p, r, 0.008333333333333333);
+    p = __builtin_fma(p, r, 0.041666666666666664);
+    p = __builtin_fma(p, r, 0.16666666666666666);
+    p = __builtin_fma(p, r, 0.5);
+    p = __builtin_fma(p, r, 1.0);
+    p = __builtin_fma(p, r, 1.0);
+    return p * wsmc_pow2i((int)kd);
+}
+
 WSMC_HD double wsmc_log(double x) {
     const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
                  Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
@@ -360,7 +384,9 @@ WSMC_HD uint32_t wsmc_strat_word(uint64_t seed, uint64_t op, uint64_t n) {
 /* ------------------------------------------------------------------------- */
 /* Normal(mu, sigma): -(z^2 + log(2pi))/2 - log(sigma),  z = (x - mu)/sigma     */
 WSMC_HD double wsmc_normal_logpdf(double mu, double sigma, double x) {
-    double z = (x - mu) / sigma;
+    /* z = (x - mu) * (1 / sigma): one reciprocal per sigma value, reused across the terms of
+       a fold that share it (wsmc_scale_memo) — a multiply per term where a division was */
+    double z = (x - mu) * (1.0 / sigma);
     return -(z * z + WSMC_LOG2PI) * 0.5 - wsmc_log(sigma);
 }
 /* Truncated(Normal(0, sigma), 0, Inf) — examples/damped_oscillator.jl:24-28 */
@@ -375,7 +401,7 @@ WSMC_HD double wsmc_uniform_logpdf(double a, double b, double x) {
 }
 /* the damped-oscillator mean, examples/damped_oscillator.jl:11 */
 WSMC_HD double wsmc_oscillator(double t, double A, double om, double ga, double ph) {
-    return A * wsmc_exp(-ga * t) * wsmc_cos(om * t + ph);
+    return A * wsmc_exp_nd(-ga * t) * wsmc_cos(om * t + ph);
 }
 
 /* ------------------------------------------------------------------------- */

@@ -52,39 +52,57 @@ WSMC_HD double wsmc_dist_mean(const wsmc_dist* d, int k, double* const* cols, in
     return wsmc_operand_eval(&d->mu[k], cols, N, i, ov);
 }
 
-/* log of a scale parameter, remembered across the terms of one fold: a particle's terms
- * often share one sigma / variance value (e.g. a sigma column), and the log of the same
- * bits is the same bits, so reusing it changes nothing but the work. */
+/* log and reciprocal of a scale parameter, remembered across the terms of one fold: a
+ * particle's terms often share one sigma / variance value (e.g. a sigma column), and the
+ * log / reciprocal of the same bits are the same bits, so reusing them changes nothing but
+ * the work. */
 typedef struct {
     uint64_t arg;
-    double val;
+    double val;      /* log(arg) */
+    double rcp;      /* 1 / arg  */
     int valid;
 } wsmc_logmemo;
-WSMC_HD double wsmc_log_memo(wsmc_logmemo* m, double x) {
-    if (!m) return wsmc_log(x);
+WSMC_HD void wsmc_scale_memo(wsmc_logmemo* m, double x, double* lg, double* rc) {
+    if (!m) {
+        *lg = wsmc_log(x);
+        *rc = 1.0 / x;
+        return;
+    }
     uint64_t b = wsmc_d2bits(x);
-    if (m->valid && m->arg == b) return m->val;
-    m->arg = b;
-    m->val = wsmc_log(x);
-    m->valid = 1;
-    return m->val;
+    if (!(m->valid && m->arg == b)) {
+        m->arg = b;
+        m->val = wsmc_log(x);
+        m->rcp = 1.0 / x;
+        m->valid = 1;
+    }
+    *lg = m->val;
+    *rc = m->rcp;
+}
+WSMC_HD double wsmc_log_memo(wsmc_logmemo* m, double x) {
+    double lg, rc;
+    wsmc_scale_memo(m, x, &lg, &rc);
+    return lg;
 }
 
 /* logpdf(D(args...), x) for the supported families */
 WSMC_HD double wsmc_dist_logpdf_m(const wsmc_dist* d, const double* x, double* const* cols, int64_t N,
                                   int64_t i, const wsmc_override* ov, wsmc_logmemo* lm) {
     switch (d->family) {
-        case WSMC_FAM_NORMAL: {   /* wsmc_normal_logpdf with a remembered log(sigma) */
+        case WSMC_FAM_NORMAL: {   /* wsmc_normal_logpdf with a remembered log(sigma), 1/sigma */
             double mu = wsmc_dist_mean(d, 0, cols, N, i, ov);
             double sg = wsmc_operand_eval(&d->scale, cols, N, i, ov);
-            double z = (x[0] - mu) / sg;
-            return -(z * z + WSMC_LOG2PI) * 0.5 - wsmc_log_memo(lm, sg);
+            double lg, rc;
+            wsmc_scale_memo(lm, sg, &lg, &rc);
+            double z = (x[0] - mu) * rc;
+            return -(z * z + WSMC_LOG2PI) * 0.5 - lg;
         }
         case WSMC_FAM_HALFNORMAL: {   /* wsmc_halfnormal_logpdf likewise */
             double sg = wsmc_operand_eval(&d->scale, cols, N, i, ov);
             if (!(x[0] >= 0.0)) return -WSMC_INF;
-            double z = (x[0] - 0.0) / sg;
-            return (-(z * z + WSMC_LOG2PI) * 0.5 - wsmc_log_memo(lm, sg)) + WSMC_LOG2;
+            double lg, rc;
+            wsmc_scale_memo(lm, sg, &lg, &rc);
+            double z = (x[0] - 0.0) * rc;
+            return (-(z * z + WSMC_LOG2PI) * 0.5 - lg) + WSMC_LOG2;
         }
         case WSMC_FAM_UNIFORM:
             return wsmc_uniform_logpdf(d->param[0], d->param[1], x[0]);
@@ -163,7 +181,7 @@ WSMC_HD double wsmc_term_logpdf(const wsmc_term* t, double* const* cols, int64_t
 WSMC_HD double wsmc_fold(const wsmc_term* terms, int32_t n, int32_t target_depth, double* const* cols,
                          int64_t N, int64_t i, const wsmc_override* ov) {
     double s = 0.0;
-    wsmc_logmemo lm = {0, 0.0, 0};
+    wsmc_logmemo lm = {0, 0.0, 0.0, 0};
     for (int32_t j = 0; j < n; ++j) {
         if (terms[j].depth >= target_depth) break;
         s = s + wsmc_term_logpdf_m(&terms[j], cols, N, i, ov, &lm);
@@ -176,7 +194,7 @@ WSMC_HD double wsmc_fold(const wsmc_term* terms, int32_t n, int32_t target_depth
 WSMC_HD double wsmc_fold_from(double s0, const wsmc_term* terms, int32_t j0, int32_t n, int32_t target_depth,
                               double* const* cols, int64_t N, int64_t i, const wsmc_override* ov) {
     double s = s0;
-    wsmc_logmemo lm = {0, 0.0, 0};
+    wsmc_logmemo lm = {0, 0.0, 0.0, 0};
     for (int32_t j = j0; j < n; ++j) {
         if (terms[j].depth >= target_depth) break;
         s = s + wsmc_term_logpdf_m(&terms[j], cols, N, i, ov, &lm);

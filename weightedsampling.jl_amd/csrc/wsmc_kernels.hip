@@ -1548,21 +1548,21 @@ __device__ __forceinline__ void fold_seg(double (&s)[K], const wsmc_term* tape, 
                                          const bool (&ok)[K]) {
     wsmc_logmemo lm[K];
 #pragma unroll
-    for (int p = 0; p < K; ++p) lm[p] = wsmc_logmemo{0, 0.0, 0};
+    for (int p = 0; p < K; ++p) lm[p] = wsmc_logmemo{0, 0.0, 0.0, 0};
     for (int32_t g = 0; g < nseg; ++g) {
         const FoldSeg sg = segs[g];
         const wsmc_term* tp = &tape[sg.tmpl];
         if (sg.kind == kSegNormalOsc) {
             // Normal(A exp(-gamma t) cos(omega t + phi), sigma) observed at y, over (t, y) pairs
-            double A[K], om[K], ga[K], ph[K], sd[K], lsd[K];
+            double A[K], om[K], ga[K], ph[K], rsd[K], lsd[K];
 #pragma unroll
             for (int p = 0; p < K; ++p) {
                 A[p] = wsmc_operand_eval(&tp->dist.mu[0], cols, 0, ix[p], nullptr);
                 om[p] = wsmc_operand_eval(&tp->dist.mu[1], cols, 0, ix[p], nullptr);
                 ga[p] = wsmc_operand_eval(&tp->dist.mu[2], cols, 0, ix[p], nullptr);
                 ph[p] = wsmc_operand_eval(&tp->dist.mu[3], cols, 0, ix[p], nullptr);
-                sd[p] = wsmc_operand_eval(&tp->dist.scale, cols, 0, ix[p], nullptr);
-                lsd[p] = wsmc_log_memo(&lm[p], sd[p]);
+                const double sd = wsmc_operand_eval(&tp->dist.scale, cols, 0, ix[p], nullptr);
+                wsmc_scale_memo(&lm[p], sd, &lsd[p], &rsd[p]);
             }
             const double* c = cst + sg.coff;
             for (int32_t k = 0; k < sg.count; ++k) {
@@ -1571,7 +1571,7 @@ __device__ __forceinline__ void fold_seg(double (&s)[K], const wsmc_term* tape, 
                 for (int p = 0; p < K; ++p) {
                     if (!ok[p]) continue;
                     const double mu = wsmc_oscillator(t, A[p], om[p], ga[p], ph[p]);
-                    const double z = (y - mu) / sd[p];
+                    const double z = (y - mu) * rsd[p];
                     s[p] = s[p] + (-(z * z + WSMC_LOG2PI) * 0.5 - lsd[p]);
                 }
             }
@@ -1581,13 +1581,13 @@ __device__ __forceinline__ void fold_seg(double (&s)[K], const wsmc_term* tape, 
             // Normal(c0 + coef0 col0 + coef1 col1, sigma) observed at y, over (c0, coef0, coef1, y)
             const wsmc_operand& m = tp->dist.mu[0];
             const bool h0 = m.col[0] >= 0, h1 = m.col[1] >= 0;
-            double v0[K], v1[K], sd[K], lsd[K];
+            double v0[K], v1[K], rsd[K], lsd[K];
 #pragma unroll
             for (int p = 0; p < K; ++p) {
                 v0[p] = h0 ? cols[m.col[0]][ix[p]] : 0.0;
                 v1[p] = h1 ? cols[m.col[1]][ix[p]] : 0.0;
-                sd[p] = wsmc_operand_eval(&tp->dist.scale, cols, 0, ix[p], nullptr);
-                lsd[p] = wsmc_log_memo(&lm[p], sd[p]);
+                const double sd = wsmc_operand_eval(&tp->dist.scale, cols, 0, ix[p], nullptr);
+                wsmc_scale_memo(&lm[p], sd, &lsd[p], &rsd[p]);
             }
             const double* c = cst + sg.coff;
             for (int32_t k = 0; k < sg.count; ++k) {
@@ -1598,7 +1598,7 @@ __device__ __forceinline__ void fold_seg(double (&s)[K], const wsmc_term* tape, 
                     double mu = c0;
                     if (h0) mu = mu + a0 * v0[p];
                     if (h1) mu = mu + a1 * v1[p];
-                    const double z = (y - mu) / sd[p];
+                    const double z = (y - mu) * rsd[p];
                     s[p] = s[p] + (-(z * z + WSMC_LOG2PI) * 0.5 - lsd[p]);
                 }
             }
@@ -1970,11 +1970,12 @@ hipError_t launch_sample_importance(hipStream_t s, double* out, int dim, const w
 }
 hipError_t launch_weigh(hipStream_t s, const wsmc_term& t, double* w, double* const* cols, int64_t N, MaxSlots* ms,
                         MaxSlots* ms_next) {
-    wsmc_logmemo lm0 = {0, 0.0, 0};
+    wsmc_logmemo lm0 = {0, 0.0, 0.0, 0};
     if (t.dist.family != WSMC_FAM_UNIFORM && wsmc_operand_is_const(&t.dist.scale)) {
         const double sc = wsmc_operand_eval(&t.dist.scale, nullptr, N, 0, nullptr);
         lm0.arg = wsmc_d2bits(sc);
         lm0.val = wsmc_log(sc);
+        lm0.rcp = 1.0 / sc;
         lm0.valid = 1;
     }
     hipLaunchKernelGGL(k_weigh, grid_for(N), dim3(kBlock), 0, s, t, w, cols, N, ms, ms_next, lm0);
