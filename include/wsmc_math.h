@@ -403,6 +403,62 @@ WSMC_HD double wsmc_uniform_logpdf(double a, double b, double x) {
 WSMC_HD double wsmc_oscillator(double t, double A, double om, double ga, double ph) {
     return A * wsmc_exp_nd(-ga * t) * wsmc_cos(om * t + ph);
 }
+/* sin and cos with wsmc_cos's reduction and kernels: *c is wsmc_cos(x) bit for bit */
+WSMC_HD void wsmc_sincos(double x, double* s, double* c) {
+    const double invpio2 = 6.36619772367581382433e-01, p1 = 1.57079632673412561417e+00,
+                 p2 = 6.07710050630396597660e-11, p3 = 2.02226624879595063154e-21;
+    if (!wsmc_isfinite(x)) {
+        *s = WSMC_NAN;
+        *c = WSMC_NAN;
+        return;
+    }
+    const double ax = wsmc_fabs(x);
+    const int small = ax <= 7.85398163397448278999e-01;
+    const double fn = (double)(int64_t)(ax * invpio2 + 0.5);
+    const double rr = ((ax - fn * p1) - fn * p2) - fn * p3;
+    const double r = small ? x : rr;
+    const int n = small ? 0 : (int)((int64_t)fn & 3);
+    const double kc = wsmc_kcos(r), ks = wsmc_ksin(r);
+    const double vc = (n & 1) ? ks : kc;
+    *c = ((n + 1) & 2) ? -vc : vc;              /* cos(r + n pi/2): kc, -ks, -kc, ks */
+    const double vs = (n & 1) ? kc : ks;
+    const double sa = (n & 2) ? -vs : vs;       /* sin(r + n pi/2): ks, kc, -ks, -kc */
+    *s = (!small && x < 0.0) ? -sa : sa;        /* reduced from |x|: sin is odd */
+}
+/* The oscillator mean by rotation (a restatement within floating-point
+ * tolerance of examples/damped_oscillator.jl:11): the phasor z(t) = A e^{-g t} e^{i(w t + p)}
+ * at an anchor t_a (Re z(t_a) is wsmc_oscillator(t_a, ...) bit for bit), advanced m times by
+ * R = e^{(-g + i w) d}: Re z(t_a + m d) at one complex multiply per step instead of an exp and
+ * a cos per term. The Observe terms of a regularly spaced run carry (t_a, d, m) (wsmc_osc_link). */
+WSMC_HD void wsmc_osc_anchor(double ta, double A, double om, double ga, double ph, double* zr, double* zi) {
+    double s, c;
+    wsmc_sincos(om * ta + ph, &s, &c);
+    const double ae = A * wsmc_exp_nd(-ga * ta);
+    *zr = ae * c;
+    *zi = ae * s;
+}
+WSMC_HD void wsmc_osc_step(double d, double om, double ga, double* rr, double* ri) {
+    double s, c;
+    wsmc_sincos(om * d, &s, &c);
+    const double e = wsmc_exp_nd(-ga * d);
+    *rr = e * c;
+    *ri = e * s;
+}
+WSMC_HD void wsmc_osc_rotate(double* zr, double* zi, double rr, double ri) {
+    const double a = *zr, b = *zi;
+    *zr = __builtin_fma(a, rr, -(b * ri));
+    *zi = __builtin_fma(a, ri, b * rr);
+}
+WSMC_HD double wsmc_osc_rolled(double ta, double d, int m, double A, double om, double ga, double ph) {
+    double zr, zi;
+    wsmc_osc_anchor(ta, A, om, ga, ph, &zr, &zi);
+    if (m > 0) {
+        double rr, ri;
+        wsmc_osc_step(d, om, ga, &rr, &ri);
+        for (int j = 0; j < m; ++j) wsmc_osc_rotate(&zr, &zi, rr, ri);
+    }
+    return zr;
+}
 
 /* ------------------------------------------------------------------------- */
 /* bound transforms of RW/autoRW (src/move_kernels.jl:37-85)                  */

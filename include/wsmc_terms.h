@@ -47,6 +47,8 @@ WSMC_HD double wsmc_dist_mean(const wsmc_dist* d, int k, double* const* cols, in
         double om = wsmc_operand_eval(&d->mu[1], cols, N, i, ov);
         double ga = wsmc_operand_eval(&d->mu[2], cols, N, i, ov);
         double ph = wsmc_operand_eval(&d->mu[3], cols, N, i, ov);
+        /* reserved = m > 0: a linked Observe term, the mean at param[0] + m param[1] by rotation */
+        if (d->reserved > 0) return wsmc_osc_rolled(d->param[0], d->param[1], d->reserved, A, om, ga, ph);
         return wsmc_oscillator(d->param[0], A, om, ga, ph);
     }
     return wsmc_operand_eval(&d->mu[k], cols, N, i, ov);
@@ -164,6 +166,73 @@ WSMC_HD void wsmc_dist_sample(const wsmc_dist* d, double* x, uint64_t seed, uint
 }
 /* the operand is a constant (reads no column) */
 WSMC_HD int wsmc_operand_is_const(const wsmc_operand* o) { return o->col[0] < 0 && o->col[1] < 0; }
+
+/* Link an oscillator Observe term to the tape's previous term (prev, null at the start): when
+ * prev is an oscillator Observe of the same operands and the times continue its block's
+ * regular step (|t - (t_a + m d)| <= 64 eps (1 + |t|)), the term becomes (t_a, d, m) =
+ * (dist.param[0], dist.param[1], dist.reserved) of its block; blocks hold at most
+ * WSMC_OSC_BLOCK terms. Otherwise it opens a block (m = 0: the direct evaluation). Called
+ * before the term is first evaluated, by the device library and the oracle alike. */
+#define WSMC_OSC_BLOCK 16
+WSMC_HD int wsmc_operand_same(const wsmc_operand* a, const wsmc_operand* b) {
+    return wsmc_d2bits(a->c0) == wsmc_d2bits(b->c0) && wsmc_d2bits(a->coef[0]) == wsmc_d2bits(b->coef[0]) &&
+           wsmc_d2bits(a->coef[1]) == wsmc_d2bits(b->coef[1]) && a->col[0] == b->col[0] && a->col[1] == b->col[1] &&
+           a->comp[0] == b->comp[0] && a->comp[1] == b->comp[1];
+}
+WSMC_HD int wsmc_osc_term(const wsmc_term* t) {
+    return t->kind == WSMC_TERM_OBSERVE && t->dist.family == WSMC_FAM_NORMAL && t->dist.dim <= 1 &&
+           t->dist.mean_fn == WSMC_MEAN_OSCILLATOR;
+}
+WSMC_HD void wsmc_osc_link(const wsmc_term* prev, wsmc_term* t) {
+    if (t->dist.mean_fn != WSMC_MEAN_OSCILLATOR) return;
+    t->dist.reserved = 0;
+    t->dist.param[1] = 0.0;
+    if (!prev || !wsmc_osc_term(t) || !wsmc_osc_term(prev)) return;
+    for (int k = 0; k < 4; ++k)
+        if (!wsmc_operand_same(&prev->dist.mu[k], &t->dist.mu[k])) return;
+    if (!wsmc_operand_same(&prev->dist.scale, &t->dist.scale)) return;
+    const int mp = prev->dist.reserved;
+    if (mp + 1 >= WSMC_OSC_BLOCK) return;
+    const double ta = prev->dist.param[0], tk = t->dist.param[0];
+    if (!wsmc_isfinite(ta) || !wsmc_isfinite(tk)) return;
+    const double d = mp == 0 ? tk - ta : prev->dist.param[1];   /* a block's step: its second term */
+    if (!wsmc_isfinite(d) || d == 0.0) return;
+    if (mp > 0 && wsmc_fabs((ta + (double)(mp + 1) * d) - tk) > 1.4210854715202004e-14 * (1.0 + wsmc_fabs(tk)))
+        return;
+    t->dist.param[0] = ta;
+    t->dist.param[1] = d;
+    t->dist.reserved = mp + 1;
+}
+
+/* a scalar Normal (affine mean) / HalfNormal / Uniform term: wsmc_term_logpdf_m's arithmetic
+ * for those families, without the other families' code (the device Move's lean fold) */
+WSMC_HD int wsmc_term_is_scalar(const wsmc_term* t) {
+    return t->dist.dim <= 1 && t->dist.mean_fn != WSMC_MEAN_OSCILLATOR &&
+           (t->dist.family == WSMC_FAM_NORMAL || t->dist.family == WSMC_FAM_HALFNORMAL ||
+            t->dist.family == WSMC_FAM_UNIFORM);
+}
+WSMC_HD double wsmc_scalar_term_logpdf_m(const wsmc_term* t, double* const* cols, int64_t N, int64_t i,
+                                         const wsmc_override* ov, wsmc_logmemo* lm) {
+    const wsmc_dist* d = &t->dist;
+    const double x0 = wsmc_operand_eval(&t->x[0], cols, N, i, ov);
+    if (d->family == WSMC_FAM_NORMAL) {
+        double mu = wsmc_operand_eval(&d->mu[0], cols, N, i, ov);
+        double sg = wsmc_operand_eval(&d->scale, cols, N, i, ov);
+        double lg, rc;
+        wsmc_scale_memo(lm, sg, &lg, &rc);
+        double z = (x0 - mu) * rc;
+        return -(z * z + WSMC_LOG2PI) * 0.5 - lg;
+    }
+    if (d->family == WSMC_FAM_HALFNORMAL) {
+        double sg = wsmc_operand_eval(&d->scale, cols, N, i, ov);
+        if (!(x0 >= 0.0)) return -WSMC_INF;
+        double lg, rc;
+        wsmc_scale_memo(lm, sg, &lg, &rc);
+        double z = (x0 - 0.0) * rc;
+        return (-(z * z + WSMC_LOG2PI) * 0.5 - lg) + WSMC_LOG2;
+    }
+    return wsmc_uniform_logpdf(d->param[0], d->param[1], x0);
+}
 
 WSMC_HD double wsmc_term_logpdf_m(const wsmc_term* t, double* const* cols, int64_t N, int64_t i,
                                   const wsmc_override* ov, wsmc_logmemo* lm) {

@@ -255,10 +255,11 @@ static int or_weigh(oracle* o, const wsmc_dist* d, const wsmc_operand* x, int ki
     memset(&t, 0, sizeof(t));
     t.dist = *d;
     for (int k = 0; k < 4; ++k) t.x[k] = x[k < d->dim ? k : 0];
-    for (int64_t i = 0; i < N; ++i) o->w[i] = o->w[i] + wsmc_term_logpdf(&t, o->colptr, N, i, 0);
-    o->weights_changed = 1;
     t.kind = kind;
     t.depth = o->depth;
+    wsmc_osc_link(o->nterms ? &o->tape[o->nterms - 1] : 0, &t);   /* before its first evaluation */
+    for (int64_t i = 0; i < N; ++i) o->w[i] = o->w[i] + wsmc_term_logpdf(&t, o->colptr, N, i, 0);
+    o->weights_changed = 1;
     or_tape_push(o, &t);
     o->depth += 1;
     return 0;

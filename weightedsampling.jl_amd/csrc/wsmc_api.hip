@@ -1814,6 +1814,7 @@ static int weigh(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x, int kin
     }
     t.kind = kind;
     t.depth = c->depth;
+    wsmc_osc_link(c->tape.empty() ? nullptr : &c->tape.back(), &t);   // before its first evaluation
     std::vector<int32_t> reads;
     cols_of(t, reads);
     if ((r = need_cols(c, reads))) return r;
@@ -2179,7 +2180,8 @@ static bool same_run(const wsmc_term& a, const wsmc_term& b, int kind) {
     for (int k = 0; k < 4; ++k)
         if (!same_operand(a.dist.mu[k], b.dist.mu[k], !osc && k == 0, !osc && k == 0, !osc && k == 0)) return false;
     if (!same_operand(a.dist.scale, b.dist.scale, false, false, false)) return false;
-    if (!(osc || same_bits(a.dist.param[0], b.dist.param[0])) || !same_bits(a.dist.param[1], b.dist.param[1]))
+    // oscillator runs: param[0], param[1], reserved are the per-term (t_a, d, m) (wsmc_osc_link)
+    if (!osc && (!same_bits(a.dist.param[0], b.dist.param[0]) || !same_bits(a.dist.param[1], b.dist.param[1])))
         return false;
     return same_operand(a.x[0], b.x[0], true, false, false);   // x[0].c0 = the observation
 }
@@ -2192,7 +2194,9 @@ static int32_t compile_fold(const std::vector<wsmc_term>& ct, int32_t j0, int32_
         int32_t e = j + 1;
         if (kind != kSegTerm)
             while (e < j1 && same_run(ct[j], ct[e], kind)) ++e;
-        if (kind == kSegTerm || e - j < 2) {
+        // a lone Normal-affine term stays a one-term segment; a lone oscillator term is a run
+        // of one (the lean fold carries no generic oscillator evaluation)
+        if (kind == kSegTerm || (kind == kSegNormalAff && e - j < 2)) {
             segs.push_back(FoldSeg{kSegTerm, 1, j, 0});
             ++j;
             continue;
@@ -2200,8 +2204,10 @@ static int32_t compile_fold(const std::vector<wsmc_term>& ct, int32_t j0, int32_
         segs.push_back(FoldSeg{kind, e - j, j, (int32_t)cst.size()});
         for (int32_t k = j; k < e; ++k) {
             const wsmc_term& t = ct[k];
-            if (kind == kSegNormalOsc) {
+            if (kind == kSegNormalOsc) {   // (t_a, d, m) of the term's rotation block
                 cst.push_back(t.dist.param[0]);
+                cst.push_back(t.dist.param[1]);
+                cst.push_back((double)t.dist.reserved);
             } else {
                 cst.push_back(t.dist.mu[0].c0);
                 cst.push_back(t.dist.mu[0].coef[0]);
@@ -2245,8 +2251,7 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
     std::vector<int32_t> reads(targets, targets + d);
     for (const auto& t : c->tape) cols_of(t, reads);
     int r = need_cols(c, reads);
-    if (!r) r = upload_colptr(c);
-    if (!r) r = upload_tape(c);
+    if (!r) r = upload_colptr(c);   // the generic fold's tape is uploaded below, only when used
     if (r) return r;
     // asynchronous (no count requested): no host wait; a pending failure flag stays set (the
     // kernels skip on it) until the next synchronizing call reports it
@@ -2262,6 +2267,9 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, c->mslots));
         const double* lp = bounded ? l : nullptr;
         const double* hp = bounded ? h : nullptr;
+        // (a last-block combine inside k_moments, an arrival counter behind a device-scope
+        // fence per block, measured 2x slower than the separate combine launch: 113.6 vs
+        // 57.7 + 13.5 us at 4M — every block's fence writes back its L2)
         WSMC_HIP(launch_moments(c->stream, c->w, c->mslots, c->d_colptr, targets, d, lp, hp, 1, c->mom, c->N,
                                 c->tilepart));
         WSMC_HIP(launch_moments_final(c->stream, c->tilepart, c->ntiles, d, 1, step, c->mom, c->dflag));
@@ -2308,25 +2316,16 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
     }
     const int32_t* mflag = (proposal == WSMC_PROPOSAL_AUTORW && !is_sharded(c)) ? c->dflag : nullptr;
     if ((int)slots.size() <= kFoldSlots) {
-        if ((int64_t)ct.size() > c->d_ctape_cap) {
-            int64_t cap = c->d_ctape_cap ? c->d_ctape_cap : 64;
-            while (cap < (int64_t)ct.size()) cap *= 2;
-            WSMC_HIP(hipStreamSynchronize(c->stream));
-            if (c->d_ctape) WSMC_HIP(hipFree(c->d_ctape));
-            WSMC_HIP(hipMalloc(&c->d_ctape, sizeof(wsmc_term) * cap));
-            c->d_ctape_cap = cap;
-        }
-        if (!ct.empty())
-            WSMC_HIP(hipMemcpyAsync(c->d_ctape, ct.data(), sizeof(wsmc_term) * ct.size(), hipMemcpyHostToDevice,
-                                    c->stream));
         // the fold program: s_new over [0, kD), s_old over [cache_from or 0, kD)
         std::vector<FoldSeg> segs;
         std::vector<double> cst;
         const int32_t nseg_new = compile_fold(ct, 0, kD, segs, cst);
         const int32_t seg_old0 = (int32_t)segs.size();
         const int32_t nseg_old = compile_fold(ct, cache_from >= 0 ? cache_from : 0, kD, segs, cst);
+        // one upload per move: [compiled tape | segments | constants]
+        const size_t ct_bytes = (sizeof(wsmc_term) * ct.size() + 255) & ~(size_t)255;
         const size_t seg_bytes = sizeof(FoldSeg) * segs.size();
-        const size_t prog_bytes = seg_bytes + sizeof(double) * cst.size();
+        const size_t prog_bytes = ct_bytes + seg_bytes + sizeof(double) * cst.size();
         if ((int64_t)prog_bytes > c->d_prog_cap) {
             int64_t cap = c->d_prog_cap ? c->d_prog_cap : 4096;
             while (cap < (int64_t)prog_bytes) cap *= 2;
@@ -2336,26 +2335,35 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
             c->d_prog_cap = cap;
         }
         std::vector<char> hprog(prog_bytes);
-        if (seg_bytes) std::memcpy(hprog.data(), segs.data(), seg_bytes);
-        if (!cst.empty()) std::memcpy(hprog.data() + seg_bytes, cst.data(), sizeof(double) * cst.size());
+        if (!ct.empty()) std::memcpy(hprog.data(), ct.data(), sizeof(wsmc_term) * ct.size());
+        if (seg_bytes) std::memcpy(hprog.data() + ct_bytes, segs.data(), seg_bytes);
+        if (!cst.empty())
+            std::memcpy(hprog.data() + ct_bytes + seg_bytes, cst.data(), sizeof(double) * cst.size());
         if (prog_bytes)
             WSMC_HIP(hipMemcpyAsync(c->d_prog, hprog.data(), prog_bytes, hipMemcpyHostToDevice, c->stream));
+        char* pbase = reinterpret_cast<char*>(c->d_prog);
+        const wsmc_term* d_ct = reinterpret_cast<const wsmc_term*>(pbase);
         FoldProgram prog;
-        prog.seg_new = reinterpret_cast<const FoldSeg*>(c->d_prog);
-        prog.seg_old = reinterpret_cast<const FoldSeg*>(c->d_prog) + seg_old0;
+        prog.seg_new = reinterpret_cast<const FoldSeg*>(pbase + ct_bytes);
+        prog.seg_old = prog.seg_new + seg_old0;
         prog.nseg_new = nseg_new;
         prog.nseg_old = nseg_old;
-        prog.cst = reinterpret_cast<const double*>(reinterpret_cast<const char*>(c->d_prog) + seg_bytes);
+        prog.cst = reinterpret_cast<const double*>(pbase + ct_bytes + seg_bytes);
         FoldSlots fs{};
         fs.n = (int32_t)slots.size();
         for (const auto& t : ct) fs.heavy |= t.dist.mean_fn == WSMC_MEAN_OSCILLATOR ? 1 : 0;
+        // lean fold: every one-term segment scalar (runs are evaluated by their own code)
+        fs.lean = 1;
+        for (const auto& sg : segs)
+            if (sg.kind == kSegTerm && !wsmc_term_is_scalar(&ct[sg.tmpl])) fs.lean = 0;
         for (size_t s = 0; s < slots.size(); ++s)
             fs.p[s] = c->cols[slots[s].first].front + (int64_t)slots[s].second * c->N;
         for (int k = 0; k < d; ++k) fs.t[k] = c->cols[targets[k]].front;
-        WSMC_HIP(launch_move_c(c->stream, c->d_ctape, kD, target_depth, fs, targets, d, bounded ? l : nullptr,
+        WSMC_HIP(launch_move_c(c->stream, d_ct, kD, target_depth, fs, targets, d, bounded ? l : nullptr,
                                bounded ? h : nullptr, bounded ? 1 : 0, c->mom + 32, c->seed, op_prop, op_acc, c->goff,
                                c->N, c->ucount, mflag, c->scache, cache_from, prog));
     } else {
+        if ((r = upload_tape(c))) return r;
         WSMC_HIP(launch_move(c->stream, c->d_tape, (int32_t)c->tape.size(), target_depth, c->d_colptr, targets, d,
                              bounded ? l : nullptr, bounded ? h : nullptr, bounded ? 1 : 0, c->mom + 32, c->seed,
                              op_prop, op_acc, c->goff, c->N, c->ucount, mflag, c->scache, cache_from));

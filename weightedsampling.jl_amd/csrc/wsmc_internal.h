@@ -315,12 +315,14 @@ struct FoldSlots {
     double* t[4];                  // the target columns (written on accept)
     int32_t n;
     int32_t heavy;                 // transcendental-heavy terms (oscillator means): one particle per thread
+    int32_t lean;                  // every term is a run term or scalar (wsmc_term_is_scalar): the lean fold
 };
 // The fold as a program of segments over the compiled tape: a run of consecutive Normal
 // terms that differ only in their constants (the observations of a model's loop, e.g.
 // examples/damped_oscillator.jl:36 or examples/linear_regression.jl:21) is one segment whose
 // per-particle invariants (the mean's column reads, sigma and its log) are evaluated once;
-// its terms' constants are packed in `cst`. Every other term is a one-term segment.
+// its terms' constants are packed in `cst` (Osc: t_a, d, m, y per term — the rotation block
+// of wsmc_osc_link; Aff: c0, coef0, coef1, y). Every other term is a one-term segment.
 enum { kSegTerm = 0, kSegNormalOsc = 1, kSegNormalAff = 2 };
 struct FoldSeg {
     int32_t kind;

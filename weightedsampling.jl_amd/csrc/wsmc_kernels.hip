@@ -1216,6 +1216,10 @@ __device__ __forceinline__ void block_sum2_u64(u64& a, u64& b, u64 (*lds)[2]) {
 //  * kOverflowBlocks blocks plan the overflow chunks from the tile sums and fill them.
 // The fill does not wait for the decision: when the step does not resample, the row it
 // writes is never read (the next step and the trace-back check the decision).
+// MODE (diagnostics only, results wrong; production = 0): 1 = the record block only marks
+// the step resampled with mean 0 (the same fill work under forced resampling: q depends on
+// lw - M only)
+template <int MODE>
 __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPlan plan, const u64* __restrict__ grp,
                                                               int G, const MaxSlots* __restrict__ ms, double ess_min,
                                                               ShardRecord* rec, Decision* dec,
@@ -1230,6 +1234,10 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
     // block 0 (dispatched first: its serial decision is the longest chain) is the record
     // block; blocks 1..ntiles fill the tiles' first chunks, the rest serve overflow chunks
     const int t = blockIdx.x == 0 ? ntiles + kOverflowBlocks : (int)blockIdx.x - 1;
+    if (MODE == 1 && t == ntiles + kOverflowBlocks) {
+        if (th == 0 && dec) { dec->resampled = 1; dec->mean = 0.0; dec->ess = 0.0; dec->M = 0.0; }
+        return;
+    }
     if (t == ntiles + kOverflowBlocks) {
         // ---- the shard record and (one GPU, dec != null) the decision; a sharded run
         // all-gathers the records and decides afterwards (k_rs_decide) ----
@@ -1384,6 +1392,52 @@ struct MomArgs {
     wsmc_operand ex[4];
 };
 
+// one block: canonical combine of tile partials; pass 1 -> mom[0..d) = mean, mom[8] = S0;
+// pass 2 -> mom[16..16+d*d) = lambda*Sigma (zeros -> min_step), mom[32..32+d*d) = chol
+__device__ __forceinline__ void moments_final_block(const double* tilepart, int64_t ntiles, int d, int pass,
+                                                    double min_step, double* mom, int32_t* flag, int raw,
+                                                    double* lds4, double* tot) {
+    const int nv = pass == 1 ? 1 + d : d * (d + 1) / 2;
+    for (int v = 0; v < nv; ++v) {
+        double acc = 0.0;
+        for (int64_t b = threadIdx.x; b < ntiles; b += kBlock) acc = acc + tilepart[(int64_t)v * ntiles + b];
+        const double s = block_sum_canon(acc, lds4);
+        if (threadIdx.x == 0) tot[v] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    for (int v = 0; v < nv; ++v) mom[48 + v] = tot[v];   // raw shard totals (sharded moves combine them)
+    if (raw == 2) return;                                // sharded: the host combines and factorises
+    if (pass == 1) {
+        const double S0 = tot[0];
+        for (int k = 0; k < d; ++k) mom[k] = tot[1 + k] / S0;
+        mom[8] = S0;
+        return;
+    }
+    const double S0 = mom[8];
+    double S[16], L[16];
+    int v = 0;
+    for (int a = 0; a < d; ++a)
+        for (int b = a; b < d; ++b) {
+            const double c = tot[v++] / S0;
+            S[a * d + b] = c;
+            S[b * d + a] = c;
+        }
+    if (raw) {   // analysis moments: the weighted covariance itself
+        for (int k = 0; k < d * d; ++k) mom[16 + k] = S[k];
+        return;
+    }
+    const double lam = 2.38 / wsmc_sqrt((double)d);
+    for (int k = 0; k < d * d; ++k) {
+        if (S[k] == 0.0) S[k] = min_step;
+        S[k] = lam * S[k];
+        mom[16 + k] = S[k];
+    }
+    const int ok = wsmc_cholesky(S, L, d);
+    for (int k = 0; k < d * d; ++k) mom[32 + k] = L[k];
+    if (!ok) flag[0] = 1;
+}
+
 // pass 1: values {e, e*z_k};  pass 2: values {(e*(z_a-mean_a))*(z_b-mean_b), a <= b}
 // written as canonical tile partials tilepart[v * ntiles + tile]
 __global__ __launch_bounds__(kBlock) void k_moments(const double* __restrict__ w, const MaxSlots* ms,
@@ -1429,52 +1483,12 @@ __global__ __launch_bounds__(kBlock) void k_moments(const double* __restrict__ w
     }
 }
 
-// one block: canonical combine of tile partials; pass 1 -> mom[0..d) = mean, mom[8] = S0;
-// pass 2 -> mom[16..16+d*d) = lambda*Sigma (zeros -> min_step), mom[32..32+d*d) = chol
 __global__ __launch_bounds__(kBlock) void k_moments_final(const double* tilepart, int64_t ntiles, int d,
                                                           int pass, double min_step, double* mom,
                                                           int32_t* flag, int raw) {
     __shared__ double lds4[4];
     __shared__ double tot[10];
-    const int nv = pass == 1 ? 1 + d : d * (d + 1) / 2;
-    for (int v = 0; v < nv; ++v) {
-        double acc = 0.0;
-        for (int64_t b = threadIdx.x; b < ntiles; b += kBlock) acc = acc + tilepart[(int64_t)v * ntiles + b];
-        const double s = block_sum_canon(acc, lds4);
-        if (threadIdx.x == 0) tot[v] = s;
-    }
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    for (int v = 0; v < nv; ++v) mom[48 + v] = tot[v];   // raw shard totals (sharded moves combine them)
-    if (raw == 2) return;                                // sharded: the host combines and factorises
-    if (pass == 1) {
-        const double S0 = tot[0];
-        for (int k = 0; k < d; ++k) mom[k] = tot[1 + k] / S0;
-        mom[8] = S0;
-        return;
-    }
-    const double S0 = mom[8];
-    double S[16], L[16];
-    int v = 0;
-    for (int a = 0; a < d; ++a)
-        for (int b = a; b < d; ++b) {
-            const double c = tot[v++] / S0;
-            S[a * d + b] = c;
-            S[b * d + a] = c;
-        }
-    if (raw) {   // analysis moments: the weighted covariance itself
-        for (int k = 0; k < d * d; ++k) mom[16 + k] = S[k];
-        return;
-    }
-    const double lam = 2.38 / wsmc_sqrt((double)d);
-    for (int k = 0; k < d * d; ++k) {
-        if (S[k] == 0.0) S[k] = min_step;
-        S[k] = lam * S[k];
-        mom[16 + k] = S[k];
-    }
-    const int ok = wsmc_cholesky(S, L, d);
-    for (int k = 0; k < d * d; ++k) mom[32 + k] = L[k];
-    if (!ok) flag[0] = 1;
+    moments_final_block(tilepart, ntiles, d, pass, min_step, mom, flag, raw, lds4, tot);
 }
 
 // Move (src/transformers.jl:588-623). scache carries each particle's score from its last
@@ -1542,7 +1556,12 @@ __global__ __launch_bounds__(kBlock) void k_move(const wsmc_term* tape, int32_t 
 // per-term arithmetic, its constants read as wave-uniform scalars. Every term's arithmetic is
 // wsmc_term_logpdf_m's (the same operations in the same order, the same log memo), so the
 // fold is bit-identical to the term-by-term one.
-template <int K>
+// LEAN (a template flag, chosen by the host from the program): 0 = any term; 1 = runs and
+// scalar Normal/HalfNormal/Uniform one-term segments only (wsmc_scalar_term_logpdf_m: the
+// same arithmetic), no oscillator; 2 = the same with oscillator runs. The lean variants carry
+// no code for the other families, so they need far fewer registers (occupancy: the fold is
+// latency-bound).
+template <int K, int LEAN = 0>
 __device__ __forceinline__ void fold_seg(double (&s)[K], const wsmc_term* tape, const FoldSeg* segs, int32_t nseg,
                                          const double* __restrict__ cst, double* const* cols, const int (&ix)[K],
                                          const bool (&ok)[K]) {
@@ -1552,7 +1571,7 @@ __device__ __forceinline__ void fold_seg(double (&s)[K], const wsmc_term* tape, 
     for (int32_t g = 0; g < nseg; ++g) {
         const FoldSeg sg = segs[g];
         const wsmc_term* tp = &tape[sg.tmpl];
-        if (sg.kind == kSegNormalOsc) {
+        if (LEAN != 1 && sg.kind == kSegNormalOsc) {
             // Normal(A exp(-gamma t) cos(omega t + phi), sigma) observed at y, over (t, y) pairs
             double A[K], om[K], ga[K], ph[K], rsd[K], lsd[K];
 #pragma unroll
@@ -1564,13 +1583,39 @@ __device__ __forceinline__ void fold_seg(double (&s)[K], const wsmc_term* tape, 
                 const double sd = wsmc_operand_eval(&tp->dist.scale, cols, 0, ix[p], nullptr);
                 wsmc_scale_memo(&lm[p], sd, &lsd[p], &rsd[p]);
             }
+            // the mean by rotation (wsmc_osc_rolled's operations): a block's first term (m = 0)
+            // is the direct phasor, each next term of the block one complex multiply by R; a
+            // fold entering a block mid-way (the carried score's continuation) anchors and rolls
+            // there, so every term has the bits of the term-by-term evaluation
             const double* c = cst + sg.coff;
+            double zr[K], zi[K], rr[K], ri[K];
+            double cur_ta = WSMC_NAN, r_d = WSMC_NAN;
+            int cur_m = -2;
             for (int32_t k = 0; k < sg.count; ++k) {
-                const double t = c[2 * k], y = c[2 * k + 1];
+                const double ta = c[4 * k], dl = c[4 * k + 1], y = c[4 * k + 3];
+                const int m = (int)c[4 * k + 2];
+                const bool next = m > 0 && m == cur_m + 1 && wsmc_d2bits(ta) == wsmc_d2bits(cur_ta) &&
+                                  wsmc_d2bits(dl) == wsmc_d2bits(r_d);
+                if (m > 0 && wsmc_d2bits(dl) != wsmc_d2bits(r_d)) {   // uniform branch
+#pragma unroll
+                    for (int p = 0; p < K; ++p) wsmc_osc_step(dl, om[p], ga[p], &rr[p], &ri[p]);
+                    r_d = dl;
+                }
+#pragma unroll
+                for (int p = 0; p < K; ++p) {
+                    if (next) {
+                        wsmc_osc_rotate(&zr[p], &zi[p], rr[p], ri[p]);
+                    } else {
+                        wsmc_osc_anchor(ta, A[p], om[p], ga[p], ph[p], &zr[p], &zi[p]);
+                        for (int j = 0; j < m; ++j) wsmc_osc_rotate(&zr[p], &zi[p], rr[p], ri[p]);
+                    }
+                }
+                cur_ta = ta;
+                cur_m = m;
 #pragma unroll
                 for (int p = 0; p < K; ++p) {
                     if (!ok[p]) continue;
-                    const double mu = wsmc_oscillator(t, A[p], om[p], ga[p], ph[p]);
+                    const double mu = zr[p];
                     const double z = (y - mu) * rsd[p];
                     s[p] = s[p] + (-(z * z + WSMC_LOG2PI) * 0.5 - lsd[p]);
                 }
@@ -1604,6 +1649,12 @@ __device__ __forceinline__ void fold_seg(double (&s)[K], const wsmc_term* tape, 
             }
             continue;
         }
+        if (LEAN) {
+#pragma unroll
+            for (int p = 0; p < K; ++p)
+                if (ok[p]) s[p] = s[p] + wsmc_scalar_term_logpdf_m(tp, cols, 0, ix[p], nullptr, &lm[p]);
+            continue;
+        }
 #pragma unroll
         for (int p = 0; p < K; ++p)
             if (ok[p]) s[p] = s[p] + wsmc_term_logpdf_m(tp, cols, 0, ix[p], nullptr, &lm[p]);
@@ -1613,7 +1664,7 @@ __device__ __forceinline__ void fold_seg(double (&s)[K], const wsmc_term* tape, 
 // The same Move over a compiled tape (slots; targets are slots 0..d-1), K particles per
 // thread: slot values staged once in LDS ([slot][K * kBlock]), proposals in their own LDS
 // rows so the s_new fold reads them through its own pointer table (no override lookups).
-template <int K>
+template <int K, int LEAN>
 __global__ __launch_bounds__(kBlock) void k_move_c(const wsmc_term* ctape, int32_t nterms, int32_t depth,
                                                    FoldSlots fs, MomArgs ma, int d, int bounded, const double* Lm,
                                                    uint64_t seed, uint64_t op_prop, uint64_t op_acc, int64_t goff,
@@ -1675,8 +1726,8 @@ __global__ __launch_bounds__(kBlock) void k_move_c(const wsmc_term* ctape, int32
         }
     }
     // s_old: the carried score continued over the new terms, or the full fold
-    fold_seg<K>(so, ctape, prog.seg_old, prog.nseg_old, prog.cst, sp, ix, ok);
-    fold_seg<K>(sn, ctape, prog.seg_new, prog.nseg_new, prog.cst, spn, ix, ok);
+    fold_seg<K, LEAN>(so, ctape, prog.seg_old, prog.nseg_old, prog.cst, sp, ix, ok);
+    fold_seg<K, LEAN>(sn, ctape, prog.seg_new, prog.nseg_new, prog.cst, spn, ix, ok);
     u64 acc = 0;
 #pragma unroll
     for (int p = 0; p < K; ++p) {
@@ -2011,8 +2062,16 @@ hipError_t launch_rs_fill_fused(hipStream_t s, int64_t N, const FillPlan& plan, 
                                 const MaxSlots* ms, double ess_min, ShardRecord* rec, Decision* dec, const u64* qbuf,
                                 int32_t* anc, hipEvent_t e0, hipEvent_t e1) {
     const dim3 g((unsigned)((N + kRsTile - 1) / kRsTile + kOverflowBlocks + 1));
-    return launch_timed(k_rs_fill_fused, g, dim3(kScanBlock), s, e0, e1, N, plan, grp, G, ms, ess_min, rec, dec, qbuf,
-                        anc);
+    static const int diag = [] {
+        const char* e = getenv("WSMC_DIAG_FILL");
+        return e ? atoi(e) : 0;
+    }();
+    switch (diag) {
+        case 1: return launch_timed(k_rs_fill_fused<1>, g, dim3(kScanBlock), s, e0, e1, N, plan, grp, G, ms, ess_min,
+                                    rec, dec, qbuf, anc);
+        default: return launch_timed(k_rs_fill_fused<0>, g, dim3(kScanBlock), s, e0, e1, N, plan, grp, G, ms, ess_min,
+                                     rec, dec, qbuf, anc);
+    }
 }
 hipError_t launch_rs_reduce(hipStream_t s, const MaxSlots* ms, const u64* tilep, int64_t N, u64* tileOff,
                             ShardRecord* rec, int decide_local, double ess_min, Decision* dec,
@@ -2344,15 +2403,26 @@ hipError_t launch_move_c(hipStream_t s, const wsmc_term* ctape, int32_t nterms, 
         const char* e = getenv("WSMC_DIAG_MOVE_K");
         return e ? atoi(e) : 0;
     }();
+    static const int nolean = [] {   // diagnostics only: the generic fold for every program
+        const char* e = getenv("WSMC_DIAG_MOVE_GENERIC");
+        return e ? atoi(e) : 0;
+    }();
+    // lean variant: 1 = scalar terms and runs without oscillators, 2 = with them, 0 = generic
+    const int lean = nolean ? 0 : (fs.lean ? (fs.heavy ? 2 : 1) : 0);
+#define WSMC_MOVE_LAUNCH(KK, LL)                                                                              \
+    hipLaunchKernelGGL((k_move_c<KK, LL>), dim3((unsigned)((N + KK * kBlock - 1) / (KK * kBlock))), dim3(kBlock), \
+                       KK * row, s, ctape, nterms, depth, fs, ma, d, bounded, L, seed, op_prop, op_acc, goff, N,    \
+                       accepted, flag, scache, cache_from, prog)
     if (kdiag == 1 || (kdiag != 2 && fs.heavy)) {
-        const dim3 g((unsigned)((N + kBlock - 1) / kBlock));
-        hipLaunchKernelGGL(k_move_c<1>, g, dim3(kBlock), row, s, ctape, nterms, depth, fs, ma, d, bounded, L, seed,
-                           op_prop, op_acc, goff, N, accepted, flag, scache, cache_from, prog);
+        if (lean == 2) WSMC_MOVE_LAUNCH(1, 2);
+        else if (lean == 1) WSMC_MOVE_LAUNCH(1, 1);
+        else WSMC_MOVE_LAUNCH(1, 0);
     } else {
-        const dim3 g((unsigned)((N + 2 * kBlock - 1) / (2 * kBlock)));
-        hipLaunchKernelGGL(k_move_c<2>, g, dim3(kBlock), 2 * row, s, ctape, nterms, depth, fs, ma, d, bounded, L,
-                           seed, op_prop, op_acc, goff, N, accepted, flag, scache, cache_from, prog);
+        if (lean == 2) WSMC_MOVE_LAUNCH(2, 2);
+        else if (lean == 1) WSMC_MOVE_LAUNCH(2, 1);
+        else WSMC_MOVE_LAUNCH(2, 0);
     }
+#undef WSMC_MOVE_LAUNCH
     return hipGetLastError();
 }
 hipError_t launch_trace_pack(hipStream_t s, const double* xpairs, const int32_t* arow, int64_t start, int64_t count,
