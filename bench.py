@@ -285,7 +285,7 @@ def main():
     prop_bytes = N * (PROP_BYTES_FIRST + (T - 1) * PROP_BYTES_STEADY + PROP_BYTES_LAST_DV)
     prop_gbs = prop_bytes / (prop_ms * 1e-3) / 1e9 if prop_ms > 0 else None
     def pmc(name):   # PMC-measured bytes (profiles/), reported only for the N they were measured at
-        f = REPO / "profiles" / name
+        f = REPO / "pmc" / name   # copies of the latest profiles/ summaries (profiles/ does not travel)
         try:
             j = json.loads(f.read_text())
             return j if j.get("n_particles", N) == N and j.get("T", T) == T else None

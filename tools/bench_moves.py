@@ -57,8 +57,10 @@ def c5(N=4_000_000, T=60, sweeps=5, reps=1, scheme="systematic", ess=1.0, divers
            "N": N, "T": T, "seconds_per_run": best, "particle_steps_per_s": N * T / best,
            "accepted": moved, "moves_offered": 2 * sweeps * T}
     if diversity is None and ess >= 1.0:
-        # score terms per particle: every move folds twice over the 5 priors + t observations
-        terms = sum(2 * 2 * sweeps * (5 + t) for t in range(1, T + 1))
+        # score terms evaluated per particle: every move folds s_new over the 5 priors + t
+        # observations; s_old is the carried score, continued over the one new observation by
+        # the step's first move (0 terms afterwards)
+        terms = sum(2 * sweeps * (5 + t) + 1 for t in range(1, T + 1))
         out.update({"score_terms_per_particle": terms, "score_terms_per_s": N * terms / best})
     return out
 
