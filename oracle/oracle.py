@@ -108,6 +108,9 @@ _SIG = {
                                C.c_uint64, C.c_int32, _D, _D, _I32P]),
     "or_sizeof_term": (C.c_int32, []),
     "or_sizeof_dist": (C.c_int32, []),
+    "or_sincos": (None, [C.c_double, _D, _D]),
+    "or_oscillator": (C.c_double, [C.c_double] * 5),
+    "or_osc_rolled": (C.c_double, [C.c_double, C.c_double, C.c_int32] + [C.c_double] * 4),
 }
 
 _lib = None

@@ -375,6 +375,12 @@ static int cmp_es(const void* a, const void* b) {
     return i < j ? -1 : (i > j);                                                           /* index asc */
 }
 double or_es_key(uint64_t seed, uint64_t op, uint64_t i, uint64_t q) { return wsmc_es_key(seed, op, i, q); }
+/* the oscillator mean's math (include/wsmc_math.h), for the known-answer tests */
+void or_sincos(double x, double* s, double* c) { wsmc_sincos(x, s, c); }
+double or_oscillator(double t, double A, double om, double ga, double ph) { return wsmc_oscillator(t, A, om, ga, ph); }
+double or_osc_rolled(double ta, double d, int32_t m, double A, double om, double ga, double ph) {
+    return wsmc_osc_rolled(ta, d, m, A, om, ga, ph);
+}
 int or_sample_particles(oracle* o, int64_t n, int32_t replace, int64_t* out) {
     const int64_t N = o->N;
     if (n <= 0 || (!replace && n > N)) return WSMC_EARG;
