@@ -288,3 +288,30 @@ def test_exact_shard_flag_is_the_single_population():
     np.testing.assert_array_equal(runs["exact"][1], runs["one"][1])
     assert runs["exact"][2] == runs["one"][2]
     assert not np.array_equal(runs["island"][1], runs["one"][1])
+
+
+def test_oscillator_rotation_known_answers():
+    """The damped-oscillator mean by rotation: sin/cos share wsmc_cos's
+    reduction (cos bit-identical to it, sin within an ulp-scale of libm), a block's first term
+    is the direct formula bit for bit, and the rolled mean at t_a + m*d (m <= 15) agrees with
+    examples/damped_oscillator.jl:11 evaluated by numpy in f64 to 2e-14 * A."""
+    import ctypes as C
+    L = O.lib()
+    rng = np.random.default_rng(7)
+    s, c = C.c_double(), C.c_double()
+    for x in rng.uniform(-400.0, 400.0, 4000):
+        L.or_sincos(float(x), C.byref(s), C.byref(c))
+        assert c.value == L.or_cos(float(x))
+        assert abs(s.value - math.sin(x)) <= 2.3e-16 * max(1.0, abs(x)) + 1e-16
+    d = 8.0 / 59.0                        # examples/damped_oscillator.jl:19, range(0, 8, length=60)
+    worst = 0.0
+    for _ in range(2000):
+        A, om, ga = rng.uniform(0, 5), rng.uniform(0, 10), rng.uniform(0, 2)
+        ph = rng.uniform(-math.pi, math.pi)
+        ta = d * 16 * int(rng.integers(0, 4))
+        assert L.or_osc_rolled(ta, d, 0, A, om, ga, ph) == L.or_oscillator(ta, A, om, ga, ph)
+        for m in range(16):
+            t = ta + m * d
+            ref = A * np.exp(-ga * t) * np.cos(om * t + ph)
+            worst = max(worst, abs(L.or_osc_rolled(ta, d, m, A, om, ga, ph) - ref) / max(A, 1e-300))
+    assert worst < 2e-14, worst
