@@ -40,9 +40,14 @@ WSMC_HD double wsmc_operand_eval(const wsmc_operand* o, double* const* cols, int
     return v;
 }
 
-WSMC_HD double wsmc_dist_mean(const wsmc_dist* d, int k, double* const* cols, int64_t N, int64_t i,
-                              const wsmc_override* ov) {
-    if (d->mean_fn == WSMC_MEAN_OSCILLATOR) {
+/* feat: the mean functions a caller may meet (WSMC_FEAT_OSC: the oscillator). A device kernel
+ * launched for affine means only passes 0, so the oscillator code is not compiled into it
+ * (registers); every other caller passes WSMC_FEAT_ALL. The arithmetic is the same. */
+#define WSMC_FEAT_OSC 1u
+#define WSMC_FEAT_ALL 1u
+WSMC_HD double wsmc_dist_mean_f(const wsmc_dist* d, int k, double* const* cols, int64_t N, int64_t i,
+                                const wsmc_override* ov, unsigned feat) {
+    if ((feat & WSMC_FEAT_OSC) && d->mean_fn == WSMC_MEAN_OSCILLATOR) {
         double A = wsmc_operand_eval(&d->mu[0], cols, N, i, ov);
         double om = wsmc_operand_eval(&d->mu[1], cols, N, i, ov);
         double ga = wsmc_operand_eval(&d->mu[2], cols, N, i, ov);
@@ -52,6 +57,10 @@ WSMC_HD double wsmc_dist_mean(const wsmc_dist* d, int k, double* const* cols, in
         return wsmc_oscillator(d->param[0], A, om, ga, ph);
     }
     return wsmc_operand_eval(&d->mu[k], cols, N, i, ov);
+}
+WSMC_HD double wsmc_dist_mean(const wsmc_dist* d, int k, double* const* cols, int64_t N, int64_t i,
+                              const wsmc_override* ov) {
+    return wsmc_dist_mean_f(d, k, cols, N, i, ov, WSMC_FEAT_ALL);
 }
 
 /* log and reciprocal of a scale parameter, remembered across the terms of one fold: a
@@ -87,11 +96,11 @@ WSMC_HD double wsmc_log_memo(wsmc_logmemo* m, double x) {
 }
 
 /* logpdf(D(args...), x) for the supported families */
-WSMC_HD double wsmc_dist_logpdf_m(const wsmc_dist* d, const double* x, double* const* cols, int64_t N,
-                                  int64_t i, const wsmc_override* ov, wsmc_logmemo* lm) {
+WSMC_HD double wsmc_dist_logpdf_mf(const wsmc_dist* d, const double* x, double* const* cols, int64_t N,
+                                   int64_t i, const wsmc_override* ov, wsmc_logmemo* lm, unsigned feat) {
     switch (d->family) {
         case WSMC_FAM_NORMAL: {   /* wsmc_normal_logpdf with a remembered log(sigma), 1/sigma */
-            double mu = wsmc_dist_mean(d, 0, cols, N, i, ov);
+            double mu = wsmc_dist_mean_f(d, 0, cols, N, i, ov, feat);
             double sg = wsmc_operand_eval(&d->scale, cols, N, i, ov);
             double lg, rc;
             wsmc_scale_memo(lm, sg, &lg, &rc);
@@ -112,13 +121,17 @@ WSMC_HD double wsmc_dist_logpdf_m(const wsmc_dist* d, const double* x, double* c
             double var = wsmc_operand_eval(&d->scale, cols, N, i, ov);
             double s = 0.0;
             for (int k = 0; k < d->dim && k < 4; ++k) {
-                double dx = x[k] - wsmc_dist_mean(d, k, cols, N, i, ov);
+                double dx = x[k] - wsmc_dist_mean_f(d, k, cols, N, i, ov, feat);
                 s = s + dx * dx;
             }
             double dd = (double)d->dim;
             return -((dd * WSMC_LOG2PI + dd * wsmc_log_memo(lm, var)) + s / var) * 0.5;
         }
     }
+}
+WSMC_HD double wsmc_dist_logpdf_m(const wsmc_dist* d, const double* x, double* const* cols, int64_t N,
+                                  int64_t i, const wsmc_override* ov, wsmc_logmemo* lm) {
+    return wsmc_dist_logpdf_mf(d, x, cols, N, i, ov, lm, WSMC_FEAT_ALL);
 }
 WSMC_HD double wsmc_dist_logpdf(const wsmc_dist* d, const double* x, double* const* cols, int64_t N,
                                 int64_t i, const wsmc_override* ov) {
@@ -128,11 +141,11 @@ WSMC_HD double wsmc_dist_logpdf(const wsmc_dist* d, const double* x, double* con
 /* rand(D(args...)) for particle i (global RNG index idx). sd_pre: for an MvNormal whose
  * variance operand is a constant, wsmc_sqrt of it evaluated once by the caller (the same
  * function of the same bits, so the same result as evaluating it per particle); else null. */
-WSMC_HD void wsmc_dist_sample_m(const wsmc_dist* d, double* x, uint64_t seed, uint64_t op, uint64_t idx,
-                                double* const* cols, int64_t N, int64_t i, const double* sd_pre) {
+WSMC_HD void wsmc_dist_sample_mf(const wsmc_dist* d, double* x, uint64_t seed, uint64_t op, uint64_t idx,
+                                 double* const* cols, int64_t N, int64_t i, const double* sd_pre, unsigned feat) {
     switch (d->family) {
         case WSMC_FAM_NORMAL: {
-            double mu = wsmc_dist_mean(d, 0, cols, N, i, 0);
+            double mu = wsmc_dist_mean_f(d, 0, cols, N, i, 0, feat);
             double sg = wsmc_operand_eval(&d->scale, cols, N, i, 0);
             x[0] = mu + sg * wsmc_normal_k(seed, op, idx, 0);
             break;
@@ -152,12 +165,16 @@ WSMC_HD void wsmc_dist_sample_m(const wsmc_dist* d, double* x, uint64_t seed, ui
             for (int k = 0; k < d->dim && k < 4; k += 2) {
                 double z0, z1;
                 wsmc_normal_pair(wsmc_rng_block(seed, op, idx, (uint32_t)(k >> 1)), &z0, &z1);
-                x[k] = wsmc_dist_mean(d, k, cols, N, i, 0) + sd * z0;
-                if (k + 1 < d->dim) x[k + 1] = wsmc_dist_mean(d, k + 1, cols, N, i, 0) + sd * z1;
+                x[k] = wsmc_dist_mean_f(d, k, cols, N, i, 0, feat) + sd * z0;
+                if (k + 1 < d->dim) x[k + 1] = wsmc_dist_mean_f(d, k + 1, cols, N, i, 0, feat) + sd * z1;
             }
             break;
         }
     }
+}
+WSMC_HD void wsmc_dist_sample_m(const wsmc_dist* d, double* x, uint64_t seed, uint64_t op, uint64_t idx,
+                                double* const* cols, int64_t N, int64_t i, const double* sd_pre) {
+    wsmc_dist_sample_mf(d, x, seed, op, idx, cols, N, i, sd_pre, WSMC_FEAT_ALL);
 }
 
 WSMC_HD void wsmc_dist_sample(const wsmc_dist* d, double* x, uint64_t seed, uint64_t op, uint64_t idx,
@@ -234,12 +251,16 @@ WSMC_HD double wsmc_scalar_term_logpdf_m(const wsmc_term* t, double* const* cols
     return wsmc_uniform_logpdf(d->param[0], d->param[1], x0);
 }
 
-WSMC_HD double wsmc_term_logpdf_m(const wsmc_term* t, double* const* cols, int64_t N, int64_t i,
-                                  const wsmc_override* ov, wsmc_logmemo* lm) {
+WSMC_HD double wsmc_term_logpdf_mf(const wsmc_term* t, double* const* cols, int64_t N, int64_t i,
+                                   const wsmc_override* ov, wsmc_logmemo* lm, unsigned feat) {
     double x[4] = {0.0, 0.0, 0.0, 0.0};
     int dim = t->dist.dim < 1 ? 1 : (t->dist.dim > 4 ? 4 : t->dist.dim);
     for (int k = 0; k < dim; ++k) x[k] = wsmc_operand_eval(&t->x[k], cols, N, i, ov);
-    return wsmc_dist_logpdf_m(&t->dist, x, cols, N, i, ov, lm);
+    return wsmc_dist_logpdf_mf(&t->dist, x, cols, N, i, ov, lm, feat);
+}
+WSMC_HD double wsmc_term_logpdf_m(const wsmc_term* t, double* const* cols, int64_t N, int64_t i,
+                                  const wsmc_override* ov, wsmc_logmemo* lm) {
+    return wsmc_term_logpdf_mf(t, cols, N, i, ov, lm, WSMC_FEAT_ALL);
 }
 WSMC_HD double wsmc_term_logpdf(const wsmc_term* t, double* const* cols, int64_t N, int64_t i,
                                 const wsmc_override* ov) {

@@ -422,7 +422,7 @@ int wsmc_destroy(wsmc_ctx* c) {
     for (auto& r : c->row_pool) (void)hipFree(r.anc);
     void* bufs[] = {c->dec_always, c->xchg, c->scache, c->scache_back, c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->cdf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount, c->wslots[0], c->wslots[1],
                     c->d_colptr, c->run_params, c->d_tape, c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp,
-                    c->vscratch, c->xscratch, c->xp, c->comb, c->anc_out, c->xbuf, c->d_comp, c->d_ctape, c->d_prog};
+                    c->vscratch, c->xscratch, c->xp, c->comb, c->anc_out, c->xbuf, c->d_comp, c->d_ctape, c->d_prog, c->rs_grp[0], c->rs_grp[1]};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (double* p : c->xrun)
@@ -1834,6 +1834,16 @@ static int weigh(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x, int kin
 int wsmc_observe(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x) { return weigh(c, d, x, WSMC_TERM_OBSERVE); }
 int wsmc_weight(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x) { return weigh(c, d, x, WSMC_TERM_WEIGHT); }
 
+// diagnostics: the generic Resample's reduce-kernel sequence instead of the fused pair
+static bool no_fused_resample() {
+    static const bool v = [] {
+        const char* e = getenv("WSMC_DIAG_RESAMPLE_REDUCE");
+        return e && atoi(e) != 0;
+    }();
+    return v;
+}
+static inline int64_t run_grp_words(int64_t N);
+
 int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resampled_out, double* ess_out) {
     if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { int32_t rs = 0; double e = 0; const bool f = x == multi_first(c); int r = wsmc_resample(x, ess_min, scheme, resampled_out ? &rs : nullptr, ess_out ? &e : nullptr); if (!r && f) { if (resampled_out) *resampled_out = rs; if (ess_out) *ess_out = e; } return r; });
     CHECK_CTX(c);
@@ -1885,12 +1895,38 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
         if ((r = resolve_decisions(c))) return r;
     Decision* hd = reinterpret_cast<Decision*>(c->pinned);
     plan.host_dec = async ? c->dec_ring_dev + c->dec_pending : reinterpret_cast<Decision*>(c->pinned_dev);
-    if ((r = enqueue_resample_stats(c, c->w, ms, c->rec, ess_min, row.dec, !pre, plan))) return r;
-    if (scheme == WSMC_RESAMPLE_MULTINOMIAL)
+    if (!is_sharded(c) && fill_resets && !no_fused_resample()) {
+        // one GPU: the fused run's two launches (statistics with group sums, then the fill
+        // whose extra block decides), then the gated weight reset — no reduce kernel. The
+        // group lines are double-buffered: each fill's record block zeroes the next call's.
+        const int64_t gw = run_grp_words(c->N);
+        if (!c->rs_grp[0]) {
+            for (int k = 0; k < 2; ++k) WSMC_HIP(hipMalloc(&c->rs_grp[k], sizeof(unsigned long long) * gw));
+            WSMC_HIP(hipMemsetAsync(c->rs_grp[0], 0, sizeof(unsigned long long) * gw, c->stream));
+            c->rs_grp_cur = 0;
+        }
+        unsigned long long* grp = c->rs_grp[c->rs_grp_cur];
+        c->rs_grp_cur ^= 1;
+        plan.w_reset = nullptr;
+        plan.grp_zero = c->rs_grp[c->rs_grp_cur];
+        plan.grp_zero_words = gw;
+        if (!pre) {
+            WSMC_HIP(hipMemsetAsync(ms, 0, sizeof(MaxSlots), c->stream));
+            WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, ms));
+        }
+        const int G = group_tiles(c->N);
+        WSMC_HIP(launch_rs_sums(c->stream, c->w, c->N, ms, c->tilep, c->qbuf, nullptr, nullptr, grp, G));
+        WSMC_HIP(launch_rs_fill_fused(c->stream, c->N, plan, grp, G, ms, ess_min, c->rec + c->rank, row.dec, c->qbuf,
+                                      row.anc));
+        WSMC_HIP(launch_fill_weights(c->stream, c->w, row.dec, c->N));
+    } else {
+        if ((r = enqueue_resample_stats(c, c->w, ms, c->rec, ess_min, row.dec, !pre, plan))) return r;
+        if (scheme == WSMC_RESAMPLE_MULTINOMIAL)
         WSMC_HIP(launch_rs_multinomial(c->stream, c->N, c->rec + c->rank, row.dec, plan, c->tileOff, c->cdf,
                                        multi_esum(c), multi_ebuf(c), row.anc));
-    else
-        WSMC_HIP(launch_rs_scan(c->stream, c->N, c->rec + c->rank, row.dec, plan, c->tileOff, c->qbuf, row.anc));
+        else
+            WSMC_HIP(launch_rs_scan(c->stream, c->N, c->rec + c->rank, row.dec, plan, c->tileOff, c->qbuf, row.anc));
+    }
     if (async) {
         c->dec_pending += 1;
         if (c->lazy) c->dec_epochs.push_back(c->epoch);   // the log entry this Resample becomes

@@ -200,6 +200,8 @@ struct wsmc_ctx {
     int64_t d_ctape_cap = 0;
     void* d_prog = nullptr;                 // compiled fold program: segments, then constants
     int64_t d_prog_cap = 0;                 // bytes
+    unsigned long long* rs_grp[2] = {nullptr, nullptr};   // generic Resample's group lines (double-buffered)
+    int rs_grp_cur = 0;
     size_t d_comp_cap = 0;
     double* tilepart = nullptr;             // [16 * ntiles] canonical-sum tile partials
     wsmc::MaxSlots* mslots = nullptr;       // [1] max slots of one generic resample / evidence
@@ -294,6 +296,8 @@ struct FillPlan {          // ancestor-fill task planning (in the reduce kernel)
     const ExactPlan* xp = nullptr;     // exact sharding: global Q / N / offsets, window-relative slots
     double* w_reset = nullptr;         // generic Resample: the tile blocks reset the weights to dec->mean
     Decision* host_dec = nullptr;      // generic Resample: the decision also written to host-mapped memory
+    unsigned long long* grp_zero = nullptr;   // fused fill: the next call's group lines, zeroed by its record block
+    int64_t grp_zero_words = 0;
 };
 hipError_t launch_rs_reduce(hipStream_t s, const MaxSlots* ms, const unsigned long long* tilep, int64_t N,
                             unsigned long long* tileOff, ShardRecord* rec, int decide_local, double ess_min,

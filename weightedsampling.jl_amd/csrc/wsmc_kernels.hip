@@ -205,6 +205,8 @@ __global__ __launch_bounds__(kBlock) void k_assign(double* out, int dim, AssignA
         if (k < dim) out[(int64_t)k * N + i] = x[k];
 }
 
+// FEAT (wsmc_terms.h): WSMC_FEAT_ALL, or 0 for affine means (no oscillator code: registers)
+template <unsigned FEAT>
 __global__ __launch_bounds__(kBlock) void k_sample(double* out, int dim, wsmc_dist d, uint64_t seed,
                                                    uint64_t op, int64_t goff, double* const* cols,
                                                    int64_t N, int has_sd, double sd) {
@@ -213,7 +215,8 @@ __global__ __launch_bounds__(kBlock) void k_sample(double* out, int dim, wsmc_di
     double x[4];
     // has_sd: a constant MvNormal variance, its sqrt evaluated once by the host (the same
     // restated function of the same bits each particle would evaluate)
-    wsmc_dist_sample_m(&d, x, seed, op, (uint64_t)(goff + i), cols, N, i, has_sd ? &sd : nullptr);
+    const double sdl = sd;   // a local (the parameter's address would live in scratch)
+    wsmc_dist_sample_mf(&d, x, seed, op, (uint64_t)(goff + i), cols, N, i, has_sd ? &sdl : nullptr, FEAT);
 #pragma unroll
     for (int k = 0; k < 4; ++k)
         if (k < dim) out[(int64_t)k * N + i] = x[k];
@@ -238,6 +241,7 @@ __global__ __launch_bounds__(kBlock) void k_sample_importance(double* out, int d
 // Observe / Weight: weights += logpdf, and the block max of the new weights into the 64
 // slots of `ms` (zero on entry), so the Resample that follows needs no max pass; block 0
 // zeroes `ms_next`, the slots the next launch will use (k_rs_max's encoding and slots)
+template <unsigned FEAT>
 __global__ __launch_bounds__(kBlock) void k_weigh(wsmc_term t, double* w, double* const* cols, int64_t N,
                                                   MaxSlots* ms, MaxSlots* ms_next, wsmc_logmemo lm0) {
     __shared__ u64 lds[4];
@@ -247,7 +251,7 @@ __global__ __launch_bounds__(kBlock) void k_weigh(wsmc_term t, double* w, double
         // lm0: a constant scale operand's log, evaluated once by the host and handed to the
         // term through the fold's log memo (the same bits every particle would compute)
         wsmc_logmemo lm = lm0;
-        const double v = w[i] + wsmc_term_logpdf_m(&t, cols, N, i, nullptr, &lm);
+        const double v = w[i] + wsmc_term_logpdf_mf(&t, cols, N, i, nullptr, &lm, FEAT);
         w[i] = v;
         m = wsmc_ord_enc(v);
     }
@@ -1241,6 +1245,7 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
     if (t == ntiles + kOverflowBlocks) {
         // ---- the shard record and (one GPU, dec != null) the decision; a sharded run
         // all-gathers the records and decides afterwards (k_rs_decide) ----
+        for (int64_t k = th; k < plan.grp_zero_words; k += kScanBlock) plan.grp_zero[k] = 0ull;
         u64 acc[kRedPart] = {0, 0, 0, 0, 0, 0};
         for (int g = th; g < ngroups; g += kScanBlock) acc[0] += grp[(int64_t)g * kGroupLine];
         for (int b = th; b < ntiles; b += kScanBlock) {
@@ -1271,7 +1276,10 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
             r.wflo = (u64)Wf; r.wfhi = (u64)(Wf >> 64);
             r.n = (u64)N;
             *rec = r;
-            if (dec) decide_records(&r, 1, 0, ess_min, dec);
+            if (dec) {
+                decide_records(&r, 1, 0, ess_min, dec);
+                if (plan.host_dec) *plan.host_dec = *dec;   // the generic Resample's host copy
+            }
         }
         return;
     }
@@ -2009,7 +2017,12 @@ hipError_t launch_sample(hipStream_t s, double* out, int dim, const wsmc_dist& d
                          int64_t goff, double* const* cols, int64_t N) {
     const int has_sd = d.family == WSMC_FAM_MVNORMAL_ISO && wsmc_operand_is_const(&d.scale);
     const double sd = has_sd ? wsmc_sqrt(wsmc_operand_eval(&d.scale, nullptr, N, 0, nullptr)) : 0.0;
-    hipLaunchKernelGGL(k_sample, grid_for(N), dim3(kBlock), 0, s, out, dim, d, seed, op, goff, cols, N, has_sd, sd);
+    if (d.mean_fn == WSMC_MEAN_OSCILLATOR)
+        hipLaunchKernelGGL(k_sample<WSMC_FEAT_ALL>, grid_for(N), dim3(kBlock), 0, s, out, dim, d, seed, op, goff, cols,
+                           N, has_sd, sd);
+    else
+        hipLaunchKernelGGL(k_sample<0u>, grid_for(N), dim3(kBlock), 0, s, out, dim, d, seed, op, goff, cols, N, has_sd,
+                           sd);
     return hipGetLastError();
 }
 hipError_t launch_sample_importance(hipStream_t s, double* out, int dim, const wsmc_dist& prop,
@@ -2029,7 +2042,10 @@ hipError_t launch_weigh(hipStream_t s, const wsmc_term& t, double* w, double* co
         lm0.rcp = 1.0 / sc;
         lm0.valid = 1;
     }
-    hipLaunchKernelGGL(k_weigh, grid_for(N), dim3(kBlock), 0, s, t, w, cols, N, ms, ms_next, lm0);
+    if (t.dist.mean_fn == WSMC_MEAN_OSCILLATOR)
+        hipLaunchKernelGGL(k_weigh<WSMC_FEAT_ALL>, grid_for(N), dim3(kBlock), 0, s, t, w, cols, N, ms, ms_next, lm0);
+    else
+        hipLaunchKernelGGL(k_weigh<0u>, grid_for(N), dim3(kBlock), 0, s, t, w, cols, N, ms, ms_next, lm0);
     return hipGetLastError();
 }
 template <typename K, typename... Args>
