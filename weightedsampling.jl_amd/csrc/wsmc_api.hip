@@ -1825,6 +1825,8 @@ static int weigh(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x, int kin
     c->wmax_buf = wb;
     c->wseq += 1;
     c->wmax_seq = c->wseq;
+    c->cur_max = c->wslots[wb];
+    c->cur_max_seq = c->wseq;
     c->tape.push_back(t);
     c->weights_changed = 1;
     c->depth += 1;
@@ -1895,6 +1897,7 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
         if ((r = resolve_decisions(c))) return r;
     Decision* hd = reinterpret_cast<Decision*>(c->pinned);
     plan.host_dec = async ? c->dec_ring_dev + c->dec_pending : reinterpret_cast<Decision*>(c->pinned_dev);
+    bool max_kept = false;   // ms holds the max of the weights after this Resample
     if (!is_sharded(c) && fill_resets && !no_fused_resample()) {
         // one GPU: the fused run's two launches (statistics with group sums, then the fill
         // whose extra block decides), then the gated weight reset — no reduce kernel. The
@@ -1918,7 +1921,10 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
         WSMC_HIP(launch_rs_sums(c->stream, c->w, c->N, ms, c->tilep, c->qbuf, nullptr, nullptr, grp, G));
         WSMC_HIP(launch_rs_fill_fused(c->stream, c->N, plan, grp, G, ms, ess_min, c->rec + c->rank, row.dec, c->qbuf,
                                       row.anc));
-        WSMC_HIP(launch_fill_weights(c->stream, c->w, row.dec, c->N));
+        // the reset also leaves the max of the new weights in ms (an Observe's slots: nothing
+        // else writes them before the next Observe, which moves on to the other buffer)
+        WSMC_HIP(launch_fill_weights(c->stream, c->w, row.dec, c->N, pre ? ms : nullptr));
+        max_kept = pre;
     } else {
         if ((r = enqueue_resample_stats(c, c->w, ms, c->rec, ess_min, row.dec, !pre, plan))) return r;
         if (scheme == WSMC_RESAMPLE_MULTINOMIAL)
@@ -1933,6 +1939,10 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
         c->wseq += 1;
         if ((r = store_resample_row(c, row, row.dec, fill_resets ? nullptr : c->w))) return r;   // gated
         c->weights_changed = 0;
+        if (max_kept) {
+            c->cur_max = ms;
+            c->cur_max_seq = c->wseq;
+        }
         return WSMC_OK;
     }
     WSMC_HIP(hipStreamSynchronize(c->stream));
@@ -1954,6 +1964,10 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
         c->resampled = 0;
     }
     c->weights_changed = 0;
+    if (max_kept) {
+        c->cur_max = ms;
+        c->cur_max_seq = c->wseq;
+    }
     if (resampled_out) *resampled_out = c->resampled;
     if (ess_out) *ess_out = d.ess;
     return WSMC_OK;
@@ -2299,18 +2313,22 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         int rr = sharded_autorw(c, targets, d, bounded ? l : nullptr, bounded ? h : nullptr, step);
         if (rr) return rr;
     } else if (proposal == WSMC_PROPOSAL_AUTORW) {
-        WSMC_HIP(hipMemsetAsync(c->mslots, 0, sizeof(MaxSlots), c->stream));
-        WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, c->mslots));
+        // the max of the weights: kept by the last Observe / fused Resample when still
+        // current (Moves leave the weights alone), else a max pass
+        const bool kept = c->cur_max && c->cur_max_seq == c->wseq;
+        MaxSlots* mms = kept ? c->cur_max : c->mslots;
+        if (!kept) {
+            WSMC_HIP(hipMemsetAsync(c->mslots, 0, sizeof(MaxSlots), c->stream));
+            WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, c->mslots));
+        }
         const double* lp = bounded ? l : nullptr;
         const double* hp = bounded ? h : nullptr;
         // (a last-block combine inside k_moments, an arrival counter behind a device-scope
         // fence per block, measured 2x slower than the separate combine launch: 113.6 vs
         // 57.7 + 13.5 us at 4M — every block's fence writes back its L2)
-        WSMC_HIP(launch_moments(c->stream, c->w, c->mslots, c->d_colptr, targets, d, lp, hp, 1, c->mom, c->N,
-                                c->tilepart));
+        WSMC_HIP(launch_moments(c->stream, c->w, mms, c->d_colptr, targets, d, lp, hp, 1, c->mom, c->N, c->tilepart));
         WSMC_HIP(launch_moments_final(c->stream, c->tilepart, c->ntiles, d, 1, step, c->mom, c->dflag));
-        WSMC_HIP(launch_moments(c->stream, c->w, c->mslots, c->d_colptr, targets, d, lp, hp, 2, c->mom, c->N,
-                                c->tilepart));
+        WSMC_HIP(launch_moments(c->stream, c->w, mms, c->d_colptr, targets, d, lp, hp, 2, c->mom, c->N, c->tilepart));
         WSMC_HIP(launch_moments_final(c->stream, c->tilepart, c->ntiles, d, 2, step, c->mom, c->dflag));
     } else {
         WSMC_HIP(hipStreamSynchronize(c->stream));

@@ -142,6 +142,10 @@ struct wsmc_ctx {
     wsmc::MaxSlots* wslots[2] = {nullptr, nullptr};
     int wnext = 0, wmax_buf = -1;
     uint64_t wseq = 0, wmax_seq = ~0ull;
+    // slots holding the max of the current weights (an Observe's, or a fused Resample's after
+    // its weight reset), valid while cur_max_seq == wseq: a Move's autoRW skips its max pass
+    wsmc::MaxSlots* cur_max = nullptr;
+    uint64_t cur_max_seq = ~0ull;
     int64_t N = 0;
     uint64_t seed = 0;
 
@@ -434,7 +438,8 @@ hipError_t launch_sample_draws_shard(hipStream_t s, int64_t n, int64_t N, const 
 hipError_t launch_es_keys_shard(hipStream_t s, const double* w, int64_t N, int64_t gN, int64_t goff,
                                 const MaxSlots* ms, uint64_t seed, uint64_t op, unsigned long long* keys,
                                 unsigned long long* idx);
-hipError_t launch_fill_weights(hipStream_t s, double* w, const Decision* dec, int64_t N);
+// ms != null: when the step resampled, ms is rewritten to hold the max of the reset weights
+hipError_t launch_fill_weights(hipStream_t s, double* w, const Decision* dec, int64_t N, MaxSlots* ms = nullptr);
 hipError_t launch_log_evidence_stats(hipStream_t s, const double* w, int64_t N, MaxSlots* ms,
                                      unsigned long long* tilep, unsigned long long* qbuf,
                                      unsigned long long* tileOff, ShardRecord* rec);

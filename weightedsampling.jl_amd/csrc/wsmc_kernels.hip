@@ -1377,10 +1377,20 @@ __global__ __launch_bounds__(kBlock) void k_gather(double* __restrict__ dst, con
     dst[i] = src[anc[i]];
 }
 
-__global__ __launch_bounds__(kBlock) void k_fill_weights(double* w, const Decision* dec, int64_t N) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= N || !dec->resampled) return;
-    w[i] = dec->mean;
+// the gated weight reset: four weights a thread, 16-B stores (w is 16-B aligned)
+__global__ __launch_bounds__(kBlock) void k_fill_weights(double* w, const Decision* dec, int64_t N, MaxSlots* ms) {
+    const int64_t i = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
+    if (!dec->resampled) return;
+    const double m = dec->mean;
+    // the max of N equal weights, in k_rs_max's encoding and slots (slot 0, the rest zero)
+    if (ms && blockIdx.x == 0 && threadIdx.x < kSlots) ms->v[threadIdx.x][0] = threadIdx.x == 0 ? wsmc_ord_enc(m) : 0ull;
+    if (i >= N) return;
+    if (i + 4 <= N) {
+        *reinterpret_cast<d2*>(w + i) = d2{m, m};
+        *reinterpret_cast<d2*>(w + i + 2) = d2{m, m};
+    } else {
+        for (int64_t k = i; k < N; ++k) w[k] = m;
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -2312,8 +2322,9 @@ hipError_t launch_gather(hipStream_t s, double* dst, const double* src, const in
     hipLaunchKernelGGL(k_gather, grid_for(N), dim3(kBlock), 0, s, dst, src, anc, N);
     return hipGetLastError();
 }
-hipError_t launch_fill_weights(hipStream_t s, double* w, const Decision* dec, int64_t N) {
-    hipLaunchKernelGGL(k_fill_weights, grid_for(N), dim3(kBlock), 0, s, w, dec, N);
+hipError_t launch_fill_weights(hipStream_t s, double* w, const Decision* dec, int64_t N, MaxSlots* ms) {
+    hipLaunchKernelGGL(k_fill_weights, dim3((unsigned)((N + 4 * kBlock - 1) / (4 * kBlock))), dim3(kBlock), 0, s, w,
+                       dec, N, ms);
     return hipGetLastError();
 }
 hipError_t launch_log_evidence_stats(hipStream_t s, const double* w, int64_t N, MaxSlots* ms, u64* tilep,
