@@ -1457,11 +1457,15 @@ __device__ __forceinline__ void moments_final_block(const double* tilepart, int6
 }
 
 // pass 1: values {e, e*z_k};  pass 2: values {(e*(z_a-mean_a))*(z_b-mean_b), a <= b}
-// written as canonical tile partials tilepart[v * ntiles + tile]
+// written as canonical tile partials tilepart[v * ntiles + tile]. D = d (1..4), a template
+// parameter so every per-particle array is unrolled into registers (the same operations in the
+// same order as a runtime d); EX: the values are operand expressions (analysis moments)
+template <int D, bool EX>
 __global__ __launch_bounds__(kBlock) void k_moments(const double* __restrict__ w, const MaxSlots* ms,
-                                                    double* const* cols, MomArgs ma, int d, int pass,
+                                                    double* const* cols, MomArgs ma, int pass,
                                                     const double* mom, int64_t N, int64_t ntiles,
                                                     double* tilepart) {
+    constexpr int d = D;
     __shared__ double lds4[4];
     const double M = wave_slots_max(ms);
     const int64_t base = (int64_t)blockIdx.x * kTile;
@@ -1480,22 +1484,28 @@ __global__ __launch_bounds__(kBlock) void k_moments(const double* __restrict__ w
         if (i < N) {
             const double e = wsmc_exp(w[i] - M);
             double z[4];
+#pragma unroll
             for (int k = 0; k < d; ++k)
-                z[k] = ma.use_ex ? wsmc_operand_eval(&ma.ex[k], cols, N, i, nullptr)
-                                 : wsmc_to_unc(cols[ma.tcol[k]][i], ma.lo[k], ma.hi[k]);
+                z[k] = EX ? wsmc_operand_eval(&ma.ex[k], cols, N, i, nullptr)
+                          : wsmc_to_unc(cols[ma.tcol[k]][i], ma.lo[k], ma.hi[k]);
             if (pass == 1) {
                 vals[0] = e;
+#pragma unroll
                 for (int k = 0; k < d; ++k) vals[1 + k] = e * z[k];
             } else {
                 int v = 0;
+#pragma unroll
                 for (int a = 0; a < d; ++a)
+#pragma unroll
                     for (int b = a; b < d; ++b) vals[v++] = (e * (z[a] - mean[a])) * (z[b] - mean[b]);
             }
         }
 #pragma unroll
         for (int v = 0; v < 10; ++v) acc[v] = acc[v] + vals[v];
     }
-    for (int v = 0; v < nv; ++v) {
+#pragma unroll
+    for (int v = 0; v < 10; ++v) {
+        if (v >= nv) break;
         const double s = block_sum_canon(acc[v], lds4);
         if (threadIdx.x == 0) tilepart[(int64_t)v * ntiles + blockIdx.x] = s;
     }
@@ -2350,8 +2360,12 @@ hipError_t launch_moments(hipStream_t s, const double* w, const MaxSlots* rec, d
     }
     ma.use_ex = 0;
     const int64_t nt = (N + kTile - 1) / kTile;
-    hipLaunchKernelGGL(k_moments, tiles_for(N), dim3(kBlock), 0, s, w, rec, cols, ma, d, pass, mom, N, nt,
-                       tilepart);
+    switch (d) {
+        case 1: hipLaunchKernelGGL((k_moments<1, false>), tiles_for(N), dim3(kBlock), 0, s, w, rec, cols, ma, pass, mom, N, nt, tilepart); break;
+        case 2: hipLaunchKernelGGL((k_moments<2, false>), tiles_for(N), dim3(kBlock), 0, s, w, rec, cols, ma, pass, mom, N, nt, tilepart); break;
+        case 3: hipLaunchKernelGGL((k_moments<3, false>), tiles_for(N), dim3(kBlock), 0, s, w, rec, cols, ma, pass, mom, N, nt, tilepart); break;
+        default: hipLaunchKernelGGL((k_moments<4, false>), tiles_for(N), dim3(kBlock), 0, s, w, rec, cols, ma, pass, mom, N, nt, tilepart); break;
+    }
     return hipGetLastError();
 }
 hipError_t launch_moments_expr(hipStream_t s, const double* w, const MaxSlots* ms, double* const* cols,
@@ -2366,7 +2380,12 @@ hipError_t launch_moments_expr(hipStream_t s, const double* w, const MaxSlots* m
     }
     ma.use_ex = 1;
     const int64_t nt = (N + kTile - 1) / kTile;
-    hipLaunchKernelGGL(k_moments, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, d, pass, mom, N, nt, tilepart);
+    switch (d) {
+        case 1: hipLaunchKernelGGL((k_moments<1, true>), tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pass, mom, N, nt, tilepart); break;
+        case 2: hipLaunchKernelGGL((k_moments<2, true>), tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pass, mom, N, nt, tilepart); break;
+        case 3: hipLaunchKernelGGL((k_moments<3, true>), tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pass, mom, N, nt, tilepart); break;
+        default: hipLaunchKernelGGL((k_moments<4, true>), tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pass, mom, N, nt, tilepart); break;
+    }
     return hipGetLastError();
 }
 // unweighted min / max of one column component (describe): ordered-encoding maxima of x and
