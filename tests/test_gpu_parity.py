@@ -417,3 +417,42 @@ def test_async_move_not_pd_reported_at_next_sync(gpu_available):
     c.move(abi.PROPOSAL_RW, [a], 0.3)
     o.move(abi.PROPOSAL_RW, [a], 0.3)
     assert_same_state(c, o)
+
+
+def _fold_paths_program(c, which):
+    """Move programs whose compiled folds take each kernel variant (lean
+    kernels): 'generic' — a tape with an MvNormal term (no lean fold); 'generic_osc' — the same
+    with oscillator Observes (the generic fold's rotation runs); 'lone_osc' — one oscillator
+    Observe (a run of one, lean with oscillators); 'scalar' — scalar priors and affine runs."""
+    from wsmc.dsl import HalfNormal, MvNormal, Normal, Oscillator, Uniform
+    R = models.resolver(c)
+    A, om = c.col_create("A"), c.col_create("om")
+    c.sample(A, HalfNormal(2.0).dist(R))
+    c.sample(om, Uniform(0.5, 3.0).dist(R))
+    if which.startswith("generic"):
+        v = c.col_create("v", 2)
+        c.sample(v, MvNormal([wsmc.Col("A"), 0.0], 0.3).dist(R))
+        c.observe(MvNormal(wsmc.Col("v"), 0.5 * np.eye(2)).dist(R), models._const([0.4, -0.2]))
+    accs = []
+    n_obs = {"generic": 0, "generic_osc": 20, "lone_osc": 1, "scalar": 0}[which]
+    ts = np.linspace(0.0, 4.0, 20)
+    for k in range(n_obs):
+        mean = Oscillator(float(ts[k]), wsmc.Col("A"), wsmc.Col("om"), 0.2, 0.3)
+        c.observe(Normal(mean, 0.8).dist(R), models._const([math.cos(ts[k])]))
+    if which in ("generic", "scalar"):
+        for k in range(6):
+            c.observe(Normal(wsmc.Col("A") + float(k) * wsmc.Col("om"), 1.1).dist(R), models._const([0.5 * k]))
+    c.resample(1.0)
+    for _ in range(2):
+        accs.append(c.move(abi.PROPOSAL_AUTORW, [A, om], 1e-3, lo=[0.0, 0.5], hi=[math.inf, 3.0]))
+        accs.append(c.move(abi.PROPOSAL_RW, [om], 0.2, lo=[0.5], hi=[3.0]))
+    return accs
+
+
+@pytest.mark.parametrize("which", ["generic", "generic_osc", "lone_osc", "scalar"])
+def test_move_fold_kernel_variants(gpu_available, which):
+    """Every compiled-fold kernel variant (generic / lean / lean with oscillators) bit for bit
+    against the oracle's term-by-term fold, carried scores included."""
+    g, o = wsmc.Context(3001, seed=17), Oracle(3001, seed=17)
+    assert _fold_paths_program(g, which) == _fold_paths_program(o, which)
+    assert_same_state(g, o)
