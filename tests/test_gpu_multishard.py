@@ -545,3 +545,32 @@ def test_multi_handle_matches_oracle(gpu_available, shards, transport, mode):
     np.testing.assert_array_equal(g.col_gather_rows(g.col_find("v"), rows),
                                   o.col_download(o.col_find("v"))[:, rows])
     g.close()
+
+
+def test_one_rank_rccl_autorw_not_pd(gpu_available):
+    """Sharded autoRW combines the ranks' moment totals on the device (k_autorw_combine): a
+    singular covariance sets the device flag, the Move leaves the state untouched and the call
+    raises PosDefException (src/move_kernels.jl:150), as on one GPU — through a one-rank RCCL
+    communicator, so the sharded path runs."""
+    import numpy as np
+    import wsmc
+    from oracle import Oracle
+    from wsmc import abi, models
+    from wsmc.dsl import Normal
+    from test_gpu_parity import assert_same_state
+    N = 2048
+    g = wsmc.Context(N, seed=4)
+    g.comm_init(wsmc.Context.comm_unique_id(), 1, 0, 0, N)
+    res = []
+    for c in (g, Oracle(N, seed=4)):
+        R = models.resolver(c)
+        a, b = c.col_create("a"), c.col_create("b")
+        c.sample(a, Normal(0.0, 1.0).dist(R))
+        c.assign(b, abi.Operand.column(a, coef=2.0))      # b = 2a: rank-1 covariance
+        c.observe(Normal(wsmc.Col("a"), 1.0).dist(R), models._const([0.2]))
+        with pytest.raises(np.linalg.LinAlgError):
+            c.move(abi.PROPOSAL_AUTORW, [a, b], 1e-3)
+        acc = c.move(abi.PROPOSAL_AUTORW, [a], 1e-3)
+        res.append((c, acc))
+    assert res[0][1] == res[1][1]
+    assert_same_state(res[0][0], res[1][0])

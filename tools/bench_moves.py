@@ -17,11 +17,18 @@ import wsmc
 from wsmc import models
 
 
-def c3(N=1_000_000, reps=3, wait_moves=True):
+def _ctx(N, one_rank):
+    ctx = wsmc.Context(N, seed=42)
+    if one_rank:   # the sharded code path (record / moment exchanges) through a one-rank communicator
+        ctx.comm_init(wsmc.Context.comm_unique_id(), 1, 0, 0, N)
+    return ctx
+
+
+def c3(N=1_000_000, reps=3, wait_moves=True, one_rank=False):
     xs, ys = models.linreg_data()
     best = math.inf
     for _ in range(reps + 1):
-        ctx = wsmc.Context(N, seed=42)
+        ctx = _ctx(N, one_rank)
         ctx.sync()
         t0 = time.perf_counter()
         acc = models.linreg_statements(ctx, xs, ys, ess_perc_min=1.0, wait_moves=wait_moves)
@@ -32,17 +39,18 @@ def c3(N=1_000_000, reps=3, wait_moves=True):
         best = min(best, dt)
     T = len(xs)
     return {"config": "C3 linear regression + autoRW (N=1M, T=10, ess 1.0)"
-                      + ("" if wait_moves else ", asynchronous moves (no accepted counts)"), "N": N, "T": T,
+                      + ("" if wait_moves else ", asynchronous moves (no accepted counts)")
+                      + (", sharded path (one-rank RCCL communicator)" if one_rank else ""), "N": N, "T": T,
             "seconds_per_run": best, "particle_steps_per_s": N * T / best, "moves": 2 * len(acc),
             "log_evidence": ev}
 
 
-def c5(N=4_000_000, T=60, sweeps=5, reps=1, scheme="systematic", ess=1.0, diversity=None):
+def c5(N=4_000_000, T=60, sweeps=5, reps=1, scheme="systematic", ess=1.0, diversity=None, one_rank=False):
     t_obs, y_obs = models.oscillator_data(n=T)
     sch = {"systematic": wsmc.RESAMPLE_SYSTEMATIC, "stratified": wsmc.RESAMPLE_STRATIFIED}[scheme]
     best, moved = math.inf, 0
     for _ in range(reps + 1):
-        ctx = wsmc.Context(N, seed=42)
+        ctx = _ctx(N, one_rank)
         ctx.sync()
         t0 = time.perf_counter()
         acc = models.oscillator_statements(ctx, t_obs, y_obs, ess_perc_min=ess, scheme=sch, sweeps=sweeps,
@@ -53,7 +61,8 @@ def c5(N=4_000_000, T=60, sweeps=5, reps=1, scheme="systematic", ess=1.0, divers
         best = min(best, dt)
         moved = sum(x for a in acc for x in a)   # accepted proposals (a skipped gated move: 0)
     gate = "ungated" if diversity is None else f"diversity={diversity}"
-    out = {"config": f"C5 damped oscillator, {scheme}, {sweeps} {gate} sweep(s) (N={N}, T={T}, ess {ess})",
+    out = {"config": f"C5 damped oscillator, {scheme}, {sweeps} {gate} sweep(s) (N={N}, T={T}, ess {ess})"
+                     + (", sharded path (one-rank RCCL communicator)" if one_rank else ""),
            "N": N, "T": T, "seconds_per_run": best, "particle_steps_per_s": N * T / best,
            "accepted": moved, "moves_offered": 2 * sweeps * T}
     if diversity is None and ess >= 1.0:
@@ -71,6 +80,8 @@ LEGS = {
     "c5_stratified": lambda: c5(scheme="stratified"),                     # the reference's scheme
     "c5_example": lambda: c5(sweeps=1, scheme="stratified", ess=0.5, diversity=0.9),   # as written
     "c3async": lambda: c3(wait_moves=False),
+    "c3_rccl1": lambda: c3(one_rank=True),
+    "c5_rccl1": lambda: c5(one_rank=True),
 }
 
 

@@ -2126,87 +2126,30 @@ int wsmc_marginal_diversity(wsmc_ctx* c, const int32_t* targets, int32_t d, doub
 // autoRW proposal factor on a sharded context: global max log-weight, then
 // each rank's canonical moment totals all-gathered and combined in rank order (the
 // oracle's sharded restatement), then the same min_step / 2.38/sqrt(d) / Cholesky as the
-// single-GPU kernel, on the host. Leaves L in mom + 32; WSMC_ENOTPD before any change.
+// single-GPU kernel — all on the stream (k_max_publish/adopt, k_autorw_combine), no host
+// round trip: a not-PD factor sets the device flag, the Move skips on it and the host reports
+// WSMC_ENOTPD after the Move (state untouched, as the reference throws before changing it).
 static int sharded_autorw(wsmc_ctx* c, const int32_t* targets, int d, const double* lo, const double* hi,
                           double min_step) {
     const int W = c->world;
-    // global max: local slots -> one encoded max per rank -> all-gather -> max
+    constexpr int kStride = 16;   // u64 words per rank in c->xchg
     WSMC_HIP(hipMemsetAsync(c->mslots, 0, sizeof(MaxSlots), c->stream));
     WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, c->mslots));
-    MaxSlots hs;
-    WSMC_HIP(hipMemcpyAsync(&hs, c->mslots, sizeof(MaxSlots), hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
-    unsigned long long menc = 0;
-    for (int k = 0; k < kSlots; ++k) menc = hs.v[k][0] > menc ? hs.v[k][0] : menc;
-    std::vector<unsigned long long> ex(W);
-    auto all_gather_host = [&](const unsigned long long* mine, int words, unsigned long long* all) -> int {
-        unsigned long long* dbuf = c->xchg;   // 16 words per rank
-        WSMC_HIP(hipMemcpyAsync(dbuf + (size_t)c->rank * words, mine, sizeof(unsigned long long) * words,
-                                hipMemcpyHostToDevice, c->stream));
-        int r = exchange_words(c, dbuf, words, c->stream);
-        if (r) return r;
-        WSMC_HIP(hipMemcpyAsync(all, dbuf, sizeof(unsigned long long) * words * W, hipMemcpyDeviceToHost, c->stream));
-        WSMC_HIP(hipStreamSynchronize(c->stream));
-        return WSMC_OK;
-    };
-    int r = all_gather_host(&menc, 1, ex.data());
+    WSMC_HIP(launch_max_publish(c->stream, c->mslots, c->xchg + (size_t)c->rank * kStride));
+    int r = exchange_words(c, c->xchg, kStride, c->stream);
     if (r) return r;
-    for (int g = 0; g < W; ++g) menc = ex[g] > menc ? ex[g] : menc;
-    std::memset(&hs, 0, sizeof(hs));
-    hs.v[0][0] = menc;
-    WSMC_HIP(hipMemcpyAsync(c->mslots, &hs, sizeof(MaxSlots), hipMemcpyHostToDevice, c->stream));
-    // pass 1: totals {sum e, sum e z_k} per rank -> rank-order sums -> means
-    const int n1 = 1 + d, n2 = d * (d + 1) / 2;
-    std::vector<unsigned long long> all(10 * W);
-    double mom[64];
-    WSMC_HIP(launch_moments(c->stream, c->w, c->mslots, c->d_colptr, targets, d, lo, hi, 1, c->mom, c->N,
-                            c->tilepart));
-    WSMC_HIP(launch_moments_final(c->stream, c->tilepart, c->ntiles, d, 1, min_step, c->mom, c->dflag, 2));
-    WSMC_HIP(hipMemcpyAsync(mom, c->mom, sizeof(mom), hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
-    if ((r = all_gather_host(reinterpret_cast<const unsigned long long*>(mom + 48), n1, all.data()))) return r;
-    std::vector<double> t1(n1);
-    for (int v = 0; v < n1; ++v) {
-        double acc = 0.0;
-        for (int g = 0; g < W; ++g) {
-            double x;
-            std::memcpy(&x, &all[(size_t)g * n1 + v], 8);
-            acc = g == 0 ? x : acc + x;
-        }
-        t1[v] = acc;
+    // the ranks' maxima sit kStride words apart: gather them into the first W words
+    WSMC_HIP(launch_autorw_max(c->stream, c->xchg, W, kStride, c->mslots));
+    for (int pass = 1; pass <= 2; ++pass) {
+        const int nv = pass == 1 ? 1 + d : d * (d + 1) / 2;
+        WSMC_HIP(launch_moments(c->stream, c->w, c->mslots, c->d_colptr, targets, d, lo, hi, pass, c->mom, c->N,
+                                c->tilepart));
+        WSMC_HIP(launch_moments_final(c->stream, c->tilepart, c->ntiles, d, pass, min_step, c->mom, c->dflag, 2));
+        WSMC_HIP(hipMemcpyAsync(c->xchg + (size_t)c->rank * kStride, c->mom + 48, sizeof(double) * nv,
+                                hipMemcpyDeviceToDevice, c->stream));
+        if ((r = exchange_words(c, c->xchg, kStride, c->stream))) return r;
+        WSMC_HIP(launch_autorw_combine(c->stream, c->xchg, W, kStride, d, pass, min_step, c->mom, c->dflag));
     }
-    const double S0 = t1[0];
-    for (int k = 0; k < d; ++k) mom[k] = t1[1 + k] / S0;
-    mom[8] = S0;
-    WSMC_HIP(hipMemcpyAsync(c->mom, mom, sizeof(double) * 16, hipMemcpyHostToDevice, c->stream));
-    // pass 2: centred products per rank -> rank-order sums -> covariance -> factor
-    WSMC_HIP(launch_moments(c->stream, c->w, c->mslots, c->d_colptr, targets, d, lo, hi, 2, c->mom, c->N,
-                            c->tilepart));
-    WSMC_HIP(launch_moments_final(c->stream, c->tilepart, c->ntiles, d, 2, min_step, c->mom, c->dflag, 2));
-    WSMC_HIP(hipMemcpyAsync(mom + 48, c->mom + 48, sizeof(double) * 16, hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
-    if ((r = all_gather_host(reinterpret_cast<const unsigned long long*>(mom + 48), n2, all.data()))) return r;
-    double S[16], L[16];
-    int v = 0;
-    for (int a = 0; a < d; ++a)
-        for (int b = a; b < d; ++b, ++v) {
-            double acc = 0.0;
-            for (int g = 0; g < W; ++g) {
-                double x;
-                std::memcpy(&x, &all[(size_t)g * n2 + v], 8);
-                acc = g == 0 ? x : acc + x;
-            }
-            const double cv = acc / S0;
-            S[a * d + b] = cv;
-            S[b * d + a] = cv;
-        }
-    const double lam = 2.38 / wsmc_sqrt((double)d);
-    for (int k = 0; k < d * d; ++k) {
-        if (S[k] == 0.0) S[k] = min_step;
-        S[k] = lam * S[k];
-    }
-    if (!wsmc_cholesky(S, L, d)) return fail(WSMC_ENOTPD, "autoRW proposal covariance is not positive definite");
-    WSMC_HIP(hipMemcpyAsync(c->mom + 32, L, sizeof(double) * 16, hipMemcpyHostToDevice, c->stream));
     return WSMC_OK;
 }
 
@@ -2368,7 +2311,7 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         for (int k = 0; k < 4; ++k) { remap(t.x[k]); remap(t.dist.mu[k]); }
         remap(t.dist.scale);
     }
-    const int32_t* mflag = (proposal == WSMC_PROPOSAL_AUTORW && !is_sharded(c)) ? c->dflag : nullptr;
+    const int32_t* mflag = proposal == WSMC_PROPOSAL_AUTORW ? c->dflag : nullptr;
     if ((int)slots.size() <= kFoldSlots) {
         // the fold program: s_new over [0, kD), s_old over [cache_from or 0, kD)
         std::vector<FoldSeg> segs;

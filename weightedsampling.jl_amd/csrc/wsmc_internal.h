@@ -368,6 +368,10 @@ hipError_t launch_gather_rows(hipStream_t s, const double* src, int64_t N, int d
                               double* out);
 // exact sharding: global max from the all-gathered per-rank maxima (words[world]) into ms
 hipError_t launch_max_adopt(hipStream_t s, const unsigned long long* words, int world, MaxSlots* ms);
+hipError_t launch_autorw_max(hipStream_t s, const unsigned long long* words, int world, int stride, MaxSlots* ms);
+// sharded autoRW: rank-order combine of the all-gathered moment totals (pass 1 means, pass 2 factor)
+hipError_t launch_autorw_combine(hipStream_t s, const unsigned long long* xchg, int world, int stride, int d,
+                                 int pass, double min_step, double* mom, int32_t* flag);
 hipError_t launch_max_publish(hipStream_t s, const MaxSlots* ms, unsigned long long* word);
 // exact sharding: records summed as integers (the single-GPU decision bits), slot windows
 hipError_t launch_rs_decide_exact(hipStream_t s, const ShardRecord* recs, int world, int rank, double ess_min,

@@ -1511,6 +1511,46 @@ __global__ __launch_bounds__(kBlock) void k_moments(const double* __restrict__ w
     }
 }
 
+// Sharded autoRW: the ranks' raw moment totals, all-gathered as `stride` u64
+// words per rank (the bits of the doubles), summed in rank order; pass 1 -> the means and S0,
+// pass 2 -> min_step, 2.38/sqrt(d), Cholesky (not PD -> flag): the host combine's arithmetic,
+// on the device (no host round trip per pass).
+__global__ void k_autorw_combine(const u64* __restrict__ xchg, int world, int stride, int d, int pass,
+                                 double min_step, double* mom, int32_t* flag) {
+    if (threadIdx.x != 0) return;
+    auto total = [&](int v) {
+        double acc = 0.0;
+        for (int g = 0; g < world; ++g) {
+            const double x = __builtin_bit_cast(double, xchg[(int64_t)g * stride + v]);
+            acc = g == 0 ? x : acc + x;
+        }
+        return acc;
+    };
+    if (pass == 1) {
+        const double S0 = total(0);
+        for (int k = 0; k < d; ++k) mom[k] = total(1 + k) / S0;
+        mom[8] = S0;
+        return;
+    }
+    const double S0 = mom[8];
+    double S[16], L[16];
+    int v = 0;
+    for (int a = 0; a < d; ++a)
+        for (int b = a; b < d; ++b, ++v) {
+            const double cv = total(v) / S0;
+            S[a * d + b] = cv;
+            S[b * d + a] = cv;
+        }
+    const double lam = 2.38 / wsmc_sqrt((double)d);
+    for (int k = 0; k < d * d; ++k) {
+        if (S[k] == 0.0) S[k] = min_step;
+        S[k] = lam * S[k];
+    }
+    const int ok = wsmc_cholesky(S, L, d);
+    for (int k = 0; k < 16; ++k) mom[32 + k] = k < d * d ? L[k] : 0.0;
+    if (!ok) flag[0] = 1;
+}
+
 __global__ __launch_bounds__(kBlock) void k_moments_final(const double* tilepart, int64_t ntiles, int d,
                                                           int pass, double min_step, double* mom,
                                                           int32_t* flag, int raw) {
@@ -2125,6 +2165,22 @@ hipError_t launch_rs_decide(hipStream_t s, const ShardRecord* recs, int world, i
 }
 hipError_t launch_max_publish(hipStream_t s, const MaxSlots* ms, u64* word) {
     hipLaunchKernelGGL(k_max_publish, dim3(1), dim3(64), 0, s, ms, word);
+    return hipGetLastError();
+}
+// the global max from the ranks' words `stride` apart (k_max_adopt's rule)
+__global__ void k_autorw_max(const u64* words, int world, int stride, MaxSlots* ms) {
+    const int th = threadIdx.x;
+    u64 m = 0;
+    for (int g = 0; g < world; ++g) m = words[(int64_t)g * stride] > m ? words[(int64_t)g * stride] : m;
+    ms->v[th & 63][0] = th == 0 ? m : 0ull;
+}
+hipError_t launch_autorw_max(hipStream_t s, const u64* words, int world, int stride, MaxSlots* ms) {
+    hipLaunchKernelGGL(k_autorw_max, dim3(1), dim3(64), 0, s, words, world, stride, ms);
+    return hipGetLastError();
+}
+hipError_t launch_autorw_combine(hipStream_t s, const u64* xchg, int world, int stride, int d, int pass,
+                                 double min_step, double* mom, int32_t* flag) {
+    hipLaunchKernelGGL(k_autorw_combine, dim3(1), dim3(64), 0, s, xchg, world, stride, d, pass, min_step, mom, flag);
     return hipGetLastError();
 }
 hipError_t launch_max_adopt(hipStream_t s, const u64* words, int world, MaxSlots* ms) {
