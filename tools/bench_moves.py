@@ -81,6 +81,7 @@ LEGS = {
     "c5_example": lambda: c5(sweeps=1, scheme="stratified", ess=0.5, diversity=0.9),   # as written
     "c3async": lambda: c3(wait_moves=False),
     "c3_rccl1": lambda: c3(one_rank=True),
+    "c3async_rccl1": lambda: c3(wait_moves=False, one_rank=True),
     "c5_rccl1": lambda: c5(one_rank=True),
 }
 

@@ -2248,7 +2248,7 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
     if (r) return r;
     // asynchronous (no count requested): no host wait; a pending failure flag stays set (the
     // kernels skip on it) until the next synchronizing call reports it
-    const bool async = !accepted_out && !is_sharded(c);
+    const bool async = !accepted_out;   // sharded too: the factor and its PD flag are device-side
     if (!async && (r = check_deferred(c))) return r;
     if (!c->move_pending) WSMC_HIP(hipMemsetAsync(c->dflag, 0, sizeof(int32_t) * 4, c->stream));
     if (accepted_out) WSMC_HIP(hipMemsetAsync(c->ucount, 0, sizeof(unsigned long long) * 4, c->stream));
