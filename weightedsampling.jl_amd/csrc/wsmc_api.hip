@@ -25,10 +25,20 @@ int fail(int code, const std::string& msg) {
 }
 }  // namespace wsmc
 
-#define CHECK_CTX(ctx)                                                   \
+// every entry point: the device, then any deferred weight reset applied before the call reads
+// or writes the weights (CHECK_CTX_KEEP: the Observe / Weight path, which applies it itself)
+#define CHECK_CTX_KEEP(ctx)                                              \
     do {                                                                 \
         if (!(ctx)) return fail(WSMC_EARG, "null context");              \
         WSMC_HIP(hipSetDevice((ctx)->device));                           \
+    } while (0)
+#define CHECK_CTX(ctx)                                                   \
+    do {                                                                 \
+        CHECK_CTX_KEEP(ctx);                                             \
+        if ((ctx)->w_reset_pending) {                                    \
+            WSMC_HIP(launch_fill_weights((ctx)->stream, (ctx)->w, (ctx)->w_reset_pending, (ctx)->N)); \
+            (ctx)->w_reset_pending = nullptr;                            \
+        }                                                                \
     } while (0)
 
 
@@ -585,7 +595,7 @@ int wsmc_comm_set_shard_mode(wsmc_ctx* c, int32_t mode) {
 // ---- store ---------------------------------------------------------------------------
 int wsmc_col_create(wsmc_ctx* c, const char* name, int32_t dim, int32_t* col_id) {
     if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { int32_t id = -1; int r = wsmc_col_create(x, name, dim, &id); if (x == multi_first(c) && col_id) *col_id = id; return r; });
-    CHECK_CTX(c);
+    CHECK_CTX_KEEP(c);   // no weights touched
     if (!name || !col_id) return fail(WSMC_EARG, "null argument");
     for (size_t k = 0; k < c->cols.size(); ++k)
         if (c->cols[k].name == name) {
@@ -1691,7 +1701,7 @@ int wsmc_log_evidence(wsmc_ctx* c, double* out) {
 // ---- operators -----------------------------------------------------------------------
 int wsmc_assign(wsmc_ctx* c, int32_t out, const wsmc_operand* expr) {
     if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { return wsmc_assign(x, out, expr); });
-    CHECK_CTX(c);
+    CHECK_CTX_KEEP(c);   // reads and writes no weights: a pending reset stays pending
     if (!valid_col(c, out) || !expr) return fail(WSMC_EARG, "bad output column");
     const int dim = c->cols[out].dim;
     for (int k = 0; k < dim; ++k) {
@@ -1756,7 +1766,7 @@ static void push_sample_term(wsmc_ctx* c, int32_t out, const wsmc_dist& d) {
 
 int wsmc_sample(wsmc_ctx* c, int32_t out, const wsmc_dist* d) {
     if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { return wsmc_sample(x, out, d); });
-    CHECK_CTX(c);
+    CHECK_CTX_KEEP(c);   // reads and writes no weights: a pending reset stays pending
     if (!valid_col(c, out) || !d) return fail(WSMC_EARG, "bad output column");
     int r = check_dist(c, *d);
     if (r) return r;
@@ -1801,7 +1811,7 @@ int wsmc_sample_importance(wsmc_ctx* c, int32_t out, const wsmc_dist* prop, cons
 
 static int weigh(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x, int kind) {
     if (c && c->multi) return multi_each(c, [&](wsmc_ctx* s) { return weigh(s, d, x, kind); });
-    CHECK_CTX(c);
+    CHECK_CTX_KEEP(c);   // a pending weight reset is applied by the kernel itself
     if (!d || !x) return fail(WSMC_EARG, "null argument");
     int r = check_dist(c, *d);
     if (r) return r;
@@ -1820,7 +1830,9 @@ static int weigh(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x, int kin
     if ((r = need_cols(c, reads))) return r;
     if ((r = upload_colptr(c))) return r;
     const int wb = c->wnext;
-    WSMC_HIP(launch_weigh(c->stream, t, c->w, c->d_colptr, c->N, c->wslots[wb], c->wslots[wb ^ 1]));
+    WSMC_HIP(launch_weigh(c->stream, t, c->w, c->d_colptr, c->N, c->wslots[wb], c->wslots[wb ^ 1],
+                          c->w_reset_pending));
+    c->w_reset_pending = nullptr;
     c->wnext = wb ^ 1;
     c->wmax_buf = wb;
     c->wseq += 1;
@@ -1848,7 +1860,7 @@ static inline int64_t run_grp_words(int64_t N);
 
 int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resampled_out, double* ess_out) {
     if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { int32_t rs = 0; double e = 0; const bool f = x == multi_first(c); int r = wsmc_resample(x, ess_min, scheme, resampled_out ? &rs : nullptr, ess_out ? &e : nullptr); if (!r && f) { if (resampled_out) *resampled_out = rs; if (ess_out) *ess_out = e; } return r; });
-    CHECK_CTX(c);
+    CHECK_CTX_KEEP(c);   // a gated no-op Resample leaves a pending weight reset pending (settled below)
     if (!valid_scheme(scheme)) return fail(WSMC_EARG, "unknown resampling scheme");
     if (scheme == WSMC_RESAMPLE_MULTINOMIAL && exact_mode(c))
         return fail(WSMC_EARG, "multinomial draws on exact shards are not supported (island mode is)");
@@ -1865,6 +1877,10 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
         if (resampled_out) *resampled_out = c->resampled;
         if (ess_out) *ess_out = c->last_ess;
         return WSMC_OK;
+    }
+    if (c->w_reset_pending) {   // (a weight write settles it first, so this does not happen)
+        WSMC_HIP(launch_fill_weights(c->stream, c->w, c->w_reset_pending, c->N));
+        c->w_reset_pending = nullptr;
     }
     if (exact_mode(c)) {
         Decision d;
@@ -1913,6 +1929,7 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
         plan.w_reset = nullptr;
         plan.grp_zero = c->rs_grp[c->rs_grp_cur];
         plan.grp_zero_words = gw;
+        plan.ms_reset = pre ? ms : nullptr;
         if (!pre) {
             WSMC_HIP(hipMemsetAsync(ms, 0, sizeof(MaxSlots), c->stream));
             WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, ms));
@@ -1921,9 +1938,16 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
         WSMC_HIP(launch_rs_sums(c->stream, c->w, c->N, ms, c->tilep, c->qbuf, nullptr, nullptr, grp, G));
         WSMC_HIP(launch_rs_fill_fused(c->stream, c->N, plan, grp, G, ms, ess_min, c->rec + c->rank, row.dec, c->qbuf,
                                       row.anc));
-        // the reset also leaves the max of the new weights in ms (an Observe's slots: nothing
-        // else writes them before the next Observe, which moves on to the other buffer)
-        WSMC_HIP(launch_fill_weights(c->stream, c->w, row.dec, c->N, pre ? ms : nullptr));
+        // the weight reset is deferred to the first reader (the next Observe applies it in
+        // its kernel; any other call runs it first, CHECK_CTX); the fill's record block
+        // already leaves the max of the reset weights in ms (an Observe's slots: nothing else
+        // writes them before the next Observe, which moves on to the other buffer)
+        static const bool eager_reset = [] {   // diagnostics: reset in the Resample (A/B)
+            const char* e = getenv("WSMC_DIAG_EAGER_RESET");
+            return e && atoi(e) != 0;
+        }();
+        if (eager_reset) WSMC_HIP(launch_fill_weights(c->stream, c->w, row.dec, c->N));
+        else c->w_reset_pending = row.dec;
         max_kept = pre;
     } else {
         if ((r = enqueue_resample_stats(c, c->w, ms, c->rec, ess_min, row.dec, !pre, plan))) return r;

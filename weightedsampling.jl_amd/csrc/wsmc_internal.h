@@ -146,6 +146,10 @@ struct wsmc_ctx {
     // its weight reset), valid while cur_max_seq == wseq: a Move's autoRW skips its max pass
     wsmc::MaxSlots* cur_max = nullptr;
     uint64_t cur_max_seq = ~0ull;
+    // a fused generic Resample's weight reset, not yet applied to `w` (the decision on the
+    // device): the next Observe / Weight applies it in its kernel, any other call first runs
+    // the gated reset (settle_weights, from CHECK_CTX)
+    wsmc::Decision* w_reset_pending = nullptr;
     int64_t N = 0;
     uint64_t seed = 0;
 
@@ -282,7 +286,7 @@ hipError_t launch_sample_importance(hipStream_t s, double* out, int dim, const w
                                     const wsmc_dist& targ, double* w, uint64_t seed, uint64_t op,
                                     int64_t goff, double* const* cols, int64_t N);
 hipError_t launch_weigh(hipStream_t s, const wsmc_term& t, double* w, double* const* cols, int64_t N, MaxSlots* ms,
-                        MaxSlots* ms_next);
+                        MaxSlots* ms_next, const Decision* wreset = nullptr);
 hipError_t launch_rs_max(hipStream_t s, const double* w, int64_t N, MaxSlots* ms);
 hipError_t launch_rs_sums(hipStream_t s, const double* w, int64_t N, const MaxSlots* ms,
                           unsigned long long* tilep, unsigned long long* qbuf,
@@ -301,6 +305,7 @@ struct FillPlan {          // ancestor-fill task planning (in the reduce kernel)
     double* w_reset = nullptr;         // generic Resample: the tile blocks reset the weights to dec->mean
     Decision* host_dec = nullptr;      // generic Resample: the decision also written to host-mapped memory
     unsigned long long* grp_zero = nullptr;   // fused fill: the next call's group lines, zeroed by its record block
+    MaxSlots* ms_reset = nullptr;      // fused fill: the record block writes the reset weights' max here
     int64_t grp_zero_words = 0;
 };
 hipError_t launch_rs_reduce(hipStream_t s, const MaxSlots* ms, const unsigned long long* tilep, int64_t N,

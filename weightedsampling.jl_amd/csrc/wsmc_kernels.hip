@@ -241,9 +241,12 @@ __global__ __launch_bounds__(kBlock) void k_sample_importance(double* out, int d
 // Observe / Weight: weights += logpdf, and the block max of the new weights into the 64
 // slots of `ms` (zero on entry), so the Resample that follows needs no max pass; block 0
 // zeroes `ms_next`, the slots the next launch will use (k_rs_max's encoding and slots)
+// wreset != null: a Resample's weight reset still pending (the fused generic Resample defers
+// it to its first reader): a particle's weight is wreset->mean when that step resampled
 template <unsigned FEAT>
 __global__ __launch_bounds__(kBlock) void k_weigh(wsmc_term t, double* w, double* const* cols, int64_t N,
-                                                  MaxSlots* ms, MaxSlots* ms_next, wsmc_logmemo lm0) {
+                                                  MaxSlots* ms, MaxSlots* ms_next, wsmc_logmemo lm0,
+                                                  const Decision* wreset) {
     __shared__ u64 lds[4];
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     u64 m = 0;
@@ -251,7 +254,8 @@ __global__ __launch_bounds__(kBlock) void k_weigh(wsmc_term t, double* w, double
         // lm0: a constant scale operand's log, evaluated once by the host and handed to the
         // term through the fold's log memo (the same bits every particle would compute)
         wsmc_logmemo lm = lm0;
-        const double v = w[i] + wsmc_term_logpdf_mf(&t, cols, N, i, nullptr, &lm, FEAT);
+        const double w0 = (wreset && wreset->resampled) ? wreset->mean : w[i];
+        const double v = w0 + wsmc_term_logpdf_mf(&t, cols, N, i, nullptr, &lm, FEAT);
         w[i] = v;
         m = wsmc_ord_enc(v);
     }
@@ -1279,6 +1283,12 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
             if (dec) {
                 decide_records(&r, 1, 0, ess_min, dec);
                 if (plan.host_dec) *plan.host_dec = *dec;   // the generic Resample's host copy
+                // the generic Resample defers its weight reset: the max of the reset (equal)
+                // weights goes into the slots now (the fill's other blocks never read them)
+                if (plan.ms_reset && dec->resampled) {
+                    plan.ms_reset->v[0][0] = wsmc_ord_enc(dec->mean);
+                    for (int k = 1; k < kSlots; ++k) plan.ms_reset->v[k][0] = 0ull;
+                }
             }
         }
         return;
@@ -2093,7 +2103,7 @@ hipError_t launch_sample_importance(hipStream_t s, double* out, int dim, const w
     return hipGetLastError();
 }
 hipError_t launch_weigh(hipStream_t s, const wsmc_term& t, double* w, double* const* cols, int64_t N, MaxSlots* ms,
-                        MaxSlots* ms_next) {
+                        MaxSlots* ms_next, const Decision* wreset) {
     wsmc_logmemo lm0 = {0, 0.0, 0.0, 0};
     if (t.dist.family != WSMC_FAM_UNIFORM && wsmc_operand_is_const(&t.dist.scale)) {
         const double sc = wsmc_operand_eval(&t.dist.scale, nullptr, N, 0, nullptr);
@@ -2103,9 +2113,10 @@ hipError_t launch_weigh(hipStream_t s, const wsmc_term& t, double* w, double* co
         lm0.valid = 1;
     }
     if (t.dist.mean_fn == WSMC_MEAN_OSCILLATOR)
-        hipLaunchKernelGGL(k_weigh<WSMC_FEAT_ALL>, grid_for(N), dim3(kBlock), 0, s, t, w, cols, N, ms, ms_next, lm0);
+        hipLaunchKernelGGL(k_weigh<WSMC_FEAT_ALL>, grid_for(N), dim3(kBlock), 0, s, t, w, cols, N, ms, ms_next, lm0,
+                           wreset);
     else
-        hipLaunchKernelGGL(k_weigh<0u>, grid_for(N), dim3(kBlock), 0, s, t, w, cols, N, ms, ms_next, lm0);
+        hipLaunchKernelGGL(k_weigh<0u>, grid_for(N), dim3(kBlock), 0, s, t, w, cols, N, ms, ms_next, lm0, wreset);
     return hipGetLastError();
 }
 template <typename K, typename... Args>
