@@ -456,3 +456,46 @@ def test_move_fold_kernel_variants(gpu_available, which):
     g, o = wsmc.Context(3001, seed=17), Oracle(3001, seed=17)
     assert _fold_paths_program(g, which) == _fold_paths_program(o, which)
     assert_same_state(g, o)
+
+
+@pytest.mark.parametrize("reader", ["observe", "weight", "importance", "evidence", "ess", "moments",
+                                    "noop_resample", "download"])
+def test_deferred_weight_reset_readers(gpu_available, reader):
+    """A one-GPU Resample defers its weight reset to the first reader: an
+    Observe / Weight applies it in its kernel, every other call settles it first; Assign,
+    Sample and a gated no-op Resample in between leave it pending. Each reader, after those,
+    against the oracle (whose Resample resets at once)."""
+    from wsmc.dsl import Normal, Uniform
+    res = []
+    for c in (wsmc.Context(5003, seed=23), Oracle(5003, seed=23)):
+        R = models.resolver(c)
+        a, b = c.col_create("a"), c.col_create("b")
+        c.sample(a, Normal(0.0, 1.5).dist(R))
+        c.observe(Normal(wsmc.Col("a"), 0.8).dist(R), models._const([0.4]))
+        c.resample(1.0, abi.RESAMPLE_SYSTEMATIC)                 # asynchronous: reset deferred
+        c.assign(b, abi.Operand.column(a, coef=0.5, c0=0.2))     # leaves it pending
+        c.sample(a, Normal(wsmc.Col("b"), 1.0).dist(R))           # leaves it pending
+        c.resample(1.0)                                          # gated no-op: leaves it pending
+        out = None
+        if reader == "observe":
+            c.observe(Normal(wsmc.Col("a"), 0.6).dist(R), models._const([-0.3]))
+        elif reader == "weight":
+            c.weight(Normal(0.0, 2.0).dist(R), [abi.Operand.column(b)])
+        elif reader == "importance":
+            c.sample_importance(b, Normal(0.0, 1.0).dist(R), Uniform(-3.0, 3.0).dist(R))
+        elif reader == "evidence":
+            out = c.log_evidence()
+        elif reader == "ess":
+            out = c.ess()
+        elif reader == "moments":
+            out = c.weighted_moments([abi.Operand.column(a), abi.Operand.column(b, coef=2.0, c0=1.0)])
+        elif reader == "noop_resample":
+            out = c.resample(1.0)
+        res.append((c, out))
+    (g, og), (o, oo) = res
+    if reader == "moments":
+        for x, y in zip(og, oo):
+            np.testing.assert_array_equal(np.asarray(x), np.asarray(y))
+    else:
+        assert og == oo
+    assert_same_state(g, o)
