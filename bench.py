@@ -104,6 +104,39 @@ def cpu_model() -> str:
 CPU_REPS = 5   # timed all-cores CPU runs after the warm-up; the median is reported
 
 
+def pin_openmp() -> dict:
+    """Bind the CPU ports' OpenMP threads one per core, packed (OMP_PLACES=cores,
+    OMP_PROC_BIND=close), so the all-cores figure does not depend on where the scheduler
+    drifts the threads. Must run before the oracle library (and its OpenMP runtime) loads."""
+    os.environ.setdefault("OMP_PLACES", "cores")
+    os.environ.setdefault("OMP_PROC_BIND", "close")
+    return {"OMP_PLACES": os.environ["OMP_PLACES"], "OMP_PROC_BIND": os.environ["OMP_PROC_BIND"]}
+
+
+def cpu_numa(threads: int) -> dict:
+    """The NUMA nodes of the first `threads` CPUs of this process's affinity mask (the cores
+    OMP_PROC_BIND=close packs the threads onto), and the node count of the host."""
+    cpus = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else []
+    nodes = set()
+    for c in cpus[:threads]:
+        try:
+            for e in os.listdir(f"/sys/devices/system/cpu/cpu{c}"):
+                if e.startswith("node") and e[4:].isdigit():
+                    nodes.add(int(e[4:]))
+        except OSError:
+            pass
+    try:
+        total = len([e for e in os.listdir("/sys/devices/system/node") if e.startswith("node") and e[4:].isdigit()])
+    except OSError:
+        total = None
+    return {"nodes_used": sorted(nodes), "host_nodes": total, "affinity_cpus": len(cpus)}
+
+
+def rep_stats(ts) -> dict:
+    t = sorted(ts)
+    return {"min_s": t[0], "median_s": t[len(t) // 2], "max_s": t[-1], "reps": len(t)}
+
+
 def _oracle():
     sys.path.insert(0, str(REPO / "oracle"))
     import oracle  # test infrastructure: only the cpu_baseline leg loads it
@@ -125,7 +158,7 @@ def cpu_baseline_mt(obs, n, T, ess, scheme, threads, seed):
                             outputs=False)
         ts.append(time.perf_counter() - t0)
     dt = sorted(ts)[len(ts) // 2]   # median
-    return n * T / dt, dt
+    return n * T / dt, dt, rep_stats(ts)
 
 
 def cpu_baseline_fast(obs, n, T, ess, threads, seed):
@@ -143,7 +176,7 @@ def cpu_baseline_fast(obs, n, T, ess, threads, seed):
         oracle.fast_ssm2d_run(n, obs[:T], ess_perc_min=ess, seed=seed, threads=threads)
         ts.append(time.perf_counter() - t0)
     dt = sorted(ts)[len(ts) // 2]   # median
-    return n * T / dt, dt
+    return n * T / dt, dt, rep_stats(ts)
 
 
 def cpu_fairness_lgssm(n=100_000, T=200, seed=42):
@@ -302,25 +335,30 @@ def main():
             cpu = None
         else:
             nth = cpu_threads(args.cpu_threads)
+            omp = pin_openmp()
+            numa = cpu_numa(nth)   # before the ports run: OpenMP then binds this thread to one core
             n, T = args.cpu_particles, args.cpu_T
-            fps, fdt = cpu_baseline_fast(obs, n, T, args.ess, nth, args.seed)
-            f1, f1dt = cpu_baseline_fast(obs, args.cpu_1t_particles, T, args.ess, 1, args.seed)
-            cps, cdt = cpu_baseline_mt(obs, n, T, args.ess, scheme, nth, args.seed)
+            fps, fdt, fst = cpu_baseline_fast(obs, n, T, args.ess, nth, args.seed)
+            f1, f1dt, _ = cpu_baseline_fast(obs, args.cpu_1t_particles, T, args.ess, 1, args.seed)
+            cps, cdt, cst = cpu_baseline_mt(obs, n, T, args.ess, scheme, nth, args.seed)
             c1, c1dt = cpu_baseline_1t(obs, args.cpu_1t_particles, T, args.ess, scheme, args.seed)
             lg, lgdt = cpu_fairness_lgssm()
             fast_leg = {"value": fps, "unit": "particle-steps/s", "cores": nth, "kind": "port",
                     "sample": f"oracle/wsmc_port_fast.c (the reference's algorithm with xoshiro256++/ziggurat/"
                               f"libm, OpenMP over particles, {nth} threads on {cpu_model()}): the full 2D SSM "
-                              f"run, N={n} T={T} ess_perc_min={args.ess}, history traced back: {fdt:.2f} s (median of {CPU_REPS})"}
+                              f"run, N={n} T={T} ess_perc_min={args.ess}, history traced back: {fdt:.2f} s (median of {CPU_REPS})",
+                    "reps": fst}
             exact_leg = {"value": cps, "unit": "particle-steps/s", "cores": nth, "kind": "port",
                      "sample": f"oracle/wsmc_port_mt.c (bit-identical to the device; OpenMP over particles, "
                                f"{nth} threads on {cpu_model()}): the full 2D SSM run, N={n} T={T} "
-                               f"ess_perc_min={args.ess}, history traced back: {cdt:.2f} s (median of {CPU_REPS})"}
+                               f"ess_perc_min={args.ess}, history traced back: {cdt:.2f} s (median of {CPU_REPS})",
+                     "reps": cst}
             # the baseline is the faster of the two all-cores ports; the other is reported beside it
             best, other, other_key = ((fast_leg, exact_leg, "exact_port") if fps >= cps
                                       else (exact_leg, fast_leg, "fast_port"))
             cpu = dict(best)
             cpu.update({
+                "threads": nth, "binding": omp, "numa": numa, "cpu_model": cpu_model(),
                 other_key: other,
                 "single_thread": {"value": f1, "unit": "particle-steps/s", "cores": 1, "kind": "port",
                                   "sample": f"oracle/wsmc_port_fast.c, 1 thread, N={args.cpu_1t_particles} "

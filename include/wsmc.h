@@ -270,7 +270,8 @@ int wsmc_move(wsmc_ctx* ctx, int32_t proposal, const int32_t* targets, int32_t d
 int wsmc_score(wsmc_ctx* ctx, int32_t target_depth, double* host_scores);
 /* marginal_diversity(store, targets)  (src/transformers.jl:560-565) */
 int wsmc_marginal_diversity(wsmc_ctx* ctx, const int32_t* targets, int32_t d, double* out);
-/* the last resample's ancestors (0-based; debug/parity; synchronising) */
+/* the last resample's ancestors (0-based; debug/parity; synchronising); a multi-device
+ * handle returns population indices (island shards resample within their own range) */
 int wsmc_last_ancestors(wsmc_ctx* ctx, int32_t* host);
 
 /* ---- fused runners (whole model loops; one HIP graph per run) ------------------
@@ -302,6 +303,12 @@ int wsmc_run_get_timing(wsmc_ctx* ctx, wsmc_run_timing* out);
  * context's current weights: kernel 0 = weight statistics, 1 = reduce, 2 = ancestor scan;
  * mode 0 = production variant, > 0 = ablations (see csrc/wsmc_kernels.hip).        */
 int wsmc_debug_kernel_bench(wsmc_ctx* ctx, int32_t kernel, int32_t mode, int32_t iters, double* avg_us);
+/* Test hook: shard `shard` of the handle (0 for a single context) fails its nth next shard
+ * record exchange (a Resample's or an evidence query's) with WSMC_EHIP before exchanging.
+ * On a multi-device handle the other shards then leave their exchange with WSMC_ERCCL
+ * instead of waiting for it; shards that left in different states mark the handle failed
+ * (every later call returns WSMC_ESTATE). nth = 0 disarms.                               */
+int wsmc_debug_inject_failure(wsmc_ctx* ctx, int32_t shard, int32_t nth);
 
 #ifdef __cplusplus
 }

@@ -150,6 +150,8 @@ double* or_col_data(oracle* o, int32_t c) { return o->cols[c].front; }
 /* resample!(store, indices): gather every column front->back, swap (src/stores.jl:105-111) */
 void or_store_resample(oracle* o, const int32_t* idx) {
     int64_t N = o->N;
+    // resample!(store, idx) with caller indices: they are the last ancestors too
+    if (idx != o->last_anc) memcpy(o->last_anc, idx, sizeof(int32_t) * (size_t)N);
     for (int c = 0; c < o->ncols; ++c) {
         or_col* col = &o->cols[c];
         for (int k = 0; k < col->dim; ++k) {

@@ -95,3 +95,64 @@ def test_lazy_explicit_store_resample(gpu_available):
     assert g.store_info()["stale_columns"] == 2
     assert_same_state(g, o)
     np.testing.assert_array_equal(g.last_ancestors(), idx2)   # the last resample!'s indices
+
+
+def _last_anc_program(c, switch, wait):
+    """Resamples that do and do not resample around a store-mode switch. After a Resample
+    the weights are equal; an Observe with no particle operand keeps them equal (exact ESS
+    1), so the next Resample at 1.0 does not resample (strict <, src/transformers.jl:484)."""
+    from wsmc.dsl import Normal
+    R = models.resolver(c)
+    a = c.col_create("a")
+    c.sample(a, Normal(0.0, 1.0).dist(R))
+    flags = []
+
+    def step(y):   # varied weights: resamples
+        c.observe(Normal(wsmc.Col("a"), 0.5).dist(R), models._const([y]))
+        flags.append(c.resample(1.0, wait=wait))
+
+    def flat():    # equal weights stay equal: no resample
+        c.observe(Normal(0.0, 1.0).dist(R), models._const([0.3]))
+        flags.append(c.resample(1.0, wait=wait))
+
+    step(0.2)
+    flat()
+    switch(c)
+    mid = c.last_ancestors()
+    step(-0.1)
+    flat()
+    flat()
+    return flags, mid
+
+
+def _one_rank_exact(c):
+    c.comm_init_host(lambda raw: [raw], 1, 0, 0, c.n)   # one rank: the all-gather is the identity
+    c.comm_set_shard_mode(abi.SHARD_EXACT)
+
+
+@pytest.mark.parametrize("switch", ["none", "eager", "eager_from_start", "exact", "store_resample"])
+@pytest.mark.parametrize("wait", [True, False])
+def test_last_ancestors_across_store_modes(gpu_available, switch, wait):
+    """last_ancestors() is the newest Resample that resampled (the oracle's last_anc), also
+    when the store turns eager or exact mid-run with asynchronous decisions still pending, when
+    later Resamples do not resample, and when resample!(store, idx) follows pending ones."""
+    N = 3000
+    idx = np.arange(N, dtype=np.int32)[::-1].copy()
+    sw = {
+        "none": lambda c: None,
+        "eager": lambda c: c.store_set_lazy(False),
+        "eager_from_start": lambda c: None,
+        "exact": _one_rank_exact,
+        "store_resample": lambda c: c.store_resample(idx),
+    }[switch]
+    g, o = wsmc.Context(N, seed=17), Oracle(N, seed=17)
+    if switch == "eager_from_start":
+        g.store_set_lazy(False)
+    _, mid_g = _last_anc_program(g, sw, wait)
+    _, mid_o = _last_anc_program(o, (lambda c: c.store_resample(idx)) if switch == "store_resample"
+                                 else (lambda c: None), True)
+    np.testing.assert_array_equal(mid_g, mid_o)
+    st = g.get_state()
+    assert st["n_resamples"] == o.get_state()["n_resamples"]
+    np.testing.assert_array_equal(g.last_ancestors(), o.last_ancestors())
+    assert_same_state(g, o)

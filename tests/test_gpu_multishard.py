@@ -574,3 +574,66 @@ def test_one_rank_rccl_autorw_not_pd(gpu_available):
         res.append((c, acc))
     assert res[0][1] == res[1][1]
     assert_same_state(res[0][0], res[1][0])
+
+
+@pytest.mark.parametrize("mode", ["island", "exact"])
+def test_multi_handle_eight_shards_c4_partition(gpu_available, mode):
+    """C4's partition through one handle: SMCState(HipColumnStore(N; gpus=8)) as
+    INTEGRATION.md binds it, here 8 shards x 20k on device 0 with the in-process exchange.
+    Statement path and fused run, against the eight-shard oracle (island) or the unsharded
+    oracle (exact), bit for bit."""
+    sys.path.insert(0, str(REPO / "oracle"))
+    from oracle import Oracle
+    import wsmc
+    from wsmc import abi, models
+    from test_gpu_parity import assert_same_state
+    G, n, T = 8, 20_000, 12
+    N = G * n
+    obs = models.ssm2d_data(T)
+    exact = mode == "exact"
+
+    def oracle():
+        return Oracle(N, seed=42, shards=G, exact=True) if exact else Oracle(N, seed=42, shards=G)
+
+    g = wsmc.Context.multi(N, G, seed=42, devices=[0] * G, transport=abi.TRANSPORT_HOST)
+    if exact:
+        g.comm_set_shard_mode(abi.SHARD_EXACT)
+    o = oracle()
+    assert models.ssm2d_statements(g, obs, ess_perc_min=0.5) == models.ssm2d_statements(o, obs, ess_perc_min=0.5)
+    assert_same_state(g, o)
+    np.testing.assert_array_equal(g.last_ancestors(), o.last_ancestors())
+    assert g.log_evidence() == o.log_evidence()
+    g.close()
+
+    f = wsmc.Context.multi(N, G, seed=42, devices=[0] * G, transport=abi.TRANSPORT_HOST)
+    if exact:
+        f.comm_set_shard_mode(abi.SHARD_EXACT)
+    ev = f.ssm2d_run(obs, ess_perc_min=1.0, keep_history=True)
+    o = oracle()
+    models.ssm2d_statements(o, obs, ess_perc_min=1.0)
+    assert_same_state(f, o)
+    assert ev == o.log_evidence()
+    f.close()
+
+
+@pytest.mark.parametrize("transport", [0, 1])
+def test_multi_handle_shard_failure_returns_error(gpu_available, transport):
+    """A shard that fails mid-call must not leave the others waiting for it (in the host
+    exchange or in an RCCL collective): the call returns the failing shard's error, and a
+    handle whose shards diverged refuses later calls instead of hanging."""
+    import wsmc
+    from wsmc import abi, models
+    shards = 3 if transport == abi.TRANSPORT_HOST else 1
+    N = 3000
+    g = wsmc.Context.multi(N, shards, seed=5, devices=[0] * shards, transport=transport)
+    obs = models.ssm2d_data(4)
+    models.ssm2d_statements(g, obs[:2], ess_perc_min=1.0)
+    g.debug_inject_failure(shards - 1, 1)
+    with pytest.raises(wsmc.WSMCError, match="injected"):
+        models.ssm2d_statements(g, obs[2:], ess_perc_min=1.0)
+    if shards > 1:   # the others were released by the abort: states diverged
+        with pytest.raises(wsmc.WSMCError, match="failed in an earlier call"):
+            g.get_state()
+    else:            # one shard: nothing diverged, the handle stays usable
+        g.get_state()
+    g.close()

@@ -1,0 +1,120 @@
+#!/bin/bash
+# One entry point for every GPU-box recipe whose output lands in profiles/ (run through
+# gpurun from the repo root, e.g. gpurun --timeout 900 -- 'bash tools/gpu.sh round r03_v1').
+# Each recipe writes gpurun_out/<tag>/ plus a MANIFEST (recipe, arguments, HEAD of the tree
+# it ran on, UTC time) so every committed profile traces back to one command. Every GPU step
+# runs under its own time limit; the first failing step ends the recipe.
+#
+#   tests <tag> [pytest args]   pytest -m gpu (default: the whole suite)
+#   round <tag>                 pytest -m gpu, smoke(), the default bench line, the statement-path
+#                               line, rocprofv3 kernel stats of the bench command, FETCH_SIZE /
+#                               WRITE_SIZE passes -> pmc_summary.json, pmc_step_bytes.json
+#   bench <tag> [bench args]    bench.py line + rocprofv3 kernel stats of the same command
+#   moves <tag>                 C3 / C5 move-program lines (tools/bench_moves.py) + C3 kernel stats
+#   c5flops <tag>               C5 FP64 work (SQ_INSTS_VALU_*_F64) against its kernel durations
+#   sq <tag> fused|c3|c5        SQ cycle split and instruction mix per kernel
+#   rccl <tag>                  one-rank RCCL bench lines (island, exact)
+#   micro <tag> <name>          run tools/micro/<name> (built here from tools/micro/<name>.hip)
+set -o pipefail
+export TMPDIR=/tmp
+recipe=$1; tag=$2
+[ -n "$recipe" ] && [ -n "$tag" ] || { echo "usage: tools/gpu.sh <recipe> <tag> [args]"; exit 2; }
+shift 2
+O=gpurun_out/$tag
+mkdir -p $O
+{
+  echo "recipe: tools/gpu.sh $recipe $tag $*"
+  echo "head: $(cat .git_head 2>/dev/null || echo unknown)"
+  echo "utc: $(date -u +%Y-%m-%dT%H:%M:%SZ)"
+} > $O/MANIFEST
+
+SQ="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES"
+step() {   # step <seconds> <log> <cmd...>: one GPU step, its own limit, tail on failure
+  local t=$1 lg=$2; shift 2
+  timeout -k 10 "$t" "$@" > "$lg" 2>&1 || { echo "FAILED: $*"; tail -30 "$lg"; exit 1; }
+}
+stats_table() {   # stats_table <kernel_stats.csv> [n]
+  python - "$1" "${2:-12}" <<'PY'
+import csv, sys
+rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda x: -float(x['TotalDurationNs']))
+for x in rows[:int(sys.argv[2])]:
+    print(x['Name'][:56], x['Calls'], round(float(x['AverageNs']) / 1e3, 2), 'us avg', round(float(x['TotalDurationNs']) / 1e6, 3), 'ms total')
+PY
+}
+sq_table() {   # sq_table <summary.json> [name filter]
+  python - "$1" "${2:-}" <<'PY'
+import json, sys
+d = json.load(open(sys.argv[1]))
+for k, r in d.items():
+    if sys.argv[2] and not any(f in k for f in sys.argv[2].split(',')): continue
+    wc = r.get('SQ_WAVE_CYCLES', 0); w = r.get('SQ_WAVES', 0)
+    if not wc or not w: continue
+    print(k[:40], 'waves', int(w), 'cyc/wave', int(wc / w),
+          'active %.2f parked %.2f stalled %.2f valu-active %.2f' % (r['SQ_ACTIVE_INST_ANY'] / wc, r['SQ_WAIT_ANY'] / wc,
+          r['SQ_WAIT_INST_ANY'] / wc, r['SQ_ACTIVE_INST_VALU'] / wc),
+          'valu/wave', int(r['SQ_INSTS_VALU'] / w), 'salu/wave', int(r['SQ_INSTS_SALU'] / w))
+PY
+}
+line() { python -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[2], '%.4g' % d['value'], d['unit'], '%.3f ms/run' % d['ms_per_run'], 'frac %.3f' % d['roofline']['frac'])" "$1" "$2"; }
+
+case $recipe in
+tests)
+  step 1100 $O/pytest_gpu.log python -u -m pytest tests -q -m gpu -x --timeout 600 --timeout-method thread "$@"
+  tail -1 $O/pytest_gpu.log ;;
+round)
+  step 1100 $O/pytest_gpu.log python -u -m pytest tests -q -m gpu -x --timeout 600 --timeout-method thread
+  tail -1 $O/pytest_gpu.log
+  step 300 $O/smoke.log python -c "import __graft_entry__ as g; g.smoke()"
+  echo smoke ok
+  timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+  line $O/bench.json bench
+  timeout -k 10 400 python bench.py --no-cpu-baseline --statements > $O/bench_statements.json 2> $O/bench_statements.err || { tail -20 $O/bench_statements.err; exit 1; }
+  line $O/bench_statements.json statements
+  step 400 $O/stats.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python bench.py --no-cpu-baseline
+  stats_table $O/stats/run_kernel_stats.csv 6
+  A="--steps 2 --warmup 1 --no-cpu-baseline"
+  step 300 $O/fetch.log rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- python bench.py $A
+  step 300 $O/write.log rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python bench.py $A
+  python tools/summarize_pmc.py $O/pmc_summary.json $O/fetch $O/write > /dev/null
+  python tools/pmc_step_bytes.py $O/pmc_summary.json 1000000 100 $O/pmc_step_bytes.json ;;
+bench)
+  timeout -k 10 400 python bench.py "$@" > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+  line $O/bench.json bench
+  step 400 $O/stats.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python bench.py --no-cpu-baseline "$@"
+  stats_table $O/stats/run_kernel_stats.csv 8 ;;
+moves)
+  timeout -k 10 400 python tools/bench_moves.py c3 c3async c5 > $O/moves.jsonl 2> $O/moves.err || { tail $O/moves.err; exit 1; }
+  cut -c1-330 $O/moves.jsonl
+  step 300 $O/c3.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/c3 -o run -- python tools/bench_moves.py c3async
+  stats_table $O/c3/run_kernel_stats.csv 10 ;;
+c5flops)
+  step 600 $O/stats.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python tools/bench_moves.py c5
+  step 900 $O/pmc.log rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 --output-format csv -d $O/pmc -o run -- python tools/bench_moves.py c5
+  python tools/summarize_pmc.py $O/pmc_summary.json $O/pmc > /dev/null
+  python tools/c5_flops.py $O ;;
+sq)
+  case $1 in
+    fused) for n in 1000000 8000000; do
+             step 120 $O/n$n.log rocprofv3 --kernel-trace --pmc $SQ --output-format csv -d $O/n$n -o run -- python bench.py --particles $n --steps 1 --warmup 1 --no-cpu-baseline
+             python tools/summarize_pmc.py $O/n$n.json $O/n$n > /dev/null
+             sq_table $O/n$n.json prop,fill,sums,final
+           done ;;
+    c3|c5) w=$1; [ $w = c3 ] && w=c3async
+           step 300 $O/p.log rocprofv3 --kernel-trace --pmc $SQ --output-format csv -d $O/p -o run -- python tools/bench_moves.py $w
+           python tools/summarize_pmc.py $O/p.json $O/p > /dev/null
+           sq_table $O/p.json ;;
+    *) echo "sq: fused|c3|c5"; exit 2 ;;
+  esac ;;
+rccl)
+  export NCCL_SOCKET_IFNAME=lo
+  for m in island exact; do
+    timeout -k 10 300 python bench.py --no-cpu-baseline --rccl-one-rank --shard-mode $m "$@" > $O/$m.json 2> $O/$m.err || { tail -30 $O/$m.err; exit 1; }
+    line $O/$m.json rccl-one-rank-$m
+  done ;;
+micro)   # the binary is built here (hipcc ... -o tools/micro/<name> tools/micro/<name>.hip): the
+         # micro sources do not travel (.gpurunignore)
+  name=$1
+  step 300 $O/$name.txt tools/micro/$name
+  cat $O/$name.txt ;;
+*) echo "unknown recipe $recipe"; exit 2 ;;
+esac

@@ -193,12 +193,27 @@ static void gc_log(wsmc_ctx* c) {
     int64_t keep = c->epoch;
     for (const auto& col : c->cols) keep = std::min(keep, col.epoch);
     if (c->anc_last_epoch >= 0) keep = std::min(keep, c->anc_last_epoch);
-    for (int64_t e : c->dec_epochs) keep = std::min(keep, e);
+    for (const auto& p : c->dec_rows)
+        if (p.epoch >= 0) keep = std::min(keep, p.epoch);
     while (c->log_base < keep && !c->alog.empty()) {
         c->row_pool.push_back(c->alog.front());
         c->alog.pop_front();
         c->log_base += 1;
     }
+}
+// the newest ancestors known to have resampled (wsmc_last_ancestors, the oracle's last_anc):
+// a lazy log entry (epoch >= 0), an eager store's row (epoch -1, owned as anc_keep until the
+// next resampling Resample), or row == nullptr: c->anc, which only the fused run and exact
+// shards write, and only when they resample
+static void set_anc_last(wsmc_ctx* c, const AncRow* row, int64_t epoch) {
+    if (c->anc_keep.anc && (!row || row->anc != c->anc_keep.anc)) {
+        c->row_pool.push_back(c->anc_keep);
+        c->anc_keep = AncRow{};
+    }
+    if (row && epoch < 0) c->anc_keep = *row;
+    c->anc_last = row ? row->anc : nullptr;
+    c->anc_last_epoch = row ? epoch : -1;
+    gc_log(c);
 }
 // Bring every stale column to the current epoch: one walk over the log per particle, from
 // the newest entry back to the oldest a stale column needs (kTraceLev entries per launch,
@@ -430,6 +445,9 @@ int wsmc_destroy(wsmc_ctx* c) {
     }
     for (auto& r : c->alog) (void)hipFree(r.anc);
     for (auto& r : c->row_pool) (void)hipFree(r.anc);
+    for (auto& p : c->dec_rows)
+        if (p.epoch < 0) (void)hipFree(p.row.anc);   // eager rows (lazy ones are in alog)
+    if (c->anc_keep.anc) (void)hipFree(c->anc_keep.anc);
     void* bufs[] = {c->dec_always, c->xchg, c->scache, c->scache_back, c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->cdf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount, c->wslots[0], c->wslots[1],
                     c->d_colptr, c->run_params, c->d_tape, c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp,
                     c->vscratch, c->xscratch, c->xp, c->comb, c->anc_out, c->xbuf, c->d_comp, c->d_ctape, c->d_prog, c->rs_grp[0], c->rs_grp[1]};
@@ -457,20 +475,20 @@ static int resolve_decisions(wsmc_ctx* c) {
         c->last_ess = d.ess;
         c->resampled = d.resampled;
         if (d.resampled) c->n_resamples += 1;
-        if (i < (int)c->dec_epochs.size()) {   // the lazy log entry of this Resample
-            const int64_t e = c->dec_epochs[i];
-            if (e >= c->log_base && e - c->log_base < (int64_t)c->alog.size()) {
-                AncRow& r = c->alog[(size_t)(e - c->log_base)];
+        if (i < (int)c->dec_rows.size()) {
+            const wsmc_ctx::PendingRow& p = c->dec_rows[i];
+            if (p.epoch < 0) {   // an eager store's row: kept only if this Resample resampled
+                if (d.resampled) set_anc_last(c, &p.row, -1);
+                else c->row_pool.push_back(p.row);
+            } else if (p.epoch >= c->log_base && p.epoch - c->log_base < (int64_t)c->alog.size()) {
+                AncRow& r = c->alog[(size_t)(p.epoch - c->log_base)];   // the lazy log entry
                 r.known = d.resampled;
-                if (d.resampled) {
-                    c->anc_last = r.anc;
-                    c->anc_last_epoch = e;
-                }
+                if (d.resampled) set_anc_last(c, &r, p.epoch);
             }
         }
     }
     c->dec_pending = 0;
-    c->dec_epochs.clear();
+    c->dec_rows.clear();
     gc_log(c);
     return WSMC_OK;
 }
@@ -580,6 +598,8 @@ int wsmc_comm_set_shard_mode(wsmc_ctx* c, int32_t mode) {
     if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { return wsmc_comm_set_shard_mode(x, mode); });
     CHECK_CTX(c);
     if (mode != WSMC_SHARD_ISLAND && mode != WSMC_SHARD_EXACT) return fail(WSMC_EARG, "unknown shard mode");
+    // pending asynchronous decisions are read back under the store mode they were issued in
+    if (int r = resolve_decisions(c)) return r;
     // exact shards move every column between ranks at each Resample: the store stays eager
     if (mode == WSMC_SHARD_EXACT) {
         if (int r = materialize_all(c)) return r;
@@ -684,18 +704,18 @@ int wsmc_store_resample(wsmc_ctx* c, const int32_t* idx) {
     if (!idx) return fail(WSMC_EARG, "null indices");
     for (int64_t i = 0; i < c->N; ++i)
         if (idx[i] < 0 || idx[i] >= c->N) return fail(WSMC_EARG, "index out of range");
-    // logged like a Resample that resampled (its decision: always)
+    // pending asynchronous Resamples come first (their rows would otherwise overtake this one)
+    int r = resolve_decisions(c);
+    if (r) return r;
+    // logged like a Resample that resampled (its decision: always); an eager store keeps the
+    // row as the last ancestors
     AncRow row;
-    row.anc = c->anc;
-    int r;
-    if (c->lazy && (r = acquire_row(c, &row))) return r;
+    if ((r = acquire_row(c, &row))) return r;
     WSMC_HIP(hipMemcpyAsync(row.anc, idx, sizeof(int32_t) * c->N, hipMemcpyHostToDevice, c->stream));
-    if (c->lazy)
-        WSMC_HIP(hipMemcpyAsync(row.dec, c->dec_always, sizeof(Decision), hipMemcpyDeviceToDevice, c->stream));
+    WSMC_HIP(hipMemcpyAsync(row.dec, c->dec_always, sizeof(Decision), hipMemcpyDeviceToDevice, c->stream));
     row.known = 1;
     if ((r = store_resample_row(c, row, nullptr, nullptr))) return r;
-    c->anc_last = row.anc;
-    c->anc_last_epoch = c->lazy ? c->epoch - 1 : -1;
+    set_anc_last(c, &row, c->lazy ? c->epoch - 1 : -1);
     WSMC_HIP(hipStreamSynchronize(c->stream));
     return WSMC_OK;
 }
@@ -833,6 +853,8 @@ static int exchange_words(wsmc_ctx* c, unsigned long long* buf, int64_t words, h
 }
 
 static int exchange_recs(wsmc_ctx* c, ShardRecord* recs) {
+    if (c->inject_fail > 0 && --c->inject_fail == 0)
+        return fail(WSMC_EHIP, "injected shard failure (wsmc_debug_inject_failure)");
     if (!is_sharded(c)) return WSMC_OK;
     const int words = (int)(sizeof(ShardRecord) / sizeof(unsigned long long));
     if (c->host_exchange) {
@@ -1888,18 +1910,20 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
         if (r) return r;
         c->last_ess = d.ess;
         c->resampled = d.resampled;
-        if (d.resampled) c->n_resamples += 1;
+        if (d.resampled) {
+            c->n_resamples += 1;
+            set_anc_last(c, nullptr, -1);   // the exact route wrote c->anc
+        }
         c->weights_changed = 0;
         if (resampled_out) *resampled_out = c->resampled;
         if (ess_out) *ess_out = d.ess;
         return WSMC_OK;
     }
-    // the ancestors and the decision land in a log row (lazy genealogy) or in c->anc / c->dec
+    // the ancestors and the decision land in a row of their own: a log entry (lazy genealogy),
+    // or (eager store) a row kept as the last ancestors only if this Resample resamples
     AncRow row;
-    row.anc = c->anc;
-    row.dec = c->dec;
     int r;
-    if (c->lazy && (r = acquire_row(c, &row))) return r;
+    if ((r = acquire_row(c, &row))) return r;
     FillPlan plan = fill_plan(c, scheme, op, nullptr);
     // stratified / systematic: the fill's tile blocks also reset the weights to the log-mean
     const bool fill_resets = scheme != WSMC_RESAMPLE_MULTINOMIAL;
@@ -1959,7 +1983,7 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
     }
     if (async) {
         c->dec_pending += 1;
-        if (c->lazy) c->dec_epochs.push_back(c->epoch);   // the log entry this Resample becomes
+        c->dec_rows.push_back({c->lazy ? c->epoch : -1, row});   // the log entry this Resample becomes
         c->wseq += 1;
         if ((r = store_resample_row(c, row, row.dec, fill_resets ? nullptr : c->w))) return r;   // gated
         c->weights_changed = 0;
@@ -1976,15 +2000,11 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
         c->wseq += 1;
         row.known = 1;
         if ((r = store_resample_row(c, row, row.dec, fill_resets ? nullptr : c->w))) return r;
-        if (c->lazy) {
-            c->anc_last = row.anc;
-            c->anc_last_epoch = c->epoch - 1;
-            gc_log(c);
-        }
+        set_anc_last(c, &row, c->lazy ? c->epoch - 1 : -1);
         c->resampled = 1;
         c->n_resamples += 1;
     } else {
-        if (c->lazy) c->row_pool.push_back(row);   // nothing to log: no particle moved
+        c->row_pool.push_back(row);   // nothing to log: no particle moved
         c->resampled = 0;
     }
     c->weights_changed = 0;
@@ -2847,8 +2867,7 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         if (hdec[t].resampled) {
             WSMC_HIP(hipMemcpyAsync(c->anc, c->anc_log + (size_t)(t - 1) * anc_stride(c->N), sizeof(int32_t) * c->N,
                                     hipMemcpyDeviceToDevice, c->stream));
-            c->anc_last = nullptr;
-            c->anc_last_epoch = -1;
+            set_anc_last(c, nullptr, -1);
             break;
         }
     // the run wrote its columns in full (traced back): current
@@ -2926,6 +2945,14 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         c->last_timing = tm;
     }
     if (log_evidence_out) return wsmc_log_evidence(c, log_evidence_out);
+    return WSMC_OK;
+}
+
+int wsmc_debug_inject_failure(wsmc_ctx* c, int32_t shard, int32_t nth) {
+    if (c && c->multi) return multi_inject_failure(c, shard, nth);
+    if (!c) return fail(WSMC_EARG, "null context");
+    if (shard != 0 || nth < 0) return fail(WSMC_EARG, "bad shard or count");
+    c->inject_fail = nth;
     return WSMC_OK;
 }
 

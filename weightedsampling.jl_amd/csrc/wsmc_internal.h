@@ -158,6 +158,7 @@ struct wsmc_ctx {
     int64_t goff = 0, gN = 0;
     ncclComm_t comm = nullptr;
     wsmc_exchange_fn host_exchange = nullptr;   // host-side record exchange (instead of RCCL)
+    int32_t inject_fail = 0;                    // wsmc_debug_inject_failure: fail the nth next record exchange
     unsigned long long* run_grp = nullptr;      // [T+1][ngroups][kGroupLine] fused-run group sums
     // Move score cache: each particle's fold over the first scache_terms tape terms (its
     // score after its last move); -1 = invalid (a column the tape reads was rewritten)
@@ -227,9 +228,16 @@ struct wsmc_ctx {
     int64_t epoch = 0, log_base = 0;
     std::deque<wsmc::AncRow> alog;
     std::vector<wsmc::AncRow> row_pool;     // free rows (ancestors + decision)
-    std::vector<int64_t> dec_epochs;        // log entry of each pending asynchronous decision
+    // each pending asynchronous decision's ancestors: a lazy log entry (epoch >= 0) or an eager
+    // store's own row (epoch -1), held until the decision is read back
+    struct PendingRow {
+        int64_t epoch;
+        wsmc::AncRow row;
+    };
+    std::vector<PendingRow> dec_rows;
     int32_t* anc_last = nullptr;            // wsmc_last_ancestors: newest row known to have resampled
-    int64_t anc_last_epoch = -1;
+    int64_t anc_last_epoch = -1;            // its log entry (lazy), -1 otherwise
+    wsmc::AncRow anc_keep{};                // eager store: the row anc_last points at (owned)
     wsmc::Decision* dec_always = nullptr;   // [1] resampled = 1 (explicit resample!(store, idx))
     bool move_pending = false;              // an asynchronous Move's PD flag not yet read back
 
@@ -532,6 +540,7 @@ int multi_col_upload(wsmc_ctx* c, int32_t col, const double* host);
 int multi_weights(wsmc_ctx* c, const double* up, double* down);
 int multi_score(wsmc_ctx* c, int32_t depth, double* host);
 int multi_last_ancestors(wsmc_ctx* c, int32_t* host);
+int multi_inject_failure(wsmc_ctx* c, int32_t shard, int32_t nth);
 int multi_gather_rows(wsmc_ctx* c, int32_t col, const int64_t* idx, int64_t n, double* out);
 int multi_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, double step, const double* lo,
                const double* hi, int32_t target_depth, double diversity, int64_t* accepted_out);

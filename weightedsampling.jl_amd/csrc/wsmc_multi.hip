@@ -54,6 +54,14 @@ struct MultiState {
     uint64_t gen_in = 0, gen_out = 0;
     std::vector<uint64_t> xbuf;
     std::vector<XArg> xargs;
+    // a shard that fails during a fan-out sets `abort`: shards waiting in the host exchange
+    // leave it with an error, and with RCCL every other shard's communicator is aborted (a
+    // collective missing its peer would never complete). Shards that then left the call with
+    // different results may hold different states: the handle is marked failed.
+    bool rccl = false;
+    bool abort = false;         // guarded by xm
+    bool rccl_aborted = false;  // guarded by xm
+    bool failed = false;        // set between fan-outs only
 };
 
 static void worker_loop(Worker* w) {
@@ -75,8 +83,28 @@ static void worker_loop(Worker* w) {
     }
 }
 
+// shard g failed: release the shards waiting for it (host exchange) or abort their
+// communicators (RCCL), once per fan-out
+static void abort_others(MultiState* M, int g) {
+    std::lock_guard<std::mutex> lk(M->xm);
+    if (M->abort) return;
+    M->abort = true;
+    M->xcv.notify_all();
+    if (M->rccl && M->G > 1) {   // one shard: no peer can be waiting for it
+        for (int h = 0; h < M->G; ++h)
+            if (h != g && M->sub[h]->comm) (void)ncclCommAbort(M->sub[h]->comm);
+        M->rccl_aborted = true;
+    }
+}
+
 // fn(g, shard) on every shard concurrently; the first failing shard's code and message
 static int run_all(MultiState* M, const std::function<int(int, wsmc_ctx*)>& fn) {
+    if (M->failed) return fail(WSMC_ESTATE, "multi-device handle failed in an earlier call (its shards diverged)");
+    {
+        std::lock_guard<std::mutex> lk(M->xm);
+        M->abort = false;
+        M->arrived = M->departed = 0;
+    }
     std::vector<int> rc(M->G, 0);
     std::vector<std::string> msg(M->G);
     for (int g = 1; g < M->G; ++g) {
@@ -84,21 +112,37 @@ static int run_all(MultiState* M, const std::function<int(int, wsmc_ctx*)>& fn) 
         std::lock_guard<std::mutex> lk(w->m);
         w->job = [&, g] {
             rc[g] = fn(g, M->sub[g]);
-            if (rc[g]) msg[g] = wsmc_last_error();
+            if (rc[g]) {
+                msg[g] = wsmc_last_error();
+                abort_others(M, g);
+            }
         };
         w->has = true;
         w->done = false;
         w->cv.notify_all();
     }
     rc[0] = fn(0, M->sub[0]);
-    if (rc[0]) msg[0] = wsmc_last_error();
+    if (rc[0]) {
+        msg[0] = wsmc_last_error();
+        abort_others(M, 0);
+    }
     for (int g = 1; g < M->G; ++g) {
         Worker* w = M->workers[g].get();
         std::unique_lock<std::mutex> lk(w->m);
         w->cv.wait(lk, [&] { return w->done; });
     }
-    for (int g = 0; g < M->G; ++g)
-        if (rc[g]) return fail(rc[g], "shard " + std::to_string(g) + ": " + msg[g]);
+    if (M->rccl_aborted) {   // aborted communicators are released: the shards must not destroy them
+        for (int h = 0; h < M->G; ++h) M->sub[h]->comm = nullptr;
+        M->failed = true;
+    }
+    bool same = true;
+    for (int g = 1; g < M->G; ++g) same &= rc[g] == rc[0];
+    if (!same) M->failed = true;
+    // report the first shard that failed by itself, not one released by the abort
+    for (int pass = 0; pass < 2; ++pass)
+        for (int g = 0; g < M->G; ++g)
+            if (rc[g] && (pass == 1 || rc[g] != WSMC_ERCCL))
+                return fail(rc[g], "shard " + std::to_string(g) + ": " + msg[g]);
     return WSMC_OK;
 }
 
@@ -111,12 +155,14 @@ static int multi_exchange(void* user, const uint64_t* mine, int32_t words, uint6
     if (M->xbuf.size() < (size_t)M->G * (size_t)words) M->xbuf.resize((size_t)M->G * (size_t)words);
     std::memcpy(M->xbuf.data() + (size_t)a->rank * words, mine, sizeof(uint64_t) * (size_t)words);
     const uint64_t g_in = M->gen_in;
+    if (M->abort) return -1;
     if (++M->arrived == M->G) {
         M->arrived = 0;
         M->gen_in += 1;
         M->xcv.notify_all();
     } else {
-        M->xcv.wait(lk, [&] { return M->gen_in != g_in; });
+        M->xcv.wait(lk, [&] { return M->gen_in != g_in || M->abort; });
+        if (M->gen_in == g_in) return -1;   // a shard failed before arriving
     }
     std::memcpy(all, M->xbuf.data(), sizeof(uint64_t) * (size_t)M->G * (size_t)words);
     const uint64_t g_out = M->gen_out;
@@ -125,7 +171,8 @@ static int multi_exchange(void* user, const uint64_t* mine, int32_t words, uint6
         M->gen_out += 1;
         M->xcv.notify_all();
     } else {
-        M->xcv.wait(lk, [&] { return M->gen_out != g_out; });
+        M->xcv.wait(lk, [&] { return M->gen_out != g_out || M->abort; });
+        if (M->gen_out == g_out) return -1;
     }
     return 0;
 }
@@ -238,8 +285,11 @@ int multi_last_ancestors(wsmc_ctx* c, int32_t* host) {
         return wsmc_last_ancestors(s, buf[g].data());
     });
     if (!r)
-        for (int g = 0; g < M->G; ++g)
-            std::memcpy(host + M->off[g], buf[g].data(), sizeof(int32_t) * nloc(M, g));
+        for (int g = 0; g < M->G; ++g) {
+            // population indices: exact shards hold global ids already, island shards their own
+            const int32_t base = M->sub[g]->shard_mode == WSMC_SHARD_EXACT ? 0 : (int32_t)M->off[g];
+            for (int64_t i = 0; i < nloc(M, g); ++i) host[M->off[g] + i] = buf[g][(size_t)i] + base;
+        }
     return r;
 }
 int multi_gather_rows(wsmc_ctx* c, int32_t col, const int64_t* idx, int64_t n, double* out) {
@@ -283,6 +333,13 @@ int multi_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d,
     return r;
 }
 
+int multi_inject_failure(wsmc_ctx* c, int32_t shard, int32_t nth) {
+    MultiState* M = c->multi;
+    if (shard < 0 || shard >= M->G || nth < 0) return fail(WSMC_EARG, "bad shard or count");
+    M->sub[shard]->inject_fail = nth;
+    return WSMC_OK;
+}
+
 }  // namespace wsmc
 
 extern "C" int wsmc_create_multi(wsmc_ctx** out, int64_t n_particles, int32_t n_gpus, const int32_t* devices,
@@ -316,6 +373,7 @@ extern "C" int wsmc_create_multi(wsmc_ctx** out, int64_t n_particles, int32_t n_
         int r = wsmc_create(&M->sub[g], M->off[g + 1] - M->off[g], devs[g], seed);
         if (r) return cleanup(r);
     }
+    M->rccl = transport == WSMC_TRANSPORT_RCCL;
     if (transport == WSMC_TRANSPORT_RCCL) {
         std::vector<ncclComm_t> comms(G);
         const ncclResult_t nr = ncclCommInitAll(comms.data(), G, devs.data());

@@ -343,6 +343,10 @@ class Context:
         check(self._L.wsmc_debug_kernel_bench(self._h, int(kernel), int(mode), int(iters), C.byref(v)))
         return float(v.value)
 
+    def debug_inject_failure(self, shard: int, nth: int) -> None:
+        """Test hook: shard `shard` fails its nth next record exchange (include/wsmc.h)."""
+        check(self._L.wsmc_debug_inject_failure(self._h, int(shard), int(nth)))
+
     def timing(self) -> dict:
         t = RunTiming()
         check(self._L.wsmc_run_get_timing(self._h, C.byref(t)))
