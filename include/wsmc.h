@@ -309,6 +309,11 @@ int wsmc_debug_kernel_bench(wsmc_ctx* ctx, int32_t kernel, int32_t mode, int32_t
  * instead of waiting for it; shards that left in different states mark the handle failed
  * (every later call returns WSMC_ESTATE). nth = 0 disarms.                               */
 int wsmc_debug_inject_failure(wsmc_ctx* ctx, int32_t shard, int32_t nth);
+/* Exact-sharded fused run: the fixed neighbour block (slots per step) and
+ * trace window (ids per level) sizes — > 0 sets, 0 restores the defaults, < 0 leaves as is —
+ * and, in stats_out[4] (may be NULL), the last run's largest block needed, its largest
+ * lineage excursion, the runs re-done on the eager path after an overflow, the block size. */
+int wsmc_debug_exact(wsmc_ctx* ctx, int64_t cap, int64_t ctr, int64_t* stats_out);
 
 #ifdef __cplusplus
 }

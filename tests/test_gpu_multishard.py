@@ -637,3 +637,39 @@ def test_multi_handle_shard_failure_returns_error(gpu_available, transport):
     else:            # one shard: nothing diverged, the handle stays usable
         g.get_state()
     g.close()
+
+
+@pytest.mark.parametrize("sizes", [(2600, 2600), (1700, 2101, 1500)])
+@pytest.mark.parametrize("small", [False, True])
+def test_exact_fused_run_without_host_round_trips(gpu_available, sizes, small):
+    """The exact-sharded fused run as it now runs: no host read inside the
+    run, particles moved between neighbours through fixed-size blocks and the lineages traced
+    through fixed trace windows. With the default sizes nothing overflows; with blocks and
+    windows of a few slots every run overflows and is re-done on the eager path. Both must
+    equal one context holding the whole population, bit for bit, on ragged shards too."""
+    sys.path.insert(0, str(REPO / "oracle"))
+    from oracle import Oracle
+    import wsmc
+    from wsmc import abi, models
+    from test_gpu_parity import assert_same_state
+    N, T = sum(sizes), 14
+    obs = models.ssm2d_data(T)
+    for ess, keep in ((1.0, True), (0.5, True), (1.0, False)):
+        o = Oracle(N, seed=21)
+        models.ssm2d_statements(o, obs, ess_perc_min=ess)
+        f = wsmc.Context.multi(N, len(sizes), seed=21, devices=[0] * len(sizes), transport=abi.TRANSPORT_HOST)
+        f.comm_set_shard_mode(abi.SHARD_EXACT)
+        if small:
+            f.debug_exact(cap=3, ctr=2)
+        ev = f.ssm2d_run(obs, ess_perc_min=ess, keep_history=keep)
+        st = f.debug_exact()
+        assert (st["eager_reruns"] >= 1) == small, st
+        assert ev == o.log_evidence()
+        np.testing.assert_array_equal(f.weights_download(), o.weights_download())
+        np.testing.assert_array_equal(f.last_ancestors(), o.last_ancestors())
+        names = ["v", "dv"] + ([f"x_{t}" for t in range(1, T + 2)] if keep else [])
+        for nm in names:
+            np.testing.assert_array_equal(f.col_download(f.col_find(nm)), o.col_download(o.col_find(nm)), err_msg=nm)
+        if not keep:
+            np.testing.assert_array_equal(f.col_download(f.col_find("x")), o.col_download(o.col_find(f"x_{T + 1}")))
+        f.close()

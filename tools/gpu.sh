@@ -58,8 +58,9 @@ PY
 line() { python -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[2], '%.4g' % d['value'], d['unit'], '%.3f ms/run' % d['ms_per_run'], 'frac %.3f' % d['roofline']['frac'])" "$1" "$2"; }
 
 case $recipe in
-tests)
-  step 1100 $O/pytest_gpu.log python -u -m pytest tests -q -m gpu -x --timeout 600 --timeout-method thread "$@"
+tests)   # [pytest args]: files / -k; the whole suite by default
+  [ $# -gt 0 ] || set -- tests
+  step 1100 $O/pytest_gpu.log python -u -m pytest -q -m gpu -x --timeout 600 --timeout-method thread "$@"
   tail -1 $O/pytest_gpu.log ;;
 round)
   step 1100 $O/pytest_gpu.log python -u -m pytest tests -q -m gpu -x --timeout 600 --timeout-method thread

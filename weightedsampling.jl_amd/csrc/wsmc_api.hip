@@ -450,7 +450,8 @@ int wsmc_destroy(wsmc_ctx* c) {
     if (c->anc_keep.anc) (void)hipFree(c->anc_keep.anc);
     void* bufs[] = {c->dec_always, c->xchg, c->scache, c->scache_back, c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->cdf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount, c->wslots[0], c->wslots[1],
                     c->d_colptr, c->run_params, c->d_tape, c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp,
-                    c->vscratch, c->xscratch, c->xp, c->comb, c->anc_out, c->xbuf, c->d_comp, c->d_ctape, c->d_prog, c->rs_grp[0], c->rs_grp[1]};
+                    c->vscratch, c->xscratch, c->xp, c->comb, c->anc_out, c->xbuf, c->d_comp, c->d_ctape, c->d_prog, c->rs_grp[0], c->rs_grp[1],
+                    c->xpairs, c->xnb, c->xwin, c->xstat, c->w_save};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (double* p : c->xrun)
@@ -2574,6 +2575,234 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
     return WSMC_OK;
 }
 
+// ---- exact shards without host round trips -------------------------------------------------
+// Fixed-size blocks to the neighbours: send[0] to rank - 1, send[1] to rank + 1; recv[0] from
+// rank - 1, recv[1] from rank + 1. RCCL: one group of send / recv on the stream (sizes fixed, so
+// it is captured with the run); host exchange (tests): every rank all-gathers its two blocks.
+static int exchange_neighbors(wsmc_ctx* c, unsigned long long* const send[2], unsigned long long* const recv[2],
+                              int64_t words, hipStream_t s) {
+    const int W = c->world, me = c->rank;
+    if (W < 2 || words <= 0) return WSMC_OK;
+    if (c->host_exchange) {
+        if (2 * words > 0x7fffffffll) return fail(WSMC_EARG, "host exchange block too large");
+        std::vector<unsigned long long> mine(2 * (size_t)words), all(2 * (size_t)words * W);
+        WSMC_HIP(hipMemcpyAsync(mine.data(), send[0], sizeof(unsigned long long) * words, hipMemcpyDeviceToHost, s));
+        WSMC_HIP(hipMemcpyAsync(mine.data() + words, send[1], sizeof(unsigned long long) * words,
+                                hipMemcpyDeviceToHost, s));
+        WSMC_HIP(hipStreamSynchronize(s));
+        if (c->host_exchange(c->host_user, reinterpret_cast<const uint64_t*>(mine.data()), (int32_t)(2 * words),
+                             reinterpret_cast<uint64_t*>(all.data())) != 0)
+            return fail(WSMC_ERCCL, "host neighbour exchange failed");
+        if (me > 0)   // the left rank's right block
+            WSMC_HIP(hipMemcpyAsync(recv[0], all.data() + (size_t)(me - 1) * 2 * words + words,
+                                    sizeof(unsigned long long) * words, hipMemcpyHostToDevice, s));
+        if (me + 1 < W)   // the right rank's left block
+            WSMC_HIP(hipMemcpyAsync(recv[1], all.data() + (size_t)(me + 1) * 2 * words,
+                                    sizeof(unsigned long long) * words, hipMemcpyHostToDevice, s));
+        WSMC_HIP(hipStreamSynchronize(s));
+        return WSMC_OK;
+    }
+    WSMC_RCCL(ncclGroupStart());
+    if (me > 0) {
+        WSMC_RCCL(ncclSend(send[0], (size_t)words, ncclUint64, me - 1, c->comm, s));
+        WSMC_RCCL(ncclRecv(recv[0], (size_t)words, ncclUint64, me - 1, c->comm, s));
+    }
+    if (me + 1 < W) {
+        WSMC_RCCL(ncclSend(send[1], (size_t)words, ncclUint64, me + 1, c->comm, s));
+        WSMC_RCCL(ncclRecv(recv[1], (size_t)words, ncclUint64, me + 1, c->comm, s));
+    }
+    WSMC_RCCL(ncclGroupEnd());
+    return WSMC_OK;
+}
+
+// the block (slots per neighbour per step) and window (ids per neighbour per level) sizes:
+// every rank derives the same values (from the global size, and the overflow statistics all
+// ranks see), so their fixed-size collectives match
+static void exact_sizes(const wsmc_ctx* c, int64_t* cap, int64_t* ctr) {
+    const int64_t nmin = c->gN / c->world;   // the smallest (ragged) shard
+    int64_t cp = c->x_cap ? c->x_cap : std::max<int64_t>(1024, nmin / 256);
+    int64_t ct = c->x_ctr ? c->x_ctr : std::max<int64_t>(1024, nmin / 128);
+    *cap = std::max<int64_t>(1, std::min(cp, nmin));
+    *ctr = std::max<int64_t>(1, std::min(ct, nmin));
+}
+static bool exact_eager_forced() {   // diagnostics / A-B: the host-driven exact run only
+    static const bool v = [] {
+        const char* e = getenv("WSMC_EXACT_EAGER");
+        return e && atoi(e) != 0;
+    }();
+    return v;
+}
+static int ensure_exact_async(wsmc_ctx* c, int32_t T, int64_t cap, int64_t ctr) {
+    int r = ensure_exact(c);
+    if (r) return r;
+    const int64_t N = c->N;
+    const int64_t wwords = (int64_t)T * ctr * 3;
+    const bool grow = !c->xpairs || cap > c->xnb_cap || wwords > c->xwin_words;
+    if (!grow && c->xstat && c->w_save) return WSMC_OK;
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    if (!c->xpairs) WSMC_HIP(hipMalloc(&c->xpairs, sizeof(double) * 6 * (size_t)N));
+    if (!c->xstat) WSMC_HIP(hipMalloc(&c->xstat, sizeof(unsigned long long) * kMaxShards * kXStat));
+    if (!c->w_save) WSMC_HIP(hipMalloc(&c->w_save, sizeof(double) * (size_t)N));
+    if (cap > c->xnb_cap) {
+        if (c->xnb) WSMC_HIP(hipFree(c->xnb));
+        WSMC_HIP(hipMalloc(&c->xnb, sizeof(unsigned long long) * 4 * (size_t)cap * kXWords));
+        c->xnb_cap = cap;
+    }
+    if (wwords > c->xwin_words) {
+        if (c->xwin) WSMC_HIP(hipFree(c->xwin));
+        WSMC_HIP(hipMalloc(&c->xwin, sizeof(unsigned long long) * 4 * (size_t)wwords));
+        c->xwin_words = wwords;
+    }
+    return WSMC_OK;
+}
+
+// The fused 2D SSM run on exact shards with no host round trip: per step the
+// propagate (ancestors as global ids: a neighbour's particle is read from the pairs it sent),
+// the global max and the records all-gathered, the single-GPU decision and window fill
+// (k_rs_decide_exact, the fill), then k_exact_route / the neighbour exchange / k_exact_recv
+// move the window's slots to their owners through fixed-size blocks; at the end the trace
+// windows are exchanged once and k_exact_final traces every lineage back, and every rank's
+// overflow statistics are all-gathered. A slot or lineage the blocks cannot carry sets an
+// overflow bit: the host then re-runs the filter on the eager path.
+static int enqueue_ssm2d_exact(wsmc_ctx* c, const RunPlan& p, int64_t cap, int64_t ctr) {
+    const int T = p.T;
+    const int64_t N = c->N;
+    const int W = c->world, me = c->rank;
+    const double cpre = 2.0 * WSMC_LOG2PI + 2.0 * wsmc_log(p.r_var);
+    WSMC_HIP(hipMemsetAsync(c->run_max, 0, sizeof(MaxSlots) * (T + 1), c->stream));
+    WSMC_HIP(hipMemsetAsync(c->run_dec, 0, sizeof(Decision) * (T + 1), c->stream));
+    WSMC_HIP(hipMemsetAsync(c->xstat, 0, sizeof(unsigned long long) * kMaxShards * kXStat, c->stream));
+    WSMC_HIP(hipMemcpyAsync(c->w_save, c->w, sizeof(double) * N, hipMemcpyDeviceToDevice, c->stream));
+    double* Xr = c->xpairs;
+    double* Vr = Xr + 2 * N;
+    double* DVr = Vr + 2 * N;
+    const int64_t bw = cap * kXWords;
+    unsigned long long* const snd[2] = {c->xnb, c->xnb + bw};
+    unsigned long long* const rcv[2] = {c->xnb + 2 * bw, c->xnb + 3 * bw};
+    double* vbuf[2] = {c->cols[p.colv].back, c->vscratch};
+    double* xbuf[2] = {p.keep ? nullptr : c->cols[p.colx].back, c->xscratch};
+    double* dvw = c->cols[p.coldv].back;
+    unsigned long long* stat = c->xstat + (size_t)me * kXStat;
+    int r;
+    for (int t = 1; t <= T; ++t) {
+        Ssm2dArgs a;
+        a.t = t;
+        a.keep_history = p.keep;
+        a.N = N;
+        a.goff = c->goff;
+        a.seed = c->seed;
+        a.op_dev = c->run_params;
+        a.obs = c->obs;
+        a.x0[0] = p.x0[0]; a.x0[1] = p.x0[1];
+        a.v0[0] = p.v0[0]; a.v0[1] = p.v0[1];
+        a.q_sd = wsmc_sqrt(p.q_var);
+        a.r_var = p.r_var;
+        a.c0 = cpre;
+        if (p.keep) {
+            a.x_prev = t > 1 ? c->cols[p.xcols[t]].back : nullptr;
+            a.x_next = c->cols[p.xcols[t + 1]].back;
+        } else {
+            a.x_prev = t > 1 ? xbuf[t & 1] : nullptr;
+            a.x_next = xbuf[(t + 1) & 1];
+        }
+        a.v_prev = t > 1 ? vbuf[t & 1] : nullptr;
+        a.v_next = vbuf[(t + 1) & 1];
+        a.dv = t == T ? dvw : nullptr;
+        a.w = c->w;
+        a.anc_prev = t > 1 ? c->anc_log + (size_t)(t - 2) * anc_stride(N) : nullptr;
+        a.dec_prev = t > 1 ? c->run_dec + (t - 1) : nullptr;
+        a.ms = c->run_max + t;
+        a.identity = 0;
+        a.xr = Xr;
+        a.vr = Vr;
+        WSMC_HIP(launch_ssm2d_propagate(c->stream, a));
+        // the global max, this shard's record relative to it (K from the global N), every
+        // rank's record: exactly the single-context statistics
+        WSMC_HIP(launch_max_publish(c->stream, c->run_max + t, c->xchg + me));
+        if ((r = exchange_words(c, c->xchg, 1, c->stream))) return r;
+        WSMC_HIP(launch_max_adopt(c->stream, c->xchg, W, c->mslots));
+        WSMC_HIP(launch_rs_sums(c->stream, c->w, N, c->mslots, c->tilep, c->qbuf, nullptr, nullptr, nullptr, 1, c->gN));
+        WSMC_HIP(launch_rs_reduce(c->stream, c->mslots, c->tilep, N, c->tileOff, c->rec + me, 0, 0.0, nullptr,
+                                  nullptr));
+        if ((r = exchange_recs(c, c->rec))) return r;
+        FillPlan plan = fill_plan(c, p.scheme, 3ull * (uint64_t)(t - 1) + 2ull, c->run_params);
+        plan.slot_base = 0;   // slots are global: their keys too
+        WSMC_HIP(launch_rs_decide_exact(c->stream, c->rec, W, me, p.ess_min, plan, c->comb, c->run_dec + t, c->xp));
+        plan.xp = c->xp;
+        WSMC_HIP(launch_rs_reduce(c->stream, c->mslots, c->tilep, N, c->tileOff, c->rec + me, 0, p.ess_min,
+                                  c->run_dec + t, &plan));
+        WSMC_HIP(launch_rs_scan(c->stream, N, c->comb, c->run_dec + t, plan, c->tileOff, c->qbuf, c->anc_out));
+        ExactStep e;
+        e.xp = c->xp;
+        e.dec = c->run_dec + t;
+        e.anc_out = c->anc_out;
+        e.x = a.x_next;
+        e.v = a.v_next;
+        e.dv = dvw;
+        e.anc_row = c->anc_log + (size_t)(t - 1) * anc_stride(N);
+        e.send[0] = snd[0]; e.send[1] = snd[1];
+        e.recv[0] = rcv[0]; e.recv[1] = rcv[1];
+        e.xr = Xr; e.vr = Vr; e.dvr = DVr;
+        e.stat = stat;
+        e.cap = cap;
+        e.N = N;
+        e.goff = c->goff;
+        e.rank = me;
+        e.world = W;
+        WSMC_HIP(launch_exact_route(c->stream, e));
+        if (W > 1) {
+            if ((r = exchange_neighbors(c, snd, rcv, bw, c->stream))) return r;
+            WSMC_HIP(launch_exact_recv(c->stream, e));
+        }
+    }
+    const int64_t ww = (int64_t)T * ctr * 3;
+    unsigned long long* const wsnd[2] = {c->xwin, c->xwin + ww};
+    unsigned long long* const wrcv[2] = {c->xwin + 2 * ww, c->xwin + 3 * ww};
+    const bool wins = p.keep && W > 1;
+    if (wins) {
+        ExactWin w;
+        w.hist_work = p.d_hist_work;
+        w.anc_log = c->anc_log;
+        w.anc_stride = anc_stride(N);
+        w.dec = c->run_dec;
+        w.out = c->xwin;
+        w.ctr = ctr;
+        w.N = N;
+        w.goff = c->goff;
+        w.T = T;
+        w.has_left = me > 0;
+        w.has_right = me + 1 < W;
+        WSMC_HIP(launch_exact_window_pack(c->stream, w));
+        if ((r = exchange_neighbors(c, wsnd, wrcv, ww, c->stream))) return r;
+    }
+    ExactFinal f;
+    f.T = T;
+    f.keep_history = p.keep;
+    f.N = N;
+    f.goff = c->goff;
+    f.ctr = ctr;
+    f.x0[0] = p.x0[0]; f.x0[1] = p.x0[1];
+    f.hist_work = p.d_hist_work;
+    f.hist_out = p.d_hist_out;
+    f.x_work = p.keep ? nullptr : xbuf[(T + 1) & 1];
+    f.x_out = p.keep ? nullptr : c->cols[p.colx].front;
+    f.v_work = vbuf[(T + 1) & 1];
+    f.v_out = c->cols[p.colv].front;
+    f.dv_work = dvw;
+    f.dv_out = c->cols[p.coldv].front;
+    f.xr = Xr; f.vr = Vr; f.dvr = DVr;
+    f.w = c->w;
+    f.anc_log = c->anc_log;
+    f.anc_stride = anc_stride(N);
+    f.dec = c->run_dec;
+    f.win[0] = wins && me > 0 ? wrcv[0] : nullptr;
+    f.win[1] = wins && me + 1 < W ? wrcv[1] : nullptr;
+    f.stat = stat;
+    WSMC_HIP(launch_exact_final(c->stream, f));
+    // every rank's overflow bits: all ranks take the same branch (re-run or not) afterwards
+    return exchange_words(c, c->xstat, kXStat, c->stream);
+}
+
 // The fused 2D SSM run on exact shards (SURVEY §8(e) item 4, C4 with the single-GPU bits),
 // eager and host-driven. Each step:
 //   propagate from the state already gathered in slot order (identity read);
@@ -2758,7 +2987,19 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
     for (auto& col : c->cols) { mix(col.front); mix(col.back); }
     mix(c->w); mix(c->anc_log); mix(c->run_rec); mix(c->run_max); mix(c->obs);
     mix(c->comm);   // a captured collective bakes its communicator
-    const std::string key = std::string(keybuf) + " ptr=" + std::to_string(h);
+    // exact shards: the run without host round trips unless it is switched off (A/B) or the
+    // scheme needs the eager path; its block / window sizes are part of the graph
+    const bool exact_async = exact_mode(c) && !exact_eager_forced();
+    int64_t xcap = 0, xctr = 0;
+    if (exact_async) {
+        exact_sizes(c, &xcap, &xctr);
+        if ((r = ensure_exact_async(c, T, xcap, xctr))) return r;
+        const void* xb[] = {c->xpairs, c->xnb, c->xwin, c->xstat, c->w_save, c->anc_out, c->taskTile, c->xp, c->comb,
+                            c->rec, c->xchg, c->mslots, c->tilep, c->tileOff, c->qbuf, c->taskOff};
+        for (const void* q : xb) mix(q);
+    }
+    const std::string key = std::string(keybuf) + " ptr=" + std::to_string(h) +
+                            (exact_async ? " exact cap=" + std::to_string(xcap) + " ctr=" + std::to_string(xctr) : "");
     auto build_tables = [&](double*** work, double*** outp) -> int {
         *work = *outp = nullptr;
         if (!p.keep) return WSMC_OK;
@@ -2783,7 +3024,8 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
     }();
     // HIP cannot time events captured in graphs; a host exchange (test mode) synchronises
     // inside the run, and exact shards are host-driven. RCCL collectives are captured.
-    const bool use_graph = !c->timing && !no_graph && !c->no_graph && !exact_mode(c) && !c->host_exchange;
+    const bool use_graph = !c->timing && !no_graph && !c->no_graph && (!exact_mode(c) || exact_async) &&
+                           !c->host_exchange;
     if (exact_mode(c) && c->timing) return fail(WSMC_ESTATE, "run timing is not available on exact shards");
     const int nev = 8 * T + 2;
     std::vector<hipEvent_t> evs;
@@ -2796,7 +3038,10 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         evs.assign(c->events.begin(), c->events.begin() + nev);
     }
     void* temp_tables = nullptr;
-    if (exact_mode(c)) {
+    auto enqueue_run = [&]() {
+        return exact_async ? enqueue_ssm2d_exact(c, p, xcap, xctr) : enqueue_ssm2d(c, p, c->timing ? &evs : nullptr);
+    };
+    if (exact_mode(c) && !exact_async) {
         if ((r = ssm2d_run_exact(c, p, op_base))) return r;
     } else {
         bool graphed = false;
@@ -2810,7 +3055,7 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
                 if ((r = build_tables(&p.d_hist_work, &p.d_hist_out))) return r;
                 ng.owned = p.d_hist_work;
                 WSMC_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-                r = enqueue_ssm2d(c, p, c->timing ? &evs : nullptr);
+                r = enqueue_run();
                 static const bool diag_fail = [] {   // diagnostics: exercise the eager fallback
                     const char* e = getenv("WSMC_DIAG_CAPTURE_FAIL");
                     return e && atoi(e) != 0;
@@ -2851,8 +3096,34 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
             // instrumented runs: a bounded delay kernel keeps the GPU busy while the host
             // queues the whole run, so no host-submission gap lands inside an event pair
             if (c->timing) WSMC_HIP(launch_delay(c->stream, 20000));
-            r = enqueue_ssm2d(c, p, c->timing ? &evs : nullptr);
+            r = enqueue_run();
             if (r) {
+                if (temp_tables) (void)hipFree(temp_tables);
+                return r;
+            }
+        }
+    }
+    if (exact_async) {
+        // every rank's overflow statistics (all-gathered by the run): the same on all ranks, so
+        // all of them re-run on the eager path together, from the weights the run started with
+        std::vector<unsigned long long> st((size_t)kMaxShards * kXStat);
+        WSMC_HIP(hipMemcpyAsync(st.data(), c->xstat, sizeof(unsigned long long) * st.size(), hipMemcpyDeviceToHost,
+                                c->stream));
+        WSMC_HIP(hipStreamSynchronize(c->stream));
+        unsigned long long bits = 0, need = 0, exc = 0;
+        for (int g = 0; g < c->world; ++g) {
+            bits |= st[(size_t)g * kXStat];
+            need = std::max(need, st[(size_t)g * kXStat + 1]);
+            exc = std::max(exc, st[(size_t)g * kXStat + 2]);
+        }
+        c->x_need = need;
+        c->x_exc = exc;
+        c->x_overflows += bits ? 1 : 0;
+        if (bits) {
+            if (bits & 1ull) c->x_cap = std::max<int64_t>(4 * xcap, 2 * (int64_t)need);
+            if (bits & 2ull) c->x_ctr = std::max<int64_t>(4 * xctr, 2 * (int64_t)exc);
+            WSMC_HIP(hipMemcpyAsync(c->w, c->w_save, sizeof(double) * c->N, hipMemcpyDeviceToDevice, c->stream));
+            if ((r = ssm2d_run_exact(c, p, op_base))) {
                 if (temp_tables) (void)hipFree(temp_tables);
                 return r;
             }
@@ -2945,6 +3216,27 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         c->last_timing = tm;
     }
     if (log_evidence_out) return wsmc_log_evidence(c, log_evidence_out);
+    return WSMC_OK;
+}
+
+int wsmc_debug_exact(wsmc_ctx* c, int64_t cap, int64_t ctr, int64_t* stats_out) {
+    if (c && c->multi) {
+        int64_t st[4];
+        int r = multi_each(c, [&](wsmc_ctx* x) { return wsmc_debug_exact(x, cap, ctr, x == multi_first(c) ? st : nullptr); });
+        if (!r && stats_out) std::memcpy(stats_out, st, sizeof(st));
+        return r;
+    }
+    if (!c) return fail(WSMC_EARG, "null context");
+    if (cap >= 0) c->x_cap = cap;
+    if (ctr >= 0) c->x_ctr = ctr;
+    if (stats_out) {
+        int64_t cp = 0, ct = 0;
+        if (c->world > 0 && c->gN > 0) exact_sizes(c, &cp, &ct);
+        stats_out[0] = (int64_t)c->x_need;
+        stats_out[1] = (int64_t)c->x_exc;
+        stats_out[2] = c->x_overflows;
+        stats_out[3] = cp;
+    }
     return WSMC_OK;
 }
 

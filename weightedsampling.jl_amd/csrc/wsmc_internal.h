@@ -205,6 +205,17 @@ struct wsmc_ctx {
     double** d_comp = nullptr;              // [2 * cap] component pointer tables (src, dst)
     double* xrun[9] = {};                    // exact-sharded fused run: gathered / scratch pair buffers
     int32_t* lineage[2] = {};                // [N] global lineage ids (distributed trace-back)
+    // exact-sharded fused run without host round trips (enqueue_ssm2d_exact)
+    double* xpairs = nullptr;               // [6N] x, v, dv pairs received from a neighbour, by slot
+    unsigned long long* xnb = nullptr;      // [4][x_cap][kXWords]: send left, right; receive left, right
+    int64_t xnb_cap = 0;                    // slots per block allocated
+    unsigned long long* xwin = nullptr;     // [4][T][x_ctr][3]: trace windows sent left, right; received
+    int64_t xwin_words = 0;                 // words per block allocated
+    unsigned long long* xstat = nullptr;    // [kMaxShards][kXStat], this rank's at rank * kXStat
+    double* w_save = nullptr;               // [N] the weights at the run's start (re-run after an overflow)
+    int64_t x_cap = 0, x_ctr = 0;           // block / window sizes in use (0: defaults; grown on overflow)
+    unsigned long long x_need = 0, x_exc = 0;   // the last run's largest block / lineage excursion
+    int64_t x_overflows = 0;                // runs re-done on the eager path
     wsmc_term* d_ctape = nullptr;           // compiled Move tape (slot operands)
     int64_t d_ctape_cap = 0;
     void* d_prog = nullptr;                 // compiled fold program: segments, then constants
@@ -407,6 +418,69 @@ hipError_t launch_exact_pack(hipStream_t s, const ExactRoute& rt, const int32_t*
                              unsigned long long* sendbuf);
 hipError_t launch_exact_unpack(hipStream_t s, const ExactRoute& rt, const unsigned long long* recvbuf,
                                double* const* dst, int32_t* anc_local);
+// exact-sharded fused run without host round trips: every count comes from the
+// device plan (ExactPlan), particles move between neighbouring ranks only, through fixed-size
+// blocks of `cap` slots per side (a collective's size must be fixed at enqueue / capture
+// time); a slot that needs a farther rank or a larger block sets the overflow flag and the
+// host re-runs the filter on the eager path (it starts from constants: the same bits).
+constexpr int kXWords = 7;                      // a moving slot: x pair, v pair, dv pair, global ancestor id
+constexpr int kXStat = 8;                       // u64 stats: [0] overflow bits, [1] largest block needed
+                                                // (slots), [2] largest trace-back excursion (ids)
+struct ExactStep {
+    const ExactPlan* xp;
+    const Decision* dec;
+    const int32_t* anc_out;                     // the window's ancestors (local ids, window-relative)
+    const double* x;                            // this rank's particles at the step (pairs, pre-resample)
+    const double* v;
+    const double* dv;                           // valid at the last step only (moved anyway)
+    int32_t* anc_row;                           // [N] global ancestor ids of this rank's slots
+    unsigned long long* send[2];                // [cap * kXWords] to the left (0) / right (1) neighbour
+    const unsigned long long* recv[2];          // from the left / right neighbour
+    double* xr;                                 // [2N] pairs received, by slot
+    double* vr;
+    double* dvr;
+    unsigned long long* stat;                   // [kXStat]
+    int64_t cap, N, goff;
+    int32_t rank, world;
+};
+hipError_t launch_exact_route(hipStream_t s, const ExactStep& e);
+hipError_t launch_exact_recv(hipStream_t s, const ExactStep& e);
+// trace-back windows: for every level L = 1..T and each side, `ctr` ids at the edge of this
+// rank's range: x_{L+1} (pair) and the ancestor of step L-1 (the id itself if it did not
+// resample), 3 words each, [L-1][side][ctr][3]
+struct ExactWin {
+    const double* const* hist_work;             // [T+2] x_t working buffers (pairs)
+    const int32_t* anc_log;
+    int64_t anc_stride;
+    const Decision* dec;                        // [T+1]
+    unsigned long long* out;
+    int64_t ctr, N, goff;
+    int32_t T, has_left, has_right;
+};
+hipError_t launch_exact_window_pack(hipStream_t s, const ExactWin& w);
+struct ExactFinal {
+    int32_t T, keep_history;
+    int64_t N, goff, ctr;
+    double x0[2];
+    double* const* hist_work;
+    double* const* hist_out;
+    const double* x_work;                       // no-history: x_{T+1}
+    double* x_out;
+    const double* v_work;
+    double* v_out;
+    const double* dv_work;
+    double* dv_out;
+    const double* xr;                           // the last step's received pairs
+    const double* vr;
+    const double* dvr;
+    double* w;
+    const int32_t* anc_log;
+    int64_t anc_stride;
+    const Decision* dec;
+    const unsigned long long* win[2];           // windows received from the left / right neighbour
+    unsigned long long* stat;
+};
+hipError_t launch_exact_final(hipStream_t s, const ExactFinal& f);
 hipError_t launch_rs_scan(hipStream_t s, int64_t N, const ShardRecord* rec, const Decision* dec,
                           const FillPlan& plan, const unsigned long long* tileOff,
                           const unsigned long long* qbuf, int32_t* anc, hipEvent_t e0 = nullptr,
@@ -504,6 +578,10 @@ struct Ssm2dArgs {
     const Decision* dec_prev;  // decision of step t-1 (nullptr at t = 1)
     MaxSlots* ms;              // this step's max slots
     int32_t identity = 0;      // exact shards: the previous state is already in slot order (no gather)
+    // exact shards without host round trips: anc_prev holds global ids; an ancestor outside
+    // [goff, goff + N) arrived from a neighbour and its pair is xr / vr at the slot itself
+    const double* xr = nullptr;
+    const double* vr = nullptr;
 };
 hipError_t launch_ssm2d_propagate(hipStream_t s, const Ssm2dArgs& a, hipEvent_t e0 = nullptr,
                                   hipEvent_t e1 = nullptr);

@@ -668,6 +668,174 @@ __global__ __launch_bounds__(kBlock) void k_exact_unpack(ExactRoute rt, const u6
     anc_local[li] = (int32_t)blk[(u64)rt.ncomp * len + idx];
 }
 
+// ---- exact shards without host round trips (ExactStep, wsmc_internal.h) -------------------
+__device__ __forceinline__ u64 overlap_d(u64 a0, u64 a1, u64 b0, u64 b1) {
+    const u64 lo = a0 > b0 ? a0 : b0, hi = a1 < b1 ? a1 : b1;
+    return hi > lo ? hi - lo : 0ull;
+}
+__device__ __forceinline__ void stat_overflow(u64* stat, u64 bit) { atomicOr(stat, bit); }
+
+// the filled window's slots to their owners: this rank's slots get their global ancestor id
+// in place, a neighbour's slots are packed with the ancestor's state into its fixed block
+__global__ __launch_bounds__(kBlock) void k_exact_route(ExactStep e) {
+    if (!e.dec->resampled) return;
+    const ExactPlan* xp = e.xp;
+    const u64 a = xp->a, b = xp->b;
+    const u64 lo = xp->gofs[e.rank], hi = xp->gofs[e.rank + 1];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        // the blocks this step needs: a slot of a rank further than a neighbour, or more
+        // than `cap` slots for one neighbour, cannot be moved this way
+        u64 need = 0;
+        for (int g = 0; g < e.world; ++g) {
+            if (g == e.rank) continue;
+            const u64 n = overlap_d(a, b, xp->gofs[g], xp->gofs[g + 1]);
+            if (!n) continue;
+            if (g != e.rank - 1 && g != e.rank + 1) stat_overflow(e.stat, 1ull);
+            need = n > need ? n : need;
+        }
+        if (need > (u64)e.cap) stat_overflow(e.stat, 1ull);
+        if (need) atomicMax(e.stat + 1, need);
+    }
+    for (u64 j = (u64)blockIdx.x * kBlock + threadIdx.x; j < b - a; j += (u64)gridDim.x * kBlock) {
+        const u64 s = a + j;
+        const int32_t m = e.anc_out[j];
+        const u64 gid = (u64)e.goff + (u64)m;
+        if (s >= lo && s < hi) {
+            e.anc_row[s - lo] = (int32_t)gid;
+            continue;
+        }
+        const int side = s < lo ? 0 : 1;
+        const int nb = side ? e.rank + 1 : e.rank - 1;
+        if (nb < 0 || nb >= e.world || s < xp->gofs[nb] || s >= xp->gofs[nb + 1]) continue;   // flagged above
+        const u64 first = a > xp->gofs[nb] ? a : xp->gofs[nb];
+        const u64 idx = s - first;
+        if (idx >= (u64)e.cap) continue;                                                       // flagged above
+        u64* blk = e.send[side] + idx * kXWords;
+        const d2 x = *reinterpret_cast<const d2*>(e.x + 2 * (int64_t)m);
+        const d2 v = *reinterpret_cast<const d2*>(e.v + 2 * (int64_t)m);
+        const d2 dv = *reinterpret_cast<const d2*>(e.dv + 2 * (int64_t)m);
+        blk[0] = (u64)wsmc_d2bits(x.x); blk[1] = (u64)wsmc_d2bits(x.y);
+        blk[2] = (u64)wsmc_d2bits(v.x); blk[3] = (u64)wsmc_d2bits(v.y);
+        blk[4] = (u64)wsmc_d2bits(dv.x); blk[5] = (u64)wsmc_d2bits(dv.y);
+        blk[6] = gid;
+    }
+}
+// the slots of this rank filled by a neighbour: the ancestor's pairs by slot, its global id
+// into the ancestor row (threads [0, cap) the left block, [cap, 2 cap) the right one)
+__global__ __launch_bounds__(kBlock) void k_exact_recv(ExactStep e) {
+    if (!e.dec->resampled) return;
+    const u64 t = (u64)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= 2 * (u64)e.cap) return;
+    const int side = t >= (u64)e.cap ? 1 : 0;
+    const u64 j = t - (side ? (u64)e.cap : 0ull);
+    const int nb = side ? e.rank + 1 : e.rank - 1;
+    if (nb < 0 || nb >= e.world) return;
+    const ExactPlan* xp = e.xp;
+    const u64 lo = xp->gofs[e.rank], hi = xp->gofs[e.rank + 1];
+    const u64 cnt = overlap_d(xp->seg[nb], xp->seg[nb + 1], lo, hi);
+    if (j >= cnt) return;                       // cnt > cap: the sender flagged it
+    const u64 li = (xp->seg[nb] > lo ? xp->seg[nb] : lo) - lo + j;
+    const u64* blk = e.recv[side] + j * kXWords;
+    *reinterpret_cast<d2*>(e.xr + 2 * li) = d2{wsmc_bits2d(blk[0]), wsmc_bits2d(blk[1])};
+    *reinterpret_cast<d2*>(e.vr + 2 * li) = d2{wsmc_bits2d(blk[2]), wsmc_bits2d(blk[3])};
+    *reinterpret_cast<d2*>(e.dvr + 2 * li) = d2{wsmc_bits2d(blk[4]), wsmc_bits2d(blk[5])};
+    e.anc_row[li] = (int32_t)blk[6];
+}
+// trace-back windows: out[side][L-1][j][3] for the first (side 0, to the left neighbour) and
+// last (side 1, to the right neighbour) ctr ids of this rank's range
+__global__ __launch_bounds__(kBlock) void k_exact_window_pack(ExactWin w) {
+    const int64_t per = (int64_t)w.T * w.ctr;
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= 2 * per) return;
+    const int side = t >= per ? 1 : 0;
+    if (side == 0 && !w.has_left) return;
+    if (side == 1 && !w.has_right) return;
+    const int64_t r = t - (side ? per : 0);
+    const int L = (int)(r / w.ctr) + 1;
+    const int64_t j = r - (int64_t)(L - 1) * w.ctr;
+    const int64_t loc = side ? w.N - w.ctr + j : j;
+    const d2 x = *reinterpret_cast<const d2*>(w.hist_work[L + 1] + 2 * loc);
+    const int32_t an = (L >= 2 && w.dec[L - 1].resampled) ? w.anc_log[(int64_t)(L - 2) * w.anc_stride + loc]
+                                                          : (int32_t)(w.goff + loc);
+    u64* o = w.out + ((int64_t)side * per + r) * 3;
+    o[0] = (u64)wsmc_d2bits(x.x);
+    o[1] = (u64)wsmc_d2bits(x.y);
+    o[2] = (u64)(uint32_t)an;
+}
+// the window entry of global id g at level L (the left neighbour's last ids or the right
+// neighbour's first ones); nullptr (and the overflow bit) outside both
+__device__ __forceinline__ const u64* exact_win(const ExactFinal& f, int L, int64_t g) {
+    if (f.win[0] && g >= f.goff - f.ctr && g < f.goff)
+        return f.win[0] + ((int64_t)(L - 1) * f.ctr + (g - (f.goff - f.ctr))) * 3;
+    if (f.win[1] && g >= f.goff + f.N && g < f.goff + f.N + f.ctr)
+        return f.win[1] + ((int64_t)(L - 1) * f.ctr + (g - (f.goff + f.N))) * 3;
+    return nullptr;
+}
+// k_ssm2d_final on exact shards: ancestors are global ids; ids of this rank read its own
+// buffers, a neighbour's come from the last step's received pairs (level T) or the trace
+// windows (levels below)
+__global__ __launch_bounds__(kBlock) void k_exact_final(ExactFinal f) {
+    __shared__ u64 lds4[4];
+    const int64_t N = f.N;
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int T = f.T;
+    const int64_t S = f.anc_stride;
+    u64 exc = 0, bad = 0;
+    if (i < N) {
+        const bool rsT = f.dec[T].resampled;
+        int64_t g = rsT ? (int64_t)f.anc_log[(int64_t)(T - 1) * S + i] : f.goff + i;
+        int64_t loc = g - f.goff;
+        const bool here = loc >= 0 && loc < N;
+        const d2 v = *reinterpret_cast<const d2*>(here ? f.v_work + 2 * loc : f.vr + 2 * i);
+        f.v_out[i] = v.x; f.v_out[N + i] = v.y;
+        const d2 dv = *reinterpret_cast<const d2*>(here ? f.dv_work + 2 * loc : f.dvr + 2 * i);
+        f.dv_out[i] = dv.x; f.dv_out[N + i] = dv.y;
+        if (rsT) f.w[i] = f.dec[T].mean;
+        const double* xt = f.keep_history ? f.hist_work[T + 1] : f.x_work;
+        const d2 xT = *reinterpret_cast<const d2*>(here ? xt + 2 * loc : f.xr + 2 * i);
+        double* dT = f.keep_history ? f.hist_out[T + 1] : f.x_out;
+        dT[i] = xT.x; dT[N + i] = xT.y;
+        if (f.keep_history) {
+            for (int s = T - 1; s >= 1; --s) {
+                loc = g - f.goff;
+                bool in = loc >= 0 && loc < N;
+                const u64* wv = in ? nullptr : exact_win(f, s + 1, g);
+                if (!in) {
+                    const u64 d = (u64)(g < f.goff ? f.goff - g : g - (f.goff + N) + 1);
+                    exc = d > exc ? d : exc;
+                }
+                if (f.dec[s].resampled) {
+                    if (in) g = f.anc_log[(int64_t)(s - 1) * S + loc];
+                    else if (wv) g = (int64_t)(int32_t)(uint32_t)wv[2];
+                    else bad = 1;
+                }
+                loc = g - f.goff;
+                in = loc >= 0 && loc < N;
+                d2 x = d2{0.0, 0.0};
+                if (in) {
+                    x = *reinterpret_cast<const d2*>(f.hist_work[s + 1] + 2 * loc);
+                } else {
+                    const u64 d = (u64)(g < f.goff ? f.goff - g : g - (f.goff + N) + 1);
+                    exc = d > exc ? d : exc;
+                    const u64* wx = exact_win(f, s, g);
+                    if (wx) x = d2{wsmc_bits2d(wx[0]), wsmc_bits2d(wx[1])};
+                    else bad = 1;
+                }
+                double* dst = f.hist_out[s + 1];
+                dst[i] = x.x; dst[N + i] = x.y;
+            }
+            double* d1 = f.hist_out[1];
+            d1[i] = f.x0[0]; d1[N + i] = f.x0[1];
+        }
+    }
+    exc = block_max_u64(exc, lds4);
+    bad = block_max_u64(bad, lds4);
+    if (threadIdx.x == 0) {
+        if (exc) atomicMax(f.stat + 2, exc);
+        if (bad) stat_overflow(f.stat, 2ull);
+    }
+}
+
 constexpr int kOverflowBlocks = 256;   // fill blocks serving overflow chunks (grid-stride)
 
 constexpr int kScatterMax = 8;          // slots a thread writes for one particle before the block helps
@@ -1918,8 +2086,17 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_prop(Ssm2dArgs a) {
                 xp[j][k] = d2{a.x0[0], a.x0[1]};
                 vp[j][k] = d2{a.v0[0], a.v0[1]};
             } else if (k == 0 || two[j]) {
-                xp[j][k] = *reinterpret_cast<const d2*>(a.x_prev + 2 * src[j][k]);
-                vp[j][k] = *reinterpret_cast<const d2*>(a.v_prev + 2 * src[j][k]);
+                if (MODE & 16) {   // exact shards: global ids; a neighbour's particle arrived at the slot
+                    const int64_t loc = rs ? src[j][k] - a.goff : src[j][k];
+                    const bool here = loc >= 0 && loc < N;
+                    const double* xs = here ? a.x_prev + 2 * loc : a.xr + 2 * (i0 + k);
+                    const double* vs = here ? a.v_prev + 2 * loc : a.vr + 2 * (i0 + k);
+                    xp[j][k] = *reinterpret_cast<const d2*>(xs);
+                    vp[j][k] = *reinterpret_cast<const d2*>(vs);
+                } else {
+                    xp[j][k] = *reinterpret_cast<const d2*>(a.x_prev + 2 * src[j][k]);
+                    vp[j][k] = *reinterpret_cast<const d2*>(a.v_prev + 2 * src[j][k]);
+                }
             }
         }
     }
@@ -2209,6 +2386,27 @@ hipError_t launch_exact_pack(hipStream_t s, const ExactRoute& rt, const int32_t*
     if (!cnt) return hipSuccess;
     hipLaunchKernelGGL(k_exact_pack, dim3((unsigned)((cnt + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rt, anc_out,
                        src, dst, anc_local, sendbuf);
+    return hipGetLastError();
+}
+hipError_t launch_exact_route(hipStream_t s, const ExactStep& e) {
+    // grid-stride over the window (any size); a window beyond N + 2 cap overflows anyway
+    int64_t nb = (e.N + 2 * e.cap + kBlock - 1) / kBlock;
+    if (nb > 4096) nb = 4096;
+    hipLaunchKernelGGL(k_exact_route, dim3((unsigned)nb), dim3(kBlock), 0, s, e);
+    return hipGetLastError();
+}
+hipError_t launch_exact_recv(hipStream_t s, const ExactStep& e) {
+    hipLaunchKernelGGL(k_exact_recv, dim3((unsigned)((2 * e.cap + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, e);
+    return hipGetLastError();
+}
+hipError_t launch_exact_window_pack(hipStream_t s, const ExactWin& w) {
+    const int64_t n = 2 * (int64_t)w.T * w.ctr;
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_exact_window_pack, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, w);
+    return hipGetLastError();
+}
+hipError_t launch_exact_final(hipStream_t s, const ExactFinal& f) {
+    hipLaunchKernelGGL(k_exact_final, grid_for(f.N), dim3(kBlock), 0, s, f);
     return hipGetLastError();
 }
 hipError_t launch_exact_unpack(hipStream_t s, const ExactRoute& rt, const u64* recvbuf, double* const* dst,
@@ -2583,6 +2781,7 @@ static int prop_mode() {
 hipError_t launch_ssm2d_propagate(hipStream_t s, const Ssm2dArgs& a, hipEvent_t e0, hipEvent_t e1) {
     const dim3 g((unsigned)((a.N + 2 * kBlock - 1) / (2 * kBlock)));
     // IT = 2 / 4 pairs per thread (grid / 2, / 4) measured 18.8 / 22.2 us against 17.0 (1M)
+    if (a.xr) return launch_timed(k_ssm2d_prop<16>, g, dim3(kBlock), s, e0, e1, a);   // exact shards
     switch (prop_mode()) {
         case 1: return launch_timed(k_ssm2d_prop<1>, g, dim3(kBlock), s, e0, e1, a);
         case 2: return launch_timed(k_ssm2d_prop<2>, g, dim3(kBlock), s, e0, e1, a);

@@ -126,6 +126,7 @@ SIGNATURES = {
     "wsmc_run_get_timing": (C.c_int, [_P, C.POINTER(RunTiming)]),
     "wsmc_debug_kernel_bench": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_int32, _D]),
     "wsmc_debug_inject_failure": (C.c_int, [_P, C.c_int32, C.c_int32]),
+    "wsmc_debug_exact": (C.c_int, [_P, C.c_int64, C.c_int64, C.POINTER(C.c_int64)]),
 }
 
 

@@ -23,6 +23,7 @@ import time
 _MAGIC = b"WSMCRDZV2"
 _HELLO = struct.Struct("<9s32sI")          # magic, job tag (padded), rank
 _MAX_MSG = 1 << 30
+_HANDSHAKE_S = 5.0                         # a listener that is not our rank 0 must not stall the scan
 
 
 # Messages are a small tagged binary encoding of the values the ranks exchange (None,
@@ -143,7 +144,7 @@ class HostComm:
             got = {}
             while len(got) < self.world - 1:
                 conn, _ = srv.accept()
-                conn.settimeout(timeout)
+                conn.settimeout(_HANDSHAKE_S)        # a peer that connects and sends nothing
                 try:
                     magic, tag, r = _HELLO.unpack(_recv_exact(conn, _HELLO.size))
                 except (OSError, ConnectionError, struct.error):
@@ -153,6 +154,7 @@ class HostComm:
                     conn.close()
                     continue
                 got[r] = conn
+                conn.settimeout(timeout)
                 conn.sendall(_MAGIC)
             srv.close()
             self.peers = [got[r] for r in range(1, self.world)]
@@ -161,9 +163,12 @@ class HostComm:
                 for k in range(16):
                     try:
                         s = socket.create_connection((addr, port + 1 + k), timeout=2.0)
-                        s.settimeout(timeout)
+                        # another process's listener on a scanned port (e.g. an RCCL bootstrap
+                        # socket) answers nothing: give up on it quickly and go on scanning
+                        s.settimeout(_HANDSHAKE_S)
                         s.sendall(_HELLO.pack(_MAGIC, self.tag, self.rank))
                         if _recv_exact(s, len(_MAGIC)) == _MAGIC:
+                            s.settimeout(timeout)
                             self.sock = s
                             break
                         s.close()
@@ -204,6 +209,20 @@ class HostComm:
 
 
 def from_env(timeout: float = 120.0) -> HostComm:
-    # one node: loopback, whatever MASTER_ADDR names
+    """The ranks of one single-node job (torch.distributed.run): rank 0 listens on loopback.
+    A job spread over several nodes cannot rendezvous here: fail at once instead of waiting
+    for the timeout."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if world != local_world:
+        raise RuntimeError(f"hostcomm serves one node: WORLD_SIZE {world} != LOCAL_WORLD_SIZE {local_world}")
+    addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    if addr not in ("127.0.0.1", "localhost", "::1", socket.gethostname()):
+        try:
+            local = socket.gethostbyname(addr).startswith("127.")
+        except OSError:
+            local = False
+        if not local:
+            raise RuntimeError(f"hostcomm serves one node: MASTER_ADDR {addr} is not this host's loopback")
     return HostComm(int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
                     "127.0.0.1", int(os.environ.get("MASTER_PORT", "29500")), timeout=timeout)
