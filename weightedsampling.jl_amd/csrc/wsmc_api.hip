@@ -451,7 +451,7 @@ int wsmc_destroy(wsmc_ctx* c) {
     void* bufs[] = {c->dec_always, c->xchg, c->scache, c->scache_back, c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->cdf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount, c->wslots[0], c->wslots[1],
                     c->d_colptr, c->run_params, c->d_tape, c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp,
                     c->vscratch, c->xscratch, c->xp, c->comb, c->anc_out, c->xbuf, c->d_comp, c->d_ctape, c->d_prog, c->rs_grp[0], c->rs_grp[1],
-                    c->xpairs, c->xnb, c->xwin, c->xstat, c->w_save};
+                    c->xpairs, c->xnb, c->xwin, c->xstat, c->w_save, c->xms, c->xanc, c->xlines};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (double* p : c->xrun)
@@ -2632,12 +2632,25 @@ static bool exact_eager_forced() {   // diagnostics / A-B: the host-driven exact
     }();
     return v;
 }
+// group-line words per rank in the all-gathered statistics: the same on every rank (the
+// larger of the two shard sizes a ragged split can give)
+static inline int64_t run_grp_words(int64_t N);
+static int64_t exact_line_words(const wsmc_ctx* c) {
+    const int64_t lo = c->gN / c->world, hi = (c->gN + c->world - 1) / c->world;
+    return std::max(run_grp_words(lo), run_grp_words(hi));
+}
 static int ensure_exact_async(wsmc_ctx* c, int32_t T, int64_t cap, int64_t ctr) {
     int r = ensure_exact(c);
     if (r) return r;
     const int64_t N = c->N;
     const int64_t wwords = (int64_t)T * ctr * 3;
-    const bool grow = !c->xpairs || cap > c->xnb_cap || wwords > c->xwin_words;
+    const int64_t astride = (N + 2 * cap + 3) & ~(int64_t)3;
+    const int64_t awords = (int64_t)T * astride;
+    const int64_t msn = (int64_t)(T + 1) * c->world;
+    const int64_t lwords = msn * exact_line_words(c);
+    const bool grow = !c->xpairs || cap > c->xnb_cap || wwords > c->xwin_words || awords > c->xanc_words ||
+                      msn > c->xms_n || lwords > c->xlines_words;
+    c->xanc_stride = astride;
     if (!grow && c->xstat && c->w_save) return WSMC_OK;
     WSMC_HIP(hipStreamSynchronize(c->stream));
     if (!c->xpairs) WSMC_HIP(hipMalloc(&c->xpairs, sizeof(double) * 6 * (size_t)N));
@@ -2652,6 +2665,21 @@ static int ensure_exact_async(wsmc_ctx* c, int32_t T, int64_t cap, int64_t ctr) 
         if (c->xwin) WSMC_HIP(hipFree(c->xwin));
         WSMC_HIP(hipMalloc(&c->xwin, sizeof(unsigned long long) * 4 * (size_t)wwords));
         c->xwin_words = wwords;
+    }
+    if (awords > c->xanc_words) {
+        if (c->xanc) WSMC_HIP(hipFree(c->xanc));
+        WSMC_HIP(hipMalloc(&c->xanc, sizeof(int32_t) * (size_t)awords));
+        c->xanc_words = awords;
+    }
+    if (msn > c->xms_n) {
+        if (c->xms) WSMC_HIP(hipFree(c->xms));
+        WSMC_HIP(hipMalloc(&c->xms, sizeof(MaxSlots) * (size_t)msn));
+        c->xms_n = msn;
+    }
+    if (lwords > c->xlines_words) {
+        if (c->xlines) WSMC_HIP(hipFree(c->xlines));
+        WSMC_HIP(hipMalloc(&c->xlines, sizeof(unsigned long long) * (size_t)lwords));
+        c->xlines_words = lwords;
     }
     return WSMC_OK;
 }
@@ -2669,9 +2697,18 @@ static int enqueue_ssm2d_exact(wsmc_ctx* c, const RunPlan& p, int64_t cap, int64
     const int64_t N = c->N;
     const int W = c->world, me = c->rank;
     const double cpre = 2.0 * WSMC_LOG2PI + 2.0 * wsmc_log(p.r_var);
-    WSMC_HIP(hipMemsetAsync(c->run_max, 0, sizeof(MaxSlots) * (T + 1), c->stream));
+    WSMC_HIP(hipMemsetAsync(c->xms, 0, sizeof(MaxSlots) * (size_t)(T + 1) * W, c->stream));
+    const int64_t xstride = exact_line_words(c);
+    const int G = group_tiles(N);
+    WSMC_HIP(hipMemsetAsync(c->xlines, 0, sizeof(unsigned long long) * (size_t)(T + 1) * W * xstride, c->stream));
     WSMC_HIP(hipMemsetAsync(c->run_dec, 0, sizeof(Decision) * (T + 1), c->stream));
     WSMC_HIP(hipMemsetAsync(c->xstat, 0, sizeof(unsigned long long) * kMaxShards * kXStat, c->stream));
+    const int64_t S = c->xanc_stride;
+    auto row = [&](int t) { return c->xanc + (size_t)(t - 1) * S; };   // step t's row, from its left margin
+    const int64_t glo = c->goff - cap;                                  // the global slot of row index 0
+    const unsigned long long row_lo = glo > 0 ? (unsigned long long)glo : 0ull;
+    const unsigned long long row_hi = std::min<unsigned long long>((unsigned long long)c->gN,
+                                                                   (unsigned long long)(c->goff + N + cap));
     WSMC_HIP(hipMemcpyAsync(c->w_save, c->w, sizeof(double) * N, hipMemcpyDeviceToDevice, c->stream));
     double* Xr = c->xpairs;
     double* Vr = Xr + 2 * N;
@@ -2709,37 +2746,52 @@ static int enqueue_ssm2d_exact(wsmc_ctx* c, const RunPlan& p, int64_t cap, int64
         a.v_next = vbuf[(t + 1) & 1];
         a.dv = t == T ? dvw : nullptr;
         a.w = c->w;
-        a.anc_prev = t > 1 ? c->anc_log + (size_t)(t - 2) * anc_stride(N) : nullptr;
+        a.anc_prev = t > 1 ? row(t - 1) + cap : nullptr;
         a.dec_prev = t > 1 ? c->run_dec + (t - 1) : nullptr;
-        a.ms = c->run_max + t;
+        MaxSlots* msx = c->xms + (size_t)t * W;   // every rank's slots of this step
+        a.ms = msx + me;
         a.identity = 0;
         a.xr = Xr;
         a.vr = Vr;
         WSMC_HIP(launch_ssm2d_propagate(c->stream, a));
-        // the global max, this shard's record relative to it (K from the global N), every
-        // rank's record: exactly the single-context statistics
-        WSMC_HIP(launch_max_publish(c->stream, c->run_max + t, c->xchg + me));
-        if ((r = exchange_words(c, c->xchg, 1, c->stream))) return r;
-        WSMC_HIP(launch_max_adopt(c->stream, c->xchg, W, c->mslots));
-        WSMC_HIP(launch_rs_sums(c->stream, c->w, N, c->mslots, c->tilep, c->qbuf, nullptr, nullptr, nullptr, 1, c->gN));
-        WSMC_HIP(launch_rs_reduce(c->stream, c->mslots, c->tilep, N, c->tileOff, c->rec + me, 0, 0.0, nullptr,
-                                  nullptr));
-        if ((r = exchange_recs(c, c->rec))) return r;
+        // every rank's max slots (the global max), this shard's record relative to it (K from
+        // the global N), every rank's record: exactly the single-context statistics
+        if ((r = exchange_words(c, reinterpret_cast<unsigned long long*>(msx), sizeof(MaxSlots) / 8, c->stream)))
+            return r;
+        // the statistics into this rank's group lines (every part), all-gathered in place of
+        // the record: the fill's blocks take the global Q and their CDF offsets from them, its
+        // record block builds every rank's record and decides (the single-GPU bits)
+        unsigned long long* lines = c->xlines + (size_t)t * W * xstride;
+        WSMC_HIP(launch_rs_sums(c->stream, c->w, N, msx, c->tilep, c->qbuf, nullptr, nullptr, lines + me * xstride,
+                                G, c->gN, W, 1));
+        if ((r = exchange_words(c, lines, xstride, c->stream))) return r;
         FillPlan plan = fill_plan(c, p.scheme, 3ull * (uint64_t)(t - 1) + 2ull, c->run_params);
         plan.slot_base = 0;   // slots are global: their keys too
-        WSMC_HIP(launch_rs_decide_exact(c->stream, c->rec, W, me, p.ess_min, plan, c->comb, c->run_dec + t, c->xp));
-        plan.xp = c->xp;
-        WSMC_HIP(launch_rs_reduce(c->stream, c->mslots, c->tilep, N, c->tileOff, c->rec + me, 0, p.ess_min,
-                                  c->run_dec + t, &plan));
-        WSMC_HIP(launch_rs_scan(c->stream, N, c->comb, c->run_dec + t, plan, c->tileOff, c->qbuf, c->anc_out));
+        plan.xlines = lines;
+        plan.xstride = xstride;
+        plan.xms = msx;
+        plan.n_global = (unsigned long long)c->gN;
+        plan.dx_world = W;
+        plan.dx_rank = me;
+        plan.dx_ess = p.ess_min;
+        plan.dx_comb = c->comb;
+        plan.dx_dec = c->run_dec + t;
+        plan.dx_xp = c->xp;
+        plan.id_base = (int32_t)c->goff;
+        plan.row_lo = row_lo;
+        plan.row_hi = row_hi;
+        plan.xstat = stat;
+        // the fill stores slot s at anc[s - row_lo]: the row index of s is s - glo
+        WSMC_HIP(launch_rs_fill_fused(c->stream, N, plan, lines + me * xstride, G, msx, p.ess_min, c->rec + me,
+                                      c->run_dec + t, c->qbuf, row(t) + ((int64_t)row_lo - glo)));
         ExactStep e;
         e.xp = c->xp;
         e.dec = c->run_dec + t;
-        e.anc_out = c->anc_out;
+        e.row = row(t);
         e.x = a.x_next;
         e.v = a.v_next;
         e.dv = dvw;
-        e.anc_row = c->anc_log + (size_t)(t - 1) * anc_stride(N);
+        e.anc_row = row(t) + cap;
         e.send[0] = snd[0]; e.send[1] = snd[1];
         e.recv[0] = rcv[0]; e.recv[1] = rcv[1];
         e.xr = Xr; e.vr = Vr; e.dvr = DVr;
@@ -2749,8 +2801,8 @@ static int enqueue_ssm2d_exact(wsmc_ctx* c, const RunPlan& p, int64_t cap, int64
         e.goff = c->goff;
         e.rank = me;
         e.world = W;
-        WSMC_HIP(launch_exact_route(c->stream, e));
         if (W > 1) {
+            WSMC_HIP(launch_exact_route(c->stream, e));
             if ((r = exchange_neighbors(c, snd, rcv, bw, c->stream))) return r;
             WSMC_HIP(launch_exact_recv(c->stream, e));
         }
@@ -2762,8 +2814,8 @@ static int enqueue_ssm2d_exact(wsmc_ctx* c, const RunPlan& p, int64_t cap, int64
     if (wins) {
         ExactWin w;
         w.hist_work = p.d_hist_work;
-        w.anc_log = c->anc_log;
-        w.anc_stride = anc_stride(N);
+        w.anc_log = c->xanc + cap;
+        w.anc_stride = S;
         w.dec = c->run_dec;
         w.out = c->xwin;
         w.ctr = ctr;
@@ -2792,8 +2844,8 @@ static int enqueue_ssm2d_exact(wsmc_ctx* c, const RunPlan& p, int64_t cap, int64
     f.dv_out = c->cols[p.coldv].front;
     f.xr = Xr; f.vr = Vr; f.dvr = DVr;
     f.w = c->w;
-    f.anc_log = c->anc_log;
-    f.anc_stride = anc_stride(N);
+    f.anc_log = c->xanc + cap;
+    f.anc_stride = S;
     f.dec = c->run_dec;
     f.win[0] = wins && me > 0 ? wrcv[0] : nullptr;
     f.win[1] = wins && me + 1 < W ? wrcv[1] : nullptr;
@@ -2994,8 +3046,8 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
     if (exact_async) {
         exact_sizes(c, &xcap, &xctr);
         if ((r = ensure_exact_async(c, T, xcap, xctr))) return r;
-        const void* xb[] = {c->xpairs, c->xnb, c->xwin, c->xstat, c->w_save, c->anc_out, c->taskTile, c->xp, c->comb,
-                            c->rec, c->xchg, c->mslots, c->tilep, c->tileOff, c->qbuf, c->taskOff};
+        const void* xb[] = {c->xpairs, c->xnb, c->xwin, c->xstat, c->w_save, c->xms, c->xanc, c->xlines, c->taskTile, c->xp,
+                            c->comb, c->rec, c->tilep, c->tileOff, c->qbuf, c->taskOff};
         for (const void* q : xb) mix(q);
     }
     const std::string key = std::string(keybuf) + " ptr=" + std::to_string(h) +
@@ -3103,6 +3155,7 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
             }
         }
     }
+    bool rows_x = exact_async;   // the ancestor rows are the exact run's (not the eager re-run's)
     if (exact_async) {
         // every rank's overflow statistics (all-gathered by the run): the same on all ranks, so
         // all of them re-run on the eager path together, from the weights the run started with
@@ -3123,6 +3176,7 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
             if (bits & 1ull) c->x_cap = std::max<int64_t>(4 * xcap, 2 * (int64_t)need);
             if (bits & 2ull) c->x_ctr = std::max<int64_t>(4 * xctr, 2 * (int64_t)exc);
             WSMC_HIP(hipMemcpyAsync(c->w, c->w_save, sizeof(double) * c->N, hipMemcpyDeviceToDevice, c->stream));
+            rows_x = false;
             if ((r = ssm2d_run_exact(c, p, op_base))) {
                 if (temp_tables) (void)hipFree(temp_tables);
                 return r;
@@ -3136,8 +3190,9 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
     // wsmc_last_ancestors reports the run's last resample, as after the statement sequence
     for (int t = T; t >= 1; --t)
         if (hdec[t].resampled) {
-            WSMC_HIP(hipMemcpyAsync(c->anc, c->anc_log + (size_t)(t - 1) * anc_stride(c->N), sizeof(int32_t) * c->N,
-                                    hipMemcpyDeviceToDevice, c->stream));
+            const int32_t* src = rows_x ? c->xanc + (size_t)(t - 1) * c->xanc_stride + xcap
+                                        : c->anc_log + (size_t)(t - 1) * anc_stride(c->N);
+            WSMC_HIP(hipMemcpyAsync(c->anc, src, sizeof(int32_t) * c->N, hipMemcpyDeviceToDevice, c->stream));
             set_anc_last(c, nullptr, -1);
             break;
         }

@@ -213,6 +213,12 @@ struct wsmc_ctx {
     int64_t xwin_words = 0;                 // words per block allocated
     unsigned long long* xstat = nullptr;    // [kMaxShards][kXStat], this rank's at rank * kXStat
     double* w_save = nullptr;               // [N] the weights at the run's start (re-run after an overflow)
+    wsmc::MaxSlots* xms = nullptr;          // [T+1][world] every rank's max slots per step (all-gathered)
+    int64_t xms_n = 0;
+    int32_t* xanc = nullptr;                // [T][xanc_stride] ancestor rows: margin, this rank's N slots, margin
+    unsigned long long* xlines = nullptr;   // [T+1][world][line words] every rank's statistics group lines
+    int64_t xlines_words = 0;
+    int64_t xanc_words = 0, xanc_stride = 0;
     int64_t x_cap = 0, x_ctr = 0;           // block / window sizes in use (0: defaults; grown on overflow)
     unsigned long long x_need = 0, x_exc = 0;   // the last run's largest block / lineage excursion
     int64_t x_overflows = 0;                // runs re-done on the eager path
@@ -311,7 +317,9 @@ hipError_t launch_rs_sums(hipStream_t s, const double* w, int64_t N, const MaxSl
                           unsigned long long* tilep, unsigned long long* qbuf,
                           hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr,
                           unsigned long long* grp = nullptr, int G = 1,
-                          int64_t Nk = 0 /* N of K = 63 - ceil(log2 N): the global N when exact */);
+                          int64_t Nk = 0 /* N of K = 63 - ceil(log2 N): the global N when exact */,
+                          int nms = 1 /* slot sets in ms (exact shards: every rank's, all-gathered) */,
+                          int gall = 0 /* exact shards: every part into the group lines (grp) */);
 struct FillPlan {          // ancestor-fill task planning (in the reduce kernel)
     const unsigned long long* tilep;   // per-tile partials (sum q first)
     int32_t* taskOff;
@@ -326,11 +334,29 @@ struct FillPlan {          // ancestor-fill task planning (in the reduce kernel)
     unsigned long long* grp_zero = nullptr;   // fused fill: the next call's group lines, zeroed by its record block
     MaxSlots* ms_reset = nullptr;      // fused fill: the record block writes the reset weights' max here
     int64_t grp_zero_words = 0;
+    // exact shards without host round trips: the fill writes global ids (id_base + local) into
+    // a row covering the global slots [row_lo, row_hi), and a slot outside sets xstat bit 0
+    int32_t id_base = 0;
+    unsigned long long row_lo = 0, row_hi = 0;
+    unsigned long long* xstat = nullptr;
+    // ... the fused fill (k_rs_fill_fused) takes its totals from every rank's all-gathered
+    // group lines (xlines, xstride words per rank) and its record block decides for all
+    const unsigned long long* xlines = nullptr;
+    int64_t xstride = 0;
+    const MaxSlots* xms = nullptr;              // every rank's max slots (all-gathered)
+    unsigned long long n_global = 0;
+    // ... and the reduce kernel takes the single-GPU decision first (k_rs_decide_exact's work)
+    const ShardRecord* dx_recs = nullptr;
+    ShardRecord* dx_comb = nullptr;
+    Decision* dx_dec = nullptr;
+    ExactPlan* dx_xp = nullptr;
+    int32_t dx_world = 0, dx_rank = 0;
+    double dx_ess = 0.0;
 };
 hipError_t launch_rs_reduce(hipStream_t s, const MaxSlots* ms, const unsigned long long* tilep, int64_t N,
                             unsigned long long* tileOff, ShardRecord* rec, int decide_local, double ess_min,
                             Decision* dec, const FillPlan* plan, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr,
-                            unsigned long long* esum = nullptr);
+                            unsigned long long* esum = nullptr, int nms = 1);
 hipError_t launch_rs_decide(hipStream_t s, const ShardRecord* recs, int world, int rank, double ess_min,
                             Decision* dec);
 // describe(): median sort keys, the StatsBase walk on the sorted prefix, histogram counts
@@ -429,11 +455,12 @@ constexpr int kXStat = 8;                       // u64 stats: [0] overflow bits,
 struct ExactStep {
     const ExactPlan* xp;
     const Decision* dec;
-    const int32_t* anc_out;                     // the window's ancestors (local ids, window-relative)
+    const int32_t* row;                         // this step's ancestor row from its left margin (cap slots
+                                                // before the rank's range; global ids)
     const double* x;                            // this rank's particles at the step (pairs, pre-resample)
     const double* v;
     const double* dv;                           // valid at the last step only (moved anyway)
-    int32_t* anc_row;                           // [N] global ancestor ids of this rank's slots
+    int32_t* anc_row;                           // row + cap: [N] global ancestor ids of this rank's slots
     unsigned long long* send[2];                // [cap * kXWords] to the left (0) / right (1) neighbour
     const unsigned long long* recv[2];          // from the left / right neighbour
     double* xr;                                 // [2N] pairs received, by slot

@@ -291,6 +291,15 @@ static_assert(kSlots == 64, "one lane per max slot");
 __device__ __forceinline__ double wave_slots_max(const MaxSlots* ms) {
     return wsmc_ord_dec(wave_max_u64(ms->v[threadIdx.x & 63][0]));
 }
+// the same over nms consecutive slot sets (exact shards: every rank's, all-gathered)
+__device__ __forceinline__ double wave_slots_max_n(const MaxSlots* ms, int nms) {
+    u64 m = 0;
+    for (int g = 0; g < nms; ++g) {
+        const u64 v = ms[g].v[threadIdx.x & 63][0];
+        m = v > m ? v : m;
+    }
+    return wsmc_ord_dec(wave_max_u64(m));
+}
 // exact integer block sums of P values through LDS (transpose, two levels)
 template <int NT, int P>
 __device__ __forceinline__ void block_sum_parts(const u64 (&acc)[P], u64 (*red)[NT], u64 (*red2)[16],
@@ -364,7 +373,7 @@ __device__ __forceinline__ u64 qacc_tile(QAcc a, double (*s_f)[NB / 64], u64* ou
         t = (u64)f;                                         // exact integer <= 2^53
         out[th] = t;
     }
-    return th == 0 ? t : 0ull;
+    return t;   // thread k < kPart: part k (thread 0: the tile's sum q), 0 elsewhere
 }
 
 // Weight statistics of one 1024-particle tile (256 threads x 4 particles, coalesced):
@@ -374,7 +383,7 @@ template <int MODE>
 __global__ __launch_bounds__(kSumBlock) void k_rs_sums_t(const double* __restrict__ w, int64_t N,
                                                          const MaxSlots* __restrict__ ms, u64* __restrict__ tilep,
                                                          u64* __restrict__ qbuf, u64* __restrict__ grp, int G,
-                                                         int64_t Nk) {
+                                                         int64_t Nk, int nms, int gall) {
     constexpr int IT = kRsTile / kSumBlock;
     __shared__ double s_f[kPart][kSumBlock / 64];
     const int th = threadIdx.x;
@@ -385,7 +394,7 @@ __global__ __launch_bounds__(kSumBlock) void k_rs_sums_t(const double* __restric
         const int64_t i = base + (int64_t)k * kSumBlock + th;
         lw[k] = i < N ? w[i] : -WSMC_INF;
     }
-    const double M = MODE == 4 ? 0.0 : wave_slots_max(ms);
+    const double M = MODE == 4 ? 0.0 : wave_slots_max_n(ms, nms);
     const double sK = wsmc_pow2i(wsmc_qbits((uint64_t)Nk));   // Nk: the global N when exact-sharded
     QAcc acc;
 #pragma unroll
@@ -410,6 +419,11 @@ __global__ __launch_bounds__(kSumBlock) void k_rs_sums_t(const double* __restric
         atomicAdd(gl, t);
         atomicMax(gl + 1, t);
     }
+    // exact shards: the group lines carry every part (they are all-gathered in place of the
+    // record): word 2 sum q2, 3 sum wf2, 4 sum wf (integer atomics, order-free); word 7 of
+    // line 0 the shard size
+    if (gall && th >= 1 && th < kPart) atomicAdd(grp + (int64_t)(blockIdx.x / G) * kGroupLine + 1 + th, t);
+    if (gall && blockIdx.x == 0 && th == kPart) atomicAdd(grp + 7, (u64)N);
 }
 
 __device__ __forceinline__ wsmc_shard_stats record_stats(const ShardRecord& r) {
@@ -453,6 +467,8 @@ __device__ void decide_records(const ShardRecord* recs, int world, int rank, dou
     dec->mean = rs ? wsmc_shard_mean(&me) : 0.0;
 }
 
+__device__ void decide_exact(const ShardRecord* recs, int world, int rank, double ess_min, const FillPlan& plan,
+                             ShardRecord* comb, Decision* dec, ExactPlan* xp);
 // one block: shard totals, tile offsets, the ancestor-fill task plan and (one GPU) the decision
 // overflow chunks (past the first) a tile with integer weight sum qb may need
 __device__ __forceinline__ int ovf_chunks(u64 qb, double ratio) {
@@ -469,7 +485,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_reduce_t(const MaxSlots* __rest
                                                         const u64* __restrict__ tilep, int64_t ntiles, int64_t N,
                                                         u64* __restrict__ tileOff, ShardRecord* rec,
                                                         int decide_local, double ess_min, Decision* dec,
-                                                        FillPlan plan, u64* __restrict__ esum) {
+                                                        FillPlan plan, u64* __restrict__ esum, int nms) {
     __shared__ u64 red[kRedPart][kRsBlock];
     __shared__ u64 red2[kRedPart][16];
     __shared__ u64 tot[kRedPart];
@@ -478,8 +494,20 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_reduce_t(const MaxSlots* __rest
     __shared__ int s_heavy[kHeavyQueue][3];
     __shared__ int s_nheavy;
     const int th = threadIdx.x;
+    // exact shards: the single-GPU decision and every rank's slot window first (the plan
+    // below reads them)
+    if (plan.dx_recs) {
+        if (th == 0)
+            decide_exact(plan.dx_recs, plan.dx_world, plan.dx_rank, plan.dx_ess, plan, plan.dx_comb, plan.dx_dec,
+                         plan.dx_xp);
+        __syncthreads();
+    }
     // the max slots are read first so their latency overlaps the partials' loads
-    const u64 mslot = th < kSlots ? ms->v[th][0] : 0ull;
+    u64 mslot = 0;
+    for (int g = 0; g < nms; ++g) {
+        const u64 v = th < kSlots ? ms[g].v[th][0] : 0ull;
+        mslot = v > mslot ? v : mslot;
+    }
     // thread th owns the contiguous tiles [b0, b1): loads each tile's partials once
     const int64_t per = (ntiles + kRsBlock - 1) / kRsBlock;
     const int64_t b0 = (int64_t)th * per < ntiles ? (int64_t)th * per : ntiles;
@@ -592,9 +620,8 @@ __global__ void k_max_adopt(const u64* words, int world, MaxSlots* ms) {
 // Sum the records as integers (every shard's q is relative to the global max with K from
 // the global N, so the sums are exactly the single-GPU ones) and decide once, as one GPU
 // does; then the global CDF offsets and every rank's window of global slots.
-__global__ void k_rs_decide_exact(const ShardRecord* recs, int world, int rank, double ess_min, FillPlan plan,
-                                  ShardRecord* comb, Decision* dec, ExactPlan* xp) {
-    if (threadIdx.x != 0) return;
+__device__ void decide_exact(const ShardRecord* recs, int world, int rank, double ess_min, const FillPlan& plan,
+                             ShardRecord* comb, Decision* dec, ExactPlan* xp) {
     ShardRecord r = recs[0];
     wsmc_u128 Wf2 = 0, Wf = 0;
     u64 Q = 0, Q2 = 0, n = 0;
@@ -626,6 +653,10 @@ __global__ void k_rs_decide_exact(const ShardRecord* recs, int world, int rank, 
     xp->cbase = cb[rank];
     xp->a = xp->seg[rank];
     xp->b = xp->seg[rank + 1];
+}
+__global__ void k_rs_decide_exact(const ShardRecord* recs, int world, int rank, double ess_min, FillPlan plan,
+                                  ShardRecord* comb, Decision* dec, ExactPlan* xp) {
+    if (threadIdx.x == 0) decide_exact(recs, world, rank, ess_min, plan, comb, dec, xp);
 }
 // slot j of the window: its owner keeps its components (written straight into the back
 // buffers if that is this rank, packed into the peer's send block otherwise)
@@ -675,13 +706,14 @@ __device__ __forceinline__ u64 overlap_d(u64 a0, u64 a1, u64 b0, u64 b1) {
 }
 __device__ __forceinline__ void stat_overflow(u64* stat, u64 bit) { atomicOr(stat, bit); }
 
-// the filled window's slots to their owners: this rank's slots get their global ancestor id
-// in place, a neighbour's slots are packed with the ancestor's state into its fixed block
+// the filled window's slots to their owners: the fill wrote this rank's slots straight into
+// its ancestor row (global ids); the slots it wrote into the row's margins belong to a
+// neighbour and are packed, with the ancestor's state, into that neighbour's fixed block
 __global__ __launch_bounds__(kBlock) void k_exact_route(ExactStep e) {
     if (!e.dec->resampled) return;
     const ExactPlan* xp = e.xp;
     const u64 a = xp->a, b = xp->b;
-    const u64 lo = xp->gofs[e.rank], hi = xp->gofs[e.rank + 1];
+    const int64_t lo = (int64_t)xp->gofs[e.rank];
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         // the blocks this step needs: a slot of a rank further than a neighbour, or more
         // than `cap` slots for one neighbour, cannot be moved this way
@@ -696,29 +728,27 @@ __global__ __launch_bounds__(kBlock) void k_exact_route(ExactStep e) {
         if (need > (u64)e.cap) stat_overflow(e.stat, 1ull);
         if (need) atomicMax(e.stat + 1, need);
     }
-    for (u64 j = (u64)blockIdx.x * kBlock + threadIdx.x; j < b - a; j += (u64)gridDim.x * kBlock) {
-        const u64 s = a + j;
-        const int32_t m = e.anc_out[j];
-        const u64 gid = (u64)e.goff + (u64)m;
-        if (s >= lo && s < hi) {
-            e.anc_row[s - lo] = (int32_t)gid;
-            continue;
-        }
-        const int side = s < lo ? 0 : 1;
-        const int nb = side ? e.rank + 1 : e.rank - 1;
-        if (nb < 0 || nb >= e.world || s < xp->gofs[nb] || s >= xp->gofs[nb + 1]) continue;   // flagged above
-        const u64 first = a > xp->gofs[nb] ? a : xp->gofs[nb];
-        const u64 idx = s - first;
-        if (idx >= (u64)e.cap) continue;                                                       // flagged above
-        u64* blk = e.send[side] + idx * kXWords;
-        const d2 x = *reinterpret_cast<const d2*>(e.x + 2 * (int64_t)m);
-        const d2 v = *reinterpret_cast<const d2*>(e.v + 2 * (int64_t)m);
-        const d2 dv = *reinterpret_cast<const d2*>(e.dv + 2 * (int64_t)m);
-        blk[0] = (u64)wsmc_d2bits(x.x); blk[1] = (u64)wsmc_d2bits(x.y);
-        blk[2] = (u64)wsmc_d2bits(v.x); blk[3] = (u64)wsmc_d2bits(v.y);
-        blk[4] = (u64)wsmc_d2bits(dv.x); blk[5] = (u64)wsmc_d2bits(dv.y);
-        blk[6] = gid;
-    }
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= 2 * e.cap) return;
+    const int side = t >= e.cap ? 1 : 0;
+    const int64_t r = side ? e.cap + e.N + (t - e.cap) : t;   // index in the row
+    const int64_t sl = lo - e.cap + r;                          // its global slot
+    if (sl < 0 || (u64)sl < a || (u64)sl >= b) return;
+    const int nb = side ? e.rank + 1 : e.rank - 1;
+    if (nb < 0 || nb >= e.world || (u64)sl < xp->gofs[nb] || (u64)sl >= xp->gofs[nb + 1]) return;   // flagged
+    const u64 first = a > xp->gofs[nb] ? a : xp->gofs[nb];
+    const u64 idx = (u64)sl - first;
+    if (idx >= (u64)e.cap) return;                                                                 // flagged
+    const int32_t gid = e.row[r];
+    const int64_t m = (int64_t)gid - e.goff;
+    u64* blk = e.send[side] + idx * kXWords;
+    const d2 x = *reinterpret_cast<const d2*>(e.x + 2 * m);
+    const d2 v = *reinterpret_cast<const d2*>(e.v + 2 * m);
+    const d2 dv = *reinterpret_cast<const d2*>(e.dv + 2 * m);
+    blk[0] = (u64)wsmc_d2bits(x.x); blk[1] = (u64)wsmc_d2bits(x.y);
+    blk[2] = (u64)wsmc_d2bits(v.x); blk[3] = (u64)wsmc_d2bits(v.y);
+    blk[4] = (u64)wsmc_d2bits(dv.x); blk[5] = (u64)wsmc_d2bits(dv.y);
+    blk[6] = (u64)(uint32_t)gid;
 }
 // the slots of this rank filled by a neighbour: the ancestor's pairs by slot, its global id
 // into the ancestor row (threads [0, cap) the left block, [cap, 2 cap) the right one)
@@ -849,22 +879,23 @@ struct FillLds {
     int32_t out[kRsChunk];                      // the chunk's ancestors, staged for coalesced stores
 };
 
-// write the staged chunk sh.out[0, n) to dst[0, n): 16-B stores on the aligned body,
+// write the staged chunk sh.out[so, so + n) to dst[0, n): 16-B stores on the aligned body,
 // single stores on the ragged ends (dst is 4-B aligned; any slot offset)
-__device__ __forceinline__ void store_chunk(int32_t* __restrict__ dst, int n, const FillLds& sh) {
+__device__ __forceinline__ void store_chunk(int32_t* __restrict__ dst, int n, const FillLds& sh, int so = 0) {
+    const int32_t* src = sh.out + so;
     const int head = (int)((4 - (((uintptr_t)dst >> 2) & 3)) & 3);    // slots before a 16-B boundary
     const int h = head < n ? head : n;
     const int nv = (n - h) >> 2;                                        // whole 16-B vectors
     for (int v = threadIdx.x; v < nv; v += kScanBlock) {
         const int k = h + 4 * v;
         int4 o;
-        o.x = sh.out[k]; o.y = sh.out[k + 1]; o.z = sh.out[k + 2]; o.w = sh.out[k + 3];
+        o.x = src[k]; o.y = src[k + 1]; o.z = src[k + 2]; o.w = src[k + 3];
         *reinterpret_cast<int4*>(dst + k) = o;
     }
     const int tail0 = h + 4 * nv;
     const int th = threadIdx.x;
-    if (th < h) dst[th] = sh.out[th];
-    else if (th >= 4 && th - 4 < n - tail0) dst[tail0 + th - 4] = sh.out[tail0 + th - 4];
+    if (th < h) dst[th] = src[th];
+    else if (th >= 4 && th - 4 < n - tail0) dst[tail0 + th - 4] = src[tail0 + th - 4];
 }
 
 // fill chunk j of tile b (block-uniform arguments; ends with a barrier so LDS can be reused).
@@ -921,8 +952,10 @@ __device__ __forceinline__ void fill_chunk_q(int64_t N, int b, int j, u64 Q, u64
 #pragma unroll
     for (int k = 0; k < IT; ++k) tsum += q[k];
     // exact sharding: targets over the global population, slots written window-relative
-    const uint64_t Nr = plan.xp ? plan.xp->N : (uint64_t)N;
-    const u64 s0 = plan.xp ? plan.xp->a : 0ull;
+    const uint64_t Nr = plan.n_global ? plan.n_global : plan.xp ? plan.xp->N : (uint64_t)N;
+    // exact shards without host round trips: slots land in this rank's ancestor row, which
+    // covers [row_lo, row_hi) (its own range and a margin per neighbour); global ids
+    const u64 s0 = plan.row_hi ? plan.row_lo : plan.xp ? plan.xp->a : 0ull;
     const double ratio = wsmc_u64_to_d(Nr) / wsmc_u64_to_d(Q);
     // the tile's slot range [L, H) = [rank(off), rank(off + Q_b)), ranked by two threads
     // while the others scan; the scan's barrier publishes them
@@ -975,7 +1008,7 @@ __device__ __forceinline__ void fill_chunk_q(int64_t N, int b, int j, u64 Q, u64
     for (int k = 0; k < IT; ++k) {
         const u64 a = lo > cs ? lo : cs;
         const u64 e = hi[k] < ce ? hi[k] : ce;
-        const int32_t m = (int32_t)(base + th * IT + k);
+        const int32_t m = (int32_t)(base + th * IT + k) + plan.id_base;
         if (a < e) {
             const int a0 = (int)(a - cs), e0 = (int)(e - cs);
             if (e0 - a0 > kScatterMax) {
@@ -997,7 +1030,13 @@ __device__ __forceinline__ void fill_chunk_q(int64_t N, int b, int j, u64 Q, u64
         for (int n = sh.heavy[x][1] + lane; n < sh.heavy[x][2]; n += 64) sh.out[n] = m;
     }
     __syncthreads();
-    store_chunk(anc + (cs - s0), (int)(ce - cs), sh);
+    if (plan.row_hi) {   // the part of the chunk the row covers; the rest cannot be routed
+        const u64 w0 = cs > plan.row_lo ? cs : plan.row_lo, w1 = ce < plan.row_hi ? ce : plan.row_hi;
+        if (threadIdx.x == 0 && (w0 != cs || w1 != ce)) atomicOr(plan.xstat, 1ull);
+        if (w1 > w0) store_chunk(anc + (w0 - s0), (int)(w1 - w0), sh, (int)(w0 - cs));
+    } else {
+        store_chunk(anc + (cs - s0), (int)(ce - cs), sh);
+    }
     __syncthreads();
 }
 
@@ -1414,6 +1453,52 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
         if (th == 0 && dec) { dec->resampled = 1; dec->mean = 0.0; dec->ess = 0.0; dec->M = 0.0; }
         return;
     }
+    if (t == ntiles + kOverflowBlocks && plan.xlines) {
+        // ---- exact shards: every rank's record from its all-gathered group lines and max
+        // slots, then the single-GPU decision and the slot windows (decide_exact) ----
+        __shared__ ShardRecord s_recs[kMaxShards];
+        const int W = plan.dx_world;
+        const int ngw = (int)(plan.xstride / kGroupLine);
+        for (int g = 0; g < W; ++g) {
+            const u64* L = plan.xlines + (int64_t)g * plan.xstride;
+            u64 q = 0, q2 = 0, f2lo = 0, f2hi = 0, flo = 0, fhi = 0;
+            for (int k = th; k < ngw; k += kScanBlock) {
+                const u64* l = L + (int64_t)k * kGroupLine;
+                q += l[0]; q2 += l[2];
+                f2lo += l[3] & 0xffffffffull; f2hi += l[3] >> 32;
+                flo += l[4] & 0xffffffffull; fhi += l[4] >> 32;
+            }
+            const u64 mv = th < kSlots ? plan.xms[g].v[th][0] : 0ull;
+            const u64 menc = wave_max_u64(mv);
+            u64 acc[kRedPart] = {q, q2, f2lo, f2hi, flo, fhi};
+#pragma unroll
+            for (int k = 0; k < kRedPart; ++k) acc[k] = wave_sum_u64(acc[k]);
+            if ((th & 63) == 0)
+#pragma unroll
+                for (int k = 0; k < kRedPart; ++k) s_parts[th >> 6][k] = acc[k];
+            __syncthreads();
+            if (th == 0) {
+                u64 tot[kRedPart] = {0, 0, 0, 0, 0, 0};
+                for (int v = 0; v < kScanBlock / 64; ++v)
+                    for (int k = 0; k < kRedPart; ++k) tot[k] += s_parts[v][k];
+                ShardRecord r;
+                r.menc = menc;
+                r.Q = tot[0];
+                r.q2 = tot[1];
+                const wsmc_u128 Wf2 = (wsmc_u128)tot[2] + ((wsmc_u128)tot[3] << 32);
+                const wsmc_u128 Wf = (wsmc_u128)tot[4] + ((wsmc_u128)tot[5] << 32);
+                r.wf2lo = (u64)Wf2; r.wf2hi = (u64)(Wf2 >> 64);
+                r.wflo = (u64)Wf; r.wfhi = (u64)(Wf >> 64);
+                r.n = L[7];
+                s_recs[g] = r;
+                if (g == plan.dx_rank) *rec = r;
+            }
+            __syncthreads();
+        }
+        if (th == 0)
+            decide_exact(s_recs, W, plan.dx_rank, plan.dx_ess, plan, plan.dx_comb, plan.dx_dec, plan.dx_xp);
+        return;
+    }
     if (t == ntiles + kOverflowBlocks) {
         // ---- the shard record and (one GPU, dec != null) the decision; a sharded run
         // all-gathers the records and decides afterwards (k_rs_decide) ----
@@ -1469,10 +1554,20 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
         const u64 qb = plan.tilep[(int64_t)t * kPart];   // every load of the block is issued here
         const int g = t / G;
         u64 pre = 0, tot = 0;
-        for (int k = th; k < ngroups; k += kScanBlock) {
-            const u64 v = grp[(int64_t)k * 8];
-            tot += v;
-            pre += k < g ? v : 0ull;
+        if (plan.xlines) {   // exact shards: the global Q; the lower ranks' Q, then this rank's groups before
+            const int ngw = (int)(plan.xstride / kGroupLine);
+            for (int k = th; k < plan.dx_world * ngw; k += kScanBlock) {
+                const int r = k / ngw, kk = k - r * ngw;
+                const u64 v = plan.xlines[(int64_t)r * plan.xstride + (int64_t)kk * kGroupLine];
+                tot += v;
+                pre += (r < plan.dx_rank || (r == plan.dx_rank && kk < g)) ? v : 0ull;
+            }
+        } else {
+            for (int k = th; k < ngroups; k += kScanBlock) {
+                const u64 v = grp[(int64_t)k * 8];
+                tot += v;
+                pre += k < g ? v : 0ull;
+            }
         }
         for (int b = g * G + th; b < t; b += kScanBlock) pre += plan.tilep[(int64_t)b * kPart];
         block_sum2_u64(pre, tot, s_red);
@@ -1480,16 +1575,26 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
         return;
     }
     // ---- overflow chunks: plan from the tile sums (contiguous tiles per thread) ----
-    u64 Q = 0, qmax = 0;
+    u64 Q = 0, qmax = 0, cbase = 0;
     for (int k = th; k < ngroups; k += kScanBlock) {
         Q += grp[(int64_t)k * kGroupLine];
         const u64 m = grp[(int64_t)k * kGroupLine + 1];
         qmax = m > qmax ? m : qmax;
     }
+    if (plan.xlines) {   // exact shards: the global Q and this rank's CDF base
+        Q = 0;
+        const int ngw = (int)(plan.xstride / kGroupLine);
+        for (int k = th; k < plan.dx_world * ngw; k += kScanBlock) {
+            const int r = k / ngw, kk = k - r * ngw;
+            const u64 v = plan.xlines[(int64_t)r * plan.xstride + (int64_t)kk * kGroupLine];
+            Q += v;
+            cbase += r < plan.dx_rank ? v : 0ull;
+        }
+    }
     qmax = block_max_u64(qmax, sh.uw);
-    u64 dummy = 0;
-    block_sum2_u64(Q, dummy, s_red);
-    const double ratio = Q ? wsmc_u64_to_d((uint64_t)N) / wsmc_u64_to_d(Q) : 0.0;
+    block_sum2_u64(Q, cbase, s_red);
+    const uint64_t Nr = plan.n_global ? plan.n_global : (uint64_t)N;
+    const double ratio = Q ? wsmc_u64_to_d(Nr) / wsmc_u64_to_d(Q) : 0.0;
     if (ovf_chunks(qmax, ratio) == 0) return;   // no tile owns more than its first chunk
 
     const int per = (ntiles + kScanBlock - 1) / kScanBlock;
@@ -1506,7 +1611,7 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
     const u64 npre = block_excl_scan_u64<kScanBlock / 64>(ns, sh.uw, &ntasks);
     for (u64 o = (u64)(t - ntiles); o < ntasks; o += kOverflowBlocks) {
         if (o >= npre && o < npre + ns) {          // exactly one thread owns task o
-            u64 c = qpre, n0 = npre;
+            u64 c = cbase + qpre, n0 = npre;
             for (int b = b0; b < b1; ++b) {
                 const u64 qb = plan.tilep[(int64_t)b * kPart];
                 const u64 k = (u64)ovf_chunks(qb, ratio);
@@ -2318,9 +2423,9 @@ hipError_t launch_rs_max(hipStream_t s, const double* w, int64_t N, MaxSlots* ms
     return hipGetLastError();
 }
 hipError_t launch_rs_sums(hipStream_t s, const double* w, int64_t N, const MaxSlots* ms, u64* tilep, u64* qbuf,
-                          hipEvent_t e0, hipEvent_t e1, u64* grp, int G, int64_t Nk) {
+                          hipEvent_t e0, hipEvent_t e1, u64* grp, int G, int64_t Nk, int nms, int gall) {
     return launch_timed(k_rs_sums_t<0>, rs_tiles_for(N), dim3(kSumBlock), s, e0, e1, w, N, ms, tilep, qbuf, grp, G,
-                        Nk > 0 ? Nk : N);
+                        Nk > 0 ? Nk : N, nms, gall);
 }
 hipError_t launch_rs_fill_fused(hipStream_t s, int64_t N, const FillPlan& plan, const u64* grp, int G,
                                 const MaxSlots* ms, double ess_min, ShardRecord* rec, Decision* dec, const u64* qbuf,
@@ -2339,12 +2444,12 @@ hipError_t launch_rs_fill_fused(hipStream_t s, int64_t N, const FillPlan& plan, 
 }
 hipError_t launch_rs_reduce(hipStream_t s, const MaxSlots* ms, const u64* tilep, int64_t N, u64* tileOff,
                             ShardRecord* rec, int decide_local, double ess_min, Decision* dec,
-                            const FillPlan* plan, hipEvent_t e0, hipEvent_t e1, u64* esum) {
+                            const FillPlan* plan, hipEvent_t e0, hipEvent_t e1, u64* esum, int nms) {
     const int64_t nt = (N + kRsTile - 1) / kRsTile;
     FillPlan p{};
     if (plan) p = *plan;
     return launch_timed(k_rs_reduce_t<0>, dim3(1), dim3(kRsBlock), s, e0, e1, ms, tilep, nt, N, tileOff, rec,
-                        decide_local, ess_min, dec, p, esum);
+                        decide_local, ess_min, dec, p, esum, nms);
 }
 hipError_t launch_rs_decide(hipStream_t s, const ShardRecord* recs, int world, int rank, double ess_min,
                             Decision* dec) {
@@ -2389,10 +2494,7 @@ hipError_t launch_exact_pack(hipStream_t s, const ExactRoute& rt, const int32_t*
     return hipGetLastError();
 }
 hipError_t launch_exact_route(hipStream_t s, const ExactStep& e) {
-    // grid-stride over the window (any size); a window beyond N + 2 cap overflows anyway
-    int64_t nb = (e.N + 2 * e.cap + kBlock - 1) / kBlock;
-    if (nb > 4096) nb = 4096;
-    hipLaunchKernelGGL(k_exact_route, dim3((unsigned)nb), dim3(kBlock), 0, s, e);
+    hipLaunchKernelGGL(k_exact_route, dim3((unsigned)((2 * e.cap + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, e);
     return hipGetLastError();
 }
 hipError_t launch_exact_recv(hipStream_t s, const ExactStep& e) {
@@ -2513,9 +2615,9 @@ hipError_t debug_kernel_bench(hipStream_t s, int kernel, int mode, int iters, co
     for (int it = 0; it < iters; ++it) {
         if (kernel == 0) {
             switch (mode) {
-                case 0: hipLaunchKernelGGL(k_rs_sums_t<0>, g, blk, 0, s, w, N, ms, tilep, qbuf, nullptr, 1, N); break;
-                case 1: hipLaunchKernelGGL(k_rs_sums_t<1>, g, blk, 0, s, w, N, ms, tilep, qbuf, nullptr, 1, N); break;
-                default: hipLaunchKernelGGL(k_rs_sums_t<4>, g, blk, 0, s, w, N, ms, tilep, qbuf, nullptr, 1, N); break;
+                case 0: hipLaunchKernelGGL(k_rs_sums_t<0>, g, blk, 0, s, w, N, ms, tilep, qbuf, nullptr, 1, N, 1, 0); break;
+                case 1: hipLaunchKernelGGL(k_rs_sums_t<1>, g, blk, 0, s, w, N, ms, tilep, qbuf, nullptr, 1, N, 1, 0); break;
+                default: hipLaunchKernelGGL(k_rs_sums_t<4>, g, blk, 0, s, w, N, ms, tilep, qbuf, nullptr, 1, N, 1, 0); break;
             }
         } else if (kernel == 3) {
             // scratch: stream4 = 4 x [2N] doubles (x src, v src, x dst, v dst), wd = w
@@ -2530,10 +2632,10 @@ hipError_t debug_kernel_bench(hipStream_t s, int kernel, int mode, int iters, co
         } else if (kernel == 1) {
             const int64_t nt = (N + kRsTile - 1) / kRsTile;
             switch (mode) {
-                case 0: hipLaunchKernelGGL(k_rs_reduce_t<0>, dim3(1), dim3(kRsBlock), 0, s, ms, tilep, nt, N, tileOff, rec, 1, 2.0, dec, plan, nullptr); break;
-                case 1: hipLaunchKernelGGL(k_rs_reduce_t<1>, dim3(1), dim3(kRsBlock), 0, s, ms, tilep, nt, N, tileOff, rec, 1, 2.0, dec, plan, nullptr); break;
-                case 2: hipLaunchKernelGGL(k_rs_reduce_t<2>, dim3(1), dim3(kRsBlock), 0, s, ms, tilep, nt, N, tileOff, rec, 1, 2.0, dec, plan, nullptr); break;
-                default: hipLaunchKernelGGL(k_rs_reduce_t<3>, dim3(1), dim3(kRsBlock), 0, s, ms, tilep, nt, N, tileOff, rec, 1, 2.0, dec, plan, nullptr); break;
+                case 0: hipLaunchKernelGGL(k_rs_reduce_t<0>, dim3(1), dim3(kRsBlock), 0, s, ms, tilep, nt, N, tileOff, rec, 1, 2.0, dec, plan, nullptr, 1); break;
+                case 1: hipLaunchKernelGGL(k_rs_reduce_t<1>, dim3(1), dim3(kRsBlock), 0, s, ms, tilep, nt, N, tileOff, rec, 1, 2.0, dec, plan, nullptr, 1); break;
+                case 2: hipLaunchKernelGGL(k_rs_reduce_t<2>, dim3(1), dim3(kRsBlock), 0, s, ms, tilep, nt, N, tileOff, rec, 1, 2.0, dec, plan, nullptr, 1); break;
+                default: hipLaunchKernelGGL(k_rs_reduce_t<3>, dim3(1), dim3(kRsBlock), 0, s, ms, tilep, nt, N, tileOff, rec, 1, 2.0, dec, plan, nullptr, 1); break;
             }
         } else {
             switch (mode) {
