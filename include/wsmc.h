@@ -260,9 +260,13 @@ int wsmc_resample(wsmc_ctx* ctx, double ess_perc_min, int32_t scheme,
  *   (pass -1 to use the context's current depth); diversity: NaN = ungated.
  *   *accepted_out (may be NULL) receives the number of accepted proposals. With
  *   accepted_out NULL the Move is asynchronous (no host wait, as the reference's Move
- *   returns nothing): a not-positive-definite autoRW covariance leaves the state untouched
- *   and is reported as WSMC_ENOTPD by the next synchronizing call (wsmc_sync, get_state,
- *   a download, a waited Resample or Move).                                          */
+ *   returns nothing): a not-positive-definite autoRW covariance leaves the Move's targets
+ *   untouched and is reported as WSMC_ENOTPD by the next synchronizing call (wsmc_sync,
+ *   get_state, a download, a waited Resample or Move). Operators enqueued in between have
+ *   run (later asynchronous Moves skip on the same flag): nothing is rolled back, the state
+ *   is the one those statements produce with the failed Moves left out, where the reference
+ *   would have thrown at the failing Move. Callers that need the reference's stop-at-the-
+ *   failure behaviour pass accepted_out.                                                  */
 int wsmc_move(wsmc_ctx* ctx, int32_t proposal, const int32_t* targets, int32_t d, double step,
               const double* lo, const double* hi, int32_t target_depth, double diversity,
               int64_t* accepted_out);

@@ -14,6 +14,8 @@
 #   c5flops <tag>               C5 FP64 work (SQ_INSTS_VALU_*_F64) against its kernel durations
 #   sq <tag> fused|c3|c5        SQ cycle split and instruction mix per kernel
 #   rccl <tag>                  one-rank RCCL bench lines (island, exact)
+#   multirank <tag>             bench.py under torch.distributed.run, 2 ranks on one GPU (host exchange)
+#   fallback <tag>              the sharded run's eager fallback after a failed graph capture
 #   micro <tag> <name>          run tools/micro/<name> (built here from tools/micro/<name>.hip)
 set -o pipefail
 export TMPDIR=/tmp
@@ -112,6 +114,21 @@ rccl)
     timeout -k 10 300 python bench.py --no-cpu-baseline --rccl-one-rank --shard-mode $m "$@" > $O/$m.json 2> $O/$m.err || { tail -30 $O/$m.err; exit 1; }
     line $O/$m.json rccl-one-rank-$m
   done ;;
+multirank)   # bench.py's multi-rank path with 2 ranks on the box's one GPU (host exchange: RCCL
+             # refuses two ranks on one device): weak island, weak exact, strong (ragged) island
+  MR="python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1"
+  A="--gpus 2 --steps 3 --warmup 1 --no-cpu-baseline --exchange host --same-device"
+  timeout -k 10 400 $MR --master-port 29611 bench.py $A --shard-mode island > $O/mr_island.json 2> $O/mr_island.err || { tail -30 $O/mr_island.err; exit 1; }
+  line $O/mr_island.json multirank-island
+  timeout -k 10 400 $MR --master-port 29612 bench.py $A --shard-mode exact > $O/mr_exact.json 2> $O/mr_exact.err || { tail -30 $O/mr_exact.err; exit 1; }
+  line $O/mr_exact.json multirank-exact
+  timeout -k 10 400 $MR --master-port 29613 bench.py $A --global-particles 1000001 > $O/mr_strong.json 2> $O/mr_strong.err || { tail -30 $O/mr_strong.err; exit 1; }
+  line $O/mr_strong.json multirank-strong ;;
+fallback)   # the sharded run's eager fallback after a failed capture (one-rank RCCL)
+  export NCCL_SOCKET_IFNAME=lo
+  WSMC_DIAG_CAPTURE_FAIL=1 timeout -k 10 300 python bench.py --no-cpu-baseline --rccl-one-rank --steps 3 > $O/fb.json 2> $O/fb.err || { tail -30 $O/fb.err; exit 1; }
+  grep -c "running it eagerly" $O/fb.err
+  line $O/fb.json capture-fallback ;;
 micro)   # the binary is built here (hipcc ... -o tools/micro/<name> tools/micro/<name>.hip): the
          # micro sources do not travel (.gpurunignore)
   name=$1
