@@ -707,6 +707,37 @@ WSMC_HD int wsmc_cholesky(const double* a, double* L, int d) {
 }
 
 /*
+ * autoRW's proposal factor from one pass over the particles (src/move_kernels.jl:144-151;
+ * StatsBase's cov(Z, ProbabilityWeights(w)) with corrected = false, i.e. the weighted
+ * covariance Σ w_i (z_i - z̄)(z_i - z̄)ᵀ / Σ w_i). With e_i = exp(w_i - M) and the values taken
+ * relative to a pivot p (one particle's values, so the shift is of the order of the spread
+ * and the subtraction below loses nothing measurable), the canonical totals are
+ *   tot[0] = Σ e_i,  tot[1 + k] = Σ e_i d_ik,  tot[1 + d + v] = Σ (e_i d_ia) d_ib (a <= b),
+ * d_ik = z_ik - p_k, and the covariance is S_ab = tot2_ab / T0 - (tot1_a / T0)(tot1_b / T0)
+ * (shift-invariant). Then zero entries -> min_step, times 2.38/sqrt(d), Cholesky.
+ * S (the scaled covariance) and L are row-major d x d; returns 0 if not positive definite.
+ */
+WSMC_HD int wsmc_autorw_factor(const double* tot, int d, double min_step, double* S, double* L) {
+    const double T0 = tot[0];
+    double m[4];
+    for (int k = 0; k < d; ++k) m[k] = tot[1 + k] / T0;
+    int v = 0;
+    for (int a = 0; a < d; ++a)
+        for (int b = a; b < d; ++b) {
+            const double c = tot[1 + d + v] / T0 - m[a] * m[b];
+            S[a * d + b] = c;
+            S[b * d + a] = c;
+            ++v;
+        }
+    const double lam = 2.38 / wsmc_sqrt((double)d);
+    for (int k = 0; k < d * d; ++k) {
+        if (S[k] == 0.0) S[k] = min_step;          /* Σ[Σ .== 0] .= min_step */
+        S[k] = lam * S[k];
+    }
+    return wsmc_cholesky(S, L, d);
+}
+
+/*
  * Per-shard weight statistics and the global Resample decision
  * (src/transformers.jl:479-489). G = 1 is the single-GPU case; G > 1 combines shard
  * records in rank order (island resampling). Shared by oracle and kernels.

@@ -72,7 +72,9 @@ _SIG = {
     "or_move": (C.c_int, [_P, C.c_int32, _I32P, C.c_int32, C.c_double, _D, _D, C.c_int32,
                           C.c_double, C.POINTER(C.c_int64)]),
     "or_score": (None, [_P, C.c_int32, _D]),
-    "or_moment_totals": (C.c_int, [_P, _I32P, C.c_int32, _D, _D, C.c_int32, C.c_double, _D, _D]),
+    "or_moment_totals": (C.c_int, [_P, _I32P, C.c_int32, _D, _D, C.c_double, _D, _D]),
+    "or_autorw_pivot": (C.c_int, [_P, _I32P, C.c_int32, _D, _D, _D]),
+    "or_autorw_factor": (C.c_int, [_D, C.c_int32, C.c_double, _D]),
     "or_factor": (C.c_int, [_D, C.c_int32, C.c_double, _D]),
     "or_move_factor": (C.c_int, [_P, _I32P, C.c_int32, _D, _D, _D, C.c_int32, C.POINTER(C.c_int64)]),
     "or_skip_move": (None, [_P]),
@@ -367,26 +369,36 @@ class Oracle:
         return int(acc.value) if wait else None
 
     # ---- one shard's part of the sharded autoRW protocol ----
-    def moment_totals(self, targets, pass_: int, M: float, mean=None, lo=None, hi=None) -> np.ndarray:
-        """pass 1: [sum e, sum e z_k]; pass 2: centred products (a <= b); e = exp(w - M)."""
+    def autorw_pivot(self, targets, lo=None, hi=None) -> np.ndarray:
+        """The unconstrained values of this shard's particle 0 (rank 0's: the pivot)."""
         t = np.ascontiguousarray(np.asarray(targets, dtype=np.int32))
         d = len(t)
         lo_a, hi_a = self._bounds(lo, d), self._bounds(hi, d)
-        m = np.ascontiguousarray(np.zeros(d) if mean is None else np.asarray(mean, float).reshape(d))
-        out = np.zeros(1 + d if pass_ == 1 else d * (d + 1) // 2)
+        out = np.zeros(d)
+        self._chk(self._L.or_autorw_pivot(self._h, t.ctypes.data_as(_I32P), d,
+                                          None if lo_a is None else _dptr(lo_a),
+                                          None if hi_a is None else _dptr(hi_a), _dptr(out)))
+        return out
+
+    def moment_totals(self, targets, M: float, pivot, lo=None, hi=None) -> np.ndarray:
+        """[sum e, sum e d_k, sum (e d_a) d_b (a <= b)], e = exp(w - M), d = z - pivot
+        (include/wsmc_math.h wsmc_autorw_factor)."""
+        t = np.ascontiguousarray(np.asarray(targets, dtype=np.int32))
+        d = len(t)
+        lo_a, hi_a = self._bounds(lo, d), self._bounds(hi, d)
+        pv = np.ascontiguousarray(np.asarray(pivot, float).reshape(d))
+        out = np.zeros(1 + d + d * (d + 1) // 2)
         self._chk(self._L.or_moment_totals(self._h, t.ctypes.data_as(_I32P), d,
                                            None if lo_a is None else _dptr(lo_a),
-                                           None if hi_a is None else _dptr(hi_a), int(pass_), float(M),
-                                           _dptr(m), _dptr(out)))
+                                           None if hi_a is None else _dptr(hi_a), float(M), _dptr(pv), _dptr(out)))
         return out
 
     @staticmethod
-    def factor(S, min_step: float):
-        """min_step fill, x 2.38/sqrt(d), lower Cholesky; None if not positive definite."""
-        S = np.ascontiguousarray(np.asarray(S, float))
-        d = S.shape[0]
+    def factor(tot, d: int, min_step: float):
+        """The proposal factor from rank-order combined totals; None if not positive definite."""
+        t = np.ascontiguousarray(np.asarray(tot, float).reshape(-1))
         L = np.zeros(d * d)
-        ok = lib().or_factor(_dptr(S.reshape(-1).copy()), d, float(min_step), _dptr(L))
+        ok = lib().or_autorw_factor(_dptr(t), int(d), float(min_step), _dptr(L))
         return L.reshape(d, d) if ok else None
 
     def move_factor(self, targets, L, lo=None, hi=None, target_depth: int = -1) -> int:

@@ -623,38 +623,58 @@ static int move_apply(oracle* o, const int32_t* targets, int32_t d, int bounded,
                       const double* L, int32_t target_depth, uint64_t op_prop, uint64_t op_acc,
                       int64_t* accepted_out);
 /* ---- one shard's part of a sharded autoRW move (the device ranks' protocol) ----
- * pass 1: out = {sum e, sum e z_k}; pass 2: out = centred products (a <= b), canonical sums
- * over this oracle's particles with e = exp(w - M) for the given global M */
-int or_moment_totals(oracle* o, const int32_t* targets, int32_t d, const double* lo, const double* hi,
-                     int32_t pass, double M, const double* mean, double* out) {
-    int64_t N = o->N;
-    if (d < 1 || d > 4) return WSMC_EARG;
-    double* e = (double*)malloc(sizeof(double) * (size_t)N);
-    double* z = (double*)malloc(sizeof(double) * (size_t)(N * d));
+ * out = this oracle's canonical totals {sum e, sum e d_k, sum (e d_a) d_b (a <= b)} with
+ * e = exp(w - M) for the given global M and d = z - pivot (include/wsmc_math.h
+ * wsmc_autorw_factor); pivot: the unconstrained values of the population's particle 0 */
+static void autorw_totals(oracle* o, int64_t a0, int64_t a1, const double* e, const double* z, int32_t d,
+                          const double* pivot, double* out) {
+    int64_t N = o->N, n = a1 - a0;
     double* v = o->scratch;
+    int nv = 0;
+    out[nv++] = or_canon_sum(e + a0, n);
+    for (int k = 0; k < d; ++k) {
+        for (int64_t i = a0; i < a1; ++i) v[i - a0] = e[i] * (z[(int64_t)k * N + i] - pivot[k]);
+        out[nv++] = or_canon_sum(v, n);
+    }
+    for (int a = 0; a < d; ++a)
+        for (int b = a; b < d; ++b) {
+            for (int64_t i = a0; i < a1; ++i)
+                v[i - a0] = (e[i] * (z[(int64_t)a * N + i] - pivot[a])) * (z[(int64_t)b * N + i] - pivot[b]);
+            out[nv++] = or_canon_sum(v, n);
+        }
+}
+static void autorw_values(oracle* o, const int32_t* targets, int32_t d, const double* lo, const double* hi,
+                          double M, double* e, double* z) {
+    int64_t N = o->N;
     for (int64_t i = 0; i < N; ++i) e[i] = wsmc_exp(o->w[i] - M);
     for (int k = 0; k < d; ++k) {
         const double* x = o->cols[targets[k]].front;
         double l = lo ? lo[k] : -WSMC_INF, h = hi ? hi[k] : WSMC_INF;
         for (int64_t i = 0; i < N; ++i) z[(int64_t)k * N + i] = wsmc_to_unc(x[i], l, h);
     }
-    int nv = 0;
-    if (pass == 1) {
-        out[nv++] = or_canon_sum(e, N);
-        for (int k = 0; k < d; ++k) {
-            for (int64_t i = 0; i < N; ++i) v[i] = e[i] * z[(int64_t)k * N + i];
-            out[nv++] = or_canon_sum(v, N);
-        }
-    } else {
-        for (int a = 0; a < d; ++a)
-            for (int b = a; b < d; ++b) {
-                for (int64_t i = 0; i < N; ++i)
-                    v[i] = (e[i] * (z[(int64_t)a * N + i] - mean[a])) * (z[(int64_t)b * N + i] - mean[b]);
-                out[nv++] = or_canon_sum(v, N);
-            }
-    }
+}
+int or_moment_totals(oracle* o, const int32_t* targets, int32_t d, const double* lo, const double* hi,
+                     double M, const double* pivot, double* out) {
+    int64_t N = o->N;
+    if (d < 1 || d > 4) return WSMC_EARG;
+    double* e = (double*)malloc(sizeof(double) * (size_t)N);
+    double* z = (double*)malloc(sizeof(double) * (size_t)(N * d));
+    autorw_values(o, targets, d, lo, hi, M, e, z);
+    autorw_totals(o, 0, N, e, z, d, pivot, out);
     free(e); free(z);
     return 0;
+}
+/* the unconstrained values of this oracle's particle 0 (rank 0's: the sharded pivot) */
+int or_autorw_pivot(oracle* o, const int32_t* targets, int32_t d, const double* lo, const double* hi, double* out) {
+    if (d < 1 || d > 4 || o->N < 1) return WSMC_EARG;
+    for (int k = 0; k < d; ++k)
+        out[k] = wsmc_to_unc(o->cols[targets[k]].front[0], lo ? lo[k] : -WSMC_INF, hi ? hi[k] : WSMC_INF);
+    return 0;
+}
+/* the factor from rank-order combined totals (the device ranks' k_autorw_combine) */
+int or_autorw_factor(const double* tot, int32_t d, double min_step, double* L) {
+    double S[16];
+    return wsmc_autorw_factor(tot, d, min_step, S, L);
 }
 /* covariance S (d x d, already divided by S0) -> zeros to min_step, x 2.38/sqrt(d), Cholesky */
 int or_factor(const double* S_in, int32_t d, double min_step, double* L) {
@@ -833,55 +853,24 @@ int or_autorw_chol(oracle* o, const int32_t* targets, int32_t d, double min_step
     for (int64_t i = 0; i < N; ++i) if (o->w[i] > M || wsmc_isnan(o->w[i])) M = o->w[i];
     double* e = (double*)malloc(sizeof(double) * (size_t)N);
     double* z = (double*)malloc(sizeof(double) * (size_t)(N * d));
-    double* v = o->scratch;
-    for (int64_t i = 0; i < N; ++i) e[i] = wsmc_exp(o->w[i] - M);
-    for (int k = 0; k < d; ++k) {
-        const double* x = o->cols[targets[k]].front;
-        double l = lo ? lo[k] : -WSMC_INF, h = hi ? hi[k] : WSMC_INF;
-        for (int64_t i = 0; i < N; ++i) z[(int64_t)k * N + i] = wsmc_to_unc(x[i], l, h);
-    }
-    /* canonical sums per shard, combined in rank order (one shard: the plain canonical sum);
-       the device ranks exchange exactly these per-shard totals */
+    autorw_values(o, targets, d, lo, hi, M, e, z);
+    /* one pass relative to the pivot (the population's particle 0), canonical totals per
+       shard combined in rank order (one shard: the plain canonical sums); the device ranks
+       exchange exactly these per-shard totals (include/wsmc_math.h wsmc_autorw_factor) */
+    double pivot[4];
+    for (int k = 0; k < d; ++k) pivot[k] = z[(int64_t)k * N];
     int G = o->nshards;
-    double S0 = 0.0;
+    double tot[15], part[15];
+    const int nv = 1 + d + d * (d + 1) / 2;
     for (int g = 0; g < G; ++g) {
-        int64_t a = o->shard_off[g], b = o->shard_off[g + 1];
-        double t = or_canon_sum(e + a, b - a);
-        S0 = g == 0 ? t : S0 + t;
-    }
-    double mean[4];
-    for (int k = 0; k < d; ++k) {
-        for (int64_t i = 0; i < N; ++i) v[i] = e[i] * z[(int64_t)k * N + i];
-        double t1 = 0.0;
-        for (int g = 0; g < G; ++g) {
-            int64_t a = o->shard_off[g], b = o->shard_off[g + 1];
-            double t = or_canon_sum(v + a, b - a);
-            t1 = g == 0 ? t : t1 + t;
-        }
-        mean[k] = t1 / S0;
+        autorw_totals(o, o->shard_off[g], o->shard_off[g + 1], e, z, d, pivot, part);
+        for (int k = 0; k < nv; ++k) tot[k] = g == 0 ? part[k] : tot[k] + part[k];
     }
     double S[16];
-    for (int a = 0; a < d; ++a)
-        for (int b = a; b < d; ++b) {
-            for (int64_t i = 0; i < N; ++i)
-                v[i] = (e[i] * (z[(int64_t)a * N + i] - mean[a])) * (z[(int64_t)b * N + i] - mean[b]);
-            double t2 = 0.0;
-            for (int g = 0; g < G; ++g) {
-                int64_t lo_ = o->shard_off[g], hi_ = o->shard_off[g + 1];
-                double t = or_canon_sum(v + lo_, hi_ - lo_);
-                t2 = g == 0 ? t : t2 + t;
-            }
-            double c = t2 / S0;
-            S[a * d + b] = c; S[b * d + a] = c;
-        }
-    double lam = 2.38 / wsmc_sqrt((double)d);
-    for (int k = 0; k < d * d; ++k) {
-        if (S[k] == 0.0) S[k] = min_step;          /* Σ[Σ .== 0] .= min_step */
-        S[k] = lam * S[k];
-    }
+    const int ok = wsmc_autorw_factor(tot, d, min_step, S, L);
     if (cov_out) for (int k = 0; k < d * d; ++k) cov_out[k] = S[k];
     free(e); free(z);
-    return wsmc_cholesky(S, L, d);
+    return ok;
 }
 
 static int move_apply(oracle* o, const int32_t* targets, int32_t d, int bounded, const double* l, const double* h,

@@ -108,17 +108,10 @@ class ShardCtx:
             for x in parts[1:]:
                 acc = acc + x
             return acc
-        t1 = rank_order_sum(self._allgather_f64(self.o.moment_totals(targets, 1, M, lo=lo, hi=hi)))
-        S0 = t1[0]
-        mean = t1[1:] / S0
-        t2 = rank_order_sum(self._allgather_f64(self.o.moment_totals(targets, 2, M, mean, lo=lo, hi=hi)))
-        S = np.zeros((d, d))
-        v = 0
-        for a in range(d):
-            for b in range(a, d):
-                S[a, b] = S[b, a] = t2[v] / S0
-                v += 1
-        L = self.o.factor(S, step)
+        # the pivot: rank 0's particle 0 (all-gathered with the max on the device)
+        pivot = self._allgather_f64(self.o.autorw_pivot(targets, lo, hi))[0]
+        tot = rank_order_sum(self._allgather_f64(self.o.moment_totals(targets, M, pivot, lo=lo, hi=hi)))
+        L = self.o.factor(tot, d, step)
         if L is None:
             self.o.skip_move()
             raise np.linalg.LinAlgError("proposal covariance not positive definite")

@@ -2180,21 +2180,23 @@ static int sharded_autorw(wsmc_ctx* c, const int32_t* targets, int d, const doub
     constexpr int kStride = 16;   // u64 words per rank in c->xchg
     WSMC_HIP(hipMemsetAsync(c->mslots, 0, sizeof(MaxSlots), c->stream));
     WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, c->mslots));
-    WSMC_HIP(launch_max_publish(c->stream, c->mslots, c->xchg + (size_t)c->rank * kStride));
+    // each rank's max word and its particle 0's unconstrained values; rank 0's are the pivot
+    WSMC_HIP(launch_autorw_publish(c->stream, c->mslots, c->d_colptr, targets, d, lo, hi,
+                                   c->xchg + (size_t)c->rank * kStride));
     int r = exchange_words(c, c->xchg, kStride, c->stream);
     if (r) return r;
     // the ranks' maxima sit kStride words apart: gather them into the first W words
     WSMC_HIP(launch_autorw_max(c->stream, c->xchg, W, kStride, c->mslots));
-    for (int pass = 1; pass <= 2; ++pass) {
-        const int nv = pass == 1 ? 1 + d : d * (d + 1) / 2;
-        WSMC_HIP(launch_moments(c->stream, c->w, c->mslots, c->d_colptr, targets, d, lo, hi, pass, c->mom, c->N,
-                                c->tilepart));
-        WSMC_HIP(launch_moments_final(c->stream, c->tilepart, c->ntiles, d, pass, min_step, c->mom, c->dflag, 2));
-        WSMC_HIP(hipMemcpyAsync(c->xchg + (size_t)c->rank * kStride, c->mom + 48, sizeof(double) * nv,
-                                hipMemcpyDeviceToDevice, c->stream));
-        if ((r = exchange_words(c, c->xchg, kStride, c->stream))) return r;
-        WSMC_HIP(launch_autorw_combine(c->stream, c->xchg, W, kStride, d, pass, min_step, c->mom, c->dflag));
-    }
+    // one pass: this rank's canonical totals relative to the pivot, all-gathered, combined in
+    // rank order (include/wsmc_math.h wsmc_autorw_factor)
+    const int nv = 1 + d + d * (d + 1) / 2;
+    WSMC_HIP(launch_autorw_moments(c->stream, c->w, c->mslots, c->d_colptr, targets, d, lo, hi, c->xchg + 1, c->N,
+                                   c->tilepart));
+    WSMC_HIP(launch_autorw_final(c->stream, c->tilepart, c->ntiles, d, min_step, c->mom, c->dflag, 1));
+    WSMC_HIP(hipMemcpyAsync(c->xchg + (size_t)c->rank * kStride, c->mom + 48, sizeof(double) * nv,
+                            hipMemcpyDeviceToDevice, c->stream));
+    if ((r = exchange_words(c, c->xchg, kStride, c->stream))) return r;
+    WSMC_HIP(launch_autorw_combine1(c->stream, c->xchg, W, kStride, d, min_step, c->mom, c->dflag));
     return WSMC_OK;
 }
 
@@ -2311,13 +2313,13 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         }
         const double* lp = bounded ? l : nullptr;
         const double* hp = bounded ? h : nullptr;
-        // (a last-block combine inside k_moments, an arrival counter behind a device-scope
-        // fence per block, measured 2x slower than the separate combine launch: 113.6 vs
-        // 57.7 + 13.5 us at 4M — every block's fence writes back its L2)
-        WSMC_HIP(launch_moments(c->stream, c->w, mms, c->d_colptr, targets, d, lp, hp, 1, c->mom, c->N, c->tilepart));
-        WSMC_HIP(launch_moments_final(c->stream, c->tilepart, c->ntiles, d, 1, step, c->mom, c->dflag));
-        WSMC_HIP(launch_moments(c->stream, c->w, mms, c->d_colptr, targets, d, lp, hp, 2, c->mom, c->N, c->tilepart));
-        WSMC_HIP(launch_moments_final(c->stream, c->tilepart, c->ntiles, d, 2, step, c->mom, c->dflag));
+        // one pass relative to the pivot (particle 0), then the one-block combine and factor
+        // (a last-block combine inside the moments kernel, an arrival counter behind a
+        // device-scope fence per block, measured 2x slower than the separate combine launch:
+        // 113.6 vs 57.7 + 13.5 us at 4M — every block's fence writes back its L2)
+        WSMC_HIP(launch_autorw_moments(c->stream, c->w, mms, c->d_colptr, targets, d, lp, hp, nullptr, c->N,
+                                       c->tilepart));
+        WSMC_HIP(launch_autorw_final(c->stream, c->tilepart, c->ntiles, d, step, c->mom, c->dflag, 0));
     } else {
         WSMC_HIP(hipStreamSynchronize(c->stream));
         double* L = reinterpret_cast<double*>(c->pinned);

@@ -423,6 +423,17 @@ hipError_t launch_autorw_max(hipStream_t s, const unsigned long long* words, int
 hipError_t launch_autorw_combine(hipStream_t s, const unsigned long long* xchg, int world, int stride, int d,
                                  int pass, double min_step, double* mom, int32_t* flag);
 hipError_t launch_max_publish(hipStream_t s, const MaxSlots* ms, unsigned long long* word);
+// autoRW in one pass (include/wsmc_math.h wsmc_autorw_factor): pivoted canonical tile partials,
+// their one-block combine and factor; sharded: publish (max word, pivot), rank-order combine
+hipError_t launch_autorw_moments(hipStream_t s, const double* w, const MaxSlots* ms, double* const* cols,
+                                 const int32_t* tcols, int d, const double* lo, const double* hi,
+                                 const unsigned long long* pv, int64_t N, double* tilepart);
+hipError_t launch_autorw_final(hipStream_t s, const double* tilepart, int64_t ntiles, int d, double min_step,
+                               double* mom, int32_t* flag, int raw);
+hipError_t launch_autorw_publish(hipStream_t s, const MaxSlots* ms, double* const* cols, const int32_t* tcols, int d,
+                                 const double* lo, const double* hi, unsigned long long* out);
+hipError_t launch_autorw_combine1(hipStream_t s, const unsigned long long* xchg, int world, int stride, int d,
+                                  double min_step, double* mom, int32_t* flag);
 // exact sharding: records summed as integers (the single-GPU decision bits), slot windows
 hipError_t launch_rs_decide_exact(hipStream_t s, const ShardRecord* recs, int world, int rank, double ess_min,
                                   const FillPlan& plan, ShardRecord* comb, Decision* dec, ExactPlan* xp);

@@ -1842,6 +1842,121 @@ __global__ __launch_bounds__(kBlock) void k_moments_final(const double* tilepart
     moments_final_block(tilepart, ntiles, d, pass, min_step, mom, flag, raw, lds4, tot);
 }
 
+// ---- autoRW in one pass (include/wsmc_math.h wsmc_autorw_factor) ------------------------
+// the pivot: the unconstrained values of the population's particle 0 (a sharded run passes
+// rank 0's, all-gathered, as the bits of doubles in pv; nullptr: this context's particle 0)
+template <int D>
+__device__ __forceinline__ void autorw_pivot(double* const* cols, const MomArgs& ma, const u64* pv, double (&p)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) p[k] = 0.0;
+#pragma unroll
+    for (int k = 0; k < D; ++k)
+        p[k] = pv ? wsmc_bits2d(pv[k]) : wsmc_to_unc(cols[ma.tcol[k]][0], ma.lo[k], ma.hi[k]);
+}
+// the canonical tile partials tilepart[v * ntiles + tile] of {e, e d_k, (e d_a) d_b (a <= b)}
+// with e = exp(w - M), d = z - pivot: the same per-thread order, butterfly and tile order as
+// k_moments, one pass
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_moments1(const double* __restrict__ w, const MaxSlots* ms,
+                                                     double* const* cols, MomArgs ma, const u64* pv, int64_t N,
+                                                     int64_t ntiles, double* tilepart) {
+    constexpr int d = D, NV = 1 + D + D * (D + 1) / 2;
+    __shared__ double lds4[4];
+    const double M = wave_slots_max(ms);
+    double p[4];
+    autorw_pivot<D>(cols, ma, pv, p);
+    const int64_t base = (int64_t)blockIdx.x * kTile;
+    double acc[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) acc[v] = 0.0;
+    for (int j = 0; j < kItems; ++j) {
+        const int64_t i = base + (int64_t)j * kBlock + threadIdx.x;
+        double vals[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) vals[v] = 0.0;
+        if (i < N) {
+            const double e = wsmc_exp(w[i] - M);
+            double dz[4];
+#pragma unroll
+            for (int k = 0; k < d; ++k) dz[k] = wsmc_to_unc(cols[ma.tcol[k]][i], ma.lo[k], ma.hi[k]) - p[k];
+            vals[0] = e;
+#pragma unroll
+            for (int k = 0; k < d; ++k) vals[1 + k] = e * dz[k];
+            int v = 1 + d;
+#pragma unroll
+            for (int a = 0; a < d; ++a)
+#pragma unroll
+                for (int b = a; b < d; ++b) vals[v++] = (e * dz[a]) * dz[b];
+        }
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[v] = acc[v] + vals[v];
+    }
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const double s = block_sum_canon(acc[v], lds4);
+        if (threadIdx.x == 0) tilepart[(int64_t)v * ntiles + blockIdx.x] = s;
+    }
+}
+// one block: the canonical combine of the tile partials (k_moments_final's order); raw: the
+// totals to mom[48..] (a sharded run all-gathers them), else the factor: mom[16..] the scaled
+// covariance, mom[32..] its Cholesky factor, flag[0] = 1 if not positive definite
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_autorw_final(const double* tilepart, int64_t ntiles, double min_step,
+                                                         double* mom, int32_t* flag, int raw) {
+    constexpr int NV = 1 + D + D * (D + 1) / 2;
+    __shared__ double lds4[4];
+    __shared__ double tot[NV];
+    for (int v = 0; v < NV; ++v) {
+        double acc = 0.0;
+        for (int64_t b = threadIdx.x; b < ntiles; b += kBlock) acc = acc + tilepart[(int64_t)v * ntiles + b];
+        const double s = block_sum_canon(acc, lds4);
+        if (threadIdx.x == 0) tot[v] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    if (raw) {
+        for (int v = 0; v < NV; ++v) mom[48 + v] = tot[v];
+        return;
+    }
+    double S[16], L[16];
+    const int ok = wsmc_autorw_factor(tot, D, min_step, S, L);
+    for (int k = 0; k < D * D; ++k) {
+        mom[16 + k] = S[k];
+        mom[32 + k] = L[k];
+    }
+    if (!ok) flag[0] = 1;
+}
+// sharded: this rank's max word and its particle 0's unconstrained values (rank 0's are the
+// pivot), 1 + d words
+template <int D>
+__global__ void k_autorw_publish(const MaxSlots* ms, double* const* cols, MomArgs ma, u64* out) {
+    const u64 m = wave_max_u64(ms->v[threadIdx.x & 63][0]);
+    if (threadIdx.x != 0) return;
+    out[0] = m;
+    double p[4];
+    autorw_pivot<D>(cols, ma, nullptr, p);
+    for (int k = 0; k < D; ++k) out[1 + k] = wsmc_d2bits(p[k]);
+}
+// sharded: the ranks' totals summed in rank order, then the factor (k_autorw_final's arithmetic)
+__global__ void k_autorw_combine1(const u64* __restrict__ xchg, int world, int stride, int d, double min_step,
+                                  double* mom, int32_t* flag) {
+    if (threadIdx.x != 0) return;
+    const int nv = 1 + d + d * (d + 1) / 2;
+    double tot[15];
+    for (int v = 0; v < nv; ++v) {
+        double acc = 0.0;
+        for (int g = 0; g < world; ++g) {
+            const double x = __builtin_bit_cast(double, xchg[(int64_t)g * stride + v]);
+            acc = g == 0 ? x : acc + x;
+        }
+        tot[v] = acc;
+    }
+    double S[16], L[16];
+    const int ok = wsmc_autorw_factor(tot, d, min_step, S, L);
+    for (int k = 0; k < 16; ++k) mom[32 + k] = k < d * d ? L[k] : 0.0;
+    if (!ok) flag[0] = 1;
+}
+
 // Move (src/transformers.jl:588-623). scache carries each particle's score from its last
 // move (the fold is a left-to-right sum, so continuing it over the terms appended since
 // [cache_from, nterms) gives the same bits as refolding); cache_from < 0 = refold.
@@ -2774,6 +2889,55 @@ __global__ __launch_bounds__(kBlock) void k_minmax(const double* __restrict__ x,
 }
 hipError_t launch_minmax(hipStream_t s, const double* x, int64_t N, MaxSlots* ms) {
     hipLaunchKernelGGL(k_minmax, grid_for(N), dim3(kBlock), 0, s, x, N, ms);
+    return hipGetLastError();
+}
+static MomArgs mom_args(const int32_t* tcols, int d, const double* lo, const double* hi) {
+    MomArgs ma;
+    for (int k = 0; k < 4; ++k) {
+        ma.tcol[k] = k < d ? tcols[k] : 0;
+        ma.lo[k] = (k < d && lo) ? lo[k] : -WSMC_INF;
+        ma.hi[k] = (k < d && hi) ? hi[k] : WSMC_INF;
+    }
+    ma.use_ex = 0;
+    return ma;
+}
+hipError_t launch_autorw_moments(hipStream_t s, const double* w, const MaxSlots* ms, double* const* cols,
+                                 const int32_t* tcols, int d, const double* lo, const double* hi, const u64* pv,
+                                 int64_t N, double* tilepart) {
+    const MomArgs ma = mom_args(tcols, d, lo, hi);
+    const int64_t nt = (N + kTile - 1) / kTile;
+    switch (d) {
+        case 1: hipLaunchKernelGGL(k_moments1<1>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart); break;
+        case 2: hipLaunchKernelGGL(k_moments1<2>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart); break;
+        case 3: hipLaunchKernelGGL(k_moments1<3>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart); break;
+        default: hipLaunchKernelGGL(k_moments1<4>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart); break;
+    }
+    return hipGetLastError();
+}
+hipError_t launch_autorw_final(hipStream_t s, const double* tilepart, int64_t ntiles, int d, double min_step,
+                               double* mom, int32_t* flag, int raw) {
+    switch (d) {
+        case 1: hipLaunchKernelGGL(k_autorw_final<1>, dim3(1), dim3(kBlock), 0, s, tilepart, ntiles, min_step, mom, flag, raw); break;
+        case 2: hipLaunchKernelGGL(k_autorw_final<2>, dim3(1), dim3(kBlock), 0, s, tilepart, ntiles, min_step, mom, flag, raw); break;
+        case 3: hipLaunchKernelGGL(k_autorw_final<3>, dim3(1), dim3(kBlock), 0, s, tilepart, ntiles, min_step, mom, flag, raw); break;
+        default: hipLaunchKernelGGL(k_autorw_final<4>, dim3(1), dim3(kBlock), 0, s, tilepart, ntiles, min_step, mom, flag, raw); break;
+    }
+    return hipGetLastError();
+}
+hipError_t launch_autorw_publish(hipStream_t s, const MaxSlots* ms, double* const* cols, const int32_t* tcols, int d,
+                                 const double* lo, const double* hi, u64* out) {
+    const MomArgs ma = mom_args(tcols, d, lo, hi);
+    switch (d) {
+        case 1: hipLaunchKernelGGL(k_autorw_publish<1>, dim3(1), dim3(64), 0, s, ms, cols, ma, out); break;
+        case 2: hipLaunchKernelGGL(k_autorw_publish<2>, dim3(1), dim3(64), 0, s, ms, cols, ma, out); break;
+        case 3: hipLaunchKernelGGL(k_autorw_publish<3>, dim3(1), dim3(64), 0, s, ms, cols, ma, out); break;
+        default: hipLaunchKernelGGL(k_autorw_publish<4>, dim3(1), dim3(64), 0, s, ms, cols, ma, out); break;
+    }
+    return hipGetLastError();
+}
+hipError_t launch_autorw_combine1(hipStream_t s, const u64* xchg, int world, int stride, int d, double min_step,
+                                  double* mom, int32_t* flag) {
+    hipLaunchKernelGGL(k_autorw_combine1, dim3(1), dim3(64), 0, s, xchg, world, stride, d, min_step, mom, flag);
     return hipGetLastError();
 }
 hipError_t launch_moments_final(hipStream_t s, const double* tilepart, int64_t ntiles, int d, int pass,
