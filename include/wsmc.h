@@ -270,6 +270,15 @@ int wsmc_resample(wsmc_ctx* ctx, double ess_perc_min, int32_t scheme,
 int wsmc_move(wsmc_ctx* ctx, int32_t proposal, const int32_t* targets, int32_t d, double step,
               const double* lo, const double* hi, int32_t target_depth, double diversity,
               int64_t* accepted_out);
+/* Move.apply! inside `if resampled ... end` (the Cond of src/rewrites.jl:360-368;
+ * examples/linear_regression.jl:23-24, examples/damped_oscillator.jl:38-41) with the condition
+ * decided on the device: the Move runs only if the last Resample resampled, and the host never
+ * reads the flag (an asynchronous Resample followed by gated Moves keeps the whole step on the
+ * stream). Asynchronous like wsmc_move with accepted_out NULL. A gated Move consumes its two
+ * op counters whether or not it runs, so its streams do not depend on the decision. With a
+ * diversity gate or on shards the decision is read on the host first.                       */
+int wsmc_move_gated(wsmc_ctx* ctx, int32_t proposal, const int32_t* targets, int32_t d, double step,
+                    const double* lo, const double* hi, int32_t target_depth, double diversity);
 /* score_logpdf!(scores, state, targets, target_depth) (src/types.jl:198-206) -> host */
 int wsmc_score(wsmc_ctx* ctx, int32_t target_depth, double* host_scores);
 /* marginal_diversity(store, targets)  (src/transformers.jl:560-565) */

@@ -12,6 +12,7 @@ both and compared bit for bit.
 from __future__ import annotations
 
 import ctypes as C
+import math
 import os
 import pathlib
 import subprocess
@@ -352,6 +353,15 @@ class Oracle:
         e = C.c_double()
         self._chk(self._L.or_resample(self._h, float(ess_perc_min), int(scheme), C.byref(r), C.byref(e)))
         return (bool(r.value), float(e.value)) if wait else None
+
+    def move_gated(self, proposal: int, targets, step: float, lo=None, hi=None, target_depth: int = -1,
+                   diversity: float = math.nan) -> None:
+        """wsmc_move_gated: the Move runs only if the last Resample resampled; its two op
+        counters are consumed either way."""
+        if not self.get_state()["resampled"]:
+            self.set_op_counter(self.get_state()["op_counter"] + 2)
+            return
+        self.move(proposal, targets, step, lo, hi, target_depth, diversity=diversity, wait=False)
 
     def move(self, proposal: int, targets, step: float, lo=None, hi=None, target_depth: int = -1,
              diversity: float = float("nan"), wait: bool = True):

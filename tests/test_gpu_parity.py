@@ -499,3 +499,22 @@ def test_deferred_weight_reset_readers(gpu_available, reader):
     else:
         assert og == oo
     assert_same_state(g, o)
+
+
+@pytest.mark.parametrize("ess", [1.0, 0.5, 0.3])
+def test_gated_moves_match_oracle(gpu_available, ess):
+    """`if resampled; α << autoRW(); β << autoRW(); end` lowered to device-gated Moves
+    (wsmc_move_gated, examples/linear_regression.jl:22-25): asynchronous Resamples, the Moves
+    decided on the device, nothing read on the host inside the loop. At 0.3 some steps do not
+    resample: their Moves only carry the scores on and consume their op counters, as the
+    oracle's gated Move does."""
+    xs, ys = models.linreg_data()
+    g, o = wsmc.Context(4099, seed=8), Oracle(4099, seed=8)
+    assert models.linreg_statements(g, xs, ys, ess_perc_min=ess, gated=True) is None
+    models.linreg_statements(o, xs, ys, ess_perc_min=ess, gated=True)
+    sg, so = g.get_state(), o.get_state()
+    assert sg["n_resamples"] == so["n_resamples"] and sg["op_counter"] == so["op_counter"]
+    if ess == 0.3:
+        assert so["n_resamples"] < len(xs) + 2   # some gated Moves were skipped
+    assert_same_state(g, o)
+    assert g.log_evidence() == o.log_evidence()

@@ -24,14 +24,14 @@ def _ctx(N, one_rank):
     return ctx
 
 
-def c3(N=1_000_000, reps=3, wait_moves=True, one_rank=False):
+def c3(N=1_000_000, reps=3, wait_moves=True, one_rank=False, gated=False):
     xs, ys = models.linreg_data()
     best = math.inf
     for _ in range(reps + 1):
         ctx = _ctx(N, one_rank)
         ctx.sync()
         t0 = time.perf_counter()
-        acc = models.linreg_statements(ctx, xs, ys, ess_perc_min=1.0, wait_moves=wait_moves)
+        acc = models.linreg_statements(ctx, xs, ys, ess_perc_min=1.0, wait_moves=wait_moves, gated=gated)
         ctx.sync()
         dt = time.perf_counter() - t0
         ev = ctx.log_evidence()
@@ -39,13 +39,15 @@ def c3(N=1_000_000, reps=3, wait_moves=True, one_rank=False):
         best = min(best, dt)
     T = len(xs)
     return {"config": "C3 linear regression + autoRW (N=1M, T=10, ess 1.0)"
-                      + ("" if wait_moves else ", asynchronous moves (no accepted counts)")
+                      + ("" if wait_moves or gated else ", asynchronous moves (no accepted counts)")
+                      + (", `if resampled` lowered to device-gated moves (no host read in the loop)" if gated else "")
                       + (", sharded path (one-rank RCCL communicator)" if one_rank else ""), "N": N, "T": T,
-            "seconds_per_run": best, "particle_steps_per_s": N * T / best, "moves": 2 * len(acc),
+            "seconds_per_run": best, "particle_steps_per_s": N * T / best, "moves": 2 * T if gated else 2 * len(acc),
             "log_evidence": ev}
 
 
-def c5(N=4_000_000, T=60, sweeps=5, reps=1, scheme="systematic", ess=1.0, diversity=None, one_rank=False):
+def c5(N=4_000_000, T=60, sweeps=5, reps=1, scheme="systematic", ess=1.0, diversity=None, one_rank=False,
+       wait_moves=True):
     t_obs, y_obs = models.oscillator_data(n=T)
     sch = {"systematic": wsmc.RESAMPLE_SYSTEMATIC, "stratified": wsmc.RESAMPLE_STRATIFIED}[scheme]
     best, moved = math.inf, 0
@@ -54,14 +56,15 @@ def c5(N=4_000_000, T=60, sweeps=5, reps=1, scheme="systematic", ess=1.0, divers
         ctx.sync()
         t0 = time.perf_counter()
         acc = models.oscillator_statements(ctx, t_obs, y_obs, ess_perc_min=ess, scheme=sch, sweeps=sweeps,
-                                           diversity=diversity)
+                                           diversity=diversity, wait_moves=wait_moves)
         ctx.sync()
         dt = time.perf_counter() - t0
         ctx.close()
         best = min(best, dt)
-        moved = sum(x for a in acc for x in a)   # accepted proposals (a skipped gated move: 0)
+        moved = sum(x for a in acc for x in a) if wait_moves else None   # accepted proposals
     gate = "ungated" if diversity is None else f"diversity={diversity}"
     out = {"config": f"C5 damped oscillator, {scheme}, {sweeps} {gate} sweep(s) (N={N}, T={T}, ess {ess})"
+                     + ("" if wait_moves else ", asynchronous moves (no accepted counts)")
                      + (", sharded path (one-rank RCCL communicator)" if one_rank else ""),
            "N": N, "T": T, "seconds_per_run": best, "particle_steps_per_s": N * T / best,
            "accepted": moved, "moves_offered": 2 * sweeps * T}
@@ -80,6 +83,8 @@ LEGS = {
     "c5_stratified": lambda: c5(scheme="stratified"),                     # the reference's scheme
     "c5_example": lambda: c5(sweeps=1, scheme="stratified", ess=0.5, diversity=0.9),   # as written
     "c3async": lambda: c3(wait_moves=False),
+    "c3gated": lambda: c3(gated=True),
+    "c5async": lambda: c5(wait_moves=False),
     "c3_rccl1": lambda: c3(one_rank=True),
     "c3async_rccl1": lambda: c3(wait_moves=False, one_rank=True),
     "c5_rccl1": lambda: c5(one_rank=True),

@@ -126,9 +126,16 @@ static bool tape_reads(const wsmc_ctx* c, int32_t col) {
     }
     return false;
 }
+// the carried Move scores are no longer valid (they are refolded by the next Move)
+static void scores_invalidate(wsmc_ctx* c) {
+    c->scache_terms = -1;
+    c->scache_anc = nullptr;
+    c->scache_dec = nullptr;
+    c->scache_lag_epoch = -1;
+}
 // a write to a column the tape reads changes past terms' values: the carried scores are stale
 static void scores_touch(wsmc_ctx* c, int32_t col) {
-    if (c->scache_terms >= 0 && tape_reads(c, col)) c->scache_terms = -1;
+    if (c->scache_terms >= 0 && tape_reads(c, col)) scores_invalidate(c);
 }
 
 // ColumnStore.resample! (src/stores.jl:105-128) of the given columns (and the carried Move
@@ -173,6 +180,18 @@ static int gather_columns(wsmc_ctx* c, const std::vector<int32_t>& which, const 
     return WSMC_OK;
 }
 
+// the carried scores' deferred gather, now (k_resample_apply through the lagged entry)
+static int resolve_scache_lag(wsmc_ctx* c) {
+    if (!c->scache_anc) return WSMC_OK;
+    const int32_t* anc = c->scache_anc;
+    const Decision* dec = c->scache_dec;
+    c->scache_anc = nullptr;
+    c->scache_dec = nullptr;
+    c->scache_lag_epoch = -1;
+    if (c->scache && c->scache_terms >= 0) return gather_columns(c, {}, anc, dec, nullptr, c->epoch);
+    return WSMC_OK;
+}
+
 // ---- lazy genealogy (AncRow, wsmc_internal.h) ---------------------------------------------
 static inline size_t row_anc_bytes(int64_t N) { return (sizeof(int32_t) * (size_t)N + 255) & ~(size_t)255; }
 static int acquire_row(wsmc_ctx* c, AncRow* out) {
@@ -193,6 +212,7 @@ static void gc_log(wsmc_ctx* c) {
     int64_t keep = c->epoch;
     for (const auto& col : c->cols) keep = std::min(keep, col.epoch);
     if (c->anc_last_epoch >= 0) keep = std::min(keep, c->anc_last_epoch);
+    if (c->scache_lag_epoch >= 0) keep = std::min(keep, c->scache_lag_epoch);
     for (const auto& p : c->dec_rows)
         if (p.epoch >= 0) keep = std::min(keep, p.epoch);
     while (c->log_base < keep && !c->alog.empty()) {
@@ -286,7 +306,10 @@ static int materialize(wsmc_ctx* c, const std::vector<int32_t>* only) {
     gc_log(c);
     return WSMC_OK;
 }
-static int materialize_all(wsmc_ctx* c) { return materialize(c, nullptr); }
+static int materialize_all(wsmc_ctx* c) {
+    if (int r = resolve_scache_lag(c)) return r;
+    return materialize(c, nullptr);
+}
 // an operator reads these columns: bring the stale ones among them up to date first (one
 // walk of the log for all of them); history the operator does not read stays behind
 static int need_cols(wsmc_ctx* c, const std::vector<int32_t>& ids) {
@@ -327,8 +350,17 @@ static int store_resample_row(wsmc_ctx* c, const AncRow& row, const Decision* de
     }
     c->alog.push_back(row);
     c->epoch += 1;
-    if (w_reset || (c->scache && c->scache_terms >= 0))
+    if (w_reset) {
+        if (int r = resolve_scache_lag(c)) return r;
         if (int r = gather_columns(c, which, row.anc, dec, w_reset, c->epoch)) return r;
+    } else if (c->scache && c->scache_terms >= 0) {
+        // the carried Move scores follow their particles at the next Move, which reads them
+        // through this entry's ancestors (no gather launch now); one entry at most
+        if (int r = resolve_scache_lag(c)) return r;
+        c->scache_anc = row.anc;
+        c->scache_dec = dec ? dec : c->dec_always;
+        c->scache_lag_epoch = c->epoch - 1;
+    }
     gc_log(c);
     return WSMC_OK;
 }
@@ -503,10 +535,12 @@ static int check_deferred(wsmc_ctx* c) {
     WSMC_HIP(hipStreamSynchronize(c->stream));
     c->move_pending = false;
     if (hf[0]) {
-        c->scache_terms = -1;
+        scores_invalidate(c);
         WSMC_HIP(hipMemsetAsync(c->dflag, 0, sizeof(int32_t) * 4, c->stream));
+        c->dflag_zero = true;
         return fail(WSMC_ENOTPD, "autoRW proposal covariance is not positive definite (an asynchronous Move)");
     }
+    c->dflag_zero = true;   // read back as zero: the next Move needs no reset
     return WSMC_OK;
 }
 
@@ -543,7 +577,7 @@ int wsmc_set_depth(wsmc_ctx* c, int32_t depth) {
     if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { return wsmc_set_depth(x, depth); });
     if (!c) return fail(WSMC_EARG, "null context");
     c->depth = depth;
-    c->scache_terms = -1;
+    scores_invalidate(c);
     return WSMC_OK;
 }
 
@@ -2264,7 +2298,9 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
               const double* hi, int32_t target_depth, double diversity, int64_t* accepted_out) {
     if (c && c->multi)
         return multi_move(c, proposal, targets, d, step, lo, hi, target_depth, diversity, accepted_out);
-    CHECK_CTX(c);
+    // the weights are read by the autoRW moments only, which apply a pending fused-Resample
+    // reset themselves (the next Observe applies it to the weights); sharded: settled below
+    CHECK_CTX_KEEP(c);
     const uint64_t op_prop = c->op++, op_acc = c->op++;
     if (accepted_out) *accepted_out = 0;
     if (!targets || d < 1 || d > 4) return fail(WSMC_EARG, "move needs 1..4 targets");
@@ -2279,6 +2315,11 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         if (div >= diversity) return WSMC_OK;
     }
     if (target_depth < 0) target_depth = c->depth;
+    // a gated Move (wsmc_move_gated) decided on the device; a diversity gate or shards read
+    // the decision on the host first (the Move then runs or not as an ordinary one)
+    const Decision* gate = c->move_gate;
+    c->move_gate = nullptr;
+    if (gate && (is_sharded(c) || proposal != WSMC_PROPOSAL_AUTORW && proposal != WSMC_PROPOSAL_RW)) gate = nullptr;
     double l[4], h[4];
     bool bounded = false;
     for (int k = 0; k < d; ++k) {
@@ -2297,9 +2338,15 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
     // kernels skip on it) until the next synchronizing call reports it
     const bool async = !accepted_out;   // sharded too: the factor and its PD flag are device-side
     if (!async && (r = check_deferred(c))) return r;
-    if (!c->move_pending) WSMC_HIP(hipMemsetAsync(c->dflag, 0, sizeof(int32_t) * 4, c->stream));
+    if (!c->move_pending && !c->dflag_zero) WSMC_HIP(hipMemsetAsync(c->dflag, 0, sizeof(int32_t) * 4, c->stream));
+    c->dflag_zero = true;
     if (accepted_out) WSMC_HIP(hipMemsetAsync(c->ucount, 0, sizeof(unsigned long long) * 4, c->stream));
     if (proposal == WSMC_PROPOSAL_AUTORW && is_sharded(c)) {
+        if (c->w_reset_pending) {   // the sharded max pass reads the weights
+            WSMC_HIP(launch_fill_weights(c->stream, c->w, c->w_reset_pending, c->N));
+            c->w_reset_pending = nullptr;
+        }
+        c->dflag_zero = false;
         int rr = sharded_autorw(c, targets, d, bounded ? l : nullptr, bounded ? h : nullptr, step);
         if (rr) return rr;
     } else if (proposal == WSMC_PROPOSAL_AUTORW) {
@@ -2308,6 +2355,10 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         const bool kept = c->cur_max && c->cur_max_seq == c->wseq;
         MaxSlots* mms = kept ? c->cur_max : c->mslots;
         if (!kept) {
+            if (c->w_reset_pending) {   // the max pass reads the weights themselves
+                WSMC_HIP(launch_fill_weights(c->stream, c->w, c->w_reset_pending, c->N));
+                c->w_reset_pending = nullptr;
+            }
             WSMC_HIP(hipMemsetAsync(c->mslots, 0, sizeof(MaxSlots), c->stream));
             WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, c->mslots));
         }
@@ -2318,8 +2369,9 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         // device-scope fence per block, measured 2x slower than the separate combine launch:
         // 113.6 vs 57.7 + 13.5 us at 4M — every block's fence writes back its L2)
         WSMC_HIP(launch_autorw_moments(c->stream, c->w, mms, c->d_colptr, targets, d, lp, hp, nullptr, c->N,
-                                       c->tilepart));
-        WSMC_HIP(launch_autorw_final(c->stream, c->tilepart, c->ntiles, d, step, c->mom, c->dflag, 0));
+                                       c->tilepart, c->w_reset_pending, gate));
+        WSMC_HIP(launch_autorw_final(c->stream, c->tilepart, c->ntiles, d, step, c->mom, c->dflag, 0, gate));
+        c->dflag_zero = false;
     } else {
         WSMC_HIP(hipStreamSynchronize(c->stream));
         double* L = reinterpret_cast<double*>(c->pinned);
@@ -2403,10 +2455,30 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         for (size_t s = 0; s < slots.size(); ++s)
             fs.p[s] = c->cols[slots[s].first].front + (int64_t)slots[s].second * c->N;
         for (int k = 0; k < d; ++k) fs.t[k] = c->cols[targets[k]].front;
+        // carried scores one lazy Resample behind: read through its ancestors, written to the
+        // other buffer (no gather launch at the Resample)
+        MoveCarry mc;
+        mc.in = c->scache;
+        mc.out = c->scache;
+        mc.gate = gate;
+        if (c->scache_anc && cache_from >= 0) {
+            mc.anc = c->scache_anc;
+            mc.dec = c->scache_dec;
+            mc.out = c->scache_back;
+        }
         WSMC_HIP(launch_move_c(c->stream, d_ct, kD, target_depth, fs, targets, d, bounded ? l : nullptr,
                                bounded ? h : nullptr, bounded ? 1 : 0, c->mom + 32, c->seed, op_prop, op_acc, c->goff,
-                               c->N, c->ucount, mflag, c->scache, cache_from, prog));
+                               c->N, c->ucount, mflag, mc, cache_from, prog));
+        if (mc.out != mc.in) std::swap(c->scache, c->scache_back);
+        c->scache_anc = nullptr;   // written in slot order now (or refolded from scratch)
+        c->scache_dec = nullptr;
+        c->scache_lag_epoch = -1;
     } else {
+        if (gate) {   // the generic kernel has no gate: decide on the host
+            if ((r = resolve_decisions(c))) return r;
+            if (!c->resampled) return WSMC_OK;   // skipped (its op counters are consumed)
+        }
+        if ((r = resolve_scache_lag(c))) return r;   // the generic kernel reads its scores in place
         if ((r = upload_tape(c))) return r;
         WSMC_HIP(launch_move(c->stream, c->d_tape, (int32_t)c->tape.size(), target_depth, c->d_colptr, targets, d,
                              bounded ? l : nullptr, bounded ? h : nullptr, bounded ? 1 : 0, c->mom + 32, c->seed,
@@ -2425,9 +2497,36 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
     WSMC_HIP(hipMemcpyAsync(hb->acc, c->ucount, sizeof(unsigned long long) * 4, hipMemcpyDeviceToHost, c->stream));
     WSMC_HIP(hipStreamSynchronize(c->stream));
     if (hb->flag[0]) return fail(WSMC_ENOTPD, "autoRW proposal covariance is not positive definite");
+    c->dflag_zero = true;
     c->scache_terms = kD;
     if (accepted_out) *accepted_out = (int64_t)hb->acc[0];
     return WSMC_OK;
+}
+
+int wsmc_move_gated(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, double step, const double* lo,
+                    const double* hi, int32_t target_depth, double diversity) {
+    if (c && c->multi)
+        return multi_each(c, [&](wsmc_ctx* x) {
+            return wsmc_move_gated(x, proposal, targets, d, step, lo, hi, target_depth, diversity);
+        });
+    CHECK_CTX_KEEP(c);
+    // the deciding Resample: the newest one still pending on the device, else the host flag
+    const Decision* gate = c->dec_pending > 0 && !c->dec_rows.empty() ? c->dec_rows.back().row.dec : nullptr;
+    if (gate && (is_sharded(c) || !std::isnan(diversity))) {
+        if (int r = resolve_decisions(c)) return r;
+        gate = nullptr;
+    }
+    if (!gate) {
+        if (!c->resampled) {   // does not run: its two op counters are consumed all the same
+            c->op += 2;
+            return WSMC_OK;
+        }
+        return wsmc_move(c, proposal, targets, d, step, lo, hi, target_depth, diversity, nullptr);
+    }
+    c->move_gate = gate;
+    const int r = wsmc_move(c, proposal, targets, d, step, lo, hi, target_depth, diversity, nullptr);
+    c->move_gate = nullptr;
+    return r;
 }
 
 // ---- fused 2D SSM runner --------------------------------------------------------------
@@ -2986,7 +3085,7 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         });
     CHECK_CTX(c);
     if (int r = resolve_decisions(c)) return r;
-    c->scache_terms = -1;   // the run rewrites columns the tape reads
+    scores_invalidate(c);   // the run rewrites columns the tape reads
     c->wseq += 1;           // ... and the weights
     if (!obs || T < 1 || !x0 || !v0) return fail(WSMC_EARG, "bad arguments");
     if (!valid_scheme(scheme)) return fail(WSMC_EARG, "unknown resampling scheme");

@@ -252,11 +252,18 @@ struct wsmc_ctx {
         wsmc::AncRow row;
     };
     std::vector<PendingRow> dec_rows;
+    // carried Move scores one lazy Resample behind (their gather deferred to the next Move,
+    // which reads them through this log entry's ancestors)
+    const int32_t* scache_anc = nullptr;
+    const wsmc::Decision* scache_dec = nullptr;
+    int64_t scache_lag_epoch = -1;
     int32_t* anc_last = nullptr;            // wsmc_last_ancestors: newest row known to have resampled
     int64_t anc_last_epoch = -1;            // its log entry (lazy), -1 otherwise
     wsmc::AncRow anc_keep{};                // eager store: the row anc_last points at (owned)
     wsmc::Decision* dec_always = nullptr;   // [1] resampled = 1 (explicit resample!(store, idx))
     bool move_pending = false;              // an asynchronous Move's PD flag not yet read back
+    bool dflag_zero = false;                // dflag known to be all zero (no memset needed)
+    const wsmc::Decision* move_gate = nullptr;   // wsmc_move_gated: the deciding Resample's device decision
 
     // fused runner state
     int32_t T_alloc = 0;
@@ -394,10 +401,20 @@ struct FoldProgram {
     int32_t nseg_new, nseg_old;
     const double* cst;
 };
+// the carried Move scores of one Move (ping-pong when a lazy Resample came in between: the
+// scores are then read through its ancestors, gated by its decision, and written to `out`)
+struct MoveCarry {
+    const double* in;
+    double* out;
+    const int32_t* anc = nullptr;
+    const Decision* dec = nullptr;
+    const Decision* gate = nullptr;   // a gated Move (wsmc_move_gated): only the scores are carried
+                                      // on when !gate->resampled
+};
 hipError_t launch_move_c(hipStream_t s, const wsmc_term* ctape, int32_t nterms, int32_t depth, const FoldSlots& fs,
                          const int32_t* tcols, int d, const double* lo, const double* hi, int bounded,
                          const double* L, uint64_t seed, uint64_t op_prop, uint64_t op_acc, int64_t goff, int64_t N,
-                         unsigned long long* accepted, const int32_t* flag, double* scache, int32_t cache_from,
+                         unsigned long long* accepted, const int32_t* flag, const MoveCarry& mc, int32_t cache_from,
                          const FoldProgram& prog);
 // exact-sharded fused run: contiguous slices of (x pair, ancestor) by global index for the
 // distributed trace-back, the lineage lookup, pairs -> SoA
@@ -427,9 +444,10 @@ hipError_t launch_max_publish(hipStream_t s, const MaxSlots* ms, unsigned long l
 // their one-block combine and factor; sharded: publish (max word, pivot), rank-order combine
 hipError_t launch_autorw_moments(hipStream_t s, const double* w, const MaxSlots* ms, double* const* cols,
                                  const int32_t* tcols, int d, const double* lo, const double* hi,
-                                 const unsigned long long* pv, int64_t N, double* tilepart);
+                                 const unsigned long long* pv, int64_t N, double* tilepart,
+                                 const Decision* wreset = nullptr, const Decision* gate = nullptr);
 hipError_t launch_autorw_final(hipStream_t s, const double* tilepart, int64_t ntiles, int d, double min_step,
-                               double* mom, int32_t* flag, int raw);
+                               double* mom, int32_t* flag, int raw, const Decision* gate = nullptr);
 hipError_t launch_autorw_publish(hipStream_t s, const MaxSlots* ms, double* const* cols, const int32_t* tcols, int d,
                                  const double* lo, const double* hi, unsigned long long* out);
 hipError_t launch_autorw_combine1(hipStream_t s, const unsigned long long* xchg, int world, int stride, int d,

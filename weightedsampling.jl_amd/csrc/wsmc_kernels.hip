@@ -1859,10 +1859,16 @@ __device__ __forceinline__ void autorw_pivot(double* const* cols, const MomArgs&
 template <int D>
 __global__ __launch_bounds__(kBlock) void k_moments1(const double* __restrict__ w, const MaxSlots* ms,
                                                      double* const* cols, MomArgs ma, const u64* pv, int64_t N,
-                                                     int64_t ntiles, double* tilepart) {
+                                                     int64_t ntiles, double* tilepart, const Decision* wreset,
+                                                     const Decision* gate) {
     constexpr int d = D, NV = 1 + D + D * (D + 1) / 2;
     __shared__ double lds4[4];
+    if (gate && !gate->resampled) return;   // a gated Move that does not run
     const double M = wave_slots_max(ms);
+    // a fused Resample's weight reset still pending (the next Observe applies it): the
+    // weights are its log-mean, all equal (the max slots already hold it)
+    const bool reset = wreset && wreset->resampled;
+    const double wr = reset ? wreset->mean : 0.0;
     double p[4];
     autorw_pivot<D>(cols, ma, pv, p);
     const int64_t base = (int64_t)blockIdx.x * kTile;
@@ -1875,7 +1881,7 @@ __global__ __launch_bounds__(kBlock) void k_moments1(const double* __restrict__ 
 #pragma unroll
         for (int v = 0; v < NV; ++v) vals[v] = 0.0;
         if (i < N) {
-            const double e = wsmc_exp(w[i] - M);
+            const double e = wsmc_exp((reset ? wr : w[i]) - M);
             double dz[4];
 #pragma unroll
             for (int k = 0; k < d; ++k) dz[k] = wsmc_to_unc(cols[ma.tcol[k]][i], ma.lo[k], ma.hi[k]) - p[k];
@@ -1902,10 +1908,11 @@ __global__ __launch_bounds__(kBlock) void k_moments1(const double* __restrict__ 
 // covariance, mom[32..] its Cholesky factor, flag[0] = 1 if not positive definite
 template <int D>
 __global__ __launch_bounds__(kBlock) void k_autorw_final(const double* tilepart, int64_t ntiles, double min_step,
-                                                         double* mom, int32_t* flag, int raw) {
+                                                         double* mom, int32_t* flag, int raw, const Decision* gate) {
     constexpr int NV = 1 + D + D * (D + 1) / 2;
     __shared__ double lds4[4];
     __shared__ double tot[NV];
+    if (gate && !gate->resampled) return;
     for (int v = 0; v < NV; ++v) {
         double acc = 0.0;
         for (int64_t b = threadIdx.x; b < ntiles; b += kBlock) acc = acc + tilepart[(int64_t)v * ntiles + b];
@@ -2134,7 +2141,7 @@ template <int K, int LEAN>
 __global__ __launch_bounds__(kBlock) void k_move_c(const wsmc_term* ctape, int32_t nterms, int32_t depth,
                                                    FoldSlots fs, MomArgs ma, int d, int bounded, const double* Lm,
                                                    uint64_t seed, uint64_t op_prop, uint64_t op_acc, int64_t goff,
-                                                   int64_t N, u64* accepted, const int32_t* flag, double* scache,
+                                                   int64_t N, u64* accepted, const int32_t* flag, MoveCarry mc,
                                                    int32_t cache_from, FoldProgram prog) {
     constexpr int W = K * kBlock;            // LDS row length
     extern __shared__ double sv[];           // [fs.n][W] current values, then [4][W] proposals
@@ -2162,16 +2169,19 @@ __global__ __launch_bounds__(kBlock) void k_move_c(const wsmc_term* ctape, int32
 #pragma unroll
         for (int p = 0; p < K; ++p) sv[sl * W + ix[p]] = ok[p] ? fs.p[sl][gi[p]] : 0.0;
     double so[K], sn[K], lpr[K];
+    const bool lag = mc.anc && mc.dec->resampled;
+    const bool run = !mc.gate || mc.gate->resampled;   // a gated Move that does not run only carries
+                                                       // its scores on over the new terms
 #pragma unroll
     for (int p = 0; p < K; ++p) {
-        so[p] = (ok[p] && cache_from >= 0) ? scache[gi[p]] : 0.0;
+        so[p] = (ok[p] && cache_from >= 0) ? mc.in[lag ? (int64_t)mc.anc[gi[p]] : gi[p]] : 0.0;
         sn[p] = 0.0;
         lpr[p] = 0.0;
     }
     __syncthreads();
 #pragma unroll
     for (int p = 0; p < K; ++p) {
-        if (!ok[p]) continue;
+        if (!ok[p] || !run) continue;
         double xi[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int k = 0; k < 4; ++k)
@@ -2193,11 +2203,15 @@ __global__ __launch_bounds__(kBlock) void k_move_c(const wsmc_term* ctape, int32
     }
     // s_old: the carried score continued over the new terms, or the full fold
     fold_seg<K, LEAN>(so, ctape, prog.seg_old, prog.nseg_old, prog.cst, sp, ix, ok);
-    fold_seg<K, LEAN>(sn, ctape, prog.seg_new, prog.nseg_new, prog.cst, spn, ix, ok);
+    if (run) fold_seg<K, LEAN>(sn, ctape, prog.seg_new, prog.nseg_new, prog.cst, spn, ix, ok);
     u64 acc = 0;
 #pragma unroll
     for (int p = 0; p < K; ++p) {
         if (!ok[p]) continue;
+        if (!run) {
+            mc.out[gi[p]] = so[p];
+            continue;
+        }
         const double u = wsmc_uniform_k(seed, op_acc, (uint64_t)(goff + gi[p]), 0);
         const bool a = wsmc_log(u) < (lpr[p] + sn[p]) - so[p];   // strict; NaN rejects (src/transformers.jl:615)
         if (a) {
@@ -2206,7 +2220,7 @@ __global__ __launch_bounds__(kBlock) void k_move_c(const wsmc_term* ctape, int32
                 if (k < d) fs.t[k][gi[p]] = prop[k * W + ix[p]];
             acc += 1;
         }
-        scache[gi[p]] = a ? sn[p] : so[p];
+        mc.out[gi[p]] = a ? sn[p] : so[p];
     }
     acc = block_sum_u64(acc, lds4);
     if (threadIdx.x == 0 && acc) atomicAdd(accepted, acc);
@@ -2903,24 +2917,24 @@ static MomArgs mom_args(const int32_t* tcols, int d, const double* lo, const dou
 }
 hipError_t launch_autorw_moments(hipStream_t s, const double* w, const MaxSlots* ms, double* const* cols,
                                  const int32_t* tcols, int d, const double* lo, const double* hi, const u64* pv,
-                                 int64_t N, double* tilepart) {
+                                 int64_t N, double* tilepart, const Decision* wreset, const Decision* gate) {
     const MomArgs ma = mom_args(tcols, d, lo, hi);
     const int64_t nt = (N + kTile - 1) / kTile;
     switch (d) {
-        case 1: hipLaunchKernelGGL(k_moments1<1>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart); break;
-        case 2: hipLaunchKernelGGL(k_moments1<2>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart); break;
-        case 3: hipLaunchKernelGGL(k_moments1<3>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart); break;
-        default: hipLaunchKernelGGL(k_moments1<4>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart); break;
+        case 1: hipLaunchKernelGGL(k_moments1<1>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart, wreset, gate); break;
+        case 2: hipLaunchKernelGGL(k_moments1<2>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart, wreset, gate); break;
+        case 3: hipLaunchKernelGGL(k_moments1<3>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart, wreset, gate); break;
+        default: hipLaunchKernelGGL(k_moments1<4>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart, wreset, gate); break;
     }
     return hipGetLastError();
 }
 hipError_t launch_autorw_final(hipStream_t s, const double* tilepart, int64_t ntiles, int d, double min_step,
-                               double* mom, int32_t* flag, int raw) {
+                               double* mom, int32_t* flag, int raw, const Decision* gate) {
     switch (d) {
-        case 1: hipLaunchKernelGGL(k_autorw_final<1>, dim3(1), dim3(kBlock), 0, s, tilepart, ntiles, min_step, mom, flag, raw); break;
-        case 2: hipLaunchKernelGGL(k_autorw_final<2>, dim3(1), dim3(kBlock), 0, s, tilepart, ntiles, min_step, mom, flag, raw); break;
-        case 3: hipLaunchKernelGGL(k_autorw_final<3>, dim3(1), dim3(kBlock), 0, s, tilepart, ntiles, min_step, mom, flag, raw); break;
-        default: hipLaunchKernelGGL(k_autorw_final<4>, dim3(1), dim3(kBlock), 0, s, tilepart, ntiles, min_step, mom, flag, raw); break;
+        case 1: hipLaunchKernelGGL(k_autorw_final<1>, dim3(1), dim3(kBlock), 0, s, tilepart, ntiles, min_step, mom, flag, raw, gate); break;
+        case 2: hipLaunchKernelGGL(k_autorw_final<2>, dim3(1), dim3(kBlock), 0, s, tilepart, ntiles, min_step, mom, flag, raw, gate); break;
+        case 3: hipLaunchKernelGGL(k_autorw_final<3>, dim3(1), dim3(kBlock), 0, s, tilepart, ntiles, min_step, mom, flag, raw, gate); break;
+        default: hipLaunchKernelGGL(k_autorw_final<4>, dim3(1), dim3(kBlock), 0, s, tilepart, ntiles, min_step, mom, flag, raw, gate); break;
     }
     return hipGetLastError();
 }
@@ -2964,7 +2978,7 @@ hipError_t launch_move(hipStream_t s, const wsmc_term* tape, int32_t nterms, int
 hipError_t launch_move_c(hipStream_t s, const wsmc_term* ctape, int32_t nterms, int32_t depth, const FoldSlots& fs,
                          const int32_t* tcols, int d, const double* lo, const double* hi, int bounded,
                          const double* L, uint64_t seed, uint64_t op_prop, uint64_t op_acc, int64_t goff, int64_t N,
-                         u64* accepted, const int32_t* flag, double* scache, int32_t cache_from,
+                         u64* accepted, const int32_t* flag, const MoveCarry& mc, int32_t cache_from,
                          const FoldProgram& prog) {
     MomArgs ma;
     for (int k = 0; k < 4; ++k) {
@@ -2989,7 +3003,7 @@ hipError_t launch_move_c(hipStream_t s, const wsmc_term* ctape, int32_t nterms, 
 #define WSMC_MOVE_LAUNCH(KK, LL)                                                                              \
     hipLaunchKernelGGL((k_move_c<KK, LL>), dim3((unsigned)((N + KK * kBlock - 1) / (KK * kBlock))), dim3(kBlock), \
                        KK * row, s, ctape, nterms, depth, fs, ma, d, bounded, L, seed, op_prop, op_acc, goff, N,    \
-                       accepted, flag, scache, cache_from, prog)
+                       accepted, flag, mc, cache_from, prog)
     if (kdiag == 1 || (kdiag != 2 && fs.heavy)) {
         if (lean == 2) WSMC_MOVE_LAUNCH(1, 2);
         else if (lean == 1) WSMC_MOVE_LAUNCH(1, 1);

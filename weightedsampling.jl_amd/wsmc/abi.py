@@ -117,6 +117,7 @@ SIGNATURES = {
     "wsmc_resample": (C.c_int, [_P, C.c_double, C.c_int32, _I32P, _D]),
     "wsmc_move": (C.c_int, [_P, C.c_int32, _I32P, C.c_int32, C.c_double, _D, _D, C.c_int32,
                             C.c_double, C.POINTER(C.c_int64)]),
+    "wsmc_move_gated": (C.c_int, [_P, C.c_int32, _I32P, C.c_int32, C.c_double, _D, _D, C.c_int32, C.c_double]),
     "wsmc_score": (C.c_int, [_P, C.c_int32, _D]),
     "wsmc_marginal_diversity": (C.c_int, [_P, _I32P, C.c_int32, _D]),
     "wsmc_last_ancestors": (C.c_int, [_P, _I32P]),

@@ -311,6 +311,21 @@ class Context:
         check(rc)
         return int(acc.value) if wait else None
 
+    def move_gated(self, proposal: int, targets, step: float, lo=None, hi=None, target_depth: int = -1,
+                   diversity: float = math.nan) -> None:
+        """Move.apply! inside `if resampled` decided on the device (wsmc_move_gated): runs only
+        if the last Resample resampled; consumes its two op counters either way."""
+        t = np.ascontiguousarray(np.asarray(targets, dtype=np.int32))
+        d = len(t)
+        lo_a = None if lo is None else np.ascontiguousarray(np.asarray(lo, float).reshape(d))
+        hi_a = None if hi is None else np.ascontiguousarray(np.asarray(hi, float).reshape(d))
+        rc = self._L.wsmc_move_gated(self._h, int(proposal), t.ctypes.data_as(_I32P), d, float(step),
+                                     None if lo_a is None else _dptr(lo_a), None if hi_a is None else _dptr(hi_a),
+                                     int(target_depth), float(diversity))
+        if rc == abi.WSMC_ENOTPD:
+            raise np.linalg.LinAlgError(self._L.wsmc_last_error().decode())
+        check(rc)
+
     def score(self, target_depth: int) -> np.ndarray:
         out = np.empty(self.n)
         check(self._L.wsmc_score(self._h, int(target_depth), _dptr(out)))

@@ -117,9 +117,11 @@ def lgssm1d_statements(ctx, data, a=0.9, q=1.0, r=0.5, x0_std=1.0, ess_perc_min=
 
 
 def linreg_statements(ctx, xs, ys, prior_sd=10.0, obs_sd=1.0, ess_perc_min=0.5,
-                      scheme=abi.RESAMPLE_STRATIFIED, min_step=1e-3, wait_moves=True):
+                      scheme=abi.RESAMPLE_STRATIFIED, min_step=1e-3, wait_moves=True, gated=False):
     """examples/linear_regression.jl:17-27: α, β ~ N(0,10); y => N(α + β x, 1);
-    `if resampled; α << autoRW(); β << autoRW(); end`."""
+    `if resampled; α << autoRW(); β << autoRW(); end`. gated=True lowers the `if resampled`
+    block to device-gated Moves (wsmc_move_gated): no Resample returns its flag, nothing waits
+    on the host inside the loop, and the function returns None."""
     R = resolver(ctx)
     ca = ctx.col_create("α", 1)
     ctx.sample(ca, Normal(0.0, prior_sd).dist(R))
@@ -130,17 +132,23 @@ def linreg_statements(ctx, xs, ys, prior_sd=10.0, obs_sd=1.0, ess_perc_min=0.5,
     accepted = []
     for x, y in zip(xs, ys):
         ctx.observe(Normal(Col("α") + Col("β") * float(x), obs_sd).dist(R), _const([y]))
+        if gated:
+            ctx.resample(ess_perc_min, scheme, wait=False)
+            ctx.move_gated(abi.PROPOSAL_AUTORW, [ca], min_step)
+            ctx.move_gated(abi.PROPOSAL_AUTORW, [cb], min_step)
+            continue
         rs, _ = ctx.resample(ess_perc_min, scheme)
         if rs:   # `if resampled` reads the flag; the moves need not return their counts
             a1 = ctx.move(abi.PROPOSAL_AUTORW, [ca], min_step, wait=wait_moves)
             a2 = ctx.move(abi.PROPOSAL_AUTORW, [cb], min_step, wait=wait_moves)
             accepted.append((a1, a2))
-    return accepted
+    return None if gated else accepted
 
 
 def oscillator_statements(ctx, t_obs, y_obs, ess_perc_min=0.5, scheme=abi.RESAMPLE_STRATIFIED,
                           sweeps=1, diversity=0.9, min_step=1e-3, wait_moves=True):
-    """examples/damped_oscillator.jl:30-43 with `sweeps` repetitions of the two moves."""
+    """examples/damped_oscillator.jl:30-43 with `sweeps` repetitions of the two moves. The model
+    has no `if resampled`: no Resample returns its flag (the decisions stay on the device)."""
     R = resolver(ctx)
     names = ["A", "ω", "γ", "ϕ", "σ"]
     priors = [HalfNormal(5.0), HalfNormal(5.0), HalfNormal(1.0), Uniform(-math.pi, math.pi), HalfNormal(1.0)]
@@ -148,14 +156,14 @@ def oscillator_statements(ctx, t_obs, y_obs, ess_perc_min=0.5, scheme=abi.RESAMP
     for n, k in zip(names, priors):
         cols[n] = ctx.col_create(n, 1)
         ctx.sample(cols[n], k.dist(R))
-        ctx.resample(ess_perc_min, scheme)
+        ctx.resample(ess_perc_min, scheme, wait=False)
     joint = [cols["A"], cols["ω"], cols["γ"], cols["σ"]]
     div = math.nan if diversity is None else float(diversity)
     accepted = []
     for t, y in zip(t_obs, y_obs):
         mean = Oscillator(float(t), Col("A"), Col("ω"), Col("γ"), Col("ϕ"))
         ctx.observe(Normal(mean, Col("σ")).dist(R), _const([y]))
-        ctx.resample(ess_perc_min, scheme)
+        ctx.resample(ess_perc_min, scheme, wait=False)
         for _ in range(sweeps):
             a1 = ctx.move(abi.PROPOSAL_AUTORW, joint, min_step, lo=[0.0] * 4, hi=[math.inf] * 4,
                           diversity=div, wait=wait_moves)
