@@ -2621,6 +2621,14 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
         a.dec_prev = t > 1 ? c->run_dec + (t - 1) : nullptr;
         MaxSlots* ms = c->run_max + t;
         ShardRecord* recs = c->run_rec + (size_t)t * c->world;
+        if (sharded && p.scheme != WSMC_RESAMPLE_MULTINOMIAL && t > 1) {
+            // island: the previous step's decision is taken in this kernel from its records
+            a.recs_prev = c->run_rec + (size_t)(t - 1) * c->world;
+            a.dec_out = c->run_dec + (t - 1);
+            a.world = c->world;
+            a.rank = c->rank;
+            a.ess_min = p.ess_min;
+        }
         a.ms = ms;
         const int k0 = 8 * (t - 1);
         WSMC_HIP(launch_ssm2d_propagate(c->stream, a, E(k0), E(k0 + 1)));
@@ -2649,10 +2657,9 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
         WSMC_HIP(launch_rs_sums(c->stream, c->w, N, ms, c->tilep, c->qbuf, E(k0 + 2), E(k0 + 3), grp, G));
         WSMC_HIP(launch_rs_fill_fused(c->stream, N, plan, grp, G, ms, p.ess_min, recs + c->rank,
                                       sharded ? nullptr : c->run_dec + t, c->qbuf, anc_row, E(k0 + 6), E(k0 + 7)));
-        if (sharded) {
+        if (sharded) {   // the next propagate (or the trace-back) decides from the records
             int r = exchange_recs(c, recs);
             if (r) return r;
-            WSMC_HIP(launch_rs_decide(c->stream, recs, c->world, c->rank, p.ess_min, c->run_dec + t));
         }
     }
     Ssm2dFinal f;
@@ -2672,6 +2679,13 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
     f.anc_log = c->anc_log;
     f.anc_stride = anc_stride(N);
     f.dec = c->run_dec;
+    if (sharded && p.scheme != WSMC_RESAMPLE_MULTINOMIAL) {
+        f.recs_last = c->run_rec + (size_t)T * c->world;
+        f.dec_out = c->run_dec + T;
+        f.world = c->world;
+        f.rank = c->rank;
+        f.ess_min = p.ess_min;
+    }
     WSMC_HIP(launch_ssm2d_finalize(c->stream, f, E(8 * T), E(8 * T + 1)));
     return WSMC_OK;
 }

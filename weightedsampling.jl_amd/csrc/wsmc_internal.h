@@ -638,6 +638,13 @@ struct Ssm2dArgs {
     // [goff, goff + N) arrived from a neighbour and its pair is xr / vr at the slot itself
     const double* xr = nullptr;
     const double* vr = nullptr;
+    // island shards: the previous step's decision is taken here from its all-gathered records
+    // (every block, the same bits as k_rs_decide) instead of by its own launch; block 0 stores
+    // it at dec_out for the host and the trace-back
+    const ShardRecord* recs_prev = nullptr;
+    Decision* dec_out = nullptr;
+    int32_t world = 1, rank = 0;
+    double ess_min = 0.0;
 };
 hipError_t launch_ssm2d_propagate(hipStream_t s, const Ssm2dArgs& a, hipEvent_t e0 = nullptr,
                                   hipEvent_t e1 = nullptr);
@@ -658,6 +665,11 @@ struct Ssm2dFinal {
     const int32_t* anc_log;    // [T][anc_stride]
     int64_t anc_stride;        // row stride of the ancestor log (N rounded up to 4)
     const Decision* dec;       // [T+1], index t
+    // island shards: the last step's decision from its all-gathered records (see Ssm2dArgs)
+    const ShardRecord* recs_last = nullptr;
+    Decision* dec_out = nullptr;
+    int32_t world = 1, rank = 0;
+    double ess_min = 0.0;
 };
 hipError_t launch_ssm2d_finalize(hipStream_t s, const Ssm2dFinal& f, hipEvent_t e0 = nullptr,
                                  hipEvent_t e1 = nullptr);

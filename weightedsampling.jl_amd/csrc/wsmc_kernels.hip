@@ -1979,8 +1979,9 @@ __global__ __launch_bounds__(kBlock) void k_move(const wsmc_term* tape, int32_t 
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     u64 acc = 0;
     if (i < N) {
-        double xi[4], dz[4];
-        for (int k = 0; k < d; ++k) xi[k] = wsmc_normal_k(seed, op_prop, (uint64_t)(goff + i), (uint32_t)k);
+        double xi[4] = {0.0, 0.0, 0.0, 0.0}, dz[4];
+        for (int k = 0; k < d; k += 2)   // one Box-Muller pair per two targets (wsmc_normal_k's values)
+            wsmc_normal_pair(wsmc_rng_block(seed, op_prop, (uint64_t)(goff + i), (uint32_t)(k >> 1)), &xi[k], &xi[k + 1]);
         for (int k = 0; k < d; ++k) {
             double s = 0.0;
             for (int j = 0; j <= k; ++j) s = s + Lm[k * d + j] * xi[j];
@@ -2182,10 +2183,13 @@ __global__ __launch_bounds__(kBlock) void k_move_c(const wsmc_term* ctape, int32
 #pragma unroll
     for (int p = 0; p < K; ++p) {
         if (!ok[p] || !run) continue;
+        // the proposal's normals: one Box-Muller pair per two targets (wsmc_normal_k(k) is
+        // component k & 1 of the pair of block k >> 1: the same values, half the work)
         double xi[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (k < d) xi[k] = wsmc_normal_k(seed, op_prop, (uint64_t)(goff + gi[p]), (uint32_t)k);
+        for (int k = 0; k < 4; k += 2)
+            if (k < d) wsmc_normal_pair(wsmc_rng_block(seed, op_prop, (uint64_t)(goff + gi[p]), (uint32_t)(k >> 1)),
+                                        &xi[k], &xi[k + 1]);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             if (k >= d) break;
@@ -2270,8 +2274,23 @@ template <int MODE, int IT = 1>
 __global__ __launch_bounds__(kBlock) void k_ssm2d_prop(Ssm2dArgs a) {
     __shared__ u64 lds4[4];
     const int64_t N = a.N;
-    const bool rs = a.t > 1 && a.dec_prev->resampled;
-    const double mean = rs ? a.dec_prev->mean : 0.0;
+    bool rs;
+    double mean;
+    if (a.recs_prev && a.t > 1) {
+        __shared__ Decision s_dec;
+        if (threadIdx.x == 0) {
+            Decision dd;
+            decide_records(a.recs_prev, a.world, a.rank, a.ess_min, &dd);
+            s_dec = dd;
+            if (blockIdx.x == 0) *a.dec_out = dd;
+        }
+        __syncthreads();
+        rs = s_dec.resampled;
+        mean = rs ? s_dec.mean : 0.0;
+    } else {
+        rs = a.t > 1 && a.dec_prev->resampled;
+        mean = rs ? a.dec_prev->mean : 0.0;
+    }
     const uint64_t op_dv = a.op_dev[0] + 3ull * (uint64_t)(a.t - 1);
     const double o0 = a.obs[2 * (a.t - 1)], o1 = a.obs[2 * (a.t - 1) + 1];
     // IT pairs per thread, a grid apart: every pair's loads are issued before any pair is
@@ -2444,17 +2463,32 @@ __global__ __launch_bounds__(kBlock) void k_iota(int32_t* __restrict__ a, int64_
 __global__ __launch_bounds__(kBlock) void k_ssm2d_final(Ssm2dFinal f) {
     const int64_t N = f.N;
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= N) return;
     const int T = f.T;
+    __shared__ Decision s_dec;
+    if (f.recs_last) {   // island shards: the last step's decision from its records
+        if (threadIdx.x == 0) {
+            Decision dd;
+            decide_records(f.recs_last, f.world, f.rank, f.ess_min, &dd);
+            s_dec = dd;
+            if (blockIdx.x == 0) *f.dec_out = dd;
+        }
+        __syncthreads();
+    } else if (threadIdx.x == 0) {
+        s_dec = f.dec[T];
+    }
+    if (!f.recs_last) __syncthreads();
+    if (i >= N) return;
+    const bool rsT = s_dec.resampled;
+    const double meanT = s_dec.mean;
     const int64_t S = f.anc_stride;
     int64_t a = i;
-    if (f.dec[T].resampled) a = f.anc_log[(int64_t)(T - 1) * S + i];
+    if (rsT) a = f.anc_log[(int64_t)(T - 1) * S + i];
     // working buffers are particle-major pairs; output columns are SoA [2][N]
     const d2 v = *reinterpret_cast<const d2*>(f.v_work + 2 * a);
     f.v_out[i] = v.x; f.v_out[N + i] = v.y;
     const d2 dv = *reinterpret_cast<const d2*>(f.dv_work + 2 * a);
     f.dv_out[i] = dv.x; f.dv_out[N + i] = dv.y;
-    if (f.dec[T].resampled) f.w[i] = f.dec[T].mean;
+    if (rsT) f.w[i] = meanT;
     if (!f.keep_history) {
         const d2 x = *reinterpret_cast<const d2*>(f.x_work + 2 * a);
         f.x_out[i] = x.x; f.x_out[N + i] = x.y;
