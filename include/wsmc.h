@@ -279,6 +279,25 @@ int wsmc_move(wsmc_ctx* ctx, int32_t proposal, const int32_t* targets, int32_t d
  * diversity gate or on shards the decision is read on the host first.                       */
 int wsmc_move_gated(wsmc_ctx* ctx, int32_t proposal, const int32_t* targets, int32_t d, double step,
                     const double* lo, const double* hi, int32_t target_depth, double diversity);
+/* One Move of a block (wsmc_move_block): wsmc_move's arguments without the diversity gate. */
+typedef struct {
+    int32_t proposal;        /* WSMC_PROPOSAL_RW / WSMC_PROPOSAL_AUTORW */
+    int32_t d;               /* 1..4 targets */
+    int32_t targets[4];
+    int32_t bounded;         /* 0: lo / hi ignored (wsmc_move's NULL lo and hi) */
+    int32_t target_depth;    /* < 0: the current depth */
+    double step;             /* RW step / autoRW min_step */
+    double lo[4], hi[4];
+} wsmc_move_spec;
+/* A statement block of consecutive Moves — `α << autoRW(); β << autoRW()` in the body of
+ * `if resampled ... end` (examples/linear_regression.jl:23-24) or a sweep of
+ * examples/damped_oscillator.jl:38-41 without its diversity gate: exactly n wsmc_move calls
+ * in order (gated != 0: n wsmc_move_gated calls), the same results bit for bit, op counters
+ * taken two per Move in order. Autorw Moves on disjoint targets (4 at most in all) with one
+ * target depth run as one moments pass, one combine and one Move kernel; anything else runs
+ * the Moves one by one. accepted_out: n counts (synchronizing, the ENOTPD check of the first
+ * failing Move as wsmc_move's) or NULL (asynchronous).                                     */
+int wsmc_move_block(wsmc_ctx* ctx, int32_t n, const wsmc_move_spec* specs, int32_t gated, int64_t* accepted_out);
 /* score_logpdf!(scores, state, targets, target_depth) (src/types.jl:198-206) -> host */
 int wsmc_score(wsmc_ctx* ctx, int32_t target_depth, double* host_scores);
 /* marginal_diversity(store, targets)  (src/transformers.jl:560-565) */

@@ -36,6 +36,11 @@
 #else
 #define WSMC_HD static inline __attribute__((always_inline))
 #endif
+#if defined(__clang__)
+#define WSMC_UNROLL _Pragma("unroll")
+#else
+#define WSMC_UNROLL _Pragma("GCC unroll 16")
+#endif
 
 typedef unsigned __int128 wsmc_u128;
 
@@ -100,11 +105,14 @@ typedef struct { uint32_t v[4]; } wsmc_u32x4;
 WSMC_HD uint32_t wsmc_mulhi32(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
 
 WSMC_HD wsmc_u32x4 wsmc_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+    /* each round's two 32x32 -> 64 products whole (one v_mad_u64_u32 each on the device,
+       where separate high and low multiplies took two), rounds unrolled (the key schedule
+       becomes scalar adds) */
+    WSMC_UNROLL
     for (int r = 0; r < 10; ++r) {
-        uint32_t hi0 = wsmc_mulhi32(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-        uint32_t hi1 = wsmc_mulhi32(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
-        uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
         k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
     }
     wsmc_u32x4 o; o.v[0] = c0; o.v[1] = c1; o.v[2] = c2; o.v[3] = c3;

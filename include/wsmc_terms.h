@@ -228,27 +228,46 @@ WSMC_HD int wsmc_term_is_scalar(const wsmc_term* t) {
            (t->dist.family == WSMC_FAM_NORMAL || t->dist.family == WSMC_FAM_HALFNORMAL ||
             t->dist.family == WSMC_FAM_UNIFORM);
 }
-WSMC_HD double wsmc_scalar_term_logpdf_m(const wsmc_term* t, double* const* cols, int64_t N, int64_t i,
-                                         const wsmc_override* ov, wsmc_logmemo* lm) {
+/* pre: for a constant scale operand, (log(sigma), 1/sigma) evaluated once by the caller (the
+ * same functions of the same bits as wsmc_scale_memo's), else null */
+WSMC_HD double wsmc_scalar_term_logpdf_p(const wsmc_term* t, double* const* cols, int64_t N, int64_t i,
+                                         const wsmc_override* ov, wsmc_logmemo* lm, const double* pre) {
     const wsmc_dist* d = &t->dist;
     const double x0 = wsmc_operand_eval(&t->x[0], cols, N, i, ov);
     if (d->family == WSMC_FAM_NORMAL) {
         double mu = wsmc_operand_eval(&d->mu[0], cols, N, i, ov);
-        double sg = wsmc_operand_eval(&d->scale, cols, N, i, ov);
         double lg, rc;
-        wsmc_scale_memo(lm, sg, &lg, &rc);
+        if (pre) {
+            lg = pre[0];
+            rc = pre[1];
+        } else {
+            wsmc_scale_memo(lm, wsmc_operand_eval(&d->scale, cols, N, i, ov), &lg, &rc);
+        }
         double z = (x0 - mu) * rc;
         return -(z * z + WSMC_LOG2PI) * 0.5 - lg;
     }
     if (d->family == WSMC_FAM_HALFNORMAL) {
-        double sg = wsmc_operand_eval(&d->scale, cols, N, i, ov);
         if (!(x0 >= 0.0)) return -WSMC_INF;
         double lg, rc;
-        wsmc_scale_memo(lm, sg, &lg, &rc);
+        if (pre) {
+            lg = pre[0];
+            rc = pre[1];
+        } else {
+            wsmc_scale_memo(lm, wsmc_operand_eval(&d->scale, cols, N, i, ov), &lg, &rc);
+        }
         double z = (x0 - 0.0) * rc;
         return (-(z * z + WSMC_LOG2PI) * 0.5 - lg) + WSMC_LOG2;
     }
     return wsmc_uniform_logpdf(d->param[0], d->param[1], x0);
+}
+WSMC_HD double wsmc_scalar_term_logpdf_m(const wsmc_term* t, double* const* cols, int64_t N, int64_t i,
+                                         const wsmc_override* ov, wsmc_logmemo* lm) {
+    return wsmc_scalar_term_logpdf_p(t, cols, N, i, ov, lm, 0);
+}
+/* the (log(sigma), 1/sigma) pair of a constant scale (wsmc_scalar_term_logpdf_p's pre) */
+WSMC_HD void wsmc_scale_pre(double sigma, double* pre) {
+    pre[0] = wsmc_log(sigma);
+    pre[1] = 1.0 / sigma;
 }
 
 WSMC_HD double wsmc_term_logpdf_mf(const wsmc_term* t, double* const* cols, int64_t N, int64_t i,

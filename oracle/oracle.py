@@ -363,6 +363,21 @@ class Oracle:
             return
         self.move(proposal, targets, step, lo, hi, target_depth, diversity=diversity, wait=False)
 
+    def move_block(self, moves, gated: bool = False, wait: bool = False):
+        """wsmc_move_block: the statement block's Moves one after the other (its definition)."""
+        out = []
+        for mv in moves:
+            proposal, targets, step = mv[0], mv[1], mv[2]
+            lo = mv[3] if len(mv) > 3 else None
+            hi = mv[4] if len(mv) > 4 else None
+            depth = mv[5] if len(mv) > 5 else -1
+            if gated and not self.get_state()["resampled"]:
+                self.set_op_counter(self.get_state()["op_counter"] + 2)
+                out.append(0)
+                continue
+            out.append(self.move(proposal, targets, step, lo, hi, depth))
+        return out if wait else None
+
     def move(self, proposal: int, targets, step: float, lo=None, hi=None, target_depth: int = -1,
              diversity: float = float("nan"), wait: bool = True):
         t = np.ascontiguousarray(np.asarray(targets, dtype=np.int32))

@@ -501,8 +501,9 @@ def test_deferred_weight_reset_readers(gpu_available, reader):
     assert_same_state(g, o)
 
 
+@pytest.mark.parametrize("block", [True, False])
 @pytest.mark.parametrize("ess", [1.0, 0.5, 0.3])
-def test_gated_moves_match_oracle(gpu_available, ess):
+def test_gated_moves_match_oracle(gpu_available, ess, block):
     """`if resampled; α << autoRW(); β << autoRW(); end` lowered to device-gated Moves
     (wsmc_move_gated, examples/linear_regression.jl:22-25): asynchronous Resamples, the Moves
     decided on the device, nothing read on the host inside the loop. At 0.3 some steps do not
@@ -510,11 +511,69 @@ def test_gated_moves_match_oracle(gpu_available, ess):
     oracle's gated Move does."""
     xs, ys = models.linreg_data()
     g, o = wsmc.Context(4099, seed=8), Oracle(4099, seed=8)
-    assert models.linreg_statements(g, xs, ys, ess_perc_min=ess, gated=True) is None
-    models.linreg_statements(o, xs, ys, ess_perc_min=ess, gated=True)
+    assert models.linreg_statements(g, xs, ys, ess_perc_min=ess, gated=True, block=block) is None
+    models.linreg_statements(o, xs, ys, ess_perc_min=ess, gated=True, block=block)
     sg, so = g.get_state(), o.get_state()
     assert sg["n_resamples"] == so["n_resamples"] and sg["op_counter"] == so["op_counter"]
     if ess == 0.3:
         assert so["n_resamples"] < len(xs) + 2   # some gated Moves were skipped
     assert_same_state(g, o)
     assert g.log_evidence() == o.log_evidence()
+
+
+def _block_model(ctx, sigma_col):
+    """a, b ~ N(0, 10), c ~ HalfNormal(2): y => N(a + b x, c or 1) (the scale a column, or a
+    constant: the precomputed-scale fold path)"""
+    from wsmc.dsl import Col, HalfNormal, Normal
+    R = models.resolver(ctx)
+    cols = []
+    for name, prior in (("a", Normal(0.0, 10.0)), ("b", Normal(0.0, 10.0)), ("c", HalfNormal(2.0))):
+        cols.append(ctx.col_create(name, 1))
+        ctx.sample(cols[-1], prior.dist(R))
+    return cols, R
+
+
+# (move groups as indices into [a, b, c]; bounded groups get lo 0, hi inf)
+_BLOCKS = {
+    "ab_c": [((0, 1), False), ((2,), True)],
+    "a_b": [((0,), False), ((1,), False)],
+    "a_b_c": [((0,), False), ((1,), False), ((2,), True)],
+    "overlap": [((0, 1), False), ((1,), False)],       # overlapping targets: the moves one by one
+    "wide": [((0, 1, 2), True), ((0,), False)],        # 4 targets over the limit with overlap
+}
+
+
+@pytest.mark.parametrize("shape", sorted(_BLOCKS))
+@pytest.mark.parametrize("gated", [False, True])
+@pytest.mark.parametrize("wait", [False, True])
+@pytest.mark.parametrize("sigma_col", [True, False])
+def test_move_block_matches_oracle(gpu_available, shape, gated, wait, sigma_col):
+    """wsmc_move_block against the oracle's Moves one after the other: columns, scores carried
+    across steps, op counters, accepted counts — bit for bit. Lazy Resamples leave the targets
+    one Resample behind, so the fused path reads them through the ancestor row."""
+    from wsmc.dsl import Col, Normal
+    xs, ys = models.linreg_data()
+    N = 3001
+    res = []
+    for ctx in (wsmc.Context(N, seed=11), Oracle(N, seed=11)):
+        cols, R = _block_model(ctx, sigma_col)
+        ctx.resample(0.5)
+        counts = []
+        for x, y in zip(xs[:8], ys[:8]):
+            sd = Col("c") if sigma_col else 1.0
+            ctx.observe(Normal(Col("a") + Col("b") * float(x), sd).dist(R), models._const([y]))
+            ctx.resample(0.7, wait=False) if gated else ctx.resample(0.7)
+            moves = []
+            for grp, bnd in _BLOCKS[shape]:
+                t = [cols[k] for k in grp]
+                if bnd:
+                    moves.append((abi.PROPOSAL_AUTORW, t, 1e-3, [0.0] * len(t), [math.inf] * len(t)))
+                else:
+                    moves.append((abi.PROPOSAL_AUTORW, t, 1e-3))
+            counts.append(ctx.move_block(moves, gated=gated, wait=wait))
+        res.append((ctx, counts))
+    (g, cg), (o, co) = res
+    assert cg == co
+    assert_same_state(g, o)
+    assert g.log_evidence() == o.log_evidence()
+    np.testing.assert_array_equal(g.score(-1), o.score(-1))

@@ -24,14 +24,15 @@ def _ctx(N, one_rank):
     return ctx
 
 
-def c3(N=1_000_000, reps=3, wait_moves=True, one_rank=False, gated=False):
+def c3(N=1_000_000, reps=3, wait_moves=True, one_rank=False, gated=False, block=True):
     xs, ys = models.linreg_data()
     best = math.inf
     for _ in range(reps + 1):
         ctx = _ctx(N, one_rank)
         ctx.sync()
         t0 = time.perf_counter()
-        acc = models.linreg_statements(ctx, xs, ys, ess_perc_min=1.0, wait_moves=wait_moves, gated=gated)
+        acc = models.linreg_statements(ctx, xs, ys, ess_perc_min=1.0, wait_moves=wait_moves, gated=gated,
+                                       block=block)
         ctx.sync()
         dt = time.perf_counter() - t0
         ev = ctx.log_evidence()
@@ -41,6 +42,7 @@ def c3(N=1_000_000, reps=3, wait_moves=True, one_rank=False, gated=False):
     return {"config": "C3 linear regression + autoRW (N=1M, T=10, ess 1.0)"
                       + ("" if wait_moves or gated else ", asynchronous moves (no accepted counts)")
                       + (", `if resampled` lowered to device-gated moves (no host read in the loop)" if gated else "")
+                      + (", the two Moves as one statement block (wsmc_move_block)" if gated and block else "")
                       + (", sharded path (one-rank RCCL communicator)" if one_rank else ""), "N": N, "T": T,
             "seconds_per_run": best, "particle_steps_per_s": N * T / best, "moves": 2 * T if gated else 2 * len(acc),
             "log_evidence": ev}
@@ -84,6 +86,7 @@ LEGS = {
     "c5_example": lambda: c5(sweeps=1, scheme="stratified", ess=0.5, diversity=0.9),   # as written
     "c3async": lambda: c3(wait_moves=False),
     "c3gated": lambda: c3(gated=True),
+    "c3gated_moves": lambda: c3(gated=True, block=False),                 # two wsmc_move_gated
     "c5async": lambda: c5(wait_moves=False),
     "c3_rccl1": lambda: c3(one_rank=True),
     "c3async_rccl1": lambda: c3(wait_moves=False, one_rank=True),

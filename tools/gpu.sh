@@ -86,7 +86,7 @@ bench)
   step 400 $O/stats.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python bench.py --no-cpu-baseline "$@"
   stats_table $O/stats/run_kernel_stats.csv 8 ;;
 moves)
-  timeout -k 10 400 python tools/bench_moves.py c3 c3async c3gated c5 c5async > $O/moves.jsonl 2> $O/moves.err || { tail $O/moves.err; exit 1; }
+  timeout -k 10 400 python tools/bench_moves.py c3 c3async c3gated_moves c3gated c5 c5async > $O/moves.jsonl 2> $O/moves.err || { tail $O/moves.err; exit 1; }
   cut -c1-330 $O/moves.jsonl
   step 300 $O/c3.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/c3 -o run -- python tools/bench_moves.py c3gated
   stats_table $O/c3/run_kernel_stats.csv 10 ;;
@@ -102,7 +102,7 @@ sq)
              python tools/summarize_pmc.py $O/n$n.json $O/n$n > /dev/null
              sq_table $O/n$n.json prop,fill,sums,final
            done ;;
-    c3|c5) w=$1; [ $w = c3 ] && w=c3async
+    c3|c5) w=$1; [ $w = c3 ] && w=c3gated
            step 300 $O/p.log rocprofv3 --kernel-trace --pmc $SQ --output-format csv -d $O/p -o run -- python tools/bench_moves.py $w
            python tools/summarize_pmc.py $O/p.json $O/p > /dev/null
            sq_table $O/p.json ;;

@@ -426,7 +426,7 @@ int wsmc_create(wsmc_ctx** out, int64_t n_particles, int32_t device, uint64_t se
     ALLOC(c->rec, sizeof(ShardRecord) * kMaxWorld);
     ALLOC(c->dec, sizeof(Decision));
     ALLOC(c->dec_always, sizeof(Decision));
-    ALLOC(c->mom, sizeof(double) * 64);
+    ALLOC(c->mom, sizeof(double) * 128);   // [64..128): a Move block's factors
     ALLOC(c->dflag, sizeof(int32_t) * 4);
     ALLOC(c->ucount, sizeof(unsigned long long) * 4);
     ALLOC(c->d_colptr, sizeof(double*) * kMaxCols);
@@ -491,6 +491,7 @@ int wsmc_destroy(wsmc_ctx* c) {
     for (int32_t* p : c->lineage)
         if (p) (void)hipFree(p);
     if (c->pinned) (void)hipHostFree(c->pinned);
+    if (c->prog_stage) (void)hipHostFree(c->prog_stage);
     if (c->dec_ring) (void)hipHostFree(c->dec_ring);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -2263,6 +2264,17 @@ static bool same_run(const wsmc_term& a, const wsmc_term& b, int kind) {
 static int32_t compile_fold(const std::vector<wsmc_term>& ct, int32_t j0, int32_t j1, std::vector<FoldSeg>& segs,
                             std::vector<double>& cst) {
     const size_t s0 = segs.size();
+    // a constant sigma's log and reciprocal, once here instead of per particle (the shared
+    // functions of the same bits: the values the per-particle memo would give)
+    auto scale_pre = [&](const wsmc_term& t) -> int32_t {
+        const bool scaled = t.dist.family == WSMC_FAM_NORMAL || t.dist.family == WSMC_FAM_HALFNORMAL;
+        if (!scaled || !wsmc_term_is_scalar(&t) || !const_operand(t.dist.scale)) return -1;
+        double pre[2];
+        wsmc_scale_pre(t.dist.scale.c0, pre);
+        cst.push_back(pre[0]);
+        cst.push_back(pre[1]);
+        return (int32_t)cst.size() - 2;
+    };
     for (int32_t j = j0; j < j1;) {
         const int kind = run_kind(ct[j]);
         int32_t e = j + 1;
@@ -2271,11 +2283,20 @@ static int32_t compile_fold(const std::vector<wsmc_term>& ct, int32_t j0, int32_
         // a lone Normal-affine term stays a one-term segment; a lone oscillator term is a run
         // of one (the lean fold carries no generic oscillator evaluation)
         if (kind == kSegTerm || (kind == kSegNormalAff && e - j < 2)) {
-            segs.push_back(FoldSeg{kSegTerm, 1, j, 0});
+            const int32_t so = scale_pre(ct[j]);
+            segs.push_back(FoldSeg{kSegTerm, 1, j, 0, so, 0});
             ++j;
             continue;
         }
-        segs.push_back(FoldSeg{kind, e - j, j, (int32_t)cst.size()});
+        int32_t soff = -1;   // runs are scalar Normals: their sigma
+        if (const_operand(ct[j].dist.scale)) {
+            double pre[2];
+            wsmc_scale_pre(ct[j].dist.scale.c0, pre);
+            soff = (int32_t)cst.size();
+            cst.push_back(pre[0]);
+            cst.push_back(pre[1]);
+        }
+        segs.push_back(FoldSeg{kind, e - j, j, (int32_t)cst.size(), soff, 0});
         for (int32_t k = j; k < e; ++k) {
             const wsmc_term& t = ct[k];
             if (kind == kSegNormalOsc) {   // (t_a, d, m) of the term's rotation block
@@ -2418,25 +2439,68 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         const int32_t nseg_new = compile_fold(ct, 0, kD, segs, cst);
         const int32_t seg_old0 = (int32_t)segs.size();
         const int32_t nseg_old = compile_fold(ct, cache_from >= 0 ? cache_from : 0, kD, segs, cst);
-        // one upload per move: [compiled tape | segments | constants]
-        const size_t ct_bytes = (sizeof(wsmc_term) * ct.size() + 255) & ~(size_t)255;
+        // the templates the segments read, compacted (the fold reads no other term)
+        std::vector<int32_t> tmap(ct.size(), -1);
+        std::vector<wsmc_term> tmpls;
+        for (auto& sg : segs) {
+            if (tmap[sg.tmpl] < 0) {
+                tmap[sg.tmpl] = (int32_t)tmpls.size();
+                tmpls.push_back(ct[sg.tmpl]);
+            }
+            sg.tmpl = tmap[sg.tmpl];
+        }
+        // [templates | segments | constants]: in the kernel's arguments when it fits (no
+        // copy), else one upload through the pinned staging ring
+        const size_t ct_bytes = sizeof(wsmc_term) * tmpls.size();
         const size_t seg_bytes = sizeof(FoldSeg) * segs.size();
         const size_t prog_bytes = ct_bytes + seg_bytes + sizeof(double) * cst.size();
-        if ((int64_t)prog_bytes > c->d_prog_cap) {
-            int64_t cap = c->d_prog_cap ? c->d_prog_cap : 4096;
-            while (cap < (int64_t)prog_bytes) cap *= 2;
-            WSMC_HIP(hipStreamSynchronize(c->stream));
-            if (c->d_prog) WSMC_HIP(hipFree(c->d_prog));
-            WSMC_HIP(hipMalloc(&c->d_prog, cap));
-            c->d_prog_cap = cap;
+        static_assert(sizeof(wsmc_term) % 8 == 0 && sizeof(FoldSeg) % 8 == 0, "program alignment");
+        static const bool no_inline = [] {   // diagnostics only: always upload the program
+            const char* e = getenv("WSMC_DIAG_PROG_COPY");
+            return e && atoi(e) != 0;
+        }();
+        // lean fold: every one-term segment scalar (runs are evaluated by their own code)
+        bool lean = true;
+        for (const auto& sg : segs)
+            if (sg.kind == kSegTerm && !wsmc_term_is_scalar(&tmpls[sg.tmpl])) lean = false;
+        const bool inl = !no_inline && lean && prog_bytes <= sizeof(ProgInline::w);
+        ProgInline pin;
+        char* hp = nullptr;
+        if (inl) {
+            hp = reinterpret_cast<char*>(pin.w);
+            pin.seg_off = (int32_t)ct_bytes;
+            pin.cst_off = (int32_t)(ct_bytes + seg_bytes);
+            pin.seg_old0 = seg_old0;
+            pin.pad = 0;
+        } else {
+            if ((int64_t)prog_bytes > c->d_prog_cap) {
+                int64_t cap = c->d_prog_cap ? c->d_prog_cap : 4096;
+                while (cap < (int64_t)prog_bytes) cap *= 2;
+                WSMC_HIP(hipStreamSynchronize(c->stream));
+                if (c->d_prog) WSMC_HIP(hipFree(c->d_prog));
+                WSMC_HIP(hipMalloc(&c->d_prog, cap));
+                c->d_prog_cap = cap;
+            }
+            const int64_t need = ((int64_t)prog_bytes + 255) & ~(int64_t)255;
+            if (c->prog_stage_at + need > c->prog_stage_cap) {   // wrap: the ring's copies are done
+                WSMC_HIP(hipStreamSynchronize(c->stream));
+                c->prog_stage_at = 0;
+                if (need > c->prog_stage_cap) {
+                    if (c->prog_stage) WSMC_HIP(hipHostFree(c->prog_stage));
+                    c->prog_stage = nullptr;
+                    int64_t cap = std::max<int64_t>(262144, need);
+                    WSMC_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->prog_stage), cap, hipHostMallocDefault));
+                    c->prog_stage_cap = cap;
+                }
+            }
+            hp = c->prog_stage + c->prog_stage_at;
+            c->prog_stage_at += need;
         }
-        std::vector<char> hprog(prog_bytes);
-        if (!ct.empty()) std::memcpy(hprog.data(), ct.data(), sizeof(wsmc_term) * ct.size());
-        if (seg_bytes) std::memcpy(hprog.data() + ct_bytes, segs.data(), seg_bytes);
-        if (!cst.empty())
-            std::memcpy(hprog.data() + ct_bytes + seg_bytes, cst.data(), sizeof(double) * cst.size());
-        if (prog_bytes)
-            WSMC_HIP(hipMemcpyAsync(c->d_prog, hprog.data(), prog_bytes, hipMemcpyHostToDevice, c->stream));
+        if (!tmpls.empty()) std::memcpy(hp, tmpls.data(), ct_bytes);
+        if (seg_bytes) std::memcpy(hp + ct_bytes, segs.data(), seg_bytes);
+        if (!cst.empty()) std::memcpy(hp + ct_bytes + seg_bytes, cst.data(), sizeof(double) * cst.size());
+        if (!inl && prog_bytes)
+            WSMC_HIP(hipMemcpyAsync(c->d_prog, hp, prog_bytes, hipMemcpyHostToDevice, c->stream));
         char* pbase = reinterpret_cast<char*>(c->d_prog);
         const wsmc_term* d_ct = reinterpret_cast<const wsmc_term*>(pbase);
         FoldProgram prog;
@@ -2448,10 +2512,7 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         FoldSlots fs{};
         fs.n = (int32_t)slots.size();
         for (const auto& t : ct) fs.heavy |= t.dist.mean_fn == WSMC_MEAN_OSCILLATOR ? 1 : 0;
-        // lean fold: every one-term segment scalar (runs are evaluated by their own code)
-        fs.lean = 1;
-        for (const auto& sg : segs)
-            if (sg.kind == kSegTerm && !wsmc_term_is_scalar(&ct[sg.tmpl])) fs.lean = 0;
+        fs.lean = lean ? 1 : 0;
         for (size_t s = 0; s < slots.size(); ++s)
             fs.p[s] = c->cols[slots[s].first].front + (int64_t)slots[s].second * c->N;
         for (int k = 0; k < d; ++k) fs.t[k] = c->cols[targets[k]].front;
@@ -2468,7 +2529,7 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         }
         WSMC_HIP(launch_move_c(c->stream, d_ct, kD, target_depth, fs, targets, d, bounded ? l : nullptr,
                                bounded ? h : nullptr, bounded ? 1 : 0, c->mom + 32, c->seed, op_prop, op_acc, c->goff,
-                               c->N, c->ucount, mflag, mc, cache_from, prog));
+                               c->N, c->ucount, mflag, mc, cache_from, prog, inl ? &pin : nullptr));
         if (mc.out != mc.in) std::swap(c->scache, c->scache_back);
         c->scache_anc = nullptr;   // written in slot order now (or refolded from scratch)
         c->scache_dec = nullptr;
@@ -2527,6 +2588,254 @@ int wsmc_move_gated(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32
     const int r = wsmc_move(c, proposal, targets, d, step, lo, hi, target_depth, diversity, nullptr);
     c->move_gate = nullptr;
     return r;
+}
+
+// ---- a block of Moves (wsmc_move_block) -----------------------------------------------------
+// The moves one by one (the definition the fused path reproduces bit for bit)
+static int move_block_each(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, int32_t gated, int64_t* accepted_out) {
+    for (int32_t m = 0; m < n; ++m) {
+        const wsmc_move_spec& sp = specs[m];
+        const double* lo = sp.bounded ? sp.lo : nullptr;
+        const double* hi = sp.bounded ? sp.hi : nullptr;
+        int r;
+        if (gated && !accepted_out) {
+            r = wsmc_move_gated(c, sp.proposal, sp.targets, sp.d, sp.step, lo, hi, sp.target_depth, WSMC_NAN);
+        } else if (gated) {   // counts requested: the host reads the condition
+            if (c->multi) {
+                r = wsmc_move_gated(c, sp.proposal, sp.targets, sp.d, sp.step, lo, hi, sp.target_depth, WSMC_NAN);
+                accepted_out[m] = 0;
+            } else {
+                if ((r = resolve_decisions(c))) return r;
+                if (!c->resampled) {
+                    c->op += 2;
+                    accepted_out[m] = 0;
+                    continue;
+                }
+                r = wsmc_move(c, sp.proposal, sp.targets, sp.d, sp.step, lo, hi, sp.target_depth, WSMC_NAN,
+                              &accepted_out[m]);
+            }
+        } else {
+            r = wsmc_move(c, sp.proposal, sp.targets, sp.d, sp.step, lo, hi, sp.target_depth, WSMC_NAN,
+                          accepted_out ? &accepted_out[m] : nullptr);
+        }
+        if (r) return r;
+    }
+    return WSMC_OK;
+}
+
+int wsmc_move_block(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, int32_t gated, int64_t* accepted_out) {
+    if (!c) return fail(WSMC_EARG, "null context");
+    if (n < 0 || (n > 0 && !specs)) return fail(WSMC_EARG, "move block needs n >= 0 specs");
+    if (accepted_out)
+        for (int32_t m = 0; m < n; ++m) accepted_out[m] = 0;
+    if (n == 0) return WSMC_OK;
+    if (c->multi) return move_block_each(c, n, specs, gated, accepted_out);
+    CHECK_CTX_KEEP(c);
+    // the fused path: autoRW Moves on disjoint scalar targets (4 in all), one target depth, one
+    // GPU, a lean fold program small enough for the kernel's arguments
+    int32_t depth = specs[0].target_depth < 0 ? c->depth : specs[0].target_depth;
+    bool fuse = !is_sharded(c) && n <= 4 && !c->move_gate;
+    int32_t D = 0;
+    int32_t utg[4] = {0, 0, 0, 0};
+    MoveBlk mb{};
+    mb.nm = n;
+    double ulo[4], uhi[4];
+    for (int32_t m = 0; m < n && fuse; ++m) {
+        const wsmc_move_spec& sp = specs[m];
+        const int32_t dm = sp.target_depth < 0 ? c->depth : sp.target_depth;
+        if (sp.proposal != WSMC_PROPOSAL_AUTORW || sp.d < 1 || sp.d > 4 || D + sp.d > 4 || dm != depth) {
+            fuse = false;
+            break;
+        }
+        mb.off[m] = D;
+        bool bounded = false;
+        for (int k = 0; k < sp.d; ++k) {
+            const int32_t t = sp.targets[k];
+            if (!valid_col(c, t) || c->cols[t].dim != 1) return fail(WSMC_EARG, "move targets must be existing scalar columns");
+            for (int u = 0; u < D; ++u)
+                if (utg[u] == t) fuse = false;   // overlapping targets: the moves one by one
+            for (int j = 0; j < k; ++j)
+                if (sp.targets[j] == t) fuse = false;
+            if (sp.bounded && (std::isfinite(sp.lo[k]) || std::isfinite(sp.hi[k]))) bounded = true;
+        }
+        for (int k = 0; k < sp.d; ++k) {
+            utg[D + k] = sp.targets[k];
+            ulo[D + k] = bounded ? sp.lo[k] : -INFINITY;
+            uhi[D + k] = bounded ? sp.hi[k] : INFINITY;
+            mb.bnd[D + k] = bounded ? 1 : 0;
+        }
+        mb.min_step[m] = sp.step;
+        D += sp.d;
+    }
+    if (!fuse) return move_block_each(c, n, specs, gated, accepted_out);
+    mb.off[n] = D;
+    for (int u = D; u < 4; ++u) {
+        ulo[u] = -INFINITY;
+        uhi[u] = INFINITY;
+    }
+    // the fold program over the union's slots (targets first), compiled before anything runs
+    int32_t kD = 0;
+    while (kD < (int32_t)c->tape.size() && c->tape[kD].depth < depth) ++kD;
+    const int32_t cache_from = (c->scache && c->scache_terms >= 0 && c->scache_terms <= kD) ? c->scache_terms : -1;
+    std::vector<std::pair<int32_t, int32_t>> slots;
+    auto slot_of = [&](int32_t col, int32_t comp) -> int32_t {
+        for (size_t q = 0; q < slots.size(); ++q)
+            if (slots[q].first == col && slots[q].second == comp) return (int32_t)q;
+        slots.emplace_back(col, comp);
+        return (int32_t)slots.size() - 1;
+    };
+    for (int u = 0; u < D; ++u) slot_of(utg[u], 0);
+    std::vector<wsmc_term> ct(c->tape.begin(), c->tape.begin() + kD);
+    auto remap = [&](wsmc_operand& o) {
+        for (int k = 0; k < 2; ++k)
+            if (o.col[k] >= 0) {
+                o.col[k] = slot_of(o.col[k], o.comp[k]);
+                o.comp[k] = 0;
+            }
+    };
+    for (auto& t : ct) {
+        for (int k = 0; k < 4; ++k) { remap(t.x[k]); remap(t.dist.mu[k]); }
+        remap(t.dist.scale);
+    }
+    std::vector<FoldSeg> segs;
+    std::vector<double> cst;
+    const int32_t nseg_new = compile_fold(ct, 0, kD, segs, cst);
+    const int32_t seg_old0 = (int32_t)segs.size();
+    const int32_t nseg_old = compile_fold(ct, cache_from >= 0 ? cache_from : 0, kD, segs, cst);
+    std::vector<int32_t> tmap(ct.size(), -1);
+    std::vector<wsmc_term> tmpls;
+    for (auto& sg : segs) {
+        if (tmap[sg.tmpl] < 0) {
+            tmap[sg.tmpl] = (int32_t)tmpls.size();
+            tmpls.push_back(ct[sg.tmpl]);
+        }
+        sg.tmpl = tmap[sg.tmpl];
+    }
+    bool lean = (int)slots.size() <= kFoldSlots;
+    for (const auto& sg : segs)
+        if (sg.kind == kSegTerm && !wsmc_term_is_scalar(&tmpls[sg.tmpl])) lean = false;
+    const size_t ct_bytes = sizeof(wsmc_term) * tmpls.size();
+    const size_t seg_bytes = sizeof(FoldSeg) * segs.size();
+    const size_t prog_bytes = ct_bytes + seg_bytes + sizeof(double) * cst.size();
+    if (!lean || prog_bytes > sizeof(ProgInline::w)) return move_block_each(c, n, specs, gated, accepted_out);
+
+    // the condition: the newest Resample still pending on the device, else the host flag
+    const Decision* gate = nullptr;
+    if (gated) {
+        gate = c->dec_pending > 0 && !c->dec_rows.empty() ? c->dec_rows.back().row.dec : nullptr;
+        if (!gate && !c->resampled) {   // does not run: the op counters are consumed all the same
+            c->op += 2 * (uint64_t)n;
+            return WSMC_OK;
+        }
+    }
+    for (int32_t m = 0; m < n; ++m) {
+        mb.op_prop[m] = c->op++;
+        mb.op_acc[m] = c->op++;
+    }
+    // columns: current, one lazy Resample behind (read through its row by the kernels, no
+    // trace), or further behind (brought up to date first)
+    std::vector<int32_t> reads;
+    for (const auto& sl : slots) reads.push_back(sl.first);
+    const bool has_lag_row = c->lazy && !c->alog.empty() && c->epoch - 1 >= c->log_base;
+    const AncRow* lrow = has_lag_row ? &c->alog.back() : nullptr;
+    std::vector<int32_t> far;
+    for (int32_t id : reads) {
+        c->cols[id].touch = c->epoch;
+        const int64_t e = c->cols[id].epoch;
+        if (e < c->epoch && !(lrow && e == c->epoch - 1)) far.push_back(id);
+    }
+    int r;
+    if (!far.empty() && (r = materialize(c, &far))) return r;
+    int lag_slots = 0, lag_targets = 0;
+    for (size_t q = 0; q < slots.size(); ++q)
+        if (c->cols[slots[q].first].epoch == c->epoch - 1 && lrow) lag_slots |= 1 << q;
+    lag_targets = lag_slots & ((1 << D) - 1);
+    if ((r = upload_colptr(c))) return r;
+    const bool async = !accepted_out;
+    if (!async && (r = check_deferred(c))) return r;
+    if (!c->move_pending && !c->dflag_zero) WSMC_HIP(hipMemsetAsync(c->dflag, 0, sizeof(int32_t) * 4, c->stream));
+    if (accepted_out) WSMC_HIP(hipMemsetAsync(c->ucount, 0, sizeof(unsigned long long) * 4, c->stream));
+    // one moments pass over the union of the targets, one combine into every move's factor
+    const bool kept = c->cur_max && c->cur_max_seq == c->wseq;
+    MaxSlots* mms = kept ? c->cur_max : c->mslots;
+    if (!kept) {
+        if (c->w_reset_pending) {
+            WSMC_HIP(launch_fill_weights(c->stream, c->w, c->w_reset_pending, c->N));
+            c->w_reset_pending = nullptr;
+        }
+        WSMC_HIP(hipMemsetAsync(c->mslots, 0, sizeof(MaxSlots), c->stream));
+        WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, c->mslots));
+    }
+    WSMC_HIP(launch_autorw_moments(c->stream, c->w, mms, c->d_colptr, utg, D, ulo, uhi, nullptr, c->N, c->tilepart,
+                                   c->w_reset_pending, gate, lrow ? lrow->anc : nullptr, lrow ? lrow->dec : nullptr,
+                                   lag_targets));
+    WSMC_HIP(launch_autorw_final_blk(c->stream, c->tilepart, c->ntiles, mb, c->mom, c->dflag, gate));
+    c->dflag_zero = false;
+    if (!c->scache) {
+        WSMC_HIP(hipMalloc(&c->scache, sizeof(double) * c->N));
+        WSMC_HIP(hipMalloc(&c->scache_back, sizeof(double) * c->N));
+    }
+    // the program in the kernel's arguments
+    ProgInline pin;
+    char* hp = reinterpret_cast<char*>(pin.w);
+    pin.seg_off = (int32_t)ct_bytes;
+    pin.cst_off = (int32_t)(ct_bytes + seg_bytes);
+    pin.seg_old0 = seg_old0;
+    pin.pad = 0;
+    if (!tmpls.empty()) std::memcpy(hp, tmpls.data(), ct_bytes);
+    if (seg_bytes) std::memcpy(hp + ct_bytes, segs.data(), seg_bytes);
+    if (!cst.empty()) std::memcpy(hp + ct_bytes + seg_bytes, cst.data(), sizeof(double) * cst.size());
+    FoldSlots fs{};
+    fs.n = (int32_t)slots.size();
+    for (const auto& t : tmpls) fs.heavy |= t.dist.mean_fn == WSMC_MEAN_OSCILLATOR ? 1 : 0;
+    fs.lean = 1;
+    for (size_t q = 0; q < slots.size(); ++q)
+        fs.p[q] = c->cols[slots[q].first].front + (int64_t)slots[q].second * c->N;
+    for (int u = 0; u < D; ++u) {
+        Column& col = c->cols[utg[u]];
+        fs.t[u] = col.front;
+        mb.tcol[u] = utg[u];
+        mb.tout[u] = ((lag_targets >> u) & 1) ? col.back : col.front;
+    }
+    mb.lag_targets = lag_targets;
+    MoveCarry mc;
+    mc.in = c->scache;
+    mc.out = c->scache;
+    mc.gate = gate;
+    if (c->scache_anc && cache_from >= 0) {
+        mc.anc = c->scache_anc;
+        mc.dec = c->scache_dec;
+        mc.out = c->scache_back;
+    }
+    WSMC_HIP(launch_move_blk(c->stream, pin, nseg_new, nseg_old, fs, ulo, uhi, mb, c->mom + 64, c->seed, c->goff, c->N,
+                             accepted_out ? c->ucount : nullptr, c->dflag, mc, cache_from, lrow ? lrow->anc : nullptr,
+                             lrow ? lrow->dec : nullptr, lag_slots, c->d_colptr));
+    if (mc.out != mc.in) std::swap(c->scache, c->scache_back);
+    c->scache_anc = nullptr;
+    c->scache_dec = nullptr;
+    c->scache_lag_epoch = -1;
+    c->scache_terms = kD;
+    for (int u = 0; u < D; ++u) {   // the moved targets are current (the lagged ones in their back buffers)
+        Column& col = c->cols[utg[u]];
+        if ((lag_targets >> u) & 1) std::swap(col.front, col.back);
+        wrote_col(c, utg[u]);
+    }
+    gc_log(c);
+    if (async) {
+        c->move_pending = true;
+        return WSMC_OK;
+    }
+    struct {
+        int32_t flag[4];
+        unsigned long long acc[4];
+    }* hb = reinterpret_cast<decltype(hb)>(c->pinned);
+    WSMC_HIP(hipMemcpyAsync(hb->flag, c->dflag, sizeof(int32_t) * 4, hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipMemcpyAsync(hb->acc, c->ucount, sizeof(unsigned long long) * 4, hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipStreamSynchronize(c->stream));
+    for (int32_t m = 0; m < n; ++m) accepted_out[m] = (int64_t)hb->acc[m];
+    if (hb->flag[0]) return fail(WSMC_ENOTPD, "autoRW proposal covariance is not positive definite");
+    c->dflag_zero = true;   // (flag[2] is rewritten by every block's combine before it is read)
+    return WSMC_OK;
 }
 
 // ---- fused 2D SSM runner --------------------------------------------------------------

@@ -226,6 +226,8 @@ struct wsmc_ctx {
     int64_t d_ctape_cap = 0;
     void* d_prog = nullptr;                 // compiled fold program: segments, then constants
     int64_t d_prog_cap = 0;                 // bytes
+    char* prog_stage = nullptr;             // pinned staging ring of the programs too large to ride
+    int64_t prog_stage_cap = 0, prog_stage_at = 0;   // in the Move's arguments (ProgInline)
     unsigned long long* rs_grp[2] = {nullptr, nullptr};   // generic Resample's group lines (double-buffered)
     int rs_grp_cur = 0;
     size_t d_comp_cap = 0;
@@ -394,6 +396,9 @@ struct FoldSeg {
     int32_t count;   // terms in the segment
     int32_t tmpl;    // index of its first term in the compiled tape
     int32_t coff;    // offset of its constants: Osc (t, y) per term; Aff (c0, coef0, coef1, y) per term
+    int32_t soff;    // a constant scale: offset of its (log sigma, 1/sigma) in the constants
+                     // (wsmc_scale_pre, evaluated once on the host), else -1
+    int32_t pad;     // 24 B: the constants after the segments stay 8-aligned
 };
 struct FoldProgram {
     const FoldSeg* seg_new;    // the s_new fold, terms [0, n)
@@ -411,11 +416,39 @@ struct MoveCarry {
     const Decision* gate = nullptr;   // a gated Move (wsmc_move_gated): only the scores are carried
                                       // on when !gate->resampled
 };
+// a lean fold program small enough to travel in the Move kernel's own arguments (read from
+// the kernarg segment with scalar loads): no upload copy per Move. Layout as the device
+// program: [templates | segments | constants], offsets in bytes
+constexpr int kProgInlineWords = 416;   // 3328 B (the kernel's other arguments stay under 4 KB)
+struct ProgInline {
+    int32_t seg_off, cst_off, seg_old0, pad;
+    unsigned long long w[kProgInlineWords];
+};
+// a block of autoRW Moves on disjoint targets in one pass (wsmc_move_block): union targets
+// u = 0..D-1 (the fold's slots 0..D-1), move m owns [off[m], off[m+1])
+struct MoveBlk {
+    int32_t nm;
+    int32_t off[5];
+    int32_t bnd[4];              // per union target: the bounded transform applies
+    int32_t tcol[4];             // column ids (device table entries moved to tout when lagged)
+    int32_t lag_targets;         // bit u: target u read through the lag row, written in full to tout
+    int32_t pad;
+    double min_step[4];          // per move
+    unsigned long long op_prop[4], op_acc[4];
+    double* tout[4];             // per union target: where its values go
+};
+hipError_t launch_autorw_final_blk(hipStream_t s, const double* tilepart, int64_t ntiles, const MoveBlk& mb,
+                                   double* mom, int32_t* flag, const Decision* gate);
+hipError_t launch_move_blk(hipStream_t s, const ProgInline& pin, int32_t nseg_new, int32_t nseg_old, const FoldSlots& fs,
+                           const double* lo, const double* hi, const MoveBlk& mb, const double* Lb, uint64_t seed,
+                           int64_t goff, int64_t N, unsigned long long* accepted, const int32_t* flag,
+                           const MoveCarry& mc, int32_t cache_from, const int32_t* lag_anc, const Decision* lag_dec,
+                           int lag_mask, double** tab);
 hipError_t launch_move_c(hipStream_t s, const wsmc_term* ctape, int32_t nterms, int32_t depth, const FoldSlots& fs,
                          const int32_t* tcols, int d, const double* lo, const double* hi, int bounded,
                          const double* L, uint64_t seed, uint64_t op_prop, uint64_t op_acc, int64_t goff, int64_t N,
                          unsigned long long* accepted, const int32_t* flag, const MoveCarry& mc, int32_t cache_from,
-                         const FoldProgram& prog);
+                         const FoldProgram& prog, const ProgInline* pin = nullptr);
 // exact-sharded fused run: contiguous slices of (x pair, ancestor) by global index for the
 // distributed trace-back, the lineage lookup, pairs -> SoA
 hipError_t launch_trace_pack(hipStream_t s, const double* xpairs, const int32_t* arow, int64_t start, int64_t count,
@@ -445,7 +478,8 @@ hipError_t launch_max_publish(hipStream_t s, const MaxSlots* ms, unsigned long l
 hipError_t launch_autorw_moments(hipStream_t s, const double* w, const MaxSlots* ms, double* const* cols,
                                  const int32_t* tcols, int d, const double* lo, const double* hi,
                                  const unsigned long long* pv, int64_t N, double* tilepart,
-                                 const Decision* wreset = nullptr, const Decision* gate = nullptr);
+                                 const Decision* wreset = nullptr, const Decision* gate = nullptr,
+                                 const int32_t* lag_anc = nullptr, const Decision* lag_dec = nullptr, int lag_mask = 0);
 hipError_t launch_autorw_final(hipStream_t s, const double* tilepart, int64_t ntiles, int d, double min_step,
                                double* mom, int32_t* flag, int raw, const Decision* gate = nullptr);
 hipError_t launch_autorw_publish(hipStream_t s, const MaxSlots* ms, double* const* cols, const int32_t* tcols, int d,

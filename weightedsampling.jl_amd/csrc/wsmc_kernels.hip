@@ -1692,6 +1692,12 @@ struct MomArgs {
     int32_t use_ex;          // analysis moments: values are operand expressions (identity transform)
     wsmc_operand ex[4];
 };
+// targets one lazy Resample behind (bit k of mask: target k read through anc when dec resampled)
+struct MomLag {
+    const int32_t* anc;
+    const Decision* dec;
+    int32_t mask;
+};
 
 // one block: canonical combine of tile partials; pass 1 -> mom[0..d) = mean, mom[8] = S0;
 // pass 2 -> mom[16..16+d*d) = lambda*Sigma (zeros -> min_step), mom[32..32+d*d) = chol
@@ -1860,7 +1866,7 @@ template <int D>
 __global__ __launch_bounds__(kBlock) void k_moments1(const double* __restrict__ w, const MaxSlots* ms,
                                                      double* const* cols, MomArgs ma, const u64* pv, int64_t N,
                                                      int64_t ntiles, double* tilepart, const Decision* wreset,
-                                                     const Decision* gate) {
+                                                     const Decision* gate, MomLag lg) {
     constexpr int d = D, NV = 1 + D + D * (D + 1) / 2;
     __shared__ double lds4[4];
     if (gate && !gate->resampled) return;   // a gated Move that does not run
@@ -1868,23 +1874,54 @@ __global__ __launch_bounds__(kBlock) void k_moments1(const double* __restrict__ 
     // a fused Resample's weight reset still pending (the next Observe applies it): the
     // weights are its log-mean, all equal (the max slots already hold it)
     const bool reset = wreset && wreset->resampled;
-    const double wr = reset ? wreset->mean : 0.0;
+    // all equal: one exp for the block (the same bits every particle's would give)
+    const double er = reset ? wsmc_exp(wreset->mean - M) : 0.0;
+    // targets one lazy Resample behind (lg.mask): read through its ancestors, gated by its
+    // decision (the values the trace would have gathered)
+    const int lmask = (lg.anc && lg.dec->resampled) ? lg.mask : 0;
+    const double* tp[D];
+#pragma unroll
+    for (int k = 0; k < d; ++k) tp[k] = cols[ma.tcol[k]];
     double p[4];
-    autorw_pivot<D>(cols, ma, pv, p);
+    if (pv) {
+        autorw_pivot<D>(cols, ma, pv, p);
+    } else {
+        const int64_t i0 = lmask ? (int64_t)lg.anc[0] : 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) p[k] = k < d ? wsmc_to_unc(tp[k][(lmask >> k) & 1 ? i0 : 0], ma.lo[k], ma.hi[k]) : 0.0;
+    }
     const int64_t base = (int64_t)blockIdx.x * kTile;
     double acc[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) acc[v] = 0.0;
+    // every load of the tile first (one memory latency per thread, not kItems in a row),
+    // then the canonical per-item accumulation
+    double xv[kItems][D], wv[kItems];
+    int64_t ai[kItems];
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+        const int64_t i = base + (int64_t)j * kBlock + threadIdx.x;
+        ai[j] = (lmask && i < N) ? (int64_t)lg.anc[i] : i;
+    }
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+        const int64_t i = base + (int64_t)j * kBlock + threadIdx.x;
+        const bool in = i < N;
+        wv[j] = (in && !reset) ? w[i] : 0.0;
+#pragma unroll
+        for (int k = 0; k < d; ++k) xv[j][k] = in ? tp[k][(lmask >> k) & 1 ? ai[j] : i] : 0.0;
+    }
+#pragma unroll
     for (int j = 0; j < kItems; ++j) {
         const int64_t i = base + (int64_t)j * kBlock + threadIdx.x;
         double vals[NV];
 #pragma unroll
         for (int v = 0; v < NV; ++v) vals[v] = 0.0;
         if (i < N) {
-            const double e = wsmc_exp((reset ? wr : w[i]) - M);
+            const double e = reset ? er : wsmc_exp(wv[j] - M);
             double dz[4];
 #pragma unroll
-            for (int k = 0; k < d; ++k) dz[k] = wsmc_to_unc(cols[ma.tcol[k]][i], ma.lo[k], ma.hi[k]) - p[k];
+            for (int k = 0; k < d; ++k) dz[k] = wsmc_to_unc(xv[j][k], ma.lo[k], ma.hi[k]) - p[k];
             vals[0] = e;
 #pragma unroll
             for (int k = 0; k < d; ++k) vals[1 + k] = e * dz[k];
@@ -2054,8 +2091,13 @@ __device__ __forceinline__ void fold_seg(double (&s)[K], const wsmc_term* tape, 
                 om[p] = wsmc_operand_eval(&tp->dist.mu[1], cols, 0, ix[p], nullptr);
                 ga[p] = wsmc_operand_eval(&tp->dist.mu[2], cols, 0, ix[p], nullptr);
                 ph[p] = wsmc_operand_eval(&tp->dist.mu[3], cols, 0, ix[p], nullptr);
-                const double sd = wsmc_operand_eval(&tp->dist.scale, cols, 0, ix[p], nullptr);
-                wsmc_scale_memo(&lm[p], sd, &lsd[p], &rsd[p]);
+                if (sg.soff >= 0) {   // a constant sigma: its pair from the host (uniform branch)
+                    lsd[p] = cst[sg.soff];
+                    rsd[p] = cst[sg.soff + 1];
+                } else {
+                    wsmc_scale_memo(&lm[p], wsmc_operand_eval(&tp->dist.scale, cols, 0, ix[p], nullptr), &lsd[p],
+                                    &rsd[p]);
+                }
             }
             // the mean by rotation (wsmc_osc_rolled's operations): a block's first term (m = 0)
             // is the direct phasor, each next term of the block one complex multiply by R; a
@@ -2105,8 +2147,13 @@ __device__ __forceinline__ void fold_seg(double (&s)[K], const wsmc_term* tape, 
             for (int p = 0; p < K; ++p) {
                 v0[p] = h0 ? cols[m.col[0]][ix[p]] : 0.0;
                 v1[p] = h1 ? cols[m.col[1]][ix[p]] : 0.0;
-                const double sd = wsmc_operand_eval(&tp->dist.scale, cols, 0, ix[p], nullptr);
-                wsmc_scale_memo(&lm[p], sd, &lsd[p], &rsd[p]);
+                if (sg.soff >= 0) {
+                    lsd[p] = cst[sg.soff];
+                    rsd[p] = cst[sg.soff + 1];
+                } else {
+                    wsmc_scale_memo(&lm[p], wsmc_operand_eval(&tp->dist.scale, cols, 0, ix[p], nullptr), &lsd[p],
+                                    &rsd[p]);
+                }
             }
             const double* c = cst + sg.coff;
             for (int32_t k = 0; k < sg.count; ++k) {
@@ -2124,9 +2171,10 @@ __device__ __forceinline__ void fold_seg(double (&s)[K], const wsmc_term* tape, 
             continue;
         }
         if (LEAN) {
+            const double* pre = sg.soff >= 0 ? cst + sg.soff : nullptr;
 #pragma unroll
             for (int p = 0; p < K; ++p)
-                if (ok[p]) s[p] = s[p] + wsmc_scalar_term_logpdf_m(tp, cols, 0, ix[p], nullptr, &lm[p]);
+                if (ok[p]) s[p] = s[p] + wsmc_scalar_term_logpdf_p(tp, cols, 0, ix[p], nullptr, &lm[p], pre);
             continue;
         }
 #pragma unroll
@@ -2139,13 +2187,13 @@ __device__ __forceinline__ void fold_seg(double (&s)[K], const wsmc_term* tape, 
 // thread: slot values staged once in LDS ([slot][K * kBlock]), proposals in their own LDS
 // rows so the s_new fold reads them through its own pointer table (no override lookups).
 template <int K, int LEAN>
-__global__ __launch_bounds__(kBlock) void k_move_c(const wsmc_term* ctape, int32_t nterms, int32_t depth,
-                                                   FoldSlots fs, MomArgs ma, int d, int bounded, const double* Lm,
-                                                   uint64_t seed, uint64_t op_prop, uint64_t op_acc, int64_t goff,
-                                                   int64_t N, u64* accepted, const int32_t* flag, MoveCarry mc,
-                                                   int32_t cache_from, FoldProgram prog) {
+__device__ __forceinline__ void move_c_body(const wsmc_term* ctape, const FoldSlots& fs, const MomArgs& ma, int d,
+                                            int bounded, const double* Lm, uint64_t seed, uint64_t op_prop,
+                                            uint64_t op_acc, int64_t goff, int64_t N, u64* accepted,
+                                            const int32_t* flag, const MoveCarry& mc, int32_t cache_from,
+                                            const FoldProgram& prog) {
     constexpr int W = K * kBlock;            // LDS row length
-    extern __shared__ double sv[];           // [fs.n][W] current values, then [4][W] proposals
+    extern __shared__ double sv[];           // [fs.n][W] current values, then [d][W] proposals
     __shared__ double* sp[kFoldSlots];
     __shared__ double* spn[kFoldSlots];
     __shared__ u64 lds4[4];
@@ -2228,6 +2276,208 @@ __global__ __launch_bounds__(kBlock) void k_move_c(const wsmc_term* ctape, int32
     }
     acc = block_sum_u64(acc, lds4);
     if (threadIdx.x == 0 && acc) atomicAdd(accepted, acc);
+}
+template <int K, int LEAN>
+__global__ __launch_bounds__(kBlock) void k_move_c(const wsmc_term* ctape, FoldSlots fs, MomArgs ma, int d,
+                                                   int bounded, const double* Lm, uint64_t seed, uint64_t op_prop,
+                                                   uint64_t op_acc, int64_t goff, int64_t N, u64* accepted,
+                                                   const int32_t* flag, MoveCarry mc, int32_t cache_from,
+                                                   FoldProgram prog) {
+    move_c_body<K, LEAN>(ctape, fs, ma, d, bounded, Lm, seed, op_prop, op_acc, goff, N, accepted, flag, mc,
+                         cache_from, prog);
+}
+// the program in the kernel's arguments (ProgInline, the first argument: offset 0 of the
+// kernarg segment): its templates, segments and constants are read in place through the
+// segment pointer with scalar loads (naming the by-value argument would copy it to scratch)
+template <int K, int LEAN>
+__global__ __launch_bounds__(kBlock) void k_move_ci(ProgInline, FoldSlots fs, MomArgs ma, int d, int bounded,
+                                                    const double* Lm, uint64_t seed, uint64_t op_prop,
+                                                    uint64_t op_acc, int64_t goff, int64_t N, u64* accepted,
+                                                    const int32_t* flag, MoveCarry mc, int32_t cache_from,
+                                                    int32_t nseg_new, int32_t nseg_old) {
+    const char* ka = (const char*)__builtin_amdgcn_kernarg_segment_ptr();
+    const int32_t* hdr = reinterpret_cast<const int32_t*>(ka);   // seg_off, cst_off, seg_old0
+    const char* b = ka + offsetof(ProgInline, w);
+    FoldProgram prog;
+    prog.seg_new = reinterpret_cast<const FoldSeg*>(b + hdr[0]);
+    prog.seg_old = prog.seg_new + hdr[2];
+    prog.nseg_new = nseg_new;
+    prog.nseg_old = nseg_old;
+    prog.cst = reinterpret_cast<const double*>(b + hdr[1]);
+    move_c_body<K, LEAN>(reinterpret_cast<const wsmc_term*>(b), fs, ma, d, bounded, Lm, seed, op_prop, op_acc, goff,
+                         N, accepted, flag, mc, cache_from, prog);
+}
+
+// ---- a block of Moves in one pass (wsmc_move_block) ----------------------------------------
+// Consecutive autoRW Moves on disjoint targets with one fold (the same target depth): each
+// move's covariance reads only its own targets and the weights, which the earlier moves of
+// the block leave alone, so one moments pass over the union of the targets serves them all
+// (each move's totals are a sub-block of the union's: the same per-value arithmetic, order
+// and tile combine as a pass over its targets alone), and one kernel runs the moves one after
+// the other per particle — the later moves' folds see the earlier moves' accepted values and
+// continue from their scores, as the sequential Moves do.
+// The factors: move m's at mom[64 + 16 m ..]; flag[0] = 1 if one is not PD, flag[2] = the
+// moves that run (those before the first non-PD one; 0 when an earlier failure is pending).
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_autorw_final_blk(const double* tilepart, int64_t ntiles, MoveBlk mb,
+                                                             double* mom, int32_t* flag, const Decision* gate) {
+    constexpr int NV = 1 + D + D * (D + 1) / 2;
+    __shared__ double lds4[4];
+    __shared__ double tot[NV];
+    if (gate && !gate->resampled) return;
+    for (int v = 0; v < NV; ++v) {
+        double acc = 0.0;
+        for (int64_t b = threadIdx.x; b < ntiles; b += kBlock) acc = acc + tilepart[(int64_t)v * ntiles + b];
+        const double s = block_sum_canon(acc, lds4);
+        if (threadIdx.x == 0) tot[v] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    const int prior = flag[0];
+    int nrun = mb.nm;
+    for (int m = 0; m < mb.nm; ++m) {
+        const int o = mb.off[m], dm = mb.off[m + 1] - o;
+        double sub[15];
+        sub[0] = tot[0];
+        for (int k = 0; k < dm; ++k) sub[1 + k] = tot[1 + o + k];
+        int v = 1 + dm;
+        for (int a = 0; a < dm; ++a)
+            for (int b = a; b < dm; ++b) {
+                const int ua = o + a, ub = o + b;
+                int pi = 0;   // (ua, ub) in the union's a <= b enumeration
+                for (int x = 0; x < ua; ++x) pi += D - x;
+                sub[v++] = tot[1 + D + pi + (ub - ua)];
+            }
+        double S[16], L[16];
+        const int ok = wsmc_autorw_factor(sub, dm, mb.min_step[m], S, L);
+        for (int k = 0; k < 16; ++k) mom[64 + 16 * m + k] = k < dm * dm ? L[k] : 0.0;
+        if (!ok) {
+            flag[0] = 1;
+            nrun = m;
+            break;
+        }
+    }
+    flag[2] = prior ? 0 : nrun;
+}
+
+template <int K, int LEAN>
+__global__ __launch_bounds__(kBlock) void k_move_blk(ProgInline, FoldSlots fs, MomArgs ma, MoveBlk mb, const double* Lb,
+                                                     uint64_t seed, int64_t goff, int64_t N, u64* accepted,
+                                                     const int32_t* flag, MoveCarry mc, int32_t cache_from,
+                                                     int32_t nseg_new, int32_t nseg_old, MomLag lg, double** tab) {
+    // the program in the kernarg segment (k_move_ci)
+    const char* ka = (const char*)__builtin_amdgcn_kernarg_segment_ptr();
+    const int32_t* hdr = reinterpret_cast<const int32_t*>(ka);
+    const char* pb = ka + offsetof(ProgInline, w);
+    const wsmc_term* ctape = reinterpret_cast<const wsmc_term*>(pb);
+    const FoldSeg* seg_new = reinterpret_cast<const FoldSeg*>(pb + hdr[0]);
+    const FoldSeg* seg_old = seg_new + hdr[2];
+    const double* cst = reinterpret_cast<const double*>(pb + hdr[1]);
+
+    constexpr int W = K * kBlock;
+    extern __shared__ double sv[];           // [fs.n][W] current values, then [D][W] proposals
+    __shared__ double* sp[kFoldSlots];
+    __shared__ double* spn[4][kFoldSlots];
+    __shared__ u64 lds4[4];
+    const int th = threadIdx.x;
+    const int nm = mb.nm;
+    double* prop = sv + fs.n * W;
+    if (th < fs.n) {
+        sp[th] = sv + th * W;
+        for (int m = 0; m < nm; ++m)
+            spn[m][th] = (th >= mb.off[m] && th < mb.off[m + 1]) ? prop + th * W : sv + th * W;
+    }
+    int ix[K];
+    bool ok[K];
+    int64_t gi[K], ai[K];
+    // slots one lazy Resample behind read through its ancestors (gated by its decision), as
+    // are the carried scores (MoveCarry)
+    const int smask = (lg.anc && lg.dec->resampled) ? lg.mask : 0;
+    const bool slag = mc.anc && mc.dec->resampled;
+    const int32_t* arow = smask ? lg.anc : mc.anc;
+#pragma unroll
+    for (int p = 0; p < K; ++p) {
+        ix[p] = p * kBlock + th;
+        gi[p] = (int64_t)blockIdx.x * W + ix[p];
+        ok[p] = gi[p] < N;
+        ai[p] = (ok[p] && (smask || slag)) ? (int64_t)arow[gi[p]] : gi[p];
+    }
+    for (int sl = 0; sl < fs.n; ++sl)
+#pragma unroll
+        for (int p = 0; p < K; ++p)
+            sv[sl * W + ix[p]] = ok[p] ? fs.p[sl][(smask >> sl) & 1 ? ai[p] : gi[p]] : 0.0;
+    double so[K], sn[K], lpr[K];
+    int chg[K];
+#pragma unroll
+    for (int p = 0; p < K; ++p) {
+        so[p] = (ok[p] && cache_from >= 0) ? mc.in[slag ? ai[p] : gi[p]] : 0.0;
+        chg[p] = 0;
+    }
+    const bool run = !mc.gate || mc.gate->resampled;
+    const int nrun = run ? flag[2] : 0;   // the final's count (uniform)
+    __syncthreads();
+    fold_seg<K, LEAN>(so, ctape, seg_old, nseg_old, cst, sp, ix, ok);
+    for (int m = 0; m < nrun; ++m) {
+        const int o = mb.off[m], dm = mb.off[m + 1] - o;
+        u64 acc = 0;
+        const double* Lm = Lb + 16 * m;
+#pragma unroll
+        for (int p = 0; p < K; ++p) {
+            sn[p] = 0.0;
+            lpr[p] = 0.0;
+            if (!ok[p]) continue;
+            double xi[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int k = 0; k < 4; k += 2)
+                if (k < dm)
+                    wsmc_normal_pair(wsmc_rng_block(seed, mb.op_prop[m], (uint64_t)(goff + gi[p]), (uint32_t)(k >> 1)),
+                                     &xi[k], &xi[k + 1]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (k >= dm) break;
+                const int u = o + k;
+                double dz = 0.0;
+#pragma unroll
+                for (int j = 0; j <= k; ++j) dz = dz + Lm[k * dm + j] * xi[j];
+                const double x = sv[u * W + ix[p]];
+                const bool bd = mb.bnd[u] != 0;
+                const double zo = bd ? wsmc_to_unc(x, ma.lo[u], ma.hi[u]) : x;
+                const double zn = zo + dz;
+                const double xn = bd ? wsmc_from_unc(zn, ma.lo[u], ma.hi[u]) : zn;
+                if (bd)
+                    lpr[p] = lpr[p] + (wsmc_log_abs_jac(zn, ma.lo[u], ma.hi[u]) - wsmc_log_abs_jac(zo, ma.lo[u], ma.hi[u]));
+                prop[u * W + ix[p]] = xn;
+            }
+        }
+        fold_seg<K, LEAN>(sn, ctape, seg_new, nseg_new, cst, spn[m], ix, ok);
+#pragma unroll
+        for (int p = 0; p < K; ++p) {
+            if (!ok[p]) continue;
+            const double uu = wsmc_uniform_k(seed, mb.op_acc[m], (uint64_t)(goff + gi[p]), 0);
+            const bool a = wsmc_log(uu) < (lpr[p] + sn[p]) - so[p];   // strict; NaN rejects (src/transformers.jl:615)
+            if (a) {
+                for (int u = o; u < o + dm; ++u) sv[u * W + ix[p]] = prop[u * W + ix[p]];
+                chg[p] |= ((1 << dm) - 1) << o;
+                acc += 1;
+                so[p] = sn[p];
+            }
+        }
+        if (accepted) {   // uniform
+            acc = block_sum_u64(acc, lds4);
+            if (th == 0 && acc) atomicAdd(accepted + m, acc);
+        }
+    }
+    const int D = mb.off[nm];
+#pragma unroll
+    for (int p = 0; p < K; ++p) {
+        if (!ok[p]) continue;
+        for (int u = 0; u < D; ++u)
+            if (((mb.lag_targets | chg[p]) >> u) & 1) mb.tout[u][gi[p]] = sv[u * W + ix[p]];
+        mc.out[gi[p]] = so[p];
+    }
+    if (mb.lag_targets && blockIdx.x == 0 && th == 0)   // the device column table follows the moved fronts
+        for (int u = 0; u < D; ++u)
+            if ((mb.lag_targets >> u) & 1) tab[mb.tcol[u]] = mb.tout[u];
 }
 
 // marginal_diversity keys: isequal semantics (all NaN equal, -0.0 != 0.0)
@@ -2951,14 +3201,16 @@ static MomArgs mom_args(const int32_t* tcols, int d, const double* lo, const dou
 }
 hipError_t launch_autorw_moments(hipStream_t s, const double* w, const MaxSlots* ms, double* const* cols,
                                  const int32_t* tcols, int d, const double* lo, const double* hi, const u64* pv,
-                                 int64_t N, double* tilepart, const Decision* wreset, const Decision* gate) {
+                                 int64_t N, double* tilepart, const Decision* wreset, const Decision* gate,
+                                 const int32_t* lag_anc, const Decision* lag_dec, int lag_mask) {
     const MomArgs ma = mom_args(tcols, d, lo, hi);
     const int64_t nt = (N + kTile - 1) / kTile;
+    const MomLag lg{lag_mask ? lag_anc : nullptr, lag_dec, lag_mask};
     switch (d) {
-        case 1: hipLaunchKernelGGL(k_moments1<1>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart, wreset, gate); break;
-        case 2: hipLaunchKernelGGL(k_moments1<2>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart, wreset, gate); break;
-        case 3: hipLaunchKernelGGL(k_moments1<3>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart, wreset, gate); break;
-        default: hipLaunchKernelGGL(k_moments1<4>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart, wreset, gate); break;
+        case 1: hipLaunchKernelGGL(k_moments1<1>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart, wreset, gate, lg); break;
+        case 2: hipLaunchKernelGGL(k_moments1<2>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart, wreset, gate, lg); break;
+        case 3: hipLaunchKernelGGL(k_moments1<3>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart, wreset, gate, lg); break;
+        default: hipLaunchKernelGGL(k_moments1<4>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart, wreset, gate, lg); break;
     }
     return hipGetLastError();
 }
@@ -2970,6 +3222,38 @@ hipError_t launch_autorw_final(hipStream_t s, const double* tilepart, int64_t nt
         case 3: hipLaunchKernelGGL(k_autorw_final<3>, dim3(1), dim3(kBlock), 0, s, tilepart, ntiles, min_step, mom, flag, raw, gate); break;
         default: hipLaunchKernelGGL(k_autorw_final<4>, dim3(1), dim3(kBlock), 0, s, tilepart, ntiles, min_step, mom, flag, raw, gate); break;
     }
+    return hipGetLastError();
+}
+hipError_t launch_autorw_final_blk(hipStream_t s, const double* tilepart, int64_t ntiles, const MoveBlk& mb,
+                                   double* mom, int32_t* flag, const Decision* gate) {
+    switch (mb.off[mb.nm]) {
+        case 1: hipLaunchKernelGGL(k_autorw_final_blk<1>, dim3(1), dim3(kBlock), 0, s, tilepart, ntiles, mb, mom, flag, gate); break;
+        case 2: hipLaunchKernelGGL(k_autorw_final_blk<2>, dim3(1), dim3(kBlock), 0, s, tilepart, ntiles, mb, mom, flag, gate); break;
+        case 3: hipLaunchKernelGGL(k_autorw_final_blk<3>, dim3(1), dim3(kBlock), 0, s, tilepart, ntiles, mb, mom, flag, gate); break;
+        default: hipLaunchKernelGGL(k_autorw_final_blk<4>, dim3(1), dim3(kBlock), 0, s, tilepart, ntiles, mb, mom, flag, gate); break;
+    }
+    return hipGetLastError();
+}
+hipError_t launch_move_blk(hipStream_t s, const ProgInline& pin, int32_t nseg_new, int32_t nseg_old, const FoldSlots& fs,
+                           const double* lo, const double* hi, const MoveBlk& mb, const double* Lb, uint64_t seed,
+                           int64_t goff, int64_t N, unsigned long long* accepted, const int32_t* flag,
+                           const MoveCarry& mc, int32_t cache_from, const int32_t* lag_anc, const Decision* lag_dec,
+                           int lag_mask, double** tab) {
+    MomArgs ma{};
+    for (int k = 0; k < 4; ++k) {
+        ma.tcol[k] = mb.tcol[k];
+        ma.lo[k] = lo[k];
+        ma.hi[k] = hi[k];
+    }
+    const MomLag lg{lag_mask ? lag_anc : nullptr, lag_dec, lag_mask};
+    const size_t row = sizeof(double) * kBlock * (size_t)(fs.n + mb.off[mb.nm]);
+    if (fs.heavy)
+        hipLaunchKernelGGL((k_move_blk<1, 2>), dim3((unsigned)((N + kBlock - 1) / kBlock)), dim3(kBlock), row, s, pin,
+                           fs, ma, mb, Lb, seed, goff, N, accepted, flag, mc, cache_from, nseg_new, nseg_old, lg, tab);
+    else
+        hipLaunchKernelGGL((k_move_blk<2, 1>), dim3((unsigned)((N + 2 * kBlock - 1) / (2 * kBlock))), dim3(kBlock),
+                           2 * row, s, pin, fs, ma, mb, Lb, seed, goff, N, accepted, flag, mc, cache_from, nseg_new,
+                           nseg_old, lg, tab);
     return hipGetLastError();
 }
 hipError_t launch_autorw_publish(hipStream_t s, const MaxSlots* ms, double* const* cols, const int32_t* tcols, int d,
@@ -3013,7 +3297,9 @@ hipError_t launch_move_c(hipStream_t s, const wsmc_term* ctape, int32_t nterms, 
                          const int32_t* tcols, int d, const double* lo, const double* hi, int bounded,
                          const double* L, uint64_t seed, uint64_t op_prop, uint64_t op_acc, int64_t goff, int64_t N,
                          u64* accepted, const int32_t* flag, const MoveCarry& mc, int32_t cache_from,
-                         const FoldProgram& prog) {
+                         const FoldProgram& prog, const ProgInline* pin) {
+    (void)nterms;
+    (void)depth;
     MomArgs ma;
     for (int k = 0; k < 4; ++k) {
         ma.tcol[k] = k < d ? tcols[k] : 0;
@@ -3023,7 +3309,7 @@ hipError_t launch_move_c(hipStream_t s, const wsmc_term* ctape, int32_t nterms, 
     // particles per thread: 2 when the terms are cheap (the scalar term chain dominates:
     // C3 3.7 vs 4.3 ms per run), 1 when they are transcendental-heavy (occupancy wins: C5
     // 0.76 vs 0.88 s); 4 was slower for both
-    const size_t row = sizeof(double) * kBlock * (size_t)(fs.n + 4);
+    const size_t row = sizeof(double) * kBlock * (size_t)(fs.n + d);
     static const int kdiag = [] {   // diagnostics only: force 1 or 2 particles per thread
         const char* e = getenv("WSMC_DIAG_MOVE_K");
         return e ? atoi(e) : 0;
@@ -3034,10 +3320,26 @@ hipError_t launch_move_c(hipStream_t s, const wsmc_term* ctape, int32_t nterms, 
     }();
     // lean variant: 1 = scalar terms and runs without oscillators, 2 = with them, 0 = generic
     const int lean = nolean ? 0 : (fs.lean ? (fs.heavy ? 2 : 1) : 0);
-#define WSMC_MOVE_LAUNCH(KK, LL)                                                                              \
-    hipLaunchKernelGGL((k_move_c<KK, LL>), dim3((unsigned)((N + KK * kBlock - 1) / (KK * kBlock))), dim3(kBlock), \
-                       KK * row, s, ctape, nterms, depth, fs, ma, d, bounded, L, seed, op_prop, op_acc, goff, N,    \
-                       accepted, flag, mc, cache_from, prog)
+#define WSMC_MOVE_LAUNCH(KK, LL)                                                                               \
+    hipLaunchKernelGGL((k_move_c<KK, LL>), dim3((unsigned)((N + KK * kBlock - 1) / (KK * kBlock))), dim3(kBlock),  \
+                       KK * row, s, ctape, fs, ma, d, bounded, L, seed, op_prop, op_acc, goff, N, accepted, flag, mc, \
+                       cache_from, prog)
+#define WSMC_MOVE_LAUNCH_I(KK, LL)                                                                             \
+    hipLaunchKernelGGL((k_move_ci<KK, LL>), dim3((unsigned)((N + KK * kBlock - 1) / (KK * kBlock))), dim3(kBlock), \
+                       KK * row, s, *pin, fs, ma, d, bounded, L, seed, op_prop, op_acc, goff, N, accepted, flag,    \
+                       mc, cache_from, prog.nseg_new, prog.nseg_old)
+    if (pin) {   // lean programs only (the host inlines no other; WSMC_DIAG_MOVE_GENERIC
+                 // applies to uploaded programs: pair it with WSMC_DIAG_PROG_COPY)
+        const bool one = kdiag == 1 || (kdiag != 2 && fs.heavy);
+        if (one) {
+            if (fs.heavy) WSMC_MOVE_LAUNCH_I(1, 2);
+            else WSMC_MOVE_LAUNCH_I(1, 1);
+        } else {
+            if (fs.heavy) WSMC_MOVE_LAUNCH_I(2, 2);
+            else WSMC_MOVE_LAUNCH_I(2, 1);
+        }
+        return hipGetLastError();
+    }
     if (kdiag == 1 || (kdiag != 2 && fs.heavy)) {
         if (lean == 2) WSMC_MOVE_LAUNCH(1, 2);
         else if (lean == 1) WSMC_MOVE_LAUNCH(1, 1);
@@ -3048,6 +3350,7 @@ hipError_t launch_move_c(hipStream_t s, const wsmc_term* ctape, int32_t nterms, 
         else WSMC_MOVE_LAUNCH(2, 0);
     }
 #undef WSMC_MOVE_LAUNCH
+#undef WSMC_MOVE_LAUNCH_I
     return hipGetLastError();
 }
 hipError_t launch_trace_pack(hipStream_t s, const double* xpairs, const int32_t* arow, int64_t start, int64_t count,

@@ -60,6 +60,13 @@ class State(C.Structure):
                 ("op_counter", C.c_uint64), ("n_resamples", C.c_int64)]
 
 
+class MoveSpec(C.Structure):
+    """wsmc_move_spec: one Move of a wsmc_move_block statement block"""
+    _fields_ = [("proposal", C.c_int32), ("d", C.c_int32), ("targets", C.c_int32 * 4),
+                ("bounded", C.c_int32), ("target_depth", C.c_int32), ("step", C.c_double),
+                ("lo", C.c_double * 4), ("hi", C.c_double * 4)]
+
+
 class RunTiming(C.Structure):
     _fields_ = [("total_ms", C.c_double), ("propagate_ms", C.c_double),
                 ("reduce_ms", C.c_double), ("resample_ms", C.c_double),
@@ -118,6 +125,7 @@ SIGNATURES = {
     "wsmc_move": (C.c_int, [_P, C.c_int32, _I32P, C.c_int32, C.c_double, _D, _D, C.c_int32,
                             C.c_double, C.POINTER(C.c_int64)]),
     "wsmc_move_gated": (C.c_int, [_P, C.c_int32, _I32P, C.c_int32, C.c_double, _D, _D, C.c_int32, C.c_double]),
+    "wsmc_move_block": (C.c_int, [_P, C.c_int32, C.POINTER(MoveSpec), C.c_int32, C.POINTER(C.c_int64)]),
     "wsmc_score": (C.c_int, [_P, C.c_int32, _D]),
     "wsmc_marginal_diversity": (C.c_int, [_P, _I32P, C.c_int32, _D]),
     "wsmc_last_ancestors": (C.c_int, [_P, _I32P]),

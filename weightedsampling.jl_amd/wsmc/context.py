@@ -326,6 +326,35 @@ class Context:
             raise np.linalg.LinAlgError(self._L.wsmc_last_error().decode())
         check(rc)
 
+    def move_block(self, moves, gated: bool = False, wait: bool = False):
+        """A statement block of consecutive Moves (wsmc_move_block): `moves` is a list of
+        (proposal, targets, step) or (proposal, targets, step, lo, hi[, target_depth]); the
+        same results as calling move / move_gated for each in order. wait=True returns the
+        accepted counts (a list), else None (asynchronous)."""
+        n = len(moves)
+        specs = (abi.MoveSpec * max(n, 1))()
+        for m, mv in enumerate(moves):
+            proposal, targets, step = mv[0], mv[1], mv[2]
+            lo = mv[3] if len(mv) > 3 else None
+            hi = mv[4] if len(mv) > 4 else None
+            depth = mv[5] if len(mv) > 5 else -1
+            t = [int(x) for x in np.asarray(targets).reshape(-1)]
+            if not 1 <= len(t) <= 4:
+                raise ValueError("a Move has 1..4 targets")
+            sp = specs[m]
+            sp.proposal, sp.d, sp.step, sp.target_depth = int(proposal), len(t), float(step), int(depth)
+            sp.bounded = 0 if (lo is None and hi is None) else 1
+            for k in range(4):
+                sp.targets[k] = t[k] if k < len(t) else -1
+                sp.lo[k] = float(lo[k]) if lo is not None and k < len(t) else -math.inf
+                sp.hi[k] = float(hi[k]) if hi is not None and k < len(t) else math.inf
+        acc = (C.c_int64 * max(n, 1))()
+        rc = self._L.wsmc_move_block(self._h, n, specs, 1 if gated else 0, acc if wait else None)
+        if rc == abi.WSMC_ENOTPD:
+            raise np.linalg.LinAlgError(self._L.wsmc_last_error().decode())
+        check(rc)
+        return [int(acc[m]) for m in range(n)] if wait else None
+
     def score(self, target_depth: int) -> np.ndarray:
         out = np.empty(self.n)
         check(self._L.wsmc_score(self._h, int(target_depth), _dptr(out)))

@@ -117,11 +117,13 @@ def lgssm1d_statements(ctx, data, a=0.9, q=1.0, r=0.5, x0_std=1.0, ess_perc_min=
 
 
 def linreg_statements(ctx, xs, ys, prior_sd=10.0, obs_sd=1.0, ess_perc_min=0.5,
-                      scheme=abi.RESAMPLE_STRATIFIED, min_step=1e-3, wait_moves=True, gated=False):
+                      scheme=abi.RESAMPLE_STRATIFIED, min_step=1e-3, wait_moves=True, gated=False,
+                      block=True):
     """examples/linear_regression.jl:17-27: α, β ~ N(0,10); y => N(α + β x, 1);
     `if resampled; α << autoRW(); β << autoRW(); end`. gated=True lowers the `if resampled`
-    block to device-gated Moves (wsmc_move_gated): no Resample returns its flag, nothing waits
-    on the host inside the loop, and the function returns None."""
+    block to device-gated Moves: no Resample returns its flag, nothing waits on the host inside
+    the loop, and the function returns None. block=True issues the two Moves as one statement
+    block (wsmc_move_block: one moments pass, one Move kernel), else as two wsmc_move_gated."""
     R = resolver(ctx)
     ca = ctx.col_create("α", 1)
     ctx.sample(ca, Normal(0.0, prior_sd).dist(R))
@@ -134,8 +136,12 @@ def linreg_statements(ctx, xs, ys, prior_sd=10.0, obs_sd=1.0, ess_perc_min=0.5,
         ctx.observe(Normal(Col("α") + Col("β") * float(x), obs_sd).dist(R), _const([y]))
         if gated:
             ctx.resample(ess_perc_min, scheme, wait=False)
-            ctx.move_gated(abi.PROPOSAL_AUTORW, [ca], min_step)
-            ctx.move_gated(abi.PROPOSAL_AUTORW, [cb], min_step)
+            if block:
+                ctx.move_block([(abi.PROPOSAL_AUTORW, [ca], min_step), (abi.PROPOSAL_AUTORW, [cb], min_step)],
+                               gated=True)
+            else:
+                ctx.move_gated(abi.PROPOSAL_AUTORW, [ca], min_step)
+                ctx.move_gated(abi.PROPOSAL_AUTORW, [cb], min_step)
             continue
         rs, _ = ctx.resample(ess_perc_min, scheme)
         if rs:   # `if resampled` reads the flag; the moves need not return their counts
