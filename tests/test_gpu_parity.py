@@ -566,8 +566,9 @@ def test_move_block_matches_oracle(gpu_available, shape, gated, wait, sigma_col)
             moves = []
             for grp, bnd in _BLOCKS[shape]:
                 t = [cols[k] for k in grp]
-                if bnd:
-                    moves.append((abi.PROPOSAL_AUTORW, t, 1e-3, [0.0] * len(t), [math.inf] * len(t)))
+                if bnd:   # c >= 0; a, b unbounded within the bounded Move
+                    lo = [0.0 if k == 2 else -math.inf for k in grp]
+                    moves.append((abi.PROPOSAL_AUTORW, t, 1e-3, lo, [math.inf] * len(t)))
                 else:
                     moves.append((abi.PROPOSAL_AUTORW, t, 1e-3))
             counts.append(ctx.move_block(moves, gated=gated, wait=wait))

@@ -1894,34 +1894,40 @@ __global__ __launch_bounds__(kBlock) void k_moments1(const double* __restrict__ 
     double acc[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) acc[v] = 0.0;
-    // every load of the tile first (one memory latency per thread, not kItems in a row),
-    // then the canonical per-item accumulation
-    double xv[kItems][D], wv[kItems];
-    int64_t ai[kItems];
+    // the tile's loads in chunks of CH items (a few memory latencies per thread, not kItems in
+    // a row; CH bounded so the loaded values stay in registers), then the canonical per-item
+    // accumulation
+    constexpr int CH = D <= 1 ? 8 : (D == 2 ? 4 : 1);
+    static_assert(kItems % CH == 0, "chunking");
+#pragma unroll 1
+    for (int j0 = 0; j0 < kItems; j0 += CH) {
+    double xv[CH][D], wv[CH];
+    int32_t ai[CH];
 #pragma unroll
-    for (int j = 0; j < kItems; ++j) {
-        const int64_t i = base + (int64_t)j * kBlock + threadIdx.x;
-        ai[j] = (lmask && i < N) ? (int64_t)lg.anc[i] : i;
+    for (int c = 0; c < CH; ++c) {
+        const int64_t i = base + (int64_t)(j0 + c) * kBlock + threadIdx.x;
+        ai[c] = (lmask && i < N) ? lg.anc[i] : 0;
     }
 #pragma unroll
-    for (int j = 0; j < kItems; ++j) {
-        const int64_t i = base + (int64_t)j * kBlock + threadIdx.x;
+    for (int c = 0; c < CH; ++c) {
+        const int64_t i = base + (int64_t)(j0 + c) * kBlock + threadIdx.x;
         const bool in = i < N;
-        wv[j] = (in && !reset) ? w[i] : 0.0;
+        wv[c] = (in && !reset) ? w[i] : 0.0;
 #pragma unroll
-        for (int k = 0; k < d; ++k) xv[j][k] = in ? tp[k][(lmask >> k) & 1 ? ai[j] : i] : 0.0;
+        for (int k = 0; k < d; ++k) xv[c][k] = in ? tp[k][(lmask >> k) & 1 ? (int64_t)ai[c] : i] : 0.0;
     }
 #pragma unroll
-    for (int j = 0; j < kItems; ++j) {
+    for (int c = 0; c < CH; ++c) {
+        const int j = j0 + c;
         const int64_t i = base + (int64_t)j * kBlock + threadIdx.x;
         double vals[NV];
 #pragma unroll
         for (int v = 0; v < NV; ++v) vals[v] = 0.0;
         if (i < N) {
-            const double e = reset ? er : wsmc_exp(wv[j] - M);
+            const double e = reset ? er : wsmc_exp(wv[c] - M);
             double dz[4];
 #pragma unroll
-            for (int k = 0; k < d; ++k) dz[k] = wsmc_to_unc(xv[j][k], ma.lo[k], ma.hi[k]) - p[k];
+            for (int k = 0; k < d; ++k) dz[k] = wsmc_to_unc(xv[c][k], ma.lo[k], ma.hi[k]) - p[k];
             vals[0] = e;
 #pragma unroll
             for (int k = 0; k < d; ++k) vals[1 + k] = e * dz[k];
@@ -1933,6 +1939,7 @@ __global__ __launch_bounds__(kBlock) void k_moments1(const double* __restrict__ 
         }
 #pragma unroll
         for (int v = 0; v < NV; ++v) acc[v] = acc[v] + vals[v];
+    }
     }
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
@@ -1950,10 +1957,16 @@ __global__ __launch_bounds__(kBlock) void k_autorw_final(const double* tilepart,
     __shared__ double lds4[4];
     __shared__ double tot[NV];
     if (gate && !gate->resampled) return;
+    // every value's partials in one walk (each value's sum in its own order), then the sums
+    double acc[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) acc[v] = 0.0;
+    for (int64_t b = threadIdx.x; b < ntiles; b += kBlock)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[v] = acc[v] + tilepart[(int64_t)v * ntiles + b];
+#pragma unroll
     for (int v = 0; v < NV; ++v) {
-        double acc = 0.0;
-        for (int64_t b = threadIdx.x; b < ntiles; b += kBlock) acc = acc + tilepart[(int64_t)v * ntiles + b];
-        const double s = block_sum_canon(acc, lds4);
+        const double s = block_sum_canon(acc[v], lds4);
         if (threadIdx.x == 0) tot[v] = s;
     }
     __syncthreads();
@@ -2325,10 +2338,16 @@ __global__ __launch_bounds__(kBlock) void k_autorw_final_blk(const double* tilep
     __shared__ double lds4[4];
     __shared__ double tot[NV];
     if (gate && !gate->resampled) return;
+    // every value's partials in one walk (each value's sum in its own order), then the sums
+    double acc[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) acc[v] = 0.0;
+    for (int64_t b = threadIdx.x; b < ntiles; b += kBlock)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[v] = acc[v] + tilepart[(int64_t)v * ntiles + b];
+#pragma unroll
     for (int v = 0; v < NV; ++v) {
-        double acc = 0.0;
-        for (int64_t b = threadIdx.x; b < ntiles; b += kBlock) acc = acc + tilepart[(int64_t)v * ntiles + b];
-        const double s = block_sum_canon(acc, lds4);
+        const double s = block_sum_canon(acc[v], lds4);
         if (threadIdx.x == 0) tot[v] = s;
     }
     __syncthreads();
