@@ -488,11 +488,25 @@ WSMC_HD double wsmc_from_unc(double z, double lo, double hi) {
 WSMC_HD double wsmc_log1pexp(double z) {
     return z > 0.0 ? z + wsmc_log1p(wsmc_exp(-z)) : wsmc_log1p(wsmc_exp(z));
 }
-WSMC_HD double wsmc_log_abs_jac(double z, double lo, double hi) {
+/* log|dx/dz| of wsmc_from_unc; lgw = wsmc_log(hi - lo) (a bounded interval: callers with
+ * constant bounds evaluate it once). log1pexp(z) and log1pexp(-z) are z+ + P and (-z)+ + P
+ * with the one P = log1p(exp(-|z|)) (z > 0: z + log1p(exp(-z)) and log1p(exp(-z)); z <= 0,
+ * -0.0 and NaN included: log1p(exp(z)) and (-z) + log1p(exp(z)) or, at 0, log1p(exp(0))):
+ * wsmc_log1pexp's values with one exp and one log1p instead of two each. */
+WSMC_HD double wsmc_log_abs_jac_pre(double z, double lo, double hi, double lgw) {
     int flo = wsmc_isfinite(lo), fhi = wsmc_isfinite(hi);
-    if (flo && fhi) return wsmc_log(hi - lo) - wsmc_log1pexp(z) - wsmc_log1pexp(-z);
+    if (flo && fhi) {
+        const double P = wsmc_log1p(wsmc_exp(z > 0.0 ? -z : z));
+        const double a = z > 0.0 ? z + P : P;            /* wsmc_log1pexp(z)  */
+        const double b = -z > 0.0 ? -z + P : P;          /* wsmc_log1pexp(-z) */
+        return lgw - a - b;
+    }
     if (flo || fhi) return z;
     return 0.0;
+}
+WSMC_HD double wsmc_log_abs_jac(double z, double lo, double hi) {
+    const int both = wsmc_isfinite(lo) && wsmc_isfinite(hi);
+    return wsmc_log_abs_jac_pre(z, lo, hi, both ? wsmc_log(hi - lo) : 0.0);
 }
 
 /* ------------------------------------------------------------------------- */

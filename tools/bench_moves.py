@@ -79,7 +79,36 @@ def c5(N=4_000_000, T=60, sweeps=5, reps=1, scheme="systematic", ess=1.0, divers
     return out
 
 
+def _oracle():
+    """the CPU port (test infrastructure: a baseline leg only), OpenMP threads bound one per
+    core before its library loads"""
+    import os
+    os.environ.setdefault("OMP_PLACES", "cores")
+    os.environ.setdefault("OMP_PROC_BIND", "close")
+    sys.path.insert(0, str(pathlib.Path(__file__).resolve().parents[1] / "oracle"))
+    from oracle import Oracle
+    return Oracle, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+
+
+def c3cpu(N=100_000, reps=2):
+    """C3 on the CPU port (the oracle: OpenMP over particles in the Move, serial elsewhere) at a
+    bounded N: the baseline beside the device's C3 lines"""
+    Oracle, threads = _oracle()
+    xs, ys = models.linreg_data()
+    best = math.inf
+    for _ in range(reps):
+        o = Oracle(N, seed=42)
+        t0 = time.perf_counter()
+        models.linreg_statements(o, xs, ys, ess_perc_min=1.0, gated=True, block=False)
+        best = min(best, time.perf_counter() - t0)
+        o.close() if hasattr(o, "close") else None
+    T = len(xs)
+    return {"config": f"C3 on the CPU port (oracle, {threads} OpenMP threads bound to cores), N={N}, T={T}, ess 1.0",
+            "N": N, "T": T, "seconds_per_run": best, "particle_steps_per_s": N * T / best, "threads": threads}
+
+
 LEGS = {
+    "c3cpu": c3cpu,
     "c3": c3,
     "c5": c5,                                                             # canonical (systematic)
     "c5_stratified": lambda: c5(scheme="stratified"),                     # the reference's scheme

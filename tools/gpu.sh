@@ -86,7 +86,7 @@ bench)
   step 400 $O/stats.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python bench.py --no-cpu-baseline "$@"
   stats_table $O/stats/run_kernel_stats.csv 8 ;;
 moves)
-  timeout -k 10 400 python tools/bench_moves.py c3 c3async c3gated_moves c3gated c5 c5async > $O/moves.jsonl 2> $O/moves.err || { tail $O/moves.err; exit 1; }
+  timeout -k 10 400 python tools/bench_moves.py c3 c3async c3gated_moves c3gated c5 c5async c3cpu > $O/moves.jsonl 2> $O/moves.err || { tail $O/moves.err; exit 1; }
   cut -c1-330 $O/moves.jsonl
   step 300 $O/c3.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/c3 -o run -- python tools/bench_moves.py c3gated
   stats_table $O/c3/run_kernel_stats.csv 10 ;;

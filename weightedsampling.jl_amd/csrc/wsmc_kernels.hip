@@ -1689,6 +1689,7 @@ __global__ __launch_bounds__(kBlock) void k_score(const wsmc_term* tape, int32_t
 struct MomArgs {
     int32_t tcol[4];
     double lo[4], hi[4];
+    double lgw[4];           // log(hi - lo) of a bounded interval (host-evaluated), else 0
     int32_t use_ex;          // analysis moments: values are operand expressions (identity transform)
     wsmc_operand ex[4];
 };
@@ -2046,7 +2047,7 @@ __global__ __launch_bounds__(kBlock) void k_move(const wsmc_term* tape, int32_t 
             const double zn = zo + dz[k];
             const double xn = bounded ? wsmc_from_unc(zn, ma.lo[k], ma.hi[k]) : zn;
             if (bounded)
-                lpr = lpr + (wsmc_log_abs_jac(zn, ma.lo[k], ma.hi[k]) - wsmc_log_abs_jac(zo, ma.lo[k], ma.hi[k]));
+                lpr = lpr + (wsmc_log_abs_jac_pre(zn, ma.lo[k], ma.hi[k], ma.lgw[k]) - wsmc_log_abs_jac_pre(zo, ma.lo[k], ma.hi[k], ma.lgw[k]));
             ov.col[k] = ma.tcol[k];
             ov.val[k] = xn;
         }
@@ -2262,7 +2263,8 @@ __device__ __forceinline__ void move_c_body(const wsmc_term* ctape, const FoldSl
             const double zn = zo + dz;
             const double xn = bounded ? wsmc_from_unc(zn, ma.lo[k], ma.hi[k]) : zn;
             if (bounded)
-                lpr[p] = lpr[p] + (wsmc_log_abs_jac(zn, ma.lo[k], ma.hi[k]) - wsmc_log_abs_jac(zo, ma.lo[k], ma.hi[k]));
+                lpr[p] = lpr[p] + (wsmc_log_abs_jac_pre(zn, ma.lo[k], ma.hi[k], ma.lgw[k]) -
+                                   wsmc_log_abs_jac_pre(zo, ma.lo[k], ma.hi[k], ma.lgw[k]));
             prop[k * W + ix[p]] = xn;
         }
     }
@@ -2464,7 +2466,8 @@ __global__ __launch_bounds__(kBlock) void k_move_blk(ProgInline, FoldSlots fs, M
                 const double zn = zo + dz;
                 const double xn = bd ? wsmc_from_unc(zn, ma.lo[u], ma.hi[u]) : zn;
                 if (bd)
-                    lpr[p] = lpr[p] + (wsmc_log_abs_jac(zn, ma.lo[u], ma.hi[u]) - wsmc_log_abs_jac(zo, ma.lo[u], ma.hi[u]));
+                    lpr[p] = lpr[p] + (wsmc_log_abs_jac_pre(zn, ma.lo[u], ma.hi[u], ma.lgw[u]) -
+                                       wsmc_log_abs_jac_pre(zo, ma.lo[u], ma.hi[u], ma.lgw[u]));
                 prop[u * W + ix[p]] = xn;
             }
         }
@@ -3156,6 +3159,7 @@ hipError_t launch_moments(hipStream_t s, const double* w, const MaxSlots* rec, d
         ma.tcol[k] = k < d ? tcols[k] : 0;
         ma.lo[k] = (k < d && lo) ? lo[k] : -WSMC_INF;
         ma.hi[k] = (k < d && hi) ? hi[k] : WSMC_INF;
+        ma.lgw[k] = (wsmc_isfinite(ma.lo[k]) && wsmc_isfinite(ma.hi[k])) ? wsmc_log(ma.hi[k] - ma.lo[k]) : 0.0;
     }
     ma.use_ex = 0;
     const int64_t nt = (N + kTile - 1) / kTile;
@@ -3175,6 +3179,7 @@ hipError_t launch_moments_expr(hipStream_t s, const double* w, const MaxSlots* m
         ma.tcol[k] = 0;
         ma.lo[k] = -WSMC_INF;
         ma.hi[k] = WSMC_INF;
+        ma.lgw[k] = (wsmc_isfinite(ma.lo[k]) && wsmc_isfinite(ma.hi[k])) ? wsmc_log(ma.hi[k] - ma.lo[k]) : 0.0;
         ma.ex[k] = ex[k < d ? k : 0];
     }
     ma.use_ex = 1;
@@ -3214,6 +3219,7 @@ static MomArgs mom_args(const int32_t* tcols, int d, const double* lo, const dou
         ma.tcol[k] = k < d ? tcols[k] : 0;
         ma.lo[k] = (k < d && lo) ? lo[k] : -WSMC_INF;
         ma.hi[k] = (k < d && hi) ? hi[k] : WSMC_INF;
+        ma.lgw[k] = (wsmc_isfinite(ma.lo[k]) && wsmc_isfinite(ma.hi[k])) ? wsmc_log(ma.hi[k] - ma.lo[k]) : 0.0;
     }
     ma.use_ex = 0;
     return ma;
@@ -3263,6 +3269,7 @@ hipError_t launch_move_blk(hipStream_t s, const ProgInline& pin, int32_t nseg_ne
         ma.tcol[k] = mb.tcol[k];
         ma.lo[k] = lo[k];
         ma.hi[k] = hi[k];
+        ma.lgw[k] = (wsmc_isfinite(ma.lo[k]) && wsmc_isfinite(ma.hi[k])) ? wsmc_log(ma.hi[k] - ma.lo[k]) : 0.0;
     }
     const MomLag lg{lag_mask ? lag_anc : nullptr, lag_dec, lag_mask};
     const size_t row = sizeof(double) * kBlock * (size_t)(fs.n + mb.off[mb.nm]);
@@ -3307,6 +3314,7 @@ hipError_t launch_move(hipStream_t s, const wsmc_term* tape, int32_t nterms, int
         ma.tcol[k] = k < d ? tcols[k] : 0;
         ma.lo[k] = (k < d && lo) ? lo[k] : -WSMC_INF;
         ma.hi[k] = (k < d && hi) ? hi[k] : WSMC_INF;
+        ma.lgw[k] = (wsmc_isfinite(ma.lo[k]) && wsmc_isfinite(ma.hi[k])) ? wsmc_log(ma.hi[k] - ma.lo[k]) : 0.0;
     }
     hipLaunchKernelGGL(k_move, grid_for(N), dim3(kBlock), 0, s, tape, nterms, depth, cols, ma, d, bounded, L,
                        seed, op_prop, op_acc, goff, N, accepted, flag, scache, cache_from);
@@ -3324,6 +3332,7 @@ hipError_t launch_move_c(hipStream_t s, const wsmc_term* ctape, int32_t nterms, 
         ma.tcol[k] = k < d ? tcols[k] : 0;
         ma.lo[k] = (k < d && lo) ? lo[k] : -WSMC_INF;
         ma.hi[k] = (k < d && hi) ? hi[k] : WSMC_INF;
+        ma.lgw[k] = (wsmc_isfinite(ma.lo[k]) && wsmc_isfinite(ma.hi[k])) ? wsmc_log(ma.hi[k] - ma.lo[k]) : 0.0;
     }
     // particles per thread: 2 when the terms are cheap (the scalar term chain dominates:
     // C3 3.7 vs 4.3 ms per run), 1 when they are transcendental-heavy (occupancy wins: C5
