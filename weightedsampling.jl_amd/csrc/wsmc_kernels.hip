@@ -2732,12 +2732,17 @@ __global__ __launch_bounds__(kBlock) void k_iota(int32_t* __restrict__ a, int64_
 
 // trace the ancestor log back once and materialise the final columns — the result
 // ColumnStore's per-resample gather of every column would have produced (src/stores.jl:105-128)
+// ISL: island shards decide the last step here, from its records (the single-GPU instance
+// reads the decision: no barrier or decide code ahead of the trace)
+template <bool ISL>
 __global__ __launch_bounds__(kBlock) void k_ssm2d_final(Ssm2dFinal f) {
     const int64_t N = f.N;
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int T = f.T;
-    __shared__ Decision s_dec;
-    if (f.recs_last) {   // island shards: the last step's decision from its records
+    bool rsT;
+    double meanT;
+    if (ISL) {
+        __shared__ Decision s_dec;
         if (threadIdx.x == 0) {
             Decision dd;
             decide_records(f.recs_last, f.world, f.rank, f.ess_min, &dd);
@@ -2745,13 +2750,13 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_final(Ssm2dFinal f) {
             if (blockIdx.x == 0) *f.dec_out = dd;
         }
         __syncthreads();
-    } else if (threadIdx.x == 0) {
-        s_dec = f.dec[T];
+        rsT = s_dec.resampled;
+        meanT = s_dec.mean;
+    } else {
+        rsT = f.dec[T].resampled;
+        meanT = f.dec[T].mean;
     }
-    if (!f.recs_last) __syncthreads();
     if (i >= N) return;
-    const bool rsT = s_dec.resampled;
-    const double meanT = s_dec.mean;
     const int64_t S = f.anc_stride;
     int64_t a = i;
     if (rsT) a = f.anc_log[(int64_t)(T - 1) * S + i];
@@ -3451,7 +3456,8 @@ hipError_t launch_delay(hipStream_t s, int microseconds) {
 }
 
 hipError_t launch_ssm2d_finalize(hipStream_t s, const Ssm2dFinal& f, hipEvent_t e0, hipEvent_t e1) {
-    return launch_timed(k_ssm2d_final, grid_for(f.N), dim3(kBlock), s, e0, e1, f);
+    if (f.recs_last) return launch_timed(k_ssm2d_final<true>, grid_for(f.N), dim3(kBlock), s, e0, e1, f);
+    return launch_timed(k_ssm2d_final<false>, grid_for(f.N), dim3(kBlock), s, e0, e1, f);
 }
 
 }  // namespace wsmc
