@@ -392,7 +392,8 @@ function apply!(::WS.Resample, state::HipState)
 end
 
 """`Move` with the built-in `RW` / `autoRW` proposals (recognised by identity)."""
-function apply!(t::WS.Move, state::HipState)
+# a Move's arguments: proposal kind, step, targets, bounds (src/move_kernels.jl:189-253)
+function move_args(t::WS.Move, state::HipState)
     s = state.store
     args = t.argfn(state)
     kind = t.proposal === WS.autoRW ? PROPOSAL_AUTORW :
@@ -402,17 +403,60 @@ function apply!(t::WS.Move, state::HipState)
     bounds = length(args) >= 2 ? args[2] : nothing
     d = length(t.targets)
     ids = Int32[s.ids[c] for c in t.targets]
-    lo = hi = C_NULL
+    lo = hi = nothing
     if bounds !== nothing
         b = WS._normalize_bounds(bounds, d)
         lo = Float64[x[1] for x in b]
         hi = Float64[x[2] for x in b]
     end
+    return kind, step, ids, lo, hi
+end
+
+function apply!(t::WS.Move, state::HipState)
+    kind, step, ids, lo, hi = move_args(t, state)
     div = t.diversity_threshold === nothing ? NaN : Float64(t.diversity_threshold)
     acc = Ref{Int64}(0)
     check(ccall((:wsmc_move, libwsmc), Cint,
                 (Ptr{Cvoid}, Int32, Ptr{Int32}, Int32, Float64, Ptr{Float64}, Ptr{Float64}, Int32, Float64, Ptr{Int64}),
-                s.ctx, kind, ids, d, step, lo, hi, state.depth, div, acc))
+                state.store.ctx, kind, ids, length(ids), step, lo === nothing ? C_NULL : lo,
+                hi === nothing ? C_NULL : hi, state.depth, div, acc))
+    return nothing
+end
+
+# wsmc_move_spec (include/wsmc.h): one Move of a statement block
+struct MoveSpec
+    proposal::Int32
+    d::Int32
+    targets::NTuple{4,Int32}
+    bounded::Int32
+    target_depth::Int32
+    step::Float64
+    lo::NTuple{4,Float64}
+    hi::NTuple{4,Float64}
+end
+
+# A Sequence of Moves — the body of `if resampled ... end` (examples/linear_regression.jl:23-24)
+# or a sweep — is one wsmc_move_block call: the sequential Moves' results, as one moments
+# pass, one combine and one Move kernel when the block fuses (disjoint autoRW targets).
+function apply!(t::WS.Sequence, state::HipState)
+    steps = t.steps
+    if !isempty(steps) && all(x -> x isa WS.Move && x.diversity_threshold === nothing, steps)
+        specs = map(steps) do m
+            kind, step, ids, lo, hi = move_args(m, state)
+            d = length(ids)
+            d <= 4 || error("WeightedSamplingHIP: a Move has at most 4 targets")
+            pad(v, x) = ntuple(k -> k <= d ? v[k] : x, 4)
+            MoveSpec(kind, d, pad(ids, Int32(-1)), lo === nothing ? 0 : 1, state.depth, step,
+                     lo === nothing ? ntuple(_ -> -Inf, 4) : pad(lo, -Inf),
+                     hi === nothing ? ntuple(_ -> Inf, 4) : pad(hi, Inf))
+        end
+        v = collect(MoveSpec, specs)
+        acc = zeros(Int64, length(v))
+        check(ccall((:wsmc_move_block, libwsmc), Cint, (Ptr{Cvoid}, Int32, Ptr{MoveSpec}, Int32, Ptr{Int64}),
+                    state.store.ctx, length(v), v, 0, acc))
+        return nothing
+    end
+    foreach(step -> apply!(step, state), steps)
     return nothing
 end
 
