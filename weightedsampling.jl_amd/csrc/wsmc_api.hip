@@ -27,10 +27,17 @@ int fail(int code, const std::string& msg) {
 
 // every entry point: the device, then any deferred weight reset applied before the call reads
 // or writes the weights (CHECK_CTX_KEEP: the Observe / Weight path, which applies it itself)
-#define CHECK_CTX_KEEP(ctx)                                              \
+// CHECK_CTX_EW: the elementwise statements (Assign / Sample / Observe / Weight), which join the
+// pending batch (ew_*); every other entry point launches the batch first (CHECK_CTX_KEEP)
+#define CHECK_CTX_EW(ctx)                                                \
     do {                                                                 \
         if (!(ctx)) return fail(WSMC_EARG, "null context");              \
         WSMC_HIP(hipSetDevice((ctx)->device));                           \
+    } while (0)
+#define CHECK_CTX_KEEP(ctx)                                              \
+    do {                                                                 \
+        CHECK_CTX_EW(ctx);                                               \
+        if (int _r = ew_flush(ctx)) return _r;                           \
     } while (0)
 #define CHECK_CTX(ctx)                                                   \
     do {                                                                 \
@@ -41,6 +48,67 @@ int fail(int code, const std::string& msg) {
         }                                                                \
     } while (0)
 
+
+// ---- the elementwise batch (EwBatch, csrc/wsmc_internal.h) ---------------------------------
+// Consecutive Assign / Sample / Observe / Weight statements join one batch, launched as one
+// kernel by the next other entry point (or when full). Each particle takes the statements in
+// order, so a statement reading what an earlier one wrote reads its own particle's value; the
+// one cross-particle read is an Assign operand one Resample behind (through the ancestors), so
+// a statement writing such a column in place launches the batch first. One context only
+// (shards exchange inside their operators); WSMC_DIAG_NO_BATCH=1 launches every statement alone.
+static bool ew_enabled(const wsmc_ctx* c) {
+    static const bool off = [] {
+        const char* e = getenv("WSMC_DIAG_NO_BATCH");
+        return e && atoi(e) != 0;
+    }();
+    return !off && !(c->world > 1 || c->comm || c->host_exchange);
+}
+static int ew_flush(wsmc_ctx* c) {
+    EwBatch* b = c->ew;
+    if (!b || b->nops == 0) return WSMC_OK;
+    const hipError_t e = launch_ew_batch(c->stream, *b, c->ew_feat, c->seed, c->goff, c->N);
+    b->nops = b->ntab = b->has_w = b->nslots = 0;
+    b->anc = nullptr;
+    b->dec = nullptr;
+    c->ew_feat = 0;
+    c->ew_lag.clear();
+    if (e != hipSuccess) return fail(WSMC_EHIP, std::string("statement batch: ") + hipGetErrorString(e));
+    return WSMC_OK;
+}
+static EwBatch* ew_open(wsmc_ctx* c) {
+    if (!c->ew) {
+        c->ew = new EwBatch;
+        std::memset(c->ew, 0, sizeof(EwBatch));
+    }
+    return c->ew;
+}
+static bool ew_reads_lagged(const wsmc_ctx* c, int32_t col) {
+    for (int32_t x : c->ew_lag)
+        if (x == col) return true;
+    return false;
+}
+// an operand's columns renumbered to the batch's slots (the column's current front); false: full
+static bool ew_remap(const wsmc_ctx* c, EwBatch* b, wsmc_operand& o) {
+    for (int m = 0; m < 2; ++m) {
+        if (o.col[m] < 0) continue;
+        const double* p = c->cols[o.col[m]].front;
+        int s = -1;
+        for (int k = 0; k < b->nslots; ++k)
+            if (b->slot[k] == p) s = k;
+        if (s < 0) {
+            if (b->nslots == kEwSlots) return false;
+            s = b->nslots++;
+            b->slot[s] = p;
+        }
+        o.col[m] = s;
+    }
+    return true;
+}
+static bool ew_remap_dist(const wsmc_ctx* c, EwBatch* b, wsmc_dist& d) {
+    for (int k = 0; k < 4; ++k)
+        if (!ew_remap(c, b, d.mu[k])) return false;
+    return ew_remap(c, b, d.scale);
+}
 
 // ---- helpers -------------------------------------------------------------------------
 static int upload_colptr(wsmc_ctx* c) {
@@ -492,6 +560,7 @@ int wsmc_destroy(wsmc_ctx* c) {
         if (p) (void)hipFree(p);
     if (c->pinned) (void)hipHostFree(c->pinned);
     if (c->prog_stage) (void)hipHostFree(c->prog_stage);
+    delete c->ew;   // statements never launched: the context goes with them
     if (c->dec_ring) (void)hipHostFree(c->dec_ring);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -651,7 +720,7 @@ int wsmc_comm_set_shard_mode(wsmc_ctx* c, int32_t mode) {
 // ---- store ---------------------------------------------------------------------------
 int wsmc_col_create(wsmc_ctx* c, const char* name, int32_t dim, int32_t* col_id) {
     if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { int32_t id = -1; int r = wsmc_col_create(x, name, dim, &id); if (x == multi_first(c) && col_id) *col_id = id; return r; });
-    CHECK_CTX_KEEP(c);   // no weights touched
+    CHECK_CTX_EW(c);   // no weights touched; a pending statement batch keeps its pointers
     if (!name || !col_id) return fail(WSMC_EARG, "null argument");
     for (size_t k = 0; k < c->cols.size(); ++k)
         if (c->cols[k].name == name) {
@@ -729,6 +798,7 @@ int wsmc_col_device_ptr(wsmc_ctx* c, int32_t col, double** dptr) {
     if (c && c->multi) return multi_G(c) == 1 ? wsmc_col_device_ptr(multi_first(c), col, dptr) : fail(WSMC_EARG, "a column of a multi-device handle lives on several devices");
     if (!c || !valid_col(c, col) || !dptr) return fail(WSMC_EARG, "bad column");
     WSMC_HIP(hipSetDevice(c->device));
+    if (int r = ew_flush(c)) return r;   // the caller reads the column on the stream
     if (int r = need_cols(c, {col})) return r;
     *dptr = c->cols[col].front;
     return WSMC_OK;
@@ -1759,7 +1829,7 @@ int wsmc_log_evidence(wsmc_ctx* c, double* out) {
 // ---- operators -----------------------------------------------------------------------
 int wsmc_assign(wsmc_ctx* c, int32_t out, const wsmc_operand* expr) {
     if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { return wsmc_assign(x, out, expr); });
-    CHECK_CTX_KEEP(c);   // reads and writes no weights: a pending reset stays pending
+    CHECK_CTX_EW(c);   // reads and writes no weights: a pending reset stays pending
     if (!valid_col(c, out) || !expr) return fail(WSMC_EARG, "bad output column");
     const int dim = c->cols[out].dim;
     for (int k = 0; k < dim; ++k) {
@@ -1798,6 +1868,13 @@ int wsmc_assign(wsmc_ctx* c, int32_t out, const wsmc_operand* expr) {
     for (size_t k = 0; k < c->cols.size(); ++k) fronts[k] = c->cols[k].front;   // before any swap
     ind.front = fronts.data();
     double* dst = c->cols[out].front;
+    EwBatch* b = ew_enabled(c) ? ew_open(c) : nullptr;
+    // the batch: full, another ancestor row, a full table-move list, or an in-place write of a
+    // column the batch reads through the ancestors -> launch it first
+    if (b && b->nops > 0 &&
+        (b->nops == kEwOps || (ind.mask && b->anc && b->anc != ind.row) || (out_read_behind && b->ntab == 4) ||
+         (!out_read_behind && ew_reads_lagged(c, out))))
+        if ((r = ew_flush(c))) return r;
     if (out_read_behind) {   // out read through the ancestors: write a fresh buffer (no read/write race)
         dst = c->cols[out].back;
         ind.tab_col = out;
@@ -1806,7 +1883,35 @@ int wsmc_assign(wsmc_ctx* c, int32_t out, const wsmc_operand* expr) {
     }
     scores_touch(c, out);
     wrote_col(c, out);
-    WSMC_HIP(launch_assign(c->stream, dst, dim, expr, c->d_colptr, c->N, ind));
+    if (b) {
+        EwOp& op = b->ops[b->nops];
+        std::memset(&op, 0, sizeof(op));
+        op.kind = 0;
+        op.dim = dim;
+        op.out = dst;
+        for (int k = 0; k < 4; ++k) {
+            op.a.e[k] = expr[k < dim ? k : 0];
+            for (int m = 0; m < 2; ++m) {
+                const int32_t id = op.a.e[k].col[m];
+                op.a.p[k][m] = id >= 0 ? fronts[id] + (int64_t)op.a.e[k].comp[m] * c->N : nullptr;
+                if (id >= 0 && k < dim && ((ind.mask >> (2 * k + m)) & 1)) c->ew_lag.push_back(id);
+            }
+        }
+        op.a.lag = ind.mask;
+        if (ind.mask) {
+            b->anc = ind.row;
+            b->dec = ind.dec;
+        }
+        if (ind.tab_col >= 0) {
+            b->tab = ind.tab;
+            b->tab_out[b->ntab] = dst;
+            b->tab_col[b->ntab] = ind.tab_col;
+            b->ntab += 1;
+        }
+        b->nops += 1;
+    } else {
+        WSMC_HIP(launch_assign(c->stream, dst, dim, expr, c->d_colptr, c->N, ind));
+    }
     gc_log(c);
     c->depth += 1;
     return WSMC_OK;
@@ -1824,7 +1929,7 @@ static void push_sample_term(wsmc_ctx* c, int32_t out, const wsmc_dist& d) {
 
 int wsmc_sample(wsmc_ctx* c, int32_t out, const wsmc_dist* d) {
     if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { return wsmc_sample(x, out, d); });
-    CHECK_CTX_KEEP(c);   // reads and writes no weights: a pending reset stays pending
+    CHECK_CTX_EW(c);   // reads and writes no weights: a pending reset stays pending
     if (!valid_col(c, out) || !d) return fail(WSMC_EARG, "bad output column");
     int r = check_dist(c, *d);
     if (r) return r;
@@ -1834,9 +1939,33 @@ int wsmc_sample(wsmc_ctx* c, int32_t out, const wsmc_dist* d) {
     if ((r = need_cols(c, reads))) return r;
     if ((r = upload_colptr(c))) return r;
     const uint64_t op = c->op++;
+    bool queued = false;
+    if (ew_enabled(c)) {   // join the batch (its kernel writes the column in place)
+        EwBatch* b = ew_open(c);
+        if (b->nops > 0 && (b->nops == kEwOps || ew_reads_lagged(c, out)))
+            if ((r = ew_flush(c))) return r;
+        EwOp& eo = b->ops[b->nops];
+        std::memset(&eo, 0, sizeof(eo));
+        eo.s.d = *d;
+        if (!ew_remap_dist(c, b, eo.s.d)) {   // slots full: launch the batch, then start anew
+            if ((r = ew_flush(c))) return r;
+            eo.s.d = *d;
+            ew_remap_dist(c, b, eo.s.d);
+        }
+        eo.kind = 1;
+        eo.dim = d->dim;
+        eo.out = c->cols[out].front;
+        eo.s.op = op;
+        eo.s.has_sd = d->family == WSMC_FAM_MVNORMAL_ISO && wsmc_operand_is_const(&d->scale);
+        eo.s.sd = eo.s.has_sd ? wsmc_sqrt(wsmc_operand_eval(&d->scale, nullptr, c->N, 0, nullptr)) : 0.0;
+        if (d->mean_fn == WSMC_MEAN_OSCILLATOR) c->ew_feat = 1;
+        b->nops += 1;
+        queued = true;
+    }
     scores_touch(c, out);
     wrote_col(c, out);
-    WSMC_HIP(launch_sample(c->stream, c->cols[out].front, d->dim, *d, c->seed, op, c->goff, c->d_colptr, c->N));
+    if (!queued)
+        WSMC_HIP(launch_sample(c->stream, c->cols[out].front, d->dim, *d, c->seed, op, c->goff, c->d_colptr, c->N));
     push_sample_term(c, out, *d);
     c->depth += 1;
     return WSMC_OK;
@@ -1869,7 +1998,7 @@ int wsmc_sample_importance(wsmc_ctx* c, int32_t out, const wsmc_dist* prop, cons
 
 static int weigh(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x, int kind) {
     if (c && c->multi) return multi_each(c, [&](wsmc_ctx* s) { return weigh(s, d, x, kind); });
-    CHECK_CTX_KEEP(c);   // a pending weight reset is applied by the kernel itself
+    CHECK_CTX_EW(c);   // a pending weight reset is applied by the kernel itself
     if (!d || !x) return fail(WSMC_EARG, "null argument");
     int r = check_dist(c, *d);
     if (r) return r;
@@ -1887,11 +2016,47 @@ static int weigh(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x, int kin
     cols_of(t, reads);
     if ((r = need_cols(c, reads))) return r;
     if ((r = upload_colptr(c))) return r;
-    const int wb = c->wnext;
-    WSMC_HIP(launch_weigh(c->stream, t, c->w, c->d_colptr, c->N, c->wslots[wb], c->wslots[wb ^ 1],
-                          c->w_reset_pending));
+    int wb = c->wnext;
+    if (ew_enabled(c)) {   // join the batch: its weight terms share one register and one max
+        EwBatch* b = ew_open(c);
+        if (b->nops == kEwOps)
+            if ((r = ew_flush(c))) return r;
+        EwOp& eo = b->ops[b->nops];
+        std::memset(&eo, 0, sizeof(eo));
+        eo.w.t = t;
+        bool ok = ew_remap_dist(c, b, eo.w.t.dist);
+        for (int k = 0; k < 4 && ok; ++k) ok = ew_remap(c, b, eo.w.t.x[k]);
+        if (!ok) {
+            if ((r = ew_flush(c))) return r;
+            eo.w.t = t;
+            ew_remap_dist(c, b, eo.w.t.dist);
+            for (int k = 0; k < 4; ++k) ew_remap(c, b, eo.w.t.x[k]);
+        }
+        eo.kind = 2;
+        eo.dim = t.dist.dim;
+        eo.w.lm0 = wsmc_logmemo{0, 0.0, 0.0, 0};
+        if (t.dist.family != WSMC_FAM_UNIFORM && wsmc_operand_is_const(&t.dist.scale)) {
+            const double sc = wsmc_operand_eval(&t.dist.scale, nullptr, c->N, 0, nullptr);
+            eo.w.lm0 = wsmc_logmemo{wsmc_d2bits(sc), wsmc_log(sc), 1.0 / sc, 1};
+        }
+        if (t.dist.mean_fn == WSMC_MEAN_OSCILLATOR) c->ew_feat = 1;
+        if (!b->has_w) {   // the batch's first weight term: the pending reset, the slot pair
+            b->has_w = 1;
+            b->w = c->w;
+            b->wreset = c->w_reset_pending;
+            b->ms = c->wslots[wb];
+            b->ms_next = c->wslots[wb ^ 1];
+            c->wnext = wb ^ 1;
+        } else {
+            wb = c->wmax_buf;   // the batch's max goes to its first term's slots
+        }
+        b->nops += 1;
+    } else {
+        WSMC_HIP(launch_weigh(c->stream, t, c->w, c->d_colptr, c->N, c->wslots[wb], c->wslots[wb ^ 1],
+                              c->w_reset_pending));
+        c->wnext = wb ^ 1;
+    }
     c->w_reset_pending = nullptr;
-    c->wnext = wb ^ 1;
     c->wmax_buf = wb;
     c->wseq += 1;
     c->wmax_seq = c->wseq;
@@ -1918,7 +2083,7 @@ static inline int64_t run_grp_words(int64_t N);
 
 int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resampled_out, double* ess_out) {
     if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { int32_t rs = 0; double e = 0; const bool f = x == multi_first(c); int r = wsmc_resample(x, ess_min, scheme, resampled_out ? &rs : nullptr, ess_out ? &e : nullptr); if (!r && f) { if (resampled_out) *resampled_out = rs; if (ess_out) *ess_out = e; } return r; });
-    CHECK_CTX_KEEP(c);   // a gated no-op Resample leaves a pending weight reset pending (settled below)
+    CHECK_CTX_EW(c);   // a gated no-op Resample leaves a pending weight reset pending (settled below)
     if (!valid_scheme(scheme)) return fail(WSMC_EARG, "unknown resampling scheme");
     if (scheme == WSMC_RESAMPLE_MULTINOMIAL && exact_mode(c))
         return fail(WSMC_EARG, "multinomial draws on exact shards are not supported (island mode is)");
@@ -1931,11 +2096,12 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
         if (int r = resolve_decisions(c)) return r;
         if (int r = check_deferred(c)) return r;
     }
-    if (!c->weights_changed) {
+    if (!c->weights_changed) {   // a no-op: the statement batch stays open
         if (resampled_out) *resampled_out = c->resampled;
         if (ess_out) *ess_out = c->last_ess;
         return WSMC_OK;
     }
+    if (int r = ew_flush(c)) return r;
     if (c->w_reset_pending) {   // (a weight write settles it first, so this does not happen)
         WSMC_HIP(launch_fill_weights(c->stream, c->w, c->w_reset_pending, c->N));
         c->w_reset_pending = nullptr;

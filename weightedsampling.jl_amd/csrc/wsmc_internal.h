@@ -123,6 +123,7 @@ struct RunGraph {
 };
 
 struct MultiState;   // wsmc_multi.hip
+struct EwBatch;      // below
 }  // namespace wsmc
 
 struct wsmc_ctx {
@@ -226,6 +227,9 @@ struct wsmc_ctx {
     int64_t d_ctape_cap = 0;
     void* d_prog = nullptr;                 // compiled fold program: segments, then constants
     int64_t d_prog_cap = 0;                 // bytes
+    wsmc::EwBatch* ew = nullptr;            // elementwise statements not launched yet (one kernel at
+    unsigned ew_feat = 0;                   // the next other entry point); the oscillator mean seen
+    std::vector<int32_t> ew_lag;            // columns the batch reads one Resample behind
     char* prog_stage = nullptr;             // pinned staging ring of the programs too large to ride
     int64_t prog_stage_cap = 0, prog_stage_at = 0;   // in the Move's arguments (ProgInline)
     unsigned long long* rs_grp[2] = {nullptr, nullptr};   // generic Resample's group lines (double-buffered)
@@ -314,6 +318,53 @@ struct Indirect {
 };
 hipError_t launch_assign(hipStream_t s, double* out, int dim, const wsmc_operand* expr,
                          double* const* cols, int64_t N, const Indirect& ind);
+// A batch of consecutive elementwise statements (Assign / Sample / Observe / Weight) run as one
+// kernel, each particle taking the statements in order (csrc/wsmc_api.hip ew_*). The batch
+// travels in the kernel's arguments (read in place through the kernarg segment).
+constexpr int kEwOps = 6;       // statements a batch holds
+constexpr int kEwSlots = 24;    // column components the Sample / weight terms read
+struct EwAssign {
+    wsmc_operand e[4];
+    const double* p[4][2];      // operand components resolved to pointers
+    uint32_t lag;               // bit 2k+m: operand read one lazy Resample behind (the batch's row)
+    int32_t pad;
+};
+struct EwSample {
+    wsmc_dist d;                // operand columns renumbered to the batch's slots
+    unsigned long long op;
+    int32_t has_sd, pad;
+    double sd;                  // a constant MvNormal variance's sqrt (host-evaluated)
+};
+struct EwWeigh {
+    wsmc_term t;                // operand columns renumbered to the batch's slots
+    wsmc_logmemo lm0;           // a constant scale's log / reciprocal (host-evaluated)
+};
+struct EwOp {
+    int32_t kind;               // 0 Assign, 1 Sample, 2 Observe / Weight
+    int32_t dim;
+    double* out;                // Assign / Sample destination (components N apart)
+    union {
+        EwAssign a;
+        EwSample s;
+        EwWeigh w;
+    };
+};
+struct EwBatch {
+    int32_t nops, ntab;
+    int32_t has_w, nslots;
+    const int32_t* anc;         // the newest lazy Resample's ancestors (lagged Assign operands)
+    const Decision* dec;        // and its decision
+    double* w;
+    const Decision* wreset;     // a pending weight reset (the first weight term applies it)
+    MaxSlots* ms;               // the max of the final weights (zero on entry)
+    MaxSlots* ms_next;          // zeroed by block 0
+    double** tab;               // device column table: entries moved by Assigns into fresh buffers
+    double* tab_out[4];
+    int32_t tab_col[4];
+    const double* slot[kEwSlots];
+    EwOp ops[kEwOps];
+};
+hipError_t launch_ew_batch(hipStream_t s, const EwBatch& b, unsigned feat, uint64_t seed, int64_t goff, int64_t N);
 hipError_t launch_sample(hipStream_t s, double* out, int dim, const wsmc_dist& d, uint64_t seed,
                          uint64_t op, int64_t goff, double* const* cols, int64_t N);
 hipError_t launch_sample_importance(hipStream_t s, double* out, int dim, const wsmc_dist& prop,

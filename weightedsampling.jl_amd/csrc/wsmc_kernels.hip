@@ -265,6 +265,70 @@ __global__ __launch_bounds__(kBlock) void k_weigh(wsmc_term t, double* w, double
         for (int k = threadIdx.x; k < kSlots * 16; k += kBlock) ms_next->v[k >> 4][k & 15] = 0ull;
 }
 
+// A batch of elementwise statements (EwBatch, the first argument: read in place through the
+// kernarg segment pointer): per particle, each statement in order with k_assign's, k_sample's
+// and k_weigh's arithmetic — one launch for a model step's Assign / Sample / Observe run. The
+// weights stay in a register across the batch's weight terms (the first applies a pending
+// reset); the block max of the final weights goes to the batch's slots.
+template <unsigned FEAT>
+__global__ __launch_bounds__(kBlock) void k_ew_batch(EwBatch, uint64_t seed, int64_t goff, int64_t N) {
+    const EwBatch* B = (const EwBatch*)(const char*)__builtin_amdgcn_kernarg_segment_ptr();
+    __shared__ u64 lds[4];
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    double* const* cols = const_cast<double* const*>(B->slot);
+    if (i == 0)
+        for (int t = 0; t < B->ntab; ++t) B->tab[B->tab_col[t]] = B->tab_out[t];
+    u64 m = 0;
+    if (i < N) {
+        const int64_t j = (B->anc && (!B->dec || B->dec->resampled)) ? (int64_t)B->anc[i] : i;
+        double wv = 0.0;
+        bool wl = false;
+        for (int k = 0; k < B->nops; ++k) {
+            const EwOp& op = B->ops[k];
+            const int dim = op.dim;
+            if (op.kind == 0) {
+                double x[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (q >= dim) continue;
+                    const wsmc_operand& o = op.a.e[q];
+                    double v = o.c0;
+                    if (o.col[0] >= 0) v = v + o.coef[0] * op.a.p[q][0][(op.a.lag >> (2 * q)) & 1 ? j : i];
+                    if (o.col[1] >= 0) v = v + o.coef[1] * op.a.p[q][1][(op.a.lag >> (2 * q + 1)) & 1 ? j : i];
+                    x[q] = v;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (q < dim) op.out[(int64_t)q * N + i] = x[q];
+            } else if (op.kind == 1) {
+                double x[4];
+                const double sdl = op.s.sd;
+                wsmc_dist_sample_mf(&op.s.d, x, seed, op.s.op, (uint64_t)(goff + i), cols, N, i,
+                                    op.s.has_sd ? &sdl : nullptr, FEAT);
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (q < dim) op.out[(int64_t)q * N + i] = x[q];
+            } else {
+                if (!wl) {
+                    wv = (B->wreset && B->wreset->resampled) ? B->wreset->mean : B->w[i];
+                    wl = true;
+                }
+                wsmc_logmemo lm = op.w.lm0;
+                wv = wv + wsmc_term_logpdf_mf(&op.w.t, cols, N, i, nullptr, &lm, FEAT);
+            }
+        }
+        if (wl) {
+            B->w[i] = wv;
+            m = wsmc_ord_enc(wv);
+        }
+    }
+    if (!B->has_w) return;
+    m = block_max_u64(m, lds);
+    if (threadIdx.x == 0) atomic_max_filtered(&B->ms->v[blockIdx.x % kSlots][0], m);
+    if (blockIdx.x == 0)
+        for (int k = threadIdx.x; k < kSlots * 16; k += kBlock) B->ms_next->v[k >> 4][k & 15] = 0ull;
+}
+
 // ------------------------------------------------------------------------------------
 // Resample (src/transformers.jl:474-498) as four passes per invocation:
 //   max      block max of the log-weights -> 64 slots (read-filtered atomicMax)
@@ -2815,6 +2879,14 @@ hipError_t launch_sample(hipStream_t s, double* out, int dim, const wsmc_dist& d
     else
         hipLaunchKernelGGL(k_sample<0u>, grid_for(N), dim3(kBlock), 0, s, out, dim, d, seed, op, goff, cols, N, has_sd,
                            sd);
+    return hipGetLastError();
+}
+hipError_t launch_ew_batch(hipStream_t s, const EwBatch& b, unsigned feat, uint64_t seed, int64_t goff, int64_t N) {
+    static_assert(sizeof(EwBatch) + 32 <= 4096, "the batch rides in the kernel arguments");
+    if (feat)
+        hipLaunchKernelGGL(k_ew_batch<WSMC_FEAT_ALL>, grid_for(N), dim3(kBlock), 0, s, b, seed, goff, N);
+    else
+        hipLaunchKernelGGL(k_ew_batch<0u>, grid_for(N), dim3(kBlock), 0, s, b, seed, goff, N);
     return hipGetLastError();
 }
 hipError_t launch_sample_importance(hipStream_t s, double* out, int dim, const wsmc_dist& prop,
