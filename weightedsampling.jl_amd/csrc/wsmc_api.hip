@@ -67,11 +67,13 @@ static int ew_flush(wsmc_ctx* c) {
     EwBatch* b = c->ew;
     if (!b || b->nops == 0) return WSMC_OK;
     const hipError_t e = launch_ew_batch(c->stream, *b, c->ew_feat, c->seed, c->goff, c->N);
-    b->nops = b->ntab = b->has_w = b->nslots = 0;
+    b->nops = b->ntab = b->has_w = b->nslots = b->nrows = b->npre = 0;
     b->anc = nullptr;
     b->dec = nullptr;
     c->ew_feat = 0;
     c->ew_lag.clear();
+    c->ew_rows.clear();
+    c->ew_unstaged.clear();
     if (e != hipSuccess) return fail(WSMC_EHIP, std::string("statement batch: ") + hipGetErrorString(e));
     return WSMC_OK;
 }
@@ -87,24 +89,78 @@ static bool ew_reads_lagged(const wsmc_ctx* c, int32_t col) {
         if (x == col) return true;
     return false;
 }
-// an operand's columns renumbered to the batch's slots (the column's current front); false: full
-static bool ew_remap(const wsmc_ctx* c, EwBatch* b, wsmc_operand& o) {
+// the LDS rows of a column buffer in the batch, read directly or through the ancestors (-1: none)
+static int ew_row_of(const wsmc_ctx* c, const double* p, int lag = 0) {
+    for (const auto& e : c->ew_rows)
+        if (e.p == p && e.lag == lag) return e.row;
+    return -1;
+}
+// rows loaded at the start for a column (all its components); -1: no room
+static int ew_preload(wsmc_ctx* c, EwBatch* b, const double* p, int dim, int lag) {
+    if (b->nrows + dim > kEwRows || b->npre + dim > kEwPre) return -1;
+    const int r = b->nrows;
+    b->nrows += dim;
+    for (int q = 0; q < dim; ++q) {
+        b->pre_src[b->npre] = p + (int64_t)q * c->N;
+        b->pre_row[b->npre] = (int8_t)(r + q);
+        b->pre_lag[b->npre] = (int8_t)lag;
+        b->npre += 1;
+    }
+    c->ew_rows.push_back({p, lag, r});
+    return r;
+}
+// rows for a statement's output (its buffer keeps the rows it has: later readers see the new
+// values there); -1: none left (the output is unstaged)
+static int ew_out_rows(wsmc_ctx* c, EwBatch* b, const double* p, int dim) {
+    int r = ew_row_of(c, p);
+    if (r >= 0) return r;
+    if (b->nrows + dim > kEwRows) {
+        c->ew_unstaged.push_back(p);
+        return -1;
+    }
+    r = b->nrows;
+    b->nrows += dim;
+    c->ew_rows.push_back({p, 0, r});
+    return r;
+}
+// an operand's columns renumbered to the batch's slots, each slot's rows an earlier output's
+// or loaded at the start; false: no room, or a column an earlier statement wrote without rows
+static bool ew_remap(wsmc_ctx* c, EwBatch* b, wsmc_operand& o) {
     for (int m = 0; m < 2; ++m) {
         if (o.col[m] < 0) continue;
-        const double* p = c->cols[o.col[m]].front;
+        const Column& col = c->cols[o.col[m]];
+        const double* p = col.front;
+        for (const double* u : c->ew_unstaged)
+            if (u == p) return false;
         int s = -1;
         for (int k = 0; k < b->nslots; ++k)
             if (b->slot[k] == p) s = k;
         if (s < 0) {
             if (b->nslots == kEwSlots) return false;
+            int r = ew_row_of(c, p);
+            if (r < 0) r = ew_preload(c, b, p, col.dim, 0);   // not written in the batch: loaded at the start
+            if (r < 0) return false;
             s = b->nslots++;
             b->slot[s] = p;
+            b->slot_row[s] = (int8_t)r;
         }
         o.col[m] = s;
     }
     return true;
 }
-static bool ew_remap_dist(const wsmc_ctx* c, EwBatch* b, wsmc_dist& d) {
+// a statement's operand columns staged all or none (the batch state restored on failure)
+template <typename F>
+static bool ew_stage(wsmc_ctx* c, EwBatch* b, F&& remap_all) {
+    const int32_t ns = b->nslots, nr = b->nrows, np = b->npre;
+    const size_t nrow = c->ew_rows.size();
+    if (remap_all()) return true;
+    b->nslots = ns;
+    b->nrows = nr;
+    b->npre = np;
+    c->ew_rows.resize(nrow);
+    return false;
+}
+static bool ew_remap_dist(wsmc_ctx* c, EwBatch* b, wsmc_dist& d) {
     for (int k = 0; k < 4; ++k)
         if (!ew_remap(c, b, d.mu[k])) return false;
     return ew_remap(c, b, d.scale);
@@ -1894,10 +1950,23 @@ int wsmc_assign(wsmc_ctx* c, int32_t out, const wsmc_operand* expr) {
             for (int m = 0; m < 2; ++m) {
                 const int32_t id = op.a.e[k].col[m];
                 op.a.p[k][m] = id >= 0 ? fronts[id] + (int64_t)op.a.e[k].comp[m] * c->N : nullptr;
-                if (id >= 0 && k < dim && ((ind.mask >> (2 * k + m)) & 1)) c->ew_lag.push_back(id);
+                op.a.fwd[k][m] = -1;
+                if (id < 0 || k >= dim) continue;
+                const int lag = (ind.mask >> (2 * k + m)) & 1;
+                if (lag) c->ew_lag.push_back(id);
+                // its LDS rows: an earlier statement's output, or loaded at the start (directly
+                // or through the ancestors); without room the kernel reads the column itself
+                int rr = ew_row_of(c, fronts[id], lag);
+                if (rr < 0) {
+                    bool unstaged = false;
+                    for (const double* u : c->ew_unstaged) unstaged |= u == fronts[id];
+                    if (!unstaged) rr = ew_preload(c, b, fronts[id], c->cols[id].dim, lag);
+                }
+                if (rr >= 0) op.a.fwd[k][m] = (int8_t)(rr + op.a.e[k].comp[m]);
             }
         }
         op.a.lag = ind.mask;
+        op.out_row = (int16_t)ew_out_rows(c, b, dst, dim);
         if (ind.mask) {
             b->anc = ind.row;
             b->dec = ind.dec;
@@ -1947,20 +2016,27 @@ int wsmc_sample(wsmc_ctx* c, int32_t out, const wsmc_dist* d) {
         EwOp& eo = b->ops[b->nops];
         std::memset(&eo, 0, sizeof(eo));
         eo.s.d = *d;
-        if (!ew_remap_dist(c, b, eo.s.d)) {   // slots full: launch the batch, then start anew
+        auto stage = [&] { return ew_stage(c, b, [&] { return ew_remap_dist(c, b, eo.s.d); }); };
+        if (!stage()) {   // no room, or a column written without rows: launch the batch first
             if ((r = ew_flush(c))) return r;
             eo.s.d = *d;
-            ew_remap_dist(c, b, eo.s.d);
+            queued = stage();
+        } else {
+            queued = true;
         }
+    }
+    if (queued) {
+        EwBatch* b = c->ew;
+        EwOp& eo = b->ops[b->nops];
         eo.kind = 1;
-        eo.dim = d->dim;
+        eo.dim = (int16_t)d->dim;
         eo.out = c->cols[out].front;
+        eo.out_row = (int16_t)ew_out_rows(c, b, eo.out, d->dim);
         eo.s.op = op;
         eo.s.has_sd = d->family == WSMC_FAM_MVNORMAL_ISO && wsmc_operand_is_const(&d->scale);
         eo.s.sd = eo.s.has_sd ? wsmc_sqrt(wsmc_operand_eval(&d->scale, nullptr, c->N, 0, nullptr)) : 0.0;
         if (d->mean_fn == WSMC_MEAN_OSCILLATOR) c->ew_feat = 1;
         b->nops += 1;
-        queued = true;
     }
     scores_touch(c, out);
     wrote_col(c, out);
@@ -2017,6 +2093,7 @@ static int weigh(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x, int kin
     if ((r = need_cols(c, reads))) return r;
     if ((r = upload_colptr(c))) return r;
     int wb = c->wnext;
+    bool queued = false;
     if (ew_enabled(c)) {   // join the batch: its weight terms share one register and one max
         EwBatch* b = ew_open(c);
         if (b->nops == kEwOps)
@@ -2024,16 +2101,28 @@ static int weigh(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x, int kin
         EwOp& eo = b->ops[b->nops];
         std::memset(&eo, 0, sizeof(eo));
         eo.w.t = t;
-        bool ok = ew_remap_dist(c, b, eo.w.t.dist);
-        for (int k = 0; k < 4 && ok; ++k) ok = ew_remap(c, b, eo.w.t.x[k]);
-        if (!ok) {
+        auto stage = [&] {
+            return ew_stage(c, b, [&] {
+                if (!ew_remap_dist(c, b, eo.w.t.dist)) return false;
+                for (int k = 0; k < 4; ++k)
+                    if (!ew_remap(c, b, eo.w.t.x[k])) return false;
+                return true;
+            });
+        };
+        if (!stage()) {   // no room, or a column written without rows: launch the batch first
             if ((r = ew_flush(c))) return r;
             eo.w.t = t;
-            ew_remap_dist(c, b, eo.w.t.dist);
-            for (int k = 0; k < 4; ++k) ew_remap(c, b, eo.w.t.x[k]);
+            queued = stage();
+        } else {
+            queued = true;
         }
+    }
+    if (queued) {
+        EwBatch* b = c->ew;
+        EwOp& eo = b->ops[b->nops];
         eo.kind = 2;
-        eo.dim = t.dist.dim;
+        eo.dim = (int16_t)t.dist.dim;
+        eo.out_row = -1;
         eo.w.lm0 = wsmc_logmemo{0, 0.0, 0.0, 0};
         if (t.dist.family != WSMC_FAM_UNIFORM && wsmc_operand_is_const(&t.dist.scale)) {
             const double sc = wsmc_operand_eval(&t.dist.scale, nullptr, c->N, 0, nullptr);

@@ -230,6 +230,13 @@ struct wsmc_ctx {
     wsmc::EwBatch* ew = nullptr;            // elementwise statements not launched yet (one kernel at
     unsigned ew_feat = 0;                   // the next other entry point); the oscillator mean seen
     std::vector<int32_t> ew_lag;            // columns the batch reads one Resample behind
+    struct EwRow {
+        const double* p;                    // column buffer
+        int lag;                            // read through the batch's ancestor row
+        int row;                            // its first LDS row in the batch
+    };
+    std::vector<EwRow> ew_rows;
+    std::vector<const double*> ew_unstaged; // outputs of the batch without rows (no later LDS reads)
     char* prog_stage = nullptr;             // pinned staging ring of the programs too large to ride
     int64_t prog_stage_cap = 0, prog_stage_at = 0;   // in the Move's arguments (ProgInline)
     unsigned long long* rs_grp[2] = {nullptr, nullptr};   // generic Resample's group lines (double-buffered)
@@ -322,12 +329,14 @@ hipError_t launch_assign(hipStream_t s, double* out, int dim, const wsmc_operand
 // kernel, each particle taking the statements in order (csrc/wsmc_api.hip ew_*). The batch
 // travels in the kernel's arguments (read in place through the kernarg segment).
 constexpr int kEwOps = 6;       // statements a batch holds
-constexpr int kEwSlots = 24;    // column components the Sample / weight terms read
+constexpr int kEwSlots = 16;    // columns the Sample / weight terms read
+constexpr int kEwRows = 12;     // LDS rows (one column component each, a value per thread)
+constexpr int kEwPre = 10;      // components loaded into LDS rows at the start
 struct EwAssign {
     wsmc_operand e[4];
     const double* p[4][2];      // operand components resolved to pointers
     uint32_t lag;               // bit 2k+m: operand read one lazy Resample behind (the batch's row)
-    int32_t pad;
+    int8_t fwd[4][2];           // >= 0: the operand is an LDS row (an earlier statement's output)
 };
 struct EwSample {
     wsmc_dist d;                // operand columns renumbered to the batch's slots
@@ -341,7 +350,9 @@ struct EwWeigh {
 };
 struct EwOp {
     int32_t kind;               // 0 Assign, 1 Sample, 2 Observe / Weight
-    int32_t dim;
+    int16_t dim;
+    int16_t out_row;            // >= 0: the output's components also go to LDS rows out_row..
+                                // (later statements of the batch read them there)
     double* out;                // Assign / Sample destination (components N apart)
     union {
         EwAssign a;
@@ -361,7 +372,14 @@ struct EwBatch {
     double** tab;               // device column table: entries moved by Assigns into fresh buffers
     double* tab_out[4];
     int32_t tab_col[4];
+    // the Sample / weight terms read their columns from LDS: slot s at rows slot_row[s] +
+    // component (an earlier statement's output, or loaded at the start: pre_src -> pre_row)
     const double* slot[kEwSlots];
+    int8_t slot_row[kEwSlots];
+    int32_t nrows, npre;
+    const double* pre_src[kEwPre];
+    int8_t pre_row[kEwPre];
+    int8_t pre_lag[kEwPre];     // loaded through the ancestor row
     EwOp ops[kEwOps];
 };
 hipError_t launch_ew_batch(hipStream_t s, const EwBatch& b, unsigned feat, uint64_t seed, int64_t goff, int64_t N);

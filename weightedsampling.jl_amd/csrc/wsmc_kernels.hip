@@ -267,57 +267,75 @@ __global__ __launch_bounds__(kBlock) void k_weigh(wsmc_term t, double* w, double
 
 // A batch of elementwise statements (EwBatch, the first argument: read in place through the
 // kernarg segment pointer): per particle, each statement in order with k_assign's, k_sample's
-// and k_weigh's arithmetic — one launch for a model step's Assign / Sample / Observe run. The
-// weights stay in a register across the batch's weight terms (the first applies a pending
-// reset); the block max of the final weights goes to the batch's slots.
+// and k_weigh's arithmetic — one launch for a model step's Assign / Sample / Observe run.
+// Values a later statement reads are kept in LDS rows (one per column component, a value per
+// thread): a statement's output is written to its global column and, when staged, to its rows;
+// the Sample / weight terms evaluate against a pointer table of rows (stride kBlock, index =
+// the thread), the columns no earlier statement wrote loaded into rows at the start — so no
+// statement re-reads from memory what an earlier one just stored. The weights stay in a
+// register across the weight terms (the first applies a pending reset); the block max of the
+// final weights goes to the batch's slots.
 template <unsigned FEAT>
 __global__ __launch_bounds__(kBlock) void k_ew_batch(EwBatch, uint64_t seed, int64_t goff, int64_t N) {
     const EwBatch* B = (const EwBatch*)(const char*)__builtin_amdgcn_kernarg_segment_ptr();
     __shared__ u64 lds[4];
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    double* const* cols = const_cast<double* const*>(B->slot);
+    __shared__ double rows[kEwRows * kBlock];
+    __shared__ double* ctab[kEwSlots];
+    const int th = threadIdx.x;
+    const int64_t i = (int64_t)blockIdx.x * kBlock + th;
+    const bool in = i < N;
     if (i == 0)
         for (int t = 0; t < B->ntab; ++t) B->tab[B->tab_col[t]] = B->tab_out[t];
+    if (th < B->nslots) ctab[th] = rows + (int)B->slot_row[th] * kBlock;
+    // every load that depends on no statement, up front: the preloaded rows, the ancestor, the
+    // weight
+    const int64_t j = (in && B->anc && (!B->dec || B->dec->resampled)) ? (int64_t)B->anc[i] : i;
+    for (int p = 0; p < B->npre; ++p)
+        rows[(int)B->pre_row[p] * kBlock + th] = in ? B->pre_src[p][B->pre_lag[p] ? j : i] : 0.0;
+    double wv = 0.0;
+    if (in && B->has_w) wv = (B->wreset && B->wreset->resampled) ? B->wreset->mean : B->w[i];
+    __syncthreads();
+    double* const* cols = ctab;
     u64 m = 0;
-    if (i < N) {
-        const int64_t j = (B->anc && (!B->dec || B->dec->resampled)) ? (int64_t)B->anc[i] : i;
-        double wv = 0.0;
-        bool wl = false;
+    if (in) {
         for (int k = 0; k < B->nops; ++k) {
             const EwOp& op = B->ops[k];
             const int dim = op.dim;
+            double x[4] = {0.0, 0.0, 0.0, 0.0};
             if (op.kind == 0) {
-                double x[4];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     if (q >= dim) continue;
                     const wsmc_operand& o = op.a.e[q];
                     double v = o.c0;
-                    if (o.col[0] >= 0) v = v + o.coef[0] * op.a.p[q][0][(op.a.lag >> (2 * q)) & 1 ? j : i];
-                    if (o.col[1] >= 0) v = v + o.coef[1] * op.a.p[q][1][(op.a.lag >> (2 * q + 1)) & 1 ? j : i];
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        if (o.col[c] < 0) continue;
+                        const int f = op.a.fwd[q][c];
+                        const double xv = f >= 0 ? rows[f * kBlock + th]
+                                                 : op.a.p[q][c][(op.a.lag >> (2 * q + c)) & 1 ? j : i];
+                        v = v + o.coef[c] * xv;
+                    }
                     x[q] = v;
                 }
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    if (q < dim) op.out[(int64_t)q * N + i] = x[q];
             } else if (op.kind == 1) {
-                double x[4];
                 const double sdl = op.s.sd;
-                wsmc_dist_sample_mf(&op.s.d, x, seed, op.s.op, (uint64_t)(goff + i), cols, N, i,
+                wsmc_dist_sample_mf(&op.s.d, x, seed, op.s.op, (uint64_t)(goff + i), cols, kBlock, th,
                                     op.s.has_sd ? &sdl : nullptr, FEAT);
+            } else {
+                wsmc_logmemo lm = op.w.lm0;
+                wv = wv + wsmc_term_logpdf_mf(&op.w.t, cols, kBlock, th, nullptr, &lm, FEAT);
+                continue;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (q < dim) op.out[(int64_t)q * N + i] = x[q];
+            if (op.out_row >= 0)
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
-                    if (q < dim) op.out[(int64_t)q * N + i] = x[q];
-            } else {
-                if (!wl) {
-                    wv = (B->wreset && B->wreset->resampled) ? B->wreset->mean : B->w[i];
-                    wl = true;
-                }
-                wsmc_logmemo lm = op.w.lm0;
-                wv = wv + wsmc_term_logpdf_mf(&op.w.t, cols, N, i, nullptr, &lm, FEAT);
-            }
+                    if (q < dim) rows[(op.out_row + q) * kBlock + th] = x[q];
         }
-        if (wl) {
+        if (B->has_w) {
             B->w[i] = wv;
             m = wsmc_ord_enc(wv);
         }
