@@ -81,6 +81,16 @@ class ShardCtx:
         acc = self._move(proposal, targets, step, lo, hi, target_depth, diversity)
         return acc if wait else None
 
+    def move_block(self, moves, gated=False, wait=False):
+        """wsmc_move_block: the block's Moves one after the other, each through the protocol"""
+        out = []
+        for mv in moves:
+            lo = mv[3] if len(mv) > 3 else None
+            hi = mv[4] if len(mv) > 4 else None
+            depth = mv[5] if len(mv) > 5 else -1
+            out.append(self._move(mv[0], mv[1], mv[2], lo, hi, depth))
+        return out if wait else None
+
     def _move(self, proposal, targets, step, lo=None, hi=None, target_depth=-1, diversity=float("nan")):
         import math
         from wsmc import abi

@@ -156,3 +156,42 @@ def test_last_ancestors_across_store_modes(gpu_available, switch, wait):
     assert st["n_resamples"] == o.get_state()["n_resamples"]
     np.testing.assert_array_equal(g.last_ancestors(), o.last_ancestors())
     assert_same_state(g, o)
+
+
+@pytest.mark.parametrize("ess", [1.0, 0.6])
+def test_statement_batch_hazards(gpu_available, ess):
+    """Statement batches (one kernel per run of Assign / Sample / Observe / Weight calls) against
+    the oracle's one-statement-at-a-time path, bit for bit, over the cases the batch must get
+    right: an Assign reading columns one Resample behind (through the ancestors) followed by an
+    in-place Sample of one of them (the batch must end first), a weight term reading what a
+    Sample of the same batch wrote (its LDS row), an Assign that reads its own output behind
+    (a fresh buffer), two weight terms in one batch (the weight register), a 2-component
+    column read by component, more statements than a batch holds, and a no-op Resample in the
+    middle (the batch stays open)."""
+    from wsmc.dsl import Col, MvNormal, Normal
+    N = 3001
+    res = []
+    for ctx in (wsmc.Context(N, seed=5), Oracle(N, seed=5)):
+        R = models.resolver(ctx)
+        ca = ctx.col_create("a", 1)
+        cb = ctx.col_create("b", 2)
+        cc = ctx.col_create("c", 1)
+        cd = ctx.col_create("d", 1)
+        ctx.sample(ca, Normal(0.0, 1.0).dist(R))
+        ctx.sample(cb, MvNormal([0.0, 0.0], np.eye(2)).dist(R))
+        for t in range(6):
+            ctx.assign(cc, models.value_operands(Col("a") + Col("b", 1) * 0.5, 1, R))   # a, b behind
+            ctx.resample(ess, wait=False)                                               # a no-op: weights unchanged
+            ctx.sample(ca, Normal(Col("c"), 1.0).dist(R))                              # a in place
+            ctx.observe(Normal(Col("a"), 1.0).dist(R), models._const([0.1 * t]))       # a from the batch
+            if t % 2:
+                ctx.resample(ess, wait=False)                                           # a Resample mid-step
+            ctx.assign(cb, models.value_operands([Col("b", 0) + Col("a"), Col("b", 1) - Col("c")], 2, R))
+            ctx.weight(Normal(Col("b", 1), 2.0).dist(R), models._const([0.3]))        # b's new buffer
+            ctx.assign(cd, models.value_operands(Col("c") * 2.0 + Col("d"), 1, R))
+            ctx.assign(cc, models.value_operands(Col("d") - Col("a"), 1, R))           # a seventh statement
+            ctx.resample(ess, wait=False)
+        res.append(ctx)
+    g, o = res
+    assert_same_state(g, o)
+    assert g.log_evidence() == o.log_evidence()

@@ -137,11 +137,18 @@ def test_linreg_autorw(gpu_available, ess):
     assert_same_state(g, o)
 
 
-def test_oscillator_bounded_autorw(gpu_available):
-    t, y = models.oscillator_data(n=12)
+@pytest.mark.parametrize("block", [False, True])
+@pytest.mark.parametrize("wait", [True, False])
+def test_oscillator_bounded_autorw(gpu_available, block, wait):
+    """C5's sweeps as two Moves or one statement block (a 5-target union: one moments pass per
+    Move, the oscillator fold in the block kernel; 20 observations take the program past the
+    kernel arguments into the uploaded form)"""
+    t, y = models.oscillator_data(n=20)
     g, o = wsmc.Context(4096, seed=42), Oracle(4096, seed=42)
-    ag = models.oscillator_statements(g, t, y, ess_perc_min=1.0, sweeps=2, diversity=None)
-    ao = models.oscillator_statements(o, t, y, ess_perc_min=1.0, sweeps=2, diversity=None)
+    ag = models.oscillator_statements(g, t, y, ess_perc_min=1.0, sweeps=2, diversity=None, block=block,
+                                      wait_moves=wait)
+    ao = models.oscillator_statements(o, t, y, ess_perc_min=1.0, sweeps=2, diversity=None, block=block,
+                                      wait_moves=wait)
     assert ag == ao
     assert_same_state(g, o)
 
@@ -522,24 +529,29 @@ def test_gated_moves_match_oracle(gpu_available, ess, block):
 
 
 def _block_model(ctx, sigma_col):
-    """a, b ~ N(0, 10), c ~ HalfNormal(2): y => N(a + b x, c or 1) (the scale a column, or a
-    constant: the precomputed-scale fold path)"""
-    from wsmc.dsl import Col, HalfNormal, Normal
+    """a, b ~ N(0, 10), c ~ HalfNormal(2), d ~ N(0, 1), e ~ Uniform(-π, π): y => N(a + b x, c or 1)
+    (the scale a column, or a constant: the precomputed-scale fold path); d and e enter the
+    score through their priors only"""
+    from wsmc.dsl import Col, HalfNormal, Normal, Uniform
     R = models.resolver(ctx)
     cols = []
-    for name, prior in (("a", Normal(0.0, 10.0)), ("b", Normal(0.0, 10.0)), ("c", HalfNormal(2.0))):
+    for name, prior in (("a", Normal(0.0, 10.0)), ("b", Normal(0.0, 10.0)), ("c", HalfNormal(2.0)),
+                        ("d", Normal(0.0, 1.0)), ("e", Uniform(-math.pi, math.pi))):
         cols.append(ctx.col_create(name, 1))
         ctx.sample(cols[-1], prior.dist(R))
     return cols, R
 
 
-# (move groups as indices into [a, b, c]; bounded groups get lo 0, hi inf)
+# (move groups as indices into [a, b, c, d, e]; a bounded group bounds c to (0, inf) and e to
+# (-π, π), the others stay unbounded)
 _BLOCKS = {
     "ab_c": [((0, 1), False), ((2,), True)],
     "a_b": [((0,), False), ((1,), False)],
     "a_b_c": [((0,), False), ((1,), False), ((2,), True)],
     "overlap": [((0, 1), False), ((1,), False)],       # overlapping targets: the moves one by one
-    "wide": [((0, 1, 2), True), ((0,), False)],        # 4 targets over the limit with overlap
+    "wide": [((0, 1, 2), True), ((0,), False)],        # overlap again
+    "five": [((0, 1, 2, 3), True), ((4,), True)],      # a union of 5: one moments pass per move
+    "eight": [((0, 1), False), ((2, 3), True), ((4,), True)],
 }
 
 
@@ -566,9 +578,10 @@ def test_move_block_matches_oracle(gpu_available, shape, gated, wait, sigma_col)
             moves = []
             for grp, bnd in _BLOCKS[shape]:
                 t = [cols[k] for k in grp]
-                if bnd:   # c >= 0; a, b unbounded within the bounded Move
-                    lo = [0.0 if k == 2 else -math.inf for k in grp]
-                    moves.append((abi.PROPOSAL_AUTORW, t, 1e-3, lo, [math.inf] * len(t)))
+                if bnd:   # c >= 0, e in (-π, π); the others unbounded within the bounded Move
+                    lo = [0.0 if k == 2 else (-math.pi if k == 4 else -math.inf) for k in grp]
+                    hi = [math.pi if k == 4 else math.inf for k in grp]
+                    moves.append((abi.PROPOSAL_AUTORW, t, 1e-3, lo, hi))
                 else:
                     moves.append((abi.PROPOSAL_AUTORW, t, 1e-3))
             counts.append(ctx.move_block(moves, gated=gated, wait=wait))

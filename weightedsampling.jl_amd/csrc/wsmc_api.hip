@@ -66,7 +66,17 @@ static bool ew_enabled(const wsmc_ctx* c) {
 static int ew_flush(wsmc_ctx* c) {
     EwBatch* b = c->ew;
     if (!b || b->nops == 0) return WSMC_OK;
-    const hipError_t e = launch_ew_batch(c->stream, *b, c->ew_feat, c->seed, c->goff, c->N);
+    // a batch of one statement: its own kernel (leaner than the batch's: no rows, no table)
+    hipError_t e;
+    const EwOp& o0 = b->ops[0];
+    if (b->nops > 1)
+        e = launch_ew_batch(c->stream, *b, c->ew_feat, c->seed, c->goff, c->N);
+    else if (o0.kind == 0)
+        e = launch_ew_assign1(c->stream, *b, c->d_colptr, c->N);
+    else if (o0.kind == 1)
+        e = launch_sample(c->stream, o0.out, o0.dim, c->ew_first.dist, c->seed, o0.s.op, c->goff, c->d_colptr, c->N);
+    else
+        e = launch_weigh(c->stream, c->ew_first, b->w, c->d_colptr, c->N, b->ms, b->ms_next, b->wreset);
     b->nops = b->ntab = b->has_w = b->nslots = b->nrows = b->npre = 0;
     b->anc = nullptr;
     b->dec = nullptr;
@@ -546,7 +556,7 @@ int wsmc_create(wsmc_ctx** out, int64_t n_particles, int32_t device, uint64_t se
     ALLOC(c->wslots[0], sizeof(MaxSlots));
     ALLOC(c->wslots[1], sizeof(MaxSlots));
     ALLOC(c->qbuf, sizeof(unsigned long long) * c->N);
-    ALLOC(c->tilepart, sizeof(double) * 16 * c->ntiles);
+    ALLOC(c->tilepart, sizeof(double) * 64 * c->ntiles);   // a Move block's per-move moment sets
     ALLOC(c->rec, sizeof(ShardRecord) * kMaxWorld);
     ALLOC(c->dec, sizeof(Decision));
     ALLOC(c->dec_always, sizeof(Decision));
@@ -2028,6 +2038,7 @@ int wsmc_sample(wsmc_ctx* c, int32_t out, const wsmc_dist* d) {
     if (queued) {
         EwBatch* b = c->ew;
         EwOp& eo = b->ops[b->nops];
+        if (b->nops == 0) c->ew_first.dist = *d;   // as called (a batch of one replays it)
         eo.kind = 1;
         eo.dim = (int16_t)d->dim;
         eo.out = c->cols[out].front;
@@ -2120,6 +2131,7 @@ static int weigh(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x, int kin
     if (queued) {
         EwBatch* b = c->ew;
         EwOp& eo = b->ops[b->nops];
+        if (b->nops == 0) c->ew_first = t;   // as called (a batch of one replays it)
         eo.kind = 2;
         eo.dim = (int16_t)t.dist.dim;
         eo.out_row = -1;
@@ -2886,23 +2898,22 @@ int wsmc_move_block(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, int32_t
     if (n == 0) return WSMC_OK;
     if (c->multi) return move_block_each(c, n, specs, gated, accepted_out);
     CHECK_CTX_KEEP(c);
-    // the fused path: autoRW Moves on disjoint scalar targets (4 in all), one target depth, one
-    // GPU, a lean fold program small enough for the kernel's arguments
+    // the fused path: autoRW Moves on disjoint scalar targets (8 in all), one target depth, one
+    // GPU, a lean fold program
     int32_t depth = specs[0].target_depth < 0 ? c->depth : specs[0].target_depth;
     bool fuse = !is_sharded(c) && n <= 4 && !c->move_gate;
     int32_t D = 0;
-    int32_t utg[4] = {0, 0, 0, 0};
+    int32_t utg[kBlkTargets] = {};
     MoveBlk mb{};
     mb.nm = n;
-    double ulo[4], uhi[4];
     for (int32_t m = 0; m < n && fuse; ++m) {
         const wsmc_move_spec& sp = specs[m];
         const int32_t dm = sp.target_depth < 0 ? c->depth : sp.target_depth;
-        if (sp.proposal != WSMC_PROPOSAL_AUTORW || sp.d < 1 || sp.d > 4 || D + sp.d > 4 || dm != depth) {
+        if (sp.proposal != WSMC_PROPOSAL_AUTORW || sp.d < 1 || sp.d > 4 || D + sp.d > kBlkTargets || dm != depth) {
             fuse = false;
             break;
         }
-        mb.off[m] = D;
+        mb.off[m] = (int8_t)D;
         bool bounded = false;
         for (int k = 0; k < sp.d; ++k) {
             const int32_t t = sp.targets[k];
@@ -2914,20 +2925,19 @@ int wsmc_move_block(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, int32_t
             if (sp.bounded && (std::isfinite(sp.lo[k]) || std::isfinite(sp.hi[k]))) bounded = true;
         }
         for (int k = 0; k < sp.d; ++k) {
-            utg[D + k] = sp.targets[k];
-            ulo[D + k] = bounded ? sp.lo[k] : -INFINITY;
-            uhi[D + k] = bounded ? sp.hi[k] : INFINITY;
-            mb.bnd[D + k] = bounded ? 1 : 0;
+            const int u = D + k;
+            utg[u] = sp.targets[k];
+            mb.lo[u] = bounded ? sp.lo[k] : -INFINITY;
+            mb.hi[u] = bounded ? sp.hi[k] : INFINITY;
+            mb.lgw[u] = (std::isfinite(mb.lo[u]) && std::isfinite(mb.hi[u])) ? wsmc_log(mb.hi[u] - mb.lo[u]) : 0.0;
+            if (bounded) mb.bnd |= 1 << u;
+            mb.tcol[u] = (int16_t)utg[u];
         }
         mb.min_step[m] = sp.step;
         D += sp.d;
     }
     if (!fuse) return move_block_each(c, n, specs, gated, accepted_out);
-    mb.off[n] = D;
-    for (int u = D; u < 4; ++u) {
-        ulo[u] = -INFINITY;
-        uhi[u] = INFINITY;
-    }
+    mb.off[n] = (int8_t)D;
     // the fold program over the union's slots (targets first), compiled before anything runs
     int32_t kD = 0;
     while (kD < (int32_t)c->tape.size() && c->tape[kD].depth < depth) ++kD;
@@ -2969,10 +2979,10 @@ int wsmc_move_block(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, int32_t
     bool lean = (int)slots.size() <= kFoldSlots;
     for (const auto& sg : segs)
         if (sg.kind == kSegTerm && !wsmc_term_is_scalar(&tmpls[sg.tmpl])) lean = false;
+    if (!lean) return move_block_each(c, n, specs, gated, accepted_out);
     const size_t ct_bytes = sizeof(wsmc_term) * tmpls.size();
     const size_t seg_bytes = sizeof(FoldSeg) * segs.size();
     const size_t prog_bytes = ct_bytes + seg_bytes + sizeof(double) * cst.size();
-    if (!lean || prog_bytes > sizeof(ProgInline::w)) return move_block_each(c, n, specs, gated, accepted_out);
 
     // the condition: the newest Resample still pending on the device, else the host flag
     const Decision* gate = nullptr;
@@ -3010,7 +3020,8 @@ int wsmc_move_block(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, int32_t
     if (!async && (r = check_deferred(c))) return r;
     if (!c->move_pending && !c->dflag_zero) WSMC_HIP(hipMemsetAsync(c->dflag, 0, sizeof(int32_t) * 4, c->stream));
     if (accepted_out) WSMC_HIP(hipMemsetAsync(c->ucount, 0, sizeof(unsigned long long) * 4, c->stream));
-    // one moments pass over the union of the targets, one combine into every move's factor
+    // the moments: one pass over the union of the targets (4 at most), else one pass per move;
+    // one combine into every move's factor
     const bool kept = c->cur_max && c->cur_max_seq == c->wseq;
     MaxSlots* mms = kept ? c->cur_max : c->mslots;
     if (!kept) {
@@ -3021,25 +3032,75 @@ int wsmc_move_block(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, int32_t
         WSMC_HIP(hipMemsetAsync(c->mslots, 0, sizeof(MaxSlots), c->stream));
         WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, c->mslots));
     }
-    WSMC_HIP(launch_autorw_moments(c->stream, c->w, mms, c->d_colptr, utg, D, ulo, uhi, nullptr, c->N, c->tilepart,
-                                   c->w_reset_pending, gate, lrow ? lrow->anc : nullptr, lrow ? lrow->dec : nullptr,
-                                   lag_targets));
-    WSMC_HIP(launch_autorw_final_blk(c->stream, c->tilepart, c->ntiles, mb, c->mom, c->dflag, gate));
+    const int sep = D > 4;
+    int32_t toff[4] = {0, 0, 0, 0};
+    const int32_t* lanc = lrow ? lrow->anc : nullptr;
+    const Decision* ldec = lrow ? lrow->dec : nullptr;
+    if (!sep) {
+        WSMC_HIP(launch_autorw_moments(c->stream, c->w, mms, c->d_colptr, utg, D, mb.lo, mb.hi, nullptr, c->N,
+                                       c->tilepart, c->w_reset_pending, gate, lanc, ldec, lag_targets));
+    } else {
+        int32_t at = 0;
+        for (int32_t m = 0; m < n; ++m) {
+            const int o = mb.off[m], dm = mb.off[m + 1] - o;
+            toff[m] = at;
+            WSMC_HIP(launch_autorw_moments(c->stream, c->w, mms, c->d_colptr, utg + o, dm, mb.lo + o, mb.hi + o,
+                                           nullptr, c->N, c->tilepart + (int64_t)at * c->ntiles, c->w_reset_pending,
+                                           gate, lanc, ldec, (lag_targets >> o) & ((1 << dm) - 1)));
+            at += 1 + dm + dm * (dm + 1) / 2;
+        }
+    }
+    WSMC_HIP(launch_autorw_final_blk(c->stream, c->tilepart, c->ntiles, mb, sep, toff, c->mom, c->dflag, gate));
     c->dflag_zero = false;
     if (!c->scache) {
         WSMC_HIP(hipMalloc(&c->scache, sizeof(double) * c->N));
         WSMC_HIP(hipMalloc(&c->scache_back, sizeof(double) * c->N));
     }
-    // the program in the kernel's arguments
-    ProgInline pin;
-    char* hp = reinterpret_cast<char*>(pin.w);
-    pin.seg_off = (int32_t)ct_bytes;
-    pin.cst_off = (int32_t)(ct_bytes + seg_bytes);
-    pin.seg_old0 = seg_old0;
-    pin.pad = 0;
+    // the program: in the kernel's arguments when it fits, else uploaded through the ring
+    ProgInlineBlk pin;
+    const bool inl = prog_bytes <= sizeof(ProgInlineBlk::w);
+    char* hp;
+    if (inl) {
+        hp = reinterpret_cast<char*>(pin.w);
+        pin.seg_off = (int32_t)ct_bytes;
+        pin.cst_off = (int32_t)(ct_bytes + seg_bytes);
+        pin.seg_old0 = seg_old0;
+        pin.pad = 0;
+    } else {
+        if ((int64_t)prog_bytes > c->d_prog_cap) {
+            int64_t cap = c->d_prog_cap ? c->d_prog_cap : 4096;
+            while (cap < (int64_t)prog_bytes) cap *= 2;
+            WSMC_HIP(hipStreamSynchronize(c->stream));
+            if (c->d_prog) WSMC_HIP(hipFree(c->d_prog));
+            WSMC_HIP(hipMalloc(&c->d_prog, cap));
+            c->d_prog_cap = cap;
+        }
+        const int64_t need = ((int64_t)prog_bytes + 255) & ~(int64_t)255;
+        if (c->prog_stage_at + need > c->prog_stage_cap) {
+            WSMC_HIP(hipStreamSynchronize(c->stream));
+            c->prog_stage_at = 0;
+            if (need > c->prog_stage_cap) {
+                if (c->prog_stage) WSMC_HIP(hipHostFree(c->prog_stage));
+                c->prog_stage = nullptr;
+                const int64_t cap = std::max<int64_t>(262144, need);
+                WSMC_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->prog_stage), cap, hipHostMallocDefault));
+                c->prog_stage_cap = cap;
+            }
+        }
+        hp = c->prog_stage + c->prog_stage_at;
+        c->prog_stage_at += need;
+    }
     if (!tmpls.empty()) std::memcpy(hp, tmpls.data(), ct_bytes);
     if (seg_bytes) std::memcpy(hp + ct_bytes, segs.data(), seg_bytes);
     if (!cst.empty()) std::memcpy(hp + ct_bytes + seg_bytes, cst.data(), sizeof(double) * cst.size());
+    if (!inl) WSMC_HIP(hipMemcpyAsync(c->d_prog, hp, prog_bytes, hipMemcpyHostToDevice, c->stream));
+    char* pbase = reinterpret_cast<char*>(c->d_prog);
+    FoldProgram prog;
+    prog.seg_new = inl ? nullptr : reinterpret_cast<const FoldSeg*>(pbase + ct_bytes);
+    prog.seg_old = inl ? nullptr : prog.seg_new + seg_old0;
+    prog.nseg_new = nseg_new;
+    prog.nseg_old = nseg_old;
+    prog.cst = inl ? nullptr : reinterpret_cast<const double*>(pbase + ct_bytes + seg_bytes);
     FoldSlots fs{};
     fs.n = (int32_t)slots.size();
     for (const auto& t : tmpls) fs.heavy |= t.dist.mean_fn == WSMC_MEAN_OSCILLATOR ? 1 : 0;
@@ -3048,8 +3109,6 @@ int wsmc_move_block(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, int32_t
         fs.p[q] = c->cols[slots[q].first].front + (int64_t)slots[q].second * c->N;
     for (int u = 0; u < D; ++u) {
         Column& col = c->cols[utg[u]];
-        fs.t[u] = col.front;
-        mb.tcol[u] = utg[u];
         mb.tout[u] = ((lag_targets >> u) & 1) ? col.back : col.front;
     }
     mb.lag_targets = lag_targets;
@@ -3062,9 +3121,9 @@ int wsmc_move_block(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, int32_t
         mc.dec = c->scache_dec;
         mc.out = c->scache_back;
     }
-    WSMC_HIP(launch_move_blk(c->stream, pin, nseg_new, nseg_old, fs, ulo, uhi, mb, c->mom + 64, c->seed, c->goff, c->N,
-                             accepted_out ? c->ucount : nullptr, c->dflag, mc, cache_from, lrow ? lrow->anc : nullptr,
-                             lrow ? lrow->dec : nullptr, lag_slots, c->d_colptr));
+    WSMC_HIP(launch_move_blk(c->stream, inl ? &pin : nullptr, reinterpret_cast<const wsmc_term*>(pbase), prog, fs, mb,
+                             c->mom + 64, c->seed, c->goff, c->N, accepted_out ? c->ucount : nullptr, c->dflag, mc,
+                             cache_from, lanc, ldec, lag_slots, c->d_colptr));
     if (mc.out != mc.in) std::swap(c->scache, c->scache_back);
     c->scache_anc = nullptr;
     c->scache_dec = nullptr;

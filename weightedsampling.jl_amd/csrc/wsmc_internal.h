@@ -237,6 +237,8 @@ struct wsmc_ctx {
     };
     std::vector<EwRow> ew_rows;
     std::vector<const double*> ew_unstaged; // outputs of the batch without rows (no later LDS reads)
+    wsmc_term ew_first;                     // the batch's first statement as called (a batch of one
+                                            // launches the statement's own kernel)
     char* prog_stage = nullptr;             // pinned staging ring of the programs too large to ride
     int64_t prog_stage_cap = 0, prog_stage_at = 0;   // in the Move's arguments (ProgInline)
     unsigned long long* rs_grp[2] = {nullptr, nullptr};   // generic Resample's group lines (double-buffered)
@@ -383,6 +385,8 @@ struct EwBatch {
     EwOp ops[kEwOps];
 };
 hipError_t launch_ew_batch(hipStream_t s, const EwBatch& b, unsigned feat, uint64_t seed, int64_t goff, int64_t N);
+// a batch of one Assign: k_assign with the batch's resolved pointers
+hipError_t launch_ew_assign1(hipStream_t s, const EwBatch& b, double* const* cols, int64_t N);
 hipError_t launch_sample(hipStream_t s, double* out, int dim, const wsmc_dist& d, uint64_t seed,
                          uint64_t op, int64_t goff, double* const* cols, int64_t N);
 hipError_t launch_sample_importance(hipStream_t s, double* out, int dim, const wsmc_dist& prop,
@@ -494,25 +498,38 @@ struct ProgInline {
     unsigned long long w[kProgInlineWords];
 };
 // a block of autoRW Moves on disjoint targets in one pass (wsmc_move_block): union targets
-// u = 0..D-1 (the fold's slots 0..D-1), move m owns [off[m], off[m+1])
+// u = 0..D-1 (the fold's slots 0..D-1, D <= 8), move m owns [off[m], off[m+1])
+constexpr int kBlkTargets = 8;
 struct MoveBlk {
     int32_t nm;
-    int32_t off[5];
-    int32_t bnd[4];              // per union target: the bounded transform applies
-    int32_t tcol[4];             // column ids (device table entries moved to tout when lagged)
+    int8_t off[5];
+    int8_t pad[3];
+    int32_t bnd;                 // bit u: the bounded transform applies to union target u
     int32_t lag_targets;         // bit u: target u read through the lag row, written in full to tout
-    int32_t pad;
+    int16_t tcol[kBlkTargets];   // column ids (device table entries moved to tout when lagged)
     double min_step[4];          // per move
     unsigned long long op_prop[4], op_acc[4];
-    double* tout[4];             // per union target: where its values go
+    double* tout[kBlkTargets];   // per union target: where its values go
+    double lo[kBlkTargets], hi[kBlkTargets];
+    double lgw[kBlkTargets];     // log(hi - lo) of a bounded interval (host-evaluated)
 };
+// a block's fold program in its kernel's arguments (the block's other arguments are larger
+// than a single Move's, so fewer words than ProgInline)
+constexpr int kProgBlkWords = 360;
+struct ProgInlineBlk {
+    int32_t seg_off, cst_off, seg_old0, pad;
+    unsigned long long w[kProgBlkWords];
+};
+// the moments of a block: one pass over the union of the targets (sep = 0, D <= 4: every
+// move's totals a sub-block of the union's), or one pass per move (its totals at
+// tilepart + toff[m] * ntiles)
 hipError_t launch_autorw_final_blk(hipStream_t s, const double* tilepart, int64_t ntiles, const MoveBlk& mb,
-                                   double* mom, int32_t* flag, const Decision* gate);
-hipError_t launch_move_blk(hipStream_t s, const ProgInline& pin, int32_t nseg_new, int32_t nseg_old, const FoldSlots& fs,
-                           const double* lo, const double* hi, const MoveBlk& mb, const double* Lb, uint64_t seed,
-                           int64_t goff, int64_t N, unsigned long long* accepted, const int32_t* flag,
-                           const MoveCarry& mc, int32_t cache_from, const int32_t* lag_anc, const Decision* lag_dec,
-                           int lag_mask, double** tab);
+                                   int sep, const int32_t* toff, double* mom, int32_t* flag, const Decision* gate);
+hipError_t launch_move_blk(hipStream_t s, const ProgInlineBlk* pin, const wsmc_term* ctape, const FoldProgram& prog,
+                           const FoldSlots& fs, const MoveBlk& mb, const double* Lb, uint64_t seed, int64_t goff,
+                           int64_t N, unsigned long long* accepted, const int32_t* flag, const MoveCarry& mc,
+                           int32_t cache_from, const int32_t* lag_anc, const Decision* lag_dec, int lag_mask,
+                           double** tab);
 hipError_t launch_move_c(hipStream_t s, const wsmc_term* ctape, int32_t nterms, int32_t depth, const FoldSlots& fs,
                          const int32_t* tcols, int d, const double* lo, const double* hi, int bounded,
                          const double* L, uint64_t seed, uint64_t op_prop, uint64_t op_acc, int64_t goff, int64_t N,

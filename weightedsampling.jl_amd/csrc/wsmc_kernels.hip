@@ -2462,21 +2462,59 @@ __global__ __launch_bounds__(kBlock) void k_autorw_final_blk(const double* tilep
     }
     flag[2] = prior ? 0 : nrun;
 }
+// the same with one moments pass per move (a union of more than 4 targets): move m's totals at
+// tilepart + toff[m] * ntiles, each combined exactly as k_autorw_final<d_m> combines them
+struct BlkOff {
+    int32_t t[4];
+};
+__global__ __launch_bounds__(kBlock) void k_autorw_final_sep(const double* tilepart, int64_t ntiles, MoveBlk mb,
+                                                             BlkOff toff, double* mom, int32_t* flag,
+                                                             const Decision* gate) {
+    __shared__ double lds4[4];
+    __shared__ double tot[4][15];
+    if (gate && !gate->resampled) return;
+    for (int m = 0; m < mb.nm; ++m) {
+        const int dm = mb.off[m + 1] - mb.off[m], nv = 1 + dm + dm * (dm + 1) / 2;
+        const double* tp = tilepart + (int64_t)toff.t[m] * ntiles;
+        double acc[15];
+#pragma unroll
+        for (int v = 0; v < 15; ++v) acc[v] = 0.0;
+        for (int64_t b = threadIdx.x; b < ntiles; b += kBlock)
+#pragma unroll
+            for (int v = 0; v < 15; ++v)
+                if (v < nv) acc[v] = acc[v] + tp[(int64_t)v * ntiles + b];
+#pragma unroll
+        for (int v = 0; v < 15; ++v) {
+            if (v >= nv) break;
+            const double s = block_sum_canon(acc[v], lds4);
+            if (threadIdx.x == 0) tot[m][v] = s;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    const int prior = flag[0];
+    int nrun = mb.nm;
+    for (int m = 0; m < mb.nm; ++m) {
+        const int dm = mb.off[m + 1] - mb.off[m];
+        double S[16], L[16];
+        const int ok = wsmc_autorw_factor(tot[m], dm, mb.min_step[m], S, L);
+        for (int k = 0; k < 16; ++k) mom[64 + 16 * m + k] = k < dm * dm ? L[k] : 0.0;
+        if (!ok) {
+            flag[0] = 1;
+            nrun = m;
+            break;
+        }
+    }
+    flag[2] = prior ? 0 : nrun;
+}
 
 template <int K, int LEAN>
-__global__ __launch_bounds__(kBlock) void k_move_blk(ProgInline, FoldSlots fs, MomArgs ma, MoveBlk mb, const double* Lb,
-                                                     uint64_t seed, int64_t goff, int64_t N, u64* accepted,
-                                                     const int32_t* flag, MoveCarry mc, int32_t cache_from,
-                                                     int32_t nseg_new, int32_t nseg_old, MomLag lg, double** tab) {
-    // the program in the kernarg segment (k_move_ci)
-    const char* ka = (const char*)__builtin_amdgcn_kernarg_segment_ptr();
-    const int32_t* hdr = reinterpret_cast<const int32_t*>(ka);
-    const char* pb = ka + offsetof(ProgInline, w);
-    const wsmc_term* ctape = reinterpret_cast<const wsmc_term*>(pb);
-    const FoldSeg* seg_new = reinterpret_cast<const FoldSeg*>(pb + hdr[0]);
-    const FoldSeg* seg_old = seg_new + hdr[2];
-    const double* cst = reinterpret_cast<const double*>(pb + hdr[1]);
-
+__device__ __forceinline__ void move_blk_body(const wsmc_term* ctape, const FoldSeg* seg_new, const FoldSeg* seg_old,
+                                              const double* cst, int32_t nseg_new, int32_t nseg_old,
+                                              const FoldSlots& fs, const MoveBlk& mb, const double* Lb,
+                                              uint64_t seed, int64_t goff, int64_t N, u64* accepted,
+                                              const int32_t* flag, const MoveCarry& mc, int32_t cache_from,
+                                              const MomLag& lg, double** tab) {
     constexpr int W = K * kBlock;
     extern __shared__ double sv[];           // [fs.n][W] current values, then [D][W] proposals
     __shared__ double* sp[kFoldSlots];
@@ -2522,8 +2560,8 @@ __global__ __launch_bounds__(kBlock) void k_move_blk(ProgInline, FoldSlots fs, M
     fold_seg<K, LEAN>(so, ctape, seg_old, nseg_old, cst, sp, ix, ok);
     for (int m = 0; m < nrun; ++m) {
         const int o = mb.off[m], dm = mb.off[m + 1] - o;
-        u64 acc = 0;
         const double* Lm = Lb + 16 * m;
+        u64 acc = 0;
 #pragma unroll
         for (int p = 0; p < K; ++p) {
             sn[p] = 0.0;
@@ -2541,15 +2579,15 @@ __global__ __launch_bounds__(kBlock) void k_move_blk(ProgInline, FoldSlots fs, M
                 const int u = o + k;
                 double dz = 0.0;
 #pragma unroll
-                for (int j = 0; j <= k; ++j) dz = dz + Lm[k * dm + j] * xi[j];
+                for (int jj = 0; jj <= k; ++jj) dz = dz + Lm[k * dm + jj] * xi[jj];
                 const double x = sv[u * W + ix[p]];
-                const bool bd = mb.bnd[u] != 0;
-                const double zo = bd ? wsmc_to_unc(x, ma.lo[u], ma.hi[u]) : x;
+                const bool bd = (mb.bnd >> u) & 1;
+                const double zo = bd ? wsmc_to_unc(x, mb.lo[u], mb.hi[u]) : x;
                 const double zn = zo + dz;
-                const double xn = bd ? wsmc_from_unc(zn, ma.lo[u], ma.hi[u]) : zn;
+                const double xn = bd ? wsmc_from_unc(zn, mb.lo[u], mb.hi[u]) : zn;
                 if (bd)
-                    lpr[p] = lpr[p] + (wsmc_log_abs_jac_pre(zn, ma.lo[u], ma.hi[u], ma.lgw[u]) -
-                                       wsmc_log_abs_jac_pre(zo, ma.lo[u], ma.hi[u], ma.lgw[u]));
+                    lpr[p] = lpr[p] + (wsmc_log_abs_jac_pre(zn, mb.lo[u], mb.hi[u], mb.lgw[u]) -
+                                       wsmc_log_abs_jac_pre(zo, mb.lo[u], mb.hi[u], mb.lgw[u]));
                 prop[u * W + ix[p]] = xn;
             }
         }
@@ -2582,6 +2620,29 @@ __global__ __launch_bounds__(kBlock) void k_move_blk(ProgInline, FoldSlots fs, M
     if (mb.lag_targets && blockIdx.x == 0 && th == 0)   // the device column table follows the moved fronts
         for (int u = 0; u < D; ++u)
             if ((mb.lag_targets >> u) & 1) tab[mb.tcol[u]] = mb.tout[u];
+}
+// the program in the kernel's arguments (ProgInlineBlk first: offset 0 of the kernarg segment)
+template <int K, int LEAN>
+__global__ __launch_bounds__(kBlock) void k_move_blk(ProgInlineBlk, FoldSlots fs, MoveBlk mb, const double* Lb,
+                                                     uint64_t seed, int64_t goff, int64_t N, u64* accepted,
+                                                     const int32_t* flag, MoveCarry mc, int32_t cache_from,
+                                                     int32_t nseg_new, int32_t nseg_old, MomLag lg, double** tab) {
+    const char* ka = (const char*)__builtin_amdgcn_kernarg_segment_ptr();
+    const int32_t* hdr = reinterpret_cast<const int32_t*>(ka);
+    const char* pb = ka + offsetof(ProgInlineBlk, w);
+    const FoldSeg* seg_new = reinterpret_cast<const FoldSeg*>(pb + hdr[0]);
+    move_blk_body<K, LEAN>(reinterpret_cast<const wsmc_term*>(pb), seg_new, seg_new + hdr[2],
+                           reinterpret_cast<const double*>(pb + hdr[1]), nseg_new, nseg_old, fs, mb, Lb, seed, goff,
+                           N, accepted, flag, mc, cache_from, lg, tab);
+}
+// the program uploaded to device memory (too large for the arguments)
+template <int K, int LEAN>
+__global__ __launch_bounds__(kBlock) void k_move_blk_g(const wsmc_term* ctape, FoldProgram prog, FoldSlots fs,
+                                                       MoveBlk mb, const double* Lb, uint64_t seed, int64_t goff,
+                                                       int64_t N, u64* accepted, const int32_t* flag, MoveCarry mc,
+                                                       int32_t cache_from, MomLag lg, double** tab) {
+    move_blk_body<K, LEAN>(ctape, prog.seg_new, prog.seg_old, prog.cst, prog.nseg_new, prog.nseg_old, fs, mb, Lb, seed,
+                           goff, N, accepted, flag, mc, cache_from, lg, tab);
 }
 
 // marginal_diversity keys: isequal semantics (all NaN equal, -0.0 != 0.0)
@@ -2897,6 +2958,24 @@ hipError_t launch_sample(hipStream_t s, double* out, int dim, const wsmc_dist& d
     else
         hipLaunchKernelGGL(k_sample<0u>, grid_for(N), dim3(kBlock), 0, s, out, dim, d, seed, op, goff, cols, N, has_sd,
                            sd);
+    return hipGetLastError();
+}
+hipError_t launch_ew_assign1(hipStream_t s, const EwBatch& b, double* const* cols, int64_t N) {
+    const EwOp& op = b.ops[0];
+    AssignArgs a;
+    for (int k = 0; k < 4; ++k) {
+        a.e[k] = op.a.e[k];
+        for (int m = 0; m < 2; ++m) a.p[k][m] = op.a.p[k][m];
+    }
+    Indirect ind;
+    ind.row = b.anc;
+    ind.dec = b.dec;
+    ind.mask = op.a.lag;
+    if (b.ntab > 0) {
+        ind.tab_col = b.tab_col[0];
+        ind.tab = b.tab;
+    }
+    hipLaunchKernelGGL(k_assign, grid_for(N), dim3(kBlock), 0, s, op.out, (int)op.dim, a, cols, N, ind);
     return hipGetLastError();
 }
 hipError_t launch_ew_batch(hipStream_t s, const EwBatch& b, unsigned feat, uint64_t seed, int64_t goff, int64_t N) {
@@ -3345,7 +3424,13 @@ hipError_t launch_autorw_final(hipStream_t s, const double* tilepart, int64_t nt
     return hipGetLastError();
 }
 hipError_t launch_autorw_final_blk(hipStream_t s, const double* tilepart, int64_t ntiles, const MoveBlk& mb,
-                                   double* mom, int32_t* flag, const Decision* gate) {
+                                   int sep, const int32_t* toff, double* mom, int32_t* flag, const Decision* gate) {
+    if (sep) {
+        BlkOff o{};
+        for (int m = 0; m < mb.nm; ++m) o.t[m] = toff[m];
+        hipLaunchKernelGGL(k_autorw_final_sep, dim3(1), dim3(kBlock), 0, s, tilepart, ntiles, mb, o, mom, flag, gate);
+        return hipGetLastError();
+    }
     switch (mb.off[mb.nm]) {
         case 1: hipLaunchKernelGGL(k_autorw_final_blk<1>, dim3(1), dim3(kBlock), 0, s, tilepart, ntiles, mb, mom, flag, gate); break;
         case 2: hipLaunchKernelGGL(k_autorw_final_blk<2>, dim3(1), dim3(kBlock), 0, s, tilepart, ntiles, mb, mom, flag, gate); break;
@@ -3354,27 +3439,29 @@ hipError_t launch_autorw_final_blk(hipStream_t s, const double* tilepart, int64_
     }
     return hipGetLastError();
 }
-hipError_t launch_move_blk(hipStream_t s, const ProgInline& pin, int32_t nseg_new, int32_t nseg_old, const FoldSlots& fs,
-                           const double* lo, const double* hi, const MoveBlk& mb, const double* Lb, uint64_t seed,
-                           int64_t goff, int64_t N, unsigned long long* accepted, const int32_t* flag,
-                           const MoveCarry& mc, int32_t cache_from, const int32_t* lag_anc, const Decision* lag_dec,
-                           int lag_mask, double** tab) {
-    MomArgs ma{};
-    for (int k = 0; k < 4; ++k) {
-        ma.tcol[k] = mb.tcol[k];
-        ma.lo[k] = lo[k];
-        ma.hi[k] = hi[k];
-        ma.lgw[k] = (wsmc_isfinite(ma.lo[k]) && wsmc_isfinite(ma.hi[k])) ? wsmc_log(ma.hi[k] - ma.lo[k]) : 0.0;
-    }
+hipError_t launch_move_blk(hipStream_t s, const ProgInlineBlk* pin, const wsmc_term* ctape, const FoldProgram& prog,
+                           const FoldSlots& fs, const MoveBlk& mb, const double* Lb, uint64_t seed, int64_t goff,
+                           int64_t N, unsigned long long* accepted, const int32_t* flag, const MoveCarry& mc,
+                           int32_t cache_from, const int32_t* lag_anc, const Decision* lag_dec, int lag_mask,
+                           double** tab) {
     const MomLag lg{lag_mask ? lag_anc : nullptr, lag_dec, lag_mask};
     const size_t row = sizeof(double) * kBlock * (size_t)(fs.n + mb.off[mb.nm]);
-    if (fs.heavy)
-        hipLaunchKernelGGL((k_move_blk<1, 2>), dim3((unsigned)((N + kBlock - 1) / kBlock)), dim3(kBlock), row, s, pin,
-                           fs, ma, mb, Lb, seed, goff, N, accepted, flag, mc, cache_from, nseg_new, nseg_old, lg, tab);
-    else
-        hipLaunchKernelGGL((k_move_blk<2, 1>), dim3((unsigned)((N + 2 * kBlock - 1) / (2 * kBlock))), dim3(kBlock),
-                           2 * row, s, pin, fs, ma, mb, Lb, seed, goff, N, accepted, flag, mc, cache_from, nseg_new,
-                           nseg_old, lg, tab);
+    const dim3 g1((unsigned)((N + kBlock - 1) / kBlock)), g2((unsigned)((N + 2 * kBlock - 1) / (2 * kBlock)));
+    if (pin) {
+        if (fs.heavy)
+            hipLaunchKernelGGL((k_move_blk<1, 2>), g1, dim3(kBlock), row, s, *pin, fs, mb, Lb, seed, goff, N, accepted,
+                               flag, mc, cache_from, prog.nseg_new, prog.nseg_old, lg, tab);
+        else
+            hipLaunchKernelGGL((k_move_blk<2, 1>), g2, dim3(kBlock), 2 * row, s, *pin, fs, mb, Lb, seed, goff, N,
+                               accepted, flag, mc, cache_from, prog.nseg_new, prog.nseg_old, lg, tab);
+    } else {
+        if (fs.heavy)
+            hipLaunchKernelGGL((k_move_blk_g<1, 2>), g1, dim3(kBlock), row, s, ctape, prog, fs, mb, Lb, seed, goff, N,
+                               accepted, flag, mc, cache_from, lg, tab);
+        else
+            hipLaunchKernelGGL((k_move_blk_g<2, 1>), g2, dim3(kBlock), 2 * row, s, ctape, prog, fs, mb, Lb, seed, goff,
+                               N, accepted, flag, mc, cache_from, lg, tab);
+    }
     return hipGetLastError();
 }
 hipError_t launch_autorw_publish(hipStream_t s, const MaxSlots* ms, double* const* cols, const int32_t* tcols, int d,
