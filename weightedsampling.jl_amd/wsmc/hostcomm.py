@@ -144,35 +144,52 @@ class HostComm:
             got = {}
             while len(got) < self.world - 1:
                 conn, _ = srv.accept()
-                conn.settimeout(_HANDSHAKE_S)        # a peer that connects and sends nothing
+                # the server speaks first (a client that gave up while the connection waited in
+                # the backlog sent nothing and is skipped here), then the client's hello, then
+                # the acknowledgement; a rank that reconnects replaces its earlier connection
+                conn.settimeout(_HANDSHAKE_S)
                 try:
+                    conn.sendall(_MAGIC)
                     magic, tag, r = _HELLO.unpack(_recv_exact(conn, _HELLO.size))
                 except (OSError, ConnectionError, struct.error):
                     conn.close()
                     continue
-                if magic != _MAGIC or tag.rstrip(b"\0") != self.tag or not 0 < r < self.world or r in got:
+                if magic != _MAGIC or tag.rstrip(b"\0") != self.tag or not 0 < r < self.world:
                     conn.close()
                     continue
+                try:
+                    conn.sendall(_MAGIC)
+                except (OSError, ConnectionError):
+                    conn.close()
+                    continue
+                if r in got:
+                    got[r].close()
                 got[r] = conn
                 conn.settimeout(timeout)
-                conn.sendall(_MAGIC)
             srv.close()
             self.peers = [got[r] for r in range(1, self.world)]
         else:
             while True:
                 for k in range(16):
+                    s = None
                     try:
                         s = socket.create_connection((addr, port + 1 + k), timeout=2.0)
                         # another process's listener on a scanned port (e.g. an RCCL bootstrap
-                        # socket) answers nothing: give up on it quickly and go on scanning
+                        # socket) does not greet: give up on it quickly and go on scanning
                         s.settimeout(_HANDSHAKE_S)
+                        if _recv_exact(s, len(_MAGIC)) != _MAGIC:
+                            s.close()
+                            continue
                         s.sendall(_HELLO.pack(_MAGIC, self.tag, self.rank))
+                        s.settimeout(max(1.0, deadline - time.time()))
                         if _recv_exact(s, len(_MAGIC)) == _MAGIC:
                             s.settimeout(timeout)
                             self.sock = s
                             break
                         s.close()
                     except (OSError, ConnectionError):
+                        if s is not None:
+                            s.close()
                         continue
                 if self.sock is not None:
                     break
