@@ -23,7 +23,7 @@ for k, r in d.items():
     per_kernel[k.split("(")[0]] = b * r["dispatches"] / runs / (N * T)
 out = {"n_particles": N, "T": T, "bytes_per_particle_step": sum(per_kernel.values()),
        "per_kernel": per_kernel, "source": sys.argv[1],
-       "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes (tools/gpu_round.sh); "
+       "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes (tools/gpu.sh round); "
                  "FETCH_SIZE x 2 (gfx950 wide-read correction), per dispatch x dispatches per run / (N T)"}
 json.dump(out, open(sys.argv[4], "w"), indent=1)
 print(json.dumps(out))
