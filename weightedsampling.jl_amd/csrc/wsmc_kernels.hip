@@ -279,7 +279,7 @@ template <unsigned FEAT>
 __global__ __launch_bounds__(kBlock) void k_ew_batch(EwBatch, uint64_t seed, int64_t goff, int64_t N) {
     const EwBatch* B = (const EwBatch*)(const char*)__builtin_amdgcn_kernarg_segment_ptr();
     __shared__ u64 lds[4];
-    __shared__ double rows[kEwRows * kBlock];
+    extern __shared__ double rows[];   // [B->nrows][kBlock], sized by the launch
     __shared__ double* ctab[kEwSlots];
     const int th = threadIdx.x;
     const int64_t i = (int64_t)blockIdx.x * kBlock + th;
@@ -290,8 +290,15 @@ __global__ __launch_bounds__(kBlock) void k_ew_batch(EwBatch, uint64_t seed, int
     // every load that depends on no statement, up front: the preloaded rows, the ancestor, the
     // weight
     const int64_t j = (in && B->anc && (!B->dec || B->dec->resampled)) ? (int64_t)B->anc[i] : i;
-    for (int p = 0; p < B->npre; ++p)
-        rows[(int)B->pre_row[p] * kBlock + th] = in ? B->pre_src[p][B->pre_lag[p] ? j : i] : 0.0;
+    // unrolled over the capacity: the loads issue back to back (a rolled loop stored each
+    // value to LDS before issuing the next load, one memory latency per column)
+    const int npre = B->npre;
+    double pv[kEwPre];
+#pragma unroll
+    for (int p = 0; p < kEwPre; ++p) pv[p] = (p < npre && in) ? B->pre_src[p][B->pre_lag[p] ? j : i] : 0.0;
+#pragma unroll
+    for (int p = 0; p < kEwPre; ++p)
+        if (p < npre) rows[(int)B->pre_row[p] * kBlock + th] = pv[p];
     double wv = 0.0;
     if (in && B->has_w) wv = (B->wreset && B->wreset->resampled) ? B->wreset->mean : B->w[i];
     __syncthreads();
@@ -319,9 +326,12 @@ __global__ __launch_bounds__(kBlock) void k_ew_batch(EwBatch, uint64_t seed, int
                     x[q] = v;
                 }
             } else if (op.kind == 1) {
-                const double sdl = op.s.sd;
-                wsmc_dist_sample_mf(&op.s.d, x, seed, op.s.op, (uint64_t)(goff + i), cols, kBlock, th,
-                                    op.s.has_sd ? &sdl : nullptr, FEAT);
+                const double sdl = op.s.sd;   // (a pointer chosen by a select would live in scratch)
+                if (op.s.has_sd)
+                    wsmc_dist_sample_mf(&op.s.d, x, seed, op.s.op, (uint64_t)(goff + i), cols, kBlock, th, &sdl, FEAT);
+                else
+                    wsmc_dist_sample_mf(&op.s.d, x, seed, op.s.op, (uint64_t)(goff + i), cols, kBlock, th, nullptr,
+                                        FEAT);
             } else {
                 wsmc_logmemo lm = op.w.lm0;
                 wv = wv + wsmc_term_logpdf_mf(&op.w.t, cols, kBlock, th, nullptr, &lm, FEAT);
@@ -2282,6 +2292,31 @@ __device__ __forceinline__ void fold_seg(double (&s)[K], const wsmc_term* tape, 
 // The same Move over a compiled tape (slots; targets are slots 0..d-1), K particles per
 // thread: slot values staged once in LDS ([slot][K * kBlock]), proposals in their own LDS
 // rows so the s_new fold reads them through its own pointer table (no override lookups).
+// a Move's slot values into LDS: loaded in chunks of 8 / K slots, every load of a chunk issued
+// before its LDS stores (a rolled slot loop waited out one memory latency per slot: the stores
+// may alias the generic slot pointers, so the compiler cannot hoist the next load)
+template <int K>
+__device__ __forceinline__ void stage_slots(double* sv, int W, const FoldSlots& fs, const int (&ix)[K],
+                                            const int64_t (&gi)[K], const int64_t (&ai)[K], const bool (&ok)[K],
+                                            int smask) {
+    constexpr int C = 8 / K;
+    for (int s0 = 0; s0 < fs.n; s0 += C) {
+        double v[C][K];
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int p = 0; p < K; ++p) {
+                const int sl = s0 + c;
+                v[c][p] = (sl < fs.n && ok[p]) ? fs.p[sl][(smask >> sl) & 1 ? ai[p] : gi[p]] : 0.0;
+            }
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int p = 0; p < K; ++p)
+                if (s0 + c < fs.n) sv[(s0 + c) * W + ix[p]] = v[c][p];
+    }
+}
+
 template <int K, int LEAN>
 __device__ __forceinline__ void move_c_body(const wsmc_term* ctape, const FoldSlots& fs, const MomArgs& ma, int d,
                                             int bounded, const double* Lm, uint64_t seed, uint64_t op_prop,
@@ -2310,9 +2345,7 @@ __device__ __forceinline__ void move_c_body(const wsmc_term* ctape, const FoldSl
         gi[p] = base + ix[p];
         ok[p] = gi[p] < N;
     }
-    for (int sl = 0; sl < fs.n; ++sl)
-#pragma unroll
-        for (int p = 0; p < K; ++p) sv[sl * W + ix[p]] = ok[p] ? fs.p[sl][gi[p]] : 0.0;
+    stage_slots<K>(sv, W, fs, ix, gi, gi, ok, 0);
     double so[K], sn[K], lpr[K];
     const bool lag = mc.anc && mc.dec->resampled;
     const bool run = !mc.gate || mc.gate->resampled;   // a gated Move that does not run only carries
@@ -2543,10 +2576,7 @@ __device__ __forceinline__ void move_blk_body(const wsmc_term* ctape, const Fold
         ok[p] = gi[p] < N;
         ai[p] = (ok[p] && (smask || slag)) ? (int64_t)arow[gi[p]] : gi[p];
     }
-    for (int sl = 0; sl < fs.n; ++sl)
-#pragma unroll
-        for (int p = 0; p < K; ++p)
-            sv[sl * W + ix[p]] = ok[p] ? fs.p[sl][(smask >> sl) & 1 ? ai[p] : gi[p]] : 0.0;
+    stage_slots<K>(sv, W, fs, ix, gi, ai, ok, smask);
     double so[K], sn[K], lpr[K];
     int chg[K];
 #pragma unroll
@@ -2980,10 +3010,11 @@ hipError_t launch_ew_assign1(hipStream_t s, const EwBatch& b, double* const* col
 }
 hipError_t launch_ew_batch(hipStream_t s, const EwBatch& b, unsigned feat, uint64_t seed, int64_t goff, int64_t N) {
     static_assert(sizeof(EwBatch) + 32 <= 4096, "the batch rides in the kernel arguments");
+    const size_t rows = sizeof(double) * kBlock * (size_t)b.nrows;   // only the rows used: occupancy
     if (feat)
-        hipLaunchKernelGGL(k_ew_batch<WSMC_FEAT_ALL>, grid_for(N), dim3(kBlock), 0, s, b, seed, goff, N);
+        hipLaunchKernelGGL(k_ew_batch<WSMC_FEAT_ALL>, grid_for(N), dim3(kBlock), rows, s, b, seed, goff, N);
     else
-        hipLaunchKernelGGL(k_ew_batch<0u>, grid_for(N), dim3(kBlock), 0, s, b, seed, goff, N);
+        hipLaunchKernelGGL(k_ew_batch<0u>, grid_for(N), dim3(kBlock), rows, s, b, seed, goff, N);
     return hipGetLastError();
 }
 hipError_t launch_sample_importance(hipStream_t s, double* out, int dim, const wsmc_dist& prop,
