@@ -49,8 +49,10 @@ def log(*a):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    # 300 runs of T = 100 steps: about 1.3 s of timed GPU work at 1M (long enough for a sampler
+    # outside the process to see the GPU busy, and a steadier per-run figure), still seconds
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--particles", type=int, default=1_000_000, help="particles per GPU (weak scaling)")
     ap.add_argument("--global-particles", type=int, default=0,
                     help="total particles split over the ranks (strong scaling, C4's 8M on 1/2/4/8 GPUs)")
