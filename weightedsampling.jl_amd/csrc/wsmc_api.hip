@@ -3322,22 +3322,28 @@ static int exchange_neighbors(wsmc_ctx* c, unsigned long long* const send[2], un
     const int W = c->world, me = c->rank;
     if (W < 2 || words <= 0) return WSMC_OK;
     if (c->host_exchange) {
-        if (2 * words > 0x7fffffffll) return fail(WSMC_EARG, "host exchange block too large");
-        std::vector<unsigned long long> mine(2 * (size_t)words), all(2 * (size_t)words * W);
-        WSMC_HIP(hipMemcpyAsync(mine.data(), send[0], sizeof(unsigned long long) * words, hipMemcpyDeviceToHost, s));
-        WSMC_HIP(hipMemcpyAsync(mine.data() + words, send[1], sizeof(unsigned long long) * words,
-                                hipMemcpyDeviceToHost, s));
-        WSMC_HIP(hipStreamSynchronize(s));
-        if (c->host_exchange(c->host_user, reinterpret_cast<const uint64_t*>(mine.data()), (int32_t)(2 * words),
-                             reinterpret_cast<uint64_t*>(all.data())) != 0)
-            return fail(WSMC_ERCCL, "host neighbour exchange failed");
-        if (me > 0)   // the left rank's right block
-            WSMC_HIP(hipMemcpyAsync(recv[0], all.data() + (size_t)(me - 1) * 2 * words + words,
-                                    sizeof(unsigned long long) * words, hipMemcpyHostToDevice, s));
-        if (me + 1 < W)   // the right rank's left block
-            WSMC_HIP(hipMemcpyAsync(recv[1], all.data() + (size_t)(me + 1) * 2 * words,
-                                    sizeof(unsigned long long) * words, hipMemcpyHostToDevice, s));
-        WSMC_HIP(hipStreamSynchronize(s));
+        // in pieces of at most 2^22 words a block (the callback counts words in an int32, a
+        // gathered message stays far below the host transport's 1 GB limit at 8 ranks, and
+        // every rank cuts the same pieces: words is the same on all of them)
+        const int64_t piece = (int64_t)1 << 22;
+        for (int64_t at = 0; at < words; at += piece) {
+            const int64_t n = std::min(piece, words - at);
+            std::vector<unsigned long long> mine(2 * (size_t)n), all(2 * (size_t)n * W);
+            WSMC_HIP(hipMemcpyAsync(mine.data(), send[0] + at, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost, s));
+            WSMC_HIP(hipMemcpyAsync(mine.data() + n, send[1] + at, sizeof(unsigned long long) * n,
+                                    hipMemcpyDeviceToHost, s));
+            WSMC_HIP(hipStreamSynchronize(s));
+            if (c->host_exchange(c->host_user, reinterpret_cast<const uint64_t*>(mine.data()), (int32_t)(2 * n),
+                                 reinterpret_cast<uint64_t*>(all.data())) != 0)
+                return fail(WSMC_ERCCL, "host neighbour exchange failed");
+            if (me > 0)   // the left rank's right block
+                WSMC_HIP(hipMemcpyAsync(recv[0] + at, all.data() + (size_t)(me - 1) * 2 * n + n,
+                                        sizeof(unsigned long long) * n, hipMemcpyHostToDevice, s));
+            if (me + 1 < W)   // the right rank's left block
+                WSMC_HIP(hipMemcpyAsync(recv[1] + at, all.data() + (size_t)(me + 1) * 2 * n,
+                                        sizeof(unsigned long long) * n, hipMemcpyHostToDevice, s));
+            WSMC_HIP(hipStreamSynchronize(s));
+        }
         return WSMC_OK;
     }
     WSMC_RCCL(ncclGroupStart());
@@ -3779,7 +3785,7 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
     mix(c->comm);   // a captured collective bakes its communicator
     // exact shards: the run without host round trips unless it is switched off (A/B) or the
     // scheme needs the eager path; its block / window sizes are part of the graph
-    const bool exact_async = exact_mode(c) && !exact_eager_forced();
+    const bool exact_async = exact_mode(c) && !exact_eager_forced() && !c->x_eager;
     int64_t xcap = 0, xctr = 0;
     if (exact_async) {
         exact_sizes(c, &xcap, &xctr);
@@ -3911,8 +3917,14 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         c->x_exc = exc;
         c->x_overflows += bits ? 1 : 0;
         if (bits) {
-            if (bits & 1ull) c->x_cap = std::max<int64_t>(4 * xcap, 2 * (int64_t)need);
-            if (bits & 2ull) c->x_ctr = std::max<int64_t>(4 * xctr, 2 * (int64_t)exc);
+            // grown for the next runs, never past a shard (a block or a level's window cannot
+            // need more than a neighbour's particles)
+            const int64_t nmax = (c->gN + c->world - 1) / c->world;
+            if (bits & 1ull) c->x_cap = std::min<int64_t>(nmax, std::max<int64_t>(4 * xcap, 2 * (int64_t)need));
+            if (bits & 2ull) c->x_ctr = std::min<int64_t>(nmax, std::max<int64_t>(4 * xctr, 2 * (int64_t)exc));
+            // margins of half a shard or more would ship most of a neighbour's history every run
+            // (T x ctr x 24 B a side): the eager path's requests cost less from then on
+            if (2 * std::max(c->x_cap, c->x_ctr) >= nmax) c->x_eager = true;
             WSMC_HIP(hipMemcpyAsync(c->w, c->w_save, sizeof(double) * c->N, hipMemcpyDeviceToDevice, c->stream));
             rows_x = false;
             if ((r = ssm2d_run_exact(c, p, op_base))) {
@@ -4022,6 +4034,7 @@ int wsmc_debug_exact(wsmc_ctx* c, int64_t cap, int64_t ctr, int64_t* stats_out) 
     if (!c) return fail(WSMC_EARG, "null context");
     if (cap >= 0) c->x_cap = cap;
     if (ctr >= 0) c->x_ctr = ctr;
+    if (cap >= 0 || ctr >= 0) c->x_eager = false;   // margins set by hand: the async run again
     if (stats_out) {
         int64_t cp = 0, ct = 0;
         if (c->world > 0 && c->gN > 0) exact_sizes(c, &cp, &ct);

@@ -8,6 +8,7 @@ through the identical protocol to compare results bit for bit.
 from __future__ import annotations
 
 import ctypes as C
+import sys
 import math
 
 import numpy as np
@@ -110,11 +111,13 @@ class Context:
                 nb = 8 * int(words)
                 recs = allgather(C.string_at(mine, nb))        # raw u64 words of this rank
                 for r, rec in enumerate(recs):
-                    if len(rec) != nb:
+                    if len(rec) != nb:   # the ranks are at different exchanges: a desync
+                        sys.stderr.write(f"wsmc host exchange: rank {rank} sent {nb} B, rank {r} {len(rec)} B\n")
                         return 1
                     C.memmove(C.addressof(out.contents) + r * nb, rec, nb)
                 return 0
-            except Exception:
+            except Exception as e:   # the reason goes to stderr; the ABI call fails with ERCCL
+                sys.stderr.write(f"wsmc host exchange: rank {rank}: {type(e).__name__}: {e}\n")
                 return 1
         self._exchange_cb = abi.EXCHANGE_FN(_exchange)   # keep alive as long as the context
         check(self._L.wsmc_comm_init_host(self._h, C.cast(self._exchange_cb, C.c_void_p), None, int(world),
