@@ -67,7 +67,10 @@ typedef enum {
     WSMC_FAM_NORMAL = 0,        /* Normal(mu, sigma), sigma a std               */
     WSMC_FAM_HALFNORMAL = 1,    /* Truncated(Normal(0, sigma), 0, Inf)          */
     WSMC_FAM_UNIFORM = 2,       /* Uniform(a, b) = param[0], param[1]           */
-    WSMC_FAM_MVNORMAL_ISO = 3   /* MvNormal(mu, var*I), dim <= 4                */
+    WSMC_FAM_MVNORMAL_ISO = 3,  /* MvNormal(mu, var*I), dim <= 4                */
+    WSMC_FAM_MVNORMAL = 4       /* MvNormal(mu, Sigma), constant covariance Sigma, dim <= 3:
+                                   build it with wsmc_dist_mvnormal_cov (the factor is
+                                   packed into the dist, see wsmc_terms.h)       */
 } wsmc_family;
 
 typedef enum {
@@ -85,6 +88,14 @@ typedef struct {
     wsmc_operand scale;         /* sigma (NORMAL, HALFNORMAL) or variance (MVNORMAL_ISO) */
     double param[2];
 } wsmc_dist;
+
+/* MvNormal(mu, Sigma) with a constant covariance Sigma (src/default_kernels.jl:93; the
+ * reference builds Distributions' MvNormal, whose PDMat factors Sigma once). On entry d->dim
+ * (1..3) and d->mu[0..dim-1] are set; Sigma is dim x dim row-major. Sets family
+ * WSMC_FAM_MVNORMAL and packs the Cholesky factor and log det Sigma into d. Host only (no
+ * device call). WSMC_EARG: bad dim or Sigma not exactly symmetric (LinearAlgebra.cholesky's
+ * ishermitian check); WSMC_ENOTPD: Sigma not positive definite (PosDefException). */
+int wsmc_dist_mvnormal_cov(wsmc_dist* d, const double* cov);
 
 typedef enum { WSMC_TERM_SAMPLE = 0, WSMC_TERM_OBSERVE = 1, WSMC_TERM_WEIGHT = 2 } wsmc_term_kind;
 

@@ -40,11 +40,13 @@ WSMC_HD double wsmc_operand_eval(const wsmc_operand* o, double* const* cols, int
     return v;
 }
 
-/* feat: the mean functions a caller may meet (WSMC_FEAT_OSC: the oscillator). A device kernel
- * launched for affine means only passes 0, so the oscillator code is not compiled into it
- * (registers); every other caller passes WSMC_FEAT_ALL. The arithmetic is the same. */
+/* feat: the mean functions and families a caller may meet (WSMC_FEAT_OSC: the oscillator,
+ * WSMC_FEAT_MVN: the full-covariance MvNormal). A device kernel launched without them passes
+ * 0 (or OSC alone), so their code is not compiled into it (registers); every other caller
+ * passes WSMC_FEAT_ALL. The arithmetic is the same. */
 #define WSMC_FEAT_OSC 1u
-#define WSMC_FEAT_ALL 1u
+#define WSMC_FEAT_MVN 2u   /* the full-covariance MvNormal family */
+#define WSMC_FEAT_ALL 3u
 WSMC_HD double wsmc_dist_mean_f(const wsmc_dist* d, int k, double* const* cols, int64_t N, int64_t i,
                                 const wsmc_override* ov, unsigned feat) {
     if ((feat & WSMC_FEAT_OSC) && d->mean_fn == WSMC_MEAN_OSCILLATOR) {
@@ -95,6 +97,111 @@ WSMC_HD double wsmc_log_memo(wsmc_logmemo* m, double x) {
     return lg;
 }
 
+/* WSMC_FAM_MVNORMAL (constant covariance, dim <= 3). Sigma = L L' with L lower triangular;
+ * the packed numbers are L row by row (dim (dim + 1) / 2 values), then log det Sigma. They sit
+ * in the double fields (c0, coef[0], coef[1]) of the unused mean operands mu[dim..3], then of
+ * scale, then in param[0..1]: every operand stays a constant (col = -1), so the code that
+ * scans operands for the columns a statement reads (lazy gathers, statement batches, remaps)
+ * never sees them. Capacity 3 (4 - dim) + 5 doubles: 8 at dim 3 (7 needed). */
+#define WSMC_MVN_MAXDIM 3
+/* packed number j of a dist of dimension n; called with constant n and j (the per-dimension
+ * instances below unroll), so every access is a fixed field of the argument struct */
+WSMC_HD double wsmc_mvn_get(const wsmc_dist* d, int n, int j) {
+    const int nfree = 4 - n;
+    const int q = j / 3, r = j - 3 * q;
+    if (q > nfree) return d->param[j - 3 * (nfree + 1)];
+    const wsmc_operand* o = q < nfree ? &d->mu[n + q] : &d->scale;
+    return r == 0 ? o->c0 : o->coef[r - 1];
+}
+WSMC_HD void wsmc_mvn_set(wsmc_dist* d, int j, double v) {
+    const int nfree = 4 - d->dim;
+    const int q = j / 3, r = j - 3 * q;
+    if (q > nfree) {
+        d->param[j - 3 * (nfree + 1)] = v;
+        return;
+    }
+    wsmc_operand* o = q < nfree ? &d->mu[d->dim + q] : &d->scale;
+    if (r == 0) o->c0 = v; else o->coef[r - 1] = v;
+}
+/* wsmc_dist_mvnormal_cov's packing (host): 0, -1 bad dim / not exactly symmetric, -2 not
+ * positive definite. Cholesky–Banachiewicz, each entry's dot product summed left to right;
+ * log det = 2 (log L00 + log L11 + ...). */
+WSMC_HD int wsmc_mvn_pack(wsmc_dist* d, const double* S) {
+    const int n = d->dim;
+    if (n < 1 || n > WSMC_MVN_MAXDIM) return -1;
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < i; ++j)
+            if (!(S[i * n + j] == S[j * n + i])) return -1;
+    double L[WSMC_MVN_MAXDIM][WSMC_MVN_MAXDIM] = {{0.0}};
+    double hl = 0.0;
+    for (int i = 0; i < n; ++i) {
+        for (int j = 0; j <= i; ++j) {
+            double s = S[i * n + j];
+            for (int k = 0; k < j; ++k) s = s - L[i][k] * L[j][k];
+            if (i == j) {
+                if (!(s > 0.0) || !wsmc_isfinite(s)) return -2;
+                L[i][i] = wsmc_sqrt(s);
+                hl = hl + wsmc_log(L[i][i]);
+            } else {
+                L[i][j] = s / L[j][j];
+            }
+        }
+    }
+    d->family = WSMC_FAM_MVNORMAL;
+    for (int k = n; k < 4; ++k) {
+        d->mu[k].c0 = 0.0;
+        d->mu[k].col[0] = d->mu[k].col[1] = -1;
+        d->mu[k].comp[0] = d->mu[k].comp[1] = 0;
+        d->mu[k].coef[0] = d->mu[k].coef[1] = 0.0;
+    }
+    d->scale.c0 = 0.0;
+    d->scale.col[0] = d->scale.col[1] = -1;
+    d->scale.comp[0] = d->scale.comp[1] = 0;
+    d->scale.coef[0] = d->scale.coef[1] = 0.0;
+    d->param[0] = d->param[1] = 0.0;
+    int p = 0;
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j <= i; ++j) wsmc_mvn_set(d, p++, L[i][j]);
+    wsmc_mvn_set(d, p, 2.0 * hl);
+    return 0;
+}
+
+/* WSMC_FAM_MVNORMAL of dimension n (a constant at every call):
+ * -(n log2pi + log det Sigma + |L^-1 (x - mu)|^2)/2, L^-1 r by forward substitution */
+WSMC_HD double wsmc_mvn_logpdf_n(const wsmc_dist* d, const int n, const double* x, double* const* cols,
+                                 int64_t N, int64_t i, const wsmc_override* ov, unsigned feat) {
+    double y[WSMC_MVN_MAXDIM] = {0.0, 0.0, 0.0};
+    double s = 0.0;
+    int p = 0;
+    WSMC_UNROLL
+    for (int k = 0; k < n; ++k) {   /* row k of L at p */
+        double r = x[k] - wsmc_dist_mean_f(d, k, cols, N, i, ov, feat);
+        WSMC_UNROLL
+        for (int m = 0; m < k; ++m) r = r - wsmc_mvn_get(d, n, p + m) * y[m];
+        y[k] = r / wsmc_mvn_get(d, n, p + k);
+        s = s + y[k] * y[k];
+        p += k + 1;
+    }
+    return -(((double)n * WSMC_LOG2PI + wsmc_mvn_get(d, n, p)) + s) * 0.5;
+}
+/* mu + L z, z drawn in pairs as for the isotropic family */
+WSMC_HD void wsmc_mvn_sample_n(const wsmc_dist* d, const int n, double* x, uint64_t seed, uint64_t op,
+                               uint64_t idx, double* const* cols, int64_t N, int64_t i, unsigned feat) {
+    double z[4] = {0.0, 0.0, 0.0, 0.0};
+    WSMC_UNROLL
+    for (int k = 0; k < n; k += 2)
+        wsmc_normal_pair(wsmc_rng_block(seed, op, idx, (uint32_t)(k >> 1)), &z[k], &z[k + 1]);
+    int p = 0;
+    WSMC_UNROLL
+    for (int k = 0; k < n; ++k) {
+        double acc = 0.0;
+        WSMC_UNROLL
+        for (int m = 0; m <= k; ++m) acc = acc + wsmc_mvn_get(d, n, p + m) * z[m];
+        x[k] = wsmc_dist_mean_f(d, k, cols, N, i, 0, feat) + acc;
+        p += k + 1;
+    }
+}
+
 /* logpdf(D(args...), x) for the supported families */
 WSMC_HD double wsmc_dist_logpdf_mf(const wsmc_dist* d, const double* x, double* const* cols, int64_t N,
                                    int64_t i, const wsmc_override* ov, wsmc_logmemo* lm, unsigned feat) {
@@ -117,6 +224,11 @@ WSMC_HD double wsmc_dist_logpdf_mf(const wsmc_dist* d, const double* x, double* 
         }
         case WSMC_FAM_UNIFORM:
             return wsmc_uniform_logpdf(d->param[0], d->param[1], x[0]);
+        case WSMC_FAM_MVNORMAL:
+            if (!(feat & WSMC_FEAT_MVN)) return __builtin_nan("");   /* never launched so */
+            if (d->dim == 2) return wsmc_mvn_logpdf_n(d, 2, x, cols, N, i, ov, feat);
+            if (d->dim == 3) return wsmc_mvn_logpdf_n(d, 3, x, cols, N, i, ov, feat);
+            return wsmc_mvn_logpdf_n(d, 1, x, cols, N, i, ov, feat);
         default: { /* WSMC_FAM_MVNORMAL_ISO: -(d log2pi + d log var + |x-mu|^2/var)/2 */
             double var = wsmc_operand_eval(&d->scale, cols, N, i, ov);
             double s = 0.0;
@@ -160,6 +272,12 @@ WSMC_HD void wsmc_dist_sample_mf(const wsmc_dist* d, double* x, uint64_t seed, u
             x[0] = a + (b - a) * wsmc_uniform_k(seed, op, idx, 0);
             break;
         }
+        case WSMC_FAM_MVNORMAL:
+            if (!(feat & WSMC_FEAT_MVN)) break;   /* never launched so */
+            if (d->dim == 2) wsmc_mvn_sample_n(d, 2, x, seed, op, idx, cols, N, i, feat);
+            else if (d->dim == 3) wsmc_mvn_sample_n(d, 3, x, seed, op, idx, cols, N, i, feat);
+            else wsmc_mvn_sample_n(d, 1, x, seed, op, idx, cols, N, i, feat);
+            break;
         default: {
             double sd = sd_pre ? *sd_pre : wsmc_sqrt(wsmc_operand_eval(&d->scale, cols, N, i, 0));
             for (int k = 0; k < d->dim && k < 4; k += 2) {

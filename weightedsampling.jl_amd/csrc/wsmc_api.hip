@@ -229,9 +229,11 @@ static int check_operand(const wsmc_ctx* c, const wsmc_operand& o) {
 }
 
 static int check_dist(const wsmc_ctx* c, const wsmc_dist& d) {
-    if (d.family < WSMC_FAM_NORMAL || d.family > WSMC_FAM_MVNORMAL_ISO) return fail(WSMC_EARG, "unknown family");
+    if (d.family < WSMC_FAM_NORMAL || d.family > WSMC_FAM_MVNORMAL) return fail(WSMC_EARG, "unknown family");
     if (d.dim < 1 || d.dim > 4) return fail(WSMC_EARG, "dist dim must be 1..4");
-    if (d.family != WSMC_FAM_MVNORMAL_ISO && d.dim != 1) return fail(WSMC_EARG, "scalar family with dim != 1");
+    if (d.family == WSMC_FAM_MVNORMAL && d.dim > WSMC_MVN_MAXDIM)
+        return fail(WSMC_EARG, "MvNormal with a full covariance: dim must be 1..3");
+    if (d.family < WSMC_FAM_MVNORMAL_ISO && d.dim != 1) return fail(WSMC_EARG, "scalar family with dim != 1");
     if (d.mean_fn == WSMC_MEAN_OSCILLATOR && (d.family != WSMC_FAM_NORMAL))
         return fail(WSMC_EARG, "oscillator mean only for Normal");
     int r;
@@ -518,6 +520,18 @@ const char* wsmc_last_error(void) { return g_err.c_str(); }
 int wsmc_version(int32_t* major, int32_t* minor) {
     if (major) *major = 0;
     if (minor) *minor = 1;
+    return WSMC_OK;
+}
+
+// MvNormal(mu, Sigma) with a constant Sigma (src/default_kernels.jl:93): the factor is packed
+// into the dist once, on the host (wsmc_terms.h wsmc_mvn_pack)
+int wsmc_dist_mvnormal_cov(wsmc_dist* d, const double* cov) {
+    if (!d || !cov) return fail(WSMC_EARG, "null argument");
+    if (d->dim < 1 || d->dim > WSMC_MVN_MAXDIM) return fail(WSMC_EARG, "MvNormal with a full covariance: dim must be 1..3");
+    if (d->mean_fn != WSMC_MEAN_AFFINE) return fail(WSMC_EARG, "MvNormal mean must be affine");
+    const int r = wsmc_mvn_pack(d, cov);
+    if (r == -1) return fail(WSMC_EARG, "covariance is not symmetric");
+    if (r == -2) return fail(WSMC_ENOTPD, "covariance is not positive definite");
     return WSMC_OK;
 }
 
@@ -2046,7 +2060,8 @@ int wsmc_sample(wsmc_ctx* c, int32_t out, const wsmc_dist* d) {
         eo.s.op = op;
         eo.s.has_sd = d->family == WSMC_FAM_MVNORMAL_ISO && wsmc_operand_is_const(&d->scale);
         eo.s.sd = eo.s.has_sd ? wsmc_sqrt(wsmc_operand_eval(&d->scale, nullptr, c->N, 0, nullptr)) : 0.0;
-        if (d->mean_fn == WSMC_MEAN_OSCILLATOR) c->ew_feat = 1;
+        if (d->mean_fn == WSMC_MEAN_OSCILLATOR) c->ew_feat |= WSMC_FEAT_OSC;
+        if (d->family == WSMC_FAM_MVNORMAL) c->ew_feat |= WSMC_FEAT_MVN;
         b->nops += 1;
     }
     scores_touch(c, out);
@@ -2140,7 +2155,8 @@ static int weigh(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x, int kin
             const double sc = wsmc_operand_eval(&t.dist.scale, nullptr, c->N, 0, nullptr);
             eo.w.lm0 = wsmc_logmemo{wsmc_d2bits(sc), wsmc_log(sc), 1.0 / sc, 1};
         }
-        if (t.dist.mean_fn == WSMC_MEAN_OSCILLATOR) c->ew_feat = 1;
+        if (t.dist.mean_fn == WSMC_MEAN_OSCILLATOR) c->ew_feat |= WSMC_FEAT_OSC;
+        if (t.dist.family == WSMC_FAM_MVNORMAL) c->ew_feat |= WSMC_FEAT_MVN;
         if (!b->has_w) {   // the batch's first weight term: the pending reset, the slot pair
             b->has_w = 1;
             b->w = c->w;

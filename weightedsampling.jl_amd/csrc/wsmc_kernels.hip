@@ -205,7 +205,8 @@ __global__ __launch_bounds__(kBlock) void k_assign(double* out, int dim, AssignA
         if (k < dim) out[(int64_t)k * N + i] = x[k];
 }
 
-// FEAT (wsmc_terms.h): WSMC_FEAT_ALL, or 0 for affine means (no oscillator code: registers)
+// FEAT (wsmc_terms.h): WSMC_FEAT_ALL, WSMC_FEAT_OSC, or 0 for affine means (no oscillator or
+// full-covariance code: registers)
 template <unsigned FEAT>
 __global__ __launch_bounds__(kBlock) void k_sample(double* out, int dim, wsmc_dist d, uint64_t seed,
                                                    uint64_t op, int64_t goff, double* const* cols,
@@ -222,19 +223,20 @@ __global__ __launch_bounds__(kBlock) void k_sample(double* out, int dim, wsmc_di
         if (k < dim) out[(int64_t)k * N + i] = x[k];
 }
 
+template <unsigned FEAT>
 __global__ __launch_bounds__(kBlock) void k_sample_importance(double* out, int dim, wsmc_dist prop,
                                                               wsmc_dist targ, double* w, uint64_t seed,
                                                               uint64_t op, int64_t goff,
                                                               double* const* cols, int64_t N) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= N) return;
-    double x[4];
-    wsmc_dist_sample(&prop, x, seed, op, (uint64_t)(goff + i), cols, N, i);
+    double x[4] = {0.0, 0.0, 0.0, 0.0};
+    wsmc_dist_sample_mf(&prop, x, seed, op, (uint64_t)(goff + i), cols, N, i, nullptr, FEAT);
 #pragma unroll
     for (int k = 0; k < 4; ++k)
         if (k < dim) out[(int64_t)k * N + i] = x[k];
-    double lt = wsmc_dist_logpdf(&targ, x, cols, N, i, nullptr);
-    double lp = wsmc_dist_logpdf(&prop, x, cols, N, i, nullptr);
+    double lt = wsmc_dist_logpdf_mf(&targ, x, cols, N, i, nullptr, nullptr, FEAT);
+    double lp = wsmc_dist_logpdf_mf(&prop, x, cols, N, i, nullptr, nullptr, FEAT);
     w[i] = w[i] + (lt - lp);
 }
 
@@ -2982,8 +2984,11 @@ hipError_t launch_sample(hipStream_t s, double* out, int dim, const wsmc_dist& d
                          int64_t goff, double* const* cols, int64_t N) {
     const int has_sd = d.family == WSMC_FAM_MVNORMAL_ISO && wsmc_operand_is_const(&d.scale);
     const double sd = has_sd ? wsmc_sqrt(wsmc_operand_eval(&d.scale, nullptr, N, 0, nullptr)) : 0.0;
-    if (d.mean_fn == WSMC_MEAN_OSCILLATOR)
+    if (d.family == WSMC_FAM_MVNORMAL)
         hipLaunchKernelGGL(k_sample<WSMC_FEAT_ALL>, grid_for(N), dim3(kBlock), 0, s, out, dim, d, seed, op, goff, cols,
+                           N, has_sd, sd);
+    else if (d.mean_fn == WSMC_MEAN_OSCILLATOR)
+        hipLaunchKernelGGL(k_sample<WSMC_FEAT_OSC>, grid_for(N), dim3(kBlock), 0, s, out, dim, d, seed, op, goff, cols,
                            N, has_sd, sd);
     else
         hipLaunchKernelGGL(k_sample<0u>, grid_for(N), dim3(kBlock), 0, s, out, dim, d, seed, op, goff, cols, N, has_sd,
@@ -3011,8 +3016,10 @@ hipError_t launch_ew_assign1(hipStream_t s, const EwBatch& b, double* const* col
 hipError_t launch_ew_batch(hipStream_t s, const EwBatch& b, unsigned feat, uint64_t seed, int64_t goff, int64_t N) {
     static_assert(sizeof(EwBatch) + 32 <= 4096, "the batch rides in the kernel arguments");
     const size_t rows = sizeof(double) * kBlock * (size_t)b.nrows;   // only the rows used: occupancy
-    if (feat)
+    if (feat & WSMC_FEAT_MVN)
         hipLaunchKernelGGL(k_ew_batch<WSMC_FEAT_ALL>, grid_for(N), dim3(kBlock), rows, s, b, seed, goff, N);
+    else if (feat)
+        hipLaunchKernelGGL(k_ew_batch<WSMC_FEAT_OSC>, grid_for(N), dim3(kBlock), rows, s, b, seed, goff, N);
     else
         hipLaunchKernelGGL(k_ew_batch<0u>, grid_for(N), dim3(kBlock), rows, s, b, seed, goff, N);
     return hipGetLastError();
@@ -3020,8 +3027,12 @@ hipError_t launch_ew_batch(hipStream_t s, const EwBatch& b, unsigned feat, uint6
 hipError_t launch_sample_importance(hipStream_t s, double* out, int dim, const wsmc_dist& prop,
                                     const wsmc_dist& targ, double* w, uint64_t seed, uint64_t op,
                                     int64_t goff, double* const* cols, int64_t N) {
-    hipLaunchKernelGGL(k_sample_importance, grid_for(N), dim3(kBlock), 0, s, out, dim, prop, targ, w, seed,
-                       op, goff, cols, N);
+    if (prop.family == WSMC_FAM_MVNORMAL || targ.family == WSMC_FAM_MVNORMAL)
+        hipLaunchKernelGGL(k_sample_importance<WSMC_FEAT_ALL>, grid_for(N), dim3(kBlock), 0, s, out, dim, prop, targ, w,
+                           seed, op, goff, cols, N);
+    else
+        hipLaunchKernelGGL(k_sample_importance<WSMC_FEAT_OSC>, grid_for(N), dim3(kBlock), 0, s, out, dim, prop, targ, w,
+                           seed, op, goff, cols, N);
     return hipGetLastError();
 }
 hipError_t launch_weigh(hipStream_t s, const wsmc_term& t, double* w, double* const* cols, int64_t N, MaxSlots* ms,
@@ -3034,8 +3045,11 @@ hipError_t launch_weigh(hipStream_t s, const wsmc_term& t, double* w, double* co
         lm0.rcp = 1.0 / sc;
         lm0.valid = 1;
     }
-    if (t.dist.mean_fn == WSMC_MEAN_OSCILLATOR)
+    if (t.dist.family == WSMC_FAM_MVNORMAL)
         hipLaunchKernelGGL(k_weigh<WSMC_FEAT_ALL>, grid_for(N), dim3(kBlock), 0, s, t, w, cols, N, ms, ms_next, lm0,
+                           wreset);
+    else if (t.dist.mean_fn == WSMC_MEAN_OSCILLATOR)
+        hipLaunchKernelGGL(k_weigh<WSMC_FEAT_OSC>, grid_for(N), dim3(kBlock), 0, s, t, w, cols, N, ms, ms_next, lm0,
                            wreset);
     else
         hipLaunchKernelGGL(k_weigh<0u>, grid_for(N), dim3(kBlock), 0, s, t, w, cols, N, ms, ms_next, lm0, wreset);

@@ -65,7 +65,8 @@ struct WsmcState
 end
 
 const WSMC_ENOTPD = 3
-const FAM_NORMAL, FAM_HALFNORMAL, FAM_UNIFORM, FAM_MVNORMAL_ISO = Int32(0), Int32(1), Int32(2), Int32(3)
+const FAM_NORMAL, FAM_HALFNORMAL, FAM_UNIFORM, FAM_MVNORMAL_ISO, FAM_MVNORMAL =
+    Int32(0), Int32(1), Int32(2), Int32(3), Int32(4)
 const MEAN_AFFINE = Int32(0)
 const RESAMPLE_STRATIFIED = Int32(0)
 const PROPOSAL_RW, PROPOSAL_AUTORW = Int32(0), Int32(1)
@@ -280,8 +281,17 @@ function device_dist(s::HipColumnStore, kernel, args)
         S = Sigma isa Base.RefValue ? Sigma[] : Sigma
         d = size(S, 1)
         var = S[1, 1]
-        S == var * I(d) || return nothing                 # isotropic covariance only
-        return WsmcDist(FAM_MVNORMAL_ISO, MEAN_AFFINE, d, 0, operands(s, mu, d), const_operand(var), (0.0, 0.0))
+        S == var * I(d) &&
+            return WsmcDist(FAM_MVNORMAL_ISO, MEAN_AFFINE, d, 0, operands(s, mu, d), const_operand(var), (0.0, 0.0))
+        d <= 3 || return nothing                          # full covariance: dim <= 3
+        # a full constant Σ: the library packs its Cholesky factor into the dist
+        # (wsmc_dist_mvnormal_cov; PosDefException / non-symmetric Σ come back as errors)
+        ops = operands(s, mu, d)
+        z = const_operand(0.0)
+        r = Ref(WsmcDist(FAM_MVNORMAL, MEAN_AFFINE, d, 0, ntuple(k -> k <= d ? ops[k] : z, 4), z, (0.0, 0.0)))
+        Sm = Matrix{Float64}(transpose(Matrix{Float64}(S)))   # row-major for the C side
+        check(ccall((:wsmc_dist_mvnormal_cov, libwsmc), Cint, (Ptr{WsmcDist}, Ptr{Float64}), r, Sm))
+        return r[]
     end
     return nothing
 end

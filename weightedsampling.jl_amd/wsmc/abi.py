@@ -14,7 +14,7 @@ LIB_PATH = _PKG_DIR / "libwsmc.so"
 
 # ---- enums (include/wsmc.h) ---------------------------------------------------------
 WSMC_OK, WSMC_EARG, WSMC_EHIP, WSMC_ENOTPD, WSMC_ERCCL, WSMC_ESTATE, WSMC_ENOMEM = range(7)
-FAM_NORMAL, FAM_HALFNORMAL, FAM_UNIFORM, FAM_MVNORMAL_ISO = range(4)
+FAM_NORMAL, FAM_HALFNORMAL, FAM_UNIFORM, FAM_MVNORMAL_ISO, FAM_MVNORMAL = range(5)
 MEAN_AFFINE, MEAN_OSCILLATOR = range(2)
 TERM_SAMPLE, TERM_OBSERVE, TERM_WEIGHT = range(3)
 RESAMPLE_STRATIFIED, RESAMPLE_SYSTEMATIC, RESAMPLE_MULTINOMIAL = range(3)
@@ -81,6 +81,7 @@ SIGNATURES = {
     "wsmc_last_error": (C.c_char_p, []),
     "wsmc_version": (C.c_int, [_I32P, _I32P]),
     "wsmc_device_count": (C.c_int, [_I32P]),
+    "wsmc_dist_mvnormal_cov": (C.c_int, [C.c_void_p, _D]),
     "wsmc_create": (C.c_int, [C.POINTER(_P), C.c_int64, C.c_int32, C.c_uint64]),
     "wsmc_destroy": (C.c_int, [_P]),
     "wsmc_create_multi": (C.c_int, [C.POINTER(_P), C.c_int64, C.c_int32, _I32P, C.c_uint64, C.c_int32]),

@@ -14,6 +14,7 @@ to two column components (``α + β * x``, ``a .* x``, ``x{t} + v``).
 """
 from __future__ import annotations
 
+import ctypes as C
 import math
 from dataclasses import dataclass, field
 from typing import Sequence, Union
@@ -122,6 +123,7 @@ class Kernel:
     mean: tuple = ()          # Exprs (or an Oscillator)
     scale: object = 1.0       # sigma (std) or variance (MvNormal iso)
     params: tuple = (0.0, 0.0)
+    cov: tuple = ()           # FAM_MVNORMAL: Σ row-major (packed by the library)
 
     def dist(self, resolve) -> Dist:
         d = Dist()
@@ -142,6 +144,9 @@ class Kernel:
         d.scale = Expr.lift(self.scale).operand(resolve)
         if self.family == abi.FAM_UNIFORM:
             d.param[0], d.param[1] = float(self.params[0]), float(self.params[1])
+        if self.family == abi.FAM_MVNORMAL:
+            S = (C.c_double * len(self.cov))(*self.cov)
+            abi.check(abi.load_library().wsmc_dist_mvnormal_cov(C.byref(d), S))
         return d
 
     def columns(self):
@@ -172,7 +177,9 @@ def Uniform(a: float, b: float) -> Kernel:
 
 
 def MvNormal(mu, cov) -> Kernel:
-    """default_kernels.MvNormal(μ, Σ) for isotropic Σ = v·I (a covariance, not a std)."""
+    """default_kernels.MvNormal(μ, Σ) — Σ is a COVARIANCE (src/default_kernels.jl:93). A scalar
+    or Σ = v·I takes the isotropic family (dim ≤ 4); any other constant Σ (dim ≤ 3) takes the
+    full-covariance family, its Cholesky factor packed once by wsmc_dist_mvnormal_cov."""
     if isinstance(cov, (int, float, np.floating)):
         var = float(cov)
         mus = mu if isinstance(mu, (list, tuple, np.ndarray)) else None
@@ -182,9 +189,11 @@ def MvNormal(mu, cov) -> Kernel:
         if S.ndim != 2 or S.shape[0] != S.shape[1]:
             raise ValueError("covariance must be square")
         var = float(S[0, 0])
-        if not np.array_equal(S, var * np.eye(S.shape[0])):
-            raise NotImplementedError("device MvNormal supports isotropic covariance v*I only")
         dim = S.shape[0]
+        if not np.array_equal(S, var * np.eye(dim)):
+            if not 1 <= dim <= 3:
+                raise ValueError("MvNormal with a full covariance: dimension must be 1..3")
+            return Kernel(abi.FAM_MVNORMAL, dim, tuple(_exprs(mu, dim)), 0.0, cov=tuple(S.ravel()))
     if dim is None:
         raise ValueError("MvNormal with a scalar variance needs an explicit mean vector")
     if not 1 <= dim <= 4:
