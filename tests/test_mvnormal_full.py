@@ -133,3 +133,25 @@ def test_full_covariance_packing_is_the_cholesky_factor():
         want = [L[i, j] for i in range(d) for j in range(i + 1)] + [2.0 * np.sum(np.log(np.diag(L)))]
         _close(np.array(fields[:len(want)]), np.array(want), f"packed factor d={d}")
         assert math.isfinite(fields[len(want) - 1])
+
+
+def test_full_covariance_c_abi_rejections():
+    """wsmc_dist_mvnormal_cov through the C ABI (host only): dim outside 1..3, an oscillator
+    mean and null pointers are argument errors; the dist is untouched by a rejection."""
+    import ctypes as C
+    lib = abi.load_library()
+    S = (C.c_double * 16)(*np.eye(4).ravel())
+    d = abi.Dist()
+    d.dim = 4
+    assert lib.wsmc_dist_mvnormal_cov(C.byref(d), S) == abi.WSMC_EARG
+    assert d.family == 0
+    d.dim, d.mean_fn = 2, abi.MEAN_OSCILLATOR
+    assert lib.wsmc_dist_mvnormal_cov(C.byref(d), S) == abi.WSMC_EARG
+    assert lib.wsmc_dist_mvnormal_cov(None, S) == abi.WSMC_EARG
+    d.mean_fn = abi.MEAN_AFFINE
+    S2 = (C.c_double * 4)(4.0, 2.0, 2.0, 5.0)
+    assert lib.wsmc_dist_mvnormal_cov(C.byref(d), S2) == abi.WSMC_OK
+    assert d.family == abi.FAM_MVNORMAL
+    # L = [[2, 0], [1, 2]]: packed into mu[2].c0, mu[2].coef[0], mu[2].coef[1], then mu[3].c0
+    assert (d.mu[2].c0, d.mu[2].coef[0], d.mu[2].coef[1]) == (2.0, 1.0, 2.0)
+    assert d.mu[3].c0 == 2.0 * (math.log(2.0) + math.log(2.0))
