@@ -9,6 +9,7 @@
 #   round <tag>                 pytest -m gpu, smoke(), the default bench line, the statement-path
 #                               line, rocprofv3 kernel stats of the bench command, FETCH_SIZE /
 #                               WRITE_SIZE passes -> pmc_summary.json, pmc_step_bytes.json
+#   prof <tag>                  the round's profile passes alone
 #   bench <tag> [bench args]    bench.py line + rocprofv3 kernel stats of the same command
 #   moves <tag>                 C3 / C5 move-program lines (tools/bench_moves.py) + C3 kernel stats
 #   c5flops <tag>               C5 FP64 work (SQ_INSTS_VALU_*_F64) against its kernel durations
@@ -59,6 +60,18 @@ PY
 }
 line() { python -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[2], '%.4g' % d['value'], d['unit'], '%.3f ms/run' % d['ms_per_run'], 'frac %.3f' % d['roofline']['frac'])" "$1" "$2"; }
 
+prof_passes() {   # kernel stats of the bench command (20 timed runs: the profiler's kernel-trace
+                  # of the default 300 graph-replayed runs crashed inside rocprofv3 on r03_v3),
+                  # then FETCH_SIZE / WRITE_SIZE in separate passes
+  step 400 $O/stats.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python bench.py --no-cpu-baseline --steps 20 --warmup 2
+  stats_table $O/stats/run_kernel_stats.csv 6
+  A="--steps 2 --warmup 1 --no-cpu-baseline"
+  step 300 $O/fetch.log rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- python bench.py $A
+  step 300 $O/write.log rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python bench.py $A
+  python tools/summarize_pmc.py $O/pmc_summary.json $O/fetch $O/write > /dev/null
+  python tools/pmc_step_bytes.py $O/pmc_summary.json 1000000 100 $O/pmc_step_bytes.json
+}
+
 case $recipe in
 tests)   # [pytest args]: files / -k; the whole suite by default
   [ $# -gt 0 ] || set -- tests
@@ -73,17 +86,12 @@ round)
   line $O/bench.json bench
   timeout -k 10 400 python bench.py --no-cpu-baseline --statements > $O/bench_statements.json 2> $O/bench_statements.err || { tail -20 $O/bench_statements.err; exit 1; }
   line $O/bench_statements.json statements
-  step 400 $O/stats.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python bench.py --no-cpu-baseline
-  stats_table $O/stats/run_kernel_stats.csv 6
-  A="--steps 2 --warmup 1 --no-cpu-baseline"
-  step 300 $O/fetch.log rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- python bench.py $A
-  step 300 $O/write.log rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python bench.py $A
-  python tools/summarize_pmc.py $O/pmc_summary.json $O/fetch $O/write > /dev/null
-  python tools/pmc_step_bytes.py $O/pmc_summary.json 1000000 100 $O/pmc_step_bytes.json ;;
-bench)
-  timeout -k 10 400 python bench.py "$@" > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+  prof_passes ;;
+prof)   # the round's profile passes alone (kernel stats, FETCH_SIZE / WRITE_SIZE)
+  prof_passes ;;
+bench)  timeout -k 10 400 python bench.py "$@" > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
   line $O/bench.json bench
-  step 400 $O/stats.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python bench.py --no-cpu-baseline "$@"
+  step 400 $O/stats.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python bench.py --no-cpu-baseline --steps 20 --warmup 2 "$@"
   stats_table $O/stats/run_kernel_stats.csv 8 ;;
 moves)
   timeout -k 10 400 python tools/bench_moves.py c3 c3async c3gated_moves c3gated c5 c5async c3cpu > $O/moves.jsonl 2> $O/moves.err || { tail $O/moves.err; exit 1; }
