@@ -2946,6 +2946,11 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_final(Ssm2dFinal f) {
         f.x_out[i] = x.x; f.x_out[N + i] = x.y;
         return;
     }
+    // The lineage a_s (x_{s+1} is read at a_s): a_s = anc_log row s-1 at a_{s+1} when step s
+    // resampled, else a_{s+1}. The chain is the kernel's critical path, so the next row's entry
+    // is loaded unconditionally (every row of the log exists; the entry is used only when its
+    // step resampled) and before this step's x gather: one memory latency a step, not two.
+    int32_t raw = f.anc_log[(int64_t)(T - 2 > 0 ? T - 2 : 0) * S + a];
     // x_{T+1} was written at step T
     {
         const d2 x = *reinterpret_cast<const d2*>(f.hist_work[T + 1] + 2 * a);
@@ -2953,7 +2958,8 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_final(Ssm2dFinal f) {
         dst[i] = x.x; dst[N + i] = x.y;
     }
     for (int s = T - 1; s >= 1; --s) {
-        if (f.dec[s].resampled) a = f.anc_log[(int64_t)(s - 1) * S + a];
+        if (f.dec[s].resampled) a = raw;
+        raw = f.anc_log[(int64_t)(s - 2 > 0 ? s - 2 : 0) * S + a];
         const d2 x = *reinterpret_cast<const d2*>(f.hist_work[s + 1] + 2 * a);
         double* dst = f.hist_out[s + 1];
         dst[i] = x.x; dst[N + i] = x.y;
