@@ -357,6 +357,14 @@ int wsmc_debug_inject_failure(wsmc_ctx* ctx, int32_t shard, int32_t nth);
  * and, in stats_out[4] (may be NULL), the last run's largest block needed, its largest
  * lineage excursion, the runs re-done on the eager path after an overflow, the block size. */
 int wsmc_debug_exact(wsmc_ctx* ctx, int64_t cap, int64_t ctr, int64_t* stats_out);
+/* Statement batches compiled for their shape at run time (hiprtc; csrc/wsmc_jit.hip):
+ * stats_out[5] = signatures compiled, signatures that failed to compile (their batches run on
+ * the interpreter kernel), batches launched on compiled kernels, batches run on the
+ * interpreter, total compile time (us) — process-wide. */
+int wsmc_debug_jit_stats(int64_t* stats_out);
+/* Compile a representative batch signature (the 2D SSM step) for gfx950 without a device:
+ * WSMC_OK, or WSMC_EHIP with hiprtc's log in wsmc_last_error(). */
+int wsmc_debug_jit_selfcheck(void);
 
 #ifdef __cplusplus
 }

@@ -48,6 +48,24 @@ def test_ssm2d_statements(gpu_available, N, ess, scheme):
     assert g.log_evidence() == o.log_evidence()
 
 
+@pytest.mark.parametrize("N", [4096, 4095])
+def test_statement_batches_run_compiled(gpu_available, N):
+    """The step's statement batch runs on its signature's compiled kernel (csrc/wsmc_jit.hip):
+    two particles a thread at even N, one at odd N; one compile serves every step."""
+    obs = models.ssm2d_data(6)
+    before = abi.jit_stats()
+    g, o = wsmc.Context(N, seed=11), Oracle(N, seed=11)
+    models.ssm2d_statements(g, obs, ess_perc_min=1.0, wait=False)
+    models.ssm2d_statements(o, obs, ess_perc_min=1.0)
+    g.sync()
+    after = abi.jit_stats()
+    assert after["failed"] == 0
+    assert after["interpreted"] == before["interpreted"]
+    assert after["launched"] - before["launched"] >= len(obs)
+    assert after["compiled"] - before["compiled"] <= 6   # the step's batch, the first steps', the x{1} / v setup
+    assert_same_state(g, o)
+
+
 @pytest.mark.parametrize("N", [1024, 5001])
 @pytest.mark.parametrize("ess", [1.0, 0.5])
 @pytest.mark.parametrize("keep", [True, False])

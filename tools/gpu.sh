@@ -116,6 +116,18 @@ sq)
            sq_table $O/p.json ;;
     *) echo "sq: fused|c3|c5"; exit 2 ;;
   esac ;;
+ew)   # the statement path (bench.py --statements): its line, kernel stats, FETCH / WRITE and SQ passes
+  timeout -k 10 400 python bench.py --no-cpu-baseline --statements "$@" > $O/bench_statements.json 2> $O/bench_statements.err || { tail -20 $O/bench_statements.err; exit 1; }
+  line $O/bench_statements.json statements
+  step 400 $O/stats.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python bench.py --no-cpu-baseline --statements --steps 20 --warmup 2 "$@"
+  stats_table $O/stats/run_kernel_stats.csv 10
+  A="--steps 2 --warmup 1 --no-cpu-baseline --statements"
+  step 300 $O/fetch.log rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- python bench.py $A "$@"
+  step 300 $O/write.log rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python bench.py $A "$@"
+  python tools/summarize_pmc.py $O/pmc_summary.json $O/fetch $O/write
+  step 300 $O/sq.log rocprofv3 --kernel-trace --pmc $SQ --output-format csv -d $O/sq -o run -- python bench.py $A "$@"
+  python tools/summarize_pmc.py $O/sq.json $O/sq > /dev/null
+  sq_table $O/sq.json ew_batch,lazy_trace,rs_ ;;
 rccl)
   export NCCL_SOCKET_IFNAME=lo
   for m in island exact; do

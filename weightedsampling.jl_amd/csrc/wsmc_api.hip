@@ -66,10 +66,13 @@ static bool ew_enabled(const wsmc_ctx* c) {
 static int ew_flush(wsmc_ctx* c) {
     EwBatch* b = c->ew;
     if (!b || b->nops == 0) return WSMC_OK;
-    // a batch of one statement: its own kernel (leaner than the batch's: no rows, no table)
-    hipError_t e;
+    // the batch's signature compiled for its shape (csrc/wsmc_jit.hip); without it a batch of
+    // one statement runs its own kernel (leaner than the interpreter's: no rows, no table)
+    hipError_t e = launch_ew_jit(c->stream, *b, c->ew_feat, c->seed, c->goff, c->N, c->device);
     const EwOp& o0 = b->ops[0];
-    if (b->nops > 1)
+    if (e != hipErrorNotSupported)
+        ;
+    else if (b->nops > 1)
         e = launch_ew_batch(c->stream, *b, c->ew_feat, c->seed, c->goff, c->N);
     else if (o0.kind == 0)
         e = launch_ew_assign1(c->stream, *b, c->d_colptr, c->N);
@@ -4093,3 +4096,15 @@ int wsmc_debug_kernel_bench(wsmc_ctx* c, int32_t kernel, int32_t mode, int32_t i
 }
 
 }  // extern "C"
+
+int wsmc_debug_jit_stats(int64_t* stats_out) {
+    if (!stats_out) return fail(WSMC_EARG, "null stats_out");
+    ew_jit_stats(stats_out);
+    return WSMC_OK;
+}
+
+int wsmc_debug_jit_selfcheck(void) {
+    std::string err;
+    if (ew_jit_selfcheck(err)) return fail(WSMC_EHIP, "statement-batch JIT: " + err);
+    return WSMC_OK;
+}

@@ -13,13 +13,12 @@
 #include "wsmc.h"
 #include "wsmc_math.h"
 #include "wsmc_terms.h"
+#include "wsmc_ew.h"
 
 namespace wsmc {
 
-constexpr int kBlock = 256;            // threads per workgroup (4 waves of 64)
 constexpr int kItems = 8;              // particles per thread in the tile kernels
 constexpr int kTile = kBlock * kItems; // 2048 particles per tile (canonical reduction tile)
-constexpr int kSlots = 64;             // max-accumulator slots (blockIdx % 64)
 constexpr int kRsBlock = 1024;         // threads of the reduce workgroup
 #ifndef WSMC_SUM_BLOCK
 #define WSMC_SUM_BLOCK 256                // build-time override for block-size experiments (tools/)
@@ -34,13 +33,6 @@ constexpr int kRsChunk = 2048;         // ancestor slots per fill task
 constexpr int kMaxCols = 4096;
 constexpr int kMaxShards = 8;     // one node: up to 8 GPUs
 
-// Max accumulator of one Resample: 64 ordered-encoded slots, one per block group
-// (blockIdx % 64), filled with read-filtered atomicMax. One 128-B line per slot: memory-side
-// atomics and filtered loads to one line serialise, so the slots must not share lines.
-struct MaxSlots {
-    unsigned long long v[kSlots][16];
-};
-
 // One shard's weight statistics: what the ranks exchange (64 B per step).
 struct ShardRecord {
     unsigned long long menc;   // ordered encoding of the shard max log-weight
@@ -53,16 +45,6 @@ struct ShardRecord {
 
 constexpr int kPart = 4;      // per-tile partials: sum q, sum q2, sum wf2, sum wf (all exact)
 constexpr int kRedPart = 6;   // reduce-kernel parts: Q, Q2, Wf2 lo32/hi, Wf lo32/hi
-
-// Resample outcome for one invocation (one step of a fused run).
-constexpr int kDecRing = 1024;   // asynchronous Resample decisions held before a forced resolve
-struct Decision {
-    int32_t resampled;
-    int32_t ntasks;     // ancestor-fill tasks of this shard (<= ntiles + N / kRsChunk + 1)
-    double mean;        // this shard's post-resample log-weight
-    double ess;         // global ESS/N
-    double M;           // this shard's max log-weight
-};
 
 // Exact cross-shard resampling: the global CDF and the slot windows,
 // built on the device from the all-gathered records (k_rs_decide_exact). Shard g's
@@ -329,63 +311,12 @@ struct Indirect {
 };
 hipError_t launch_assign(hipStream_t s, double* out, int dim, const wsmc_operand* expr,
                          double* const* cols, int64_t N, const Indirect& ind);
-// A batch of consecutive elementwise statements (Assign / Sample / Observe / Weight) run as one
-// kernel, each particle taking the statements in order (csrc/wsmc_api.hip ew_*). The batch
-// travels in the kernel's arguments (read in place through the kernarg segment).
-constexpr int kEwOps = 6;       // statements a batch holds
-constexpr int kEwSlots = 16;    // columns the Sample / weight terms read
-constexpr int kEwRows = 12;     // LDS rows (one column component each, a value per thread)
-constexpr int kEwPre = 10;      // components loaded into LDS rows at the start
-struct EwAssign {
-    wsmc_operand e[4];
-    const double* p[4][2];      // operand components resolved to pointers
-    uint32_t lag;               // bit 2k+m: operand read one lazy Resample behind (the batch's row)
-    int8_t fwd[4][2];           // >= 0: the operand is an LDS row (an earlier statement's output)
-};
-struct EwSample {
-    wsmc_dist d;                // operand columns renumbered to the batch's slots
-    unsigned long long op;
-    int32_t has_sd, pad;
-    double sd;                  // a constant MvNormal variance's sqrt (host-evaluated)
-};
-struct EwWeigh {
-    wsmc_term t;                // operand columns renumbered to the batch's slots
-    wsmc_logmemo lm0;           // a constant scale's log / reciprocal (host-evaluated)
-};
-struct EwOp {
-    int32_t kind;               // 0 Assign, 1 Sample, 2 Observe / Weight
-    int16_t dim;
-    int16_t out_row;            // >= 0: the output's components also go to LDS rows out_row..
-                                // (later statements of the batch read them there)
-    double* out;                // Assign / Sample destination (components N apart)
-    union {
-        EwAssign a;
-        EwSample s;
-        EwWeigh w;
-    };
-};
-struct EwBatch {
-    int32_t nops, ntab;
-    int32_t has_w, nslots;
-    const int32_t* anc;         // the newest lazy Resample's ancestors (lagged Assign operands)
-    const Decision* dec;        // and its decision
-    double* w;
-    const Decision* wreset;     // a pending weight reset (the first weight term applies it)
-    MaxSlots* ms;               // the max of the final weights (zero on entry)
-    MaxSlots* ms_next;          // zeroed by block 0
-    double** tab;               // device column table: entries moved by Assigns into fresh buffers
-    double* tab_out[4];
-    int32_t tab_col[4];
-    // the Sample / weight terms read their columns from LDS: slot s at rows slot_row[s] +
-    // component (an earlier statement's output, or loaded at the start: pre_src -> pre_row)
-    const double* slot[kEwSlots];
-    int8_t slot_row[kEwSlots];
-    int32_t nrows, npre;
-    const double* pre_src[kEwPre];
-    int8_t pre_row[kEwPre];
-    int8_t pre_lag[kEwPre];     // loaded through the ancestor row
-    EwOp ops[kEwOps];
-};
+// the statement batch (csrc/wsmc_ew.h) on the interpreter kernel, or on its signature's kernel
+// compiled at run time (csrc/wsmc_jit.hip; hipErrorNotSupported: none, run the interpreter)
+hipError_t launch_ew_jit(hipStream_t s, const EwBatch& b, unsigned feat, uint64_t seed, int64_t goff, int64_t N,
+                         int device);
+void ew_jit_stats(int64_t* out);   // compiled, failed, launched, interpreted, compile time (us)
+int ew_jit_selfcheck(std::string& err);   // hiprtc builds a representative signature (no device)
 hipError_t launch_ew_batch(hipStream_t s, const EwBatch& b, unsigned feat, uint64_t seed, int64_t goff, int64_t N);
 // a batch of one Assign: k_assign with the batch's resolved pointers
 hipError_t launch_ew_assign1(hipStream_t s, const EwBatch& b, double* const* cols, int64_t N);

@@ -1,0 +1,346 @@
+// wsmc_jit.hip — statement batches compiled for their shape at run time (hiprtc).
+//
+// A model's step issues the same statements every step (examples/2D_ssm.jl:11-16: Assign,
+// Sample, Assign, Observe), so the batch csrc/wsmc_api.hip collects for it has the same shape
+// every step: the same op kinds and dims, the same rows, the same columns read through the
+// ancestors. Only the values change (buffer pointers, constants, observations, op counters).
+// The shape is the signature (EwSig, csrc/wsmc_ew_body.h); the first launch of a signature on a
+// device generates a translation unit that instantiates ew_body<signature>, compiles it with
+// hiprtc for the device's architecture from the headers embedded at build time (the same text
+// hipcc compiled into this library, -ffp-contract=off, no fast math: the same bits), loads the
+// code object and keeps it for the process. This is the device analogue of the reference's
+// per-model specialisation: Julia compiles the broadcasts `vectorize` emits for each @model
+// (src/rewrites.jl:146-219) the first time the model runs.
+//
+// A batch whose signature fails to compile (or WSMC_DIAG_NO_JIT=1) runs on the interpreter
+// kernel k_ew_batch, which computes the same bits; wsmc_debug_jit_stats counts both.
+#include <hip/hiprtc.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+
+#include "wsmc_ew_body.h"
+#include "wsmc_internal.h"
+
+namespace wsmc {
+namespace {
+
+struct JitHeader {
+    const char* name;
+    const char* text;
+};
+const JitHeader kJitHeaders[] = {
+#include "wsmc_jit_headers.inc"
+};
+
+struct JitKernel {
+    hipModule_t mod = nullptr;
+    hipFunction_t f[2] = {nullptr, nullptr};   // P = 1, P = 2
+    bool ok = false;
+};
+
+struct JitCache {
+    std::mutex mu;
+    std::map<std::pair<int, std::string>, JitKernel> k;
+    int64_t compiled = 0, failed = 0, launched = 0, interpreted = 0;
+    double compile_s = 0.0;
+};
+JitCache& cache() {
+    static JitCache* c = new JitCache;   // never destroyed: modules live for the process
+    return *c;
+}
+
+bool jit_off() {
+    static const bool v = [] {
+        const char* e = getenv("WSMC_DIAG_NO_JIT");
+        return e && atoi(e) != 0;
+    }();
+    return v;
+}
+bool jit_verbose() {
+    static const bool v = [] {
+        const char* e = getenv("WSMC_JIT_VERBOSE");
+        return e && atoi(e) != 0;
+    }();
+    return v;
+}
+
+// the row an operand of a Sample / weight term reads (its column renumbered to a batch slot)
+int8_t slot_rowc(const EwBatch& b, int32_t col, int32_t comp) {
+    return col < 0 ? (int8_t)-1 : (int8_t)(b.slot_row[col] + comp);
+}
+
+EwSig signature(const EwBatch& b, unsigned feat) {
+    EwSig g;
+    std::memset(&g, 0, sizeof(g));
+    g.nops = (int8_t)b.nops;
+    g.has_w = (int8_t)(b.has_w != 0);
+    g.has_reset = (int8_t)(b.has_w && b.wreset != nullptr);
+    g.has_anc = (int8_t)(b.anc != nullptr);
+    g.has_dec = (int8_t)(b.dec != nullptr);
+    g.ntab = (int8_t)b.ntab;
+    g.npre = (int8_t)b.npre;
+    for (int k = 0; k < b.npre; ++k) {
+        g.pre_row[k] = b.pre_row[k];
+        g.pre_lag[k] = b.pre_lag[k];
+    }
+    g.feat = feat;
+    for (int k = 0; k < b.nops; ++k) {
+        const EwOp& op = b.ops[k];
+        EwSigOp& o = g.op[k];
+        std::memset(&o, -1, sizeof(o));
+        o.kind = (int8_t)op.kind;
+        o.dim = (int8_t)op.dim;
+        o.out_row = (int8_t)op.out_row;
+        o.family = o.mean_fn = o.ddim = o.has_sd = o.pad = 0;
+        for (int q = 0; q < 4; ++q)
+            for (int m = 0; m < 2; ++m) {
+                o.asrc[q][m] = kSrcNone;
+                o.arow[q][m] = 0;
+            }
+        if (op.kind == 0) {
+            for (int q = 0; q < op.dim; ++q)
+                for (int m = 0; m < 2; ++m) {
+                    if (op.a.e[q].col[m] < 0) continue;
+                    if (op.a.fwd[q][m] >= 0) {
+                        o.asrc[q][m] = kSrcRow;
+                        o.arow[q][m] = op.a.fwd[q][m];
+                    } else {
+                        o.asrc[q][m] = ((op.a.lag >> (2 * q + m)) & 1) ? kSrcLag : kSrcMem;
+                    }
+                }
+            continue;
+        }
+        const wsmc_dist& d = op.kind == 1 ? op.s.d : op.w.t.dist;
+        o.family = (int8_t)d.family;
+        o.mean_fn = (int8_t)d.mean_fn;
+        o.ddim = (int8_t)d.dim;
+        o.has_sd = (int8_t)(op.kind == 1 && op.s.has_sd);
+        for (int q = 0; q < 4; ++q)
+            for (int m = 0; m < 2; ++m) o.mrow[q][m] = slot_rowc(b, d.mu[q].col[m], d.mu[q].comp[m]);
+        for (int m = 0; m < 2; ++m) o.srow[m] = slot_rowc(b, d.scale.col[m], d.scale.comp[m]);
+        if (op.kind == 2)
+            for (int q = 0; q < 4; ++q)
+                for (int m = 0; m < 2; ++m) o.xrow[q][m] = slot_rowc(b, op.w.t.x[q].col[m], op.w.t.x[q].comp[m]);
+    }
+    return g;
+}
+
+// the signature as a C++ aggregate initializer (also the cache key)
+std::string sig_text(const EwSig& g) {
+    std::string s;
+    auto num = [&](int v) { s += std::to_string(v); s += ','; };
+    auto arr = [&](const int8_t* a, int n) {
+        s += '{';
+        for (int k = 0; k < n; ++k) num(a[k]);
+        s += "},";
+    };
+    s += '{';
+    num(g.nops); num(g.has_w); num(g.has_reset); num(g.has_anc); num(g.has_dec); num(g.ntab); num(g.npre); num(0);
+    arr(g.pre_row, kEwPre);
+    arr(g.pre_lag, kEwPre);
+    s += std::to_string(g.feat) + "u,{";
+    for (int k = 0; k < kEwOps; ++k) {
+        const EwSigOp& o = g.op[k];
+        s += '{';
+        num(o.kind); num(o.dim); num(o.out_row); num(o.family); num(o.mean_fn); num(o.ddim); num(o.has_sd); num(0);
+        s += '{'; for (int q = 0; q < 4; ++q) arr(o.asrc[q], 2); s += "},";
+        s += '{'; for (int q = 0; q < 4; ++q) arr(o.arow[q], 2); s += "},";
+        s += '{'; for (int q = 0; q < 4; ++q) arr(o.mrow[q], 2); s += "},";
+        arr(o.srow, 2);
+        s += '{'; for (int q = 0; q < 4; ++q) arr(o.xrow[q], 2); s += "}";
+        s += "},";
+    }
+    s += "}}";
+    return s;
+}
+
+std::string tu_source(const std::string& sig) {
+    return "#include \"wsmc_ew_body.h\"\n"
+           "struct WsmcSig { static constexpr wsmc::EwSig sig = " + sig + "; };\n"
+           "extern \"C\" __global__ __launch_bounds__(256) void wsmc_ew_p1(wsmc::EwBatch, uint64_t seed, int64_t goff, "
+           "int64_t N) { wsmc::ew_body<WsmcSig, 1>(seed, goff, N); }\n"
+           "extern \"C\" __global__ __launch_bounds__(256) void wsmc_ew_p2(wsmc::EwBatch, uint64_t seed, int64_t goff, "
+           "int64_t N) { wsmc::ew_body<WsmcSig, 2>(seed, goff, N); }\n";
+}
+
+// compile a signature's translation unit for `arch` (the code object in `code`)
+bool compile_code(const std::string& arch, const std::string& sig, std::string& code, std::string& err) {
+    const std::string src = tu_source(sig);
+    const int nh = (int)(sizeof(kJitHeaders) / sizeof(kJitHeaders[0]));
+    const char* htext[8];
+    const char* hname[8];
+    for (int k = 0; k < nh; ++k) {
+        htext[k] = kJitHeaders[k].text;
+        hname[k] = kJitHeaders[k].name;
+    }
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "wsmc_ew_jit.hip", nh, htext, hname) != HIPRTC_SUCCESS) {
+        err = "hiprtcCreateProgram failed";
+        return false;
+    }
+    const std::string arch_opt = "--offload-arch=" + arch;
+    const char* opts[] = {arch_opt.c_str(), "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
+                          "-munsafe-fp-atomics", "-Wno-unused-result"};
+    const hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof(opts) / sizeof(opts[0])), opts);
+    if (rc != HIPRTC_SUCCESS) {
+        size_t n = 0;
+        hiprtcGetProgramLogSize(prog, &n);
+        std::string log(n, '\0');
+        if (n) hiprtcGetProgramLog(prog, &log[0]);
+        err = std::string("hiprtcCompileProgram: ") + hiprtcGetErrorString(rc) + "\n" + log;
+        hiprtcDestroyProgram(&prog);
+        return false;
+    }
+    size_t n = 0;
+    hiprtcGetCodeSize(prog, &n);
+    code.assign(n, '\0');
+    hiprtcGetCode(prog, &code[0]);
+    hiprtcDestroyProgram(&prog);
+    return true;
+}
+
+bool compile(int device, const std::string& sig, JitKernel& out, std::string& err) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+        err = "hipGetDeviceProperties failed";
+        return false;
+    }
+    std::string arch = prop.gcnArchName;   // e.g. "gfx950:sramecc+:xnack-": the processor alone
+    arch = arch.substr(0, arch.find(':'));
+    std::string code;
+    if (!compile_code(arch, sig, code, err)) return false;
+    int cur = 0;
+    hipGetDevice(&cur);
+    hipSetDevice(device);
+    hipError_t e = hipModuleLoadData(&out.mod, code.data());
+    if (e == hipSuccess) e = hipModuleGetFunction(&out.f[0], out.mod, "wsmc_ew_p1");
+    if (e == hipSuccess) e = hipModuleGetFunction(&out.f[1], out.mod, "wsmc_ew_p2");
+    hipSetDevice(cur);
+    if (e != hipSuccess) {
+        err = std::string("hipModuleLoadData: ") + hipGetErrorString(e);
+        return false;
+    }
+    return true;
+}
+
+bool aligned(const void* p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; }
+
+// two particles a thread: N even and every direct (not gathered) access 16-B aligned
+bool pair_ok(const EwBatch& b, int64_t N) {
+    if (N & 1) return false;
+    if (b.anc && !aligned(b.anc, 8)) return false;
+    if (b.has_w && !aligned(b.w, 16)) return false;
+    for (int k = 0; k < b.npre; ++k)
+        if (!b.pre_lag[k] && !aligned(b.pre_src[k], 16)) return false;
+    for (int k = 0; k < b.nops; ++k) {
+        const EwOp& op = b.ops[k];
+        if (op.kind != 2 && !aligned(op.out, 16)) return false;
+        if (op.kind == 0)
+            for (int q = 0; q < op.dim; ++q)
+                for (int m = 0; m < 2; ++m)
+                    if (op.a.e[q].col[m] >= 0 && op.a.fwd[q][m] < 0 && !((op.a.lag >> (2 * q + m)) & 1) &&
+                        !aligned(op.a.p[q][m], 16))
+                        return false;
+    }
+    return true;
+}
+
+}  // namespace
+
+// the batch on its signature's compiled kernel; hipErrorNotSupported: no kernel (JIT off or the
+// signature failed to compile) — the caller runs the interpreter
+hipError_t launch_ew_jit(hipStream_t s, const EwBatch& b, unsigned feat, uint64_t seed, int64_t goff, int64_t N,
+                         int device) {
+    JitCache& C = cache();
+    if (jit_off()) {
+        std::lock_guard<std::mutex> lk(C.mu);
+        C.interpreted += 1;
+        return hipErrorNotSupported;
+    }
+    const std::string key = sig_text(signature(b, feat));
+    JitKernel* jk = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(C.mu);
+        auto it = C.k.find({device, key});
+        if (it == C.k.end()) {
+            JitKernel k;
+            std::string err;
+            const auto t0 = std::chrono::steady_clock::now();
+            k.ok = compile(device, key, k, err);
+            const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            C.compile_s += dt;
+            if (k.ok) {
+                C.compiled += 1;
+                if (jit_verbose()) fprintf(stderr, "[wsmc jit] device %d: signature compiled in %.2f s\n", device, dt);
+            } else {
+                C.failed += 1;
+                fprintf(stderr, "[wsmc jit] device %d: a statement-batch signature did not compile; it runs on the "
+                                "interpreter kernel\n%s\n", device, err.c_str());
+            }
+            it = C.k.emplace(std::make_pair(device, key), k).first;
+        }
+        jk = &it->second;
+        if (!jk->ok) {
+            C.interpreted += 1;
+            return hipErrorNotSupported;
+        }
+        C.launched += 1;
+    }
+    const int P = pair_ok(b, N) ? 2 : 1;
+    const int64_t threads = (N + P - 1) / P;
+    const unsigned grid = (unsigned)((threads + kBlock - 1) / kBlock);
+    EwBatch bb = b;   // the kernel arguments (copied by the launch)
+    void* args[] = {&bb, &seed, &goff, &N};
+    return hipModuleLaunchKernel(jk->f[P - 1], grid, 1, 1, kBlock, 1, 1, 0, s, args, nullptr);
+}
+
+// compile a representative signature (the 2D SSM step: Assign through the ancestors, Sample,
+// Assign, Observe) for gfx950 without a device: the embedded headers build under hiprtc
+int ew_jit_selfcheck(std::string& err) {
+    EwSig g;
+    std::memset(&g, 0, sizeof(g));
+    g.nops = 4; g.has_w = 1; g.has_reset = 1; g.has_anc = 1; g.has_dec = 1; g.ntab = 1; g.npre = 4;
+    for (int k = 0; k < 4; ++k) { g.pre_row[k] = (int8_t)k; g.pre_lag[k] = 1; }
+    const int8_t rows[4][2][2] = {{{0, 2}, {1, 3}}, {{0, 0}, {0, 0}}, {{2, 6}, {3, 7}}, {{0, 0}, {0, 0}}};
+    for (int k = 0; k < 4; ++k) {
+        EwSigOp& o = g.op[k];
+        std::memset(&o, -1, sizeof(o));
+        o.kind = (int8_t)(k == 3 ? 2 : (k == 1 ? 1 : 0));
+        o.dim = 2;
+        o.out_row = (int8_t)(k == 3 ? -1 : 4 + 2 * k);
+        o.family = (int8_t)(o.kind == 0 ? 0 : WSMC_FAM_MVNORMAL_ISO);
+        o.mean_fn = 0;
+        o.ddim = (int8_t)(o.kind == 0 ? 0 : 2);
+        o.has_sd = (int8_t)(k == 1);
+        o.pad = 0;
+        for (int q = 0; q < 4; ++q)
+            for (int m = 0; m < 2; ++m) {
+                o.asrc[q][m] = (o.kind == 0 && q < 2) ? kSrcRow : kSrcNone;
+                o.arow[q][m] = (o.kind == 0 && q < 2) ? rows[k][q][m] : 0;
+            }
+        if (k == 3) {
+            o.mrow[0][0] = 4;
+            o.mrow[1][0] = 5;
+        }
+    }
+    std::string code;
+    return compile_code("gfx950", sig_text(g), code, err) ? 0 : -1;
+}
+
+void ew_jit_stats(int64_t* out) {
+    JitCache& C = cache();
+    std::lock_guard<std::mutex> lk(C.mu);
+    out[0] = C.compiled;
+    out[1] = C.failed;
+    out[2] = C.launched;
+    out[3] = C.interpreted;
+    out[4] = (int64_t)(C.compile_s * 1e6);
+}
+
+}  // namespace wsmc

@@ -137,7 +137,17 @@ SIGNATURES = {
     "wsmc_debug_kernel_bench": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_int32, _D]),
     "wsmc_debug_inject_failure": (C.c_int, [_P, C.c_int32, C.c_int32]),
     "wsmc_debug_exact": (C.c_int, [_P, C.c_int64, C.c_int64, C.POINTER(C.c_int64)]),
+    "wsmc_debug_jit_stats": (C.c_int, [C.POINTER(C.c_int64)]),
+    "wsmc_debug_jit_selfcheck": (C.c_int, []),
 }
+
+
+def jit_stats() -> dict:
+    """Process-wide counters of the statement batches compiled for their shape (csrc/wsmc_jit.hip)."""
+    st = (C.c_int64 * 5)()
+    check(load_library().wsmc_debug_jit_stats(st))
+    return {"compiled": st[0], "failed": st[1], "launched": st[2], "interpreted": st[3],
+            "compile_s": st[4] / 1e6}
 
 
 # int exchange(void* user, const uint64_t* mine, int32_t words, uint64_t* all)
