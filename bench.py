@@ -107,22 +107,30 @@ CPU_REPS = 5   # timed all-cores CPU runs after the warm-up; the median is repor
 
 
 def pin_openmp() -> dict:
-    """Bind the CPU ports' OpenMP threads one per core, packed (OMP_PLACES=cores,
-    OMP_PROC_BIND=close), so the all-cores figure does not depend on where the scheduler
-    drifts the threads. Must run before the oracle library (and its OpenMP runtime) loads."""
+    """Bind the CPU ports' OpenMP threads one per core, spread over the whole affinity mask
+    (OMP_PLACES=cores, OMP_PROC_BIND=spread): both sockets / NUMA nodes take threads, and the
+    threads do not pile onto the first cores of the mask, where other jobs on a shared host
+    pack theirs (round 3 bound them `close` and measured 4x apart from box to box). The ports
+    first-touch their buffers in the same parallel loops that use them, so every node holds
+    the pages its threads work on. Must run before the oracle library (and its OpenMP runtime)
+    loads."""
     os.environ.setdefault("OMP_PLACES", "cores")
-    os.environ.setdefault("OMP_PROC_BIND", "close")
+    os.environ.setdefault("OMP_PROC_BIND", "spread")
     return {"OMP_PLACES": os.environ["OMP_PLACES"], "OMP_PROC_BIND": os.environ["OMP_PROC_BIND"]}
 
 
-def cpu_numa(threads: int) -> dict:
-    """The NUMA nodes of the first `threads` CPUs of this process's affinity mask (the cores
-    OMP_PROC_BIND=close packs the threads onto), and the node count of the host."""
+def cpu_topology() -> dict:
+    """Physical cores (distinct (package, core) pairs) and NUMA nodes of this process's
+    affinity mask, the host's node count and its load average when the ports ran."""
     cpus = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else []
-    nodes = set()
-    for c in cpus[:threads]:
+    cores, nodes = set(), set()
+    for c in cpus:
+        base = f"/sys/devices/system/cpu/cpu{c}"
         try:
-            for e in os.listdir(f"/sys/devices/system/cpu/cpu{c}"):
+            pkg = open(f"{base}/topology/physical_package_id").read().strip()
+            core = open(f"{base}/topology/core_id").read().strip()
+            cores.add((pkg, core))
+            for e in os.listdir(base):
                 if e.startswith("node") and e[4:].isdigit():
                     nodes.add(int(e[4:]))
         except OSError:
@@ -131,7 +139,12 @@ def cpu_numa(threads: int) -> dict:
         total = len([e for e in os.listdir("/sys/devices/system/node") if e.startswith("node") and e[4:].isdigit()])
     except OSError:
         total = None
-    return {"nodes_used": sorted(nodes), "host_nodes": total, "affinity_cpus": len(cpus)}
+    try:
+        load = [round(x, 2) for x in os.getloadavg()]
+    except OSError:
+        load = None
+    return {"affinity_cpus": len(cpus), "physical_cores": len(cores) or None, "nodes_used": sorted(nodes),
+            "host_nodes": total, "loadavg_1_5_15": load}
 
 
 def rep_stats(ts) -> dict:
@@ -338,7 +351,7 @@ def main():
         else:
             nth = cpu_threads(args.cpu_threads)
             omp = pin_openmp()
-            numa = cpu_numa(nth)   # before the ports run: OpenMP then binds this thread to one core
+            topo = cpu_topology()   # before the ports run: OpenMP then binds this thread to one core
             n, T = args.cpu_particles, args.cpu_T
             fps, fdt, fst = cpu_baseline_fast(obs, n, T, args.ess, nth, args.seed)
             f1, f1dt, _ = cpu_baseline_fast(obs, args.cpu_1t_particles, T, args.ess, 1, args.seed)
@@ -359,8 +372,18 @@ def main():
             best, other, other_key = ((fast_leg, exact_leg, "exact_port") if fps >= cps
                                       else (exact_leg, fast_leg, "fast_port"))
             cpu = dict(best)
+            pc = topo["physical_cores"] or nth
             cpu.update({
-                "threads": nth, "binding": omp, "numa": numa, "cpu_model": cpu_model(),
+                "threads": nth, "binding": omp, "numa": topo, "cpu_model": cpu_model(),
+                # the GPU pool sets OMP_NUM_THREADS to the job's CPU share of the shared host (16
+                # for one GPU) and asks jobs to leave it: `threads` honours it. For scale, the
+                # same rate per thread times every physical core of the mask — a linear upper
+                # bound on the whole host (memory bandwidth would cap it first), labelled so
+                "threads_policy": ("OMP_NUM_THREADS (the GPU pool's CPU share of the host, left as set)"
+                                   if os.environ.get("OMP_NUM_THREADS", "").isdigit() else "affinity mask"),
+                "all_physical_cores_linear_bound": {
+                    "value": best["value"] / nth * pc, "cores": pc, "kind": "extrapolation",
+                    "gpu_over_it": value / (best["value"] / nth * pc)},
                 other_key: other,
                 "single_thread": {"value": f1, "unit": "particle-steps/s", "cores": 1, "kind": "port",
                                   "sample": f"oracle/wsmc_port_fast.c, 1 thread, N={args.cpu_1t_particles} "

@@ -639,6 +639,43 @@ def test_multi_handle_shard_failure_returns_error(gpu_available, transport):
     g.close()
 
 
+@pytest.mark.parametrize("mode", ["island", "exact"])
+def test_multi_handle_symmetric_errors_keep_the_handle(gpu_available, mode):
+    """Errors every shard meets at the same point do not abort the handle: an
+    argument error (before any exchange) and a population-wide not-positive-definite autoRW
+    covariance (after the same exchanges on every shard) return the error, the shards keep
+    one state, and later calls work — bit for bit against the three-shard oracle."""
+    sys.path.insert(0, str(REPO / "oracle"))
+    from oracle import Oracle
+    import wsmc
+    from wsmc import abi, models
+    from wsmc.dsl import Normal
+    from test_gpu_parity import assert_same_state
+    G, N = 3, 3000
+    exact = mode == "exact"
+    g = wsmc.Context.multi(N, G, seed=4, devices=[0] * G, transport=abi.TRANSPORT_HOST)
+    if exact:
+        g.comm_set_shard_mode(abi.SHARD_EXACT)
+    o = Oracle(N, seed=4, shards=G, exact=exact)
+    res = []
+    for c in (g, o):
+        R = models.resolver(c)
+        a, b = c.col_create("a"), c.col_create("b")
+        c.sample(a, Normal(0.0, 1.0).dist(R))
+        c.assign(b, abi.Operand.column(a, coef=2.0))      # b = 2a: rank-1 covariance
+        c.observe(Normal(wsmc.Col("a"), 1.0).dist(R), models._const([0.2]))
+        with pytest.raises(np.linalg.LinAlgError):
+            c.move(abi.PROPOSAL_AUTORW, [a, b], 1e-3)
+        acc = c.move(abi.PROPOSAL_AUTORW, [a], 1e-3)
+        res.append(acc)
+    assert res[0] == res[1]
+    with pytest.raises(wsmc.WSMCError):
+        g.assign(999, abi.Operand.column(0))             # an unknown column on every shard
+    g.get_state()                                        # still one state: the handle works
+    assert_same_state(g, o)
+    g.close()
+
+
 @pytest.mark.parametrize("sizes", [(2600, 2600), (1700, 2101, 1500)])
 @pytest.mark.parametrize("small", [False, True])
 def test_exact_fused_run_without_host_round_trips(gpu_available, sizes, small):

@@ -7,6 +7,8 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -17,6 +19,31 @@
 using namespace wsmc;
 
 namespace wsmc {
+bool peer_aborted(wsmc_ctx* c) {
+    if (!c->peer_abort || !c->peer_abort->load(std::memory_order_acquire)) return false;
+    if (c->comm) {   // this shard's thread is the only user of its communicator
+        (void)ncclCommAbort(c->comm);
+        c->comm = nullptr;
+    }
+    c->released = true;
+    return true;
+}
+hipError_t ctx_sync(wsmc_ctx* c, hipStream_t s) {
+    if (!c->peer_abort) return hipStreamSynchronize(s);
+    for (int spin = 0;; ++spin) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e != hipErrorNotReady) return e;
+        if (peer_aborted(c)) {
+            // the abort ends the collectives in flight; what remains on the stream completes
+            (void)hipStreamSynchronize(s);
+            return hipErrorLaunchFailure;
+        }
+        if (spin < 4096)
+            std::this_thread::yield();
+        else
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
 int fail(int code, const std::string& msg) {
@@ -182,7 +209,7 @@ static bool ew_remap_dist(wsmc_ctx* c, EwBatch* b, wsmc_dist& d) {
 // ---- helpers -------------------------------------------------------------------------
 static int upload_colptr(wsmc_ctx* c) {
     if (!c->colptr_dirty) return WSMC_OK;
-    WSMC_HIP(hipStreamSynchronize(c->stream));   // the pinned table may still be in flight
+    WSMC_HIP(ctx_sync(c, c->stream));   // the pinned table may still be in flight
     double** host = reinterpret_cast<double**>(c->pinned);
     // pinned staging holds 512 pointers; larger tables go through a synchronous copy
     if (c->cols.size() <= 256) {
@@ -194,7 +221,7 @@ static int upload_colptr(wsmc_ctx* c) {
         for (size_t k = 0; k < c->cols.size(); ++k) tab[k] = c->cols[k].front;
         WSMC_HIP(hipMemcpyAsync(c->d_colptr, tab.data(), sizeof(double*) * tab.size(), hipMemcpyHostToDevice,
                                 c->stream));
-        WSMC_HIP(hipStreamSynchronize(c->stream));
+        WSMC_HIP(ctx_sync(c, c->stream));
     }
     c->colptr_dirty = false;
     return WSMC_OK;
@@ -206,7 +233,7 @@ static int upload_tape(wsmc_ctx* c) {
     if (n > c->d_tape_cap) {
         int64_t cap = c->d_tape_cap ? c->d_tape_cap : 64;
         while (cap < n) cap *= 2;
-        WSMC_HIP(hipStreamSynchronize(c->stream));
+        WSMC_HIP(ctx_sync(c, c->stream));
         if (c->d_tape) WSMC_HIP(hipFree(c->d_tape));
         WSMC_HIP(hipMalloc(&c->d_tape, sizeof(wsmc_term) * cap));
         c->d_tape_cap = cap;
@@ -214,7 +241,7 @@ static int upload_tape(wsmc_ctx* c) {
     }
     WSMC_HIP(hipMemcpyAsync(c->d_tape + c->d_tape_n, c->tape.data() + c->d_tape_n,
                             sizeof(wsmc_term) * (n - c->d_tape_n), hipMemcpyHostToDevice, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     c->d_tape_n = n;
     return WSMC_OK;
 }
@@ -596,7 +623,7 @@ int wsmc_create(wsmc_ctx** out, int64_t n_particles, int32_t device, uint64_t se
         always.resampled = 1;
         e = hipMemcpy(c->dec_always, &always, sizeof(Decision), hipMemcpyHostToDevice);
     }
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = ctx_sync(c, c->stream);
     {   // diagnostics / A-B: the reference's eager gather of every column at every resample
         const char* eg = getenv("WSMC_EAGER_GATHER");
         c->lazy = !(eg && atoi(eg) != 0);
@@ -655,7 +682,7 @@ int wsmc_destroy(wsmc_ctx* c) {
 // mirror of state.resampled / n_resamples / last_ess
 static int resolve_decisions(wsmc_ctx* c) {
     if (!c->dec_pending) return WSMC_OK;
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     for (int i = 0; i < c->dec_pending; ++i) {
         const Decision& d = c->dec_ring[i];
         c->last_ess = d.ess;
@@ -685,7 +712,7 @@ static int check_deferred(wsmc_ctx* c) {
     if (!c->move_pending) return WSMC_OK;
     int32_t* hf = reinterpret_cast<int32_t*>(c->pinned) + 1000;
     WSMC_HIP(hipMemcpyAsync(hf, c->dflag, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     c->move_pending = false;
     if (hf[0]) {
         scores_invalidate(c);
@@ -700,7 +727,7 @@ static int check_deferred(wsmc_ctx* c) {
 int wsmc_sync(wsmc_ctx* c) {
     if (c && c->multi) return multi_sync(c);
     CHECK_CTX(c);
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     if (int r = check_deferred(c)) return r;
     return WSMC_OK;
 }
@@ -861,7 +888,7 @@ int wsmc_col_download(wsmc_ctx* c, int32_t col, double* host) {
     if (int r = check_deferred(c)) return r;
     WSMC_HIP(hipMemcpyAsync(host, c->cols[col].front, sizeof(double) * c->cols[col].dim * c->N,
                             hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     return WSMC_OK;
 }
 
@@ -873,7 +900,7 @@ int wsmc_col_upload(wsmc_ctx* c, int32_t col, const double* host) {
     wrote_col(c, col);
     WSMC_HIP(hipMemcpyAsync(c->cols[col].front, host, sizeof(double) * c->cols[col].dim * c->N,
                             hipMemcpyHostToDevice, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     return WSMC_OK;
 }
 
@@ -905,7 +932,7 @@ int wsmc_store_resample(wsmc_ctx* c, const int32_t* idx) {
     row.known = 1;
     if ((r = store_resample_row(c, row, nullptr, nullptr))) return r;
     set_anc_last(c, &row, c->lazy ? c->epoch - 1 : -1);
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     return WSMC_OK;
 }
 
@@ -949,7 +976,7 @@ int wsmc_weights_upload(wsmc_ctx* c, const double* host) {
     if (!host) return fail(WSMC_EARG, "null buffer");
     c->wseq += 1;
     WSMC_HIP(hipMemcpyAsync(c->w, host, sizeof(double) * c->N, hipMemcpyHostToDevice, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     return WSMC_OK;
 }
 
@@ -959,7 +986,7 @@ int wsmc_weights_download(wsmc_ctx* c, double* host) {
     if (!host) return fail(WSMC_EARG, "null buffer");
     if (int r = check_deferred(c)) return r;
     WSMC_HIP(hipMemcpyAsync(host, c->w, sizeof(double) * c->N, hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     return WSMC_OK;
 }
 
@@ -1027,16 +1054,17 @@ static int exchange_words(wsmc_ctx* c, unsigned long long* buf, int64_t words, h
         std::vector<unsigned long long> h((size_t)words * c->world);
         WSMC_HIP(hipMemcpyAsync(h.data() + (size_t)c->rank * words, buf + (size_t)c->rank * words,
                                 sizeof(unsigned long long) * words, hipMemcpyDeviceToHost, s));
-        WSMC_HIP(hipStreamSynchronize(s));
+        WSMC_HIP(ctx_sync(c, s));
         const std::vector<unsigned long long> mine(h.begin() + (size_t)c->rank * words,
                                                    h.begin() + (size_t)(c->rank + 1) * words);
         if (c->host_exchange(c->host_user, reinterpret_cast<const uint64_t*>(mine.data()), (int32_t)words,
                              reinterpret_cast<uint64_t*>(h.data())) != 0)
             return fail(WSMC_ERCCL, "host exchange failed");
         WSMC_HIP(hipMemcpyAsync(buf, h.data(), sizeof(unsigned long long) * h.size(), hipMemcpyHostToDevice, s));
-        WSMC_HIP(hipStreamSynchronize(s));
+        WSMC_HIP(ctx_sync(c, s));
         return WSMC_OK;
     }
+    WSMC_RCCL_GUARD(c);
     WSMC_RCCL(ncclAllGather(buf + (size_t)c->rank * words, buf, (size_t)words, ncclUint64, c->comm, s));
     return WSMC_OK;
 }
@@ -1049,15 +1077,16 @@ static int exchange_recs(wsmc_ctx* c, ShardRecord* recs) {
     if (c->host_exchange) {
         std::vector<ShardRecord> h(c->world);
         WSMC_HIP(hipMemcpyAsync(&h[c->rank], recs + c->rank, sizeof(ShardRecord), hipMemcpyDeviceToHost, c->stream));
-        WSMC_HIP(hipStreamSynchronize(c->stream));
+        WSMC_HIP(ctx_sync(c, c->stream));
         const ShardRecord mine = h[c->rank];
         if (c->host_exchange(c->host_user, reinterpret_cast<const uint64_t*>(&mine), words,
                              reinterpret_cast<uint64_t*>(h.data())) != 0)
             return fail(WSMC_ERCCL, "host record exchange failed");
         WSMC_HIP(hipMemcpyAsync(recs, h.data(), sizeof(ShardRecord) * c->world, hipMemcpyHostToDevice, c->stream));
-        WSMC_HIP(hipStreamSynchronize(c->stream));
+        WSMC_HIP(ctx_sync(c, c->stream));
         return WSMC_OK;
     }
+    WSMC_RCCL_GUARD(c);
     WSMC_RCCL(ncclAllGather(recs + c->rank, recs, words, ncclUint64, c->comm, c->stream));
     return WSMC_OK;
 }
@@ -1072,7 +1101,7 @@ static int ensure_exact(wsmc_ctx* c) {
     if (!c->task_global) {
         // a shard may own up to all gN slots: sum_b floor((Q_b gN / Q + 3) / kRsChunk)
         // <= gN / kRsChunk + ntiles overflow tasks
-        WSMC_HIP(hipStreamSynchronize(c->stream));
+        WSMC_HIP(ctx_sync(c, c->stream));
         WSMC_HIP(hipFree(c->taskTile));
         WSMC_HIP(hipMalloc(&c->taskTile, sizeof(int32_t) * (size_t)(c->nrstiles + c->gN / kRsChunk + 1)));
         c->task_global = true;
@@ -1101,7 +1130,7 @@ static int exact_global_stats(wsmc_ctx* c, wsmc_shard_stats* st) {
     if (r) return r;
     std::vector<ShardRecord> h(c->world);
     WSMC_HIP(hipMemcpyAsync(h.data(), c->rec, sizeof(ShardRecord) * c->world, hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     *st = host_record_stats(h[0]);
     st->Q = 0; st->Q2 = 0; st->Wf2 = 0; st->Wf = 0; st->n = 0;
     for (int g = 0; g < c->world; ++g) {
@@ -1126,7 +1155,7 @@ static int exact_route(wsmc_ctx* c, const ExactPlan& x, const std::vector<const 
     const int nc = (int)src.size();
     const size_t need = 2 * (size_t)(nc > 0 ? nc : 1);
     if (c->d_comp_cap < need) {
-        WSMC_HIP(hipStreamSynchronize(c->stream));
+        WSMC_HIP(ctx_sync(c, c->stream));
         if (c->d_comp) WSMC_HIP(hipFree(c->d_comp));
         WSMC_HIP(hipMalloc(&c->d_comp, sizeof(double*) * need));
         c->d_comp_cap = need;
@@ -1137,7 +1166,7 @@ static int exact_route(wsmc_ctx* c, const ExactPlan& x, const std::vector<const 
         tab[nc + k] = dst[k];
     }
     WSMC_HIP(hipMemcpyAsync(c->d_comp, tab.data(), sizeof(double*) * need, hipMemcpyHostToDevice, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));   // `tab` is pageable and local
+    WSMC_HIP(ctx_sync(c, c->stream));   // `tab` is pageable and local
     // routing tables (every rank derives every rank's blocks from the same plan)
     const unsigned long long D = (unsigned long long)nc + 1;
     auto sendlen = [&](int g, int r) { return overlap(x.seg[g], x.seg[g + 1], x.gofs[r], x.gofs[r + 1]); };
@@ -1165,7 +1194,7 @@ static int exact_route(wsmc_ctx* c, const ExactPlan& x, const std::vector<const 
     }
     const size_t words = (size_t)(S + R) + 1;
     if (c->xbuf_cap < words) {
-        WSMC_HIP(hipStreamSynchronize(c->stream));
+        WSMC_HIP(ctx_sync(c, c->stream));
         if (c->xbuf) WSMC_HIP(hipFree(c->xbuf));
         WSMC_HIP(hipMalloc(&c->xbuf, sizeof(unsigned long long) * words));
         c->xbuf_cap = words;
@@ -1182,7 +1211,7 @@ static int exact_route(wsmc_ctx* c, const ExactPlan& x, const std::vector<const 
             std::vector<unsigned long long> mine(maxS, 0ull), all((size_t)maxS * W);
             if (S) WSMC_HIP(hipMemcpyAsync(mine.data(), sendbuf, sizeof(unsigned long long) * S, hipMemcpyDeviceToHost,
                                            c->stream));
-            WSMC_HIP(hipStreamSynchronize(c->stream));
+            WSMC_HIP(ctx_sync(c, c->stream));
             if (c->host_exchange(c->host_user, reinterpret_cast<const uint64_t*>(mine.data()), (int32_t)maxS,
                                  reinterpret_cast<uint64_t*>(all.data())) != 0)
                 return fail(WSMC_ERCCL, "host particle exchange failed");
@@ -1197,9 +1226,10 @@ static int exact_route(wsmc_ctx* c, const ExactPlan& x, const std::vector<const 
             }
             if (R) WSMC_HIP(hipMemcpyAsync(recvbuf, rv.data(), sizeof(unsigned long long) * R, hipMemcpyHostToDevice,
                                            c->stream));
-            WSMC_HIP(hipStreamSynchronize(c->stream));
+            WSMC_HIP(ctx_sync(c, c->stream));
         }
     } else {
+        WSMC_RCCL_GUARD(c);
         WSMC_RCCL(ncclGroupStart());
         for (int r = 0; r < W; ++r) {
             if (r == me) continue;
@@ -1254,7 +1284,7 @@ static int exact_decide_fill(wsmc_ctx* c, double ess_min, int32_t scheme, uint64
     static_assert(sizeof(Host) <= 4096, "pinned staging");
     WSMC_HIP(hipMemcpyAsync(&h->d, dec_dev, sizeof(Decision), hipMemcpyDeviceToHost, c->stream));
     WSMC_HIP(hipMemcpyAsync(&h->x, c->xp, sizeof(ExactPlan), hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     *hd = h->d;
     *hx = h->x;
     return WSMC_OK;
@@ -1283,7 +1313,7 @@ static int trace_level(wsmc_ctx* c, const ExactPlan& x, const double* hist, cons
     int32_t* h2 = reinterpret_cast<int32_t*>(c->pinned);
     WSMC_HIP(hipMemcpyAsync(h2, a, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     WSMC_HIP(hipMemcpyAsync(h2 + 1, a + n - 1, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     std::vector<unsigned long long> rng(2 * (size_t)W);
     {
         unsigned long long* mine = reinterpret_cast<unsigned long long*>(c->pinned) + 64;   // pinned staging
@@ -1295,7 +1325,7 @@ static int trace_level(wsmc_ctx* c, const ExactPlan& x, const double* hist, cons
         if (r) return r;
         WSMC_HIP(hipMemcpyAsync(rng.data(), c->xchg, sizeof(unsigned long long) * 2 * W, hipMemcpyDeviceToHost,
                                 c->stream));
-        WSMC_HIP(hipStreamSynchronize(c->stream));
+        WSMC_HIP(ctx_sync(c, c->stream));
     }
     auto part = [&](int owner, int req) {   // [start, end) global of owner's rows requester needs
         const unsigned long long lo = rng[2 * req] > x.gofs[owner] ? rng[2 * req] : x.gofs[owner];
@@ -1314,7 +1344,7 @@ static int trace_level(wsmc_ctx* c, const ExactPlan& x, const double* hist, cons
     }
     const size_t words = (size_t)(S + R) + 1;
     if (c->xbuf_cap < words) {
-        WSMC_HIP(hipStreamSynchronize(c->stream));
+        WSMC_HIP(ctx_sync(c, c->stream));
         if (c->xbuf) WSMC_HIP(hipFree(c->xbuf));
         WSMC_HIP(hipMalloc(&c->xbuf, sizeof(unsigned long long) * words));
         c->xbuf_cap = words;
@@ -1337,7 +1367,7 @@ static int trace_level(wsmc_ctx* c, const ExactPlan& x, const double* hist, cons
             std::vector<unsigned long long> mine(maxS, 0ull), all((size_t)maxS * W);
             if (S) WSMC_HIP(hipMemcpyAsync(mine.data(), sendbuf, sizeof(unsigned long long) * S, hipMemcpyDeviceToHost,
                                            c->stream));
-            WSMC_HIP(hipStreamSynchronize(c->stream));
+            WSMC_HIP(ctx_sync(c, c->stream));
             if (c->host_exchange(c->host_user, reinterpret_cast<const uint64_t*>(mine.data()), (int32_t)maxS,
                                  reinterpret_cast<uint64_t*>(all.data())) != 0)
                 return fail(WSMC_ERCCL, "host trace-back exchange failed");
@@ -1352,9 +1382,10 @@ static int trace_level(wsmc_ctx* c, const ExactPlan& x, const double* hist, cons
                                         sizeof(unsigned long long) * (pr.second - pr.first) * 3, hipMemcpyHostToDevice,
                                         c->stream));
             }
-            WSMC_HIP(hipStreamSynchronize(c->stream));
+            WSMC_HIP(ctx_sync(c, c->stream));
         }
     } else {
+        WSMC_RCCL_GUARD(c);
         WSMC_RCCL(ncclGroupStart());
         for (int r = 0; r < W; ++r) {
             if (r == me) continue;
@@ -1382,7 +1413,7 @@ static int allgather_host_words(wsmc_ctx* c, const unsigned long long* mine, int
     if (r) return r;
     WSMC_HIP(hipMemcpyAsync(all, dbuf, sizeof(unsigned long long) * words * c->world, hipMemcpyDeviceToHost,
                             c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     return WSMC_OK;
 }
 // the population's max log-weight into c->mslots (slot 0; the others zero), so that every
@@ -1392,7 +1423,7 @@ static int adopt_global_max(wsmc_ctx* c) {
     WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, c->mslots));
     MaxSlots hs;
     WSMC_HIP(hipMemcpyAsync(&hs, c->mslots, sizeof(MaxSlots), hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     unsigned long long menc = 0;
     for (int k = 0; k < kSlots; ++k) menc = hs.v[k][0] > menc ? hs.v[k][0] : menc;
     std::vector<unsigned long long> ex(c->world);
@@ -1442,7 +1473,7 @@ int wsmc_weighted_moments(wsmc_ctx* c, const wsmc_operand* exprs, int32_t d, dou
         WSMC_HIP(launch_moments_expr(c->stream, c->w, c->mslots, c->d_colptr, ex, d, 1, c->mom, c->N, c->tilepart));
         WSMC_HIP(launch_moments_final(c->stream, c->tilepart, c->ntiles, d, 1, 0.0, c->mom, c->dflag, 2));
         WSMC_HIP(hipMemcpyAsync(mom, c->mom, sizeof(mom), hipMemcpyDeviceToHost, c->stream));
-        WSMC_HIP(hipStreamSynchronize(c->stream));
+        WSMC_HIP(ctx_sync(c, c->stream));
         if ((r = allgather_host_words(c, reinterpret_cast<const unsigned long long*>(mom + 48), n1, all.data())))
             return r;
         double t1[5];
@@ -1455,7 +1486,7 @@ int wsmc_weighted_moments(wsmc_ctx* c, const wsmc_operand* exprs, int32_t d, dou
         WSMC_HIP(launch_moments_expr(c->stream, c->w, c->mslots, c->d_colptr, ex, d, 2, c->mom, c->N, c->tilepart));
         WSMC_HIP(launch_moments_final(c->stream, c->tilepart, c->ntiles, d, 2, 0.0, c->mom, c->dflag, 2));
         WSMC_HIP(hipMemcpyAsync(mom + 48, c->mom + 48, sizeof(double) * 16, hipMemcpyDeviceToHost, c->stream));
-        WSMC_HIP(hipStreamSynchronize(c->stream));
+        WSMC_HIP(ctx_sync(c, c->stream));
         if ((r = allgather_host_words(c, reinterpret_cast<const unsigned long long*>(mom + 48), n2, all.data())))
             return r;
         double t2[10];
@@ -1479,7 +1510,7 @@ int wsmc_weighted_moments(wsmc_ctx* c, const wsmc_operand* exprs, int32_t d, dou
     }
     double h[32];
     WSMC_HIP(hipMemcpyAsync(h, c->mom, sizeof(double) * 32, hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     for (int k = 0; k < d; ++k) mean[k] = h[k];
     if (cov)
         for (int k = 0; k < d * d; ++k) cov[k] = h[16 + k];
@@ -1497,7 +1528,7 @@ int wsmc_col_minmax(wsmc_ctx* c, int32_t col, int32_t comp, double* mn, double* 
     WSMC_HIP(launch_minmax(c->stream, c->cols[col].front + (int64_t)comp * c->N, c->N, c->mslots));
     MaxSlots h;
     WSMC_HIP(hipMemcpyAsync(&h, c->mslots, sizeof(MaxSlots), hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     unsigned long long a = 0, b = 0;
     for (int k = 0; k < kSlots; ++k) {
         a = h.v[k][0] > a ? h.v[k][0] : a;
@@ -1526,7 +1557,7 @@ static int local_q(wsmc_ctx* c, unsigned long long* Q) {
     WSMC_HIP(launch_rs_reduce(c->stream, c->mslots, c->tilep, c->N, c->tileOff, c->rec, 0, 0.0, nullptr, nullptr));
     ShardRecord* hr = reinterpret_cast<ShardRecord*>(c->pinned);
     WSMC_HIP(hipMemcpyAsync(hr, c->rec, sizeof(ShardRecord), hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     *Q = hr->Q;
     return WSMC_OK;
 }
@@ -1557,7 +1588,7 @@ static int median_of(wsmc_ctx* c, const double* x, const unsigned long long* q, 
     if (e == hipSuccess) e = hipcub::DeviceScan::InclusiveSum(ts, t, vin, kout, (int)n, c->stream);
     if (e == hipSuccess) e = launch_median_pick(c->stream, kin, vin, kout, n, dout);
     if (e == hipSuccess) e = hipMemcpyAsync(out, dout, sizeof(double), hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = ctx_sync(c, c->stream);
     if (ts) (void)hipFree(ts);
     if (dout) (void)hipFree(dout);
     (void)hipFree(buf);
@@ -1589,7 +1620,7 @@ int wsmc_weighted_median(wsmc_ctx* c, int32_t col, int32_t comp, double* out) {
     WSMC_HIP(launch_rs_reduce(c->stream, c->mslots, c->tilep, c->N, c->tileOff, c->rec, 0, 0.0, nullptr, nullptr));
     ShardRecord* hr = reinterpret_cast<ShardRecord*>(c->pinned);
     WSMC_HIP(hipMemcpyAsync(hr, c->rec, sizeof(ShardRecord), hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     const u64 mine[2] = {(u64)c->N, hr->Q};
     std::vector<u64> all(2 * c->world);
     if ((r = allgather_host_words(c, mine, 2, all.data()))) return r;
@@ -1642,7 +1673,7 @@ int wsmc_histogram(wsmc_ctx* c, int32_t col, int32_t comp, int32_t levels[8]) {
                                   nullptr));
         ShardRecord* hr = reinterpret_cast<ShardRecord*>(c->pinned);
         WSMC_HIP(hipMemcpyAsync(hr, c->rec, sizeof(ShardRecord), hipMemcpyDeviceToHost, c->stream));
-        WSMC_HIP(hipStreamSynchronize(c->stream));
+        WSMC_HIP(ctx_sync(c, c->stream));
         const unsigned long long mine = hr->Q;
         std::vector<unsigned long long> all(c->world);
         if ((r = allgather_host_words(c, &mine, 1, all.data()))) return r;
@@ -1658,7 +1689,7 @@ int wsmc_histogram(wsmc_ctx* c, int32_t col, int32_t comp, int32_t levels[8]) {
     WSMC_HIP(launch_hist(c->stream, c->cols[col].front + (int64_t)comp * c->N, c->qbuf, c->N, edges, cnt));
     unsigned long long h[8];
     WSMC_HIP(hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     if (sh) {   // integer bin sums: order-free
         std::vector<unsigned long long> all(8 * c->world);
         if ((r = allgather_host_words(c, h, 8, all.data()))) return r;
@@ -1691,7 +1722,7 @@ int wsmc_ess(wsmc_ctx* c, double* ess_perc) {
     if (r) return r;
     std::vector<ShardRecord> h(c->world);
     WSMC_HIP(hipMemcpyAsync(h.data(), c->rec, sizeof(ShardRecord) * c->world, hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     wsmc_shard_stats st[kMaxWorld];
     for (int g = 0; g < c->world; ++g) st[g] = host_record_stats(h[g]);
     *ess_perc = wsmc_global_ess(st, c->world);
@@ -1715,7 +1746,7 @@ static int sample_particles_sharded(wsmc_ctx* c, int64_t n, int32_t replace, int
     WSMC_HIP(launch_rs_reduce(c->stream, c->mslots, c->tilep, c->N, c->tileOff, c->rec, 0, 0.0, nullptr, nullptr));
     ShardRecord* hr = reinterpret_cast<ShardRecord*>(c->pinned);
     WSMC_HIP(hipMemcpyAsync(hr, c->rec, sizeof(ShardRecord), hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     const u64 mine = hr->Q, mine2[2] = {hr->Q, (u64)c->N};
     std::vector<u64> qs(2 * W);
     if ((r = allgather_host_words(c, mine2, 2, qs.data()))) return r;
@@ -1756,7 +1787,7 @@ static int sample_particles_sharded(wsmc_ctx* c, int64_t n, int32_t replace, int
         if ((r = exchange_words(c, reinterpret_cast<u64*>(all), n, c->stream))) return done(r);
         std::vector<int64_t> h((size_t)n * W);
         SP_HIP(hipMemcpyAsync(h.data(), all, sizeof(int64_t) * h.size(), hipMemcpyDeviceToHost, c->stream));
-        SP_HIP(hipStreamSynchronize(c->stream));
+        SP_HIP(ctx_sync(c, c->stream));
         for (int64_t j = 0; j < n; ++j) {   // exactly one rank owns each draw
             int64_t v = 0;
             for (int g = 0; g < W; ++g) v = h[(size_t)g * n + j] ? h[(size_t)g * n + j] : v;
@@ -1801,7 +1832,7 @@ static int sample_particles_sharded(wsmc_ctx* c, int64_t n, int32_t replace, int
     t = tmax;
     SP_HIP(hipcub::DeviceRadixSort::SortPairsDescending(ts, t, k1, k2, i1, i2, (int)U, 0, 64, c->stream));
     SP_HIP(hipMemcpyAsync(idx_out, i2, sizeof(int64_t) * n, hipMemcpyDeviceToHost, c->stream));
-    SP_HIP(hipStreamSynchronize(c->stream));
+    SP_HIP(ctx_sync(c, c->stream));
 #undef SP_HIP
     return done(WSMC_OK);
 }
@@ -1828,14 +1859,14 @@ int wsmc_sample_particles(wsmc_ctx* c, int64_t n, int32_t replace, int64_t* idx_
     WSMC_HIP(launch_rs_reduce(c->stream, c->mslots, c->tilep, c->N, c->tileOff, c->rec, 0, 0.0, nullptr, nullptr));
     ShardRecord* hr = reinterpret_cast<ShardRecord*>(c->pinned);
     WSMC_HIP(hipMemcpyAsync(hr, c->rec, sizeof(ShardRecord), hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     if (hr->Q == 0) return fail(WSMC_ESTATE, "the weights do not normalise (all -Inf or NaN)");
     if (replace) {
         int64_t* d = nullptr;
         WSMC_HIP(hipMalloc(&d, sizeof(int64_t) * (size_t)n));
         hipError_t e = launch_sample_draws(c->stream, n, c->N, c->rec, c->tileOff, c->cdf, c->seed, op, d);
         if (e == hipSuccess) e = hipMemcpyAsync(idx_out, d, sizeof(int64_t) * n, hipMemcpyDeviceToHost, c->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e == hipSuccess) e = ctx_sync(c, c->stream);
         (void)hipFree(d);
         if (e != hipSuccess) return fail(WSMC_EHIP, std::string("sample: ") + hipGetErrorString(e));
         return WSMC_OK;
@@ -1855,7 +1886,7 @@ int wsmc_sample_particles(wsmc_ctx* c, int64_t n, int32_t replace, int64_t* idx_
                                                                 c->stream);
     if (e == hipSuccess)
         e = hipMemcpyAsync(idx_out, vout, sizeof(int64_t) * n, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = ctx_sync(c, c->stream);
     (void)hipFree(tstore);
     if (e != hipSuccess) return fail(WSMC_EHIP, std::string("sample: ") + hipGetErrorString(e));
     return WSMC_OK;
@@ -1877,7 +1908,7 @@ int wsmc_col_gather_rows(wsmc_ctx* c, int32_t col, const int64_t* idx, int64_t n
     if (e == hipSuccess) e = hipMemcpyAsync(d, idx, sizeof(int64_t) * n, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = launch_gather_rows(c->stream, c->cols[col].front, c->N, dim, d, n, o);
     if (e == hipSuccess) e = hipMemcpyAsync(out, o, sizeof(double) * n * dim, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = ctx_sync(c, c->stream);
     (void)hipFree(d);
     if (o) (void)hipFree(o);
     if (e != hipSuccess) return fail(WSMC_EHIP, std::string("gather rows: ") + hipGetErrorString(e));
@@ -1902,7 +1933,7 @@ int wsmc_log_evidence(wsmc_ctx* c, double* out) {
     if (r) return r;
     std::vector<ShardRecord> h(c->world);
     WSMC_HIP(hipMemcpyAsync(h.data(), c->rec, sizeof(ShardRecord) * c->world, hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     wsmc_shard_stats st[kMaxWorld];
     for (int g = 0; g < c->world; ++g) st[g] = host_record_stats(h[g]);
     *out = wsmc_global_log_evidence(st, c->world);
@@ -2315,7 +2346,7 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
         }
         return WSMC_OK;
     }
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     const Decision d = *hd;
     c->last_ess = d.ess;
     if (d.resampled) {
@@ -2346,7 +2377,7 @@ int wsmc_last_ancestors(wsmc_ctx* c, int32_t* host) {
     if (int r = resolve_decisions(c)) return r;   // which pending Resample resampled last
     const int32_t* src = c->anc_last ? c->anc_last : c->anc;
     WSMC_HIP(hipMemcpyAsync(host, src, sizeof(int32_t) * c->N, hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     return WSMC_OK;
 }
 
@@ -2362,7 +2393,7 @@ int wsmc_score(wsmc_ctx* c, int32_t depth, double* host) {
     if (r) return r;
     WSMC_HIP(launch_score(c->stream, c->d_tape, (int32_t)c->tape.size(), depth, c->d_colptr, c->N, c->tmp));
     WSMC_HIP(hipMemcpyAsync(host, c->tmp, sizeof(double) * c->N, hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     return WSMC_OK;
 }
 
@@ -2406,7 +2437,7 @@ static int global_unique(wsmc_ctx* c, const unsigned long long* sorted, unsigned
     if (r) return done(r);
     std::vector<u64> hc(W);
     GU_HIP(hipMemcpyAsync(hc.data(), cnt, sizeof(u64) * W, hipMemcpyDeviceToHost, c->stream));
-    GU_HIP(hipStreamSynchronize(c->stream));
+    GU_HIP(ctx_sync(c, c->stream));
     u64 M = 1, tot = 0;
     for (int g = 0; g < W; ++g) {
         M = hc[g] > M ? hc[g] : M;
@@ -2432,7 +2463,7 @@ static int global_unique(wsmc_ctx* c, const unsigned long long* sorted, unsigned
     GU_HIP(hipMemsetAsync(nsel, 0, sizeof(u64), c->stream));
     GU_HIP(launch_count_unique(c->stream, alls, (int64_t)tot, nsel));
     GU_HIP(hipMemcpyAsync(u_out, nsel, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
-    GU_HIP(hipStreamSynchronize(c->stream));
+    GU_HIP(ctx_sync(c, c->stream));
     return done(WSMC_OK);
 #undef GU_HIP
 }
@@ -2475,7 +2506,7 @@ int wsmc_marginal_diversity(wsmc_ctx* c, const int32_t* targets, int32_t d, doub
             if (e == hipSuccess) e = launch_count_unique(c->stream, kout, c->N, c->ucount);
             if (e == hipSuccess)
                 e = hipMemcpyAsync(&u, c->ucount, sizeof(u), hipMemcpyDeviceToHost, c->stream);
-            if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+            if (e == hipSuccess) e = ctx_sync(c, c->stream);
             if (e != hipSuccess) {
                 (void)hipFree(tstore);
                 return fail(WSMC_EHIP, std::string("marginal_diversity: ") + hipGetErrorString(e));
@@ -2680,7 +2711,7 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         WSMC_HIP(launch_autorw_final(c->stream, c->tilepart, c->ntiles, d, step, c->mom, c->dflag, 0, gate));
         c->dflag_zero = false;
     } else {
-        WSMC_HIP(hipStreamSynchronize(c->stream));
+        WSMC_HIP(ctx_sync(c, c->stream));
         double* L = reinterpret_cast<double*>(c->pinned);
         for (int k = 0; k < 16; ++k) L[k] = 0.0;
         for (int k = 0; k < d; ++k) L[k * d + k] = step;
@@ -2762,14 +2793,14 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
             if ((int64_t)prog_bytes > c->d_prog_cap) {
                 int64_t cap = c->d_prog_cap ? c->d_prog_cap : 4096;
                 while (cap < (int64_t)prog_bytes) cap *= 2;
-                WSMC_HIP(hipStreamSynchronize(c->stream));
+                WSMC_HIP(ctx_sync(c, c->stream));
                 if (c->d_prog) WSMC_HIP(hipFree(c->d_prog));
                 WSMC_HIP(hipMalloc(&c->d_prog, cap));
                 c->d_prog_cap = cap;
             }
             const int64_t need = ((int64_t)prog_bytes + 255) & ~(int64_t)255;
             if (c->prog_stage_at + need > c->prog_stage_cap) {   // wrap: the ring's copies are done
-                WSMC_HIP(hipStreamSynchronize(c->stream));
+                WSMC_HIP(ctx_sync(c, c->stream));
                 c->prog_stage_at = 0;
                 if (need > c->prog_stage_cap) {
                     if (c->prog_stage) WSMC_HIP(hipHostFree(c->prog_stage));
@@ -2842,7 +2873,7 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
     }* hb = reinterpret_cast<decltype(hb)>(c->pinned);
     WSMC_HIP(hipMemcpyAsync(hb->flag, c->dflag, sizeof(int32_t) * 4, hipMemcpyDeviceToHost, c->stream));
     WSMC_HIP(hipMemcpyAsync(hb->acc, c->ucount, sizeof(unsigned long long) * 4, hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     if (hb->flag[0]) return fail(WSMC_ENOTPD, "autoRW proposal covariance is not positive definite");
     c->dflag_zero = true;
     c->scache_terms = kD;
@@ -3089,14 +3120,14 @@ int wsmc_move_block(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, int32_t
         if ((int64_t)prog_bytes > c->d_prog_cap) {
             int64_t cap = c->d_prog_cap ? c->d_prog_cap : 4096;
             while (cap < (int64_t)prog_bytes) cap *= 2;
-            WSMC_HIP(hipStreamSynchronize(c->stream));
+            WSMC_HIP(ctx_sync(c, c->stream));
             if (c->d_prog) WSMC_HIP(hipFree(c->d_prog));
             WSMC_HIP(hipMalloc(&c->d_prog, cap));
             c->d_prog_cap = cap;
         }
         const int64_t need = ((int64_t)prog_bytes + 255) & ~(int64_t)255;
         if (c->prog_stage_at + need > c->prog_stage_cap) {
-            WSMC_HIP(hipStreamSynchronize(c->stream));
+            WSMC_HIP(ctx_sync(c, c->stream));
             c->prog_stage_at = 0;
             if (need > c->prog_stage_cap) {
                 if (c->prog_stage) WSMC_HIP(hipHostFree(c->prog_stage));
@@ -3164,7 +3195,7 @@ int wsmc_move_block(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, int32_t
     }* hb = reinterpret_cast<decltype(hb)>(c->pinned);
     WSMC_HIP(hipMemcpyAsync(hb->flag, c->dflag, sizeof(int32_t) * 4, hipMemcpyDeviceToHost, c->stream));
     WSMC_HIP(hipMemcpyAsync(hb->acc, c->ucount, sizeof(unsigned long long) * 4, hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     for (int32_t m = 0; m < n; ++m) accepted_out[m] = (int64_t)hb->acc[m];
     if (hb->flag[0]) return fail(WSMC_ENOTPD, "autoRW proposal covariance is not positive definite");
     c->dflag_zero = true;   // (flag[2] is rewritten by every block's combine before it is read)
@@ -3185,7 +3216,7 @@ static inline size_t run_grp_bytes(int64_t N, int32_t T) {
 
 static int ensure_run_buffers(wsmc_ctx* c, int32_t T) {
     if (c->T_alloc >= T && c->run_rec) return WSMC_OK;
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     void* old[] = {c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp};
     for (void* p : old)
         if (p) WSMC_HIP(hipFree(p));
@@ -3351,7 +3382,7 @@ static int exchange_neighbors(wsmc_ctx* c, unsigned long long* const send[2], un
             WSMC_HIP(hipMemcpyAsync(mine.data(), send[0] + at, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost, s));
             WSMC_HIP(hipMemcpyAsync(mine.data() + n, send[1] + at, sizeof(unsigned long long) * n,
                                     hipMemcpyDeviceToHost, s));
-            WSMC_HIP(hipStreamSynchronize(s));
+            WSMC_HIP(ctx_sync(c, s));
             if (c->host_exchange(c->host_user, reinterpret_cast<const uint64_t*>(mine.data()), (int32_t)(2 * n),
                                  reinterpret_cast<uint64_t*>(all.data())) != 0)
                 return fail(WSMC_ERCCL, "host neighbour exchange failed");
@@ -3361,10 +3392,11 @@ static int exchange_neighbors(wsmc_ctx* c, unsigned long long* const send[2], un
             if (me + 1 < W)   // the right rank's left block
                 WSMC_HIP(hipMemcpyAsync(recv[1] + at, all.data() + (size_t)(me + 1) * 2 * n,
                                         sizeof(unsigned long long) * n, hipMemcpyHostToDevice, s));
-            WSMC_HIP(hipStreamSynchronize(s));
+            WSMC_HIP(ctx_sync(c, s));
         }
         return WSMC_OK;
     }
+    WSMC_RCCL_GUARD(c);
     WSMC_RCCL(ncclGroupStart());
     if (me > 0) {
         WSMC_RCCL(ncclSend(send[0], (size_t)words, ncclUint64, me - 1, c->comm, s));
@@ -3415,7 +3447,7 @@ static int ensure_exact_async(wsmc_ctx* c, int32_t T, int64_t cap, int64_t ctr) 
                       msn > c->xms_n || lwords > c->xlines_words;
     c->xanc_stride = astride;
     if (!grow && c->xstat && c->w_save) return WSMC_OK;
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     if (!c->xpairs) WSMC_HIP(hipMalloc(&c->xpairs, sizeof(double) * 6 * (size_t)N));
     if (!c->xstat) WSMC_HIP(hipMalloc(&c->xstat, sizeof(unsigned long long) * kMaxShards * kXStat));
     if (!c->w_save) WSMC_HIP(hipMalloc(&c->w_save, sizeof(double) * (size_t)N));
@@ -3785,7 +3817,7 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
     }
     if ((r = ensure_run_buffers(c, T))) return r;
     // per-run values: obs, op base
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     const uint64_t op_base = c->op;
     std::vector<double> hobs(obs, obs + 2 * (size_t)T);
     WSMC_HIP(hipMemcpyAsync(c->obs, hobs.data(), sizeof(double) * 2 * T, hipMemcpyHostToDevice, c->stream));
@@ -3828,7 +3860,7 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         WSMC_HIP(hipMemcpyAsync(tabs, hw.data(), sizeof(double*) * (T + 2), hipMemcpyHostToDevice, c->stream));
         WSMC_HIP(hipMemcpyAsync(tabs + (T + 2), ho.data(), sizeof(double*) * (T + 2), hipMemcpyHostToDevice,
                                 c->stream));
-        WSMC_HIP(hipStreamSynchronize(c->stream));
+        WSMC_HIP(ctx_sync(c, c->stream));
         *work = tabs;
         *outp = tabs + (T + 2);
         return WSMC_OK;
@@ -3925,7 +3957,7 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         std::vector<unsigned long long> st((size_t)kMaxShards * kXStat);
         WSMC_HIP(hipMemcpyAsync(st.data(), c->xstat, sizeof(unsigned long long) * st.size(), hipMemcpyDeviceToHost,
                                 c->stream));
-        WSMC_HIP(hipStreamSynchronize(c->stream));
+        WSMC_HIP(ctx_sync(c, c->stream));
         unsigned long long bits = 0, need = 0, exc = 0;
         for (int g = 0; g < c->world; ++g) {
             bits |= st[(size_t)g * kXStat];
@@ -3954,7 +3986,7 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
     }
     std::vector<Decision> hdec(T + 1);
     WSMC_HIP(hipMemcpyAsync(hdec.data(), c->run_dec, sizeof(Decision) * (T + 1), hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipStreamSynchronize(c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
     if (temp_tables) (void)hipFree(temp_tables);
     // wsmc_last_ancestors reports the run's last resample, as after the statement sequence
     for (int t = T; t >= 1; --t)

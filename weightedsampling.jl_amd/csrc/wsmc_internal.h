@@ -6,6 +6,7 @@
 
 #include <cstdint>
 #include <deque>
+#include <atomic>
 #include <functional>
 #include <string>
 #include <vector>
@@ -140,6 +141,12 @@ struct wsmc_ctx {
     int world = 1, rank = 0;
     int64_t goff = 0, gN = 0;
     ncclComm_t comm = nullptr;
+    // a shard of a multi-device handle (wsmc_multi.hip): the handle's abort request. Only the
+    // shard's own thread touches its communicator: before every collective and while it waits
+    // for its stream it checks the request and, when set, aborts its own communicator (a
+    // collective missing a failed peer would never complete) and leaves with `released` set
+    const std::atomic<bool>* peer_abort = nullptr;
+    bool released = false;
     wsmc_exchange_fn host_exchange = nullptr;   // host-side record exchange (instead of RCCL)
     int32_t inject_fail = 0;                    // wsmc_debug_inject_failure: fail the nth next record exchange
     unsigned long long* run_grp = nullptr;      // [T+1][ngroups][kGroupLine] fused-run group sums
@@ -292,6 +299,13 @@ int fail(int code, const std::string& msg);
             return ::wsmc::fail(WSMC_EHIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
     } while (0)
 
+// a multi-device handle asked its shards to abort (a peer failed): this shard's communicator
+// is aborted by its own thread, the call leaves with WSMC_ERCCL (released)
+bool peer_aborted(wsmc_ctx* c);
+// hipStreamSynchronize that a peer's abort request interrupts (multi-device shards poll)
+hipError_t ctx_sync(wsmc_ctx* c, hipStream_t s);
+#define WSMC_RCCL_GUARD(ctx)                                                             \
+    if (::wsmc::peer_aborted(ctx)) return ::wsmc::fail(WSMC_ERCCL, "communicator aborted: a peer shard failed")
 #define WSMC_RCCL(expr)                                                                  \
     do {                                                                                 \
         ncclResult_t _r = (expr);                                                        \

@@ -1732,19 +1732,67 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
 // each entry from the newest back (a = anc[a] where that Resample resampled) the columns
 // whose values predate the entries applied so far read src[a]. Rows are monotone
 // (stratified / systematic / sorted multinomial), so the gathers stay nearly coalesced.
+// The walk is a chain of dependent loads (the entry of each row at the lineage so far), so
+// its speed is the number of chains in flight: P = 2 particles a thread (two chains, 16-B
+// stores of the outputs; N even, 16-B aligned outputs) keeps a 1M population resident in one
+// round of waves, and each level's entry is loaded before that level's column gathers (every
+// row exists; the entry is used only if its Resample resampled), so a level costs one memory
+// latency, not two.
+template <int P>
 __global__ __launch_bounds__(kBlock) void k_lazy_trace(TraceArgs t, int64_t N) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= N) return;
-    if (i == 0)   // the columns' new fronts into the device pointer table
+    const int64_t i0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * P;
+    // every level's decision up front, one per lane, before any lane leaves (ballots: a
+    // decision read inside the walk is a vector load the next level waits for, together with
+    // every store in flight)
+    const TraceArgs* T = (const TraceArgs*)(const char*)__builtin_amdgcn_kernarg_segment_ptr();
+    const int lane = threadIdx.x & 63;
+    static_assert(kTraceLev <= 128, "two decision words");
+    const u64 rs0 = __ballot(lane < t.nlev && T->decs[lane]->resampled);
+    const u64 rs1 = __ballot(lane + 64 < t.nlev && T->decs[lane + 64]->resampled);
+    if (i0 >= N) return;
+    if (i0 == 0)   // the columns' new fronts into the device pointer table
         for (int c = 0; c < t.ncomp; ++c)
             if (t.comp[c].col >= 0) t.tab[t.comp[c].col] = t.comp[c].dst;
-    int64_t a = t.a_in ? t.a_in[i] : i;
+    int64_t a[P];
+    if (t.a_in) {
+        if constexpr (P == 2) {
+            const int2 v = *reinterpret_cast<const int2*>(t.a_in + i0);
+            a[0] = v.x;
+            a[1] = v.y;
+        } else {
+            a[0] = t.a_in[i0];
+        }
+    } else {
+#pragma unroll
+        for (int p = 0; p < P; ++p) a[p] = i0 + p;
+    }
+    int32_t nx[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) nx[p] = t.nlev > 0 ? t.rows[0][a[p]] : 0;
     int k = 0;
     for (int lev = 0; lev < t.nlev; ++lev) {
-        if (t.decs[lev]->resampled) a = t.rows[lev][a];
-        for (; k < t.ncomp && t.comp[k].level == lev + 1; ++k) t.comp[k].dst[i] = t.comp[k].src[a];
+        if (((lev < 64 ? rs0 : rs1) >> (lev & 63)) & 1)
+#pragma unroll
+            for (int p = 0; p < P; ++p) a[p] = nx[p];
+        if (lev + 1 < t.nlev)
+#pragma unroll
+            for (int p = 0; p < P; ++p) nx[p] = t.rows[lev + 1][a[p]];
+        for (; k < t.ncomp && t.comp[k].level == lev + 1; ++k) {
+            const double* src = t.comp[k].src;
+            if constexpr (P == 2) {
+                *reinterpret_cast<d2*>(t.comp[k].dst + i0) = d2{src[a[0]], src[a[1]]};
+            } else {
+                t.comp[k].dst[i0] = src[a[0]];
+            }
+        }
     }
-    if (t.a_out) t.a_out[i] = (int32_t)a;
+    if (t.a_out) {
+        if constexpr (P == 2) {
+            *reinterpret_cast<int2*>(t.a_out + i0) = int2{(int)a[0], (int)a[1]};
+        } else {
+            t.a_out[i0] = (int32_t)a[0];
+        }
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_gather(double* __restrict__ dst, const double* __restrict__ src,
@@ -2909,10 +2957,22 @@ __global__ __launch_bounds__(kBlock) void k_iota(int32_t* __restrict__ a, int64_
 // ColumnStore's per-resample gather of every column would have produced (src/stores.jl:105-128)
 // ISL: island shards decide the last step here, from its records (the single-GPU instance
 // reads the decision: no barrier or decide code ahead of the trace)
-template <bool ISL>
+// P = 2: two particles a thread (N even): two lineage chains in flight per thread, so a 1M
+// population is resident in one round of waves, and every SoA output is a 16-B store.
+// The walk is software-pipelined so that a step waits for one memory latency, its ancestor
+// entry, and nothing else: the step's decision and its history pointers come from LDS (staged
+// 64 steps at a time), and the x gathered at a step is stored one step later, after the next
+// step's loads are issued (stores count in vmcnt: storing at once would make the next step's
+// wait for its ancestor entry also wait for the store acknowledgements).
+constexpr int kFinChunk = 64;   // steps whose decisions and history pointers are staged at a time
+// a pointer read back from LDS is a generic (flat) pointer, and flat accesses count in both
+// vmcnt and lgkmcnt (every LDS wait then also waits for them): cast to the global address space
+typedef const double __attribute__((address_space(1)))* gcdp;
+typedef double __attribute__((address_space(1)))* gdp;
+template <bool ISL, int P>
 __global__ __launch_bounds__(kBlock) void k_ssm2d_final(Ssm2dFinal f) {
     const int64_t N = f.N;
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t i0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * P;
     const int T = f.T;
     bool rsT;
     double meanT;
@@ -2931,41 +2991,105 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_final(Ssm2dFinal f) {
         rsT = f.dec[T].resampled;
         meanT = f.dec[T].mean;
     }
-    if (i >= N) return;
+    // lanes past N take the last particles' walk and store the same bits again: every lane
+    // stays in the block's barriers and every step has the same memory operations
+    const int64_t ib = i0 < N ? i0 : N - P;
     const int64_t S = f.anc_stride;
-    int64_t a = i;
-    if (rsT) a = f.anc_log[(int64_t)(T - 1) * S + i];
+    // component pairs of P particles: (x.x of each, x.y of each) -> SoA dst[ib..], dst[N + ib..]
+    auto put = [&](double* dst0, const d2 (&x)[P]) {
+        gdp dst = (gdp)dst0;
+        if constexpr (P >= 2) {
+#pragma unroll
+            for (int p = 0; p < P; p += 2) {
+                *reinterpret_cast<__attribute__((address_space(1))) d2*>(dst + ib + p) = d2{x[p].x, x[p + 1].x};
+                *reinterpret_cast<__attribute__((address_space(1))) d2*>(dst + N + ib + p) = d2{x[p].y, x[p + 1].y};
+            }
+        } else {
+            dst[ib] = x[0].x;
+            dst[N + ib] = x[0].y;
+        }
+    };
+    int64_t a[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) a[p] = rsT ? f.anc_log[(int64_t)(T - 1) * S + ib + p] : ib + p;
     // working buffers are particle-major pairs; output columns are SoA [2][N]
-    const d2 v = *reinterpret_cast<const d2*>(f.v_work + 2 * a);
-    f.v_out[i] = v.x; f.v_out[N + i] = v.y;
-    const d2 dv = *reinterpret_cast<const d2*>(f.dv_work + 2 * a);
-    f.dv_out[i] = dv.x; f.dv_out[N + i] = dv.y;
-    if (rsT) f.w[i] = meanT;
+    {
+        d2 v[P], dv[P];
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            v[p] = *reinterpret_cast<const d2*>(f.v_work + 2 * a[p]);
+            dv[p] = *reinterpret_cast<const d2*>(f.dv_work + 2 * a[p]);
+        }
+        put(f.v_out, v);
+        put(f.dv_out, dv);
+    }
+    if (rsT) {
+        if constexpr (P >= 2) {
+#pragma unroll
+            for (int p = 0; p < P; p += 2) *reinterpret_cast<d2*>(f.w + ib + p) = d2{meanT, meanT};
+        } else {
+            f.w[ib] = meanT;
+        }
+    }
     if (!f.keep_history) {
-        const d2 x = *reinterpret_cast<const d2*>(f.x_work + 2 * a);
-        f.x_out[i] = x.x; f.x_out[N + i] = x.y;
+        d2 x[P];
+#pragma unroll
+        for (int p = 0; p < P; ++p) x[p] = *reinterpret_cast<const d2*>(f.x_work + 2 * a[p]);
+        put(f.x_out, x);
         return;
     }
     // The lineage a_s (x_{s+1} is read at a_s): a_s = anc_log row s-1 at a_{s+1} when step s
-    // resampled, else a_{s+1}. The chain is the kernel's critical path, so the next row's entry
-    // is loaded unconditionally (every row of the log exists; the entry is used only when its
-    // step resampled) and before this step's x gather: one memory latency a step, not two.
-    int32_t raw = f.anc_log[(int64_t)(T - 2 > 0 ? T - 2 : 0) * S + a];
-    // x_{T+1} was written at step T
-    {
-        const d2 x = *reinterpret_cast<const d2*>(f.hist_work[T + 1] + 2 * a);
-        double* dst = f.hist_out[T + 1];
-        dst[i] = x.x; dst[N + i] = x.y;
+    // resampled, else a_{s+1}. x_{T+1} was written at step T (read at a_T = a).
+    __shared__ const double* s_work[kFinChunk];
+    __shared__ double* s_out[kFinChunk];
+    __shared__ u64 s_rs;
+    d2 xp[P];   // gathered, not yet stored
+#pragma unroll
+    for (int p = 0; p < P; ++p) xp[p] = *reinterpret_cast<const d2*>(f.hist_work[T + 1] + 2 * a[p]);
+    double* outp = f.hist_out[T + 1];
+    // the entry of step T - 1's row (T - 2 in the log) at the lineage so far; every later entry
+    // is loaded by the step before (across chunks too), so the inner loop's entry state is the
+    // same from the chunk prologue and from its own back edge (one wait a step, for the entry)
+    int32_t raw[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) raw[p] = f.anc_log[(int64_t)(T - 2 > 0 ? T - 2 : 0) * S + a[p]];
+    for (int s0 = T - 1; s0 >= 1; s0 -= kFinChunk) {
+        const int n = s0 < kFinChunk ? s0 : kFinChunk;   // steps s0, s0 - 1, ..., s0 - n + 1
+        __syncthreads();   // the previous chunk's readers are done
+        if (threadIdx.x < kFinChunk) {
+            const int k = threadIdx.x, s = s0 - k;
+            const bool rs = k < n && f.dec[s].resampled;
+            s_work[k] = k < n ? f.hist_work[s + 1] : nullptr;
+            s_out[k] = k < n ? f.hist_out[s + 1] : nullptr;
+            const u64 m = __ballot(rs);
+            if (k == 0) s_rs = m;
+        }
+        __syncthreads();
+        const u64 rsw = s_rs;
+        for (int k = 0; k < n; ++k) {
+            const int s = s0 - k;
+            if ((rsw >> k) & 1)
+#pragma unroll
+                for (int p = 0; p < P; ++p) a[p] = raw[p];
+            const int64_t ro = (int64_t)(s - 2 > 0 ? s - 2 : 0) * S;
+            gcdp src = (gcdp)s_work[k];
+            d2 xn[P];
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                raw[p] = f.anc_log[ro + a[p]];
+                xn[p] = *reinterpret_cast<const __attribute__((address_space(1))) d2*>(src + 2 * a[p]);
+            }
+            put(outp, xp);
+            outp = s_out[k];
+#pragma unroll
+            for (int p = 0; p < P; ++p) xp[p] = xn[p];
+        }
     }
-    for (int s = T - 1; s >= 1; --s) {
-        if (f.dec[s].resampled) a = raw;
-        raw = f.anc_log[(int64_t)(s - 2 > 0 ? s - 2 : 0) * S + a];
-        const d2 x = *reinterpret_cast<const d2*>(f.hist_work[s + 1] + 2 * a);
-        double* dst = f.hist_out[s + 1];
-        dst[i] = x.x; dst[N + i] = x.y;
-    }
-    double* d1 = f.hist_out[1];
-    d1[i] = f.x0[0]; d1[N + i] = f.x0[1];
+    put(outp, xp);
+    d2 x1[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) x1[p] = d2{f.x0[0], f.x0[1]};
+    put(f.hist_out[1], x1);
 }
 
 // ------------------------------------------------------------------------------------
@@ -3072,7 +3196,12 @@ static hipError_t launch_timed(K kernel, dim3 grid, dim3 block, hipStream_t s, h
 }
 
 hipError_t launch_lazy_trace(hipStream_t s, const TraceArgs& a, int64_t N) {
-    hipLaunchKernelGGL(k_lazy_trace, grid_for(N), dim3(kBlock), 0, s, a, N);
+    bool pair = (N & 1) == 0 && (!a.a_in || ((uintptr_t)a.a_in & 7) == 0) && (!a.a_out || ((uintptr_t)a.a_out & 7) == 0);
+    for (int c = 0; c < a.ncomp; ++c) pair = pair && ((uintptr_t)a.comp[c].dst & 15) == 0;
+    if (pair)
+        hipLaunchKernelGGL(k_lazy_trace<2>, grid_for(N / 2), dim3(kBlock), 0, s, a, N);
+    else
+        hipLaunchKernelGGL(k_lazy_trace<1>, grid_for(N), dim3(kBlock), 0, s, a, N);
     return hipGetLastError();
 }
 hipError_t launch_rs_max(hipStream_t s, const double* w, int64_t N, MaxSlots* ms) {
@@ -3684,8 +3813,23 @@ hipError_t launch_delay(hipStream_t s, int microseconds) {
 }
 
 hipError_t launch_ssm2d_finalize(hipStream_t s, const Ssm2dFinal& f, hipEvent_t e0, hipEvent_t e1) {
-    if (f.recs_last) return launch_timed(k_ssm2d_final<true>, grid_for(f.N), dim3(kBlock), s, e0, e1, f);
-    return launch_timed(k_ssm2d_final<false>, grid_for(f.N), dim3(kBlock), s, e0, e1, f);
+    // two particles a thread when the SoA outputs' second components stay 16-B aligned
+    bool pair = (f.N & 1) == 0 && ((uintptr_t)f.w & 15) == 0;
+    static const int diag_p = [] {   // diagnostics (tools/): particles a thread, 1 / 2 / 4
+        const char* e = getenv("WSMC_DIAG_FINAL_P");
+        return e ? atoi(e) : 0;
+    }();
+    if (diag_p == 4 && (f.N & 3) == 0 && pair) {
+        if (f.recs_last) return launch_timed(k_ssm2d_final<true, 4>, grid_for(f.N / 4), dim3(kBlock), s, e0, e1, f);
+        return launch_timed(k_ssm2d_final<false, 4>, grid_for(f.N / 4), dim3(kBlock), s, e0, e1, f);
+    }
+    if (diag_p == 1) pair = false;
+    if (pair) {
+        if (f.recs_last) return launch_timed(k_ssm2d_final<true, 2>, grid_for(f.N / 2), dim3(kBlock), s, e0, e1, f);
+        return launch_timed(k_ssm2d_final<false, 2>, grid_for(f.N / 2), dim3(kBlock), s, e0, e1, f);
+    }
+    if (f.recs_last) return launch_timed(k_ssm2d_final<true, 1>, grid_for(f.N), dim3(kBlock), s, e0, e1, f);
+    return launch_timed(k_ssm2d_final<false, 1>, grid_for(f.N), dim3(kBlock), s, e0, e1, f);
 }
 
 }  // namespace wsmc

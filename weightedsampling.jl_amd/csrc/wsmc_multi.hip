@@ -10,7 +10,10 @@
 // the collectives of the G shards meet. Host buffers of N particles are split by shard on the
 // way in and joined on the way out; population-wide results (evidence, ESS, moments, median,
 // histogram, diversity, sample, flags) are identical on every shard and taken from shard 0.
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -54,15 +57,24 @@ struct MultiState {
     uint64_t gen_in = 0, gen_out = 0;
     std::vector<uint64_t> xbuf;
     std::vector<XArg> xargs;
-    // a shard that fails during a fan-out sets `abort`: shards waiting in the host exchange
-    // leave it with an error, and with RCCL every other shard's communicator is aborted (a
-    // collective missing its peer would never complete). Shards that then left the call with
-    // different results may hold different states: the handle is marked failed.
+    // A shard that fails by itself during a fan-out (a HIP or exchange failure: its peers may
+    // be waiting in a collective for it) sets `abort`: shards waiting in the host exchange leave
+    // it with an error, and RCCL shards abort their own communicators (each from its own thread,
+    // before its next collective or while it waits for its stream: a collective missing its
+    // peer would never complete) and leave with WSMC_ERCCL. An error every shard meets at the
+    // same point — an argument error before any collective, a population-wide not-PD
+    // covariance after the same collectives — sets nothing: the failing shard waits for its
+    // peers (at most kPeerWaitS, then it requests the abort after all). Shards that left the
+    // call with different results may hold different states: the handle is marked failed.
     bool rccl = false;
-    bool abort = false;         // guarded by xm
-    bool rccl_aborted = false;  // guarded by xm
-    bool failed = false;        // set between fan-outs only
+    std::atomic<bool> abort{false};   // written under xm
+    int finished = 0;                 // shards back from this fan-out's call (guarded by xm)
+    bool failed = false;              // set between fan-outs only
 };
+
+// seconds a shard that met a symmetric error waits for its peers before requesting the abort
+constexpr double kPeerWaitS = 30.0;
+static bool symmetric_error(int code) { return code == WSMC_EARG || code == WSMC_ENOTPD; }
 
 static void worker_loop(Worker* w) {
     for (;;) {
@@ -83,17 +95,36 @@ static void worker_loop(Worker* w) {
     }
 }
 
-// shard g failed: release the shards waiting for it (host exchange) or abort their
-// communicators (RCCL), once per fan-out
-static void abort_others(MultiState* M, int g) {
+// a shard failed by itself: release the shards waiting for it in the host exchange, and ask
+// the RCCL shards to abort their communicators (they do it on their own threads)
+static void request_abort(MultiState* M) {
     std::lock_guard<std::mutex> lk(M->xm);
-    if (M->abort) return;
-    M->abort = true;
+    if (M->abort.load()) return;
+    M->abort.store(true, std::memory_order_release);
     M->xcv.notify_all();
-    if (M->rccl && M->G > 1) {   // one shard: no peer can be waiting for it
-        for (int h = 0; h < M->G; ++h)
-            if (h != g && M->sub[h]->comm) (void)ncclCommAbort(M->sub[h]->comm);
-        M->rccl_aborted = true;
+}
+
+// shard g is back from its call with code rc
+static void shard_done(MultiState* M, int g, int rc) {
+    if (rc && !symmetric_error(rc) && M->G > 1) request_abort(M);   // one shard: no peer waits for it
+    bool wait_peers = false;
+    {
+        std::lock_guard<std::mutex> lk(M->xm);
+        M->finished += 1;
+        M->xcv.notify_all();
+        wait_peers = rc && symmetric_error(rc) && M->G > 1;
+    }
+    if (!wait_peers) return;
+    // every shard should meet the same error at the same point: wait for them, and abort the
+    // call after all if one is still inside it (then it was waiting for this shard)
+    std::unique_lock<std::mutex> lk(M->xm);
+    const bool all = M->xcv.wait_for(lk, std::chrono::duration<double>(kPeerWaitS),
+                                     [&] { return M->finished == M->G || M->abort.load(); });
+    lk.unlock();
+    if (!all) {
+        fprintf(stderr, "[wsmc multi] shard %d met error %d and its peers did not return within %.0f s: aborting\n",
+                g, rc, kPeerWaitS);
+        request_abort(M);
     }
 }
 
@@ -102,9 +133,11 @@ static int run_all(MultiState* M, const std::function<int(int, wsmc_ctx*)>& fn) 
     if (M->failed) return fail(WSMC_ESTATE, "multi-device handle failed in an earlier call (its shards diverged)");
     {
         std::lock_guard<std::mutex> lk(M->xm);
-        M->abort = false;
+        M->abort.store(false);
         M->arrived = M->departed = 0;
+        M->finished = 0;
     }
+    for (auto* s : M->sub) s->released = false;
     std::vector<int> rc(M->G, 0);
     std::vector<std::string> msg(M->G);
     for (int g = 1; g < M->G; ++g) {
@@ -112,27 +145,29 @@ static int run_all(MultiState* M, const std::function<int(int, wsmc_ctx*)>& fn) 
         std::lock_guard<std::mutex> lk(w->m);
         w->job = [&, g] {
             rc[g] = fn(g, M->sub[g]);
-            if (rc[g]) {
-                msg[g] = wsmc_last_error();
-                abort_others(M, g);
-            }
+            if (rc[g]) msg[g] = wsmc_last_error();
+            shard_done(M, g, rc[g]);
         };
         w->has = true;
         w->done = false;
         w->cv.notify_all();
     }
     rc[0] = fn(0, M->sub[0]);
-    if (rc[0]) {
-        msg[0] = wsmc_last_error();
-        abort_others(M, 0);
-    }
+    if (rc[0]) msg[0] = wsmc_last_error();
+    shard_done(M, 0, rc[0]);
     for (int g = 1; g < M->G; ++g) {
         Worker* w = M->workers[g].get();
         std::unique_lock<std::mutex> lk(w->m);
         w->cv.wait(lk, [&] { return w->done; });
     }
-    if (M->rccl_aborted) {   // aborted communicators are released: the shards must not destroy them
-        for (int h = 0; h < M->G; ++h) M->sub[h]->comm = nullptr;
+    if (M->abort.load() && M->rccl) {
+        // every thread is back: the communicators no shard aborted (shards that had finished
+        // before the request) are aborted here, and the handle is done with RCCL
+        for (auto* s : M->sub)
+            if (s->comm) {
+                (void)ncclCommAbort(s->comm);
+                s->comm = nullptr;
+            }
         M->failed = true;
     }
     bool same = true;
@@ -141,7 +176,7 @@ static int run_all(MultiState* M, const std::function<int(int, wsmc_ctx*)>& fn) 
     // report the first shard that failed by itself, not one released by the abort
     for (int pass = 0; pass < 2; ++pass)
         for (int g = 0; g < M->G; ++g)
-            if (rc[g] && (pass == 1 || rc[g] != WSMC_ERCCL))
+            if (rc[g] && (pass == 1 || (rc[g] != WSMC_ERCCL && !M->sub[g]->released)))
                 return fail(rc[g], "shard " + std::to_string(g) + ": " + msg[g]);
     return WSMC_OK;
 }
@@ -385,6 +420,7 @@ extern "C" int wsmc_create_multi(wsmc_ctx** out, int64_t n_particles, int32_t n_
             s->goff = M->off[g];
             s->gN = n_particles;
             s->comm = comms[g];   // the shard's destroy releases it
+            s->peer_abort = &M->abort;
         }
     } else {
         for (int g = 0; g < G; ++g) {
