@@ -270,6 +270,9 @@ def main():
         if args.shard_mode == "exact":
             ctx.comm_set_shard_mode(abi.SHARD_EXACT)
     exact = (comm is not None or args.rccl_one_rank) and args.shard_mode == "exact"
+    if os.environ.get("WSMC_DUMP_MAPS"):   # diagnostics: the load map, to symbolise a crash's raw frames
+        with open(os.environ["WSMC_DUMP_MAPS"], "w") as f:
+            f.write(open("/proc/self/maps").read())
 
     def barrier():
         ctx.sync()

@@ -354,8 +354,10 @@ int wsmc_debug_kernel_bench(wsmc_ctx* ctx, int32_t kernel, int32_t mode, int32_t
 int wsmc_debug_inject_failure(wsmc_ctx* ctx, int32_t shard, int32_t nth);
 /* Exact-sharded fused run: the fixed neighbour block (slots per step) and
  * trace window (ids per level) sizes — > 0 sets, 0 restores the defaults, < 0 leaves as is —
- * and, in stats_out[4] (may be NULL), the last run's largest block needed, its largest
- * lineage excursion, the runs re-done on the eager path after an overflow, the block size. */
+ * and, in stats_out[6] (may be NULL), the last run's largest block needed, its largest
+ * lineage excursion, the runs re-done on the eager path after a block overflow, the block
+ * size, the runs whose history was traced across ranks after a window overflow, and 1 when
+ * later runs ship no trace windows (lineages wander past half a shard). */
 int wsmc_debug_exact(wsmc_ctx* ctx, int64_t cap, int64_t ctr, int64_t* stats_out);
 /* Statement batches compiled for their shape at run time (hiprtc; csrc/wsmc_jit.hip):
  * stats_out[5] = signatures compiled, signatures that failed to compile (their batches run on

@@ -677,13 +677,14 @@ def test_multi_handle_symmetric_errors_keep_the_handle(gpu_available, mode):
 
 
 @pytest.mark.parametrize("sizes", [(2600, 2600), (1700, 2101, 1500)])
-@pytest.mark.parametrize("small", [False, True])
+@pytest.mark.parametrize("small", [False, True, "windows"])
 def test_exact_fused_run_without_host_round_trips(gpu_available, sizes, small):
     """The exact-sharded fused run as it now runs: no host read inside the
     run, particles moved between neighbours through fixed-size blocks and the lineages traced
     through fixed trace windows. With the default sizes nothing overflows; with blocks and
-    windows of a few slots every run overflows and is re-done on the eager path. Both must
-    equal one context holding the whole population, bit for bit, on ragged shards too."""
+    windows of a few slots every run overflows and is re-done on the eager path; with windows
+    alone of a few ids the filter stands and only the history is traced across ranks. All
+    must equal one context holding the whole population, bit for bit, on ragged shards too."""
     sys.path.insert(0, str(REPO / "oracle"))
     from oracle import Oracle
     import wsmc
@@ -696,11 +697,15 @@ def test_exact_fused_run_without_host_round_trips(gpu_available, sizes, small):
         models.ssm2d_statements(o, obs, ess_perc_min=ess)
         f = wsmc.Context.multi(N, len(sizes), seed=21, devices=[0] * len(sizes), transport=abi.TRANSPORT_HOST)
         f.comm_set_shard_mode(abi.SHARD_EXACT)
-        if small:
+        if small == "windows":
+            f.debug_exact(ctr=2)
+        elif small:
             f.debug_exact(cap=3, ctr=2)
         ev = f.ssm2d_run(obs, ess_perc_min=ess, keep_history=keep)
         st = f.debug_exact()
-        assert (st["eager_reruns"] >= 1) == small, st
+        assert (st["eager_reruns"] >= 1) == (small is True), st
+        if small == "windows" and keep:
+            assert st["history_traces"] >= 1, st
         assert ev == o.log_evidence()
         np.testing.assert_array_equal(f.weights_download(), o.weights_download())
         np.testing.assert_array_equal(f.last_ancestors(), o.last_ancestors())

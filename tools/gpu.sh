@@ -128,6 +128,13 @@ ew)   # the statement path (bench.py --statements): its line, kernel stats, FETC
   step 300 $O/sq.log rocprofv3 --kernel-trace --pmc $SQ --output-format csv -d $O/sq -o run -- python bench.py $A "$@"
   python tools/summarize_pmc.py $O/sq.json $O/sq > /dev/null
   sq_table $O/sq.json ew_batch,lazy_trace,rs_ ;;
+segv)  # the r03 crash under the kernel tracer: the libwsmc-free graph repro first, then the bench's
+       # default 300 runs with its load map dumped (a crash ends the recipe: nothing runs after it)
+  step 300 $O/graph_trace.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/gt -o run -- tools/micro/graph_trace 100 300
+  tail -1 $O/graph_trace.log
+  WSMC_DUMP_MAPS=$O/maps.txt timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python bench.py --no-cpu-baseline "$@" > $O/stats.log 2>&1
+  rc=$?; echo "bench under the tracer: exit $rc"; grep -A30 "Aborted at" $O/stats.log | head -40
+  [ $rc = 0 ] && stats_table $O/stats/run_kernel_stats.csv 6 ;;
 rccl)
   export NCCL_SOCKET_IFNAME=lo
   for m in island exact; do

@@ -3605,7 +3605,7 @@ static int enqueue_ssm2d_exact(wsmc_ctx* c, const RunPlan& p, int64_t cap, int64
     const int64_t ww = (int64_t)T * ctr * 3;
     unsigned long long* const wsnd[2] = {c->xwin, c->xwin + ww};
     unsigned long long* const wrcv[2] = {c->xwin + 2 * ww, c->xwin + 3 * ww};
-    const bool wins = p.keep && W > 1;
+    const bool wins = p.keep && W > 1 && !c->x_trace;
     if (wins) {
         ExactWin w;
         w.hist_work = p.d_hist_work;
@@ -3753,6 +3753,41 @@ static int ssm2d_run_exact(wsmc_ctx* c, const RunPlan& p, uint64_t op_base) {
     return WSMC_OK;
 }
 
+// The history of an exact-shard run whose filter completed on the device but whose lineages
+// left the trace windows (overflow bit 1 only: every particle moved within its blocks, so the
+// weights, the final columns and the global-id ancestor rows are right): x_2..x_{T+1} traced
+// across ranks level by level (trace_level, the eager path's exchange) over the rows the run
+// wrote, instead of re-running the filter.
+static int exact_trace_history(wsmc_ctx* c, const RunPlan& p, int64_t cap) {
+    const int T = p.T;
+    const int64_t N = c->N;
+    int r = ensure_exact(c);
+    if (r) return r;
+    for (int k = 0; k < 2; ++k)
+        if (!c->lineage[k]) WSMC_HIP(hipMalloc(&c->lineage[k], sizeof(int32_t) * (size_t)N));
+    ExactPlan hx;
+    std::vector<Decision> hdec(T + 1);
+    WSMC_HIP(hipMemcpyAsync(&hx, c->xp, sizeof(ExactPlan), hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(hipMemcpyAsync(hdec.data(), c->run_dec, sizeof(Decision) * (T + 1), hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));
+    const int64_t S = c->xanc_stride;
+    auto arow_of = [&](int t) { return c->xanc + (size_t)(t - 1) * S + cap; };   // step t's global ancestor ids
+    int32_t* A = c->lineage[0];
+    int32_t* B = c->lineage[1];
+    if (hdec[T].resampled)
+        WSMC_HIP(hipMemcpyAsync(A, arow_of(T), sizeof(int32_t) * N, hipMemcpyDeviceToDevice, c->stream));
+    else
+        WSMC_HIP(launch_iota(c->stream, A, N, c->goff));
+    for (int t = T; t >= 1; --t) {
+        const int32_t* arow = (t >= 2 && hdec[t - 1].resampled) ? arow_of(t - 1) : nullptr;
+        if ((r = trace_level(c, hx, c->cols[p.xcols[t + 1]].back, arow, A, B, c->cols[p.xcols[t + 1]].front)))
+            return r;
+        std::swap(A, B);
+    }
+    c->x_traces += 1;
+    return WSMC_OK;
+}
+
 int wsmc_run_set_timing(wsmc_ctx* c, int32_t enabled) {
     if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { return wsmc_run_set_timing(x, enabled); });
     if (!c) return fail(WSMC_EARG, "null context");
@@ -3846,7 +3881,9 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         for (const void* q : xb) mix(q);
     }
     const std::string key = std::string(keybuf) + " ptr=" + std::to_string(h) +
-                            (exact_async ? " exact cap=" + std::to_string(xcap) + " ctr=" + std::to_string(xctr) : "");
+                            (exact_async ? " exact cap=" + std::to_string(xcap) + " ctr=" + std::to_string(xctr) +
+                                               " trace=" + std::to_string((int)c->x_trace)
+                                         : "");
     auto build_tables = [&](double*** work, double*** outp) -> int {
         *work = *outp = nullptr;
         if (!p.keep) return WSMC_OK;
@@ -3967,18 +4004,31 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         c->x_need = need;
         c->x_exc = exc;
         c->x_overflows += bits ? 1 : 0;
-        if (bits) {
-            // grown for the next runs, never past a shard (a block or a level's window cannot
-            // need more than a neighbour's particles)
-            const int64_t nmax = (c->gN + c->world - 1) / c->world;
-            if (bits & 1ull) c->x_cap = std::min<int64_t>(nmax, std::max<int64_t>(4 * xcap, 2 * (int64_t)need));
+        const int64_t nmax = (c->gN + c->world - 1) / c->world;
+        if (bits & 1ull) {
+            // a block overflowed: particles are missing, re-run the filter on the eager path.
+            // Grown for the next runs, never past a shard (a block cannot need more than a
+            // neighbour's particles); blocks of half a shard or more would ship most of a
+            // neighbour's state every step: the eager path's exchanges cost less from then on
+            c->x_cap = std::min<int64_t>(nmax, std::max<int64_t>(4 * xcap, 2 * (int64_t)need));
             if (bits & 2ull) c->x_ctr = std::min<int64_t>(nmax, std::max<int64_t>(4 * xctr, 2 * (int64_t)exc));
-            // margins of half a shard or more would ship most of a neighbour's history every run
-            // (T x ctr x 24 B a side): the eager path's requests cost less from then on
-            if (2 * std::max(c->x_cap, c->x_ctr) >= nmax) c->x_eager = true;
+            if (2 * c->x_cap >= nmax) c->x_eager = true;
             WSMC_HIP(hipMemcpyAsync(c->w, c->w_save, sizeof(double) * c->N, hipMemcpyDeviceToDevice, c->stream));
             rows_x = false;
             if ((r = ssm2d_run_exact(c, p, op_base))) {
+                if (temp_tables) (void)hipFree(temp_tables);
+                return r;
+            }
+        } else if (bits & 2ull) {
+            // only the trace windows overflowed: the filter is right, the history is traced
+            // across ranks now. Windows that would need half a shard (T x ctr x 24 B a side every
+            // run) are dropped instead of grown: later runs trace their history this way
+            const int64_t grown = std::min<int64_t>(nmax, std::max<int64_t>(4 * xctr, 2 * (int64_t)exc));
+            if (2 * grown >= nmax)
+                c->x_trace = true;
+            else
+                c->x_ctr = grown;
+            if ((r = exact_trace_history(c, p, xcap))) {
                 if (temp_tables) (void)hipFree(temp_tables);
                 return r;
             }
@@ -4077,7 +4127,7 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
 
 int wsmc_debug_exact(wsmc_ctx* c, int64_t cap, int64_t ctr, int64_t* stats_out) {
     if (c && c->multi) {
-        int64_t st[4];
+        int64_t st[6];
         int r = multi_each(c, [&](wsmc_ctx* x) { return wsmc_debug_exact(x, cap, ctr, x == multi_first(c) ? st : nullptr); });
         if (!r && stats_out) std::memcpy(stats_out, st, sizeof(st));
         return r;
@@ -4085,14 +4135,16 @@ int wsmc_debug_exact(wsmc_ctx* c, int64_t cap, int64_t ctr, int64_t* stats_out) 
     if (!c) return fail(WSMC_EARG, "null context");
     if (cap >= 0) c->x_cap = cap;
     if (ctr >= 0) c->x_ctr = ctr;
-    if (cap >= 0 || ctr >= 0) c->x_eager = false;   // margins set by hand: the async run again
+    if (cap >= 0 || ctr >= 0) c->x_eager = c->x_trace = false;   // margins set by hand: the async run again
     if (stats_out) {
         int64_t cp = 0, ct = 0;
         if (c->world > 0 && c->gN > 0) exact_sizes(c, &cp, &ct);
         stats_out[0] = (int64_t)c->x_need;
         stats_out[1] = (int64_t)c->x_exc;
-        stats_out[2] = c->x_overflows;
+        stats_out[2] = c->x_overflows - c->x_traces;
         stats_out[3] = cp;
+        stats_out[4] = c->x_traces;
+        stats_out[5] = c->x_trace ? 1 : 0;
     }
     return WSMC_OK;
 }

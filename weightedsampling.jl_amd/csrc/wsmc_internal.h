@@ -212,8 +212,12 @@ struct wsmc_ctx {
     int64_t x_cap = 0, x_ctr = 0;           // block / window sizes in use (0: defaults; grown on overflow)
     unsigned long long x_need = 0, x_exc = 0;   // the last run's largest block / lineage excursion
     int64_t x_overflows = 0;                // runs re-done on the eager path
-    bool x_eager = false;                   // the margins grew past half a shard (lineages wander
+    bool x_eager = false;                   // the blocks grew past half a shard (particles move
                                             // far): later runs take the eager path directly
+    bool x_trace = false;                   // the trace windows would need half a shard (lineages
+                                            // wander far): later runs ship no windows and trace the
+                                            // history across ranks after the run (exact_trace_history)
+    int64_t x_traces = 0;                   // runs whose history was traced across ranks
     wsmc_term* d_ctape = nullptr;           // compiled Move tape (slot operands)
     int64_t d_ctape_cap = 0;
     void* d_prog = nullptr;                 // compiled fold program: segments, then constants

@@ -393,9 +393,10 @@ class Context:
     def debug_exact(self, cap: int = -1, ctr: int = -1) -> dict:
         """Exact-sharded fused run: set the neighbour block / trace window sizes (> 0 sets, 0
         restores the defaults, < 0 keeps) and return the last run's statistics."""
-        st = (C.c_int64 * 4)()
+        st = (C.c_int64 * 6)()
         check(self._L.wsmc_debug_exact(self._h, int(cap), int(ctr), st))
-        return {"need": st[0], "excursion": st[1], "eager_reruns": st[2], "cap": st[3]}
+        return {"need": st[0], "excursion": st[1], "eager_reruns": st[2], "cap": st[3],
+                "history_traces": st[4], "no_windows": st[5]}
 
     def debug_inject_failure(self, shard: int, nth: int) -> None:
         """Test hook: shard `shard` fails its nth next record exchange (include/wsmc.h)."""
