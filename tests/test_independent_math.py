@@ -365,3 +365,35 @@ def test_oscillator_matches_reference_math_oracle(scheme):
 def test_oscillator_full_horizon_matches_reference_math_hip(scheme, gpu_available):
     """C5's 60 observations (the rotation blocks included), one sweep per step."""
     assert run_oscillator_checked("hip", 16_384, 60, 1, scheme) <= 4
+
+
+# ---------------------------------------------------------------------------------------
+# the one-pass autoRW covariance with an outlying pivot (ADVICE r03)
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("D", [0.0, 1e2, 1e4])
+def test_autorw_pivot_outlier_error_bound(D):
+    """wsmc_autorw_factor takes the population's particle 0 as the pivot of its one-pass
+    moments (S = T2/T0 - m m^T relative to it). With particle 0 D standard deviations from the
+    weighted mean and a weight of e^-600, the cancellation costs about eps (D/sd)^2 relative:
+    measured here against the numpy two-pass covariance (tests/refmath.py) — 1e-12 at D = 0,
+    within 64 eps D^2 beyond. The configs' pivots sit inside the weighted mass (D of a few)."""
+    from oracle import Oracle
+    n = 4096
+    rng = np.random.default_rng(7)
+    Z = rng.normal(0.0, 1.0, size=(2, n))
+    Z[1] = 0.5 * Z[0] + Z[1]
+    Z[:, 0] = (D, -D)
+    lw = rng.normal(0.0, 0.3, size=n)
+    lw[0] = -600.0
+    o = Oracle(n, seed=SEED)
+    ca, cb = o.col_create("a"), o.col_create("b")
+    o.col_upload(ca, Z[0])
+    o.col_upload(cb, Z[1])
+    o.weights_upload(lw)
+    ok, cov, _ = o.autorw_cov([ca, cb], 1e-3)
+    assert ok
+    want, _ = R.autorw_factor(Z, lw, 1e-3)
+    rel = np.max(np.abs(cov - want)) / np.max(np.abs(want))
+    bound = max(1e-12, 64 * np.finfo(float).eps * D * D)
+    assert rel <= bound, (D, rel, bound)
+    o.close()

@@ -60,11 +60,15 @@ PY
 }
 line() { python -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[2], '%.4g' % d['value'], d['unit'], '%.3f ms/run' % d['ms_per_run'], 'frac %.3f' % d['roofline']['frac'])" "$1" "$2"; }
 
-prof_passes() {   # kernel stats of the bench command (20 timed runs: the profiler's kernel-trace
-                  # of the default 300 graph-replayed runs crashed inside rocprofv3 on r03_v3),
-                  # then FETCH_SIZE / WRITE_SIZE in separate passes
-  step 400 $O/stats.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python bench.py --no-cpu-baseline --steps 20 --warmup 2
+prof_passes() {   # kernel stats of the bench command at its default 300 runs, submitted eagerly
+                  # (WSMC_DIAG_NO_GRAPH=1: the same kernels; rocprofv3's kernel trace segfaults on
+                  # graph replays past a few thousand dispatches, tools/micro/graph_trace.hip and
+                  # DESIGN.md §4), the graph-launched run's stats at 20 runs beside it, then
+                  # FETCH_SIZE / WRITE_SIZE in separate passes
+  WSMC_DIAG_NO_GRAPH=1 step 600 $O/stats.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python bench.py --no-cpu-baseline
   stats_table $O/stats/run_kernel_stats.csv 6
+  step 400 $O/gstats.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/gstats -o run -- python bench.py --no-cpu-baseline --steps 20 --warmup 2
+  stats_table $O/gstats/run_kernel_stats.csv 6
   A="--steps 2 --warmup 1 --no-cpu-baseline"
   step 300 $O/fetch.log rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- python bench.py $A
   step 300 $O/write.log rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python bench.py $A
@@ -128,13 +132,15 @@ ew)   # the statement path (bench.py --statements): its line, kernel stats, FETC
   step 300 $O/sq.log rocprofv3 --kernel-trace --pmc $SQ --output-format csv -d $O/sq -o run -- python bench.py $A "$@"
   python tools/summarize_pmc.py $O/sq.json $O/sq > /dev/null
   sq_table $O/sq.json ew_batch,lazy_trace,rs_ ;;
-segv)  # the r03 crash under the kernel tracer: the libwsmc-free graph repro first, then the bench's
-       # default 300 runs with its load map dumped (a crash ends the recipe: nothing runs after it)
-  step 300 $O/graph_trace.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/gt -o run -- tools/micro/graph_trace 100 300
-  tail -1 $O/graph_trace.log
-  WSMC_DUMP_MAPS=$O/maps.txt timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python bench.py --no-cpu-baseline "$@" > $O/stats.log 2>&1
-  rc=$?; echo "bench under the tracer: exit $rc"; grep -A30 "Aborted at" $O/stats.log | head -40
-  [ $rc = 0 ] && stats_table $O/stats/run_kernel_stats.csv 6 ;;
+segv)  # the r03 crash under the kernel tracer: the libwsmc-free repro on plain stream
+       # launches, the bench's default 300 runs submitted eagerly (WSMC_DIAG_NO_GRAPH=1) under the
+       # tracer, then the repro's graph replays at R = $1 (a crash ends the recipe: it runs last)
+  step 300 $O/stream_trace.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/st -o run -- tools/micro/graph_trace 100 300 1000000 0 0
+  tail -1 $O/stream_trace.log
+  WSMC_DIAG_NO_GRAPH=1 step 600 $O/stats.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python bench.py --no-cpu-baseline
+  stats_table $O/stats/run_kernel_stats.csv 6
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/gt -o run -- tools/micro/graph_trace 100 ${1:-100} > $O/graph_trace.log 2>&1
+  rc=$?; echo "graph replays R=${1:-100} under the tracer: exit $rc"; tail -1 $O/graph_trace.log ;;
 rccl)
   export NCCL_SOCKET_IFNAME=lo
   for m in island exact; do

@@ -2,7 +2,8 @@
 // r03): one HIP graph of 3 x T streaming-kernel nodes captured from a stream, replayed R times,
 // then synchronised. Run under `rocprofv3 --kernel-trace --stats` to see whether the tracer
 // alone fails on R x 3T graph-launched dispatches.
-//   tools/micro/graph_trace [T=100] [R=300] [N=1000000]
+//   tools/micro/graph_trace [T=100] [R=300] [N=1000000] [sync=0: 1 synchronises after every replay]
+//                           [graph=1: 0 launches the same kernels on the stream, no graph]
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -26,6 +27,8 @@ int main(int argc, char** argv) {
     const int T = argc > 1 ? atoi(argv[1]) : 100;
     const int R = argc > 2 ? atoi(argv[2]) : 300;
     const long n = argc > 3 ? atol(argv[3]) : 1000000;
+    const int sync_each = argc > 4 ? atoi(argv[4]) : 0;
+    const int use_graph = argc > 5 ? atoi(argv[5]) : 1;
     double *x, *y;
     unsigned long long* q;
     int* a;
@@ -36,16 +39,28 @@ int main(int argc, char** argv) {
     hipGraph_t g;
     hipGraphExec_t ge;
     const dim3 grid((unsigned)((n + 255) / 256));
-    CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    for (int t = 0; t < T; ++t) {
-        hipLaunchKernelGGL(k_a, grid, dim3(256), 0, s, x, y, n);
-        hipLaunchKernelGGL(k_b, grid, dim3(256), 0, s, y, q, n);
-        hipLaunchKernelGGL(k_c, grid, dim3(256), 0, s, q, a, n);
+    auto enqueue = [&]() {
+        for (int t = 0; t < T; ++t) {
+            hipLaunchKernelGGL(k_a, grid, dim3(256), 0, s, x, y, n);
+            hipLaunchKernelGGL(k_b, grid, dim3(256), 0, s, y, q, n);
+            hipLaunchKernelGGL(k_c, grid, dim3(256), 0, s, q, a, n);
+        }
+    };
+    if (use_graph) {
+        CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        enqueue();
+        CK(hipStreamEndCapture(s, &g));
+        CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
     }
-    CK(hipStreamEndCapture(s, &g));
-    CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
-    for (int r = 0; r < R; ++r) CK(hipGraphLaunch(ge, s));
+    for (int r = 0; r < R; ++r) {
+        if (use_graph)
+            CK(hipGraphLaunch(ge, s));
+        else
+            enqueue();
+        if (sync_each) CK(hipStreamSynchronize(s));
+    }
     CK(hipStreamSynchronize(s));
-    printf("graph_trace: %d replays of %d kernel nodes, %d dispatches: ok\n", R, 3 * T, 3 * T * R);
+    printf("graph_trace: %d %s of %d kernels, %d dispatches%s: ok\n", R, use_graph ? "graph replays" : "stream runs",
+           3 * T, 3 * T * R, sync_each ? ", synchronised after each" : "");
     return 0;
 }

@@ -445,16 +445,30 @@ struct MoveSpec
     hi::NTuple{4,Float64}
 end
 
+# A Move's arguments do not read the state when its argfn gives the same arguments without one
+# (`autoRW()`, `autoRW(1e-3, (0, Inf))`: the @model lowering's literal arguments); an argfn
+# that reads the state (say a step from a column's spread) must see the state after the Moves
+# before it, as the reference applies the steps in order (src/transformers.jl:331-334).
+function state_free_args(m::WS.Move, state::HipState)
+    try
+        return m.argfn(nothing) == m.argfn(state)
+    catch
+        return false
+    end
+end
+
 # A Sequence of Moves — the body of `if resampled ... end` (examples/linear_regression.jl:23-24)
 # or a sweep — is one wsmc_move_block call: the sequential Moves' results, as one moments
-# pass, one combine and one Move kernel when the block fuses (disjoint autoRW targets).
+# pass, one combine and one Move kernel when the block fuses (disjoint autoRW targets). Only
+# when every Move's arguments are state-free and it has at most 4 targets; otherwise the
+# steps run one by one, each argfn evaluated when its Move runs.
 function apply!(t::WS.Sequence, state::HipState)
     steps = t.steps
-    if !isempty(steps) && all(x -> x isa WS.Move && x.diversity_threshold === nothing, steps)
+    if !isempty(steps) && all(x -> x isa WS.Move && x.diversity_threshold === nothing &&
+                                   length(x.targets) <= 4 && state_free_args(x, state), steps)
         specs = map(steps) do m
             kind, step, ids, lo, hi = move_args(m, state)
             d = length(ids)
-            d <= 4 || error("WeightedSamplingHIP: a Move has at most 4 targets")
             pad(v, x) = ntuple(k -> k <= d ? v[k] : x, 4)
             MoveSpec(kind, d, pad(ids, Int32(-1)), lo === nothing ? 0 : 1, state.depth, step,
                      lo === nothing ? ntuple(_ -> -Inf, 4) : pad(lo, -Inf),

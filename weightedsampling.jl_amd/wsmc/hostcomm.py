@@ -227,19 +227,13 @@ class HostComm:
 
 def from_env(timeout: float = 120.0) -> HostComm:
     """The ranks of one single-node job (torch.distributed.run): rank 0 listens on loopback.
-    A job spread over several nodes cannot rendezvous here: fail at once instead of waiting
-    for the timeout."""
+    A job spread over several nodes cannot rendezvous here: WORLD_SIZE != LOCAL_WORLD_SIZE
+    says so, and fails at once instead of waiting for the timeout. MASTER_ADDR is not
+    consulted: on one node every rank reaches rank 0 through 127.0.0.1 whatever name the
+    launcher exported (torch.distributed.run --standalone exports the host's FQDN)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     if world != local_world:
         raise RuntimeError(f"hostcomm serves one node: WORLD_SIZE {world} != LOCAL_WORLD_SIZE {local_world}")
-    addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
-    if addr not in ("127.0.0.1", "localhost", "::1", socket.gethostname()):
-        try:
-            local = socket.gethostbyname(addr).startswith("127.")
-        except OSError:
-            local = False
-        if not local:
-            raise RuntimeError(f"hostcomm serves one node: MASTER_ADDR {addr} is not this host's loopback")
     return HostComm(int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
                     "127.0.0.1", int(os.environ.get("MASTER_PORT", "29500")), timeout=timeout)
