@@ -3,6 +3,7 @@
 * C5 (examples/damped_oscillator.jl:20, 30-43): all 60 observations, the canonical five
   ungated sweeps of the bounded 4-D + 1-D autoRW moves, 50k particles — the longest score
   folds (5 + 60 terms per particle, twice per move) bit for bit against the oracle.
+* C5 at its 4-GPU partition: four shards of 12.5k in one handle, island and exact.
 * C4 (C2 sharded): eight shards on the one GPU of a test box (eight processes, records
   exchanged through the host in place of RCCL, which refuses two ranks on one device), and
   C4's own population of 8M as two shards of 4M, island and exact, T = 100, every traced-back
@@ -35,6 +36,36 @@ def test_c5_full_horizon_matches_oracle(gpu_available, scheme):
     assert ag == ao                      # accepted counts of all 600 moves
     assert_same_state(g, o)
     assert g.log_evidence() == o.log_evidence()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("mode", ["island", "exact"])
+@pytest.mark.parametrize("scheme", [0, 1])
+def test_c5_four_shards_full_horizon(gpu_available, mode, scheme):
+    """C5 at its 4-GPU partition (BASELINE configs[4]) on one GPU: SMCState over 4 shards of
+    12.5k in one handle (wsmc_create_multi, the in-process exchange standing in for RCCL), all
+    60 observations, 5 ungated sweeps of the bounded 4-D + 1-D autoRW moves (600 moves, the
+    sharded autoRW combine at every one). Island shards against the four-shard oracle, exact
+    shards against it in exact mode (one population's bits), accepted counts and every column
+    bit for bit."""
+    import wsmc
+    from oracle import Oracle
+    from wsmc import abi
+    from test_gpu_parity import assert_same_state
+    G, N = 4, 50_000
+    exact = mode == "exact"
+    t, y = wsmc.models.oscillator_data(n=60)
+    g = wsmc.Context.multi(N, G, seed=4, devices=[0] * G, transport=abi.TRANSPORT_HOST)
+    if exact:
+        g.comm_set_shard_mode(abi.SHARD_EXACT)
+    o = Oracle(N, seed=4, shards=G, exact=exact)
+    ag = wsmc.models.oscillator_statements(g, t, y, ess_perc_min=1.0, scheme=scheme, sweeps=5, diversity=None)
+    ao = wsmc.models.oscillator_statements(o, t, y, ess_perc_min=1.0, scheme=scheme, sweeps=5, diversity=None)
+    assert len(ag) == 60 * 5
+    assert ag == ao
+    assert_same_state(g, o)
+    assert g.log_evidence() == o.log_evidence()
+    g.close()
 
 
 # ---- C4's partition ----------------------------------------------------------------------
