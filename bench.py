@@ -80,6 +80,10 @@ def parse():
     # the path a Julia run! on HipColumnStore takes) instead of the fused runner; with
     # --eager-store the store gathers every column at every resample, as the reference's
     # ColumnStore does (src/stores.jl:105-128)
+    # diagnostics: one process, one multi-device handle of this many shards on GPU 0 with the
+    # in-process exchange (wsmc_create_multi, transport HOST): the sharded run's device path
+    # with a memcpy for a collective (the one-GPU stand-in for RCCL between ranks); N per shard
+    ap.add_argument("--multi-shards", type=int, default=0)
     ap.add_argument("--statements", action="store_true")
     ap.add_argument("--eager-store", action="store_true")
     return ap.parse_args()
@@ -256,7 +260,14 @@ def main():
     T = args.T
     obs = wsmc.models.ssm2d_data(max(T, args.cpu_T), seed=args.seed)
     # one seed for every rank: the Philox streams are keyed by the global particle index
-    ctx = wsmc.Context(N, seed=args.seed, device=0 if args.same_device else local)
+    if args.multi_shards > 1 and comm is None:
+        G = args.multi_shards
+        gN = G * N
+        ctx = wsmc.Context.multi(gN, G, seed=args.seed, devices=[0] * G, transport=abi.TRANSPORT_HOST)
+        if args.shard_mode == "exact":
+            ctx.comm_set_shard_mode(abi.SHARD_EXACT)
+    else:
+        ctx = wsmc.Context(N, seed=args.seed, device=0 if args.same_device else local)
     if comm is not None:
         if args.exchange == "host":
             ctx.comm_init_host(comm.allgather, world, rank, goff, gN)
@@ -269,7 +280,7 @@ def main():
         ctx.comm_init(wsmc.Context.comm_unique_id(), 1, 0, 0, N)
         if args.shard_mode == "exact":
             ctx.comm_set_shard_mode(abi.SHARD_EXACT)
-    exact = (comm is not None or args.rccl_one_rank) and args.shard_mode == "exact"
+    exact = (comm is not None or args.rccl_one_rank or args.multi_shards > 1) and args.shard_mode == "exact"
     if os.environ.get("WSMC_DUMP_MAPS"):   # diagnostics: the load map, to symbolise a crash's raw frames
         with open(os.environ["WSMC_DUMP_MAPS"], "w") as f:
             f.write(open("/proc/self/maps").read())
@@ -307,13 +318,14 @@ def main():
         elapsed = comm.max(elapsed)
     st = ctx.get_state()
     ev = ctx.log_evidence()
+    xst = ctx.debug_exact() if exact else None   # exact shards: block / window needs, re-runs, history traces
 
     # per-kernel durations: HIP events recorded on the context stream around every launch of
     # the same graph (a separate instrumented pass of `steps` runs); not available on exact
     # shards (their eager, host-driven run is not instrumented)
     prop_ms = red_ms = rs_ms = fin_ms = tot_ms = 0.0
     nres = 0
-    if not exact and not args.statements:
+    if not exact and not args.statements and args.multi_shards <= 1:
         ctx.set_timing(True)
         inst_runs = max(1, min(args.steps, 5))
         one_run()  # capture the instrumented graph
@@ -426,10 +438,13 @@ def main():
                        # island shards resample within themselves after the global decision: a
                        # different (unbiased) estimator than the reference's single-population
                        # Resample, which exact shards reproduce bit for bit
-                       "estimator": ("reference (single population)" if (world == 1 and not args.rccl_one_rank)
+                       "estimator": ("reference (single population)" if (world == 1 and not args.rccl_one_rank
+                                                                         and args.multi_shards <= 1)
                                      or args.shard_mode == "exact"
                                      else "island resampling (per-shard strata, global decision)"),
-                       "parallelism": (f"{args.shard_mode}-shard x{world}"
+                       "parallelism": (f"{args.shard_mode}-shard x{args.multi_shards} in one handle on one GPU "
+                                       "(in-process exchange, diagnostic)") if args.multi_shards > 1 else
+                                      (f"{args.shard_mode}-shard x{world}"
                                        + (" (host exchange, test mode)" if args.exchange == "host" else ""))
                            if world > 1 else ("single GPU, one-rank RCCL communicator (diagnostic)"
                                               if args.rccl_one_rank else "single GPU")},
@@ -454,6 +469,8 @@ def main():
                 "resamples_per_run": nres, "forced_every_step": forced},
             "log_evidence_last": ev,
         }
+        if xst is not None:
+            line["exact_stats"] = xst
         os.write(json_fd, (json.dumps(line) + "\n").encode())
     ctx.close()
     if comm is not None:

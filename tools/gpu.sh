@@ -156,7 +156,13 @@ multirank)   # bench.py's multi-rank path with 2 ranks on the box's one GPU (hos
   timeout -k 10 400 $MR --master-port 29612 bench.py $A --shard-mode exact > $O/mr_exact.json 2> $O/mr_exact.err || { tail -30 $O/mr_exact.err; exit 1; }
   line $O/mr_exact.json multirank-exact
   timeout -k 10 400 $MR --master-port 29613 bench.py $A --global-particles 1000001 > $O/mr_strong.json 2> $O/mr_strong.err || { tail -30 $O/mr_strong.err; exit 1; }
-  line $O/mr_strong.json multirank-strong ;;
+  line $O/mr_strong.json multirank-strong
+  # the same two shards in one process (one handle, in-process exchange: the device path of
+  # the sharded run with a memcpy for the collective), island and exact
+  for m in island exact; do
+    timeout -k 10 400 python bench.py --multi-shards 2 --steps 5 --warmup 2 --no-cpu-baseline --shard-mode $m > $O/mh_$m.json 2> $O/mh_$m.err || { tail -30 $O/mh_$m.err; exit 1; }
+    line $O/mh_$m.json multihandle-$m
+  done ;;
 fallback)   # the sharded run's eager fallback after a failed capture (one-rank RCCL)
   export NCCL_SOCKET_IFNAME=lo
   WSMC_DIAG_CAPTURE_FAIL=1 timeout -k 10 300 python bench.py --no-cpu-baseline --rccl-one-rank --steps 3 > $O/fb.json 2> $O/fb.err || { tail -30 $O/fb.err; exit 1; }

@@ -1327,6 +1327,16 @@ static int trace_level(wsmc_ctx* c, const ExactPlan& x, const double* hist, cons
                                 c->stream));
         WSMC_HIP(ctx_sync(c, c->stream));
     }
+    static const bool dbg = [] {   // diagnostics: every level's requested id range
+        const char* e = getenv("WSMC_TRACE_DEBUG");
+        return e && atoi(e) != 0;
+    }();
+    if (dbg && me == 0)
+        std::fprintf(stderr, "[trace_level] ranges:%s\n", [&] {
+            std::string t;
+            for (int g = 0; g < W; ++g) t += " [" + std::to_string(rng[2 * g]) + "," + std::to_string(rng[2 * g + 1]) + ")";
+            return t;
+        }().c_str());
     auto part = [&](int owner, int req) {   // [start, end) global of owner's rows requester needs
         const unsigned long long lo = rng[2 * req] > x.gofs[owner] ? rng[2 * req] : x.gofs[owner];
         const unsigned long long hi = rng[2 * req + 1] < x.gofs[owner + 1] ? rng[2 * req + 1] : x.gofs[owner + 1];
@@ -3871,7 +3881,11 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
     mix(c->comm);   // a captured collective bakes its communicator
     // exact shards: the run without host round trips unless it is switched off (A/B) or the
     // scheme needs the eager path; its block / window sizes are part of the graph
-    const bool exact_async = exact_mode(c) && !exact_eager_forced() && !c->x_eager;
+    // a caller's host transport (wsmc_comm_init_host: a test vehicle, every exchange a host
+    // round trip) ships the async run's fixed blocks of cap slots every step; the eager path
+    // ships only the slots that move, so it runs there
+    const bool exact_async = exact_mode(c) && !exact_eager_forced() && !c->x_eager &&
+                             (!c->host_exchange || c->host_inproc);
     int64_t xcap = 0, xctr = 0;
     if (exact_async) {
         exact_sizes(c, &xcap, &xctr);
@@ -4005,13 +4019,35 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         c->x_exc = exc;
         c->x_overflows += bits ? 1 : 0;
         const int64_t nmax = (c->gN + c->world - 1) / c->world;
+        // trace windows cost T x ctr x 24 B a side every run, the distributed trace one range
+        // exchange a level: windows grow at most to 4x their default, past that (lineages
+        // wander far: coalescence) they are dropped and the history is traced across ranks
+        auto grow_windows = [&]() {
+            int64_t d_cap = 0, d_ctr = 0;
+            const int64_t saved = c->x_ctr;
+            c->x_ctr = 0;
+            exact_sizes(c, &d_cap, &d_ctr);
+            c->x_ctr = saved;
+            const int64_t grown = std::min<int64_t>(nmax, std::max<int64_t>(4 * xctr, 2 * (int64_t)exc));
+            if (grown > 4 * d_ctr || 2 * grown >= nmax)
+                c->x_trace = true;
+            else
+                c->x_ctr = grown;
+        };
+        if (!(bits & 1ull) && need > 0 && 8 * (int64_t)need < xcap && xcap > 256) {
+            // the blocks ship cap slots a side every step whatever moves: shrink them toward
+            // the need (4x margin, a power of two, so a captured graph is rebuilt rarely)
+            int64_t cp = 256;
+            while (cp < 4 * (int64_t)need) cp *= 2;
+            c->x_cap = cp;
+        }
         if (bits & 1ull) {
             // a block overflowed: particles are missing, re-run the filter on the eager path.
             // Grown for the next runs, never past a shard (a block cannot need more than a
             // neighbour's particles); blocks of half a shard or more would ship most of a
             // neighbour's state every step: the eager path's exchanges cost less from then on
             c->x_cap = std::min<int64_t>(nmax, std::max<int64_t>(4 * xcap, 2 * (int64_t)need));
-            if (bits & 2ull) c->x_ctr = std::min<int64_t>(nmax, std::max<int64_t>(4 * xctr, 2 * (int64_t)exc));
+            if (bits & 2ull) grow_windows();
             if (2 * c->x_cap >= nmax) c->x_eager = true;
             WSMC_HIP(hipMemcpyAsync(c->w, c->w_save, sizeof(double) * c->N, hipMemcpyDeviceToDevice, c->stream));
             rows_x = false;
@@ -4021,13 +4057,8 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
             }
         } else if (bits & 2ull) {
             // only the trace windows overflowed: the filter is right, the history is traced
-            // across ranks now. Windows that would need half a shard (T x ctr x 24 B a side every
-            // run) are dropped instead of grown: later runs trace their history this way
-            const int64_t grown = std::min<int64_t>(nmax, std::max<int64_t>(4 * xctr, 2 * (int64_t)exc));
-            if (2 * grown >= nmax)
-                c->x_trace = true;
-            else
-                c->x_ctr = grown;
+            // across ranks now
+            grow_windows();
             if ((r = exact_trace_history(c, p, xcap))) {
                 if (temp_tables) (void)hipFree(temp_tables);
                 return r;

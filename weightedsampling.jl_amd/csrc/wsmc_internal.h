@@ -148,6 +148,8 @@ struct wsmc_ctx {
     const std::atomic<bool>* peer_abort = nullptr;
     bool released = false;
     wsmc_exchange_fn host_exchange = nullptr;   // host-side record exchange (instead of RCCL)
+    bool host_inproc = false;                   // ... between threads of this process (a multi-device
+                                                // handle's: a memcpy), not a caller's transport
     int32_t inject_fail = 0;                    // wsmc_debug_inject_failure: fail the nth next record exchange
     unsigned long long* run_grp = nullptr;      // [T+1][ngroups][kGroupLine] fused-run group sums
     // Move score cache: each particle's fold over the first scache_terms tape terms (its

@@ -427,6 +427,7 @@ extern "C" int wsmc_create_multi(wsmc_ctx** out, int64_t n_particles, int32_t n_
             M->xargs[g] = XArg{M, g};
             int r = wsmc_comm_init_host(M->sub[g], multi_exchange, &M->xargs[g], G, g, M->off[g], n_particles);
             if (r) return cleanup(r);
+            M->sub[g]->host_inproc = true;
         }
     }
     M->workers.resize(G);
