@@ -249,6 +249,44 @@ int wsmc_col_gather_rows(wsmc_ctx* ctx, int32_t col_id, const int64_t* idx, int6
 /* ---- operators (apply!) ------------------------------------------------------ */
 /* Assign: out[k] .= expr[k] for k < dim(out)            src/transformers.jl:28-32 */
 int wsmc_assign(wsmc_ctx* ctx, int32_t out_col, const wsmc_operand* expr);
+/* Assign of a general expression: out[k] .= f_k(columns...) for k < dim(out).
+ * The reference's `vectorize` (src/rewrites.jl:146-219) turns the right-hand side into one
+ * fused broadcast over the columns: calls f.(args...), `cond ? a : b` as ifelse.(...),
+ * `a || b` / `a && b` as .| / .&, `x[j]` component reads. The device form is one postfix
+ * program per output component, the components' programs back to back in `prog`, len[k]
+ * instructions for component k (k < dim(out)); at most WSMC_XPROG_MAX instructions in all and
+ * WSMC_XSTACK_MAX values on the stack. Binary operators pop b (the top) then a and push
+ * f(a, b); each component's program must leave exactly one value. The arithmetic is
+ * wsmc_xop1 / wsmc_xop2 (include/wsmc_terms.h). Columns read one lazy Resample behind are
+ * read through its ancestors (as wsmc_assign). WSMC_EARG: a malformed program, an unknown
+ * column or component. Domain errors Julia throws (sqrt / log of a negative, a negative
+ * base to a fractional power) give NaN. */
+typedef enum {
+    WSMC_X_CONST = 0,   /* push c                                                         */
+    WSMC_X_COL = 1,     /* push column col, component comp                                */
+    WSMC_X_NEG = 2, WSMC_X_ABS = 3, WSMC_X_SQRT = 4, WSMC_X_EXP = 5, WSMC_X_LOG = 6,
+    WSMC_X_LOG1P = 7, WSMC_X_SIN = 8, WSMC_X_COS = 9,
+    WSMC_X_POWI = 10,   /* a^n, n = c (an integer, |n| < 2^62): Base.literal_pow for
+                           n in -2..3, else Base's compensated power by squaring       */
+    WSMC_X_NOT = 11,    /* !a: 1 if a == 0 else 0                                        */
+    WSMC_X_ADD = 16, WSMC_X_SUB = 17, WSMC_X_MUL = 18, WSMC_X_DIV = 19,
+    WSMC_X_MIN = 20, WSMC_X_MAX = 21,   /* Base.min / max (NaN-propagating, -0.0 < 0.0)   */
+    WSMC_X_POW = 22,    /* a^b: integer b as POWI, else exp(b * log(a))                   */
+    WSMC_X_LT = 23, WSMC_X_LE = 24, WSMC_X_GT = 25, WSMC_X_GE = 26, WSMC_X_EQ = 27,
+    WSMC_X_NE = 28,     /* comparisons: 1.0 / 0.0                                         */
+    WSMC_X_AND = 29, WSMC_X_OR = 30,    /* (a != 0) & (b != 0), (a != 0) | (b != 0)       */
+    WSMC_X_IFELSE = 31  /* pops f, t, cond: cond != 0 ? t : f (both evaluated)            */
+} wsmc_xop;
+typedef struct {
+    int32_t op;         /* wsmc_xop */
+    int32_t col;        /* WSMC_X_COL: the column */
+    int32_t comp;       /* WSMC_X_COL: its component */
+    int32_t reserved;
+    double  c;          /* WSMC_X_CONST: the value; WSMC_X_POWI: the exponent */
+} wsmc_xinst;
+#define WSMC_XPROG_MAX 96
+#define WSMC_XSTACK_MAX 8
+int wsmc_assign_expr(wsmc_ctx* ctx, int32_t out_col, const wsmc_xinst* prog, const int32_t* len);
 /* Sample: out ~ dist (weighter === nothing)            src/transformers.jl:172-182 */
 int wsmc_sample(wsmc_ctx* ctx, int32_t out_col, const wsmc_dist* dist);
 /* Sample with importance_kernel(proposal, target)      src/default_kernels.jl:69-73 */

@@ -334,6 +334,84 @@ WSMC_HD double wsmc_cos(double x) {
     return ((n + 1) & 2) ? -v : v;   /* n = 1, 2 negate */
 }
 
+/* sin(x), the same reduction and kernels as wsmc_cos: sin(|x|) by quadrant, the sign of x
+   restored (ksin is odd bit for bit, so the small case is ksin(x) itself) */
+WSMC_HD double wsmc_sin(double x) {
+    const double invpio2 = 6.36619772367581382433e-01, p1 = 1.57079632673412561417e+00,
+                 p2 = 6.07710050630396597660e-11, p3 = 2.02226624879595063154e-21;
+    if (!wsmc_isfinite(x)) return WSMC_NAN;
+    const double ax = wsmc_fabs(x);
+    const int small = ax <= 7.85398163397448278999e-01;
+    const double fn = (double)(int64_t)(ax * invpio2 + 0.5);
+    const double rr = ((ax - fn * p1) - fn * p2) - fn * p3;
+    const double r = small ? ax : rr;
+    const int n = small ? 0 : (int)((int64_t)fn & 3);
+    const double kc = wsmc_kcos(r), ks = wsmc_ksin(r);
+    double v = (n & 1) ? kc : ks;
+    v = (n & 2) ? -v : v;            /* n = 2, 3 negate */
+    return (wsmc_d2bits(x) >> 63) ? -v : v;
+}
+
+/* Base.min / Base.max for Float64 (Julia >= 1.9): the difference's sign picks the operand,
+   so min(-0.0, 0.0) = -0.0; a NaN operand gives the (NaN) difference */
+WSMC_HD double wsmc_min(double a, double b) {
+    const double d = a - b;
+    const double m = (wsmc_d2bits(d) >> 63) ? a : b;
+    return (wsmc_isnan(a) || wsmc_isnan(b)) ? d : m;
+}
+WSMC_HD double wsmc_max(double a, double b) {
+    const double d = a - b;
+    const double m = (wsmc_d2bits(d) >> 63) ? b : a;
+    return (wsmc_isnan(a) || wsmc_isnan(b)) ? d : m;
+}
+
+/* x^n for an integer n: Base.literal_pow's forms for n in -2..3 (x^2 = x*x, x^3 = x*x*x,
+   x^-1 = inv(x), x^-2 = inv(x)^2), else Base.pow_body(::Float64, ::Integer): power by
+   squaring carrying each product's rounding error (two_mul by fma), muladd taken as fma */
+WSMC_HD double wsmc_powi(double x, int64_t n) {
+    if (n == 0) return 1.0;
+    if (n == 1) return x;
+    if (n == 2) return x * x;
+    if (n == 3) return x * x * x;
+    if (n == -1) return 1.0 / x;
+    if (n == -2) {
+        const double r = 1.0 / x;
+        return r * r;
+    }
+    double y = 1.0, xnlo = 0.0, ynlo = 0.0;
+    if (n < 0) {
+        const double rx = 1.0 / x;
+        if (wsmc_isfinite(x)) xnlo = -__builtin_fma(x, rx, -1.0) * rx;
+        x = rx;
+        n = -n;
+    }
+    while (n > 1) {
+        if (n & 1) {
+            const double err = __builtin_fma(y, xnlo, x * ynlo);
+            const double h = x * y;
+            ynlo = __builtin_fma(x, y, -h) + err;
+            y = h;
+        }
+        const double err = x * 2.0 * xnlo;
+        const double h = x * x;
+        xnlo = __builtin_fma(x, x, -h) + err;
+        x = h;
+        n >>= 1;
+    }
+    const double err = __builtin_fma(y, xnlo, x * ynlo);
+    return (wsmc_isfinite(x) && wsmc_isfinite(err)) ? __builtin_fma(x, y, err) : x * y;
+}
+
+/* a^b (Base.^(::Float64, ::Float64)): 1 for a == 1, NaN for a NaN b, an integer b as x^n,
+   else exp(b log a) — NaN for a < 0 (Julia throws a DomainError); relative error about
+   |b log a| 2^-53 beyond the restated exp / log (Julia's double-double log is tighter) */
+WSMC_HD double wsmc_pow(double a, double b) {
+    if (a == 1.0) return 1.0;
+    if (wsmc_isnan(b)) return b;
+    if (wsmc_fabs(b) < 4611686018427387904.0 && b == (double)(int64_t)b) return wsmc_powi(a, (int64_t)b);
+    return wsmc_exp(b * wsmc_log(a));
+}
+
 /* ------------------------------------------------------------------------- */
 /* draws                                                                      */
 /* ------------------------------------------------------------------------- */

@@ -40,6 +40,104 @@ WSMC_HD double wsmc_operand_eval(const wsmc_operand* o, double* const* cols, int
     return v;
 }
 
+/* ---- expressions (wsmc_assign_expr): one postfix program per output component ----------
+ * The operators of the fused broadcast `vectorize` emits (src/rewrites.jl:146-219), each a
+ * fixed IEEE sequence shared by the device and the oracle. */
+WSMC_HD double wsmc_xop1(int op, double a, double c) {
+    switch (op) {
+        case WSMC_X_NEG: return -a;
+        case WSMC_X_ABS: return wsmc_fabs(a);
+        case WSMC_X_SQRT: return a < 0.0 ? WSMC_NAN : wsmc_sqrt(a);
+        case WSMC_X_EXP: return wsmc_exp(a);
+        case WSMC_X_LOG: return wsmc_log(a);
+        case WSMC_X_LOG1P: return wsmc_log1p(a);
+        case WSMC_X_SIN: return wsmc_sin(a);
+        case WSMC_X_COS: return wsmc_cos(a);
+        case WSMC_X_POWI: return wsmc_powi(a, (int64_t)c);
+        case WSMC_X_NOT: return a == 0.0 ? 1.0 : 0.0;
+        default: return WSMC_NAN;
+    }
+}
+WSMC_HD double wsmc_xop2(int op, double a, double b) {
+    switch (op) {
+        case WSMC_X_ADD: return a + b;
+        case WSMC_X_SUB: return a - b;
+        case WSMC_X_MUL: return a * b;
+        case WSMC_X_DIV: return a / b;
+        case WSMC_X_MIN: return wsmc_min(a, b);
+        case WSMC_X_MAX: return wsmc_max(a, b);
+        case WSMC_X_POW: return wsmc_pow(a, b);
+        case WSMC_X_LT: return a < b ? 1.0 : 0.0;
+        case WSMC_X_LE: return a <= b ? 1.0 : 0.0;
+        case WSMC_X_GT: return a > b ? 1.0 : 0.0;
+        case WSMC_X_GE: return a >= b ? 1.0 : 0.0;
+        case WSMC_X_EQ: return a == b ? 1.0 : 0.0;
+        case WSMC_X_NE: return a != b ? 1.0 : 0.0;
+        case WSMC_X_AND: return (a != 0.0 && b != 0.0) ? 1.0 : 0.0;
+        case WSMC_X_OR: return (a != 0.0 || b != 0.0) ? 1.0 : 0.0;
+        default: return WSMC_NAN;
+    }
+}
+/* stack effect of one instruction (pops, pushes); pops < 0: not an operator */
+WSMC_HD int wsmc_xarity(int op) {
+    if (op == WSMC_X_CONST || op == WSMC_X_COL) return 0;
+    if (op >= WSMC_X_NEG && op <= WSMC_X_NOT) return 1;
+    if (op >= WSMC_X_ADD && op <= WSMC_X_OR) return 2;
+    if (op == WSMC_X_IFELSE) return 3;
+    return -1;
+}
+/* the program's shape (columns are the caller's to check): 0, or -1 for an unknown
+   operator, -2 a stack underflow, -3 more than WSMC_XSTACK_MAX values, -4 a component not
+   leaving one value, -5 too many instructions, -6 a POWI exponent that is no integer */
+WSMC_HD int wsmc_xprog_check(const wsmc_xinst* prog, const int32_t* len, int dim) {
+    int64_t total = 0;
+    for (int k = 0; k < dim; ++k) {
+        if (len[k] < 1) return -4;
+        total += len[k];
+    }
+    if (total > WSMC_XPROG_MAX) return -5;
+    int pc = 0;
+    for (int k = 0; k < dim; ++k) {
+        int sp = 0;
+        for (int e = pc + len[k]; pc < e; ++pc) {
+            const int a = wsmc_xarity(prog[pc].op);
+            if (a < 0) return -1;
+            if (sp < a) return -2;
+            sp += 1 - a;
+            if (sp > WSMC_XSTACK_MAX) return -3;
+            if (prog[pc].op == WSMC_X_POWI) {
+                const double c = prog[pc].c;
+                if (!(wsmc_fabs(c) < 4611686018427387904.0) || c != (double)(int64_t)c) return -6;
+            }
+        }
+        if (sp != 1) return -4;
+    }
+    return 0;
+}
+/* one component of one particle, a plain stack (the oracle's machine; the device keeps its
+   stack in registers and applies the same operators) */
+WSMC_HD double wsmc_xeval(const wsmc_xinst* p, int n, double* const* cols, int64_t N, int64_t i) {
+    double st[WSMC_XSTACK_MAX];
+    int sp = 0;
+    for (int k = 0; k < n; ++k) {
+        const int op = p[k].op;
+        if (op == WSMC_X_CONST) {
+            st[sp++] = p[k].c;
+        } else if (op == WSMC_X_COL) {
+            st[sp++] = cols[p[k].col][(int64_t)p[k].comp * N + i];
+        } else if (op == WSMC_X_IFELSE) {
+            const double f = st[--sp], t = st[--sp];
+            st[sp - 1] = st[sp - 1] != 0.0 ? t : f;
+        } else if (wsmc_xarity(op) == 1) {
+            st[sp - 1] = wsmc_xop1(op, st[sp - 1], p[k].c);
+        } else {
+            const double b = st[--sp];
+            st[sp - 1] = wsmc_xop2(op, st[sp - 1], b);
+        }
+    }
+    return st[0];
+}
+
 /* feat: the mean functions and families a caller may meet (WSMC_FEAT_OSC: the oscillator,
  * WSMC_FEAT_MVN: the full-covariance MvNormal). A device kernel launched without them passes
  * 0 (or OSC alone), so their code is not compiled into it (registers); every other caller

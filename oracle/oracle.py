@@ -61,6 +61,7 @@ _SIG = {
     "or_col_data": (_D, [_P, C.c_int32]),
     "or_store_resample": (None, [_P, _I32P]),
     "or_assign": (C.c_int, [_P, C.c_int32, _P]),
+    "or_assign_expr": (C.c_int, [_P, C.c_int32, _P, _P]),
     "or_sample": (C.c_int, [_P, C.c_int32, _P]),
     "or_sample_importance": (C.c_int, [_P, C.c_int32, _P, _P]),
     "or_observe": (C.c_int, [_P, _P, _P]),
@@ -333,6 +334,11 @@ class Oracle:
         arr = _operand_array(exprs)
         self._chk(self._L.or_assign(self._h, out, _addr(arr)))
         self.depth_bump = None
+
+    def assign_expr(self, out: int, prog, lens) -> None:
+        """prog: a ctypes XInst array (wsmc.dsl.xprogram), lens: the per-component lengths"""
+        ln = (C.c_int32 * 4)(*(list(lens) + [0] * (4 - len(lens))))
+        self._chk(self._L.or_assign_expr(self._h, int(out), _addr(prog), _addr(ln)))
 
     def sample(self, out: int, dist) -> None:
         self._chk(self._L.or_sample(self._h, out, _addr(dist)))

@@ -194,6 +194,24 @@ int or_assign(oracle* o, int32_t out, const wsmc_operand* expr) {
     return 0;
 }
 
+/* Assign of a general expression (src/transformers.jl:28-32 over the fused broadcast
+   src/rewrites.jl:146-219 emits): component k of every particle by wsmc_xeval */
+int or_assign_expr(oracle* o, int32_t out, const wsmc_xinst* prog, const int32_t* len) {
+    int64_t N = o->N;
+    int dim = o->cols[out].dim;
+    if (wsmc_xprog_check(prog, len, dim)) return -1;
+    double* tmp = o->tmp;
+    int pc = 0;
+    for (int k = 0; k < dim; ++k) {
+        for (int64_t i = 0; i < N; ++i)
+            tmp[(int64_t)k * N + i] = wsmc_xeval(prog + pc, len[k], o->colptr, N, i);
+        pc += len[k];
+    }
+    memcpy(o->cols[out].front, tmp, sizeof(double) * (size_t)(dim * N));
+    o->depth += 1;
+    return 0;
+}
+
 static void sample_into(oracle* o, int32_t out, const wsmc_dist* d, uint64_t op, double* tmp) {
     int64_t N = o->N;
     int dim = o->cols[out].dim;

@@ -66,6 +66,44 @@ def test_statement_batches_run_compiled(gpu_available, N):
     assert_same_state(g, o)
 
 
+@pytest.mark.parametrize("N", [4096, 3001])
+@pytest.mark.parametrize("reader", ["lagged_assign", "same_epoch_assign", "observe", "download", "resample_eager",
+                                    "move"])
+def test_unstored_sample_outputs_materialise_for_every_reader(gpu_available, N, reader):
+    """A Sample whose distribution reads no column keeps its values in the batch's rows and
+    writes the column only when something reads it (wsmc_ctx::VirtCol): through the ancestors
+    one Resample later, in the same epoch, as an Observe's value, by a download, by an eager
+    store's gather, by a Move's fold. Every reader sees the oracle's bits."""
+    from wsmc.dsl import Col, MvNormal, Normal, value_operands
+    g, o = wsmc.Context(N, seed=17), Oracle(N, seed=17)
+    for c in (g, o):
+        R = models.resolver(c)
+        cx = c.col_create("x", 2)
+        c.assign(cx, models._const([0.0, 0.5]))
+        cdv = c.col_create("dv", 2)
+        c.sample(cdv, MvNormal([0.0, 0.0], 0.3 * np.eye(2)).dist(R))      # unstored on the device
+        c.assign(cx, value_operands(Col("x") + Col("dv"), 2, R))           # reads dv from rows
+        c.observe(MvNormal(Col("x"), 0.5 * np.eye(2)).dist(R), models._const([0.3, -0.2]))
+        if reader == "resample_eager" and c is g:   # (the oracle's store is the eager ColumnStore)
+            c.store_set_lazy(False)
+        c.resample(1.0, abi.RESAMPLE_STRATIFIED, wait=False)
+        cy = c.col_create("y", 2)
+        if reader == "lagged_assign":      # dv one Resample behind, read through its ancestors
+            c.assign(cy, value_operands(Col("dv") * 2.0, 2, R))
+        elif reader == "same_epoch_assign":
+            c.sample(cdv, MvNormal([0.0, 0.0], 0.2 * np.eye(2)).dist(R))   # a new unstored dv
+            c.assign(cy, value_operands(Col("dv") + Col("x"), 2, R))
+        elif reader == "observe":
+            c.observe(MvNormal(Col("dv"), 1.0 * np.eye(2)).dist(R), models._const([0.1, 0.1]))
+        elif reader == "move":
+            ca = c.col_create("a", 1)
+            c.sample(ca, Normal(0.0, 1.0).dist(R))                             # unstored, then folded
+            c.observe(Normal(Col("a"), 1.0).dist(R), models._const([0.4]))
+            c.resample(1.0, abi.RESAMPLE_STRATIFIED, wait=False)
+            c.move(abi.PROPOSAL_AUTORW, [ca], 1e-3)
+    assert_same_state(g, o)
+
+
 @pytest.mark.parametrize("N", [1024, 5001])
 @pytest.mark.parametrize("ess", [1.0, 0.5])
 @pytest.mark.parametrize("keep", [True, False])

@@ -65,6 +65,7 @@ int fail(int code, const std::string& msg) {
     do {                                                                 \
         CHECK_CTX_EW(ctx);                                               \
         if (int _r = ew_flush(ctx)) return _r;                           \
+        if (int _r = virt_all(ctx)) return _r;                           \
     } while (0)
 #define CHECK_CTX(ctx)                                                   \
     do {                                                                 \
@@ -96,8 +97,9 @@ static int ew_flush(wsmc_ctx* c) {
     // the batch's signature compiled for its shape (csrc/wsmc_jit.hip); without it a batch of
     // one statement runs its own kernel (leaner than the interpreter's: no rows, no table)
     hipError_t e = launch_ew_jit(c->stream, *b, c->ew_feat, c->seed, c->goff, c->N, c->device);
+    const bool launched_jit = e != hipErrorNotSupported;
     const EwOp& o0 = b->ops[0];
-    if (e != hipErrorNotSupported)
+    if (launched_jit)
         ;
     else if (b->nops > 1)
         e = launch_ew_batch(c->stream, *b, c->ew_feat, c->seed, c->goff, c->N);
@@ -107,6 +109,12 @@ static int ew_flush(wsmc_ctx* c) {
         e = launch_sample(c->stream, o0.out, o0.dim, c->ew_first.dist, c->seed, o0.s.op, c->goff, c->d_colptr, c->N);
     else
         e = launch_weigh(c->stream, c->ew_first, b->w, c->d_colptr, c->N, b->ms, b->ms_next, b->wreset);
+    // the compiled batch and the interpreter leave nostore outputs unwritten (a batch of one
+    // on its own kernel writes them): they become VirtCol entries
+    const bool honoured = launched_jit || b->nops > 1;
+    for (auto& v : c->ew_virt)
+        if (honoured) c->virt.push_back(v);
+    c->ew_virt.clear();
     b->nops = b->ntab = b->has_w = b->nslots = b->nrows = b->npre = 0;
     b->anc = nullptr;
     b->dec = nullptr;
@@ -124,6 +132,45 @@ static EwBatch* ew_open(wsmc_ctx* c) {
     }
     return c->ew;
 }
+// ---- unstored Sample outputs (wsmc_ctx::VirtCol) ------------------------------------------
+// write column `col`'s values now: the Sample kernel of its entry, into the buffer it would
+// have written (the same function of the same seed, op and particle indices: the same bits)
+static int virt_write(wsmc_ctx* c, const wsmc_ctx::VirtCol& v) {
+    if (c->cols[v.col].front != v.buf)
+        return fail(WSMC_ESTATE, "unstored Sample output of column " + c->cols[v.col].name + " lost its buffer");
+    WSMC_HIP(launch_sample(c->stream, const_cast<double*>(v.buf), v.d.dim, v.d, c->seed, v.op, c->goff, c->d_colptr,
+                           c->N));
+    return WSMC_OK;
+}
+// a statement or a kernel is about to read `col`: materialise it if its Sample left it unstored
+static int virt_one(wsmc_ctx* c, int32_t col) {
+    for (size_t k = 0; k < c->virt.size(); ++k)
+        if (c->virt[k].col == col) {
+            const wsmc_ctx::VirtCol v = c->virt[k];
+            c->virt.erase(c->virt.begin() + (long)k);
+            return virt_write(c, v);
+        }
+    return WSMC_OK;
+}
+static int virt_all(wsmc_ctx* c) {
+    while (!c->virt.empty()) {
+        const wsmc_ctx::VirtCol v = c->virt.back();
+        c->virt.pop_back();
+        if (int r = virt_write(c, v)) return r;
+    }
+    return WSMC_OK;
+}
+// `col` is about to be overwritten in full: its unstored values (of a launched batch or of the
+// open one, whose later statements read them from rows) are never needed
+static void virt_drop(wsmc_ctx* c, int32_t col) {
+    for (auto* v : {&c->virt, &c->ew_virt})
+        for (size_t k = 0; k < v->size(); ++k)
+            if ((*v)[k].col == col) {
+                v->erase(v->begin() + (long)k);
+                break;
+            }
+}
+
 static bool ew_reads_lagged(const wsmc_ctx* c, int32_t col) {
     for (int32_t x : c->ew_lag)
         if (x == col) return true;
@@ -312,6 +359,8 @@ static void scores_touch(wsmc_ctx* c, int32_t col) {
 // The gathered columns' values become those of epoch `to_epoch`.
 static int gather_columns(wsmc_ctx* c, const std::vector<int32_t>& which, const int32_t* anc, const Decision* dec,
                           double* w_reset, int64_t to_epoch) {
+    for (int32_t id : which)
+        if (int r = virt_one(c, id)) return r;
     GatherSet gs;
     gs.n = 0;
     gs.tab = c->d_colptr;   // the kernel moves each gathered column's table entry to its new front
@@ -405,6 +454,12 @@ static void set_anc_last(wsmc_ctx* c, const AncRow* row, int64_t epoch) {
 // the newest entry back to the oldest a stale column needs (kTraceLev entries per launch,
 // the composed index carried between launches), each column read where its epoch is reached.
 static int materialize(wsmc_ctx* c, const std::vector<int32_t>* only) {
+    if (only) {   // an unstored Sample output is written before it is traced
+        for (int32_t id : *only)
+            if (int r = virt_one(c, id)) return r;
+    } else if (int r = virt_all(c)) {
+        return r;
+    }
     std::vector<std::pair<int64_t, int32_t>> stale;   // (levels to apply, column)
     std::vector<char> want(c->cols.size(), only ? 0 : 1);
     if (only)
@@ -1960,6 +2015,12 @@ int wsmc_assign(wsmc_ctx* c, int32_t out, const wsmc_operand* expr) {
         int r = check_operand(c, expr[k]);
         if (r) return r;
     }
+    // an operand column its Sample left unstored is written first; the output is overwritten
+    for (int k = 0; k < dim; ++k)
+        for (int m = 0; m < 2; ++m)
+            if (expr[k].col[m] >= 0)
+                if (int rv = virt_one(c, expr[k].col[m])) return rv;
+    virt_drop(c, out);
     // operand columns one Resample behind are read through that Resample's ancestors inside
     // the kernel (no materialising pass); any further behind are brought up to date first
     std::vector<int32_t> deep;
@@ -2054,6 +2115,81 @@ int wsmc_assign(wsmc_ctx* c, int32_t out, const wsmc_operand* expr) {
     return WSMC_OK;
 }
 
+// Assign of a general expression (include/wsmc.h): the program checked on the host, its column
+// reads resolved to component pointers; columns one lazy Resample behind are read through that
+// Resample's ancestors (deeper ones are brought up to date first), as wsmc_assign's
+int wsmc_assign_expr(wsmc_ctx* c, int32_t out, const wsmc_xinst* prog, const int32_t* len) {
+    if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { return wsmc_assign_expr(x, out, prog, len); });
+    CHECK_CTX_EW(c);   // reads and writes no weights: a pending reset stays pending
+    if (!valid_col(c, out) || !prog || !len) return fail(WSMC_EARG, "bad output column or program");
+    const int dim = c->cols[out].dim;
+    static const char* const kWhy[] = {"", "an unknown operator", "a stack underflow",
+                                       "more than WSMC_XSTACK_MAX values on the stack",
+                                       "a component program that does not leave one value",
+                                       "more than WSMC_XPROG_MAX instructions", "a POWI exponent that is no integer"};
+    if (int e = wsmc_xprog_check(prog, len, dim)) return fail(WSMC_EARG, std::string("expression: ") + kWhy[-e]);
+    int total = 0;
+    for (int k = 0; k < dim; ++k) total += len[k];
+    std::vector<int32_t> reads;
+    for (int q = 0; q < total; ++q) {
+        if (prog[q].op != WSMC_X_COL) continue;
+        const int32_t id = prog[q].col;
+        if (!valid_col(c, id)) return fail(WSMC_EARG, "expression references an unknown column");
+        if (prog[q].comp < 0 || prog[q].comp >= c->cols[id].dim)
+            return fail(WSMC_EARG, "expression component out of range for column " + c->cols[id].name);
+        reads.push_back(id);
+    }
+    // the statement batch runs first (program order); unstored Sample outputs read here are
+    // written, the output's is dropped (overwritten)
+    if (int r = ew_flush(c)) return r;
+    for (int32_t id : reads)
+        if (int r = virt_one(c, id)) return r;
+    virt_drop(c, out);
+    std::vector<int32_t> deep;
+    for (int32_t id : reads)
+        if (c->cols[id].epoch < c->epoch - 1) deep.push_back(id);
+    int r = deep.empty() ? WSMC_OK : materialize(c, &deep);
+    if (!r) r = upload_colptr(c);
+    if (r) return r;
+    XProg x;
+    std::memset(&x, 0, sizeof(x));
+    x.N = c->N;
+    x.dim = dim;
+    x.tab_col = -1;
+    for (int k = 0; k < dim; ++k) x.len[k] = len[k];
+    bool out_read_behind = false;
+    for (int q = 0; q < total; ++q) {
+        XIns& I = x.ins[q];
+        I.op = prog[q].op;
+        I.c = prog[q].c;
+        if (I.op != WSMC_X_COL) continue;
+        const int32_t id = prog[q].col;
+        c->cols[id].touch = c->epoch;
+        I.p = c->cols[id].front + (int64_t)prog[q].comp * c->N;
+        I.lag = c->cols[id].epoch < c->epoch;
+        x.any_lag |= I.lag;
+        out_read_behind |= I.lag && id == out;
+    }
+    if (x.any_lag) {
+        const AncRow& nr = c->alog.back();   // entry epoch - 1 (kept alive by the stale column)
+        x.row = nr.anc;
+        x.dec = nr.dec;
+    }
+    x.out = c->cols[out].front;
+    if (out_read_behind) {   // out read through the ancestors: write a fresh buffer (no read/write race)
+        x.out = c->cols[out].back;
+        x.tab_col = out;
+        x.tab = c->d_colptr;
+        std::swap(c->cols[out].front, c->cols[out].back);
+    }
+    scores_touch(c, out);
+    wrote_col(c, out);
+    WSMC_HIP(launch_assign_expr(c->stream, x));
+    gc_log(c);
+    c->depth += 1;
+    return WSMC_OK;
+}
+
 static void push_sample_term(wsmc_ctx* c, int32_t out, const wsmc_dist& d) {
     wsmc_term t;
     std::memset(&t, 0, sizeof(t));
@@ -2073,6 +2209,9 @@ int wsmc_sample(wsmc_ctx* c, int32_t out, const wsmc_dist* d) {
     if (d->dim != c->cols[out].dim) return fail(WSMC_EARG, "dist dim != column dim");
     std::vector<int32_t> reads;
     cols_of(*d, reads);
+    for (int32_t id : reads)
+        if ((r = virt_one(c, id))) return r;
+    virt_drop(c, out);   // overwritten in full: earlier unstored values are never needed
     if ((r = need_cols(c, reads))) return r;
     if ((r = upload_colptr(c))) return r;
     const uint64_t op = c->op++;
@@ -2106,6 +2245,15 @@ int wsmc_sample(wsmc_ctx* c, int32_t out, const wsmc_dist* d) {
         eo.s.sd = eo.s.has_sd ? wsmc_sqrt(wsmc_operand_eval(&d->scale, nullptr, c->N, 0, nullptr)) : 0.0;
         if (d->mean_fn == WSMC_MEAN_OSCILLATOR) c->ew_feat |= WSMC_FEAT_OSC;
         if (d->family == WSMC_FAM_MVNORMAL) c->ew_feat |= WSMC_FEAT_MVN;
+        // a distribution that reads no column: the values are a function of (seed, op,
+        // particle), kept in the batch's rows and written only when read (lazy store: a
+        // Resample gathers nothing). WSMC_DIAG_STORE_SAMPLES=1 stores them (A/B)
+        static const bool store_all = [] {
+            const char* e = getenv("WSMC_DIAG_STORE_SAMPLES");
+            return e && atoi(e) != 0;
+        }();
+        eo.nostore = (int16_t)(reads.empty() && c->lazy && eo.out_row >= 0 && !store_all);
+        if (eo.nostore) c->ew_virt.push_back({out, eo.out, *d, op});
         b->nops += 1;
     }
     scores_touch(c, out);
@@ -2160,6 +2308,8 @@ static int weigh(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x, int kin
     wsmc_osc_link(c->tape.empty() ? nullptr : &c->tape.back(), &t);   // before its first evaluation
     std::vector<int32_t> reads;
     cols_of(t, reads);
+    for (int32_t id : reads)
+        if ((r = virt_one(c, id))) return r;
     if ((r = need_cols(c, reads))) return r;
     if ((r = upload_colptr(c))) return r;
     int wb = c->wnext;
@@ -2263,6 +2413,8 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
         return WSMC_OK;
     }
     if (int r = ew_flush(c)) return r;
+    if (!c->lazy || is_sharded(c))   // every column gathered now: the unstored ones written first
+        if (int r = virt_all(c)) return r;
     if (c->w_reset_pending) {   // (a weight write settles it first, so this does not happen)
         WSMC_HIP(launch_fill_weights(c->stream, c->w, c->w_reset_pending, c->N));
         c->w_reset_pending = nullptr;

@@ -53,7 +53,8 @@ struct EwWeigh {
     wsmc_logmemo lm0;           // a constant scale's log / reciprocal (host-evaluated)
 };
 struct EwOp {
-    int32_t kind;               // 0 Assign, 1 Sample, 2 Observe / Weight
+    int16_t kind;               // 0 Assign, 1 Sample, 2 Observe / Weight
+    int16_t nostore;            // a Sample whose output is recomputed when read (VirtCol): rows only
     int16_t dim;
     int16_t out_row;            // >= 0: the output's components also go to LDS rows out_row..
                                 // (later statements of the batch read them there)

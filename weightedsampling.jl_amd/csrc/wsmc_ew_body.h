@@ -28,7 +28,7 @@ namespace wsmc {
 enum : int8_t { kSrcNone = 0, kSrcRow = 1, kSrcMem = 2, kSrcLag = 3 };
 struct EwSigOp {
     int8_t kind, dim, out_row;          // EwOp's; out_row -1: the output has no rows
-    int8_t family, mean_fn, ddim, has_sd, pad;
+    int8_t family, mean_fn, ddim, has_sd, nostore;   // nostore: the output stays in its rows
     int8_t asrc[4][2];                  // Assign operand (component q, column c): kSrc*
     int8_t arow[4][2];                  // ... its row (kSrcRow)
     int8_t mrow[4][2];                  // Sample / weight dist mean operands: row (-1: no column)
@@ -162,7 +162,7 @@ __device__ __forceinline__ void ew_op(const EwBatch* B, EwLanes<P>& L, uint64_t 
         double v[P];
 #pragma unroll
         for (int p = 0; p < P; ++p) v[p] = x[p][q];
-        ew_store<P>(op.out + (int64_t)q * N, i0, v);
+        if constexpr (!o.nostore) ew_store<P>(op.out + (int64_t)q * N, i0, v);
         if (o.out_row >= 0)
 #pragma unroll
             for (int p = 0; p < P; ++p) L.r[p][o.out_row + q] = v[p];

@@ -234,6 +234,19 @@ struct wsmc_ctx {
     };
     std::vector<EwRow> ew_rows;
     std::vector<const double*> ew_unstaged; // outputs of the batch without rows (no later LDS reads)
+    // Sample outputs not stored (EwOp.nostore): a Sample whose distribution reads no column
+    // (dv ~ MvNormal(0, 0.1 I)) has values that are a function of (seed, op, particle) alone,
+    // so the batch keeps them in rows for its later statements and the column is written only
+    // if something reads it before the next full overwrite (the next step's Sample): VirtCol
+    // entries, materialised by every reader (virt_*), dropped by an overwrite
+    struct VirtCol {
+        int32_t col;
+        const double* buf;                  // the column's front when sampled (checked on use)
+        wsmc_dist d;
+        uint64_t op;
+    };
+    std::vector<VirtCol> virt;              // launched batches' unstored Sample outputs
+    std::vector<VirtCol> ew_virt;           // ... of the open batch (moved to virt at its launch)
     wsmc_term ew_first;                     // the batch's first statement as called (a batch of one
                                             // launches the statement's own kernel)
     char* prog_stage = nullptr;             // pinned staging ring of the programs too large to ride
@@ -331,6 +344,24 @@ struct Indirect {
 };
 hipError_t launch_assign(hipStream_t s, double* out, int dim, const wsmc_operand* expr,
                          double* const* cols, int64_t N, const Indirect& ind);
+// Assign of a general expression (wsmc_assign_expr): the program with its column reads resolved
+// to component pointers; lag = read through `row` (one lazy Resample behind)
+struct XIns {
+    int32_t op, lag;
+    const double* p;   // WSMC_X_COL: the component
+    double c;
+};
+struct XProg {
+    double* out;
+    int64_t N;
+    const int32_t* row;
+    const Decision* dec;
+    double** tab;      // tab_col >= 0: `out` becomes that column's table entry
+    int32_t tab_col, dim, any_lag, pad;
+    int32_t len[4];
+    XIns ins[WSMC_XPROG_MAX];
+};
+hipError_t launch_assign_expr(hipStream_t s, const XProg& x);
 // the statement batch (csrc/wsmc_ew.h) on the interpreter kernel, or on its signature's kernel
 // compiled at run time (csrc/wsmc_jit.hip; hipErrorNotSupported: none, run the interpreter)
 hipError_t launch_ew_jit(hipStream_t s, const EwBatch& b, unsigned feat, uint64_t seed, int64_t goff, int64_t N,

@@ -97,7 +97,8 @@ EwSig signature(const EwBatch& b, unsigned feat) {
         o.kind = (int8_t)op.kind;
         o.dim = (int8_t)op.dim;
         o.out_row = (int8_t)op.out_row;
-        o.family = o.mean_fn = o.ddim = o.has_sd = o.pad = 0;
+        o.family = o.mean_fn = o.ddim = o.has_sd = 0;
+        o.nostore = (int8_t)(op.kind == 1 && op.nostore);
         for (int q = 0; q < 4; ++q)
             for (int m = 0; m < 2; ++m) {
                 o.asrc[q][m] = kSrcNone;
@@ -148,7 +149,8 @@ std::string sig_text(const EwSig& g) {
     for (int k = 0; k < kEwOps; ++k) {
         const EwSigOp& o = g.op[k];
         s += '{';
-        num(o.kind); num(o.dim); num(o.out_row); num(o.family); num(o.mean_fn); num(o.ddim); num(o.has_sd); num(0);
+        num(o.kind); num(o.dim); num(o.out_row); num(o.family); num(o.mean_fn); num(o.ddim); num(o.has_sd);
+        num(o.nostore);
         s += '{'; for (int q = 0; q < 4; ++q) arr(o.asrc[q], 2); s += "},";
         s += '{'; for (int q = 0; q < 4; ++q) arr(o.arow[q], 2); s += "},";
         s += '{'; for (int q = 0; q < 4; ++q) arr(o.mrow[q], 2); s += "},";
@@ -318,7 +320,7 @@ int ew_jit_selfcheck(std::string& err) {
         o.mean_fn = 0;
         o.ddim = (int8_t)(o.kind == 0 ? 0 : 2);
         o.has_sd = (int8_t)(k == 1);
-        o.pad = 0;
+        o.nostore = 0;
         for (int q = 0; q < 4; ++q)
             for (int m = 0; m < 2; ++m) {
                 o.asrc[q][m] = (o.kind == 0 && q < 2) ? kSrcRow : kSrcNone;

@@ -205,6 +205,51 @@ __global__ __launch_bounds__(kBlock) void k_assign(double* out, int dim, AssignA
         if (k < dim) out[(int64_t)k * N + i] = x[k];
 }
 
+// Assign of a general expression (wsmc_assign_expr; the fused broadcast of src/rewrites.jl:146-219
+// into src/transformers.jl:28-32). The program (XProg, the only argument) is read in place through
+// the kernarg segment pointer: every lane runs the same instruction, so the loads are scalar and
+// the branches uniform, and the stack index is uniform too (the stack stays in registers, indexed
+// through M0). Each operator is wsmc_xop1 / wsmc_xop2, as in the oracle's wsmc_xeval; a COL read
+// with `lag` goes through the newest log entry's ancestors (k_assign's gather-on-read).
+__global__ __launch_bounds__(kBlock) void k_assign_expr(XProg) {
+    const XProg* X = (const XProg*)(const char*)__builtin_amdgcn_kernarg_segment_ptr();
+    const int64_t N = X->N;
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= N) return;
+    if (i == 0 && X->tab_col >= 0) X->tab[X->tab_col] = X->out;
+    const int64_t j = (X->any_lag && (!X->dec || X->dec->resampled)) ? (int64_t)X->row[i] : i;
+    int pc = 0;
+    double res[4];   // every component before any store: a component may read another of `out`
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (k >= X->dim) break;
+        double st[WSMC_XSTACK_MAX];
+        int sp = 0;
+        for (const int e = pc + X->len[k]; pc < e; ++pc) {
+            const XIns& I = X->ins[pc];
+            const int op = I.op;
+            if (op == WSMC_X_CONST) {
+                st[sp++] = I.c;
+            } else if (op == WSMC_X_COL) {
+                st[sp++] = I.p[I.lag ? j : i];
+            } else if (op == WSMC_X_IFELSE) {
+                const double f = st[sp - 1], t = st[sp - 2];
+                sp -= 2;
+                st[sp - 1] = st[sp - 1] != 0.0 ? t : f;
+            } else if (op < WSMC_X_ADD) {
+                st[sp - 1] = wsmc_xop1(op, st[sp - 1], I.c);
+            } else {
+                const double b = st[--sp];
+                st[sp - 1] = wsmc_xop2(op, st[sp - 1], b);
+            }
+        }
+        res[k] = st[0];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (k < X->dim) X->out[(int64_t)k * N + i] = res[k];
+}
+
 // FEAT (wsmc_terms.h): WSMC_FEAT_ALL, WSMC_FEAT_OSC, or 0 for affine means (no oscillator or
 // full-covariance code: registers)
 template <unsigned FEAT>
@@ -339,9 +384,10 @@ __global__ __launch_bounds__(kBlock) void k_ew_batch(EwBatch, uint64_t seed, int
                 wv = wv + wsmc_term_logpdf_mf(&op.w.t, cols, kBlock, th, nullptr, &lm, FEAT);
                 continue;
             }
+            if (!op.nostore)
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (q < dim) op.out[(int64_t)q * N + i] = x[q];
+                for (int q = 0; q < 4; ++q)
+                    if (q < dim) op.out[(int64_t)q * N + i] = x[q];
             if (op.out_row >= 0)
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
@@ -3108,6 +3154,12 @@ hipError_t launch_assign(hipStream_t s, double* out, int dim, const wsmc_operand
             a.p[k][m] = a.e[k].col[m] >= 0 ? ind.front[a.e[k].col[m]] + (int64_t)a.e[k].comp[m] * N : nullptr;
     }
     hipLaunchKernelGGL(k_assign, grid_for(N), dim3(kBlock), 0, s, out, dim, a, cols, N, ind);
+    return hipGetLastError();
+}
+hipError_t launch_assign_expr(hipStream_t s, const XProg& x) {
+    static_assert(sizeof(XProg) + 32 <= 4096, "the program rides in the kernel arguments");
+    if (x.N <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_assign_expr, grid_for(x.N), dim3(kBlock), 0, s, x);
     return hipGetLastError();
 }
 hipError_t launch_sample(hipStream_t s, double* out, int dim, const wsmc_dist& d, uint64_t seed, uint64_t op,

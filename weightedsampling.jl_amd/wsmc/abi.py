@@ -44,6 +44,19 @@ class Operand(C.Structure):
         return o
 
 
+class XInst(C.Structure):
+    """wsmc_xinst: one instruction of a wsmc_assign_expr postfix program"""
+    _fields_ = [("op", C.c_int32), ("col", C.c_int32), ("comp", C.c_int32), ("reserved", C.c_int32),
+                ("c", C.c_double)]
+
+
+# wsmc_xop (include/wsmc.h)
+X_CONST, X_COL, X_NEG, X_ABS, X_SQRT, X_EXP, X_LOG, X_LOG1P, X_SIN, X_COS, X_POWI, X_NOT = range(12)
+X_ADD, X_SUB, X_MUL, X_DIV, X_MIN, X_MAX, X_POW, X_LT, X_LE, X_GT, X_GE, X_EQ, X_NE, X_AND, X_OR, \
+    X_IFELSE = range(16, 32)
+XPROG_MAX, XSTACK_MAX = 96, 8
+
+
 class Dist(C.Structure):
     _fields_ = [("family", C.c_int32), ("mean_fn", C.c_int32), ("dim", C.c_int32),
                 ("reserved", C.c_int32), ("mu", Operand * 4), ("scale", Operand),
@@ -118,6 +131,7 @@ SIGNATURES = {
     "wsmc_sample_particles": (C.c_int, [_P, C.c_int64, C.c_int32, C.POINTER(C.c_int64)]),
     "wsmc_col_gather_rows": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_int64), C.c_int64, _D]),
     "wsmc_assign": (C.c_int, [_P, C.c_int32, C.POINTER(Operand)]),
+    "wsmc_assign_expr": (C.c_int, [_P, C.c_int32, C.POINTER(XInst), _I32P]),
     "wsmc_sample": (C.c_int, [_P, C.c_int32, C.POINTER(Dist)]),
     "wsmc_sample_importance": (C.c_int, [_P, C.c_int32, C.POINTER(Dist), C.POINTER(Dist)]),
     "wsmc_observe": (C.c_int, [_P, C.POINTER(Dist), C.POINTER(Operand)]),

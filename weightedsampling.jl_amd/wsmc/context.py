@@ -273,6 +273,12 @@ class Context:
     def assign(self, out: int, exprs) -> None:
         check(self._L.wsmc_assign(self._h, int(out), _operands4(exprs)))
 
+    def assign_expr(self, out: int, prog, lens) -> None:
+        """wsmc_assign_expr: prog a ctypes XInst array (wsmc.dsl.xprogram), lens the
+        per-component program lengths"""
+        ln = (C.c_int32 * 4)(*(list(lens) + [0] * (4 - len(lens))))
+        check(self._L.wsmc_assign_expr(self._h, int(out), prog, ln))
+
     def sample(self, out: int, dist: Dist) -> None:
         check(self._L.wsmc_sample(self._h, int(out), C.byref(dist)))
 

@@ -39,11 +39,18 @@ class Expr:
             return v
         if isinstance(v, (int, float, np.floating, np.integer)):
             return Expr(float(v), ())
+        if isinstance(v, Fx):
+            raise TypeError("a distribution argument must be affine in at most two columns (the "
+                            "operand form); assign the general expression to a column first")
         raise TypeError(f"cannot use {v!r} as a particle argument")
 
     def __add__(self, o):
+        if isinstance(o, Fx):
+            return Fx.lift(self) + o
         o = Expr.lift(o)
-        return Expr(self.c0 + o.c0, self.terms + o.terms)._checked()
+        if len(self.terms) + len(o.terms) > 2:   # beyond the operand form: a general expression
+            return Fx.lift(self) + Fx.lift(o)
+        return Expr(self.c0 + o.c0, self.terms + o.terms)
 
     __radd__ = __add__
 
@@ -51,28 +58,55 @@ class Expr:
         return Expr(-self.c0, tuple((n, c, -k) for n, c, k in self.terms))
 
     def __sub__(self, o):
+        if isinstance(o, Fx):
+            return Fx.lift(self) - o
         return self + (-Expr.lift(o))
 
     def __rsub__(self, o):
         return Expr.lift(o) + (-self)
 
+    # the non-affine operators give general expressions (Assign only: wsmc_assign_expr)
+    def __truediv__(self, o):
+        return Fx.lift(self) / o
+
+    def __rtruediv__(self, o):
+        return Fx.lift(o) / Fx.lift(self)
+
+    def __pow__(self, o):
+        return Fx.lift(self) ** o
+
+    def __rpow__(self, o):
+        return Fx.lift(o) ** Fx.lift(self)
+
+    def __abs__(self):
+        return abs(Fx.lift(self))
+
+    def __lt__(self, o):
+        return Fx.lift(self) < o
+
+    def __le__(self, o):
+        return Fx.lift(self) <= o
+
+    def __gt__(self, o):
+        return Fx.lift(self) > o
+
+    def __ge__(self, o):
+        return Fx.lift(self) >= o
+
     def __mul__(self, k):
+        if isinstance(k, Fx):
+            return Fx.lift(self) * k
         if isinstance(k, Expr):
             if not k.terms:
                 k = k.c0
             elif not self.terms:
                 return k * self.c0
-            else:
-                raise TypeError("products of two particle columns are not affine")
+            else:   # a product of two particle columns: a general expression
+                return Fx.lift(self) * Fx.lift(k)
         k = float(k)
         return Expr(self.c0 * k, tuple((n, c, coef * k) for n, c, coef in self.terms))
 
     __rmul__ = __mul__
-
-    def _checked(self) -> "Expr":
-        if len(self.terms) > 2:
-            raise ValueError("device argument forms support at most two column terms")
-        return self
 
     def operand(self, resolve) -> Operand:
         o = Operand.const(self.c0)
@@ -203,3 +237,149 @@ def MvNormal(mu, cov) -> Kernel:
 
 def value_operands(v, dim: int, resolve) -> list[Operand]:
     return [e.operand(resolve) for e in _exprs(v, dim)]
+
+
+# ---------------------------------------------------------------------------------------
+# general expressions (wsmc_assign_expr)
+# ---------------------------------------------------------------------------------------
+_COMMUTATIVE = (abi.X_ADD, abi.X_MUL)
+
+
+class Fx:
+    """A general particle expression: the fused broadcast `vectorize` emits for an Assign's
+    right-hand side (src/rewrites.jl:146-219) — calls, `cond ? a : b` (ifelse), `||` / `&&`,
+    comparisons — as a tree over columns and constants, lowered to wsmc_assign_expr's postfix
+    program. Booleans are 1.0 / 0.0 (the columns are Float64)."""
+
+    __slots__ = ("op", "args", "c", "col", "comp")
+
+    def __init__(self, op: int, args=(), c: float = 0.0, col=None, comp: int = 0):
+        self.op, self.args, self.c, self.col, self.comp = int(op), tuple(args), float(c), col, int(comp)
+
+    @staticmethod
+    def lift(v) -> "Fx":
+        if isinstance(v, Fx):
+            return v
+        if isinstance(v, (bool, np.bool_)):
+            return Fx(abi.X_CONST, c=1.0 if v else 0.0)
+        if isinstance(v, (int, float, np.floating, np.integer)):
+            return Fx(abi.X_CONST, c=float(v))
+        if isinstance(v, Expr):
+            # the affine form's terms in order (x, coef * x, -x), its constant last when nonzero
+            e = None
+            for name, comp, coef in v.terms:
+                x = Fx(abi.X_COL, col=name, comp=comp)
+                t = x if coef == 1.0 else (Fx(abi.X_NEG, (x,)) if coef == -1.0 else
+                                           Fx(abi.X_MUL, (Fx(abi.X_CONST, c=coef), x)))
+                e = t if e is None else Fx(abi.X_ADD, (e, t))
+            if e is None:
+                return Fx(abi.X_CONST, c=v.c0)
+            return Fx(abi.X_ADD, (e, Fx(abi.X_CONST, c=v.c0))) if v.c0 != 0.0 else e
+        raise TypeError(f"cannot use {v!r} in a particle expression")
+
+    def _bin(self, op, o, swap=False):
+        a, b = (Fx.lift(o), self) if swap else (self, Fx.lift(o))
+        return Fx(op, (a, b))
+
+    __add__ = lambda s, o: s._bin(abi.X_ADD, o)
+    __radd__ = lambda s, o: s._bin(abi.X_ADD, o, True)
+    __sub__ = lambda s, o: s._bin(abi.X_SUB, o)
+    __rsub__ = lambda s, o: s._bin(abi.X_SUB, o, True)
+    __mul__ = lambda s, o: s._bin(abi.X_MUL, o)
+    __rmul__ = lambda s, o: s._bin(abi.X_MUL, o, True)
+    __truediv__ = lambda s, o: s._bin(abi.X_DIV, o)
+    __rtruediv__ = lambda s, o: s._bin(abi.X_DIV, o, True)
+    __lt__ = lambda s, o: s._bin(abi.X_LT, o)
+    __le__ = lambda s, o: s._bin(abi.X_LE, o)
+    __gt__ = lambda s, o: s._bin(abi.X_GT, o)
+    __ge__ = lambda s, o: s._bin(abi.X_GE, o)
+    __neg__ = lambda s: Fx(abi.X_NEG, (s,))
+    __abs__ = lambda s: Fx(abi.X_ABS, (s,))
+
+    def __pow__(self, o):
+        if isinstance(o, (int, np.integer)) and not isinstance(o, bool):   # x^n (Base.literal_pow / pow_body)
+            return Fx(abi.X_POWI, (self,), c=float(o))
+        return self._bin(abi.X_POW, o)
+
+    def __rpow__(self, o):
+        return self._bin(abi.X_POW, o, True)
+
+    def __bool__(self):
+        raise TypeError("a particle expression has no truth value on the host; use ifelse / and_ / or_")
+
+    # ---- lowering ----
+    def _need(self) -> int:
+        """stack values needed to evaluate (Sethi–Ullman, with the operand order _emit uses)"""
+        if not self.args:
+            return 1
+        if self.op in _COMMUTATIVE:
+            a, b = sorted((x._need() for x in self.args), reverse=True)
+            return max(a, b + 1)
+        return max(x._need() + k for k, x in enumerate(self.args))
+
+    def _emit(self, resolve, out: list) -> None:
+        args = self.args
+        if self.op in _COMMUTATIVE and args[1]._need() > args[0]._need():
+            args = (args[1], args[0])   # a + b == b + a, a * b == b * a bit for bit: the deeper first
+        for a in args:
+            a._emit(resolve, out)
+        col = resolve(self.col) if self.op == abi.X_COL else -1
+        out.append((self.op, col, self.comp if self.op == abi.X_COL else 0, self.c))
+
+    def columns(self):
+        if self.op == abi.X_COL:
+            return [self.col]
+        return [n for a in self.args for n in a.columns()]
+
+    def __repr__(self):
+        if self.op == abi.X_CONST:
+            return repr(self.c)
+        if self.op == abi.X_COL:
+            return f"Col({self.col!r}, {self.comp})" if self.comp else f"Col({self.col!r})"
+        return f"Fx({self.op}, {self.args!r}{', c=%r' % self.c if self.op == abi.X_POWI else ''})"
+
+
+def _un(op):
+    return lambda x: Fx(op, (Fx.lift(x),))
+
+
+exp, log, log1p, sqrt, sin, cos, not_ = (_un(o) for o in (abi.X_EXP, abi.X_LOG, abi.X_LOG1P, abi.X_SQRT, abi.X_SIN,
+                                                       abi.X_COS, abi.X_NOT))
+exp.__doc__ = "exp.(x)"
+
+
+def _bin2(op):
+    return lambda a, b: Fx(op, (Fx.lift(a), Fx.lift(b)))
+
+
+min_, max_, eq, ne, and_, or_ = (_bin2(o) for o in (abi.X_MIN, abi.X_MAX, abi.X_EQ, abi.X_NE, abi.X_AND, abi.X_OR))
+
+
+def ifelse(cond, a, b) -> Fx:
+    """cond ? a : b — ifelse.(cond, a, b): both sides evaluated (src/rewrites.jl:193-200)"""
+    return Fx(abi.X_IFELSE, (Fx.lift(cond), Fx.lift(a), Fx.lift(b)))
+
+
+def is_general(v) -> bool:
+    """True when an Assign right-hand side needs wsmc_assign_expr (not the operand form)"""
+    vs = v if isinstance(v, (list, tuple)) else [v]
+    return any(isinstance(x, Fx) for x in vs)
+
+
+def xprogram(components, resolve):
+    """(XInst array, per-component lengths) for wsmc_assign_expr / the oracle's or_assign_expr"""
+    ins = []
+    lens = []
+    for e in components:
+        e = Fx.lift(e)
+        if e._need() > abi.XSTACK_MAX:
+            raise ValueError(f"expression needs more than {abi.XSTACK_MAX} stack values: {e!r}")
+        n0 = len(ins)
+        e._emit(resolve, ins)
+        lens.append(len(ins) - n0)
+    if len(ins) > abi.XPROG_MAX:
+        raise ValueError(f"expression longer than {abi.XPROG_MAX} instructions")
+    arr = (abi.XInst * max(1, len(ins)))()
+    for k, (op, col, comp, c) in enumerate(ins):
+        arr[k].op, arr[k].col, arr[k].comp, arr[k].c = op, col, comp, c
+    return arr, lens

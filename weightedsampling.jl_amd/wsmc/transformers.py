@@ -8,7 +8,7 @@ per-particle operation executed by the HIP library through the context protocol:
     SMCState(N; ess_perc_min)              SMCState(N, ess_perc_min=...)
     state[:x] / getcol(store, :x)          state["x"] / state.store.getcol("x")
     apply!(t, state) / run!(root, state)   apply(t, state) / run(root, state)
-    Assign(:x, argfn)                      Assign("x", Col("y") + 1.0)
+    Assign(:x, argfn)                      Assign("x", Col("y") + 1.0), Assign("p", ifelse(Col("f"), .9, .01))
     Sample(:x, kernel, argfn)              Sample("x", Normal(Col("x") * a, q))
     Observe(lhsfn, kernel, argfn)          Observe(y, Normal(Col("x"), r))
     Weight(kernel, argfn)                  Weight(Normal(Col("x"), r), y)
@@ -31,7 +31,7 @@ import numpy as np
 from . import abi
 from .abi import Operand
 from .context import Context
-from .dsl import Expr, Kernel, _exprs, value_operands
+from .dsl import Expr, Kernel, _exprs, is_general, value_operands, xprogram
 
 
 # ---------------------------------------------------------------------------------------
@@ -162,6 +162,14 @@ class Assign(ParticleTransformer):
     def apply(self, state):
         dim = len(self.rhs) if isinstance(self.rhs, (list, tuple, np.ndarray)) else \
             (state.ctx.col_dim(state.ctx.col_find(self.lhs)) if state.store.hascol(self.lhs) else 1)
+        if is_general(self.rhs):   # beyond the operand form: the general expression program
+            comps = list(self.rhs) if isinstance(self.rhs, (list, tuple)) else [self.rhs]
+            if len(comps) != dim:
+                raise ValueError(f"{self.lhs}: give one expression per component ({dim})")
+            c = _ensure_col(state, self.lhs, dim)
+            prog, lens = xprogram(comps, state.store.resolve)
+            state.ctx.assign_expr(c, prog, lens)
+            return
         c = _ensure_col(state, self.lhs, dim)
         state.ctx.assign(c, value_operands(self.rhs, dim, state.store.resolve))
 
