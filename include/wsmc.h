@@ -68,9 +68,21 @@ typedef enum {
     WSMC_FAM_HALFNORMAL = 1,    /* Truncated(Normal(0, sigma), 0, Inf)          */
     WSMC_FAM_UNIFORM = 2,       /* Uniform(a, b) = param[0], param[1]           */
     WSMC_FAM_MVNORMAL_ISO = 3,  /* MvNormal(mu, var*I), dim <= 4                */
-    WSMC_FAM_MVNORMAL = 4       /* MvNormal(mu, Sigma), constant covariance Sigma, dim <= 3:
+    WSMC_FAM_MVNORMAL = 4,      /* MvNormal(mu, Sigma), constant covariance Sigma, dim <= 3:
                                    build it with wsmc_dist_mvnormal_cov (the factor is
                                    packed into the dist, see wsmc_terms.h)       */
+    /* scalar families of src/default_kernels.jl:83-102 with closed-form draws (one uniform
+       word pair each) and Distributions.jl's logpdf formulas; location mu[0], scale `scale`: */
+    WSMC_FAM_BERNOULLI = 5,     /* Bernoulli(p = mu[0]): x in {0.0, 1.0}            */
+    WSMC_FAM_BERNOULLI_LOGIT = 6, /* BernoulliLogit(logitp = mu[0])                   */
+    WSMC_FAM_EXPONENTIAL = 7,   /* Exponential(theta = scale), theta the mean       */
+    WSMC_FAM_LOGNORMAL = 8,     /* LogNormal(mu, sigma)                             */
+    WSMC_FAM_LAPLACE = 9,       /* Laplace(mu, theta)                               */
+    WSMC_FAM_CAUCHY = 10,       /* Cauchy(mu, sigma)                                */
+    WSMC_FAM_LOGISTIC = 11,     /* Logistic(mu, theta)                              */
+    WSMC_FAM_GUMBEL = 12,       /* Gumbel(mu, theta)                                */
+    WSMC_FAM_RAYLEIGH = 13,     /* Rayleigh(sigma = scale)                          */
+    WSMC_FAM_GEOMETRIC = 14     /* Geometric(p = mu[0]): failures before the first success */
 } wsmc_family;
 
 typedef enum {

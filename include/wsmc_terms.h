@@ -144,7 +144,8 @@ WSMC_HD double wsmc_xeval(const wsmc_xinst* p, int n, double* const* cols, int64
  * passes WSMC_FEAT_ALL. The arithmetic is the same. */
 #define WSMC_FEAT_OSC 1u
 #define WSMC_FEAT_MVN 2u   /* the full-covariance MvNormal family */
-#define WSMC_FEAT_ALL 3u
+#define WSMC_FEAT_EXT 4u   /* the scalar families from WSMC_FAM_BERNOULLI on */
+#define WSMC_FEAT_ALL 7u
 WSMC_HD double wsmc_dist_mean_f(const wsmc_dist* d, int k, double* const* cols, int64_t N, int64_t i,
                                 const wsmc_override* ov, unsigned feat) {
     if ((feat & WSMC_FEAT_OSC) && d->mean_fn == WSMC_MEAN_OSCILLATOR) {
@@ -300,6 +301,90 @@ WSMC_HD void wsmc_mvn_sample_n(const wsmc_dist* d, const int n, double* x, uint6
     }
 }
 
+/* the feature bits a dist needs in a kernel (wsmc_dist_logpdf_mf / wsmc_dist_sample_mf's feat) */
+WSMC_HD unsigned wsmc_dist_feat(const wsmc_dist* d) {
+    return (d->mean_fn == WSMC_MEAN_OSCILLATOR ? WSMC_FEAT_OSC : 0u) |
+           (d->family == WSMC_FAM_MVNORMAL ? WSMC_FEAT_MVN : 0u) |
+           (d->family >= WSMC_FAM_BERNOULLI ? WSMC_FEAT_EXT : 0u);
+}
+
+/* ---- the scalar families from WSMC_FAM_BERNOULLI on (src/default_kernels.jl:83-102) -----
+ * location m = mu[0] (p, logitp for the Bernoullis and Geometric), scale s = `scale`.
+ * logpdf: Distributions.jl's formulas, operation for operation where they are written out
+ * (zval as the Normal family's (x - m) * (1/s)); outside the support -Inf. */
+WSMC_HD double wsmc_ext_logpdf(int fam, double x, double m, double s, wsmc_logmemo* lm) {
+    switch (fam) {
+        case WSMC_FAM_BERNOULLI:   /* x == 0 ? log(failprob) : x == 1 ? log(succprob) : -Inf */
+            return x == 0.0 ? wsmc_log(1.0 - m) : (x == 1.0 ? wsmc_log(m) : -WSMC_INF);
+        case WSMC_FAM_BERNOULLI_LOGIT:   /* -log1pexp(x ? -logitp : logitp) */
+            return x == 0.0 ? -wsmc_log1pexp(m) : (x == 1.0 ? -wsmc_log1pexp(-m) : -WSMC_INF);
+        case WSMC_FAM_EXPONENTIAL: {   /* λ = rate = 1/θ: log(λ) - λ x */
+            const double r = 1.0 / s;
+            return x < 0.0 ? -WSMC_INF : wsmc_log(r) - r * x;
+        }
+        case WSMC_FAM_LOGNORMAL: {   /* normlogpdf(μ, σ, log x) - log x */
+            if (!(x > 0.0)) return -WSMC_INF;
+            const double lx = wsmc_log(x);
+            double lg, rc;
+            wsmc_scale_memo(lm, s, &lg, &rc);
+            const double z = (lx - m) * rc;
+            return (-(z * z + WSMC_LOG2PI) * 0.5 - lg) - lx;
+        }
+        case WSMC_FAM_LAPLACE:   /* -(|x - μ| / θ + log(2θ)) */
+            return -(wsmc_fabs(x - m) / s + wsmc_log(2.0 * s));
+        case WSMC_FAM_CAUCHY: {   /* -(log1psq((x - μ)/σ) + log π + log σ) */
+            double lg, rc;
+            wsmc_scale_memo(lm, s, &lg, &rc);
+            const double az = wsmc_fabs((x - m) * rc);
+            const double l1 = az < 9007199254740992.0 ? wsmc_log1p(az * az) : 2.0 * wsmc_log(az);
+            return -((l1 + 1.14472988584940017414) + lg);
+        }
+        case WSMC_FAM_LOGISTIC: {   /* u = -|z|: u - 2 log1pexp(u) - log θ */
+            double lg, rc;
+            wsmc_scale_memo(lm, s, &lg, &rc);
+            const double u = -wsmc_fabs((x - m) * rc);
+            return (u - 2.0 * wsmc_log1pexp(u)) - lg;
+        }
+        case WSMC_FAM_GUMBEL: {   /* -(z + exp(-z) + log θ) */
+            double lg, rc;
+            wsmc_scale_memo(lm, s, &lg, &rc);
+            const double z = (x - m) * rc;
+            return -((z + wsmc_exp(-z)) + lg);
+        }
+        case WSMC_FAM_RAYLEIGH: {   /* σ² = σ^2: x < 0 ? -Inf : log(x / σ²) - x^2 / (2σ²) */
+            const double s2 = s * s;
+            return x < 0.0 ? -WSMC_INF : wsmc_log(x / s2) - (x * x) / (2.0 * s2);
+        }
+        default: {   /* WSMC_FAM_GEOMETRIC: insupport ? log(p) + log1p(-p) x : -Inf */
+            if (!(x >= 0.0 && x == wsmc_floor(x))) return -WSMC_INF;
+            return wsmc_log(m) + wsmc_log1p(-m) * x;
+        }
+    }
+}
+/* one draw: u the op's first uniform in [0, 1), e = -log(1 - u) an Exp(1) variate (a
+ * uniform's inverse CDF; Julia's randexp draws the same distribution by a ziggurat) */
+WSMC_HD double wsmc_ext_sample(int fam, double m, double s, uint64_t seed, uint64_t op, uint64_t idx) {
+    if (fam == WSMC_FAM_LOGNORMAL) return wsmc_exp(m + s * wsmc_normal_k(seed, op, idx, 0));
+    const wsmc_u32x4 w = wsmc_rng_block(seed, op, idx, 0x80u);
+    const double u = wsmc_u01(w.v[0], w.v[1]);
+    const double e = -wsmc_log(1.0 - u);
+    switch (fam) {
+        case WSMC_FAM_BERNOULLI: return u < m ? 1.0 : 0.0;
+        case WSMC_FAM_BERNOULLI_LOGIT: return u < 1.0 / (1.0 + wsmc_exp(-m)) ? 1.0 : 0.0;
+        case WSMC_FAM_EXPONENTIAL: return s * e;
+        case WSMC_FAM_LAPLACE: return m + s * ((w.v[2] >> 31) ? e : -e);   /* randexp * ±1 */
+        case WSMC_FAM_CAUCHY: {   /* μ + σ tan(π (u - 1/2)) = μ - σ cos(π u) / sin(π u) */
+            double sn, cs;
+            wsmc_sincos2pi(0.5 * u, &sn, &cs);
+            return m - s * (cs / sn);
+        }
+        case WSMC_FAM_LOGISTIC: return m + s * wsmc_log(u / (1.0 - u));   /* μ + θ logit(u) */
+        case WSMC_FAM_GUMBEL: return m - s * wsmc_log(e);                 /* μ - θ log(randexp) */
+        case WSMC_FAM_RAYLEIGH: return s * wsmc_sqrt(2.0 * e);            /* σ sqrt(2 randexp) */
+        default: return wsmc_floor(-e / wsmc_log1p(-m));                   /* Geometric */
+    }
+}
+
 /* logpdf(D(args...), x) for the supported families */
 WSMC_HD double wsmc_dist_logpdf_mf(const wsmc_dist* d, const double* x, double* const* cols, int64_t N,
                                    int64_t i, const wsmc_override* ov, wsmc_logmemo* lm, unsigned feat) {
@@ -322,6 +407,12 @@ WSMC_HD double wsmc_dist_logpdf_mf(const wsmc_dist* d, const double* x, double* 
         }
         case WSMC_FAM_UNIFORM:
             return wsmc_uniform_logpdf(d->param[0], d->param[1], x[0]);
+        case WSMC_FAM_BERNOULLI: case WSMC_FAM_BERNOULLI_LOGIT: case WSMC_FAM_EXPONENTIAL:
+        case WSMC_FAM_LOGNORMAL: case WSMC_FAM_LAPLACE: case WSMC_FAM_CAUCHY: case WSMC_FAM_LOGISTIC:
+        case WSMC_FAM_GUMBEL: case WSMC_FAM_RAYLEIGH: case WSMC_FAM_GEOMETRIC:
+            if (!(feat & WSMC_FEAT_EXT)) return __builtin_nan("");   /* never launched so */
+            return wsmc_ext_logpdf(d->family, x[0], wsmc_operand_eval(&d->mu[0], cols, N, i, ov),
+                                   wsmc_operand_eval(&d->scale, cols, N, i, ov), lm);
         case WSMC_FAM_MVNORMAL:
             if (!(feat & WSMC_FEAT_MVN)) return __builtin_nan("");   /* never launched so */
             if (d->dim == 2) return wsmc_mvn_logpdf_n(d, 2, x, cols, N, i, ov, feat);
@@ -370,6 +461,13 @@ WSMC_HD void wsmc_dist_sample_mf(const wsmc_dist* d, double* x, uint64_t seed, u
             x[0] = a + (b - a) * wsmc_uniform_k(seed, op, idx, 0);
             break;
         }
+        case WSMC_FAM_BERNOULLI: case WSMC_FAM_BERNOULLI_LOGIT: case WSMC_FAM_EXPONENTIAL:
+        case WSMC_FAM_LOGNORMAL: case WSMC_FAM_LAPLACE: case WSMC_FAM_CAUCHY: case WSMC_FAM_LOGISTIC:
+        case WSMC_FAM_GUMBEL: case WSMC_FAM_RAYLEIGH: case WSMC_FAM_GEOMETRIC:
+            if (!(feat & WSMC_FEAT_EXT)) break;   /* never launched so */
+            x[0] = wsmc_ext_sample(d->family, wsmc_operand_eval(&d->mu[0], cols, N, i, 0),
+                                   wsmc_operand_eval(&d->scale, cols, N, i, 0), seed, op, idx);
+            break;
         case WSMC_FAM_MVNORMAL:
             if (!(feat & WSMC_FEAT_MVN)) break;   /* never launched so */
             if (d->dim == 2) wsmc_mvn_sample_n(d, 2, x, seed, op, idx, cols, N, i, feat);

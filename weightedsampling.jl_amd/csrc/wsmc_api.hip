@@ -306,11 +306,12 @@ static int check_operand(const wsmc_ctx* c, const wsmc_operand& o) {
 }
 
 static int check_dist(const wsmc_ctx* c, const wsmc_dist& d) {
-    if (d.family < WSMC_FAM_NORMAL || d.family > WSMC_FAM_MVNORMAL) return fail(WSMC_EARG, "unknown family");
+    if (d.family < WSMC_FAM_NORMAL || d.family > WSMC_FAM_GEOMETRIC) return fail(WSMC_EARG, "unknown family");
     if (d.dim < 1 || d.dim > 4) return fail(WSMC_EARG, "dist dim must be 1..4");
     if (d.family == WSMC_FAM_MVNORMAL && d.dim > WSMC_MVN_MAXDIM)
         return fail(WSMC_EARG, "MvNormal with a full covariance: dim must be 1..3");
-    if (d.family < WSMC_FAM_MVNORMAL_ISO && d.dim != 1) return fail(WSMC_EARG, "scalar family with dim != 1");
+    if (d.family != WSMC_FAM_MVNORMAL_ISO && d.family != WSMC_FAM_MVNORMAL && d.dim != 1)
+        return fail(WSMC_EARG, "scalar family with dim != 1");
     if (d.mean_fn == WSMC_MEAN_OSCILLATOR && (d.family != WSMC_FAM_NORMAL))
         return fail(WSMC_EARG, "oscillator mean only for Normal");
     int r;
@@ -2243,8 +2244,7 @@ int wsmc_sample(wsmc_ctx* c, int32_t out, const wsmc_dist* d) {
         eo.s.op = op;
         eo.s.has_sd = d->family == WSMC_FAM_MVNORMAL_ISO && wsmc_operand_is_const(&d->scale);
         eo.s.sd = eo.s.has_sd ? wsmc_sqrt(wsmc_operand_eval(&d->scale, nullptr, c->N, 0, nullptr)) : 0.0;
-        if (d->mean_fn == WSMC_MEAN_OSCILLATOR) c->ew_feat |= WSMC_FEAT_OSC;
-        if (d->family == WSMC_FAM_MVNORMAL) c->ew_feat |= WSMC_FEAT_MVN;
+        c->ew_feat |= wsmc_dist_feat(d);
         // a distribution that reads no column: the values are a function of (seed, op,
         // particle), kept in the batch's rows and written only when read (lazy store: a
         // Resample gathers nothing). WSMC_DIAG_STORE_SAMPLES=1 stores them (A/B)
@@ -2349,8 +2349,7 @@ static int weigh(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x, int kin
             const double sc = wsmc_operand_eval(&t.dist.scale, nullptr, c->N, 0, nullptr);
             eo.w.lm0 = wsmc_logmemo{wsmc_d2bits(sc), wsmc_log(sc), 1.0 / sc, 1};
         }
-        if (t.dist.mean_fn == WSMC_MEAN_OSCILLATOR) c->ew_feat |= WSMC_FEAT_OSC;
-        if (t.dist.family == WSMC_FAM_MVNORMAL) c->ew_feat |= WSMC_FEAT_MVN;
+        c->ew_feat |= wsmc_dist_feat(&t.dist);
         if (!b->has_w) {   // the batch's first weight term: the pending reset, the slot pair
             b->has_w = 1;
             b->w = c->w;

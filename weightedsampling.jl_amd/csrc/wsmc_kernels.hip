@@ -3166,7 +3166,7 @@ hipError_t launch_sample(hipStream_t s, double* out, int dim, const wsmc_dist& d
                          int64_t goff, double* const* cols, int64_t N) {
     const int has_sd = d.family == WSMC_FAM_MVNORMAL_ISO && wsmc_operand_is_const(&d.scale);
     const double sd = has_sd ? wsmc_sqrt(wsmc_operand_eval(&d.scale, nullptr, N, 0, nullptr)) : 0.0;
-    if (d.family == WSMC_FAM_MVNORMAL)
+    if (wsmc_dist_feat(&d) & (WSMC_FEAT_MVN | WSMC_FEAT_EXT))
         hipLaunchKernelGGL(k_sample<WSMC_FEAT_ALL>, grid_for(N), dim3(kBlock), 0, s, out, dim, d, seed, op, goff, cols,
                            N, has_sd, sd);
     else if (d.mean_fn == WSMC_MEAN_OSCILLATOR)
@@ -3198,7 +3198,7 @@ hipError_t launch_ew_assign1(hipStream_t s, const EwBatch& b, double* const* col
 hipError_t launch_ew_batch(hipStream_t s, const EwBatch& b, unsigned feat, uint64_t seed, int64_t goff, int64_t N) {
     static_assert(sizeof(EwBatch) + 32 <= 4096, "the batch rides in the kernel arguments");
     const size_t rows = sizeof(double) * kBlock * (size_t)b.nrows;   // only the rows used: occupancy
-    if (feat & WSMC_FEAT_MVN)
+    if (feat & (WSMC_FEAT_MVN | WSMC_FEAT_EXT))
         hipLaunchKernelGGL(k_ew_batch<WSMC_FEAT_ALL>, grid_for(N), dim3(kBlock), rows, s, b, seed, goff, N);
     else if (feat)
         hipLaunchKernelGGL(k_ew_batch<WSMC_FEAT_OSC>, grid_for(N), dim3(kBlock), rows, s, b, seed, goff, N);
@@ -3209,7 +3209,7 @@ hipError_t launch_ew_batch(hipStream_t s, const EwBatch& b, unsigned feat, uint6
 hipError_t launch_sample_importance(hipStream_t s, double* out, int dim, const wsmc_dist& prop,
                                     const wsmc_dist& targ, double* w, uint64_t seed, uint64_t op,
                                     int64_t goff, double* const* cols, int64_t N) {
-    if (prop.family == WSMC_FAM_MVNORMAL || targ.family == WSMC_FAM_MVNORMAL)
+    if ((wsmc_dist_feat(&prop) | wsmc_dist_feat(&targ)) & (WSMC_FEAT_MVN | WSMC_FEAT_EXT))
         hipLaunchKernelGGL(k_sample_importance<WSMC_FEAT_ALL>, grid_for(N), dim3(kBlock), 0, s, out, dim, prop, targ, w,
                            seed, op, goff, cols, N);
     else
@@ -3227,7 +3227,7 @@ hipError_t launch_weigh(hipStream_t s, const wsmc_term& t, double* w, double* co
         lm0.rcp = 1.0 / sc;
         lm0.valid = 1;
     }
-    if (t.dist.family == WSMC_FAM_MVNORMAL)
+    if (wsmc_dist_feat(&t.dist) & (WSMC_FEAT_MVN | WSMC_FEAT_EXT))
         hipLaunchKernelGGL(k_weigh<WSMC_FEAT_ALL>, grid_for(N), dim3(kBlock), 0, s, t, w, cols, N, ms, ms_next, lm0,
                            wreset);
     else if (t.dist.mean_fn == WSMC_MEAN_OSCILLATOR)

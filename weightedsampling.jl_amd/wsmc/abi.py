@@ -15,6 +15,8 @@ LIB_PATH = _PKG_DIR / "libwsmc.so"
 # ---- enums (include/wsmc.h) ---------------------------------------------------------
 WSMC_OK, WSMC_EARG, WSMC_EHIP, WSMC_ENOTPD, WSMC_ERCCL, WSMC_ESTATE, WSMC_ENOMEM = range(7)
 FAM_NORMAL, FAM_HALFNORMAL, FAM_UNIFORM, FAM_MVNORMAL_ISO, FAM_MVNORMAL = range(5)
+(FAM_BERNOULLI, FAM_BERNOULLI_LOGIT, FAM_EXPONENTIAL, FAM_LOGNORMAL, FAM_LAPLACE, FAM_CAUCHY, FAM_LOGISTIC,
+ FAM_GUMBEL, FAM_RAYLEIGH, FAM_GEOMETRIC) = range(5, 15)
 MEAN_AFFINE, MEAN_OSCILLATOR = range(2)
 TERM_SAMPLE, TERM_OBSERVE, TERM_WEIGHT = range(3)
 RESAMPLE_STRATIFIED, RESAMPLE_SYSTEMATIC, RESAMPLE_MULTINOMIAL = range(3)

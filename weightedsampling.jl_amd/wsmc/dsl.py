@@ -210,6 +210,53 @@ def Uniform(a: float, b: float) -> Kernel:
     return Kernel(abi.FAM_UNIFORM, 1, (Expr.lift(0.0),), 1.0, (float(a), float(b)))
 
 
+def _scalar(fam, loc=0.0, scale=1.0) -> Kernel:
+    return Kernel(fam, 1, (Expr.lift(loc),), scale)
+
+
+def Bernoulli(p) -> Kernel:
+    """default_kernels.Bernoulli(p): draws 1.0 / 0.0"""
+    return _scalar(abi.FAM_BERNOULLI, p)
+
+
+def BernoulliLogit(logitp) -> Kernel:
+    return _scalar(abi.FAM_BERNOULLI_LOGIT, logitp)
+
+
+def Exponential(theta=1.0) -> Kernel:
+    """default_kernels.Exponential(θ) — θ is the scale (the mean)"""
+    return _scalar(abi.FAM_EXPONENTIAL, 0.0, theta)
+
+
+def LogNormal(mu=0.0, sigma=1.0) -> Kernel:
+    return _scalar(abi.FAM_LOGNORMAL, mu, sigma)
+
+
+def Laplace(mu=0.0, theta=1.0) -> Kernel:
+    return _scalar(abi.FAM_LAPLACE, mu, theta)
+
+
+def Cauchy(mu=0.0, sigma=1.0) -> Kernel:
+    return _scalar(abi.FAM_CAUCHY, mu, sigma)
+
+
+def Logistic(mu=0.0, theta=1.0) -> Kernel:
+    return _scalar(abi.FAM_LOGISTIC, mu, theta)
+
+
+def Gumbel(mu=0.0, theta=1.0) -> Kernel:
+    return _scalar(abi.FAM_GUMBEL, mu, theta)
+
+
+def Rayleigh(sigma=1.0) -> Kernel:
+    return _scalar(abi.FAM_RAYLEIGH, 0.0, sigma)
+
+
+def Geometric(p) -> Kernel:
+    """default_kernels.Geometric(p): failures before the first success (0, 1, 2, ...)"""
+    return _scalar(abi.FAM_GEOMETRIC, p)
+
+
 def MvNormal(mu, cov) -> Kernel:
     """default_kernels.MvNormal(μ, Σ) — Σ is a COVARIANCE (src/default_kernels.jl:93). A scalar
     or Σ = v·I takes the isotropic family (dim ≤ 4); any other constant Σ (dim ≤ 3) takes the
