@@ -2748,8 +2748,11 @@ __device__ __forceinline__ void move_blk_body(const wsmc_term* ctape, const Fold
             if ((mb.lag_targets >> u) & 1) tab[mb.tcol[u]] = mb.tout[u];
 }
 // the program in the kernel's arguments (ProgInlineBlk first: offset 0 of the kernarg segment)
+#ifndef WSMC_MOVE_WAVES
+#define WSMC_MOVE_WAVES 1
+#endif
 template <int K, int LEAN>
-__global__ __launch_bounds__(kBlock) void k_move_blk(ProgInlineBlk, FoldSlots fs, MoveBlk mb, const double* Lb,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WSMC_MOVE_WAVES))) void k_move_blk(ProgInlineBlk, FoldSlots fs, MoveBlk mb, const double* Lb,
                                                      uint64_t seed, int64_t goff, int64_t N, u64* accepted,
                                                      const int32_t* flag, MoveCarry mc, int32_t cache_from,
                                                      int32_t nseg_new, int32_t nseg_old, MomLag lg, double** tab) {

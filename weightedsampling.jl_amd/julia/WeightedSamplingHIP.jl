@@ -15,8 +15,11 @@ against the same library on MI355X. See INTEGRATION.md.
 Device arguments are recognised structurally. `getcol` on a `HipColumnStore` returns a
 `DeviceColumn` proxy. Broadcasting `+ - *` over proxies and `Ref` constants (the shapes
 `vectorize` emits, src/rewrites.jl:146-219) builds a lazy affine `DeviceExpr`, which
-becomes a `wsmc_operand`. Any other expression is materialised on the host (download →
-compute → temporary device column), which is correct but slow.
+becomes a `wsmc_operand`. Any other fused broadcast over the operators `wsmc_assign_expr`
+knows (arithmetic, `^`, `min`/`max`, `abs`, `sqrt`, `exp`, `log`, `log1p`, `sin`, `cos`,
+comparisons, `!`, `&`, `|`, `ifelse`) becomes a `DeviceProgram`: an Assign evaluates it on the
+device, a distribution argument through a temporary device column. Only a function outside
+that set is materialised on the host (download → compute → temporary column).
 """
 module WeightedSamplingHIP
 
@@ -64,9 +67,22 @@ struct WsmcState
     n_resamples::Int64
 end
 
+struct WsmcXInst            # wsmc_xinst: one instruction of a postfix program
+    op::Int32
+    col::Int32
+    comp::Int32
+    reserved::Int32
+    c::Float64
+end
+
 const WSMC_ENOTPD = 3
 const FAM_NORMAL, FAM_HALFNORMAL, FAM_UNIFORM, FAM_MVNORMAL_ISO, FAM_MVNORMAL =
     Int32(0), Int32(1), Int32(2), Int32(3), Int32(4)
+# the scalar families from WSMC_FAM_BERNOULLI on: (kernel name, family, location index, scale index)
+# into the kernel's argument tuple (0: none)
+const EXT_FAMILIES = ((:Bernoulli, 5, 1, 0), (:BernoulliLogit, 6, 1, 0), (:Exponential, 7, 0, 1),
+                      (:LogNormal, 8, 1, 2), (:Laplace, 9, 1, 2), (:Cauchy, 10, 1, 2), (:Logistic, 11, 1, 2),
+                      (:Gumbel, 12, 1, 2), (:Rayleigh, 13, 0, 1), (:Geometric, 14, 1, 0))
 const MEAN_AFFINE = Int32(0)
 const RESAMPLE_STRATIFIED = Int32(0)
 const PROPOSAL_RW, PROPOSAL_AUTORW = Int32(0), Int32(1)
@@ -224,9 +240,82 @@ affine(::typeof(getindex), a::DeviceExpr, k::Integer) =                    # x[k
     DeviceExpr(a.store, a.c0, [(n, Int32(k - 1), coef) for (n, _, coef) in a.terms])
 affine(f, args...) = nothing                                               # not affine: host path
 
+# general expressions (wsmc_assign_expr, include/wsmc.h) ---------------------------------------
+"""A fused broadcast as a postfix program (`wsmc_xinst`s) over device columns."""
+struct DeviceProgram
+    store::HipColumnStore
+    ins::Vector{WsmcXInst}
+end
+const XOP1 = Dict{Any,Int32}(- => 2, abs => 3, sqrt => 4, exp => 5, log => 6, log1p => 7, sin => 8, cos => 9, (!) => 11)
+const XOP2 = Dict{Any,Int32}(+ => 16, - => 17, * => 18, / => 19, min => 20, max => 21, (^) => 22, (<) => 23,
+                             (<=) => 24, (>) => 25, (>=) => 26, (==) => 27, (!=) => 28, (&) => 29, (|) => 30)
+xconst(v) = WsmcXInst(0, -1, 0, 0, Float64(v))
+# postfix code of one broadcast argument, or nothing when something has no device form
+function xcode(s::HipColumnStore, x)
+    x isa Base.RefValue && x[] isa Real && return [xconst(x[])]
+    x isa Real && return [xconst(x)]
+    x isa DeviceColumn && return [WsmcXInst(1, s.ids[x.name], max(x.comp, 0), 0, 0.0)]
+    x isa DeviceExpr && return xcode_affine(s, x)
+    x isa Broadcast.Broadcasted || return nothing
+    f, a = x.f, x.args
+    if f === ifelse && length(a) == 3
+        parts = map(y -> xcode(s, y), a)
+        any(isnothing, parts) && return nothing
+        return vcat(parts..., [WsmcXInst(31, -1, 0, 0, 0.0)])
+    elseif f === (^) && length(a) == 2 && (a[2] isa Integer || (a[2] isa Base.RefValue && a[2][] isa Integer))
+        n = a[2] isa Integer ? a[2] : a[2][]                       # x^n: literal_pow / pow_body
+        b = xcode(s, a[1])
+        return b === nothing ? nothing : vcat(b, [WsmcXInst(10, -1, 0, 0, Float64(n))])
+    elseif f === Base.literal_pow && length(a) == 3                # x^2 lowered by the parser
+        n = typeof(a[3] isa Base.RefValue ? a[3][] : a[3]).parameters[1]
+        b = xcode(s, a[2])
+        return b === nothing ? nothing : vcat(b, [WsmcXInst(10, -1, 0, 0, Float64(n))])
+    elseif length(a) == 1 && haskey(XOP1, f)
+        b = xcode(s, a[1])
+        return b === nothing ? nothing : vcat(b, [WsmcXInst(XOP1[f], -1, 0, 0, 0.0)])
+    elseif length(a) >= 2 && haskey(XOP2, f)                      # n-ary + and * fold left, as Julia's
+        parts = map(y -> xcode(s, y), a)
+        any(isnothing, parts) && return nothing
+        code = parts[1]
+        for p in parts[2:end]
+            code = vcat(code, p, [WsmcXInst(XOP2[f], -1, 0, 0, 0.0)])
+        end
+        return code
+    end
+    return nothing
+end
+function xcode_affine(s::HipColumnStore, e::DeviceExpr)
+    code = WsmcXInst[]
+    for (k, (n, c, coef)) in enumerate(e.terms)
+        t = coef == 1.0 ? [WsmcXInst(1, s.ids[n], max(c, 0), 0, 0.0)] :
+            [xconst(coef), WsmcXInst(1, s.ids[n], max(c, 0), 0, 0.0), WsmcXInst(18, -1, 0, 0, 0.0)]
+        code = k == 1 ? t : vcat(code, t, [WsmcXInst(16, -1, 0, 0, 0.0)])
+    end
+    isempty(code) && return [xconst(e.c0)]
+    return e.c0 == 0.0 ? code : vcat(code, [xconst(e.c0), WsmcXInst(16, -1, 0, 0, 0.0)])
+end
+# the stack depth a program needs (the library refuses > 8 values, > 96 instructions)
+function xdepth(ins)
+    sp = 0; m = 0
+    for i in ins
+        sp += i.op <= 1 ? 1 : i.op <= 11 ? 0 : i.op == 31 ? -2 : -1
+        m = max(m, sp)
+    end
+    return m
+end
+"""Evaluate a program on the device into column `id` (component 0) (wsmc_assign_expr)."""
+function assign_program!(s::HipColumnStore, id::Int32, p::DeviceProgram)
+    len = Int32[length(p.ins), 0, 0, 0]
+    check(ccall((:wsmc_assign_expr, libwsmc), Cint, (Ptr{Cvoid}, Int32, Ptr{WsmcXInst}, Ptr{Int32}),
+                s.ctx, id, p.ins, len))
+end
+
 function Broadcast.materialize(bc::Broadcast.Broadcasted{DeviceStyle})
     e = lift(bc)
     e isa DeviceExpr && length(e.terms) <= 2 && return e
+    s = first(a.store for a in Broadcast.flatten(bc).args if a isa DeviceColumn)
+    code = xcode(s, bc)
+    code !== nothing && length(code) <= 96 && xdepth(code) <= 8 && return DeviceProgram(s, code)
     return Broadcast.materialize(Broadcast.broadcasted(bc.f, map(materialize_host, bc.args)...))
 end
 
@@ -240,6 +329,12 @@ function operand(s::HipColumnStore, x)
     x isa Base.RefValue && return const_operand(x[])
     x isa Real && return const_operand(x)
     x isa DeviceColumn && (x = lift(x))
+    if x isa DeviceProgram                        # a general argument: a temporary device column
+        s.tmp += 1
+        id = column!(s, Symbol("__wsmc_tmp", s.tmp), 1)
+        assign_program!(s, id, x)
+        return WsmcOperand(0.0, (id, Int32(-1)), (Int32(0), Int32(0)), (1.0, 0.0))
+    end
     if x isa DeviceExpr
         cols = [(s.ids[n], c < 0 ? Int32(0) : c, k) for (n, c, k) in x.terms]
         pad = (Int32(-1), Int32(0), 0.0)
@@ -293,6 +388,13 @@ function device_dist(s::HipColumnStore, kernel, args)
         check(ccall((:wsmc_dist_mvnormal_cov, libwsmc), Cint, (Ptr{WsmcDist}, Ptr{Float64}), r, Sm))
         return r[]
     end
+    for (name, fam, li, si) in EXT_FAMILIES
+        if hasproperty(K, name) && kernel === getproperty(K, name)
+            loc = li == 0 ? const_operand(0.0) : operand(s, args[li])
+            sc = si == 0 ? const_operand(1.0) : operand(s, args[si])
+            return WsmcDist(Int32(fam), MEAN_AFFINE, 1, 0, (loc, loc, loc, loc), sc, (0.0, 0.0))
+        end
+    end
     return nothing
 end
 
@@ -312,6 +414,10 @@ end
 function apply!(t::WS.Assign, state::HipState)
     s = state.store
     v = t.argfn(state)
+    if v isa DeviceProgram                        # a general right-hand side: wsmc_assign_expr
+        assign_program!(s, column!(s, t.lhs, 1), v)
+        return WS.advance!(state)
+    end
     d = v isa DeviceColumn && v.comp < 0 ? s.dims[v.name] : 1
     id = column!(s, t.lhs, d)
     ops = operands(s, v, d)
