@@ -417,6 +417,17 @@ int wsmc_debug_jit_stats(int64_t* stats_out);
 /* Compile a representative batch signature (the 2D SSM step) for gfx950 without a device:
  * WSMC_OK, or WSMC_EHIP with hiprtc's log in wsmc_last_error(). */
 int wsmc_debug_jit_selfcheck(void);
+/* The Move acceptance screen (csrc/wsmc_kernels.hip move_accept) on the current device: for each
+ * u[i], out[2i] = the single-precision estimate of log u and out[2i+1] = the restated double log,
+ * so a test can check the screen's band bound. Host buffers of n and 2n doubles. */
+int wsmc_debug_log_screen(const double* u, int64_t n, double* out);
+/* Move blocks compiled for their shape at run time (hiprtc; csrc/wsmc_mv_body.h): stats_out[5]
+ * = signatures compiled, signatures that failed to compile, blocks launched on compiled kernels,
+ * blocks run on the interpreter kernels, total compile time (us) — process-wide. */
+int wsmc_debug_mv_jit_stats(int64_t* stats_out);
+/* Compile a representative Move block (C3's shape) for gfx950 without a device: WSMC_OK, or
+ * WSMC_EHIP with hiprtc's log in wsmc_last_error(). */
+int wsmc_debug_mv_jit_selfcheck(void);
 
 #ifdef __cplusplus
 }

@@ -504,7 +504,9 @@ WSMC_HD int wsmc_operand_is_const(const wsmc_operand* o) { return o->col[0] < 0 
  * (dist.param[0], dist.param[1], dist.reserved) of its block; blocks hold at most
  * WSMC_OSC_BLOCK terms. Otherwise it opens a block (m = 0: the direct evaluation). Called
  * before the term is first evaluated, by the device library and the oracle alike. */
-#define WSMC_OSC_BLOCK 16
+#ifndef WSMC_OSC_BLOCK
+#define WSMC_OSC_BLOCK 64
+#endif
 WSMC_HD int wsmc_operand_same(const wsmc_operand* a, const wsmc_operand* b) {
     return wsmc_d2bits(a->c0) == wsmc_d2bits(b->c0) && wsmc_d2bits(a->coef[0]) == wsmc_d2bits(b->coef[0]) &&
            wsmc_d2bits(a->coef[1]) == wsmc_d2bits(b->coef[1]) && a->col[0] == b->col[0] && a->col[1] == b->col[1] &&

@@ -68,3 +68,14 @@ def test_statement_batch_jit_compiles_without_a_device():
     assert rc == abi.WSMC_OK, lib.wsmc_last_error().decode()
     st = abi.jit_stats()
     assert set(st) == {"compiled", "failed", "launched", "interpreted", "compile_s"}
+
+
+def test_move_block_jit_compiles_without_a_device():
+    """The run-time compiled Move blocks (csrc/wsmc_mv_body.h): hiprtc builds C3's block shape
+    (two 1-D unbounded autoRW moves over two Normal priors and an affine Normal run) from the
+    headers embedded in the library, for gfx950, with no device."""
+    lib = wsmc.load_library()
+    rc = lib.wsmc_debug_mv_jit_selfcheck()
+    assert rc == abi.WSMC_OK, lib.wsmc_last_error().decode()
+    st = abi.mv_jit_stats()
+    assert set(st) == {"compiled", "failed", "launched", "interpreted", "compile_s"}

@@ -293,8 +293,9 @@ def test_exact_shard_flag_is_the_single_population():
 def test_oscillator_rotation_known_answers():
     """The damped-oscillator mean by rotation: sin/cos share wsmc_cos's
     reduction (cos bit-identical to it, sin within an ulp-scale of libm), a block's first term
-    is the direct formula bit for bit, and the rolled mean at t_a + m*d (m <= 15) agrees with
-    examples/damped_oscillator.jl:11 evaluated by numpy in f64 to 2e-14 * A."""
+    is the direct formula bit for bit, and the rolled mean at t_a + m*d (m <= 63, a block of
+    WSMC_OSC_BLOCK = 64 terms) agrees with examples/damped_oscillator.jl:11 evaluated by numpy in
+    f64 to 1e-13 * A."""
     import ctypes as C
     L = O.lib()
     rng = np.random.default_rng(7)
@@ -308,10 +309,11 @@ def test_oscillator_rotation_known_answers():
     for _ in range(2000):
         A, om, ga = rng.uniform(0, 5), rng.uniform(0, 10), rng.uniform(0, 2)
         ph = rng.uniform(-math.pi, math.pi)
-        ta = d * 16 * int(rng.integers(0, 4))
+        ta = d * 64 * int(rng.integers(0, 2))
         assert L.or_osc_rolled(ta, d, 0, A, om, ga, ph) == L.or_oscillator(ta, A, om, ga, ph)
-        for m in range(16):
+        for m in range(64):
             t = ta + m * d
             ref = A * np.exp(-ga * t) * np.cos(om * t + ph)
             worst = max(worst, abs(L.or_osc_rolled(ta, d, m, A, om, ga, ph) - ref) / max(A, 1e-300))
-    assert worst < 2e-14, worst
+    print('worst rolled-mean error / A', worst)
+    assert worst < 1e-13, worst

@@ -2837,9 +2837,15 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
     // kernels skip on it) until the next synchronizing call reports it
     const bool async = !accepted_out;   // sharded too: the factor and its PD flag are device-side
     if (!async && (r = check_deferred(c))) return r;
-    if (!c->move_pending && !c->dflag_zero) WSMC_HIP(hipMemsetAsync(c->dflag, 0, sizeof(int32_t) * 4, c->stream));
+    // the flag words and accepted counters: zeroed by the moments kernel on the one-context
+    // autoRW path (block 0, before anything reads them), else by memsets
+    int32_t* zflag = (!c->move_pending && !c->dflag_zero) ? c->dflag : nullptr;
     c->dflag_zero = true;
-    if (accepted_out) WSMC_HIP(hipMemsetAsync(c->ucount, 0, sizeof(unsigned long long) * 4, c->stream));
+    unsigned long long* zcount = accepted_out ? c->ucount : nullptr;
+    if (proposal != WSMC_PROPOSAL_AUTORW || is_sharded(c)) {
+        if (zflag) WSMC_HIP(hipMemsetAsync(zflag, 0, sizeof(int32_t) * 4, c->stream));
+        if (zcount) WSMC_HIP(hipMemsetAsync(zcount, 0, sizeof(unsigned long long) * 4, c->stream));
+    }
     if (proposal == WSMC_PROPOSAL_AUTORW && is_sharded(c)) {
         if (c->w_reset_pending) {   // the sharded max pass reads the weights
             WSMC_HIP(launch_fill_weights(c->stream, c->w, c->w_reset_pending, c->N));
@@ -2868,7 +2874,7 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         // device-scope fence per block, measured 2x slower than the separate combine launch:
         // 113.6 vs 57.7 + 13.5 us at 4M — every block's fence writes back its L2)
         WSMC_HIP(launch_autorw_moments(c->stream, c->w, mms, c->d_colptr, targets, d, lp, hp, nullptr, c->N,
-                                       c->tilepart, c->w_reset_pending, gate));
+                                       c->tilepart, c->w_reset_pending, gate, nullptr, nullptr, 0, zflag, zcount));
         WSMC_HIP(launch_autorw_final(c->stream, c->tilepart, c->ntiles, d, step, c->mom, c->dflag, 0, gate));
         c->dflag_zero = false;
     } else {
@@ -3101,6 +3107,53 @@ static int move_block_each(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, 
     return WSMC_OK;
 }
 
+// a Move block's shape for csrc/wsmc_mv_body.h (false: outside what it compiles — the
+// interpreter kernels run the block): its moves, which targets are bounded or read through the
+// lag row, and the lean fold program's segments with the slots each template operand reads
+static bool mv_signature(const FoldSlots& fs, const MoveBlk& mb, int D, int lag_slots, int lag_targets,
+                         int32_t cache_from, const std::vector<wsmc_term>& tmpls, const std::vector<FoldSeg>& segs,
+                         int32_t nseg_new, int32_t nseg_old, MvSig& g) {
+    std::memset(&g, 0, sizeof(g));
+    if (fs.n < 1 || fs.n > kFoldSlots || D < 1 || D > kBlkTargets || mb.nm < 1 || mb.nm > 4) return false;
+    if (nseg_new > kMvSegs || nseg_old > kMvSegs || tmpls.size() > 64) return false;
+    g.K = fs.heavy ? 1 : 2;
+    g.nm = (int8_t)mb.nm;
+    g.D = (int8_t)D;
+    g.ns = (int8_t)fs.n;
+    g.ntmpl = (int8_t)tmpls.size();
+    g.nnew = (int8_t)nseg_new;
+    g.nold = (int8_t)nseg_old;
+    g.carry = cache_from >= 0 ? 1 : 0;
+    for (int k = 0; k <= mb.nm; ++k) g.off[k] = mb.off[k];
+    for (int k = mb.nm + 1; k < 5; ++k) g.off[k] = mb.off[mb.nm];
+    g.bnd = (uint8_t)(mb.bnd & 0xff);
+    g.lagt = (uint8_t)(lag_targets & 0xff);
+    g.smask = (uint16_t)(lag_slots & 0xffff);
+    auto shape = [](const wsmc_operand& o, MvSigOp& q) {
+        for (int k = 0; k < 2; ++k) q.c[k] = (int8_t)(o.col[k] >= 0 ? o.col[k] : -1);
+    };
+    for (int32_t i = 0; i < nseg_new + nseg_old; ++i) {
+        const FoldSeg& sg = segs[i];
+        MvSigSeg& q = g.seg[i < nseg_new ? i : kMvSegs + (i - nseg_new)];
+        const wsmc_term& t = tmpls[sg.tmpl];
+        q.kind = (int8_t)sg.kind;
+        q.fam = (int8_t)t.dist.family;
+        q.pre = sg.soff >= 0 ? 1 : 0;
+        shape(t.x[0], q.x);
+        for (int k = 0; k < 4; ++k) shape(t.dist.mu[k], q.mu[k]);
+        shape(t.dist.scale, q.sc);
+        if (sg.kind == kSegTerm) {
+            if (!wsmc_term_is_scalar(&t)) return false;
+        } else if (sg.kind == kSegNormalOsc) {
+            if (!fs.heavy) return false;
+        } else if (sg.kind != kSegNormalAff) {
+            return false;
+        }
+    }
+    for (int i = nseg_new; i < kMvSegs; ++i) g.seg[i].kind = 0;
+    return true;
+}
+
 int wsmc_move_block(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, int32_t gated, int64_t* accepted_out) {
     if (!c) return fail(WSMC_EARG, "null context");
     if (n < 0 || (n > 0 && !specs)) return fail(WSMC_EARG, "move block needs n >= 0 specs");
@@ -3229,8 +3282,9 @@ int wsmc_move_block(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, int32_t
     if ((r = upload_colptr(c))) return r;
     const bool async = !accepted_out;
     if (!async && (r = check_deferred(c))) return r;
-    if (!c->move_pending && !c->dflag_zero) WSMC_HIP(hipMemsetAsync(c->dflag, 0, sizeof(int32_t) * 4, c->stream));
-    if (accepted_out) WSMC_HIP(hipMemsetAsync(c->ucount, 0, sizeof(unsigned long long) * 4, c->stream));
+    // the flag words and accepted counters are zeroed by the first moments launch (block 0)
+    int32_t* zflag = (!c->move_pending && !c->dflag_zero) ? c->dflag : nullptr;
+    unsigned long long* zcount = accepted_out ? c->ucount : nullptr;
     // the moments: one pass over the union of the targets (4 at most), else one pass per move;
     // one combine into every move's factor
     const bool kept = c->cur_max && c->cur_max_seq == c->wseq;
@@ -3249,7 +3303,7 @@ int wsmc_move_block(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, int32_t
     const Decision* ldec = lrow ? lrow->dec : nullptr;
     if (!sep) {
         WSMC_HIP(launch_autorw_moments(c->stream, c->w, mms, c->d_colptr, utg, D, mb.lo, mb.hi, nullptr, c->N,
-                                       c->tilepart, c->w_reset_pending, gate, lanc, ldec, lag_targets));
+                                       c->tilepart, c->w_reset_pending, gate, lanc, ldec, lag_targets, zflag, zcount));
     } else {
         int32_t at = 0;
         for (int32_t m = 0; m < n; ++m) {
@@ -3257,7 +3311,8 @@ int wsmc_move_block(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, int32_t
             toff[m] = at;
             WSMC_HIP(launch_autorw_moments(c->stream, c->w, mms, c->d_colptr, utg + o, dm, mb.lo + o, mb.hi + o,
                                            nullptr, c->N, c->tilepart + (int64_t)at * c->ntiles, c->w_reset_pending,
-                                           gate, lanc, ldec, (lag_targets >> o) & ((1 << dm) - 1)));
+                                           gate, lanc, ldec, (lag_targets >> o) & ((1 << dm) - 1), m == 0 ? zflag : nullptr,
+                                           m == 0 ? zcount : nullptr));
             at += 1 + dm + dm * (dm + 1) / 2;
         }
     }
@@ -3332,9 +3387,30 @@ int wsmc_move_block(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, int32_t
         mc.dec = c->scache_dec;
         mc.out = c->scache_back;
     }
-    WSMC_HIP(launch_move_blk(c->stream, inl ? &pin : nullptr, reinterpret_cast<const wsmc_term*>(pbase), prog, fs, mb,
-                             c->mom + 64, c->seed, c->goff, c->N, accepted_out ? c->ucount : nullptr, c->dflag, mc,
-                             cache_from, lanc, ldec, lag_slots, c->d_colptr));
+    // the block on its shape's compiled kernel (csrc/wsmc_mv_body.h), else the interpreter
+    MvSig sig;
+    hipError_t je = hipErrorNotSupported;
+    if (mv_signature(fs, mb, D, lag_slots, lag_targets, cache_from, tmpls, segs, nseg_new, nseg_old, sig)) {
+        MvArgs ma;
+        ma.fs = fs;
+        ma.mb = mb;
+        ma.Lb = c->mom + 64;
+        ma.seed = c->seed;
+        ma.goff = c->goff;
+        ma.N = c->N;
+        ma.accepted = accepted_out ? c->ucount : nullptr;
+        ma.flag = c->dflag;
+        ma.mc = mc;
+        ma.lg = MomLag{lag_slots ? lanc : nullptr, ldec, lag_slots};
+        ma.tab = c->d_colptr;
+        ma.prog = inl ? nullptr : pbase;
+        je = launch_mv_jit(c->stream, sig, inl ? &pin : nullptr, ma, c->device);
+        if (je != hipSuccess && je != hipErrorNotSupported) WSMC_HIP(je);
+    }
+    if (je == hipErrorNotSupported)
+        WSMC_HIP(launch_move_blk(c->stream, inl ? &pin : nullptr, reinterpret_cast<const wsmc_term*>(pbase), prog, fs,
+                                 mb, c->mom + 64, c->seed, c->goff, c->N, accepted_out ? c->ucount : nullptr, c->dflag,
+                                 mc, cache_from, lanc, ldec, lag_slots, c->d_colptr));
     if (mc.out != mc.in) std::swap(c->scache, c->scache_back);
     c->scache_anc = nullptr;
     c->scache_dec = nullptr;
@@ -4367,6 +4443,32 @@ int wsmc_debug_jit_stats(int64_t* stats_out) {
     if (!stats_out) return fail(WSMC_EARG, "null stats_out");
     ew_jit_stats(stats_out);
     return WSMC_OK;
+}
+
+int wsmc_debug_mv_jit_stats(int64_t* stats_out) {
+    if (!stats_out) return fail(WSMC_EARG, "null stats_out");
+    mv_jit_stats(stats_out);
+    return WSMC_OK;
+}
+
+int wsmc_debug_mv_jit_selfcheck(void) {
+    std::string err;
+    if (mv_jit_selfcheck(err)) return fail(WSMC_EHIP, "Move-block JIT: " + err);
+    return WSMC_OK;
+}
+
+int wsmc_debug_log_screen(const double* u, int64_t n, double* out) {
+    if (!u || !out || n < 0) return fail(WSMC_EARG, "null buffer or n < 0");
+    if (n == 0) return WSMC_OK;
+    double *du = nullptr, *dout = nullptr;
+    hipError_t e = hipMalloc(&du, n * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc(&dout, 2 * n * sizeof(double));
+    if (e == hipSuccess) e = hipMemcpy(du, u, n * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_debug_log_screen(nullptr, du, n, dout);
+    if (e == hipSuccess) e = hipMemcpy(out, dout, 2 * n * sizeof(double), hipMemcpyDeviceToHost);
+    hipFree(du);
+    hipFree(dout);
+    return e == hipSuccess ? WSMC_OK : fail(WSMC_EHIP, std::string("log screen: ") + hipGetErrorString(e));
 }
 
 int wsmc_debug_jit_selfcheck(void) {

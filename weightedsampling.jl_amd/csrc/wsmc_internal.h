@@ -15,6 +15,8 @@
 #include "wsmc_math.h"
 #include "wsmc_terms.h"
 #include "wsmc_ew.h"
+#include "wsmc_mv.h"
+#include "wsmc_mv_body.h"
 
 namespace wsmc {
 
@@ -432,46 +434,11 @@ hipError_t launch_median_pick(hipStream_t s, const unsigned long long* v, const 
                               const unsigned long long* S, int64_t N, double* out);
 hipError_t launch_hist(hipStream_t s, const double* x, const unsigned long long* q, int64_t N, const double* edges,
                        unsigned long long* cnt);
-// Move over a compiled tape (operands renumbered to slots; the targets are slots 0..d-1)
-constexpr int kFoldSlots = 16;
-struct FoldSlots {
-    const double* p[kFoldSlots];   // slot s = column component values [N]
-    double* t[4];                  // the target columns (written on accept)
-    int32_t n;
-    int32_t heavy;                 // transcendental-heavy terms (oscillator means): one particle per thread
-    int32_t lean;                  // every term is a run term or scalar (wsmc_term_is_scalar): the lean fold
-};
-// The fold as a program of segments over the compiled tape: a run of consecutive Normal
-// terms that differ only in their constants (the observations of a model's loop, e.g.
-// examples/damped_oscillator.jl:36 or examples/linear_regression.jl:21) is one segment whose
-// per-particle invariants (the mean's column reads, sigma and its log) are evaluated once;
-// its terms' constants are packed in `cst` (Osc: t_a, d, m, y per term — the rotation block
-// of wsmc_osc_link; Aff: c0, coef0, coef1, y). Every other term is a one-term segment.
-enum { kSegTerm = 0, kSegNormalOsc = 1, kSegNormalAff = 2 };
-struct FoldSeg {
-    int32_t kind;
-    int32_t count;   // terms in the segment
-    int32_t tmpl;    // index of its first term in the compiled tape
-    int32_t coff;    // offset of its constants: Osc (t, y) per term; Aff (c0, coef0, coef1, y) per term
-    int32_t soff;    // a constant scale: offset of its (log sigma, 1/sigma) in the constants
-                     // (wsmc_scale_pre, evaluated once on the host), else -1
-    int32_t pad;     // 24 B: the constants after the segments stay 8-aligned
-};
 struct FoldProgram {
     const FoldSeg* seg_new;    // the s_new fold, terms [0, n)
     const FoldSeg* seg_old;    // the s_old fold, terms [cache_from or 0, n)
     int32_t nseg_new, nseg_old;
     const double* cst;
-};
-// the carried Move scores of one Move (ping-pong when a lazy Resample came in between: the
-// scores are then read through its ancestors, gated by its decision, and written to `out`)
-struct MoveCarry {
-    const double* in;
-    double* out;
-    const int32_t* anc = nullptr;
-    const Decision* dec = nullptr;
-    const Decision* gate = nullptr;   // a gated Move (wsmc_move_gated): only the scores are carried
-                                      // on when !gate->resampled
 };
 // a lean fold program small enough to travel in the Move kernel's own arguments (read from
 // the kernarg segment with scalar loads): no upload copy per Move. Layout as the device
@@ -481,32 +448,15 @@ struct ProgInline {
     int32_t seg_off, cst_off, seg_old0, pad;
     unsigned long long w[kProgInlineWords];
 };
-// a block of autoRW Moves on disjoint targets in one pass (wsmc_move_block): union targets
-// u = 0..D-1 (the fold's slots 0..D-1, D <= 8), move m owns [off[m], off[m+1])
-constexpr int kBlkTargets = 8;
-struct MoveBlk {
-    int32_t nm;
-    int8_t off[5];
-    int8_t pad[3];
-    int32_t bnd;                 // bit u: the bounded transform applies to union target u
-    int32_t lag_targets;         // bit u: target u read through the lag row, written in full to tout
-    int16_t tcol[kBlkTargets];   // column ids (device table entries moved to tout when lagged)
-    double min_step[4];          // per move
-    unsigned long long op_prop[4], op_acc[4];
-    double* tout[kBlkTargets];   // per union target: where its values go
-    double lo[kBlkTargets], hi[kBlkTargets];
-    double lgw[kBlkTargets];     // log(hi - lo) of a bounded interval (host-evaluated)
-};
-// a block's fold program in its kernel's arguments (the block's other arguments are larger
-// than a single Move's, so fewer words than ProgInline)
-constexpr int kProgBlkWords = 360;
-struct ProgInlineBlk {
-    int32_t seg_off, cst_off, seg_old0, pad;
-    unsigned long long w[kProgBlkWords];
-};
 // the moments of a block: one pass over the union of the targets (sep = 0, D <= 4: every
 // move's totals a sub-block of the union's), or one pass per move (its totals at
 // tilepart + toff[m] * ntiles)
+// a Move block on its signature's compiled kernel (csrc/wsmc_jit.hip); hipErrorNotSupported: none
+// (JIT off or the signature failed to compile) — the caller runs the interpreter kernels
+hipError_t launch_mv_jit(hipStream_t s, const MvSig& sig, const ProgInlineBlk* pin, const MvArgs& a, int device);
+int mv_jit_selfcheck(std::string& err);
+void mv_jit_stats(int64_t* out);
+hipError_t launch_debug_log_screen(hipStream_t s, const double* u, int64_t n, double* out);
 hipError_t launch_autorw_final_blk(hipStream_t s, const double* tilepart, int64_t ntiles, const MoveBlk& mb,
                                    int sep, const int32_t* toff, double* mom, int32_t* flag, const Decision* gate);
 hipError_t launch_move_blk(hipStream_t s, const ProgInlineBlk* pin, const wsmc_term* ctape, const FoldProgram& prog,
@@ -545,11 +495,16 @@ hipError_t launch_autorw_combine(hipStream_t s, const unsigned long long* xchg, 
 hipError_t launch_max_publish(hipStream_t s, const MaxSlots* ms, unsigned long long* word);
 // autoRW in one pass (include/wsmc_math.h wsmc_autorw_factor): pivoted canonical tile partials,
 // their one-block combine and factor; sharded: publish (max word, pivot), rank-order combine
+struct MomZero {   // words the moments kernel zeroes first (block 0): a Move block's flags, counters
+    int32_t* flag;
+    unsigned long long* count;
+};
 hipError_t launch_autorw_moments(hipStream_t s, const double* w, const MaxSlots* ms, double* const* cols,
                                  const int32_t* tcols, int d, const double* lo, const double* hi,
                                  const unsigned long long* pv, int64_t N, double* tilepart,
                                  const Decision* wreset = nullptr, const Decision* gate = nullptr,
-                                 const int32_t* lag_anc = nullptr, const Decision* lag_dec = nullptr, int lag_mask = 0);
+                                 const int32_t* lag_anc = nullptr, const Decision* lag_dec = nullptr, int lag_mask = 0,
+                                 int32_t* zflag = nullptr, unsigned long long* zcount = nullptr);
 hipError_t launch_autorw_final(hipStream_t s, const double* tilepart, int64_t ntiles, int d, double min_step,
                                double* mom, int32_t* flag, int raw, const Decision* gate = nullptr);
 hipError_t launch_autorw_publish(hipStream_t s, const MaxSlots* ms, double* const* cols, const int32_t* tcols, int d,

@@ -49,6 +49,8 @@ struct JitCache {
     std::map<std::pair<int, std::string>, JitKernel> k;
     int64_t compiled = 0, failed = 0, launched = 0, interpreted = 0;
     double compile_s = 0.0;
+    int64_t mv_compiled = 0, mv_failed = 0, mv_launched = 0, mv_interpreted = 0;   // Move blocks
+    double mv_compile_s = 0.0;
 };
 JitCache& cache() {
     static JitCache* c = new JitCache;   // never destroyed: modules live for the process
@@ -171,9 +173,8 @@ std::string tu_source(const std::string& sig) {
            "int64_t N) { wsmc::ew_body<WsmcSig, 2>(seed, goff, N); }\n";
 }
 
-// compile a signature's translation unit for `arch` (the code object in `code`)
-bool compile_code(const std::string& arch, const std::string& sig, std::string& code, std::string& err) {
-    const std::string src = tu_source(sig);
+// compile a translation unit for `arch` (the code object in `code`)
+bool compile_src(const std::string& arch, const std::string& src, std::string& code, std::string& err) {
     const int nh = (int)(sizeof(kJitHeaders) / sizeof(kJitHeaders[0]));
     const char* htext[8];
     const char* hname[8];
@@ -204,6 +205,38 @@ bool compile_code(const std::string& arch, const std::string& sig, std::string& 
     code.assign(n, '\0');
     hiprtcGetCode(prog, &code[0]);
     hiprtcDestroyProgram(&prog);
+    return true;
+}
+
+bool compile_code(const std::string& arch, const std::string& sig, std::string& code, std::string& err) {
+    return compile_src(arch, tu_source(sig), code, err);
+}
+
+bool device_arch(int device, std::string& arch, std::string& err) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+        err = "hipGetDeviceProperties failed";
+        return false;
+    }
+    arch = prop.gcnArchName;   // e.g. "gfx950:sramecc+:xnack-": the processor alone
+    arch = arch.substr(0, arch.find(':'));
+    return true;
+}
+
+// load a code object on `device` and look up its kernels f[0], f[1]
+bool load_module(int device, const std::string& code, const char* f0, const char* f1, JitKernel& out,
+                 std::string& err) {
+    int cur = 0;
+    hipGetDevice(&cur);
+    hipSetDevice(device);
+    hipError_t e = hipModuleLoadData(&out.mod, code.data());
+    if (e == hipSuccess) e = hipModuleGetFunction(&out.f[0], out.mod, f0);
+    if (e == hipSuccess) e = hipModuleGetFunction(&out.f[1], out.mod, f1);
+    hipSetDevice(cur);
+    if (e != hipSuccess) {
+        err = std::string("hipModuleLoadData: ") + hipGetErrorString(e);
+        return false;
+    }
     return true;
 }
 
@@ -343,6 +376,138 @@ void ew_jit_stats(int64_t* out) {
     out[2] = C.launched;
     out[3] = C.interpreted;
     out[4] = (int64_t)(C.compile_s * 1e6);
+}
+
+// ---- Move blocks compiled for their shape (csrc/wsmc_mv_body.h) ------------------------
+namespace {
+std::string mv_sig_text(const MvSig& g) {
+    std::string s;
+    auto num = [&](int v) { s += std::to_string(v); s += ','; };
+    auto op = [&](const MvSigOp& o) { s += '{'; s += '{'; num(o.c[0]); num(o.c[1]); s += "}},"; };
+    s += '{';
+    num(g.K); num(g.nm); num(g.D); num(g.ns); num(g.ntmpl); num(g.nnew); num(g.nold); num(g.carry);
+    s += '{';
+    for (int k = 0; k < 5; ++k) num(g.off[k]);
+    s += "},";
+    num(g.bnd); num(g.lagt); num(0); num(g.smask); num(0);
+    s += '{';
+    for (int k = 0; k < 2 * kMvSegs; ++k) {
+        const MvSigSeg& q = g.seg[k];
+        s += '{';
+        num(q.kind); num(q.fam); num(q.pre); num(0);
+        op(q.x);
+        s += '{';
+        for (int j = 0; j < 4; ++j) op(q.mu[j]);
+        s += "},";
+        op(q.sc);
+        s += "},";
+    }
+    s += "}}";
+    return s;
+}
+
+// two entries: the program in the kernel arguments (read through the kernarg segment, scalar
+// loads) or in device memory; MvArgs after ProgInlineBlk at its own alignment
+std::string mv_tu(const std::string& sig) {
+    return "#include \"wsmc_mv_body.h\"\n"
+           "struct WsmcMvSig { static constexpr wsmc::MvSig sig = " + sig + "; };\n"
+           "constexpr unsigned kMvArgsAt = (sizeof(wsmc::ProgInlineBlk) + alignof(wsmc::MvArgs) - 1) & "
+           "~(unsigned)(alignof(wsmc::MvArgs) - 1);\n"
+           "extern \"C\" __global__ __launch_bounds__(256) void wsmc_mv_i(wsmc::ProgInlineBlk, wsmc::MvArgs) {\n"
+           "  const char* ka = (const char*)__builtin_amdgcn_kernarg_segment_ptr();\n"
+           "  wsmc::mv_body<WsmcMvSig>(ka + __builtin_offsetof(wsmc::ProgInlineBlk, w), "
+           "*reinterpret_cast<const wsmc::MvArgs*>(ka + kMvArgsAt));\n}\n"
+           "extern \"C\" __global__ __launch_bounds__(256) void wsmc_mv_g(wsmc::ProgInlineBlk, wsmc::MvArgs) {\n"
+           "  const char* ka = (const char*)__builtin_amdgcn_kernarg_segment_ptr();\n"
+           "  const wsmc::MvArgs& a = *reinterpret_cast<const wsmc::MvArgs*>(ka + kMvArgsAt);\n"
+           "  wsmc::mv_body<WsmcMvSig>(a.prog, a);\n}\n";
+}
+}  // namespace
+
+hipError_t launch_mv_jit(hipStream_t s, const MvSig& sig, const ProgInlineBlk* pin, const MvArgs& a, int device) {
+    JitCache& C = cache();
+    if (jit_off()) {
+        std::lock_guard<std::mutex> lk(C.mu);
+        C.mv_interpreted += 1;
+        return hipErrorNotSupported;
+    }
+    const std::string key = "mv:" + mv_sig_text(sig);
+    JitKernel* jk = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(C.mu);
+        auto it = C.k.find({device, key});
+        if (it == C.k.end()) {
+            JitKernel k;
+            std::string err, arch, code;
+            const auto t0 = std::chrono::steady_clock::now();
+            k.ok = device_arch(device, arch, err) && compile_src(arch, mv_tu(key.substr(3)), code, err) &&
+                   load_module(device, code, "wsmc_mv_i", "wsmc_mv_g", k, err);
+            const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            C.mv_compile_s += dt;
+            if (k.ok) {
+                C.mv_compiled += 1;
+                if (jit_verbose()) fprintf(stderr, "[wsmc jit] device %d: Move block compiled in %.2f s\n", device, dt);
+            } else {
+                C.mv_failed += 1;
+                fprintf(stderr, "[wsmc jit] device %d: a Move-block signature did not compile; it runs on the "
+                                "interpreter kernel\n%s\n", device, err.c_str());
+            }
+            it = C.k.emplace(std::make_pair(device, key), k).first;
+        }
+        jk = &it->second;
+        if (!jk->ok) {
+            C.mv_interpreted += 1;
+            return hipErrorNotSupported;
+        }
+        C.mv_launched += 1;
+    }
+    const unsigned grid = (unsigned)((a.N + sig.K * kBlock - 1) / (sig.K * kBlock));
+    ProgInlineBlk pb;
+    if (pin) {
+        pb = *pin;
+    } else {
+        std::memset(&pb, 0, sizeof(pb));
+    }
+    MvArgs aa = a;
+    void* args[] = {&pb, &aa};
+    return hipModuleLaunchKernel(jk->f[pin ? 0 : 1], grid, 1, 1, kBlock, 1, 1, 0, s, args, nullptr);
+}
+
+// compile a representative Move block (C3's: two 1-D unbounded moves, two Normal priors and an
+// affine Normal run; the old fold one Normal term) for gfx950 without a device
+int mv_jit_selfcheck(std::string& err) {
+    MvSig g;
+    std::memset(&g, 0, sizeof(g));
+    for (auto& q : g.seg) {
+        q.x.c[0] = q.x.c[1] = q.sc.c[0] = q.sc.c[1] = -1;
+        for (auto& m : q.mu) m.c[0] = m.c[1] = -1;
+    }
+    g.K = 2; g.nm = 2; g.D = 2; g.ns = 2; g.ntmpl = 4; g.nnew = 3; g.nold = 1; g.carry = 1;
+    g.off[0] = 0; g.off[1] = 1; g.off[2] = 2; g.off[3] = 2; g.off[4] = 2;
+    for (int k = 0; k < 2; ++k) {
+        g.seg[k].kind = kSegTerm;
+        g.seg[k].fam = WSMC_FAM_NORMAL;
+        g.seg[k].pre = 1;
+        g.seg[k].x.c[0] = (int8_t)k;
+    }
+    g.seg[2].kind = kSegNormalAff;
+    g.seg[2].pre = 1;
+    g.seg[2].mu[0].c[0] = 0;
+    g.seg[2].mu[0].c[1] = 1;
+    g.seg[kMvSegs] = g.seg[0];
+    g.seg[kMvSegs].mu[0].c[0] = 0;
+    std::string code;
+    return compile_src("gfx950", mv_tu(mv_sig_text(g)), code, err) ? 0 : -1;
+}
+
+void mv_jit_stats(int64_t* out) {
+    JitCache& C = cache();
+    std::lock_guard<std::mutex> lk(C.mu);
+    out[0] = C.mv_compiled;
+    out[1] = C.mv_failed;
+    out[2] = C.mv_launched;
+    out[3] = C.mv_interpreted;
+    out[4] = (int64_t)(C.mv_compile_s * 1e6);
 }
 
 }  // namespace wsmc

@@ -1882,11 +1882,6 @@ struct MomArgs {
     wsmc_operand ex[4];
 };
 // targets one lazy Resample behind (bit k of mask: target k read through anc when dec resampled)
-struct MomLag {
-    const int32_t* anc;
-    const Decision* dec;
-    int32_t mask;
-};
 
 // one block: canonical combine of tile partials; pass 1 -> mom[0..d) = mean, mom[8] = S0;
 // pass 2 -> mom[16..16+d*d) = lambda*Sigma (zeros -> min_step), mom[32..32+d*d) = chol
@@ -2055,9 +2050,15 @@ template <int D>
 __global__ __launch_bounds__(kBlock) void k_moments1(const double* __restrict__ w, const MaxSlots* ms,
                                                      double* const* cols, MomArgs ma, const u64* pv, int64_t N,
                                                      int64_t ntiles, double* tilepart, const Decision* wreset,
-                                                     const Decision* gate, MomLag lg) {
+                                                     const Decision* gate, MomLag lg, MomZero z) {
     constexpr int d = D, NV = 1 + D + D * (D + 1) / 2;
     __shared__ double lds4[4];
+    // the Move block's flag words and accepted counters, zeroed here rather than by two memset
+    // launches (the combine and the Move kernel, which use them, run after this kernel)
+    if (blockIdx.x == 0 && threadIdx.x < 4) {
+        if (z.flag) z.flag[threadIdx.x] = 0;
+        if (z.count) z.count[threadIdx.x] = 0;
+    }
     if (gate && !gate->resampled) return;   // a gated Move that does not run
     const double M = wave_slots_max(ms);
     // a fused Resample's weight reset still pending (the next Observe applies it): the
@@ -2203,6 +2204,20 @@ __global__ void k_autorw_combine1(const u64* __restrict__ xchg, int world, int s
     if (!ok) flag[0] = 1;
 }
 
+// its band half-width and estimate, for the device check of the bound
+__global__ void k_debug_log_screen(const double* u, int64_t n, double* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double L = (double)__builtin_amdgcn_logf((float)u[i]) * 0.69314718055994530942;
+    out[2 * i] = L;
+    out[2 * i + 1] = wsmc_log(u[i]);
+}
+
+hipError_t launch_debug_log_screen(hipStream_t s, const double* u, int64_t n, double* out) {
+    hipLaunchKernelGGL(k_debug_log_screen, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, u, n, out);
+    return hipGetLastError();
+}
+
 // Move (src/transformers.jl:588-623). scache carries each particle's score from its last
 // move (the fold is a left-to-right sum, so continuing it over the terms appended since
 // [cache_from, nterms) gives the same bits as refolding); cache_from < 0 = refold.
@@ -2244,7 +2259,7 @@ __global__ __launch_bounds__(kBlock) void k_move(const wsmc_term* tape, int32_t 
                                  : wsmc_fold(tape, nterms, depth, cols, N, i, nullptr);
         const double s_new = wsmc_fold(tape, nterms, depth, cols, N, i, &ov);
         const double u = wsmc_uniform_k(seed, op_acc, (uint64_t)(goff + i), 0);
-        if (wsmc_log(u) < (lpr + s_new) - s_old) {   // strict; NaN rejects (src/transformers.jl:615)
+        if (move_accept(u, (lpr + s_new) - s_old)) {   // strict; NaN rejects (src/transformers.jl:615)
             for (int k = 0; k < d; ++k) cols[ma.tcol[k]][i] = ov.val[k];
             acc = 1;
         }
@@ -2309,9 +2324,19 @@ __device__ __forceinline__ void fold_seg(double (&s)[K], const wsmc_term* tape, 
             double zr[K], zi[K], rr[K], ri[K];
             double cur_ta = WSMC_NAN, r_d = WSMC_NAN;
             int cur_m = -2;
+            // each term's constants are scalar loads: the next term's are issued before this
+            // term's arithmetic, so the loop waits out no scalar-memory latency per term
+            const bool any = sg.count > 0;
+            double q0 = any ? c[0] : 0.0, q1 = any ? c[1] : 0.0, q2 = any ? c[2] : 0.0, q3 = any ? c[3] : 0.0;
             for (int32_t k = 0; k < sg.count; ++k) {
-                const double ta = c[4 * k], dl = c[4 * k + 1], y = c[4 * k + 3];
-                const int m = (int)c[4 * k + 2];
+                const double ta = q0, dl = q1, y = q3;
+                const int m = (int)q2;
+                if (k + 1 < sg.count) {   // uniform
+                    q0 = c[4 * k + 4];
+                    q1 = c[4 * k + 5];
+                    q2 = c[4 * k + 6];
+                    q3 = c[4 * k + 7];
+                }
                 const bool next = m > 0 && m == cur_m + 1 && wsmc_d2bits(ta) == wsmc_d2bits(cur_ta) &&
                                   wsmc_d2bits(dl) == wsmc_d2bits(r_d);
                 if (m > 0 && wsmc_d2bits(dl) != wsmc_d2bits(r_d)) {   // uniform branch
@@ -2358,8 +2383,16 @@ __device__ __forceinline__ void fold_seg(double (&s)[K], const wsmc_term* tape, 
                 }
             }
             const double* c = cst + sg.coff;
+            const bool any = sg.count > 0;   // the next term's constants, loaded ahead
+            double q0 = any ? c[0] : 0.0, q1 = any ? c[1] : 0.0, q2 = any ? c[2] : 0.0, q3 = any ? c[3] : 0.0;
             for (int32_t k = 0; k < sg.count; ++k) {
-                const double c0 = c[4 * k], a0 = c[4 * k + 1], a1 = c[4 * k + 2], y = c[4 * k + 3];
+                const double c0 = q0, a0 = q1, a1 = q2, y = q3;
+                if (k + 1 < sg.count) {   // uniform
+                    q0 = c[4 * k + 4];
+                    q1 = c[4 * k + 5];
+                    q2 = c[4 * k + 6];
+                    q3 = c[4 * k + 7];
+                }
 #pragma unroll
                 for (int p = 0; p < K; ++p) {
                     if (!ok[p]) continue;
@@ -2481,7 +2514,12 @@ __device__ __forceinline__ void move_c_body(const wsmc_term* ctape, const FoldSl
     }
     // s_old: the carried score continued over the new terms, or the full fold
     fold_seg<K, LEAN>(so, ctape, prog.seg_old, prog.nseg_old, prog.cst, sp, ix, ok);
+#ifndef WSMC_ABL_NOFOLD
     if (run) fold_seg<K, LEAN>(sn, ctape, prog.seg_new, prog.nseg_new, prog.cst, spn, ix, ok);
+#else
+#pragma unroll
+    for (int p = 0; p < K; ++p) sn[p] = -0.5 * prop[ix[p]] * prop[ix[p]];
+#endif
     u64 acc = 0;
 #pragma unroll
     for (int p = 0; p < K; ++p) {
@@ -2491,7 +2529,7 @@ __device__ __forceinline__ void move_c_body(const wsmc_term* ctape, const FoldSl
             continue;
         }
         const double u = wsmc_uniform_k(seed, op_acc, (uint64_t)(goff + gi[p]), 0);
-        const bool a = wsmc_log(u) < (lpr[p] + sn[p]) - so[p];   // strict; NaN rejects (src/transformers.jl:615)
+        const bool a = move_accept(u, (lpr[p] + sn[p]) - so[p]);   // strict; NaN rejects (src/transformers.jl:615)
         if (a) {
 #pragma unroll
             for (int k = 0; k < 4; ++k)
@@ -2637,7 +2675,9 @@ __global__ __launch_bounds__(kBlock) void k_autorw_final_sep(const double* tilep
     flag[2] = prior ? 0 : nrun;
 }
 
-template <int K, int LEAN>
+// BND = 0: no union target is bounded (the host checks mb.bnd), so the transforms' code is left
+// out (with it the unrolled per-target bodies carry 2K copies of log / exp / log1p: code size)
+template <int K, int LEAN, int BND = 1>
 __device__ __forceinline__ void move_blk_body(const wsmc_term* ctape, const FoldSeg* seg_new, const FoldSeg* seg_old,
                                               const double* cst, int32_t nseg_new, int32_t nseg_old,
                                               const FoldSlots& fs, const MoveBlk& mb, const double* Lb,
@@ -2694,11 +2734,15 @@ __device__ __forceinline__ void move_blk_body(const wsmc_term* ctape, const Fold
             lpr[p] = 0.0;
             if (!ok[p]) continue;
             double xi[4] = {0.0, 0.0, 0.0, 0.0};
+#ifndef WSMC_ABL_NODRAW   // ablation builds only (tools/build_variant.sh): what each part of the block costs
 #pragma unroll
             for (int k = 0; k < 4; k += 2)
                 if (k < dm)
                     wsmc_normal_pair(wsmc_rng_block(seed, mb.op_prop[m], (uint64_t)(goff + gi[p]), (uint32_t)(k >> 1)),
                                      &xi[k], &xi[k + 1]);
+#else
+            xi[0] = xi[1] = xi[2] = xi[3] = 0.01 * (double)(gi[p] & 7);
+#endif
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 if (k >= dm) break;
@@ -2707,7 +2751,7 @@ __device__ __forceinline__ void move_blk_body(const wsmc_term* ctape, const Fold
 #pragma unroll
                 for (int jj = 0; jj <= k; ++jj) dz = dz + Lm[k * dm + jj] * xi[jj];
                 const double x = sv[u * W + ix[p]];
-                const bool bd = (mb.bnd >> u) & 1;
+                const bool bd = BND && ((mb.bnd >> u) & 1);
                 const double zo = bd ? wsmc_to_unc(x, mb.lo[u], mb.hi[u]) : x;
                 const double zn = zo + dz;
                 const double xn = bd ? wsmc_from_unc(zn, mb.lo[u], mb.hi[u]) : zn;
@@ -2717,12 +2761,21 @@ __device__ __forceinline__ void move_blk_body(const wsmc_term* ctape, const Fold
                 prop[u * W + ix[p]] = xn;
             }
         }
+#ifndef WSMC_ABL_NOFOLD
         fold_seg<K, LEAN>(sn, ctape, seg_new, nseg_new, cst, spn[m], ix, ok);
+#else
+#pragma unroll
+        for (int p = 0; p < K; ++p) sn[p] = -0.5 * prop[o * W + ix[p]] * prop[o * W + ix[p]];
+#endif
 #pragma unroll
         for (int p = 0; p < K; ++p) {
             if (!ok[p]) continue;
+#ifndef WSMC_ABL_NOACC
             const double uu = wsmc_uniform_k(seed, mb.op_acc[m], (uint64_t)(goff + gi[p]), 0);
-            const bool a = wsmc_log(uu) < (lpr[p] + sn[p]) - so[p];   // strict; NaN rejects (src/transformers.jl:615)
+#else
+            const double uu = 0.25 + 0.0625 * (double)(gi[p] & 7);
+#endif
+            const bool a = move_accept(uu, (lpr[p] + sn[p]) - so[p]);   // strict; NaN rejects (src/transformers.jl:615)
             if (a) {
                 for (int u = o; u < o + dm; ++u) sv[u * W + ix[p]] = prop[u * W + ix[p]];
                 chg[p] |= ((1 << dm) - 1) << o;
@@ -2751,7 +2804,10 @@ __device__ __forceinline__ void move_blk_body(const wsmc_term* ctape, const Fold
 #ifndef WSMC_MOVE_WAVES
 #define WSMC_MOVE_WAVES 1
 #endif
-template <int K, int LEAN>
+#ifndef WSMC_BLK_K   // particles a thread of the unbounded lean block
+#define WSMC_BLK_K 2
+#endif
+template <int K, int LEAN, int BND>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WSMC_MOVE_WAVES))) void k_move_blk(ProgInlineBlk, FoldSlots fs, MoveBlk mb, const double* Lb,
                                                      uint64_t seed, int64_t goff, int64_t N, u64* accepted,
                                                      const int32_t* flag, MoveCarry mc, int32_t cache_from,
@@ -2760,7 +2816,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WSMC_MOV
     const int32_t* hdr = reinterpret_cast<const int32_t*>(ka);
     const char* pb = ka + offsetof(ProgInlineBlk, w);
     const FoldSeg* seg_new = reinterpret_cast<const FoldSeg*>(pb + hdr[0]);
-    move_blk_body<K, LEAN>(reinterpret_cast<const wsmc_term*>(pb), seg_new, seg_new + hdr[2],
+    move_blk_body<K, LEAN, BND>(reinterpret_cast<const wsmc_term*>(pb), seg_new, seg_new + hdr[2],
                            reinterpret_cast<const double*>(pb + hdr[1]), nseg_new, nseg_old, fs, mb, Lb, seed, goff,
                            N, accepted, flag, mc, cache_from, lg, tab);
 }
@@ -3636,15 +3692,17 @@ static MomArgs mom_args(const int32_t* tcols, int d, const double* lo, const dou
 hipError_t launch_autorw_moments(hipStream_t s, const double* w, const MaxSlots* ms, double* const* cols,
                                  const int32_t* tcols, int d, const double* lo, const double* hi, const u64* pv,
                                  int64_t N, double* tilepart, const Decision* wreset, const Decision* gate,
-                                 const int32_t* lag_anc, const Decision* lag_dec, int lag_mask) {
+                                 const int32_t* lag_anc, const Decision* lag_dec, int lag_mask, int32_t* zflag,
+                                 u64* zcount) {
     const MomArgs ma = mom_args(tcols, d, lo, hi);
     const int64_t nt = (N + kTile - 1) / kTile;
     const MomLag lg{lag_mask ? lag_anc : nullptr, lag_dec, lag_mask};
+    const MomZero z{zflag, zcount};
     switch (d) {
-        case 1: hipLaunchKernelGGL(k_moments1<1>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart, wreset, gate, lg); break;
-        case 2: hipLaunchKernelGGL(k_moments1<2>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart, wreset, gate, lg); break;
-        case 3: hipLaunchKernelGGL(k_moments1<3>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart, wreset, gate, lg); break;
-        default: hipLaunchKernelGGL(k_moments1<4>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart, wreset, gate, lg); break;
+        case 1: hipLaunchKernelGGL(k_moments1<1>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart, wreset, gate, lg, z); break;
+        case 2: hipLaunchKernelGGL(k_moments1<2>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart, wreset, gate, lg, z); break;
+        case 3: hipLaunchKernelGGL(k_moments1<3>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart, wreset, gate, lg, z); break;
+        default: hipLaunchKernelGGL(k_moments1<4>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart, wreset, gate, lg, z); break;
     }
     return hipGetLastError();
 }
@@ -3682,13 +3740,21 @@ hipError_t launch_move_blk(hipStream_t s, const ProgInlineBlk* pin, const wsmc_t
     const MomLag lg{lag_mask ? lag_anc : nullptr, lag_dec, lag_mask};
     const size_t row = sizeof(double) * kBlock * (size_t)(fs.n + mb.off[mb.nm]);
     const dim3 g1((unsigned)((N + kBlock - 1) / kBlock)), g2((unsigned)((N + 2 * kBlock - 1) / (2 * kBlock)));
+    const dim3 gk((unsigned)((N + WSMC_BLK_K * kBlock - 1) / (WSMC_BLK_K * kBlock)));
     if (pin) {
-        if (fs.heavy)
-            hipLaunchKernelGGL((k_move_blk<1, 2>), g1, dim3(kBlock), row, s, *pin, fs, mb, Lb, seed, goff, N, accepted,
+        const bool bnd = mb.bnd != 0;
+        if (fs.heavy && bnd)
+            hipLaunchKernelGGL((k_move_blk<1, 2, 1>), g1, dim3(kBlock), row, s, *pin, fs, mb, Lb, seed, goff, N, accepted,
                                flag, mc, cache_from, prog.nseg_new, prog.nseg_old, lg, tab);
-        else
-            hipLaunchKernelGGL((k_move_blk<2, 1>), g2, dim3(kBlock), 2 * row, s, *pin, fs, mb, Lb, seed, goff, N,
+        else if (fs.heavy)
+            hipLaunchKernelGGL((k_move_blk<1, 2, 0>), g1, dim3(kBlock), row, s, *pin, fs, mb, Lb, seed, goff, N, accepted,
+                               flag, mc, cache_from, prog.nseg_new, prog.nseg_old, lg, tab);
+        else if (bnd)
+            hipLaunchKernelGGL((k_move_blk<2, 1, 1>), g2, dim3(kBlock), 2 * row, s, *pin, fs, mb, Lb, seed, goff, N,
                                accepted, flag, mc, cache_from, prog.nseg_new, prog.nseg_old, lg, tab);
+        else
+            hipLaunchKernelGGL((k_move_blk<WSMC_BLK_K, 1, 0>), gk, dim3(kBlock), WSMC_BLK_K * row, s, *pin, fs, mb, Lb,
+                               seed, goff, N, accepted, flag, mc, cache_from, prog.nseg_new, prog.nseg_old, lg, tab);
     } else {
         if (fs.heavy)
             hipLaunchKernelGGL((k_move_blk_g<1, 2>), g1, dim3(kBlock), row, s, ctape, prog, fs, mb, Lb, seed, goff, N,

@@ -155,6 +155,9 @@ SIGNATURES = {
     "wsmc_debug_exact": (C.c_int, [_P, C.c_int64, C.c_int64, C.POINTER(C.c_int64)]),
     "wsmc_debug_jit_stats": (C.c_int, [C.POINTER(C.c_int64)]),
     "wsmc_debug_jit_selfcheck": (C.c_int, []),
+    "wsmc_debug_log_screen": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p]),
+    "wsmc_debug_mv_jit_stats": (C.c_int, [C.POINTER(C.c_int64)]),
+    "wsmc_debug_mv_jit_selfcheck": (C.c_int, []),
 }
 
 
@@ -162,6 +165,14 @@ def jit_stats() -> dict:
     """Process-wide counters of the statement batches compiled for their shape (csrc/wsmc_jit.hip)."""
     st = (C.c_int64 * 5)()
     check(load_library().wsmc_debug_jit_stats(st))
+    return {"compiled": st[0], "failed": st[1], "launched": st[2], "interpreted": st[3],
+            "compile_s": st[4] / 1e6}
+
+
+def mv_jit_stats() -> dict:
+    """Process-wide counters of the Move blocks compiled for their shape (csrc/wsmc_mv_body.h)."""
+    st = (C.c_int64 * 5)()
+    check(load_library().wsmc_debug_mv_jit_stats(st))
     return {"compiled": st[0], "failed": st[1], "launched": st[2], "interpreted": st[3],
             "compile_s": st[4] / 1e6}
 
