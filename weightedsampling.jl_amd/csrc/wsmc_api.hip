@@ -717,7 +717,7 @@ int wsmc_destroy(wsmc_ctx* c) {
     void* bufs[] = {c->dec_always, c->xchg, c->scache, c->scache_back, c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->cdf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount, c->wslots[0], c->wslots[1],
                     c->d_colptr, c->run_params, c->d_tape, c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp,
                     c->vscratch, c->xscratch, c->xp, c->comb, c->anc_out, c->xbuf, c->d_comp, c->d_ctape, c->d_prog, c->rs_grp[0], c->rs_grp[1],
-                    c->xpairs, c->xnb, c->xwin, c->xstat, c->w_save, c->xms, c->xanc, c->xlines};
+                    c->xpairs, c->xnb, c->xwin, c->xstat, c->w_save, c->xms, c->xanc, c->xlines, c->xpeer};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (double* p : c->xrun)
@@ -2793,6 +2793,35 @@ static int32_t compile_fold(const std::vector<wsmc_term>& ct, int32_t j0, int32_
     return (int32_t)(segs.size() - s0);
 }
 
+static int move_block_fused(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, int32_t gated,
+                            int64_t* accepted_out, bool* done);
+// WSMC_DIAG_NO_BLOCK1=1: single Moves keep their own kernels (k_move_c / k_move_ci), for comparison
+static bool no_block1() {
+    static const bool v = [] {
+        const char* e = getenv("WSMC_DIAG_NO_BLOCK1");
+        return e && atoi(e) != 0;
+    }();
+    return v;
+}
+// a single Move as a block of one: wsmc_move's arguments as a wsmc_move_spec (false: not
+// expressible — the Move takes its own path)
+static bool move_spec_of(int32_t proposal, const int32_t* targets, int32_t d, double step, const double* lo,
+                         const double* hi, int32_t target_depth, wsmc_move_spec& sp) {
+    if (proposal != WSMC_PROPOSAL_AUTORW || !targets || d < 1 || d > 4) return false;
+    std::memset(&sp, 0, sizeof(sp));
+    sp.proposal = proposal;
+    sp.d = d;
+    for (int k = 0; k < d; ++k) {
+        sp.targets[k] = targets[k];
+        sp.lo[k] = lo ? lo[k] : -INFINITY;
+        sp.hi[k] = hi ? hi[k] : INFINITY;
+    }
+    sp.bounded = (lo || hi) ? 1 : 0;
+    sp.target_depth = target_depth;
+    sp.step = step;
+    return true;
+}
+
 int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, double step, const double* lo,
               const double* hi, int32_t target_depth, double diversity, int64_t* accepted_out) {
     if (c && c->multi)
@@ -2800,6 +2829,15 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
     // the weights are read by the autoRW moments only, which apply a pending fused-Resample
     // reset themselves (the next Observe applies it to the weights); sharded: settled below
     CHECK_CTX_KEEP(c);
+    // an autoRW Move without a diversity gate: a block of one (the fused block path, compiled for
+    // its shape), the same bits (tests/test_gpu_parity.py)
+    wsmc_move_spec sp1;
+    if (std::isnan(diversity) && !c->move_gate && !is_sharded(c) && !no_block1() &&
+        move_spec_of(proposal, targets, d, step, lo, hi, target_depth, sp1)) {
+        bool done = false;
+        const int r = move_block_fused(c, 1, &sp1, 0, accepted_out, &done);
+        if (done) return r;
+    }
     const uint64_t op_prop = c->op++, op_acc = c->op++;
     if (accepted_out) *accepted_out = 0;
     if (!targets || d < 1 || d > 4) return fail(WSMC_EARG, "move needs 1..4 targets");
@@ -3068,6 +3106,12 @@ int wsmc_move_gated(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32
         }
         return wsmc_move(c, proposal, targets, d, step, lo, hi, target_depth, diversity, nullptr);
     }
+    wsmc_move_spec sp1;
+    if (!no_block1() && move_spec_of(proposal, targets, d, step, lo, hi, target_depth, sp1)) {
+        bool done = false;
+        const int r = move_block_fused(c, 1, &sp1, 1, nullptr, &done);
+        if (done) return r;
+    }
     c->move_gate = gate;
     const int r = wsmc_move(c, proposal, targets, d, step, lo, hi, target_depth, diversity, nullptr);
     c->move_gate = nullptr;
@@ -3162,6 +3206,17 @@ int wsmc_move_block(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, int32_t
     if (n == 0) return WSMC_OK;
     if (c->multi) return move_block_each(c, n, specs, gated, accepted_out);
     CHECK_CTX_KEEP(c);
+    bool done = false;
+    const int r = move_block_fused(c, n, specs, gated, accepted_out, &done);
+    return done ? r : move_block_each(c, n, specs, gated, accepted_out);
+}
+
+// The fused path of a block (also a single autoRW Move's, wsmc_move / wsmc_move_gated): *done
+// false when the block is outside it — nothing has been changed then, and the caller runs the
+// moves one by one
+static int move_block_fused(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, int32_t gated,
+                            int64_t* accepted_out, bool* done) {
+    *done = false;
     // the fused path: autoRW Moves on disjoint scalar targets (8 in all), one target depth, one
     // GPU, a lean fold program
     int32_t depth = specs[0].target_depth < 0 ? c->depth : specs[0].target_depth;
@@ -3200,7 +3255,7 @@ int wsmc_move_block(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, int32_t
         mb.min_step[m] = sp.step;
         D += sp.d;
     }
-    if (!fuse) return move_block_each(c, n, specs, gated, accepted_out);
+    if (!fuse) return WSMC_OK;
     mb.off[n] = (int8_t)D;
     // the fold program over the union's slots (targets first), compiled before anything runs
     int32_t kD = 0;
@@ -3243,7 +3298,8 @@ int wsmc_move_block(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, int32_t
     bool lean = (int)slots.size() <= kFoldSlots;
     for (const auto& sg : segs)
         if (sg.kind == kSegTerm && !wsmc_term_is_scalar(&tmpls[sg.tmpl])) lean = false;
-    if (!lean) return move_block_each(c, n, specs, gated, accepted_out);
+    if (!lean) return WSMC_OK;
+    *done = true;
     const size_t ct_bytes = sizeof(wsmc_term) * tmpls.size();
     const size_t seg_bytes = sizeof(FoldSeg) * segs.size();
     const size_t prog_bytes = ct_bytes + seg_bytes + sizeof(double) * cst.size();
@@ -3687,6 +3743,7 @@ static int ensure_exact_async(wsmc_ctx* c, int32_t T, int64_t cap, int64_t ctr) 
     WSMC_HIP(ctx_sync(c, c->stream));
     if (!c->xpairs) WSMC_HIP(hipMalloc(&c->xpairs, sizeof(double) * 6 * (size_t)N));
     if (!c->xstat) WSMC_HIP(hipMalloc(&c->xstat, sizeof(unsigned long long) * kMaxShards * kXStat));
+    if (c->peer_ok && !c->xpeer) WSMC_HIP(hipMalloc(&c->xpeer, sizeof(unsigned long long) * kMaxShards * 8));
     if (!c->w_save) WSMC_HIP(hipMalloc(&c->w_save, sizeof(double) * (size_t)N));
     if (cap > c->xnb_cap) {
         if (c->xnb) WSMC_HIP(hipFree(c->xnb));
@@ -3842,7 +3899,17 @@ static int enqueue_ssm2d_exact(wsmc_ctx* c, const RunPlan& p, int64_t cap, int64
     const int64_t ww = (int64_t)T * ctr * 3;
     unsigned long long* const wsnd[2] = {c->xwin, c->xwin + ww};
     unsigned long long* const wrcv[2] = {c->xwin + 2 * ww, c->xwin + 3 * ww};
-    const bool wins = p.keep && W > 1 && !c->x_trace;
+    // shards of one process that can read each other's memory trace lineages through the
+    // owners' rows and history in place (no windows, no cross-rank trace after the run)
+    const bool peer = c->peer_ok && p.keep && W > 1 && c->xpeer;
+    const bool wins = p.keep && W > 1 && !c->x_trace && !peer;
+    if (peer) {
+        const unsigned long long pw[8] = {(unsigned long long)(uintptr_t)(c->xanc + cap), (unsigned long long)S,
+                                          (unsigned long long)(uintptr_t)p.d_hist_work,
+                                          (unsigned long long)c->goff, (unsigned long long)N, 0ull, 0ull, 0ull};
+        WSMC_HIP(launch_put_words(c->stream, c->xpeer + (size_t)me * 8, pw));
+        if ((r = exchange_words(c, c->xpeer, 8, c->stream))) return r;
+    }
     if (wins) {
         ExactWin w;
         w.hist_work = p.d_hist_work;
@@ -3882,6 +3949,8 @@ static int enqueue_ssm2d_exact(wsmc_ctx* c, const RunPlan& p, int64_t cap, int64
     f.win[0] = wins && me > 0 ? wrcv[0] : nullptr;
     f.win[1] = wins && me + 1 < W ? wrcv[1] : nullptr;
     f.stat = stat;
+    f.peer = peer ? c->xpeer : nullptr;
+    f.world = W;
     WSMC_HIP(launch_exact_final(c->stream, f));
     // every rank's overflow bits: all ranks take the same branch (re-run or not) afterwards
     return exchange_words(c, c->xstat, kXStat, c->stream);

@@ -222,6 +222,11 @@ struct wsmc_ctx {
                                             // wander far): later runs ship no windows and trace the
                                             // history across ranks after the run (exact_trace_history)
     int64_t x_traces = 0;                   // runs whose history was traced across ranks
+    bool peer_ok = false;                   // every rank is a shard of this process's multi-device
+                                            // handle and can read the others' memory (same device,
+                                            // or peer access over xGMI): the exact trace-back reads
+                                            // the owners' ancestor rows and history in place
+    unsigned long long* xpeer = nullptr;    // [kMaxShards][8] every rank's trace-back words (all-gathered)
     wsmc_term* d_ctape = nullptr;           // compiled Move tape (slot operands)
     int64_t d_ctape_cap = 0;
     void* d_prog = nullptr;                 // compiled fold program: segments, then constants
@@ -573,6 +578,9 @@ struct ExactWin {
     int32_t T, has_left, has_right;
 };
 hipError_t launch_exact_window_pack(hipStream_t s, const ExactWin& w);
+struct PutWords {   // eight words for k_put_words (kernel arguments: capturable, no host buffer)
+    unsigned long long w[8];
+};
 struct ExactFinal {
     int32_t T, keep_history;
     int64_t N, goff, ctr;
@@ -594,8 +602,14 @@ struct ExactFinal {
     const Decision* dec;
     const unsigned long long* win[2];           // windows received from the left / right neighbour
     unsigned long long* stat;
+    // peer reads (ctx peer_ok): every rank's {ancestor rows at its own slot 0, row stride,
+    // history table, first global index, N} (8 words a rank); lineages outside this shard read
+    // the owner's rows and history in place, no windows
+    const unsigned long long* peer = nullptr;
+    int32_t world = 1;
 };
 hipError_t launch_exact_final(hipStream_t s, const ExactFinal& f);
+hipError_t launch_put_words(hipStream_t s, unsigned long long* dst, const unsigned long long (&w)[8]);
 hipError_t launch_rs_scan(hipStream_t s, int64_t N, const ShardRecord* rec, const Decision* dec,
                           const FillPlan& plan, const unsigned long long* tileOff,
                           const unsigned long long* qbuf, int32_t* anc, hipEvent_t e0 = nullptr,

@@ -941,9 +941,31 @@ __device__ __forceinline__ const u64* exact_win(const ExactFinal& f, int L, int6
         return f.win[1] + ((int64_t)(L - 1) * f.ctr + (g - (f.goff + f.N))) * 3;
     return nullptr;
 }
+// the owner of global index g among the ranks' peer words (W <= kMaxShards): its ancestor row
+// entry at level L (row L - 1) and its history pair at level L; false if no rank holds g
+__device__ __forceinline__ bool exact_peer_of(const ExactFinal& f, int64_t g, int& h, int64_t& loc) {
+    for (int r = 0; r < f.world; ++r) {
+        const int64_t o = (int64_t)f.peer[8 * r + 3], n = (int64_t)f.peer[8 * r + 4];
+        if (g >= o && g < o + n) {
+            h = r;
+            loc = g - o;
+            return true;
+        }
+    }
+    return false;
+}
+__global__ void k_put_words(unsigned long long* dst, PutWords w) {
+    if (threadIdx.x < 8) dst[threadIdx.x] = w.w[threadIdx.x];
+}
+hipError_t launch_put_words(hipStream_t s, unsigned long long* dst, const unsigned long long (&w)[8]) {
+    PutWords pw;
+    for (int k = 0; k < 8; ++k) pw.w[k] = w[k];
+    hipLaunchKernelGGL(k_put_words, dim3(1), dim3(64), 0, s, dst, pw);
+    return hipGetLastError();
+}
 // k_ssm2d_final on exact shards: ancestors are global ids; ids of this rank read its own
 // buffers, a neighbour's come from the last step's received pairs (level T) or the trace
-// windows (levels below)
+// windows (levels below), or — shards of one process (f.peer) — the owner's buffers in place
 __global__ __launch_bounds__(kBlock) void k_exact_final(ExactFinal f) {
     __shared__ u64 lds4[4];
     const int64_t N = f.N;
@@ -975,8 +997,12 @@ __global__ __launch_bounds__(kBlock) void k_exact_final(ExactFinal f) {
                     exc = d > exc ? d : exc;
                 }
                 if (f.dec[s].resampled) {
+                    int h;
+                    int64_t pl;
                     if (in) g = f.anc_log[(int64_t)(s - 1) * S + loc];
                     else if (wv) g = (int64_t)(int32_t)(uint32_t)wv[2];
+                    else if (f.peer && exact_peer_of(f, g, h, pl))   // the owner's row, in place
+                        g = reinterpret_cast<const int32_t*>(f.peer[8 * h])[(int64_t)(s - 1) * (int64_t)f.peer[8 * h + 1] + pl];
                     else bad = 1;
                 }
                 loc = g - f.goff;
@@ -988,7 +1014,11 @@ __global__ __launch_bounds__(kBlock) void k_exact_final(ExactFinal f) {
                     const u64 d = (u64)(g < f.goff ? f.goff - g : g - (f.goff + N) + 1);
                     exc = d > exc ? d : exc;
                     const u64* wx = exact_win(f, s, g);
+                    int h;
+                    int64_t pl;
                     if (wx) x = d2{wsmc_bits2d(wx[0]), wsmc_bits2d(wx[1])};
+                    else if (f.peer && exact_peer_of(f, g, h, pl))   // the owner's history, in place
+                        x = *reinterpret_cast<const d2*>(reinterpret_cast<double* const*>(f.peer[8 * h + 2])[s + 1] + 2 * pl);
                     else bad = 1;
                 }
                 double* dst = f.hist_out[s + 1];

@@ -14,6 +14,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -430,6 +431,31 @@ extern "C" int wsmc_create_multi(wsmc_ctx** out, int64_t n_particles, int32_t n_
             M->sub[g]->host_inproc = true;
         }
     }
+    // the shards can read each other's device memory (one device, or peer access over xGMI):
+    // the exact trace-back then reads lineages in their owners' buffers (csrc/wsmc_kernels.hip
+    // k_exact_final); WSMC_DIAG_NO_PEER=1 keeps the trace windows and the cross-rank trace
+    bool peer = G > 1;
+    {
+        const char* e = getenv("WSMC_DIAG_NO_PEER");
+        if (e && atoi(e) != 0) peer = false;
+    }
+    int cur = 0;
+    hipGetDevice(&cur);
+    for (int g = 0; g < G && peer; ++g)
+        for (int h = 0; h < G && peer; ++h) {
+            if (devs[g] == devs[h]) continue;
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, devs[g], devs[h]) != hipSuccess || !can) {
+                peer = false;
+                break;
+            }
+            hipSetDevice(devs[g]);
+            const hipError_t e = hipDeviceEnablePeerAccess(devs[h], 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) peer = false;
+        }
+    (void)hipGetLastError();
+    hipSetDevice(cur);
+    for (int g = 0; g < G; ++g) M->sub[g]->peer_ok = peer;
     M->workers.resize(G);
     for (int g = 1; g < G; ++g) {
         M->workers[g] = std::make_unique<Worker>();
