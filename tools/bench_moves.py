@@ -49,7 +49,7 @@ def c3(N=1_000_000, reps=3, wait_moves=True, one_rank=False, gated=False, block=
 
 
 def c5(N=4_000_000, T=60, sweeps=5, reps=1, scheme="systematic", ess=1.0, diversity=None, one_rank=False,
-       wait_moves=True):
+       wait_moves=True, block=False):
     t_obs, y_obs = models.oscillator_data(n=T)
     sch = {"systematic": wsmc.RESAMPLE_SYSTEMATIC, "stratified": wsmc.RESAMPLE_STRATIFIED}[scheme]
     best, moved = math.inf, 0
@@ -58,7 +58,7 @@ def c5(N=4_000_000, T=60, sweeps=5, reps=1, scheme="systematic", ess=1.0, divers
         ctx.sync()
         t0 = time.perf_counter()
         acc = models.oscillator_statements(ctx, t_obs, y_obs, ess_perc_min=ess, scheme=sch, sweeps=sweeps,
-                                           diversity=diversity, wait_moves=wait_moves)
+                                           diversity=diversity, wait_moves=wait_moves, block=block)
         ctx.sync()
         dt = time.perf_counter() - t0
         ctx.close()
@@ -67,6 +67,7 @@ def c5(N=4_000_000, T=60, sweeps=5, reps=1, scheme="systematic", ess=1.0, divers
     gate = "ungated" if diversity is None else f"diversity={diversity}"
     out = {"config": f"C5 damped oscillator, {scheme}, {sweeps} {gate} sweep(s) (N={N}, T={T}, ess {ess})"
                      + ("" if wait_moves else ", asynchronous moves (no accepted counts)")
+                     + (", each sweep one Move block (wsmc_move_block)" if block else "")
                      + (", sharded path (one-rank RCCL communicator)" if one_rank else ""),
            "N": N, "T": T, "seconds_per_run": best, "particle_steps_per_s": N * T / best,
            "accepted": moved, "moves_offered": 2 * sweeps * T}
@@ -117,6 +118,8 @@ LEGS = {
     "c3gated": lambda: c3(gated=True),
     "c3gated_moves": lambda: c3(gated=True, block=False),                 # two wsmc_move_gated
     "c5async": lambda: c5(wait_moves=False),
+    "c5block": lambda: c5(block=True),
+    "c5blockasync": lambda: c5(block=True, wait_moves=False),
     "c3_rccl1": lambda: c3(one_rank=True),
     "c3async_rccl1": lambda: c3(wait_moves=False, one_rank=True),
     "c5_rccl1": lambda: c5(one_rank=True),

@@ -98,10 +98,12 @@ bench)  timeout -k 10 400 python bench.py "$@" > $O/bench.json 2> $O/bench.err |
   step 400 $O/stats.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python bench.py --no-cpu-baseline --steps 20 --warmup 2 "$@"
   stats_table $O/stats/run_kernel_stats.csv 8 ;;
 moves)
-  timeout -k 10 400 python tools/bench_moves.py c3 c3async c3gated_moves c3gated c5 c5async c3cpu > $O/moves.jsonl 2> $O/moves.err || { tail $O/moves.err; exit 1; }
+  timeout -k 10 400 python tools/bench_moves.py c3 c3async c3gated_moves c3gated c5 c5async c5block c5blockasync c3cpu > $O/moves.jsonl 2> $O/moves.err || { tail $O/moves.err; exit 1; }
   cut -c1-330 $O/moves.jsonl
   step 300 $O/c3.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/c3 -o run -- python tools/bench_moves.py c3gated
-  stats_table $O/c3/run_kernel_stats.csv 10 ;;
+  stats_table $O/c3/run_kernel_stats.csv 10
+  step 300 $O/c5.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/c5 -o run -- python tools/bench_moves.py c5
+  stats_table $O/c5/run_kernel_stats.csv 8 ;;
 c5flops)
   step 600 $O/stats.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python tools/bench_moves.py c5
   step 900 $O/pmc.log rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 --output-format csv -d $O/pmc -o run -- python tools/bench_moves.py c5

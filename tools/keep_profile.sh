@@ -10,7 +10,7 @@ for f in MANIFEST bench.json bench_statements.json pmc_summary.json pmc_step_byt
          mr_island.json mr_exact.json mr_strong.json mh_island.json mh_exact.json; do
   [ -f "$O/$f" ] && cp "$O/$f" "profiles/${tag}_${f/pytest_gpu.log/pytest_gpu.txt}"
 done
-for d in stats gstats st c3; do
+for d in stats gstats st c3 c5; do
   [ -f "$O/$d/run_kernel_stats.csv" ] && cp "$O/$d/run_kernel_stats.csv" "profiles/${tag}_${d}_kernel_stats.csv"
 done
 for f in "$O"/*.txt; do [ -f "$f" ] && cp "$f" "profiles/${tag}_$(basename "$f")"; done

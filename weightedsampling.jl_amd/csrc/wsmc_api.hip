@@ -3151,6 +3151,15 @@ static int move_block_each(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, 
     return WSMC_OK;
 }
 
+// WSMC_DIAG_MV_K1=1: oscillator (heavy) blocks compiled one particle a thread, as the
+// interpreter runs them (two a thread by default: the run loop's per-term control is shared)
+static bool mv_heavy_k1() {
+    static const bool v = [] {
+        const char* e = getenv("WSMC_DIAG_MV_K1");
+        return e && atoi(e) != 0;
+    }();
+    return v;
+}
 // a Move block's shape for csrc/wsmc_mv_body.h (false: outside what it compiles — the
 // interpreter kernels run the block): its moves, which targets are bounded or read through the
 // lag row, and the lean fold program's segments with the slots each template operand reads
@@ -3160,7 +3169,7 @@ static bool mv_signature(const FoldSlots& fs, const MoveBlk& mb, int D, int lag_
     std::memset(&g, 0, sizeof(g));
     if (fs.n < 1 || fs.n > kFoldSlots || D < 1 || D > kBlkTargets || mb.nm < 1 || mb.nm > 4) return false;
     if (nseg_new > kMvSegs || nseg_old > kMvSegs || tmpls.size() > 64) return false;
-    g.K = fs.heavy ? 1 : 2;
+    g.K = (fs.heavy && mv_heavy_k1()) ? 1 : 2;
     g.nm = (int8_t)mb.nm;
     g.D = (int8_t)D;
     g.ns = (int8_t)fs.n;

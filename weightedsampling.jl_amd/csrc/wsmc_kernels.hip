@@ -99,6 +99,25 @@ __device__ __forceinline__ double block_sum_canon(double v, double* lds4) {
     __syncthreads();
     return r;
 }
+// block_sum_canon of NV values at once: the same butterfly and wave order per value (the same
+// bits), their shuffles interleaved and one barrier pair for all of them; lds [NV][4]
+template <int NV>
+__device__ __forceinline__ void block_sum_canon_n(const double (&v)[NV], double (*lds)[4], double (&out)[NV]) {
+    double x[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) x[k] = v[k];
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) x[k] = x[k] + __shfl_xor(x[k], off, 64);
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) lds[k][threadIdx.x >> 6] = x[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NV; ++k) out[k] = (lds[k][0] + lds[k][1]) + (lds[k][2] + lds[k][3]);
+    __syncthreads();
+}
 __device__ __forceinline__ u64 block_sum_u64(u64 v, u64* lds4) {
     v = wave_sum_u64(v);
     if ((threadIdx.x & 63) == 0) lds4[threadIdx.x >> 6] = v;
@@ -2161,11 +2180,12 @@ __global__ __launch_bounds__(kBlock) void k_moments1(const double* __restrict__ 
         for (int v = 0; v < NV; ++v) acc[v] = acc[v] + vals[v];
     }
     }
+    __shared__ double ldsn[NV][4];
+    double tot[NV];
+    block_sum_canon_n<NV>(acc, ldsn, tot);
+    if (threadIdx.x == 0)
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-        const double s = block_sum_canon(acc[v], lds4);
-        if (threadIdx.x == 0) tilepart[(int64_t)v * ntiles + blockIdx.x] = s;
-    }
+        for (int v = 0; v < NV; ++v) tilepart[(int64_t)v * ntiles + blockIdx.x] = tot[v];
 }
 // one block: the canonical combine of the tile partials (k_moments_final's order); raw: the
 // totals to mom[48..] (a sharded run all-gathers them), else the factor: mom[16..] the scaled
@@ -2184,10 +2204,13 @@ __global__ __launch_bounds__(kBlock) void k_autorw_final(const double* tilepart,
     for (int64_t b = threadIdx.x; b < ntiles; b += kBlock)
 #pragma unroll
         for (int v = 0; v < NV; ++v) acc[v] = acc[v] + tilepart[(int64_t)v * ntiles + b];
+    {
+        __shared__ double ldsn[NV][4];
+        double t[NV];
+        block_sum_canon_n<NV>(acc, ldsn, t);
+        if (threadIdx.x == 0)
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-        const double s = block_sum_canon(acc[v], lds4);
-        if (threadIdx.x == 0) tot[v] = s;
+            for (int v = 0; v < NV; ++v) tot[v] = t[v];
     }
     __syncthreads();
     if (threadIdx.x != 0) return;
@@ -2626,10 +2649,13 @@ __global__ __launch_bounds__(kBlock) void k_autorw_final_blk(const double* tilep
     for (int64_t b = threadIdx.x; b < ntiles; b += kBlock)
 #pragma unroll
         for (int v = 0; v < NV; ++v) acc[v] = acc[v] + tilepart[(int64_t)v * ntiles + b];
+    {
+        __shared__ double ldsn[NV][4];
+        double t[NV];
+        block_sum_canon_n<NV>(acc, ldsn, t);
+        if (threadIdx.x == 0)
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-        const double s = block_sum_canon(acc[v], lds4);
-        if (threadIdx.x == 0) tot[v] = s;
+            for (int v = 0; v < NV; ++v) tot[v] = t[v];
     }
     __syncthreads();
     if (threadIdx.x != 0) return;
