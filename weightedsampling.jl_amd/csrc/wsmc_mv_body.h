@@ -178,37 +178,41 @@ __device__ __forceinline__ void mv_fold(double (&s)[K], const double (&v)[K][NS]
             }
             const double* c = cst + h.coff;
             double zr[K], zi[K], rr[K], ri[K];
-            double cur_ta = WSMC_NAN, r_d = WSMC_NAN;
-            int cur_m = -2;
+            // a run's terms come from wsmc_osc_link on consecutive tape terms: after the fold's
+            // first term each one either opens a block (m = 0: its direct phasor) or continues the
+            // previous term's block (m = m' + 1, the same t_a and step), so the continuation test of
+            // fold_seg reduces to m != 0 — a scalar compare of the constant's bits, no conversion.
+            // The step R is recomputed when the block's step changes (at its m = 1 term, whose
+            // predecessor's phasor is the anchor: one rotation of it gives fold_seg's anchor + 1
+            // rotation bit for bit). The first term may enter a block mid-way: anchor, m rotations.
+            double r_d = WSMC_NAN;
             const bool any = h.count > 0;
             double q0 = any ? c[0] : 0.0, q1 = any ? c[1] : 0.0, q2 = any ? c[2] : 0.0, q3 = any ? c[3] : 0.0;
             for (int32_t k = 0; k < h.count; ++k) {
-                const double ta = q0, dl = q1, y = q3;
-                const int m = (int)q2;
+                const double ta = q0, dl = q1, mq = q2, y = q3;
                 if (k + 1 < h.count) {
                     q0 = c[4 * k + 4];
                     q1 = c[4 * k + 5];
                     q2 = c[4 * k + 6];
                     q3 = c[4 * k + 7];
                 }
-                const bool next = m > 0 && m == cur_m + 1 && wsmc_d2bits(ta) == wsmc_d2bits(cur_ta) &&
-                                  wsmc_d2bits(dl) == wsmc_d2bits(r_d);
-                if (m > 0 && wsmc_d2bits(dl) != wsmc_d2bits(r_d)) {   // uniform
+                const bool m0 = wsmc_d2bits(mq) == 0;
+                if (!m0 && wsmc_d2bits(dl) != wsmc_d2bits(r_d)) {   // uniform
 #pragma unroll
                     for (int p = 0; p < K; ++p) wsmc_osc_step(dl, om[p], ga[p], &rr[p], &ri[p]);
                     r_d = dl;
                 }
+                if (m0 || k == 0) {   // uniform
+                    const int m = m0 ? 0 : (int)mq;
 #pragma unroll
-                for (int p = 0; p < K; ++p) {
-                    if (next) {
-                        wsmc_osc_rotate(&zr[p], &zi[p], rr[p], ri[p]);
-                    } else {
+                    for (int p = 0; p < K; ++p) {
                         wsmc_osc_anchor(ta, A[p], om[p], ga[p], ph[p], &zr[p], &zi[p]);
                         for (int j = 0; j < m; ++j) wsmc_osc_rotate(&zr[p], &zi[p], rr[p], ri[p]);
                     }
+                } else {
+#pragma unroll
+                    for (int p = 0; p < K; ++p) wsmc_osc_rotate(&zr[p], &zi[p], rr[p], ri[p]);
                 }
-                cur_ta = ta;
-                cur_m = m;
 #pragma unroll
                 for (int p = 0; p < K; ++p) {
                     const double z = (y - zr[p]) * rsd[p];
