@@ -49,9 +49,9 @@ def log(*a):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # 300 runs of T = 100 steps: about 1.3 s of timed GPU work at 1M (long enough for a sampler
+    # 1000 runs of T = 100 steps: about 4 s of timed GPU work at 1M (long enough for a sampler
     # outside the process to see the GPU busy, and a steadier per-run figure), still seconds
-    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--particles", type=int, default=1_000_000, help="particles per GPU (weak scaling)")
     ap.add_argument("--global-particles", type=int, default=0,

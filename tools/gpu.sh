@@ -65,7 +65,7 @@ prof_passes() {   # kernel stats of the bench command at its default 300 runs, s
                   # graph replays past a few thousand dispatches, tools/micro/graph_trace.hip and
                   # DESIGN.md §4), the graph-launched run's stats at 20 runs beside it, then
                   # FETCH_SIZE / WRITE_SIZE in separate passes
-  WSMC_DIAG_NO_GRAPH=1 step 600 $O/stats.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python bench.py --no-cpu-baseline
+  WSMC_DIAG_NO_GRAPH=1 step 600 $O/stats.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python bench.py --no-cpu-baseline --steps 300
   stats_table $O/stats/run_kernel_stats.csv 6
   step 400 $O/gstats.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/gstats -o run -- python bench.py --no-cpu-baseline --steps 20 --warmup 2
   stats_table $O/gstats/run_kernel_stats.csv 6
@@ -139,7 +139,7 @@ segv)  # the r03 crash under the kernel tracer: the libwsmc-free
        # tracer, then the repro's graph replays at R = $1 (a crash ends the recipe: it runs last)
   step 300 $O/stream_trace.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/st -o run -- tools/micro/graph_trace 100 300 1000000 0 0
   tail -1 $O/stream_trace.log
-  WSMC_DIAG_NO_GRAPH=1 step 600 $O/stats.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python bench.py --no-cpu-baseline
+  WSMC_DIAG_NO_GRAPH=1 step 600 $O/stats.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python bench.py --no-cpu-baseline --steps 300
   stats_table $O/stats/run_kernel_stats.csv 6
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/gt -o run -- tools/micro/graph_trace 100 ${1:-100} > $O/graph_trace.log 2>&1
   rc=$?; echo "graph replays R=${1:-100} under the tracer: exit $rc"; tail -1 $O/graph_trace.log ;;
