@@ -3180,6 +3180,11 @@ static bool mv_signature(const FoldSlots& fs, const MoveBlk& mb, int D, int lag_
     for (int k = 0; k <= mb.nm; ++k) g.off[k] = mb.off[k];
     for (int k = mb.nm + 1; k < 5; ++k) g.off[k] = mb.off[mb.nm];
     g.bnd = (uint8_t)(mb.bnd & 0xff);
+    for (int u = 0; u < D; ++u) {
+        if (!((mb.bnd >> u) & 1)) continue;
+        if (std::isfinite(mb.lo[u])) g.flo |= (uint8_t)(1 << u);
+        if (std::isfinite(mb.hi[u])) g.fhi |= (uint8_t)(1 << u);
+    }
     g.lagt = (uint8_t)(lag_targets & 0xff);
     g.smask = (uint16_t)(lag_slots & 0xffff);
     auto shape = [](const wsmc_operand& o, MvSigOp& q) {

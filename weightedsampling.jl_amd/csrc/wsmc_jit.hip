@@ -389,7 +389,7 @@ std::string mv_sig_text(const MvSig& g) {
     s += '{';
     for (int k = 0; k < 5; ++k) num(g.off[k]);
     s += "},";
-    num(g.bnd); num(g.lagt); num(0); num(g.smask); num(0);
+    num(g.bnd); num(g.lagt); num(g.flo); num(g.fhi); num(g.smask);
     s += '{';
     for (int k = 0; k < 2 * kMvSegs; ++k) {
         const MvSigSeg& q = g.seg[k];
