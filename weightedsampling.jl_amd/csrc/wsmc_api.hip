@@ -3160,6 +3160,15 @@ static bool mv_heavy_k1() {
     }();
     return v;
 }
+// WSMC_DIAG_MV_K=1|2|4: particles a thread of the compiled lean (non-oscillator) blocks (2)
+static int mv_lean_k() {
+    static const int v = [] {
+        const char* e = getenv("WSMC_DIAG_MV_K");
+        const int k = e ? atoi(e) : 2;
+        return (k == 1 || k == 4) ? k : 2;
+    }();
+    return v;
+}
 // a Move block's shape for csrc/wsmc_mv_body.h (false: outside what it compiles — the
 // interpreter kernels run the block): its moves, which targets are bounded or read through the
 // lag row, and the lean fold program's segments with the slots each template operand reads
@@ -3169,7 +3178,7 @@ static bool mv_signature(const FoldSlots& fs, const MoveBlk& mb, int D, int lag_
     std::memset(&g, 0, sizeof(g));
     if (fs.n < 1 || fs.n > kFoldSlots || D < 1 || D > kBlkTargets || mb.nm < 1 || mb.nm > 4) return false;
     if (nseg_new > kMvSegs || nseg_old > kMvSegs || tmpls.size() > 64) return false;
-    g.K = (fs.heavy && mv_heavy_k1()) ? 1 : 2;
+    g.K = (fs.heavy && mv_heavy_k1()) ? 1 : (fs.heavy ? 2 : mv_lean_k());
     g.nm = (int8_t)mb.nm;
     g.D = (int8_t)D;
     g.ns = (int8_t)fs.n;
