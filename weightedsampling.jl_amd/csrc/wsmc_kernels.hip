@@ -2118,9 +2118,15 @@ __global__ __launch_bounds__(kBlock) void k_moments1(const double* __restrict__ 
     // targets one lazy Resample behind (lg.mask): read through its ancestors, gated by its
     // decision (the values the trace would have gathered)
     const int lmask = (lg.anc && lg.dec->resampled) ? lg.mask : 0;
-    const double* tp[D];
+    // the column pointers come from a device table: cast to the global address space, so the
+    // gathers are global loads (a generic pointer's flat loads also count in lgkmcnt)
+    typedef const double __attribute__((address_space(1)))* gdp_t;
+    typedef const int32_t __attribute__((address_space(1)))* gip_t;
+    gdp_t tp[D];
 #pragma unroll
-    for (int k = 0; k < d; ++k) tp[k] = cols[ma.tcol[k]];
+    for (int k = 0; k < d; ++k) tp[k] = (gdp_t)cols[ma.tcol[k]];
+    const gip_t lanc = (gip_t)lg.anc;
+    const gdp_t gw = (gdp_t)w;
     double p[4];
     if (pv) {
         autorw_pivot<D>(cols, ma, pv, p);
@@ -2136,24 +2142,32 @@ __global__ __launch_bounds__(kBlock) void k_moments1(const double* __restrict__ 
     // the tile's loads in chunks of CH items (a few memory latencies per thread, not kItems in
     // a row; CH bounded so the loaded values stay in registers), then the canonical per-item
     // accumulation
-    constexpr int CH = D <= 1 ? 8 : (D == 2 ? 4 : 1);
+    constexpr int CH = D <= 1 ? 8 : (D == 2 ? 4 : 2);
     static_assert(kItems % CH == 0, "chunking");
 #pragma unroll 1
     for (int j0 = 0; j0 < kItems; j0 += CH) {
     double xv[CH][D], wv[CH];
     int32_t ai[CH];
+    // every load of the chunk unconditional (an index past N reads particle N - 1, unused), so
+    // they issue back to back with one wait: a load under its own `i < N` branch waited for
+    // each in turn
+    if (lmask) {   // uniform: one branch around the chunk's ancestor loads
 #pragma unroll
-    for (int c = 0; c < CH; ++c) {
-        const int64_t i = base + (int64_t)(j0 + c) * kBlock + threadIdx.x;
-        ai[c] = (lmask && i < N) ? lg.anc[i] : 0;
+        for (int c = 0; c < CH; ++c) {
+            const int64_t i = base + (int64_t)(j0 + c) * kBlock + threadIdx.x;
+            ai[c] = lanc[i < N ? i : N - 1];
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < CH; ++c) ai[c] = 0;
     }
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
         const int64_t i = base + (int64_t)(j0 + c) * kBlock + threadIdx.x;
-        const bool in = i < N;
-        wv[c] = (in && !reset) ? w[i] : 0.0;
+        const int64_t ic = i < N ? i : N - 1;
+        wv[c] = reset ? 0.0 : gw[ic];
 #pragma unroll
-        for (int k = 0; k < d; ++k) xv[c][k] = in ? tp[k][(lmask >> k) & 1 ? (int64_t)ai[c] : i] : 0.0;
+        for (int k = 0; k < d; ++k) xv[c][k] = tp[k][(lmask >> k) & 1 ? (int64_t)ai[c] : ic];
     }
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
