@@ -15,6 +15,16 @@ resampling by default — ranks exchange one statistics payload per step over RC
 `--shard-mode exact` resamples the whole population with the single-GPU bits (particles
 move between ranks).
 
+`--gpus N` is what the line measures, or the run refuses (exit 2, the reason on stderr):
+  * under a launcher (WORLD_SIZE set) WORLD_SIZE must equal N, and each node must see a HIP
+    device per local rank (unless `--same-device`, the one-GPU test mode);
+  * without a launcher and N > 1, one process drives N devices through one multi-device
+    handle (wsmc_create_multi: ncclCommInitAll over devices 0..N-1, peer access, one host
+    thread per shard issuing its own collectives, as a process per GPU would); fewer than N
+    visible devices is a refusal, never a one-GPU run.
+The line's `ranks` object carries what the communicator itself reports (ncclCommCount), the
+devices and the particles per shard.
+
 Rank 0 prints ONE JSON line (metric/value/.../roofline/cpu_baseline). Everything else
 goes to stderr.
 """
@@ -87,6 +97,48 @@ def parse():
     ap.add_argument("--statements", action="store_true")
     ap.add_argument("--eager-store", action="store_true")
     return ap.parse_args()
+
+
+class LayoutError(Exception):
+    """--gpus N cannot be measured as labelled (bench.py exits 2 with this message)."""
+
+
+def visible_devices_note(env) -> str:
+    vis = [f"{k}={env[k]}" for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
+           if k in env]
+    return ", ".join(vis) if vis else "no *_VISIBLE_DEVICES set"
+
+
+def plan_layout(gpus: int, env, device_count, same_device: bool = False, multi_shards: int = 0) -> dict:
+    """How `--gpus N` maps onto processes and devices. `device_count()` is called only when
+    the answer depends on it (it initialises HIP). Raises LayoutError rather than measure a
+    different number of GPUs than the line would say."""
+    if gpus < 1:
+        raise LayoutError(f"--gpus must be >= 1 (got {gpus})")
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        world = int(ws)
+        if world != gpus:
+            raise LayoutError(f"--gpus {gpus} but the launcher started WORLD_SIZE={world} ranks: the line would "
+                              f"not measure what it labels; launch --nproc-per-node {gpus} or pass --gpus {world}")
+        if multi_shards > 1 and world > 1:
+            raise LayoutError("--multi-shards is a one-process diagnostic; do not combine it with a launcher")
+        local_world = int(env.get("LOCAL_WORLD_SIZE", world))
+        if world > 1 and not same_device:
+            n = device_count()
+            if n < local_world:
+                raise LayoutError(f"{local_world} ranks on this node need {local_world} HIP devices (one per rank); "
+                                  f"{n} visible ({visible_devices_note(env)})")
+        return {"mode": "launcher" if world > 1 else "single", "world": world}
+    if gpus > 1:
+        if multi_shards > 1:
+            raise LayoutError("--multi-shards (shards on GPU 0, host exchange) measures one GPU: use it with --gpus 1")
+        n = device_count()
+        if n < gpus:
+            raise LayoutError(f"--gpus {gpus} needs {gpus} HIP devices; {n} visible ({visible_devices_note(env)}); "
+                              f"refusing to measure fewer GPUs than the line would say")
+        return {"mode": "in-process", "world": gpus, "devices": list(range(gpus))}
+    return {"mode": "single", "world": 1}
 
 
 def cpu_threads(requested: int) -> int:
@@ -236,12 +288,27 @@ def main():
     sys.stdout.flush()
     json_fd = os.dup(1)
     os.dup2(2, 1)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import wsmc
     from wsmc import abi
     from wsmc.hostcomm import from_env
+
+    def ndev():
+        try:
+            return wsmc.Context.device_count()
+        except Exception as e:   # no HIP runtime / no device: zero devices, said so
+            log(f"bench: device count failed: {e}")
+            return 0
+    try:
+        lay = plan_layout(args.gpus, os.environ, ndev, same_device=args.same_device,
+                          multi_shards=args.multi_shards)
+    except LayoutError as e:
+        log(f"bench: refusing --gpus {args.gpus}: {e}")
+        sys.exit(2)
+    inproc = lay["mode"] == "in-process"
+    world = 1 if inproc else lay["world"]   # processes
+    G = lay["world"]                         # GPUs the line measures
     # host rendezvous / barriers / max-over-ranks over TCP; the rank process never imports
     # torch (its bundled HIP runtime would clash with libwsmc's ROCm one). The data path
     # between ranks is RCCL inside libwsmc.
@@ -250,20 +317,28 @@ def main():
     scheme = {"stratified": abi.RESAMPLE_STRATIFIED, "systematic": abi.RESAMPLE_SYSTEMATIC,
               "multinomial": abi.RESAMPLE_MULTINOMIAL}[args.scheme]
     if args.global_particles > 0:   # strong scaling: ragged contiguous shards of one population
-        G = args.global_particles
-        N = G // world + (1 if rank < G % world else 0)
-        goff = rank * (G // world) + min(rank, G % world)
-        gN = G
-    else:                           # weak scaling: N per rank
+        P = args.global_particles
+        N = P // world + (1 if rank < P % world else 0)
+        goff = rank * (P // world) + min(rank, P % world)
+        gN = P
+    else:                           # weak scaling: N per GPU
         N = args.particles
         goff, gN = rank * N, world * N
+    if inproc:   # one process, G devices: the handle splits gN into G contiguous shards
+        gN = args.global_particles if args.global_particles > 0 else G * args.particles
+        N, goff = gN // G, 0
     T = args.T
     obs = wsmc.models.ssm2d_data(max(T, args.cpu_T), seed=args.seed)
     # one seed for every rank: the Philox streams are keyed by the global particle index
-    if args.multi_shards > 1 and comm is None:
-        G = args.multi_shards
-        gN = G * N
-        ctx = wsmc.Context.multi(gN, G, seed=args.seed, devices=[0] * G, transport=abi.TRANSPORT_HOST)
+    if inproc:
+        log(f"bench: one process over {G} devices {lay['devices']} (wsmc_create_multi, RCCL), {gN} particles")
+        ctx = wsmc.Context.multi(gN, G, seed=args.seed, devices=lay["devices"], transport=abi.TRANSPORT_RCCL)
+        if args.shard_mode == "exact":
+            ctx.comm_set_shard_mode(abi.SHARD_EXACT)
+    elif args.multi_shards > 1 and comm is None:
+        MS = args.multi_shards
+        gN = MS * N
+        ctx = wsmc.Context.multi(gN, MS, seed=args.seed, devices=[0] * MS, transport=abi.TRANSPORT_HOST)
         if args.shard_mode == "exact":
             ctx.comm_set_shard_mode(abi.SHARD_EXACT)
     else:
@@ -280,7 +355,20 @@ def main():
         ctx.comm_init(wsmc.Context.comm_unique_id(), 1, 0, 0, N)
         if args.shard_mode == "exact":
             ctx.comm_set_shard_mode(abi.SHARD_EXACT)
-    exact = (comm is not None or args.rccl_one_rank or args.multi_shards > 1) and args.shard_mode == "exact"
+    exact = (comm is not None or args.rccl_one_rank or args.multi_shards > 1 or inproc) and args.shard_mode == "exact"
+    # what the communicator reports: every rank's view in rank order (a launcher's ranks
+    # gather theirs over the host rendezvous)
+    info = ctx.comm_info()
+    if comm is not None:
+        got = comm.allgather([info["rank"], info["rccl_ranks"], info["devices"][0], info["shard_n"][0]])
+        ranks = {"launcher": "torch.distributed.run", "processes": world, "rccl_ranks": info["rccl_ranks"],
+                 "transport": info["transport"], "devices": [g[2] for g in got], "shard_n": [g[3] for g in got]}
+    else:
+        ranks = {"launcher": None, "processes": 1, "rccl_ranks": info["rccl_ranks"], "transport": info["transport"],
+                 "devices": info["devices"], "shard_n": info["shard_n"]}
+    if (inproc or comm is not None) and args.exchange == "rccl" and ranks["rccl_ranks"] != G:
+        log(f"bench: the RCCL communicator reports {ranks['rccl_ranks']} ranks, --gpus {G}: refusing the line")
+        sys.exit(2)
     if os.environ.get("WSMC_DUMP_MAPS"):   # diagnostics: the load map, to symbolise a crash's raw frames
         with open(os.environ["WSMC_DUMP_MAPS"], "w") as f:
             f.write(open("/proc/self/maps").read())
@@ -325,7 +413,7 @@ def main():
     # shards (their eager, host-driven run is not instrumented)
     prop_ms = red_ms = rs_ms = fin_ms = tot_ms = 0.0
     nres = 0
-    if not exact and not args.statements and args.multi_shards <= 1:
+    if not exact and not args.statements and args.multi_shards <= 1 and not inproc:
         ctx.set_timing(True)
         inst_runs = max(1, min(args.steps, 5))
         one_run()  # capture the instrumented graph
@@ -360,7 +448,7 @@ def main():
     step_traffic = sj.get("bytes_per_particle_step") if sj and not args.statements else None
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:   # the baseline is an N=1 figure
+    if rank == 0 and G == 1 and not args.no_cpu_baseline:   # the baseline is an N=1 figure
         if scheme == abi.RESAMPLE_MULTINOMIAL:   # the MT port covers the strata (the reference's scheme)
             cpu = None
         else:
@@ -418,7 +506,7 @@ def main():
             "metric": METRIC,
             "value": value,
             "unit": "particle-steps/s",
-            "n_gpus": world,
+            "n_gpus": G,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,          # one bench step = one full T-step run
@@ -438,11 +526,13 @@ def main():
                        # island shards resample within themselves after the global decision: a
                        # different (unbiased) estimator than the reference's single-population
                        # Resample, which exact shards reproduce bit for bit
-                       "estimator": ("reference (single population)" if (world == 1 and not args.rccl_one_rank
+                       "estimator": ("reference (single population)" if (G == 1 and not args.rccl_one_rank
                                                                          and args.multi_shards <= 1)
                                      or args.shard_mode == "exact"
                                      else "island resampling (per-shard strata, global decision)"),
-                       "parallelism": (f"{args.shard_mode}-shard x{args.multi_shards} in one handle on one GPU "
+                       "parallelism": (f"{args.shard_mode}-shard x{G}, one process over {G} GPUs "
+                                       "(wsmc_create_multi: ncclCommInitAll, one host thread per shard)") if inproc else
+                                      (f"{args.shard_mode}-shard x{args.multi_shards} in one handle on one GPU "
                                        "(in-process exchange, diagnostic)") if args.multi_shards > 1 else
                                       (f"{args.shard_mode}-shard x{world}"
                                        + (" (host exchange, test mode)" if args.exchange == "host" else ""))
@@ -452,8 +542,8 @@ def main():
             # 104 algorithmic B (CDF materialisation and trace-back count as overhead); traffic =
             # the PMC-measured HBM bytes per particle-step of every kernel of the run (trace-back
             # included). The dominant kernel's own figure (HIP events on its dispatches) beside it.
-            "roofline": {"bound": "hbm", "achieved": value / world * STEP_BYTES / 1e9, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": value / world * STEP_BYTES / 1e9 / HBM_PEAK_GBS,
+            "roofline": {"bound": "hbm", "achieved": value / G * STEP_BYTES / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": value / G * STEP_BYTES / 1e9 / HBM_PEAK_GBS,
                          "traffic": step_traffic, "algorithmic_bytes_per_particle_step": STEP_BYTES,
                          "definition": "whole step: particle-steps/s per GPU x 104 B / 8 TB/s (SURVEY.md 8d)",
                          "dominant_kernel": None if args.statements else {
@@ -468,6 +558,7 @@ def main():
                 "finalize_traceback": fin_ms, "instrumented_total": tot_ms,
                 "resamples_per_run": nres, "forced_every_step": forced},
             "log_evidence_last": ev,
+            "ranks": ranks,
         }
         if xst is not None:
             line["exact_stats"] = xst

@@ -192,6 +192,21 @@ int wsmc_comm_init_host(wsmc_ctx* ctx, wsmc_exchange_fn exchange, void* user, in
  * across ranks); multinomial draws on exact shards return WSMC_EARG. */
 typedef enum { WSMC_SHARD_ISLAND = 0, WSMC_SHARD_EXACT = 1 } wsmc_shard_mode;
 int wsmc_comm_set_shard_mode(wsmc_ctx* ctx, int32_t mode);
+/* What a context (or a multi-device handle) is sharded over, as the communicator itself
+ * reports it — for a benchmark line that must say how many devices it measured (no reference
+ * counterpart: the reference is single-threaded, /root/reference/TODO.md:28).
+ *   shards      shards in this handle (1 for a plain context, G for wsmc_create_multi)
+ *   world/rank  the sharding (world 1: unsharded)
+ *   rccl_ranks  ncclCommCount of the (first) shard's communicator, 0 when it has none
+ *   transport   WSMC_TRANSPORT_RCCL, WSMC_TRANSPORT_HOST, or -1 (unsharded)
+ *   shard_mode  WSMC_SHARD_ISLAND / WSMC_SHARD_EXACT
+ *   devices[g], shard_n[g]  HIP device and particle count of shard g < min(shards, 8) */
+typedef struct {
+    int32_t shards, world, rank, rccl_ranks, transport, shard_mode;
+    int32_t devices[8];
+    int64_t shard_n[8];
+} wsmc_comm_info_t;
+int wsmc_comm_info(wsmc_ctx* ctx, wsmc_comm_info_t* out);
 
 /* ---- store: AbstractParticleStore (src/stores.jl:1-35) ----------------------- */
 /* broadcast_setcol! column creation (src/stores.jl:85-96); existing name => same id */

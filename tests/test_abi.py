@@ -34,6 +34,7 @@ def test_struct_layouts_match_c():
     assert C.sizeof(abi.Term) == L.or_sizeof_term()
     assert C.sizeof(abi.Dist) == L.or_sizeof_dist()
     assert C.sizeof(abi.Operand) == 40
+    assert C.sizeof(abi.CommInfo) == 120   # 6 int32, devices[8] int32, shard_n[8] int64
 
 
 def test_version_and_error_channel():

@@ -547,6 +547,32 @@ def test_multi_handle_matches_oracle(gpu_available, shards, transport, mode):
     g.close()
 
 
+def test_comm_info_reports_the_communicator(gpu_available):
+    """wsmc_comm_info (bench.py's `ranks` object): a plain context is unsharded; a one-rank
+    RCCL communicator reports ncclCommCount = 1; a multi-device handle reports its shards, their
+    devices and sizes (one RCCL shard on GPU 0, and three host-exchange shards sharing it)."""
+    import wsmc
+    from wsmc import abi
+    c = wsmc.Context(1000, seed=1)
+    i = c.comm_info()
+    assert (i["shards"], i["world"], i["rccl_ranks"], i["transport"]) == (1, 1, 0, "none")
+    assert i["devices"] == [0] and i["shard_n"] == [1000]
+    c.comm_init(wsmc.Context.comm_unique_id(), 1, 0, 0, 1000)
+    i = c.comm_info()
+    assert (i["world"], i["rank"], i["rccl_ranks"], i["transport"]) == (1, 0, 1, "rccl")
+    c.close()
+    g = wsmc.Context.multi(1001, 1, seed=1, devices=[0], transport=abi.TRANSPORT_RCCL)
+    i = g.comm_info()
+    assert (i["shards"], i["rccl_ranks"], i["transport"], i["devices"], i["shard_n"]) == (1, 1, "rccl", [0], [1001])
+    g.close()
+    g = wsmc.Context.multi(1001, 3, seed=1, devices=[0] * 3, transport=abi.TRANSPORT_HOST)
+    g.comm_set_shard_mode(abi.SHARD_EXACT)
+    i = g.comm_info()
+    assert (i["shards"], i["world"], i["rccl_ranks"], i["transport"], i["shard_mode"]) == (3, 3, 0, "host", "exact")
+    assert i["devices"] == [0, 0, 0] and i["shard_n"] == [333, 334, 334]
+    g.close()
+
+
 def test_one_rank_rccl_autorw_not_pd(gpu_available):
     """Sharded autoRW combines the ranks' moment totals on the device (k_autorw_combine): a
     singular covariance sets the device flag, the Move leaves the state untouched and the call

@@ -865,6 +865,27 @@ int wsmc_comm_init_host(wsmc_ctx* c, wsmc_exchange_fn exchange, void* user, int3
     return WSMC_OK;
 }
 
+int wsmc_comm_info(wsmc_ctx* c, wsmc_comm_info_t* out) {
+    if (!out) return fail(WSMC_EARG, "null argument");
+    if (c && c->multi) return multi_comm_info(c, out);
+    CHECK_CTX(c);
+    *out = wsmc_comm_info_t{};
+    out->shards = 1;
+    out->world = c->world;
+    out->rank = c->rank;
+    out->transport = c->comm ? WSMC_TRANSPORT_RCCL : c->host_exchange ? WSMC_TRANSPORT_HOST : -1;
+    out->shard_mode = c->shard_mode;
+    if (c->comm) {
+        int n = 0;
+        WSMC_RCCL(ncclCommCount(c->comm, &n));
+        out->rccl_ranks = n;
+    }
+    for (int g = 0; g < 8; ++g) out->devices[g] = -1;
+    out->devices[0] = c->device;
+    out->shard_n[0] = c->N;
+    return WSMC_OK;
+}
+
 int wsmc_comm_set_shard_mode(wsmc_ctx* c, int32_t mode) {
     if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { return wsmc_comm_set_shard_mode(x, mode); });
     CHECK_CTX(c);

@@ -760,6 +760,7 @@ int multi_weights(wsmc_ctx* c, const double* up, double* down);
 int multi_score(wsmc_ctx* c, int32_t depth, double* host);
 int multi_last_ancestors(wsmc_ctx* c, int32_t* host);
 int multi_inject_failure(wsmc_ctx* c, int32_t shard, int32_t nth);
+int multi_comm_info(wsmc_ctx* c, wsmc_comm_info_t* out);
 int multi_gather_rows(wsmc_ctx* c, int32_t col, const int64_t* idx, int64_t n, double* out);
 int multi_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, double step, const double* lo,
                const double* hi, int32_t target_depth, double diversity, int64_t* accepted_out);

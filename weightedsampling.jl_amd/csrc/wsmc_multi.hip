@@ -376,6 +376,19 @@ int multi_inject_failure(wsmc_ctx* c, int32_t shard, int32_t nth) {
     return WSMC_OK;
 }
 
+int multi_comm_info(wsmc_ctx* c, wsmc_comm_info_t* out) {
+    MultiState* M = c->multi;
+    wsmc_comm_info_t first{};
+    if (int r = wsmc_comm_info(M->sub[0], &first)) return r;
+    *out = first;
+    out->shards = M->G;
+    for (int g = 0; g < 8; ++g) {
+        out->devices[g] = g < M->G ? M->sub[g]->device : -1;
+        out->shard_n[g] = g < M->G ? nloc(M, g) : 0;
+    }
+    return WSMC_OK;
+}
+
 }  // namespace wsmc
 
 extern "C" int wsmc_create_multi(wsmc_ctx** out, int64_t n_particles, int32_t n_gpus, const int32_t* devices,

@@ -75,6 +75,13 @@ class State(C.Structure):
                 ("op_counter", C.c_uint64), ("n_resamples", C.c_int64)]
 
 
+class CommInfo(C.Structure):
+    """wsmc_comm_info_t: what a context or multi-device handle is sharded over"""
+    _fields_ = [("shards", C.c_int32), ("world", C.c_int32), ("rank", C.c_int32),
+                ("rccl_ranks", C.c_int32), ("transport", C.c_int32), ("shard_mode", C.c_int32),
+                ("devices", C.c_int32 * 8), ("shard_n", C.c_int64 * 8)]
+
+
 class MoveSpec(C.Structure):
     """wsmc_move_spec: one Move of a wsmc_move_block statement block"""
     _fields_ = [("proposal", C.c_int32), ("d", C.c_int32), ("targets", C.c_int32 * 4),
@@ -109,6 +116,7 @@ SIGNATURES = {
     "wsmc_comm_init": (C.c_int, [_P, C.POINTER(C.c_uint8), C.c_int32, C.c_int32, C.c_int64,
                                  C.c_int64]),
     "wsmc_comm_set_shard_mode": (C.c_int, [_P, C.c_int32]),
+    "wsmc_comm_info": (C.c_int, [_P, C.POINTER(CommInfo)]),
     "wsmc_comm_init_host": (C.c_int, [_P, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int64,
                                       C.c_int64]),
     "wsmc_col_create": (C.c_int, [_P, C.c_char_p, C.c_int32, _I32P]),

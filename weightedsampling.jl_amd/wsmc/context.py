@@ -124,6 +124,25 @@ class Context:
                                           int(rank), int(global_offset), int(global_n)))
         self.world, self.rank = int(world), int(rank)
 
+    def comm_info(self) -> dict:
+        """wsmc_comm_info: shards, world/rank, the RCCL communicator's own rank count
+        (ncclCommCount), transport, shard mode, and each shard's device and size."""
+        ci = abi.CommInfo()
+        check(self._L.wsmc_comm_info(self._h, C.byref(ci)))
+        k = min(int(ci.shards), 8)
+        return {"shards": int(ci.shards), "world": int(ci.world), "rank": int(ci.rank),
+                "rccl_ranks": int(ci.rccl_ranks),
+                "transport": {abi.TRANSPORT_RCCL: "rccl", abi.TRANSPORT_HOST: "host"}.get(int(ci.transport), "none"),
+                "shard_mode": "exact" if ci.shard_mode == abi.SHARD_EXACT else "island",
+                "devices": [int(ci.devices[g]) for g in range(k)],
+                "shard_n": [int(ci.shard_n[g]) for g in range(k)]}
+
+    @staticmethod
+    def device_count() -> int:
+        n = C.c_int32()
+        check(load_library().wsmc_device_count(C.byref(n)))
+        return int(n.value)
+
     def comm_set_shard_mode(self, mode: int) -> None:
         """abi.SHARD_ISLAND (default) or abi.SHARD_EXACT: sharded Resample over the whole
         population, bit-identical to one context holding every particle (include/wsmc.h)."""
