@@ -451,15 +451,18 @@ WSMC_HD uint64_t wsmc_strat_key(uint64_t seed, uint64_t op) {
     z ^= z >> 33;
     return z;
 }
-WSMC_HD uint32_t wsmc_strat_hash(uint64_t key, uint64_t n) {
-    uint32_t x = (uint32_t)n ^ (uint32_t)key;
-    x ^= (uint32_t)(n >> 32) * 0x85EBCA6Bu ^ (uint32_t)(key >> 32);
+WSMC_HD uint32_t wsmc_strat_fin(uint32_t x) {   /* lowbias32 */
     x ^= x >> 16;
     x *= 0x7FEB352Du;
     x ^= x >> 15;
     x *= 0x846CA68Bu;
     x ^= x >> 16;
     return x;
+}
+WSMC_HD uint32_t wsmc_strat_hash(uint64_t key, uint64_t n) {
+    /* (lo32(n) ^ lo32(k)) ^ (hi32(n) c' ^ hi32(k)): the device splits the second term off once
+       per launch when hi32(n) is constant over the slots (csrc/wsmc_kernels.hip SlotHash) */
+    return wsmc_strat_fin((uint32_t)n ^ (uint32_t)key ^ ((uint32_t)(n >> 32) * 0x85EBCA6Bu ^ (uint32_t)(key >> 32)));
 }
 WSMC_HD uint32_t wsmc_strat_word(uint64_t seed, uint64_t op, uint64_t n) {
     return wsmc_strat_hash(wsmc_strat_key(seed, op), n);

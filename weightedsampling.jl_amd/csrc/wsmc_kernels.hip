@@ -1057,50 +1057,68 @@ __global__ __launch_bounds__(kBlock) void k_exact_final(ExactFinal f) {
 
 constexpr int kOverflowBlocks = 256;   // fill blocks serving overflow chunks (grid-stride)
 
-constexpr int kScatterMax = 8;          // slots a thread writes for one particle before the block helps
+// ---- the ancestor fill of one chunk of a tile's slots --------------------------------------
+// Particle m owns the output slots [hi_{m-1}, hi_m), hi_m = rank(C_m), rank(c) = #{n : x_n < c}
+// (include/wsmc_math.h wsmc_rank_r), so a chunk [cs, ce) of the tile's slot range [L, H) is
+// filled in three data-parallel passes with no per-slot loop:
+//   ranks    every thread ranks its 4 (blocked) particles from the tile's local f64 prefix of q
+//            (exact: a tile's q sum stays below 2^53), by the fast path below, exact fallback;
+//   marks    a particle owning slots of the chunk writes its id at its first one (one LDS
+//            store; the chunk's slots start at -1);
+//   expand   a block max-scan over the chunk's slots (8 a thread: running max, DPP wave scan,
+//            one LDS round) gives every slot the last mark at or before it — its owner, since
+//            ids increase with the slot — and the thread stores its slots with 16-B stores.
+// A particle owning many slots (a dominant weight) costs one mark, not a loop.
+// Fast rank: y = fma(cl, N/Q, fl(off) N/Q) estimates z = c N / Q (c = off + cl) to within
+// 6 * 2^-53 * N <= 2^-19 for N < 2^31; if frac(y) is further than 2^-15 from 0 and 1,
+// floor(z) = floor(y), and rank(c) = floor(z) + [R / 2^32 < frac(z)] (R the stratum word of
+// slot floor(z)) is decided unless R / 2^32 is within 2^-15 of frac(y). The rest (about 1e-4
+// of the particles, and c = 0 or c >= Q) take the exact 64x32-bit path.
+constexpr int kFillSlots = kRsChunk / kScanBlock;   // slots a thread expands (8)
+constexpr int kFillWin = kRsChunk + 4;              // the chunk, placed 16-B aligned (<= 3 slots of head)
+static_assert(kRsTile / kScanBlock == 4 && kFillSlots == 8, "fill: 4 particles and 8 slots a thread");
 
 struct FillLds {
-    u64 LH[2];
-    u64 uw[kScanBlock / 64];
-    u64 last[kScanBlock / 64];
-    int nheavy;
-    int heavy[kRsChunk / kScatterMax + 1][3];   // particle (tile-local), first slot, end slot (chunk-local)
-    int32_t out[kRsChunk];                      // the chunk's ancestors, staged for coalesced stores
+    u64 LH[2];                              // the tile's slot range [L, H)
+    double uw[kScanBlock / 64];             // block scan of the tile's q
+    u64 red[kScanBlock / 64][2];            // fused fill: the tile's CDF offset and the total Q
+    uint32_t last[kScanBlock / 64];         // each wave's last particle's end slot
+    int wmax[kScanBlock / 64];              // each wave's last mark
+    alignas(16) int32_t out[kFillWin];      // marks -> ancestors, window slot p = slot - cs + head
 };
 
-// write the staged chunk sh.out[so, so + n) to dst[0, n): 16-B stores on the aligned body,
-// single stores on the ragged ends (dst is 4-B aligned; any slot offset)
-__device__ __forceinline__ void store_chunk(int32_t* __restrict__ dst, int n, const FillLds& sh, int so = 0) {
-    const int32_t* src = sh.out + so;
-    const int head = (int)((4 - (((uintptr_t)dst >> 2) & 3)) & 3);    // slots before a 16-B boundary
-    const int h = head < n ? head : n;
-    const int nv = (n - h) >> 2;                                        // whole 16-B vectors
-    for (int v = threadIdx.x; v < nv; v += kScanBlock) {
-        const int k = h + 4 * v;
-        int4 o;
-        o.x = src[k]; o.y = src[k + 1]; o.z = src[k + 2]; o.w = src[k + 3];
-        *reinterpret_cast<int4*>(dst + k) = o;
-    }
-    const int tail0 = h + 4 * nv;
-    const int th = threadIdx.x;
-    if (th < h) dst[th] = src[th];
-    else if (th >= 4 && th - 4 < n - tail0) dst[tail0 + th - 4] = src[tail0 + th - 4];
+// slot words: R = wsmc_strat_hash(key, slot_base + n) with the 64-bit slot split once per
+// launch when its high word is constant over the slots (always on one GPU)
+struct SlotHash {
+    uint64_t key, base;
+    uint32_t kx, blo;
+    int fast;          // hi32(base + n) == hi32(base) for every slot n < Nr
+    int sys;           // systematic: one word for every slot
+    double rsys;       // its R / 2^32
+};
+__device__ __forceinline__ SlotHash slot_hash_of(const FillPlan& plan, uint64_t opx, uint64_t Nr) {
+    SlotHash h;
+    h.key = wsmc_strat_key(plan.seed, opx);
+    h.base = (uint64_t)plan.slot_base;
+    h.fast = (h.base >> 32) == ((h.base + Nr) >> 32);
+    h.kx = (uint32_t)h.key ^ ((uint32_t)(h.base >> 32) * 0x85EBCA6Bu ^ (uint32_t)(h.key >> 32));
+    h.blo = (uint32_t)h.base;
+    h.sys = plan.scheme == 1;
+    h.rsys = (double)wsmc_strat_hash(h.key, h.base) * 2.3283064365386963e-10;
+    return h;
+}
+__device__ __forceinline__ double slot_word_d(const SlotHash& h, uint32_t ns) {
+    if (h.sys) return h.rsys;
+    const uint32_t R = h.fast ? wsmc_strat_fin((h.blo + ns) ^ h.kx) : wsmc_strat_hash(h.key, h.base + ns);
+    return (double)R * 2.3283064365386963e-10;   // R / 2^32, exact
 }
 
-// fill chunk j of tile b (block-uniform arguments; ends with a barrier so LDS can be reused).
-// Particle m owns the slots [hi_{m-1}, hi_m) with hi_m = rank(C_m); each thread ranks its 4
-// (blocked) particles and scatters their slots within the chunk. A particle owning more
-// than kScatterMax slots of the chunk is queued and filled by the whole block, so a lane
-// never loops long whatever the weights.
-// rank(c) = #{n : x_n < c} (include/wsmc_math.h wsmc_rank_r), bit-identical, decided in f64
-// when f64 provably decides it. With y = c N / Q evaluated as fl(fl(c) * fl(N / Q)) (four
-// roundings: |y - cN/Q| <= 4 * 2^-53 * N <= 2^-17 for N <= 2^34, any global population of
-// one node), the exact rank is floor(cN/Q) + [R / 2^32 < frac(cN/Q)] (R the slot's stratum
-// word). If frac(y) is further than 2^-15 from 0 and 1, floor(y) is the exact floor; if
-// R / 2^32 is further than 2^-15 from frac(y), the comparison is the exact one. Otherwise
-// (about 2e-4 of the particles) the exact 64x32-bit path decides. The fast path is a conversion, a product, a floor, the 32-bit slot
-// hash and two compares, where the exact path is three 64x32 products and 128-bit compares.
-__device__ __forceinline__ u64 d_small_to_u64(double d);
+// an exact integer u64 below 2^52 -> double (q <= 2^43)
+__device__ __forceinline__ double u64_small_to_d(u64 v) {
+    return __builtin_bit_cast(double, v | 0x4330000000000000ull) - 4503599627370496.0;
+}
+
+// rank(c) exactly, c = off + cl; the fast path above, else wsmc_rank_r
 __device__ __forceinline__ u64 rank_fast(u64 c, u64 Q, u64 N, double ratio, int scheme, uint64_t seed,
                                          uint64_t op, uint64_t slot_base, uint64_t key) {
     if (c == 0) return 0;
@@ -1110,7 +1128,7 @@ __device__ __forceinline__ u64 rank_fast(u64 c, u64 Q, u64 N, double ratio, int 
     const double fl = wsmc_floor(y);
     const double f = y - fl;                        // exact
     if (f > kMargin && f < 1.0 - kMargin) {
-        const u64 ns = d_small_to_u64(fl);
+        const u64 ns = (u64)fl;
         if (ns < N) {
             const uint32_t R = wsmc_strat_hash(key, scheme == 1 ? slot_base : slot_base + ns);
             const double dd = f - (double)R * 2.3283064365386963e-10;   // f - R / 2^32
@@ -1121,6 +1139,35 @@ __device__ __forceinline__ u64 rank_fast(u64 c, u64 Q, u64 N, double ratio, int 
     return wsmc_rank_r(c, Q, N, ratio, scheme, seed, op, slot_base);
 }
 
+template <int CTRL, int ROW = 0xf, int BANK = 0xf>
+__device__ __forceinline__ int dpp_i32_or(int v, int idn) {
+    return __builtin_amdgcn_update_dpp(idn, v, CTRL, ROW, BANK, false);
+}
+// inclusive max over the wave's lanes (identity -1)
+__device__ __forceinline__ int wave_incl_max_i32(int v) {
+    int x = max(v, dpp_i32_or<kDppRowShr1>(v, -1));
+    x = max(x, dpp_i32_or<kDppRowShr2>(v, -1));
+    x = max(x, dpp_i32_or<kDppRowShr3>(v, -1));
+    x = max(x, dpp_i32_or<kDppRowShr4, 0xf, 0xe>(x, -1));
+    x = max(x, dpp_i32_or<kDppRowShr8, 0xf, 0xc>(x, -1));
+    x = max(x, dpp_i32_or<kDppBcast15, 0xa, 0xf>(x, -1));
+    x = max(x, dpp_i32_or<kDppBcast31, 0xc, 0xf>(x, -1));
+    return x;
+}
+// inclusive prefix sum of exact-integer f64 values over the wave (sums below 2^53)
+__device__ __forceinline__ double wave_incl_scan_f64(double v) {
+    double x = v + dpp_f64<kDppRowShr1>(v);
+    x = x + dpp_f64<kDppRowShr2>(v);
+    x = x + dpp_f64<kDppRowShr3>(v);
+    x = x + __builtin_bit_cast(double, dpp_u64<kDppRowShr4, 0xf, 0xe>(__builtin_bit_cast(u64, x)));
+    x = x + __builtin_bit_cast(double, dpp_u64<kDppRowShr8, 0xf, 0xc>(__builtin_bit_cast(u64, x)));
+    x = x + __builtin_bit_cast(double, dpp_u64<kDppBcast15, 0xa, 0xf>(__builtin_bit_cast(u64, x)));
+    x = x + __builtin_bit_cast(double, dpp_u64<kDppBcast31, 0xc, 0xf>(__builtin_bit_cast(u64, x)));
+    return x;
+}
+
+// the tile's q in registers (4 blocked particles a thread) as exact doubles, and the thread's
+// inclusive local prefixes (exact: a tile's sum is at most 2^53)
 template <int IT>
 __device__ __forceinline__ void load_tile_q(int64_t N, int b, const u64* __restrict__ qbuf, u64 (&q)[IT]) {
 #pragma unroll
@@ -1130,105 +1177,194 @@ __device__ __forceinline__ void load_tile_q(int64_t N, int b, const u64* __restr
     }
 }
 
+// every slot of the window starts at -1 (no mark); the caller's next barrier orders it
+__device__ __forceinline__ void fill_clear(FillLds& sh) {
+    const int4 m1 = make_int4(-1, -1, -1, -1);
+    int4* o = reinterpret_cast<int4*>(sh.out);
+    o[2 * threadIdx.x] = m1;
+    o[2 * threadIdx.x + 1] = m1;
+    if (threadIdx.x == 0) o[2 * kScanBlock] = m1;
+}
+
+// store window slots [p0, p0 + 4) (16-B aligned in dst) keeping those in [a, e)
+__device__ __forceinline__ void fill_store4(int32_t* __restrict__ dst, int p0, int a, int e, int4 v) {
+    if (p0 >= a && p0 + 4 <= e) {
+        *reinterpret_cast<int4*>(dst + p0) = v;
+    } else if (p0 + 4 > a && p0 < e) {
+        if (p0 >= a && p0 < e) dst[p0] = v.x;
+        if (p0 + 1 >= a && p0 + 1 < e) dst[p0 + 1] = v.y;
+        if (p0 + 2 >= a && p0 + 2 < e) dst[p0 + 2] = v.z;
+        if (p0 + 3 >= a && p0 + 3 < e) dst[p0 + 3] = v.w;
+    }
+}
+
+// Fill chunk j of tile b, given the tile's CDF offset `off`, the total Q, the thread's q and
+// its exclusive local prefix `pre` (f64). Entered after a barrier that published `pre` and
+// after fill_clear; ends with a barrier when `reuse` (the window is used again).
+// MODE (diagnostics only; production = 0): 1 = no exact rank (the estimate, clamped),
+// 2 = ranks only (no marks / stores), 3 = scan only
 template <int MODE>
-__device__ __forceinline__ void fill_chunk_q(int64_t N, int b, int j, u64 Q, u64 off, u64 qb, const FillPlan& plan,
-                                             uint64_t opx, const u64 (&q)[kRsTile / kScanBlock],
-                                             int32_t* __restrict__ anc, FillLds& sh) {
-    constexpr int IT = kRsTile / kScanBlock;   // 4 particles per thread, blocked
+__device__ __forceinline__ void fill_chunk_core(int64_t N, int b, int j, u64 Q, u64 off, u64 qb, double pre,
+                                                const FillPlan& plan, uint64_t opx,
+                                                const u64 (&q)[kRsTile / kScanBlock], int32_t* __restrict__ anc,
+                                                FillLds& sh, bool reuse) {
+    constexpr int IT = kRsTile / kScanBlock;
+    constexpr double kMargin = 3.0517578125e-05;    // 2^-15
     const int th = threadIdx.x, lane = th & 63, wv = th >> 6;
-    const int64_t base = (int64_t)b * kRsTile;
-    u64 tsum = 0;
-#pragma unroll
-    for (int k = 0; k < IT; ++k) tsum += q[k];
     // exact sharding: targets over the global population, slots written window-relative
     const uint64_t Nr = plan.n_global ? plan.n_global : plan.xp ? plan.xp->N : (uint64_t)N;
     // exact shards without host round trips: slots land in this rank's ancestor row, which
     // covers [row_lo, row_hi) (its own range and a margin per neighbour); global ids
     const u64 s0 = plan.row_hi ? plan.row_lo : plan.xp ? plan.xp->a : 0ull;
     const double ratio = wsmc_u64_to_d(Nr) / wsmc_u64_to_d(Q);
+    const double yoff = wsmc_u64_to_d(off) * ratio;
+    const SlotHash sh_ = slot_hash_of(plan, opx, Nr);
     // the tile's slot range [L, H) = [rank(off), rank(off + Q_b)), ranked by two threads
-    // while the others scan; the scan's barrier publishes them
-    const uint64_t key = wsmc_strat_key(plan.seed, opx);   // uniform: the slot hash's key
+    // while the others rank their particles; the next barrier publishes them
     if (th < 2) {
         const u64 c = th == 0 ? off : off + qb;
-        sh.LH[th] = rank_fast(c, Q, Nr, ratio, plan.scheme, plan.seed, opx, (uint64_t)plan.slot_base, key);
-    }
-    if (th == 0) sh.nheavy = 0;
-    u64 tot;
-    const u64 pre = block_excl_scan_u64<kScanBlock / 64>(tsum, sh.uw, &tot);
-    const u64 L = sh.LH[0], H = sh.LH[1];
-    const u64 cs = L + (u64)j * kRsChunk;
-    const u64 ce = cs + kRsChunk < H ? cs + kRsChunk : H;
-    if (cs >= ce) {                                // uniform; keep LDS reuse ordered
-        __syncthreads();
-        return;
+        sh.LH[th] = rank_fast(c, Q, Nr, ratio, plan.scheme, plan.seed, opx, sh_.base, sh_.key);
     }
     if (MODE == 3) {
-        if (pre == 0x123456789ull) anc[0] = 1;
+        if (pre == 0.123) anc[0] = 1;
         return;
     }
-    u64 C = off + pre;
-    u64 hi[IT];
-    u64 prev = L;
+    // ---- ranks: hi[k] = rank(off + cl_k) as a slot index (< 2^31) ----
+    const double Nd = wsmc_u64_to_d(Nr);
+    uint32_t hi[IT];
+    uint32_t slow = 0;                             // particles left to the exact path (bits)
+    double cl = pre;
 #pragma unroll
     for (int k = 0; k < IT; ++k) {
-        C += q[k];
-        u64 h = prev;                              // a particle with q = 0 owns no slots
-        if (q[k] || k == 0) h = MODE == 1 ? (u64)(wsmc_u64_to_d(C) * ratio)
-                                : rank_fast(C, Q, Nr, ratio, plan.scheme, plan.seed, opx,
-                                            (uint64_t)plan.slot_base, key);
-        if (MODE == 1 && h > H) h = H;
-        if (MODE == 1 && h < L) h = L;
+        cl = cl + u64_small_to_d(q[k]);
+        const double y = __builtin_fma(cl, ratio, yoff);
+        const double fl = wsmc_floor(y);
+        const double f = y - fl;                   // exact
+        const bool inr = fl < Nd;
+        const uint32_t ns = (uint32_t)(inr ? fl : 0.0);
+        uint32_t h = ns;
+        bool ok = f > kMargin && f < 1.0 - kMargin && inr;
+        if (MODE == 1) {
+            ok = true;
+            h = fl < Nd ? ns : (uint32_t)Nr;
+        } else {
+            const double dd = f - slot_word_d(sh_, ns);
+            ok = ok && (dd > kMargin || dd < -kMargin);
+            h = ns + (dd > kMargin ? 1u : 0u);
+        }
+        if (k > 0 && q[k] == 0) {                  // no slots: ends where the previous particle ends
+            h = hi[k - 1];
+            ok = !((slow >> (k - 1)) & 1u);        // final once the previous one is
+        }
         hi[k] = h;
-        prev = h;
+        slow |= (ok ? 0u : 1u) << k;
     }
-    // first slot of the thread's first particle = hi of the previous thread's last particle
-    u64 lo = dpp_u64<kDppWaveShr1>(hi[IT - 1]);   // lane l gets lane l-1's (lane 0: set below)
-    if (lane == 63) sh.last[wv] = hi[IT - 1];
-    __syncthreads();
-    if (lane == 0) lo = wv > 0 ? sh.last[wv - 1] : L;
-    if (MODE == 2) {
-        if (lo == 0x123456789ull) anc[0] = 1;
-        return;
-    }
-    // the chunk's ancestors are scattered into LDS, then stored coalesced (a particle's
-    // slots written straight to HBM were one masked 4-B store per slot per lane)
+    if (MODE != 1 && slow) {                       // the exact path (rare; c = 0 and c >= Q too)
+        double c2 = pre;
 #pragma unroll
-    for (int k = 0; k < IT; ++k) {
-        const u64 a = lo > cs ? lo : cs;
-        const u64 e = hi[k] < ce ? hi[k] : ce;
-        const int32_t m = (int32_t)(base + th * IT + k) + plan.id_base;
-        if (a < e) {
-            const int a0 = (int)(a - cs), e0 = (int)(e - cs);
-            if (e0 - a0 > kScatterMax) {
-                const int x = atomicAdd(&sh.nheavy, 1);
-                sh.heavy[x][0] = m;
-                sh.heavy[x][1] = a0;
-                sh.heavy[x][2] = e0;
-            } else {
-                for (int n = a0; n < e0; ++n) sh.out[n] = m;
+        for (int k = 0; k < IT; ++k) {
+            c2 = c2 + u64_small_to_d(q[k]);
+            if (slow >> k & 1u) {
+                if (k > 0 && q[k] == 0) {
+                    hi[k] = hi[k - 1];
+                } else {
+                    const u64 c = off + (u64)c2;
+                    hi[k] = (uint32_t)wsmc_rank_r(c, Q, Nr, ratio, plan.scheme, plan.seed, opx, sh_.base);
+                }
             }
         }
+    }
+    // first slot of the thread's first particle = the previous thread's last end
+    uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi[IT - 1], kDppWaveShr1, 0xf, 0xf, false);
+    if (lane == 63) sh.last[wv] = hi[IT - 1];
+    __syncthreads();
+    const u64 L = sh.LH[0], H = sh.LH[1];
+    if (lane == 0) lo = wv > 0 ? sh.last[wv - 1] : (uint32_t)L;
+    if (MODE == 1) {
+#pragma unroll
+        for (int k = 0; k < IT; ++k) hi[k] = hi[k] < (uint32_t)L ? (uint32_t)L : hi[k] > (uint32_t)H ? (uint32_t)H : hi[k];
+        lo = lo < (uint32_t)L ? (uint32_t)L : lo > (uint32_t)H ? (uint32_t)H : lo;
+    }
+    const u64 cs64 = L + (u64)j * kRsChunk;
+    const u64 ce64 = cs64 + kRsChunk < H ? cs64 + kRsChunk : H;
+    if (cs64 >= ce64) {                            // uniform: no slots in this chunk
+        if (reuse) __syncthreads();
+        return;
+    }
+    if (MODE == 2) {
+        if (lo == 0x12345678u) anc[0] = 1;
+        if (reuse) __syncthreads();
+        return;
+    }
+    const uint32_t cs = (uint32_t)cs64, ce = (uint32_t)ce64;
+    // the window: slot s at p = s - cs + head, with p = 0 mod 4 on 16-B boundaries of the row
+    int32_t* const dst0 = anc + (cs64 - s0);
+    const int head = (int)(((uintptr_t)dst0 >> 2) & 3);
+    // ---- marks ----
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        const uint32_t a = lo > cs ? lo : cs;
+        const uint32_t e = hi[k] < ce ? hi[k] : ce;
+        if (a < e) sh.out[a - cs + head] = (int32_t)(b * kRsTile + th * IT + k) + plan.id_base;
         lo = hi[k];
     }
     __syncthreads();
-    // queued particles: one per wave at a time, the wave's lanes striding over its slots
-    const int nh = sh.nheavy;
-    for (int x = wv; x < nh; x += kScanBlock / 64) {
-        const int m = sh.heavy[x][0];
-        for (int n = sh.heavy[x][1] + lane; n < sh.heavy[x][2]; n += 64) sh.out[n] = m;
-    }
+    // ---- expand: block max-scan over the window, 8 slots a thread ----
+    const int4* o4 = reinterpret_cast<const int4*>(sh.out);
+    int4 v0 = o4[2 * th], v1 = o4[2 * th + 1];
+    v0.y = max(v0.y, v0.x); v0.z = max(v0.z, v0.y); v0.w = max(v0.w, v0.z);
+    v1.x = max(v1.x, v0.w); v1.y = max(v1.y, v1.x); v1.z = max(v1.z, v1.y); v1.w = max(v1.w, v1.z);
+    const int inc = wave_incl_max_i32(v1.w);
+    int carry = __builtin_amdgcn_update_dpp(-1, inc, kDppWaveShr1, 0xf, 0xf, false);
+    if (lane == 63) sh.wmax[wv] = inc;
     __syncthreads();
-    if (plan.row_hi) {   // the part of the chunk the row covers; the rest cannot be routed
-        const u64 w0 = cs > plan.row_lo ? cs : plan.row_lo, w1 = ce < plan.row_hi ? ce : plan.row_hi;
-        if (threadIdx.x == 0 && (w0 != cs || w1 != ce)) atomicOr(plan.xstat, 1ull);
-        if (w1 > w0) store_chunk(anc + (w0 - s0), (int)(w1 - w0), sh, (int)(w0 - cs));
-    } else {
-        store_chunk(anc + (cs - s0), (int)(ce - cs), sh);
+#pragma unroll
+    for (int k = 0; k < kScanBlock / 64 - 1; ++k)
+        if (k < wv) carry = max(carry, sh.wmax[k]);
+    v0.x = max(v0.x, carry); v0.y = max(v0.y, carry); v0.z = max(v0.z, carry); v0.w = max(v0.w, carry);
+    v1.x = max(v1.x, carry); v1.y = max(v1.y, carry); v1.z = max(v1.z, carry); v1.w = max(v1.w, carry);
+    // ---- stores: the window's [a, e) (exact shards: the part of the chunk the row covers;
+    // the rest cannot be routed) ----
+    int a = head, e = head + (int)(ce - cs);
+    if (plan.row_hi) {
+        const u64 w0 = cs64 > plan.row_lo ? cs64 : plan.row_lo, w1 = ce64 < plan.row_hi ? ce64 : plan.row_hi;
+        if (th == 0 && (w0 != cs64 || w1 != ce64)) atomicOr(plan.xstat, 1ull);
+        a = w1 > w0 ? head + (int)(w0 - cs64) : 0;
+        e = w1 > w0 ? head + (int)(w1 - cs64) : 0;
     }
-    __syncthreads();
+    int32_t* const dst = dst0 - head;              // window slot p lands at dst[p]
+    fill_store4(dst, 8 * th, a, e, v0);
+    fill_store4(dst, 8 * th + 4, a, e, v1);
+    if (th == kScanBlock - 1 && e > kRsChunk) {    // the window's last (head) slots
+        int4 v2 = o4[2 * kScanBlock];
+        v2.x = max(v2.x, v1.w); v2.y = max(v2.y, v2.x); v2.z = max(v2.z, v2.y); v2.w = max(v2.w, v2.z);
+        fill_store4(dst, kRsChunk, a, e, v2);
+    }
+    if (reuse) __syncthreads();
 }
 
+// block exclusive prefix of the threads' tile-q sums (exact f64); ends with the barrier that
+// publishes it
+__device__ __forceinline__ double fill_scan_q(double tsum, FillLds& sh) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const double x = wave_incl_scan_f64(tsum);
+    if (lane == 63) sh.uw[wv] = x;
+    __syncthreads();
+    double pre = 0.0;
+#pragma unroll
+    for (int k = 0; k < kScanBlock / 64 - 1; ++k)
+        if (k < wv) pre = pre + sh.uw[k];
+    return pre + (x - tsum);
+}
+
+__device__ __forceinline__ double tile_q_sum(const u64 (&q)[kRsTile / kScanBlock]) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < kRsTile / kScanBlock; ++k) s = s + u64_small_to_d(q[k]);
+    return s;
+}
+
+// a whole chunk given the tile's offset and Q (generic Resample, overflow chunks)
 template <int MODE>
 __device__ __forceinline__ void fill_chunk(int64_t N, int b, int j, u64 Q, u64 off, const FillPlan& plan,
                                            uint64_t opx, const u64* __restrict__ qbuf, int32_t* __restrict__ anc,
@@ -1236,7 +1372,9 @@ __device__ __forceinline__ void fill_chunk(int64_t N, int b, int j, u64 Q, u64 o
     u64 q[kRsTile / kScanBlock];
     load_tile_q(N, b, qbuf, q);
     const u64 qb = plan.tilep[(int64_t)b * kPart];
-    fill_chunk_q<MODE>(N, b, j, Q, off, qb, plan, opx, q, anc, sh);
+    fill_clear(sh);
+    const double pre = fill_scan_q(tile_q_sum(q), sh);
+    fill_chunk_core<MODE>(N, b, j, Q, off, qb, pre, plan, opx, q, anc, sh, true);
 }
 
 // Ancestor fill (the icdf merge, src/resampling.jl:13-26): ancestor(slot n) = smallest m
@@ -1632,6 +1770,7 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
     __shared__ u64 s_red[kScanBlock / 64][2];
     __shared__ u64 s_parts[kScanBlock / 64][kRedPart];
     __shared__ u64 s_task[3];
+    __shared__ u64 s_u[kScanBlock / 64];
     const int th = threadIdx.x;
     const int ntiles = (int)((N + kRsTile - 1) / kRsTile);
     const int ngroups = (ntiles + G - 1) / G;
@@ -1759,8 +1898,28 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
             }
         }
         for (int b = g * G + th; b < t; b += kScanBlock) pre += plan.tilep[(int64_t)b * kPart];
-        block_sum2_u64(pre, tot, s_red);
-        fill_chunk_q<0>(N, t, 0, tot, pre, qb, plan, opx, q, anc, sh);
+        fill_clear(sh);
+        // one barrier for the tile's CDF offset, the total Q and the scan of its q
+        const int lane = th & 63, wv = th >> 6;
+        pre = wave_sum_u64(pre);
+        tot = wave_sum_u64(tot);
+        const double tsum = tile_q_sum(q);
+        const double x = wave_incl_scan_f64(tsum);
+        if (lane == 63) {
+            sh.uw[wv] = x;
+            sh.red[wv][0] = pre;
+            sh.red[wv][1] = tot;
+        }
+        __syncthreads();
+        u64 off = 0, Q = 0;
+        double lp = 0.0;
+#pragma unroll
+        for (int k = 0; k < kScanBlock / 64; ++k) {
+            off += sh.red[k][0];
+            Q += sh.red[k][1];
+            if (k < wv) lp = lp + sh.uw[k];
+        }
+        fill_chunk_core<0>(N, t, 0, Q, off, qb, lp + (x - tsum), plan, opx, q, anc, sh, false);
         return;
     }
     // ---- overflow chunks: plan from the tile sums (contiguous tiles per thread) ----
@@ -1780,7 +1939,7 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
             cbase += r < plan.dx_rank ? v : 0ull;
         }
     }
-    qmax = block_max_u64(qmax, sh.uw);
+    qmax = block_max_u64(qmax, s_u);
     block_sum2_u64(Q, cbase, s_red);
     const uint64_t Nr = plan.n_global ? plan.n_global : (uint64_t)N;
     const double ratio = Q ? wsmc_u64_to_d(Nr) / wsmc_u64_to_d(Q) : 0.0;
@@ -1796,8 +1955,8 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
         ns += (u64)ovf_chunks(qb, ratio);
     }
     u64 qtot, ntasks;
-    const u64 qpre = block_excl_scan_u64<kScanBlock / 64>(qs, sh.uw, &qtot);
-    const u64 npre = block_excl_scan_u64<kScanBlock / 64>(ns, sh.uw, &ntasks);
+    const u64 qpre = block_excl_scan_u64<kScanBlock / 64>(qs, s_u, &qtot);
+    const u64 npre = block_excl_scan_u64<kScanBlock / 64>(ns, s_u, &ntasks);
     for (u64 o = (u64)(t - ntiles); o < ntasks; o += kOverflowBlocks) {
         if (o >= npre && o < npre + ns) {          // exactly one thread owns task o
             u64 c = cbase + qpre, n0 = npre;
