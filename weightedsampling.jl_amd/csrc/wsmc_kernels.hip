@@ -1107,10 +1107,11 @@ __device__ __forceinline__ SlotHash slot_hash_of(const FillPlan& plan, uint64_t 
     h.rsys = (double)wsmc_strat_hash(h.key, h.base) * 2.3283064365386963e-10;
     return h;
 }
+// R / 2^32 of slot ns (exact), branch-free; valid when h.fast (the rank's caller sends the other
+// case, a slot range crossing a 2^32 boundary, to the exact path)
 __device__ __forceinline__ double slot_word_d(const SlotHash& h, uint32_t ns) {
-    if (h.sys) return h.rsys;
-    const uint32_t R = h.fast ? wsmc_strat_fin((h.blo + ns) ^ h.kx) : wsmc_strat_hash(h.key, h.base + ns);
-    return (double)R * 2.3283064365386963e-10;   // R / 2^32, exact
+    const double r = (double)wsmc_strat_fin((h.blo + ns) ^ h.kx) * 2.3283064365386963e-10;
+    return h.sys ? h.rsys : r;
 }
 
 // an exact integer u64 below 2^52 -> double (q <= 2^43)
@@ -1243,7 +1244,7 @@ __device__ __forceinline__ void fill_chunk_core(int64_t N, int b, int j, u64 Q, 
         const bool inr = fl < Nd;
         const uint32_t ns = (uint32_t)(inr ? fl : 0.0);
         uint32_t h = ns;
-        bool ok = f > kMargin && f < 1.0 - kMargin && inr;
+        bool ok = f > kMargin && f < 1.0 - kMargin && inr && sh_.fast;
         if (MODE == 1) {
             ok = true;
             h = fl < Nd ? ns : (uint32_t)Nr;
