@@ -44,6 +44,19 @@
 
 typedef unsigned __int128 wsmc_u128;
 
+/* WSMC_K(c): a polynomial coefficient. On the device it is held in a scalar register pair, so a
+ * Horner step is one v_fma_f64 with an SGPR operand instead of two v_mov_b32 of the literal and a
+ * v_fmac_f64 (the value and every rounding are the same; only where the constant lives differs). */
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ inline __attribute__((always_inline)) double wsmc_sreg(double c) {
+    __asm__ volatile("" : "+s"(c));
+    return c;
+}
+#define WSMC_K(c) wsmc_sreg(c)
+#else
+#define WSMC_K(c) (c)
+#endif
+
 /* ------------------------------------------------------------------------- */
 /* bit casts                                                                  */
 /* ------------------------------------------------------------------------- */
@@ -189,24 +202,28 @@ WSMC_HD double wsmc_exp(double x) {
  * statistics keep) and NaN for NaN. |error| ~ 2 ulp on [-80, 0].
  */
 WSMC_HD double wsmc_expw(double x) {
-    if (!(x >= -80.0)) return wsmc_isnan(x) ? x : 0.0;
+    /* branch-free (a select at the end): the device evaluates the polynomial for every lane */
+    const int ok = x >= -80.0;
+    const double xr = x;
+    x = ok ? x : -80.0;
     const double kd = wsmc_floor(x * 1.44269504088896338700e+00 + 0.5);
     const double r = (x - kd * 6.93147180369123816490e-01) - kd * 1.90821492927058770002e-10;
     double p = 1.6059043836821613e-10;                 /* 1/13! */
-    p = __builtin_fma(p, r, 2.08767569878681e-09);
-    p = __builtin_fma(p, r, 2.505210838544172e-08);
-    p = __builtin_fma(p, r, 2.755731922398589e-07);
-    p = __builtin_fma(p, r, 2.7557319223985893e-06);
-    p = __builtin_fma(p, r, 2.48015873015873e-05);
-    p = __builtin_fma(p, r, 0.0001984126984126984);
-    p = __builtin_fma(p, r, 0.001388888888888889);
-    p = __builtin_fma(p, r, 0.008333333333333333);
-    p = __builtin_fma(p, r, 0.041666666666666664);
-    p = __builtin_fma(p, r, 0.16666666666666666);
+    p = __builtin_fma(p, r, WSMC_K(2.08767569878681e-09));
+    p = __builtin_fma(p, r, WSMC_K(2.505210838544172e-08));
+    p = __builtin_fma(p, r, WSMC_K(2.755731922398589e-07));
+    p = __builtin_fma(p, r, WSMC_K(2.7557319223985893e-06));
+    p = __builtin_fma(p, r, WSMC_K(2.48015873015873e-05));
+    p = __builtin_fma(p, r, WSMC_K(0.0001984126984126984));
+    p = __builtin_fma(p, r, WSMC_K(0.001388888888888889));
+    p = __builtin_fma(p, r, WSMC_K(0.008333333333333333));
+    p = __builtin_fma(p, r, WSMC_K(0.041666666666666664));
+    p = __builtin_fma(p, r, WSMC_K(0.16666666666666666));
     p = __builtin_fma(p, r, 0.5);
     p = __builtin_fma(p, r, 1.0);
     p = __builtin_fma(p, r, 1.0);
-    return p * wsmc_pow2i((int)kd);
+    const double y = p * wsmc_pow2i((int)kd);
+    return ok ? y : (wsmc_isnan(xr) ? xr : 0.0);
 }
 
 /* exp without a division (the damped-oscillator mean, evaluated O(t) times per particle per
@@ -313,7 +330,120 @@ WSMC_HD void wsmc_sincos2pi(double u, double* s, double* c) {
     *s = (o & 4) ? -b : b;                          /* o = 4..7 */
 }
 
-/* cos(x) for |x| < 2^19*pi/2 (Cody–Waite three-part pi/2); NaN/inf -> NaN */
+
+/* ---- argument reduction by pi/2 for large |x| (Payne-Hanek) --------------------------------
+ * The Cody-Waite three-part reduction below is exact only while fn * p1 is (fn < 2^20), i.e.
+ * |x| < 2^19 pi/2. Past that (and up to the largest double) x mod pi/2 comes from the binary
+ * expansion of 2/pi: x = M 2^E (M a 53-bit integer), and only the 2/pi bits from E - 1 onward
+ * reach x (2/pi) mod 4 (earlier bits give multiples of 4). A 192-bit window W of those bits gives
+ * y = M W / 2^190: bits 190-191 the quadrant, bits 62-189 the fraction (128 bits, so a remainder
+ * as small as any double's distance to a multiple of pi/2, about 2^-61, keeps 53+ significant
+ * bits; the bits past the window move y by < 2^-136). The fraction times pi/2 in double-double
+ * is rounded once. Julia's rem_pio2 is exact too, so sin/cos of huge arguments now agree with
+ * Base to the kernels' accuracy. */
+WSMC_HD uint64_t wsmc_2opi_word(int j) {   /* bits 64j+1 .. 64j+64 of 2/pi (MSB first), j < 20 */
+    static const uint64_t t[20] = {
+        0xa2f9836e4e441529ULL, 0xfc2757d1f534ddc0ULL, 0xdb6295993c439041ULL, 0xfe5163abdebbc561ULL,
+        0xb7246e3a424dd2e0ULL, 0x06492eea09d1921cULL, 0xfe1deb1cb129a73eULL, 0xe88235f52ebb4484ULL,
+        0xe99c7026b45f7e41ULL, 0x3991d639835339f4ULL, 0x9c845f8bbdf9283bULL, 0x1ff897ffde05980fULL,
+        0xef2f118b5a0a6d1fULL, 0x6d367ecf27cb09b7ULL, 0x4f463f669e5fea2dULL, 0x7527bac7ebe5f17bULL,
+        0x3d0739f78a5292eaULL, 0x6bfb5fb11f8d5d08ULL, 0x56033046fc7b6babULL, 0xf0cfbc209af4361dULL};
+    return (unsigned)j < 20u ? t[j] : 0;
+}
+WSMC_HD int wsmc_clz64(uint64_t v) { return v ? __builtin_clzll(v) : 64; }
+/* 64 bits of 2/pi from bit pos on (bits at pos <= 0 are 0: 2/pi < 1) */
+WSMC_HD uint64_t wsmc_2opi_bits(int pos) {
+    if (pos <= -63) return 0;
+    if (pos <= 0) return wsmc_2opi_word(0) >> (1 - pos);
+    const int j = (pos - 1) >> 6, sh = (pos - 1) & 63;
+    return sh ? (wsmc_2opi_word(j) << sh) | (wsmc_2opi_word(j + 1) >> (64 - sh)) : wsmc_2opi_word(j);
+}
+/* ax finite, ax >= 2^19 pi/2: r in [-pi/4, pi/4] and the quadrant n with ax = r + n pi/2 (mod 2 pi).
+ * Out of line on the device (returned by value, no stack): inlined at every sin / cos it tripled
+ * the compile time of the run-time compiled Move blocks whose folds carry oscillator terms. */
+typedef struct { double r; int n; } wsmc_rq;
+#if defined(__HIPCC__) || defined(__HIP__)
+__host__ __device__ inline __attribute__((noinline))
+#else
+static __attribute__((noinline))
+#endif
+wsmc_rq wsmc_rem_pio2_large_rq(double ax) {
+    int n = 0;
+    wsmc_rq o;
+    o.r = 0.0;
+    {
+    const uint64_t b = wsmc_d2bits(ax);
+    const int E = (int)((b >> 52) & 0x7ff) - 1075;       /* ax = M 2^E */
+    const uint64_t M = (b & 0x000fffffffffffffULL) | 0x0010000000000000ULL;
+    /* window W (192 bits) = 2/pi bits E-1 .. E+190: y = M W / 2^190 */
+    const int s = E - 1;
+    /* P = M W limb by limb, low to high (a rolled loop: one multiply in the code, which keeps the
+       inlined path small where sin / cos sit in unrolled folds) */
+    uint64_t L0 = 0, L1 = 0, L2 = 0;
+    wsmc_u128 acc = 0;
+#if defined(__clang__)
+#pragma nounroll
+#endif
+    for (int i = 0; i < 3; ++i) {
+        acc += (wsmc_u128)M * wsmc_2opi_bits(s + 128 - 64 * i);
+        L0 = L1; L1 = L2; L2 = (uint64_t)acc;
+        acc >>= 64;
+    }                                              /* bits >= 192 (acc): multiples of 4 in y */
+    int q = (int)(L2 >> 62);                                /* bits 190-191 */
+    wsmc_u128 G = ((wsmc_u128)(L2 & ((1ULL << 62) - 1)) << 66) | ((wsmc_u128)L1 << 2) | (L0 >> 62);
+    int neg = 0;
+    if (G >> 127) {                                /* fraction >= 1/2: the next quadrant, r < 0 */
+        q = (q + 1) & 3;
+        G = (wsmc_u128)0 - G;
+        neg = 1;
+    }
+    n = q;
+    if (G == 0) { o.n = n; return o; }
+    const uint64_t gh = (uint64_t)(G >> 64), gl = (uint64_t)G;
+    const int lz = gh ? wsmc_clz64(gh) : 64 + wsmc_clz64(gl);
+    const wsmc_u128 Gn = G << lz;                  /* MSB at bit 127 */
+    const uint64_t h53 = (uint64_t)(Gn >> 75), l53 = (uint64_t)(Gn >> 22) & ((1ULL << 53) - 1);
+    const double fh = (double)(int64_t)h53 * wsmc_pow2i(-53 - lz);      /* exact */
+    const double fl = (double)(int64_t)l53 * wsmc_pow2i(-106 - lz);     /* exact (lz <= 127) */
+    const double pio2_hi = 1.5707963267948966, pio2_lo = 6.123233995736766e-17;
+    const double rh = fh * pio2_hi;
+    const double e = __builtin_fma(fh, pio2_hi, -rh);
+    const double rl = e + (fh * pio2_lo + fl * pio2_hi);
+    const double r = rh + rl;
+    o.r = neg ? -r : r;
+    o.n = n;
+    return o;
+    }
+}
+WSMC_HD double wsmc_rem_pio2_large(double ax, int* n) {
+    const wsmc_rq o = wsmc_rem_pio2_large_rq(ax);
+    *n = o.n;
+    return o.r;
+}
+#define WSMC_PIO2_LARGE 823549.0                   /* < 2^19 pi/2: Cody-Waite below, Payne-Hanek above */
+
+/* cos(x) by the Cody–Waite reduction alone, for the damped-oscillator phase w t + p (its mean and
+ * the rotation anchors, wsmc_sincos): exact below WSMC_PIO2_LARGE (2^19 pi/2 = 8.2e5 rad), NaN past
+ * it — a phase that large makes the term's log-density NaN (no weight, a rejected proposal) rather
+ * than a silently wrong value. The fold kernels keep the reduction inline and small this way; the
+ * general operators below reduce exactly at any |x|. */
+WSMC_HD double wsmc_cos_cw(double x) {
+    const double invpio2 = 6.36619772367581382433e-01, p1 = 1.57079632673412561417e+00,
+                 p2 = 6.07710050630396597660e-11, p3 = 2.02226624879595063154e-21;
+    if (!wsmc_isfinite(x)) return WSMC_NAN;
+    const double ax = wsmc_fabs(x);
+    const int small = ax <= 7.85398163397448278999e-01;
+    const double axr = ax < WSMC_PIO2_LARGE ? ax : 0.0;
+    const double fn = (double)(int64_t)(axr * invpio2 + 0.5);
+    const double rr = ax < WSMC_PIO2_LARGE ? ((ax - fn * p1) - fn * p2) - fn * p3 : WSMC_NAN;
+    const double r = small ? x : rr;
+    const int n = small ? 0 : (int)((int64_t)fn & 3);
+    const double kc = wsmc_kcos(r), ks = wsmc_ksin(r);
+    const double v = (n & 1) ? ks : kc;
+    return ((n + 1) & 2) ? -v : v;
+}
+
+/* cos(x) for every finite x (Cody–Waite three-part pi/2 below WSMC_PIO2_LARGE, Payne–Hanek above); NaN/inf -> NaN */
 WSMC_HD double wsmc_cos(double x) {
     const double invpio2 = 6.36619772367581382433e-01,
                  p1 = 1.57079632673412561417e+00,   /* first 33 bits of pi/2 */
@@ -325,10 +455,13 @@ WSMC_HD double wsmc_cos(double x) {
        are those of the branchy form (kcos(x) for small |x|, else the quadrant's kernel). */
     const double ax = wsmc_fabs(x);
     const int small = ax <= 7.85398163397448278999e-01;
-    const double fn = (double)(int64_t)(ax * invpio2 + 0.5);
-    const double rr = ((ax - fn * p1) - fn * p2) - fn * p3;
+    const double axr = ax < WSMC_PIO2_LARGE ? ax : 0.0;
+    const double fn = (double)(int64_t)(axr * invpio2 + 0.5);
+    double rr = ((ax - fn * p1) - fn * p2) - fn * p3;
+    int nr = (int)((int64_t)fn & 3);
+    if (ax >= WSMC_PIO2_LARGE) rr = wsmc_rem_pio2_large(ax, &nr);
     const double r = small ? x : rr;
-    const int n = small ? 0 : (int)((int64_t)fn & 3);
+    const int n = small ? 0 : nr;
     const double kc = wsmc_kcos(r), ks = wsmc_ksin(r);
     const double v = (n & 1) ? ks : kc;
     return ((n + 1) & 2) ? -v : v;   /* n = 1, 2 negate */
@@ -342,10 +475,13 @@ WSMC_HD double wsmc_sin(double x) {
     if (!wsmc_isfinite(x)) return WSMC_NAN;
     const double ax = wsmc_fabs(x);
     const int small = ax <= 7.85398163397448278999e-01;
-    const double fn = (double)(int64_t)(ax * invpio2 + 0.5);
-    const double rr = ((ax - fn * p1) - fn * p2) - fn * p3;
+    const double axr = ax < WSMC_PIO2_LARGE ? ax : 0.0;
+    const double fn = (double)(int64_t)(axr * invpio2 + 0.5);
+    double rr = ((ax - fn * p1) - fn * p2) - fn * p3;
+    int nr = (int)((int64_t)fn & 3);
+    if (ax >= WSMC_PIO2_LARGE) rr = wsmc_rem_pio2_large(ax, &nr);
     const double r = small ? ax : rr;
-    const int n = small ? 0 : (int)((int64_t)fn & 3);
+    const int n = small ? 0 : nr;
     const double kc = wsmc_kcos(r), ks = wsmc_ksin(r);
     double v = (n & 1) ? kc : ks;
     v = (n & 2) ? -v : v;            /* n = 2, 3 negate */
@@ -490,9 +626,10 @@ WSMC_HD double wsmc_uniform_logpdf(double a, double b, double x) {
 }
 /* the damped-oscillator mean, examples/damped_oscillator.jl:11 */
 WSMC_HD double wsmc_oscillator(double t, double A, double om, double ga, double ph) {
-    return A * wsmc_exp_nd(-ga * t) * wsmc_cos(om * t + ph);
+    return A * wsmc_exp_nd(-ga * t) * wsmc_cos_cw(om * t + ph);
 }
-/* sin and cos with wsmc_cos's reduction and kernels: *c is wsmc_cos(x) bit for bit */
+/* sin and cos with wsmc_cos_cw's reduction and kernels (the oscillator's phase): *c is wsmc_cos_cw(x)
+   bit for bit, so wsmc_cos(x) below WSMC_PIO2_LARGE; NaN past it */
 WSMC_HD void wsmc_sincos(double x, double* s, double* c) {
     const double invpio2 = 6.36619772367581382433e-01, p1 = 1.57079632673412561417e+00,
                  p2 = 6.07710050630396597660e-11, p3 = 2.02226624879595063154e-21;
@@ -503,8 +640,9 @@ WSMC_HD void wsmc_sincos(double x, double* s, double* c) {
     }
     const double ax = wsmc_fabs(x);
     const int small = ax <= 7.85398163397448278999e-01;
-    const double fn = (double)(int64_t)(ax * invpio2 + 0.5);
-    const double rr = ((ax - fn * p1) - fn * p2) - fn * p3;
+    const double axr = ax < WSMC_PIO2_LARGE ? ax : 0.0;
+    const double fn = (double)(int64_t)(axr * invpio2 + 0.5);
+    const double rr = ax < WSMC_PIO2_LARGE ? ((ax - fn * p1) - fn * p2) - fn * p3 : WSMC_NAN;
     const double r = small ? x : rr;
     const int n = small ? 0 : (int)((int64_t)fn & 3);
     const double kc = wsmc_kcos(r), ks = wsmc_ksin(r);

@@ -93,6 +93,7 @@ _SIG = {
     "or_log": (C.c_double, [C.c_double]),
     "or_log1p": (C.c_double, [C.c_double]),
     "or_cos": (C.c_double, [C.c_double]),
+    "or_sin": (C.c_double, [C.c_double]),
     "or_sincos2pi": (None, [C.c_double, _D, _D]),
     "or_normal_k": (C.c_double, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32]),
     "or_uniform_k": (C.c_double, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32]),

@@ -981,6 +981,7 @@ double or_expw(double x) { return wsmc_expw(x); }
 double or_log(double x) { return wsmc_log(x); }
 double or_log1p(double x) { return wsmc_log1p(x); }
 double or_cos(double x) { return wsmc_cos(x); }
+double or_sin(double x) { return wsmc_sin(x); }
 void or_sincos2pi(double u, double* s, double* c) { wsmc_sincos2pi(u, s, c); }
 double or_normal_k(uint64_t seed, uint64_t op, uint64_t idx, uint32_t k) { return wsmc_normal_k(seed, op, idx, k); }
 double or_uniform_k(uint64_t seed, uint64_t op, uint64_t idx, uint32_t k) { return wsmc_uniform_k(seed, op, idx, k); }

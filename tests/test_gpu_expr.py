@@ -27,13 +27,16 @@ EXPRS = {
     "logic": lambda: ifelse(or_(Col("c"), Col("a") > 1.0), 0.98, 0.01) + and_(Col("c"), not_(Col("a") < 0.0)),
     "oscillator": lambda: Col("b") * exp(-0.1 * Col("b") * 3.0) * cos(Col("a") * 3.0 + Col("d")),
     "abs_neg": lambda: abs(Col("a")) - (-Col("d")),
+    # |e| from 1e5 to 1e300: the Payne-Hanek reduction past 2^19 pi/2 (include/wsmc_math.h)
+    "sincos_large": lambda: sin(Col("e")) - 2.0 * cos(Col("e")),
 }
 
 
 def fill(ctx, N, seed=3):
     rng = np.random.default_rng(seed)
     vals = {"a": rng.normal(0.0, 2.0, N), "b": rng.uniform(0.1, 3.0, N), "c": rng.integers(0, 2, N).astype(float),
-            "d": rng.normal(0.0, 30.0, N)}
+            "d": rng.normal(0.0, 30.0, N),
+            "e": np.exp(rng.uniform(np.log(1e5), np.log(1e300), N)) * rng.choice([-1.0, 1.0], N)}
     vals["a"][:4] = [-0.0, 0.0, np.nan, np.inf]
     for name, v in vals.items():
         ctx.col_upload(ctx.col_create(name), v)

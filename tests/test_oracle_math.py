@@ -317,3 +317,63 @@ def test_oscillator_rotation_known_answers():
             worst = max(worst, abs(L.or_osc_rolled(ta, d, m, A, om, ga, ph) - ref) / max(A, 1e-300))
     print('worst rolled-mean error / A', worst)
     assert worst < 1e-13, worst
+
+
+def _pi_fraction(bits=1600):
+    """pi to `bits` bits, exact integer Machin formula (pi = 16 atan(1/5) - 4 atan(1/239))"""
+    from fractions import Fraction
+
+    def atan_inv(x):
+        one = 1 << bits
+        t = one // x
+        s, k, sign = t, 1, -1
+        while t:
+            t //= x * x
+            s += sign * (t // (2 * k + 1))
+            sign, k = -sign, k + 1
+        return s
+    return Fraction(16 * atan_inv(5) - 4 * atan_inv(239), 1 << bits)
+
+
+def _sincos_exact(x, pi):
+    """sin(x), cos(x) from the exact remainder x mod pi/2 (a Fraction), then libm on |r| <= pi/4"""
+    from fractions import Fraction
+    q = Fraction(x) / (pi / 2)
+    n = q.numerator // q.denominator
+    f = q - n
+    if f > Fraction(1, 2):
+        n, f = n + 1, f - 1
+    r = float(f * pi / 2)
+    s, c = math.sin(r), math.cos(r)
+    return [(s, c), (c, -s), (-s, -c), (-c, s)][n % 4]
+
+
+def test_trig_large_arguments_exact():
+    """past 2^19 pi/2 the three-part Cody-Waite reduction loses the quadrant; the
+    Payne-Hanek path (include/wsmc_math.h wsmc_rem_pio2_large) reduces exactly for every finite
+    x, as Julia's rem_pio2 does. sin / cos / sincos against the exact remainder (x mod pi/2 in
+    rational arithmetic with a 1600-bit pi, then libm on the remainder) at 1e6 .. 1e308, 2^63 and
+    2^64 (where the old int64 cast was undefined), random large magnitudes, and the double closest
+    to a multiple of pi/2 (6381956970095103 * 2^797, remainder 4.7e-19 — numpy's cos is 8 ulp off
+    there), to 2 ulp of the result."""
+    import ctypes
+    L = O.lib()
+    pi = _pi_fraction()
+    rng = np.random.default_rng(7)
+    xs = [823549.0, 823550.5, 1e6, 1e10, 1e15, 1e22, 1e300, 2.0 ** 63, 2.0 ** 64, 1.7976931348623157e308,
+          6381956970095103.0 * 2.0 ** 797, 5.0e15 + 0.5]
+    xs += [float(v) for v in np.exp(rng.uniform(np.log(1e6), np.log(1e300), 300))]
+    xs += [-x for x in xs[:20]]
+    for x in xs:
+        c, sn = L.or_cos(x), L.or_sin(x)
+        s2, c2 = ctypes.c_double(), ctypes.c_double()
+        L.or_sincos(x, ctypes.byref(s2), ctypes.byref(c2))
+        rs, rc = _sincos_exact(x, pi)
+        assert abs(c - rc) <= 2 * np.spacing(abs(rc)), (x, c, rc)
+        assert abs(sn - rs) <= 2 * np.spacing(abs(rs)), (x, sn, rs)
+        # the oscillator's phase reduction (wsmc_sincos) stops at the Cody-Waite range: NaN past it
+        assert math.isnan(c2.value) and math.isnan(s2.value)
+    # below the switch the Cody-Waite path is unchanged
+    for x in (0.5, 3.0, 1e3, 1e5, 8e5):
+        rs, rc = _sincos_exact(x, pi)
+        assert abs(L.or_cos(x) - rc) <= 2 * np.spacing(abs(rc)) and abs(L.or_sin(x) - rs) <= 2 * np.spacing(abs(rs))

@@ -32,10 +32,13 @@ enum : int {
     kDppRowShr1 = 0x111, kDppRowShr2 = 0x112, kDppRowShr3 = 0x113, kDppRowShr4 = 0x114,
     kDppRowShr8 = 0x118, kDppBcast15 = 0x142, kDppBcast31 = 0x143, kDppWaveShr1 = 0x138
 };
+// lanes with no source read 0 (the identity of every use: sums, unsigned max). With full row
+// and bank masks that is bound_ctrl, and no `old` value has to be materialised first.
 template <int CTRL, int ROW = 0xf, int BANK = 0xf>
 __device__ __forceinline__ u64 dpp_u64(u64 v) {
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, ROW, BANK, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, ROW, BANK, false);
+    constexpr bool full = ROW == 0xf && BANK == 0xf;
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, ROW, BANK, full);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, ROW, BANK, full);
     return ((u64)(uint32_t)hi << 32) | (uint32_t)lo;
 }
 template <int CTRL>
