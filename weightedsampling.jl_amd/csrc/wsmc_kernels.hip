@@ -1390,7 +1390,7 @@ __device__ __forceinline__ void fill_chunk(int64_t N, int b, int j, u64 Q, u64 o
 // MODE (diagnostics only; production = 0): 1 = no rank (cheap estimate), 2 = no fill,
 // 3 = scan only
 template <int MODE>
-__global__ __launch_bounds__(kScanBlock) void k_rs_scan_t(int64_t N, const ShardRecord* __restrict__ rec,
+__global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(6))) void k_rs_scan_t(int64_t N, const ShardRecord* __restrict__ rec,
                                                           const Decision* __restrict__ dec, FillPlan plan,
                                                           const u64* __restrict__ tileOff,
                                                           const u64* __restrict__ qbuf, int32_t* __restrict__ anc) {
@@ -1766,7 +1766,7 @@ __device__ __forceinline__ void block_sum2_u64(u64& a, u64& b, u64 (*lds)[2]) {
 // the step resampled with mean 0 (the same fill work under forced resampling: q depends on
 // lw - M only)
 template <int MODE>
-__global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPlan plan, const u64* __restrict__ grp,
+__global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(6))) void k_rs_fill_fused(int64_t N, FillPlan plan, const u64* __restrict__ grp,
                                                               int G, const MaxSlots* __restrict__ ms, double ess_min,
                                                               ShardRecord* rec, Decision* dec,
                                                               const u64* __restrict__ qbuf, int32_t* __restrict__ anc) {
@@ -1961,12 +1961,27 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
     u64 qtot, ntasks;
     const u64 qpre = block_excl_scan_u64<kScanBlock / 64>(qs, s_u, &qtot);
     const u64 npre = block_excl_scan_u64<kScanBlock / 64>(ns, s_u, &ntasks);
-    for (u64 o = (u64)(t - ntiles); o < ntasks; o += kOverflowBlocks) {
-        if (o >= npre && o < npre + ns) {          // exactly one thread owns task o
-            u64 c = cbase + qpre, n0 = npre;
-            for (int b = b0; b < b1; ++b) {
+    // the plan goes to LDS: nothing per thread stays live across the chunk fills (their
+    // registers bound the whole kernel's occupancy, the tile blocks' included)
+    __shared__ uint32_t s_npre[kScanBlock], s_ns[kScanBlock];
+    __shared__ u64 s_c0[kScanBlock];
+    s_npre[th] = (uint32_t)npre;
+    s_ns[th] = (uint32_t)ns;
+    s_c0[th] = cbase + qpre;
+    const u64 Qu = ((u64)__builtin_amdgcn_readfirstlane((int)(Q >> 32)) << 32) |
+                   (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)Q);
+    const uint32_t nt = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)ntasks);
+    for (uint32_t o = (uint32_t)(t - ntiles); o < nt; o += kOverflowBlocks) {
+        const uint32_t n0_ = s_npre[th], k_ = s_ns[th];
+        if (o >= n0_ && o < n0_ + k_) {            // exactly one thread owns task o
+            u64 c = s_c0[th];
+            uint32_t n0 = n0_;
+            const int per_ = (ntiles + kScanBlock - 1) / kScanBlock;
+            const int bb0 = th * per_ < ntiles ? th * per_ : ntiles;
+            const int bb1 = bb0 + per_ < ntiles ? bb0 + per_ : ntiles;
+            for (int b = bb0; b < bb1; ++b) {
                 const u64 qb = plan.tilep[(int64_t)b * kPart];
-                const u64 k = (u64)ovf_chunks(qb, ratio);
+                const uint32_t k = (uint32_t)ovf_chunks(qb, ratio);
                 if (o < n0 + k) {
                     s_task[0] = (u64)b;
                     s_task[1] = 1 + (o - n0);
@@ -1978,10 +1993,11 @@ __global__ __launch_bounds__(kScanBlock) void k_rs_fill_fused(int64_t N, FillPla
             }
         }
         __syncthreads();
-        const int b = (int)s_task[0];
-        const int j = (int)s_task[1];
-        const u64 off = s_task[2];
-        fill_chunk<0>(N, b, j, Q, off, plan, opx, qbuf, anc, sh);   // ends with a barrier
+        const int b = __builtin_amdgcn_readfirstlane((int)s_task[0]);
+        const int j = __builtin_amdgcn_readfirstlane((int)s_task[1]);
+        const u64 off = ((u64)__builtin_amdgcn_readfirstlane((int)(s_task[2] >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)s_task[2]);
+        fill_chunk<0>(N, b, j, Qu, off, plan, opx, qbuf, anc, sh);   // ends with a barrier
     }
 }
 
