@@ -415,7 +415,9 @@ int wsmc_debug_kernel_bench(wsmc_ctx* ctx, int32_t kernel, int32_t mode, int32_t
  * record exchange (a Resample's or an evidence query's) with WSMC_EHIP before exchanging.
  * On a multi-device handle the other shards then leave their exchange with WSMC_ERCCL
  * instead of waiting for it; shards that left in different states mark the handle failed
- * (every later call returns WSMC_ESTATE). nth = 0 disarms.                               */
+ * (every later call returns WSMC_ESTATE). nth = 0 disarms. nth >= 1000: the failure is a
+ * WSMC_EARG at exchange nth - 1000 (an argument error one shard meets alone past an exchange:
+ * it requests the abort at once rather than waiting for peers that meet the same error). */
 int wsmc_debug_inject_failure(wsmc_ctx* ctx, int32_t shard, int32_t nth);
 /* Exact-sharded fused run: the fixed neighbour block (slots per step) and
  * trace window (ids per level) sizes — > 0 sets, 0 restores the defaults, < 0 leaves as is —

@@ -542,9 +542,20 @@ WSMC_HD double wsmc_powi(double x, int64_t n) {
    else exp(b log a) — NaN for a < 0 (Julia throws a DomainError); relative error about
    |b log a| 2^-53 beyond the restated exp / log (Julia's double-double log is tighter) */
 WSMC_HD double wsmc_pow(double a, double b) {
+    /* Base.^(::Float64, ::Float64): |y| clamped to 1.5 2^62 first (past it every power over- or
+       underflows, and an even integer keeps a negative base's sign right: (-2.0)^1e19 = Inf), an
+       integer y as the integer power, then the domain cases (a negative base is Julia's
+       DomainError: NaN here; 0^y and Inf^y by sign), else exp(y log x) */
     if (a == 1.0) return 1.0;
-    if (wsmc_isnan(b)) return b;
-    if (wsmc_fabs(b) < 4611686018427387904.0 && b == (double)(int64_t)b) return wsmc_powi(a, (int64_t)b);
+    if (!(wsmc_fabs(b) < 6917529027641081856.0)) {   /* 0x1.8p62 */
+        if (wsmc_isnan(b)) return b;
+        b = b > 0.0 ? 6917529027641081856.0 : -6917529027641081856.0;
+    }
+    const int64_t bi = (int64_t)b;
+    if (b == (double)bi) return wsmc_powi(a, bi);
+    if (a < 0.0) return WSMC_NAN;
+    if (a == 0.0) return b > 0.0 ? 0.0 : WSMC_INF;
+    if (!wsmc_isfinite(a)) return (b > 0.0 || wsmc_isnan(a)) ? a : 0.0;
     return wsmc_exp(b * wsmc_log(a));
 }
 

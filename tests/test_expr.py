@@ -192,3 +192,40 @@ def test_fire_alarm_probabilities_as_expressions():
     np.testing.assert_array_equal(r, (bits[0] == 1) & (bits[1] == 0))
     t = run(o, ne(Col("fire"), Col("smoke")), "xor")
     np.testing.assert_array_equal(t, bits[0] != bits[1])
+
+
+def test_julia_pow_huge_and_edge_exponents():
+    """ADVICE r04: Base.^(::Float64, ::Float64) clamps |y| to 1.5 2^62 before its integer test,
+    so a negative base to a huge even exponent is the integer power (Inf / 0), not NaN; 0^y and
+    Inf^y go by the sign of y (Julia 1.10 values, restated in include/wsmc_math.h wsmc_pow)."""
+    o = Oracle(12, seed=1)
+    a = np.array([-2.0, -2.0, -0.5, 2.0, 0.5, 0.0, 0.0, np.inf, np.inf, -np.inf, np.nan, -3.0])
+    b = np.array([1e19, -1e19, 1e300, np.inf, np.inf, 0.5, -0.5, 0.5, -0.5, 1e19, 2.5, 2.5])
+    o.col_upload(o.col_create("a"), a)
+    o.col_upload(o.col_create("b"), b)
+    p = run(o, Col("a") ** Col("b"), "p")
+    assert p[0] == np.inf and p[1] == 0.0      # (-2.0)^1e19 = Inf, (-2.0)^-1e19 = 0.0
+    assert p[2] == 0.0                         # (-0.5)^1e300 = 0.0
+    assert p[3] == np.inf and p[4] == 0.0      # 2^Inf = Inf, 0.5^Inf = 0
+    assert p[5] == 0.0 and p[6] == np.inf      # 0^0.5 = 0, 0^-0.5 = Inf
+    assert p[7] == np.inf and p[8] == 0.0      # Inf^0.5 = Inf, Inf^-0.5 = 0
+    assert p[9] == np.inf                      # (-Inf)^1e19: an even integer power
+    assert np.isnan(p[10]) and np.isnan(p[11])  # NaN^2.5; (-3)^2.5 is Julia's DomainError
+
+
+def test_affine_constant_keeps_the_operation_order():
+    """an affine Expr that enters a program sums as ((c0 + t0) + t1) + ..., the order
+    wsmc_operand_eval uses and, c0 + x being x + c0 exactly, Julia's ((x + 1) + y) + z."""
+    rng = np.random.default_rng(4)
+    n = 4096
+    x, y, z = (rng.normal(0, 1, n) * 10.0 ** rng.integers(-8, 8, n) for _ in range(3))
+    o = Oracle(n, seed=1)
+    for name, v in (("x", x), ("y", y), ("z", z)):
+        o.col_upload(o.col_create(name), v)
+    got = run(o, Col("x") + 1.0 + Col("y") + Col("z"), "s")
+    assert (got.view(np.uint64) == (((x + 1.0) + y) + z).view(np.uint64)).all()
+    # two terms stay an operand; the same value through a program (a no-op max with itself)
+    two = run(o, Col("x") * 3.0 + 1.5 + Col("y"), "t2")
+    prog = run(o, max_(Col("x") * 3.0 + 1.5 + Col("y"), Col("x") * 3.0 + 1.5 + Col("y")), "t3")
+    assert (two.view(np.uint64) == prog.view(np.uint64)).all()
+    assert (two.view(np.uint64) == ((1.5 + 3.0 * x) + y).view(np.uint64)).all()

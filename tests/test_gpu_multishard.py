@@ -665,6 +665,28 @@ def test_multi_handle_shard_failure_returns_error(gpu_available, transport):
     g.close()
 
 
+def test_multi_handle_lone_argument_error_returns_promptly(gpu_available):
+    """an argument error one shard meets alone after an exchange of the call (an
+    exact Resample's record exchange follows its max exchange) must not be taken for a symmetric
+    error: the shard requests the abort at once — the call returns within seconds, not after the
+    30 s peer wait — and the diverged handle refuses later calls."""
+    import time
+    import wsmc
+    from wsmc import abi, models
+    g = wsmc.Context.multi(3000, 3, seed=5, devices=[0] * 3, transport=abi.TRANSPORT_HOST)
+    g.comm_set_shard_mode(abi.SHARD_EXACT)
+    obs = models.ssm2d_data(4)
+    models.ssm2d_statements(g, obs[:2], ess_perc_min=1.0)
+    g.debug_inject_failure(2, 1001)
+    t0 = time.perf_counter()
+    with pytest.raises(wsmc.WSMCError, match="injected shard argument error"):
+        models.ssm2d_statements(g, obs[2:], ess_perc_min=1.0)
+    assert time.perf_counter() - t0 < 10.0
+    with pytest.raises(wsmc.WSMCError, match="failed in an earlier call"):
+        g.get_state()
+    g.close()
+
+
 @pytest.mark.parametrize("mode", ["island", "exact"])
 def test_multi_handle_symmetric_errors_keep_the_handle(gpu_available, mode):
     """Errors every shard meets at the same point do not abort the handle: an

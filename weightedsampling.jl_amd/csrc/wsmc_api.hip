@@ -1125,6 +1125,13 @@ static int enqueue_resample_stats(wsmc_ctx* c, const double* w, MaxSlots* ms, Sh
 }
 
 // all-gather `words` u64 per rank in place (rank r's block at buf + r * words) on stream s
+// a host-provided exchange (wsmc_comm_init_host), counted: a multi-device handle's shard that
+// fails after its first exchange of a call requests the abort at once (csrc/wsmc_multi.hip)
+static inline int host_xchg(wsmc_ctx* c, const uint64_t* mine, int32_t words, uint64_t* all) {
+    c->exchanges += 1;
+    return c->host_exchange(c->host_user, mine, words, all);
+}
+
 static int exchange_words(wsmc_ctx* c, unsigned long long* buf, int64_t words, hipStream_t s) {
     if (!is_sharded(c)) return WSMC_OK;
     if (c->host_exchange) {
@@ -1134,7 +1141,7 @@ static int exchange_words(wsmc_ctx* c, unsigned long long* buf, int64_t words, h
         WSMC_HIP(ctx_sync(c, s));
         const std::vector<unsigned long long> mine(h.begin() + (size_t)c->rank * words,
                                                    h.begin() + (size_t)(c->rank + 1) * words);
-        if (c->host_exchange(c->host_user, reinterpret_cast<const uint64_t*>(mine.data()), (int32_t)words,
+        if (host_xchg(c, reinterpret_cast<const uint64_t*>(mine.data()), (int32_t)words,
                              reinterpret_cast<uint64_t*>(h.data())) != 0)
             return fail(WSMC_ERCCL, "host exchange failed");
         WSMC_HIP(hipMemcpyAsync(buf, h.data(), sizeof(unsigned long long) * h.size(), hipMemcpyHostToDevice, s));
@@ -1142,13 +1149,15 @@ static int exchange_words(wsmc_ctx* c, unsigned long long* buf, int64_t words, h
         return WSMC_OK;
     }
     WSMC_RCCL_GUARD(c);
+    c->exchanges += 1;
     WSMC_RCCL(ncclAllGather(buf + (size_t)c->rank * words, buf, (size_t)words, ncclUint64, c->comm, s));
     return WSMC_OK;
 }
 
 static int exchange_recs(wsmc_ctx* c, ShardRecord* recs) {
     if (c->inject_fail > 0 && --c->inject_fail == 0)
-        return fail(WSMC_EHIP, "injected shard failure (wsmc_debug_inject_failure)");
+        return c->inject_earg ? fail(WSMC_EARG, "injected shard argument error (wsmc_debug_inject_failure)")
+                              : fail(WSMC_EHIP, "injected shard failure (wsmc_debug_inject_failure)");
     if (!is_sharded(c)) return WSMC_OK;
     const int words = (int)(sizeof(ShardRecord) / sizeof(unsigned long long));
     if (c->host_exchange) {
@@ -1156,7 +1165,7 @@ static int exchange_recs(wsmc_ctx* c, ShardRecord* recs) {
         WSMC_HIP(hipMemcpyAsync(&h[c->rank], recs + c->rank, sizeof(ShardRecord), hipMemcpyDeviceToHost, c->stream));
         WSMC_HIP(ctx_sync(c, c->stream));
         const ShardRecord mine = h[c->rank];
-        if (c->host_exchange(c->host_user, reinterpret_cast<const uint64_t*>(&mine), words,
+        if (host_xchg(c, reinterpret_cast<const uint64_t*>(&mine), words,
                              reinterpret_cast<uint64_t*>(h.data())) != 0)
             return fail(WSMC_ERCCL, "host record exchange failed");
         WSMC_HIP(hipMemcpyAsync(recs, h.data(), sizeof(ShardRecord) * c->world, hipMemcpyHostToDevice, c->stream));
@@ -1164,6 +1173,7 @@ static int exchange_recs(wsmc_ctx* c, ShardRecord* recs) {
         return WSMC_OK;
     }
     WSMC_RCCL_GUARD(c);
+    c->exchanges += 1;
     WSMC_RCCL(ncclAllGather(recs + c->rank, recs, words, ncclUint64, c->comm, c->stream));
     return WSMC_OK;
 }
@@ -1289,7 +1299,7 @@ static int exact_route(wsmc_ctx* c, const ExactPlan& x, const std::vector<const 
             if (S) WSMC_HIP(hipMemcpyAsync(mine.data(), sendbuf, sizeof(unsigned long long) * S, hipMemcpyDeviceToHost,
                                            c->stream));
             WSMC_HIP(ctx_sync(c, c->stream));
-            if (c->host_exchange(c->host_user, reinterpret_cast<const uint64_t*>(mine.data()), (int32_t)maxS,
+            if (host_xchg(c, reinterpret_cast<const uint64_t*>(mine.data()), (int32_t)maxS,
                                  reinterpret_cast<uint64_t*>(all.data())) != 0)
                 return fail(WSMC_ERCCL, "host particle exchange failed");
             std::vector<unsigned long long> rv((size_t)R + 1);
@@ -1307,6 +1317,7 @@ static int exact_route(wsmc_ctx* c, const ExactPlan& x, const std::vector<const 
         }
     } else {
         WSMC_RCCL_GUARD(c);
+        c->exchanges += 1;
         WSMC_RCCL(ncclGroupStart());
         for (int r = 0; r < W; ++r) {
             if (r == me) continue;
@@ -1455,7 +1466,7 @@ static int trace_level(wsmc_ctx* c, const ExactPlan& x, const double* hist, cons
             if (S) WSMC_HIP(hipMemcpyAsync(mine.data(), sendbuf, sizeof(unsigned long long) * S, hipMemcpyDeviceToHost,
                                            c->stream));
             WSMC_HIP(ctx_sync(c, c->stream));
-            if (c->host_exchange(c->host_user, reinterpret_cast<const uint64_t*>(mine.data()), (int32_t)maxS,
+            if (host_xchg(c, reinterpret_cast<const uint64_t*>(mine.data()), (int32_t)maxS,
                                  reinterpret_cast<uint64_t*>(all.data())) != 0)
                 return fail(WSMC_ERCCL, "host trace-back exchange failed");
             for (int g = 0; g < W; ++g) {
@@ -1473,6 +1484,7 @@ static int trace_level(wsmc_ctx* c, const ExactPlan& x, const double* hist, cons
         }
     } else {
         WSMC_RCCL_GUARD(c);
+        c->exchanges += 1;
         WSMC_RCCL(ncclGroupStart());
         for (int r = 0; r < W; ++r) {
             if (r == me) continue;
@@ -3720,7 +3732,7 @@ static int exchange_neighbors(wsmc_ctx* c, unsigned long long* const send[2], un
             WSMC_HIP(hipMemcpyAsync(mine.data() + n, send[1] + at, sizeof(unsigned long long) * n,
                                     hipMemcpyDeviceToHost, s));
             WSMC_HIP(ctx_sync(c, s));
-            if (c->host_exchange(c->host_user, reinterpret_cast<const uint64_t*>(mine.data()), (int32_t)(2 * n),
+            if (host_xchg(c, reinterpret_cast<const uint64_t*>(mine.data()), (int32_t)(2 * n),
                                  reinterpret_cast<uint64_t*>(all.data())) != 0)
                 return fail(WSMC_ERCCL, "host neighbour exchange failed");
             if (me > 0)   // the left rank's right block
@@ -3734,7 +3746,8 @@ static int exchange_neighbors(wsmc_ctx* c, unsigned long long* const send[2], un
         return WSMC_OK;
     }
     WSMC_RCCL_GUARD(c);
-    WSMC_RCCL(ncclGroupStart());
+    c->exchanges += 1;
+        WSMC_RCCL(ncclGroupStart());
     if (me > 0) {
         WSMC_RCCL(ncclSend(send[0], (size_t)words, ncclUint64, me - 1, c->comm, s));
         WSMC_RCCL(ncclRecv(recv[0], (size_t)words, ncclUint64, me - 1, c->comm, s));
@@ -3752,7 +3765,13 @@ static int exchange_neighbors(wsmc_ctx* c, unsigned long long* const send[2], un
 // ranks see), so their fixed-size collectives match
 static void exact_sizes(const wsmc_ctx* c, int64_t* cap, int64_t* ctr) {
     const int64_t nmin = c->gN / c->world;   // the smallest (ragged) shard
-    int64_t cp = c->x_cap ? c->x_cap : std::max<int64_t>(1024, nmin / 256);
+    // the default block: a shard's slot window moves by the weight mass its particles hold
+    // beyond their share, which grows like sqrt(n) (C4's 2 x 1M forced run needed 6.2k slots;
+    // the blocks a run settles at after a first overflow were 4x that): 16 sqrt(n), so a first
+    // run at that shape does not overflow and re-run eagerly, at most half a shard
+    int64_t cdef = 1024;
+    while (cdef * cdef < 256 * nmin && 2 * cdef <= nmin) cdef *= 2;
+    int64_t cp = c->x_cap ? c->x_cap : cdef;
     int64_t ct = c->x_ctr ? c->x_ctr : std::max<int64_t>(1024, nmin / 128);
     *cap = std::max<int64_t>(1, std::min(cp, nmin));
     *ctr = std::max<int64_t>(1, std::min(ct, nmin));
@@ -4524,7 +4543,8 @@ int wsmc_debug_inject_failure(wsmc_ctx* c, int32_t shard, int32_t nth) {
     if (c && c->multi) return multi_inject_failure(c, shard, nth);
     if (!c) return fail(WSMC_EARG, "null context");
     if (shard != 0 || nth < 0) return fail(WSMC_EARG, "bad shard or count");
-    c->inject_fail = nth;
+    c->inject_earg = nth >= 1000;
+    c->inject_fail = nth >= 1000 ? nth - 1000 : nth;
     return WSMC_OK;
 }
 

@@ -153,6 +153,8 @@ struct wsmc_ctx {
     bool host_inproc = false;                   // ... between threads of this process (a multi-device
                                                 // handle's: a memcpy), not a caller's transport
     int32_t inject_fail = 0;                    // wsmc_debug_inject_failure: fail the nth next record exchange
+    bool inject_earg = false;                   // ... as WSMC_EARG (nth >= 1000) instead of WSMC_EHIP
+    int64_t exchanges = 0;                      // exchanges (collectives / host rendezvous) issued so far
     unsigned long long* run_grp = nullptr;      // [T+1][ngroups][kGroupLine] fused-run group sums
     // Move score cache: each particle's fold over the first scache_terms tape terms (its
     // score after its last move); -1 = invalid (a column the tape reads was rewritten)

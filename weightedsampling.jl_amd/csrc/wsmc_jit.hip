@@ -23,6 +23,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "wsmc_ew_body.h"
 #include "wsmc_internal.h"
@@ -176,14 +177,13 @@ std::string tu_source(const std::string& sig) {
 // compile a translation unit for `arch` (the code object in `code`)
 bool compile_src(const std::string& arch, const std::string& src, std::string& code, std::string& err) {
     const int nh = (int)(sizeof(kJitHeaders) / sizeof(kJitHeaders[0]));
-    const char* htext[8];
-    const char* hname[8];
+    std::vector<const char*> htext(nh), hname(nh);   // sized from the generated list (build.py JIT_HEADERS)
     for (int k = 0; k < nh; ++k) {
         htext[k] = kJitHeaders[k].text;
         hname[k] = kJitHeaders[k].name;
     }
     hiprtcProgram prog;
-    if (hiprtcCreateProgram(&prog, src.c_str(), "wsmc_ew_jit.hip", nh, htext, hname) != HIPRTC_SUCCESS) {
+    if (hiprtcCreateProgram(&prog, src.c_str(), "wsmc_ew_jit.hip", nh, htext.data(), hname.data()) != HIPRTC_SUCCESS) {
         err = "hiprtcCreateProgram failed";
         return false;
     }

@@ -102,25 +102,7 @@ __device__ __forceinline__ double block_sum_canon(double v, double* lds4) {
     __syncthreads();
     return r;
 }
-// block_sum_canon of NV values at once: the same butterfly and wave order per value (the same
-// bits), their shuffles interleaved and one barrier pair for all of them; lds [NV][4]
-template <int NV>
-__device__ __forceinline__ void block_sum_canon_n(const double (&v)[NV], double (*lds)[4], double (&out)[NV]) {
-    double x[NV];
-#pragma unroll
-    for (int k = 0; k < NV; ++k) x[k] = v[k];
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1)
-#pragma unroll
-        for (int k = 0; k < NV; ++k) x[k] = x[k] + __shfl_xor(x[k], off, 64);
-    if ((threadIdx.x & 63) == 0)
-#pragma unroll
-        for (int k = 0; k < NV; ++k) lds[k][threadIdx.x >> 6] = x[k];
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < NV; ++k) out[k] = (lds[k][0] + lds[k][1]) + (lds[k][2] + lds[k][3]);
-    __syncthreads();
-}
+// block_sum_canon_n (NV values at once): csrc/wsmc_mv_body.h, shared with the compiled Move blocks
 __device__ __forceinline__ u64 block_sum_u64(u64 v, u64* lds4) {
     v = wave_sum_u64(v);
     if ((threadIdx.x & 63) == 0) lds4[threadIdx.x >> 6] = v;
@@ -2284,8 +2266,8 @@ __global__ __launch_bounds__(kBlock) void k_moments1(const double* __restrict__ 
     // the Move block's flag words and accepted counters, zeroed here rather than by two memset
     // launches (the combine and the Move kernel, which use them, run after this kernel)
     if (blockIdx.x == 0 && threadIdx.x < 4) {
-        if (z.flag) z.flag[threadIdx.x] = 0;
         if (z.count) z.count[threadIdx.x] = 0;
+        if (z.flag) z.flag[threadIdx.x] = 0;
     }
     if (gate && !gate->resampled) return;   // a gated Move that does not run
     const double M = wave_slots_max(ms);

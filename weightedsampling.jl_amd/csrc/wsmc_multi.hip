@@ -75,7 +75,13 @@ struct MultiState {
 
 // seconds a shard that met a symmetric error waits for its peers before requesting the abort
 constexpr double kPeerWaitS = 30.0;
-static bool symmetric_error(int code) { return code == WSMC_EARG || code == WSMC_ENOTPD; }
+// errors every shard meets at the same point: an argument error before the call's first
+// exchange (validation, the same arguments on every shard), and a not-PD autoRW covariance (it
+// is factored from all-gathered totals, so every shard computes the same); anything else a shard
+// meets alone — an argument error past an exchange included — requests the abort at once
+static bool symmetric_error(const wsmc_ctx* s, int code) {
+    return code == WSMC_ENOTPD || (code == WSMC_EARG && s->exchanges == 0);
+}
 
 static void worker_loop(Worker* w) {
     for (;;) {
@@ -107,13 +113,14 @@ static void request_abort(MultiState* M) {
 
 // shard g is back from its call with code rc
 static void shard_done(MultiState* M, int g, int rc) {
-    if (rc && !symmetric_error(rc) && M->G > 1) request_abort(M);   // one shard: no peer waits for it
+    const bool sym = symmetric_error(M->sub[g], rc);
+    if (rc && !sym && M->G > 1) request_abort(M);   // one shard: no peer waits for it
     bool wait_peers = false;
     {
         std::lock_guard<std::mutex> lk(M->xm);
         M->finished += 1;
         M->xcv.notify_all();
-        wait_peers = rc && symmetric_error(rc) && M->G > 1;
+        wait_peers = rc && sym && M->G > 1;
     }
     if (!wait_peers) return;
     // every shard should meet the same error at the same point: wait for them, and abort the
@@ -138,7 +145,10 @@ static int run_all(MultiState* M, const std::function<int(int, wsmc_ctx*)>& fn) 
         M->arrived = M->departed = 0;
         M->finished = 0;
     }
-    for (auto* s : M->sub) s->released = false;
+    for (auto* s : M->sub) {
+        s->released = false;
+        s->exchanges = 0;   // this call's exchanges
+    }
     std::vector<int> rc(M->G, 0);
     std::vector<std::string> msg(M->G);
     for (int g = 1; g < M->G; ++g) {
@@ -372,7 +382,8 @@ int multi_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d,
 int multi_inject_failure(wsmc_ctx* c, int32_t shard, int32_t nth) {
     MultiState* M = c->multi;
     if (shard < 0 || shard >= M->G || nth < 0) return fail(WSMC_EARG, "bad shard or count");
-    M->sub[shard]->inject_fail = nth;
+    M->sub[shard]->inject_earg = nth >= 1000;
+    M->sub[shard]->inject_fail = nth >= 1000 ? nth - 1000 : nth;
     return WSMC_OK;
 }
 

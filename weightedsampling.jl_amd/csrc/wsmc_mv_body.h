@@ -67,6 +67,27 @@ struct MvArgs {
     const char* prog;         // the program in device memory, or null: in the kernel arguments
 };
 
+// canonical f64 block sum of NV values at once (256 threads): an xor butterfly 1..32 inside each
+// wave, then (w0 + w1) + (w2 + w3), every value in the same order (the autoRW moments' tile and
+// combine order, oracle/wsmc_oracle.c canon_block); lds [NV][4]
+template <int NV>
+__device__ __forceinline__ void block_sum_canon_n(const double (&v)[NV], double (*lds)[4], double (&out)[NV]) {
+    double x[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) x[k] = v[k];
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) x[k] = x[k] + __shfl_xor(x[k], off, 64);
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) lds[k][threadIdx.x >> 6] = x[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NV; ++k) out[k] = (lds[k][0] + lds[k][1]) + (lds[k][2] + lds[k][3]);
+    __syncthreads();
+}
+
 __device__ __forceinline__ unsigned long long mv_block_sum(unsigned long long v, unsigned long long* lds4) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

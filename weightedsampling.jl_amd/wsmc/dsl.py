@@ -27,11 +27,23 @@ from .abi import Dist, Operand
 Number = Union[int, float]
 
 
+def _pow2(k: float) -> bool:
+    m, _ = math.frexp(k)
+    return k != 0.0 and math.isfinite(k) and abs(m) == 0.5
+
+
 @dataclass(frozen=True)
 class Expr:
-    """c0 + sum coef * column[comp] over at most two (column, component) pairs."""
+    """c0 + sum coef * column[comp] over at most two (column, component) pairs — the operand form,
+    evaluated as (c0 + coef0 x0) + coef1 x1 (include/wsmc_terms.h wsmc_operand_eval). While that
+    order rounds exactly as the user's own operations (Julia's broadcast) `fx` is None; an
+    operation that would round differently in the merged form (a constant added after two terms,
+    a sum scaled by a non power of two, ...) records the user's order in `fx`, and a program
+    (wsmc_assign_expr) evaluates that instead. A distribution argument always takes the operand
+    form (its value then within a rounding of the broadcast's)."""
     c0: float = 0.0
     terms: tuple = ()   # ((name, comp, coef), ...)
+    fx: object = field(default=None, compare=False)
 
     @staticmethod
     def lift(v) -> "Expr":
@@ -44,18 +56,35 @@ class Expr:
                             "operand form); assign the general expression to a column first")
         raise TypeError(f"cannot use {v!r} as a particle argument")
 
-    def __add__(self, o):
-        if isinstance(o, Fx):
-            return Fx.lift(self) + o
-        o = Expr.lift(o)
-        if len(self.terms) + len(o.terms) > 2:   # beyond the operand form: a general expression
-            return Fx.lift(self) + Fx.lift(o)
-        return Expr(self.c0 + o.c0, self.terms + o.terms)
+    def _sum_exact(self, o: "Expr") -> bool:
+        """(self) + (o) rounds as the merged operand form does (signed zeros aside)"""
+        if self.fx is not None or o.fx is not None:
+            return False
+        na, nb = len(self.terms), len(o.terms)
+        if nb == 0:
+            return o.c0 == 0.0 or (self.c0 == 0.0 and na <= 1)
+        if na == 0:
+            return self.c0 == 0.0 or (o.c0 == 0.0 and nb <= 1)
+        return o.c0 == 0.0
 
-    __radd__ = __add__
+    def __add__(self, o, swap=False):
+        if isinstance(o, Fx):
+            return o + Fx.lift(self) if swap else Fx.lift(self) + o
+        o = Expr.lift(o)
+        a, b = (o, self) if swap else (self, o)
+        if len(a.terms) + len(b.terms) > 2:   # beyond the operand form: a general expression
+            return Fx.lift(a) + Fx.lift(b)
+        merged = Expr(a.c0 + b.c0, a.terms + b.terms)
+        if a._sum_exact(b):
+            return merged
+        return Expr(merged.c0, merged.terms, Fx(abi.X_ADD, (Fx.lift(a), Fx.lift(b))))
+
+    def __radd__(self, o):
+        return self.__add__(o, swap=True)
 
     def __neg__(self):
-        return Expr(-self.c0, tuple((n, c, -k) for n, c, k in self.terms))
+        return Expr(-self.c0, tuple((n, c, -k) for n, c, k in self.terms),
+                    None if self.fx is None else -self.fx)
 
     def __sub__(self, o):
         if isinstance(o, Fx):
@@ -63,7 +92,7 @@ class Expr:
         return self + (-Expr.lift(o))
 
     def __rsub__(self, o):
-        return Expr.lift(o) + (-self)
+        return Expr.lift(o) + (-self)   # a - b is a + (-b) exactly
 
     # the non-affine operators give general expressions (Assign only: wsmc_assign_expr)
     def __truediv__(self, o):
@@ -104,7 +133,13 @@ class Expr:
             else:   # a product of two particle columns: a general expression
                 return Fx.lift(self) * Fx.lift(k)
         k = float(k)
-        return Expr(self.c0 * k, tuple((n, c, coef * k) for n, c, coef in self.terms))
+        scaled = Expr(self.c0 * k, tuple((n, c, coef * k) for n, c, coef in self.terms))
+        # k (c0 + coef x + ...) distributes exactly for a constant, k = +-2^n, or k * x alone
+        exact = self.fx is None and (not self.terms or _pow2(k) or
+                                     (len(self.terms) == 1 and self.c0 == 0.0 and self.terms[0][2] == 1.0))
+        if exact:
+            return scaled
+        return Expr(scaled.c0, scaled.terms, Fx(abi.X_MUL, (Fx.lift(self), Fx(abi.X_CONST, c=k))))
 
     __rmul__ = __mul__
 
@@ -312,16 +347,19 @@ class Fx:
         if isinstance(v, (int, float, np.floating, np.integer)):
             return Fx(abi.X_CONST, c=float(v))
         if isinstance(v, Expr):
-            # the affine form's terms in order (x, coef * x, -x), its constant last when nonzero
-            e = None
+            if v.fx is not None:   # the user's order (the merged form would round differently)
+                return v.fx
+            # the affine form in wsmc_operand_eval's order: its constant first when nonzero, then
+            # the terms left to right (x, coef * x, -x), ((c0 + t0) + t1): the user's own order
+            # whenever fx is None (Expr._sum_exact), so the value is the same bits as an operand
+            # or inside a program
+            e = Fx(abi.X_CONST, c=v.c0) if v.c0 != 0.0 else None
             for name, comp, coef in v.terms:
                 x = Fx(abi.X_COL, col=name, comp=comp)
                 t = x if coef == 1.0 else (Fx(abi.X_NEG, (x,)) if coef == -1.0 else
                                            Fx(abi.X_MUL, (Fx(abi.X_CONST, c=coef), x)))
                 e = t if e is None else Fx(abi.X_ADD, (e, t))
-            if e is None:
-                return Fx(abi.X_CONST, c=v.c0)
-            return Fx(abi.X_ADD, (e, Fx(abi.X_CONST, c=v.c0))) if v.c0 != 0.0 else e
+            return e if e is not None else Fx(abi.X_CONST, c=v.c0)
         raise TypeError(f"cannot use {v!r} in a particle expression")
 
     def _bin(self, op, o, swap=False):
