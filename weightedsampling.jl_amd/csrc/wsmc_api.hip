@@ -725,6 +725,8 @@ int wsmc_destroy(wsmc_ctx* c) {
     for (int32_t* p : c->lineage)
         if (p) (void)hipFree(p);
     if (c->pinned) (void)hipHostFree(c->pinned);
+    for (auto& sl : c->prog_slots)
+        if (sl.dev) (void)hipFree(sl.dev);
     if (c->prog_stage) (void)hipHostFree(c->prog_stage);
     delete c->ew;   // statements never launched: the context goes with them
     if (c->dec_ring) (void)hipHostFree(c->dec_ring);
@@ -2826,6 +2828,39 @@ static int32_t compile_fold(const std::vector<wsmc_term>& ct, int32_t j0, int32_
     return (int32_t)(segs.size() - s0);
 }
 
+// the device copy of a fold program written at hp (prog_bytes, `need` bytes of the staging ring):
+// a content hit in the context's few program slots uploads nothing (and returns the ring space),
+// a miss copies into the least recently used slot
+static int prog_device(wsmc_ctx* c, const char* hp, size_t prog_bytes, int64_t need, char** dev) {
+    const uint64_t tick = ++c->prog_tick;
+    for (auto& sl : c->prog_slots)
+        if (sl.dev && sl.host.size() == prog_bytes && std::memcmp(sl.host.data(), hp, prog_bytes) == 0) {
+            sl.used = tick;
+            c->prog_stage_at -= need;   // the staged bytes are not needed (nothing was enqueued from them)
+            c->prog_hits += 1;
+            *dev = reinterpret_cast<char*>(sl.dev);
+            return WSMC_OK;
+        }
+    wsmc_ctx::ProgSlot* v = &c->prog_slots[0];
+    for (auto& sl : c->prog_slots)
+        if (sl.used < v->used) v = &sl;
+    if ((int64_t)prog_bytes > v->cap) {
+        int64_t cap = v->cap ? v->cap : 4096;
+        while (cap < (int64_t)prog_bytes) cap *= 2;
+        WSMC_HIP(ctx_sync(c, c->stream));   // launches still reading the slot
+        if (v->dev) WSMC_HIP(hipFree(v->dev));
+        v->dev = nullptr;
+        WSMC_HIP(hipMalloc(&v->dev, cap));
+        v->cap = cap;
+    }
+    WSMC_HIP(hipMemcpyAsync(v->dev, hp, prog_bytes, hipMemcpyHostToDevice, c->stream));
+    v->host.assign(hp, hp + prog_bytes);
+    v->used = tick;
+    c->prog_uploads += 1;
+    *dev = reinterpret_cast<char*>(v->dev);
+    return WSMC_OK;
+}
+
 static int move_block_fused(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, int32_t gated,
                             int64_t* accepted_out, bool* done);
 // WSMC_DIAG_NO_BLOCK1=1: single Moves keep their own kernels (k_move_c / k_move_ci), for comparison
@@ -3021,6 +3056,7 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         const bool inl = !no_inline && lean && prog_bytes <= sizeof(ProgInline::w);
         ProgInline pin;
         char* hp = nullptr;
+        int64_t need = 0;
         if (inl) {
             hp = reinterpret_cast<char*>(pin.w);
             pin.seg_off = (int32_t)ct_bytes;
@@ -3028,15 +3064,7 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
             pin.seg_old0 = seg_old0;
             pin.pad = 0;
         } else {
-            if ((int64_t)prog_bytes > c->d_prog_cap) {
-                int64_t cap = c->d_prog_cap ? c->d_prog_cap : 4096;
-                while (cap < (int64_t)prog_bytes) cap *= 2;
-                WSMC_HIP(ctx_sync(c, c->stream));
-                if (c->d_prog) WSMC_HIP(hipFree(c->d_prog));
-                WSMC_HIP(hipMalloc(&c->d_prog, cap));
-                c->d_prog_cap = cap;
-            }
-            const int64_t need = ((int64_t)prog_bytes + 255) & ~(int64_t)255;
+            need = ((int64_t)prog_bytes + 255) & ~(int64_t)255;
             if (c->prog_stage_at + need > c->prog_stage_cap) {   // wrap: the ring's copies are done
                 WSMC_HIP(ctx_sync(c, c->stream));
                 c->prog_stage_at = 0;
@@ -3054,9 +3082,8 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         if (!tmpls.empty()) std::memcpy(hp, tmpls.data(), ct_bytes);
         if (seg_bytes) std::memcpy(hp + ct_bytes, segs.data(), seg_bytes);
         if (!cst.empty()) std::memcpy(hp + ct_bytes + seg_bytes, cst.data(), sizeof(double) * cst.size());
-        if (!inl && prog_bytes)
-            WSMC_HIP(hipMemcpyAsync(c->d_prog, hp, prog_bytes, hipMemcpyHostToDevice, c->stream));
-        char* pbase = reinterpret_cast<char*>(c->d_prog);
+        char* pbase = nullptr;
+        if (!inl && prog_bytes && (r = prog_device(c, hp, prog_bytes, need, &pbase))) return r;
         const wsmc_term* d_ct = reinterpret_cast<const wsmc_term*>(pbase);
         FoldProgram prog;
         prog.seg_new = reinterpret_cast<const FoldSeg*>(pbase + ct_bytes);
@@ -3438,6 +3465,7 @@ static int move_block_fused(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs,
     ProgInlineBlk pin;
     const bool inl = prog_bytes <= sizeof(ProgInlineBlk::w);
     char* hp;
+    int64_t need = 0;
     if (inl) {
         hp = reinterpret_cast<char*>(pin.w);
         pin.seg_off = (int32_t)ct_bytes;
@@ -3445,15 +3473,7 @@ static int move_block_fused(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs,
         pin.seg_old0 = seg_old0;
         pin.pad = 0;
     } else {
-        if ((int64_t)prog_bytes > c->d_prog_cap) {
-            int64_t cap = c->d_prog_cap ? c->d_prog_cap : 4096;
-            while (cap < (int64_t)prog_bytes) cap *= 2;
-            WSMC_HIP(ctx_sync(c, c->stream));
-            if (c->d_prog) WSMC_HIP(hipFree(c->d_prog));
-            WSMC_HIP(hipMalloc(&c->d_prog, cap));
-            c->d_prog_cap = cap;
-        }
-        const int64_t need = ((int64_t)prog_bytes + 255) & ~(int64_t)255;
+        need = ((int64_t)prog_bytes + 255) & ~(int64_t)255;
         if (c->prog_stage_at + need > c->prog_stage_cap) {
             WSMC_HIP(ctx_sync(c, c->stream));
             c->prog_stage_at = 0;
@@ -3471,8 +3491,8 @@ static int move_block_fused(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs,
     if (!tmpls.empty()) std::memcpy(hp, tmpls.data(), ct_bytes);
     if (seg_bytes) std::memcpy(hp + ct_bytes, segs.data(), seg_bytes);
     if (!cst.empty()) std::memcpy(hp + ct_bytes + seg_bytes, cst.data(), sizeof(double) * cst.size());
-    if (!inl) WSMC_HIP(hipMemcpyAsync(c->d_prog, hp, prog_bytes, hipMemcpyHostToDevice, c->stream));
-    char* pbase = reinterpret_cast<char*>(c->d_prog);
+    char* pbase = nullptr;
+    if (!inl && (r = prog_device(c, hp, prog_bytes, need, &pbase))) return r;
     FoldProgram prog;
     prog.seg_new = inl ? nullptr : reinterpret_cast<const FoldSeg*>(pbase + ct_bytes);
     prog.seg_old = inl ? nullptr : prog.seg_new + seg_old0;

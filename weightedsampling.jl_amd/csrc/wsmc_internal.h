@@ -233,6 +233,17 @@ struct wsmc_ctx {
     int64_t d_ctape_cap = 0;
     void* d_prog = nullptr;                 // compiled fold program: segments, then constants
     int64_t d_prog_cap = 0;                 // bytes
+    // device copies of the last few fold programs, keyed by content: a sweep alternates a few
+    // programs (C5's two Moves repeat theirs five times a step), so most Moves upload nothing
+    struct ProgSlot {
+        std::vector<char> host;             // the bytes the device copy holds
+        void* dev = nullptr;
+        int64_t cap = 0;
+        uint64_t used = 0;                  // LRU stamp
+    };
+    ProgSlot prog_slots[4];
+    uint64_t prog_tick = 0;
+    int64_t prog_uploads = 0, prog_hits = 0;
     wsmc::EwBatch* ew = nullptr;            // elementwise statements not launched yet (one kernel at
     unsigned ew_feat = 0;                   // the next other entry point); the oscillator mean seen
     std::vector<int32_t> ew_lag;            // columns the batch reads one Resample behind

@@ -523,7 +523,7 @@ __device__ __forceinline__ u64 qacc_tile(QAcc a, double (*s_f)[NB / 64], u64* ou
 // Weight statistics of one 1024-particle tile (256 threads x 4 particles, coalesced):
 // q (stored for the fill) and the tile partials of qacc_tile.
 // MODE (diagnostics only; production = 0): 1 = no exp, 4 = load/store only.
-template <int MODE>
+template <int MODE, bool MULTI = false>
 __global__ __launch_bounds__(kSumBlock) void k_rs_sums_t(const double* __restrict__ w, int64_t N,
                                                          const MaxSlots* __restrict__ ms, u64* __restrict__ tilep,
                                                          u64* __restrict__ qbuf, u64* __restrict__ grp, int G,
@@ -532,13 +532,20 @@ __global__ __launch_bounds__(kSumBlock) void k_rs_sums_t(const double* __restric
     __shared__ double s_f[kPart][kSumBlock / 64];
     const int th = threadIdx.x;
     const int64_t base = (int64_t)blockIdx.x * kRsTile;
+    u64 mv = MODE == 4 ? 0ull : ms[0].v[th & 63][0];
     double lw[IT];
 #pragma unroll
     for (int k = 0; k < IT; ++k) {
         const int64_t i = base + (int64_t)k * kSumBlock + th;
         lw[k] = i < N ? w[i] : -WSMC_INF;
     }
-    const double M = MODE == 4 ? 0.0 : wave_slots_max_n(ms, nms);
+    if (MULTI)   // exact shards: every rank's slots (a separate instance: the loop's loads would
+                 // make the single-rank path wait for the weights' loads too)
+        for (int g = 1; g < nms; ++g) {
+            const u64 v = ms[g].v[th & 63][0];
+            mv = v > mv ? v : mv;
+        }
+    const double M = MODE == 4 ? 0.0 : wsmc_ord_dec(wave_max_u64(mv));
     const double sK = wsmc_pow2i(wsmc_qbits((uint64_t)Nk));   // Nk: the global N when exact-sharded
     QAcc acc;
 #pragma unroll
@@ -3555,6 +3562,9 @@ hipError_t launch_rs_max(hipStream_t s, const double* w, int64_t N, MaxSlots* ms
 }
 hipError_t launch_rs_sums(hipStream_t s, const double* w, int64_t N, const MaxSlots* ms, u64* tilep, u64* qbuf,
                           hipEvent_t e0, hipEvent_t e1, u64* grp, int G, int64_t Nk, int nms, int gall) {
+    if (nms > 1)
+        return launch_timed(k_rs_sums_t<0, true>, rs_tiles_for(N), dim3(kSumBlock), s, e0, e1, w, N, ms, tilep, qbuf,
+                            grp, G, Nk > 0 ? Nk : N, nms, gall);
     return launch_timed(k_rs_sums_t<0>, rs_tiles_for(N), dim3(kSumBlock), s, e0, e1, w, N, ms, tilep, qbuf, grp, G,
                         Nk > 0 ? Nk : N, nms, gall);
 }
