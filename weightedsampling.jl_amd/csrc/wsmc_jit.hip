@@ -65,6 +65,21 @@ bool jit_off() {
     }();
     return v;
 }
+// diagnostics: WSMC_JIT_DUMP=<dir> writes each compiled code object (<dir>/<kind>_<n>.co) and its
+// signature (<dir>/<kind>_<n>.sig), for the ISA and register counts of the run-time kernels
+void jit_dump(const char* kind, int64_t n, const std::string& key, const std::string& code) {
+    const char* d = getenv("WSMC_JIT_DUMP");
+    if (!d || !*d) return;
+    const std::string base = std::string(d) + "/" + kind + "_" + std::to_string(n);
+    if (FILE* f = fopen((base + ".co").c_str(), "wb")) {
+        fwrite(code.data(), 1, code.size(), f);
+        fclose(f);
+    }
+    if (FILE* f = fopen((base + ".sig").c_str(), "w")) {
+        fwrite(key.data(), 1, key.size(), f);
+        fclose(f);
+    }
+}
 bool jit_verbose() {
     static const bool v = [] {
         const char* e = getenv("WSMC_JIT_VERBOSE");
@@ -442,6 +457,7 @@ hipError_t launch_mv_jit(hipStream_t s, const MvSig& sig, const ProgInlineBlk* p
             const auto t0 = std::chrono::steady_clock::now();
             k.ok = device_arch(device, arch, err) && compile_src(arch, mv_tu(key.substr(3)), code, err) &&
                    load_module(device, code, "wsmc_mv_i", "wsmc_mv_g", k, err);
+            if (k.ok) jit_dump("mv", C.mv_compiled, key, code);
             const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
             C.mv_compile_s += dt;
             if (k.ok) {
