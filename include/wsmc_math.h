@@ -618,12 +618,21 @@ WSMC_HD uint32_t wsmc_strat_word(uint64_t seed, uint64_t op, uint64_t n) {
 /* ------------------------------------------------------------------------- */
 /* log-densities (Distributions.jl semantics)                                 */
 /* ------------------------------------------------------------------------- */
-/* Normal(mu, sigma): -(z^2 + log(2pi))/2 - log(sigma),  z = (x - mu)/sigma     */
+/* Normal(mu, sigma): -(z^2 + log(2pi))/2 - log(sigma),  z = (x - mu)/sigma
+ * evaluated as fma(-h, h, c) with h = (x - mu) rh: per sigma value the pair
+ *   c  = -log(2pi)/2 - log(sigma)   (wsmc_normal_c)
+ *   rh = (1/sigma) / sqrt(2)        (wsmc_normal_rh)
+ * (one log and one reciprocal per sigma value, reused across the terms of a fold that share it:
+ * wsmc_scale_memo, or the host's wsmc_scale_pre), then per term a subtraction, a multiply and an
+ * fma — -(z^2)/2 = -h^2 within a few ulps of z^2, rounded once into c. Five roundings per term
+ * were a Move fold's dominant cost (the oscillator runs of examples/damped_oscillator.jl). */
+#define WSMC_SQRT1_2 0.70710678118654752440
+WSMC_HD double wsmc_normal_c(double lg) { return (-0.5 * WSMC_LOG2PI) - lg; }
+WSMC_HD double wsmc_normal_rh(double rc) { return rc * WSMC_SQRT1_2; }
+WSMC_HD double wsmc_normal_lh(double h, double c) { return __builtin_fma(-h, h, c); }
 WSMC_HD double wsmc_normal_logpdf(double mu, double sigma, double x) {
-    /* z = (x - mu) * (1 / sigma): one reciprocal per sigma value, reused across the terms of
-       a fold that share it (wsmc_scale_memo) — a multiply per term where a division was */
-    double z = (x - mu) * (1.0 / sigma);
-    return -(z * z + WSMC_LOG2PI) * 0.5 - wsmc_log(sigma);
+    const double h = (x - mu) * wsmc_normal_rh(1.0 / sigma);
+    return wsmc_normal_lh(h, wsmc_normal_c(wsmc_log(sigma)));
 }
 /* Truncated(Normal(0, sigma), 0, Inf) — examples/damped_oscillator.jl:24-28 */
 WSMC_HD double wsmc_halfnormal_logpdf(double sigma, double x) {

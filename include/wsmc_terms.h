@@ -327,8 +327,7 @@ WSMC_HD double wsmc_ext_logpdf(int fam, double x, double m, double s, wsmc_logme
             const double lx = wsmc_log(x);
             double lg, rc;
             wsmc_scale_memo(lm, s, &lg, &rc);
-            const double z = (lx - m) * rc;
-            return (-(z * z + WSMC_LOG2PI) * 0.5 - lg) - lx;
+            return wsmc_normal_lh((lx - m) * wsmc_normal_rh(rc), wsmc_normal_c(lg)) - lx;
         }
         case WSMC_FAM_LAPLACE:   /* -(|x - μ| / θ + log(2θ)) */
             return -(wsmc_fabs(x - m) / s + wsmc_log(2.0 * s));
@@ -394,16 +393,14 @@ WSMC_HD double wsmc_dist_logpdf_mf(const wsmc_dist* d, const double* x, double* 
             double sg = wsmc_operand_eval(&d->scale, cols, N, i, ov);
             double lg, rc;
             wsmc_scale_memo(lm, sg, &lg, &rc);
-            double z = (x[0] - mu) * rc;
-            return -(z * z + WSMC_LOG2PI) * 0.5 - lg;
+            return wsmc_normal_lh((x[0] - mu) * wsmc_normal_rh(rc), wsmc_normal_c(lg));
         }
         case WSMC_FAM_HALFNORMAL: {   /* wsmc_halfnormal_logpdf likewise */
             double sg = wsmc_operand_eval(&d->scale, cols, N, i, ov);
             if (!(x[0] >= 0.0)) return -WSMC_INF;
             double lg, rc;
             wsmc_scale_memo(lm, sg, &lg, &rc);
-            double z = (x[0] - 0.0) * rc;
-            return (-(z * z + WSMC_LOG2PI) * 0.5 - lg) + WSMC_LOG2;
+            return wsmc_normal_lh((x[0] - 0.0) * wsmc_normal_rh(rc), wsmc_normal_c(lg)) + WSMC_LOG2;
         }
         case WSMC_FAM_UNIFORM:
             return wsmc_uniform_logpdf(d->param[0], d->param[1], x[0]);
@@ -544,35 +541,32 @@ WSMC_HD int wsmc_term_is_scalar(const wsmc_term* t) {
            (t->dist.family == WSMC_FAM_NORMAL || t->dist.family == WSMC_FAM_HALFNORMAL ||
             t->dist.family == WSMC_FAM_UNIFORM);
 }
-/* pre: for a constant scale operand, (log(sigma), 1/sigma) evaluated once by the caller (the
- * same functions of the same bits as wsmc_scale_memo's), else null */
+/* a Normal's per-sigma pair (c, rh) of wsmc_normal_logpdf through the fold's memo */
+WSMC_HD void wsmc_normal_scale(wsmc_logmemo* lm, double sigma, double* c, double* rh) {
+    double lg, rc;
+    wsmc_scale_memo(lm, sigma, &lg, &rc);
+    *c = wsmc_normal_c(lg);
+    *rh = wsmc_normal_rh(rc);
+}
+/* pre: for a constant scale operand, the pair (c, rh) evaluated once by the caller
+ * (wsmc_scale_pre: the same functions of the same bits as wsmc_normal_scale's), else null */
 WSMC_HD double wsmc_scalar_term_logpdf_p(const wsmc_term* t, double* const* cols, int64_t N, int64_t i,
                                          const wsmc_override* ov, wsmc_logmemo* lm, const double* pre) {
     const wsmc_dist* d = &t->dist;
     const double x0 = wsmc_operand_eval(&t->x[0], cols, N, i, ov);
-    if (d->family == WSMC_FAM_NORMAL) {
-        double mu = wsmc_operand_eval(&d->mu[0], cols, N, i, ov);
-        double lg, rc;
+    if (d->family == WSMC_FAM_NORMAL || d->family == WSMC_FAM_HALFNORMAL) {
+        const int half = d->family == WSMC_FAM_HALFNORMAL;
+        if (half && !(x0 >= 0.0)) return -WSMC_INF;
+        const double mu = half ? 0.0 : wsmc_operand_eval(&d->mu[0], cols, N, i, ov);
+        double c, rh;
         if (pre) {
-            lg = pre[0];
-            rc = pre[1];
+            c = pre[0];
+            rh = pre[1];
         } else {
-            wsmc_scale_memo(lm, wsmc_operand_eval(&d->scale, cols, N, i, ov), &lg, &rc);
+            wsmc_normal_scale(lm, wsmc_operand_eval(&d->scale, cols, N, i, ov), &c, &rh);
         }
-        double z = (x0 - mu) * rc;
-        return -(z * z + WSMC_LOG2PI) * 0.5 - lg;
-    }
-    if (d->family == WSMC_FAM_HALFNORMAL) {
-        if (!(x0 >= 0.0)) return -WSMC_INF;
-        double lg, rc;
-        if (pre) {
-            lg = pre[0];
-            rc = pre[1];
-        } else {
-            wsmc_scale_memo(lm, wsmc_operand_eval(&d->scale, cols, N, i, ov), &lg, &rc);
-        }
-        double z = (x0 - 0.0) * rc;
-        return (-(z * z + WSMC_LOG2PI) * 0.5 - lg) + WSMC_LOG2;
+        const double l = wsmc_normal_lh((x0 - mu) * rh, c);
+        return half ? l + WSMC_LOG2 : l;
     }
     return wsmc_uniform_logpdf(d->param[0], d->param[1], x0);
 }
@@ -580,10 +574,10 @@ WSMC_HD double wsmc_scalar_term_logpdf_m(const wsmc_term* t, double* const* cols
                                          const wsmc_override* ov, wsmc_logmemo* lm) {
     return wsmc_scalar_term_logpdf_p(t, cols, N, i, ov, lm, 0);
 }
-/* the (log(sigma), 1/sigma) pair of a constant scale (wsmc_scalar_term_logpdf_p's pre) */
+/* the (c, rh) pair of a constant scale (wsmc_scalar_term_logpdf_p's pre) */
 WSMC_HD void wsmc_scale_pre(double sigma, double* pre) {
-    pre[0] = wsmc_log(sigma);
-    pre[1] = 1.0 / sigma;
+    pre[0] = wsmc_normal_c(wsmc_log(sigma));
+    pre[1] = wsmc_normal_rh(1.0 / sigma);
 }
 
 WSMC_HD double wsmc_term_logpdf_mf(const wsmc_term* t, double* const* cols, int64_t N, int64_t i,

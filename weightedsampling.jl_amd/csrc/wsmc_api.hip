@@ -2810,18 +2810,43 @@ static int32_t compile_fold(const std::vector<wsmc_term>& ct, int32_t j0, int32_
             cst.push_back(pre[1]);
         }
         segs.push_back(FoldSeg{kind, e - j, j, (int32_t)cst.size(), soff, 0});
-        for (int32_t k = j; k < e; ++k) {
-            const wsmc_term& t = ct[k];
-            if (kind == kSegNormalOsc) {   // (t_a, d, m) of the term's rotation block
-                cst.push_back(t.dist.param[0]);
-                cst.push_back(t.dist.param[1]);
-                cst.push_back((double)t.dist.reserved);
-            } else {
+        if (kind == kSegNormalOsc) {
+            // rotation runs (wsmc_mv.h): a term continues the open run when it is the next
+            // rotation of the same block (m = m' + 1, the same t_a and step bits) — the
+            // continuation test of the term-by-term evaluation; any other term opens a run
+            // (anchor, m rotations)
+            size_t head = 0;
+            int32_t run_m = 0, run_n = 0;
+            for (int32_t k = j; k < e; ++k) {
+                const wsmc_term& t = ct[k];
+                const int32_t m = t.dist.reserved;
+                const bool next = run_n > 0 && m > 0 && m == run_m + run_n &&
+                                  same_bits(t.dist.param[0], cst[head]) &&
+                                  (run_n == 1 && run_m == 0 ? true : same_bits(t.dist.param[1], cst[head + 1]));
+                if (next) {
+                    if (run_n == 1 && run_m == 0) cst[head + 1] = t.dist.param[1];   // the block's step
+                    ++run_n;
+                    cst[head + 3] = osc_run_word(run_n);
+                } else {
+                    head = cst.size();
+                    run_m = m;
+                    run_n = 1;
+                    cst.push_back(t.dist.param[0]);
+                    cst.push_back(t.dist.param[1]);
+                    cst.push_back(osc_run_word(m));
+                    cst.push_back(osc_run_word(1));
+                }
+                cst.push_back(t.x[0].c0);
+            }
+            cst.push_back(0.0);   // the pad word: the device loads a run's next observation ahead
+        } else {
+            for (int32_t k = j; k < e; ++k) {
+                const wsmc_term& t = ct[k];
                 cst.push_back(t.dist.mu[0].c0);
                 cst.push_back(t.dist.mu[0].coef[0]);
                 cst.push_back(t.dist.mu[0].coef[1]);
+                cst.push_back(t.x[0].c0);
             }
-            cst.push_back(t.x[0].c0);
         }
         j = e;
     }

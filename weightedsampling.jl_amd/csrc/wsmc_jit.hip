@@ -423,16 +423,26 @@ std::string mv_sig_text(const MvSig& g) {
 
 // two entries: the program in the kernel arguments (read through the kernarg segment, scalar
 // loads) or in device memory; MvArgs after ProgInlineBlk at its own alignment
+// WSMC_DIAG_MV_WAVES=n: the blocks compiled for n waves a SIMD (amdgpu_waves_per_eu), for comparison
+std::string mv_waves_attr() {
+    static const std::string a = [] {
+        const char* e = getenv("WSMC_DIAG_MV_WAVES");
+        const int n = e ? atoi(e) : 0;
+        return n > 0 ? " __attribute__((amdgpu_waves_per_eu(" + std::to_string(n) + ")))" : std::string();
+    }();
+    return a;
+}
 std::string mv_tu(const std::string& sig) {
+    const std::string lb = "__launch_bounds__(256)" + mv_waves_attr();
     return "#include \"wsmc_mv_body.h\"\n"
            "struct WsmcMvSig { static constexpr wsmc::MvSig sig = " + sig + "; };\n"
            "constexpr unsigned kMvArgsAt = (sizeof(wsmc::ProgInlineBlk) + alignof(wsmc::MvArgs) - 1) & "
            "~(unsigned)(alignof(wsmc::MvArgs) - 1);\n"
-           "extern \"C\" __global__ __launch_bounds__(256) void wsmc_mv_i(wsmc::ProgInlineBlk, wsmc::MvArgs) {\n"
+           "extern \"C\" __global__ " + lb + " void wsmc_mv_i(wsmc::ProgInlineBlk, wsmc::MvArgs) {\n"
            "  const char* ka = (const char*)__builtin_amdgcn_kernarg_segment_ptr();\n"
            "  wsmc::mv_body<WsmcMvSig>(ka + __builtin_offsetof(wsmc::ProgInlineBlk, w), "
            "*reinterpret_cast<const wsmc::MvArgs*>(ka + kMvArgsAt));\n}\n"
-           "extern \"C\" __global__ __launch_bounds__(256) void wsmc_mv_g(wsmc::ProgInlineBlk, wsmc::MvArgs) {\n"
+           "extern \"C\" __global__ " + lb + " void wsmc_mv_g(wsmc::ProgInlineBlk, wsmc::MvArgs) {\n"
            "  const char* ka = (const char*)__builtin_amdgcn_kernarg_segment_ptr();\n"
            "  const wsmc::MvArgs& a = *reinterpret_cast<const wsmc::MvArgs*>(ka + kMvArgsAt);\n"
            "  wsmc::mv_body<WsmcMvSig>(a.prog, a);\n}\n";

@@ -2536,7 +2536,7 @@ __device__ __forceinline__ void fold_seg(double (&s)[K], const wsmc_term* tape, 
         const wsmc_term* tp = &tape[sg.tmpl];
         if (LEAN != 1 && sg.kind == kSegNormalOsc) {
             // Normal(A exp(-gamma t) cos(omega t + phi), sigma) observed at y, over (t, y) pairs
-            double A[K], om[K], ga[K], ph[K], rsd[K], lsd[K];
+            double A[K], om[K], ga[K], ph[K], rh[K], nc[K];
 #pragma unroll
             for (int p = 0; p < K; ++p) {
                 A[p] = wsmc_operand_eval(&tp->dist.mu[0], cols, 0, ix[p], nullptr);
@@ -2544,58 +2544,49 @@ __device__ __forceinline__ void fold_seg(double (&s)[K], const wsmc_term* tape, 
                 ga[p] = wsmc_operand_eval(&tp->dist.mu[2], cols, 0, ix[p], nullptr);
                 ph[p] = wsmc_operand_eval(&tp->dist.mu[3], cols, 0, ix[p], nullptr);
                 if (sg.soff >= 0) {   // a constant sigma: its pair from the host (uniform branch)
-                    lsd[p] = cst[sg.soff];
-                    rsd[p] = cst[sg.soff + 1];
+                    nc[p] = cst[sg.soff];
+                    rh[p] = cst[sg.soff + 1];
                 } else {
-                    wsmc_scale_memo(&lm[p], wsmc_operand_eval(&tp->dist.scale, cols, 0, ix[p], nullptr), &lsd[p],
-                                    &rsd[p]);
+                    wsmc_normal_scale(&lm[p], wsmc_operand_eval(&tp->dist.scale, cols, 0, ix[p], nullptr), &nc[p],
+                                     &rh[p]);
                 }
             }
             // the mean by rotation (wsmc_osc_rolled's operations): a block's first term (m = 0)
             // is the direct phasor, each next term of the block one complex multiply by R; a
             // fold entering a block mid-way (the carried score's continuation) anchors and rolls
             // there, so every term has the bits of the term-by-term evaluation
+            // over the segment's rotation runs (t_a, d, m, n, y_0 .. y_{n-1}; csrc/wsmc_mv.h)
             const double* c = cst + sg.coff;
             double zr[K], zi[K], rr[K], ri[K];
-            double cur_ta = WSMC_NAN, r_d = WSMC_NAN;
-            int cur_m = -2;
-            // each term's constants are scalar loads: the next term's are issued before this
-            // term's arithmetic, so the loop waits out no scalar-memory latency per term
-            const bool any = sg.count > 0;
-            double q0 = any ? c[0] : 0.0, q1 = any ? c[1] : 0.0, q2 = any ? c[2] : 0.0, q3 = any ? c[3] : 0.0;
-            for (int32_t k = 0; k < sg.count; ++k) {
-                const double ta = q0, dl = q1, y = q3;
-                const int m = (int)q2;
-                if (k + 1 < sg.count) {   // uniform
-                    q0 = c[4 * k + 4];
-                    q1 = c[4 * k + 5];
-                    q2 = c[4 * k + 6];
-                    q3 = c[4 * k + 7];
-                }
-                const bool next = m > 0 && m == cur_m + 1 && wsmc_d2bits(ta) == wsmc_d2bits(cur_ta) &&
-                                  wsmc_d2bits(dl) == wsmc_d2bits(r_d);
-                if (m > 0 && wsmc_d2bits(dl) != wsmc_d2bits(r_d)) {   // uniform branch
+            double r_d = WSMC_NAN;
+            for (int32_t left = sg.count; left > 0;) {   // uniform
+                const double ta = c[0], dl = c[1];
+                const int32_t m = osc_run_int(c[2]);
+                const int32_t n0 = osc_run_int(c[3]), n = n0 < 1 ? 1 : n0;
+                const double* yv = c + 4;
+                c = yv + n;
+                left -= n;
+                if ((m > 0 || n > 1) && wsmc_d2bits(dl) != wsmc_d2bits(r_d)) {   // uniform branch
 #pragma unroll
                     for (int p = 0; p < K; ++p) wsmc_osc_step(dl, om[p], ga[p], &rr[p], &ri[p]);
                     r_d = dl;
                 }
+                for (int32_t k = 0; k < n; ++k) {
+                    const double y = yv[k];
 #pragma unroll
-                for (int p = 0; p < K; ++p) {
-                    if (next) {
-                        wsmc_osc_rotate(&zr[p], &zi[p], rr[p], ri[p]);
-                    } else {
-                        wsmc_osc_anchor(ta, A[p], om[p], ga[p], ph[p], &zr[p], &zi[p]);
-                        for (int j = 0; j < m; ++j) wsmc_osc_rotate(&zr[p], &zi[p], rr[p], ri[p]);
+                    for (int p = 0; p < K; ++p) {
+                        if (k > 0) {
+                            wsmc_osc_rotate(&zr[p], &zi[p], rr[p], ri[p]);
+                        } else {
+                            wsmc_osc_anchor(ta, A[p], om[p], ga[p], ph[p], &zr[p], &zi[p]);
+                            for (int j = 0; j < m; ++j) wsmc_osc_rotate(&zr[p], &zi[p], rr[p], ri[p]);
+                        }
                     }
-                }
-                cur_ta = ta;
-                cur_m = m;
 #pragma unroll
-                for (int p = 0; p < K; ++p) {
-                    if (!ok[p]) continue;
-                    const double mu = zr[p];
-                    const double z = (y - mu) * rsd[p];
-                    s[p] = s[p] + (-(z * z + WSMC_LOG2PI) * 0.5 - lsd[p]);
+                    for (int p = 0; p < K; ++p) {
+                        if (!ok[p]) continue;
+                        s[p] = s[p] + wsmc_normal_lh((y - zr[p]) * rh[p], nc[p]);
+                    }
                 }
             }
             continue;
@@ -2604,17 +2595,17 @@ __device__ __forceinline__ void fold_seg(double (&s)[K], const wsmc_term* tape, 
             // Normal(c0 + coef0 col0 + coef1 col1, sigma) observed at y, over (c0, coef0, coef1, y)
             const wsmc_operand& m = tp->dist.mu[0];
             const bool h0 = m.col[0] >= 0, h1 = m.col[1] >= 0;
-            double v0[K], v1[K], rsd[K], lsd[K];
+            double v0[K], v1[K], rh[K], nc[K];
 #pragma unroll
             for (int p = 0; p < K; ++p) {
                 v0[p] = h0 ? cols[m.col[0]][ix[p]] : 0.0;
                 v1[p] = h1 ? cols[m.col[1]][ix[p]] : 0.0;
                 if (sg.soff >= 0) {
-                    lsd[p] = cst[sg.soff];
-                    rsd[p] = cst[sg.soff + 1];
+                    nc[p] = cst[sg.soff];
+                    rh[p] = cst[sg.soff + 1];
                 } else {
-                    wsmc_scale_memo(&lm[p], wsmc_operand_eval(&tp->dist.scale, cols, 0, ix[p], nullptr), &lsd[p],
-                                    &rsd[p]);
+                    wsmc_normal_scale(&lm[p], wsmc_operand_eval(&tp->dist.scale, cols, 0, ix[p], nullptr), &nc[p],
+                                     &rh[p]);
                 }
             }
             const double* c = cst + sg.coff;
@@ -2634,8 +2625,7 @@ __device__ __forceinline__ void fold_seg(double (&s)[K], const wsmc_term* tape, 
                     double mu = c0;
                     if (h0) mu = mu + a0 * v0[p];
                     if (h1) mu = mu + a1 * v1[p];
-                    const double z = (y - mu) * rsd[p];
-                    s[p] = s[p] + (-(z * z + WSMC_LOG2PI) * 0.5 - lsd[p]);
+                    s[p] = s[p] + wsmc_normal_lh((y - mu) * rh[p], nc[p]);
                 }
             }
             continue;

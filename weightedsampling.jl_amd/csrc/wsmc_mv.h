@@ -20,15 +20,20 @@ struct FoldSlots {
 // terms that differ only in their constants (the observations of a model's loop, e.g.
 // examples/damped_oscillator.jl:36 or examples/linear_regression.jl:21) is one segment whose
 // per-particle invariants (the mean's column reads, sigma and its log) are evaluated once;
-// its terms' constants are packed in `cst` (Osc: t_a, d, m, y per term — the rotation block
-// of wsmc_osc_link; Aff: c0, coef0, coef1, y). Every other term is a one-term segment.
+// its terms' constants are packed in `cst`. Aff: (c0, coef0, coef1, y) per term. Osc: rotation
+// runs back to back, each (t_a, d, m, n, y_0 .. y_{n-1}) — n terms of one rotation block of
+// wsmc_osc_link, the first the block's term m (its anchor and m rotations by the step d), each
+// next one rotation further (m and n ride as osc_run_word bits). Every other term is a
+// one-term segment.
 enum { kSegTerm = 0, kSegNormalOsc = 1, kSegNormalAff = 2 };
+WSMC_HD double osc_run_word(int32_t v) { return wsmc_bits2d((uint64_t)(uint32_t)v); }
+WSMC_HD int32_t osc_run_int(double w) { return (int32_t)(uint32_t)wsmc_d2bits(w); }
 struct FoldSeg {
     int32_t kind;
     int32_t count;   // terms in the segment
     int32_t tmpl;    // index of its first term in the compiled tape
-    int32_t coff;    // offset of its constants: Osc (t, y) per term; Aff (c0, coef0, coef1, y) per term
-    int32_t soff;    // a constant scale: offset of its (log sigma, 1/sigma) in the constants
+    int32_t coff;    // offset of its constants (the layouts above)
+    int32_t soff;    // a constant scale: offset of its Normal pair (c, rh) in the constants
                      // (wsmc_scale_pre, evaluated once on the host), else -1
     int32_t pad;     // 24 B: the constants after the segments stay 8-aligned
 };

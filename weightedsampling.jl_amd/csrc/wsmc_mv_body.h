@@ -37,7 +37,7 @@ struct MvSigOp {
 struct MvSigSeg {
     int8_t kind;              // kSegTerm / kSegNormalOsc / kSegNormalAff
     int8_t fam;               // a one-term segment's family: WSMC_FAM_NORMAL / HALFNORMAL / UNIFORM
-    int8_t pre;               // a constant scale: (log sigma, 1/sigma) at the segment's soff
+    int8_t pre;               // a constant scale: its Normal pair (c, rh) at the segment's soff
     int8_t pad;
     MvSigOp x, mu[4], sc;     // the template's operand slots
 };
@@ -149,20 +149,18 @@ __device__ __forceinline__ void mv_fold(double (&s)[K], const double (&v)[K][NS]
                 const double x0 = mv_opv<NS>(&t->x[0], q.x, v[p]);
                 double term;
                 if (q.fam == WSMC_FAM_NORMAL || q.fam == WSMC_FAM_HALFNORMAL) {
-                    double lg, rc;
+                    double nc, rh;
                     if (q.pre) {
-                        lg = cst[h.soff];
-                        rc = cst[h.soff + 1];
+                        nc = cst[h.soff];
+                        rh = cst[h.soff + 1];
                     } else {
-                        wsmc_scale_memo(nullptr, mv_opv<NS>(&t->dist.scale, q.sc, v[p]), &lg, &rc);
+                        wsmc_normal_scale(nullptr, mv_opv<NS>(&t->dist.scale, q.sc, v[p]), &nc, &rh);
                     }
                     if (q.fam == WSMC_FAM_NORMAL) {
                         const double mu = mv_opv<NS>(&t->dist.mu[0], q.mu[0], v[p]);
-                        const double z = (x0 - mu) * rc;
-                        term = -(z * z + WSMC_LOG2PI) * 0.5 - lg;
+                        term = wsmc_normal_lh((x0 - mu) * rh, nc);
                     } else {
-                        const double z = (x0 - 0.0) * rc;
-                        term = (x0 >= 0.0) ? (-(z * z + WSMC_LOG2PI) * 0.5 - lg) + WSMC_LOG2 : -WSMC_INF;
+                        term = (x0 >= 0.0) ? wsmc_normal_lh((x0 - 0.0) * rh, nc) + WSMC_LOG2 : -WSMC_INF;
                     }
                 } else {
                     term = wsmc_uniform_logpdf(t->dist.param[0], t->dist.param[1], x0);
@@ -172,16 +170,16 @@ __device__ __forceinline__ void mv_fold(double (&s)[K], const double (&v)[K][NS]
         } else if (q.kind == kSegNormalAff) {
             // Normal(c0 + coef0 col0 + coef1 col1, sigma) at y over (c0, coef0, coef1, y) per term
             const bool h0 = q.mu[0].c[0] >= 0, h1 = q.mu[0].c[1] >= 0;
-            double v0[K], v1[K], rsd[K], lsd[K];
+            double v0[K], v1[K], rh[K], nc[K];
 #pragma unroll
             for (int p = 0; p < K; ++p) {
                 v0[p] = h0 ? v[p][q.mu[0].c[0] < 0 ? 0 : q.mu[0].c[0]] : 0.0;
                 v1[p] = h1 ? v[p][q.mu[0].c[1] < 0 ? 0 : q.mu[0].c[1]] : 0.0;
                 if (q.pre) {
-                    lsd[p] = cst[h.soff];
-                    rsd[p] = cst[h.soff + 1];
+                    nc[p] = cst[h.soff];
+                    rh[p] = cst[h.soff + 1];
                 } else {
-                    wsmc_scale_memo(nullptr, mv_opv<NS>(&t->dist.scale, q.sc, v[p]), &lsd[p], &rsd[p]);
+                    wsmc_normal_scale(nullptr, mv_opv<NS>(&t->dist.scale, q.sc, v[p]), &nc[p], &rh[p]);
                 }
             }
             const double* c = cst + h.coff;
@@ -200,15 +198,14 @@ __device__ __forceinline__ void mv_fold(double (&s)[K], const double (&v)[K][NS]
                     double mu = c0;
                     if (h0) mu = mu + a0 * v0[p];
                     if (h1) mu = mu + a1 * v1[p];
-                    const double z = (y - mu) * rsd[p];
-                    s[p] = s[p] + (-(z * z + WSMC_LOG2PI) * 0.5 - lsd[p]);
+                    s[p] = s[p] + wsmc_normal_lh((y - mu) * rh[p], nc[p]);
                 }
             }
         } else {
             // Normal(A exp(-gamma t) cos(omega t + phi), sigma) at y, over (t_a, d, m, y) per term:
             // fold_seg's rotation walk (a block's first term the direct phasor, each next term one
             // complex multiply, a fold entering a block mid-way anchors and rolls there)
-            double A[K], om[K], ga[K], ph[K], rsd[K], lsd[K];
+            double A[K], om[K], ga[K], ph[K], rh[K], nc[K];
 #pragma unroll
             for (int p = 0; p < K; ++p) {
                 A[p] = mv_opv<NS>(&t->dist.mu[0], q.mu[0], v[p]);
@@ -216,53 +213,51 @@ __device__ __forceinline__ void mv_fold(double (&s)[K], const double (&v)[K][NS]
                 ga[p] = mv_opv<NS>(&t->dist.mu[2], q.mu[2], v[p]);
                 ph[p] = mv_opv<NS>(&t->dist.mu[3], q.mu[3], v[p]);
                 if (q.pre) {
-                    lsd[p] = cst[h.soff];
-                    rsd[p] = cst[h.soff + 1];
+                    nc[p] = cst[h.soff];
+                    rh[p] = cst[h.soff + 1];
                 } else {
-                    wsmc_scale_memo(nullptr, mv_opv<NS>(&t->dist.scale, q.sc, v[p]), &lsd[p], &rsd[p]);
+                    wsmc_normal_scale(nullptr, mv_opv<NS>(&t->dist.scale, q.sc, v[p]), &nc[p], &rh[p]);
                 }
             }
             const double* c = cst + h.coff;
             double zr[K], zi[K], rr[K], ri[K];
-            // a run's terms come from wsmc_osc_link on consecutive tape terms: after the fold's
-            // first term each one either opens a block (m = 0: its direct phasor) or continues the
-            // previous term's block (m = m' + 1, the same t_a and step), so the continuation test of
-            // fold_seg reduces to m != 0 — a scalar compare of the constant's bits, no conversion.
-            // The step R is recomputed when the block's step changes (at its m = 1 term, whose
-            // predecessor's phasor is the anchor: one rotation of it gives fold_seg's anchor + 1
-            // rotation bit for bit). The first term may enter a block mid-way: anchor, m rotations.
+            // the segment's rotation runs (wsmc_mv.h): a run's first term is its anchor and m
+            // rotations by the block's step R, each next term one rotation — the term-by-term
+            // evaluation's operations bit for bit; the step is recomputed only when a run needs it
+            // and its bits change. The inner loop is a rotation and a score per term, one scalar
+            // load (the next observation, issued a term ahead)
             double r_d = WSMC_NAN;
-            const bool any = h.count > 0;
-            double q0 = any ? c[0] : 0.0, q1 = any ? c[1] : 0.0, q2 = any ? c[2] : 0.0, q3 = any ? c[3] : 0.0;
-            for (int32_t k = 0; k < h.count; ++k) {
-                const double ta = q0, dl = q1, mq = q2, y = q3;
-                if (k + 1 < h.count) {
-                    q0 = c[4 * k + 4];
-                    q1 = c[4 * k + 5];
-                    q2 = c[4 * k + 6];
-                    q3 = c[4 * k + 7];
-                }
-                const bool m0 = wsmc_d2bits(mq) == 0;
-                if (!m0 && wsmc_d2bits(dl) != wsmc_d2bits(r_d)) {   // uniform
+            for (int32_t left = h.count; left > 0;) {   // uniform
+                const double ta = c[0], dl = c[1];
+                const int32_t m = osc_run_int(c[2]);
+                const int32_t n0 = osc_run_int(c[3]), n = n0 < 1 ? 1 : n0;
+                const double* yv = c + 4;
+                c = yv + n;
+                left -= n;
+                if ((m > 0 || n > 1) && wsmc_d2bits(dl) != wsmc_d2bits(r_d)) {
 #pragma unroll
                     for (int p = 0; p < K; ++p) wsmc_osc_step(dl, om[p], ga[p], &rr[p], &ri[p]);
                     r_d = dl;
                 }
-                if (m0 || k == 0) {   // uniform
-                    const int m = m0 ? 0 : (int)mq;
-#pragma unroll
-                    for (int p = 0; p < K; ++p) {
-                        wsmc_osc_anchor(ta, A[p], om[p], ga[p], ph[p], &zr[p], &zi[p]);
-                        for (int j = 0; j < m; ++j) wsmc_osc_rotate(&zr[p], &zi[p], rr[p], ri[p]);
-                    }
-                } else {
-#pragma unroll
-                    for (int p = 0; p < K; ++p) wsmc_osc_rotate(&zr[p], &zi[p], rr[p], ri[p]);
-                }
 #pragma unroll
                 for (int p = 0; p < K; ++p) {
-                    const double z = (y - zr[p]) * rsd[p];
-                    s[p] = s[p] + (-(z * z + WSMC_LOG2PI) * 0.5 - lsd[p]);
+                    wsmc_osc_anchor(ta, A[p], om[p], ga[p], ph[p], &zr[p], &zi[p]);
+                    for (int j = 0; j < m; ++j) wsmc_osc_rotate(&zr[p], &zi[p], rr[p], ri[p]);
+                }
+                // yv[k + 1] is in the program for every k < n (the next run's header or the
+                // segment's pad word), so the next observation's load is unconditional
+                double yn = yv[1];
+#pragma unroll
+                for (int p = 0; p < K; ++p) s[p] = s[p] + wsmc_normal_lh((yv[0] - zr[p]) * rh[p], nc[p]);
+#pragma unroll 2
+                for (int32_t k = 1; k < n; ++k) {
+                    const double y = yn;
+                    yn = yv[k + 1];
+#pragma unroll
+                    for (int p = 0; p < K; ++p) {
+                        wsmc_osc_rotate(&zr[p], &zi[p], rr[p], ri[p]);
+                        s[p] = s[p] + wsmc_normal_lh((y - zr[p]) * rh[p], nc[p]);
+                    }
                 }
             }
         }
