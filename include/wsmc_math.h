@@ -747,6 +747,41 @@ WSMC_HD double wsmc_log_abs_jac(double z, double lo, double hi) {
     const int both = wsmc_isfinite(lo) && wsmc_isfinite(hi);
     return wsmc_log_abs_jac_pre(z, lo, hi, both ? wsmc_log(hi - lo) : 0.0);
 }
+/* One proposal step of a target under bounds (src/move_kernels.jl:154-172): from the current
+ * value x and the unconstrained increment dz, the proposal xn = from_unc(to_unc(x) + dz)
+ * (returned) and *dj = log|dx/dz|(zn) - log|dx/dz|(zo), the Jacobian part of the log proposal
+ * ratio. flo / fhi: the bounds' finiteness (wsmc_isfinite, or known at compile time). With
+ * both bounds finite the step shares its transcendentals, a restatement within rounding of the
+ * term-by-term transforms above:
+ *   la = log(x - lo), lb = log(hi - x), zo = la - lb                      (to_unc, the same bits)
+ *   log|dx/dz|(zo) = log((x - lo)(hi - x)/(hi - lo)) = (la + lb) - lgw    (no exp, no log1p)
+ *   e = exp(-|zn|), P = log1p(e): log|dx/dz|(zn) = (lgw - |zn|) - 2P   (= lgw - log1pexp(zn)
+ *                                                                         - log1pexp(-zn))
+ *   xn = lo + w/(1 + e) for zn >= 0, lo + (w e)/(1 + e) below (w = hi - lo; 1/(1 + exp(-zn)))
+ * — three logs, one exp and two divisions where the transforms took four logs, three exps and
+ * three divisions. One finite bound: zo = log(x - lo) or log(hi - x), xn = lo + exp(zn) or
+ * hi - exp(zn), *dj = zn - zo; none: xn = x + dz, *dj = 0. */
+WSMC_HD double wsmc_bounded_step(double x, double dz, double lo, double hi, double lgw, int flo, int fhi,
+                                 double* dj) {
+    if (flo && fhi) {
+        const double la = wsmc_log(x - lo), lb = wsmc_log(hi - x);
+        const double zn = (la - lb) + dz;
+        const double az = wsmc_fabs(zn);
+        const double e = wsmc_exp(-az);
+        const double u = 1.0 + e;
+        const double w = hi - lo;
+        *dj = ((lgw - az) - 2.0 * wsmc_log1p(e)) - ((la + lb) - lgw);
+        return lo + (zn >= 0.0 ? w / u : (w * e) / u);
+    }
+    if (flo || fhi) {
+        const double zo = flo ? wsmc_log(x - lo) : wsmc_log(hi - x);
+        const double zn = zo + dz;
+        *dj = zn - zo;
+        return flo ? lo + wsmc_exp(zn) : hi - wsmc_exp(zn);
+    }
+    *dj = 0.0;
+    return x + dz;
+}
 
 /* ------------------------------------------------------------------------- */
 /* integer weights, ESS, and the stratified/systematic target map            */

@@ -941,10 +941,13 @@ static int move_apply(oracle* o, const int32_t* targets, int32_t d, int bounded,
         double lpr = 0.0;
         for (int k = 0; k < d; ++k) {
             double x = o->cols[targets[k]].front[i];
-            double zo = bounded ? wsmc_to_unc(x, l[k], h[k]) : x;
-            double zn = zo + dz[k];
-            double xn = bounded ? wsmc_from_unc(zn, l[k], h[k]) : zn;
-            if (bounded) lpr = lpr + (wsmc_log_abs_jac(zn, l[k], h[k]) - wsmc_log_abs_jac(zo, l[k], h[k]));
+            double xn = x + dz[k];
+            if (bounded) {   /* to_unc, the step, from_unc and the Jacobian difference */
+                const int fl = wsmc_isfinite(l[k]), fh = wsmc_isfinite(h[k]);
+                double dj;
+                xn = wsmc_bounded_step(x, dz[k], l[k], h[k], fl && fh ? wsmc_log(h[k] - l[k]) : 0.0, fl, fh, &dj);
+                lpr = lpr + dj;
+            }
             ov.col[k] = targets[k];
             ov.val[k] = xn;
             newv[(int64_t)k * N + i] = xn;

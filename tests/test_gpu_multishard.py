@@ -582,18 +582,14 @@ def test_one_rank_rccl_autorw_not_pd(gpu_available):
     import wsmc
     from oracle import Oracle
     from wsmc import abi, models
-    from wsmc.dsl import Normal
-    from test_gpu_parity import assert_same_state
+    from test_gpu_parity import assert_same_state, not_pd_seed, rank1_case
     N = 2048
-    g = wsmc.Context(N, seed=4)
+    seed = not_pd_seed(lambda s: Oracle(N, seed=s))
+    g = wsmc.Context(N, seed=seed)
     g.comm_init(wsmc.Context.comm_unique_id(), 1, 0, 0, N)
     res = []
-    for c in (g, Oracle(N, seed=4)):
-        R = models.resolver(c)
-        a, b = c.col_create("a"), c.col_create("b")
-        c.sample(a, Normal(0.0, 1.0).dist(R))
-        c.assign(b, abi.Operand.column(a, coef=2.0))      # b = 2a: rank-1 covariance
-        c.observe(Normal(wsmc.Col("a"), 1.0).dist(R), models._const([0.2]))
+    for c in (g, Oracle(N, seed=seed)):
+        a, b = rank1_case(c)                               # b = 2a: rank-1 covariance
         with pytest.raises(np.linalg.LinAlgError):
             c.move(abi.PROPOSAL_AUTORW, [a, b], 1e-3)
         acc = c.move(abi.PROPOSAL_AUTORW, [a], 1e-3)
@@ -697,21 +693,17 @@ def test_multi_handle_symmetric_errors_keep_the_handle(gpu_available, mode):
     from oracle import Oracle
     import wsmc
     from wsmc import abi, models
-    from wsmc.dsl import Normal
-    from test_gpu_parity import assert_same_state
+    from test_gpu_parity import assert_same_state, not_pd_seed, rank1_case
     G, N = 3, 3000
     exact = mode == "exact"
-    g = wsmc.Context.multi(N, G, seed=4, devices=[0] * G, transport=abi.TRANSPORT_HOST)
+    seed = not_pd_seed(lambda s: Oracle(N, seed=s, shards=G, exact=exact))
+    g = wsmc.Context.multi(N, G, seed=seed, devices=[0] * G, transport=abi.TRANSPORT_HOST)
     if exact:
         g.comm_set_shard_mode(abi.SHARD_EXACT)
-    o = Oracle(N, seed=4, shards=G, exact=exact)
+    o = Oracle(N, seed=seed, shards=G, exact=exact)
     res = []
     for c in (g, o):
-        R = models.resolver(c)
-        a, b = c.col_create("a"), c.col_create("b")
-        c.sample(a, Normal(0.0, 1.0).dist(R))
-        c.assign(b, abi.Operand.column(a, coef=2.0))      # b = 2a: rank-1 covariance
-        c.observe(Normal(wsmc.Col("a"), 1.0).dist(R), models._const([0.2]))
+        a, b = rank1_case(c)                               # b = 2a: rank-1 covariance
         with pytest.raises(np.linalg.LinAlgError):
             c.move(abi.PROPOSAL_AUTORW, [a, b], 1e-3)
         acc = c.move(abi.PROPOSAL_AUTORW, [a], 1e-3)

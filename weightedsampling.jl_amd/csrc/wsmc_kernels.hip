@@ -2481,11 +2481,13 @@ __global__ __launch_bounds__(kBlock) void k_move(const wsmc_term* tape, int32_t 
         double lpr = 0.0;
         for (int k = 0; k < d; ++k) {
             const double x = cols[ma.tcol[k]][i];
-            const double zo = bounded ? wsmc_to_unc(x, ma.lo[k], ma.hi[k]) : x;
-            const double zn = zo + dz[k];
-            const double xn = bounded ? wsmc_from_unc(zn, ma.lo[k], ma.hi[k]) : zn;
-            if (bounded)
-                lpr = lpr + (wsmc_log_abs_jac_pre(zn, ma.lo[k], ma.hi[k], ma.lgw[k]) - wsmc_log_abs_jac_pre(zo, ma.lo[k], ma.hi[k], ma.lgw[k]));
+            double xn = x + dz[k];
+            if (bounded) {
+                double dj;
+                xn = wsmc_bounded_step(x, dz[k], ma.lo[k], ma.hi[k], ma.lgw[k], wsmc_isfinite(ma.lo[k]),
+                                       wsmc_isfinite(ma.hi[k]), &dj);
+                lpr = lpr + dj;
+            }
             ov.col[k] = ma.tcol[k];
             ov.val[k] = xn;
         }
@@ -2728,12 +2730,13 @@ __device__ __forceinline__ void move_c_body(const wsmc_term* ctape, const FoldSl
 #pragma unroll
             for (int j = 0; j <= k; ++j) dz = dz + Lm[k * d + j] * xi[j];
             const double x = sv[k * W + ix[p]];
-            const double zo = bounded ? wsmc_to_unc(x, ma.lo[k], ma.hi[k]) : x;
-            const double zn = zo + dz;
-            const double xn = bounded ? wsmc_from_unc(zn, ma.lo[k], ma.hi[k]) : zn;
-            if (bounded)
-                lpr[p] = lpr[p] + (wsmc_log_abs_jac_pre(zn, ma.lo[k], ma.hi[k], ma.lgw[k]) -
-                                   wsmc_log_abs_jac_pre(zo, ma.lo[k], ma.hi[k], ma.lgw[k]));
+            double xn = x + dz;
+            if (bounded) {
+                double dj;
+                xn = wsmc_bounded_step(x, dz, ma.lo[k], ma.hi[k], ma.lgw[k], wsmc_isfinite(ma.lo[k]),
+                                       wsmc_isfinite(ma.hi[k]), &dj);
+                lpr[p] = lpr[p] + dj;
+            }
             prop[k * W + ix[p]] = xn;
         }
     }
@@ -2980,12 +2983,13 @@ __device__ __forceinline__ void move_blk_body(const wsmc_term* ctape, const Fold
                 for (int jj = 0; jj <= k; ++jj) dz = dz + Lm[k * dm + jj] * xi[jj];
                 const double x = sv[u * W + ix[p]];
                 const bool bd = BND && ((mb.bnd >> u) & 1);
-                const double zo = bd ? wsmc_to_unc(x, mb.lo[u], mb.hi[u]) : x;
-                const double zn = zo + dz;
-                const double xn = bd ? wsmc_from_unc(zn, mb.lo[u], mb.hi[u]) : zn;
-                if (bd)
-                    lpr[p] = lpr[p] + (wsmc_log_abs_jac_pre(zn, mb.lo[u], mb.hi[u], mb.lgw[u]) -
-                                       wsmc_log_abs_jac_pre(zo, mb.lo[u], mb.hi[u], mb.lgw[u]));
+                double xn = x + dz;
+                if (bd) {
+                    double dj;
+                    xn = wsmc_bounded_step(x, dz, mb.lo[u], mb.hi[u], mb.lgw[u], wsmc_isfinite(mb.lo[u]),
+                                           wsmc_isfinite(mb.hi[u]), &dj);
+                    lpr[p] = lpr[p] + dj;
+                }
                 prop[u * W + ix[p]] = xn;
             }
         }

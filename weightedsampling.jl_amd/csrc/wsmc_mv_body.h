@@ -19,7 +19,7 @@
 //     offsets, issued together;
 //   * each fold is straight-line code for its segments (runs keep a run-time term count).
 // The arithmetic is the interpreter's operation for operation (wsmc_operand_eval's order,
-// wsmc_scalar_term_logpdf_p, the run loops of fold_seg, the draws, wsmc_to_unc/from_unc,
+// wsmc_scalar_term_logpdf_p, the run loops of fold_seg, the draws, wsmc_bounded_step,
 // move_accept), so the bits are the interpreter's and the oracle's.
 #pragma once
 
@@ -96,31 +96,6 @@ __device__ __forceinline__ unsigned long long mv_block_sum(unsigned long long v,
     const unsigned long long r = (lds4[0] + lds4[1]) + (lds4[2] + lds4[3]);
     __syncthreads();
     return r;
-}
-
-// wsmc_to_unc / wsmc_from_unc / wsmc_log_abs_jac_pre with the bounds' finiteness known at
-// compile time (the same arithmetic for each case; only the untaken cases' code goes)
-__device__ __forceinline__ double mv_to_unc(double x, double lo, double hi, bool flo, bool fhi) {
-    if (flo && fhi) return wsmc_log(x - lo) - wsmc_log(hi - x);
-    if (flo) return wsmc_log(x - lo);
-    if (fhi) return wsmc_log(hi - x);
-    return x;
-}
-__device__ __forceinline__ double mv_from_unc(double z, double lo, double hi, bool flo, bool fhi) {
-    if (flo && fhi) return lo + (hi - lo) / (1.0 + wsmc_exp(-z));
-    if (flo) return lo + wsmc_exp(z);
-    if (fhi) return hi - wsmc_exp(z);
-    return z;
-}
-__device__ __forceinline__ double mv_log_abs_jac(double z, double lgw, bool flo, bool fhi) {
-    if (flo && fhi) {
-        const double P = wsmc_log1p(wsmc_exp(z > 0.0 ? -z : z));
-        const double a = z > 0.0 ? z + P : P;
-        const double b = -z > 0.0 ? -z + P : P;
-        return lgw - a - b;
-    }
-    if (flo || fhi) return z;
-    return 0.0;
 }
 
 // wsmc_operand_eval with the slot reads resolved at compile time
@@ -331,12 +306,12 @@ __device__ __forceinline__ void mv_body(const char* pb, const MvArgs& a) {
                 for (int jj = 0; jj <= k; ++jj) dz = dz + Lm[k * dm + jj] * xi[jj];
                 const double x = v[p][u];
                 const bool bd = (G.bnd >> u) & 1, flo = (G.flo >> u) & 1, fhi = (G.fhi >> u) & 1;
-                const double zo = bd ? mv_to_unc(x, a.mb.lo[u], a.mb.hi[u], flo, fhi) : x;
-                const double zn = zo + dz;
-                const double xn = bd ? mv_from_unc(zn, a.mb.lo[u], a.mb.hi[u], flo, fhi) : zn;
-                if (bd)
-                    lpr[p] = lpr[p] + (mv_log_abs_jac(zn, a.mb.lgw[u], flo, fhi) -
-                                       mv_log_abs_jac(zo, a.mb.lgw[u], flo, fhi));
+                double xn = x + dz;
+                if (bd) {   // the bounds' finiteness known at compile time: only its case's code
+                    double dj;
+                    xn = wsmc_bounded_step(x, dz, a.mb.lo[u], a.mb.hi[u], a.mb.lgw[u], flo, fhi, &dj);
+                    lpr[p] = lpr[p] + dj;
+                }
                 pr[p][k] = xn;
             }
         }
