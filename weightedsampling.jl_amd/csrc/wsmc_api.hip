@@ -411,15 +411,26 @@ static int resolve_scache_lag(wsmc_ctx* c) {
 // ---- lazy genealogy (AncRow, wsmc_internal.h) ---------------------------------------------
 static inline size_t row_anc_bytes(int64_t N) { return (sizeof(int32_t) * (size_t)N + 255) & ~(size_t)255; }
 static int acquire_row(wsmc_ctx* c, AncRow* out) {
-    if (!c->row_pool.empty()) {
-        *out = c->row_pool.back();
-        c->row_pool.pop_back();
-    } else {
+    if (c->row_pool.empty()) {
+        // a slab of as many rows as exist (at least 4): a lazy log that keeps growing (columns
+        // read one Resample behind) costs a hipMalloc every few Resamples, not one each — a
+        // hipMalloc is tens of microseconds of host time, more than a step's launches
+        const int64_t n = std::max<int64_t>(4, c->rows_made);
+        const size_t stride = row_anc_bytes(c->N) + 256;
         void* p = nullptr;
-        WSMC_HIP(hipMalloc(&p, row_anc_bytes(c->N) + 256));
-        out->anc = reinterpret_cast<int32_t*>(p);
-        out->dec = reinterpret_cast<Decision*>(reinterpret_cast<char*>(p) + row_anc_bytes(c->N));
+        WSMC_HIP(hipMalloc(&p, stride * (size_t)n));
+        c->row_slabs.push_back(p);
+        c->rows_made += n;
+        for (int64_t k = n - 1; k >= 0; --k) {
+            char* q = reinterpret_cast<char*>(p) + stride * (size_t)k;
+            AncRow r{};
+            r.anc = reinterpret_cast<int32_t*>(q);
+            r.dec = reinterpret_cast<Decision*>(q + row_anc_bytes(c->N));
+            c->row_pool.push_back(r);
+        }
     }
+    *out = c->row_pool.back();
+    c->row_pool.pop_back();
     out->known = -1;
     return WSMC_OK;
 }
@@ -709,11 +720,7 @@ int wsmc_destroy(wsmc_ctx* c) {
         (void)hipFree(col.front);
         (void)hipFree(col.back);
     }
-    for (auto& r : c->alog) (void)hipFree(r.anc);
-    for (auto& r : c->row_pool) (void)hipFree(r.anc);
-    for (auto& p : c->dec_rows)
-        if (p.epoch < 0) (void)hipFree(p.row.anc);   // eager rows (lazy ones are in alog)
-    if (c->anc_keep.anc) (void)hipFree(c->anc_keep.anc);
+    for (void* p : c->row_slabs) (void)hipFree(p);   // every row (log, pool, eager, anc_keep) lives in a slab
     void* bufs[] = {c->dec_always, c->xchg, c->scache, c->scache_back, c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->cdf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount, c->wslots[0], c->wslots[1],
                     c->d_colptr, c->run_params, c->d_tape, c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp,
                     c->vscratch, c->xscratch, c->xp, c->comb, c->anc_out, c->xbuf, c->d_comp, c->d_ctape, c->d_prog, c->rs_grp[0], c->rs_grp[1],

@@ -290,6 +290,8 @@ struct wsmc_ctx {
     int64_t epoch = 0, log_base = 0;
     std::deque<wsmc::AncRow> alog;
     std::vector<wsmc::AncRow> row_pool;     // free rows (ancestors + decision)
+    std::vector<void*> row_slabs;           // the rows' memory: slabs of several rows, one hipMalloc each
+    int64_t rows_made = 0;
     // each pending asynchronous decision's ancestors: a lazy log entry (epoch >= 0) or an eager
     // store's own row (epoch -1), held until the decision is read back
     struct PendingRow {
