@@ -2310,7 +2310,13 @@ __global__ __launch_bounds__(kBlock) void k_moments1(const double* __restrict__ 
     // the tile's loads in chunks of CH items (a few memory latencies per thread, not kItems in
     // a row; CH bounded so the loaded values stay in registers), then the canonical per-item
     // accumulation
-    constexpr int CH = D <= 1 ? 8 : (D == 2 ? 4 : 2);
+#ifndef WSMC_MOM_CH
+#define WSMC_MOM_CH 0
+#endif
+    // measured (tools/ab.sh, round 5): twice these (8, 8, 4) slower on C3 and C5 (1.02 / 0.96 ms,
+    // 162 / 156 ms: the registers cost more waves than the extra loads in flight gain); half of
+    // them (4, 2, 1: WSMC_MOM_CH=2) even (0.93 / 0.93 ms, 155.0 / 155.5 ms)
+    constexpr int CH = WSMC_MOM_CH == 2 ? (D <= 1 ? 4 : (D == 2 ? 2 : 1)) : (D <= 1 ? 8 : (D == 2 ? 4 : 2));
     static_assert(kItems % CH == 0, "chunking");
 #pragma unroll 1
     for (int j0 = 0; j0 < kItems; j0 += CH) {
