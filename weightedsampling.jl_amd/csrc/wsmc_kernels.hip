@@ -3339,13 +3339,24 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_final(Ssm2dFinal f) {
     const int64_t ib = i0 < N ? i0 : N - P;
     const int64_t S = f.anc_stride;
     // component pairs of P particles: (x.x of each, x.y of each) -> SoA dst[ib..], dst[N + ib..]
+// WSMC_FIN_NT=1 (diagnostics): nontemporal history stores. Measured (tools/ab_bench.sh, round 5):
+// 447 against 438 us a run, the bench line even (2.51e10 both): not kept
+#ifndef WSMC_FIN_NT
+#define WSMC_FIN_NT 0
+#endif
     auto put = [&](double* dst0, const d2 (&x)[P]) {
         gdp dst = (gdp)dst0;
         if constexpr (P >= 2) {
 #pragma unroll
             for (int p = 0; p < P; p += 2) {
-                *reinterpret_cast<__attribute__((address_space(1))) d2*>(dst + ib + p) = d2{x[p].x, x[p + 1].x};
-                *reinterpret_cast<__attribute__((address_space(1))) d2*>(dst + N + ib + p) = d2{x[p].y, x[p + 1].y};
+                if (WSMC_FIN_NT) {
+                    typedef double __attribute__((ext_vector_type(2))) v2d;
+                    __builtin_nontemporal_store(v2d{x[p].x, x[p + 1].x}, reinterpret_cast<__attribute__((address_space(1))) v2d*>(dst + ib + p));
+                    __builtin_nontemporal_store(v2d{x[p].y, x[p + 1].y}, reinterpret_cast<__attribute__((address_space(1))) v2d*>(dst + N + ib + p));
+                } else {
+                    *reinterpret_cast<__attribute__((address_space(1))) d2*>(dst + ib + p) = d2{x[p].x, x[p + 1].x};
+                    *reinterpret_cast<__attribute__((address_space(1))) d2*>(dst + N + ib + p) = d2{x[p].y, x[p + 1].y};
+                }
             }
         } else {
             dst[ib] = x[0].x;
