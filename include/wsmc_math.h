@@ -66,6 +66,7 @@ WSMC_HD double wsmc_bits2d(uint64_t u) { union { double d; uint64_t u; } v; v.u 
 #define WSMC_INF (wsmc_bits2d(0x7ff0000000000000ULL))
 #define WSMC_NAN (wsmc_bits2d(0x7ff8000000000000ULL))
 #define WSMC_LOG2PI 1.8378770664093453     /* log(2*pi) rounded to double */
+#include "wsmc_log_table.h"
 #define WSMC_LOG2   0.69314718055994530942 /* log(2) */
 #define WSMC_PI     3.14159265358979311600
 #define WSMC_TWO_PI 6.28318530717958623200
@@ -158,7 +159,7 @@ WSMC_HD double wsmc_u01_open0(uint32_t hi, uint32_t lo) {
 }
 
 /* ------------------------------------------------------------------------- */
-/* exp / log / log1p  (fdlibm e_exp.c / e_log.c algorithms, restated)         */
+/* exp (fdlibm e_exp.c restated) / log (table-driven) / log1p                  */
 /* ------------------------------------------------------------------------- */
 WSMC_HD double wsmc_scalbn_small(double y, int k) {
     /* y in [0.5, 2), returns y * 2^k with a single rounding for normal results */
@@ -250,35 +251,54 @@ WSMC_HD double wsmc_exp_nd(double x) {
     return p * wsmc_pow2i((int)kd);
 }
 
+/* log(x), table-driven (the approach of Julia's own Base.log and of glibc's log, restated with
+ * this file's table: include/wsmc_log_table.h, generated by tools/gen_log_table.py). x = 2^k z
+ * with z in [0x1.6p-1, 0x1.6p0); the top 7 bits of z's mantissa above 0x3fe6... select an
+ * interval with centre c, invc = 1/c and logc = -log(invc) correctly rounded; then
+ *   r = fma(z, invc, -1)             |r| < 2^-7 (one rounding of z/c - 1; exact when c = 1)
+ *   log x = k ln2 + logc + log1p(r),  log1p(r) = r + r^2 q(r), q the Taylor series to r^6
+ * summed as hi = (k ln2hi + logc) + r plus both sums' rounding errors, k ln2lo and r^2 q. The two
+ * intervals around 1 have c = 1 exactly, so log x near 1 is r + r^2 q(r) with r = x - 1 exact:
+ * relative accuracy where the result is small. No division (the fdlibm form it replaces
+ * divided f / (2 + f)): about 30 instructions where there were 65. Within 0.6 ulp
+ * (tests/test_oracle_math.py checks it against decimal logs). Zero, negatives, subnormals,
+ * infinities and NaN take one rarely-taken branch. */
+WSMC_HD void wsmc_log_entry(uint32_t i, double* invc, double* logc) {
+    static const double t[2 * WSMC_LOG_TABLE_N] = WSMC_LOG_TAB_INIT;
+    *invc = t[2 * i];
+    *logc = t[2 * i + 1];
+}
 WSMC_HD double wsmc_log(double x) {
-    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
-                 Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
-                 Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
-                 Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
-                 Lg7 = 1.479819860511658591e-01;
-    if (wsmc_isnan(x)) return x;
-    if (x < 0.0) return WSMC_NAN;
-    if (x == 0.0) return -WSMC_INF;
-    if (x == WSMC_INF) return x;
+    const double ln2hi = 6.93147180369123816490e-01, ln2lo = 1.90821492927058770002e-10;
     uint64_t b = wsmc_d2bits(x);
-    int k = 0;
-    if ((b >> 52) == 0) { x *= 18014398509481984.0; b = wsmc_d2bits(x); k = -54; } /* subnormal: *2^54 */
-    uint32_t hx = (uint32_t)(b >> 32);
-    k += (int)(hx >> 20) - 1023;
-    hx &= 0x000fffffu;
-    uint32_t i = (hx + 0x95f64u) & 0x100000u;
-    b = ((uint64_t)(hx | (i ^ 0x3ff00000u)) << 32) | (b & 0xffffffffULL);
-    x = wsmc_bits2d(b);                   /* x in [sqrt(2)/2, sqrt(2)) */
-    k += (int)(i >> 20);
-    double f = x - 1.0;
-    double s = f / (2.0 + f);
-    double dk = (double)k;
-    double z = s * s, w = z * z;
-    double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
-    double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
-    double R = t2 + t1;
-    double hfsq = 0.5 * f * f;
-    return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+    if (b - 0x0010000000000000ULL >= 0x7fe0000000000000ULL) {   /* not a positive normal */
+        if (wsmc_isnan(x)) return x;
+        if (x < 0.0) return WSMC_NAN;
+        if (x == 0.0) return -WSMC_INF;
+        if (x == WSMC_INF) return x;
+        b = wsmc_d2bits(x * 4503599627370496.0) - (52ULL << 52);   /* subnormal: 2^52 x, k - 52 */
+    }
+    const uint64_t tmp = b - 0x3fe6000000000000ULL;
+    const uint32_t i = (uint32_t)(tmp >> 45) & (WSMC_LOG_TABLE_N - 1);
+    const int k = (int32_t)(uint32_t)(tmp >> 32) >> 20;   /* (int64_t)tmp >> 52, from the high word */
+    const double z = wsmc_bits2d(b - (tmp & (0xfffULL << 52)));
+    double invc, logc;
+    wsmc_log_entry(i, &invc, &logc);
+    const double r = __builtin_fma(z, invc, -1.0);
+    const double kd = (double)k;
+    const double kh = kd * ln2hi;   /* exact: ln2hi has 32 trailing zero bits */
+    const double w = kh + logc;
+    const double we = (kh - w) + logc;   /* w's rounding error (|kh| >= |logc| unless kh = 0) */
+    const double hi = w + r;
+    const double lo = (kd * ln2lo + we) + ((w - hi) + r);
+    double q = -0.125;
+    q = __builtin_fma(q, r, WSMC_K(0.14285714285714285));   /* 1/7 */
+    q = __builtin_fma(q, r, WSMC_K(-0.16666666666666666));  /* -1/6 */
+    q = __builtin_fma(q, r, WSMC_K(0.2));
+    q = __builtin_fma(q, r, -0.25);
+    q = __builtin_fma(q, r, WSMC_K(0.3333333333333333));    /* 1/3 */
+    q = __builtin_fma(q, r, -0.5);
+    return hi + __builtin_fma(r * r, q, lo);
 }
 
 /* log1p via the Goldberg correction (accurate to a few ulp; used for log1pexp) */
