@@ -10,6 +10,7 @@
 #                               line, rocprofv3 kernel stats of the bench command, FETCH_SIZE /
 #                               WRITE_SIZE passes -> pmc_summary.json, pmc_step_bytes.json
 #   prof <tag>                  the round's profile passes alone
+#   big <tag>                   the 8M line, its kernel stats and PMC step bytes
 #   bench <tag> [bench args]    bench.py line + rocprofv3 kernel stats of the same command
 #   moves <tag>                 C3 / C5 move-program lines (tools/bench_moves.py) + C3 kernel stats
 #   c5flops <tag>               C5 FP64 work (SQ_INSTS_VALU_*_F64) against its kernel durations
@@ -91,6 +92,17 @@ round)
   timeout -k 10 400 python bench.py --no-cpu-baseline --statements > $O/bench_statements.json 2> $O/bench_statements.err || { tail -20 $O/bench_statements.err; exit 1; }
   line $O/bench_statements.json statements
   prof_passes ;;
+big)    # the beyond-MALL line: 8M particles, its kernel stats and PMC step bytes
+  timeout -k 10 400 python bench.py --particles 8000000 --steps 40 --warmup 3 > $O/bench8m.json 2> $O/bench8m.err || { tail -20 $O/bench8m.err; exit 1; }
+  line $O/bench8m.json bench-8M
+  step 400 $O/stats8m.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats8m -o run -- python bench.py --no-cpu-baseline --particles 8000000 --steps 10 --warmup 2
+  stats_table $O/stats8m/run_kernel_stats.csv 6
+  A="--particles 8000000 --steps 2 --warmup 1 --no-cpu-baseline"
+  step 300 $O/fetch.log rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- python bench.py $A
+  step 300 $O/write.log rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python bench.py $A
+  python tools/summarize_pmc.py $O/pmc_summary8m.json $O/fetch $O/write > /dev/null
+  python tools/pmc_step_bytes.py $O/pmc_summary8m.json 8000000 100 $O/pmc_step_bytes8m.json
+  cat $O/pmc_step_bytes8m.json ;;
 prof)   # the round's profile passes alone (kernel stats, FETCH_SIZE / WRITE_SIZE)
   prof_passes ;;
 bench)  timeout -k 10 400 python bench.py "$@" > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
