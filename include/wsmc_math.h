@@ -204,10 +204,26 @@ WSMC_HD double wsmc_exp_fd(double x) {
  * one fma. No division (fdlibm's form, kept for |x| >= 512 and NaN, divides): about 30
  * instructions where there were 70. Within 0.6 ulp (tests/test_oracle_math.py against
  * decimal). */
-WSMC_HD void wsmc_exp_entry(uint32_t j, uint64_t* sbits, double* tail) {
+WSMC_HD const uint64_t* wsmc_exp_table(void) {
     static const uint64_t t[2 * WSMC_EXP_TABLE_N] = WSMC_EXP_TAB_INIT;
+    return t;
+}
+/* WSMC_TABLES_LDS (a kernel's translation unit defines it; the kernel calls
+ * wsmc_tables_to_lds() first): the lookups read LDS copies of the log / exp tables, the same
+ * values at LDS latency instead of a vector gather through the caches */
+#if defined(WSMC_TABLES_LDS) && defined(__HIP_DEVICE_COMPILE__)
+__shared__ uint64_t wsmc_lds_exp_tab[2 * WSMC_EXP_TABLE_N];
+__shared__ double wsmc_lds_log_tab[2 * WSMC_LOG_TABLE_N];
+#endif
+WSMC_HD void wsmc_exp_entry(uint32_t j, uint64_t* sbits, double* tail) {
+#if defined(WSMC_TABLES_LDS) && defined(__HIP_DEVICE_COMPILE__)
+    *sbits = wsmc_lds_exp_tab[2 * j];
+    *tail = wsmc_bits2d(wsmc_lds_exp_tab[2 * j + 1]);
+#else
+    const uint64_t* t = wsmc_exp_table();
     *sbits = t[2 * j];
     *tail = wsmc_bits2d(t[2 * j + 1]);
+#endif
 }
 WSMC_HD double wsmc_exp(double x) {
     if (!(wsmc_fabs(x) < 512.0)) return wsmc_exp_fd(x);   /* rare: large |x|, infinities, NaN */
@@ -295,11 +311,30 @@ WSMC_HD double wsmc_exp_nd(double x) {
  * divided f / (2 + f)): about 30 instructions where there were 65. Within 0.6 ulp
  * (tests/test_oracle_math.py checks it against decimal logs). Zero, negatives, subnormals,
  * infinities and NaN take one rarely-taken branch. */
-WSMC_HD void wsmc_log_entry(uint32_t i, double* invc, double* logc) {
+WSMC_HD const double* wsmc_log_table(void) {
     static const double t[2 * WSMC_LOG_TABLE_N] = WSMC_LOG_TAB_INIT;
+    return t;
+}
+WSMC_HD void wsmc_log_entry(uint32_t i, double* invc, double* logc) {
+#if defined(WSMC_TABLES_LDS) && defined(__HIP_DEVICE_COMPILE__)
+    *invc = wsmc_lds_log_tab[2 * i];
+    *logc = wsmc_lds_log_tab[2 * i + 1];
+#else
+    const double* t = wsmc_log_table();
     *invc = t[2 * i];
     *logc = t[2 * i + 1];
+#endif
 }
+#if defined(WSMC_TABLES_LDS) && defined(__HIP_DEVICE_COMPILE__)
+/* every thread of the block copies its share of both tables, then one barrier */
+__device__ inline void wsmc_tables_to_lds(void) {
+    const double* lt = wsmc_log_table();
+    const uint64_t* et = wsmc_exp_table();
+    for (int k = (int)threadIdx.x; k < 2 * WSMC_LOG_TABLE_N; k += (int)blockDim.x) wsmc_lds_log_tab[k] = lt[k];
+    for (int k = (int)threadIdx.x; k < 2 * WSMC_EXP_TABLE_N; k += (int)blockDim.x) wsmc_lds_exp_tab[k] = et[k];
+    __syncthreads();
+}
+#endif
 WSMC_HD double wsmc_log(double x) {
     const double ln2hi = 6.93147180369123816490e-01, ln2lo = 1.90821492927058770002e-10;
     uint64_t b = wsmc_d2bits(x);

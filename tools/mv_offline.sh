@@ -12,7 +12,7 @@ import sys
 sig = open(sys.argv[1]).read().strip()
 if sig.startswith("mv:"):
     sig = sig[3:]
-src = ('#include "wsmc_mv_body.h"\n'
+src = ('#define WSMC_TABLES_LDS 1\n#include "wsmc_mv_body.h"\n'
        'struct WsmcMvSig { static constexpr wsmc::MvSig sig = ' + sig + '; };\n'
        'constexpr unsigned kMvArgsAt = (sizeof(wsmc::ProgInlineBlk) + alignof(wsmc::MvArgs) - 1) & '
        '~(unsigned)(alignof(wsmc::MvArgs) - 1);\n'

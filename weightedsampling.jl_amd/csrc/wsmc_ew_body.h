@@ -186,6 +186,9 @@ __device__ __forceinline__ void ew_body(uint64_t seed, int64_t goff, int64_t N) 
     constexpr EwSig g = S::sig;
     const EwBatch* B = (const EwBatch*)(const char*)__builtin_amdgcn_kernarg_segment_ptr();
     __shared__ unsigned long long lds4[4];
+#ifdef WSMC_TABLES_LDS
+    wsmc_tables_to_lds();   // before any log / exp (every thread: it ends in a barrier)
+#endif
     const int th = threadIdx.x;
     const int64_t t = (int64_t)blockIdx.x * kBlock + th;
     const int64_t i0 = t * P;

@@ -180,8 +180,9 @@ std::string sig_text(const EwSig& g) {
     return s;
 }
 
+const char* mv_tables_def();
 std::string tu_source(const std::string& sig) {
-    return "#include \"wsmc_ew_body.h\"\n"
+    return std::string(mv_tables_def()) + "#include \"wsmc_ew_body.h\"\n"
            "struct WsmcSig { static constexpr wsmc::EwSig sig = " + sig + "; };\n"
            "extern \"C\" __global__ __launch_bounds__(256) void wsmc_ew_p1(wsmc::EwBatch, uint64_t seed, int64_t goff, "
            "int64_t N) { wsmc::ew_body<WsmcSig, 1>(seed, goff, N); }\n"
@@ -432,9 +433,19 @@ std::string mv_waves_attr() {
     }();
     return a;
 }
+// the run-time compiled kernels (statement batches, Move blocks) read the log / exp tables from
+// LDS copies (WSMC_TABLES_LDS, include/wsmc_math.h); WSMC_DIAG_MV_TABLES_GLOBAL=1 keeps the
+// gathers through the caches, for comparison
+const char* mv_tables_def() {
+    static const bool g = [] {
+        const char* e = getenv("WSMC_DIAG_MV_TABLES_GLOBAL");
+        return e && *e && *e != '0';
+    }();
+    return g ? "" : "#define WSMC_TABLES_LDS 1\n";
+}
 std::string mv_tu(const std::string& sig) {
     const std::string lb = "__launch_bounds__(256)" + mv_waves_attr();
-    return "#include \"wsmc_mv_body.h\"\n"
+    return std::string(mv_tables_def()) + "#include \"wsmc_mv_body.h\"\n"
            "struct WsmcMvSig { static constexpr wsmc::MvSig sig = " + sig + "; };\n"
            "constexpr unsigned kMvArgsAt = (sizeof(wsmc::ProgInlineBlk) + alignof(wsmc::MvArgs) - 1) & "
            "~(unsigned)(alignof(wsmc::MvArgs) - 1);\n"

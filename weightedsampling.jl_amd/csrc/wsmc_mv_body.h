@@ -247,6 +247,9 @@ __device__ __forceinline__ void mv_body(const char* pb, const MvArgs& a) {
     static_assert(NS > 0 && NS <= kFoldSlots && D > 0 && D <= NS, "block shape");
     constexpr int W = K * kBlock;
     __shared__ unsigned long long lds4[4];
+#ifdef WSMC_TABLES_LDS
+    wsmc_tables_to_lds();   // before any log / exp (every thread: it ends in a barrier)
+#endif
     const wsmc_term* tp = reinterpret_cast<const wsmc_term*>(pb);
     const FoldSeg* segs = reinterpret_cast<const FoldSeg*>(pb + G.ntmpl * (int)sizeof(wsmc_term));
     const double* cst =
