@@ -180,9 +180,17 @@ std::string sig_text(const EwSig& g) {
     return s;
 }
 
-const char* mv_tables_def();
-std::string tu_source(const std::string& sig) {
-    return std::string(mv_tables_def()) + "#include \"wsmc_ew_body.h\"\n"
+bool tables_global();
+// the log / exp tables in LDS for a batch that draws (a Sample's normals take a log each);
+// the copy and its barrier are pure cost to a batch without draws (C3's Observe batch: 2 %)
+bool ew_tables_lds(const EwSig& g) {
+    if (tables_global()) return false;
+    for (int k = 0; k < g.nops; ++k)
+        if (g.op[k].kind == 1) return true;
+    return false;
+}
+std::string tu_source(const std::string& sig, bool lds) {
+    return std::string(lds ? "#define WSMC_TABLES_LDS 1\n" : "") + "#include \"wsmc_ew_body.h\"\n"
            "struct WsmcSig { static constexpr wsmc::EwSig sig = " + sig + "; };\n"
            "extern \"C\" __global__ __launch_bounds__(256) void wsmc_ew_p1(wsmc::EwBatch, uint64_t seed, int64_t goff, "
            "int64_t N) { wsmc::ew_body<WsmcSig, 1>(seed, goff, N); }\n"
@@ -224,8 +232,8 @@ bool compile_src(const std::string& arch, const std::string& src, std::string& c
     return true;
 }
 
-bool compile_code(const std::string& arch, const std::string& sig, std::string& code, std::string& err) {
-    return compile_src(arch, tu_source(sig), code, err);
+bool compile_code(const std::string& arch, const std::string& sig, std::string& code, std::string& err, bool lds) {
+    return compile_src(arch, tu_source(sig, lds), code, err);
 }
 
 bool device_arch(int device, std::string& arch, std::string& err) {
@@ -256,7 +264,7 @@ bool load_module(int device, const std::string& code, const char* f0, const char
     return true;
 }
 
-bool compile(int device, const std::string& sig, JitKernel& out, std::string& err) {
+bool compile(int device, const std::string& sig, JitKernel& out, std::string& err, bool lds) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
         err = "hipGetDeviceProperties failed";
@@ -265,7 +273,7 @@ bool compile(int device, const std::string& sig, JitKernel& out, std::string& er
     std::string arch = prop.gcnArchName;   // e.g. "gfx950:sramecc+:xnack-": the processor alone
     arch = arch.substr(0, arch.find(':'));
     std::string code;
-    if (!compile_code(arch, sig, code, err)) return false;
+    if (!compile_code(arch, sig, code, err, lds)) return false;
     int cur = 0;
     hipGetDevice(&cur);
     hipSetDevice(device);
@@ -314,7 +322,8 @@ hipError_t launch_ew_jit(hipStream_t s, const EwBatch& b, unsigned feat, uint64_
         C.interpreted += 1;
         return hipErrorNotSupported;
     }
-    const std::string key = sig_text(signature(b, feat));
+    const EwSig sg = signature(b, feat);
+    const std::string key = sig_text(sg);
     JitKernel* jk = nullptr;
     {
         std::lock_guard<std::mutex> lk(C.mu);
@@ -323,7 +332,7 @@ hipError_t launch_ew_jit(hipStream_t s, const EwBatch& b, unsigned feat, uint64_
             JitKernel k;
             std::string err;
             const auto t0 = std::chrono::steady_clock::now();
-            k.ok = compile(device, key, k, err);
+            k.ok = compile(device, key, k, err, ew_tables_lds(sg));
             const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
             C.compile_s += dt;
             if (k.ok) {
@@ -381,7 +390,7 @@ int ew_jit_selfcheck(std::string& err) {
         }
     }
     std::string code;
-    return compile_code("gfx950", sig_text(g), code, err) ? 0 : -1;
+    return compile_code("gfx950", sig_text(g), code, err, ew_tables_lds(g)) ? 0 : -1;
 }
 
 void ew_jit_stats(int64_t* out) {
@@ -433,19 +442,28 @@ std::string mv_waves_attr() {
     }();
     return a;
 }
-// the run-time compiled kernels (statement batches, Move blocks) read the log / exp tables from
-// LDS copies (WSMC_TABLES_LDS, include/wsmc_math.h); WSMC_DIAG_MV_TABLES_GLOBAL=1 keeps the
-// gathers through the caches, for comparison
-const char* mv_tables_def() {
+// the run-time compiled kernels whose work is transcendental-heavy read the log / exp tables
+// from LDS copies (WSMC_TABLES_LDS, include/wsmc_math.h); WSMC_DIAG_MV_TABLES_GLOBAL=1 keeps
+// the gathers through the caches everywhere, for comparison
+bool tables_global() {
     static const bool g = [] {
         const char* e = getenv("WSMC_DIAG_MV_TABLES_GLOBAL");
         return e && *e && *e != '0';
     }();
-    return g ? "" : "#define WSMC_TABLES_LDS 1\n";
+    return g;
 }
-std::string mv_tu(const std::string& sig) {
+// a Move block with bounded targets (log / exp transforms) or oscillator terms (anchors):
+// C5's blocks 158.5 -> 153.5 ms; C3's unbounded affine blocks measured 2 % slower with the copy
+bool mv_tables_lds(const MvSig& g) {
+    if (tables_global()) return false;
+    if (g.bnd) return true;
+    for (int k = 0; k < 2 * kMvSegs; ++k)
+        if (g.seg[k].kind == kSegNormalOsc) return true;
+    return false;
+}
+std::string mv_tu(const std::string& sig, bool lds) {
     const std::string lb = "__launch_bounds__(256)" + mv_waves_attr();
-    return std::string(mv_tables_def()) + "#include \"wsmc_mv_body.h\"\n"
+    return std::string(lds ? "#define WSMC_TABLES_LDS 1\n" : "") + "#include \"wsmc_mv_body.h\"\n"
            "struct WsmcMvSig { static constexpr wsmc::MvSig sig = " + sig + "; };\n"
            "constexpr unsigned kMvArgsAt = (sizeof(wsmc::ProgInlineBlk) + alignof(wsmc::MvArgs) - 1) & "
            "~(unsigned)(alignof(wsmc::MvArgs) - 1);\n"
@@ -476,7 +494,7 @@ hipError_t launch_mv_jit(hipStream_t s, const MvSig& sig, const ProgInlineBlk* p
             JitKernel k;
             std::string err, arch, code;
             const auto t0 = std::chrono::steady_clock::now();
-            k.ok = device_arch(device, arch, err) && compile_src(arch, mv_tu(key.substr(3)), code, err) &&
+            k.ok = device_arch(device, arch, err) && compile_src(arch, mv_tu(key.substr(3), mv_tables_lds(sig)), code, err) &&
                    load_module(device, code, "wsmc_mv_i", "wsmc_mv_g", k, err);
             if (k.ok) jit_dump("mv", C.mv_compiled, key, code);
             const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -534,7 +552,7 @@ int mv_jit_selfcheck(std::string& err) {
     g.seg[kMvSegs] = g.seg[0];
     g.seg[kMvSegs].mu[0].c[0] = 0;
     std::string code;
-    return compile_src("gfx950", mv_tu(mv_sig_text(g)), code, err) ? 0 : -1;
+    return compile_src("gfx950", mv_tu(mv_sig_text(g), mv_tables_lds(g)), code, err) ? 0 : -1;
 }
 
 void mv_jit_stats(int64_t* out) {
