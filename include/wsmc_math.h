@@ -315,16 +315,13 @@ WSMC_HD const double* wsmc_log_table(void) {
     static const double t[2 * WSMC_LOG_TABLE_N] = WSMC_LOG_TAB_INIT;
     return t;
 }
-WSMC_HD void wsmc_log_entry(uint32_t i, double* invc, double* logc) {
+/* the table wsmc_log reads: the LDS copy in a WSMC_TABLES_LDS translation unit, else the
+ * constant one (a kernel may also pass its own LDS copy to wsmc_log_t) */
 #if defined(WSMC_TABLES_LDS) && defined(__HIP_DEVICE_COMPILE__)
-    *invc = wsmc_lds_log_tab[2 * i];
-    *logc = wsmc_lds_log_tab[2 * i + 1];
+#define WSMC_LOG_TAB wsmc_lds_log_tab
 #else
-    const double* t = wsmc_log_table();
-    *invc = t[2 * i];
-    *logc = t[2 * i + 1];
+#define WSMC_LOG_TAB wsmc_log_table()
 #endif
-}
 #if defined(WSMC_TABLES_LDS) && defined(__HIP_DEVICE_COMPILE__)
 /* every thread of the block copies its share of both tables, then one barrier */
 __device__ inline void wsmc_tables_to_lds(void) {
@@ -335,7 +332,7 @@ __device__ inline void wsmc_tables_to_lds(void) {
     __syncthreads();
 }
 #endif
-WSMC_HD double wsmc_log(double x) {
+WSMC_HD double wsmc_log_t(double x, const double* tab) {
     const double ln2hi = 6.93147180369123816490e-01, ln2lo = 1.90821492927058770002e-10;
     uint64_t b = wsmc_d2bits(x);
     if (b - 0x0010000000000000ULL >= 0x7fe0000000000000ULL) {   /* not a positive normal */
@@ -349,8 +346,7 @@ WSMC_HD double wsmc_log(double x) {
     const uint32_t i = (uint32_t)(tmp >> 45) & (WSMC_LOG_TABLE_N - 1);
     const int k = (int32_t)(uint32_t)(tmp >> 32) >> 20;   /* (int64_t)tmp >> 52, from the high word */
     const double z = wsmc_bits2d(b - (tmp & (0xfffULL << 52)));
-    double invc, logc;
-    wsmc_log_entry(i, &invc, &logc);
+    const double invc = tab[2 * i], logc = tab[2 * i + 1];
     const double r = __builtin_fma(z, invc, -1.0);
     const double kd = (double)k;
     const double kh = kd * ln2hi;   /* exact: ln2hi has 32 trailing zero bits */
@@ -367,6 +363,7 @@ WSMC_HD double wsmc_log(double x) {
     q = __builtin_fma(q, r, -0.5);
     return hi + __builtin_fma(r * r, q, lo);
 }
+WSMC_HD double wsmc_log(double x) { return wsmc_log_t(x, WSMC_LOG_TAB); }
 
 /* log1p via the Goldberg correction (accurate to a few ulp; used for log1pexp) */
 WSMC_HD double wsmc_log1p(double x) {
@@ -650,14 +647,15 @@ WSMC_HD double wsmc_pow(double a, double b) {
 /* draws                                                                      */
 /* ------------------------------------------------------------------------- */
 /* Box–Muller pair from one Philox block: z0 = r cos(2πu2), z1 = r sin(2πu2) */
-WSMC_HD void wsmc_normal_pair(wsmc_u32x4 w, double* z0, double* z1) {
+WSMC_HD void wsmc_normal_pair_t(wsmc_u32x4 w, double* z0, double* z1, const double* logtab) {
     double u1 = wsmc_u01_open0(w.v[0], w.v[1]);
     double u2 = wsmc_u01(w.v[2], w.v[3]);
-    double r = wsmc_sqrt(-2.0 * wsmc_log(u1));
+    double r = wsmc_sqrt(-2.0 * wsmc_log_t(u1, logtab));
     double s, c;
     wsmc_sincos2pi(u2, &s, &c);
     *z0 = r * c; *z1 = r * s;
 }
+WSMC_HD void wsmc_normal_pair(wsmc_u32x4 w, double* z0, double* z1) { wsmc_normal_pair_t(w, z0, z1, WSMC_LOG_TAB); }
 /* k-th standard normal of (op, idx) */
 WSMC_HD double wsmc_normal_k(uint64_t seed, uint64_t op, uint64_t idx, uint32_t k) {
     double z0, z1;

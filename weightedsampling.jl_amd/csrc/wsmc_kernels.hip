@@ -3108,9 +3108,19 @@ __device__ __forceinline__ double aff2(double a, double b) {
 // 36 B read + 40 B write per particle. Write-through (sc1) or nontemporal 16-B stores were
 // slower (22-25 us); loading the ancestors speculatively beside the decision flag changed
 // nothing.
+#ifndef WSMC_PROP_LDS_LOG   // the draws' log table from an LDS copy (0: the cached gathers, for comparison)
+#define WSMC_PROP_LDS_LOG 1
+#endif
 template <int MODE, int IT = 1>
 __global__ __launch_bounds__(kBlock) void k_ssm2d_prop(Ssm2dArgs a) {
     __shared__ u64 lds4[4];
+    __shared__ double s_logtab[2 * WSMC_LOG_TABLE_N];
+    if (WSMC_PROP_LDS_LOG && (MODE & 1) == 0) {   // every thread, before the first draw
+        const double* lt = wsmc_log_table();
+        for (int k = (int)threadIdx.x; k < 2 * WSMC_LOG_TABLE_N; k += kBlock) s_logtab[k] = lt[k];
+        __syncthreads();
+    }
+    const double* logtab = WSMC_PROP_LDS_LOG ? s_logtab : wsmc_log_table();
     const int64_t N = a.N;
     bool rs;
     double mean;
@@ -3201,7 +3211,8 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_prop(Ssm2dArgs a) {
         if ((MODE & 1) == 0) {
 #pragma unroll
             for (int k = 0; k < 2; ++k)
-                wsmc_normal_pair(wsmc_rng_block(a.seed, op_dv, (uint64_t)(a.goff + i0 + k), 0u), &z[k][0], &z[k][1]);
+                wsmc_normal_pair_t(wsmc_rng_block(a.seed, op_dv, (uint64_t)(a.goff + i0 + k), 0u), &z[k][0], &z[k][1],
+                                   logtab);
         }
         d2 xn[2], vn[2], dvv[2];
         double wn[2];
