@@ -215,26 +215,22 @@ WSMC_HD const uint64_t* wsmc_exp_table(void) {
 __shared__ uint64_t wsmc_lds_exp_tab[2 * WSMC_EXP_TABLE_N];
 __shared__ double wsmc_lds_log_tab[2 * WSMC_LOG_TABLE_N];
 #endif
-WSMC_HD void wsmc_exp_entry(uint32_t j, uint64_t* sbits, double* tail) {
+/* the table wsmc_exp reads (as WSMC_LOG_TAB for the log) */
 #if defined(WSMC_TABLES_LDS) && defined(__HIP_DEVICE_COMPILE__)
-    *sbits = wsmc_lds_exp_tab[2 * j];
-    *tail = wsmc_bits2d(wsmc_lds_exp_tab[2 * j + 1]);
+#define WSMC_EXP_TAB wsmc_lds_exp_tab
 #else
-    const uint64_t* t = wsmc_exp_table();
-    *sbits = t[2 * j];
-    *tail = wsmc_bits2d(t[2 * j + 1]);
+#define WSMC_EXP_TAB wsmc_exp_table()
 #endif
-}
-WSMC_HD double wsmc_exp(double x) {
+WSMC_HD double wsmc_exp_t(double x, const uint64_t* tab) {
     if (!(wsmc_fabs(x) < 512.0)) return wsmc_exp_fd(x);   /* rare: large |x|, infinities, NaN */
     const double shift = 6755399441055744.0;              /* 0x1.8p52: z + shift rounds z to an integer */
     const double kd0 = x * WSMC_EXP_INVLN2N + shift;
     const uint64_t ki = wsmc_d2bits(kd0);
     const double kd = kd0 - shift;
     const double r = (x - kd * WSMC_EXP_LN2HIN) - kd * WSMC_EXP_LN2LON;   /* kd * hi exact */
-    uint64_t sb;
-    double tail;
-    wsmc_exp_entry((uint32_t)ki & (WSMC_EXP_TABLE_N - 1), &sb, &tail);
+    const uint32_t j = (uint32_t)ki & (WSMC_EXP_TABLE_N - 1);
+    const uint64_t sb = tab[2 * j];
+    const double tail = wsmc_bits2d(tab[2 * j + 1]);
     const double scale = wsmc_bits2d(sb + (ki << 45));
     const double r2 = r * r;
     const double p = __builtin_fma(r, WSMC_K(0.16666666666666666), 0.5) +
@@ -242,6 +238,7 @@ WSMC_HD double wsmc_exp(double x) {
     const double tmp = tail + (r + r2 * p);
     return __builtin_fma(scale, tmp, scale);
 }
+WSMC_HD double wsmc_exp(double x) { return wsmc_exp_t(x, WSMC_EXP_TAB); }
 
 /*
  * exp(x) for the Resample statistics, x = lw - M <= 0 (include/wsmc_math.h wsmc_qparts):
@@ -795,13 +792,14 @@ WSMC_HD double wsmc_osc_rolled(double ta, double d, int m, double A, double om, 
 /* ------------------------------------------------------------------------- */
 /* bound transforms of RW/autoRW (src/move_kernels.jl:37-85)                  */
 /* ------------------------------------------------------------------------- */
-WSMC_HD double wsmc_to_unc(double x, double lo, double hi) {
+WSMC_HD double wsmc_to_unc_t(double x, double lo, double hi, const double* logtab) {
     int flo = wsmc_isfinite(lo), fhi = wsmc_isfinite(hi);
-    if (flo && fhi) return wsmc_log(x - lo) - wsmc_log(hi - x);
-    if (flo) return wsmc_log(x - lo);
-    if (fhi) return wsmc_log(hi - x);
+    if (flo && fhi) return wsmc_log_t(x - lo, logtab) - wsmc_log_t(hi - x, logtab);
+    if (flo) return wsmc_log_t(x - lo, logtab);
+    if (fhi) return wsmc_log_t(hi - x, logtab);
     return x;
 }
+WSMC_HD double wsmc_to_unc(double x, double lo, double hi) { return wsmc_to_unc_t(x, lo, hi, WSMC_LOG_TAB); }
 WSMC_HD double wsmc_from_unc(double z, double lo, double hi) {
     int flo = wsmc_isfinite(lo), fhi = wsmc_isfinite(hi);
     if (flo && fhi) return lo + (hi - lo) / (1.0 + wsmc_exp(-z));

@@ -2281,6 +2281,31 @@ __global__ __launch_bounds__(kBlock) void k_moments1(const double* __restrict__ 
     // a fused Resample's weight reset still pending (the next Observe applies it): the
     // weights are its log-mean, all equal (the max slots already hold it)
     const bool reset = wreset && wreset->resampled;
+    // the log / exp tables from LDS copies for the 3- and 4-target passes when they evaluate
+    // them per particle (bounded targets, weights not reset): C5's 4-target pass, 154.3 ->
+    // 152.1 ms a run on one box; C3's 2-target pass measured 3 % slower with the copy's LDS
+    // and barrier in the kernel, so it keeps the cached gathers (uniform branch)
+#ifndef WSMC_MOM_LDS_TABLES   // 0: the cached gathers everywhere, for comparison
+#define WSMC_MOM_LDS_TABLES 1
+#endif
+    constexpr bool kLds = WSMC_MOM_LDS_TABLES && D >= 3;
+    __shared__ double s_logtab[kLds ? 2 * WSMC_LOG_TABLE_N : 1];
+    __shared__ uint64_t s_exptab[kLds ? 2 * WSMC_EXP_TABLE_N : 1];
+    if constexpr (kLds) {
+        bool bnd = false;
+#pragma unroll
+        for (int k = 0; k < D; ++k) bnd = bnd || wsmc_isfinite(ma.lo[k]) || wsmc_isfinite(ma.hi[k]);
+        if (bnd || !reset) {
+            const double* lt = wsmc_log_table();
+            const uint64_t* et = wsmc_exp_table();
+            for (int k = (int)threadIdx.x; k < 2 * WSMC_LOG_TABLE_N; k += kBlock) s_logtab[k] = lt[k];
+            for (int k = (int)threadIdx.x; k < 2 * WSMC_EXP_TABLE_N; k += kBlock) s_exptab[k] = et[k];
+            __syncthreads();
+        }
+    }
+    // read only when filled: without bounds to_unc takes no log, with the reset no exp is taken
+    const double* logtab = kLds ? (const double*)s_logtab : wsmc_log_table();
+    const uint64_t* exptab = kLds ? (const uint64_t*)s_exptab : wsmc_exp_table();
     // all equal: one exp for the block (the same bits every particle's would give)
     const double er = reset ? wsmc_exp(wreset->mean - M) : 0.0;
     // targets one lazy Resample behind (lg.mask): read through its ancestors, gated by its
@@ -2351,10 +2376,10 @@ __global__ __launch_bounds__(kBlock) void k_moments1(const double* __restrict__ 
 #pragma unroll
         for (int v = 0; v < NV; ++v) vals[v] = 0.0;
         if (i < N) {
-            const double e = reset ? er : wsmc_exp(wv[c] - M);
+            const double e = reset ? er : wsmc_exp_t(wv[c] - M, exptab);
             double dz[4];
 #pragma unroll
-            for (int k = 0; k < d; ++k) dz[k] = wsmc_to_unc(xv[c][k], ma.lo[k], ma.hi[k]) - p[k];
+            for (int k = 0; k < d; ++k) dz[k] = wsmc_to_unc_t(xv[c][k], ma.lo[k], ma.hi[k], logtab) - p[k];
             vals[0] = e;
 #pragma unroll
             for (int k = 0; k < d; ++k) vals[1 + k] = e * dz[k];
