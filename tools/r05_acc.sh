@@ -1,0 +1,5 @@
+set -o pipefail
+O=gpurun_out/$1; mkdir -p $O
+timeout -k 10 1000 python -u -m pytest tests -q -m gpu -x --timeout 600 --timeout-method thread > $O/pytest_gpu.txt 2>&1 || { tail -40 $O/pytest_gpu.txt; exit 1; }
+tail -1 $O/pytest_gpu.txt
+bash tools/ab_env.sh $1_ab WSMC_DIAG_MV_K1=0 c5 c5async c3gated

@@ -673,7 +673,7 @@ int wsmc_create(wsmc_ctx** out, int64_t n_particles, int32_t device, uint64_t se
     ALLOC(c->dec_always, sizeof(Decision));
     ALLOC(c->mom, sizeof(double) * 128);   // [64..128): a Move block's factors
     ALLOC(c->dflag, sizeof(int32_t) * 4);
-    ALLOC(c->ucount, sizeof(unsigned long long) * 4);
+    ALLOC(c->ucount, sizeof(unsigned long long) * (4 * kAccMove + 4));
     ALLOC(c->d_colptr, sizeof(double*) * kMaxCols);
     ALLOC(c->run_params, sizeof(uint64_t) * 8);
 #undef ALLOC
@@ -2982,7 +2982,7 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
     unsigned long long* zcount = accepted_out ? c->ucount : nullptr;
     if (proposal != WSMC_PROPOSAL_AUTORW || is_sharded(c)) {
         if (zflag) WSMC_HIP(hipMemsetAsync(zflag, 0, sizeof(int32_t) * 4, c->stream));
-        if (zcount) WSMC_HIP(hipMemsetAsync(zcount, 0, sizeof(unsigned long long) * 4, c->stream));
+        if (zcount) WSMC_HIP(hipMemsetAsync(zcount, 0, sizeof(unsigned long long) * 4 * kAccMove, c->stream));
     }
     if (proposal == WSMC_PROPOSAL_AUTORW && is_sharded(c)) {
         if (c->w_reset_pending) {   // the sharded max pass reads the weights
@@ -3169,7 +3169,9 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         unsigned long long acc[4];
     }* hb = reinterpret_cast<decltype(hb)>(c->pinned);
     WSMC_HIP(hipMemcpyAsync(hb->flag, c->dflag, sizeof(int32_t) * 4, hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipMemcpyAsync(hb->acc, c->ucount, sizeof(unsigned long long) * 4, hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(launch_acc_sum(c->stream, c->ucount, c->ucount + 4 * kAccMove));
+    WSMC_HIP(hipMemcpyAsync(hb->acc, c->ucount + 4 * kAccMove, sizeof(unsigned long long) * 4, hipMemcpyDeviceToHost,
+                            c->stream));
     WSMC_HIP(ctx_sync(c, c->stream));
     if (hb->flag[0]) return fail(WSMC_ENOTPD, "autoRW proposal covariance is not positive definite");
     c->dflag_zero = true;
@@ -3243,12 +3245,15 @@ static int move_block_each(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, 
     return WSMC_OK;
 }
 
-// WSMC_DIAG_MV_K1=1: oscillator (heavy) blocks compiled one particle a thread, as the
-// interpreter runs them (two a thread by default: the run loop's per-term control is shared)
+// oscillator (heavy) blocks compiled one particle a thread. Round 4 measured two a thread
+// faster (the run loop's per-term control shared: 0.242 -> 0.235 s); with the loop reduced to a
+// rotation and a score per term and the log / exp tables in LDS, the halved registers win:
+// C5 151.7 -> 143.9 ms asynchronous on one box (round 5, tools/ab_env.sh). WSMC_DIAG_MV_K1=0
+// compiles two a thread, for comparison
 static bool mv_heavy_k1() {
     static const bool v = [] {
         const char* e = getenv("WSMC_DIAG_MV_K1");
-        return e && atoi(e) != 0;
+        return !(e && *e && atoi(e) == 0);
     }();
     return v;
 }
@@ -3595,7 +3600,9 @@ static int move_block_fused(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs,
         unsigned long long acc[4];
     }* hb = reinterpret_cast<decltype(hb)>(c->pinned);
     WSMC_HIP(hipMemcpyAsync(hb->flag, c->dflag, sizeof(int32_t) * 4, hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(hipMemcpyAsync(hb->acc, c->ucount, sizeof(unsigned long long) * 4, hipMemcpyDeviceToHost, c->stream));
+    WSMC_HIP(launch_acc_sum(c->stream, c->ucount, c->ucount + 4 * kAccMove));
+    WSMC_HIP(hipMemcpyAsync(hb->acc, c->ucount + 4 * kAccMove, sizeof(unsigned long long) * 4, hipMemcpyDeviceToHost,
+                            c->stream));
     WSMC_HIP(ctx_sync(c, c->stream));
     for (int32_t m = 0; m < n; ++m) accepted_out[m] = (int64_t)hb->acc[m];
     if (hb->flag[0]) return fail(WSMC_ENOTPD, "autoRW proposal covariance is not positive definite");

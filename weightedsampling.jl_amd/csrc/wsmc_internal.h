@@ -280,7 +280,7 @@ struct wsmc_ctx {
     wsmc::Decision* dec = nullptr;          // [1] decision of one generic resample
     double* mom = nullptr;                  // [64] moment / covariance / Cholesky results
     int32_t* dflag = nullptr;               // [4] device error flags
-    unsigned long long* ucount = nullptr;   // [4] device counters
+    unsigned long long* ucount = nullptr;   // 4 moves x kAccSlots line-separated count slots, then [4] sums
     void* pinned = nullptr;                 // 4 KB pinned staging
     int64_t ntiles = 0;      // canonical-sum tiles (2048)
     int64_t nrstiles = 0;    // resample tiles (1024)
@@ -525,6 +525,7 @@ hipError_t launch_autorw_moments(hipStream_t s, const double* w, const MaxSlots*
                                  const Decision* wreset = nullptr, const Decision* gate = nullptr,
                                  const int32_t* lag_anc = nullptr, const Decision* lag_dec = nullptr, int lag_mask = 0,
                                  int32_t* zflag = nullptr, unsigned long long* zcount = nullptr);
+hipError_t launch_acc_sum(hipStream_t s, const unsigned long long* acc, unsigned long long* out);
 hipError_t launch_autorw_final(hipStream_t s, const double* tilepart, int64_t ntiles, int d, double min_step,
                                double* mom, int32_t* flag, int raw, const Decision* gate = nullptr);
 hipError_t launch_autorw_publish(hipStream_t s, const MaxSlots* ms, double* const* cols, const int32_t* tcols, int d,

@@ -2272,9 +2272,9 @@ __global__ __launch_bounds__(kBlock) void k_moments1(const double* __restrict__ 
     __shared__ double lds4[4];
     // the Move block's flag words and accepted counters, zeroed here rather than by two memset
     // launches (the combine and the Move kernel, which use them, run after this kernel)
-    if (blockIdx.x == 0 && threadIdx.x < 4) {
-        if (z.count) z.count[threadIdx.x] = 0;
-        if (z.flag) z.flag[threadIdx.x] = 0;
+    if (blockIdx.x == 0) {   // 4 moves x 64 count slots: one a thread
+        if (z.count) *acc_slot(z.count, (int)threadIdx.x / kAccSlots, threadIdx.x) = 0;
+        if (z.flag && threadIdx.x < 4) z.flag[threadIdx.x] = 0;
     }
     if (gate && !gate->resampled) return;   // a gated Move that does not run
     const double M = wave_slots_max(ms);
@@ -2534,7 +2534,7 @@ __global__ __launch_bounds__(kBlock) void k_move(const wsmc_term* tape, int32_t 
         scache[i] = acc ? s_new : s_old;
     }
     acc = block_sum_u64(acc, lds4);
-    if (threadIdx.x == 0 && acc) atomicAdd(accepted, acc);
+    if (threadIdx.x == 0 && acc) atomicAdd(acc_slot(accepted, 0, blockIdx.x), acc);
 }
 
 // The same Move over a compiled tape: the host renumbers every (column, component) the
@@ -2798,7 +2798,7 @@ __device__ __forceinline__ void move_c_body(const wsmc_term* ctape, const FoldSl
         mc.out[gi[p]] = a ? sn[p] : so[p];
     }
     acc = block_sum_u64(acc, lds4);
-    if (threadIdx.x == 0 && acc) atomicAdd(accepted, acc);
+    if (threadIdx.x == 0 && acc) atomicAdd(acc_slot(accepted, 0, blockIdx.x), acc);
 }
 template <int K, int LEAN>
 __global__ __launch_bounds__(kBlock) void k_move_c(const wsmc_term* ctape, FoldSlots fs, MomArgs ma, int d,
@@ -3048,7 +3048,7 @@ __device__ __forceinline__ void move_blk_body(const wsmc_term* ctape, const Fold
         }
         if (accepted) {   // uniform
             acc = block_sum_u64(acc, lds4);
-            if (th == 0 && acc) atomicAdd(accepted + m, acc);
+            if (th == 0 && acc) atomicAdd(acc_slot(accepted, m, blockIdx.x), acc);
         }
     }
     const int D = mb.off[nm];
@@ -3480,6 +3480,15 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_final(Ssm2dFinal f) {
 #pragma unroll
     for (int p = 0; p < P; ++p) x1[p] = d2{f.x0[0], f.x0[1]};
     put(f.hist_out[1], x1);
+}
+
+// the 4 moves' accepted counts from their 64 slots each (one wave a move, DPP-free shuffles)
+__global__ __launch_bounds__(kBlock) void k_acc_sum(const u64* __restrict__ acc, u64* __restrict__ out) {
+    const int m = threadIdx.x >> 6, s = threadIdx.x & 63;
+    u64 v = acc[(size_t)m * kAccMove + (size_t)s * kAccStride];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (s == 0) out[m] = v;
 }
 
 // ------------------------------------------------------------------------------------
@@ -3992,6 +4001,10 @@ hipError_t launch_autorw_moments(hipStream_t s, const double* w, const MaxSlots*
         case 3: hipLaunchKernelGGL(k_moments1<3>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart, wreset, gate, lg, z); break;
         default: hipLaunchKernelGGL(k_moments1<4>, tiles_for(N), dim3(kBlock), 0, s, w, ms, cols, ma, pv, N, nt, tilepart, wreset, gate, lg, z); break;
     }
+    return hipGetLastError();
+}
+hipError_t launch_acc_sum(hipStream_t s, const u64* acc, u64* out) {
+    hipLaunchKernelGGL(k_acc_sum, dim3(1), dim3(kBlock), 0, s, acc, out);
     return hipGetLastError();
 }
 hipError_t launch_autorw_final(hipStream_t s, const double* tilepart, int64_t ntiles, int d, double min_step,

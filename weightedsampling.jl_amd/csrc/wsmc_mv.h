@@ -7,6 +7,14 @@
 
 namespace wsmc {
 
+// A Move's accepted count: 64 line-separated slots per move (block b adds into slot b mod 64;
+// one address for every block serialised the atomics: 15.6k blocks of a 4M Move at one
+// particle a thread cost 40 us a Move), summed by launch_acc_sum before the host reads them
+constexpr int kAccSlots = 64, kAccStride = 16, kAccMove = kAccSlots * kAccStride;
+__host__ __device__ inline unsigned long long* acc_slot(unsigned long long* acc, int m, unsigned block) {
+    return acc + (size_t)m * kAccMove + (size_t)(block % kAccSlots) * kAccStride;
+}
+
 // Move over a compiled tape (operands renumbered to slots; the targets are slots 0..d-1)
 constexpr int kFoldSlots = 16;
 struct FoldSlots {

@@ -343,7 +343,7 @@ __device__ __forceinline__ void mv_body(const char* pb, const MvArgs& a) {
         }
         if (a.accepted) {   // uniform
             acc = mv_block_sum(acc, lds4);
-            if (th == 0 && acc) atomicAdd(a.accepted + m, acc);
+            if (th == 0 && acc) atomicAdd(acc_slot(a.accepted, m, blockIdx.x), acc);
         }
     }
 #pragma unroll
