@@ -2284,7 +2284,8 @@ __global__ __launch_bounds__(kBlock) void k_moments1(const double* __restrict__ 
     // the log / exp tables from LDS copies for the 3- and 4-target passes when they evaluate
     // them per particle (bounded targets, weights not reset): C5's 4-target pass, 154.3 ->
     // 152.1 ms a run on one box; C3's 2-target pass measured 3 % slower with the copy's LDS
-    // and barrier in the kernel, so it keeps the cached gathers (uniform branch)
+    // and barrier in the kernel, so it keeps the cached gathers (uniform branch); the 1-target
+    // pass with the copies measured even (C5 143.8 ms either way, round 5)
 #ifndef WSMC_MOM_LDS_TABLES   // 0: the cached gathers everywhere, for comparison
 #define WSMC_MOM_LDS_TABLES 1
 #endif
