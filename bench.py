@@ -46,14 +46,49 @@ import numpy as np  # noqa: E402
 METRIC = json.loads((REPO / "BASELINE.json").read_text())["metric"] if (REPO / "BASELINE.json").exists() else \
     "particle-steps/sec (N_particles × T_steps / wall-s), 2D SSM bootstrap filter"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-PROP_BYTES_STEADY = 76         # propagate kernel, per particle, 2 <= t < T after a resample
-PROP_BYTES_FIRST = 48          # step 1: x0/v0 are constants (write x, v, w)
+PROP_BYTES_STEADY = 84         # propagate kernel, per particle, 2 <= t < T after a resample: 76 of the model's
+                               # state + 8 of q, its Resample statistics taken in the same pass
+PROP_BYTES_FIRST = 56          # step 1: x0/v0 are constants (read w, write x, v, w, and w for a replay)
 PROP_BYTES_LAST_DV = 16        # dv is stored at the last step only
 STEP_BYTES = 104               # whole step algorithmic bytes
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+# ---- the multi-GPU line's own parity proof ----------------------------
+CHECK_PARTICLES = 65536   # per GPU
+CHECK_T = 8
+
+
+def state_digests(ctx, lo, hi):
+    """xxh3-64 of the weights and of every column (name order) over particles [lo, hi) of the
+    context's view, plus the log evidence's bits: the fingerprint two runs must share."""
+    import xxhash
+    h = xxhash.xxh3_64()
+    for name in sorted(ctx.col_names()):
+        a = ctx.col_download(ctx.col_find(name))
+        h.update(name.encode())
+        h.update(np.ascontiguousarray(a[..., lo:hi]).tobytes())
+    h.update(np.ascontiguousarray(ctx.weights_download()[lo:hi]).tobytes())
+    return h.hexdigest()
+
+
+def check_verdict(ref, got, ev_ref, ev_got):
+    """ref / got: per-shard digests of the one-GPU context and of the sharded run; the sharded
+    line stands only if every shard and the evidence are bit-identical."""
+    bad = [g for g, (a, b) in enumerate(zip(ref, got)) if a != b]
+    ok = not bad and len(ref) == len(got) and ev_ref == ev_got
+    return {"exact_vs_1gpu": ok, "mismatched_shards": bad, "evidence_equal": ev_ref == ev_got,
+            "digests": got}
+
+
+def refuse_on_mismatch(verdict):
+    if not verdict["exact_vs_1gpu"]:
+        log(f"bench: the sharded run differs from one GPU (shards {verdict['mismatched_shards']}, "
+            f"evidence equal: {verdict['evidence_equal']}): refusing the line")
+        sys.exit(2)
 
 
 def parse():
@@ -94,6 +129,12 @@ def parse():
     # in-process exchange (wsmc_create_multi, transport HOST): the sharded run's device path
     # with a memcpy for a collective (the one-GPU stand-in for RCCL between ranks); N per shard
     ap.add_argument("--multi-shards", type=int, default=0)
+    # a sharded line first proves itself: an exact-shard run of CHECK_PARTICLES a GPU x CHECK_T
+    # steps against one context holding that population (digests of every column and weight)
+    ap.add_argument("--no-self-check", action="store_true")
+    # every stream wait of a sharded run is bounded (wsmc_comm_set_timeout: the communicator is
+    # aborted and the run exits non-zero), and the whole process by the double of it
+    ap.add_argument("--watchdog", type=float, default=120.0)
     ap.add_argument("--statements", action="store_true")
     ap.add_argument("--eager-store", action="store_true")
     return ap.parse_args()
@@ -280,6 +321,62 @@ def cpu_baseline_1t(obs, n, T, ess, scheme, seed):
     return n * T / dt, dt
 
 
+def sharded_self_check(args, wsmc, abi, comm, rank, world, local, lay, G, obs, scheme):
+    """Before a sharded line is timed: the same population of CHECK_PARTICLES a GPU, CHECK_T steps,
+    once on exact shards over the line's own layout and transport, once on one context; the
+    shards' digests (state_digests) and the evidence must be bit-identical."""
+    n = CHECK_PARTICLES
+    gn = n * G
+    kw = dict(ess_perc_min=args.ess, scheme=scheme if scheme != abi.RESAMPLE_MULTINOMIAL else abi.RESAMPLE_STRATIFIED,
+              keep_history=True)
+    o = obs[:CHECK_T]
+    info = {"particles": gn, "T": CHECK_T, "shard_mode": "exact"}
+    if comm is None:   # one process: a multi-device handle, or shards on GPU 0 (host transport)
+        devs = lay["devices"] if lay["mode"] == "in-process" else [0] * G
+        tr = abi.TRANSPORT_RCCL if lay["mode"] == "in-process" else abi.TRANSPORT_HOST
+        ref = wsmc.Context(gn, seed=args.seed, device=devs[0])
+        ev_ref = ref.ssm2d_run(o, **kw)
+        dref = [state_digests(ref, g * n, (g + 1) * n) for g in range(G)]
+        ref.close()
+        m = wsmc.Context.multi(gn, G, seed=args.seed, devices=devs, transport=tr)
+        m.comm_set_shard_mode(abi.SHARD_EXACT)
+        if tr == abi.TRANSPORT_RCCL and args.watchdog > 0:
+            m.comm_set_timeout(args.watchdog)
+        ev = m.ssm2d_run(o, **kw)
+        dgot = [state_digests(m, g * n, (g + 1) * n) for g in range(G)]
+        m.close()
+        info.update(check_verdict(dref, dgot, ev_ref, ev))
+        info["transport"] = "rccl" if tr == abi.TRANSPORT_RCCL else "host"
+        return info
+    # a launcher's ranks: each runs its shard; rank 0 also the one-GPU population
+    c = wsmc.Context(n, seed=args.seed, device=0 if args.same_device else local)
+    if args.exchange == "host":
+        c.comm_init_host(comm.allgather, world, rank, rank * n, gn)
+    else:
+        uid = comm.broadcast(wsmc.Context.comm_unique_id() if rank == 0 else None)
+        c.comm_init(uid, world, rank, rank * n, gn)
+        if args.watchdog > 0:
+            c.comm_set_timeout(args.watchdog)
+    c.comm_set_shard_mode(abi.SHARD_EXACT)
+    ev = c.ssm2d_run(o, **kw)
+    mine = state_digests(c, 0, n)
+    c.close()
+    got = comm.allgather([mine, ev])
+    verdict = None
+    if rank == 0:
+        ref = wsmc.Context(gn, seed=args.seed, device=0 if args.same_device else local)
+        ev_ref = ref.ssm2d_run(o, **kw)
+        dref = [state_digests(ref, g * n, (g + 1) * n) for g in range(world)]
+        ref.close()
+        verdict = check_verdict(dref, [g[0] for g in got], ev_ref, got[0][1])
+        if any(g[1] != got[0][1] for g in got):
+            verdict["exact_vs_1gpu"] = False
+    verdict = json.loads(comm.broadcast(json.dumps(verdict) if rank == 0 else None))   # (hostcomm sends no dicts)
+    info.update(verdict)
+    info["transport"] = args.exchange
+    return info
+
+
 def main():
     args = parse()
     # stdout carries the one JSON line only: native libraries write to fd 1 too (RCCL prints
@@ -369,6 +466,22 @@ def main():
     if (inproc or comm is not None) and args.exchange == "rccl" and ranks["rccl_ranks"] != G:
         log(f"bench: the RCCL communicator reports {ranks['rccl_ranks']} ranks, --gpus {G}: refusing the line")
         sys.exit(2)
+    sharded = inproc or comm is not None or args.multi_shards > 1
+    if sharded and args.watchdog > 0:
+        import faulthandler
+        # the process as a whole: a hang anywhere (a host exchange included) ends it with the
+        # Python stacks on stderr; a collective's own wait is bounded below it
+        faulthandler.dump_traceback_later(2 * args.watchdog + 60 * (args.steps + args.warmup) * T / 100, exit=True)
+        if args.exchange == "rccl" or inproc:
+            ctx.comm_set_timeout(args.watchdog)
+
+    self_check = None
+    if sharded and not args.no_self_check:
+        S = G if inproc else args.multi_shards if args.multi_shards > 1 else world   # shards
+        self_check = sharded_self_check(args, wsmc, abi, comm, rank, world, local, lay, S, obs, scheme)
+        refuse_on_mismatch(self_check)
+        log(f"bench: self-check passed (exact shards x{S} == one GPU, {self_check['particles']} particles, "
+            f"T={CHECK_T})")
     if os.environ.get("WSMC_DUMP_MAPS"):   # diagnostics: the load map, to symbolise a crash's raw frames
         with open(os.environ["WSMC_DUMP_MAPS"], "w") as f:
             f.write(open("/proc/self/maps").read())
@@ -562,6 +675,8 @@ def main():
         }
         if xst is not None:
             line["exact_stats"] = xst
+        if self_check is not None:
+            line["self_check"] = self_check
         os.write(json_fd, (json.dumps(line) + "\n").encode())
     ctx.close()
     if comm is not None:

@@ -192,6 +192,11 @@ int wsmc_comm_init_host(wsmc_ctx* ctx, wsmc_exchange_fn exchange, void* user, in
  * across ranks); multinomial draws on exact shards return WSMC_EARG. */
 typedef enum { WSMC_SHARD_ISLAND = 0, WSMC_SHARD_EXACT = 1 } wsmc_shard_mode;
 int wsmc_comm_set_shard_mode(wsmc_ctx* ctx, int32_t mode);
+/* A watchdog on every wait for the context's stream (each shard's, on a multi-device handle)
+ * while it holds an RCCL communicator: a wait longer than `seconds` (a collective whose peer
+ * never arrives) aborts the communicator (ncclCommAbort) and the call returns WSMC_ERCCL, so a
+ * lost rank ends the job instead of hanging the node. 0 (the default) waits without bound. */
+int wsmc_comm_set_timeout(wsmc_ctx* ctx, double seconds);
 /* What a context (or a multi-device handle) is sharded over, as the communicator itself
  * reports it — for a benchmark line that must say how many devices it measured (no reference
  * counterpart: the reference is single-threaded, /root/reference/TODO.md:28).
@@ -445,6 +450,12 @@ int wsmc_debug_mv_jit_stats(int64_t* stats_out);
 /* Compile a representative Move block (C3's shape) for gfx950 without a device: WSMC_OK, or
  * WSMC_EHIP with hiprtc's log in wsmc_last_error(). */
 int wsmc_debug_mv_jit_selfcheck(void);
+/* The fused 2D-SSM run's Resample statistics, cumulative over the context's
+ * runs: stats_out[0] = the steps whose propagate guessed the reference point wrong (one GPU: found
+ * by the fill; sharded: recomputed in place, k_rs_qfix), stats_out[1] = where the statistics are
+ * taken (0 = their own kernel, 1 = the propagate with q stored, 2 = the propagate, the fill
+ * recomputing q), stats_out[2] = the runs re-done on the exact path after a miss (one GPU). */
+int wsmc_debug_run_stats(wsmc_ctx* ctx, int64_t* stats_out);
 
 #ifdef __cplusplus
 }

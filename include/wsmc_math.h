@@ -214,9 +214,24 @@ WSMC_HD const uint64_t* wsmc_exp_table(void) {
 #if defined(WSMC_TABLES_LDS) && defined(__HIP_DEVICE_COMPILE__)
 __shared__ uint64_t wsmc_lds_exp_tab[2 * WSMC_EXP_TABLE_N];
 __shared__ double wsmc_lds_log_tab[2 * WSMC_LOG_TABLE_N];
+#ifdef WSMC_LDS_TABLE_CHECK
+/* the check build: every entry point of a WSMC_TABLES_LDS translation unit must call
+ * wsmc_tables_to_lds() before its first log / exp. wsmc_tables_to_lds marks the copies ready; a
+ * lookup that finds them unmarked reports the kernel once a block (printf) and reads the constant
+ * tables instead, so the mistake shows in the log and not as wrong values. */
+__shared__ uint32_t wsmc_lds_tab_ready;
+#define WSMC_LDS_TAB_READY 0x7AB1E5u
+__device__ inline bool wsmc_lds_tabs_ok(void) {
+    if (wsmc_lds_tab_ready == WSMC_LDS_TAB_READY) return true;
+    if (threadIdx.x == 0) printf("wsmc: log/exp table lookup before wsmc_tables_to_lds() (block %u)\n", blockIdx.x);
+    return false;
+}
+#endif
 #endif
 /* the table wsmc_exp reads (as WSMC_LOG_TAB for the log) */
-#if defined(WSMC_TABLES_LDS) && defined(__HIP_DEVICE_COMPILE__)
+#if defined(WSMC_TABLES_LDS) && defined(__HIP_DEVICE_COMPILE__) && defined(WSMC_LDS_TABLE_CHECK)
+#define WSMC_EXP_TAB (wsmc_lds_tabs_ok() ? wsmc_lds_exp_tab : wsmc_exp_table())
+#elif defined(WSMC_TABLES_LDS) && defined(__HIP_DEVICE_COMPILE__)
 #define WSMC_EXP_TAB wsmc_lds_exp_tab
 #else
 #define WSMC_EXP_TAB wsmc_exp_table()
@@ -314,7 +329,9 @@ WSMC_HD const double* wsmc_log_table(void) {
 }
 /* the table wsmc_log reads: the LDS copy in a WSMC_TABLES_LDS translation unit, else the
  * constant one (a kernel may also pass its own LDS copy to wsmc_log_t) */
-#if defined(WSMC_TABLES_LDS) && defined(__HIP_DEVICE_COMPILE__)
+#if defined(WSMC_TABLES_LDS) && defined(__HIP_DEVICE_COMPILE__) && defined(WSMC_LDS_TABLE_CHECK)
+#define WSMC_LOG_TAB (wsmc_lds_tabs_ok() ? wsmc_lds_log_tab : wsmc_log_table())
+#elif defined(WSMC_TABLES_LDS) && defined(__HIP_DEVICE_COMPILE__)
 #define WSMC_LOG_TAB wsmc_lds_log_tab
 #else
 #define WSMC_LOG_TAB wsmc_log_table()
@@ -326,6 +343,9 @@ __device__ inline void wsmc_tables_to_lds(void) {
     const uint64_t* et = wsmc_exp_table();
     for (int k = (int)threadIdx.x; k < 2 * WSMC_LOG_TABLE_N; k += (int)blockDim.x) wsmc_lds_log_tab[k] = lt[k];
     for (int k = (int)threadIdx.x; k < 2 * WSMC_EXP_TABLE_N; k += (int)blockDim.x) wsmc_lds_exp_tab[k] = et[k];
+#ifdef WSMC_LDS_TABLE_CHECK
+    if (threadIdx.x == 0) wsmc_lds_tab_ready = WSMC_LDS_TAB_READY;
+#endif
     __syncthreads();
 }
 #endif
@@ -503,22 +523,38 @@ WSMC_HD double wsmc_rem_pio2_large(double ax, int* n) {
 }
 #define WSMC_PIO2_LARGE 823549.0                   /* < 2^19 pi/2: Cody-Waite below, Payne-Hanek above */
 
-/* cos(x) by the Cody–Waite reduction alone, for the damped-oscillator phase w t + p (its mean and
- * the rotation anchors, wsmc_sincos): exact below WSMC_PIO2_LARGE (2^19 pi/2 = 8.2e5 rad), NaN past
- * it — a phase that large makes the term's log-density NaN (no weight, a rejected proposal) rather
- * than a silently wrong value. The fold kernels keep the reduction inline and small this way; the
- * general operators below reduce exactly at any |x|. */
-WSMC_HD double wsmc_cos_cw(double x) {
+/* The oscillator phase's reduction (wsmc_cos_cw, wsmc_sincos), inline and branch-free: the
+ * three-part Cody–Waite form below WSMC_PIO2_LARGE (2^19 pi/2 = 8.2e5 rad; the values of every
+ * earlier round), and from there to WSMC_PIO2_FMA_MAX (2^43 = 8.8e12 rad) two FMAs against pi/2 =
+ * P1 + P2 (double-double): ax - fn P1 is exact in one fma (ax and fn P1 are multiples of 2^-52 and
+ * their difference is below 0.79 in magnitude), so r carries one rounding plus fn |pi/2 - P1 - P2|
+ * <= 2^-64 of absolute error; fn, rounded from ax 2/pi, is off by at most 2^-10 of a quadrant, so
+ * |r| <= pi/4 + 2^-9 stays in the kernels' range. Round 6: the phase past 8.2e5 rad was NaN, so a long time span or a
+ * large w gave NaN weights where the reference's cos(w t + p) is finite
+ * (examples/damped_oscillator.jl:11); the Payne–Hanek call the general wsmc_cos makes would cost
+ * the run-time compiled Move blocks 7 VGPRs (3 -> 2 waves a SIMD). Past 2^43 rad (no physical
+ * phase) the value is NaN. */
+#define WSMC_PIO2_FMA_MAX 8796093022208.0          /* 2^43 */
+WSMC_HD double wsmc_osc_reduce(double ax, int* n) {
     const double invpio2 = 6.36619772367581382433e-01, p1 = 1.57079632673412561417e+00,
                  p2 = 6.07710050630396597660e-11, p3 = 2.02226624879595063154e-21;
+    const double P1 = 1.5707963267948966, P2 = 6.123233995736766e-17;     /* pi/2 = P1 + P2 + O(2^-107) */
+    const double axr = ax < WSMC_PIO2_FMA_MAX ? ax : 0.0;
+    const double fn = (double)(int64_t)(axr * invpio2 + 0.5);
+    const double rcw = ((ax - fn * p1) - fn * p2) - fn * p3;
+    const double rfm = __builtin_fma(-fn, P2, __builtin_fma(-fn, P1, ax));
+    *n = (int)((int64_t)fn & 3);
+    return ax < WSMC_PIO2_LARGE ? rcw : ax < WSMC_PIO2_FMA_MAX ? rfm : WSMC_NAN;
+}
+/* cos(x) for the damped-oscillator phase w t + p (its mean and the rotation anchors, wsmc_sincos) */
+WSMC_HD double wsmc_cos_cw(double x) {
     if (!wsmc_isfinite(x)) return WSMC_NAN;
     const double ax = wsmc_fabs(x);
     const int small = ax <= 7.85398163397448278999e-01;
-    const double axr = ax < WSMC_PIO2_LARGE ? ax : 0.0;
-    const double fn = (double)(int64_t)(axr * invpio2 + 0.5);
-    const double rr = ax < WSMC_PIO2_LARGE ? ((ax - fn * p1) - fn * p2) - fn * p3 : WSMC_NAN;
+    int nr;
+    const double rr = wsmc_osc_reduce(ax, &nr);
     const double r = small ? x : rr;
-    const int n = small ? 0 : (int)((int64_t)fn & 3);
+    const int n = small ? 0 : nr;
     const double kc = wsmc_kcos(r), ks = wsmc_ksin(r);
     const double v = (n & 1) ? ks : kc;
     return ((n + 1) & 2) ? -v : v;
@@ -731,10 +767,8 @@ WSMC_HD double wsmc_oscillator(double t, double A, double om, double ga, double 
     return A * wsmc_exp_nd(-ga * t) * wsmc_cos_cw(om * t + ph);
 }
 /* sin and cos with wsmc_cos_cw's reduction and kernels (the oscillator's phase): *c is wsmc_cos_cw(x)
-   bit for bit, so wsmc_cos(x) below WSMC_PIO2_LARGE; NaN past it */
+   bit for bit (wsmc_cos(x) below WSMC_PIO2_LARGE, within an ulp of it up to 2^43 rad) */
 WSMC_HD void wsmc_sincos(double x, double* s, double* c) {
-    const double invpio2 = 6.36619772367581382433e-01, p1 = 1.57079632673412561417e+00,
-                 p2 = 6.07710050630396597660e-11, p3 = 2.02226624879595063154e-21;
     if (!wsmc_isfinite(x)) {
         *s = WSMC_NAN;
         *c = WSMC_NAN;
@@ -742,11 +776,10 @@ WSMC_HD void wsmc_sincos(double x, double* s, double* c) {
     }
     const double ax = wsmc_fabs(x);
     const int small = ax <= 7.85398163397448278999e-01;
-    const double axr = ax < WSMC_PIO2_LARGE ? ax : 0.0;
-    const double fn = (double)(int64_t)(axr * invpio2 + 0.5);
-    const double rr = ax < WSMC_PIO2_LARGE ? ((ax - fn * p1) - fn * p2) - fn * p3 : WSMC_NAN;
+    int nr;
+    const double rr = wsmc_osc_reduce(ax, &nr);
     const double r = small ? x : rr;
-    const int n = small ? 0 : (int)((int64_t)fn & 3);
+    const int n = small ? 0 : nr;
     const double kc = wsmc_kcos(r), ks = wsmc_ksin(r);
     const double vc = (n & 1) ? ks : kc;
     *c = ((n + 1) & 2) ? -vc : vc;              /* cos(r + n pi/2): kc, -ks, -kc, ks */
@@ -884,7 +917,21 @@ WSMC_HD int wsmc_qbits(uint64_t n) {
     const int k = n <= 1 ? 63 : 63 - (64 - __builtin_clzll(n - 1));
     return k < 43 ? k : 43;
 }
+/*
+ * The reference point of the integer weights (round 6): R = ceil(M) for a finite max M (M
+ * itself when it is +-inf or NaN). Every q, wf, q2, wf2 is taken against R, not M: e_i =
+ * expw(lw_i - R) <= 1, the largest e lies in (1/e, 1], so the fixed point keeps all but
+ * log2(e) = 1.44 bits of its resolution. R is a function of M alone, so the statement path
+ * and the oracle need nothing else; but a kernel that knows an upper bound U >= M before M
+ * itself (the fused 2D-SSM propagate: U = the previous step's max or log-mean + the
+ * observation density's maximum) computes every q against ceil(U) in the same pass as the
+ * weights, and ceil(U) == ceil(M) except when M and U straddle an integer — checked after
+ * the fact, with the exact statistics recomputed then.
+ */
+WSMC_HD double wsmc_qref(double M) { return (M - M == 0.0) ? __builtin_ceil(M) : M; }
+
 WSMC_HD uint64_t wsmc_qweight(double lw, double M, int K) {
+    /* M: the reference point (wsmc_qref of the max) */
     double e = wsmc_expw(lw - M);
     if (!(e > 0.0)) return 0;            /* -inf weights, NaN */
     return wsmc_d_to_u64_trunc(e * wsmc_pow2i(K));
@@ -908,6 +955,7 @@ WSMC_HD uint64_t wsmc_qweight(double lw, double M, int K) {
  * (Q2 <= Q <= 2^63, since e2 <= e).
  */
 typedef struct { uint64_t q, wf, q2, wf2; } wsmc_qparts;
+/* M: the reference point (wsmc_qref of the max) */
 WSMC_HD wsmc_qparts wsmc_qparts_of(double lw, double M, int K) {
     wsmc_qparts p = {0, 0, 0, 0};
     double e = wsmc_expw(lw - M);
@@ -1122,7 +1170,7 @@ WSMC_HD int wsmc_autorw_factor(const double* tot, int d, double min_step, double
  * records in rank order (island resampling). Shared by oracle and kernels.
  */
 typedef struct {
-    double M;          /* shard max log-weight (NaN if any NaN) */
+    double M;          /* shard max log-weight (NaN if any NaN); the sums are against wsmc_qref(M) */
     uint64_t Q;        /* sum q_i */
     uint64_t Q2;       /* sum q2_i */
     wsmc_u128 Wf2;     /* sum wf2_i (sum floor(e_i^2 2^(K+42)) = Q2 2^42 + Wf2) */
@@ -1130,55 +1178,79 @@ typedef struct {
     uint64_t n;        /* shard size */
 } wsmc_shard_stats;
 
-/* sum exp(lw_i - M) of one shard, from its fixed point sum floor(e 2^(K+42)) */
+/* sum exp(lw_i - R) of one shard (R = wsmc_qref(M)), from its fixed point sum floor(e 2^(K+42)) */
 WSMC_HD double wsmc_shard_expsum(const wsmc_shard_stats* s) {
     int K = wsmc_qbits(s->n);
     wsmc_u128 W = ((wsmc_u128)s->Q << 42) + s->Wf;
     return wsmc_u128_to_d(W) * wsmc_pow2i(-(K + 42));
 }
-/* sum exp(lw_i - M)^2 of one shard, from its fixed point Q2 2^42 + Wf2 */
+/* sum exp(lw_i - R)^2 of one shard, from its fixed point Q2 2^42 + Wf2 */
 WSMC_HD double wsmc_shard_expsum2(const wsmc_shard_stats* s) {
     int K = wsmc_qbits(s->n);
     wsmc_u128 W = ((wsmc_u128)s->Q2 << 42) + s->Wf2;
     return wsmc_u128_to_d(W) * wsmc_pow2i(-(K + 42));
 }
+/* A flat shard: every particle's fixed point floor(e 2^(K+42)) equals the max particle's, i.e.
+ * sum = n * (the max's), since no term exceeds the max's. Its weights are equal (to within the
+ * resolution of expw), so its ESS is exactly 1 and its log-mean is M itself, as with e = 1 exactly
+ * (the reference point R = ceil(M) makes the common e < 1, and the f64 ratio of the two sums
+ * would otherwise round either way of 1). */
+WSMC_HD int wsmc_shard_flat(const wsmc_shard_stats* s) {
+    if (!(s->M - s->M == 0.0) || s->n == 0) return 0;
+    const wsmc_qparts p = wsmc_qparts_of(s->M, wsmc_qref(s->M), wsmc_qbits(s->n));
+    const wsmc_u128 a = ((wsmc_u128)p.q << 42) + p.wf;
+    return ((wsmc_u128)s->Q << 42) + s->Wf == (wsmc_u128)s->n * a;
+}
+/* every shard flat at one common max: the population's weights are all equal */
+WSMC_HD int wsmc_all_flat(const wsmc_shard_stats* st, int G) {
+    for (int g = 0; g < G; ++g)
+        if (!wsmc_shard_flat(&st[g]) || st[g].M != st[0].M) return 0;
+    return G > 0;
+}
 /* ess_perc = 1 / (N sum w^2), w = exp_norm(weights) (src/resampling.jl:51-54), i.e.
- * (sum e)^2 / (N sum e^2), over every shard's fixed-point sums rescaled by exp(M_g - M)
- * (rank order). One shard: f = 1 and the value is the exact-sum ratio; all-equal weights
- * give exactly 1. */
+ * (sum e)^2 / (N sum e^2), over every shard's fixed-point sums rescaled by exp(R_g - R) (rank
+ * order; R_g - R is an integer). All-equal weights give exactly 1. */
 WSMC_HD double wsmc_global_ess(const wsmc_shard_stats* st, int G) {
-    double M = -WSMC_INF;
+    if (wsmc_all_flat(st, G)) return 1.0;
+    double R = -WSMC_INF;
     uint64_t N = 0;
     int nan = 0;
     for (int g = 0; g < G; ++g) {
-        if (wsmc_isnan(st[g].M)) nan = 1;
-        else if (st[g].M > M) M = st[g].M;
+        const double Rg = wsmc_qref(st[g].M);
+        if (wsmc_isnan(Rg)) nan = 1;
+        else if (Rg > R) R = Rg;
         N += st[g].n;
     }
-    if (nan) M = WSMC_NAN;
+    if (nan) R = WSMC_NAN;
     double s1 = 0.0, s2 = 0.0;
     for (int g = 0; g < G; ++g) {
-        double f = wsmc_exp(st[g].M - M);
+        double f = wsmc_exp(wsmc_qref(st[g].M) - R);
         s1 = s1 + wsmc_shard_expsum(&st[g]) * f;
         s2 = s2 + wsmc_shard_expsum2(&st[g]) * (f * f);
     }
     return (s1 * s1) / (wsmc_u64_to_d(N) * s2);
 }
-/* logsumexp(shard weights) - log(n): the value every weight is reset to (src/transformers.jl:486-489) */
+/* logsumexp(shard weights) - log(n): the value every weight is reset to (src/transformers.jl:486-489);
+ * a flat shard's sum is n exactly against M */
 WSMC_HD double wsmc_shard_mean(const wsmc_shard_stats* s) {
-    return (s->M + wsmc_log(wsmc_shard_expsum(s))) - wsmc_log(wsmc_u64_to_d(s->n));
+    const double ln = wsmc_log(wsmc_u64_to_d(s->n));
+    if (wsmc_shard_flat(s)) return (s->M + ln) - ln;
+    return (wsmc_qref(s->M) + wsmc_log(wsmc_shard_expsum(s))) - ln;
 }
 /* logsumexp(all weights) - log(N)  (src/utils.jl:21) */
 WSMC_HD double wsmc_global_log_evidence(const wsmc_shard_stats* st, int G) {
-    double M = -WSMC_INF;
     uint64_t N = 0;
+    for (int g = 0; g < G; ++g) N += st[g].n;
+    const double lN = wsmc_log(wsmc_u64_to_d(N));
+    if (wsmc_all_flat(st, G)) return (st[0].M + lN) - lN;
+    double R = -WSMC_INF;
     for (int g = 0; g < G; ++g) {
-        if (st[g].M > M || wsmc_isnan(st[g].M)) M = st[g].M;
-        N += st[g].n;
+        const double Rg = wsmc_qref(st[g].M);
+        if (Rg > R || wsmc_isnan(Rg)) R = Rg;
     }
     double S = 0.0;
-    for (int g = 0; g < G; ++g) S = S + wsmc_shard_expsum(&st[g]) * wsmc_exp(st[g].M - M);
-    return (M + wsmc_log(S)) - wsmc_log(wsmc_u64_to_d(N));
+    for (int g = 0; g < G; ++g) S = S + wsmc_shard_expsum(&st[g]) * wsmc_exp(wsmc_qref(st[g].M) - R);
+    return (R + wsmc_log(S)) - lN;
 }
 
 #endif /* WSMC_MATH_H */

@@ -103,6 +103,7 @@ _SIG = {
     "or_strat_word": (C.c_uint32, [C.c_uint64, C.c_uint64, C.c_uint64]),
     "or_qweight": (C.c_uint64, [C.c_double, C.c_double, C.c_int]),
     "or_qbits": (C.c_int, [C.c_uint64]),
+    "or_qref": (C.c_double, [C.c_double]),
     "or_ssm2d_run_mt": (C.c_int, [C.c_int64, C.c_uint64, C.c_uint64, C.c_uint64, _D, _D, C.c_int32, _D, _D, C.c_double,
                                   C.c_double, C.c_double, C.c_int32, C.c_int32, C.c_int32, _D, _D, _D, _D,
                                   _I32P, _D]),

@@ -302,8 +302,9 @@ static or_stats shard_stats(const double* lw, int64_t n, int K) {
     }
     s.M = nan ? WSMC_NAN : M;                    /* maximum() propagates NaN */
     s.Q = 0; s.Q2 = 0; s.Wf2 = 0; s.Wf = 0; s.n = (uint64_t)n;
+    const double R = wsmc_qref(s.M);             /* the reference point (round 6) */
     for (int64_t i = 0; i < n; ++i) {
-        wsmc_qparts p = wsmc_qparts_of(lw[i], s.M, K);
+        wsmc_qparts p = wsmc_qparts_of(lw[i], R, K);
         s.Q += p.q;
         s.Q2 += p.q2;
         s.Wf2 += p.wf2;
@@ -315,6 +316,7 @@ static or_stats shard_stats(const double* lw, int64_t n, int K) {
 /* the icdf merge (src/resampling.jl:13-26) on the integer CDF, one shard */
 static void shard_ancestors(const double* lw, int64_t n, int K, double M, uint64_t Q, int scheme,
                             uint64_t seed, uint64_t op, uint64_t slot_base, int32_t* anc) {
+    M = wsmc_qref(M);                               /* M: the shard max; q against its reference point */
     if (scheme == WSMC_RESAMPLE_MULTINOMIAL) {
         /* sorted draws from exponential spacings, then the same merge as the strata */
         uint64_t PN = 0;
@@ -409,7 +411,7 @@ int or_sample_particles(oracle* o, int64_t n, int32_t replace, int64_t* out) {
     if (st.Q == 0) return WSMC_ESTATE;                  /* exp_norm of these weights is NaN */
     const int K = wsmc_qbits((uint64_t)N);
     uint64_t* q = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)N);
-    for (int64_t i = 0; i < N; ++i) q[i] = wsmc_qweight(o->w[i], st.M, K);
+    for (int64_t i = 0; i < N; ++i) q[i] = wsmc_qweight(o->w[i], wsmc_qref(st.M), K);
     if (replace) {
         uint64_t* C = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)N);
         uint64_t acc = 0;
@@ -451,7 +453,7 @@ static uint64_t* or_qvec(oracle* o) {
     or_stats st = shard_stats(o->w, o->N, wsmc_qbits((uint64_t)o->N));
     const int K = wsmc_qbits((uint64_t)o->N);
     uint64_t* q = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)o->N);
-    for (int64_t i = 0; i < o->N; ++i) q[i] = wsmc_qweight(o->w[i], st.M, K);
+    for (int64_t i = 0; i < o->N; ++i) q[i] = wsmc_qweight(o->w[i], wsmc_qref(st.M), K);
     return q;
 }
 int or_weighted_median(oracle* o, int32_t col, int32_t comp, double* out) {
@@ -521,7 +523,7 @@ void or_exact_record(oracle* o, double M, int64_t gN, uint64_t* out) {
     uint64_t Q = 0, Q2 = 0;
     wsmc_u128 Wf2 = 0, Wf = 0;
     for (int64_t i = 0; i < o->N; ++i) {
-        wsmc_qparts p = wsmc_qparts_of(o->w[i], M, K);
+        wsmc_qparts p = wsmc_qparts_of(o->w[i], wsmc_qref(M), K);
         Q += p.q; Q2 += p.q2; Wf2 += p.wf2; Wf += p.wf;
     }
     out[0] = wsmc_d2bits(M); out[1] = Q; out[2] = Q2;
@@ -565,7 +567,7 @@ int or_exact_window(oracle* o, double M, int64_t gN, uint64_t Q, uint64_t cbase,
     const uint64_t a = wsmc_rank(C, Q, (uint64_t)gN, scheme, o->seed, op, 0);
     uint64_t lo = a;
     for (int64_t m = 0; m < o->N; ++m) {
-        C += wsmc_qweight(o->w[m], M, K);
+        C += wsmc_qweight(o->w[m], wsmc_qref(M), K);
         const uint64_t hi = wsmc_rank(C, Q, (uint64_t)gN, scheme, o->seed, op, 0);
         for (uint64_t sl = lo; sl < hi; ++sl) anc_out[sl - a] = (int32_t)m;
         lo = hi;
@@ -994,6 +996,7 @@ uint64_t or_rank(uint64_t c, uint64_t Q, uint64_t N, int scheme, uint64_t seed, 
 uint64_t or_target(uint64_t n, uint32_t R, uint64_t Q, uint64_t N) { return wsmc_target(n, R, Q, N); }
 uint32_t or_strat_word(uint64_t seed, uint64_t op, uint64_t n) { return wsmc_strat_word(seed, op, n); }
 uint64_t or_qweight(double lw, double M, int K) { return wsmc_qweight(lw, M, K); }
+double or_qref(double M) { return wsmc_qref(M); }
 int or_qbits(uint64_t n) { return wsmc_qbits(n); }
 int32_t or_sizeof_term(void) { return (int32_t)sizeof(wsmc_term); }
 int32_t or_sizeof_dist(void) { return (int32_t)sizeof(wsmc_dist); }

@@ -136,7 +136,8 @@ int or_ssm2d_run_mt(int64_t N, uint64_t seed, uint64_t op_base, uint64_t goff, c
             else if (ps[k].M > M) M = ps[k].M;
         }
         if (nan) M = WSMC_NAN;                    /* maximum() propagates NaN */
-        /* ---- exact integer statistics (order-free) ---- */
+        /* ---- exact integer statistics (order-free), against the reference point ---- */
+        const double R = wsmc_qref(M);
 #pragma omp parallel num_threads(nthreads)
         {
             const int th = omp_get_thread_num();
@@ -144,7 +145,7 @@ int or_ssm2d_run_mt(int64_t N, uint64_t seed, uint64_t op_base, uint64_t goff, c
             wsmc_u128 Wf2 = 0, Wf = 0;
 #pragma omp for schedule(static)
             for (int64_t n = 0; n < N; ++n) {
-                const wsmc_qparts p = wsmc_qparts_of(w[n], M, K);
+                const wsmc_qparts p = wsmc_qparts_of(w[n], R, K);
                 q[n] = p.q;
                 Q += p.q;
                 Q2 += p.q2;
@@ -223,7 +224,7 @@ int or_ssm2d_run_mt(int64_t N, uint64_t seed, uint64_t op_base, uint64_t goff, c
         wsmc_shard_stats st;
         st.M = nan ? WSMC_NAN : M; st.Q = 0; st.Q2 = 0; st.Wf2 = 0; st.Wf = 0; st.n = (uint64_t)N;
         for (int64_t i = 0; i < N; ++i) {
-            const wsmc_qparts p = wsmc_qparts_of(w[i], st.M, K);
+            const wsmc_qparts p = wsmc_qparts_of(w[i], wsmc_qref(st.M), K);
             st.Q += p.q; st.Q2 += p.q2; st.Wf2 += p.wf2; st.Wf += p.wf;
         }
         *log_evidence = wsmc_global_log_evidence(&st, 1);

@@ -87,3 +87,62 @@ def test_script_refuses_launcher_mismatch():
     assert r.returncode == 2, r.stderr[-2000:]
     assert "WORLD_SIZE=1" in r.stderr
     assert r.stdout.strip() == ""
+
+
+class _FakeCtx:
+    """col_names / col_find / col_download / weights_download over numpy arrays (the calls
+    bench.state_digests makes)."""
+    def __init__(self, cols, w):
+        self.cols, self.w = cols, w
+
+    def col_names(self):
+        return list(self.cols)
+
+    def col_find(self, name):
+        return name
+
+    def col_download(self, c):
+        return self.cols[c]
+
+    def weights_download(self):
+        return self.w
+
+
+def _population(n=12, seed=0):
+    import numpy as np
+    r = np.random.default_rng(seed)
+    return {"x_1": r.standard_normal((2, n)), "v": r.standard_normal((2, n)), "a": r.standard_normal(n)}, \
+        r.standard_normal(n)
+
+
+def test_self_check_digests_and_verdict():
+    """a sharded line carries its own parity proof. The digests of a shard
+    slice of one population equal those of the same slice held by a shard; the verdict passes
+    only when every shard and the evidence agree."""
+    cols, w = _population()
+    full = _FakeCtx(cols, w)
+    shard1 = _FakeCtx({k: v[..., 6:12] for k, v in cols.items()}, w[6:12])
+    ref = [bench.state_digests(full, 0, 6), bench.state_digests(full, 6, 12)]
+    assert bench.state_digests(shard1, 0, 6) == ref[1]
+    assert bench.state_digests(full, 0, 12) != ref[0]
+    ok = bench.check_verdict(ref, list(ref), -1.5, -1.5)
+    assert ok["exact_vs_1gpu"] and ok["mismatched_shards"] == []
+    bench.refuse_on_mismatch(ok)                       # passes silently
+
+
+def test_self_check_mismatch_refuses_the_line():
+    cols, w = _population()
+    full = _FakeCtx(cols, w)
+    ref = [bench.state_digests(full, 0, 6), bench.state_digests(full, 6, 12)]
+    bad_w = w.copy()
+    bad_w[8] = -bad_w[8]                               # one weight of shard 1 differs
+    got = [ref[0], bench.state_digests(_FakeCtx(cols, bad_w), 6, 12)]
+    v = bench.check_verdict(ref, got, -1.5, -1.5)
+    assert not v["exact_vs_1gpu"] and v["mismatched_shards"] == [1]
+    with pytest.raises(SystemExit) as e:
+        bench.refuse_on_mismatch(v)
+    assert e.value.code == 2
+    v = bench.check_verdict(ref, list(ref), -1.5, -1.5000000000000002)   # the evidence alone
+    assert not v["exact_vs_1gpu"] and not v["evidence_equal"]
+    with pytest.raises(SystemExit):
+        bench.refuse_on_mismatch(v)

@@ -83,3 +83,57 @@ def test_columns_as_parameters_and_unknown_families_are_refused_on_host():
     f, s = o.col_download(cf), o.col_download(cs)
     assert abs(s[f == 1].mean() - 0.9) < 0.02 and abs(s[f == 0].mean() - 0.01) < 0.01
     assert abi.FAM_GEOMETRIC == 14
+
+
+def _dec_logpdf_normal(mu, sigma, x):
+    """-(z^2 + log 2pi)/2 - log sigma in 60-digit decimal (the textbook formula the reference's
+    normlogpdf evaluates)"""
+    from decimal import Decimal, getcontext
+    getcontext().prec = 60
+    pi = Decimal("3.14159265358979323846264338327950288419716939937510582097494459")
+    z = (Decimal(x) - Decimal(mu)) / Decimal(sigma)
+    return -(z * z + (2 * pi).ln()) / 2 - Decimal(sigma).ln()
+
+
+@pytest.mark.parametrize("family", ["normal", "halfnormal", "lognormal"])
+def test_normal_family_logpdf_against_decimal(family):
+    """the Normal log-density is evaluated as fma(-h, h, c) (include/wsmc_math.h
+    wsmc_normal_lh) and the goldens were regenerated from the oracle, so nothing pinned it to
+    the textbook -(z^2 + log 2pi)/2 - log sigma. Here: Normal, HalfNormal (+ log 2) and LogNormal
+    (log-space Normal - log x) against that formula in 60-digit decimal over z in [0, 40] and
+    sigma over 1e-3 .. 1e3, including the cancellation z^2/2 ~ -log(sigma sqrt(2 pi)) where the
+    density is near 1. The bound is 8 ulp of the terms' magnitudes (log 2pi / 2 + |log sigma| +
+    z^2 / 2 + |log x|): the result's absolute error cannot be smaller than their rounding, and
+    rh = (1/sigma)/sqrt(2) carries two roundings into h^2 (about 3 ulp of z^2 / 2 measured)."""
+    from decimal import Decimal
+    rng = np.random.default_rng(11)
+    mus, sigmas, xs = [], [], []
+    for s in np.exp(rng.uniform(np.log(1e-3), np.log(1e3), 60)):
+        c = -0.5 * np.log(2 * np.pi) - np.log(s)
+        zs = list(rng.uniform(0, 40, 6)) + ([np.sqrt(2 * c)] if c > 0 else [])   # the density near 1
+        for z in zs:
+            mus.append(0.0 if family == "halfnormal" else 0.7)
+            sigmas.append(float(s))
+            xs.append(float((0.0 if family == "halfnormal" else 0.7) + z * s))
+    for mu, s, x in zip(mus, sigmas, xs):
+        if family == "normal":
+            kern, xv = wsmc.Normal(mu, s), x
+            want = _dec_logpdf_normal(mu, s, x)
+        elif family == "halfnormal":
+            kern, xv = wsmc.HalfNormal(s), x
+            want = _dec_logpdf_normal(0.0, s, x) + Decimal(2).ln()
+        else:
+            xv = float(np.exp(x))
+            if not (0.0 < xv < np.inf):
+                continue
+            kern = wsmc.LogNormal(mu, s)
+            want = _dec_logpdf_normal(mu, s, Decimal(xv).ln()) - Decimal(xv).ln()
+        got = observe_at(kern, [xv])[0]
+        z = (x - mu) / s
+        # the intermediates' magnitudes (log 2pi / 2, log sigma, z^2 / 2, log x): any f64
+        # evaluation of the formula rounds at their scale
+        scale = 0.5 * np.log(2 * np.pi) + abs(np.log(s)) + 0.5 * z * z + (abs(np.log(xv)) if family == "lognormal" else 0)
+        tol = 8 * np.spacing(max(scale, 1e-300))
+        if family == "lognormal":   # log x itself is good to an ulp; (log x - mu)/sigma amplifies that
+            tol += 2 * abs(z) * np.spacing(abs(np.log(xv))) / s
+        assert abs(Decimal(got) - want) <= Decimal(tol), (family, mu, s, x, got, want)

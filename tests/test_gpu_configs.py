@@ -38,6 +38,28 @@ def test_c5_full_horizon_matches_oracle(gpu_available, scheme):
     assert g.log_evidence() == o.log_evidence()
 
 
+@pytest.mark.timeout(300)
+def test_c5_per_gpu_shard_size_matches_oracle(gpu_available):
+    """C5 at its per-GPU size (configs[4]: 4M particles over 4 GPUs, 1M a GPU), which no other
+    test reaches: 1M particles, the first 5 observations, the canonical five
+    ungated sweeps, systematic resampling — every column, weight, accepted count and the
+    evidence bit for bit against the oracle (about 16 s of CPU for the oracle)."""
+    import wsmc
+    from oracle import Oracle
+    from test_gpu_parity import assert_same_state
+    N = 1_000_000
+    t, y = wsmc.models.oscillator_data(n=60)
+    t, y = t[:5], y[:5]
+    kw = dict(ess_perc_min=1.0, scheme=1, sweeps=5, diversity=None)
+    g = wsmc.Context(N, seed=42)
+    ag = wsmc.models.oscillator_statements(g, t, y, **kw)
+    o = Oracle(N, seed=42)
+    ao = wsmc.models.oscillator_statements(o, t, y, **kw)
+    assert len(ag) == 5 * 5 and ag == ao
+    assert_same_state(g, o)
+    assert g.log_evidence() == o.log_evidence()
+
+
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("mode", ["island", "exact"])
 @pytest.mark.parametrize("scheme", [0, 1])

@@ -760,3 +760,18 @@ def test_exact_fused_run_without_host_round_trips(gpu_available, sizes, small, p
         if not keep:
             np.testing.assert_array_equal(f.col_download(f.col_find("x")), o.col_download(o.col_find(f"x_{T + 1}")))
         f.close()
+
+
+def test_global_population_limit(gpu_available):
+    """ancestor ids are int32 and the exact fill ranks slots in 32 bits, so a sharded
+    population of 2^31 particles or more is refused at the boundary (wsmc_comm_init_host /
+    wsmc_comm_init / wsmc_create_multi) instead of truncating slots silently."""
+    import wsmc
+    from wsmc import abi
+    c = wsmc.Context(1024, seed=1)
+    with pytest.raises(abi.WSMCError):
+        c.comm_init_host(lambda mine: [mine, mine], 2, 0, 0, 1 << 31)
+    c.comm_init_host(lambda mine: [mine, mine], 2, 0, 0, 2048)   # a valid shard still initialises
+    c.close()
+    with pytest.raises(abi.WSMCError):
+        wsmc.Context.multi(1 << 31, 2, devices=[0, 0])

@@ -357,6 +357,54 @@ def test_ssm2d_fused_nan_observation(gpu_available):
     assert math.isnan(evg) and math.isnan(o.log_evidence())
 
 
+@pytest.mark.parametrize("ess", [1.0, 0.5])
+@pytest.mark.parametrize("N", [4096, 5001])
+def test_ssm2d_fused_statistics_guess_and_recompute(gpu_available, N, ess):
+    """The fused run takes each step's Resample statistics in the propagate against a guessed
+    reference point ceil(U), U = the previous log-mean (or max, when the step did not resample)
+    + the observation density's maximum (include/wsmc_math.h wsmc_qref). Outlier observations
+    (no particle near them: the max lies far below U) make the guess wrong, and k_rs_qfix
+    recomputes the statistics against ceil(M); ess = 0.5 exercises the carried (not resampled)
+    bound. Either way the run equals the statement oracle bit for bit."""
+    obs = models.ssm2d_data(16).copy()
+    obs[5] += (40.0, -25.0)          # far from every particle: the bound is ~1000 nats loose
+    obs[11] += (0.0, 9.0)
+    g = wsmc.Context(N, seed=21)
+    before = g.run_stats()
+    ev = g.ssm2d_run(obs, ess_perc_min=ess, keep_history=True)
+    st = g.run_stats()
+    o = Oracle(N, seed=21)
+    flags = models.ssm2d_statements(o, obs, ess_perc_min=ess)
+    assert_same_state(g, o)
+    np.testing.assert_array_equal(g.last_ancestors(), o.last_ancestors())
+    assert ev == o.log_evidence()
+    assert g.get_state()["n_resamples"] == sum(flags)
+    if st["qstat_mode"]:
+        # both outlier steps missed, and the run was re-done on the exact path
+        assert st["missed_steps"] - before["missed_steps"] >= 2
+        assert st["replays"] - before["replays"] == 1
+    # the next run on the same state continues the stream like run! would, guesses and all
+    ev2 = g.ssm2d_run(obs, ess_perc_min=ess, keep_history=True)
+    models.ssm2d_statements(o, obs, ess_perc_min=ess)
+    assert_same_state(g, o)
+    assert ev2 == o.log_evidence()
+
+
+def test_ssm2d_fused_statistics_guess_holds(gpu_available):
+    """On the model's own data the guess is the reference point almost always: only a step whose
+    max and bound straddle an integer misses (the first step of a run has no bound and takes the
+    statistics' own kernel)."""
+    obs = models.ssm2d_data(40)
+    g = wsmc.Context(1 << 16, seed=5)
+    before = g.run_stats()
+    for _ in range(3):
+        g.ssm2d_run(obs, ess_perc_min=1.0, keep_history=False)
+    st = g.run_stats()
+    if st["qstat_mode"]:
+        assert st["missed_steps"] - before["missed_steps"] <= 1
+        assert st["replays"] - before["replays"] <= 1
+
+
 def _move_program(c, variant):
     """Moves interleaved with every operation that can stale a carried score."""
     from wsmc.dsl import Normal
@@ -466,6 +514,22 @@ def test_oscillator_long_tape_matches_oracle(gpu_available):
     kw = dict(ess_perc_min=1.0, scheme=abi.RESAMPLE_SYSTEMATIC, sweeps=5, diversity=None)
     assert models.oscillator_statements(g, t, y, **kw) == models.oscillator_statements(o, t, y, **kw)
     assert_same_state(g, o)
+    assert g.log_evidence() == o.log_evidence()
+
+
+def test_oscillator_large_phase_matches_oracle(gpu_available):
+    """observation times near 2e5 put the oscillator phase w t + p past 8.2e5 rad
+    for most particles (w ~ HalfNormal(5)), where the Cody-Waite reduction used to give NaN
+    log-densities. The FMA reduction (include/wsmc_math.h wsmc_osc_reduce) keeps every weight
+    finite on the device, bit for bit with the oracle, through Observes, rotation-linked
+    blocks and Moves."""
+    t, y = models.oscillator_data(n=12)
+    t = t + 2.0e5
+    g, o = wsmc.Context(8192, seed=4), Oracle(8192, seed=4)
+    kw = dict(ess_perc_min=1.0, scheme=abi.RESAMPLE_SYSTEMATIC, sweeps=1, diversity=None)
+    assert models.oscillator_statements(g, t, y, **kw) == models.oscillator_statements(o, t, y, **kw)
+    assert_same_state(g, o)
+    assert np.all(np.isfinite(g.weights_download()))
     assert g.log_evidence() == o.log_evidence()
 
 

@@ -296,7 +296,7 @@ def test_multinomial_matches_python_restatement(N):
     op = o.get_state()["op_counter"]
     rs, _ = o.resample(2.0, abi.RESAMPLE_MULTINOMIAL)
     assert rs
-    K, M = L.or_qbits(N), float(np.max(w))
+    K, M = L.or_qbits(N), L.or_qref(float(np.max(w)))   # q against the reference point ceil(max)
     C, acc = [], 0
     for x in w:
         acc += L.or_qweight(float(x), M, K)
@@ -430,8 +430,25 @@ def test_trig_large_arguments_exact():
         rs, rc = _sincos_exact(x, pi)
         assert abs(c - rc) <= 2 * np.spacing(abs(rc)), (x, c, rc)
         assert abs(sn - rs) <= 2 * np.spacing(abs(rs)), (x, sn, rs)
-        # the oscillator's phase reduction (wsmc_sincos) stops at the Cody-Waite range: NaN past it
-        assert math.isnan(c2.value) and math.isnan(s2.value)
+        if abs(x) < 2.0 ** 43:
+            # the oscillator's phase reduction (wsmc_osc_reduce: two FMAs against a
+            # double-double pi/2 past the Cody-Waite range) is finite and accurate to 2^43 rad:
+            # within 2^-64 absolute of the exact remainder plus the kernels' ulp
+            assert abs(c2.value - rc) <= 2 * np.spacing(max(abs(rc), 2.0 ** -10)), (x, c2.value, rc)
+            assert abs(s2.value - rs) <= 2 * np.spacing(max(abs(rs), 2.0 ** -10)), (x, s2.value, rs)
+        else:   # past it (no physical phase): NaN
+            assert math.isnan(c2.value) and math.isnan(s2.value)
+    # the oscillator reduction over its whole FMA range, and the oscillator mean itself (a time
+    # span t = 1e4 at w = 100 puts the phase at 1e6, NaN before round 6)
+    for x in [float(v) for v in np.exp(rng.uniform(np.log(823549.0), np.log(2.0 ** 43), 400))]:
+        s2, c2 = ctypes.c_double(), ctypes.c_double()
+        L.or_sincos(x, ctypes.byref(s2), ctypes.byref(c2))
+        rs, rc = _sincos_exact(x, pi)
+        assert abs(c2.value - rc) <= 2 * np.spacing(max(abs(rc), 2.0 ** -10)), (x, c2.value, rc)
+        assert abs(s2.value - rs) <= 2 * np.spacing(max(abs(rs), 2.0 ** -10)), (x, s2.value, rs)
+    A, om, ga, ph, t = 2.0, 100.0, 0.0, 0.3, 1.0e4
+    ref = A * _sincos_exact(om * t + ph, pi)[1]
+    assert abs(L.or_oscillator(t, A, om, ga, ph) - ref) <= 4 * np.spacing(A)
     # below the switch the Cody-Waite path is unchanged
     for x in (0.5, 3.0, 1e3, 1e5, 8e5):
         rs, rc = _sincos_exact(x, pi)

@@ -39,7 +39,7 @@ def _state(lw, seed=3):
 def _q(o):
     w = o.weights_download()
     N = len(w)
-    K, M = L.or_qbits(N), float(np.max(w))
+    K, M = L.or_qbits(N), L.or_qref(float(np.max(w)))   # q against the reference point ceil(max)
     return [L.or_qweight(float(x), M, K) for x in w]
 
 

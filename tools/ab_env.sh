@@ -1,6 +1,10 @@
 # A/B of an environment switch on one box: tools/ab_env.sh <tag> <VAR=value> <bench_moves legs...>:
 # the legs without and with the setting, alternated twice
 set -o pipefail
+# the switches are read by the diagnostic build only (python tools/build_variant.py diag -DWSMC_DIAG_BUILD):
+# both legs run it, so the A/B isolates the switch
+export WSMC_LIB=${WSMC_LIB:-tools/variants/diag/libwsmc.so}
+[ -f "$WSMC_LIB" ] || { echo "no diagnostic build at $WSMC_LIB"; exit 2; }
 O=gpurun_out/$1; E=$2; shift 2; mkdir -p $O
 for r in 1 2; do
   timeout -k 10 300 python tools/bench_moves.py "$@" > $O/a$r.jsonl 2> $O/a$r.err || { tail $O/a$r.err; exit 1; }

@@ -182,6 +182,23 @@ fallback)   # the sharded run's eager fallback after a failed capture (one-rank 
   WSMC_DIAG_CAPTURE_FAIL=1 timeout -k 10 300 python bench.py --no-cpu-baseline --rccl-one-rank --steps 3 > $O/fb.json 2> $O/fb.err || { tail -30 $O/fb.err; exit 1; }
   grep -c "running it eagerly" $O/fb.err
   line $O/fb.json capture-fallback ;;
+abn)   # A/B/n of environment settings on the diagnostic build (python tools/build_variant.py diag
+       # -DWSMC_DIAG_BUILD), alternated twice:  abn <tag> "<bench args>" SPEC...  (SPEC: VAR=v[,VAR=v] or base)
+  export WSMC_LIB=${WSMC_LIB:-tools/variants/diag/libwsmc.so}
+  [ -f "$WSMC_LIB" ] || { echo "no diagnostic build at $WSMC_LIB"; exit 2; }
+  args=$1; shift
+  for r in 1 2; do
+    for spec in "$@"; do
+      f=$O/$(echo "$spec" | tr '=,' '__')_$r
+      ev=""; [ "$spec" = base ] || ev=$(echo "$spec" | tr ',' ' ')
+      env $ev timeout -k 10 300 python bench.py --no-cpu-baseline $args > $f.json 2> $f.err || { tail -20 $f.err; exit 1; }
+      python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], '%.4g' % d['value'], round(d['ms_per_step'], 4), 'ms')" $f.json "$spec"
+    done
+  done ;;
+timeline)   # per-kernel durations and the gaps between them over a few graph-replayed runs:
+            # timeline <tag> "<bench args>" [kernel filter]
+  step 300 $O/t.log rocprofv3 --kernel-trace --output-format csv -d $O/t -o run -- python bench.py --no-cpu-baseline --steps 3 --warmup 1 $1
+  python tools/timeline.py $O/t/run_kernel_trace.csv "${2:-void wsmc::k_ssm2d_prop}" 24 ;;
 micro)   # the binary is built here (hipcc ... -o tools/micro/<name> tools/micro/<name>.hip): the
          # micro sources do not travel (.gpurunignore)
   name=$1

@@ -29,12 +29,25 @@ bool peer_aborted(wsmc_ctx* c) {
     return true;
 }
 hipError_t ctx_sync(wsmc_ctx* c, hipStream_t s) {
-    if (!c->peer_abort) return hipStreamSynchronize(s);
+    const bool watch = c->comm && c->comm_timeout_s > 0.0;
+    if (!c->peer_abort && !watch) return hipStreamSynchronize(s);
+    const auto t0 = std::chrono::steady_clock::now();
     for (int spin = 0;; ++spin) {
         const hipError_t e = hipStreamQuery(s);
         if (e != hipErrorNotReady) return e;
         if (peer_aborted(c)) {
             // the abort ends the collectives in flight; what remains on the stream completes
+            (void)hipStreamSynchronize(s);
+            return hipErrorLaunchFailure;
+        }
+        if (watch && (spin & 255) == 255 &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->comm_timeout_s) {
+            // the watchdog (wsmc_comm_set_timeout): a collective's peer never arrived
+            std::fprintf(stderr, "wsmc: a stream wait exceeded %.0f s (rank %d of %d): aborting its communicator\n",
+                         c->comm_timeout_s, c->rank, c->world);
+            (void)ncclCommAbort(c->comm);
+            c->comm = nullptr;
+            c->released = true;
             (void)hipStreamSynchronize(s);
             return hipErrorLaunchFailure;
         }
@@ -86,7 +99,7 @@ int fail(int code, const std::string& msg) {
 // (shards exchange inside their operators); WSMC_DIAG_NO_BATCH=1 launches every statement alone.
 static bool ew_enabled(const wsmc_ctx* c) {
     static const bool off = [] {
-        const char* e = getenv("WSMC_DIAG_NO_BATCH");
+        const char* e = diag_env("WSMC_DIAG_NO_BATCH");
         return e && atoi(e) != 0;
     }();
     return !off && !(c->world > 1 || c->comm || c->host_exchange);
@@ -414,9 +427,12 @@ static int acquire_row(wsmc_ctx* c, AncRow* out) {
     if (c->row_pool.empty()) {
         // a slab of as many rows as exist (at least 4): a lazy log that keeps growing (columns
         // read one Resample behind) costs a hipMalloc every few Resamples, not one each — a
-        // hipMalloc is tens of microseconds of host time, more than a step's launches
-        const int64_t n = std::max<int64_t>(4, c->rows_made);
+        // hipMalloc is tens of microseconds of host time, more than a step's launches. Capped at
+        // 8 rows and 256 MB a slab (doubling at 8M particles, 32 MB a row, one row past
+        // 32 took another 1 GB); slabs are freed with the context
         const size_t stride = row_anc_bytes(c->N) + 256;
+        const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(8, (int64_t)((256u << 20) / stride)));
+        const int64_t n = std::min<int64_t>(std::max<int64_t>(4, c->rows_made), std::max<int64_t>(cap, 1));
         void* p = nullptr;
         WSMC_HIP(hipMalloc(&p, stride * (size_t)n));
         c->row_slabs.push_back(p);
@@ -722,7 +738,7 @@ int wsmc_destroy(wsmc_ctx* c) {
     }
     for (void* p : c->row_slabs) (void)hipFree(p);   // every row (log, pool, eager, anc_keep) lives in a slab
     void* bufs[] = {c->dec_always, c->xchg, c->scache, c->scache_back, c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->cdf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount, c->wslots[0], c->wslots[1],
-                    c->d_colptr, c->run_params, c->d_tape, c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp,
+                    c->d_colptr, c->run_params, c->d_tape, c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp, c->run_rg, c->run_nfix, c->run_w0,
                     c->vscratch, c->xscratch, c->xp, c->comb, c->anc_out, c->xbuf, c->d_comp, c->d_ctape, c->d_prog, c->rs_grp[0], c->rs_grp[1],
                     c->xpairs, c->xnb, c->xwin, c->xstat, c->w_save, c->xms, c->xanc, c->xlines, c->xpeer};
     for (void* p : bufs)
@@ -846,6 +862,9 @@ int wsmc_comm_init(wsmc_ctx* c, const uint8_t id[128], int32_t world, int32_t ra
     CHECK_CTX(c);
     if (world < 1 || world > kMaxWorld || rank < 0 || rank >= world) return fail(WSMC_EARG, "bad world/rank");
     if (goff < 0 || goff + c->N > gN) return fail(WSMC_EARG, "shard outside the global population");
+    // ancestor ids are int32 and the exact fill keeps slot ranks in 32 bits: a population of
+    // 2^31 or more would truncate them
+    if (gN >= (int64_t(1) << 31)) return fail(WSMC_EARG, "global population of 2^31 particles or more");
     c->world = world;
     c->rank = rank;
     c->goff = goff;
@@ -865,6 +884,9 @@ int wsmc_comm_init_host(wsmc_ctx* c, wsmc_exchange_fn exchange, void* user, int3
     if (!exchange) return fail(WSMC_EARG, "null exchange");
     if (world < 1 || world > kMaxWorld || rank < 0 || rank >= world) return fail(WSMC_EARG, "bad world/rank");
     if (goff < 0 || goff + c->N > gN) return fail(WSMC_EARG, "shard outside the global population");
+    // ancestor ids are int32 and the exact fill keeps slot ranks in 32 bits: a population of
+    // 2^31 or more would truncate them
+    if (gN >= (int64_t(1) << 31)) return fail(WSMC_EARG, "global population of 2^31 particles or more");
     c->world = world;
     c->rank = rank;
     c->goff = goff;
@@ -892,6 +914,14 @@ int wsmc_comm_info(wsmc_ctx* c, wsmc_comm_info_t* out) {
     for (int g = 0; g < 8; ++g) out->devices[g] = -1;
     out->devices[0] = c->device;
     out->shard_n[0] = c->N;
+    return WSMC_OK;
+}
+
+int wsmc_comm_set_timeout(wsmc_ctx* c, double seconds) {
+    if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { return wsmc_comm_set_timeout(x, seconds); });
+    CHECK_CTX(c);
+    if (!(seconds >= 0.0)) return fail(WSMC_EARG, "timeout must be >= 0");
+    c->comm_timeout_s = seconds;
     return WSMC_OK;
 }
 
@@ -2291,7 +2321,7 @@ int wsmc_sample(wsmc_ctx* c, int32_t out, const wsmc_dist* d) {
         // particle), kept in the batch's rows and written only when read (lazy store: a
         // Resample gathers nothing). WSMC_DIAG_STORE_SAMPLES=1 stores them (A/B)
         static const bool store_all = [] {
-            const char* e = getenv("WSMC_DIAG_STORE_SAMPLES");
+            const char* e = diag_env("WSMC_DIAG_STORE_SAMPLES");
             return e && atoi(e) != 0;
         }();
         eo.nostore = (int16_t)(reads.empty() && c->lazy && eo.out_row >= 0 && !store_all);
@@ -2426,7 +2456,7 @@ int wsmc_weight(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x) { return
 // diagnostics: the generic Resample's reduce-kernel sequence instead of the fused pair
 static bool no_fused_resample() {
     static const bool v = [] {
-        const char* e = getenv("WSMC_DIAG_RESAMPLE_REDUCE");
+        const char* e = diag_env("WSMC_DIAG_RESAMPLE_REDUCE");
         return e && atoi(e) != 0;
     }();
     return v;
@@ -2523,7 +2553,7 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
         // already leaves the max of the reset weights in ms (an Observe's slots: nothing else
         // writes them before the next Observe, which moves on to the other buffer)
         static const bool eager_reset = [] {   // diagnostics: reset in the Resample (A/B)
-            const char* e = getenv("WSMC_DIAG_EAGER_RESET");
+            const char* e = diag_env("WSMC_DIAG_EAGER_RESET");
             return e && atoi(e) != 0;
         }();
         if (eager_reset) WSMC_HIP(launch_fill_weights(c->stream, c->w, row.dec, c->N));
@@ -2898,7 +2928,7 @@ static int move_block_fused(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs,
 // WSMC_DIAG_NO_BLOCK1=1: single Moves keep their own kernels (k_move_c / k_move_ci), for comparison
 static bool no_block1() {
     static const bool v = [] {
-        const char* e = getenv("WSMC_DIAG_NO_BLOCK1");
+        const char* e = diag_env("WSMC_DIAG_NO_BLOCK1");
         return e && atoi(e) != 0;
     }();
     return v;
@@ -3078,7 +3108,7 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         const size_t prog_bytes = ct_bytes + seg_bytes + sizeof(double) * cst.size();
         static_assert(sizeof(wsmc_term) % 8 == 0 && sizeof(FoldSeg) % 8 == 0, "program alignment");
         static const bool no_inline = [] {   // diagnostics only: always upload the program
-            const char* e = getenv("WSMC_DIAG_PROG_COPY");
+            const char* e = diag_env("WSMC_DIAG_PROG_COPY");
             return e && atoi(e) != 0;
         }();
         // lean fold: every one-term segment scalar (runs are evaluated by their own code)
@@ -3252,7 +3282,7 @@ static int move_block_each(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs, 
 // compiles two a thread, for comparison
 static bool mv_heavy_k1() {
     static const bool v = [] {
-        const char* e = getenv("WSMC_DIAG_MV_K1");
+        const char* e = diag_env("WSMC_DIAG_MV_K1");
         return !(e && *e && atoi(e) == 0);
     }();
     return v;
@@ -3260,7 +3290,7 @@ static bool mv_heavy_k1() {
 // WSMC_DIAG_MV_K=1|2|4: particles a thread of the compiled lean (non-oscillator) blocks (2)
 static int mv_lean_k() {
     static const int v = [] {
-        const char* e = getenv("WSMC_DIAG_MV_K");
+        const char* e = diag_env("WSMC_DIAG_MV_K");
         const int k = e ? atoi(e) : 2;
         return (k == 1 || k == 4) ? k : 2;
     }();
@@ -3625,10 +3655,16 @@ static inline size_t run_grp_bytes(int64_t N, int32_t T) {
 static int ensure_run_buffers(wsmc_ctx* c, int32_t T) {
     if (c->T_alloc >= T && c->run_rec) return WSMC_OK;
     WSMC_HIP(ctx_sync(c, c->stream));
-    void* old[] = {c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp};
+    void* old[] = {c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp, c->run_rg};
     for (void* p : old)
         if (p) WSMC_HIP(hipFree(p));
     WSMC_HIP(hipMalloc(&c->run_max, sizeof(MaxSlots) * (T + 1)));
+    WSMC_HIP(hipMalloc(&c->run_rg, sizeof(double) * (T + 1)));
+    if (!c->run_w0) WSMC_HIP(hipMalloc(&c->run_w0, sizeof(double) * c->N));
+    if (!c->run_nfix) {
+        WSMC_HIP(hipMalloc(&c->run_nfix, sizeof(unsigned long long)));
+        WSMC_HIP(hipMemsetAsync(c->run_nfix, 0, sizeof(unsigned long long), c->stream));
+    }
     WSMC_HIP(hipMalloc(&c->run_rec, sizeof(ShardRecord) * (T + 1) * kMaxWorld));
     WSMC_HIP(hipMalloc(&c->run_dec, sizeof(Decision) * (T + 1)));
     WSMC_HIP(hipMalloc(&c->anc_log, sizeof(int32_t) * (size_t)T * anc_stride(c->N)));
@@ -3648,6 +3684,7 @@ static int ensure_run_buffers(wsmc_ctx* c, int32_t T) {
 
 struct RunPlan {
     int32_t T = 0, keep = 0, scheme = 0;
+    bool exact_stats = false;   // the statistics' own kernel at every step (a replay after a missed guess)
     double ess_min = 0, q_var = 0, r_var = 0;
     double x0[2] = {0, 0}, v0[2] = {0, 0};
     int32_t colx = -1, colv = -1, coldv = -1;
@@ -3655,6 +3692,24 @@ struct RunPlan {
     double** d_hist_work = nullptr;
     double** d_hist_out = nullptr;
 };
+
+// where the fused run takes the Resample statistics (see enqueue_ssm2d); measured in round 6
+// (DESIGN.md §3). A diagnostic build (tools/build_variant.py -DWSMC_DIAG_BUILD) reads
+// WSMC_DIAG_QSTAT for A/B runs; the product library ignores the environment.
+#ifndef WSMC_QSTAT_DEFAULT
+#define WSMC_QSTAT_DEFAULT 1   // round 6: q stored 1-2 % ahead of q recomputed by the fill (1M and 8M)
+#endif
+static int run_qstat_mode() {
+#ifdef WSMC_DIAG_BUILD
+    static const int v = [] {
+        const char* e = diag_env("WSMC_DIAG_QSTAT");
+        return e ? atoi(e) : WSMC_QSTAT_DEFAULT;
+    }();
+    return v;
+#else
+    return WSMC_QSTAT_DEFAULT;
+#endif
+}
 
 // events (timing mode): per step 8 = {prop, sums, reduce, scan} x {start, stop} bound to the
 // dispatches themselves (hipExtLaunchKernelGGL), then 2 for the finalize kernel
@@ -3671,7 +3726,16 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
     WSMC_HIP(hipMemsetAsync(c->run_grp, 0, run_grp_bytes(N, T), c->stream));
     double* vbuf[2] = {c->cols[p.colv].back, c->vscratch};
     double* xbuf[2] = {p.keep ? nullptr : c->cols[p.colx].back, c->xscratch};
+    // the Resample statistics' place (round 6): 0 = their own kernel (k_rs_sums_t), 1 = in the
+    // propagate with q stored for the fill, 2 = in the propagate, the fill recomputing q
+    // From step 2 on the propagate guesses the reference point from a bound (k_ssm2d_prop QS); the
+    // first step has no bound and takes the statistics' own kernel. One GPU: the fill's record
+    // block checks the guess and counts a miss into run_dec[0].ntasks, and the host re-does a run
+    // with a miss on the exact path (wsmc_ssm2d_run); sharded: k_rs_qfix checks and recomputes in
+    // place (the shards' decisions are global, so a replay would have to be too).
+    const int qs = p.scheme == WSMC_RESAMPLE_MULTINOMIAL || p.exact_stats ? 0 : run_qstat_mode();
     for (int t = 1; t <= T; ++t) {
+        const bool guess = qs && t > 1;
         Ssm2dArgs a;
         a.t = t;
         a.keep_history = p.keep;
@@ -3711,6 +3775,16 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
             a.ess_min = p.ess_min;
         }
         a.ms = ms;
+        if (qs && t == 1 && !sharded) a.w_save = c->run_w0;   // a replay starts from these weights
+        if (guess) {   // stratified / systematic: the propagate takes the Resample statistics too
+            a.qstat = true;
+            a.ms_prev = t > 1 ? c->run_max + (t - 1) : nullptr;
+            a.rg_out = c->run_rg + t;
+            a.tilep = c->tilep;
+            a.grp = c->run_grp + (size_t)t * run_grp_words(N);
+            a.G = G;
+            a.qbuf = qs == 1 ? c->qbuf : nullptr;
+        }
         const int k0 = 8 * (t - 1);
         WSMC_HIP(launch_ssm2d_propagate(c->stream, a, E(k0), E(k0 + 1)));
         const FillPlan plan = fill_plan(c, p.scheme, 3ull * (uint64_t)(t - 1) + 2ull, c->run_params);
@@ -3735,9 +3809,23 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
         // every rank decides in rank order (k_rs_decide); island resampling fills from the
         // shard's own Q, so the fill never waits for the collective.
         unsigned long long* grp = c->run_grp + (size_t)t * run_grp_words(N);
-        WSMC_HIP(launch_rs_sums(c->stream, c->w, N, ms, c->tilep, c->qbuf, E(k0 + 2), E(k0 + 3), grp, G));
-        WSMC_HIP(launch_rs_fill_fused(c->stream, N, plan, grp, G, ms, p.ess_min, recs + c->rank,
-                                      sharded ? nullptr : c->run_dec + t, c->qbuf, anc_row, E(k0 + 6), E(k0 + 7)));
+        FillPlan fp = plan;
+        if (guess && sharded) {   // check the propagate's reference point (usually a no-op) and fix
+            WSMC_HIP(launch_rs_qfix(c->stream, c->w, N, ms, c->run_rg + t, c->tilep, qs == 1 ? c->qbuf : nullptr, grp, G,
+                                    c->run_nfix, E(k0 + 2), E(k0 + 3)));
+        } else if (guess) {       // checked by the fill's record block
+            fp.rg_check = c->run_rg + t;
+            fp.rg_miss = &c->run_dec[0].ntasks;
+            if (E(k0 + 2)) {      // (instrumented runs: no statistics kernel, an empty interval)
+                WSMC_HIP(hipEventRecord(E(k0 + 2), c->stream));
+                WSMC_HIP(hipEventRecord(E(k0 + 3), c->stream));
+            }
+        } else {
+            WSMC_HIP(launch_rs_sums(c->stream, c->w, N, ms, c->tilep, c->qbuf, E(k0 + 2), E(k0 + 3), grp, G));
+        }
+        WSMC_HIP(launch_rs_fill_fused(c->stream, N, fp, grp, G, ms, p.ess_min, recs + c->rank,
+                                      sharded ? nullptr : c->run_dec + t, c->qbuf, anc_row, E(k0 + 6), E(k0 + 7),
+                                      guess && qs == 2 ? c->w : nullptr));
         if (sharded) {   // the next propagate (or the trace-back) decides from the records
             int r = exchange_recs(c, recs);
             if (r) return r;
@@ -4487,6 +4575,27 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
     WSMC_HIP(hipMemcpyAsync(hdec.data(), c->run_dec, sizeof(Decision) * (T + 1), hipMemcpyDeviceToHost, c->stream));
     WSMC_HIP(ctx_sync(c, c->stream));
     if (temp_tables) (void)hipFree(temp_tables);
+    temp_tables = nullptr;
+    if (hdec[0].ntasks > 0 && !exact_mode(c)) {
+        // a step's guessed reference point missed (the max and its bound straddle an integer, an
+        // outlier observation): the run is re-done from the weights it started with, every step
+        // taking its statistics against the exact max — the canonical bits, as if never guessed
+        c->run_missed += hdec[0].ntasks;
+        c->run_replays += 1;
+        WSMC_HIP(hipMemcpyAsync(c->w, c->run_w0, sizeof(double) * c->N, hipMemcpyDeviceToDevice, c->stream));
+        p.exact_stats = true;
+        if ((r = build_tables(&p.d_hist_work, &p.d_hist_out))) return r;
+        temp_tables = p.d_hist_work;
+        r = enqueue_ssm2d(c, p, nullptr);
+        if (!r) {
+            WSMC_HIP(hipMemcpyAsync(hdec.data(), c->run_dec, sizeof(Decision) * (T + 1), hipMemcpyDeviceToHost,
+                                    c->stream));
+            r = ctx_sync(c, c->stream) == hipSuccess ? WSMC_OK : fail(WSMC_EHIP, "replay sync failed");
+        }
+        (void)hipFree(temp_tables);
+        temp_tables = nullptr;
+        if (r) return r;
+    }
     // wsmc_last_ancestors reports the run's last resample, as after the statement sequence
     for (int t = T; t >= 1; --t)
         if (hdec[t].resampled) {
@@ -4634,6 +4743,20 @@ int wsmc_debug_kernel_bench(wsmc_ctx* c, int32_t kernel, int32_t mode, int32_t i
 int wsmc_debug_jit_stats(int64_t* stats_out) {
     if (!stats_out) return fail(WSMC_EARG, "null stats_out");
     ew_jit_stats(stats_out);
+    return WSMC_OK;
+}
+
+int wsmc_debug_run_stats(wsmc_ctx* c, int64_t* stats_out) {
+    if (c && c->multi) return wsmc_debug_run_stats(multi_first(c), stats_out);
+    if (!c || !stats_out) return fail(WSMC_EARG, "null argument");
+    unsigned long long nfix = 0;
+    if (c->run_nfix) {
+        WSMC_HIP(ctx_sync(c, c->stream));
+        WSMC_HIP(hipMemcpy(&nfix, c->run_nfix, sizeof(nfix), hipMemcpyDeviceToHost));
+    }
+    stats_out[0] = (int64_t)nfix + c->run_missed;
+    stats_out[1] = run_qstat_mode();
+    stats_out[2] = c->run_replays;
     return WSMC_OK;
 }
 

@@ -20,6 +20,23 @@
 
 namespace wsmc {
 
+// Environment switches for A/B experiments (tools/): kernel variants, ablations and
+// alternative paths, read only by a diagnostic build (tools/build_variant.py NAME -DWSMC_DIAG_BUILD,
+// selected with WSMC_LIB). The product library ignores them, so no stray variable in a user's
+// environment can change its results. The four it honours change no result (tests select paths
+// with them): WSMC_DIAG_NO_GRAPH (the fused run enqueued eagerly, for kernel tracers),
+// WSMC_DIAG_NO_JIT (the interpreter kernels in place of the run-time compiled ones),
+// WSMC_DIAG_CAPTURE_FAIL (the eager fallback after a failed graph capture) and WSMC_DIAG_NO_PEER
+// (exact shards trace lineages through windows instead of peer reads).
+inline const char* diag_env(const char* name) {
+#ifdef WSMC_DIAG_BUILD
+    return getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
+
 constexpr int kItems = 8;              // particles per thread in the tile kernels
 constexpr int kTile = kBlock * kItems; // 2048 particles per tile (canonical reduction tile)
 constexpr int kRsBlock = 1024;         // threads of the reduce workgroup
@@ -149,6 +166,7 @@ struct wsmc_ctx {
     // collective missing a failed peer would never complete) and leaves with `released` set
     const std::atomic<bool>* peer_abort = nullptr;
     bool released = false;
+    double comm_timeout_s = 0.0;                // wsmc_comm_set_timeout: bound on a stream wait (0: none)
     wsmc_exchange_fn host_exchange = nullptr;   // host-side record exchange (instead of RCCL)
     bool host_inproc = false;                   // ... between threads of this process (a multi-device
                                                 // handle's: a memcpy), not a caller's transport
@@ -315,6 +333,10 @@ struct wsmc_ctx {
     // fused runner state
     int32_t T_alloc = 0;
     wsmc::MaxSlots* run_max = nullptr;      // [T+1]
+    double* run_rg = nullptr;               // [T+1] the propagate's guessed reference points (round 6)
+    unsigned long long* run_nfix = nullptr; // [1] steps whose statistics k_rs_qfix recomputed (cumulative)
+    double* run_w0 = nullptr;               // [N] the weights a run started from (its replay's start)
+    int64_t run_missed = 0, run_replays = 0; // single GPU: steps whose guess missed, runs re-done
     wsmc::ShardRecord* run_rec = nullptr;   // [(T+1) * world]
     wsmc::Decision* run_dec = nullptr;      // [T+1]
     int32_t* anc_log = nullptr;             // [T][N]
@@ -440,6 +462,10 @@ struct FillPlan {          // ancestor-fill task planning (in the reduce kernel)
     ExactPlan* dx_xp = nullptr;
     int32_t dx_world = 0, dx_rank = 0;
     double dx_ess = 0.0;
+    // the fused run's guessed reference point (round 6): the record block compares it with
+    // wsmc_qref of the step's max and counts a miss (the run is then re-done on the exact path)
+    const double* rg_check = nullptr;
+    int32_t* rg_miss = nullptr;
 };
 hipError_t launch_rs_reduce(hipStream_t s, const MaxSlots* ms, const unsigned long long* tilep, int64_t N,
                             unsigned long long* tileOff, ShardRecord* rec, int decide_local, double ess_min,
@@ -652,7 +678,7 @@ inline int group_tiles(int64_t N) {   // tiles per group: ~sqrt(ntiles), >= 16
 hipError_t launch_rs_fill_fused(hipStream_t s, int64_t N, const FillPlan& plan, const unsigned long long* grp,
                                 int G, const MaxSlots* ms, double ess_min, ShardRecord* rec, Decision* dec,
                                 const unsigned long long* qbuf, int32_t* anc, hipEvent_t e0 = nullptr,
-                                hipEvent_t e1 = nullptr);
+                                hipEvent_t e1 = nullptr, const double* wq = nullptr);
 hipError_t launch_gather(hipStream_t s, double* dst, const double* src, const int32_t* anc, int64_t N);
 hipError_t launch_lazy_trace(hipStream_t s, const TraceArgs& a, int64_t N);
 // up to kGatherSet (dst, src) column-component pairs of one Resample, passed by value
@@ -734,7 +760,23 @@ struct Ssm2dArgs {
     Decision* dec_out = nullptr;
     int32_t world = 1, rank = 0;
     double ess_min = 0.0;
+    // the Resample statistics in the propagate (round 6, k_ssm2d_prop QS): the previous step's max
+    // slots (the bound when it did not resample), where the guessed reference point goes (for
+    // k_rs_qfix), this step's tile partials and group lines, and q itself when the fill reads it
+    // (null: the fill recomputes q from the weights)
+    bool qstat = false;
+    double* w_save = nullptr;          // the first step's incoming weights go here (a replay's start)
+    const MaxSlots* ms_prev = nullptr;
+    double* rg_out = nullptr;
+    unsigned long long* tilep = nullptr;
+    unsigned long long* grp = nullptr;
+    int32_t G = 1;
+    unsigned long long* qbuf = nullptr;
 };
+// k_rs_qfix: the statistics again against ceil(M) when the propagate's guess was not it
+hipError_t launch_rs_qfix(hipStream_t s, const double* w, int64_t N, const MaxSlots* ms, const double* rg,
+                          unsigned long long* tilep, unsigned long long* qbuf, unsigned long long* grp, int G,
+                          unsigned long long* nfix, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t launch_ssm2d_propagate(hipStream_t s, const Ssm2dArgs& a, hipEvent_t e0 = nullptr,
                                   hipEvent_t e1 = nullptr);
 struct Ssm2dFinal {

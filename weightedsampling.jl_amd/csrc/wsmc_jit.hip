@@ -213,7 +213,11 @@ bool compile_src(const std::string& arch, const std::string& src, std::string& c
     }
     const std::string arch_opt = "--offload-arch=" + arch;
     const char* opts[] = {arch_opt.c_str(), "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
-                          "-munsafe-fp-atomics", "-Wno-unused-result"};
+                          "-munsafe-fp-atomics", "-Wno-unused-result",
+#ifdef WSMC_LDS_TABLE_CHECK   // the library's check build checks its run-time compiled kernels too
+                          "-DWSMC_LDS_TABLE_CHECK",
+#endif
+    };
     const hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof(opts) / sizeof(opts[0])), opts);
     if (rc != HIPRTC_SUCCESS) {
         size_t n = 0;
@@ -436,7 +440,7 @@ std::string mv_sig_text(const MvSig& g) {
 // WSMC_DIAG_MV_WAVES=n: the blocks compiled for n waves a SIMD (amdgpu_waves_per_eu), for comparison
 std::string mv_waves_attr() {
     static const std::string a = [] {
-        const char* e = getenv("WSMC_DIAG_MV_WAVES");
+        const char* e = diag_env("WSMC_DIAG_MV_WAVES");
         const int n = e ? atoi(e) : 0;
         return n > 0 ? " __attribute__((amdgpu_waves_per_eu(" + std::to_string(n) + ")))" : std::string();
     }();
@@ -447,7 +451,7 @@ std::string mv_waves_attr() {
 // the gathers through the caches everywhere, for comparison
 bool tables_global() {
     static const bool g = [] {
-        const char* e = getenv("WSMC_DIAG_MV_TABLES_GLOBAL");
+        const char* e = diag_env("WSMC_DIAG_MV_TABLES_GLOBAL");
         return e && *e && *e != '0';
     }();
     return g;

@@ -545,7 +545,7 @@ __global__ __launch_bounds__(kSumBlock) void k_rs_sums_t(const double* __restric
             const u64 v = ms[g].v[th & 63][0];
             mv = v > mv ? v : mv;
         }
-    const double M = MODE == 4 ? 0.0 : wsmc_ord_dec(wave_max_u64(mv));
+    const double M = MODE == 4 ? 0.0 : wsmc_qref(wsmc_ord_dec(wave_max_u64(mv)));   // the reference point
     const double sK = wsmc_pow2i(wsmc_qbits((uint64_t)Nk));   // Nk: the global N when exact-sharded
     QAcc acc;
 #pragma unroll
@@ -577,6 +577,46 @@ __global__ __launch_bounds__(kSumBlock) void k_rs_sums_t(const double* __restric
     if (gall && blockIdx.x == 0 && th == kPart) atomicAdd(grp + 7, (u64)N);
 }
 
+// The fused run's statistics check (round 6): the propagate took every q against its guess R_g
+// (k_ssm2d_prop QS); they are the canonical ones iff R_g == wsmc_qref(M) (numerically: -0.0 and
+// +0.0 give the same expw). Then every block returns at once. Otherwise (M and the bound straddle
+// an integer, the first step, a NaN) the blocks recompute, grid-stride, each tile's q (when the
+// fill reads it from qbuf), its partials, and correct the group lines by the difference of the
+// tile's sum (u64 wrap-around arithmetic: exact) and a max with the new one (the overflow plan's
+// gate only needs an upper bound). nfix counts the steps that took this path.
+__global__ __launch_bounds__(kSumBlock) void k_rs_qfix(const double* __restrict__ w, int64_t N,
+                                                     const MaxSlots* __restrict__ ms, const double* __restrict__ rg,
+                                                     u64* __restrict__ tilep, u64* __restrict__ qbuf,
+                                                     u64* __restrict__ grp, int G, u64* nfix) {
+    constexpr int IT = kRsTile / kSumBlock;
+    __shared__ double s_f[kPart][kSumBlock / 64];
+    const double R = wsmc_qref(wave_slots_max(ms));
+    if (R == *rg) return;                                   // uniform: the guess was the reference point
+    if (nfix && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(nfix, 1ull);
+    const int th = threadIdx.x;
+    const int ntiles = (int)((N + kRsTile - 1) / kRsTile);
+    const double sK = wsmc_pow2i(wsmc_qbits((uint64_t)N));
+    for (int b = blockIdx.x; b < ntiles; b += gridDim.x) {
+        const int64_t base = (int64_t)b * kRsTile;
+        const u64 old = th == 0 ? tilep[(int64_t)b * kPart] : 0ull;
+        QAcc acc;
+#pragma unroll
+        for (int k = 0; k < IT; ++k) {
+            const int64_t i = base + (int64_t)k * kSumBlock + th;
+            const double lw = i < N ? w[i] : -WSMC_INF;
+            const u64 q = qacc_add(acc, wsmc_expw(lw - R), sK);
+            if (qbuf && i < N) qbuf[i] = q;
+        }
+        const u64 t = qacc_tile<kSumBlock>(acc, s_f, tilep + (int64_t)b * kPart);
+        if (th == 0) {
+            u64* gl = grp + (int64_t)(b / G) * kGroupLine;
+            atomicAdd(gl, t - old);
+            atomicMax(gl + 1, t);
+        }
+        __syncthreads();                                    // s_f is reused by the next tile
+    }
+}
+
 __device__ __forceinline__ wsmc_shard_stats record_stats(const ShardRecord& r) {
     wsmc_shard_stats st;
     st.M = wsmc_ord_dec(r.menc);
@@ -591,25 +631,28 @@ __device__ __forceinline__ wsmc_shard_stats record_stats(const ShardRecord& r) {
 // Global decision from the shard records (rank order): the same arithmetic as
 // wsmc_global_ess / wsmc_shard_mean, streamed over the records (no local arrays).
 __device__ void decide_records(const ShardRecord* recs, int world, int rank, double ess_min, Decision* dec) {
-    double M = -WSMC_INF;
+    double R = -WSMC_INF;
     uint64_t N = 0;
-    int nan = 0;
+    int nan = 0, flat = world > 0;
+    const double M0 = wsmc_ord_dec(recs[0].menc);
     for (int g = 0; g < world; ++g) {
-        const double Mg = wsmc_ord_dec(recs[g].menc);
-        if (wsmc_isnan(Mg)) nan = 1;
-        else if (Mg > M) M = Mg;
+        const wsmc_shard_stats st = record_stats(recs[g]);
+        const double Rg = wsmc_qref(st.M);
+        if (wsmc_isnan(Rg)) nan = 1;
+        else if (Rg > R) R = Rg;
         N += recs[g].n;
+        flat = flat && wsmc_shard_flat(&st) && st.M == M0;   // wsmc_all_flat
     }
-    if (nan) M = WSMC_NAN;
+    if (nan) R = WSMC_NAN;
     double s1 = 0.0, s2 = 0.0;
     for (int g = 0; g < world; ++g) {
         // the arithmetic of wsmc_global_ess, streamed over the records
         const wsmc_shard_stats st = record_stats(recs[g]);
-        const double f = wsmc_exp(st.M - M);
+        const double f = wsmc_exp(wsmc_qref(st.M) - R);
         s1 = s1 + wsmc_shard_expsum(&st) * f;
         s2 = s2 + wsmc_shard_expsum2(&st) * (f * f);
     }
-    const double ess = (s1 * s1) / (wsmc_u64_to_d(N) * s2);
+    const double ess = flat ? 1.0 : (s1 * s1) / (wsmc_u64_to_d(N) * s2);
     const int rs = ess < ess_min;
     const wsmc_shard_stats me = record_stats(recs[rank]);
     dec->resampled = rs;
@@ -1170,6 +1213,29 @@ __device__ __forceinline__ void load_tile_q(int64_t N, int b, const u64* __restr
     }
 }
 
+// the same q recomputed from the log-weights against the reference point (the fused run's fill
+// when the propagate did not store q: qacc_add's arithmetic, bit for bit)
+// (against the guessed reference point rref when the fill checks a guess: consistent with the tile
+// partials the propagate took, whether or not the guess was right)
+template <int IT>
+__device__ __forceinline__ void load_tile_qw(int64_t N, int b, const double* __restrict__ w,
+                                             const MaxSlots* __restrict__ ms, const double* rref, u64 (&q)[IT]) {
+    double lw[IT];
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        const int64_t i = (int64_t)b * kRsTile + (int64_t)threadIdx.x * IT + k;
+        lw[k] = i < N ? w[i] : -WSMC_INF;
+    }
+    const double R = rref ? *rref : wsmc_qref(wave_slots_max(ms));
+    const double sK = wsmc_pow2i(wsmc_qbits((uint64_t)N));
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        double e = wsmc_expw(lw[k] - R);
+        e = e > 0.0 ? e : 0.0;
+        q[k] = d_small_to_u64(wsmc_floor(e * sK));
+    }
+}
+
 // every slot of the window starts at -1 (no mark); the caller's next barrier orders it
 __device__ __forceinline__ void fill_clear(FillLds& sh) {
     const int4 m1 = make_int4(-1, -1, -1, -1);
@@ -1357,13 +1423,18 @@ __device__ __forceinline__ double tile_q_sum(const u64 (&q)[kRsTile / kScanBlock
     return s;
 }
 
-// a whole chunk given the tile's offset and Q (generic Resample, overflow chunks)
-template <int MODE>
+// a whole chunk given the tile's offset and Q (generic Resample, overflow chunks); QW: q from the
+// log-weights wq against the reference point of the max slots ms
+template <int MODE, bool QW = false>
 __device__ __forceinline__ void fill_chunk(int64_t N, int b, int j, u64 Q, u64 off, const FillPlan& plan,
                                            uint64_t opx, const u64* __restrict__ qbuf, int32_t* __restrict__ anc,
-                                           FillLds& sh) {
+                                           FillLds& sh, const double* __restrict__ wq = nullptr,
+                                           const MaxSlots* __restrict__ ms = nullptr) {
     u64 q[kRsTile / kScanBlock];
-    load_tile_q(N, b, qbuf, q);
+    if (QW)
+        load_tile_qw(N, b, wq, ms, plan.rg_check, q);
+    else
+        load_tile_q(N, b, qbuf, q);
     const u64 qb = plan.tilep[(int64_t)b * kPart];
     fill_clear(sh);
     const double pre = fill_scan_q(tile_q_sum(q), sh);
@@ -1429,7 +1500,7 @@ __global__ __launch_bounds__(kSumBlock) void k_rs_sums_multi(const double* __res
     double lw[IT];
 #pragma unroll
     for (int k = 0; k < IT; ++k) lw[k] = base + k < N ? w[base + k] : -WSMC_INF;
-    const double M = wave_slots_max(ms);
+    const double M = wsmc_qref(wave_slots_max(ms));   // the reference point
     const double sK = wsmc_pow2i(wsmc_qbits((uint64_t)N));
     const uint64_t opx = op_eff(plan.op, plan.op_dev);
     u64 q[IT], E = 0;
@@ -1612,7 +1683,7 @@ __global__ __launch_bounds__(kBlock) void k_sample_draws(int64_t n, int64_t N, c
 __global__ __launch_bounds__(kBlock) void k_es_keys(const double* __restrict__ w, int64_t N,
                                                     const MaxSlots* __restrict__ ms, uint64_t seed, uint64_t op,
                                                     u64* __restrict__ keys, u64* __restrict__ idx) {
-    const double M = wave_slots_max(ms);
+    const double M = wsmc_qref(wave_slots_max(ms));   // the reference point
     const int K = wsmc_qbits((uint64_t)N);
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= N) return;
@@ -1652,7 +1723,7 @@ __global__ __launch_bounds__(kBlock) void k_es_keys_shard(const double* __restri
                                                           int64_t goff, const MaxSlots* __restrict__ ms,
                                                           uint64_t seed, uint64_t op, u64* __restrict__ keys,
                                                           u64* __restrict__ idx) {
-    const double M = wave_slots_max(ms);
+    const double M = wsmc_qref(wave_slots_max(ms));   // the reference point
     const int K = wsmc_qbits((uint64_t)gN);
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= N) return;
@@ -1754,11 +1825,14 @@ __device__ __forceinline__ void block_sum2_u64(u64& a, u64& b, u64 (*lds)[2]) {
 // MODE (diagnostics only, results wrong; production = 0): 1 = the record block only marks
 // the step resampled with mean 0 (the same fill work under forced resampling: q depends on
 // lw - M only)
-template <int MODE>
+// QW (round 6, the fused run after a propagate that took the statistics): the tile blocks
+// recompute q from the weights wq instead of loading it (no q in HBM)
+template <int MODE, bool QW = false>
 __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(6))) void k_rs_fill_fused(int64_t N, FillPlan plan, const u64* __restrict__ grp,
                                                               int G, const MaxSlots* __restrict__ ms, double ess_min,
                                                               ShardRecord* rec, Decision* dec,
-                                                              const u64* __restrict__ qbuf, int32_t* __restrict__ anc) {
+                                                              const u64* __restrict__ qbuf, int32_t* __restrict__ anc,
+                                                              const double* __restrict__ wq) {
     __shared__ FillLds sh;
     __shared__ u64 s_red[kScanBlock / 64][2];
     __shared__ u64 s_parts[kScanBlock / 64][kRedPart];
@@ -1854,6 +1928,10 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(6)))
             r.wflo = (u64)Wf; r.wfhi = (u64)(Wf >> 64);
             r.n = (u64)N;
             *rec = r;
+            // the propagate took the statistics against its guess: a miss makes this step's
+            // decision and fill non-canonical (but consistent with one another: no hazard); the
+            // host re-does the run on the exact path
+            if (plan.rg_check && !(wsmc_qref(wsmc_ord_dec(menc)) == *plan.rg_check)) atomicAdd(plan.rg_miss, 1);
             if (dec) {
                 decide_records(&r, 1, 0, ess_min, dec);
                 if (plan.host_dec) *plan.host_dec = *dec;   // the generic Resample's host copy
@@ -1871,7 +1949,10 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(6)))
     if (t < ntiles) {
         // ---- first chunk of tile t (its q loads in flight while the offset is summed) ----
         u64 q[kRsTile / kScanBlock];
-        load_tile_q(N, t, qbuf, q);
+        if (QW)
+            load_tile_qw(N, t, wq, ms, plan.rg_check, q);
+        else
+            load_tile_q(N, t, qbuf, q);
         const u64 qb = plan.tilep[(int64_t)t * kPart];   // every load of the block is issued here
         const int g = t / G;
         u64 pre = 0, tot = 0;
@@ -1986,7 +2067,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(6)))
         const int j = __builtin_amdgcn_readfirstlane((int)s_task[1]);
         const u64 off = ((u64)__builtin_amdgcn_readfirstlane((int)(s_task[2] >> 32)) << 32) |
                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)s_task[2]);
-        fill_chunk<0>(N, b, j, Qu, off, plan, opx, qbuf, anc, sh);   // ends with a barrier
+        fill_chunk<0, QW>(N, b, j, Qu, off, plan, opx, qbuf, anc, sh, wq, ms);   // ends with a barrier
     }
 }
 
@@ -3137,13 +3218,20 @@ __device__ __forceinline__ double aff2(double a, double b) {
 #ifndef WSMC_PROP_LDS_LOG   // the draws' log table from an LDS copy (0: the cached gathers, for comparison)
 #define WSMC_PROP_LDS_LOG 1
 #endif
-template <int MODE, int IT = 1>
-__global__ __launch_bounds__(kBlock) void k_ssm2d_prop(Ssm2dArgs a) {
-    __shared__ u64 lds4[4];
+// QS (round 6, the single-GPU and island runs): NT = 512 threads, so a block is one 1024-particle
+// Resample tile, and the block also takes the tile's Resample statistics (k_rs_sums_t's q, tile
+// partials and group sums) against a guessed reference point R_g = ceil(U), U = (the previous
+// step's log-mean, or its max when it did not resample) + the observation density's maximum
+// -c0/2: every weight of the step is <= U (rounding is monotone), so R_g >= ceil(M), and R_g is
+// the canonical ceil(M) unless M and U straddle an integer. k_rs_qfix checks that once M is
+// known and recomputes the statistics when it is not (include/wsmc_math.h wsmc_qref).
+template <int MODE, int IT = 1, int NT = kBlock, bool QS = false>
+__global__ __launch_bounds__(NT) void k_ssm2d_prop(Ssm2dArgs a) {
+    __shared__ u64 lds4[NT / 64];
     __shared__ double s_logtab[2 * WSMC_LOG_TABLE_N];
     if (WSMC_PROP_LDS_LOG && (MODE & 1) == 0) {   // every thread, before the first draw
         const double* lt = wsmc_log_table();
-        for (int k = (int)threadIdx.x; k < 2 * WSMC_LOG_TABLE_N; k += kBlock) s_logtab[k] = lt[k];
+        for (int k = (int)threadIdx.x; k < 2 * WSMC_LOG_TABLE_N; k += NT) s_logtab[k] = lt[k];
         __syncthreads();
     }
     const double* logtab = WSMC_PROP_LDS_LOG ? s_logtab : wsmc_log_table();
@@ -3169,8 +3257,8 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_prop(Ssm2dArgs a) {
     const double o0 = a.obs[2 * (a.t - 1)], o1 = a.obs[2 * (a.t - 1) + 1];
     // IT pairs per thread, a grid apart: every pair's loads are issued before any pair is
     // computed and stored, so one pair's stores overlap the next pair's reads
-    const int64_t stride = (int64_t)gridDim.x * kBlock * 2;
-    const int64_t ib = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 2;
+    const int64_t stride = (int64_t)gridDim.x * NT * 2;
+    const int64_t ib = ((int64_t)blockIdx.x * NT + threadIdx.x) * 2;
     int64_t src[IT][2];
     bool ok[IT], two[IT];
 #pragma unroll
@@ -3203,8 +3291,10 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_prop(Ssm2dArgs a) {
             if (two[j]) {
                 const d2 w2 = *reinterpret_cast<const d2*>(a.w + i0);
                 wb[j][0] = w2.x; wb[j][1] = w2.y;
+                if (a.w_save) *reinterpret_cast<d2*>(a.w_save + i0) = w2;
             } else {
                 wb[j][0] = a.w[i0];
+                if (a.w_save) a.w_save[i0] = wb[j][0];
             }
         }
 #pragma unroll
@@ -3228,6 +3318,17 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_prop(Ssm2dArgs a) {
         }
     }
     u64 menc = 0;
+    QAcc acc;          // QS: the tile's Resample statistics
+    double Rg = 0.0, sK = 0.0;
+    if (QS) {
+        // the guess: every weight of this step is wb + lp <= base + lpmax (lp <= -c0/2, wb <= base)
+        double base = WSMC_NAN;   // the first step: no bound (k_rs_qfix takes the statistics)
+        if (a.t > 1 && a.ms_prev) base = rs ? mean : wave_slots_max(a.ms_prev);
+        const double lpmax = -(a.c0 + 0.0) * 0.5;
+        Rg = wsmc_qref(base + lpmax);
+        sK = wsmc_pow2i(wsmc_qbits((uint64_t)N));
+        if (blockIdx.x == 0 && threadIdx.x == 0) *a.rg_out = Rg;
+    }
 #pragma unroll
     for (int j = 0; j < IT; ++j) {
         if (!ok[j]) continue;
@@ -3267,6 +3368,8 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_prop(Ssm2dArgs a) {
         if (a.dv) *reinterpret_cast<d2*>(a.dv + 2 * i0) = dvv[0];
         u64 e0 = wsmc_ord_enc(wn[0]);
         menc = e0 > menc ? e0 : menc;
+        u64 q0 = 0, q1 = 0;
+        if (QS) q0 = qacc_add(acc, wsmc_expw(wn[0] - Rg), sK);
         if (two[j]) {
             *reinterpret_cast<d2*>(a.x_next + 2 * i0 + 2) = xn[1];
             *reinterpret_cast<d2*>(a.v_next + 2 * i0 + 2) = vn[1];
@@ -3274,9 +3377,47 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_prop(Ssm2dArgs a) {
             *reinterpret_cast<d2*>(a.w + i0) = d2{wn[0], wn[1]};
             const u64 e1 = wsmc_ord_enc(wn[1]);
             menc = e1 > menc ? e1 : menc;
+            if (QS) q1 = qacc_add(acc, wsmc_expw(wn[1] - Rg), sK);
+            if (QS && a.qbuf) *reinterpret_cast<ulonglong2*>(a.qbuf + i0) = make_ulonglong2(q0, q1);
         } else {
             a.w[i0] = wn[0];
+            if (QS && a.qbuf) a.qbuf[i0] = q0;
         }
+    }
+    if (QS) {
+        // one barrier for the block max and the tile partials (qacc_tile's layout, the group lines
+        // of k_rs_sums_t)
+        __shared__ double s_f[kPart][NT / 64];
+        const int th = threadIdx.x, wv = th >> 6;
+        acc.Q = wave_sum_f64_exact(acc.Q);
+        acc.Q2 = wave_sum_f64_exact(acc.Q2);
+        acc.WF2 = wave_sum_f64_exact(acc.WF2);
+        acc.WF = wave_sum_f64_exact(acc.WF);
+        menc = wave_max_u64(menc);
+        if ((th & 63) == 0) {
+            s_f[0][wv] = acc.Q; s_f[1][wv] = acc.Q2;
+            s_f[2][wv] = acc.WF2; s_f[3][wv] = acc.WF;
+            lds4[wv] = menc;
+        }
+        __syncthreads();
+        if (th < kPart) {
+            double f = 0.0;
+#pragma unroll
+            for (int v = 0; v < NT / 64; ++v) f = f + s_f[th][v];
+            const u64 t = (u64)f;                     // exact integer <= 2^53
+            a.tilep[(int64_t)blockIdx.x * kPart + th] = t;
+            if (th == 0) {
+                u64* gl = a.grp + (int64_t)(blockIdx.x / a.G) * kGroupLine;
+                atomicAdd(gl, t);
+                atomicMax(gl + 1, t);
+            }
+        } else if (th == 64) {
+            u64 m = 0;
+#pragma unroll
+            for (int v = 0; v < NT / 64; ++v) m = lds4[v] > m ? lds4[v] : m;
+            atomic_max_filtered(&a.ms->v[blockIdx.x % kSlots][0], m);
+        }
+        return;
     }
     if (MODE & 4) {                                  // diag: no block max / atomic
         if (menc == 0x123456789ull) a.w[0] = 0.0;
@@ -3627,18 +3768,42 @@ hipError_t launch_rs_sums(hipStream_t s, const double* w, int64_t N, const MaxSl
 }
 hipError_t launch_rs_fill_fused(hipStream_t s, int64_t N, const FillPlan& plan, const u64* grp, int G,
                                 const MaxSlots* ms, double ess_min, ShardRecord* rec, Decision* dec, const u64* qbuf,
-                                int32_t* anc, hipEvent_t e0, hipEvent_t e1) {
+                                int32_t* anc, hipEvent_t e0, hipEvent_t e1, const double* wq) {
     const dim3 g((unsigned)((N + kRsTile - 1) / kRsTile + kOverflowBlocks + 1));
+    if (wq)
+        return launch_timed(k_rs_fill_fused<0, true>, g, dim3(kScanBlock), s, e0, e1, N, plan, grp, G, ms, ess_min,
+                            rec, dec, qbuf, anc, wq);
+#ifdef WSMC_DIAG_BUILD
     static const int diag = [] {
-        const char* e = getenv("WSMC_DIAG_FILL");
+        const char* e = diag_env("WSMC_DIAG_FILL");
         return e ? atoi(e) : 0;
     }();
-    switch (diag) {
-        case 1: return launch_timed(k_rs_fill_fused<1>, g, dim3(kScanBlock), s, e0, e1, N, plan, grp, G, ms, ess_min,
-                                    rec, dec, qbuf, anc);
-        default: return launch_timed(k_rs_fill_fused<0>, g, dim3(kScanBlock), s, e0, e1, N, plan, grp, G, ms, ess_min,
-                                     rec, dec, qbuf, anc);
+    if (diag == 1)
+        return launch_timed(k_rs_fill_fused<1>, g, dim3(kScanBlock), s, e0, e1, N, plan, grp, G, ms, ess_min,
+                            rec, dec, qbuf, anc, wq);
+#endif
+    return launch_timed(k_rs_fill_fused<0>, g, dim3(kScanBlock), s, e0, e1, N, plan, grp, G, ms, ess_min,
+                        rec, dec, qbuf, anc, wq);
+}
+hipError_t launch_rs_qfix(hipStream_t s, const double* w, int64_t N, const MaxSlots* ms, const double* rg, u64* tilep,
+                          u64* qbuf, u64* grp, int G, u64* nfix, hipEvent_t e0, hipEvent_t e1) {
+    // few blocks: in the common case each one only reads the slots and returns
+    const int64_t nt = (N + kRsTile - 1) / kRsTile;
+    int64_t nb = 256;
+#ifdef WSMC_DIAG_BUILD
+    static const int diag = [] {   // blocks; 0 = no check at all (wrong results on a miss: timing only)
+        const char* e = diag_env("WSMC_DIAG_QFIX_BLOCKS");
+        return e ? atoi(e) : -1;
+    }();
+    if (diag == 0) {
+        if (e0) (void)hipEventRecord(e0, s);
+        if (e1) (void)hipEventRecord(e1, s);
+        return hipSuccess;
     }
+    if (diag > 0) nb = diag;
+#endif
+    const dim3 g((unsigned)(nt < nb ? nt : nb));
+    return launch_timed(k_rs_qfix, g, dim3(kSumBlock), s, e0, e1, w, N, ms, rg, tilep, qbuf, grp, G, nfix);
 }
 hipError_t launch_rs_reduce(hipStream_t s, const MaxSlots* ms, const u64* tilep, int64_t N, u64* tileOff,
                             ShardRecord* rec, int decide_local, double ess_min, Decision* dec,
@@ -3810,6 +3975,25 @@ hipError_t debug_kernel_bench(hipStream_t s, int kernel, int mode, int iters, co
         return e0;
     }
     const dim3 g = rs_tiles_for(N), blk(kSumBlock), gs = fill_tasks_for(N), bs(kScanBlock);
+#ifndef WSMC_DIAG_BUILD
+    // the ablations (mode > 0) and the streaming calibration kernel exist in the diagnostic
+    // build only (tools/build_variant.py NAME -DWSMC_DIAG_BUILD)
+    if (mode != 0 || kernel == 3) {
+        (void)hipEventDestroy(a);
+        (void)hipEventDestroy(b);
+        return hipErrorNotSupported;
+    }
+    for (int it = 0; it < iters; ++it) {
+        if (kernel == 0)
+            hipLaunchKernelGGL(k_rs_sums_t<0>, g, blk, 0, s, w, N, ms, tilep, qbuf, nullptr, 1, N, 1, 0);
+        else if (kernel == 1)
+            hipLaunchKernelGGL(k_rs_reduce_t<0>, dim3(1), dim3(kRsBlock), 0, s, ms, tilep,
+                               (N + kRsTile - 1) / kRsTile, N, tileOff, rec, 1, 2.0, dec, plan, nullptr, 1);
+        else
+            hipLaunchKernelGGL(k_rs_scan_t<0>, gs, bs, 0, s, N, rec, dec, plan, tileOff, qbuf, anc);
+    }
+    (void)stream4;
+#else
     for (int it = 0; it < iters; ++it) {
         if (kernel == 0) {
             switch (mode) {
@@ -3844,6 +4028,7 @@ hipError_t debug_kernel_bench(hipStream_t s, int kernel, int mode, int iters, co
             }
         }
     }
+#endif
     hipError_t e = hipEventRecord(b, s);
     if (e == hipSuccess) e = hipEventSynchronize(b);
     float t = 0.f;
@@ -4124,11 +4309,11 @@ hipError_t launch_move_c(hipStream_t s, const wsmc_term* ctape, int32_t nterms, 
     // 0.76 vs 0.88 s); 4 was slower for both
     const size_t row = sizeof(double) * kBlock * (size_t)(fs.n + d);
     static const int kdiag = [] {   // diagnostics only: force 1 or 2 particles per thread
-        const char* e = getenv("WSMC_DIAG_MOVE_K");
+        const char* e = diag_env("WSMC_DIAG_MOVE_K");
         return e ? atoi(e) : 0;
     }();
     static const int nolean = [] {   // diagnostics only: the generic fold for every program
-        const char* e = getenv("WSMC_DIAG_MOVE_GENERIC");
+        const char* e = diag_env("WSMC_DIAG_MOVE_GENERIC");
         return e ? atoi(e) : 0;
     }();
     // lean variant: 1 = scalar terms and runs without oscillators, 2 = with them, 0 = generic
@@ -4201,17 +4386,24 @@ hipError_t launch_count_unique(hipStream_t s, const u64* keys, int64_t N, u64* c
     hipLaunchKernelGGL(k_count_unique, dim3((unsigned)nb), dim3(kBlock), 0, s, keys, N, count);
     return hipGetLastError();
 }
+#ifdef WSMC_DIAG_BUILD
 static int prop_mode() {
     static int v = [] {
-        const char* e = getenv("WSMC_DIAG_PROP_MODE");   // diagnostics only: ablated propagate
+        const char* e = diag_env("WSMC_DIAG_PROP_MODE");   // diagnostics only: ablated propagate
         return e ? atoi(e) & 15 : 0;
     }();
     return v;
 }
+#endif
 hipError_t launch_ssm2d_propagate(hipStream_t s, const Ssm2dArgs& a, hipEvent_t e0, hipEvent_t e1) {
+    if (a.qstat)   // one 1024-particle Resample tile a block
+        return launch_timed(k_ssm2d_prop<0, 1, 512, true>, rs_tiles_for(a.N), dim3(512), s, e0, e1, a);
     const dim3 g((unsigned)((a.N + 2 * kBlock - 1) / (2 * kBlock)));
     // IT = 2 / 4 pairs per thread (grid / 2, / 4) measured 18.8 / 22.2 us against 17.0 (1M)
     if (a.xr) return launch_timed(k_ssm2d_prop<16>, g, dim3(kBlock), s, e0, e1, a);   // exact shards
+#ifndef WSMC_DIAG_BUILD
+    return launch_timed(k_ssm2d_prop<0>, g, dim3(kBlock), s, e0, e1, a);
+#else
     switch (prop_mode()) {
         case 1: return launch_timed(k_ssm2d_prop<1>, g, dim3(kBlock), s, e0, e1, a);
         case 2: return launch_timed(k_ssm2d_prop<2>, g, dim3(kBlock), s, e0, e1, a);
@@ -4221,6 +4413,7 @@ hipError_t launch_ssm2d_propagate(hipStream_t s, const Ssm2dArgs& a, hipEvent_t 
         case 8: return launch_timed(k_ssm2d_prop<8>, g, dim3(kBlock), s, e0, e1, a);
         default: return launch_timed(k_ssm2d_prop<0>, g, dim3(kBlock), s, e0, e1, a);
     }
+#endif
 }
 // bounded spin on the 100 MHz constant clock (always exits): queue-filling delay for
 // instrumented runs
@@ -4239,7 +4432,7 @@ hipError_t launch_ssm2d_finalize(hipStream_t s, const Ssm2dFinal& f, hipEvent_t 
     // two particles a thread when the SoA outputs' second components stay 16-B aligned
     bool pair = (f.N & 1) == 0 && ((uintptr_t)f.w & 15) == 0;
     static const int diag_p = [] {   // diagnostics (tools/): particles a thread, 1 / 2 / 4
-        const char* e = getenv("WSMC_DIAG_FINAL_P");
+        const char* e = diag_env("WSMC_DIAG_FINAL_P");
         return e ? atoi(e) : 0;
     }();
     if (diag_p == 4 && (f.N & 3) == 0 && pair) {

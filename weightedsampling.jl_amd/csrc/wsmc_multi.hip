@@ -408,6 +408,7 @@ extern "C" int wsmc_create_multi(wsmc_ctx** out, int64_t n_particles, int32_t n_
     *out = nullptr;
     if (n_gpus < 1 || n_gpus > kMaxWorld) return fail(WSMC_EARG, "n_gpus must be 1..8");
     if (n_particles < n_gpus) return fail(WSMC_EARG, "fewer particles than shards");
+    if (n_particles >= (int64_t(1) << 31)) return fail(WSMC_EARG, "global population of 2^31 particles or more");
     if (transport != WSMC_TRANSPORT_RCCL && transport != WSMC_TRANSPORT_HOST) return fail(WSMC_EARG, "unknown transport");
     const int G = n_gpus;
     std::vector<int32_t> devs(G);

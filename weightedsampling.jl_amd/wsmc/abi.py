@@ -166,6 +166,8 @@ SIGNATURES = {
     "wsmc_debug_log_screen": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p]),
     "wsmc_debug_mv_jit_stats": (C.c_int, [C.POINTER(C.c_int64)]),
     "wsmc_debug_mv_jit_selfcheck": (C.c_int, []),
+    "wsmc_debug_run_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64)]),
+    "wsmc_comm_set_timeout": (C.c_int, [C.c_void_p, C.c_double]),
 }
 
 

@@ -124,6 +124,10 @@ class Context:
                                           int(rank), int(global_offset), int(global_n)))
         self.world, self.rank = int(world), int(rank)
 
+    def comm_set_timeout(self, seconds: float) -> None:
+        """wsmc_comm_set_timeout: abort the communicator when a stream wait exceeds `seconds`."""
+        check(self._L.wsmc_comm_set_timeout(self._h, float(seconds)))
+
     def comm_info(self) -> dict:
         """wsmc_comm_info: shards, world/rank, the RCCL communicator's own rank count
         (ncclCommCount), transport, shard mode, and each shard's device and size."""
@@ -395,6 +399,13 @@ class Context:
         return float(v.value)
 
     # ---- fused runners ----
+    def run_stats(self) -> dict:
+        """The fused run's Resample statistics (wsmc_debug_run_stats): steps whose statistics
+        were recomputed against the exact reference point (cumulative), and where they are taken."""
+        st = (C.c_int64 * 3)()
+        check(self._L.wsmc_debug_run_stats(self._h, st))
+        return {"missed_steps": st[0], "qstat_mode": st[1], "replays": st[2]}
+
     def ssm2d_run(self, obs, x0=(0.0, 0.0), v0=(1.0, 0.0), q_var=0.1, r_var=0.5, ess_perc_min=0.5,
                   scheme: int = abi.RESAMPLE_STRATIFIED, keep_history: bool = True,
                   want_evidence: bool = True):
