@@ -390,6 +390,40 @@ def test_ssm2d_fused_statistics_guess_and_recompute(gpu_available, N, ess):
     assert ev2 == o.log_evidence()
 
 
+@pytest.mark.parametrize("ess", [1.0, 0.5])
+@pytest.mark.parametrize("keep", [True, False])
+def test_ssm2d_fused_async_runs(gpu_available, ess, keep):
+    """Runs that return nothing to the host are asynchronous (round 6): the call returns once
+    the run is enqueued and the next run (or any other entry point) folds its decisions in.
+    Back-to-back asynchronous runs, one with outlier observations in the middle (its guessed
+    reference points miss: it and the run enqueued after it are re-done on the exact path),
+    then the state: bit for bit the oracle's after the same runs as statements."""
+    obs = models.ssm2d_data(10)
+    bad = obs.copy()
+    bad[4] += (30.0, 30.0)
+    seq = [obs, obs, bad, obs, obs]
+    N = 4096
+    g, o = wsmc.Context(N, seed=33), Oracle(N, seed=33)
+    before = g.run_stats()
+    for ob in seq:
+        assert g.ssm2d_run(ob, ess_perc_min=ess, keep_history=keep, want_evidence=False) is None
+    st = g.run_stats()          # (an entry point: folds the last run in)
+    for ob in seq:
+        models.ssm2d_statements(o, ob, ess_perc_min=ess)
+    if keep:
+        assert_same_state(g, o)
+    else:
+        np.testing.assert_array_equal(g.col_download(g.col_find("x")), o.col_download(o.col_find("x_11")))
+        np.testing.assert_array_equal(g.weights_download(), o.weights_download())
+        gs, os_ = g.get_state(), o.get_state()
+        for k in ("resampled", "n_resamples", "op_counter"):
+            assert gs[k] == os_[k], k
+    np.testing.assert_array_equal(g.last_ancestors(), o.last_ancestors())
+    assert g.log_evidence() == o.log_evidence()
+    if st["qstat_mode"]:
+        assert st["replays"] - before["replays"] >= 1
+
+
 def test_ssm2d_fused_statistics_guess_holds(gpu_available):
     """On the model's own data the guess is the reference point almost always: only a step whose
     max and bound straddle an integer misses (the first step of a run has no bound and takes the

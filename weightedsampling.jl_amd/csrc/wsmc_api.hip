@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <memory>
 #include <thread>
 #include <cmath>
 #include <cstdio>
@@ -69,10 +70,17 @@ int fail(int code, const std::string& msg) {
 // or writes the weights (CHECK_CTX_KEEP: the Observe / Weight path, which applies it itself)
 // CHECK_CTX_EW: the elementwise statements (Assign / Sample / Observe / Weight), which join the
 // pending batch (ew_*); every other entry point launches the batch first (CHECK_CTX_KEEP)
-#define CHECK_CTX_EW(ctx)                                                \
+// CHECK_CTX_DEV: the device only (column creation: no state an asynchronous run changes);
+// every other entry point first folds in an asynchronous fused run (resolve_run)
+#define CHECK_CTX_DEV(ctx)                                               \
     do {                                                                 \
         if (!(ctx)) return fail(WSMC_EARG, "null context");              \
         WSMC_HIP(hipSetDevice((ctx)->device));                           \
+    } while (0)
+#define CHECK_CTX_EW(ctx)                                                \
+    do {                                                                 \
+        CHECK_CTX_DEV(ctx);                                              \
+        if (int _r = resolve_run(ctx)) return _r;                        \
     } while (0)
 #define CHECK_CTX_KEEP(ctx)                                              \
     do {                                                                 \
@@ -89,6 +97,9 @@ int fail(int code, const std::string& msg) {
         }                                                                \
     } while (0)
 
+
+static int resolve_run(wsmc_ctx* c);        // an asynchronous fused run's decisions (wsmc_ssm2d_run)
+static void run_pend_free(RunPend* r);
 
 // ---- the elementwise batch (EwBatch, csrc/wsmc_internal.h) ---------------------------------
 // Consecutive Assign / Sample / Observe / Weight statements join one batch, launched as one
@@ -732,13 +743,18 @@ int wsmc_destroy(wsmc_ctx* c) {
         if (g.owned) (void)hipFree(g.owned);
     }
     for (auto ev : c->events) (void)hipEventDestroy(ev);
+    for (auto ev : c->run_ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (c->run_hdec) (void)hipHostFree(c->run_hdec);
+    run_pend_free(c->run_pend);   // (its run completed with the stream above; nothing to fold in any more)
+    c->run_pend = nullptr;
     for (auto& col : c->cols) {
         (void)hipFree(col.front);
         (void)hipFree(col.back);
     }
     for (void* p : c->row_slabs) (void)hipFree(p);   // every row (log, pool, eager, anc_keep) lives in a slab
     void* bufs[] = {c->dec_always, c->xchg, c->scache, c->scache_back, c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->cdf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount, c->wslots[0], c->wslots[1],
-                    c->d_colptr, c->run_params, c->d_tape, c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp, c->run_rg, c->run_nfix, c->run_w0,
+                    c->d_colptr, c->run_params, c->d_tape, c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs_buf, c->run_grp, c->run_rg, c->run_nfix, c->run_w0,
                     c->vscratch, c->xscratch, c->xp, c->comb, c->anc_out, c->xbuf, c->d_comp, c->d_ctape, c->d_prog, c->rs_grp[0], c->rs_grp[1],
                     c->xpairs, c->xnb, c->xwin, c->xstat, c->w_save, c->xms, c->xanc, c->xlines, c->xpeer};
     for (void* p : bufs)
@@ -946,7 +962,7 @@ int wsmc_comm_set_shard_mode(wsmc_ctx* c, int32_t mode) {
 // ---- store ---------------------------------------------------------------------------
 int wsmc_col_create(wsmc_ctx* c, const char* name, int32_t dim, int32_t* col_id) {
     if (c && c->multi) return multi_each(c, [&](wsmc_ctx* x) { int32_t id = -1; int r = wsmc_col_create(x, name, dim, &id); if (x == multi_first(c) && col_id) *col_id = id; return r; });
-    CHECK_CTX_EW(c);   // no weights touched; a pending statement batch keeps its pointers
+    CHECK_CTX_DEV(c);   // no weights touched; a pending statement batch keeps its pointers
     if (!name || !col_id) return fail(WSMC_EARG, "null argument");
     for (size_t k = 0; k < c->cols.size(); ++k)
         if (c->cols[k].name == name) {
@@ -3654,13 +3670,18 @@ static inline size_t run_grp_bytes(int64_t N, int32_t T) {
 
 static int ensure_run_buffers(wsmc_ctx* c, int32_t T) {
     if (c->T_alloc >= T && c->run_rec) return WSMC_OK;
+    if (int r = resolve_run(c)) return r;   // (a pending run reads these buffers)
     WSMC_HIP(ctx_sync(c, c->stream));
-    void* old[] = {c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs, c->run_grp, c->run_rg};
+    void* old[] = {c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs_buf, c->run_grp, c->run_rg};
     for (void* p : old)
         if (p) WSMC_HIP(hipFree(p));
+    if (c->run_hdec) WSMC_HIP(hipHostFree(c->run_hdec));
     WSMC_HIP(hipMalloc(&c->run_max, sizeof(MaxSlots) * (T + 1)));
     WSMC_HIP(hipMalloc(&c->run_rg, sizeof(double) * (T + 1)));
-    if (!c->run_w0) WSMC_HIP(hipMalloc(&c->run_w0, sizeof(double) * c->N));
+    if (!c->run_w0) WSMC_HIP(hipMalloc(&c->run_w0, sizeof(double) * 2 * c->N));
+    WSMC_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->run_hdec), sizeof(Decision) * 2 * (T + 1), hipHostMallocDefault));
+    for (int k = 0; k < 2; ++k)
+        if (!c->run_ev[k]) WSMC_HIP(hipEventCreateWithFlags(&c->run_ev[k], hipEventDisableTiming));
     if (!c->run_nfix) {
         WSMC_HIP(hipMalloc(&c->run_nfix, sizeof(unsigned long long)));
         WSMC_HIP(hipMemsetAsync(c->run_nfix, 0, sizeof(unsigned long long), c->stream));
@@ -3668,7 +3689,8 @@ static int ensure_run_buffers(wsmc_ctx* c, int32_t T) {
     WSMC_HIP(hipMalloc(&c->run_rec, sizeof(ShardRecord) * (T + 1) * kMaxWorld));
     WSMC_HIP(hipMalloc(&c->run_dec, sizeof(Decision) * (T + 1)));
     WSMC_HIP(hipMalloc(&c->anc_log, sizeof(int32_t) * (size_t)T * anc_stride(c->N)));
-    WSMC_HIP(hipMalloc(&c->obs, sizeof(double) * 2 * (T + 1)));
+    WSMC_HIP(hipMalloc(&c->obs_buf, sizeof(double) * 4 * (T + 1)));
+    c->obs = c->obs_buf;
     WSMC_HIP(hipMalloc(&c->run_grp, run_grp_bytes(c->N, T)));
     if (!c->vscratch) WSMC_HIP(hipMalloc(&c->vscratch, sizeof(double) * 2 * c->N));
     if (!c->xscratch) WSMC_HIP(hipMalloc(&c->xscratch, sizeof(double) * 2 * c->N));
@@ -3742,7 +3764,7 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
         a.N = N;
         a.goff = c->goff;
         a.seed = c->seed;
-        a.op_dev = c->run_params;
+        a.op_dev = c->run_op;
         a.obs = c->obs;
         a.x0[0] = p.x0[0]; a.x0[1] = p.x0[1];
         a.v0[0] = p.v0[0]; a.v0[1] = p.v0[1];
@@ -3775,7 +3797,8 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
             a.ess_min = p.ess_min;
         }
         a.ms = ms;
-        if (qs && t == 1 && !sharded) a.w_save = c->run_w0;   // a replay starts from these weights
+        if (qs && t == 1 && !sharded)   // a replay starts from these weights (this run's parity)
+            a.w_save = c->run_w0 + (size_t)((c->run_op - c->run_params) / 4) * N;
         if (guess) {   // stratified / systematic: the propagate takes the Resample statistics too
             a.qstat = true;
             a.ms_prev = t > 1 ? c->run_max + (t - 1) : nullptr;
@@ -3787,7 +3810,7 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
         }
         const int k0 = 8 * (t - 1);
         WSMC_HIP(launch_ssm2d_propagate(c->stream, a, E(k0), E(k0 + 1)));
-        const FillPlan plan = fill_plan(c, p.scheme, 3ull * (uint64_t)(t - 1) + 2ull, c->run_params);
+        const FillPlan plan = fill_plan(c, p.scheme, 3ull * (uint64_t)(t - 1) + 2ull, c->run_op);
         int32_t* anc_row = c->anc_log + (size_t)(t - 1) * anc_stride(N);
         if (p.scheme == WSMC_RESAMPLE_MULTINOMIAL) {
             // unsorted draws: sums, reduce (tile offsets, record), [exchange + decide], CDF + search
@@ -4027,7 +4050,7 @@ static int enqueue_ssm2d_exact(wsmc_ctx* c, const RunPlan& p, int64_t cap, int64
         a.N = N;
         a.goff = c->goff;
         a.seed = c->seed;
-        a.op_dev = c->run_params;
+        a.op_dev = c->run_op;
         a.obs = c->obs;
         a.x0[0] = p.x0[0]; a.x0[1] = p.x0[1];
         a.v0[0] = p.v0[0]; a.v0[1] = p.v0[1];
@@ -4064,7 +4087,7 @@ static int enqueue_ssm2d_exact(wsmc_ctx* c, const RunPlan& p, int64_t cap, int64
         WSMC_HIP(launch_rs_sums(c->stream, c->w, N, msx, c->tilep, c->qbuf, nullptr, nullptr, lines + me * xstride,
                                 G, c->gN, W, 1));
         if ((r = exchange_words(c, lines, xstride, c->stream))) return r;
-        FillPlan plan = fill_plan(c, p.scheme, 3ull * (uint64_t)(t - 1) + 2ull, c->run_params);
+        FillPlan plan = fill_plan(c, p.scheme, 3ull * (uint64_t)(t - 1) + 2ull, c->run_op);
         plan.slot_base = 0;   // slots are global: their keys too
         plan.xlines = lines;
         plan.xstride = xstride;
@@ -4204,7 +4227,7 @@ static int ssm2d_run_exact(wsmc_ctx* c, const RunPlan& p, uint64_t op_base) {
         a.N = N;
         a.goff = c->goff;
         a.seed = c->seed;
-        a.op_dev = c->run_params;
+        a.op_dev = c->run_op;
         a.obs = c->obs;
         a.x0[0] = p.x0[0]; a.x0[1] = p.x0[1];
         a.v0[0] = p.v0[0]; a.v0[1] = p.v0[1];
@@ -4318,6 +4341,25 @@ int wsmc_run_get_timing(wsmc_ctx* c, wsmc_run_timing* out) {
     return WSMC_OK;
 }
 
+// ---- asynchronous fused runs (round 6) -----------------------------------------------------
+// A run enqueued without anything the caller reads back returns at once; its decisions land in
+// pinned memory behind it (wsmc_ctx::run_hdec, by parity) and are folded in by the next entry
+// point, or by the next run right after that run's own launch, so the device goes from one run
+// to the next without waiting for the host. A run whose guessed reference point missed (the
+// fill's record block counted it) is re-done then on the exact path, from the weights it
+// started with — and so is a run enqueued after it, which started from its state.
+struct RunPend {
+    int par = 0;                   // buffer parity
+    RunPlan p;
+    uint64_t op_base = 0;
+    std::vector<double> hobs;      // its observations (a replay uploads them again)
+    bool guessed = false;          // the statistics were guessed (a miss is possible)
+    void* temp_tables = nullptr;   // an eagerly enqueued run's history tables, freed when folded
+};
+static void run_book(wsmc_ctx* c, const RunPlan& p, const double* obs);
+static void run_fold_decisions(wsmc_ctx* c, const Decision* hdec, int T);
+static int fold_run(wsmc_ctx* c, RunPend* P, RunPend* Q);
+
 int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, const double* v0, double q_var,
                    double r_var, double ess_min, int32_t scheme, int32_t keep_history, double* log_evidence_out) {
     if (c && c->multi)
@@ -4328,7 +4370,23 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
             if (!r && log_evidence_out && x == multi_first(c)) *log_evidence_out = ev;
             return r;
         });
-    CHECK_CTX(c);
+    CHECK_CTX_DEV(c);
+    static const bool no_graph = [] {   // diagnostics only: the same run enqueued eagerly
+        const char* e = getenv("WSMC_DIAG_NO_GRAPH");
+        return e && atoi(e) != 0;
+    }();
+    // asynchronous (round 6) when nothing in the call needs the run's results on the host: the
+    // call returns once the run is enqueued, the previous asynchronous run is folded in after
+    // this one's launch (so the device never waits for the host between runs)
+    const bool async_run = !exact_mode(c) && !c->timing && !c->host_exchange && !log_evidence_out && !no_graph;
+    if (!async_run)
+        if (int r = resolve_run(c)) return r;
+    if (int r = ew_flush(c)) return r;
+    if (int r = virt_all(c)) return r;
+    if (c->w_reset_pending) {
+        WSMC_HIP(launch_fill_weights(c->stream, c->w, c->w_reset_pending, c->N));
+        c->w_reset_pending = nullptr;
+    }
     if (int r = resolve_decisions(c)) return r;
     scores_invalidate(c);   // the run rewrites columns the tape reads
     c->wseq += 1;           // ... and the weights
@@ -4367,14 +4425,19 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         if ((r = wsmc_col_create(c, "dv", 2, &p.coldv))) return r;
     }
     if ((r = ensure_run_buffers(c, T))) return r;
-    // per-run values: obs, op base
-    WSMC_HIP(ctx_sync(c, c->stream));
+    // per-run values: obs, op base — in this run's parity of the buffers (the previous run may
+    // still read the other one; the one before it has been folded in, so it is done)
+    const int par = c->run_par;
+    c->run_par ^= 1;
+    c->obs = c->obs_buf + (size_t)par * 2 * (c->T_alloc + 1);
+    c->run_op = c->run_params + 4 * par;
     const uint64_t op_base = c->op;
     std::vector<double> hobs(obs, obs + 2 * (size_t)T);
     WSMC_HIP(hipMemcpyAsync(c->obs, hobs.data(), sizeof(double) * 2 * T, hipMemcpyHostToDevice, c->stream));
-    uint64_t* hp = reinterpret_cast<uint64_t*>(c->pinned);
+    // a pinned word per parity, clear of the staging other calls use (bytes 0..3839, 4000..)
+    uint64_t* hp = reinterpret_cast<uint64_t*>(c->pinned) + 480 + par;
     hp[0] = op_base;
-    WSMC_HIP(hipMemcpyAsync(c->run_params, hp, sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+    WSMC_HIP(hipMemcpyAsync(c->run_op, hp, sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
 
     char keybuf[512];
     std::snprintf(keybuf, sizeof(keybuf), "ssm2d T=%d keep=%d sch=%d ess=%.17g q=%.17g r=%.17g x0=%.17g,%.17g v0=%.17g,%.17g w=%d tm=%d",
@@ -4422,10 +4485,6 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         *outp = tabs + (T + 2);
         return WSMC_OK;
     };
-    static const bool no_graph = [] {   // diagnostics only: the same run enqueued eagerly
-        const char* e = getenv("WSMC_DIAG_NO_GRAPH");
-        return e && atoi(e) != 0;
-    }();
     // HIP cannot time events captured in graphs; a host exchange (test mode) synchronises
     // inside the run, and exact shards are host-driven. RCCL collectives are captured.
     const bool use_graph = !c->timing && !no_graph && !c->no_graph && (!exact_mode(c) || exact_async) &&
@@ -4507,6 +4566,27 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
             }
         }
     }
+    if (async_run) {
+        // the decisions come back behind the run into this parity's pinned slots; the last
+        // resampled row is copied into the last-ancestors buffer on the device
+        Decision* hd = c->run_hdec + (size_t)par * (c->T_alloc + 1);
+        WSMC_HIP(hipMemcpyAsync(hd, c->run_dec, sizeof(Decision) * (T + 1), hipMemcpyDeviceToHost, c->stream));
+        WSMC_HIP(launch_last_row(c->stream, c->run_dec, T, c->anc_log, anc_stride(c->N), c->anc, c->N));
+        WSMC_HIP(hipEventRecord(c->run_ev[par], c->stream));
+        run_book(c, p, obs);
+        RunPend* P = new RunPend;
+        P->par = par;
+        P->p = p;
+        P->p.d_hist_work = P->p.d_hist_out = nullptr;
+        P->op_base = op_base;
+        P->hobs = std::move(hobs);
+        P->guessed = !is_sharded(c) && p.scheme != WSMC_RESAMPLE_MULTINOMIAL && run_qstat_mode() != 0;
+        P->temp_tables = temp_tables;
+        RunPend* prev = c->run_pend;
+        c->run_pend = P;
+        if (prev) return fold_run(c, prev, P);
+        return WSMC_OK;
+    }
     bool rows_x = exact_async;   // the ancestor rows are the exact run's (not the eager re-run's)
     if (exact_async) {
         // every rank's overflow statistics (all-gathered by the run): the same on all ranks, so
@@ -4582,7 +4662,8 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         // taking its statistics against the exact max — the canonical bits, as if never guessed
         c->run_missed += hdec[0].ntasks;
         c->run_replays += 1;
-        WSMC_HIP(hipMemcpyAsync(c->w, c->run_w0, sizeof(double) * c->N, hipMemcpyDeviceToDevice, c->stream));
+        WSMC_HIP(hipMemcpyAsync(c->w, c->run_w0 + (size_t)par * c->N, sizeof(double) * c->N, hipMemcpyDeviceToDevice,
+                                c->stream));
         p.exact_stats = true;
         if ((r = build_tables(&p.d_hist_work, &p.d_hist_out))) return r;
         temp_tables = p.d_hist_work;
@@ -4605,61 +4686,11 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
             set_anc_last(c, nullptr, -1);
             break;
         }
-    // the run wrote its columns in full (traced back): current
-    if (p.keep) {
-        for (int t = 1; t <= T + 1; ++t) wrote_col(c, p.xcols[t]);
-    } else {
-        wrote_col(c, p.colx);
-    }
-    wrote_col(c, p.colv);
-    wrote_col(c, p.coldv);
-    gc_log(c);
-
-    // bookkeeping identical to issuing the statements one by one
-    int32_t nres = 0;
-    c->depth += 2;  // x{1} .= x0, v .= v0
-    for (int t = 1; t <= T; ++t) {
-        wsmc_dist dv;
-        std::memset(&dv, 0, sizeof(dv));
-        dv.family = WSMC_FAM_MVNORMAL_ISO;
-        dv.mean_fn = WSMC_MEAN_AFFINE;
-        dv.dim = 2;
-        for (int k = 0; k < 4; ++k) {
-            dv.mu[k].col[0] = dv.mu[k].col[1] = -1;
-        }
-        dv.scale.c0 = q_var;
-        dv.scale.col[0] = dv.scale.col[1] = -1;
-        c->depth += 1;  // x{t+1} .= x{t} + v
-        push_sample_term(c, p.coldv, dv);
-        c->depth += 1;  // dv ~ ...
-        c->depth += 1;  // v .= v + dv
-        wsmc_term ob;
-        std::memset(&ob, 0, sizeof(ob));
-        ob.dist.family = WSMC_FAM_MVNORMAL_ISO;
-        ob.dist.mean_fn = WSMC_MEAN_AFFINE;
-        ob.dist.dim = 2;
-        const int32_t xc = p.keep ? p.xcols[t + 1] : p.colx;
-        for (int k = 0; k < 4; ++k) ob.dist.mu[k] = col_operand(k < 2 ? xc : -1, k);
-        ob.dist.scale.c0 = r_var;
-        ob.dist.scale.col[0] = ob.dist.scale.col[1] = -1;
-        for (int k = 0; k < 4; ++k) {
-            std::memset(&ob.x[k], 0, sizeof(wsmc_operand));
-            ob.x[k].c0 = k < 2 ? obs[2 * (t - 1) + k] : 0.0;
-            ob.x[k].col[0] = ob.x[k].col[1] = -1;
-        }
-        ob.kind = WSMC_TERM_OBSERVE;
-        ob.depth = c->depth;
-        c->tape.push_back(ob);
-        c->depth += 1;  // o => ...
-        if (hdec[t].resampled) ++nres;
-    }
-    c->op = op_base + 3ull * (uint64_t)T;
-    c->resampled = hdec[T].resampled;
-    c->weights_changed = 0;
-    c->last_ess = hdec[T].ess;
-    c->n_resamples += nres;
-    c->colptr_dirty = true;
+    run_book(c, p, obs);
+    run_fold_decisions(c, hdec.data(), T);
     if (c->timing) {
+        int32_t nres = 0;
+        for (int t = 1; t <= T; ++t) nres += hdec[t].resampled ? 1 : 0;
         wsmc_run_timing tm{};
         float ms = 0.f;
         for (int t = 1; t <= T; ++t) {
@@ -4681,6 +4712,172 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
     }
     if (log_evidence_out) return wsmc_log_evidence(c, log_evidence_out);
     return WSMC_OK;
+}
+
+// the decision-independent bookkeeping of a run: the state issuing the statements one by one
+// leaves (columns current, the score tape, depth, op counter)
+static void run_book(wsmc_ctx* c, const RunPlan& p, const double* obs) {
+    const int T = p.T;
+    // the run wrote its columns in full (traced back): current
+    if (p.keep) {
+        for (int t = 1; t <= T + 1; ++t) wrote_col(c, p.xcols[t]);
+    } else {
+        wrote_col(c, p.colx);
+    }
+    wrote_col(c, p.colv);
+    wrote_col(c, p.coldv);
+    gc_log(c);
+
+    // bookkeeping identical to issuing the statements one by one
+    const uint64_t op_base = c->op;
+    c->depth += 2;  // x{1} .= x0, v .= v0
+    for (int t = 1; t <= T; ++t) {
+        wsmc_dist dv;
+        std::memset(&dv, 0, sizeof(dv));
+        dv.family = WSMC_FAM_MVNORMAL_ISO;
+        dv.mean_fn = WSMC_MEAN_AFFINE;
+        dv.dim = 2;
+        for (int k = 0; k < 4; ++k) {
+            dv.mu[k].col[0] = dv.mu[k].col[1] = -1;
+        }
+        dv.scale.c0 = p.q_var;
+        dv.scale.col[0] = dv.scale.col[1] = -1;
+        c->depth += 1;  // x{t+1} .= x{t} + v
+        push_sample_term(c, p.coldv, dv);
+        c->depth += 1;  // dv ~ ...
+        c->depth += 1;  // v .= v + dv
+        wsmc_term ob;
+        std::memset(&ob, 0, sizeof(ob));
+        ob.dist.family = WSMC_FAM_MVNORMAL_ISO;
+        ob.dist.mean_fn = WSMC_MEAN_AFFINE;
+        ob.dist.dim = 2;
+        const int32_t xc = p.keep ? p.xcols[t + 1] : p.colx;
+        for (int k = 0; k < 4; ++k) ob.dist.mu[k] = col_operand(k < 2 ? xc : -1, k);
+        ob.dist.scale.c0 = p.r_var;
+        ob.dist.scale.col[0] = ob.dist.scale.col[1] = -1;
+        for (int k = 0; k < 4; ++k) {
+            std::memset(&ob.x[k], 0, sizeof(wsmc_operand));
+            ob.x[k].c0 = k < 2 ? obs[2 * (t - 1) + k] : 0.0;
+            ob.x[k].col[0] = ob.x[k].col[1] = -1;
+        }
+        ob.kind = WSMC_TERM_OBSERVE;
+        ob.depth = c->depth;
+        c->tape.push_back(ob);
+        c->depth += 1;  // o => ...
+    }
+    c->op = op_base + 3ull * (uint64_t)T;
+    c->weights_changed = 0;
+    c->colptr_dirty = true;
+}
+
+// the decision-dependent part, from the run's decisions [T+1] on the host
+static void run_fold_decisions(wsmc_ctx* c, const Decision* hdec, int T) {
+    int32_t nres = 0;
+    for (int t = 1; t <= T; ++t) nres += hdec[t].resampled ? 1 : 0;
+    c->resampled = hdec[T].resampled;
+    c->last_ess = hdec[T].ess;
+    c->n_resamples += nres;
+    if (nres) set_anc_last(c, nullptr, -1);   // the last resampled row is in c->anc
+}
+
+// a run's history tables (x_t working / output buffers by step), uploaded (synchronous)
+static int build_run_tables(wsmc_ctx* c, RunPlan& p) {
+    p.d_hist_work = p.d_hist_out = nullptr;
+    if (!p.keep) return WSMC_OK;
+    const int T = p.T;
+    std::vector<double*> hw(T + 2, nullptr), ho(T + 2, nullptr);
+    for (int t = 1; t <= T + 1; ++t) {
+        hw[t] = c->cols[p.xcols[t]].back;
+        ho[t] = c->cols[p.xcols[t]].front;
+    }
+    double** tabs = nullptr;
+    WSMC_HIP(hipMalloc(&tabs, sizeof(double*) * 2 * (T + 2)));
+    WSMC_HIP(hipMemcpy(tabs, hw.data(), sizeof(double*) * (T + 2), hipMemcpyHostToDevice));
+    WSMC_HIP(hipMemcpy(tabs + (T + 2), ho.data(), sizeof(double*) * (T + 2), hipMemcpyHostToDevice));
+    p.d_hist_work = tabs;
+    p.d_hist_out = tabs + (T + 2);
+    return WSMC_OK;
+}
+
+// an event's wait, bounded like ctx_sync's (a peer's abort, the communicator watchdog)
+static hipError_t ev_sync(wsmc_ctx* c, hipEvent_t ev) {
+    const bool watch = c->comm && c->comm_timeout_s > 0.0;
+    if (!c->peer_abort && !watch) return hipEventSynchronize(ev);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int spin = 0;; ++spin) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e != hipErrorNotReady) return e;
+        if (peer_aborted(c)) return ctx_sync(c, c->stream);
+        if (watch && (spin & 255) == 255 &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->comm_timeout_s)
+            return ctx_sync(c, c->stream);   // (aborts the communicator past the same bound)
+        if (spin < 4096)
+            std::this_thread::yield();
+        else
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
+
+// re-do a run on the exact path (every step's statistics against the exact max), synchronously:
+// from the weights it started with (restore_w) or from the current ones (the run after a re-done
+// one); its decisions into its parity's pinned slots
+static int replay_run(wsmc_ctx* c, RunPend* R, bool restore_w) {
+    const int T = R->p.T;
+    if (restore_w)
+        WSMC_HIP(hipMemcpyAsync(c->w, c->run_w0 + (size_t)R->par * c->N, sizeof(double) * c->N,
+                                hipMemcpyDeviceToDevice, c->stream));
+    c->obs = c->obs_buf + (size_t)R->par * 2 * (c->T_alloc + 1);
+    c->run_op = c->run_params + 4 * R->par;
+    WSMC_HIP(hipMemcpyAsync(c->obs, R->hobs.data(), sizeof(double) * 2 * T, hipMemcpyHostToDevice, c->stream));
+    uint64_t* hp = reinterpret_cast<uint64_t*>(c->pinned) + 480 + R->par;
+    WSMC_HIP(ctx_sync(c, c->stream));
+    hp[0] = R->op_base;
+    WSMC_HIP(hipMemcpyAsync(c->run_op, hp, sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+    RunPlan p = R->p;
+    p.exact_stats = true;
+    if (int r = build_run_tables(c, p)) return r;
+    int r = enqueue_ssm2d(c, p, nullptr);
+    Decision* hd = c->run_hdec + (size_t)R->par * (c->T_alloc + 1);
+    if (!r) {
+        WSMC_HIP(hipMemcpyAsync(hd, c->run_dec, sizeof(Decision) * (T + 1), hipMemcpyDeviceToHost, c->stream));
+        WSMC_HIP(launch_last_row(c->stream, c->run_dec, T, c->anc_log, anc_stride(c->N), c->anc, c->N));
+        if (ctx_sync(c, c->stream) != hipSuccess) r = fail(WSMC_EHIP, "replay sync failed");
+    }
+    if (p.d_hist_work) (void)hipFree(p.d_hist_work);
+    return r;
+}
+
+static int fold_run(wsmc_ctx* c, RunPend* P, RunPend* Q) {
+    std::unique_ptr<RunPend> own(P);
+    WSMC_HIP(ev_sync(c, c->run_ev[P->par]));
+    if (P->temp_tables) {
+        (void)hipFree(P->temp_tables);
+        P->temp_tables = nullptr;
+    }
+    const Decision* hd = c->run_hdec + (size_t)P->par * (c->T_alloc + 1);
+    if (P->guessed && hd[0].ntasks > 0) {
+        c->run_missed += hd[0].ntasks;
+        c->run_replays += 1;
+        WSMC_HIP(ctx_sync(c, c->stream));   // (the run after it, if any, ends too)
+        if (int r = replay_run(c, P, true)) return r;
+        if (Q) {
+            if (int r = replay_run(c, Q, false)) return r;
+            Q->guessed = false;   // folded later from its replayed decisions
+        }
+    }
+    run_fold_decisions(c, hd, P->p.T);
+    return WSMC_OK;
+}
+
+static int resolve_run(wsmc_ctx* c) {
+    if (!c->run_pend) return WSMC_OK;
+    RunPend* P = c->run_pend;
+    c->run_pend = nullptr;
+    return fold_run(c, P, nullptr);
+}
+static void run_pend_free(RunPend* r) {
+    if (r && r->temp_tables) (void)hipFree(r->temp_tables);
+    delete r;
 }
 
 int wsmc_debug_exact(wsmc_ctx* c, int64_t cap, int64_t ctr, int64_t* stats_out) {

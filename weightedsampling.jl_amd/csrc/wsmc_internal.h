@@ -335,12 +335,23 @@ struct wsmc_ctx {
     wsmc::MaxSlots* run_max = nullptr;      // [T+1]
     double* run_rg = nullptr;               // [T+1] the propagate's guessed reference points (round 6)
     unsigned long long* run_nfix = nullptr; // [1] steps whose statistics k_rs_qfix recomputed (cumulative)
-    double* run_w0 = nullptr;               // [N] the weights a run started from (its replay's start)
+    double* run_w0 = nullptr;               // [2][N] the weights a run started from (its replay's start), by parity
+    // asynchronous fused runs (round 6): wsmc_ssm2d_run returns once its graph is launched; the
+    // decisions come back into pinned memory behind it and the next entry point (or the next run,
+    // after its own launch) folds them in — and re-does the run if its guessed reference point
+    // missed. A run's per-call buffers alternate by parity so the next run can be enqueued while
+    // it executes.
+    struct RunPend* run_pend = nullptr;     // the run whose decisions are still on the device
+    int run_par = 0;                        // the next run's buffer parity
+    uint64_t* run_op = nullptr;             // this run's op-base word: run_params + 4 parity
+    wsmc::Decision* run_hdec = nullptr;     // pinned [2][T+1]: each parity's decisions, read back
+    hipEvent_t run_ev[2] = {nullptr, nullptr};   // recorded behind each parity's read-back
     int64_t run_missed = 0, run_replays = 0; // single GPU: steps whose guess missed, runs re-done
     wsmc::ShardRecord* run_rec = nullptr;   // [(T+1) * world]
     wsmc::Decision* run_dec = nullptr;      // [T+1]
     int32_t* anc_log = nullptr;             // [T][N]
-    double* obs = nullptr;                  // [T*2]
+    double* obs = nullptr;                  // [T*2] this run's observations (obs_buf + parity)
+    double* obs_buf = nullptr;              // [2][T+1][2]
     double* vscratch = nullptr;             // [2N] second ping-pong buffer for v / x
     double* xscratch = nullptr;             // [2N]
     uint64_t* run_params = nullptr;         // [8] device copy of per-run values (op base)
@@ -777,6 +788,8 @@ struct Ssm2dArgs {
 hipError_t launch_rs_qfix(hipStream_t s, const double* w, int64_t N, const MaxSlots* ms, const double* rg,
                           unsigned long long* tilep, unsigned long long* qbuf, unsigned long long* grp, int G,
                           unsigned long long* nfix, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+hipError_t launch_last_row(hipStream_t s, const Decision* dec, int T, const int32_t* anc_log, int64_t stride,
+                           int32_t* out, int64_t N);
 hipError_t launch_ssm2d_propagate(hipStream_t s, const Ssm2dArgs& a, hipEvent_t e0 = nullptr,
                                   hipEvent_t e1 = nullptr);
 struct Ssm2dFinal {

@@ -3624,6 +3624,37 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_final(Ssm2dFinal f) {
     put(f.hist_out[1], x1);
 }
 
+// An asynchronous fused run's last ancestors (wsmc_last_ancestors after run!): the row of its last
+// step that resampled, found on the device from the run's decisions (one wave, 64 steps a ballot,
+// newest first), copied into out; no step resampled: out is left as it was.
+__global__ __launch_bounds__(kBlock) void k_last_row(const Decision* __restrict__ dec, int T,
+                                                     const int32_t* __restrict__ anc_log, int64_t stride,
+                                                     int32_t* __restrict__ out, int64_t N) {
+    __shared__ int s_t;
+    if (threadIdx.x < 64) {
+        int best = 0;
+        for (int top = T; top >= 1 && best == 0; top -= 64) {   // steps (top - 64, top]
+            const int t = top - (int)threadIdx.x;
+            const u64 m = __ballot(t >= 1 && dec[t].resampled);
+            if (m) best = top - __builtin_ctzll(m);              // the lowest lane: the newest step
+        }
+        if (threadIdx.x == 0) s_t = best;
+    }
+    __syncthreads();
+    const int t = s_t;
+    if (t == 0) return;
+    const int32_t* row = anc_log + (int64_t)(t - 1) * stride;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < N; i += (int64_t)gridDim.x * kBlock)
+        out[i] = row[i];
+}
+hipError_t launch_last_row(hipStream_t s, const Decision* dec, int T, const int32_t* anc_log, int64_t stride,
+                           int32_t* out, int64_t N) {
+    int64_t nb = (N + kBlock * 4 - 1) / (kBlock * 4);
+    nb = nb < 1 ? 1 : nb > 1024 ? 1024 : nb;
+    hipLaunchKernelGGL(k_last_row, dim3((unsigned)nb), dim3(kBlock), 0, s, dec, T, anc_log, stride, out, N);
+    return hipGetLastError();
+}
+
 // the 4 moves' accepted counts from their 64 slots each (one wave a move, DPP-free shuffles)
 __global__ __launch_bounds__(kBlock) void k_acc_sum(const u64* __restrict__ acc, u64* __restrict__ out) {
     const int m = threadIdx.x >> 6, s = threadIdx.x & 63;
