@@ -746,6 +746,7 @@ int wsmc_destroy(wsmc_ctx* c) {
     for (auto ev : c->run_ev)
         if (ev) (void)hipEventDestroy(ev);
     if (c->run_hdec) (void)hipHostFree(c->run_hdec);
+    if (c->run_hstage) (void)hipHostFree(c->run_hstage);
     run_pend_free(c->run_pend);   // (its run completed with the stream above; nothing to fold in any more)
     c->run_pend = nullptr;
     for (auto& col : c->cols) {
@@ -3214,10 +3215,9 @@ int wsmc_move(wsmc_ctx* c, int32_t proposal, const int32_t* targets, int32_t d, 
         int32_t flag[4];
         unsigned long long acc[4];
     }* hb = reinterpret_cast<decltype(hb)>(c->pinned);
-    WSMC_HIP(hipMemcpyAsync(hb->flag, c->dflag, sizeof(int32_t) * 4, hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(launch_acc_sum(c->stream, c->ucount, c->ucount + 4 * kAccMove));
-    WSMC_HIP(hipMemcpyAsync(hb->acc, c->ucount + 4 * kAccMove, sizeof(unsigned long long) * 4, hipMemcpyDeviceToHost,
-                            c->stream));
+    // the counts and flags into the pinned words by the summing kernel itself
+    auto* hbd = reinterpret_cast<decltype(hb)>(c->pinned_dev);
+    WSMC_HIP(launch_acc_sum(c->stream, c->ucount, hbd->acc, c->dflag, hbd->flag));
     WSMC_HIP(ctx_sync(c, c->stream));
     if (hb->flag[0]) return fail(WSMC_ENOTPD, "autoRW proposal covariance is not positive definite");
     c->dflag_zero = true;
@@ -3645,10 +3645,9 @@ static int move_block_fused(wsmc_ctx* c, int32_t n, const wsmc_move_spec* specs,
         int32_t flag[4];
         unsigned long long acc[4];
     }* hb = reinterpret_cast<decltype(hb)>(c->pinned);
-    WSMC_HIP(hipMemcpyAsync(hb->flag, c->dflag, sizeof(int32_t) * 4, hipMemcpyDeviceToHost, c->stream));
-    WSMC_HIP(launch_acc_sum(c->stream, c->ucount, c->ucount + 4 * kAccMove));
-    WSMC_HIP(hipMemcpyAsync(hb->acc, c->ucount + 4 * kAccMove, sizeof(unsigned long long) * 4, hipMemcpyDeviceToHost,
-                            c->stream));
+    // the counts and flags into the pinned words by the summing kernel itself
+    auto* hbd = reinterpret_cast<decltype(hb)>(c->pinned_dev);
+    WSMC_HIP(launch_acc_sum(c->stream, c->ucount, hbd->acc, c->dflag, hbd->flag));
     WSMC_HIP(ctx_sync(c, c->stream));
     for (int32_t m = 0; m < n; ++m) accepted_out[m] = (int64_t)hb->acc[m];
     if (hb->flag[0]) return fail(WSMC_ENOTPD, "autoRW proposal covariance is not positive definite");
@@ -3676,10 +3675,14 @@ static int ensure_run_buffers(wsmc_ctx* c, int32_t T) {
     for (void* p : old)
         if (p) WSMC_HIP(hipFree(p));
     if (c->run_hdec) WSMC_HIP(hipHostFree(c->run_hdec));
+    if (c->run_hstage) WSMC_HIP(hipHostFree(c->run_hstage));
     WSMC_HIP(hipMalloc(&c->run_max, sizeof(MaxSlots) * (T + 1)));
     WSMC_HIP(hipMalloc(&c->run_rg, sizeof(double) * (T + 1)));
     if (!c->run_w0) WSMC_HIP(hipMalloc(&c->run_w0, sizeof(double) * 2 * c->N));
-    WSMC_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->run_hdec), sizeof(Decision) * 2 * (T + 1), hipHostMallocDefault));
+    // coherent: written by the trace-back kernel / read by the head kernel in place
+    WSMC_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->run_hdec), sizeof(Decision) * 2 * (T + 1), hipHostMallocCoherent));
+    WSMC_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->run_hstage), sizeof(double) * 2 * (2 * (size_t)T + 4),
+                           hipHostMallocCoherent));
     for (int k = 0; k < 2; ++k)
         if (!c->run_ev[k]) WSMC_HIP(hipEventCreateWithFlags(&c->run_ev[k], hipEventDisableTiming));
     if (!c->run_nfix) {
@@ -3735,17 +3738,41 @@ static int run_qstat_mode() {
 
 // events (timing mode): per step 8 = {prop, sums, reduce, scan} x {start, stop} bound to the
 // dispatches themselves (hipExtLaunchKernelGGL), then 2 for the finalize kernel
+// a parity's pinned staging: [op-base bits, pad, obs 2T] (ensure_run_buffers sizes it)
+static inline double* run_stage(wsmc_ctx* c, int par) {
+    return c->run_hstage + (size_t)par * (2 * (size_t)c->T_alloc + 4);
+}
+static void run_stage_fill(wsmc_ctx* c, int par, uint64_t op_base, const double* obs, int T) {
+    double* st = run_stage(c, par);
+    st[0] = wsmc_bits2d(op_base);
+    st[1] = 0.0;
+    std::memcpy(st + 2, obs, sizeof(double) * 2 * (size_t)T);
+}
+
 static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEvent_t>* ev) {
     const int T = p.T;
     const int64_t N = c->N;
     const double r_var = p.r_var;
     const double cpre = 2.0 * WSMC_LOG2PI + 2.0 * wsmc_log(r_var);
     auto E = [&](int k) -> hipEvent_t { return ev ? (*ev)[k] : nullptr; };
-    WSMC_HIP(hipMemsetAsync(c->run_max, 0, sizeof(MaxSlots) * (T + 1), c->stream));
-    WSMC_HIP(hipMemsetAsync(c->run_dec, 0, sizeof(Decision) * (T + 1), c->stream));
     const bool sharded = is_sharded(c);
     const int G = group_tiles(N);
-    WSMC_HIP(hipMemsetAsync(c->run_grp, 0, run_grp_bytes(N, T), c->stream));
+    // this run's parity (its op word, observations, saved weights and read-back)
+    const int64_t par = (c->run_op - c->run_params) / 4;
+    {   // the head: per-step words zeroed, op word and observations in (one launch)
+        RunHead h;
+        h.z[0] = reinterpret_cast<unsigned long long*>(c->run_max);
+        h.zwords[0] = (int64_t)(sizeof(MaxSlots) / 8) * (T + 1);
+        h.z[1] = reinterpret_cast<unsigned long long*>(c->run_dec);
+        h.zwords[1] = (int64_t)(sizeof(Decision) / 8) * (T + 1);
+        h.z[2] = c->run_grp;
+        h.zwords[2] = (int64_t)(run_grp_bytes(N, T) / 8);
+        h.hstage = run_stage(c, (int)par);
+        h.obs = c->obs;
+        h.nobs = 2 * T;
+        h.op = c->run_op;
+        WSMC_HIP(launch_run_head(c->stream, h));
+    }
     double* vbuf[2] = {c->cols[p.colv].back, c->vscratch};
     double* xbuf[2] = {p.keep ? nullptr : c->cols[p.colx].back, c->xscratch};
     // the Resample statistics' place (round 6): 0 = their own kernel (k_rs_sums_t), 1 = in the
@@ -3798,7 +3825,7 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
         }
         a.ms = ms;
         if (qs && t == 1 && !sharded)   // a replay starts from these weights (this run's parity)
-            a.w_save = c->run_w0 + (size_t)((c->run_op - c->run_params) / 4) * N;
+            a.w_save = c->run_w0 + (size_t)par * N;
         if (guess) {   // stratified / systematic: the propagate takes the Resample statistics too
             a.qstat = true;
             a.ms_prev = t > 1 ? c->run_max + (t - 1) : nullptr;
@@ -3871,6 +3898,8 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
     f.anc_log = c->anc_log;
     f.anc_stride = anc_stride(N);
     f.dec = c->run_dec;
+    f.hdec = c->run_hdec + (size_t)par * (c->T_alloc + 1);
+    f.last_anc = c->anc;
     if (sharded && p.scheme != WSMC_RESAMPLE_MULTINOMIAL) {
         f.recs_last = c->run_rec + (size_t)T * c->world;
         f.dec_out = c->run_dec + T;
@@ -4433,11 +4462,14 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
     c->run_op = c->run_params + 4 * par;
     const uint64_t op_base = c->op;
     std::vector<double> hobs(obs, obs + 2 * (size_t)T);
-    WSMC_HIP(hipMemcpyAsync(c->obs, hobs.data(), sizeof(double) * 2 * T, hipMemcpyHostToDevice, c->stream));
-    // a pinned word per parity, clear of the staging other calls use (bytes 0..3839, 4000..)
-    uint64_t* hp = reinterpret_cast<uint64_t*>(c->pinned) + 480 + par;
-    hp[0] = op_base;
-    WSMC_HIP(hipMemcpyAsync(c->run_op, hp, sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+    // this parity's pinned staging (the run two calls back, its last reader, has been folded in):
+    // the head kernel of the run copies it; the exact-shard paths copy it here
+    run_stage_fill(c, par, op_base, obs, T);
+    if (exact_mode(c)) {
+        const double* st = run_stage(c, par);
+        WSMC_HIP(hipMemcpyAsync(c->obs, st + 2, sizeof(double) * 2 * T, hipMemcpyHostToDevice, c->stream));
+        WSMC_HIP(hipMemcpyAsync(c->run_op, st, sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+    }
 
     char keybuf[512];
     std::snprintf(keybuf, sizeof(keybuf), "ssm2d T=%d keep=%d sch=%d ess=%.17g q=%.17g r=%.17g x0=%.17g,%.17g v0=%.17g,%.17g w=%d tm=%d",
@@ -4567,11 +4599,8 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         }
     }
     if (async_run) {
-        // the decisions come back behind the run into this parity's pinned slots; the last
-        // resampled row is copied into the last-ancestors buffer on the device
-        Decision* hd = c->run_hdec + (size_t)par * (c->T_alloc + 1);
-        WSMC_HIP(hipMemcpyAsync(hd, c->run_dec, sizeof(Decision) * (T + 1), hipMemcpyDeviceToHost, c->stream));
-        WSMC_HIP(launch_last_row(c->stream, c->run_dec, T, c->anc_log, anc_stride(c->N), c->anc, c->N));
+        // the trace-back kernel wrote the decisions into this parity's pinned slots and the last
+        // resampled row into the last-ancestors buffer
         WSMC_HIP(hipEventRecord(c->run_ev[par], c->stream));
         run_book(c, p, obs);
         RunPend* P = new RunPend;
@@ -4651,9 +4680,15 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
             }
         }
     }
+    // the decisions: exact shards copy them back; every other run's trace-back kernel wrote them
+    // into this parity's pinned slots (and the last resampled row into c->anc)
+    const bool kernel_rb = !exact_mode(c);
+    const Decision* hd = c->run_hdec + (size_t)par * (c->T_alloc + 1);
     std::vector<Decision> hdec(T + 1);
-    WSMC_HIP(hipMemcpyAsync(hdec.data(), c->run_dec, sizeof(Decision) * (T + 1), hipMemcpyDeviceToHost, c->stream));
+    if (!kernel_rb)
+        WSMC_HIP(hipMemcpyAsync(hdec.data(), c->run_dec, sizeof(Decision) * (T + 1), hipMemcpyDeviceToHost, c->stream));
     WSMC_HIP(ctx_sync(c, c->stream));
+    if (kernel_rb) std::memcpy(hdec.data(), hd, sizeof(Decision) * (T + 1));
     if (temp_tables) (void)hipFree(temp_tables);
     temp_tables = nullptr;
     if (hdec[0].ntasks > 0 && !exact_mode(c)) {
@@ -4669,9 +4704,8 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         temp_tables = p.d_hist_work;
         r = enqueue_ssm2d(c, p, nullptr);
         if (!r) {
-            WSMC_HIP(hipMemcpyAsync(hdec.data(), c->run_dec, sizeof(Decision) * (T + 1), hipMemcpyDeviceToHost,
-                                    c->stream));
             r = ctx_sync(c, c->stream) == hipSuccess ? WSMC_OK : fail(WSMC_EHIP, "replay sync failed");
+            if (!r) std::memcpy(hdec.data(), hd, sizeof(Decision) * (T + 1));
         }
         (void)hipFree(temp_tables);
         temp_tables = nullptr;
@@ -4680,9 +4714,11 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
     // wsmc_last_ancestors reports the run's last resample, as after the statement sequence
     for (int t = T; t >= 1; --t)
         if (hdec[t].resampled) {
-            const int32_t* src = rows_x ? c->xanc + (size_t)(t - 1) * c->xanc_stride + xcap
-                                        : c->anc_log + (size_t)(t - 1) * anc_stride(c->N);
-            WSMC_HIP(hipMemcpyAsync(c->anc, src, sizeof(int32_t) * c->N, hipMemcpyDeviceToDevice, c->stream));
+            if (!kernel_rb) {
+                const int32_t* src = rows_x ? c->xanc + (size_t)(t - 1) * c->xanc_stride + xcap
+                                            : c->anc_log + (size_t)(t - 1) * anc_stride(c->N);
+                WSMC_HIP(hipMemcpyAsync(c->anc, src, sizeof(int32_t) * c->N, hipMemcpyDeviceToDevice, c->stream));
+            }
             set_anc_last(c, nullptr, -1);
             break;
         }
@@ -4828,21 +4864,14 @@ static int replay_run(wsmc_ctx* c, RunPend* R, bool restore_w) {
                                 hipMemcpyDeviceToDevice, c->stream));
     c->obs = c->obs_buf + (size_t)R->par * 2 * (c->T_alloc + 1);
     c->run_op = c->run_params + 4 * R->par;
-    WSMC_HIP(hipMemcpyAsync(c->obs, R->hobs.data(), sizeof(double) * 2 * T, hipMemcpyHostToDevice, c->stream));
-    uint64_t* hp = reinterpret_cast<uint64_t*>(c->pinned) + 480 + R->par;
-    WSMC_HIP(ctx_sync(c, c->stream));
-    hp[0] = R->op_base;
-    WSMC_HIP(hipMemcpyAsync(c->run_op, hp, sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+    WSMC_HIP(ctx_sync(c, c->stream));   // (nothing in flight reads the staging now)
+    run_stage_fill(c, R->par, R->op_base, R->hobs.data(), T);
     RunPlan p = R->p;
     p.exact_stats = true;
     if (int r = build_run_tables(c, p)) return r;
+    // the head copies the staging in; the trace-back writes the decisions and the last row
     int r = enqueue_ssm2d(c, p, nullptr);
-    Decision* hd = c->run_hdec + (size_t)R->par * (c->T_alloc + 1);
-    if (!r) {
-        WSMC_HIP(hipMemcpyAsync(hd, c->run_dec, sizeof(Decision) * (T + 1), hipMemcpyDeviceToHost, c->stream));
-        WSMC_HIP(launch_last_row(c->stream, c->run_dec, T, c->anc_log, anc_stride(c->N), c->anc, c->N));
-        if (ctx_sync(c, c->stream) != hipSuccess) r = fail(WSMC_EHIP, "replay sync failed");
-    }
+    if (!r && ctx_sync(c, c->stream) != hipSuccess) r = fail(WSMC_EHIP, "replay sync failed");
     if (p.d_hist_work) (void)hipFree(p.d_hist_work);
     return r;
 }

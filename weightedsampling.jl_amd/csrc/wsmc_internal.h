@@ -344,7 +344,10 @@ struct wsmc_ctx {
     struct RunPend* run_pend = nullptr;     // the run whose decisions are still on the device
     int run_par = 0;                        // the next run's buffer parity
     uint64_t* run_op = nullptr;             // this run's op-base word: run_params + 4 parity
-    wsmc::Decision* run_hdec = nullptr;     // pinned [2][T+1]: each parity's decisions, read back
+    wsmc::Decision* run_hdec = nullptr;     // pinned, coherent [2][T+1]: each parity's decisions, written
+                                            // by the run's trace-back kernel
+    double* run_hstage = nullptr;           // pinned, coherent [2][2T + 4]: each parity's op-base word
+                                            // (bits) and observations, read by the run's head kernel
     hipEvent_t run_ev[2] = {nullptr, nullptr};   // recorded behind each parity's read-back
     int64_t run_missed = 0, run_replays = 0; // single GPU: steps whose guess missed, runs re-done
     wsmc::ShardRecord* run_rec = nullptr;   // [(T+1) * world]
@@ -562,7 +565,8 @@ hipError_t launch_autorw_moments(hipStream_t s, const double* w, const MaxSlots*
                                  const Decision* wreset = nullptr, const Decision* gate = nullptr,
                                  const int32_t* lag_anc = nullptr, const Decision* lag_dec = nullptr, int lag_mask = 0,
                                  int32_t* zflag = nullptr, unsigned long long* zcount = nullptr);
-hipError_t launch_acc_sum(hipStream_t s, const unsigned long long* acc, unsigned long long* out);
+hipError_t launch_acc_sum(hipStream_t s, const unsigned long long* acc, unsigned long long* out,
+                          const int32_t* flag = nullptr, int32_t* flag_out = nullptr);
 hipError_t launch_autorw_final(hipStream_t s, const double* tilepart, int64_t ntiles, int d, double min_step,
                                double* mom, int32_t* flag, int raw, const Decision* gate = nullptr);
 hipError_t launch_autorw_publish(hipStream_t s, const MaxSlots* ms, double* const* cols, const int32_t* tcols, int d,
@@ -788,8 +792,6 @@ struct Ssm2dArgs {
 hipError_t launch_rs_qfix(hipStream_t s, const double* w, int64_t N, const MaxSlots* ms, const double* rg,
                           unsigned long long* tilep, unsigned long long* qbuf, unsigned long long* grp, int G,
                           unsigned long long* nfix, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
-hipError_t launch_last_row(hipStream_t s, const Decision* dec, int T, const int32_t* anc_log, int64_t stride,
-                           int32_t* out, int64_t N);
 hipError_t launch_ssm2d_propagate(hipStream_t s, const Ssm2dArgs& a, hipEvent_t e0 = nullptr,
                                   hipEvent_t e1 = nullptr);
 struct Ssm2dFinal {
@@ -809,12 +811,28 @@ struct Ssm2dFinal {
     const int32_t* anc_log;    // [T][anc_stride]
     int64_t anc_stride;        // row stride of the ancestor log (N rounded up to 4)
     const Decision* dec;       // [T+1], index t
+    // the run's read-back (block 0): every step's decision into pinned host memory; and the row
+    // of the last step that resampled into last_anc (wsmc_last_ancestors after run!)
+    Decision* hdec = nullptr;
+    int32_t* last_anc = nullptr;
     // island shards: the last step's decision from its all-gathered records (see Ssm2dArgs)
     const ShardRecord* recs_last = nullptr;
     Decision* dec_out = nullptr;
     int32_t world = 1, rank = 0;
     double ess_min = 0.0;
 };
+// a fused run's head: zeroes its per-step max slots, decisions and group sums and copies its
+// op-base word and observations from pinned host memory (one launch for three memsets and two
+// copies)
+struct RunHead {
+    unsigned long long* z[3];
+    int64_t zwords[3];
+    const double* hstage;      // [op bits, pad, obs...]
+    double* obs;
+    int32_t nobs;
+    uint64_t* op;
+};
+hipError_t launch_run_head(hipStream_t s, const RunHead& h);
 hipError_t launch_ssm2d_finalize(hipStream_t s, const Ssm2dFinal& f, hipEvent_t e0 = nullptr,
                                  hipEvent_t e1 = nullptr);
 hipError_t launch_delay(hipStream_t s, int microseconds);

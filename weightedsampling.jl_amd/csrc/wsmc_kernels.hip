@@ -3497,6 +3497,7 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_final(Ssm2dFinal f) {
     const int T = f.T;
     bool rsT;
     double meanT;
+    Decision decT{};   // island shards: the last step's decision, taken here
     if (ISL) {
         __shared__ Decision s_dec;
         if (threadIdx.x == 0) {
@@ -3506,6 +3507,7 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_final(Ssm2dFinal f) {
             if (blockIdx.x == 0) *f.dec_out = dd;
         }
         __syncthreads();
+        decT = s_dec;
         rsT = s_dec.resampled;
         meanT = s_dec.mean;
     } else {
@@ -3544,6 +3546,36 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_final(Ssm2dFinal f) {
     int64_t a[P];
 #pragma unroll
     for (int p = 0; p < P; ++p) a[p] = rsT ? f.anc_log[(int64_t)(T - 1) * S + ib + p] : ib + p;
+    // the run's read-back: block 0 copies the decisions to the host's pinned words (island
+    // shards: the last one is this kernel's); every thread copies its particles' entry of the
+    // last resampled row (step T's is a, already loaded; else the newest step that resampled,
+    // found by the first wave, 64 steps a ballot; none: last_anc is left as it was)
+    if (f.hdec && blockIdx.x == 0)
+        for (int t = (int)threadIdx.x; t <= T; t += kBlock) {
+            f.hdec[t] = (ISL && t == T) ? decT : f.dec[t];
+        }
+    if (f.last_anc) {
+        if (rsT) {
+#pragma unroll
+            for (int p = 0; p < P; ++p) f.last_anc[ib + p] = (int32_t)a[p];
+        } else {
+            __shared__ int s_tl;
+            if (threadIdx.x < 64) {
+                int best = 0;
+                for (int top = T - 1; top >= 1 && best == 0; top -= 64) {   // steps (top - 64, top]
+                    const int t = top - (int)threadIdx.x;
+                    const u64 m = __ballot(t >= 1 && f.dec[t].resampled);
+                    if (m) best = top - __builtin_ctzll(m);                  // the lowest lane: the newest
+                }
+                if (threadIdx.x == 0) s_tl = best;
+            }
+            __syncthreads();
+            const int tl = s_tl;
+            if (tl > 0)
+#pragma unroll
+                for (int p = 0; p < P; ++p) f.last_anc[ib + p] = f.anc_log[(int64_t)(tl - 1) * S + ib + p];
+        }
+    }
     // working buffers are particle-major pairs; output columns are SoA [2][N]
     {
         d2 v[P], dv[P];
@@ -3624,44 +3656,39 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_final(Ssm2dFinal f) {
     put(f.hist_out[1], x1);
 }
 
-// An asynchronous fused run's last ancestors (wsmc_last_ancestors after run!): the row of its last
-// step that resampled, found on the device from the run's decisions (one wave, 64 steps a ballot,
-// newest first), copied into out; no step resampled: out is left as it was.
-__global__ __launch_bounds__(kBlock) void k_last_row(const Decision* __restrict__ dec, int T,
-                                                     const int32_t* __restrict__ anc_log, int64_t stride,
-                                                     int32_t* __restrict__ out, int64_t N) {
-    __shared__ int s_t;
-    if (threadIdx.x < 64) {
-        int best = 0;
-        for (int top = T; top >= 1 && best == 0; top -= 64) {   // steps (top - 64, top]
-            const int t = top - (int)threadIdx.x;
-            const u64 m = __ballot(t >= 1 && dec[t].resampled);
-            if (m) best = top - __builtin_ctzll(m);              // the lowest lane: the newest step
-        }
-        if (threadIdx.x == 0) s_t = best;
+// A fused run's head (RunHead): the per-step words its kernels accumulate into, zeroed, and its
+// op-base word and observations copied from pinned host memory (the last block; coherent
+// memory, read once, 16 B a run per observation pair)
+__global__ __launch_bounds__(kBlock) void k_run_head(RunHead h) {
+    const int64_t tid = (int64_t)blockIdx.x * kBlock + threadIdx.x, nth = (int64_t)gridDim.x * kBlock;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+        for (int64_t i = tid; i < h.zwords[r]; i += nth) h.z[r][i] = 0ull;
+    if (blockIdx.x == gridDim.x - 1) {
+        for (int i = (int)threadIdx.x; i < h.nobs; i += kBlock) h.obs[i] = h.hstage[2 + i];
+        if (threadIdx.x == 0) *h.op = (uint64_t)wsmc_d2bits(h.hstage[0]);
     }
-    __syncthreads();
-    const int t = s_t;
-    if (t == 0) return;
-    const int32_t* row = anc_log + (int64_t)(t - 1) * stride;
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < N; i += (int64_t)gridDim.x * kBlock)
-        out[i] = row[i];
 }
-hipError_t launch_last_row(hipStream_t s, const Decision* dec, int T, const int32_t* anc_log, int64_t stride,
-                           int32_t* out, int64_t N) {
-    int64_t nb = (N + kBlock * 4 - 1) / (kBlock * 4);
-    nb = nb < 1 ? 1 : nb > 1024 ? 1024 : nb;
-    hipLaunchKernelGGL(k_last_row, dim3((unsigned)nb), dim3(kBlock), 0, s, dec, T, anc_log, stride, out, N);
+hipError_t launch_run_head(hipStream_t s, const RunHead& h) {
+    int64_t w = h.zwords[0] > h.zwords[1] ? h.zwords[0] : h.zwords[1];
+    w = w > h.zwords[2] ? w : h.zwords[2];
+    int64_t nb = (w + kBlock * 4 - 1) / (kBlock * 4);
+    nb = nb < 1 ? 1 : nb > 256 ? 256 : nb;
+    hipLaunchKernelGGL(k_run_head, dim3((unsigned)nb), dim3(kBlock), 0, s, h);
     return hipGetLastError();
 }
 
-// the 4 moves' accepted counts from their 64 slots each (one wave a move, DPP-free shuffles)
-__global__ __launch_bounds__(kBlock) void k_acc_sum(const u64* __restrict__ acc, u64* __restrict__ out) {
+// the 4 moves' accepted counts from their 64 slots each (one wave a move, DPP-free shuffles),
+// and the 4 flag words, written straight into the host's pinned words (a synchronous Move's
+// read-back: no copy launches behind it)
+__global__ __launch_bounds__(kBlock) void k_acc_sum(const u64* __restrict__ acc, u64* __restrict__ out,
+                                                    const int32_t* __restrict__ flag, int32_t* __restrict__ flag_out) {
     const int m = threadIdx.x >> 6, s = threadIdx.x & 63;
     u64 v = acc[(size_t)m * kAccMove + (size_t)s * kAccStride];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     if (s == 0) out[m] = v;
+    if (flag_out && threadIdx.x < 4) flag_out[threadIdx.x] = flag[threadIdx.x];
 }
 
 // ------------------------------------------------------------------------------------
@@ -4220,8 +4247,8 @@ hipError_t launch_autorw_moments(hipStream_t s, const double* w, const MaxSlots*
     }
     return hipGetLastError();
 }
-hipError_t launch_acc_sum(hipStream_t s, const u64* acc, u64* out) {
-    hipLaunchKernelGGL(k_acc_sum, dim3(1), dim3(kBlock), 0, s, acc, out);
+hipError_t launch_acc_sum(hipStream_t s, const u64* acc, u64* out, const int32_t* flag, int32_t* flag_out) {
+    hipLaunchKernelGGL(k_acc_sum, dim3(1), dim3(kBlock), 0, s, acc, out, flag, flag_out);
     return hipGetLastError();
 }
 hipError_t launch_autorw_final(hipStream_t s, const double* tilepart, int64_t ntiles, int d, double min_step,
