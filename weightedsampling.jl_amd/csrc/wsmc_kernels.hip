@@ -3490,7 +3490,9 @@ constexpr int kFinChunk = 64;   // steps whose decisions and history pointers ar
 // vmcnt and lgkmcnt (every LDS wait then also waits for them): cast to the global address space
 typedef const double __attribute__((address_space(1)))* gcdp;
 typedef double __attribute__((address_space(1)))* gdp;
-template <bool ISL, int P>
+// DG (diagnostic build only; results wrong): 1 = the walk and its gathers without the history
+// stores, 2 = the ancestor chain alone
+template <bool ISL, int P, int DG = 0>
 __global__ __launch_bounds__(kBlock) void k_ssm2d_final(Ssm2dFinal f) {
     const int64_t N = f.N;
     const int64_t i0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * P;
@@ -3617,6 +3619,7 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_final(Ssm2dFinal f) {
     int32_t raw[P];
 #pragma unroll
     for (int p = 0; p < P; ++p) raw[p] = f.anc_log[(int64_t)(T - 2 > 0 ? T - 2 : 0) * S + a[p]];
+    double sink = 0.0;   // (DG: keeps the walk's loads live)
     for (int s0 = T - 1; s0 >= 1; s0 -= kFinChunk) {
         const int n = s0 < kFinChunk ? s0 : kFinChunk;   // steps s0, s0 - 1, ..., s0 - n + 1
         __syncthreads();   // the previous chunk's readers are done
@@ -3641,9 +3644,16 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_final(Ssm2dFinal f) {
 #pragma unroll
             for (int p = 0; p < P; ++p) {
                 raw[p] = f.anc_log[ro + a[p]];
-                xn[p] = *reinterpret_cast<const __attribute__((address_space(1))) d2*>(src + 2 * a[p]);
+                if (DG == 2)
+                    xn[p] = d2{(double)raw[p], 0.0};
+                else
+                    xn[p] = *reinterpret_cast<const __attribute__((address_space(1))) d2*>(src + 2 * a[p]);
             }
-            put(outp, xp);
+            if (DG == 0)
+                put(outp, xp);
+            else
+#pragma unroll
+                for (int p = 0; p < P; ++p) sink += xp[p].x + xp[p].y;
             outp = s_out[k];
 #pragma unroll
             for (int p = 0; p < P; ++p) xp[p] = xn[p];
@@ -3654,6 +3664,7 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_final(Ssm2dFinal f) {
 #pragma unroll
     for (int p = 0; p < P; ++p) x1[p] = d2{f.x0[0], f.x0[1]};
     put(f.hist_out[1], x1);
+    if (DG) f.w[ib] = sink;
 }
 
 // A fused run's head (RunHead): the per-step words its kernels accumulate into, zeroed, and its
@@ -4498,6 +4509,17 @@ hipError_t launch_ssm2d_finalize(hipStream_t s, const Ssm2dFinal& f, hipEvent_t 
         return launch_timed(k_ssm2d_final<false, 4>, grid_for(f.N / 4), dim3(kBlock), s, e0, e1, f);
     }
     if (diag_p == 1) pair = false;
+#ifdef WSMC_DIAG_BUILD
+    // 1: no history stores, 2: the ancestor chain alone (timing only, results wrong)
+    static const int diag_fin = [] {
+        const char* e = diag_env("WSMC_DIAG_FIN");
+        return e ? atoi(e) : 0;
+    }();
+    if (pair && !f.recs_last && diag_fin == 1)
+        return launch_timed(k_ssm2d_final<false, 2, 1>, grid_for(f.N / 2), dim3(kBlock), s, e0, e1, f);
+    if (pair && !f.recs_last && diag_fin == 2)
+        return launch_timed(k_ssm2d_final<false, 2, 2>, grid_for(f.N / 2), dim3(kBlock), s, e0, e1, f);
+#endif
     if (pair) {
         if (f.recs_last) return launch_timed(k_ssm2d_final<true, 2>, grid_for(f.N / 2), dim3(kBlock), s, e0, e1, f);
         return launch_timed(k_ssm2d_final<false, 2>, grid_for(f.N / 2), dim3(kBlock), s, e0, e1, f);
