@@ -23,11 +23,13 @@ namespace wsmc {
 // Environment switches for A/B experiments (tools/): kernel variants, ablations and
 // alternative paths, read only by a diagnostic build (tools/build_variant.py NAME -DWSMC_DIAG_BUILD,
 // selected with WSMC_LIB). The product library ignores them, so no stray variable in a user's
-// environment can change its results. The four it honours change no result (tests select paths
-// with them): WSMC_DIAG_NO_GRAPH (the fused run enqueued eagerly, for kernel tracers),
-// WSMC_DIAG_NO_JIT (the interpreter kernels in place of the run-time compiled ones),
-// WSMC_DIAG_CAPTURE_FAIL (the eager fallback after a failed graph capture) and WSMC_DIAG_NO_PEER
-// (exact shards trace lineages through windows instead of peer reads).
+// environment can change its results. The ones it honours change no result (tests select paths
+// with them, or they only print): WSMC_DIAG_NO_GRAPH (the fused run enqueued eagerly, for kernel
+// tracers), WSMC_DIAG_NO_JIT (the interpreter kernels in place of the run-time compiled ones),
+// WSMC_DIAG_CAPTURE_FAIL (the eager fallback after a failed graph capture), WSMC_DIAG_NO_PEER
+// (exact shards trace lineages through windows instead of peer reads), WSMC_EXACT_EAGER (the
+// host-driven exact-shard run), WSMC_EAGER_GATHER (columns gathered at each Resample instead of
+// lazily), and WSMC_JIT_DUMP / WSMC_JIT_VERBOSE / WSMC_TRACE_DEBUG (diagnostic output only).
 inline const char* diag_env(const char* name) {
 #ifdef WSMC_DIAG_BUILD
     return getenv(name);

@@ -1827,8 +1827,11 @@ __device__ __forceinline__ void block_sum2_u64(u64& a, u64& b, u64 (*lds)[2]) {
 // lw - M only)
 // QW (round 6, the fused run after a propagate that took the statistics): the tile blocks
 // recompute q from the weights wq instead of loading it (no q in HBM)
+#ifndef WSMC_FILL_WAVES   // build-time override for occupancy experiments (tools/build_variant.py)
+#define WSMC_FILL_WAVES 6
+#endif
 template <int MODE, bool QW = false>
-__global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(6))) void k_rs_fill_fused(int64_t N, FillPlan plan, const u64* __restrict__ grp,
+__global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(WSMC_FILL_WAVES))) void k_rs_fill_fused(int64_t N, FillPlan plan, const u64* __restrict__ grp,
                                                               int G, const MaxSlots* __restrict__ ms, double ess_min,
                                                               ShardRecord* rec, Decision* dec,
                                                               const u64* __restrict__ qbuf, int32_t* __restrict__ anc,
