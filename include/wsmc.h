@@ -454,7 +454,9 @@ int wsmc_debug_mv_jit_selfcheck(void);
  * runs: stats_out[0] = the steps whose propagate guessed the reference point wrong (one GPU: found
  * by the fill; sharded: recomputed in place, k_rs_qfix), stats_out[1] = where the statistics are
  * taken (0 = their own kernel, 1 = the propagate with q stored, 2 = the propagate, the fill
- * recomputing q), stats_out[2] = the runs re-done on the exact path after a miss (one GPU). */
+ * recomputing q), stats_out[2] = the runs re-done on the exact path after a miss (one GPU),
+ * stats_out[3] = the generic Resamples whose statistics the statement batch took (round 6; its
+ * misses, recomputed by k_rs_qfix, count in stats_out[0]). stats_out holds 4 values. */
 int wsmc_debug_run_stats(wsmc_ctx* ctx, int64_t* stats_out);
 
 #ifdef __cplusplus

@@ -439,6 +439,48 @@ def test_ssm2d_fused_statistics_guess_holds(gpu_available):
         assert st["replays"] - before["replays"] <= 1
 
 
+@pytest.mark.parametrize("ess,wait", [(1.0, False), (0.5, False), (0.5, True)])
+@pytest.mark.parametrize("N", [4096, 5002])
+def test_statements_batch_statistics_guess_and_recompute(gpu_available, N, ess, wait):
+    """The statement path's Resample statistics in the Observe batch (round 6): after a fused
+    Resample, a batch whose weight terms all have a largest value (here the isotropic MvNormal
+    observation) takes q and the tile partials against ceil(entering max + bound), and k_rs_qfix
+    checks the guess (outlier observations miss: it recomputes against ceil(M)). ess 0.5 carries
+    not-resampled weights into the bound; wait=True reads every flag. Bit for bit the oracle,
+    with the batch statistics counted and the outlier steps among the misses."""
+    obs = models.ssm2d_data(16).copy()
+    obs[5] += (40.0, -25.0)
+    obs[11] += (0.0, 9.0)
+    g, o = wsmc.Context(N, seed=29), Oracle(N, seed=29)
+    before = g.run_stats()
+    fg = models.ssm2d_statements(g, obs, ess_perc_min=ess, wait=wait)
+    fo = models.ssm2d_statements(o, obs, ess_perc_min=ess, wait=wait)
+    assert fg == fo
+    st = g.run_stats()
+    assert_same_state(g, o)
+    np.testing.assert_array_equal(g.last_ancestors(), o.last_ancestors())
+    assert g.log_evidence() == o.log_evidence()
+    if st["qstat_mode"] and N % 2 == 0:
+        assert st["batch_statistics"] - before["batch_statistics"] >= 10   # every step after the first
+        assert st["missed_steps"] - before["missed_steps"] >= 2            # the two outlier steps
+
+
+def test_statements_batch_statistics_linreg(gpu_available):
+    """C3's Observe batch (a constant-scale Normal) takes the statistics too; with the Moves
+    between the Resamples the guess starts from the Resample's log-mean: bit for bit."""
+    N = 4096
+    xs, ys = models.linreg_data()
+    g, o = wsmc.Context(N, seed=8), Oracle(N, seed=8)
+    before = g.run_stats()
+    models.linreg_statements(g, xs, ys, ess_perc_min=1.0, gated=True, block=True)
+    models.linreg_statements(o, xs, ys, ess_perc_min=1.0, gated=True, block=True)
+    st = g.run_stats()
+    assert_same_state(g, o)
+    assert g.log_evidence() == o.log_evidence()
+    if st["qstat_mode"]:
+        assert st["batch_statistics"] - before["batch_statistics"] >= len(xs) - 1
+
+
 def _move_program(c, variant):
     """Moves interleaved with every operation that can stale a carried score."""
     from wsmc.dsl import Normal

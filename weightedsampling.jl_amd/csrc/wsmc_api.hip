@@ -99,6 +99,7 @@ int fail(int code, const std::string& msg) {
 
 
 static int resolve_run(wsmc_ctx* c);        // an asynchronous fused run's decisions (wsmc_ssm2d_run)
+static int run_qstat_mode();                // where the Resample statistics are taken (0: their own kernel)
 static void run_pend_free(RunPend* r);
 
 // ---- the elementwise batch (EwBatch, csrc/wsmc_internal.h) ---------------------------------
@@ -115,8 +116,11 @@ static bool ew_enabled(const wsmc_ctx* c) {
     }();
     return !off && !(c->world > 1 || c->comm || c->host_exchange);
 }
-static int ew_flush(wsmc_ctx* c) {
+// qs_done: the batch carried the Resample statistics (EwBatch::qs_base, set by wsmc_resample)
+// and its compiled kernel took them
+static int ew_flush(wsmc_ctx* c, bool* qs_done = nullptr) {
     EwBatch* b = c->ew;
+    if (qs_done) *qs_done = false;
     if (!b || b->nops == 0) return WSMC_OK;
     // the batch's signature compiled for its shape (csrc/wsmc_jit.hip); without it a batch of
     // one statement runs its own kernel (leaner than the interpreter's: no rows, no table)
@@ -139,6 +143,10 @@ static int ew_flush(wsmc_ctx* c) {
     for (auto& v : c->ew_virt)
         if (honoured) c->virt.push_back(v);
     c->ew_virt.clear();
+    if (qs_done) *qs_done = launched_jit && b->qs_base != nullptr && e == hipSuccess;
+    b->qs_base = nullptr;
+    b->nqb = 0;
+    c->ew_qs_ok = false;
     b->nops = b->ntab = b->has_w = b->nslots = b->nrows = b->npre = 0;
     b->anc = nullptr;
     b->dec = nullptr;
@@ -756,7 +764,7 @@ int wsmc_destroy(wsmc_ctx* c) {
     for (void* p : c->row_slabs) (void)hipFree(p);   // every row (log, pool, eager, anc_keep) lives in a slab
     void* bufs[] = {c->dec_always, c->xchg, c->scache, c->scache_back, c->w, c->anc, c->tmp, c->tilep, c->tileOff, c->taskOff, c->taskTile, c->mslots, c->qbuf, c->cdf, c->tilepart, c->rec, c->dec, c->mom, c->dflag, c->ucount, c->wslots[0], c->wslots[1],
                     c->d_colptr, c->run_params, c->d_tape, c->run_max, c->run_rec, c->run_dec, c->anc_log, c->obs_buf, c->run_grp, c->run_rg, c->run_nfix, c->run_w0,
-                    c->vscratch, c->xscratch, c->xp, c->comb, c->anc_out, c->xbuf, c->d_comp, c->d_ctape, c->d_prog, c->rs_grp[0], c->rs_grp[1],
+                    c->vscratch, c->xscratch, c->xp, c->comb, c->anc_out, c->xbuf, c->d_comp, c->d_ctape, c->d_prog, c->rs_grp[0], c->rs_grp[1], c->rs_qs,
                     c->xpairs, c->xnb, c->xwin, c->xstat, c->w_save, c->xms, c->xanc, c->xlines, c->xpeer};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
@@ -2379,6 +2387,27 @@ int wsmc_sample_importance(wsmc_ctx* c, int32_t out, const wsmc_dist* prop, cons
     return WSMC_OK;
 }
 
+// the largest value a weight term's log density can take, computed as the kernels compute it
+// (the same header functions): a constant-scale Normal is fma(-h, h, c) <= c, HalfNormal that
+// plus log 2 (or -inf), an isotropic MvNormal -((d log 2pi + d log var) + s / var) / 2 with
+// s >= 0. Rounding is monotone, so w + lp <= base + bound for every particle. None: false.
+static bool term_lp_bound(const wsmc_term& t, double* b) {
+    const wsmc_dist& d = t.dist;
+    if (!wsmc_operand_is_const(&d.scale)) return false;
+    const double sc = wsmc_operand_eval(&d.scale, nullptr, 0, 0, nullptr);
+    if (!(sc > 0.0) || !(sc < WSMC_INF)) return false;
+    switch (d.family) {
+        case WSMC_FAM_NORMAL: *b = wsmc_normal_c(wsmc_log(sc)); return true;
+        case WSMC_FAM_HALFNORMAL: *b = wsmc_normal_c(wsmc_log(sc)) + WSMC_LOG2; return true;
+        case WSMC_FAM_MVNORMAL_ISO: {
+            const double dd = (double)d.dim;
+            *b = -((dd * WSMC_LOG2PI + dd * wsmc_log(sc)) + 0.0) * 0.5;
+            return true;
+        }
+        default: return false;
+    }
+}
+
 static int weigh(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x, int kind) {
     if (c && c->multi) return multi_each(c, [&](wsmc_ctx* s) { return weigh(s, d, x, kind); });
     CHECK_CTX_EW(c);   // a pending weight reset is applied by the kernel itself
@@ -2446,9 +2475,17 @@ static int weigh(wsmc_ctx* c, const wsmc_dist* d, const wsmc_operand* x, int kin
             b->ms = c->wslots[wb];
             b->ms_next = c->wslots[wb ^ 1];
             c->wnext = wb ^ 1;
+            // the weights entering the batch are the last fused Resample's (statistics guess)
+            c->ew_qs_ok = c->rs_base_seq == c->wseq;
+            b->nqb = 0;
         } else {
             wb = c->wmax_buf;   // the batch's max goes to its first term's slots
         }
+        double bd = 0.0;
+        if (c->ew_qs_ok && b->nqb < kEwOps && term_lp_bound(t, &bd))
+            b->qb[b->nqb++] = bd;
+        else
+            c->ew_qs_ok = false;
         b->nops += 1;
     } else {
         WSMC_HIP(launch_weigh(c->stream, t, c->w, c->d_colptr, c->N, c->wslots[wb], c->wslots[wb ^ 1],
@@ -2500,7 +2537,34 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
         if (ess_out) *ess_out = c->last_ess;
         return WSMC_OK;
     }
-    if (int r = ew_flush(c)) return r;
+    // the statistics in the statement batch (round 6; the fused run's statistics in the
+    // propagate, for the drop-in statements): when the open batch writes the weights from the
+    // last fused Resample's and each of its weight terms has a bound, its kernel takes q and the
+    // tile partials against the guessed reference point ceil(base + bounds); k_rs_qfix then
+    // checks the guess against the max (a miss recomputes them) in place of k_rs_sums_t
+    const bool fused_rs = !is_sharded(c) && !exact_mode(c) && scheme != WSMC_RESAMPLE_MULTINOMIAL && !no_fused_resample();
+    if (fused_rs && !c->rs_grp[0]) {
+        const int64_t gw = run_grp_words(c->N);
+        for (int k = 0; k < 2; ++k) WSMC_HIP(hipMalloc(&c->rs_grp[k], sizeof(unsigned long long) * gw));
+        WSMC_HIP(hipMemsetAsync(c->rs_grp[0], 0, sizeof(unsigned long long) * gw, c->stream));
+        c->rs_grp_cur = 0;
+    }
+    bool qs_done = false;
+    if (fused_rs && c->ew && c->ew->nops > 0 && c->ew->has_w && c->ew_qs_ok && c->rs_qs && run_qstat_mode() != 0 &&
+        ew_pair_ok(*c->ew, c->N)) {
+        if (!c->run_nfix) {
+            WSMC_HIP(hipMalloc(&c->run_nfix, sizeof(unsigned long long)));
+            WSMC_HIP(hipMemsetAsync(c->run_nfix, 0, sizeof(unsigned long long), c->stream));
+        }
+        EwBatch* b = c->ew;
+        b->qs_base = c->rs_qs;
+        b->rg_out = c->rs_qs + 1;
+        b->qbuf = c->qbuf;
+        b->tilep = c->tilep;
+        b->grp = c->rs_grp[c->rs_grp_cur];
+        b->G = group_tiles(c->N);
+    }
+    if (int r = ew_flush(c, &qs_done)) return r;
     if (!c->lazy || is_sharded(c))   // every column gathered now: the unstored ones written first
         if (int r = virt_all(c)) return r;
     if (c->w_reset_pending) {   // (a weight write settles it first, so this does not happen)
@@ -2541,16 +2605,11 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
     Decision* hd = reinterpret_cast<Decision*>(c->pinned);
     plan.host_dec = async ? c->dec_ring_dev + c->dec_pending : reinterpret_cast<Decision*>(c->pinned_dev);
     bool max_kept = false;   // ms holds the max of the weights after this Resample
-    if (!is_sharded(c) && fill_resets && !no_fused_resample()) {
+    if (fused_rs) {
         // one GPU: the fused run's two launches (statistics with group sums, then the fill
         // whose extra block decides), then the gated weight reset — no reduce kernel. The
         // group lines are double-buffered: each fill's record block zeroes the next call's.
         const int64_t gw = run_grp_words(c->N);
-        if (!c->rs_grp[0]) {
-            for (int k = 0; k < 2; ++k) WSMC_HIP(hipMalloc(&c->rs_grp[k], sizeof(unsigned long long) * gw));
-            WSMC_HIP(hipMemsetAsync(c->rs_grp[0], 0, sizeof(unsigned long long) * gw, c->stream));
-            c->rs_grp_cur = 0;
-        }
         unsigned long long* grp = c->rs_grp[c->rs_grp_cur];
         c->rs_grp_cur ^= 1;
         plan.w_reset = nullptr;
@@ -2562,7 +2621,14 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
             WSMC_HIP(launch_rs_max(c->stream, c->w, c->N, ms));
         }
         const int G = group_tiles(c->N);
-        WSMC_HIP(launch_rs_sums(c->stream, c->w, c->N, ms, c->tilep, c->qbuf, nullptr, nullptr, grp, G));
+        if (qs_done) {   // the batch took the statistics: check its guess (a miss recomputes them)
+            c->rs_qs_batches += 1;
+            WSMC_HIP(launch_rs_qfix(c->stream, c->w, c->N, ms, c->rs_qs + 1, c->tilep, c->qbuf, grp, G, c->run_nfix));
+        } else {
+            WSMC_HIP(launch_rs_sums(c->stream, c->w, c->N, ms, c->tilep, c->qbuf, nullptr, nullptr, grp, G));
+        }
+        if (!c->rs_qs) WSMC_HIP(hipMalloc(&c->rs_qs, sizeof(double) * 2));
+        plan.base_out = c->rs_qs;   // the next batch's guess starts from the max this leaves
         WSMC_HIP(launch_rs_fill_fused(c->stream, c->N, plan, grp, G, ms, ess_min, c->rec + c->rank, row.dec, c->qbuf,
                                       row.anc));
         // the weight reset is deferred to the first reader (the next Observe applies it in
@@ -2594,6 +2660,7 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
             c->cur_max = ms;
             c->cur_max_seq = c->wseq;
         }
+        if (fused_rs) c->rs_base_seq = c->wseq;
         return WSMC_OK;
     }
     WSMC_HIP(ctx_sync(c, c->stream));
@@ -2615,6 +2682,7 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
         c->cur_max = ms;
         c->cur_max_seq = c->wseq;
     }
+    if (fused_rs) c->rs_base_seq = c->wseq;
     if (resampled_out) *resampled_out = c->resampled;
     if (ess_out) *ess_out = d.ess;
     return WSMC_OK;
@@ -4983,6 +5051,7 @@ int wsmc_debug_run_stats(wsmc_ctx* c, int64_t* stats_out) {
     stats_out[0] = (int64_t)nfix + c->run_missed;
     stats_out[1] = run_qstat_mode();
     stats_out[2] = c->run_replays;
+    stats_out[3] = c->rs_qs_batches;
     return WSMC_OK;
 }
 

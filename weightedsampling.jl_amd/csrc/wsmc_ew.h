@@ -29,6 +29,39 @@ struct Decision {
     double M;           // this shard's max log-weight
 };
 
+// The Resample statistics' tiles and per-particle parts (include/wsmc_math.h wsmc_qparts),
+// shared by the library's kernels and the statement batches compiled at run time
+constexpr int kRsTile = 1024;    // particles per resample tile
+constexpr int kPart = 4;         // per-tile partials: sum q, sum q2, sum wf2, sum wf (all exact)
+constexpr int kGroupLine = 8;    // u64 words of a tile group's line (sum q, max tile sum, ...)
+// q and the tile accumulators of q, q2, wf2, wf: all four are exact integers held in f64
+// (q, q2 <= 2^K <= 2^43 and wf, wf2 < 2^42), so a 1024-particle tile's sums stay below 2^53
+// (wsmc_qbits) and f64 accumulation is exact and order-free — no 64-bit integer arithmetic or
+// conversion per particle.
+struct QAcc {
+    double Q = 0.0, Q2 = 0.0, WF2 = 0.0, WF = 0.0;
+};
+#if defined(__HIPCC__) || defined(__HIPCC_RTC__)
+// an exact integer-valued double in [0, 2^52) -> u64 (the low mantissa bits of d + 2^52)
+__device__ __forceinline__ unsigned long long d_small_to_u64(double d) {
+    return __builtin_bit_cast(unsigned long long, d + 4503599627370496.0) - 0x4330000000000000ull;
+}
+__device__ __forceinline__ unsigned long long qacc_add(QAcc& a, double e, double sK) {
+    e = e > 0.0 ? e : 0.0;                                  // -inf weights, NaN: all parts 0
+    const double sc = e * sK;
+    const double qd = wsmc_floor(sc);
+    const double wf = wsmc_floor((sc - qd) * 4398046511104.0);      // 2^42
+    const double sc2 = (e * e) * sK;
+    const double q2d = wsmc_floor(sc2);
+    const double wf2 = wsmc_floor((sc2 - q2d) * 4398046511104.0);
+    a.Q = a.Q + qd;
+    a.Q2 = a.Q2 + q2d;
+    a.WF2 = a.WF2 + wf2;
+    a.WF = a.WF + wf;
+    return d_small_to_u64(qd);
+}
+#endif
+
 // A batch of consecutive elementwise statements (Assign / Sample / Observe / Weight) run as one
 // kernel, each particle taking the statements in order (csrc/wsmc_api.hip ew_*). The batch
 // travels in the kernel's arguments (read in place through the kernarg segment).
@@ -86,5 +119,18 @@ struct EwBatch {
     int8_t pre_row[kEwPre];
     int8_t pre_lag[kEwPre];     // loaded through the ancestor row
     EwOp ops[kEwOps];
+    // the Resample statistics of the final weights (EwSig::qs, round 6; the statement path's
+    // form of the fused run's statistics in the propagate): every particle's q against the
+    // guessed reference point R_g = wsmc_qref(fl(fl(*qs_base + qb[0]) + qb[1]) ...) — the
+    // entering weights' max plus each weight term's largest value, a bound of the new max —
+    // into qbuf, each 1024-particle tile's partials into tilep and its sum q into its group's
+    // line (grp, G tiles a group); R_g into rg_out, which k_rs_qfix checks against the max
+    const double* qs_base;
+    double* rg_out;
+    unsigned long long* qbuf;
+    unsigned long long* tilep;
+    unsigned long long* grp;
+    int32_t G, nqb;
+    double qb[kEwOps];
 };
 }  // namespace wsmc

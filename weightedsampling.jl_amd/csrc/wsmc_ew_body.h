@@ -36,7 +36,8 @@ struct EwSigOp {
     int8_t xrow[4][2];                  // weight term value operands
 };
 struct EwSig {
-    int8_t nops, has_w, has_reset, has_anc, has_dec, ntab, npre, pad;
+    int8_t nops, has_w, has_reset, has_anc, has_dec, ntab, npre;
+    int8_t qs;                          // the Resample statistics of the final weights (EwBatch)
     int8_t pre_row[kEwPre];
     int8_t pre_lag[kEwPre];
     uint32_t feat;
@@ -180,17 +181,20 @@ struct EwOps {
     }
 };
 
-// P particles a thread: i0 = P * (global thread index); with P = 2 the host guarantees N even
-template <class S, int P>
+// P particles a thread: i0 = P * (global thread index); with P = 2 the host guarantees N even.
+// NT threads a block; with the statistics (g.qs) P = 2 and NT = 512: a block is one Resample tile
+template <class S, int P, int NT = kBlock>
 __device__ __forceinline__ void ew_body(uint64_t seed, int64_t goff, int64_t N) {
     constexpr EwSig g = S::sig;
+    static_assert(!g.qs || (g.has_w && P * NT == kRsTile), "the statistics: one tile a block");
+    constexpr int NW = NT / 64;
     const EwBatch* B = (const EwBatch*)(const char*)__builtin_amdgcn_kernarg_segment_ptr();
-    __shared__ unsigned long long lds4[4];
+    __shared__ unsigned long long ldsw[NW];
 #ifdef WSMC_TABLES_LDS
     wsmc_tables_to_lds();   // before any log / exp (every thread: it ends in a barrier)
 #endif
     const int th = threadIdx.x;
-    const int64_t t = (int64_t)blockIdx.x * kBlock + th;
+    const int64_t t = (int64_t)blockIdx.x * NT + th;
     const int64_t i0 = t * P;
     const bool in = i0 < N;
     if (t == 0)
@@ -245,26 +249,71 @@ __device__ __forceinline__ void ew_body(uint64_t seed, int64_t goff, int64_t N) 
             }
         }
     }
+    // the Resample statistics (g.qs): q against the guessed reference point, the tile's exact
+    // partials (k_rs_sums_t's arithmetic: qacc_add on the final weights, 0 past N)
+    QAcc acc;
+    if constexpr (g.qs) {
+        double U = *B->qs_base;
+        for (int k = 0; k < B->nqb; ++k) U = U + B->qb[k];   // (uniform)
+        const double R = wsmc_qref(U);
+        const double sK = wsmc_pow2i(wsmc_qbits((uint64_t)N));
+        unsigned long long q[P];
+#pragma unroll
+        for (int p = 0; p < P; ++p) q[p] = qacc_add(acc, in ? wsmc_expw(L.wv[p] - R) : 0.0, sK);
+        if (in) *reinterpret_cast<ulonglong2*>(B->qbuf + i0) = make_ulonglong2(q[0], q[1]);
+        if (blockIdx.x == 0 && th == 0) *B->rg_out = R;
+    }
     if constexpr (g.has_w) {
         // block max (a wave's by DPP-free shuffles; the batch is not on the resample leg's
-        // critical path), one filtered atomic per block into slot blockIdx % 64
+        // critical path), one filtered atomic per block into slot blockIdx % 64; with the
+        // statistics, the tile's partials in the same barrier round (exact integers in f64:
+        // any order gives the same sums)
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
             const unsigned long long o = __shfl_xor(m, off, 64);
             m = o > m ? o : m;
+            if constexpr (g.qs) {
+                acc.Q = acc.Q + __shfl_xor(acc.Q, off, 64);
+                acc.Q2 = acc.Q2 + __shfl_xor(acc.Q2, off, 64);
+                acc.WF2 = acc.WF2 + __shfl_xor(acc.WF2, off, 64);
+                acc.WF = acc.WF + __shfl_xor(acc.WF, off, 64);
+            }
         }
-        if ((th & 63) == 0) lds4[th >> 6] = m;
+        __shared__ double ldsq[g.qs ? kPart : 1][NW];
+        if ((th & 63) == 0) {
+            ldsw[th >> 6] = m;
+            if constexpr (g.qs) {
+                ldsq[0][th >> 6] = acc.Q;
+                ldsq[1][th >> 6] = acc.Q2;
+                ldsq[2][th >> 6] = acc.WF2;
+                ldsq[3][th >> 6] = acc.WF;
+            }
+        }
         __syncthreads();
         if (th == 0) {
-            unsigned long long a = lds4[0] > lds4[1] ? lds4[0] : lds4[1];
-            const unsigned long long b = lds4[2] > lds4[3] ? lds4[2] : lds4[3];
-            a = a > b ? a : b;
+            unsigned long long a = 0;
+#pragma unroll
+            for (int k = 0; k < NW; ++k) a = ldsw[k] > a ? ldsw[k] : a;
             unsigned long long* slot = &B->ms->v[blockIdx.x % kSlots][0];
             const unsigned long long cur = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (a > cur) atomicMax(slot, a);
         }
+        if constexpr (g.qs) {
+            if (th < kPart) {
+                double f = 0.0;
+#pragma unroll
+                for (int k = 0; k < NW; ++k) f = f + ldsq[th][k];
+                const unsigned long long tsum = (unsigned long long)f;   // exact integer <= 2^53
+                B->tilep[(int64_t)blockIdx.x * kPart + th] = tsum;
+                if (th == 0) {   // the tile's sum q into its group's line (integer atomics: order-free)
+                    unsigned long long* gl = B->grp + (int64_t)(blockIdx.x / B->G) * kGroupLine;
+                    atomicAdd(gl, tsum);
+                    atomicMax(gl + 1, tsum);
+                }
+            }
+        }
         if (blockIdx.x == 0)
-            for (int k = th; k < kSlots * 16; k += kBlock) B->ms_next->v[k >> 4][k & 15] = 0ull;
+            for (int k = th; k < kSlots * 16; k += NT) B->ms_next->v[k >> 4][k & 15] = 0ull;
     }
 }
 

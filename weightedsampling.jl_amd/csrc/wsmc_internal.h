@@ -49,7 +49,6 @@ constexpr int kRsBlock = 1024;         // threads of the reduce workgroup
 #define WSMC_SCAN_BLOCK 256
 #endif
 constexpr int kSumBlock = WSMC_SUM_BLOCK;   // threads of the weight-statistics workgroup (1024 / kSumBlock particles each)
-constexpr int kRsTile = 1024;          // particles per resample tile
 constexpr int kScanBlock = WSMC_SCAN_BLOCK;   // threads of the ancestor-fill workgroup (1024 / kScanBlock particles each)
 constexpr int kRsChunk = 2048;         // ancestor slots per fill task
 constexpr int kMaxCols = 4096;
@@ -65,7 +64,6 @@ struct ShardRecord {
     unsigned long long n;      // shard size
 };
 
-constexpr int kPart = 4;      // per-tile partials: sum q, sum q2, sum wf2, sum wf (all exact)
 constexpr int kRedPart = 6;   // reduce-kernel parts: Q, Q2, Wf2 lo32/hi, Wf lo32/hi
 
 // Exact cross-shard resampling: the global CDF and the slot windows,
@@ -293,6 +291,14 @@ struct wsmc_ctx {
     int64_t prog_stage_cap = 0, prog_stage_at = 0;   // in the Move's arguments (ProgInline)
     unsigned long long* rs_grp[2] = {nullptr, nullptr};   // generic Resample's group lines (double-buffered)
     int rs_grp_cur = 0;
+    // the Resample statistics in the statement batch (round 6): rs_qs[0] the max of the weights
+    // the last fused Resample left (its record block writes it), rs_qs[1] the batch's guessed
+    // reference point; valid for the next batch while rs_base_seq == wseq. ew_qs_ok: the open
+    // batch's weight terms all have a bound (EwBatch::qb) and it started from that base
+    double* rs_qs = nullptr;
+    uint64_t rs_base_seq = ~0ull;
+    bool ew_qs_ok = false;
+    int64_t rs_qs_batches = 0;   // Resamples whose statistics the batch took (wsmc_debug_run_stats)
     size_t d_comp_cap = 0;
     double* tilepart = nullptr;             // [16 * ntiles] canonical-sum tile partials
     wsmc::MaxSlots* mslots = nullptr;       // [1] max slots of one generic resample / evidence
@@ -427,6 +433,7 @@ hipError_t launch_assign_expr(hipStream_t s, const XProg& x);
 hipError_t launch_ew_jit(hipStream_t s, const EwBatch& b, unsigned feat, uint64_t seed, int64_t goff, int64_t N,
                          int device);
 void ew_jit_stats(int64_t* out);   // compiled, failed, launched, interpreted, compile time (us)
+bool ew_pair_ok(const EwBatch& b, int64_t N);   // the batch can run two particles a thread
 int ew_jit_selfcheck(std::string& err);   // hiprtc builds a representative signature (no device)
 hipError_t launch_ew_batch(hipStream_t s, const EwBatch& b, unsigned feat, uint64_t seed, int64_t goff, int64_t N);
 // a batch of one Assign: k_assign with the batch's resolved pointers
@@ -482,6 +489,10 @@ struct FillPlan {          // ancestor-fill task planning (in the reduce kernel)
     // wsmc_qref of the step's max and counts a miss (the run is then re-done on the exact path)
     const double* rg_check = nullptr;
     int32_t* rg_miss = nullptr;
+    // generic Resample (round 6): the record block writes the max of the weights it leaves (the
+    // log-mean if it resampled, else the max it read) — the next statement batch's guess starts
+    // from it (EwBatch::qs_base)
+    double* base_out = nullptr;
 };
 hipError_t launch_rs_reduce(hipStream_t s, const MaxSlots* ms, const unsigned long long* tilep, int64_t N,
                             unsigned long long* tileOff, ShardRecord* rec, int decide_local, double ess_min,
@@ -683,8 +694,8 @@ hipError_t launch_rs_multinomial(hipStream_t s, int64_t N, const ShardRecord* re
                                  const unsigned long long* lcdf, const unsigned long long* esum,
                                  const uint32_t* ebuf, int32_t* anc, hipEvent_t e0 = nullptr,
                                  hipEvent_t e1 = nullptr);
-// fused run: group sums of q (kGroupLine u64 per group, one line each) replace the reduce kernel
-constexpr int kGroupLine = 8;
+// fused run: group sums of q (kGroupLine u64 per group, one line each, csrc/wsmc_ew.h) replace
+// the reduce kernel
 constexpr int kMaxWorld = kMaxShards;   // ranks of one node
 inline int group_tiles(int64_t N) {   // tiles per group: ~sqrt(ntiles), >= 16
     const int64_t nt = (N + kRsTile - 1) / kRsTile;

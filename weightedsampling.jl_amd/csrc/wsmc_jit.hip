@@ -103,6 +103,7 @@ EwSig signature(const EwBatch& b, unsigned feat) {
     g.has_dec = (int8_t)(b.dec != nullptr);
     g.ntab = (int8_t)b.ntab;
     g.npre = (int8_t)b.npre;
+    g.qs = (int8_t)(b.has_w && b.qs_base != nullptr);
     for (int k = 0; k < b.npre; ++k) {
         g.pre_row[k] = b.pre_row[k];
         g.pre_lag[k] = b.pre_lag[k];
@@ -160,7 +161,7 @@ std::string sig_text(const EwSig& g) {
         s += "},";
     };
     s += '{';
-    num(g.nops); num(g.has_w); num(g.has_reset); num(g.has_anc); num(g.has_dec); num(g.ntab); num(g.npre); num(0);
+    num(g.nops); num(g.has_w); num(g.has_reset); num(g.has_anc); num(g.has_dec); num(g.ntab); num(g.npre); num(g.qs);
     arr(g.pre_row, kEwPre);
     arr(g.pre_lag, kEwPre);
     s += std::to_string(g.feat) + "u,{";
@@ -189,9 +190,15 @@ bool ew_tables_lds(const EwSig& g) {
         if (g.op[k].kind == 1) return true;
     return false;
 }
-std::string tu_source(const std::string& sig, bool lds) {
-    return std::string(lds ? "#define WSMC_TABLES_LDS 1\n" : "") + "#include \"wsmc_ew_body.h\"\n"
-           "struct WsmcSig { static constexpr wsmc::EwSig sig = " + sig + "; };\n"
+std::string tu_source(const std::string& sig, bool lds, bool qs) {
+    const std::string head = std::string(lds ? "#define WSMC_TABLES_LDS 1\n" : "") + "#include \"wsmc_ew_body.h\"\n"
+                             "struct WsmcSig { static constexpr wsmc::EwSig sig = " + sig + "; };\n";
+    if (qs)   // the statistics: two particles a thread, 512 threads = one Resample tile a block
+        return head +
+               "extern \"C\" __global__ void wsmc_ew_p1(wsmc::EwBatch, uint64_t, int64_t, int64_t) {}\n"
+               "extern \"C\" __global__ __launch_bounds__(512) void wsmc_ew_p2(wsmc::EwBatch, uint64_t seed, "
+               "int64_t goff, int64_t N) { wsmc::ew_body<WsmcSig, 2, 512>(seed, goff, N); }\n";
+    return head +
            "extern \"C\" __global__ __launch_bounds__(256) void wsmc_ew_p1(wsmc::EwBatch, uint64_t seed, int64_t goff, "
            "int64_t N) { wsmc::ew_body<WsmcSig, 1>(seed, goff, N); }\n"
            "extern \"C\" __global__ __launch_bounds__(256) void wsmc_ew_p2(wsmc::EwBatch, uint64_t seed, int64_t goff, "
@@ -236,8 +243,9 @@ bool compile_src(const std::string& arch, const std::string& src, std::string& c
     return true;
 }
 
-bool compile_code(const std::string& arch, const std::string& sig, std::string& code, std::string& err, bool lds) {
-    return compile_src(arch, tu_source(sig, lds), code, err);
+bool compile_code(const std::string& arch, const std::string& sig, std::string& code, std::string& err, bool lds,
+                  bool qs) {
+    return compile_src(arch, tu_source(sig, lds, qs), code, err);
 }
 
 bool device_arch(int device, std::string& arch, std::string& err) {
@@ -268,7 +276,7 @@ bool load_module(int device, const std::string& code, const char* f0, const char
     return true;
 }
 
-bool compile(int device, const std::string& sig, JitKernel& out, std::string& err, bool lds) {
+bool compile(int device, const std::string& sig, JitKernel& out, std::string& err, bool lds, bool qs) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
         err = "hipGetDeviceProperties failed";
@@ -277,7 +285,7 @@ bool compile(int device, const std::string& sig, JitKernel& out, std::string& er
     std::string arch = prop.gcnArchName;   // e.g. "gfx950:sramecc+:xnack-": the processor alone
     arch = arch.substr(0, arch.find(':'));
     std::string code;
-    if (!compile_code(arch, sig, code, err, lds)) return false;
+    if (!compile_code(arch, sig, code, err, lds, qs)) return false;
     int cur = 0;
     hipGetDevice(&cur);
     hipSetDevice(device);
@@ -336,7 +344,7 @@ hipError_t launch_ew_jit(hipStream_t s, const EwBatch& b, unsigned feat, uint64_
             JitKernel k;
             std::string err;
             const auto t0 = std::chrono::steady_clock::now();
-            k.ok = compile(device, key, k, err, ew_tables_lds(sg));
+            k.ok = compile(device, key, k, err, ew_tables_lds(sg), sg.qs != 0);
             const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
             C.compile_s += dt;
             if (k.ok) {
@@ -357,12 +365,15 @@ hipError_t launch_ew_jit(hipStream_t s, const EwBatch& b, unsigned feat, uint64_
         C.launched += 1;
     }
     const int P = pair_ok(b, N) ? 2 : 1;
+    if (sg.qs && P != 2) return hipErrorInvalidValue;   // (the caller checked ew_pair_ok)
+    const int NT = sg.qs ? 512 : kBlock;
     const int64_t threads = (N + P - 1) / P;
-    const unsigned grid = (unsigned)((threads + kBlock - 1) / kBlock);
+    const unsigned grid = (unsigned)((threads + NT - 1) / NT);
     EwBatch bb = b;   // the kernel arguments (copied by the launch)
     void* args[] = {&bb, &seed, &goff, &N};
-    return hipModuleLaunchKernel(jk->f[P - 1], grid, 1, 1, kBlock, 1, 1, 0, s, args, nullptr);
+    return hipModuleLaunchKernel(jk->f[P - 1], grid, 1, 1, NT, 1, 1, 0, s, args, nullptr);
 }
+bool ew_pair_ok(const EwBatch& b, int64_t N) { return pair_ok(b, N); }
 
 // compile a representative signature (the 2D SSM step: Assign through the ancestors, Sample,
 // Assign, Observe) for gfx950 without a device: the embedded headers build under hiprtc
@@ -394,7 +405,9 @@ int ew_jit_selfcheck(std::string& err) {
         }
     }
     std::string code;
-    return compile_code("gfx950", sig_text(g), code, err, ew_tables_lds(g)) ? 0 : -1;
+    if (!compile_code("gfx950", sig_text(g), code, err, ew_tables_lds(g), false)) return -1;
+    g.qs = 1;   // and its form with the Resample statistics
+    return compile_code("gfx950", sig_text(g), code, err, ew_tables_lds(g), true) ? 0 : -1;
 }
 
 void ew_jit_stats(int64_t* out) {

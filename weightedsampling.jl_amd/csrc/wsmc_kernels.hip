@@ -468,32 +468,7 @@ __device__ __forceinline__ void block_sum_parts(const u64 (&acc)[P], u64 (*red)[
     }
 }
 
-// The per-particle Resample statistics (include/wsmc_math.h wsmc_qparts): q and the tile
-// accumulators of q, q2, wf2, wf.
-// All four are exact integers held in f64: q, q2 <= 2^K <= 2^43 and wf, wf2 < 2^42, so a
-// 1024-particle tile's sums stay below 2^53 (wsmc_qbits) and f64 accumulation is exact and
-// order-free — no 64-bit integer arithmetic or conversion per particle.
-struct QAcc {
-    double Q = 0.0, Q2 = 0.0, WF2 = 0.0, WF = 0.0;
-};
-// an exact integer-valued double in [0, 2^52) -> u64 (the low mantissa bits of d + 2^52)
-__device__ __forceinline__ u64 d_small_to_u64(double d) {
-    return __builtin_bit_cast(u64, d + 4503599627370496.0) - 0x4330000000000000ull;
-}
-__device__ __forceinline__ u64 qacc_add(QAcc& a, double e, double sK) {
-    e = e > 0.0 ? e : 0.0;                                  // -inf weights, NaN: all parts 0
-    const double sc = e * sK;
-    const double qd = wsmc_floor(sc);
-    const double wf = wsmc_floor((sc - qd) * 4398046511104.0);      // 2^42
-    const double sc2 = (e * e) * sK;
-    const double q2d = wsmc_floor(sc2);
-    const double wf2 = wsmc_floor((sc2 - q2d) * 4398046511104.0);
-    a.Q = a.Q + qd;
-    a.Q2 = a.Q2 + q2d;
-    a.WF2 = a.WF2 + wf2;
-    a.WF = a.WF + wf;
-    return d_small_to_u64(qd);
-}
+// The per-particle Resample statistics: QAcc, qacc_add (csrc/wsmc_ew.h).
 // a block's QAcc -> the tile partials (sum q, sum q2, sum wf2, sum wf) in threads < kPart;
 // s_f [4][nw] LDS; returns the tile's sum q in thread 0 (0 elsewhere)
 template <int NB>
@@ -1938,6 +1913,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(WSMC
             if (dec) {
                 decide_records(&r, 1, 0, ess_min, dec);
                 if (plan.host_dec) *plan.host_dec = *dec;   // the generic Resample's host copy
+                if (plan.base_out) *plan.base_out = dec->resampled ? dec->mean : wsmc_ord_dec(menc);
                 // the generic Resample defers its weight reset: the max of the reset (equal)
                 // weights goes into the slots now (the fill's other blocks never read them)
                 if (plan.ms_reset && dec->resampled) {

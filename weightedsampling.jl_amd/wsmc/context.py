@@ -402,9 +402,9 @@ class Context:
     def run_stats(self) -> dict:
         """The fused run's Resample statistics (wsmc_debug_run_stats): steps whose statistics
         were recomputed against the exact reference point (cumulative), and where they are taken."""
-        st = (C.c_int64 * 3)()
+        st = (C.c_int64 * 4)()
         check(self._L.wsmc_debug_run_stats(self._h, st))
-        return {"missed_steps": st[0], "qstat_mode": st[1], "replays": st[2]}
+        return {"missed_steps": st[0], "qstat_mode": st[1], "replays": st[2], "batch_statistics": st[3]}
 
     def ssm2d_run(self, obs, x0=(0.0, 0.0), v0=(1.0, 0.0), q_var=0.1, r_var=0.5, ess_perc_min=0.5,
                   scheme: int = abi.RESAMPLE_STRATIFIED, keep_history: bool = True,
