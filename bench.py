@@ -46,8 +46,9 @@ import numpy as np  # noqa: E402
 METRIC = json.loads((REPO / "BASELINE.json").read_text())["metric"] if (REPO / "BASELINE.json").exists() else \
     "particle-steps/sec (N_particles × T_steps / wall-s), 2D SSM bootstrap filter"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-PROP_BYTES_STEADY = 84         # propagate kernel, per particle, 2 <= t < T after a resample: 76 of the model's
-                               # state + 8 of q, its Resample statistics taken in the same pass
+PROP_BYTES_STEADY = 76         # propagate kernel, per particle, 2 <= t < T after a resample: the model's state,
+PROP_BYTES_Q = 8               # + q, the Resample statistics taken in the same pass, when the propagate stores it
+                               # (statistics mode 1, below 3M particles a GPU)
 PROP_BYTES_FIRST = 56          # step 1: x0/v0 are constants (read w, write x, v, w, and w for a replay)
 PROP_BYTES_LAST_DV = 16        # dv is stored at the last step only
 STEP_BYTES = 104               # whole step algorithmic bytes
@@ -546,7 +547,9 @@ def main():
     # through ancestors; t = 1 starts from the constant x0/v0)
     # every step resampled (step 1 of a fresh single-GPU state has equal weights, ESS = 1)
     forced = nres >= T - 1
-    prop_bytes = N * (PROP_BYTES_FIRST + (T - 1) * PROP_BYTES_STEADY + PROP_BYTES_LAST_DV)
+    qmode = ctx.run_stats()["qstat_mode"] if hasattr(ctx, "run_stats") else 1
+    steady = PROP_BYTES_STEADY + (PROP_BYTES_Q if qmode == 1 else 0)
+    prop_bytes = N * (PROP_BYTES_FIRST + (T - 1) * steady + PROP_BYTES_LAST_DV)
     prop_gbs = prop_bytes / (prop_ms * 1e-3) / 1e9 if prop_ms > 0 else None
     def pmc(name):   # PMC-measured bytes (profiles/), reported only for the N they were measured at
         f = REPO / "pmc" / name   # copies of the latest profiles/ summaries (profiles/ does not travel)

@@ -568,6 +568,32 @@ def test_ssm2d_fused_full_size_matches_port(gpu_available):
     g.close()
 
 
+@pytest.mark.timeout(300)
+def test_ssm2d_fused_recomputed_q_matches_port(gpu_available):
+    """From 4M particles a GPU the fused run's fill recomputes q from the weights instead of
+    reading the propagate's (statistics mode 2: 8 B a particle less traffic beyond the MALL).
+    4M particles, 24 steps with an outlier observation (its guessed reference point misses: the
+    run is re-done on the exact path), then a second run: every column against the bit-exact
+    CPU port."""
+    import os
+    import oracle as orc
+    N, T = 4_000_000, 24
+    obs = models.ssm2d_data(T).copy()
+    obs[9] += (35.0, -20.0)
+    g = wsmc.Context(N, seed=17)
+    before = g.run_stats()
+    ev = g.ssm2d_run(obs, ess_perc_min=1.0, keep_history=True)
+    st = g.run_stats()
+    r = orc.ssm2d_run_mt(N, obs, seed=17, ess_perc_min=1.0, threads=min(16, os.cpu_count() or 1))
+    assert ev == r["log_evidence"]
+    np.testing.assert_array_equal(g.weights_download(), r["weights"])
+    for name in ["x_%d" % t for t in range(1, T + 2)] + ["v", "dv"]:
+        np.testing.assert_array_equal(g.col_download(g.col_find(name)), r[name], err_msg=name)
+    assert st["qstat_mode"] == 2
+    assert st["replays"] - before["replays"] == 1
+    g.close()
+
+
 def test_linreg_full_size_matches_oracle(gpu_available):
     """C3 at its configured size (BASELINE configs[2]: 1M particles, forced resampling, an
     autoRW pair after every resample) against the statement oracle, bit for bit: the

@@ -99,7 +99,7 @@ int fail(int code, const std::string& msg) {
 
 
 static int resolve_run(wsmc_ctx* c);        // an asynchronous fused run's decisions (wsmc_ssm2d_run)
-static int run_qstat_mode();                // where the Resample statistics are taken (0: their own kernel)
+static int run_qstat_mode(int64_t N);       // where the Resample statistics are taken (0: their own kernel)
 static void run_pend_free(RunPend* r);
 
 // ---- the elementwise batch (EwBatch, csrc/wsmc_internal.h) ---------------------------------
@@ -2550,7 +2550,7 @@ int wsmc_resample(wsmc_ctx* c, double ess_min, int32_t scheme, int32_t* resample
         c->rs_grp_cur = 0;
     }
     bool qs_done = false;
-    if (fused_rs && c->ew && c->ew->nops > 0 && c->ew->has_w && c->ew_qs_ok && c->rs_qs && run_qstat_mode() != 0 &&
+    if (fused_rs && c->ew && c->ew->nops > 0 && c->ew->has_w && c->ew_qs_ok && c->rs_qs && run_qstat_mode(c->N) != 0 &&
         ew_pair_ok(*c->ew, c->N)) {
         if (!c->run_nfix) {
             WSMC_HIP(hipMalloc(&c->run_nfix, sizeof(unsigned long long)));
@@ -3789,18 +3789,22 @@ struct RunPlan {
 // where the fused run takes the Resample statistics (see enqueue_ssm2d); measured in round 6
 // (DESIGN.md §3). A diagnostic build (tools/build_variant.py -DWSMC_DIAG_BUILD) reads
 // WSMC_DIAG_QSTAT for A/B runs; the product library ignores the environment.
-#ifndef WSMC_QSTAT_DEFAULT
-#define WSMC_QSTAT_DEFAULT 1   // round 6: q stored 1-2 % ahead of q recomputed by the fill (1M and 8M)
-#endif
-static int run_qstat_mode() {
+// q stored by the propagate (1) or recomputed by the fill from the weights (2): stored is ahead
+// while a step's working set stays in the MALL, recomputed (8 B a particle less traffic) beyond
+// it — measured alternated on one box (profiles/r06_p*): 1M 3.035 / 3.096 against 3.008 / 3.010e10,
+// 2M 3.752 / 3.766 against 3.735 / 3.741e10, 4M 3.994 / 3.998 against 4.010 / 4.009e10, 8M 4.082
+// / 4.081 against 4.151 / 4.164e10
+constexpr int64_t kQstatRecomputeN = 3000000;   // between the 2M and 4M measurements
+static int run_qstat_mode(int64_t N) {
+    const int dflt = N >= kQstatRecomputeN ? 2 : 1;
 #ifdef WSMC_DIAG_BUILD
     static const int v = [] {
         const char* e = diag_env("WSMC_DIAG_QSTAT");
-        return e ? atoi(e) : WSMC_QSTAT_DEFAULT;
+        return e ? atoi(e) : -1;
     }();
-    return v;
+    return v >= 0 ? v : dflt;
 #else
-    return WSMC_QSTAT_DEFAULT;
+    return dflt;
 #endif
 }
 
@@ -3850,7 +3854,7 @@ static int enqueue_ssm2d(wsmc_ctx* c, const RunPlan& p, const std::vector<hipEve
     // block checks the guess and counts a miss into run_dec[0].ntasks, and the host re-does a run
     // with a miss on the exact path (wsmc_ssm2d_run); sharded: k_rs_qfix checks and recomputes in
     // place (the shards' decisions are global, so a replay would have to be too).
-    const int qs = p.scheme == WSMC_RESAMPLE_MULTINOMIAL || p.exact_stats ? 0 : run_qstat_mode();
+    const int qs = p.scheme == WSMC_RESAMPLE_MULTINOMIAL || p.exact_stats ? 0 : run_qstat_mode(N);
     for (int t = 1; t <= T; ++t) {
         const bool guess = qs && t > 1;
         Ssm2dArgs a;
@@ -4677,7 +4681,7 @@ int wsmc_ssm2d_run(wsmc_ctx* c, const double* obs, int32_t T, const double* x0, 
         P->p.d_hist_work = P->p.d_hist_out = nullptr;
         P->op_base = op_base;
         P->hobs = std::move(hobs);
-        P->guessed = !is_sharded(c) && p.scheme != WSMC_RESAMPLE_MULTINOMIAL && run_qstat_mode() != 0;
+        P->guessed = !is_sharded(c) && p.scheme != WSMC_RESAMPLE_MULTINOMIAL && run_qstat_mode(c->N) != 0;
         P->temp_tables = temp_tables;
         RunPend* prev = c->run_pend;
         c->run_pend = P;
@@ -5049,7 +5053,7 @@ int wsmc_debug_run_stats(wsmc_ctx* c, int64_t* stats_out) {
         WSMC_HIP(hipMemcpy(&nfix, c->run_nfix, sizeof(nfix), hipMemcpyDeviceToHost));
     }
     stats_out[0] = (int64_t)nfix + c->run_missed;
-    stats_out[1] = run_qstat_mode();
+    stats_out[1] = run_qstat_mode(c->N);
     stats_out[2] = c->run_replays;
     stats_out[3] = c->rs_qs_batches;
     return WSMC_OK;
