@@ -82,6 +82,12 @@ tests)   # [pytest args]: files / -k; the whole suite by default
   [ $# -gt 0 ] || set -- tests
   step 1100 $O/pytest_gpu.log python -u -m pytest -q -m gpu -x --timeout 600 --timeout-method thread "$@"
   tail -1 $O/pytest_gpu.log ;;
+evidence)   # the round's measurements without the test suite (run `tests` before it)
+  timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+  line $O/bench.json bench
+  timeout -k 10 400 python bench.py --no-cpu-baseline --statements > $O/bench_statements.json 2> $O/bench_statements.err || { tail -20 $O/bench_statements.err; exit 1; }
+  line $O/bench_statements.json statements
+  prof_passes ;;
 round)
   step 1100 $O/pytest_gpu.log python -u -m pytest tests -q -m gpu -x --timeout 600 --timeout-method thread
   tail -1 $O/pytest_gpu.log
