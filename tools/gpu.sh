@@ -87,6 +87,8 @@ evidence)   # the round's measurements without the test suite (run `tests` befor
   line $O/bench.json bench
   timeout -k 10 400 python bench.py --no-cpu-baseline --statements > $O/bench_statements.json 2> $O/bench_statements.err || { tail -20 $O/bench_statements.err; exit 1; }
   line $O/bench_statements.json statements
+  step 300 $O/st.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/st -o run -- python bench.py --no-cpu-baseline --statements --steps 20 --warmup 2
+  stats_table $O/st/run_kernel_stats.csv 8
   prof_passes ;;
 round)
   step 1100 $O/pytest_gpu.log python -u -m pytest tests -q -m gpu -x --timeout 600 --timeout-method thread
