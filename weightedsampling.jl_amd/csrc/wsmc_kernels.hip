@@ -3521,9 +3521,28 @@ __global__ __launch_bounds__(kBlock) void k_ssm2d_final(Ssm2dFinal f) {
 #ifndef WSMC_FIN_NT
 #define WSMC_FIN_NT 0
 #endif
+// WSMC_FIN_SC1=1 (diagnostics): the history stores write-through (buffer stores with sc1, aux 16),
+// so the streamed history does not stay in the XCD L2 over the walk's reused ancestor entries
+#ifndef WSMC_FIN_SC1
+#define WSMC_FIN_SC1 0
+#endif
     auto put = [&](double* dst0, const d2 (&x)[P]) {
         gdp dst = (gdp)dst0;
-        if constexpr (P >= 2) {
+        if constexpr (P >= 2 && WSMC_FIN_SC1) {
+            typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+            const uint64_t base = (uint64_t)(uintptr_t)dst0;
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)base);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(base >> 32));
+            void* ub = (void*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc(ub, 0, (int)(16 * N), 0x00020000);
+#pragma unroll
+            for (int p = 0; p < P; p += 2) {
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, d2{x[p].x, x[p + 1].x}), rs,
+                                                       (int)(8 * (ib + p)), 0, 16);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, d2{x[p].y, x[p + 1].y}), rs,
+                                                       (int)(8 * (N + ib + p)), 0, 16);
+            }
+        } else if constexpr (P >= 2) {
 #pragma unroll
             for (int p = 0; p < P; p += 2) {
                 if (WSMC_FIN_NT) {
