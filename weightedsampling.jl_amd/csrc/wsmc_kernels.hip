@@ -1821,7 +1821,22 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(WSMC
     const int ngroups = (ntiles + G - 1) / G;
     // block 0 (dispatched first: its serial decision is the longest chain) is the record
     // block; blocks 1..ntiles fill the tiles' first chunks, the rest serve overflow chunks
+#ifndef WSMC_FILL_XCD
+#define WSMC_FILL_XCD 1
+#endif
+#if WSMC_FILL_XCD
+    // tile t on block t + 8: the XCD (blockIdx % 8) of the propagate block that wrote its q,
+    // tile partials and group line (k_ssm2d_prop: tile t on block t), so the first loads can hit
+    // that XCD's L2; blocks 1..7 serve overflow chunks 0..6, the blocks after the tiles the rest
+    const int bx = (int)blockIdx.x;
+    const int t = bx == 0 ? ntiles + kOverflowBlocks
+                : bx < 8 ? ntiles + (bx - 1)
+                : bx < 8 + ntiles ? bx - 8
+                : ntiles + 7 + (bx - 8 - ntiles);
+    static_assert(kOverflowBlocks >= 7, "blocks 1..7 are overflow blocks");
+#else
     const int t = blockIdx.x == 0 ? ntiles + kOverflowBlocks : (int)blockIdx.x - 1;
+#endif
     if (MODE == 1 && t == ntiles + kOverflowBlocks) {
         if (th == 0 && dec) { dec->resampled = 1; dec->mean = 0.0; dec->ess = 0.0; dec->M = 0.0; }
         return;
